@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ETA predictions/sec for the whole node (3-layer MLP, bf16 MFMA) plus the
+p50 latency of a single ``/predict`` request through the serving stack.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched by
+``torch.distributed.run`` with one rank per GPU (RCCL backend).  Each rank scores a fixed
+per-GPU batch of packed synthetic trip records every step (weak scaling):
+
+    step = H2D copy of the raw 16-byte request records (pinned host -> HBM)
+           + ONE fused featurize+MLP HIP launch (K1+K2)
+           + D2H copy of the predicted minutes (HBM -> pinned host)
+
+Copies and compute are software-pipelined over two HIP streams (copy of batch i+1 overlaps the
+kernel of batch i), as a serving engine would run them.  K steps are timed between a barrier +
+``torch.cuda.synchronize()`` on both sides; the max over ranks is reported by rank 0 as ONE JSON
+line.  Weights are random-init (seeded), data is synthetic (no network, no checkpoints).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=1 << 21, help="rows per GPU per step")
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--io", choices=["host", "device"], default="host",
+                    help="host: include H2D of records + D2H of predictions in each step")
+    ap.add_argument("--variant", type=int, default=-1)
+    ap.add_argument("--p50", type=int, default=1, help="measure single-request p50 latency")
+    ap.add_argument("--p50-requests", type=int, default=2000)
+    return ap.parse_args()
+
+
+def main() -> None:
+    a = parse_args()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    from routest_amd.data.synth import synth_records
+    from routest_amd.models.features import records_to_features
+    from routest_amd.models.mlp3 import EtaMLP
+    from routest_amd.ops.eta_mlp import EtaMlpKernel, records_to_tensor
+
+    torch.manual_seed(1234)
+    model = EtaMLP(a.hidden)
+    norm_rec, norm_y = synth_records(65536, seed=11)
+    model.fit_normalization(records_to_features(norm_rec), norm_y)
+    kern = EtaMlpKernel(model, dev, variant=a.variant)
+
+    B = a.batch
+    rec, _ = synth_records(B, seed=100 + rank)
+    host_rec = records_to_tensor(rec).pin_memory()
+    nbuf = 2
+    dev_rec = [torch.empty_like(host_rec, device=dev) for _ in range(nbuf)]
+    host_out = [torch.empty(B, dtype=torch.float32).pin_memory() for _ in range(nbuf)]
+    dev_out = [None] * nbuf
+    copy_s = torch.cuda.Stream(dev)
+    comp_s = torch.cuda.Stream(dev)
+    h2d_done = [torch.cuda.Event() for _ in range(nbuf)]
+    comp_done = [torch.cuda.Event() for _ in range(nbuf)]
+    d2h_done = [torch.cuda.Event() for _ in range(nbuf)]
+    for i in range(nbuf):
+        dev_rec[i].copy_(host_rec)
+    torch.cuda.synchronize()
+
+    def step(i: int) -> None:
+        k = i % nbuf
+        if a.io == "host":
+            with torch.cuda.stream(copy_s):
+                copy_s.wait_event(d2h_done[k])          # slot k free (its previous D2H finished)
+                dev_rec[k].copy_(host_rec, non_blocking=True)
+                h2d_done[k].record(copy_s)
+            with torch.cuda.stream(comp_s):
+                comp_s.wait_event(h2d_done[k])
+                dev_out[k] = kern(dev_rec[k])
+                comp_done[k].record(comp_s)
+            with torch.cuda.stream(copy_s):
+                copy_s.wait_event(comp_done[k])
+                host_out[k].copy_(dev_out[k], non_blocking=True)
+                d2h_done[k].record(copy_s)
+        else:
+            with torch.cuda.stream(comp_s):
+                dev_out[k] = kern(dev_rec[k])
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # sanity: predictions finite
+    chk = kern(dev_rec[0][:1024])
+    ok = bool(torch.isfinite(chk).all().item())
+
+    p50_ms = None
+    p99_ms = None
+    if a.p50 and rank == 0:
+        # single-request latency through the host featurize/pack + H2D + kernel + D2H path
+        lat = []
+        import datetime as _dt
+        from routest_amd.models.features import pack_records
+        one = {"weather": "Sunny", "traffic": "Medium", "distance_m": 12_345.0,
+               "pickup": _dt.datetime(2026, 10, 15, 8, 30), "driver_age": 34.0}
+        pin = records_to_tensor(pack_records([one])).pin_memory()
+        drec = torch.empty_like(pin, device=dev)
+        hout = torch.empty(1, dtype=torch.float32).pin_memory()
+        for j in range(a.p50_requests):
+            t1 = time.perf_counter()
+            pin.copy_(records_to_tensor(pack_records([one])))
+            drec.copy_(pin, non_blocking=True)
+            hout.copy_(kern(drec), non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            _ = float(hout[0])
+            lat.append(time.perf_counter() - t1)
+        lat = sorted(lat[len(lat) // 10:])
+        p50_ms = lat[len(lat) // 2] * 1e3
+        p99_ms = lat[int(len(lat) * 0.99) - 1] * 1e3
+
+    if rank == 0:
+        preds = B * a.steps * world
+        value = preds / elapsed
+        out = {
+            "metric": "ETA preds/sec (whole node) + p50 /predict latency, 3-layer MLP bf16",
+            "value": value,
+            "unit": "predictions/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (seeded trip records, random-init weights)",
+            "config": {"model": f"mlp3 12->{a.hidden}->{a.hidden}->1 (fused featurize+MLP HIP kernel)",
+                       "global_batch": B * world, "seq_len": None,
+                       "parallelism": f"dp{world} (inference sharding, 1 replica/GPU)",
+                       "io": a.io},
+            "p50_predict_ms": p50_ms,
+            "p99_predict_ms": p99_ms,
+            "finite": ok,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,138 @@
+"""ETA feature schema (R16) — CPU reference implementation and the packed record format
+that the GPU featurize kernel (K1, ``csrc/eta_mlp.hip``) consumes.
+
+Reference: ``RO/Flaskr/ml.py:35-51`` builds exactly 12 columns in this order::
+
+    weather_{Cloudy,Stormy,Sunny,Windy}, traffic_{High,Jam,Low,Medium},
+    weekday_ordered (Mon=0), hour_ordered, distance_km = distance_m/1000, driver_age (default 30)
+
+Unknown categories produce all-zero one-hots (`==` comparisons).  Instead of building a pandas
+DataFrame per request we pack each request into one 16-byte record (one ``dwordx4`` load per row
+on the GPU)::
+
+    struct EtaRecord { float distance_m; float driver_age; int32 wallclock_s; u8 weather; u8 traffic; u16 pad; }
+
+``wallclock_s`` is the pickup wall-clock time in seconds since 2020-01-01 (tz ignored, exactly like
+``datetime.weekday()``/``.hour``), from which the kernel derives weekday and hour.
+"""
+from __future__ import annotations
+
+import datetime as dt
+from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..utils.timeutil import KERNEL_EPOCH_WEEKDAY, coerce_pickup, wallclock_seconds
+
+FEATURE_COLUMNS: List[str] = [
+    "weather_Cloudy", "weather_Stormy", "weather_Sunny", "weather_Windy",
+    "traffic_High", "traffic_Jam", "traffic_Low", "traffic_Medium",
+    "weekday_ordered", "hour_ordered", "distance_km", "driver_age",
+]
+NUM_FEATURES = len(FEATURE_COLUMNS)
+WEATHERS: Tuple[str, ...] = ("Cloudy", "Stormy", "Sunny", "Windy")
+TRAFFICS: Tuple[str, ...] = ("High", "Jam", "Low", "Medium")
+UNKNOWN_CODE = 255
+_W = {w: i for i, w in enumerate(WEATHERS)}
+_T = {t: i for i, t in enumerate(TRAFFICS)}
+
+RECORD_DTYPE = np.dtype([("distance_m", "<f4"), ("driver_age", "<f4"), ("wallclock_s", "<i4"),
+                         ("weather", "u1"), ("traffic", "u1"), ("pad", "<u2")])
+assert RECORD_DTYPE.itemsize == 16
+
+
+def weather_code(w: Any) -> int:
+    return _W.get(w, UNKNOWN_CODE) if isinstance(w, str) else UNKNOWN_CODE
+
+
+def traffic_code(t: Any) -> int:
+    return _T.get(t, UNKNOWN_CODE) if isinstance(t, str) else UNKNOWN_CODE
+
+
+def feature_dict(*, weather: Any, traffic: Any, distance_m: Any, pickup_time: Any,
+                 driver_age: Any = 30.0) -> Tuple[Dict[str, Any], dt.datetime]:
+    """Exact R16 feature dict (same Python types as the reference's DataFrame row)."""
+    p = coerce_pickup(pickup_time)
+    feats = {
+        "weather_Cloudy": weather == "Cloudy",
+        "weather_Stormy": weather == "Stormy",
+        "weather_Sunny": weather == "Sunny",
+        "weather_Windy": weather == "Windy",
+        "traffic_High": traffic == "High",
+        "traffic_Jam": traffic == "Jam",
+        "traffic_Low": traffic == "Low",
+        "traffic_Medium": traffic == "Medium",
+        "weekday_ordered": p.weekday(),
+        "hour_ordered": p.hour,
+        "distance_km": float(distance_m or 0) / 1000.0,
+        "driver_age": float(driver_age or 30.0),
+    }
+    return feats, p
+
+
+def features_row(**kw: Any) -> np.ndarray:
+    feats, _ = feature_dict(**kw)
+    return np.array([float(feats[c]) for c in FEATURE_COLUMNS], dtype=np.float32)
+
+
+def pack_record(*, weather: Any, traffic: Any, distance_m: Any, pickup: dt.datetime,
+                driver_age: Any = 30.0) -> Tuple:
+    return (float(distance_m or 0), float(driver_age or 30.0), wallclock_seconds(pickup),
+            weather_code(weather), traffic_code(traffic), 0)
+
+
+def pack_records(rows: Sequence[Dict[str, Any]]) -> np.ndarray:
+    """Pack request dicts (weather, traffic, distance_m, pickup(datetime), driver_age)."""
+    out = np.empty(len(rows), dtype=RECORD_DTYPE)
+    for i, r in enumerate(rows):
+        out[i] = pack_record(**r)
+    return out
+
+
+def records_to_features(rec: np.ndarray) -> np.ndarray:
+    """CPU reference of the K1 featurize kernel: records -> [B,12] float32 (R16 order)."""
+    rec = np.asarray(rec, dtype=RECORD_DTYPE)
+    b = rec.shape[0]
+    x = np.zeros((b, NUM_FEATURES), dtype=np.float32)
+    w = rec["weather"].astype(np.int64)
+    t = rec["traffic"].astype(np.int64)
+    for i in range(4):
+        x[:, i] = (w == i)
+        x[:, 4 + i] = (t == i)
+    secs = rec["wallclock_s"].astype(np.int64)
+    days = np.floor_divide(secs, 86400)
+    sod = secs - days * 86400
+    x[:, 8] = (days + KERNEL_EPOCH_WEEKDAY) % 7
+    x[:, 9] = sod // 3600
+    x[:, 10] = rec["distance_m"].astype(np.float32) / np.float32(1000.0)
+    x[:, 11] = rec["driver_age"]
+    return x
+
+
+def dataframe_to_features(df: Any) -> np.ndarray:
+    """Accept a reference-style pandas DataFrame (12 named columns) -> [B,12] float32."""
+    cols = list(df.columns)
+    if cols != FEATURE_COLUMNS:
+        missing = [c for c in FEATURE_COLUMNS if c not in cols]
+        if missing:
+            raise ValueError(f"missing feature columns: {missing}")
+        df = df[FEATURE_COLUMNS]
+    return df.to_numpy(dtype=np.float32)
+
+
+def features_to_records(x: np.ndarray, base_day: int = 0) -> np.ndarray:
+    """Inverse map for synthetic data: [B,12] features -> records (weekday/hour re-encoded)."""
+    x = np.asarray(x, dtype=np.float32)
+    rec = np.zeros(x.shape[0], dtype=RECORD_DTYPE)
+    w = np.where(x[:, 0:4].max(1) > 0.5, x[:, 0:4].argmax(1), UNKNOWN_CODE)
+    t = np.where(x[:, 4:8].max(1) > 0.5, x[:, 4:8].argmax(1), UNKNOWN_CODE)
+    wd = x[:, 8].astype(np.int64)
+    hr = x[:, 9].astype(np.int64)
+    # choose a day whose weekday matches: day d has weekday (d + EPOCH_WD) % 7
+    day = base_day + ((wd - KERNEL_EPOCH_WEEKDAY - base_day) % 7)
+    rec["wallclock_s"] = (day * 86400 + hr * 3600).astype(np.int32)
+    rec["distance_m"] = x[:, 10] * 1000.0
+    rec["driver_age"] = x[:, 11]
+    rec["weather"] = w.astype(np.uint8)
+    rec["traffic"] = t.astype(np.uint8)
+    return rec

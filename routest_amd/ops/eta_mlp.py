@@ -1,0 +1,184 @@
+"""Host side of the fused ETA MLP kernel (K1 featurize + K2 forward, ``csrc/eta_mlp_fwd.hip``).
+
+:func:`pack_mlp3` turns an :class:`~routest_amd.models.mlp3.EtaMLP` into the kernel's weight blob:
+
+* ``W1k [H,16]``: W1 on normalised features, with the km/age columns duplicated into the pad
+  slots k = 12, 13 (the kernel feeds a bf16 hi/lo split of those two inputs there).
+* A fragments for ``mfma_f32_32x32x16_bf16``: lane l holds ``A[row l&31][k = 8(l>>5) + j]``.
+  For layer 2 the B operand is the layer-1 accumulator, whose element j of lane half h is hidden
+  unit ``16ks + 8(j>>2) + 4h + (j&3)`` (cdna_hip_programming.md §3), so W2's columns are permuted
+  the same way here, once, on the host.
+* bias / w3 vectors in accumulator-register order: ``v[mt][h][i] = v[32mt + (i&3) + 8(i>>2) + 4h]``.
+* the target de-normalisation (y_std, y_mean) is folded into w3 / b3.
+
+:func:`emulate_kernel` reproduces the kernel's numerics (bf16 operands, fp32 accumulate) on any
+device with plain PyTorch; tests compare the HIP kernel against it and against the fp32 model.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..models.features import RECORD_DTYPE
+from ..models.mlp3 import EtaMLP
+from . import _ext
+
+
+def _acc_rows(h: int) -> np.ndarray:
+    i = np.arange(16)
+    return (i & 3) + 8 * (i >> 2) + 4 * h
+
+
+@dataclass
+class PackedMLP3:
+    hidden: int
+    blob: torch.Tensor          # uint8 [2H^2 + 44H]
+    norm: List[float]           # 4 scales + 4 shifts (weekday, hour, km, age)
+    b3: float
+    # fp32 kernel-view tensors (for emulation / debugging)
+    w1k: torch.Tensor
+    b1: torch.Tensor
+    w2: torch.Tensor
+    b2: torch.Tensor
+    w3: torch.Tensor
+
+    def to(self, device) -> "PackedMLP3":
+        return PackedMLP3(self.hidden, self.blob.to(device), list(self.norm), self.b3,
+                          self.w1k, self.b1, self.w2, self.b2, self.w3)
+
+
+@torch.no_grad()
+def pack_mlp3(model: EtaMLP) -> PackedMLP3:
+    H = model.hidden
+    MT, KS = H // 32, H // 16
+    W1 = model.l1.weight.detach().float().cpu()                   # [H,12]
+    x_std = model.x_std.detach().float().cpu()
+    x_mean = model.x_mean.detach().float().cpu()
+    # one-hot inputs are used raw by the kernel: fold any (non-default) one-hot normalisation in
+    W1n = W1 / x_std
+    b1 = model.l1.bias.detach().float().cpu().clone()
+    b1 -= (W1n[:, :8] * x_mean[:8]).sum(1)
+    W1eff = W1.clone()
+    W1eff[:, :8] = W1n[:, :8]
+    w1k = torch.zeros(H, 16)
+    w1k[:, :12] = W1eff
+    w1k[:, 12] = W1eff[:, 10]
+    w1k[:, 13] = W1eff[:, 11]
+    W2 = model.l2.weight.detach().float().cpu()                   # [H,H] (out, in)
+    b2 = model.l2.bias.detach().float().cpu()
+    y_std = float(model.y_std)
+    y_mean = float(model.y_mean)
+    w3 = model.l3.weight.detach().float().cpu().reshape(H) * y_std
+    b3 = float(model.l3.bias.detach().float().cpu().reshape(())) * y_std + y_mean
+
+    lane = np.arange(64)
+    r = lane & 31
+    hh = lane >> 5
+    j = np.arange(8)
+    # w1p[mt][l][j] = W1k[32mt + r][8h + j]
+    rows = (32 * np.arange(MT)[:, None, None] + r[None, :, None])
+    cols = (8 * hh[None, :, None] + j[None, None, :])
+    w1p = w1k.numpy()[rows, np.broadcast_to(cols, (MT, 64, 8))]
+    # w2p[mt][ks][l][j] = W2[32mt + r][16ks + 8(j>>2) + 4h + (j&3)]
+    rows2 = 32 * np.arange(MT)[:, None, None, None] + r[None, None, :, None]
+    cols2 = (16 * np.arange(KS)[None, :, None, None] + 8 * (j >> 2)[None, None, None, :]
+             + 4 * hh[None, None, :, None] + (j & 3)[None, None, None, :])
+    rows2 = np.broadcast_to(rows2, (MT, KS, 64, 8))
+    cols2 = np.broadcast_to(cols2, (MT, KS, 64, 8))
+    w2p = W2.numpy()[rows2, cols2]
+
+    def vec_pack(v: torch.Tensor) -> np.ndarray:
+        vv = v.numpy()
+        out = np.empty((MT, 2, 16), dtype=np.float32)
+        for mt in range(MT):
+            for h in range(2):
+                out[mt, h] = vv[32 * mt + _acc_rows(h)]
+        return out
+
+    def bf16_bytes(a: np.ndarray) -> np.ndarray:
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16)
+        return t.view(torch.int16).numpy().view(np.uint8).reshape(-1)
+
+    parts = [bf16_bytes(w2p), bf16_bytes(w1p),
+             vec_pack(b1).view(np.uint8).reshape(-1),
+             vec_pack(b2).view(np.uint8).reshape(-1),
+             vec_pack(w3).view(np.uint8).reshape(-1)]
+    blob = torch.from_numpy(np.concatenate(parts).copy())
+    assert blob.numel() == 2 * H * H + 44 * H
+    scale = (1.0 / x_std[8:12]).tolist()
+    shift = (-x_mean[8:12] / x_std[8:12]).tolist()
+    return PackedMLP3(H, blob, scale + shift, b3, w1k, b1, W2.clone(), b2.clone(), w3)
+
+
+def records_to_tensor(rec: np.ndarray) -> torch.Tensor:
+    """numpy EtaRecord array -> int32 [B,4] tensor view (16-byte rows)."""
+    rec = np.ascontiguousarray(rec, dtype=RECORD_DTYPE)
+    return torch.from_numpy(rec.view(np.int32).reshape(-1, 4))
+
+
+def featurize_torch(rec_i32: torch.Tensor) -> torch.Tensor:
+    """PyTorch reference of K1 on any device: int32 [B,4] -> R16 features [B,12] fp32."""
+    r = rec_i32
+    dist = r[:, 0].view(torch.float32) if r.dtype == torch.int32 else r[:, 0]
+    age = r[:, 1].view(torch.float32)
+    secs = r[:, 2].to(torch.int64)
+    w = r[:, 3] & 0xFF
+    t = (r[:, 3] >> 8) & 0xFF
+    ar = torch.arange(4, device=r.device)
+    oh_w = (w[:, None] == ar[None]).float()
+    oh_t = (t[:, None] == ar[None]).float()
+    days = torch.div(secs, 86400, rounding_mode="floor")
+    sod = secs - days * 86400
+    wd = torch.remainder(days + 2, 7).float()
+    hr = torch.div(sod, 3600, rounding_mode="floor").float()
+    return torch.cat([oh_w, oh_t, wd[:, None], hr[:, None], (dist / 1000.0)[:, None],
+                      age[:, None]], 1)
+
+
+def emulate_kernel(p: PackedMLP3, rec_i32: torch.Tensor) -> torch.Tensor:
+    """Bit-faithful-ish PyTorch emulation of the kernel numerics (bf16 operands, fp32 acc)."""
+    x = featurize_torch(rec_i32)
+    dev = x.device
+    sc = torch.tensor(p.norm[:4], device=dev)
+    sh = torch.tensor(p.norm[4:], device=dev)
+    num = x[:, 8:12] * sc + sh
+    hi = num.to(torch.bfloat16).float()
+    f = torch.zeros(x.shape[0], 16, device=dev)
+    f[:, :8] = x[:, :8]
+    f[:, 8] = hi[:, 0]
+    f[:, 9] = hi[:, 1]
+    f[:, 10] = hi[:, 2]
+    f[:, 11] = hi[:, 3]
+    f[:, 12] = num[:, 2] - hi[:, 2]
+    f[:, 13] = num[:, 3] - hi[:, 3]
+    bf = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+    h1 = torch.relu(bf(f) @ bf(p.w1k.to(dev)).T + p.b1.to(dev))
+    h2 = torch.relu(bf(h1) @ bf(p.w2.to(dev)).T + p.b2.to(dev))
+    return h2 @ p.w3.to(dev) + p.b3
+
+
+class EtaMlpKernel:
+    """A packed MLP resident on one device; ``__call__(records_i32) -> minutes``.
+
+    On a GPU device this ALWAYS runs the HIP kernel (raises if the extension is missing).
+    On CPU it runs the fp32 PyTorch model (the reference path)."""
+
+    def __init__(self, model: EtaMLP, device: Optional[torch.device] = None, variant: int = -1):
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.model_cpu = model.float().cpu().eval()
+        self.packed = pack_mlp3(self.model_cpu).to(self.device)
+        self.hidden = model.hidden
+        self.variant = variant
+        self._C = _ext.native(required=True) if self.device.type == "cuda" else None
+        if self.device.type == "cuda" and self.hidden not in (64, 128, 256):
+            raise ValueError(f"HIP MLP kernel supports hidden in (64,128,256), got {self.hidden}")
+
+    def __call__(self, rec: torch.Tensor) -> torch.Tensor:
+        if self.device.type == "cuda":
+            return self._C.eta_mlp3_forward(rec, self.packed.blob, self.hidden, self.packed.norm,
+                                            self.packed.b3, self.variant)
+        with torch.no_grad():
+            return self.model_cpu(featurize_torch(rec))

@@ -1,0 +1,88 @@
+"""Numerics of the fused featurize + MLP HIP kernel (K1+K2) against PyTorch fp32 references."""
+import numpy as np
+import pytest
+import torch
+
+from routest_amd.data.synth import synth_records
+from routest_amd.models.features import RECORD_DTYPE, records_to_features
+from routest_amd.models.mlp3 import EtaMLP
+from routest_amd.ops import _ext
+from routest_amd.ops.eta_mlp import (EtaMlpKernel, emulate_kernel, featurize_torch, pack_mlp3,
+                                     records_to_tensor)
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(H, seed=0):
+    torch.manual_seed(seed)
+    m = EtaMLP(H)
+    rec, y = synth_records(4096, seed)
+    m.fit_normalization(records_to_features(rec), y)
+    return m
+
+
+def test_extension_loaded():
+    C = _ext.native(required=True)
+    assert C.ARCH == "gfx950"
+
+
+def test_featurize_kernel_exact():
+    C = _ext.native()
+    rec, _ = synth_records(5000, 3)
+    # include pre-2020 pickups (negative seconds) and unknown categories
+    rec["wallclock_s"][:50] = -np.arange(50, dtype=np.int32) * 40_000 - 1
+    rec["weather"][50:60] = 255
+    rec["traffic"][60:70] = 7
+    rt = records_to_tensor(rec)
+    got = C.eta_featurize(rt.cuda()).cpu()
+    ref = torch.from_numpy(records_to_features(rec))
+    assert torch.equal(got, ref)
+    assert torch.equal(featurize_torch(rt), ref)
+
+
+@pytest.mark.parametrize("H", [64, 128, 256])
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("B", [1, 31, 33, 1000, 70_001])
+def test_mlp3_forward_matches_fp32(H, variant, B):
+    m = _model(H)
+    k = EtaMlpKernel(m, torch.device("cuda:0"), variant=variant)
+    rec, _ = synth_records(B, 7)
+    rt = records_to_tensor(rec)
+    got = k(rt.cuda())
+    torch.cuda.synchronize()
+    got = got.cpu()
+    ref = m(torch.from_numpy(records_to_features(rec))).detach()
+    emu = emulate_kernel(k.packed.to("cpu"), rt)
+    assert got.shape == (B,)
+    assert torch.isfinite(got).all()
+    # vs the kernel-numerics emulation: only accumulation order differs
+    torch.testing.assert_close(got, emu, rtol=2e-3, atol=2e-3)
+    # vs the fp32 model: bf16 tolerance
+    torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
+
+
+def test_mlp3_forward_deterministic():
+    m = _model(256, 1)
+    k = EtaMlpKernel(m, torch.device("cuda:0"), variant=1)
+    rec, _ = synth_records(100_000, 9)
+    rt = records_to_tensor(rec).cuda()
+    a = k(rt)
+    b = k(rt)
+    assert torch.equal(a, b)
+
+
+def test_mlp3_forward_graph_capture():
+    m = _model(128, 2)
+    k = EtaMlpKernel(m, torch.device("cuda:0"), variant=0)
+    rec, _ = synth_records(512, 4)
+    rt = records_to_tensor(rec).cuda()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        k(rt)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = k(rt)
+    g.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, k(rt))

@@ -1,0 +1,121 @@
+#!/usr/bin/env python3
+"""In-tree build of the native extensions (no torch JIT cache, no hipify step).
+
+* ``routest_amd/_C*.so``  — gfx950 HIP kernels (csrc/*.hip, hipcc --offload-arch=gfx950) + the
+  torch binding TU (csrc/bindings.cpp).  Loaded by :mod:`routest_amd.ops`.
+* ``routest_amd/_rt*.so`` — CPU-only C++ runtime (csrc/runtime/*.cpp, g++ + pybind11):
+  greedy-CVRP reference, request packing, micro-batch queue.  Works on machines without a GPU.
+
+Incremental: an object is rebuilt only when its source or any header is newer.
+Usage: ``python tools/build_ext.py [--force] [--jobs N] [--only C|rt]``.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from typing import List
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+PKG = os.path.join(ROOT, "routest_amd")
+BUILD = os.path.join(ROOT, "build", "native")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension as ce
+    inc = ce.include_paths()
+    libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, libdir, abi
+
+
+def _newer(target: str, deps: List[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _run(cmd: List[str]) -> None:
+    print("+", " ".join(cmd[:6]), "...", cmd[-1], flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout)
+        raise SystemExit(f"build failed: {' '.join(cmd)}")
+
+
+def build_C(force: bool = False, jobs: int = 8) -> str:
+    inc, libdir, abi = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    os.makedirs(BUILD, exist_ok=True)
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    hip_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}"]
+    jobs_list = []
+    objs = []
+    for src in hip_srcs:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _newer(obj, [src] + headers):
+            jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics",
+                              "-I", CSRC, "-c", src, "-o", obj])
+    bsrc = os.path.join(CSRC, "bindings.cpp")
+    bobj = os.path.join(BUILD, "bindings.cpp.o")
+    objs.append(bobj)
+    if force or _newer(bobj, [bsrc] + headers):
+        cmd = [hipcc, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+               "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+               "-I", CSRC, "-I", py_inc]
+        for d in inc:
+            cmd += ["-I", d]
+        cmd += ["-Wno-unused-result", "-Wno-deprecated-declarations", "-c", bsrc, "-o", bobj]
+        jobs_list.append(cmd)
+    with ThreadPoolExecutor(max(1, jobs)) as ex:
+        list(ex.map(_run, jobs_list))
+    out = os.path.join(PKG, "_C" + EXT_SUFFIX)
+    if force or jobs_list or _newer(out, objs):
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, *objs,
+              "-L", libdir, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+              "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{libdir}"])
+    return out
+
+
+def build_rt(force: bool = False, jobs: int = 8) -> str:
+    import pybind11
+    py_inc = sysconfig.get_paths()["include"]
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    headers = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
+    out = os.path.join(PKG, "_rt" + EXT_SUFFIX)
+    if not srcs:
+        return ""
+    if force or _newer(out, srcs + headers):
+        _run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-pthread",
+              "-I", pybind11.get_include(), "-I", py_inc, "-I", os.path.join(CSRC, "runtime"),
+              *srcs, "-o", out])
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--only", choices=["C", "rt"], default=None)
+    a = ap.parse_args()
+    if a.only in (None, "rt"):
+        print("built", build_rt(a.force, a.jobs))
+    if a.only in (None, "C"):
+        print("built", build_C(a.force, a.jobs))
+
+
+if __name__ == "__main__":
+    main()
