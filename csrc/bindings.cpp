@@ -79,6 +79,50 @@ torch::Tensor eta_featurize(torch::Tensor records) {
   return out;
 }
 
+torch::Tensor route_haversine_matrix(torch::Tensor lat, torch::Tensor lon, torch::Tensor npts,
+                                     double circuity) {
+  check_dev(lat, "lat");
+  check_dev(lon, "lon");
+  check_dev(npts, "npts");
+  TORCH_CHECK(lat.scalar_type() == torch::kFloat64 && lat.dim() == 2, "lat must be f64 [R,NM]");
+  TORCH_CHECK(lon.sizes() == lat.sizes() && lon.scalar_type() == torch::kFloat64, "lon mismatch");
+  TORCH_CHECK(npts.scalar_type() == torch::kInt32 && npts.numel() == lat.size(0), "npts mismatch");
+  const c10::DeviceGuard guard(lat.device());
+  const int R = (int)lat.size(0), NM = (int)lat.size(1);
+  auto D = torch::empty({R, NM, NM}, lat.options());
+  RT_CHECK_HIP(rt::launch_haversine_matrix(lat.data_ptr<double>(), lon.data_ptr<double>(),
+                                           npts.data_ptr<int>(), R, NM, circuity,
+                                           D.data_ptr<double>(), cur_stream(lat)));
+  return D;
+}
+
+std::vector<torch::Tensor> route_greedy_cvrp(torch::Tensor D, torch::Tensor npts,
+                                             torch::Tensor demand, torch::Tensor cap,
+                                             torch::Tensor maxd) {
+  for (auto* t : {&D, &npts, &demand, &cap, &maxd}) check_dev(*t, "route tensor");
+  TORCH_CHECK(D.scalar_type() == torch::kFloat64 && D.dim() == 3 && D.size(1) == D.size(2),
+              "D must be f64 [R,NM,NM]");
+  const int R = (int)D.size(0), NM = (int)D.size(1);
+  TORCH_CHECK(NM <= 4096, "at most 4095 stops per request");
+  TORCH_CHECK(npts.scalar_type() == torch::kInt32 && npts.numel() == R, "npts must be i32 [R]");
+  TORCH_CHECK(demand.scalar_type() == torch::kFloat64 && demand.numel() == (int64_t)R * NM,
+              "demand must be f64 [R,NM]");
+  TORCH_CHECK(cap.scalar_type() == torch::kFloat64 && cap.numel() == R, "cap must be f64 [R]");
+  TORCH_CHECK(maxd.scalar_type() == torch::kFloat64 && maxd.numel() == R, "maxd must be f64 [R]");
+  const c10::DeviceGuard guard(D.device());
+  auto iopt = D.options().dtype(torch::kInt32);
+  auto visit = torch::empty({R, NM}, iopt);
+  auto trip_of = torch::empty({R, NM}, iopt);
+  auto ntrips = torch::empty({R}, iopt);
+  auto status = torch::empty({R}, iopt);
+  RT_CHECK_HIP(rt::launch_greedy_cvrp(D.data_ptr<double>(), npts.data_ptr<int>(),
+                                      demand.data_ptr<double>(), cap.data_ptr<double>(),
+                                      maxd.data_ptr<double>(), R, NM, visit.data_ptr<int>(),
+                                      trip_of.data_ptr<int>(), ntrips.data_ptr<int>(),
+                                      status.data_ptr<int>(), cur_stream(D)));
+  return {visit, trip_of, ntrips, status};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -86,5 +130,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("eta_mlp3_forward", &eta_mlp3_forward, "fused featurize + 3-layer MLP forward (bf16 MFMA)");
   m.def("eta_featurize", &eta_featurize, "K1: packed records -> R16 features [B,12] fp32");
   m.def("eta_mlp3_blob_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_blob_bytes((int)H); });
+  m.def("route_haversine_matrix", &route_haversine_matrix, "K5: batched haversine matrices (f64)");
+  m.def("route_greedy_cvrp", &route_greedy_cvrp, "K6: batched greedy multi-trip CVRP");
   m.attr("ARCH") = "gfx950";
 }

@@ -16,4 +16,11 @@ hipError_t launch_eta_mlp3_fwd(const void* rec, float* out, int B, const void* b
                                hipStream_t stream);
 hipError_t launch_eta_featurize(const void* rec, float* out, int B, hipStream_t stream);
 
+// ---- batched routing (K5 distance matrix + K6 greedy CVRP) : route_kernels.hip ----
+hipError_t launch_haversine_matrix(const double* lat, const double* lon, const int* npts, int R,
+                                   int NM, double circuity, double* D, hipStream_t stream);
+hipError_t launch_greedy_cvrp(const double* D, const int* npts, const double* demand,
+                              const double* cap, const double* maxd, int R, int NM, int* visit,
+                              int* trip_of, int* ntrips, int* status, hipStream_t stream);
+
 }  // namespace rt

@@ -1,0 +1,372 @@
+"""HTTP API: the reference's 11 Flask routes under ``/api`` (``RO/Flaskr/routes.py``) + SSE mount
+(``RO/Flaskr/__init__.py:28``), re-implemented on FastAPI/ASGI, plus the north-star aliases
+``POST /predict`` (single or batched) and ``POST /route``, ``/metrics`` and admin endpoints.
+
+Wire compatibility notes:
+* ``/api/request_route`` returns **200** with an ``{"error": ...}`` body (quirk #1, behind
+  ``compat_request_route_200``); ``/api/optimize_route`` returns 400 on errors.
+* ``/api/predict_eta`` returns 503 ``{"error": "model unavailable"}`` without a model.
+* ``/api/health`` is always HTTP 200 with keys ``backend, checks{engine,redis,supabase}, db, osrm,
+  redis, tiles, status, version`` (+ ``gpu``, ``model``).
+* ``/api/history`` without a store returns 503 like the detail route (fix #6; ``compat_history_500``
+  restores the reference's 500).
+* The SSE stream speaks Flask-SSE's wire format on ``/api/realtime_feed?channel=``.
+"""
+from __future__ import annotations
+
+import asyncio
+import datetime as dt
+import json
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+from fastapi import FastAPI, Request
+from fastapi.middleware.cors import CORSMiddleware
+from fastapi.responses import JSONResponse, PlainTextResponse, Response, StreamingResponse
+from starlette.concurrency import run_in_threadpool
+
+from ..config import Settings, get_settings
+from ..realtime.broker import MemoryBroker, Simulator, format_sse_data, make_broker
+from ..routing.optimizer import optimize_many, optimize_route
+from ..routing.providers import HaversineProvider, ORSProvider
+from ..serve.eta_service import EtaService
+from ..store.store import StoreUnavailable, open_store
+from ..utils.logging import get_logger
+from ..utils.metrics import REGISTRY
+
+log = get_logger("api")
+
+
+@dataclass
+class Services:
+    settings: Settings
+    eta: EtaService
+    provider: Any
+    store: Any
+    broker: MemoryBroker
+    simulator: Simulator
+    route_device: Optional[Any] = None
+    started: float = field(default_factory=time.time)
+
+
+def build_services(settings: Optional[Settings] = None, eta: Optional[EtaService] = None,
+                   provider: Any = None, store: Any = "default") -> Services:
+    s = settings or get_settings()
+    if eta is None:
+        model_path = s.default_model_dir or s.eta_model_path
+        import os
+        eta = EtaService(model_path=model_path, device=s.device, devices=s.devices,
+                         batch_max=s.batch_max, timeout_us=s.batch_timeout_us,
+                         allow_pickle=os.environ.get("ROUTEST_ALLOW_PICKLE") == "1")
+    if provider is None:
+        if s.provider == "ors" and s.ors_api_key:
+            provider = ORSProvider(s.ors_api_key)
+        elif s.provider == "graph":
+            from ..routing.graph import GraphProvider
+            provider = GraphProvider.synthetic()
+        else:
+            provider = HaversineProvider()
+    if store == "default":
+        store = open_store(s.store_url, s.supabase_url, s.supabase_service_key)
+    broker = make_broker(s.broker, s.redis_url)
+    sim = Simulator(broker, s.sim_tick_min_s, s.sim_tick_max_s, s.max_simulations, s.sse_delta)
+    route_device = None
+    try:
+        import torch
+        if s.device != "cpu" and torch.cuda.is_available():
+            route_device = torch.device("cuda", (s.devices or [0])[0])
+    except Exception:
+        pass
+    return Services(s, eta, provider, store, broker, sim, route_device)
+
+
+class _MetricsASGI:
+    """Pure-ASGI timing middleware (cheaper than BaseHTTPMiddleware)."""
+
+    def __init__(self, app):
+        self.app = app
+
+    async def __call__(self, scope, receive, send):
+        if scope["type"] != "http":
+            return await self.app(scope, receive, send)
+        t0 = time.perf_counter()
+        status = {"code": 500}
+
+        async def _send(msg):
+            if msg["type"] == "http.response.start":
+                status["code"] = msg["status"]
+            await send(msg)
+        try:
+            await self.app(scope, receive, _send)
+        finally:
+            path = scope.get("path", "")
+            if not path.startswith("/api/realtime_feed"):
+                REGISTRY.latency.observe(time.perf_counter() - t0)
+            REGISTRY.requests.inc(route=path if path.count("/") <= 2 else path.rsplit("/", 1)[0],
+                                  status=str(status["code"]))
+
+
+async def _json_body(request: Request, silent: bool):
+    """Flask ``get_json()`` semantics: non-silent -> 415 on non-JSON content type, 400 on bad JSON;
+    silent -> None on either."""
+    ctype = request.headers.get("content-type", "")
+    raw = await request.body()
+    if "json" not in ctype.lower():
+        if silent:
+            return None
+        return JSONResponse({"error": "Unsupported Media Type: expected application/json"}, 415)
+    try:
+        return json.loads(raw) if raw else None
+    except ValueError:
+        if silent:
+            return None
+        return JSONResponse({"error": "Bad Request: failed to decode JSON object"}, 400)
+
+
+def create_app(services: Optional[Services] = None, settings: Optional[Settings] = None) -> FastAPI:
+    sv = services or build_services(settings)
+    s = sv.settings
+
+    from contextlib import asynccontextmanager
+
+    @asynccontextmanager
+    async def lifespan(_app):
+        yield
+        await sv.simulator.shutdown()
+        sv.eta.close()
+
+    app = FastAPI(title="routest_amd", version="1.0", lifespan=lifespan)
+    app.state.services = sv
+    app.add_middleware(CORSMiddleware, allow_origins=s.cors_origins,
+                       allow_origin_regex=s.cors_origin_regex, allow_credentials=True,
+                       allow_methods=["*"], allow_headers=["*"])
+    app.add_middleware(_MetricsASGI)
+
+    # ------------------------------------------------------------------ routing
+    @app.post("/api/request_route")
+    async def request_route(request: Request):
+        data = await _json_body(request, silent=False)
+        if isinstance(data, Response):
+            return data
+        result = await run_in_threadpool(optimize_route, data, sv.provider, s.engine_name)
+        if not result:
+            return JSONResponse({"error": "no response acquired from the optimizer."}, 400)
+        if isinstance(result, dict) and result.get("error") and not s.compat_request_route_200:
+            return JSONResponse(result, 400)
+        return JSONResponse(result, 200)
+
+    async def _optimize(request: Request):
+        payload = await _json_body(request, silent=True) or {}
+        if not isinstance(payload, dict):
+            payload = {}
+        result = await run_in_threadpool(optimize_route, payload, sv.provider, s.engine_name)
+        if isinstance(result, dict) and result.get("error"):
+            return JSONResponse(result, 400)
+        if payload.get("use_ml_eta"):
+            props = result.setdefault("properties", {}) or {}
+            summary = props.get("summary", {}) or {}
+            try:
+                distance_m = float(summary.get("distance") or 0)
+                ctx = payload.get("context") or {}
+                driver_age = float((payload.get("driver_details") or {}).get("driver_age", 30))
+                eta_min, eta_iso = await sv.eta.apredict(
+                    weather=ctx.get("weather", "Sunny"), traffic=ctx.get("traffic", "Low"),
+                    distance_m=distance_m, pickup_time=dt.datetime.now(), driver_age=driver_age)
+            except (TypeError, ValueError):
+                eta_min, eta_iso = None, None
+            if eta_min is not None:
+                props["eta_minutes_ml"] = eta_min
+                props["eta_completion_time_ml"] = eta_iso
+        if sv.store is not None:
+            try:
+                rid = await run_in_threadpool(sv.store.persist_request_and_result, payload, result)
+                if rid:
+                    result.setdefault("properties", {})["request_id"] = rid
+                    result["properties"]["saved"] = True
+            except Exception as e:  # best-effort persistence (routes.py:119-125)
+                log.warning("Persist failed: %r", e)
+        return JSONResponse(result, 200)
+
+    app.post("/api/optimize_route")(_optimize)
+    app.post("/route")(_optimize)
+
+    @app.post("/api/optimize_routes_batch")
+    async def optimize_batch(request: Request):
+        """Many independent requests in one call: K5+K6 batched on the GPU."""
+        body = await _json_body(request, silent=True)
+        reqs = body.get("requests") if isinstance(body, dict) else body
+        if not isinstance(reqs, list):
+            return JSONResponse({"error": "expected a JSON array of route requests"}, 400)
+        res = await run_in_threadpool(optimize_many, reqs, sv.provider, s.engine_name, sv.route_device)
+        return JSONResponse({"results": res}, 200)
+
+    # ------------------------------------------------------------------ ETA
+    async def _predict_one(body: Dict[str, Any]):
+        summary = body.get("summary") or {}
+        pickup = body.get("pickup_time") or dt.datetime.now().isoformat()
+        try:
+            driver_age = float(body.get("driver_age", 30))
+            distance_m = float(summary.get("distance") or 0) if isinstance(summary, dict) else 0.0
+            if isinstance(pickup, str):
+                from ..utils.timeutil import parse_iso
+                parse_iso(pickup)
+        except (TypeError, ValueError) as e:
+            return None, None, f"invalid input: {e}"
+        if not sv.eta.available:
+            return None, None, None
+        m, iso = await sv.eta.apredict(weather=body.get("weather", "Sunny"),
+                                       traffic=body.get("traffic", "Low"), distance_m=distance_m,
+                                       pickup_time=pickup, driver_age=driver_age)
+        return m, iso, None
+
+    @app.post("/api/predict_eta")
+    async def predict_eta(request: Request):
+        body = await _json_body(request, silent=True) or {}
+        if not isinstance(body, dict):
+            body = {}
+        m, iso, err = await _predict_one(body)
+        if err:
+            return JSONResponse({"error": err}, 400)
+        if m is None:
+            return JSONResponse({"error": "model unavailable"}, 503)
+        REGISTRY.preds.inc()
+        return JSONResponse({"eta_minutes_ml": m, "eta_completion_time_ml": iso}, 200)
+
+    @app.post("/predict")
+    async def predict(request: Request):
+        body = await _json_body(request, silent=True)
+        items = body if isinstance(body, list) else (body.get("items") if isinstance(body, dict) and
+                                                     isinstance(body.get("items"), list) else None)
+        if items is None:
+            return await predict_eta(request)
+        res = await asyncio.gather(*[_predict_one(b if isinstance(b, dict) else {}) for b in items])
+        if any(m is None and err is None for m, _, err in res):
+            return JSONResponse({"error": "model unavailable"}, 503)
+        REGISTRY.preds.inc(len(items))
+        return JSONResponse({"predictions": [
+            {"error": err} if err else {"eta_minutes_ml": m, "eta_completion_time_ml": iso}
+            for m, iso, err in res]}, 200)
+
+    @app.post("/api/admin/reload_model")
+    async def reload_model(request: Request):
+        body = await _json_body(request, silent=True) or {}
+        path = body.get("path") if isinstance(body, dict) else None
+        ok = await run_in_threadpool(sv.eta.reload, path)
+        return JSONResponse({"ok": ok, "model": sv.eta.describe()}, 200 if ok else 503)
+
+    # ------------------------------------------------------------------ realtime
+    @app.post("/api/confirm_route")
+    async def confirm_route(request: Request):
+        data = await _json_body(request, silent=False)
+        if isinstance(data, Response):
+            return data
+        if not isinstance(data, dict) or not sv.simulator.start(data):
+            if isinstance(data, dict):
+                return JSONResponse({"error": "too many active simulations"}, 503)
+        return JSONResponse({"status": "route simulation initialized."}, 200)
+
+    @app.post("/api/update_tracker")
+    async def update_tracker(request: Request):
+        data = await _json_body(request, silent=False)
+        if isinstance(data, Response):
+            return data
+        if not data:
+            return JSONResponse({"error": "no data provided in the publish request."}, 400)
+        try:
+            msg = format_sse_data(data)
+        except (KeyError, TypeError, ValueError) as e:
+            return JSONResponse({"error": f"invalid tracker payload: {e!r}"}, 400)
+        sv.broker.publish(msg, channel=f"{data.get('route_id')}")
+        return JSONResponse({"status": "published"}, 200)
+
+    @app.get("/api/realtime_feed")
+    async def realtime_feed(request: Request, channel: str = "sse"):
+        q = sv.broker.subscribe(channel)
+
+        async def gen():
+            try:
+                yield ": connected\n\n"
+                while True:
+                    try:
+                        msg = await asyncio.wait_for(q.get(), timeout=15.0)
+                        yield msg
+                    except asyncio.TimeoutError:
+                        yield ": keep-alive\n\n"
+                    if await request.is_disconnected():
+                        break
+            finally:
+                sv.broker.unsubscribe(channel, q)
+        return StreamingResponse(gen(), media_type="text/event-stream",
+                                 headers={"Cache-Control": "no-cache", "X-Accel-Buffering": "no"})
+
+    # ------------------------------------------------------------------ misc
+    @app.get("/api/ping")
+    async def ping():
+        return JSONResponse({"ok": True, "service": "route-optimizer"}, 200)
+
+    @app.get("/api/health")
+    async def health():
+        from .health import health_payload
+        return JSONResponse(await run_in_threadpool(health_payload, sv), 200)
+
+    @app.get("/api/locations")
+    async def locations():
+        if sv.store is not None and hasattr(sv.store, "locations"):
+            try:
+                return JSONResponse(await run_in_threadpool(sv.store.locations), 200)
+            except Exception as e:
+                return JSONResponse({"error": str(e)}, 500)
+        from ..data.synth import seed_locations
+        return JSONResponse(seed_locations(), 200)
+
+    @app.get("/metrics")
+    async def metrics():
+        return PlainTextResponse(REGISTRY.render(), media_type="text/plain; version=0.0.4")
+
+    # ------------------------------------------------------------------ history
+    def _no_store() -> JSONResponse:
+        if s.compat_history_500:
+            return JSONResponse({"error": "supabase fetch failed (status n/a): not configured"}, 500)
+        return JSONResponse({"error": "history disabled: SUPABASE not configured"}, 503)
+
+    @app.get("/api/history")
+    async def history(limit: str = "20"):
+        try:
+            lim = int(limit)
+        except ValueError:
+            lim = 20
+        lim = max(1, min(lim, 100))
+        if sv.store is None:
+            return _no_store()
+        try:
+            items = await run_in_threadpool(sv.store.history, lim)
+        except Exception as e:
+            return JSONResponse({"error": f"history fetch failed: {e}"}, 500)
+        return JSONResponse({"items": items}, 200)
+
+    @app.get("/api/history/{req_id}")
+    async def history_detail(req_id: str):
+        if sv.store is None:
+            return JSONResponse({"error": "history disabled: SUPABASE not configured"}, 503)
+        try:
+            d = await run_in_threadpool(sv.store.history_detail, req_id)
+        except Exception as e:
+            return JSONResponse({"error": f"history fetch failed: {e}"}, 500)
+        if d is None:
+            return JSONResponse({"error": "not found"}, 404)
+        return JSONResponse(d, 200)
+
+    @app.delete("/api/history/{req_id}")
+    async def delete_history(req_id: str):
+        if sv.store is None:
+            return JSONResponse({"error": "history disabled: SUPABASE not configured"}, 503)
+        try:
+            await run_in_threadpool(sv.store.delete, req_id)
+        except StoreUnavailable as e:
+            return JSONResponse({"error": str(e)}, 500)
+        except Exception as e:
+            return JSONResponse({"error": f"delete failed: {e}"}, 500)
+        return Response(status_code=204)
+
+    return app
