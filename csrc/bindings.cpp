@@ -41,7 +41,7 @@ void check_dev(const torch::Tensor& t, const char* name) {
 }
 
 torch::Tensor eta_mlp3_forward(torch::Tensor records, torch::Tensor blob, int64_t H,
-                               std::vector<double> norm, double b3, int64_t variant) {
+                               std::vector<double> norm, int64_t variant) {
   check_dev(records, "records");
   check_dev(blob, "blob");
   TORCH_CHECK(records.scalar_type() == torch::kInt32 && records.dim() == 2 && records.size(1) == 4,
@@ -62,7 +62,7 @@ torch::Tensor eta_mlp3_forward(torch::Tensor records, torch::Tensor blob, int64_
     np.shift[i] = (float)norm[4 + i];
   }
   RT_CHECK_HIP(rt::launch_eta_mlp3_fwd(records.data_ptr(), out.data_ptr<float>(), B,
-                                       blob.data_ptr(), (int)H, np, (float)b3, (int)variant,
+                                       blob.data_ptr(), (int)H, np, (int)variant,
                                        num_cus(records.device().index()), cur_stream(records)));
   return out;
 }
@@ -123,6 +123,92 @@ std::vector<torch::Tensor> route_greedy_cvrp(torch::Tensor D, torch::Tensor npts
   return {visit, trip_of, ntrips, status};
 }
 
+rt::NormParams norm_from(const std::vector<double>& norm) {
+  TORCH_CHECK(norm.size() == 8, "norm must hold 4 scales + 4 shifts");
+  rt::NormParams np;
+  for (int i = 0; i < 4; ++i) {
+    np.scale[i] = (float)norm[i];
+    np.shift[i] = (float)norm[4 + i];
+  }
+  return np;
+}
+
+void check_bf16(const torch::Tensor& t, const char* name, int64_t rows, int64_t cols) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.numel() == rows * cols, name, " must have ", rows, "x", cols, " elements");
+}
+
+// Writes every output in place (static buffers: the step is HIP-graph capturable).
+void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tensor blob, int64_t H,
+                        std::vector<double> norm, double gscale, torch::Tensor xf,
+                        torch::Tensor h1a, torch::Tensor h2a, torch::Tensor dz2, torch::Tensor dyb,
+                        torch::Tensor loss_tiles, torch::Tensor step_ctr) {
+  check_dev(records, "records");
+  check_dev(target, "target");
+  check_dev(blob, "blob");
+  TORCH_CHECK(records.scalar_type() == torch::kInt32 && records.dim() == 2 && records.size(1) == 4,
+              "records must be int32 [B,4]");
+  const int64_t B = records.size(0);
+  TORCH_CHECK(target.scalar_type() == torch::kFloat32 && target.numel() == B, "target must be f32 [B]");
+  TORCH_CHECK(blob.scalar_type() == torch::kUInt8 &&
+              (size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
+  check_bf16(xf, "xf", B, 16);
+  check_bf16(h1a, "h1a", B, H + 16);
+  check_bf16(h2a, "h2a", B, H + 16);
+  check_bf16(dz2, "dz2", B, H);
+  check_bf16(dyb, "dyb", B, 1);
+  check_dev(loss_tiles, "loss_tiles");
+  TORCH_CHECK(loss_tiles.scalar_type() == torch::kFloat32 && loss_tiles.numel() >= (B + 31) / 32,
+              "loss_tiles must be f32 [ceil(B/32)]");
+  check_dev(step_ctr, "step_ctr");
+  TORCH_CHECK(step_ctr.scalar_type() == torch::kInt32 && step_ctr.numel() >= 1, "step_ctr i32");
+  const c10::DeviceGuard guard(records.device());
+  RT_CHECK_HIP(rt::launch_eta_mlp3_train_fwd(
+      records.data_ptr(), target.data_ptr<float>(), (int)B, blob.data_ptr(), (int)H,
+      norm_from(norm), (float)gscale, xf.data_ptr(), h1a.data_ptr(), h2a.data_ptr(),
+      dz2.data_ptr(), dyb.data_ptr(), loss_tiles.data_ptr<float>(), step_ctr.data_ptr<int>(),
+      num_cus(records.device().index()), cur_stream(records)));
+}
+
+void relu_bwd(torch::Tensor dh1, torch::Tensor h1a, torch::Tensor dz1) {
+  check_dev(dh1, "dh1");
+  check_dev(h1a, "h1a");
+  check_dev(dz1, "dz1");
+  TORCH_CHECK(dh1.dim() == 2 && dh1.sizes() == dz1.sizes(), "dh1/dz1 shape");
+  const int64_t B = dh1.size(0), H = dh1.size(1);
+  TORCH_CHECK(H % 8 == 0 && h1a.size(0) == B && h1a.size(1) >= H, "h1a shape");
+  TORCH_CHECK(dh1.scalar_type() == torch::kBFloat16 && h1a.scalar_type() == torch::kBFloat16 &&
+              dz1.scalar_type() == torch::kBFloat16, "bf16 tensors expected");
+  const c10::DeviceGuard guard(dh1.device());
+  RT_CHECK_HIP(rt::launch_relu_bwd(dh1.data_ptr(), h1a.data_ptr(), (int)h1a.size(1),
+                                   dz1.data_ptr(), (int)B, (int)H, cur_stream(dh1)));
+}
+
+void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor V,
+                torch::Tensor blob, torch::Tensor w2bf, torch::Tensor step, int64_t H, double lr,
+                double beta1, double beta2, double eps, double wd, int64_t warmup,
+                int64_t total_steps, double min_lr_ratio, bool update) {
+  const int64_t N = rt::mlp3_num_params((int)H);
+  for (auto* t : {&P, &M, &V}) {
+    check_dev(*t, "adam state");
+    TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->numel() == N, "P/M/V must be f32 [", N, "]");
+  }
+  check_dev(G, "G");
+  TORCH_CHECK(G.scalar_type() == torch::kFloat32 && G.numel() == rt::mlp3_grad_bucket_floats((int)H),
+              "G must be the flat f32 gradient bucket");
+  TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
+  check_bf16(w2bf, "w2bf", H, H);
+  check_dev(step, "step");
+  const c10::DeviceGuard guard(P.device());
+  RT_CHECK_HIP(rt::launch_adamw_pack(P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(),
+                                     V.data_ptr<float>(), blob.data_ptr(), w2bf.data_ptr(),
+                                     step.data_ptr<int>(), (int)H, (float)lr, (float)beta1,
+                                     (float)beta2, (float)eps, (float)wd, (int)warmup,
+                                     (int)total_steps, (float)min_lr_ratio, update ? 1 : 0,
+                                     cur_stream(P)));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -132,5 +218,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("eta_mlp3_blob_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_blob_bytes((int)H); });
   m.def("route_haversine_matrix", &route_haversine_matrix, "K5: batched haversine matrices (f64)");
   m.def("route_greedy_cvrp", &route_greedy_cvrp, "K6: batched greedy multi-trip CVRP");
+  m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad");
+  m.def("relu_bwd", &relu_bwd, "dz1 = dh1 * (h1 > 0)");
+  m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + MFMA fragment re-pack");
+  m.def("mlp3_num_params", [](int64_t H) { return (int64_t)rt::mlp3_num_params((int)H); });
+  m.def("mlp3_grad_bucket_floats", [](int64_t H) { return (int64_t)rt::mlp3_grad_bucket_floats((int)H); });
   m.attr("ARCH") = "gfx950";
 }

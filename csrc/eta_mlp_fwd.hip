@@ -22,44 +22,24 @@
 //   LDSW = false: weights read straight from global (L2-resident, lane-linear 1 KiB per wave
 //                 instruction) — for small serving batches where staging 139 KiB per CU would
 //                 dominate.
-#include "common.h"
+#include "mlp3_tile.h"
 #include "ops.h"
 
 namespace rt {
 
-template <int H>
-struct Mlp3Layout {
-  static constexpr int MT = H / 32;   // 32-row hidden tiles
-  static constexpr int KS = H / 16;   // 16-deep k-steps over the hidden dim
-  static constexpr size_t W2B = (size_t)H * H * 2;
-  static constexpr size_t W1B = (size_t)H * 16 * 2;
-  static constexpr size_t VB = (size_t)H * 4;
-  static constexpr size_t BLOB = W2B + W1B + 3 * VB;
-};
-
 template <int H, bool LDSW>
-__global__ __launch_bounds__(LDSW ? 512 : 256, LDSW ? 2 : 1) void eta_mlp3_fwd_kernel(const int4* __restrict__ rec,
-                                                              float* __restrict__ out, int B,
-                                                              const unsigned char* __restrict__ blob,
-                                                              NormParams np, float b3) {
-  using L = Mlp3Layout<H>;
-  constexpr int MT = L::MT, KS = L::KS;
+__global__ __launch_bounds__(LDSW ? 512 : 256, LDSW ? 2 : 1) void eta_mlp3_fwd_kernel(
+    const int4* __restrict__ rec, float* __restrict__ out, int B,
+    const unsigned char* __restrict__ blob, NormParams np) {
+  constexpr int MT = H / 32, KS = H / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
   const unsigned char* base = blob;
   if constexpr (LDSW) {
-    const int4* src = reinterpret_cast<const int4*>(blob);
-    int4* dst = reinterpret_cast<int4*>(smem);
-    constexpr int N16 = (int)(L::BLOB / 16);
-    for (int i = threadIdx.x; i < N16; i += blockDim.x) dst[i] = src[i];
-    __syncthreads();
+    stage_blob<H>(blob, smem);
     base = smem;
   }
-  const bf16x8* w2p = reinterpret_cast<const bf16x8*>(base);
-  const bf16x8* w1p = reinterpret_cast<const bf16x8*>(base + L::W2B);
-  const f32x4* b1p = reinterpret_cast<const f32x4*>(base + L::W2B + L::W1B);
-  const f32x4* b2p = b1p + H / 4;
-  const f32x4* w3p = b2p + H / 4;
+  const Mlp3View<H> w(base);
+  const float b3 = w.tail[0];
 
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
@@ -75,54 +55,17 @@ __global__ __launch_bounds__(LDSW ? 512 : 256, LDSW ? 2 : 1) void eta_mlp3_fwd_k
     featurize_f32(rc, h, np, f);
     const bf16x8 xb = to_bf16x8(f);
 
-    // ---- layer 1: h1^T = relu(W1k x^T + b1), kept as bf16 B fragments ----
     bf16x8 h1[KS];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      f32x16 acc;
-      const f32x4* bp = b1p + (mt * 2 + h) * 4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 bv = bp[q];
-        acc[4 * q + 0] = bv[0];
-        acc[4 * q + 1] = bv[1];
-        acc[4 * q + 2] = bv[2];
-        acc[4 * q + 3] = bv[3];
-      }
-      acc = mfma32(w1p[mt * 64 + lane], xb, acc);
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) h1[2 * mt + s][j] = (__bf16)fmaxf(acc[8 * s + j], 0.f);
-      }
-    }
+    mlp3_layer1<H>(w, xb, lane, h, h1);
 
-    // ---- layer 2 + fused layer 3 ----
+    // layer 2 + fused layer 3 (relu(acc) . w3 reduced in registers)
     float ys = 0.f;
 #pragma unroll 1
     for (int mt = 0; mt < MT; ++mt) {
-      f32x16 acc;
-      const f32x4* bp = b2p + (mt * 2 + h) * 4;
+      const f32x16 acc = mlp3_layer2_tile<H>(w, h1, mt, lane, h);
+      const f32x16 w3 = load_vec16(w.w3p, mt, h);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 bv = bp[q];
-        acc[4 * q + 0] = bv[0];
-        acc[4 * q + 1] = bv[1];
-        acc[4 * q + 2] = bv[2];
-        acc[4 * q + 3] = bv[3];
-      }
-      const bf16x8* wa = w2p + (size_t)mt * KS * 64 + lane;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) acc = mfma32(wa[ks * 64], h1[ks], acc);
-      const f32x4* wp = w3p + (mt * 2 + h) * 4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 wv = wp[q];
-        ys += fmaxf(acc[4 * q + 0], 0.f) * wv[0];
-        ys += fmaxf(acc[4 * q + 1], 0.f) * wv[1];
-        ys += fmaxf(acc[4 * q + 2], 0.f) * wv[2];
-        ys += fmaxf(acc[4 * q + 3], 0.f) * wv[3];
-      }
+      for (int i = 0; i < 16; ++i) ys += fmaxf(acc[i], 0.f) * w3[i];
     }
     ys += __shfl_xor(ys, 32);
     if (h == 0 && row < B) out[row] = ys + b3;
@@ -145,8 +88,7 @@ __global__ __launch_bounds__(256) void eta_featurize_kernel(const int4* __restri
 
 template <int H>
 static hipError_t launch_fwd_h(const void* rec, float* out, int B, const void* blob,
-                               const NormParams& np, float b3, int variant, int num_cus,
-                               hipStream_t stream) {
+                               const NormParams& np, int variant, int num_cus, hipStream_t stream) {
   using L = Mlp3Layout<H>;
   const int ntiles = (B + 31) / 32;
   if (ntiles == 0) return hipSuccess;
@@ -166,28 +108,27 @@ static hipError_t launch_fwd_h(const void* rec, float* out, int B, const void* b
     int grid = (waves_needed + 7) / 8;
     if (grid > num_cus) grid = num_cus;
     hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, true>), dim3(grid), dim3(512), L::BLOB, stream,
-                       (const int4*)rec, out, B, (const unsigned char*)blob, np, b3);
+                       (const int4*)rec, out, B, (const unsigned char*)blob, np);
   } else {
     // 4 waves per workgroup, one tile per wave
     int grid = (ntiles + 3) / 4;
     hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, false>), dim3(grid), dim3(256), 0, stream,
-                       (const int4*)rec, out, B, (const unsigned char*)blob, np, b3);
+                       (const int4*)rec, out, B, (const unsigned char*)blob, np);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_eta_mlp3_fwd(const void* rec, float* out, int B, const void* blob, int H,
-                               const NormParams& np, float b3, int variant, int num_cus,
-                               hipStream_t stream) {
+                               const NormParams& np, int variant, int num_cus, hipStream_t stream) {
   switch (H) {
-    case 64: return launch_fwd_h<64>(rec, out, B, blob, np, b3, variant, num_cus, stream);
-    case 128: return launch_fwd_h<128>(rec, out, B, blob, np, b3, variant, num_cus, stream);
-    case 256: return launch_fwd_h<256>(rec, out, B, blob, np, b3, variant, num_cus, stream);
+    case 64: return launch_fwd_h<64>(rec, out, B, blob, np, variant, num_cus, stream);
+    case 128: return launch_fwd_h<128>(rec, out, B, blob, np, variant, num_cus, stream);
+    case 256: return launch_fwd_h<256>(rec, out, B, blob, np, variant, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }
 
-size_t eta_mlp3_blob_bytes(int H) { return (size_t)2 * H * H + 44 * (size_t)H; }
+size_t eta_mlp3_blob_bytes(int H) { return mlp3_blob_bytes(H); }
 
 hipError_t launch_eta_featurize(const void* rec, float* out, int B, hipStream_t stream) {
   if (B <= 0) return hipSuccess;

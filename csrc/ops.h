@@ -12,9 +12,23 @@ struct NormParams;
 size_t eta_mlp3_blob_bytes(int H);
 // variant: -1 auto, 0 weights from global/L2, 1 weights staged in LDS (persistent grid)
 hipError_t launch_eta_mlp3_fwd(const void* rec, float* out, int B, const void* blob, int H,
-                               const NormParams& np, float b3, int variant, int num_cus,
-                               hipStream_t stream);
+                               const NormParams& np, int variant, int num_cus, hipStream_t stream);
 hipError_t launch_eta_featurize(const void* rec, float* out, int B, hipStream_t stream);
+
+// ---- ETA MLP training (K3) : eta_mlp_train.hip ----
+hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B, const void* blob,
+                                     int H, const NormParams& np, float gscale, void* xf,
+                                     void* h1a, void* h2a, void* dz2, void* dyb,
+                                     float* loss_tiles, int* step_ctr, int num_cus,
+                                     hipStream_t stream);
+hipError_t launch_relu_bwd(const void* dh1, const void* h1a, int lda, void* dz1, int B, int H,
+                           hipStream_t stream);
+int mlp3_num_params(int H);
+int mlp3_grad_bucket_floats(int H);
+hipError_t launch_adamw_pack(float* P, const float* G, float* M, float* V, void* blob, void* w2bf,
+                             const int* step, int H, float lr, float beta1, float beta2, float eps,
+                             float wd, int warmup, int total_steps, float min_lr_ratio, int update,
+                             hipStream_t stream);
 
 // ---- batched routing (K5 distance matrix + K6 greedy CVRP) : route_kernels.hip ----
 hipError_t launch_haversine_matrix(const double* lat, const double* lon, const int* npts, int R,

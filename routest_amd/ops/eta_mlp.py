@@ -32,6 +32,11 @@ def _acc_rows(h: int) -> np.ndarray:
     return (i & 3) + 8 * (i >> 2) + 4 * h
 
 
+def blob_bytes(H: int) -> int:
+    """[w2p | w1p | b1p | b2p | w3p | tail(b3,0,0,0)] — csrc/mlp3_tile.h"""
+    return 2 * H * H + 44 * H + 16
+
+
 @dataclass
 class PackedMLP3:
     hidden: int
@@ -105,9 +110,10 @@ def pack_mlp3(model: EtaMLP) -> PackedMLP3:
     parts = [bf16_bytes(w2p), bf16_bytes(w1p),
              vec_pack(b1).view(np.uint8).reshape(-1),
              vec_pack(b2).view(np.uint8).reshape(-1),
-             vec_pack(w3).view(np.uint8).reshape(-1)]
+             vec_pack(w3).view(np.uint8).reshape(-1),
+             np.array([b3, 0.0, 0.0, 0.0], dtype=np.float32).view(np.uint8)]
     blob = torch.from_numpy(np.concatenate(parts).copy())
-    assert blob.numel() == 2 * H * H + 44 * H
+    assert blob.numel() == blob_bytes(H)
     scale = (1.0 / x_std[8:12]).tolist()
     shift = (-x_mean[8:12] / x_std[8:12]).tolist()
     return PackedMLP3(H, blob, scale + shift, b3, w1k, b1, W2.clone(), b2.clone(), w3)
@@ -179,6 +185,6 @@ class EtaMlpKernel:
     def __call__(self, rec: torch.Tensor) -> torch.Tensor:
         if self.device.type == "cuda":
             return self._C.eta_mlp3_forward(rec, self.packed.blob, self.hidden, self.packed.norm,
-                                            self.packed.b3, self.variant)
+                                            self.variant)
         with torch.no_grad():
             return self.model_cpu(featurize_torch(rec))

@@ -1,0 +1,180 @@
+"""Fused HIP trainer for the ETA MLP (K3) — one rank of data-parallel training.
+
+Per step (all on the current HIP stream, no host synchronisation, HIP-graph capturable):
+
+  eta_mlp3_train_fwd (HIP)  : featurize + 3 layers + MSE grad; writes xf, h1a, h2a, dz2, dy
+  dh1 = dz2 @ W2            : hipBLASLt (bf16, fp32 accumulate)
+  relu_bwd (HIP)            : dz1 = dh1 * (h1 > 0)
+  G[W2|b2] = dz2^T [h1|1]   : hipBLASLt, fp32 out, written straight into the flat bucket
+  G[w3|b3] = dy^T  [h2|1]
+  G[W1k|b1] = dz1^T [xf]    (xf slot 14 == 1)
+  all_reduce(G)             : ONE RCCL collective (SUM; dy was pre-scaled by 2/global_batch)
+  adamw_pack (HIP)          : AdamW on fp32 master params + re-pack of the bf16 MFMA blob
+
+Training runs in normalised-target space (y' = (y - y_mean)/y_std); :meth:`to_model` writes the
+learned weights back into an :class:`EtaMLP` whose buffers carry the scaling.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from ..models.mlp3 import EtaMLP
+from ..ops import _ext
+from ..ops.eta_mlp import blob_bytes
+from ..parallel.dp import allreduce_flat
+
+
+def flatten_params(model: EtaMLP) -> torch.Tensor:
+    H = model.hidden
+    parts = [model.l1.weight.detach().reshape(-1), model.l1.bias.detach(),
+             model.l2.weight.detach().reshape(-1), model.l2.bias.detach(),
+             model.l3.weight.detach().reshape(-1), model.l3.bias.detach()]
+    flat = torch.cat([p.float().cpu() for p in parts])
+    assert flat.numel() == H * H + 15 * H + 1
+    return flat
+
+
+@torch.no_grad()
+def unflatten_into(model: EtaMLP, flat: torch.Tensor) -> None:
+    H = model.hidden
+    f = flat.detach().float().cpu()
+    o = 0
+    for t, n in ((model.l1.weight, 12 * H), (model.l1.bias, H), (model.l2.weight, H * H),
+                 (model.l2.bias, H), (model.l3.weight, H), (model.l3.bias, 1)):
+        t.copy_(f[o:o + n].view_as(t))
+        o += n
+
+
+def grads_from_bucket(G: torch.Tensor, H: int):
+    """Python mirror of adamw_pack_kernel's bucket -> parameter-gradient mapping (tests)."""
+    G = G.detach().float().cpu()
+    ldg = H + 16
+    gW2a = G[:H * ldg].view(H, ldg)
+    gW3a = G[H * ldg:H * ldg + ldg]
+    gW1a = G[H * ldg + ldg:].view(H, 16)
+    gW1 = gW1a[:, :12].clone()
+    gW1[:, 10] += gW1a[:, 12]
+    gW1[:, 11] += gW1a[:, 13]
+    return {"l1.weight": gW1, "l1.bias": gW1a[:, 14].clone(), "l2.weight": gW2a[:, :H].clone(),
+            "l2.bias": gW2a[:, H].clone(), "l3.weight": gW3a[:H].view(1, H).clone(),
+            "l3.bias": gW3a[H:H + 1].clone()}
+
+
+def _mm_f32(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> None:
+    try:
+        torch.mm(a, b, out_dtype=torch.float32, out=out)
+    except (RuntimeError, TypeError):
+        out.copy_(torch.mm(a, b))
+
+
+class FusedMlp3Trainer:
+    def __init__(self, model: EtaMLP, device: torch.device, batch_local: int, global_batch: int,
+                 lr: float = 2e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 warmup: int = 0, total_steps: int = 0, min_lr_ratio: float = 0.1,
+                 allreduce: bool = True):
+        if model.hidden not in (64, 128, 256):
+            raise ValueError("fused trainer supports hidden in (64, 128, 256)")
+        self.C = _ext.native(required=True)
+        self.model = model
+        self.H = H = model.hidden
+        self.dev = torch.device(device)
+        self.B = batch_local
+        self.global_batch = global_batch
+        self.hp = dict(lr=lr, beta1=betas[0], beta2=betas[1], eps=eps, wd=weight_decay, warmup=warmup,
+                       total_steps=total_steps, min_lr_ratio=min_lr_ratio)
+        self.allreduce = allreduce
+        xs = model.x_std.float().cpu()
+        xm = model.x_mean.float().cpu()
+        if (xm[:8] != 0).any() or (xs[:8] != 1).any():
+            raise ValueError("one-hot features must not be normalised")
+        self.norm = (1.0 / xs[8:12]).tolist() + (-xm[8:12] / xs[8:12]).tolist()
+        self.y_mean = float(model.y_mean)
+        self.y_std = float(model.y_std)
+        d = self.dev
+        bf = torch.bfloat16
+        self.P = flatten_params(model).to(d)
+        self.M = torch.zeros_like(self.P)
+        self.V = torch.zeros_like(self.P)
+        self.G = torch.zeros(self.C.mlp3_grad_bucket_floats(H), dtype=torch.float32, device=d)
+        ldg = H + 16
+        self.gW2a = self.G[:H * ldg].view(H, ldg)
+        self.gW3a = self.G[H * ldg:H * ldg + ldg].view(1, ldg)
+        self.gW1a = self.G[H * ldg + ldg:].view(H, 16)
+        self.blob = torch.zeros(blob_bytes(H), dtype=torch.uint8, device=d)
+        self.w2bf = torch.empty(H, H, dtype=bf, device=d)
+        self.step_ctr = torch.zeros(1, dtype=torch.int32, device=d)
+        B = batch_local
+        self.xf = torch.empty(B, 16, dtype=bf, device=d)
+        self.h1a = torch.empty(B, H + 16, dtype=bf, device=d)
+        self.h2a = torch.empty(B, H + 16, dtype=bf, device=d)
+        self.dz2 = torch.empty(B, H, dtype=bf, device=d)
+        self.dyb = torch.empty(B, dtype=bf, device=d)
+        self.dh1 = torch.empty(B, H, dtype=bf, device=d)
+        self.dz1 = torch.empty(B, H, dtype=bf, device=d)
+        self.loss_tiles = torch.zeros((B + 31) // 32, dtype=torch.float32, device=d)
+        self._pack(update=False)
+
+    def _pack(self, update: bool) -> None:
+        h = self.hp
+        self.C.adamw_pack(self.P, self.G, self.M, self.V, self.blob, self.w2bf, self.step_ctr, self.H,
+                          h["lr"], h["beta1"], h["beta2"], h["eps"], h["wd"], h["warmup"],
+                          h["total_steps"], h["min_lr_ratio"], update)
+
+    def normalize_targets(self, y: torch.Tensor) -> torch.Tensor:
+        return ((y.float() - self.y_mean) / self.y_std).contiguous()
+
+    def forward_backward(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> None:
+        """Fills the flat gradient bucket G (local contribution, pre-scaled for the global mean)."""
+        C, H = self.C, self.H
+        C.eta_mlp3_train_fwd(rec, tgt_norm, self.blob, H, self.norm, 2.0 / self.global_batch,
+                             self.xf, self.h1a, self.h2a, self.dz2, self.dyb, self.loss_tiles,
+                             self.step_ctr)
+        torch.mm(self.dz2, self.w2bf, out=self.dh1)
+        C.relu_bwd(self.dh1, self.h1a, self.dz1)
+        _mm_f32(self.dz2.t(), self.h1a, self.gW2a)
+        _mm_f32(self.dyb.view(1, -1), self.h2a, self.gW3a)
+        _mm_f32(self.dz1.t(), self.xf, self.gW1a)
+
+    def step(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> torch.Tensor:
+        """One optimizer step; returns the device tensor of per-tile squared errors (no sync)."""
+        self.forward_backward(rec, tgt_norm)
+        if self.allreduce:
+            allreduce_flat(self.G, average=False)
+        self._pack(update=True)
+        return self.loss_tiles
+
+    def local_mse(self) -> float:
+        return float(self.loss_tiles.sum().item()) / self.B
+
+    @torch.no_grad()
+    def to_model(self) -> EtaMLP:
+        unflatten_into(self.model, self.P)
+        return self.model
+
+    def optimizer_state(self) -> dict:
+        return {"exp_avg": self.M.detach().cpu(), "exp_avg_sq": self.V.detach().cpu(),
+                "step": self.step_ctr.detach().cpu().to(torch.int64)}
+
+    def load_optimizer_state(self, st: dict) -> None:
+        self.M.copy_(st["exp_avg"].to(self.dev))
+        self.V.copy_(st["exp_avg_sq"].to(self.dev))
+        self.step_ctr.copy_(st["step"].to(torch.int32).to(self.dev))
+
+    def set_params(self, flat: torch.Tensor) -> None:
+        self.P.copy_(flat.to(self.dev))
+        self._pack(update=False)
+
+
+def lr_at(step: int, lr: float, warmup: int, total: int, min_ratio: float) -> float:
+    """Host mirror of adamw_pack_kernel's schedule (for the autograd path and tests)."""
+    t = max(1, step)
+    out = lr
+    if warmup > 0 and t < warmup:
+        out *= t / warmup
+    if total > 0 and t > warmup:
+        prog = min(1.0, (t - warmup) / max(1.0, total - warmup))
+        out *= min_ratio + (1 - min_ratio) * 0.5 * (1 + math.cos(math.pi * prog))
+    return out

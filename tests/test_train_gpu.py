@@ -1,0 +1,130 @@
+"""K3 training kernels on the GPU vs PyTorch fp32 autograd references."""
+import copy
+
+import pytest
+import torch
+
+from routest_amd.data.synth import synth_records
+from routest_amd.models.features import records_to_features
+from routest_amd.models.mlp3 import EtaMLP
+from routest_amd.ops.eta_mlp import featurize_torch, pack_mlp3, records_to_tensor
+from routest_amd.train.fused import FusedMlp3Trainer, flatten_params, grads_from_bucket
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _model(H, seed=0):
+    torch.manual_seed(seed)
+    m = EtaMLP(H)
+    rec, y = synth_records(8192, seed)
+    m.fit_normalization(records_to_features(rec), y)
+    return m
+
+
+def _batch(B, m, seed=3):
+    rec, y = synth_records(B, seed)
+    rt = records_to_tensor(rec)
+    yn = (torch.from_numpy(y) - m.y_mean) / m.y_std
+    return rt, yn.float()
+
+
+@pytest.mark.parametrize("H", [64, 128, 256])
+def test_initial_pack_matches_host_pack(H):
+    m = _model(H)
+    tr = FusedMlp3Trainer(m, DEV, 1024, 1024)
+    mm = copy.deepcopy(m)
+    mm.y_mean.fill_(0.0)
+    mm.y_std.fill_(1.0)
+    ref = pack_mlp3(mm).blob
+    assert torch.equal(tr.blob.cpu(), ref)
+
+
+@pytest.mark.parametrize("H", [64, 256])
+@pytest.mark.parametrize("B", [1000, 8192])
+def test_fused_gradients_match_autograd(H, B):
+    m = _model(H)
+    rt, yn = _batch(B, m)
+    tr = FusedMlp3Trainer(m, DEV, B, B)
+    tr.forward_backward(rt.to(DEV), yn.to(DEV))
+    torch.cuda.synchronize()
+    got = grads_from_bucket(tr.G, H)
+    ref_m = copy.deepcopy(m)
+    loss = torch.nn.functional.mse_loss(ref_m.forward_normalized(featurize_torch(rt)), yn)
+    loss.backward()
+    for name, p in ref_m.named_parameters():
+        g, r = got[name].reshape(-1), p.grad.reshape(-1)
+        rel = (g - r).norm() / r.norm().clamp_min(1e-12)
+        assert rel < 3e-2, (name, float(rel))
+    # loss partials: per-tile squared errors of the forward pass
+    mse = float(tr.loss_tiles.sum()) / B
+    assert abs(mse - float(loss)) / float(loss) < 2e-2
+
+
+def test_adamw_step_matches_torch():
+    H, B = 64, 2048
+    m = _model(H)
+    rt, yn = _batch(B, m)
+    tr = FusedMlp3Trainer(m, DEV, B, B, lr=1e-3, weight_decay=0.01)
+    tr.forward_backward(rt.to(DEV), yn.to(DEV))
+    g = grads_from_bucket(tr.G, H)
+    p0 = flatten_params(m)
+    tr.step_ctr.fill_(1)  # forward_backward already bumped it; one optimizer step = t=1
+    tr._pack(update=True)
+    torch.cuda.synchronize()
+    ref = copy.deepcopy(m)
+    for n, p in ref.named_parameters():
+        p.grad = g[n].view_as(p).clone()
+    opt = torch.optim.AdamW([{"params": [ref.l1.weight, ref.l2.weight, ref.l3.weight], "weight_decay": 0.01},
+                             {"params": [ref.l1.bias, ref.l2.bias, ref.l3.bias], "weight_decay": 0.0}],
+                            lr=1e-3, betas=(0.9, 0.999), eps=1e-8)
+    opt.step()
+    torch.testing.assert_close(tr.P.cpu(), flatten_params(ref), rtol=1e-5, atol=1e-6)
+    assert not torch.equal(tr.P.cpu(), p0)
+
+
+def test_fused_training_converges_and_serves():
+    from routest_amd.ops.eta_mlp import EtaMlpKernel
+    H, B = 128, 16384
+    m = _model(H, 1)
+    rec, y = synth_records(B * 8, 11)
+    rt = records_to_tensor(rec).to(DEV)
+    yn = ((torch.from_numpy(y) - m.y_mean) / m.y_std).float().to(DEV)
+    tr = FusedMlp3Trainer(m, DEV, B, B, lr=3e-3, warmup=10, total_steps=300)
+    losses = []
+    for s in range(300):
+        k = s % 8
+        tr.step(rt[k * B:(k + 1) * B], yn[k * B:(k + 1) * B])
+        if s % 50 == 0 or s == 299:
+            losses.append(tr.local_mse())
+    assert losses[-1] < 0.2 * losses[0], losses
+    model = tr.to_model()
+    erec, ey = synth_records(4096, 99)
+    pred = EtaMlpKernel(model, DEV)(records_to_tensor(erec).to(DEV)).cpu()
+    mae = (pred - torch.from_numpy(ey)).abs().mean()
+    assert mae < 0.25 * torch.from_numpy(ey).abs().mean(), float(mae)
+
+
+def test_graph_captured_step_matches_eager():
+    H, B = 64, 4096
+    m = _model(H, 2)
+    rt, yn = _batch(B, m, 4)
+    rt, yn = rt.to(DEV), yn.to(DEV)
+    eager = FusedMlp3Trainer(copy.deepcopy(m), DEV, B, B, lr=1e-3)
+    graphed = FusedMlp3Trainer(copy.deepcopy(m), DEV, B, B, lr=1e-3)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm up hipBLASLt outside capture
+        graphed.forward_backward(rt, yn)
+    torch.cuda.current_stream().wait_stream(s)
+    graphed.step_ctr.zero_()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        graphed.step(rt, yn)
+    for _ in range(5):
+        eager.step(rt, yn)
+        g.replay()
+    torch.cuda.synchronize()
+    assert int(graphed.step_ctr.item()) == 5
+    torch.testing.assert_close(graphed.P, eager.P, rtol=1e-5, atol=1e-6)
