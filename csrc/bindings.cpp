@@ -157,7 +157,7 @@ void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tens
   check_bf16(h1a, "h1a", B, H + 16);
   check_bf16(h2a, "h2a", B, H + 16);
   check_bf16(dz2, "dz2", B, H);
-  check_bf16(dyb, "dyb", B, 1);
+  check_bf16(dyb, "dyb", B, 8);
   check_dev(loss_tiles, "loss_tiles");
   TORCH_CHECK(loss_tiles.scalar_type() == torch::kFloat32 && loss_tiles.numel() >= (B + 31) / 32,
               "loss_tiles must be f32 [ceil(B/32)]");
@@ -209,6 +209,39 @@ void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor
                                      cur_stream(P)));
 }
 
+// slab: f32 [S, stride]; the partial of k-slice s is written at slab[s, offset + m*ldo + n].
+void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N, torch::Tensor slab,
+           int64_t offset, int64_t ldo) {
+  check_dev(A, "A");
+  check_dev(Bm, "Bm");
+  check_dev(slab, "slab");
+  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && Bm.scalar_type() == torch::kBFloat16, "bf16 A/Bm");
+  TORCH_CHECK(A.dim() == 2 && Bm.dim() == 2 && A.size(0) == Bm.size(0), "A/Bm must be [K, *]");
+  TORCH_CHECK(M <= A.size(1) && N <= Bm.size(1) && Mout <= M, "M/N exceed operand widths");
+  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && A.size(1) % 8 == 0 && Bm.size(1) % 8 == 0,
+              "M, N and leading dims must be multiples of 8");
+  const int NT = (int)((N + 31) / 32);
+  TORCH_CHECK(NT == 1 || NT == 2 || NT == 3 || NT == 5 || NT == 9, "unsupported N=", N);
+  TORCH_CHECK(slab.scalar_type() == torch::kFloat32 && slab.dim() == 2, "slab must be f32 [S, stride]");
+  TORCH_CHECK(offset + (Mout - 1) * ldo + N <= slab.size(1), "slab region out of range");
+  const c10::DeviceGuard guard(A.device());
+  RT_CHECK_HIP(rt::launch_wgrad(A.data_ptr(), (int)A.size(1), (int)M, (int)Mout, Bm.data_ptr(),
+                                (int)Bm.size(1), (int)N, (int)A.size(0), (int)slab.size(0),
+                                slab.data_ptr<float>() + offset, (int)ldo, (long long)slab.size(1),
+                                cur_stream(A)));
+}
+
+void wgrad_reduce(torch::Tensor slab, torch::Tensor G) {
+  check_dev(slab, "slab");
+  check_dev(G, "G");
+  TORCH_CHECK(slab.scalar_type() == torch::kFloat32 && G.scalar_type() == torch::kFloat32, "f32");
+  TORCH_CHECK(slab.dim() == 2 && slab.size(1) >= G.numel(), "slab/G shape");
+  const c10::DeviceGuard guard(G.device());
+  RT_CHECK_HIP(rt::launch_wgrad_reduce(slab.data_ptr<float>(), (int)slab.size(0),
+                                       (long long)slab.size(1), G.data_ptr<float>(), (int)G.numel(),
+                                       cur_stream(G)));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -223,5 +256,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + MFMA fragment re-pack");
   m.def("mlp3_num_params", [](int64_t H) { return (int64_t)rt::mlp3_num_params((int)H); });
   m.def("mlp3_grad_bucket_floats", [](int64_t H) { return (int64_t)rt::mlp3_grad_bucket_floats((int)H); });
+  m.def("wgrad", &wgrad, "split-K weight-gradient GEMM (K = batch) into fp32 slabs");
+  m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs");
+  m.def("num_cus", [](int64_t dev) { return (int64_t)num_cus((int)dev); });
   m.attr("ARCH") = "gfx950";
 }

@@ -10,8 +10,9 @@
 //        xf  [B,16]   the exact bf16 features the MFMA consumed, slot 14 := 1 (bias-grad column)
 //        h1a [B,H+16] relu(z1) with column H := 1   (dW2 | db2 = dz2^T h1a)
 //        h2a [B,H+16] relu(z2) with column H := 1   (dW3 | db3 = dy^T h2a)
-//        dz2 [B,H], dy [B] (already scaled by 2 / global_batch), per-tile squared-error sums.
-//   2. dh1 = dz2 W2 and the three weight-gradient GEMMs (K = batch) on hipBLASLt (plain GEMMs).
+//        dz2 [B,H], dy [B,8] (col 0; pre-scaled by 2 / global_batch), per-tile squared errors.
+//   2. dh1 = dz2 W2 on hipBLASLt (a plain [B,H]x[H,H] GEMM); the three weight-gradient GEMMs
+//      (K = batch) on the split-K wgrad kernel (wgrad.hip) + one deterministic slab reduction.
 //   3. relu_bwd_kernel: dz1 = dh1 * (h1 > 0).
 //   4. ONE flat fp32 gradient bucket -> one RCCL all-reduce over xGMI.
 //   5. adamw_pack_kernel: AdamW on the flat fp32 master params, writing back the bf16 fragment
@@ -127,7 +128,13 @@ __global__ __launch_bounds__(train_tpb<H>(), H >= 256 ? 1 : 2) void eta_mlp3_tra
     const float y = ys + b3;
     const float diff = valid ? (y - target[row]) : 0.f;
     const float dy = gscale * diff;
-    if (valid && h == 0) dyb[row] = (__bf16)dy;
+    if (valid && h == 0) {  // dy as an [B,8] bf16 operand (cols 1..7 zero) for the wgrad kernel
+      bf16x8 dv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dv[j] = (__bf16)0.f;
+      dv[0] = (__bf16)dy;
+      *reinterpret_cast<bf16x8*>(dyb + (size_t)row * 8) = dv;
+    }
     // per-tile squared error (h = 0 half only), wave reduction
     float l = (h == 0) ? diff * diff : 0.f;
 #pragma unroll

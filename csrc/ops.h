@@ -30,6 +30,14 @@ hipError_t launch_adamw_pack(float* P, const float* G, float* M, float* V, void*
                              float wd, int warmup, int total_steps, float min_lr_ratio, int update,
                              hipStream_t stream);
 
+// ---- weight-gradient GEMMs with K = batch : wgrad.hip ----
+hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm, int ldb, int N,
+                        int K, int S, float* slab, int ldo, long long slab_stride,
+                        hipStream_t stream);
+hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, float* G, int n,
+                               hipStream_t stream);
+size_t wgrad_lds_bytes(int NT);
+
 // ---- batched routing (K5 distance matrix + K6 greedy CVRP) : route_kernels.hip ----
 hipError_t launch_haversine_matrix(const double* lat, const double* lon, const int* npts, int R,
                                    int NM, double circuity, double* D, hipStream_t stream);

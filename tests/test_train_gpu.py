@@ -128,3 +128,23 @@ def test_graph_captured_step_matches_eager():
     torch.cuda.synchronize()
     assert int(graphed.step_ctr.item()) == 5
     torch.testing.assert_close(graphed.P, eager.P, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("K,M,Mout,N,S", [(65536, 256, 256, 272, 256), (1000, 256, 256, 272, 7),
+                                           (4133, 8, 1, 272, 16), (777, 256, 200, 16, 3),
+                                           (64, 64, 64, 96, 1)])
+def test_wgrad_kernel_vs_fp32(K, M, Mout, N, S):
+    from routest_amd.ops import _ext
+    C = _ext.native()
+    g = torch.Generator().manual_seed(K)
+    A = torch.randn(K, M, generator=g).to(torch.bfloat16)
+    Bm = torch.randn(K, N + 8, generator=g).to(torch.bfloat16)   # ldb > N
+    ref = (A.float().t() @ Bm.float()[:, :N])[:Mout]
+    ldo = N + 4
+    stride = Mout * ldo + 16
+    slab = torch.full((S, stride), float("nan"), device=DEV)
+    C.wgrad(A.to(DEV), M, Mout, Bm.to(DEV), N, slab, 8, ldo)
+    G = torch.zeros(stride, device=DEV)
+    C.wgrad_reduce(slab[:, :], G)
+    got = G[8:8 + Mout * ldo].view(Mout, ldo)[:, :N].cpu()
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3 * (K ** 0.5))
