@@ -34,9 +34,10 @@ __device__ __forceinline__ f32x16 mfma32(const bf16x8 a, const bf16x8 b, const f
 //   2020-01-01 (Wednesday), w = weather | traffic << 8.
 // Returns the 8 features of lane-half h for the MFMA B operand (k = 8h + j):
 //   h = 0: weather one-hot [0..3], traffic one-hot [4..7]
-//   h = 1: weekday, hour, km_hi, age_hi, km_lo, age_lo, 0, 0
+//   h = 1: weekday, hour, km_hi, age_hi, km_lo, age_lo, 1, 1
 // km/age are split into a bf16 hi part and a bf16 residual so layer 1 sees ~16 mantissa bits of
-// the continuous inputs; the host duplicates W1's km/age columns into k = 12, 13.
+// the continuous inputs; the host duplicates W1's km/age columns into k = 12, 13.  The two
+// constant-1 inputs at k = 14, 15 carry b1 as a bf16 hi/lo pair, so layer 1 is a bare MFMA.
 __device__ __forceinline__ void featurize_f32(const int4 rc, const int h, const NormParams& np,
                                               float f[8]) {
   if (h == 0) {
@@ -70,8 +71,8 @@ __device__ __forceinline__ void featurize_f32(const int4 rc, const int h, const 
     f[3] = agh;
     f[4] = kmn - kmh;
     f[5] = agn - agh;
-    f[6] = 0.f;
-    f[7] = 0.f;
+    f[6] = 1.f;
+    f[7] = 1.f;
   }
 }
 

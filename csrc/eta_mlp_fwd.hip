@@ -27,11 +27,11 @@
 
 namespace rt {
 
-template <int H, bool LDSW>
-__global__ __launch_bounds__(LDSW ? 512 : 256, LDSW ? 2 : 1) void eta_mlp3_fwd_kernel(
+template <int H, bool LDSW, int TPB, bool PIN = false>
+__global__ __launch_bounds__(TPB, LDSW ? TPB / 256 : 1) void eta_mlp3_fwd_kernel(
     const int4* __restrict__ rec, float* __restrict__ out, int B,
     const unsigned char* __restrict__ blob, NormParams np) {
-  constexpr int MT = H / 32, KS = H / 16;
+  constexpr int KS = H / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const unsigned char* base = blob;
   if constexpr (LDSW) {
@@ -40,6 +40,8 @@ __global__ __launch_bounds__(LDSW ? 512 : 256, LDSW ? 2 : 1) void eta_mlp3_fwd_k
   }
   const Mlp3View<H> w(base);
   const float b3 = w.tail[0];
+  W1Frags<H> w1;
+  w1.load(w, threadIdx.x & 63);
 
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
@@ -56,17 +58,15 @@ __global__ __launch_bounds__(LDSW ? 512 : 256, LDSW ? 2 : 1) void eta_mlp3_fwd_k
     const bf16x8 xb = to_bf16x8(f);
 
     bf16x8 h1[KS];
-    mlp3_layer1<H>(w, xb, lane, h, h1);
+    mlp3_layer1<H>(w1, xb, h1);
 
     // layer 2 + fused layer 3 (relu(acc) . w3 reduced in registers)
     float ys = 0.f;
-#pragma unroll 1
-    for (int mt = 0; mt < MT; ++mt) {
-      const f32x16 acc = mlp3_layer2_tile<H>(w, h1, mt, lane, h);
+    mlp3_layer2<H, PIN>(w, h1, lane, h, [&](int mt, const f32x16& acc) {
       const f32x16 w3 = load_vec16(w.w3p, mt, h);
 #pragma unroll
       for (int i = 0; i < 16; ++i) ys += fmaxf(acc[i], 0.f) * w3[i];
-    }
+    });
     ys += __shfl_xor(ys, 32);
     if (h == 0 && row < B) out[row] = ys + b3;
   }
@@ -86,33 +86,49 @@ __global__ __launch_bounds__(256) void eta_featurize_kernel(const int4* __restri
   o[2] = make_float4(f[8], f[9], f[10], f[11]);
 }
 
+// Persistent LDS-staged launch: one workgroup of T threads per CU (139 KiB of LDS at H = 256).
+template <int H, int T, bool PIN>
+static hipError_t launch_lds(const void* rec, float* out, int B, const void* blob,
+                             const NormParams& np, int num_cus, hipStream_t stream) {
+  using L = Mlp3Layout<H>;
+  static bool attr_set[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!attr_set[dev & 63]) {
+    hipError_t e = hipFuncSetAttribute((const void*)eta_mlp3_fwd_kernel<H, true, T, PIN>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::BLOB);
+    if (e != hipSuccess) return e;
+    attr_set[dev & 63] = true;
+  }
+  const int ntiles = (B + 31) / 32;
+  int grid = (ntiles + T / 64 - 1) / (T / 64);
+  if (grid > num_cus) grid = num_cus;
+  hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, true, T, PIN>), dim3(grid), dim3(T), L::BLOB, stream,
+                     (const int4*)rec, out, B, (const unsigned char*)blob, np);
+  return hipGetLastError();
+}
+
 template <int H>
 static hipError_t launch_fwd_h(const void* rec, float* out, int B, const void* blob,
                                const NormParams& np, int variant, int num_cus, hipStream_t stream) {
+  // variant: -1 auto, 0 global weights, LDS-staged: 1 = 512 thr, 2 = 768 thr, 3/4 = same + pinned
+  // read/MFMA interleave
   using L = Mlp3Layout<H>;
   const int ntiles = (B + 31) / 32;
   if (ntiles == 0) return hipSuccess;
   const bool lds_fits = L::BLOB <= 160 * 1024;
-  bool use_lds = lds_fits && (variant == 1 || (variant < 0 && ntiles >= num_cus * 8 * 2));
+  bool use_lds = lds_fits && (variant >= 1 || (variant < 0 && ntiles >= num_cus * 8 * 2));
   if (use_lds) {
-    static bool attr_set[64] = {};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (!attr_set[dev & 63]) {
-      hipError_t e = hipFuncSetAttribute((const void*)eta_mlp3_fwd_kernel<H, true>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::BLOB);
-      if (e != hipSuccess) return e;
-      attr_set[dev & 63] = true;
+    switch (variant) {
+      case 2: return launch_lds<H, 768, false>(rec, out, B, blob, np, num_cus, stream);
+      case 3: return launch_lds<H, 512, true>(rec, out, B, blob, np, num_cus, stream);
+      case 4: return launch_lds<H, 768, true>(rec, out, B, blob, np, num_cus, stream);
+      default: return launch_lds<H, 512, false>(rec, out, B, blob, np, num_cus, stream);
     }
-    const int waves_needed = ntiles;
-    int grid = (waves_needed + 7) / 8;
-    if (grid > num_cus) grid = num_cus;
-    hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, true>), dim3(grid), dim3(512), L::BLOB, stream,
-                       (const int4*)rec, out, B, (const unsigned char*)blob, np);
   } else {
     // 4 waves per workgroup, one tile per wave
     int grid = (ntiles + 3) / 4;
-    hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, false>), dim3(grid), dim3(256), 0, stream,
+    hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, false, 256>), dim3(grid), dim3(256), 0, stream,
                        (const int4*)rec, out, B, (const unsigned char*)blob, np);
   }
   return hipGetLastError();

@@ -44,13 +44,12 @@ __device__ __forceinline__ void store_act(__bf16* base_row, const bf16x8 (&a)[H 
   }
 }
 
-// H = 256 needs more than the 256 VGPRs two waves per SIMD leave (h1 fragments + masks + stores),
-// so it runs one 4-wave workgroup per CU with the full 512-register file per wave.
+// 8 waves per workgroup (2 per SIMD; <= 256 VGPRs incl. register-resident W1 fragments).
 template <int H>
-constexpr int train_tpb() { return H >= 256 ? 256 : 512; }
+constexpr int train_tpb() { return 512; }
 
 template <int H>
-__global__ __launch_bounds__(train_tpb<H>(), H >= 256 ? 1 : 2) void eta_mlp3_train_fwd_kernel(
+__global__ __launch_bounds__(512, 2) void eta_mlp3_train_fwd_kernel(
     const int4* __restrict__ rec, const float* __restrict__ target, int B,
     const unsigned char* __restrict__ blob, NormParams np, float gscale, __bf16* __restrict__ xf,
     __bf16* __restrict__ h1a, __bf16* __restrict__ h2a, __bf16* __restrict__ dz2,
@@ -63,6 +62,8 @@ __global__ __launch_bounds__(train_tpb<H>(), H >= 256 ? 1 : 2) void eta_mlp3_tra
   stage_blob<H>(blob, smem);
   const Mlp3View<H> w(smem);
   const float b3 = w.tail[0];
+  W1Frags<H> w1;
+  w1.load(w, threadIdx.x & 63);
 
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
@@ -78,14 +79,11 @@ __global__ __launch_bounds__(train_tpb<H>(), H >= 256 ? 1 : 2) void eta_mlp3_tra
     float f[8];
     featurize_f32(rc, h, np, f);
     const bf16x8 xb = to_bf16x8(f);
-    if (valid) {
-      bf16x8 xs = xb;
-      if (h == 1) xs[6] = (__bf16)1.f;   // slot 14: ones column for db1
-      *reinterpret_cast<bf16x8*>(xf + (size_t)row * 16 + 8 * h) = xs;
-    }
+    if (valid)  // slots 14, 15 hold 1.0 (the b1 hi/lo inputs): dW1k[:,14] == db1
+      *reinterpret_cast<bf16x8*>(xf + (size_t)row * 16 + 8 * h) = xb;
 
     bf16x8 h1[KS];
-    mlp3_layer1<H>(w, xb, lane, h, h1);
+    mlp3_layer1<H>(w1, xb, h1);
     __bf16* h1row = h1a + (size_t)row * LDA;
     __bf16* h2row = h2a + (size_t)row * LDA;
     if (valid) {
@@ -101,9 +99,7 @@ __global__ __launch_bounds__(train_tpb<H>(), H >= 256 ? 1 : 2) void eta_mlp3_tra
     // layer 2 + layer 3; relu(z2) goes straight to memory, only its mask stays in registers
     unsigned long long mask_lo = 0, mask_hi = 0;   // 16 mask bits per 32-row hidden tile
     float ys = 0.f;
-#pragma unroll 1
-    for (int mt = 0; mt < MT; ++mt) {
-      const f32x16 acc = mlp3_layer2_tile<H>(w, h1, mt, lane, h);
+    mlp3_layer2<H>(w, h1, lane, h, [&](int mt, const f32x16& acc) {
       const f32x16 w3 = load_vec16(w.w3p, mt, h);
       unsigned mk = 0;
 #pragma unroll
@@ -123,7 +119,7 @@ __global__ __launch_bounds__(train_tpb<H>(), H >= 256 ? 1 : 2) void eta_mlp3_tra
       }
       if (mt < 4) mask_lo |= (unsigned long long)mk << (16 * mt);
       else mask_hi |= (unsigned long long)mk << (16 * (mt - 4));
-    }
+    });
     ys += __shfl_xor(ys, 32);
     const float y = ys + b3;
     const float diff = valid ? (y - target[row]) : 0.f;
@@ -289,8 +285,13 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
     const int hh = (rr >> 2) & 1;
     const int ii = (rr & 3) + 4 * (rr >> 3);
     const int idx = (mt * 2 + hh) * 16 + ii;
-    if (e < OFF_W2) b1p[idx] = p;
-    else if (e < OFF_W3) b2p[idx] = p;
+    if (e < OFF_W2) {
+      b1p[idx] = p;
+      const __bf16 hi = (__bf16)p;
+      const int ln = rr;  // k = 14, 15 live in lane half 1: lane = rr + 32
+      w1p[((size_t)(mt * 64 + ln + 32)) * 8 + 6] = hi;
+      w1p[((size_t)(mt * 64 + ln + 32)) * 8 + 7] = (__bf16)(p - (float)hi);
+    } else if (e < OFF_W3) b2p[idx] = p;
     else w3p[idx] = p;
   } else {
     tail[0] = p;

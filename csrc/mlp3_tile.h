@@ -68,14 +68,27 @@ __device__ __forceinline__ f32x16 load_vec16(const f32x4* v, int mt, int h) {
   return acc;
 }
 
-// Layer 1: h1^T = relu(W1k f^T + b1) as bf16 B fragments h1[ks] (ks = 2*mt + s).
+// The H/32 layer-1 A fragments of this lane (W1k incl. the b1 hi/lo columns): loaded once per
+// kernel and kept in registers by persistent waves.
 template <int H>
-__device__ __forceinline__ void mlp3_layer1(const Mlp3View<H>& w, const bf16x8 xb, int lane, int h,
+struct W1Frags {
+  bf16x8 f[H / 32];
+  __device__ __forceinline__ void load(const Mlp3View<H>& w, int lane) {
+#pragma unroll
+    for (int mt = 0; mt < H / 32; ++mt) f[mt] = w.w1p[mt * 64 + lane];
+  }
+};
+
+// Layer 1: h1^T = relu(W1k f^T) (bias folded into k = 14, 15) as bf16 B fragments h1[ks].
+template <int H>
+__device__ __forceinline__ void mlp3_layer1(const W1Frags<H>& w1, const bf16x8 xb,
                                             bf16x8 (&h1)[H / 16]) {
 #pragma unroll
   for (int mt = 0; mt < H / 32; ++mt) {
-    f32x16 acc = load_vec16(w.b1p, mt, h);
-    acc = mfma32(w.w1p[mt * 64 + lane], xb, acc);
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    acc = mfma32(w1.f[mt], xb, acc);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
 #pragma unroll
@@ -84,16 +97,42 @@ __device__ __forceinline__ void mlp3_layer1(const Mlp3View<H>& w, const bf16x8 x
   }
 }
 
-// Layer 2 pre-activation tile mt: z2^T[32mt .. 32mt+31][batch] = W2 h1^T + b2.
-template <int H>
-__device__ __forceinline__ f32x16 mlp3_layer2_tile(const Mlp3View<H>& w, const bf16x8 (&h1)[H / 16],
-                                                   int mt, int lane, int h) {
-  constexpr int KS = H / 16;
-  f32x16 acc = load_vec16(w.b2p, mt, h);
-  const bf16x8* wa = w.w2p + (size_t)mt * KS * 64 + lane;
+// Layer 2 over all hidden tiles with a 4-deep ring of A-fragment prefetches that runs across tile
+// boundaries (fragment f = mt*KS + ks; loads for f+1..f+4 are in flight while f feeds the MFMA),
+// so no MFMA waits on the LDS read issued just before it.  epi(mt, acc) consumes each finished
+// 32-row pre-activation tile z2^T[32mt..32mt+31][batch].
+template <int H, bool PIN = false, typename Epi>
+__device__ __forceinline__ void mlp3_layer2(const Mlp3View<H>& w, const bf16x8 (&h1)[H / 16],
+                                            int lane, int h, Epi&& epi) {
+  constexpr int MT = H / 32, KS = H / 16, NF = MT * KS, D = 4;
+  const bf16x8* wa = w.w2p + lane;
+  bf16x8 r0 = wa[0 * 64], r1 = wa[1 * 64], r2 = wa[2 * 64], r3 = wa[3 * 64];
+#pragma unroll 1
+  for (int mt = 0; mt < MT; ++mt) {
+    f32x16 acc = load_vec16(w.b2p, mt, h);
+    const int base = mt * KS;
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) acc = mfma32(wa[ks * 64], h1[ks], acc);
-  return acc;
+    for (int ks = 0; ks < KS; ks += D) {
+      // consume r0..r3 (fragments base+ks .. +3), refill with base+ks+4 .. +7 (clamped in range)
+      const bf16x8 c0 = r0, c1 = r1, c2 = r2, c3 = r3;
+      const int nf = base + ks + D;
+      r0 = wa[min(nf + 0, NF - 1) * 64];
+      r1 = wa[min(nf + 1, NF - 1) * 64];
+      r2 = wa[min(nf + 2, NF - 1) * 64];
+      r3 = wa[min(nf + 3, NF - 1) * 64];
+      acc = mfma32(c0, h1[ks + 0], acc);
+      acc = mfma32(c1, h1[ks + 1], acc);
+      acc = mfma32(c2, h1[ks + 2], acc);
+      acc = mfma32(c3, h1[ks + 3], acc);
+      // pin the order: the 4 refill reads issue BEFORE the 4 MFMAs that consume older fragments
+      // (hipcc otherwise sinks each read next to its MFMA and waits lgkmcnt(0) on it)
+      if constexpr (PIN) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      }
+    }
+    epi(mt, acc);
+  }
 }
 
 }  // namespace rt

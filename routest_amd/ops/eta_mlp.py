@@ -3,7 +3,8 @@
 :func:`pack_mlp3` turns an :class:`~routest_amd.models.mlp3.EtaMLP` into the kernel's weight blob:
 
 * ``W1k [H,16]``: W1 on normalised features, with the km/age columns duplicated into the pad
-  slots k = 12, 13 (the kernel feeds a bf16 hi/lo split of those two inputs there).
+  slots k = 12, 13 (the kernel feeds a bf16 hi/lo split of those two inputs there) and b1 as a
+  bf16 hi/lo pair in k = 14, 15 (whose inputs are the constant 1), so layer 1 is one bare MFMA.
 * A fragments for ``mfma_f32_32x32x16_bf16``: lane l holds ``A[row l&31][k = 8(l>>5) + j]``.
   For layer 2 the B operand is the layer-1 accumulator, whose element j of lane half h is hidden
   unit ``16ks + 8(j>>2) + 4h + (j&3)`` (cdna_hip_programming.md §3), so W2's columns are permuted
@@ -72,6 +73,9 @@ def pack_mlp3(model: EtaMLP) -> PackedMLP3:
     w1k[:, :12] = W1eff
     w1k[:, 12] = W1eff[:, 10]
     w1k[:, 13] = W1eff[:, 11]
+    b1_hi = b1.to(torch.bfloat16).float()
+    w1k[:, 14] = b1_hi            # constant-1 inputs k = 14, 15 carry b1 as bf16 hi + lo
+    w1k[:, 15] = b1 - b1_hi
     W2 = model.l2.weight.detach().float().cpu()                   # [H,H] (out, in)
     b2 = model.l2.bias.detach().float().cpu()
     y_std = float(model.y_std)
@@ -160,8 +164,10 @@ def emulate_kernel(p: PackedMLP3, rec_i32: torch.Tensor) -> torch.Tensor:
     f[:, 11] = hi[:, 3]
     f[:, 12] = num[:, 2] - hi[:, 2]
     f[:, 13] = num[:, 3] - hi[:, 3]
+    f[:, 14] = 1.0
+    f[:, 15] = 1.0
     bf = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
-    h1 = torch.relu(bf(f) @ bf(p.w1k.to(dev)).T + p.b1.to(dev))
+    h1 = torch.relu(bf(f) @ bf(p.w1k.to(dev)).T)
     h2 = torch.relu(bf(h1) @ bf(p.w2.to(dev)).T + p.b2.to(dev))
     return h2 @ p.w3.to(dev) + p.b3
 
