@@ -44,8 +44,9 @@ torch::Tensor eta_mlp3_forward(torch::Tensor records, torch::Tensor blob, int64_
                                std::vector<double> norm, int64_t variant) {
   check_dev(records, "records");
   check_dev(blob, "blob");
-  TORCH_CHECK(records.scalar_type() == torch::kInt32 && records.dim() == 2 && records.size(1) == 4,
-              "records must be int32 [B,4] (16-byte EtaRecord rows)");
+  TORCH_CHECK(records.scalar_type() == torch::kInt32 && records.dim() == 2 &&
+                  (records.size(1) == 4 || records.size(1) == 2),
+              "records must be int32 [B,4] (16-byte records) or [B,2] (8-byte compact records)");
   TORCH_CHECK(blob.scalar_type() == torch::kUInt8, "blob must be uint8");
   TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H),
               "blob has ", blob.numel(), " bytes, expected ", rt::eta_mlp3_blob_bytes((int)H),
@@ -63,8 +64,38 @@ torch::Tensor eta_mlp3_forward(torch::Tensor records, torch::Tensor blob, int64_
   }
   RT_CHECK_HIP(rt::launch_eta_mlp3_fwd(records.data_ptr(), out.data_ptr<float>(), B,
                                        blob.data_ptr(), (int)H, np, (int)variant,
-                                       num_cus(records.device().index()), cur_stream(records)));
+                                       num_cus(records.device().index()), cur_stream(records),
+                                       records.size(1) == 2));
   return out;
+}
+
+// Zero-copy variant: records/out are PINNED HOST tensors; the kernel reads and writes them directly
+// over PCIe through their device-mapped addresses (no copy-engine transfers, no staging buffers).
+void eta_mlp3_forward_hostio(torch::Tensor records, torch::Tensor out, torch::Tensor blob, int64_t H,
+                             std::vector<double> norm, int64_t variant) {
+  TORCH_CHECK(!records.is_cuda() && records.is_pinned() && !out.is_cuda() && out.is_pinned(),
+              "records/out must be pinned host tensors");
+  TORCH_CHECK(records.scalar_type() == torch::kInt32 && records.dim() == 2 &&
+                  (records.size(1) == 4 || records.size(1) == 2) && records.is_contiguous(),
+              "records must be contiguous int32 [B,4] or [B,2]");
+  TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.numel() == records.size(0) &&
+              out.is_contiguous(), "out must be f32 [B]");
+  check_dev(blob, "blob");
+  TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
+  TORCH_CHECK(norm.size() == 8, "norm must hold 4 scales + 4 shifts");
+  const c10::DeviceGuard guard(blob.device());
+  void* drec = nullptr;
+  void* dout = nullptr;
+  RT_CHECK_HIP(hipHostGetDevicePointer(&drec, records.data_ptr(), 0));
+  RT_CHECK_HIP(hipHostGetDevicePointer(&dout, out.data_ptr(), 0));
+  rt::NormParams np;
+  for (int i = 0; i < 4; ++i) {
+    np.scale[i] = (float)norm[i];
+    np.shift[i] = (float)norm[4 + i];
+  }
+  RT_CHECK_HIP(rt::launch_eta_mlp3_fwd(drec, (float*)dout, (int)records.size(0), blob.data_ptr(),
+                                       (int)H, np, (int)variant, num_cus(blob.device().index()),
+                                       cur_stream(blob), records.size(1) == 2));
 }
 
 torch::Tensor eta_featurize(torch::Tensor records) {
@@ -247,6 +278,8 @@ void wgrad_reduce(torch::Tensor slab, torch::Tensor G) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "routest_amd native gfx950 kernels";
   m.def("eta_mlp3_forward", &eta_mlp3_forward, "fused featurize + 3-layer MLP forward (bf16 MFMA)");
+  m.def("eta_mlp3_forward_hostio", &eta_mlp3_forward_hostio,
+        "zero-copy: fused kernel reads records / writes minutes in pinned host memory");
   m.def("eta_featurize", &eta_featurize, "K1: packed records -> R16 features [B,12] fp32");
   m.def("eta_mlp3_blob_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_blob_bytes((int)H); });
   m.def("route_haversine_matrix", &route_haversine_matrix, "K5: batched haversine matrices (f64)");

@@ -10,6 +10,7 @@
 // (routest_amd/ops/eta_mlp.py::pack_mlp3).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
 #include <stdint.h>
 
 namespace rt {
@@ -63,6 +64,38 @@ __device__ __forceinline__ void featurize_f32(const int4 rc, const int h, const 
     const float hrn = hour * np.scale[1] + np.shift[1];
     const float kmn = km * np.scale[2] + np.shift[2];
     const float agn = age * np.scale[3] + np.shift[3];
+    const float kmh = (float)(__bf16)kmn;
+    const float agh = (float)(__bf16)agn;
+    f[0] = wdn;
+    f[1] = hrn;
+    f[2] = kmh;
+    f[3] = agh;
+    f[4] = kmn - kmh;
+    f[5] = agn - agh;
+    f[6] = 1.f;
+    f[7] = 1.f;
+  }
+}
+
+// Compact 8-byte record (features.py::RECORD8_DTYPE): x = distance_m bits, y = fp16 age |
+// weekday << 16 | hour << 19 | weather << 24 | traffic << 27.  Same lane-half feature split.
+__device__ __forceinline__ void featurize8_f32(const int2 rc, const int h, const NormParams& np,
+                                               float f[8]) {
+  const unsigned pk = (unsigned)rc.y;
+  if (h == 0) {
+    const int w = (pk >> 24) & 7;
+    const int t = (pk >> 27) & 7;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] = (w == j) ? 1.f : 0.f;
+      f[4 + j] = (t == j) ? 1.f : 0.f;
+    }
+  } else {
+    const float wdn = (float)((pk >> 16) & 7) * np.scale[0] + np.shift[0];
+    const float hrn = (float)((pk >> 19) & 31) * np.scale[1] + np.shift[1];
+    const float kmn = (__int_as_float(rc.x) / 1000.f) * np.scale[2] + np.shift[2];
+    const float agn = __half2float(__ushort_as_half((unsigned short)(pk & 0xffffu))) * np.scale[3] +
+                      np.shift[3];
     const float kmh = (float)(__bf16)kmn;
     const float agh = (float)(__bf16)agn;
     f[0] = wdn;

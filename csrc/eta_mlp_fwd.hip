@@ -27,9 +27,29 @@
 
 namespace rt {
 
-template <int H, bool LDSW, int TPB, bool PIN = false>
+// Record loads for the two wire formats (16-byte full record, 8-byte compact record).
+template <bool REC8>
+struct RecT;
+template <>
+struct RecT<false> {
+  using T = int4;
+  static __device__ __forceinline__ T zero() { return make_int4(0, 0, 0, 0); }
+  static __device__ __forceinline__ void feat(const T& r, int h, const NormParams& np, float f[8]) {
+    featurize_f32(r, h, np, f);
+  }
+};
+template <>
+struct RecT<true> {
+  using T = int2;
+  static __device__ __forceinline__ T zero() { return make_int2(0, 0); }
+  static __device__ __forceinline__ void feat(const T& r, int h, const NormParams& np, float f[8]) {
+    featurize8_f32(r, h, np, f);
+  }
+};
+
+template <int H, bool LDSW, int TPB, bool PIN = false, bool REC8 = false>
 __global__ __launch_bounds__(TPB, LDSW ? TPB / 256 : 1) void eta_mlp3_fwd_kernel(
-    const int4* __restrict__ rec, float* __restrict__ out, int B,
+    const typename RecT<REC8>::T* __restrict__ rec, float* __restrict__ out, int B,
     const unsigned char* __restrict__ blob, NormParams np) {
   constexpr int KS = H / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -50,11 +70,19 @@ __global__ __launch_bounds__(TPB, LDSW ? TPB / 256 : 1) void eta_mlp3_fwd_kernel
   const int ntiles = (B + 31) >> 5;
   const int stride = gridDim.x * wpb;
 
-  for (int tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntiles; tile += stride) {
+  // records are prefetched one tile ahead: with zero-copy I/O they come straight from pinned host
+  // memory over PCIe, and the next tile's load then overlaps this tile's ~4k MFMA cycles
+  int tile = blockIdx.x * wpb + (threadIdx.x >> 6);
+  using R = RecT<REC8>;
+  typename R::T rc_next = R::zero();
+  if (tile < ntiles && tile * 32 + r < B) rc_next = rec[tile * 32 + r];
+  for (; tile < ntiles; tile += stride) {
     const int row = tile * 32 + r;
-    const int4 rc = row < B ? rec[row] : make_int4(0, 0, 0, 0);
+    const typename R::T rc = rc_next;
+    const int nrow = (tile + stride) * 32 + r;
+    if (tile + stride < ntiles && nrow < B) rc_next = rec[nrow];
     float f[8];
-    featurize_f32(rc, h, np, f);
+    R::feat(rc, h, np, f);
     const bf16x8 xb = to_bf16x8(f);
 
     bf16x8 h1[KS];
@@ -87,15 +115,16 @@ __global__ __launch_bounds__(256) void eta_featurize_kernel(const int4* __restri
 }
 
 // Persistent LDS-staged launch: one workgroup of T threads per CU (139 KiB of LDS at H = 256).
-template <int H, int T, bool PIN>
+template <int H, int T, bool PIN, bool REC8>
 static hipError_t launch_lds(const void* rec, float* out, int B, const void* blob,
                              const NormParams& np, int num_cus, hipStream_t stream) {
+  using RT = typename RecT<REC8>::T;
   using L = Mlp3Layout<H>;
   static bool attr_set[64] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (!attr_set[dev & 63]) {
-    hipError_t e = hipFuncSetAttribute((const void*)eta_mlp3_fwd_kernel<H, true, T, PIN>,
+    hipError_t e = hipFuncSetAttribute((const void*)eta_mlp3_fwd_kernel<H, true, T, PIN, REC8>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::BLOB);
     if (e != hipSuccess) return e;
     attr_set[dev & 63] = true;
@@ -103,16 +132,17 @@ static hipError_t launch_lds(const void* rec, float* out, int B, const void* blo
   const int ntiles = (B + 31) / 32;
   int grid = (ntiles + T / 64 - 1) / (T / 64);
   if (grid > num_cus) grid = num_cus;
-  hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, true, T, PIN>), dim3(grid), dim3(T), L::BLOB, stream,
-                     (const int4*)rec, out, B, (const unsigned char*)blob, np);
+  hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, true, T, PIN, REC8>), dim3(grid), dim3(T), L::BLOB,
+                     stream, (const RT*)rec, out, B, (const unsigned char*)blob, np);
   return hipGetLastError();
 }
 
-template <int H>
+template <int H, bool REC8>
 static hipError_t launch_fwd_h(const void* rec, float* out, int B, const void* blob,
                                const NormParams& np, int variant, int num_cus, hipStream_t stream) {
+  using RT = typename RecT<REC8>::T;
   // variant: -1 auto, 0 global weights, LDS-staged: 1 = 512 thr, 2 = 768 thr, 3/4 = same + pinned
-  // read/MFMA interleave
+  // read/MFMA interleave (auto -> 3, the measured best)
   using L = Mlp3Layout<H>;
   const int ntiles = (B + 31) / 32;
   if (ntiles == 0) return hipSuccess;
@@ -120,26 +150,35 @@ static hipError_t launch_fwd_h(const void* rec, float* out, int B, const void* b
   bool use_lds = lds_fits && (variant >= 1 || (variant < 0 && ntiles >= num_cus * 8 * 2));
   if (use_lds) {
     switch (variant) {
-      case 2: return launch_lds<H, 768, false>(rec, out, B, blob, np, num_cus, stream);
-      case 3: return launch_lds<H, 512, true>(rec, out, B, blob, np, num_cus, stream);
-      case 4: return launch_lds<H, 768, true>(rec, out, B, blob, np, num_cus, stream);
-      default: return launch_lds<H, 512, false>(rec, out, B, blob, np, num_cus, stream);
+      case 2: return launch_lds<H, 768, false, REC8>(rec, out, B, blob, np, num_cus, stream);
+      case 1: return launch_lds<H, 512, false, REC8>(rec, out, B, blob, np, num_cus, stream);
+      case 4: return launch_lds<H, 768, true, REC8>(rec, out, B, blob, np, num_cus, stream);
+      default: return launch_lds<H, 512, true, REC8>(rec, out, B, blob, np, num_cus, stream);
     }
   } else {
     // 4 waves per workgroup, one tile per wave
     int grid = (ntiles + 3) / 4;
-    hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, false, 256>), dim3(grid), dim3(256), 0, stream,
-                       (const int4*)rec, out, B, (const unsigned char*)blob, np);
+    hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, false, 256, false, REC8>), dim3(grid), dim3(256), 0,
+                       stream, (const RT*)rec, out, B, (const unsigned char*)blob, np);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_eta_mlp3_fwd(const void* rec, float* out, int B, const void* blob, int H,
-                               const NormParams& np, int variant, int num_cus, hipStream_t stream) {
+                               const NormParams& np, int variant, int num_cus, hipStream_t stream,
+                               bool rec8) {
+  if (rec8) {
+    switch (H) {
+      case 64: return launch_fwd_h<64, true>(rec, out, B, blob, np, variant, num_cus, stream);
+      case 128: return launch_fwd_h<128, true>(rec, out, B, blob, np, variant, num_cus, stream);
+      case 256: return launch_fwd_h<256, true>(rec, out, B, blob, np, variant, num_cus, stream);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (H) {
-    case 64: return launch_fwd_h<64>(rec, out, B, blob, np, variant, num_cus, stream);
-    case 128: return launch_fwd_h<128>(rec, out, B, blob, np, variant, num_cus, stream);
-    case 256: return launch_fwd_h<256>(rec, out, B, blob, np, variant, num_cus, stream);
+    case 64: return launch_fwd_h<64, false>(rec, out, B, blob, np, variant, num_cus, stream);
+    case 128: return launch_fwd_h<128, false>(rec, out, B, blob, np, variant, num_cus, stream);
+    case 256: return launch_fwd_h<256, false>(rec, out, B, blob, np, variant, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }

@@ -23,7 +23,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from ..models.features import RECORD_DTYPE
+from ..models.features import RECORD8_DTYPE, RECORD_DTYPE
 from ..models.mlp3 import EtaMLP
 from . import _ext
 
@@ -129,8 +129,29 @@ def records_to_tensor(rec: np.ndarray) -> torch.Tensor:
     return torch.from_numpy(rec.view(np.int32).reshape(-1, 4))
 
 
+def records8_to_tensor(rec8: np.ndarray) -> torch.Tensor:
+    """numpy compact (8-byte) records -> int32 [B,2] tensor view."""
+    rec8 = np.ascontiguousarray(rec8, dtype=RECORD8_DTYPE)
+    return torch.from_numpy(rec8.view(np.int32).reshape(-1, 2))
+
+
+def featurize8_torch(rec8_i32: torch.Tensor) -> torch.Tensor:
+    """PyTorch reference of K1 for compact records: int32 [B,2] -> [B,12] fp32."""
+    dist = rec8_i32[:, 0].view(torch.float32)
+    pk = rec8_i32[:, 1].to(torch.int64) & 0xFFFFFFFF
+    age = (pk & 0xFFFF).to(torch.int16).view(torch.float16).float()
+    w = (pk >> 24) & 7
+    t = (pk >> 27) & 7
+    ar = torch.arange(4, device=rec8_i32.device)
+    return torch.cat([(w[:, None] == ar[None]).float(), (t[:, None] == ar[None]).float(),
+                      ((pk >> 16) & 7).float()[:, None], ((pk >> 19) & 31).float()[:, None],
+                      (dist / 1000.0)[:, None], age[:, None]], 1)
+
+
 def featurize_torch(rec_i32: torch.Tensor) -> torch.Tensor:
-    """PyTorch reference of K1 on any device: int32 [B,4] -> R16 features [B,12] fp32."""
+    """PyTorch reference of K1 on any device: int32 [B,4] (or compact [B,2]) -> [B,12] fp32."""
+    if rec_i32.shape[1] == 2:
+        return featurize8_torch(rec_i32)
     r = rec_i32
     dist = r[:, 0].view(torch.float32) if r.dtype == torch.int32 else r[:, 0]
     age = r[:, 1].view(torch.float32)
@@ -187,6 +208,12 @@ class EtaMlpKernel:
         self._C = _ext.native(required=True) if self.device.type == "cuda" else None
         if self.device.type == "cuda" and self.hidden not in (64, 128, 256):
             raise ValueError(f"HIP MLP kernel supports hidden in (64,128,256), got {self.hidden}")
+
+    def forward_hostio(self, rec_pinned: torch.Tensor, out_pinned: torch.Tensor) -> None:
+        """Zero-copy scoring: the kernel reads pinned host records and writes pinned host minutes
+        directly over PCIe (asynchronous on the current stream; synchronize before reading)."""
+        self._C.eta_mlp3_forward_hostio(rec_pinned, out_pinned, self.packed.blob, self.hidden,
+                                        self.packed.norm, self.variant)
 
     def __call__(self, rec: torch.Tensor) -> torch.Tensor:
         if self.device.type == "cuda":

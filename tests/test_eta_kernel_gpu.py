@@ -86,3 +86,40 @@ def test_mlp3_forward_graph_capture():
     g.replay()
     torch.cuda.synchronize()
     torch.testing.assert_close(out, k(rt))
+
+
+@pytest.mark.parametrize("variant,B", [(0, 777), (1, 300_001)])
+def test_mlp3_forward_zero_copy_host_io(variant, B):
+    m = _model(256, 3)
+    k = EtaMlpKernel(m, torch.device("cuda:0"), variant=variant)
+    rec, _ = synth_records(B, 21)
+    host = records_to_tensor(rec).pin_memory()
+    out = torch.full((B,), float("nan")).pin_memory()
+    k.forward_hostio(host, out)
+    torch.cuda.synchronize()
+    ref = k(host.cuda()).cpu()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 3])
+def test_mlp3_forward_compact_records(variant):
+    from routest_amd.models.features import compact_to_features, records_to_compact
+    from routest_amd.ops.eta_mlp import records8_to_tensor
+    m = _model(256, 4)
+    k = EtaMlpKernel(m, torch.device("cuda:0"), variant=variant)
+    rec, _ = synth_records(70_001, 22)
+    rec["weather"][:100] = 255
+    rec["driver_age"][100:200] = 33.7
+    r8 = records_to_compact(rec)
+    x8 = compact_to_features(r8)
+    x16 = records_to_features(rec)
+    assert np.array_equal(x8[:, :11], x16[:, :11])
+    assert np.allclose(x8[:, 11], x16[:, 11], atol=0.02)
+    got = k(records8_to_tensor(r8).cuda()).cpu()
+    ref = m(torch.from_numpy(x8)).detach()
+    torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
+    host = records8_to_tensor(r8).pin_memory()
+    out = torch.empty(len(r8)).pin_memory()
+    k.forward_hostio(host, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, got)
