@@ -273,6 +273,99 @@ void wgrad_reduce(torch::Tensor slab, torch::Tensor G) {
                                        cur_stream(G)));
 }
 
+void check_csr(const torch::Tensor& indptr, const torch::Tensor& indices, const torch::Tensor& values) {
+  for (auto* t : {&indptr, &indices, &values}) check_dev(*t, "csr");
+  TORCH_CHECK(indptr.scalar_type() == torch::kInt32 && indices.scalar_type() == torch::kInt32 &&
+              values.scalar_type() == torch::kFloat32, "CSR must be int32/int32/f32");
+  TORCH_CHECK(indices.numel() == values.numel(), "indices/values length");
+}
+
+void gcn_agg_gemm(torch::Tensor X, torch::Tensor indptr, torch::Tensor indices, torch::Tensor values,
+                  torch::Tensor wfrag, c10::optional<torch::Tensor> bias, torch::Tensor Y, int64_t fin,
+                  int64_t fout, bool agg, bool relu, int64_t row0, int64_t row1) {
+  check_dev(X, "X");
+  check_dev(wfrag, "wfrag");
+  check_dev(Y, "Y");
+  check_csr(indptr, indices, values);
+  TORCH_CHECK(X.scalar_type() == torch::kBFloat16 && X.dim() == 2 && X.size(1) == fin, "X bf16 [N,fin]");
+  TORCH_CHECK(Y.scalar_type() == torch::kBFloat16 && Y.dim() == 2 && Y.size(1) == fout &&
+              Y.size(0) >= row1, "Y bf16 [N,fout]");
+  TORCH_CHECK(wfrag.scalar_type() == torch::kBFloat16 && wfrag.numel() == fin * fout, "wfrag");
+  TORCH_CHECK(0 <= row0 && row0 <= row1 && row1 <= X.size(0) && indptr.numel() >= row1 + 1, "rows");
+  const float* bptr = nullptr;
+  if (bias.has_value()) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == fout, "bias f32 [fout]");
+    bptr = bias->data_ptr<float>();
+  }
+  const c10::DeviceGuard guard(X.device());
+  RT_CHECK_HIP(rt::launch_gcn_agg_gemm(X.data_ptr(), indptr.data_ptr<int>(), indices.data_ptr<int>(),
+                                       values.data_ptr<float>(), wfrag.data_ptr(), bptr, Y.data_ptr(),
+                                       (int)fin, (int)fout, agg, relu, (int)row0, (int)row1,
+                                       num_cus(X.device().index()), cur_stream(X)));
+}
+
+void gcn_spmm_score(torch::Tensor Z, torch::Tensor indptr, torch::Tensor indices, torch::Tensor values,
+                    torch::Tensor b2, torch::Tensor wo, double bo, torch::Tensor delay, int64_t row0,
+                    int64_t row1) {
+  check_dev(Z, "Z");
+  check_csr(indptr, indices, values);
+  TORCH_CHECK(Z.scalar_type() == torch::kBFloat16 && Z.dim() == 2 && Z.size(1) == 32, "Z bf16 [N,32]");
+  TORCH_CHECK(b2.numel() == 32 && wo.numel() == 32, "b2/wo [32]");
+  TORCH_CHECK(delay.scalar_type() == torch::kFloat32 && delay.numel() >= row1, "delay f32 [N]");
+  const c10::DeviceGuard guard(Z.device());
+  RT_CHECK_HIP(rt::launch_gcn_spmm_score(Z.data_ptr(), indptr.data_ptr<int>(), indices.data_ptr<int>(),
+                                         values.data_ptr<float>(), b2.data_ptr<float>(),
+                                         wo.data_ptr<float>(), (float)bo, delay.data_ptr<float>(),
+                                         (int)row0, (int)row1, cur_stream(Z)));
+}
+
+torch::Tensor route_score(torch::Tensor rptr, torch::Tensor nodes, torch::Tensor lat, torch::Tensor lon,
+                          torch::Tensor delay) {
+  for (auto* t : {&rptr, &nodes, &lat, &lon, &delay}) check_dev(*t, "route_score input");
+  TORCH_CHECK(rptr.scalar_type() == torch::kInt32 && nodes.scalar_type() == torch::kInt32, "i32 routes");
+  TORCH_CHECK(lat.scalar_type() == torch::kFloat32 && lon.scalar_type() == torch::kFloat32 &&
+              delay.scalar_type() == torch::kFloat32, "f32 lat/lon/delay");
+  const c10::DeviceGuard guard(rptr.device());
+  const int R = (int)rptr.numel() - 1;
+  auto score = torch::empty({R}, delay.options());
+  RT_CHECK_HIP(rt::launch_route_score(rptr.data_ptr<int>(), nodes.data_ptr<int>(), lat.data_ptr<float>(),
+                                      lon.data_ptr<float>(), delay.data_ptr<float>(),
+                                      score.data_ptr<float>(), R, cur_stream(rptr)));
+  return score;
+}
+
+// Runs queries [q0, q0 + slots) of (src, dst); workspace g/parent [S,N], heap [S,cap] (int64),
+// touched [S,cap] must be initialised to (inf, 0x7fffffff) once; the kernel restores them.
+void astar(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torch::Tensor lat,
+           torch::Tensor lon, torch::Tensor src, torch::Tensor dst, torch::Tensor g,
+           torch::Tensor parent, torch::Tensor heap, torch::Tensor touched, torch::Tensor out_cost,
+           torch::Tensor out_len, torch::Tensor out_status, torch::Tensor out_path, int64_t q0,
+           int64_t max_iters, double inv_vmax) {
+  for (auto* t : {&indptr, &indices, &cost, &lat, &lon, &src, &dst, &g, &parent, &heap, &touched,
+                  &out_cost, &out_len, &out_status, &out_path})
+    check_dev(*t, "astar tensor");
+  const int64_t N = lat.numel();
+  TORCH_CHECK(indptr.numel() == N + 1 && cost.numel() == indices.numel(), "graph shapes");
+  TORCH_CHECK(g.dim() == 2 && g.size(1) == N && parent.sizes() == g.sizes(), "g/parent must be [S,N]");
+  TORCH_CHECK(heap.scalar_type() == torch::kInt64 && heap.dim() == 2 && heap.size(0) == g.size(0),
+              "heap must be int64 [S,cap]");
+  TORCH_CHECK(touched.sizes() == heap.sizes(), "touched must be [S,cap]");
+  const int64_t Q = src.numel();
+  TORCH_CHECK(dst.numel() == Q && out_cost.numel() == Q && out_len.numel() == Q &&
+              out_status.numel() == Q && out_path.dim() == 2 && out_path.size(0) == Q, "outputs [Q]");
+  TORCH_CHECK(0 <= q0 && q0 <= Q, "q0");
+  const c10::DeviceGuard guard(g.device());
+  RT_CHECK_HIP(rt::launch_astar(indptr.data_ptr<int>(), indices.data_ptr<int>(), cost.data_ptr<float>(),
+                                lat.data_ptr<float>(), lon.data_ptr<float>(), src.data_ptr<int>(),
+                                dst.data_ptr<int>(), g.data_ptr<float>(), parent.data_ptr<int>(),
+                                heap.data_ptr(), touched.data_ptr<int>(), out_cost.data_ptr<float>(),
+                                out_len.data_ptr<int>(), out_status.data_ptr<int>(),
+                                out_path.data_ptr<int>(), (int)N, (int)Q, (int)q0, (int)g.size(0),
+                                (int)heap.size(1), (int)out_path.size(1), (int)max_iters,
+                                (float)inv_vmax, cur_stream(g)));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -292,5 +385,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad", &wgrad, "split-K weight-gradient GEMM (K = batch) into fp32 slabs");
   m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs");
   m.def("num_cus", [](int64_t dev) { return (int64_t)num_cus((int)dev); });
+  m.def("gcn_agg_gemm", &gcn_agg_gemm, "K8: fused CSR aggregation + MFMA GEMM + bias/ReLU");
+  m.def("gcn_spmm_score", &gcn_spmm_score, "K8: layer-2 aggregation + delay head");
+  m.def("route_score", &route_score, "K8: per-route delay-weighted length");
+  m.def("astar", &astar, "K9: batched A* (one lane per query) with learned edge costs");
   m.attr("ARCH") = "gfx950";
 }

@@ -1,0 +1,196 @@
+// K8: 2-layer GCN road-graph route scorer on gfx950 (north-star config 4; no reference
+// counterpart — the reference only calls remote routing engines, RO/Flaskr/utils.py:55,97,151).
+//
+//   H1    = relu( (Â X) W1 + b1 )          gcn_agg_gemm_kernel<FIN=32, FOUT=128, AGG=true>
+//   Z     = H1 W2                          gcn_agg_gemm_kernel<128, 32, AGG=false>  (transform first:
+//                                          aggregating 32 features is 4x cheaper than 128)
+//   delay = 0.5 + softplus( (Â Z + b2) . wo + bo )   gcn_spmm_score_kernel (aggregation + head)
+//   score(route) = sum_i delay(v_i) * |v_i v_{i+1}|   route_score_kernel (one wave per route)
+//
+// gcn_agg_gemm_kernel: each wave owns a 32-node tile.  Lanes are grouped FIN/8 per node (16 B of
+// bf16 features each) and walk that node's CSR neighbour list with fp32 accumulation; the aggregated
+// tile goes to the wave's private LDS tile (row-major, padded), which is directly the A operand
+// (row = node, k = feature) of mfma_f32_32x32x16_bf16.  W is staged into LDS once per workgroup in
+// B-fragment order (lane-linear 16-B reads).  The accumulator has the output feature on the lane,
+// so the bias is a per-lane scalar and each result register is one node's 32 contiguous outputs.
+#include "common.h"
+#include "ops.h"
+
+namespace rt {
+
+template <int FIN, int FOUT, bool AGG, bool RELU>
+__global__ __launch_bounds__(256) void gcn_agg_gemm_kernel(
+    const __bf16* __restrict__ X, const int* __restrict__ indptr, const int* __restrict__ indices,
+    const float* __restrict__ values, const bf16x8* __restrict__ wfrag, const float* __restrict__ bias,
+    __bf16* __restrict__ Y, int row0, int row1) {
+  constexpr int G = FIN / 8, RPP = 64 / G, KS = FIN / 16, NT = FOUT / 32;
+  constexpr int LDT = FIN + 8;  // padded LDS row (bf16 elements): conflict-free ds_read_b128
+  __shared__ __attribute__((aligned(16))) bf16x8 s_w[NT * KS * 64];
+  __shared__ __attribute__((aligned(16))) __bf16 s_t[4][32 * LDT];
+  for (int i = threadIdx.x; i < NT * KS * 64; i += blockDim.x) s_w[i] = wfrag[i];
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  __bf16* tile = s_t[w];
+  const int n_rows = row1 - row0;
+  const int ntiles = (n_rows + 31) / 32;
+  for (int t = blockIdx.x * 4 + w; t < ntiles; t += gridDim.x * 4) {
+    const int base = row0 + t * 32;
+#pragma unroll
+    for (int pass = 0; pass < 32 / RPP; ++pass) {
+      const int rr = pass * RPP + lane / G;
+      const int c = (lane % G) * 8;
+      const int v = base + rr;
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+      if (v < row1) {
+        if constexpr (AGG) {
+          const int e0 = indptr[v], e1 = indptr[v + 1];
+          for (int e = e0; e < e1; ++e) {
+            const int u = indices[e];
+            const float wv = values[e];
+            const bf16x8 x = *reinterpret_cast<const bf16x8*>(X + (size_t)u * FIN + c);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += wv * (float)x[j];
+          }
+        } else {
+          const bf16x8 x = *reinterpret_cast<const bf16x8*>(X + (size_t)v * FIN + c);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] = (float)x[j];
+        }
+      }
+      *reinterpret_cast<bf16x8*>(tile + rr * LDT + c) = to_bf16x8(acc);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // this wave's LDS writes complete (wave-private tile)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + (lane & 31) * LDT + 16 * ks + 8 * h);
+        acc = mfma32(a, s_w[(nt * KS + ks) * 64 + lane], acc);
+      }
+      const int n = 32 * nt + (lane & 31);
+      const float b = bias ? bias[n] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int v = base + (e & 3) + 8 * (e >> 2) + 4 * h;
+        float o = acc[e] + b;
+        if (RELU) o = fmaxf(o, 0.f);
+        if (v < row1) Y[(size_t)v * FOUT + n] = (__bf16)o;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// delay[v] = 0.5 + softplus( sum_f (sum_u Â[v,u] Z[u,f] + b2[f]) * wo[f] + bo ),  F = 32 (4 lanes/row)
+__global__ __launch_bounds__(256) void gcn_spmm_score_kernel(
+    const __bf16* __restrict__ Z, const int* __restrict__ indptr, const int* __restrict__ indices,
+    const float* __restrict__ values, const float* __restrict__ b2, const float* __restrict__ wo,
+    float bo, float* __restrict__ delay, int row0, int row1) {
+  constexpr int F = 32, G = F / 8;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int v = row0 + gid / G;
+  const int c = (gid % G) * 8;
+  float part = 0.f;
+  if (v < row1) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    const int e0 = indptr[v], e1 = indptr[v + 1];
+    for (int e = e0; e < e1; ++e) {
+      const int u = indices[e];
+      const float wv = values[e];
+      const bf16x8 z = *reinterpret_cast<const bf16x8*>(Z + (size_t)u * F + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += wv * (float)z[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part += (acc[j] + b2[c + j]) * wo[c + j];
+  }
+  part += __shfl_xor(part, 1);
+  part += __shfl_xor(part, 2);
+  if (v < row1 && (gid % G) == 0) {
+    const float x = part + bo;
+    const float sp = x > 20.f ? x : log1pf(expf(x));
+    delay[v] = 0.5f + sp;
+  }
+}
+
+// score[r] = sum_i delay[v_i] * haversine(v_i, v_{i+1}) over route r's node list (one wave / route)
+__global__ __launch_bounds__(256) void route_score_kernel(const int* __restrict__ rptr,
+                                                          const int* __restrict__ nodes,
+                                                          const float* __restrict__ lat,
+                                                          const float* __restrict__ lon,
+                                                          const float* __restrict__ delay,
+                                                          float* __restrict__ score, int R) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const int p0 = rptr[r], p1 = rptr[r + 1];
+  float s = 0.f;
+  const float k = 0.017453292519943295f;
+  for (int i = p0 + lane; i < p1 - 1; i += 64) {
+    const int a = nodes[i], b = nodes[i + 1];
+    const float la1 = lat[a] * k, la2 = lat[b] * k;
+    const float dphi = la2 - la1, dl = (lon[b] - lon[a]) * k;
+    const float s1 = __sinf(0.5f * dphi), s2 = __sinf(0.5f * dl);
+    const float hv = s1 * s1 + __cosf(la1) * __cosf(la2) * s2 * s2;
+    const float d = 2.f * 6371000.f * asinf(sqrtf(fminf(1.f, fmaxf(0.f, hv))));
+    s += delay[a] * d;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) score[r] = s;
+}
+
+hipError_t launch_gcn_agg_gemm(const void* X, const int* indptr, const int* indices,
+                               const float* values, const void* wfrag, const float* bias, void* Y,
+                               int fin, int fout, bool agg, bool relu, int row0, int row1,
+                               int num_cus, hipStream_t stream) {
+  const int ntiles = (row1 - row0 + 31) / 32;
+  if (ntiles <= 0) return hipSuccess;
+  int grid = (ntiles + 3) / 4;
+  if (grid > num_cus * 4) grid = num_cus * 4;
+#define RT_GCN(FI, FO, AG, RL)                                                                   \
+  if (fin == FI && fout == FO && agg == AG && relu == RL) {                                      \
+    hipLaunchKernelGGL((gcn_agg_gemm_kernel<FI, FO, AG, RL>), dim3(grid), dim3(256), 0, stream,  \
+                       (const __bf16*)X, indptr, indices, values, (const bf16x8*)wfrag, bias,    \
+                       (__bf16*)Y, row0, row1);                                                  \
+    return hipGetLastError();                                                                    \
+  }
+  RT_GCN(32, 128, true, true)
+  RT_GCN(128, 32, false, false)
+  RT_GCN(64, 64, true, true)
+  RT_GCN(32, 32, true, true)
+  RT_GCN(128, 128, true, true)
+#undef RT_GCN
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_gcn_spmm_score(const void* Z, const int* indptr, const int* indices,
+                                 const float* values, const float* b2, const float* wo, float bo,
+                                 float* delay, int row0, int row1, hipStream_t stream) {
+  const long long threads = (long long)(row1 - row0) * 4;
+  if (threads <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gcn_spmm_score_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     stream, (const __bf16*)Z, indptr, indices, values, b2, wo, bo, delay, row0,
+                     row1);
+  return hipGetLastError();
+}
+
+hipError_t launch_route_score(const int* rptr, const int* nodes, const float* lat,
+                              const float* lon, const float* delay, float* score, int R,
+                              hipStream_t stream) {
+  if (R <= 0) return hipSuccess;
+  hipLaunchKernelGGL(route_score_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, rptr, nodes, lat,
+                     lon, delay, score, R);
+  return hipGetLastError();
+}
+
+}  // namespace rt

@@ -39,6 +39,25 @@ hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, 
                                hipStream_t stream);
 size_t wgrad_lds_bytes(int NT);
 
+// ---- GCN route scorer (K8) : gcn.hip ----
+hipError_t launch_gcn_agg_gemm(const void* X, const int* indptr, const int* indices,
+                               const float* values, const void* wfrag, const float* bias, void* Y,
+                               int fin, int fout, bool agg, bool relu, int row0, int row1,
+                               int num_cus, hipStream_t stream);
+hipError_t launch_gcn_spmm_score(const void* Z, const int* indptr, const int* indices,
+                                 const float* values, const float* b2, const float* wo, float bo,
+                                 float* delay, int row0, int row1, hipStream_t stream);
+hipError_t launch_route_score(const int* rptr, const int* nodes, const float* lat,
+                              const float* lon, const float* delay, float* score, int R,
+                              hipStream_t stream);
+
+// ---- batched A* (K9) : astar.hip ----
+hipError_t launch_astar(const int* indptr, const int* indices, const float* cost, const float* lat,
+                        const float* lon, const int* src, const int* dst, float* g, int* parent,
+                        void* heap, int* touched, float* out_cost, int* out_len, int* out_status,
+                        int* out_path, int N, int Q, int q0, int slots, int cap, int max_path,
+                        int max_iters, float inv_vmax, hipStream_t stream);
+
 // ---- batched routing (K5 distance matrix + K6 greedy CVRP) : route_kernels.hip ----
 hipError_t launch_haversine_matrix(const double* lat, const double* lon, const int* npts, int R,
                                    int NM, double circuity, double* D, hipStream_t stream);

@@ -1,0 +1,164 @@
+"""Synthetic road graph for the GCN route scorer (config 4) and batched A* (config 5).
+
+The reference routes over a remote road network (ORS: ``RO/Flaskr/utils.py:55,97,151``; OSRM in the
+dashboard).  Offline, we generate a reproducible road-like graph over the Metro-Manila box the seed
+locations live in (``LV/database/seeders/LocationsTableSeeder.php:13-34``):
+
+* nodes on a jittered grid (``rows x cols``, 100k nodes by default);
+* 4-neighbour streets plus random diagonals; every 8th row/col is a secondary road, every 32nd a
+  primary, every 64th a highway (speed limits 30/45/60/80 km/h);
+* undirected, stored as directed CSR (both directions), edge lengths by haversine;
+* GCN operator Â = D^-1/2 (A + I) D^-1/2 as CSR values (self loops included);
+* 32 node features (position, degree, incident road-class mix, fixed random projections).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+
+from ..routing.providers import haversine_m
+
+BBOX = (14.35, 120.90, 14.80, 121.15)   # lat_min, lon_min, lat_max, lon_max
+CLASS_SPEED_KMH = np.array([30.0, 45.0, 60.0, 80.0], dtype=np.float32)
+
+
+@dataclass
+class RoadGraph:
+    lat: np.ndarray          # [N] f64
+    lon: np.ndarray          # [N] f64
+    indptr: np.ndarray       # [N+1] i32 (CSR over directed edges, rows = source)
+    indices: np.ndarray      # [E] i32 (targets)
+    length_m: np.ndarray     # [E] f32
+    road_class: np.ndarray   # [E] u8
+    gcn_indptr: np.ndarray   # [N+1] i32 (Â incl. self loops)
+    gcn_indices: np.ndarray  # [E+N] i32
+    gcn_values: np.ndarray   # [E+N] f32
+    features: np.ndarray     # [N, F] f32
+    rows: int = 0
+    cols: int = 0
+
+    @property
+    def num_nodes(self) -> int:
+        return int(self.lat.shape[0])
+
+    @property
+    def num_edges(self) -> int:
+        return int(self.indices.shape[0])
+
+    def degree(self) -> np.ndarray:
+        return np.diff(self.indptr)
+
+    def nearest_node(self, lat: float, lon: float) -> int:
+        from scipy.spatial import cKDTree
+        if getattr(self, "_tree", None) is None:
+            self._tree = cKDTree(np.stack([self.lat, self.lon * np.cos(np.radians(14.6))], 1))
+        _, i = self._tree.query([lat, lon * np.cos(np.radians(14.6))])
+        return int(i)
+
+    def nearest_nodes(self, lats, lons) -> np.ndarray:
+        self.nearest_node(float(self.lat[0]), float(self.lon[0]))
+        _, i = self._tree.query(np.stack([np.asarray(lats), np.asarray(lons) * np.cos(np.radians(14.6))], 1))
+        return i.astype(np.int32)
+
+    def save(self, path: str) -> None:
+        np.savez_compressed(path, **{k: getattr(self, k) for k in (
+            "lat", "lon", "indptr", "indices", "length_m", "road_class", "gcn_indptr", "gcn_indices",
+            "gcn_values", "features")}, rows=self.rows, cols=self.cols)
+
+    @staticmethod
+    def load(path: str) -> "RoadGraph":
+        z = np.load(path, allow_pickle=False)
+        kw = {k: z[k] for k in z.files if k not in ("rows", "cols")}
+        return RoadGraph(**kw, rows=int(z["rows"]), cols=int(z["cols"]))
+
+
+def _edge_class(r0, c0, r1, c1) -> np.ndarray:
+    """Road class of a street segment by the grid line it runs along."""
+    horiz = r0 == r1
+    line = np.where(horiz, r0, c0)
+    straight = (r0 == r1) | (c0 == c1)
+    cls = np.zeros(r0.shape, dtype=np.uint8)
+    cls = np.where(straight & (line % 8 == 0), 1, cls)
+    cls = np.where(straight & (line % 32 == 0), 2, cls)
+    cls = np.where(straight & (line % 64 == 0), 3, cls)
+    return cls.astype(np.uint8)
+
+
+def synth_road_graph(num_nodes: int = 100_000, seed: int = 0, feat_dim: int = 32,
+                     diag_prob: float = 0.15) -> RoadGraph:
+    rng = np.random.default_rng(seed)
+    rows = int(np.sqrt(num_nodes))
+    cols = int(np.ceil(num_nodes / rows))
+    n = rows * cols
+    lat0, lon0, lat1, lon1 = BBOX
+    rr, cc = np.divmod(np.arange(n), cols)
+    dlat = (lat1 - lat0) / max(1, rows - 1)
+    dlon = (lon1 - lon0) / max(1, cols - 1)
+    lat = lat0 + rr * dlat + rng.uniform(-0.3, 0.3, n) * dlat
+    lon = lon0 + cc * dlon + rng.uniform(-0.3, 0.3, n) * dlon
+
+    src, dst = [], []
+    ids = np.arange(n).reshape(rows, cols)
+    src.append(ids[:, :-1].ravel()); dst.append(ids[:, 1:].ravel())      # east
+    src.append(ids[:-1, :].ravel()); dst.append(ids[1:, :].ravel())      # south
+    d1 = rng.random((rows - 1, cols - 1)) < diag_prob
+    src.append(ids[:-1, :-1][d1]); dst.append(ids[1:, 1:][d1])           # south-east diagonals
+    s = np.concatenate(src)
+    d = np.concatenate(dst)
+    cls = _edge_class(rr[s], cc[s], rr[d], cc[d])
+    # directed both ways
+    s2 = np.concatenate([s, d])
+    d2 = np.concatenate([d, s])
+    cls2 = np.concatenate([cls, cls])
+    order = np.lexsort((d2, s2))
+    s2, d2, cls2 = s2[order], d2[order], cls2[order]
+    indptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(indptr, s2 + 1, 1)
+    indptr = np.cumsum(indptr).astype(np.int32)
+    length = haversine_m(lat[s2], lon[s2], lat[d2], lon[d2]).astype(np.float32) * np.float32(1.15)
+
+    deg = np.diff(indptr).astype(np.float64) + 1.0
+    # Â with self loops, row-sorted CSR
+    gs = np.concatenate([s2, np.arange(n)])
+    gd = np.concatenate([d2, np.arange(n)])
+    go = np.lexsort((gd, gs))
+    gs, gd = gs[go], gd[go]
+    gval = (1.0 / np.sqrt(deg[gs] * deg[gd])).astype(np.float32)
+    gptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(gptr, gs + 1, 1)
+    gptr = np.cumsum(gptr).astype(np.int32)
+
+    # node features
+    f = np.zeros((n, feat_dim), dtype=np.float32)
+    f[:, 0] = (lat - lat0) / (lat1 - lat0) * 2 - 1
+    f[:, 1] = (lon - lon0) / (lon1 - lon0) * 2 - 1
+    f[:, 2] = (deg - deg.mean()) / deg.std()
+    cls_mix = np.zeros((n, 4), dtype=np.float32)
+    np.add.at(cls_mix, (s2, cls2), 1.0)
+    f[:, 3:7] = cls_mix / np.maximum(1.0, cls_mix.sum(1, keepdims=True))
+    k = feat_dim - 7
+    proj = rng.standard_normal((2, k)).astype(np.float32)
+    f[:, 7:] = np.sin(f[:, 0:2] @ proj * 3.0)
+    return RoadGraph(lat, lon, indptr, d2.astype(np.int32), length, cls2, gptr, gd.astype(np.int32),
+                     gval, f, rows, cols)
+
+
+def synth_route_queries(g: RoadGraph, n: int, seed: int = 0, min_km: float = 1.0,
+                        max_km: float = 25.0) -> Tuple[np.ndarray, np.ndarray]:
+    """Random (source, target) node pairs with a great-circle distance in [min_km, max_km]."""
+    rng = np.random.default_rng(seed)
+    out_s, out_t = [], []
+    need = n
+    while need > 0:
+        s = rng.integers(0, g.num_nodes, need * 2)
+        t = rng.integers(0, g.num_nodes, need * 2)
+        dist = haversine_m(g.lat[s], g.lon[s], g.lat[t], g.lon[t]) / 1000.0
+        ok = (dist >= min_km) & (dist <= max_km)
+        out_s.append(s[ok][:need])
+        out_t.append(t[ok][:need])
+        need -= int(ok[:need * 2].sum()) if ok.sum() < need else need
+    s = np.concatenate(out_s)[:n].astype(np.int32)
+    t = np.concatenate(out_t)[:n].astype(np.int32)
+    return s, t

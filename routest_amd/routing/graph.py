@@ -1,0 +1,197 @@
+"""Road-graph routing: learned edge costs + batched A* (K9) + a directions provider.
+
+* :func:`edge_costs` — travel time per edge from the ETA MLP: every directed edge becomes one
+  request record (distance = edge length, plus the trip context: weather, traffic, pickup time,
+  driver age), all scored by ONE fused featurize+MLP launch (the same K1+K2 kernel as
+  ``/predict``), scaled by a road-class factor and floored at free-flow time at ``V_MAX`` so the
+  A* heuristic stays admissible.
+* :class:`BatchedAstar` — many point-to-point queries at once on the GPU (one lane per query,
+  ``csrc/astar.hip``); CPU reference = scipy Dijkstra.
+* :class:`GraphProvider` — ``directions()`` along road-graph shortest paths (replaces the
+  reference's per-trip ORS directions call, ``RO/Flaskr/utils.py:151-156``), ``matrix()`` by
+  great-circle distance (the greedy CVRP's max-distance semantics are in metres).
+"""
+from __future__ import annotations
+
+import datetime as dt
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..data.graph import RoadGraph, synth_road_graph
+from ..models.features import RECORD_DTYPE, pack_record
+from .providers import HaversineProvider, PROFILE_SPEED_MPS, _bbox, haversine_m
+
+V_MAX_MPS = 130 / 3.6
+CLASS_FACTOR = np.array([1.15, 1.0, 0.85, 0.65], dtype=np.float32)   # residential .. highway
+
+
+def edge_records(g: RoadGraph, weather: str = "Sunny", traffic: str = "Medium",
+                 pickup: Optional[dt.datetime] = None, driver_age: float = 35.0) -> np.ndarray:
+    pickup = pickup or dt.datetime(2025, 8, 25, 9, 0)
+    proto = np.array([pack_record(weather=weather, traffic=traffic, distance_m=0.0, pickup=pickup,
+                                  driver_age=driver_age)], dtype=RECORD_DTYPE)
+    rec = np.repeat(proto, g.num_edges)
+    rec["distance_m"] = g.length_m
+    return rec
+
+
+def edge_costs(g: RoadGraph, eta_model, device=None, **ctx: Any) -> np.ndarray:
+    """Seconds per directed edge: the ETA MLP's MARGINAL time for the edge's length under the
+    trip context (minutes(len) - minutes(0), so the model's fixed per-trip overhead is not charged
+    per edge), times a road-class factor, floored at length / V_MAX."""
+    from ..ops.eta_mlp import EtaMlpKernel, featurize_torch, records_to_tensor
+    er = edge_records(g, **ctx)
+    zero = er[:1].copy()
+    zero["distance_m"] = 0.0
+    rec = records_to_tensor(np.concatenate([er, zero]))
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cuda":
+        minutes = EtaMlpKernel(eta_model, dev)(rec.to(dev)).cpu().numpy()
+    else:
+        with torch.no_grad():
+            minutes = eta_model.float().cpu()(featurize_torch(rec)).numpy()
+    marginal = minutes[:-1].astype(np.float32) - np.float32(minutes[-1])
+    sec = marginal * 60.0 * CLASS_FACTOR[g.road_class]
+    return np.maximum(sec, g.length_m / V_MAX_MPS).astype(np.float32)
+
+
+def dijkstra_ref(g: RoadGraph, cost: np.ndarray, src: Sequence[int], dst: Sequence[int]) -> np.ndarray:
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import dijkstra
+    m = csr_matrix((cost.astype(np.float64), g.indices, g.indptr), shape=(g.num_nodes, g.num_nodes))
+    out = np.empty(len(src))
+    uniq = np.unique(np.asarray(src))
+    d = dijkstra(m, directed=True, indices=uniq)
+    row = {int(s): i for i, s in enumerate(uniq)}
+    for k, (s, t) in enumerate(zip(src, dst)):
+        out[k] = d[row[int(s)], int(t)]
+    return out
+
+
+class BatchedAstar:
+    """GPU batched A*; workspace sized for ``slots`` concurrent searches (dense per-slot state)."""
+
+    def __init__(self, g: RoadGraph, cost: np.ndarray, device, slots: int = 16384, cap: int = 16384,
+                 max_path: int = 4096, max_iters: int = 2_000_000):
+        from ..ops import _ext
+        self.C = _ext.native(required=True)
+        self.g = g
+        self.dev = d = torch.device(device)
+        self.indptr = torch.from_numpy(g.indptr).to(d)
+        self.indices = torch.from_numpy(g.indices).to(d)
+        self.cost = torch.from_numpy(np.asarray(cost, dtype=np.float32)).to(d)
+        self.lat = torch.from_numpy(g.lat.astype(np.float32)).to(d)
+        self.lon = torch.from_numpy(g.lon.astype(np.float32)).to(d)
+        self.slots, self.cap, self.max_path, self.max_iters = slots, cap, max_path, max_iters
+        N = g.num_nodes
+        self.gbuf = torch.full((slots, N), float("inf"), dtype=torch.float32, device=d)
+        self.parent = torch.full((slots, N), 0x7FFFFFFF, dtype=torch.int32, device=d)
+        self.heap = torch.empty((slots, cap), dtype=torch.int64, device=d)
+        self.touched = torch.empty((slots, cap), dtype=torch.int32, device=d)
+
+    def update_costs(self, cost: np.ndarray) -> None:
+        self.cost.copy_(torch.from_numpy(np.asarray(cost, dtype=np.float32)))
+
+    def run(self, src: Sequence[int], dst: Sequence[int]):
+        """Returns (cost_s [Q] tensor, path_len [Q], status [Q], paths [Q, max_path]) on device."""
+        d = self.dev
+        s = torch.as_tensor(np.asarray(src, dtype=np.int32)).to(d)
+        t = torch.as_tensor(np.asarray(dst, dtype=np.int32)).to(d)
+        Q = s.numel()
+        out_cost = torch.empty(Q, dtype=torch.float32, device=d)
+        out_len = torch.empty(Q, dtype=torch.int32, device=d)
+        out_status = torch.empty(Q, dtype=torch.int32, device=d)
+        out_path = torch.empty((Q, self.max_path), dtype=torch.int32, device=d)
+        for q0 in range(0, Q, self.slots):
+            self.C.astar(self.indptr, self.indices, self.cost, self.lat, self.lon, s, t, self.gbuf,
+                         self.parent, self.heap, self.touched, out_cost, out_len, out_status, out_path,
+                         q0, self.max_iters, 1.0 / V_MAX_MPS)
+        return out_cost, out_len, out_status, out_path
+
+    def paths(self, src, dst) -> List[Tuple[float, List[int]]]:
+        c, n, st, p = self.run(src, dst)
+        c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
+        return [(float(c[i]), p[i, :n[i]].tolist()) if st[i] == 0 else (float("nan"), [])
+                for i in range(len(c))]
+
+
+class GraphProvider(HaversineProvider):
+    """Directions along shortest paths of the road graph (durations from learned edge costs)."""
+
+    name = "graph"
+
+    def __init__(self, g: RoadGraph, cost: np.ndarray, device=None):
+        super().__init__()
+        self.g = g
+        self.cost = np.asarray(cost, dtype=np.float32)
+        self.device = device
+        self._astar = None
+        self._csr = None
+
+    @classmethod
+    def synthetic(cls, num_nodes: int = 100_000, eta_model=None, device=None) -> "GraphProvider":
+        g = synth_road_graph(num_nodes)
+        if eta_model is None:
+            from ..serve.eta_service import default_model
+            eta_model = default_model(hidden=64, steps=100)
+        return cls(g, edge_costs(g, eta_model, device), device)
+
+    def _shortest(self, pairs: List[Tuple[int, int]]) -> List[Tuple[float, List[int]]]:
+        if self.device is not None and torch.device(self.device).type == "cuda":
+            if self._astar is None:
+                self._astar = BatchedAstar(self.g, self.cost, self.device, slots=1024, cap=65536)
+            return self._astar.paths([p[0] for p in pairs], [p[1] for p in pairs])
+        from scipy.sparse import csr_matrix
+        from scipy.sparse.csgraph import dijkstra
+        if self._csr is None:
+            self._csr = csr_matrix((self.cost.astype(np.float64), self.g.indices, self.g.indptr),
+                                   shape=(self.g.num_nodes,) * 2)
+        out = []
+        for s, t in pairs:
+            dist, pred = dijkstra(self._csr, directed=True, indices=s, return_predecessors=True)
+            if not np.isfinite(dist[t]):
+                out.append((float("nan"), []))
+                continue
+            path = [t]
+            while path[-1] != s:
+                path.append(int(pred[path[-1]]))
+            out.append((float(dist[t]), path[::-1]))
+        return out
+
+    def directions(self, coords: List[List[float]], profile: str) -> Dict[str, Any]:
+        nodes = self.g.nearest_nodes([c[1] for c in coords], [c[0] for c in coords])
+        legs = self._shortest([(int(nodes[k]), int(nodes[k + 1])) for k in range(len(nodes) - 1)])
+        speed_scale = PROFILE_SPEED_MPS["driving-car"] / PROFILE_SPEED_MPS.get(profile, PROFILE_SPEED_MPS["driving-car"])
+        geometry: List[List[float]] = [[float(coords[0][0]), float(coords[0][1])]]
+        segments, way_points = [], [0]
+        tot_d = tot_t = 0.0
+        for k, (sec, path) in enumerate(legs):
+            start = len(geometry) - 1
+            if not path:
+                path = [int(nodes[k]), int(nodes[k + 1])]
+                sec = float(haversine_m(self.g.lat[path[0]], self.g.lon[path[0]], self.g.lat[path[1]],
+                                        self.g.lon[path[1]]) / PROFILE_SPEED_MPS["driving-car"])
+            p = np.asarray(path)
+            dist = float(haversine_m(self.g.lat[p[:-1]], self.g.lon[p[:-1]], self.g.lat[p[1:]],
+                                     self.g.lon[p[1:]]).sum() * 1.15) if len(p) > 1 else 0.0
+            for v in path:
+                geometry.append([round(float(self.g.lon[v]), 6), round(float(self.g.lat[v]), 6)])
+            geometry.append([float(coords[k + 1][0]), float(coords[k + 1][1])])
+            end = len(geometry) - 1
+            way_points.append(end)
+            dur = sec * speed_scale
+            segments.append({"distance": round(dist, 1), "duration": round(dur, 1), "steps": [
+                {"distance": round(dist, 1), "duration": round(dur, 1), "type": 11 if k == 0 else 1,
+                 "instruction": "Follow the road network", "name": "-", "way_points": [start, end]},
+                {"distance": 0.0, "duration": 0.0, "type": 10, "instruction": "Arrive at your destination"
+                 if k == len(legs) - 1 else f"Arrive at waypoint {k + 1}", "name": "-",
+                 "way_points": [end, end]}]})
+            tot_d += dist
+            tot_t += dur
+        return {"type": "Feature", "bbox": _bbox(geometry),
+                "geometry": {"type": "LineString", "coordinates": geometry},
+                "properties": {"segments": segments,
+                               "summary": {"distance": round(tot_d, 1), "duration": round(tot_t, 1)},
+                               "way_points": way_points}}
