@@ -9,8 +9,9 @@
 //     the closed bit; the heuristic is consistent, so a node's first pop is final);
 //   * a touched list, so only the entries a search wrote are reset afterwards (no N-sized memset
 //     per query).
-// Heuristic: great-circle distance / v_max; edge costs are floored at length / v_max on the host,
-// so h is admissible and consistent.  Every lane stops within max_iters pops (status 3), on heap
+// Heuristic: max(great-circle distance x circuity / v_max, ALT landmark bound); edge costs are
+// floored at length / v_max on the host, so both are admissible and consistent (ALT tables are
+// shrunk by 1e-4 against fp32 rounding).  Every lane stops within max_iters pops (status 3), on heap
 // or touched-list overflow (status 2) or when the open set empties (status 1): the grid always
 // drains.  Paths are written target->source then reversed in place.
 #include "common.h"
@@ -36,7 +37,11 @@ struct AstarArgs {
   int* out_path;         // [Q][max_path]
   int N, Q, q0, cap, max_path, max_iters;
   float inv_vmax;        // seconds per metre at v_max
+  const float* lm;       // [N][2K] ALT landmark tables: d(L_k -> v), d(v -> L_k) (nullptr: off)
+  int K;
 };
+
+constexpr int KMAX = 16;
 
 __device__ __forceinline__ float hdist(const AstarArgs& a, int v, float tlat, float tlon, float ctl) {
   const float k = 0.017453292519943295f;
@@ -48,10 +53,28 @@ __device__ __forceinline__ float hdist(const AstarArgs& a, int v, float tlat, fl
   return 0.999f * 2.f * 6371000.f * asinf(sqrtf(fminf(1.f, fmaxf(0.f, hv)))) * a.inv_vmax;
 }
 
+// ALT lower bound on d(v -> t): max_k max(d(L_k,t) - d(L_k,v), d(v,L_k) - d(t,L_k)).
+template <int K>
+__device__ __forceinline__ float halt(const AstarArgs& a, int v, const float (&ft)[KMAX],
+                                      const float (&bt)[KMAX]) {
+  const float4* row = reinterpret_cast<const float4*>(a.lm + (size_t)v * 2 * K);
+  float best = 0.f;
+#pragma unroll
+  for (int q = 0; q < K / 2; ++q) {     // one float4 = (fwd_k, fwd_k+1, bwd_k, bwd_k+1)
+    const float4 x = row[q];
+    best = fmaxf(best, ft[2 * q] - x.x);
+    best = fmaxf(best, ft[2 * q + 1] - x.y);
+    best = fmaxf(best, x.z - bt[2 * q]);
+    best = fmaxf(best, x.w - bt[2 * q + 1]);
+  }
+  return best * 0.9999f;
+}
+
 __device__ __forceinline__ unsigned long long hkey(float f, int v) {
   return ((unsigned long long)__float_as_uint(f) << 32) | (unsigned)v;   // f >= 0: monotone bits
 }
 
+template <int K>
 __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
   const int q = a.q0 + slot;
@@ -65,11 +88,29 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
   const float tlat = a.lat[t] * k, tlon = a.lon[t] * k, ctl = __cosf(tlat);
   const unsigned CLOSED = 0x80000000u;
 
+  float ft[KMAX], bt[KMAX];  // landmark distances of the target (registers: K is a constant)
+  if constexpr (K > 0) {
+    const float4* row = reinterpret_cast<const float4*>(a.lm + (size_t)t * 2 * K);
+#pragma unroll
+    for (int q = 0; q < K / 2; ++q) {
+      const float4 x = row[q];
+      ft[2 * q] = x.x;
+      ft[2 * q + 1] = x.y;
+      bt[2 * q] = x.z;
+      bt[2 * q + 1] = x.w;
+    }
+  }
+  auto heur = [&](int v) {
+    float hv = hdist(a, v, tlat, tlon, ctl);
+    if constexpr (K > 0) hv = fmaxf(hv, halt<K>(a, v, ft, bt));
+    return hv;
+  };
+
   int hn = 0, nt = 0, status = 1;
   g[s] = 0.f;
   par[s] = -1 & 0x7fffffff;
   touched[nt++] = s;
-  heap[hn++] = hkey(hdist(a, s, tlat, tlon, ctl), s);
+  heap[hn++] = hkey(heur(s), s);
   int it = 0;
   for (; hn > 0; ++it) {
     if (it >= a.max_iters) { status = 3; break; }
@@ -115,7 +156,7 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
         par[u] = v;
         if (hn >= a.cap) { overflow = true; break; }
         // push + sift up
-        unsigned long long key = hkey(ng + hdist(a, u, tlat, tlon, ctl), u);
+        unsigned long long key = hkey(ng + heur(u), u);
         int i = hn++;
         while (i > 0) {
           const int p = (i - 1) >> 1;
@@ -167,13 +208,18 @@ hipError_t launch_astar(const int* indptr, const int* indices, const float* cost
                         const float* lon, const int* src, const int* dst, float* g, int* parent,
                         void* heap, int* touched, float* out_cost, int* out_len, int* out_status,
                         int* out_path, int N, int Q, int q0, int slots, int cap, int max_path,
-                        int max_iters, float inv_vmax, hipStream_t stream) {
+                        int max_iters, float inv_vmax, const float* lm, int K,
+                        hipStream_t stream) {
   const int n = min(slots, Q - q0);
   if (n <= 0) return hipSuccess;
+  if (lm != nullptr && K != 16 && K != 8) return hipErrorInvalidValue;
   AstarArgs a{indptr, indices, cost, lat, lon, src, dst, g, parent,
               (unsigned long long*)heap, touched, out_cost, out_len, out_status, out_path,
-              N, Q, q0, cap, max_path, max_iters, inv_vmax};
-  hipLaunchKernelGGL(astar_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
+              N, Q, q0, cap, max_path, max_iters, inv_vmax, lm, K};
+  const dim3 grid((n + 255) / 256), block(256);
+  if (lm == nullptr) hipLaunchKernelGGL(astar_kernel<0>, grid, block, 0, stream, a);
+  else if (K == 8) hipLaunchKernelGGL(astar_kernel<8>, grid, block, 0, stream, a);
+  else hipLaunchKernelGGL(astar_kernel<16>, grid, block, 0, stream, a);
   return hipGetLastError();
 }
 

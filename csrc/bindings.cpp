@@ -341,7 +341,7 @@ void astar(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torc
            torch::Tensor lon, torch::Tensor src, torch::Tensor dst, torch::Tensor g,
            torch::Tensor parent, torch::Tensor heap, torch::Tensor touched, torch::Tensor out_cost,
            torch::Tensor out_len, torch::Tensor out_status, torch::Tensor out_path, int64_t q0,
-           int64_t max_iters, double inv_vmax) {
+           int64_t max_iters, double inv_vmax, c10::optional<torch::Tensor> landmarks) {
   for (auto* t : {&indptr, &indices, &cost, &lat, &lon, &src, &dst, &g, &parent, &heap, &touched,
                   &out_cost, &out_len, &out_status, &out_path})
     check_dev(*t, "astar tensor");
@@ -355,6 +355,16 @@ void astar(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torc
   TORCH_CHECK(dst.numel() == Q && out_cost.numel() == Q && out_len.numel() == Q &&
               out_status.numel() == Q && out_path.dim() == 2 && out_path.size(0) == Q, "outputs [Q]");
   TORCH_CHECK(0 <= q0 && q0 <= Q, "q0");
+  const float* lm = nullptr;
+  int K = 0;
+  if (landmarks.has_value()) {
+    check_dev(*landmarks, "landmarks");
+    TORCH_CHECK(landmarks->scalar_type() == torch::kFloat32 && landmarks->dim() == 2 &&
+                landmarks->size(0) == N && landmarks->size(1) % 4 == 0 && landmarks->size(1) <= 32,
+                "landmarks must be f32 [N, 2K] with K even <= 16");
+    lm = landmarks->data_ptr<float>();
+    K = (int)landmarks->size(1) / 2;
+  }
   const c10::DeviceGuard guard(g.device());
   RT_CHECK_HIP(rt::launch_astar(indptr.data_ptr<int>(), indices.data_ptr<int>(), cost.data_ptr<float>(),
                                 lat.data_ptr<float>(), lon.data_ptr<float>(), src.data_ptr<int>(),
@@ -363,7 +373,7 @@ void astar(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torc
                                 out_len.data_ptr<int>(), out_status.data_ptr<int>(),
                                 out_path.data_ptr<int>(), (int)N, (int)Q, (int)q0, (int)g.size(0),
                                 (int)heap.size(1), (int)out_path.size(1), (int)max_iters,
-                                (float)inv_vmax, cur_stream(g)));
+                                (float)inv_vmax, lm, K, cur_stream(g)));
 }
 
 }  // namespace

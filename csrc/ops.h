@@ -56,7 +56,7 @@ hipError_t launch_astar(const int* indptr, const int* indices, const float* cost
                         const float* lon, const int* src, const int* dst, float* g, int* parent,
                         void* heap, int* touched, float* out_cost, int* out_len, int* out_status,
                         int* out_path, int N, int Q, int q0, int slots, int cap, int max_path,
-                        int max_iters, float inv_vmax, hipStream_t stream);
+                        int max_iters, float inv_vmax, const float* lm, int K, hipStream_t stream);
 
 // ---- batched routing (K5 distance matrix + K6 greedy CVRP) : route_kernels.hip ----
 hipError_t launch_haversine_matrix(const double* lat, const double* lon, const int* npts, int R,

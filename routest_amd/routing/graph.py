@@ -27,33 +27,53 @@ V_MAX_MPS = 130 / 3.6
 CLASS_FACTOR = np.array([1.15, 1.0, 0.85, 0.65], dtype=np.float32)   # residential .. highway
 
 
-def edge_records(g: RoadGraph, weather: str = "Sunny", traffic: str = "Medium",
+TRAFFIC_LEVELS = ("Low", "Medium", "High", "Jam")
+L_REF_M = 10_000.0
+
+
+def edge_traffic(g: RoadGraph, congestion: int = 1) -> np.ndarray:
+    """Synthetic per-edge traffic level (index into TRAFFIC_LEVELS): busier on big roads near the
+    centre of the box; ``congestion`` (0..3) shifts the whole city."""
+    mid_lat, mid_lon = float(g.lat.mean()), float(g.lon.mean())
+    src = np.repeat(np.arange(g.num_nodes), np.diff(g.indptr))
+    dc = haversine_m(g.lat[src], g.lon[src], mid_lat, mid_lon) / 1000.0
+    lvl = (g.road_class.astype(np.int32) >= 2).astype(np.int32) + (dc < 8.0) + (dc < 4.0)
+    return np.clip(lvl + congestion - 1, 0, 3).astype(np.int32)
+
+
+def edge_records(g: RoadGraph, weather: str = "Sunny", congestion: int = 1,
                  pickup: Optional[dt.datetime] = None, driver_age: float = 35.0) -> np.ndarray:
+    """Two records per directed edge: (edge traffic, L_REF) and (edge traffic, 0 m)."""
+    from ..models.features import traffic_code
     pickup = pickup or dt.datetime(2025, 8, 25, 9, 0)
-    proto = np.array([pack_record(weather=weather, traffic=traffic, distance_m=0.0, pickup=pickup,
+    proto = np.array([pack_record(weather=weather, traffic="Low", distance_m=0.0, pickup=pickup,
                                   driver_age=driver_age)], dtype=RECORD_DTYPE)
-    rec = np.repeat(proto, g.num_edges)
-    rec["distance_m"] = g.length_m
+    lvl = edge_traffic(g, congestion)
+    codes = np.array([traffic_code(t) for t in TRAFFIC_LEVELS], dtype=np.uint8)[lvl]
+    rec = np.repeat(proto, 2 * g.num_edges)
+    rec["traffic"][0::2] = codes
+    rec["traffic"][1::2] = codes
+    rec["distance_m"][0::2] = L_REF_M
+    rec["distance_m"][1::2] = 0.0
     return rec
 
 
 def edge_costs(g: RoadGraph, eta_model, device=None, **ctx: Any) -> np.ndarray:
-    """Seconds per directed edge: the ETA MLP's MARGINAL time for the edge's length under the
-    trip context (minutes(len) - minutes(0), so the model's fixed per-trip overhead is not charged
-    per edge), times a road-class factor, floored at length / V_MAX."""
+    """Seconds per directed edge from the ETA MLP: each edge's marginal rate under ITS traffic
+    level, measured over a 10 km reference trip so the model's fixed per-trip overhead cancels
+    and bf16 rounding stays ~0.1 %:  len/L_REF * (f(ctx_e, L_REF) - f(ctx_e, 0)) minutes, times a
+    road-class factor, floored at free-flow time at V_MAX (keeps A*'s heuristic admissible).
+    All 2E records go through ONE fused featurize+MLP launch on the GPU."""
     from ..ops.eta_mlp import EtaMlpKernel, featurize_torch, records_to_tensor
-    er = edge_records(g, **ctx)
-    zero = er[:1].copy()
-    zero["distance_m"] = 0.0
-    rec = records_to_tensor(np.concatenate([er, zero]))
+    rec = records_to_tensor(edge_records(g, **ctx))
     dev = torch.device(device) if device is not None else torch.device("cpu")
     if dev.type == "cuda":
         minutes = EtaMlpKernel(eta_model, dev)(rec.to(dev)).cpu().numpy()
     else:
         with torch.no_grad():
             minutes = eta_model.float().cpu()(featurize_torch(rec)).numpy()
-    marginal = minutes[:-1].astype(np.float32) - np.float32(minutes[-1])
-    sec = marginal * 60.0 * CLASS_FACTOR[g.road_class]
+    rate = (minutes[0::2] - minutes[1::2]).astype(np.float32) * np.float32(60.0 / L_REF_M)
+    sec = rate * g.length_m * CLASS_FACTOR[g.road_class]
     return np.maximum(sec, g.length_m / V_MAX_MPS).astype(np.float32)
 
 
@@ -70,11 +90,38 @@ def dijkstra_ref(g: RoadGraph, cost: np.ndarray, src: Sequence[int], dst: Sequen
     return out
 
 
+def landmark_tables(g: RoadGraph, cost: np.ndarray, k: int = 16, seed: int = 0) -> np.ndarray:
+    """ALT preprocessing: K landmarks spread around the periphery (by angle from the centre),
+    forward d(L -> v) and backward d(v -> L) shortest-path tables, interleaved per node as
+    [N][2K] = (fwd_k, fwd_k+1, bwd_k, bwd_k+1) float4 groups (csrc/astar.hip::halt)."""
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import dijkstra
+    clat, clon = float(g.lat.mean()), float(g.lon.mean())
+    ang = np.arctan2(g.lat - clat, (g.lon - clon) * np.cos(np.radians(clat)))
+    rad = haversine_m(g.lat, g.lon, clat, clon)
+    lms = []
+    for i in range(k):
+        lo, hi = -np.pi + 2 * np.pi * i / k, -np.pi + 2 * np.pi * (i + 1) / k
+        sector = np.where((ang >= lo) & (ang < hi))[0]
+        lms.append(int(sector[np.argmax(rad[sector])]) if len(sector) else int(np.argmax(rad)))
+    m = csr_matrix((np.asarray(cost, dtype=np.float64), g.indices, g.indptr), shape=(g.num_nodes,) * 2)
+    fwd = dijkstra(m, directed=True, indices=lms)
+    bwd = dijkstra(m.T.tocsr(), directed=True, indices=lms)
+    fwd = np.where(np.isfinite(fwd), fwd, 0.0).astype(np.float32)
+    bwd = np.where(np.isfinite(bwd), bwd, 0.0).astype(np.float32)
+    out = np.empty((g.num_nodes, k // 2, 4), dtype=np.float32)
+    out[:, :, 0] = fwd[0::2].T
+    out[:, :, 1] = fwd[1::2].T
+    out[:, :, 2] = bwd[0::2].T
+    out[:, :, 3] = bwd[1::2].T
+    return out.reshape(g.num_nodes, 2 * k)
+
+
 class BatchedAstar:
     """GPU batched A*; workspace sized for ``slots`` concurrent searches (dense per-slot state)."""
 
-    def __init__(self, g: RoadGraph, cost: np.ndarray, device, slots: int = 16384, cap: int = 16384,
-                 max_path: int = 4096, max_iters: int = 2_000_000):
+    def __init__(self, g: RoadGraph, cost: np.ndarray, device, slots: int = 16384, cap: int = 65536,
+                 max_path: int = 4096, max_iters: int = 2_000_000, landmarks: int = 16):
         from ..ops import _ext
         self.C = _ext.native(required=True)
         self.g = g
@@ -86,13 +133,25 @@ class BatchedAstar:
         self.lon = torch.from_numpy(g.lon.astype(np.float32)).to(d)
         self.slots, self.cap, self.max_path, self.max_iters = slots, cap, max_path, max_iters
         N = g.num_nodes
+        # tightest admissible + consistent heuristic: every edge length is 1.15 x its great-circle
+        # length (so any path >= 1.15 x the great-circle s-t distance) and every edge is traversed
+        # no faster than the fastest edge of the graph
+        cost_np = np.asarray(cost, dtype=np.float64)
+        self.v_max = float((g.length_m / np.maximum(cost_np, 1e-6)).max()) * 1.0001
+        self.inv_vmax = 1.15 / self.v_max
+        self.lm = (torch.from_numpy(landmark_tables(g, cost, landmarks)).to(d) if landmarks else None)
         self.gbuf = torch.full((slots, N), float("inf"), dtype=torch.float32, device=d)
         self.parent = torch.full((slots, N), 0x7FFFFFFF, dtype=torch.int32, device=d)
         self.heap = torch.empty((slots, cap), dtype=torch.int64, device=d)
         self.touched = torch.empty((slots, cap), dtype=torch.int32, device=d)
 
     def update_costs(self, cost: np.ndarray) -> None:
-        self.cost.copy_(torch.from_numpy(np.asarray(cost, dtype=np.float32)))
+        cost = np.asarray(cost, dtype=np.float32)
+        self.cost.copy_(torch.from_numpy(cost))
+        self.v_max = float((self.g.length_m / np.maximum(cost.astype(np.float64), 1e-6)).max()) * 1.0001
+        self.inv_vmax = 1.15 / self.v_max
+        if self.lm is not None:
+            self.lm.copy_(torch.from_numpy(landmark_tables(self.g, cost, self.lm.shape[1] // 2)))
 
     def run(self, src: Sequence[int], dst: Sequence[int]):
         """Returns (cost_s [Q] tensor, path_len [Q], status [Q], paths [Q, max_path]) on device."""
@@ -107,7 +166,7 @@ class BatchedAstar:
         for q0 in range(0, Q, self.slots):
             self.C.astar(self.indptr, self.indices, self.cost, self.lat, self.lon, s, t, self.gbuf,
                          self.parent, self.heap, self.touched, out_cost, out_len, out_status, out_path,
-                         q0, self.max_iters, 1.0 / V_MAX_MPS)
+                         q0, self.max_iters, self.inv_vmax, self.lm)
         return out_cost, out_len, out_status, out_path
 
     def paths(self, src, dst) -> List[Tuple[float, List[int]]]:
