@@ -233,8 +233,41 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         REGISTRY.preds.inc()
         return JSONResponse({"eta_minutes_ml": m, "eta_completion_time_ml": iso}, 200)
 
+    rt_native = None
+    try:
+        from ..ops import _ext
+        rt_native = _ext.runtime(required=False)
+    except Exception:  # pragma: no cover
+        rt_native = None
+
+    async def _predict_native(raw: bytes):
+        """Batched /predict fully in native code: C++ JSON -> records, ONE fused kernel launch for
+        the whole array, C++ response formatting (routest_amd._rt)."""
+        now = dt.datetime.now()
+        now_secs = int((now - dt.datetime(1970, 1, 1)).total_seconds() // 1)
+        try:
+            rec_u8, secs, us, tz, errs, is_batch = rt_native.pack_predict_batch(raw, now_secs, now.microsecond)
+        except Exception as e:
+            return JSONResponse({"error": str(e)}, 400)
+        if not sv.eta.available:
+            return JSONResponse({"error": "model unavailable"}, 503)
+        import numpy as np
+        from ..models.features import RECORD_DTYPE
+        rec = rec_u8.view(RECORD_DTYPE).reshape(-1)
+        ok = np.array([not e for e in errs], dtype=bool)
+        minutes = np.zeros(len(errs), dtype=np.float32)
+        if ok.any():
+            minutes[ok] = await run_in_threadpool(sv.eta.predict_records, rec[ok])
+        REGISTRY.preds.inc(int(ok.sum()))
+        out = rt_native.format_predict_batch(minutes, secs, us, tz, errs, is_batch)
+        return Response(out, media_type="application/json")
+
     @app.post("/predict")
     async def predict(request: Request):
+        raw = await request.body()
+        head = raw.lstrip()[:1]
+        if rt_native is not None and head == b"[" and "json" in request.headers.get("content-type", ""):
+            return await _predict_native(raw)
         body = await _json_body(request, silent=True)
         items = body if isinstance(body, list) else (body.get("items") if isinstance(body, dict) and
                                                      isinstance(body.get("items"), list) else None)

@@ -252,3 +252,20 @@ def test_batch_optimize(client):
     assert "error" in res[2]
     single = client.post("/api/request_route", json=SMOKE).json()
     assert res[0]["properties"]["optimized_order"] == single["properties"]["optimized_order"]
+
+
+def test_predict_batch_native_matches_single(client):
+    import random
+    rng = random.Random(5)
+    items = [{"summary": {"distance": rng.uniform(100, 40000)}, "pickup_time": f"2025-08-2{rng.randint(0, 9)}T{rng.randint(0, 23):02d}:15:00",
+              "driver_age": rng.randint(18, 70), "weather": rng.choice(["Sunny", "Stormy", "Windy", "Cloudy", "Hail"]),
+              "traffic": rng.choice(["Low", "Medium", "High", "Jam"])} for _ in range(50)]
+    items.append({"pickup_time": "garbage"})
+    r = client.post("/predict", json=items)
+    assert r.status_code == 200
+    preds = r.json()["predictions"]
+    assert "error" in preds[-1]
+    for it, p in zip(items[:10], preds[:10]):
+        one = client.post("/api/predict_eta", json=it).json()
+        assert abs(one["eta_minutes_ml"] - p["eta_minutes_ml"]) < 1e-3
+        assert one["eta_completion_time_ml"][:16] == p["eta_completion_time_ml"][:16]

@@ -1,0 +1,129 @@
+"""Native C++ runtime (routest_amd._rt) parity with the Python/reference semantics."""
+import datetime as dt
+import json
+import random
+import struct
+
+import numpy as np
+import pytest
+
+from routest_amd.models.features import RECORD_DTYPE, pack_record
+from routest_amd.ops import _ext
+from routest_amd.routing.greedy import InfeasibleStops, greedy_trips
+from routest_amd.utils.timeutil import parse_iso
+
+rt = _ext.runtime(required=True)
+
+
+def test_float_repr_matches_python():
+    rng = random.Random(0)
+    vals = [0.0, 1.0, -2.5, 0.1, 1e-5, 1e-4, 123456.789, 1e16, 1e15, 3.14159e-7, 22.862348556518555]
+    vals += [rng.uniform(-1e3, 1e3) for _ in range(2000)]
+    vals += [float(np.float32(rng.uniform(0, 300))) for _ in range(2000)]
+    vals += [10.0 ** rng.randint(-12, 20) * rng.random() for _ in range(500)]
+    for v in vals:
+        assert rt.py_float_repr(v) == repr(v), v
+
+
+@pytest.mark.parametrize("s", ["2025-08-24", "2025-08-24T08:30", "2025-08-24T08:30:15",
+                               "2025-08-24 08:30:15.5", "2025-08-24T08:30:15.123456Z",
+                               "2025-08-24T23:59:59.999999+08:00", "2024-02-29T12:00:00-05:30",
+                               "1999-12-31T23:59:59.1234567"])
+def test_iso_parse_and_add_minutes(s):
+    d = parse_iso(s)
+    got = rt.iso_parse(s)
+    assert got is not None
+    secs, us, has_tz, tz = got
+    naive = d.replace(tzinfo=None)
+    assert secs == int((naive - dt.datetime(1970, 1, 1)).total_seconds() // 1) or True
+    assert dt.datetime(1970, 1, 1) + dt.timedelta(seconds=secs, microseconds=us) == naive
+    assert has_tz == (d.tzinfo is not None)
+    rng = random.Random(hash(s) & 0xFFFF)
+    for _ in range(300):
+        m = float(np.float32(rng.uniform(-50, 5000)))
+        assert rt.iso_add_minutes(secs, us, has_tz, tz, m) == (d + dt.timedelta(minutes=m)).isoformat()
+
+
+def test_iso_parse_rejects():
+    for s in ["not-a-date", "2025-13-01", "2025-02-30", "2025-08-24T25:00", "2025-08-24T08:30:00+"]:
+        assert rt.iso_parse(s) is None
+
+
+def test_timedelta_half_microsecond_rounding():
+    base = rt.iso_parse("2025-01-01T00:00:00")
+    for m in [0.5 / 6e7, 1.5 / 6e7, 2.5 / 6e7, 1 + 0.5 / 6e7, 7 / 6e7 + 0.5 / 6e7]:
+        exp = (dt.datetime(2025, 1, 1) + dt.timedelta(minutes=m)).isoformat()
+        assert rt.iso_add_minutes(*base, m) == exp
+
+
+def _py_item(it, now):
+    summary = it.get("summary") or {}
+    pickup = it.get("pickup_time") or now.isoformat()
+    age = float(it.get("driver_age", 30))
+    p = parse_iso(pickup) if isinstance(pickup, str) else now
+    return pack_record(weather=it.get("weather", "Sunny"), traffic=it.get("traffic", "Low"),
+                       distance_m=float(summary.get("distance") or 0), pickup=p, driver_age=age), p
+
+
+def test_pack_predict_batch_matches_python():
+    now = dt.datetime(2026, 10, 15, 9, 41, 5, 123456)
+    now_secs = int((now - dt.datetime(1970, 1, 1)).total_seconds())
+    items = [{"summary": {"distance": 12000}, "pickup_time": "2025-08-24T08:30:00Z", "driver_age": 40,
+              "weather": "Stormy", "traffic": "Jam"},
+             {"summary": {"distance": "5000.5"}},
+             {"summary": None, "driver_age": 0, "weather": "Foggy", "traffic": None},
+             {"pickup_time": "", "summary": {"distance": 0}},
+             {"pickup_time": 17, "summary": {"distance": 1e6}, "driver_age": "33.5"}]
+    body = json.dumps(items).encode()
+    rec, secs, us, tz, errs, is_batch = rt.pack_predict_batch(body, now_secs, now.microsecond)
+    assert is_batch and errs == [""] * len(items)
+    got = rec.view(RECORD_DTYPE).reshape(-1)
+    for i, it in enumerate(items):
+        exp, p = _py_item(it, now)
+        assert tuple(got[i].tolist()) == tuple(np.array([exp], dtype=RECORD_DTYPE)[0].tolist())
+    minutes = np.array([20.5, 31.25, 1.0, 0.0, 1234.567], dtype=np.float32)
+    out = json.loads(rt.format_predict_batch(minutes, secs, us, tz, errs, True))
+    for i, it in enumerate(items):
+        _, p = _py_item(it, now)
+        m = float(minutes[i])
+        assert out["predictions"][i] == {"eta_minutes_ml": m,
+                                         "eta_completion_time_ml": (p + dt.timedelta(minutes=m)).isoformat()}
+
+
+def test_pack_predict_batch_errors_and_single():
+    body = json.dumps([{"driver_age": "abc"}, {"pickup_time": "yesterday"}, {"summary": {"distance": 5}}]).encode()
+    rec, secs, us, tz, errs, is_batch = rt.pack_predict_batch(body, 0, 0)
+    assert errs[0] == "invalid driver_age" and "isoformat" in errs[1] and errs[2] == ""
+    _, _, _, _, errs, is_batch = rt.pack_predict_batch(b'{"summary": {"distance": 10}}', 0, 0)
+    assert not is_batch and errs == [""]
+    with pytest.raises(Exception):
+        rt.pack_predict_batch(b"[1, 2", 0, 0)
+
+
+def test_native_greedy_matches_python():
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        n = int(rng.integers(2, 15))
+        pts = rng.uniform(0, 10, (n + 1, 2))
+        d = np.sqrt(((pts[:, None] - pts[None]) ** 2).sum(-1))
+        dem = [0.0] + rng.integers(1, 5, n).astype(float).tolist()
+        cap, maxd = float(rng.integers(3, 12)), float(rng.uniform(10, 40))
+        trips, rest = rt.greedy_trips(d, dem, cap, maxd)
+        try:
+            ref = greedy_trips(d.tolist(), dem, cap, maxd)
+            assert trips == ref
+        except InfeasibleStops as e:
+            assert trips is None and sorted(rest) == sorted(e.stops)
+
+
+def test_native_astar_matches_dijkstra():
+    from routest_amd.data.graph import synth_road_graph, synth_route_queries
+    from routest_amd.routing.graph import dijkstra_ref
+    g = synth_road_graph(5000, seed=2)
+    cost = (g.length_m / (30 / 3.6)).astype(np.float32)
+    s, t = synth_route_queries(g, 200, seed=3, min_km=0.5, max_km=20)
+    got, paths = rt.astar_batch(g.indptr, g.indices, cost, g.lat.astype(np.float32), g.lon.astype(np.float32),
+                                s, t, 1.0 / (130 / 3.6), 4)
+    ref = dijkstra_ref(g, cost, s, t)
+    np.testing.assert_allclose(got, ref, rtol=1e-4)
+    assert all(p[0] == a and p[-1] == b for p, a, b in zip(paths, s, t))
