@@ -376,6 +376,26 @@ void astar(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torc
                                 (float)inv_vmax, lm, K, cur_stream(g)));
 }
 
+torch::Tensor forest_predict(torch::Tensor records, torch::Tensor values, torch::Tensor info,
+                             torch::Tensor roots, double base, bool le, std::vector<int64_t> fmap) {
+  for (auto* t : {&records, &values, &info, &roots}) check_dev(*t, "forest tensor");
+  TORCH_CHECK(records.scalar_type() == torch::kInt32 && records.dim() == 2 && records.size(1) == 4,
+              "records must be int32 [B,4]");
+  TORCH_CHECK(values.scalar_type() == torch::kFloat32 && info.scalar_type() == torch::kInt32 &&
+              values.numel() == info.numel() && roots.scalar_type() == torch::kInt32, "forest arrays");
+  TORCH_CHECK(fmap.size() == 12, "fmap must have 12 entries");
+  const c10::DeviceGuard guard(records.device());
+  const int B = (int)records.size(0);
+  auto out = torch::empty({B}, values.options());
+  int fm[12];
+  for (int j = 0; j < 12; ++j) fm[j] = (int)fmap[j];
+  RT_CHECK_HIP(rt::launch_forest(records.data_ptr(), values.data_ptr<float>(),
+                                 (const unsigned*)info.data_ptr<int>(), roots.data_ptr<int>(),
+                                 out.data_ptr<float>(), B, (int)roots.numel(), (int)values.numel(),
+                                 (float)base, le ? 1 : 0, fm, cur_stream(records)));
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -399,5 +419,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gcn_spmm_score", &gcn_spmm_score, "K8: layer-2 aggregation + delay head");
   m.def("route_score", &route_score, "K8: per-route delay-weighted length");
   m.def("astar", &astar, "K9: batched A* (one lane per query) with learned edge costs");
+  m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
   m.attr("ARCH") = "gfx950";
 }

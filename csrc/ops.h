@@ -58,6 +58,11 @@ hipError_t launch_astar(const int* indptr, const int* indices, const float* cost
                         int* out_path, int N, int Q, int q0, int slots, int cap, int max_path,
                         int max_iters, float inv_vmax, const float* lm, int K, hipStream_t stream);
 
+// ---- tree ensemble (K4) : forest.hip ----
+hipError_t launch_forest(const void* rec, const float* values, const unsigned* info, const int* roots,
+                         float* out, int B, int T, int M, float base, int le, const int* fmap,
+                         hipStream_t stream);
+
 // ---- batched routing (K5 distance matrix + K6 greedy CVRP) : route_kernels.hip ----
 hipError_t launch_haversine_matrix(const double* lat, const double* lon, const int* npts, int R,
                                    int NM, double circuity, double* D, hipStream_t stream);

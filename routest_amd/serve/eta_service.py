@@ -52,6 +52,20 @@ def _cpu_runner(model: Any):
     return run_df
 
 
+class ForestKernel:
+    """Tree ensemble resident on one GPU (K4: fused featurize + traversal, csrc/forest.hip)."""
+
+    def __init__(self, model, device):
+        from ..ops import _ext
+        self.C = _ext.native(required=True)
+        self.m = model
+        self.values, self.info, self.roots = model.device_arrays(device)
+
+    def __call__(self, rec: torch.Tensor) -> torch.Tensor:
+        return self.C.forest_predict(rec, self.values, self.info, self.roots, self.m.base_score, self.m.le,
+                                     list(self.m.feature_map))
+
+
 class EtaService:
     def __init__(self, model: Any = None, model_path: Optional[str] = None, device: str = "auto",
                  devices: Sequence[int] = (), batch_max: int = 4096, timeout_us: int = 200,
@@ -86,9 +100,14 @@ class EtaService:
         from ..ops.eta_mlp import EtaMlpKernel
         runners = []
         devs: List[torch.device] = []
+        from ..models.forest import ForestModel
         if isinstance(model, EtaMLP) and model.hidden in (64, 128, 256):
             for d in self._gpu_devices():
                 runners.append(GpuRunner(EtaMlpKernel(model, d), d, self.batch_max))
+                devs.append(d)
+        elif isinstance(model, ForestModel):
+            for d in self._gpu_devices():
+                runners.append(GpuRunner(ForestKernel(model, d), d, self.batch_max))
                 devs.append(d)
         if not runners:
             runners = [_cpu_runner(model)]
