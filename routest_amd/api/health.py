@@ -65,8 +65,9 @@ def health_payload(sv: Any) -> Dict[str, Any]:
         db_res = sv.store.ping()
     gpu_res = _check_gpu(sv)
     model = sv.eta.describe()
-    model_res = {"status": "ok" if sv.eta.batcher is not None else "skipped", **model}
-    parts = (redis_res["status"], engine_res["status"], db_res["status"], gpu_res["status"])
+    model_res = {"status": ("degraded" if model.get("degraded") else "ok") if sv.eta.batcher is not None
+                 else "skipped", **model}
+    parts = (redis_res["status"], engine_res["status"], db_res["status"], gpu_res["status"], model_res["status"])
     overall = "degraded" if any(p in ("error", "degraded") for p in parts) else "ok"
     return {
         "backend": True,

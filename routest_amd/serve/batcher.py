@@ -3,14 +3,19 @@ request, ``RO/Flaskr/routes.py:365-383``).
 
 Requests are packed into 16-byte records as they arrive and pushed on one queue.  Each device
 has a worker thread that takes the first waiting request, keeps collecting until ``batch_max``
-rows or ``timeout_us`` elapsed, and runs ONE fused featurize+MLP launch for the batch:
+rows or ``timeout_us`` elapsed, and runs ONE fused featurize+MLP launch for the batch.  For the
+MLP the kernel reads the records straight out of pinned host memory and writes the minutes back
+the same way (zero-copy over PCIe), so a batch is exactly one launch + one stream sync:
 
-    pinned host records --H2D--> HBM --K1+K2 kernel--> minutes --D2H--> pinned host
+    pinned host records --(kernel loads over PCIe)--> K1+K2 --(kernel stores)--> pinned host
 
-All workers pull from the same queue, so several GPUs in one process share load without a
-router.  The queue + batch assembly can run in the native C++ runtime (``routest_amd._rt``,
-``csrc/runtime/batch_queue.cpp``) which releases the GIL while waiting; a pure-Python queue is
-the fallback.
+All workers pull from the same queue (a C-implemented ``queue.SimpleQueue``, which releases the
+GIL while blocked), so several GPUs in one process share load without a router.
+
+Failure handling: a device whose batch raises has that batch re-run on the CPU
+fallback runner (requests are not failed); after ``max_failures`` consecutive failures the
+device is quarantined and its worker leaves the pool; when no device is left the CPU fallback
+worker takes over the queue.  A watchdog counts batches slower than ``watchdog_ms``.
 """
 from __future__ import annotations
 
@@ -25,6 +30,7 @@ import numpy as np
 import torch
 
 from ..models.features import RECORD_DTYPE
+from ..utils.faults import maybe_fail
 from ..utils.logging import get_logger
 from ..utils.metrics import REGISTRY
 
@@ -34,32 +40,45 @@ Runner = Callable[[np.ndarray], np.ndarray]
 
 
 class GpuRunner:
-    """Runs the fused ETA kernel on one GPU with pinned staging buffers and a private stream."""
+    """Runs a fused ETA kernel on one GPU with pinned staging buffers and a private stream.
+
+    Kernels exposing ``forward_hostio`` (the MLP) run zero-copy; others (the tree ensemble) go
+    through an explicit H2D copy, the kernel, and a D2H copy on the same stream."""
 
     def __init__(self, kernel, device: torch.device, batch_max: int):
         self.kernel = kernel
         self.device = torch.device(device)
         self.batch_max = batch_max
+        self.zero_copy = hasattr(kernel, "forward_hostio")
         with torch.cuda.device(self.device):
             self.stream = torch.cuda.Stream(self.device)
             self.h_rec = torch.empty((batch_max, 4), dtype=torch.int32).pin_memory()
             self.h_out = torch.empty(batch_max, dtype=torch.float32).pin_memory()
-            self.d_rec = torch.empty((batch_max, 4), dtype=torch.int32, device=self.device)
+            self.d_rec = None if self.zero_copy else torch.empty((batch_max, 4), dtype=torch.int32,
+                                                                 device=self.device)
         self.h_rec_np = self.h_rec.numpy().view(np.uint8).reshape(batch_max, 16).view(RECORD_DTYPE).reshape(-1)
+        self.h_out_np = self.h_out.numpy()
         self.lock = threading.Lock()
 
+    def __repr__(self) -> str:
+        return f"GpuRunner({self.device})"
+
     def __call__(self, rec: np.ndarray) -> np.ndarray:
+        maybe_fail("gpu_fail")
         n = rec.shape[0]
         out = np.empty(n, dtype=np.float32)
         with self.lock, torch.cuda.device(self.device), torch.cuda.stream(self.stream):
             for s in range(0, n, self.batch_max):
                 m = min(self.batch_max, n - s)
                 self.h_rec_np[:m] = rec[s:s + m]
-                self.d_rec[:m].copy_(self.h_rec[:m], non_blocking=True)
-                y = self.kernel(self.d_rec[:m])
-                self.h_out[:m].copy_(y, non_blocking=True)
+                if self.zero_copy:
+                    self.kernel.forward_hostio(self.h_rec[:m], self.h_out[:m])
+                else:
+                    self.d_rec[:m].copy_(self.h_rec[:m], non_blocking=True)
+                    y = self.kernel(self.d_rec[:m])
+                    self.h_out[:m].copy_(y, non_blocking=True)
                 self.stream.synchronize()
-                out[s:s + m] = self.h_out.numpy()[:m]
+                out[s:s + m] = self.h_out_np[:m]
         return out
 
 
@@ -72,18 +91,40 @@ class _Item:
 
 class MicroBatcher:
     def __init__(self, runners: Sequence[Runner], batch_max: int = 4096, timeout_us: int = 200,
-                 name: str = "eta"):
+                 name: str = "eta", fallback: Optional[Runner] = None, max_failures: int = 3,
+                 watchdog_ms: float = 250.0):
         self.runners = list(runners)
         self.batch_max = batch_max
         self.timeout_s = timeout_us / 1e6
+        self.fallback = fallback
+        self.max_failures = max_failures
+        self.watchdog_s = watchdog_ms / 1e3
+        self.name = name
         self.q: "queue.SimpleQueue[Optional[_Item]]" = queue.SimpleQueue()
         self._stop = False
+        self._state_lock = threading.Lock()
+        self.failures = [0] * len(self.runners)
+        self.healthy = [True] * len(self.runners)
+        self._fallback_started = False
         # adaptive deadline: only wait for stragglers when the last batch showed concurrency
         self._last_batch = 1
-        self.threads = [threading.Thread(target=self._worker, args=(r,), name=f"{name}-batch-{i}",
+        self.threads = [threading.Thread(target=self._worker, args=(r, i), name=f"{name}-batch-{i}",
                                          daemon=True) for i, r in enumerate(self.runners)]
         for t in self.threads:
             t.start()
+
+    def health(self) -> List[dict]:
+        with self._state_lock:
+            rows = [{"runner": repr(r), "healthy": h, "consecutive_failures": f}
+                    for r, h, f in zip(self.runners, self.healthy, self.failures)]
+        if self._fallback_started:
+            rows.append({"runner": "cpu-fallback", "healthy": True, "consecutive_failures": 0})
+        return rows
+
+    @property
+    def degraded(self) -> bool:
+        with self._state_lock:
+            return not all(self.healthy)
 
     # ---- producer side ----
     def submit_nowait(self, rec_tuple, loop: Optional[asyncio.AbstractEventLoop] = None):
@@ -145,7 +186,56 @@ class MicroBatcher:
         else:
             _set()
 
-    def _worker(self, runner: Runner) -> None:
+    def _run_batch(self, runner: Runner, idx: int, batch: List[_Item]) -> bool:
+        """Score one batch; returns False when the runner was quarantined by this failure."""
+        t_q = time.perf_counter()
+        rec = np.array([it.rec for it in batch], dtype=RECORD_DTYPE)
+        alive = True
+        try:
+            ys = runner(rec)
+            dt = time.perf_counter() - t_q
+            REGISTRY.gpu_time.observe(dt)
+            if dt > self.watchdog_s:
+                REGISTRY.slow_batches.inc()
+                log.warning("watchdog: batch of %d on %r took %.1f ms", len(batch), runner, dt * 1e3)
+            if idx >= 0 and self.failures[idx]:
+                with self._state_lock:
+                    self.failures[idx] = 0
+        except BaseException as e:
+            log.error("batch of %d failed on %r: %r", len(batch), runner, e)
+            ys = None
+            if idx >= 0:
+                REGISTRY.device_failures.inc()
+                with self._state_lock:
+                    self.failures[idx] += 1
+                    if self.failures[idx] >= self.max_failures:
+                        self.healthy[idx] = False
+                        alive = False
+                        log.error("quarantining %r after %d consecutive failures", runner, self.failures[idx])
+                        start_fb = (not any(self.healthy) and self.fallback is not None
+                                    and not self._fallback_started)
+                        if start_fb:
+                            self._fallback_started = True
+                if not alive and start_fb:
+                    threading.Thread(target=self._worker, args=(self.fallback, -1),
+                                     name=f"{self.name}-batch-cpu", daemon=True).start()
+            if self.fallback is not None and idx >= 0:
+                try:
+                    ys = self.fallback(rec)
+                except BaseException as e2:  # noqa: BLE001
+                    e = e2
+            if ys is None:
+                for it in batch:
+                    self._resolve(it, exc=e)
+        if ys is not None:
+            for it, y in zip(batch, ys.tolist()):
+                self._resolve(it, float(y))
+        self._last_batch = len(batch)
+        REGISTRY.batch.observe(len(batch))
+        REGISTRY.queue_wait.observe(t_q - batch[0].t0)
+        return alive
+
+    def _worker(self, runner: Runner, idx: int) -> None:
         while True:
             first = self.q.get()
             if first is None:
@@ -156,24 +246,11 @@ class MicroBatcher:
             if batch and batch[-1] is None:
                 batch.pop()
                 stop = True
-            if batch:
-                t_q = time.perf_counter()
-                rec = np.array([it.rec for it in batch], dtype=RECORD_DTYPE)
-                try:
-                    t1 = time.perf_counter()
-                    ys = runner(rec)
-                    REGISTRY.gpu_time.observe(time.perf_counter() - t1)
-                    for it, y in zip(batch, ys.tolist()):
-                        self._resolve(it, float(y))
-                except BaseException as e:  # device failure: fail the batch, keep serving
-                    log.error("batch of %d failed: %r", len(batch), e)
-                    for it in batch:
-                        self._resolve(it, exc=e)
-                self._last_batch = len(batch)
-                REGISTRY.batch.observe(len(batch))
-                REGISTRY.queue_wait.observe(t_q - batch[0].t0)
+            alive = self._run_batch(runner, idx, batch) if batch else True
             if stop:
                 self.q.put(None)
+                return
+            if not alive:
                 return
 
     def close(self) -> None:

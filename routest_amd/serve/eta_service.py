@@ -32,7 +32,8 @@ log = get_logger("eta")
 
 def _cpu_runner(model: Any):
     if isinstance(model, EtaMLP):
-        m = model.float().cpu().eval()
+        import copy
+        m = copy.deepcopy(model).float().cpu().eval()
 
         def run(rec: np.ndarray) -> np.ndarray:
             with torch.no_grad():
@@ -109,13 +110,15 @@ class EtaService:
             for d in self._gpu_devices():
                 runners.append(GpuRunner(ForestKernel(model, d), d, self.batch_max))
                 devs.append(d)
+        fallback = None
         if not runners:
             runners = [_cpu_runner(model)]
             self.backend = "cpu"
         else:
             self.backend = "hip"
+            fallback = _cpu_runner(model)   # failed GPU batches are re-run here
         old = self.batcher
-        self.batcher = MicroBatcher(runners, self.batch_max, self.timeout_us)
+        self.batcher = MicroBatcher(runners, self.batch_max, self.timeout_us, fallback=fallback)
         self.devices = devs
         self.model = model
         self.error = None
@@ -197,7 +200,9 @@ class EtaService:
         return {"backend": self.backend, "devices": [str(d) for d in self.devices],
                 "arch": getattr(self.model, "arch", type(self.model).__name__ if self.model else None),
                 "hidden": getattr(self.model, "hidden", None), "error": self.error,
-                "batch_max": self.batch_max, "timeout_us": self.timeout_us}
+                "batch_max": self.batch_max, "timeout_us": self.timeout_us,
+                "runners": self.batcher.health() if self.batcher is not None else [],
+                "degraded": bool(self.batcher is not None and self.batcher.degraded)}
 
 
 def default_model(seed: int = 0, hidden: int = 256, steps: int = 300) -> EtaMLP:

@@ -95,9 +95,13 @@ class Registry:
         self.gpu_time = Histogram("routest_batch_device_seconds", "device time per batch",
                                   [1e-5, 2.5e-5, 5e-5, 1e-4, 2.5e-4, 5e-4, 1e-3, 5e-3])
 
+        self.device_failures = Counter("routest_device_failures_total", "batches that raised on a device")
+        self.slow_batches = Counter("routest_slow_batches_total", "batches slower than the watchdog limit")
+
     def render(self) -> str:
         lines: List[str] = []
-        for m in (self.requests, self.preds, self.latency, self.batch, self.queue_wait, self.gpu_time):
+        for m in (self.requests, self.preds, self.latency, self.batch, self.queue_wait, self.gpu_time,
+                  self.device_failures, self.slow_batches):
             lines.extend(m.render())
         return "\n".join(lines) + "\n"
 

@@ -1,0 +1,105 @@
+"""Micro-batcher failure handling: fallback re-run, quarantine, CPU takeover,
+watchdog, gpu_fail fault injection — all with CPU fake runners."""
+import numpy as np
+import pytest
+
+from routest_amd.models.features import pack_record
+from routest_amd.serve.batcher import MicroBatcher
+from routest_amd.utils.faults import clear_faults, maybe_fail, set_faults
+from routest_amd.utils.metrics import REGISTRY
+from routest_amd.utils.timeutil import parse_iso
+
+
+def _rec(d=5000.0):
+    return pack_record(weather="Sunny", traffic="Low", distance_m=d,
+                       pickup=parse_iso("2025-08-25T08:30:00"), driver_age=30)
+
+
+class FlakyRunner:
+    def __init__(self, fail_first):
+        self.fail_first, self.calls = fail_first, 0
+
+    def __repr__(self):
+        return "FlakyRunner"
+
+    def __call__(self, rec):
+        self.calls += 1
+        if self.calls <= self.fail_first:
+            raise RuntimeError("device lost")
+        return np.full(len(rec), 7.0, np.float32)
+
+
+def cpu_runner(rec):
+    return np.full(len(rec), 3.0, np.float32)
+
+
+def test_failed_batch_rerun_on_fallback():
+    b = MicroBatcher([FlakyRunner(1)], batch_max=8, timeout_us=0, fallback=cpu_runner)
+    try:
+        assert b.predict_sync(_rec()) == 3.0      # failed on the device, served by the fallback
+        assert b.predict_sync(_rec()) == 7.0      # device recovered
+        assert not b.degraded
+    finally:
+        b.close()
+
+
+def test_quarantine_then_cpu_takeover():
+    f0 = REGISTRY.device_failures.value()
+    b = MicroBatcher([FlakyRunner(10 ** 9)], batch_max=8, timeout_us=0, fallback=cpu_runner, max_failures=2)
+    try:
+        vals = [b.predict_sync(_rec(), timeout=10) for _ in range(6)]
+        assert vals == [3.0] * 6
+        assert b.degraded
+        h = b.health()
+        assert h[0]["healthy"] is False and h[-1]["runner"] == "cpu-fallback"
+        assert REGISTRY.device_failures.value() - f0 == 2   # quarantined after 2, then CPU worker
+    finally:
+        b.close()
+
+
+def test_without_fallback_errors_propagate():
+    b = MicroBatcher([FlakyRunner(1)], batch_max=8, timeout_us=0)
+    try:
+        with pytest.raises(RuntimeError):
+            b.predict_sync(_rec(), timeout=10)
+        assert b.predict_sync(_rec(), timeout=10) == 7.0
+    finally:
+        b.close()
+
+
+def test_watchdog_counts_slow_batches():
+    import time
+
+    def slow(rec):
+        time.sleep(0.02)
+        return np.zeros(len(rec), np.float32)
+    s0 = REGISTRY.slow_batches.value()
+    b = MicroBatcher([slow], batch_max=8, timeout_us=0, watchdog_ms=5)
+    try:
+        b.predict_sync(_rec())
+        assert REGISTRY.slow_batches.value() - s0 >= 1
+    finally:
+        b.close()
+
+
+def test_gpu_fail_fault_injection():
+    set_faults("gpu_fail")
+    try:
+        with pytest.raises(Exception):
+            maybe_fail("gpu_fail")
+    finally:
+        clear_faults()
+    maybe_fail("gpu_fail")  # cleared
+
+
+def test_service_reports_runner_health():
+    from routest_amd.models.mlp3 import LinearETA
+    from routest_amd.serve.eta_service import EtaService
+    from routest_amd.data.synth import synth_trips
+    x, y = synth_trips(500, 0)
+    svc = EtaService(model=LinearETA().fit(x, y), device="cpu")
+    try:
+        d = svc.describe()
+        assert "runners" in d and d["degraded"] is False
+    finally:
+        svc.close()
