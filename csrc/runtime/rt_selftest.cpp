@@ -1,0 +1,128 @@
+// Host-only self-test + fuzz harness for the native runtime core (rt_core.h, json_lite.h).
+// Built with -fsanitize=address,undefined by `tools/build_ext.py --sanitize` or the CMake `asan`
+// preset (the reference has no race detection / sanitizers at all), and run by
+// tests/test_sanitize_cpu.py.  Exit code 0 = all invariants held and no sanitizer report.
+//
+//   rt_selftest [iterations] [seed]
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "rt_core.h"
+
+using namespace rtc;
+
+static int g_fail = 0;
+#define CHECK(c, ...)                                      \
+  do {                                                     \
+    if (!(c)) {                                            \
+      std::fprintf(stderr, "CHECK failed %s:%d: ", __FILE__, __LINE__); \
+      std::fprintf(stderr, __VA_ARGS__);                   \
+      std::fprintf(stderr, "\n");                          \
+      ++g_fail;                                            \
+    }                                                      \
+  } while (0)
+
+static const char* SEEDS[] = {
+    R"({"summary":{"distance":12345},"pickup_time":"2025-08-25T08:30:00","driver_age":34,"weather":"Sunny","traffic":"Medium"})",
+    R"([{"summary":{"distance":1000.5}},{"summary":{"distance":"2500"},"traffic":"Jam","pickup_time":"2024-02-29 23:59:59.999999+05:30"}])",
+    R"({"items":[{"summary":null,"driver_age":0,"weather":"Hail"},{"pickup_time":"2025-01-01T00:00:00Z"}]})",
+    R"({"summary":{"distance":1e308},"driver_age":"abc","pickup_time":"not-a-date"})",
+    R"([1, "x", null, true, {"a":[1,2,{"b":NaN}],"c":Infinity,"d":-Infinity,"e":"é\"\\"}])",
+};
+
+static void fuzz_json(std::mt19937_64& rng, int iters) {
+  const Stamp now{1756110600, 123456, false, 0, 0};
+  for (int it = 0; it < iters; ++it) {
+    std::string s = SEEDS[rng() % (sizeof SEEDS / sizeof *SEEDS)];
+    const int muts = (int)(rng() % 6);
+    for (int k = 0; k < muts && !s.empty(); ++k) {
+      const size_t p = rng() % s.size();
+      switch (rng() % 4) {
+        case 0: s[p] = (char)(rng() & 0xFF); break;                       // flip a byte
+        case 1: s.erase(p, 1 + rng() % 8); break;                          // delete a run
+        case 2: s.insert(p, s.substr(rng() % s.size(), 1 + rng() % 16)); break;  // duplicate
+        default: s.resize(p); break;                                       // truncate
+      }
+    }
+    rtj::Value root;
+    try {
+      root = rtj::Parser(s.data(), s.size()).parse();
+    } catch (...) {
+      continue;  // malformed JSON is rejected, never read out of bounds
+    }
+    std::vector<const rtj::Value*> items;
+    if (root.kind == rtj::Value::Arr)
+      for (auto& v : root.arr) items.push_back(&v);
+    else
+      items.push_back(&root);
+    std::string out;
+    for (const rtj::Value* v : items) {
+      EtaRecord r{};
+      Stamp st;
+      std::string err = pack_item(*v, now, r, st);
+      if (err.empty()) {
+        CHECK(r.weather <= 3 || r.weather == 255, "weather code %d", r.weather);
+        CHECK(r.traffic <= 3 || r.traffic == 255, "traffic code %d", r.traffic);
+      }
+      static const double MINS[] = {17.25, 0.0, -3.5, 1e30, NAN, INFINITY, 1234567.891};
+      format_one(out, MINS[rng() % 7], st.secs, st.us, st.has_tz, st.tz_sec, err);
+    }
+  }
+}
+
+static void fuzz_iso(std::mt19937_64& rng, int iters) {
+  static const char alpha[] = "0123456789-:T .Z+z,";
+  for (int it = 0; it < iters; ++it) {
+    std::string s;
+    const int n = (int)(rng() % 40);
+    for (int k = 0; k < n; ++k) s += alpha[rng() % (sizeof alpha - 1)];
+    Stamp st;
+    if (parse_iso(s, st)) {
+      // a parsed stamp re-formats to a string that parses to the same instant
+      std::string f = isoformat(st.secs, st.us, st);
+      Stamp st2;
+      CHECK(parse_iso(f, st2) && st2.secs == st.secs && st2.us == st.us && st2.tz_sec == st.tz_sec,
+            "iso round trip '%s' -> '%s'", s.c_str(), f.c_str());
+    }
+  }
+  // calendar round trip over 600 years
+  for (int64_t d = -80000; d < 140000; d += 17) {
+    int64_t y;
+    unsigned m, dd;
+    civil_from_days(d, y, m, dd);
+    CHECK(days_from_civil(y, m, dd) == d, "civil round trip %lld", (long long)d);
+  }
+}
+
+static void fuzz_float(std::mt19937_64& rng, int iters) {
+  for (int it = 0; it < iters; ++it) {
+    double v;
+    switch (rng() % 3) {
+      case 0: { uint64_t b = rng(); std::memcpy(&v, &b, 8); break; }         // any bit pattern
+      case 1: v = std::ldexp((double)(rng() % 100000), (int)(rng() % 80) - 40); break;
+      default: v = (double)(float)((rng() % 200000) / 997.0); break;           // float32 minutes
+    }
+    std::string o;
+    append_pyfloat(o, v);
+    if (std::isfinite(v)) {
+      CHECK(std::strtod(o.c_str(), nullptr) == v, "repr round trip %.17g -> %s", v, o.c_str());
+    }
+    const int64_t us = timedelta_minutes_us(std::isfinite(v) && std::fabs(v) < 1e9 ? v : 1.5);
+    (void)us;
+  }
+  CHECK(timedelta_minutes_us(0.5) == 30000000, "timedelta 0.5 min");
+  CHECK(timedelta_minutes_us(1.0 / 60000000.0 * 2.5) == 2, "half-even rounding");
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? std::atoi(argv[1]) : 20000;
+  std::mt19937_64 rng(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 1234);
+  fuzz_json(rng, iters);
+  fuzz_iso(rng, iters);
+  fuzz_float(rng, iters);
+  std::printf("rt_selftest: %d iterations, %d failures\n", iters, g_fail);
+  return g_fail ? 1 : 0;
+}

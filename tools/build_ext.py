@@ -4,10 +4,13 @@
 * ``routest_amd/_C*.so``  — gfx950 HIP kernels (csrc/*.hip, hipcc --offload-arch=gfx950) + the
   torch binding TU (csrc/bindings.cpp).  Loaded by :mod:`routest_amd.ops`.
 * ``routest_amd/_rt*.so`` — CPU-only C++ runtime (csrc/runtime/*.cpp, g++ + pybind11):
-  greedy-CVRP reference, request packing, micro-batch queue.  Works on machines without a GPU.
+  /predict JSON packing + response formatting, ISO parsing, greedy-CVRP and A* CPU fallbacks.
+  Works on machines without a GPU.
+* ``build/native/rt_selftest_asan`` (``--sanitize``) — the runtime core built host-only with
+  ``-fsanitize=address,undefined`` into a fuzz/self-test executable.
 
 Incremental: an object is rebuilt only when its source or any header is newer.
-Usage: ``python tools/build_ext.py [--force] [--jobs N] [--only C|rt]``.
+Usage: ``python tools/build_ext.py [--force] [--jobs N] [--only C|rt|sanitize] [--sanitize]``.
 """
 from __future__ import annotations
 
@@ -93,7 +96,8 @@ def build_C(force: bool = False, jobs: int = 8) -> str:
 def build_rt(force: bool = False, jobs: int = 8) -> str:
     import pybind11
     py_inc = sysconfig.get_paths()["include"]
-    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    srcs = sorted(p for p in glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))
+                  if not p.endswith("_selftest.cpp"))
     headers = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
     out = os.path.join(PKG, "_rt" + EXT_SUFFIX)
     if not srcs:
@@ -105,12 +109,29 @@ def build_rt(force: bool = False, jobs: int = 8) -> str:
     return out
 
 
+def build_sanitize(force: bool = False) -> str:
+    """Host-only ASan+UBSan build of the runtime core fuzz harness (no GPU code involved)."""
+    rdir = os.path.join(CSRC, "runtime")
+    src = os.path.join(rdir, "rt_selftest.cpp")
+    out = os.path.join(BUILD, "rt_selftest_asan")
+    os.makedirs(BUILD, exist_ok=True)
+    if force or _newer(out, [src] + glob.glob(os.path.join(rdir, "*.h"))):
+        _run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+              "-fno-omit-frame-pointer", "-I", rdir, src, "-o", out])
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
-    ap.add_argument("--only", choices=["C", "rt"], default=None)
+    ap.add_argument("--only", choices=["C", "rt", "sanitize"], default=None)
+    ap.add_argument("--sanitize", action="store_true", help="also build the ASan/UBSan runtime harness")
     a = ap.parse_args()
+    if a.only == "sanitize" or a.sanitize:
+        print("built", build_sanitize(a.force))
+        if a.only == "sanitize":
+            return
     if a.only in (None, "rt"):
         print("built", build_rt(a.force, a.jobs))
     if a.only in (None, "C"):
