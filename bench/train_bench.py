@@ -19,6 +19,16 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+class _Pinned:
+    """DeviceComm with a fixed algorithm (for A/B sweeps)."""
+
+    def __init__(self, comm, algo):
+        self.comm, self.algo = comm, algo
+
+    def all_reduce(self, t):
+        return self.comm.all_reduce(t, self.algo)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536, help="per-GPU batch")
@@ -26,6 +36,8 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--modes", default="fused,graph,hipblaslt,autograd")
+    ap.add_argument("--comm", default="torch", choices=["torch", "rccl", "oneshot", "auto"],
+                    help="gradient all-reduce for the fused modes: ProcessGroup, or native (csrc/comm.hip)")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -42,13 +54,20 @@ def main() -> None:
     B = a.batch
     rec, y = synth_records(B, 100 + di.rank)
     rt = records_to_tensor(rec).to(dev)
+    comm = None
+    if a.comm != "torch" and di.world > 1:
+        from routest_amd.parallel.comm import DeviceComm
+        comm = DeviceComm(dev)
+        comm_algo = a.comm
     results = {}
     for mode in a.modes.split(","):
         m = EtaMLP(a.hidden)
         m.fit_normalization(xs, ys)
         yn = ((torch.from_numpy(y) - m.y_mean) / m.y_std).float().to(dev)
         if mode in ("fused", "graph", "hipblaslt"):
-            tr = FusedMlp3Trainer(m, dev, B, B * di.world, lr=1e-3, allreduce=di.world > 1)
+            tr = FusedMlp3Trainer(m, dev, B, B * di.world, lr=1e-3, allreduce=di.world > 1, comm=comm)
+            if comm is not None and comm_algo != "auto":
+                tr.comm = _Pinned(comm, comm_algo)
             tr.use_hipblaslt_wgrad = mode == "hipblaslt"
             step = lambda: tr.step(rt, yn)  # noqa: E731
             if mode == "graph":
@@ -92,7 +111,7 @@ def main() -> None:
         results[mode] = {"ms_per_step": el / a.steps * 1e3,
                          "samples_per_s": B * di.world * a.steps / el}
     if di.is_main:
-        print(json.dumps({"metric": "ETA MLP DP training samples/s", "n_gpus": di.world,
+        print(json.dumps({"metric": "ETA MLP DP training samples/s", "n_gpus": di.world, "comm": a.comm,
                           "batch_per_gpu": B, "hidden": a.hidden, "results": results}), flush=True)
     if di.world > 1:
         dist.destroy_process_group()

@@ -396,6 +396,70 @@ torch::Tensor forest_predict(torch::Tensor records, torch::Tensor values, torch:
   return out;
 }
 
+// ---------------------------------------------------------------- native collectives (comm.hip)
+py::bytes comm_unique_id() {
+  char id[128];
+  TORCH_CHECK(rt::comm_unique_id(id) == 0, "ncclGetUniqueId failed");
+  return py::bytes(id, 128);
+}
+
+int64_t comm_create(py::bytes uid, int64_t rank, int64_t world, int64_t device, int64_t oneshot_bytes,
+                    bool use_rccl) {
+  std::string u = uid;
+  TORCH_CHECK(!use_rccl || u.size() == 128, "unique id must be 128 bytes");
+  u.resize(128);
+  std::string err;
+  int64_t h;
+  {
+    py::gil_scoped_release nogil;   // ncclCommInitRank blocks until every rank joined
+    h = rt::comm_create(u.data(), (int)rank, (int)world, (int)device, (size_t)oneshot_bytes, use_rccl, err);
+  }
+  TORCH_CHECK(h >= 0, "comm_create: ", err);
+  return h;
+}
+
+py::bytes comm_ipc_handles(int64_t h) {
+  std::string out(rt::comm_ipc_handle_bytes(), '\0');
+  const int r = rt::comm_ipc_handles(h, out.data());
+  TORCH_CHECK(r == 0, "hipIpcGetMemHandle failed (", r, ")");
+  return py::bytes(out);
+}
+
+void comm_open_peers(int64_t h, std::vector<py::bytes> handles) {
+  std::vector<std::string> hs(handles.begin(), handles.end());
+  std::string err;
+  TORCH_CHECK(rt::comm_open_peers(h, hs, err) == 0, "comm_open_peers: ", err);
+}
+
+void comm_all_reduce(int64_t h, torch::Tensor t, int64_t algo) {
+  check_dev(t, "all_reduce tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, "all_reduce: float32 buckets only");
+  const c10::DeviceGuard guard(t.device());
+  std::string err;
+  const hipError_t e = rt::comm_all_reduce_f32(h, t.data_ptr<float>(), (size_t)t.numel(), (int)algo, cur_stream(t), err);
+  TORCH_CHECK(e == hipSuccess, "comm_all_reduce: ", err.empty() ? hipGetErrorString(e) : err);
+}
+
+int dtype_code(const torch::Tensor& t) {
+  if (t.scalar_type() == torch::kFloat32) return 0;
+  if (t.scalar_type() == torch::kBFloat16) return 1;
+  if (t.scalar_type() == torch::kInt32) return 2;
+  TORCH_CHECK(false, "collective dtype must be float32, bfloat16 or int32");
+  return -1;
+}
+
+void comm_collective(int64_t h, int64_t op, torch::Tensor in, torch::Tensor out, int64_t root) {
+  check_dev(in, "input");
+  check_dev(out, "output");
+  TORCH_CHECK(in.scalar_type() == out.scalar_type(), "dtype mismatch");
+  const c10::DeviceGuard guard(in.device());
+  std::string err;
+  // counts are per-rank for all_gather / reduce_scatter (nccl convention)
+  const size_t count = op == 0 ? (size_t)in.numel() : (op == 1 ? (size_t)out.numel() : (size_t)in.numel());
+  TORCH_CHECK(rt::comm_nccl_call(h, (int)op, in.data_ptr(), out.data_ptr(), count, dtype_code(in), (int)root,
+                                 cur_stream(in), err) == 0, "RCCL collective: ", err);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -420,5 +484,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("route_score", &route_score, "K8: per-route delay-weighted length");
   m.def("astar", &astar, "K9: batched A* (one lane per query) with learned edge costs");
   m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
+  m.def("comm_unique_id", &comm_unique_id, "RCCL unique id (128 bytes) for comm_create");
+  m.def("comm_create", &comm_create, "own RCCL communicator + one-shot IPC buffers");
+  m.def("comm_ipc_handles", &comm_ipc_handles, "IPC handles of this rank's one-shot buffers");
+  m.def("comm_open_peers", &comm_open_peers, "map every peer's one-shot buffers (xGMI)");
+  m.def("comm_all_reduce", &comm_all_reduce, "in-place SUM all-reduce on the current stream (0=rccl, 1=oneshot)");
+  m.def("comm_collective", &comm_collective, "RCCL all_gather(0)/reduce_scatter(1)/broadcast(2)/all_reduce(3)");
+  m.def("comm_error", [](int64_t h) { return (int64_t)rt::comm_error(h); });
+  m.def("comm_destroy", [](int64_t h) { rt::comm_destroy(h); });
+  m.def("rccl_version", []() { return (int64_t)rt::comm_rccl_version(); });
   m.attr("ARCH") = "gfx950";
 }

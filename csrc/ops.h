@@ -1,6 +1,9 @@
 // Host-side launcher declarations for every routest_amd HIP kernel (gfx950).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -69,5 +72,20 @@ hipError_t launch_haversine_matrix(const double* lat, const double* lon, const i
 hipError_t launch_greedy_cvrp(const double* D, const int* npts, const double* demand,
                               const double* cap, const double* maxd, int R, int NM, int* visit,
                               int* trip_of, int* ntrips, int* status, hipStream_t stream);
+
+// ---- native collectives (rccl_ops) : comm.hip ----
+int comm_unique_id(char out[128]);
+int64_t comm_create(const char* uid, int rank, int world, int device, size_t oneshot_bytes, bool use_rccl,
+                    std::string& errmsg);
+int comm_ipc_handle_bytes();
+int comm_ipc_handles(int64_t h, char* out);
+int comm_open_peers(int64_t h, const std::vector<std::string>& handles, std::string& errmsg);
+hipError_t comm_all_reduce_f32(int64_t h, float* data, size_t n, int algo, hipStream_t stream,
+                               std::string& errmsg);
+int comm_nccl_call(int64_t h, int op, const void* in, void* out, size_t count, int dtype, int root,
+                   hipStream_t stream, std::string& errmsg);
+int comm_error(int64_t h);
+void comm_destroy(int64_t h);
+int comm_rccl_version();
 
 }  // namespace rt

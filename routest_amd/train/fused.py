@@ -74,7 +74,7 @@ class FusedMlp3Trainer:
     def __init__(self, model: EtaMLP, device: torch.device, batch_local: int, global_batch: int,
                  lr: float = 2e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  warmup: int = 0, total_steps: int = 0, min_lr_ratio: float = 0.1,
-                 allreduce: bool = True):
+                 allreduce: bool = True, comm=None):
         if model.hidden not in (64, 128, 256):
             raise ValueError("fused trainer supports hidden in (64, 128, 256)")
         self.C = _ext.native(required=True)
@@ -86,6 +86,7 @@ class FusedMlp3Trainer:
         self.hp = dict(lr=lr, beta1=betas[0], beta2=betas[1], eps=eps, wd=weight_decay, warmup=warmup,
                        total_steps=total_steps, min_lr_ratio=min_lr_ratio)
         self.allreduce = allreduce
+        self.comm = comm          # parallel.comm.DeviceComm: native RCCL / one-shot all-reduce
         xs = model.x_std.float().cpu()
         xm = model.x_mean.float().cpu()
         if (xm[:8] != 0).any() or (xs[:8] != 1).any():
@@ -152,7 +153,9 @@ class FusedMlp3Trainer:
     def step(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> torch.Tensor:
         """One optimizer step; returns the device tensor of per-tile squared errors (no sync)."""
         self.forward_backward(rec, tgt_norm)
-        if self.allreduce:
+        if self.comm is not None:
+            self.comm.all_reduce(self.G)
+        elif self.allreduce:
             allreduce_flat(self.G, average=False)
         self._pack(update=True)
         return self.loss_tiles

@@ -53,6 +53,7 @@ class TrainConfig:
     ckpt_every: int = 0
     eval_rows: int = 65536
     dist_backend: str = ""         # "" = nccl on GPU, gloo on CPU
+    comm: str = "torch"            # gradient all-reduce: torch (ProcessGroup) | rccl | oneshot (native, fused backend)
 
 
 def train_linear(cfg: TrainConfig) -> LinearETA:
@@ -130,7 +131,7 @@ class Trainer:
             self.fused = FusedMlp3Trainer(self.model, self.di.device, cfg.batch_local, self.global_batch,
                                           lr=cfg.lr, weight_decay=cfg.weight_decay, warmup=cfg.warmup,
                                           total_steps=total, min_lr_ratio=cfg.min_lr_ratio,
-                                          allreduce=self.di.world > 1)
+                                          allreduce=self.di.world > 1, comm=self._native_comm())
             if self._opt_state is not None:
                 self.fused.load_optimizer_state(self._opt_state)
         else:
@@ -145,6 +146,15 @@ class Trainer:
                 self.opt, lambda k: lr_at(k + 1, 1.0, cfg.warmup, total, cfg.min_lr_ratio))
             if self._opt_state is not None:
                 self._load_torch_opt(self._opt_state)
+
+    def _native_comm(self):
+        if self.cfg.comm == "torch" or self.di.world == 1:
+            return None
+        from ..parallel.comm import DeviceComm
+        c = DeviceComm(self.di.device)
+        if self.cfg.comm == "oneshot" and not c.oneshot:
+            raise RuntimeError("one-shot all-reduce needs all ranks on one node (<= 8 GPUs)")
+        return c
 
     def _load_torch_opt(self, st: Dict[str, torch.Tensor]) -> None:
         m_flat, v_flat = st["exp_avg"], st["exp_avg_sq"]

@@ -71,7 +71,7 @@ def build_C(force: bool = False, jobs: int = 8) -> str:
         objs.append(obj)
         if force or _newer(obj, [src] + headers):
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics",
-                              "-I", CSRC, "-c", src, "-o", obj])
+                              "-I", CSRC, "-I", os.path.join(ROCM, "include"), "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(BUILD, "bindings.cpp.o")
     objs.append(bobj)
@@ -87,9 +87,11 @@ def build_C(force: bool = False, jobs: int = 8) -> str:
         list(ex.map(_run, jobs_list))
     out = os.path.join(PKG, "_C" + EXT_SUFFIX)
     if force or jobs_list or _newer(out, objs):
-        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, *objs,
+        # RCCL: link the copy torch itself loads (torch/lib/librccl.so, no SONAME) so one RCCL
+        # instance serves both torch.distributed and our own communicators
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-L", libdir, "-o", out, *objs,
               "-L", libdir, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-              "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{libdir}"])
+              "-ltorch_python", "-lamdhip64", "-l:librccl.so", f"-Wl,-rpath,{libdir}"])
     return out
 
 
