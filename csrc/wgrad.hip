@@ -149,28 +149,58 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
   }
 }
 
-// G[e] = sum_s slab[s][e] for e in [0, n), fixed order over s (deterministic).
+// G[e] = sum_s slab[s][e] for e in [0, n) — deterministic (fixed summation tree, no atomics).
+//
+// 256 threads = 16 slab-lanes x 16 float4 columns: thread (sl, c) sums slabs sl, sl+16, ... of
+// column c with 4 independent loads in flight, then the 16 partials are combined in LDS in a fixed
+// order.  ~n/64 workgroups (1157 for the H=256 bucket) keep every CU streaming the 76 MB of slabs;
+// the previous one-thread-per-column version ran 73 workgroups and 256 dependent loads per thread.
+constexpr int RED_SL = 16, RED_COLS = 16;
+
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, int S,
                                                            long long slab_stride,
                                                            float* __restrict__ G, int n) {
-  const int i4 = blockIdx.x * blockDim.x + threadIdx.x;
-  const int e = i4 * 4;
-  if (e >= n) return;
-  if (e + 4 <= n && (slab_stride % 4) == 0) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s = 0; s < S; ++s) {
-      const float4 v = *reinterpret_cast<const float4*>(slab + s * slab_stride + e);
-      acc.x += v.x;
-      acc.y += v.y;
-      acc.z += v.z;
-      acc.w += v.w;
+  __shared__ float4 part[RED_SL][RED_COLS + 1];
+  const int c = threadIdx.x & (RED_COLS - 1), sl = threadIdx.x / RED_COLS;
+  const int e = (blockIdx.x * RED_COLS + c) * 4;
+  const bool vec = (slab_stride % 4) == 0 && e + 4 <= n;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < n) {
+    if (vec) {
+      f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+      auto ld = [&](int k) {
+        return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(slab + (long long)k * slab_stride + e));
+      };
+      int s = sl;
+      for (; s + 3 * RED_SL < S; s += 4 * RED_SL) {
+        const f32x4 v0 = ld(s), v1 = ld(s + RED_SL), v2 = ld(s + 2 * RED_SL), v3 = ld(s + 3 * RED_SL);
+        a4 += v0;
+        a4 += v1;
+        a4 += v2;
+        a4 += v3;
+      }
+      for (; s < S; s += RED_SL) a4 += ld(s);
+      acc = make_float4(a4[0], a4[1], a4[2], a4[3]);
+    } else {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int s = sl; s < S; s += RED_SL)
+        for (int q = 0; q < 4 && e + q < n; ++q) t[q] += slab[(long long)s * slab_stride + e + q];
+      acc = make_float4(t[0], t[1], t[2], t[3]);
     }
-    *reinterpret_cast<float4*>(G + e) = acc;
-  } else {
-    for (int q = e; q < min(n, e + 4); ++q) {
-      float acc = 0.f;
-      for (int s = 0; s < S; ++s) acc += slab[s * slab_stride + q];
-      G[q] = acc;
+  }
+  part[sl][c] = acc;
+  __syncthreads();
+  if (sl == 0 && e < n) {
+    float4 r = part[0][c];
+    for (int k = 1; k < RED_SL; ++k) {
+      const float4 v = part[k][c];
+      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    if (vec) {
+      *reinterpret_cast<float4*>(G + e) = r;
+    } else {
+      const float rr[4] = {r.x, r.y, r.z, r.w};
+      for (int q = 0; q < 4 && e + q < n; ++q) G[e + q] = rr[q];
     }
   }
 }
@@ -214,8 +244,7 @@ hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm,
 
 hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, float* G, int n,
                                hipStream_t stream) {
-  const int threads = (n + 3) / 4;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, slab,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((n + 4 * RED_COLS - 1) / (4 * RED_COLS)), dim3(256), 0, stream, slab,
                      S, slab_stride, G, n);
   return hipGetLastError();
 }

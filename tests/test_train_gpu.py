@@ -148,3 +148,19 @@ def test_wgrad_kernel_vs_fp32(K, M, Mout, N, S):
     C.wgrad_reduce(slab[:, :], G)
     got = G[8:8 + Mout * ldo].view(Mout, ldo)[:, :N].cpu()
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3 * (K ** 0.5))
+
+
+@pytest.mark.parametrize("S,n,stride", [(256, 74000, 74000), (37, 1001, 1003), (5, 4096, 4100), (1, 3, 3)])
+def test_wgrad_reduce_exact_and_deterministic(S, n, stride):
+    from routest_amd.ops import _ext
+    C = _ext.native()
+    g = torch.Generator().manual_seed(S * 7 + n)
+    slab = torch.randn(S, stride, generator=g)
+    G1 = torch.zeros(n, device=DEV)
+    G2 = torch.zeros(n, device=DEV)
+    sd = slab.to(DEV)
+    C.wgrad_reduce(sd, G1)      # slab rows may be longer than the bucket
+    C.wgrad_reduce(sd, G2)
+    ref = slab.double().sum(0)[:n].float()
+    torch.testing.assert_close(G1.cpu(), ref, rtol=1e-5, atol=1e-4)
+    assert torch.equal(G1, G2)
