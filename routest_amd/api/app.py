@@ -107,6 +107,108 @@ class _MetricsASGI:
                                   status=str(status["code"]))
 
 
+class _FastPredictASGI:
+    """Pure-ASGI fast path for single-item ``POST /api/predict_eta`` and ``POST /predict``,
+    dispatched by :class:`RoutestApp` ahead of Starlette's whole middleware stack.
+
+    The request body goes straight to the native packer (``_rt.pack_predict_batch``: C++ JSON ->
+    16-byte record with the reference's field semantics), the record to the micro-batcher, and the
+    minutes back through the native formatter — no FastAPI routing, Request object, ``json.loads``
+    or ``JSONResponse`` rendering on the hot path.  Anything that is not a clean single prediction
+    (pack error, batch body, model unavailable, no native runtime) is replayed unchanged into the
+    FastAPI handler, which owns the error semantics (RO/Flaskr/routes.py:365-383)."""
+
+    PATHS = (b"/api/predict_eta", b"/predict")
+
+    def __init__(self, app, sv, rt_native):
+        self.app, self.sv, self.rt = app, sv, rt_native
+
+    def matches(self, scope) -> bool:
+        if scope["type"] != "http" or scope["method"] != "POST" or self.rt is None:
+            return False
+        if scope.get("raw_path", scope["path"].encode()) not in self.PATHS:
+            return False
+        for k, _ in scope.get("headers", ()):
+            if k == b"origin":          # cross-origin: let CORSMiddleware add its headers
+                return False
+        return True
+
+    async def __call__(self, scope, receive, send):
+        t0 = time.perf_counter()
+        chunks = []
+        more = True
+        while more:
+            msg = await receive()
+            if msg["type"] != "http.request":
+                return await self.app(scope, _replay(b"".join(chunks), msg), send)
+            chunks.append(msg.get("body", b""))
+            more = msg.get("more_body", False)
+        raw = b"".join(chunks)
+        out = await self._try(scope, raw)
+        if out is None:
+            return await self.app(scope, _replay(raw), send)
+        await send({"type": "http.response.start", "status": 200,
+                    "headers": [(b"content-type", b"application/json"),
+                                (b"content-length", str(len(out)).encode())]})
+        await send({"type": "http.response.body", "body": out})
+        REGISTRY.latency.observe(time.perf_counter() - t0)
+        REGISTRY.requests.inc(route=scope["path"], status="200")
+
+    async def _try(self, scope, raw: bytes):
+        ctype = b""
+        for k, v in scope.get("headers", ()):
+            if k == b"content-type":
+                ctype = v
+        if b"json" not in ctype.lower():
+            raw = b"{}"                 # Flask get_json(silent=True) -> None -> {} (both routes)
+        eta = self.sv.eta
+        if eta.batcher is None or not eta.available:
+            return None
+        now = dt.datetime.now()
+        now_secs = int((now - dt.datetime(1970, 1, 1)).total_seconds() // 1)
+        try:
+            rec_u8, secs, us, tz, errs, is_batch = self.rt.pack_predict_batch(raw, now_secs, now.microsecond)
+        except Exception:
+            return None                 # malformed JSON: the handler applies silent semantics
+        if is_batch or errs[0]:
+            return None
+        from ..models.features import RECORD_DTYPE
+        rec = rec_u8.view(RECORD_DTYPE).reshape(-1)[0].item()
+        try:
+            minutes = await eta.batcher.submit(rec)
+        except Exception:
+            return None
+        import numpy as np
+        REGISTRY.preds.inc()
+        return self.rt.format_predict_batch(np.array([minutes], dtype=np.float32), secs, us, tz, errs, False)
+
+
+class RoutestApp(FastAPI):
+    """FastAPI app whose ASGI entry first offers the request to the native single-predict fast
+    path (``fast``); everything else takes the normal middleware + router stack."""
+
+    fast: Optional[_FastPredictASGI] = None
+
+    async def __call__(self, scope, receive, send):
+        f = self.fast
+        if f is not None and f.matches(scope):
+            return await f(scope, receive, send)
+        return await super().__call__(scope, receive, send)
+
+
+def _replay(body: bytes, tail=None):
+    sent = [False]
+
+    async def receive():
+        if not sent[0]:
+            sent[0] = True
+            return {"type": "http.request", "body": body, "more_body": False}
+        if tail is not None:
+            return tail
+        return {"type": "http.disconnect"}
+    return receive
+
+
 async def _json_body(request: Request, silent: bool):
     """Flask ``get_json()`` semantics: non-silent -> 415 on non-JSON content type, 400 on bad JSON;
     silent -> None on either."""
@@ -136,12 +238,22 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         await sv.simulator.shutdown()
         sv.eta.close()
 
-    app = FastAPI(title="routest_amd", version="1.0", lifespan=lifespan)
+    app = RoutestApp(title="routest_amd", version="1.0", lifespan=lifespan)
     app.state.services = sv
+    rt_fast = None
+    if s.fast_predict:
+        try:
+            from ..ops import _ext
+            rt_fast = _ext.runtime(required=False)
+        except Exception:  # pragma: no cover
+            rt_fast = None
     app.add_middleware(CORSMiddleware, allow_origins=s.cors_origins,
                        allow_origin_regex=s.cors_origin_regex, allow_credentials=True,
                        allow_methods=["*"], allow_headers=["*"])
     app.add_middleware(_MetricsASGI)
+    if rt_fast is not None:
+        # fall-through requests re-enter the full stack (middleware + router) with the body replayed
+        app.fast = _FastPredictASGI(super(RoutestApp, app).__call__, sv, rt_fast)
 
     # ------------------------------------------------------------------ routing
     @app.post("/api/request_route")

@@ -103,3 +103,28 @@ def test_service_reports_runner_health():
         assert "runners" in d and d["degraded"] is False
     finally:
         svc.close()
+
+
+def test_inline_when_idle_and_queue_under_load():
+    import asyncio
+    calls = []
+
+    def runner(rec):
+        calls.append(len(rec))
+        return np.full(len(rec), 2.0, np.float32)
+    b = MicroBatcher([runner], batch_max=64, timeout_us=2000)
+    try:
+        async def one():
+            return await b.submit(_rec())
+        assert asyncio.run(one()) == 2.0 and calls == [1]
+
+        async def many():
+            b._busy += 1          # pretend a batch is in flight: everything must queue
+            try:
+                return await asyncio.gather(*[b.submit(_rec()) for _ in range(32)])
+            finally:
+                b._busy -= 1
+        assert asyncio.run(many()) == [2.0] * 32
+        assert sum(calls[1:]) == 32
+    finally:
+        b.close()
