@@ -22,6 +22,7 @@
 #include <queue>
 #include <stdexcept>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -35,6 +36,56 @@ using namespace rtc;
 //          (has_tz, offset_s), errors list[str], is_batch)
 py::tuple pack_predict_batch(py::bytes body, int64_t now_secs, int32_t now_us) {
   std::string b = body;
+  Stamp now;
+  now.secs = now_secs;
+  now.us = now_us;
+  // Fast path for big top-level arrays: split items with one scan, then parse + pack them in
+  // parallel (each item is an independent JSON value).  Anything else takes the DOM path.
+  std::vector<std::pair<size_t, size_t>> spans;
+  bool split = false;
+  {
+    py::gil_scoped_release nogil;
+    if (b.size() > (64u << 10)) split = split_top_array(b.data(), b.size(), spans);
+  }
+  if (split) {
+    const size_t n = spans.size();
+    py::array_t<uint8_t> rec({(py::ssize_t)n, (py::ssize_t)16});
+    py::array_t<int64_t> secs(n);
+    py::array_t<int32_t> us(n);
+    py::array_t<int32_t> tz({(py::ssize_t)n, (py::ssize_t)2});
+    std::vector<std::string> errs(n);
+    std::atomic<bool> bad{false};
+    std::string bad_msg;
+    std::mutex bad_mu;
+    {
+      auto R = rec.mutable_unchecked<2>();
+      auto S = secs.mutable_unchecked<1>();
+      auto U = us.mutable_unchecked<1>();
+      auto T = tz.mutable_unchecked<2>();
+      py::gil_scoped_release nogil;
+      parallel_chunks(n, 1024, 16, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi && !bad.load(std::memory_order_relaxed); ++i) {
+          EtaRecord r{};
+          Stamp st;
+          try {
+            rtj::Value v = rtj::Parser(b.data() + spans[i].first, spans[i].second - spans[i].first).parse();
+            errs[i] = pack_item(v, now, r, st);
+          } catch (const std::exception& e) {
+            std::lock_guard<std::mutex> lk(bad_mu);
+            if (!bad.exchange(true)) bad_msg = e.what();
+            return;
+          }
+          std::memcpy(&R(i, 0), &r, 16);
+          S(i) = st.secs;
+          U(i) = st.us;
+          T(i, 0) = st.has_tz ? 1 : 0;
+          T(i, 1) = st.tz_sec;
+        }
+      });
+    }
+    if (bad) throw std::runtime_error(bad_msg);
+    return py::make_tuple(rec, secs, us, tz, errs, true);
+  }
   rtj::Value root;
   {
     py::gil_scoped_release nogil;
@@ -59,25 +110,24 @@ py::tuple pack_predict_batch(py::bytes body, int64_t now_secs, int32_t now_us) {
   py::array_t<int32_t> us(n);
   py::array_t<int32_t> tz({(py::ssize_t)n, (py::ssize_t)2});
   std::vector<std::string> errs(n);
-  Stamp now;
-  now.secs = now_secs;
-  now.us = now_us;
   {
     auto R = rec.mutable_unchecked<2>();
     auto S = secs.mutable_unchecked<1>();
     auto U = us.mutable_unchecked<1>();
     auto T = tz.mutable_unchecked<2>();
     py::gil_scoped_release nogil;
-    for (size_t i = 0; i < n; ++i) {
-      EtaRecord r{};
-      Stamp st;
-      errs[i] = pack_item((*items)[i], now, r, st);
-      std::memcpy(&R(i, 0), &r, 16);
-      S(i) = st.secs;
-      U(i) = st.us;
-      T(i, 0) = st.has_tz ? 1 : 0;
-      T(i, 1) = st.tz_sec;
-    }
+    parallel_chunks(n, 2048, 16, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        EtaRecord r{};
+        Stamp st;
+        errs[i] = pack_item((*items)[i], now, r, st);
+        std::memcpy(&R(i, 0), &r, 16);
+        S(i) = st.secs;
+        U(i) = st.us;
+        T(i, 0) = st.has_tz ? 1 : 0;
+        T(i, 1) = st.tz_sec;
+      }
+    });
   }
   return py::make_tuple(rec, secs, us, tz, errs, is_batch);
 }
@@ -97,9 +147,28 @@ py::bytes format_predict_batch(py::array_t<float, py::array::c_style | py::array
     py::gil_scoped_release nogil;
     o.reserve(n * 96 + 32);
     if (is_batch) o += "{\"predictions\":[";
-    for (size_t i = 0; i < n; ++i) {
-      if (i) o += ',';
-      format_one(o, (double)M(i), S(i), U(i), T(i, 0) != 0, T(i, 1), errs[i]);
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = std::min<size_t>(std::min(hw, 16u), n / 2048);
+    if (nt <= 1) {
+      for (size_t i = 0; i < n; ++i) {
+        if (i) o += ',';
+        format_one(o, (double)M(i), S(i), U(i), T(i, 0) != 0, T(i, 1), errs[i]);
+      }
+    } else {
+      std::vector<std::string> parts(nt);
+      const size_t per = (n + nt - 1) / nt;
+      parallel_chunks(nt, 1, 16, [&](size_t klo, size_t khi) {
+        for (size_t k = klo; k < khi; ++k) {
+          std::string& part = parts[k];
+          const size_t lo = k * per, hi = std::min(n, lo + per);
+          part.reserve((hi - lo) * 96);
+          for (size_t i = lo; i < hi; ++i) {
+            if (i) part += ',';
+            format_one(part, (double)M(i), S(i), U(i), T(i, 0) != 0, T(i, 1), errs[i]);
+          }
+        }
+      });
+      for (auto& part : parts) o += part;
     }
     if (is_batch) o += "]}";
   }

@@ -12,6 +12,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <utility>
+#include <vector>
 
 #include "json_lite.h"
 
@@ -161,83 +164,99 @@ inline void append_2(std::string& o, int v) {
 }
 
 // datetime.isoformat() of (secs, us) [+ offset]
-inline std::string isoformat(int64_t secs, int64_t us, const Stamp& tz) {
+inline void append_isoformat(std::string& o, int64_t secs, int64_t us, const Stamp& tz) {
   int64_t days = secs >= 0 ? secs / 86400 : -((-secs + 86399) / 86400);
   int64_t sod = secs - days * 86400;
   int64_t y;
   unsigned m, d;
   civil_from_days(days, y, m, d);
-  std::string o;
-  o.reserve(40);
-  char yb[8];
-  std::snprintf(yb, sizeof yb, "%04lld", (long long)y);
-  o += yb;
-  o += '-';
-  append_2(o, (int)m);
-  o += '-';
-  append_2(o, (int)d);
-  o += 'T';
-  append_2(o, (int)(sod / 3600));
-  o += ':';
-  append_2(o, (int)(sod / 60 % 60));
-  o += ':';
-  append_2(o, (int)(sod % 60));
+  char b[48];
+  int k = 0;
+  if (y < 0 || y > 9999) {
+    k = std::snprintf(b, sizeof b, "%04lld", (long long)y);
+  } else {
+    b[k++] = (char)('0' + y / 1000);
+    b[k++] = (char)('0' + y / 100 % 10);
+    b[k++] = (char)('0' + y / 10 % 10);
+    b[k++] = (char)('0' + y % 10);
+  }
+  auto two = [&](int v) { b[k++] = (char)('0' + v / 10); b[k++] = (char)('0' + v % 10); };
+  b[k++] = '-'; two((int)m); b[k++] = '-'; two((int)d); b[k++] = 'T';
+  two((int)(sod / 3600)); b[k++] = ':'; two((int)(sod / 60 % 60)); b[k++] = ':'; two((int)(sod % 60));
   if (us) {
-    char ub[8];
-    std::snprintf(ub, sizeof ub, ".%06lld", (long long)us);
-    o += ub;
+    b[k++] = '.';
+    int64_t u = us;
+    for (int div = 100000; div; div /= 10) { b[k++] = (char)('0' + u / div % 10); }
   }
   if (tz.has_tz) {
     int off = tz.tz_sec;
-    o += off < 0 ? '-' : '+';
+    b[k++] = off < 0 ? '-' : '+';
     off = std::abs(off);
-    append_2(o, off / 3600);
-    o += ':';
-    append_2(o, off / 60 % 60);
-    if (off % 60) {
-      o += ':';
-      append_2(o, off % 60);
-    }
+    two(off / 3600); b[k++] = ':'; two(off / 60 % 60);
+    if (off % 60) { b[k++] = ':'; two(off % 60); }
   }
+  o.append(b, k);
+}
+
+// datetime.isoformat() of (secs, us) [+ offset]
+inline std::string isoformat(int64_t secs, int64_t us, const Stamp& tz) {
+  std::string o;
+  append_isoformat(o, secs, us, tz);
   return o;
 }
 
-// Python repr(float)
+// Python repr(float): shortest round-trip digits (to_chars), laid out with CPython's rule — fixed
+// notation when -4 <= exponent < 16, else d[.ddd]e[+-]XX.  Char buffers only (no allocation).
 inline void append_pyfloat(std::string& o, double v) {
   if (std::isnan(v)) { o += "NaN"; return; }
   if (std::isinf(v)) { o += v > 0 ? "Infinity" : "-Infinity"; return; }
   char buf[64];
-  auto r = std::to_chars(buf, buf + sizeof buf, v, std::chars_format::scientific);
-  std::string sci(buf, r.ptr);
-  // sci = [-]d[.ddd]e[+-]XX
-  size_t epos = sci.find('e');
-  int exp = std::stoi(sci.substr(epos + 1));
-  std::string mant = sci.substr(0, epos);
-  bool neg = mant[0] == '-';
-  if (neg) mant = mant.substr(1);
-  std::string digs;
-  for (char c : mant)
-    if (c != '.') digs += c;
-  std::string out;
+  const auto r = std::to_chars(buf, buf + sizeof buf, v, std::chars_format::scientific);
+  const char* p = buf;
+  const char* end = r.ptr;
+  const char* epos = p;
+  while (epos < end && *epos != 'e') ++epos;
+  int exp = 0;
+  std::from_chars(epos + 1 + (epos[1] == '+'), end, exp);
+  if (*p == '-') { o += '-'; ++p; }
+  char digs[32];
+  int nd = 0;
+  for (const char* q = p; q < epos; ++q)
+    if (*q != '.') digs[nd++] = *q;
+  char out[64];
+  int k = 0;
   if (exp >= -4 && exp < 16) {
     if (exp >= 0) {
-      if ((int)digs.size() <= exp + 1) {
-        out = digs + std::string(exp + 1 - digs.size(), '0') + ".0";
+      if (nd <= exp + 1) {
+        for (int i = 0; i < nd; ++i) out[k++] = digs[i];
+        for (int i = nd; i < exp + 1; ++i) out[k++] = '0';
+        out[k++] = '.';
+        out[k++] = '0';
       } else {
-        out = digs.substr(0, exp + 1) + "." + digs.substr(exp + 1);
+        for (int i = 0; i < exp + 1; ++i) out[k++] = digs[i];
+        out[k++] = '.';
+        for (int i = exp + 1; i < nd; ++i) out[k++] = digs[i];
       }
     } else {
-      out = "0." + std::string(-exp - 1, '0') + digs;
+      out[k++] = '0';
+      out[k++] = '.';
+      for (int i = 0; i < -exp - 1; ++i) out[k++] = '0';
+      for (int i = 0; i < nd; ++i) out[k++] = digs[i];
     }
   } else {
-    out = digs.substr(0, 1);
-    if (digs.size() > 1) out += "." + digs.substr(1);
-    char eb[16];
-    std::snprintf(eb, sizeof eb, "e%c%02d", exp < 0 ? '-' : '+', std::abs(exp));
-    out += eb;
+    out[k++] = digs[0];
+    if (nd > 1) {
+      out[k++] = '.';
+      for (int i = 1; i < nd; ++i) out[k++] = digs[i];
+    }
+    out[k++] = 'e';
+    out[k++] = exp < 0 ? '-' : '+';
+    const int ae = exp < 0 ? -exp : exp;
+    if (ae >= 100) out[k++] = (char)('0' + ae / 100);
+    out[k++] = (char)('0' + ae / 10 % 10);
+    out[k++] = (char)('0' + ae % 10);
   }
-  if (neg) o += '-';
-  o += out;
+  o.append(out, k);
 }
 
 inline bool num_of(const rtj::Value* v, double& out) {
@@ -339,8 +358,72 @@ inline void format_one(std::string& o, double m, int64_t secs, int32_t us, bool 
   o += "{\"eta_minutes_ml\":";
   append_pyfloat(o, m);
   o += ",\"eta_completion_time_ml\":\"";
-  o += isoformat(s, u, tzs);
+  append_isoformat(o, s, u, tzs);
   o += "\"}";
+}
+
+
+// Split a top-level JSON array into item spans with one string-aware pass (no DOM), so items can
+// be parsed in parallel.  Returns false on anything unusual; callers then run the full parser,
+// which produces the proper error.
+inline bool split_top_array(const char* s, size_t n, std::vector<std::pair<size_t, size_t>>& spans) {
+  size_t p = 0;
+  auto ws = [&]() { while (p < n && (s[p] == ' ' || s[p] == '\n' || s[p] == '\r' || s[p] == '\t')) ++p; };
+  ws();
+  if (p >= n || s[p] != '[') return false;
+  ++p;
+  ws();
+  if (p < n && s[p] == ']') {
+    ++p;
+    ws();
+    return p == n;
+  }
+  size_t start = p;
+  int depth = 0;
+  bool in_str = false;
+  for (; p < n; ++p) {
+    const char c = s[p];
+    if (in_str) {
+      if (c == '\\') ++p;
+      else if (c == '"') in_str = false;
+      continue;
+    }
+    if (c == '"') in_str = true;
+    else if (c == '{' || c == '[') ++depth;
+    else if (c == '}' || c == ']') {
+      if (depth == 0) {             // the closing bracket of the top-level array
+        if (c != ']') return false;
+        spans.emplace_back(start, p);
+        ++p;
+        ws();
+        return p == n;
+      }
+      --depth;
+    } else if (c == ',' && depth == 0) {
+      spans.emplace_back(start, p);
+      start = p + 1;
+    }
+  }
+  return false;
+}
+
+// Run fn(begin, end) over [0, n) on up to `max_threads` threads (serial below `min_per_thread`).
+template <class F>
+inline void parallel_chunks(size_t n, size_t min_per_thread, unsigned max_threads, F fn) {
+  unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  size_t t = std::min<size_t>({(size_t)std::min(hw, max_threads), n / std::max<size_t>(1, min_per_thread)});
+  if (t <= 1) {
+    fn((size_t)0, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  const size_t per = (n + t - 1) / t;
+  for (size_t k = 0; k < t; ++k) {
+    const size_t b = k * per, e = std::min(n, b + per);
+    if (b >= e) break;
+    pool.emplace_back([=, &fn]() { fn(b, e); });
+  }
+  for (auto& th : pool) th.join();
 }
 
 }  // namespace rtc

@@ -48,11 +48,29 @@ static void fuzz_json(std::mt19937_64& rng, int iters) {
       }
     }
     rtj::Value root;
+    bool full_ok = true;
     try {
       root = rtj::Parser(s.data(), s.size()).parse();
     } catch (...) {
-      continue;  // malformed JSON is rejected, never read out of bounds
+      full_ok = false;  // malformed JSON is rejected, never read out of bounds
     }
+    // the parallel item splitter must agree with the full parser whenever it accepts a body
+    std::vector<std::pair<size_t, size_t>> spans;
+    if (split_top_array(s.data(), s.size(), spans)) {
+      bool items_ok = true;
+      for (auto& sp : spans) {
+        try {
+          rtj::Parser(s.data() + sp.first, sp.second - sp.first).parse();
+        } catch (...) {
+          items_ok = false;
+        }
+      }
+      CHECK(items_ok == full_ok, "splitter/parser disagree on validity: %s", s.c_str());
+      if (items_ok && full_ok)
+        CHECK(root.kind == rtj::Value::Arr && root.arr.size() == spans.size(), "item count %zu vs %zu",
+              root.arr.size(), spans.size());
+    }
+    if (!full_ok) continue;
     std::vector<const rtj::Value*> items;
     if (root.kind == rtj::Value::Arr)
       for (auto& v : root.arr) items.push_back(&v);
