@@ -4,9 +4,11 @@ Reference: Flask-SSE publishes through Redis ``PUBLISH`` and streams with ``SUBS
 (``RO/Flaskr/__init__.py:8,25,28``, ``routes.py:86``); the simulator thread POSTs every tick back
 to its own ``/api/update_tracker`` over loopback HTTP with retries (``utils.py:206-251``).
 
-Here the broker is in-process (asyncio queues, thread-safe ``publish``), so a simulator tick is a
-direct publish — no loopback HTTP, no Redis needed.  A Redis broker is used instead when
-``ROUTEST_BROKER=redis`` and the ``redis`` module is importable (not in this image).
+Here the default broker is in-process (asyncio queues, thread-safe ``publish``), so a simulator
+tick is a direct publish — no loopback HTTP, no Redis needed.  With ``ROUTEST_BROKER=redis`` and
+``REDIS_URL`` set, :class:`RedisBroker` speaks Flask-SSE's Redis format through our own RESP client
+(``realtime/redis_resp.py``), so several server processes — or this service and a reference Flask
+deployment — share live-tracking channels.
 The wire format is Flask-SSE's: ``data:<json>\\n\\n`` (default ``message`` event), which the
 dashboard's ``EventSource.onmessage`` consumes (``FE/app/ui/page.jsx:598-650``).
 """
@@ -17,6 +19,7 @@ import datetime as dt
 import json
 import random
 import threading
+import time
 from typing import Any, Dict, List, Optional, Set, Tuple
 
 from ..utils.logging import get_logger
@@ -102,12 +105,84 @@ class MemoryBroker:
         return {"status": "ok", "latency_ms": 0, "kind": self.kind}
 
 
-def make_broker(kind: str, redis_url: Optional[str]):
-    if kind == "redis" and redis_url:
+class RedisBroker:
+    """Flask-SSE-compatible broker over Redis pub/sub: ``PUBLISH <channel> {"data":..,"type":..}``;
+    each SSE stream holds its own ``SUBSCRIBE`` connection (an asyncio task feeding a queue)."""
+
+    kind = "redis"
+
+    def __init__(self, url: str, max_queue: int = 1024, timeout: float = 2.0):
+        from .redis_resp import RespClient
+        self.url = url
+        self.client = RespClient(url, timeout=timeout)
+        self.max_queue = max_queue
+        self.published = 0
+        self._subs: Dict[int, Tuple[str, Any]] = {}
+        self._lock = threading.Lock()
+
+    def publish(self, data: Any, channel: str = "sse", type_: Optional[str] = None) -> int:
+        payload: Dict[str, Any] = {"data": data}
+        if type_:
+            payload["type"] = type_
         try:
-            import redis  # noqa: F401
-        except ImportError:
-            log.warning("redis module not available; using the in-process broker")
+            n = self.client.execute("PUBLISH", str(channel), json.dumps(payload))
+        except Exception as e:  # best effort, like the reference's publish path
+            log.warning("redis publish failed: %r", e)
+            return 0
+        self.published += 1
+        return int(n or 0)
+
+    def subscribe(self, channel: str) -> asyncio.Queue:
+        from .redis_resp import subscribe_stream
+        q: asyncio.Queue = asyncio.Queue()
+
+        def on_message(raw: bytes) -> None:
+            try:
+                d = json.loads(raw)
+                msg = sse_message(d.get("data"), d.get("type"), d.get("id"))
+            except (ValueError, AttributeError):
+                return
+            if q.qsize() < self.max_queue:
+                q.put_nowait(msg)
+
+        async def run():
+            try:
+                await subscribe_stream(self.url, str(channel), on_message)
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:
+                log.warning("redis subscribe(%s) ended: %r", channel, e)
+
+        task = asyncio.get_running_loop().create_task(run())
+        with self._lock:
+            self._subs[id(q)] = (str(channel), task)
+        return q
+
+    def unsubscribe(self, channel: str, q: asyncio.Queue) -> None:
+        with self._lock:
+            item = self._subs.pop(id(q), None)
+        if item is not None:
+            item[1].cancel()
+
+    def subscribers(self, channel: str) -> int:
+        with self._lock:
+            return sum(1 for ch, _ in self._subs.values() if ch == str(channel))
+
+    def ping(self) -> Dict[str, Any]:
+        t0 = time.time()
+        try:
+            ms = self.client.ping()
+            return {"status": "ok", "latency_ms": int(ms), "kind": self.kind}
+        except Exception as e:
+            return {"status": "error", "latency_ms": int((time.time() - t0) * 1000), "kind": self.kind,
+                    "error": str(e)[:200]}
+
+
+def make_broker(kind: str, redis_url: Optional[str]):
+    if kind == "redis":
+        if redis_url:
+            return RedisBroker(redis_url)
+        log.warning("ROUTEST_BROKER=redis without REDIS_URL; using the in-process broker")
     return MemoryBroker()
 
 
