@@ -460,6 +460,29 @@ void comm_collective(int64_t h, int64_t op, torch::Tensor in, torch::Tensor out,
                                  cur_stream(in), err) == 0, "RCCL collective: ", err);
 }
 
+// LDS-staged tree ensemble: nodes2 int32 [M,2] = (value bits, info), chunks int32 [C+1,2]
+torch::Tensor forest_predict_lds(torch::Tensor records, torch::Tensor nodes2, torch::Tensor roots,
+                                 torch::Tensor chunks, double base, bool le, std::vector<int64_t> fmap) {
+  for (auto* t : {&records, &nodes2, &roots, &chunks}) check_dev(*t, "forest tensor");
+  TORCH_CHECK(records.scalar_type() == torch::kInt32 && records.dim() == 2 && records.size(1) == 4,
+              "records must be int32 [B,4]");
+  TORCH_CHECK(nodes2.scalar_type() == torch::kInt32 && nodes2.dim() == 2 && nodes2.size(1) == 2, "nodes2 int32 [M,2]");
+  TORCH_CHECK(chunks.scalar_type() == torch::kInt32 && chunks.dim() == 2 && chunks.size(1) == 2 &&
+              chunks.size(0) >= 2, "chunks int32 [C+1,2]");
+  TORCH_CHECK(roots.scalar_type() == torch::kInt32, "roots int32");
+  TORCH_CHECK(fmap.size() == 12, "fmap must have 12 entries");
+  const c10::DeviceGuard guard(records.device());
+  const int B = (int)records.size(0);
+  auto out = torch::empty({B}, records.options().dtype(torch::kFloat32));
+  int fm[12];
+  for (int j = 0; j < 12; ++j) fm[j] = (int)fmap[j];
+  RT_CHECK_HIP(rt::launch_forest_lds(records.data_ptr(), nodes2.data_ptr(), roots.data_ptr<int>(),
+                                     chunks.data_ptr<int>(), (int)chunks.size(0) - 1, out.data_ptr<float>(), B,
+                                     (int)roots.numel(), (int)nodes2.size(0), (float)base, le ? 1 : 0, fm,
+                                     num_cus(records.device().index()), cur_stream(records)));
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -484,6 +507,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("route_score", &route_score, "K8: per-route delay-weighted length");
   m.def("astar", &astar, "K9: batched A* (one lane per query) with learned edge costs");
   m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
+  m.def("forest_predict_lds", &forest_predict_lds, "K4: LDS-staged tree chunks, 2 walks per thread");
   m.def("comm_unique_id", &comm_unique_id, "RCCL unique id (128 bytes) for comm_create");
   m.def("comm_create", &comm_create, "own RCCL communicator + one-shot IPC buffers");
   m.def("comm_ipc_handles", &comm_ipc_handles, "IPC handles of this rank's one-shot buffers");

@@ -58,6 +58,96 @@ __global__ __launch_bounds__(256) void forest_kernel(ForestArgs a) {
   a.out[row] = acc;
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-staged variant.  The ensemble is cut (on the host, at tree boundaries) into chunks of at
+// most FOREST_LDS_NODES nodes.  One 1024-thread workgroup per CU: for each chunk it stages the
+// chunk's nodes into LDS ONCE, then streams all of its row tiles through it (featurize the tile's
+// records into the per-thread LDS feature rows, walk the chunk's trees, add the partial sum into
+// the output row, which this workgroup owns for every chunk).  Each thread walks two trees at a time
+// so the two dependent LDS-load chains overlap.  LDS: 96 KB nodes + 52 KB features.
+constexpr int FOREST_LDS_NODES = 12288;
+constexpr int FOREST_TPB = 1024;
+
+__global__ __launch_bounds__(FOREST_TPB, 1) void forest_lds_kernel(ForestArgs a, const int* __restrict__ chunks,
+                                                                    int nchunks) {
+  __shared__ int2 nodes[FOREST_LDS_NODES];
+  __shared__ float xs[FOREST_TPB][13];
+  const int tid = threadIdx.x;
+  const int ntiles = (a.B + FOREST_TPB - 1) / FOREST_TPB;
+  for (int c = 0; c < nchunks; ++c) {
+    const int t0 = chunks[2 * c], n0 = chunks[2 * c + 1];
+    const int t1 = chunks[2 * c + 2], n1 = chunks[2 * c + 3];
+    __syncthreads();                           // previous chunk fully consumed
+    const int2* src = reinterpret_cast<const int2*>(a.values);   // (value, info) interleaved
+    for (int i = tid; i < n1 - n0; i += FOREST_TPB) nodes[i] = src[n0 + i];
+    __syncthreads();
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+      const int row = tile * FOREST_TPB + tid;
+      const bool live = row < a.B;
+      if (live) {
+        float raw[12];
+        featurize_raw12(a.rec[row], raw);
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+          float v = raw[0];
+#pragma unroll
+          for (int q = 1; q < 12; ++q) v = (a.fmap[j] == q) ? raw[q] : v;
+          xs[tid][j] = v;
+        }
+      }
+      float acc = 0.f;
+      if (live) {
+        int t = t0;
+        for (; t + 1 < t1; t += 2) {           // two independent walks in flight
+          const int r0 = a.roots[t] - n0, r1 = a.roots[t + 1] - n0;
+          int m0 = r0, m1 = r1;
+          int2 d0 = nodes[m0], d1 = nodes[m1];
+          int guard = 0;
+          while ((d0.y >= 0 || d1.y >= 0) && guard++ < 64) {   // bit 31 set (negative) = leaf
+            if (d0.y >= 0) {
+              const unsigned inf = (unsigned)d0.y;
+              const unsigned f = (inf >> 24) & 63;
+              const float v = xs[tid][f < 12 ? f : 0];
+              const float thr = __int_as_float(d0.x);
+              const bool left = (v != v) ? ((inf >> 30) & 1) : (a.le ? (v <= thr) : (v < thr));
+              m0 = r0 + (int)(inf & 0xFFFFFFu) + (left ? 0 : 1);
+              d0 = nodes[m0 < n1 - n0 ? m0 : r0];
+            }
+            if (d1.y >= 0) {
+              const unsigned inf = (unsigned)d1.y;
+              const unsigned f = (inf >> 24) & 63;
+              const float v = xs[tid][f < 12 ? f : 0];
+              const float thr = __int_as_float(d1.x);
+              const bool left = (v != v) ? ((inf >> 30) & 1) : (a.le ? (v <= thr) : (v < thr));
+              m1 = r1 + (int)(inf & 0xFFFFFFu) + (left ? 0 : 1);
+              d1 = nodes[m1 < n1 - n0 ? m1 : r1];
+            }
+          }
+          acc += __int_as_float(d0.x);
+          acc += __int_as_float(d1.x);
+        }
+        if (t < t1) {
+          const int r0 = a.roots[t] - n0;
+          int m0 = r0;
+          int2 d0 = nodes[m0];
+          int guard = 0;
+          while (d0.y >= 0 && guard++ < 64) {
+            const unsigned inf = (unsigned)d0.y;
+            const unsigned f = (inf >> 24) & 63;
+              const float v = xs[tid][f < 12 ? f : 0];
+            const float thr = __int_as_float(d0.x);
+            const bool left = (v != v) ? ((inf >> 30) & 1) : (a.le ? (v <= thr) : (v < thr));
+            m0 = r0 + (int)(inf & 0xFFFFFFu) + (left ? 0 : 1);
+            d0 = nodes[m0 < n1 - n0 ? m0 : r0];
+          }
+          acc += __int_as_float(d0.x);
+        }
+        a.out[row] = (c == 0 ? a.base : a.out[row]) + acc;
+      }
+    }
+  }
+}
+
 hipError_t launch_forest(const void* rec, const float* values, const unsigned* info, const int* roots,
                          float* out, int B, int T, int M, float base, int le, const int* fmap,
                          hipStream_t stream) {
@@ -65,6 +155,19 @@ hipError_t launch_forest(const void* rec, const float* values, const unsigned* i
   ForestArgs a{(const int4*)rec, values, info, roots, out, B, T, M, base, le, {}};
   for (int j = 0; j < 12; ++j) a.fmap[j] = fmap[j];
   hipLaunchKernelGGL(forest_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+// nodes2: [M] int2 (value bits, info) interleaved; chunks: [nchunks+1][2] (first tree, first node)
+hipError_t launch_forest_lds(const void* rec, const void* nodes2, const int* roots, const int* chunks,
+                             int nchunks, float* out, int B, int T, int M, float base, int le,
+                             const int* fmap, int num_cus, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  ForestArgs a{(const int4*)rec, (const float*)nodes2, nullptr, roots, out, B, T, M, base, le, {}};
+  for (int j = 0; j < 12; ++j) a.fmap[j] = fmap[j];
+  const int ntiles = (B + FOREST_TPB - 1) / FOREST_TPB;
+  const int grid = ntiles < num_cus ? ntiles : num_cus;
+  hipLaunchKernelGGL(forest_lds_kernel, dim3(grid), dim3(FOREST_TPB), 0, stream, a, chunks, nchunks);
   return hipGetLastError();
 }
 

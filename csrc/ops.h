@@ -66,6 +66,10 @@ hipError_t launch_forest(const void* rec, const float* values, const unsigned* i
                          float* out, int B, int T, int M, float base, int le, const int* fmap,
                          hipStream_t stream);
 
+hipError_t launch_forest_lds(const void* rec, const void* nodes2, const int* roots, const int* chunks,
+                             int nchunks, float* out, int B, int T, int M, float base, int le,
+                             const int* fmap, int num_cus, hipStream_t stream);
+
 // ---- batched routing (K5 distance matrix + K6 greedy CVRP) : route_kernels.hip ----
 hipError_t launch_haversine_matrix(const double* lat, const double* lon, const int* npts, int R,
                                    int NM, double circuity, double* D, hipStream_t stream);

@@ -188,6 +188,29 @@ class ForestModel:
         return (torch.from_numpy(self.values).to(d), torch.from_numpy(self.info.view(np.int32)).to(d),
                 torch.from_numpy(self.roots).to(d))
 
+    LDS_NODES = 12288      # csrc/forest.hip FOREST_LDS_NODES (96 KB of 8-byte nodes per chunk)
+
+    def chunk_table(self, cap: int = LDS_NODES) -> Optional[np.ndarray]:
+        """Greedy cut of the tree list into chunks of <= cap nodes at tree boundaries:
+        int32 [C+1, 2] of (first tree, first node).  None if one tree alone exceeds cap."""
+        ends = np.append(self.roots[1:], len(self.values)).astype(np.int64)
+        sizes = ends - self.roots
+        if len(sizes) == 0 or sizes.max() > cap:
+            return None
+        rows = [(0, 0)]
+        cur = 0
+        for t, sz in enumerate(sizes):
+            if cur + sz > cap:
+                rows.append((t, int(self.roots[t])))
+                cur = 0
+            cur += int(sz)
+        rows.append((len(sizes), len(self.values)))
+        return np.asarray(rows, dtype=np.int32)
+
+    def nodes2(self) -> np.ndarray:
+        """(value bits, info) interleaved int32 [M, 2] for the LDS kernel's 8-byte node loads."""
+        return np.stack([self.values.view(np.int32), self.info.view(np.int32)], axis=1).copy()
+
     def predict(self, df: Any) -> np.ndarray:
         from .features import dataframe_to_features
         x = dataframe_to_features(df) if hasattr(df, "columns") else np.asarray(df, dtype=np.float32)

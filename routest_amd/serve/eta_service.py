@@ -56,13 +56,19 @@ def _cpu_runner(model: Any):
 class ForestKernel:
     """Tree ensemble resident on one GPU (K4: fused featurize + traversal, csrc/forest.hip)."""
 
-    def __init__(self, model, device):
+    def __init__(self, model, device, lds: bool = True):
         from ..ops import _ext
         self.C = _ext.native(required=True)
         self.m = model
         self.values, self.info, self.roots = model.device_arrays(device)
+        tab = model.chunk_table() if lds else None
+        self.chunks = torch.from_numpy(tab).to(device) if tab is not None else None
+        self.nodes2 = torch.from_numpy(model.nodes2()).to(device) if tab is not None else None
 
     def __call__(self, rec: torch.Tensor) -> torch.Tensor:
+        if self.chunks is not None:   # whole trees fit the LDS chunk: staged kernel
+            return self.C.forest_predict_lds(rec, self.nodes2, self.roots, self.chunks, self.m.base_score,
+                                             self.m.le, list(self.m.feature_map))
         return self.C.forest_predict(rec, self.values, self.info, self.roots, self.m.base_score, self.m.le,
                                      list(self.m.feature_map))
 

@@ -54,15 +54,33 @@ def test_xgboost_feature_name_reorder(hgb):
 
 
 @pytest.mark.gpu
-def test_forest_kernel_vs_cpu(hgb):
+@pytest.mark.parametrize("lds", [False, True])
+@pytest.mark.parametrize("fmt", ["xgb", "sklearn"])
+def test_forest_kernel_vs_cpu(hgb, lds, fmt):
     from routest_amd.ops.eta_mlp import records_to_tensor
     from routest_amd.serve.eta_service import ForestKernel
-    m = ForestModel.from_xgboost_json(ForestModel.from_sklearn_hgb(hgb).to_xgboost_json())
-    rec, _ = synth_records(100_000, 4)
-    k = ForestKernel(m, "cuda:0")
+    m = ForestModel.from_sklearn_hgb(hgb)
+    if fmt == "xgb":
+        m = ForestModel.from_xgboost_json(m.to_xgboost_json())
+    rec, _ = synth_records(100_003, 4)
+    k = ForestKernel(m, "cuda:0", lds=lds)
+    assert (k.chunks is not None) == lds
     got = k(records_to_tensor(rec).cuda()).cpu().numpy()
     ref = m.predict_features(records_to_features(rec))
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-4)
+
+
+def test_chunk_table():
+    rng = np.random.default_rng(0)
+    sizes = rng.integers(1, 300, size=200) * 2 - 1          # odd node counts (full binary trees)
+    roots = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int32)
+    M = int(sizes.sum())
+    m = ForestModel(np.zeros(M, np.float32), np.full(M, 1 << 31, np.uint32), roots, 0.0, True)
+    tab = m.chunk_table(cap=1000)
+    assert tab[0].tolist() == [0, 0] and tab[-1].tolist() == [200, M]
+    for (t0, n0), (t1, n1) in zip(tab[:-1], tab[1:]):
+        assert n1 - n0 <= 1000 and roots[t0] == n0 and t1 > t0
+    assert m.chunk_table(cap=10) is None
 
 
 def test_service_serves_forest_on_cpu(hgb):
