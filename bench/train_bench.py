@@ -36,6 +36,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--modes", default="fused,graph,hipblaslt,autograd")
+    ap.add_argument("--trace", default="", help="write a Chrome trace of 3 extra steps per mode (prefix)")
     ap.add_argument("--comm", default="torch", choices=["torch", "rccl", "oneshot", "auto"],
                     help="gradient all-reduce for the fused modes: ProcessGroup, or native (csrc/comm.hip)")
     a = ap.parse_args()
@@ -108,6 +109,11 @@ def main() -> None:
         barrier(dev)
         torch.cuda.synchronize()
         el = allreduce_scalars([time.perf_counter() - t0], dev, op="max")[0]
+        if a.trace and di.is_main:           # outside the timed region
+            from routest_amd.utils.profiling import chrome_trace
+            with chrome_trace(f"{a.trace}_{mode}.json"):
+                for _ in range(3):
+                    step()
         results[mode] = {"ms_per_step": el / a.steps * 1e3,
                          "samples_per_s": B * di.world * a.steps / el}
     if di.is_main:

@@ -71,6 +71,8 @@ def cmd_synth(a: argparse.Namespace) -> None:
 
 
 def main(argv=None) -> None:
+    from .utils.profiling import apply_debug_env
+    apply_debug_env()          # ROUTEST_DEBUG_SYNC=1: serialised kernels, synchronous launch errors
     ap = argparse.ArgumentParser(prog="routest_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
     s = sub.add_parser("serve", help="run the HTTP API (uvicorn)")

@@ -103,7 +103,24 @@ class Registry:
         for m in (self.requests, self.preds, self.latency, self.batch, self.queue_wait, self.gpu_time,
                   self.device_failures, self.slow_batches):
             lines.extend(m.render())
+        lines.extend(_device_gauges())
         return "\n".join(lines) + "\n"
+
+
+def _device_gauges() -> List[str]:
+    """HBM used/total per visible GPU (gauges; empty without a GPU)."""
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return []
+        out = ["# HELP routest_gpu_hbm_bytes HBM per device", "# TYPE routest_gpu_hbm_bytes gauge"]
+        for i in range(torch.cuda.device_count()):
+            free, total = torch.cuda.mem_get_info(i)
+            out.append(f'routest_gpu_hbm_bytes{{device="{i}",kind="used"}} {total - free}')
+            out.append(f'routest_gpu_hbm_bytes{{device="{i}",kind="total"}} {total}')
+        return out
+    except Exception:  # pragma: no cover - metrics must never fail a scrape
+        return []
 
 
 REGISTRY = Registry()

@@ -164,3 +164,27 @@ def test_wgrad_reduce_exact_and_deterministic(S, n, stride):
     ref = slab.double().sum(0)[:n].float()
     torch.testing.assert_close(G1.cpu(), ref, rtol=1e-5, atol=1e-4)
     assert torch.equal(G1, G2)
+
+
+def test_fused_training_bitwise_deterministic():
+    """Two trainers from the same init on the same batches end bit-identical (fixed-order slab
+    reduction, no atomics in the gradient path) — SURVEY §5.2 determinism check."""
+    from routest_amd.data.synth import synth_records, synth_trips
+    from routest_amd.models.mlp3 import EtaMLP
+    from routest_amd.ops.eta_mlp import records_to_tensor
+    from routest_amd.train.fused import FusedMlp3Trainer
+    xs, ys = synth_trips(20000, 0)
+    rec, y = synth_records(16384, 5)
+    rt = records_to_tensor(rec).to(DEV)
+    Ps = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        m = EtaMLP(256)
+        m.fit_normalization(xs, ys)
+        tr = FusedMlp3Trainer(m, DEV, 16384, 16384, lr=1e-3, allreduce=False)
+        yn = tr.normalize_targets(torch.from_numpy(y).to(DEV))
+        for _ in range(4):
+            tr.step(rt, yn)
+        torch.cuda.synchronize()
+        Ps.append(tr.P.clone())
+    assert torch.equal(Ps[0], Ps[1])
