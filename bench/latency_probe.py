@@ -94,6 +94,37 @@ def main() -> None:
                 out.append(time.perf_counter() - t0)
         return out
     res["asgi_get_ping_us"] = med(asyncio.run(aping()))
+
+    # real HTTP/1.1 over loopback: uvicorn in a background thread of this process, http.client
+    import http.client
+    import socket
+    import threading
+    import uvicorn
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    server = uvicorn.Server(uvicorn.Config(app, host="127.0.0.1", port=port, log_level="warning",
+                                           access_log=False, lifespan="off"))
+    th = threading.Thread(target=server.run, daemon=True)
+    th.start()
+    while not server.started:
+        time.sleep(0.01)
+    conn = http.client.HTTPConnection("127.0.0.1", port)
+    raw = json.dumps(body).encode()
+    hdr = {"Content-Type": "application/json"}
+    out = []
+    for j in range(N + 200):
+        t0 = time.perf_counter()
+        conn.request("POST", "/api/predict_eta", body=raw, headers=hdr)
+        r = conn.getresponse()
+        r.read()
+        if j >= 200:
+            out.append(time.perf_counter() - t0)
+    res["http_loopback_inproc_server_us"] = med(out)
+    res["http_loopback_p99_us"] = sorted(out)[int(len(out) * 0.99)] * 1e6
+    server.should_exit = True
+    th.join(timeout=10)
     svc.close()
     print(json.dumps({"metric": "single-request latency breakdown (median us)", **res}), flush=True)
 

@@ -242,8 +242,18 @@ void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor
 
 // slab: f32 [S, stride]; the partial of k-slice s is written at slab[s, offset + m*ldo + n].
 void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N, torch::Tensor slab,
-           int64_t offset, int64_t ldo) {
+           int64_t offset, int64_t ldo, c10::optional<torch::Tensor> mask) {
   check_dev(A, "A");
+  const void* mptr = nullptr;
+  int ldm = 0;
+  if (mask.has_value() && mask->defined()) {
+    check_dev(*mask, "mask");
+    TORCH_CHECK(mask->scalar_type() == torch::kBFloat16 && mask->dim() == 2 && mask->size(0) == A.size(0) &&
+                    mask->size(1) >= M && mask->size(1) % 8 == 0, "mask must be bf16 [K, >=M] (ld % 8 == 0)");
+    TORCH_CHECK((N + 31) / 32 == 1, "masked wgrad supports N <= 32");
+    mptr = mask->data_ptr();
+    ldm = (int)mask->size(1);
+  }
   check_dev(Bm, "Bm");
   check_dev(slab, "slab");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && Bm.scalar_type() == torch::kBFloat16, "bf16 A/Bm");
@@ -259,7 +269,7 @@ void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N
   RT_CHECK_HIP(rt::launch_wgrad(A.data_ptr(), (int)A.size(1), (int)M, (int)Mout, Bm.data_ptr(),
                                 (int)Bm.size(1), (int)N, (int)A.size(0), (int)slab.size(0),
                                 slab.data_ptr<float>() + offset, (int)ldo, (long long)slab.size(1),
-                                cur_stream(A)));
+                                cur_stream(A), mptr, ldm));
 }
 
 void wgrad_reduce(torch::Tensor slab, torch::Tensor G) {
@@ -499,7 +509,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + MFMA fragment re-pack");
   m.def("mlp3_num_params", [](int64_t H) { return (int64_t)rt::mlp3_num_params((int)H); });
   m.def("mlp3_grad_bucket_floats", [](int64_t H) { return (int64_t)rt::mlp3_grad_bucket_floats((int)H); });
-  m.def("wgrad", &wgrad, "split-K weight-gradient GEMM (K = batch) into fp32 slabs");
+  m.def("wgrad", &wgrad, "split-K weight-gradient GEMM (K = batch) into fp32 slabs",
+        py::arg("A"), py::arg("M"), py::arg("Mout"), py::arg("Bm"), py::arg("N"), py::arg("slab"),
+        py::arg("offset"), py::arg("ldo"), py::arg("mask") = py::none());
   m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs");
   m.def("num_cus", [](int64_t dev) { return (int64_t)num_cus((int)dev); });
   m.def("gcn_agg_gemm", &gcn_agg_gemm, "K8: fused CSR aggregation + MFMA GEMM + bias/ReLU");

@@ -49,12 +49,22 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* base, int stride, int k0
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int NT>
+// keep each bf16 of `a` whose counterpart in `m` is > 0 (relu'(h) from the saved activation)
+__device__ __forceinline__ int relu_mask_word(int a, int m) {
+  const int lo = ((short)(m & 0xFFFF) > 0) ? 0x0000FFFF : 0;
+  const int hi = ((short)((unsigned)m >> 16) > 0) ? (int)0xFFFF0000u : 0;
+  return a & (lo | hi);
+}
+
+// MASK: A_eff = A * (mask > 0) applied while staging (mask has A's shape, leading dim ldm) — fuses
+// the ReLU backward of the first layer into dW1 = dz1^T x, so dz1 is never materialised.
+template <int NT, bool MASK>
 __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict__ A, int lda, int M,
                                                        int Mout, const __bf16* __restrict__ Bm,
                                                        int ldb, int N, int K, int kslice,
                                                        float* __restrict__ slab, int ldo,
-                                                       long long slab_stride) {
+                                                       long long slab_stride,
+                                                       const __bf16* __restrict__ mask, int ldm) {
   constexpr int KB = 32, AW = 256, BW = 32 * NT;
   constexpr int ACH = AW / 8, BCH = BW / 8;           // 16-B chunks per staged row
   constexpr int TPB = 512;
@@ -85,6 +95,15 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
       const int k = kb + r, m = m_base + ch * 8;
       ra[u] = (c < KB * ACH && k < k_end && m < M)
                   ? *reinterpret_cast<const int4*>(A + (size_t)k * lda + m) : make_int4(0, 0, 0, 0);
+      if constexpr (MASK) {
+        if (c < KB * ACH && k < k_end && m < M) {
+          const int4 mk = *reinterpret_cast<const int4*>(mask + (size_t)k * ldm + m);
+          ra[u].x = relu_mask_word(ra[u].x, mk.x);
+          ra[u].y = relu_mask_word(ra[u].y, mk.y);
+          ra[u].z = relu_mask_word(ra[u].z, mk.z);
+          ra[u].w = relu_mask_word(ra[u].w, mk.w);
+        }
+      }
     }
 #pragma unroll
     for (int u = 0; u < BPT; ++u) {
@@ -214,24 +233,28 @@ size_t wgrad_lds_bytes(int NT) {
   return (size_t)32 * pad(256) + (size_t)32 * pad(32 * NT);
 }
 
-template <int NT>
+template <int NT, bool MASK = false>
 static hipError_t launch_wgrad_nt(const void* A, int lda, int M, int Mout, const void* Bm, int ldb,
                                   int N, int K, int S, float* slab, int ldo, long long slab_stride,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, const void* mask = nullptr, int ldm = 0) {
   const int kslice = ((K + S - 1) / S + 31) / 32 * 32;
   const int mblocks = (M + 255) / 256;
   const size_t lds = wgrad_lds_bytes(NT);
-  hipLaunchKernelGGL(wgrad_kernel<NT>, dim3(S, mblocks), dim3(512), lds, stream,
+  hipLaunchKernelGGL((wgrad_kernel<NT, MASK>), dim3(S, mblocks), dim3(512), lds, stream,
                      (const __bf16*)A, lda, M, Mout, (const __bf16*)Bm, ldb, N, K, kslice, slab, ldo,
-                     slab_stride);
+                     slab_stride, (const __bf16*)mask, ldm);
   return hipGetLastError();
 }
 
 hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm, int ldb, int N,
                         int K, int S, float* slab, int ldo, long long slab_stride,
-                        hipStream_t stream) {
+                        hipStream_t stream, const void* mask, int ldm) {
   if (M % 8 || N % 8 || lda % 8 || ldb % 8) return hipErrorInvalidValue;
   const int NT = (N + 31) / 32;
+  if (mask != nullptr) {
+    if (ldm % 8 || NT != 1) return hipErrorInvalidValue;   // the dW1 shape (N = 16)
+    return launch_wgrad_nt<1, true>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm);
+  }
   switch (NT) {
     case 1: return launch_wgrad_nt<1>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream);
     case 2: return launch_wgrad_nt<2>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream);

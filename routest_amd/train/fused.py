@@ -4,10 +4,10 @@ Per step (all on the current HIP stream, no host synchronisation, HIP-graph capt
 
   eta_mlp3_train_fwd (HIP)  : featurize + 3 layers + MSE grad; writes xf, h1a, h2a, dz2, dy
   dh1 = dz2 @ W2            : hipBLASLt (bf16, fp32 accumulate)
-  relu_bwd (HIP)            : dz1 = dh1 * (h1 > 0)
   G[W2|b2] = dz2^T [h1|1]   : split-K wgrad HIP kernel (K = batch) -> fp32 slabs laid out like
   G[w3|b3] = dy^T  [h2|1]     the flat bucket, then ONE deterministic slab reduction into G
-  G[W1k|b1] = dz1^T [xf]    (xf slot 14 == 1)
+  G[W1k|b1] = dz1^T [xf]    with dz1 = dh1 * (h1 > 0) applied inside the wgrad kernel's A staging
+                            (ReLU backward fused: dz1 is never written; xf slot 14 == 1)
   all_reduce(G)             : ONE RCCL collective (SUM; dy was pre-scaled by 2/global_batch)
   adamw_pack (HIP)          : AdamW on fp32 master params + re-pack of the bf16 MFMA blob
 
@@ -118,7 +118,7 @@ class FusedMlp3Trainer:
         self.slab = torch.empty(self.S, self.G.numel(), dtype=torch.float32, device=d)
         self.use_hipblaslt_wgrad = False
         self.dh1 = torch.empty(B, H, dtype=bf, device=d)
-        self.dz1 = torch.empty(B, H, dtype=bf, device=d)
+        self.dz1 = None                # only the hipBLASLt A/B path materialises dz1
         self.loss_tiles = torch.zeros((B + 31) // 32, dtype=torch.float32, device=d)
         self._pack(update=False)
 
@@ -138,8 +138,10 @@ class FusedMlp3Trainer:
                              self.xf, self.h1a, self.h2a, self.dz2, self.dyb, self.loss_tiles,
                              self.step_ctr)
         torch.mm(self.dz2, self.w2bf, out=self.dh1)
-        C.relu_bwd(self.dh1, self.h1a, self.dz1)
         if self.use_hipblaslt_wgrad:  # library baseline, kept for A/B measurements
+            if self.dz1 is None:
+                self.dz1 = torch.empty_like(self.dh1)
+            C.relu_bwd(self.dh1, self.h1a, self.dz1)
             _mm_f32(self.dz2.t(), self.h1a, self.gW2a)
             _mm_f32(self.dyb[:, :1].t(), self.h2a, self.gW3a)
             _mm_f32(self.dz1.t(), self.xf, self.gW1a)
@@ -147,7 +149,8 @@ class FusedMlp3Trainer:
         ldg = H + 16
         C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab, 0, ldg)
         C.wgrad(self.dyb, 8, 1, self.h2a, ldg, self.slab, H * ldg, ldg)
-        C.wgrad(self.dz1, H, H, self.xf, 16, self.slab, H * ldg + ldg, 16)
+        # dW1 = (dh1 * relu'(h1))^T x: the ReLU backward is applied while staging (no dz1 tensor)
+        C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, H * ldg + ldg, 16, self.h1a)
         C.wgrad_reduce(self.slab, self.G)
 
     def step(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> torch.Tensor:

@@ -188,3 +188,22 @@ def test_fused_training_bitwise_deterministic():
         torch.cuda.synchronize()
         Ps.append(tr.P.clone())
     assert torch.equal(Ps[0], Ps[1])
+
+
+@pytest.mark.parametrize("K,S", [(65536, 256), (1000, 7), (40, 1)])
+def test_wgrad_masked_relu_backward(K, S):
+    """dW1 path: wgrad(dh1, x, mask=h1a) == ((dh1 * (h1 > 0))^T x) in fp32."""
+    from routest_amd.ops import _ext
+    C = _ext.native()
+    g = torch.Generator().manual_seed(K)
+    H = 256
+    dh1 = torch.randn(K, H, generator=g).to(torch.bfloat16)
+    h1a = torch.randn(K, H + 16, generator=g).to(torch.bfloat16)
+    h1a[:, :H][torch.rand(K, H, generator=g) < 0.1] = 0.0          # exact zeros are masked too
+    x = torch.randn(K, 16, generator=g).to(torch.bfloat16)
+    ref = ((dh1.float() * (h1a[:, :H].float() > 0)).t() @ x.float())
+    slab = torch.zeros(S, H * 16, device=DEV)
+    C.wgrad(dh1.to(DEV), H, H, x.to(DEV), 16, slab, 0, 16, h1a.to(DEV))
+    G = torch.zeros(H * 16, device=DEV)
+    C.wgrad_reduce(slab, G)
+    torch.testing.assert_close(G.view(H, 16).cpu(), ref, rtol=1e-4, atol=1e-3 * (K ** 0.5))
