@@ -216,7 +216,10 @@ hipError_t launch_astar(const int* indptr, const int* indices, const float* cost
   AstarArgs a{indptr, indices, cost, lat, lon, src, dst, g, parent,
               (unsigned long long*)heap, touched, out_cost, out_len, out_status, out_path,
               N, Q, q0, cap, max_path, max_iters, inv_vmax, lm, K};
-  const dim3 grid((n + 255) / 256), block(256);
+  // one wavefront per workgroup: with length-sorted queries each wave is homogeneous, and the
+  // dispatcher's round-robin placement spreads short and long waves over all CUs (256-lane
+  // workgroups would pile the longest searches onto a few CUs and leave a serial tail)
+  const dim3 grid((n + 63) / 64), block(64);
   if (lm == nullptr) hipLaunchKernelGGL(astar_kernel<0>, grid, block, 0, stream, a);
   else if (K == 8) hipLaunchKernelGGL(astar_kernel<8>, grid, block, 0, stream, a);
   else hipLaunchKernelGGL(astar_kernel<16>, grid, block, 0, stream, a);

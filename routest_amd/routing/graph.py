@@ -153,11 +153,23 @@ class BatchedAstar:
         if self.lm is not None:
             self.lm.copy_(torch.from_numpy(landmark_tables(self.g, cost, self.lm.shape[1] // 2)))
 
-    def run(self, src: Sequence[int], dst: Sequence[int]):
-        """Returns (cost_s [Q] tensor, path_len [Q], status [Q], paths [Q, max_path]) on device."""
+    def run(self, src: Sequence[int], dst: Sequence[int], sort: bool = False):
+        """Returns (cost_s [Q] tensor, path_len [Q], status [Q], paths [Q, max_path]) on device.
+
+        ``sort``: launch queries in order of straight-line length so the 64 searches of a wavefront
+        have similar sizes, results scattered back to the caller's order.  Measured neutral on the
+        config-5 bench (826 vs 811 ms/step: the searches are bound by dependent heap/state loads,
+        not by wave divergence), so it is off by default."""
         d = self.dev
-        s = torch.as_tensor(np.asarray(src, dtype=np.int32)).to(d)
-        t = torch.as_tensor(np.asarray(dst, dtype=np.int32)).to(d)
+        src = np.asarray(src, dtype=np.int32)
+        dst = np.asarray(dst, dtype=np.int32)
+        order = None
+        if sort and len(src) > 64:
+            g = self.g
+            order = np.argsort(haversine_m(g.lat[src], g.lon[src], g.lat[dst], g.lon[dst]), kind="stable")
+            src, dst = src[order], dst[order]
+        s = torch.as_tensor(src).to(d)
+        t = torch.as_tensor(dst).to(d)
         Q = s.numel()
         out_cost = torch.empty(Q, dtype=torch.float32, device=d)
         out_len = torch.empty(Q, dtype=torch.int32, device=d)
@@ -167,6 +179,14 @@ class BatchedAstar:
             self.C.astar(self.indptr, self.indices, self.cost, self.lat, self.lon, s, t, self.gbuf,
                          self.parent, self.heap, self.touched, out_cost, out_len, out_status, out_path,
                          q0, self.max_iters, self.inv_vmax, self.lm)
+        if order is not None:
+            idx = torch.from_numpy(order.astype(np.int64)).to(d)
+            res = []
+            for x in (out_cost, out_len, out_status, out_path):
+                y = torch.empty_like(x)
+                y[idx] = x
+                res.append(y)
+            return tuple(res)
         return out_cost, out_len, out_status, out_path
 
     def paths(self, src, dst) -> List[Tuple[float, List[int]]]:
