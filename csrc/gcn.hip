@@ -34,7 +34,11 @@ __global__ __launch_bounds__(256) void gcn_agg_gemm_kernel(
   __bf16* tile = s_t[w];
   const int n_rows = row1 - row0;
   const int ntiles = (n_rows + 31) / 32;
-  for (int t = blockIdx.x * 4 + w; t < ntiles; t += gridDim.x * 4) {
+  // XCD-aware placement: workgroup b runs on XCD b % 8, so give each XCD one contiguous range of
+  // node tiles (gridDim.x is a multiple of 8).  Neighbour rows of a road graph are nearby ids, so a
+  // node's feature row is then re-read from the same XCD's L2 instead of from all eight.
+  const int lb = (int)(blockIdx.x % 8u) * (int)(gridDim.x / 8u) + (int)(blockIdx.x / 8u);
+  for (int t = lb * 4 + w; t < ntiles; t += gridDim.x * 4) {
     const int base = row0 + t * 32;
 #pragma unroll
     for (int pass = 0; pass < 32 / RPP; ++pass) {
@@ -157,6 +161,7 @@ hipError_t launch_gcn_agg_gemm(const void* X, const int* indptr, const int* indi
   if (ntiles <= 0) return hipSuccess;
   int grid = (ntiles + 3) / 4;
   if (grid > num_cus * 4) grid = num_cus * 4;
+  grid = (grid + 7) / 8 * 8;   // XCD remap in the kernel needs a multiple of 8 (extra WGs idle)
 #define RT_GCN(FI, FO, AG, RL)                                                                   \
   if (fin == FI && fout == FO && agg == AG && relu == RL) {                                      \
     hipLaunchKernelGGL((gcn_agg_gemm_kernel<FI, FO, AG, RL>), dim3(grid), dim3(256), 0, stream,  \
