@@ -406,6 +406,27 @@ torch::Tensor forest_predict(torch::Tensor records, torch::Tensor values, torch:
   return out;
 }
 
+// ---------------------------------------------------------------- native predict server
+int64_t native_server_start(int64_t port, int64_t threads, torch::Tensor blob, int64_t H, std::vector<double> norm,
+                            int64_t variant, int64_t max_batch, std::vector<std::string> cors, bool cors_vercel,
+                            bool bind_any) {
+  check_dev(blob, "blob");
+  TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
+  TORCH_CHECK(norm.size() == 8, "norm must hold 4 scales + 4 shifts");
+  TORCH_CHECK(max_batch >= 1 && max_batch <= (1 << 24), "max_batch out of range");
+  rt::NormParams np;
+  for (int i = 0; i < 4; ++i) {
+    np.scale[i] = (float)norm[i];
+    np.shift[i] = (float)norm[4 + i];
+  }
+  std::string err;
+  const int dev = blob.device().index();
+  const int64_t h = rt::native_server_start((int)port, (int)threads, dev, blob.data_ptr(), (int)H, np, (int)variant,
+                                            num_cus(dev), (int)max_batch, cors, cors_vercel, bind_any, err);
+  TORCH_CHECK(h >= 0, "native server: ", err);
+  return h;
+}
+
 // ---------------------------------------------------------------- native collectives (comm.hip)
 py::bytes comm_unique_id() {
   char id[128];
@@ -520,6 +541,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("astar", &astar, "K9: batched A* (one lane per query) with learned edge costs");
   m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
   m.def("forest_predict_lds", &forest_predict_lds, "K4: LDS-staged tree chunks, 2 walks per thread");
+  m.def("native_server_start", &native_server_start, "native HTTP front end for /api/predict_eta and /predict");
+  m.def("native_server_stop", [](int64_t h) {
+    py::gil_scoped_release nogil;
+    rt::native_server_stop(h);
+  });
+  m.def("native_server_stats", [](int64_t h) {
+    long long v[4];
+    rt::native_server_stats(h, v);
+    return std::vector<int64_t>{v[0], v[1], v[2], v[3]};
+  });
   m.def("comm_unique_id", &comm_unique_id, "RCCL unique id (128 bytes) for comm_create");
   m.def("comm_create", &comm_create, "own RCCL communicator + one-shot IPC buffers");
   m.def("comm_ipc_handles", &comm_ipc_handles, "IPC handles of this rank's one-shot buffers");

@@ -1,0 +1,567 @@
+// Native prediction front end: HTTP/1.1 server for POST /api/predict_eta and POST /predict with
+// no Python on the request path (SURVEY §7.5 hard part 2: "p50 is dominated by the host stack";
+// the reference serves this route through Flask, RO/Flaskr/routes.py:365-383).
+//
+// Design (one process, MI355X-first):
+//  * R reactor threads, each with its own SO_REUSEPORT listening socket (the kernel spreads
+//    connections), its own epoll set, HIP stream and pinned (mapped) record/output buffers.
+//  * Natural batching: every epoll wake-up parses ALL complete requests that arrived on all ready
+//    connections (native JSON -> 16-byte EtaRecords, csrc/runtime/rt_core.h — the same code as the
+//    batched /predict path), then issues ONE zero-copy launch of the fused featurize+MLP kernel
+//    (K1+K2 read the records from pinned host memory and write minutes back over PCIe), one
+//    stream sync, and formats every response with the CPython-exact formatter.  An idle server
+//    answers a lone request after one launch; under load, batches grow with concurrency.
+//  * Semantics follow the FastAPI handlers (api/app.py): non-JSON content type or malformed JSON
+//    on /api/predict_eta reads as {} (Flask get_json(silent=True)); a JSON array (or {"items": []})
+//    on /predict is a batch answered as {"predictions": [...]}; per-item errors -> 400 for single
+//    requests, {"error": ...} entries in batches.  GET /api/ping is answered natively; everything
+//    else is 404 (the full API stays on the uvicorn port).
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <sys/time.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+#include "ops.h"
+#include "runtime/rt_core.h"
+
+namespace rt {
+
+namespace {
+
+using rtc::EtaRecord;
+using rtc::Stamp;
+
+struct ServerCfg {
+  int port = 0, threads = 1, device = 0, H = 256, variant = -1, num_cus = 256;
+  const void* blob = nullptr;
+  NormParams np{};
+  int max_batch = 1 << 20;
+  std::vector<std::string> cors_exact;
+  bool cors_vercel = true;
+};
+
+struct Conn {
+  int fd = -1;
+  std::string in, out;
+  size_t out_off = 0;
+  bool close_after = false;
+  int npending = 0;      // requests of this connection waiting for the batch launch
+};
+
+// One parsed prediction request waiting for the batch launch.
+struct Pending {
+  int fd;
+  size_t first = 0, count = 0;         // record range in this round's batch
+  std::vector<Stamp> stamps;
+  std::vector<std::string> errs;
+  bool batch = false, keep_alive = true;
+  std::string origin;
+};
+
+struct Stats {
+  std::atomic<long long> requests{0}, predictions{0}, launches{0}, errors{0};
+};
+
+inline Stamp now_local() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  struct tm lt;
+  time_t t = ts.tv_sec;
+  localtime_r(&t, &lt);
+  Stamp s;
+  s.secs = rtc::days_from_civil(lt.tm_year + 1900, (unsigned)lt.tm_mon + 1, (unsigned)lt.tm_mday) * 86400 +
+           lt.tm_hour * 3600 + lt.tm_min * 60 + lt.tm_sec;
+  s.us = (int32_t)(ts.tv_nsec / 1000);
+  return s;
+}
+
+inline bool ieq(const char* a, size_t n, const char* b) {
+  if (std::strlen(b) != n) return false;
+  for (size_t i = 0; i < n; ++i)
+    if (std::tolower((unsigned char)a[i]) != std::tolower((unsigned char)b[i])) return false;
+  return true;
+}
+
+class Reactor {
+ public:
+  Reactor(const ServerCfg& cfg, Stats& st, std::atomic<bool>& stop) : cfg_(cfg), st_(st), stop_(stop) {}
+
+  bool init(std::string& err) {
+    lfd_ = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+    int one = 1;
+    setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    setsockopt(lfd_, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)cfg_.port);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (bind_any_) a.sin_addr.s_addr = htonl(INADDR_ANY);
+    if (bind(lfd_, (sockaddr*)&a, sizeof a) != 0 || listen(lfd_, 1024) != 0) {
+      err = std::string("bind/listen: ") + std::strerror(errno);
+      return false;
+    }
+    ep_ = epoll_create1(0);
+    wake_ = eventfd(0, EFD_NONBLOCK);
+    add(lfd_);
+    add(wake_);
+    return true;
+  }
+
+  void set_bind_any(bool v) { bind_any_ = v; }
+  int wake_fd() const { return wake_; }
+
+  void run() {
+    if (hipSetDevice(cfg_.device) != hipSuccess) return;
+    if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return;
+    cap_ = cfg_.max_batch;
+    if (hipHostMalloc((void**)&h_rec_, (size_t)cap_ * 16, hipHostMallocMapped) != hipSuccess ||
+        hipHostMalloc((void**)&h_out_, (size_t)cap_ * 4, hipHostMallocMapped) != hipSuccess)
+      return;
+    if (hipHostGetDevicePointer(&d_rec_, h_rec_, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&d_out_, h_out_, 0) != hipSuccess)
+      return;
+    epoll_event evs[256];
+    while (!stop_.load(std::memory_order_relaxed)) {
+      const int n = epoll_wait(ep_, evs, 256, 100);
+      for (int i = 0; i < n; ++i) {
+        const int fd = evs[i].data.fd;
+        if (fd == lfd_) { accept_all(); continue; }
+        if (fd == wake_) { uint64_t v; (void)!read(wake_, &v, 8); continue; }
+        auto it = conns_.find(fd);
+        if (it == conns_.end()) continue;
+        if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) on_readable(it->second);
+        if (evs[i].events & EPOLLOUT) flush(it->second);
+      }
+      run_batch();
+      for (int fd : to_close_) close_conn(fd);
+      to_close_.clear();
+    }
+    for (auto& kv : conns_) close(kv.first);
+    conns_.clear();
+    close(lfd_);
+    close(ep_);
+    close(wake_);
+    (void)hipHostFree(h_rec_);
+    (void)hipHostFree(h_out_);
+    (void)hipStreamDestroy(stream_);
+  }
+
+ private:
+  const ServerCfg& cfg_;
+  Stats& st_;
+  std::atomic<bool>& stop_;
+  bool bind_any_ = false;
+  int lfd_ = -1, ep_ = -1, wake_ = -1;
+  hipStream_t stream_{};
+  EtaRecord* h_rec_ = nullptr;
+  float* h_out_ = nullptr;
+  void* d_rec_ = nullptr;
+  float* d_out_ = nullptr;
+  int cap_ = 0;
+  size_t nrec_ = 0;
+  std::unordered_map<int, Conn> conns_;
+  std::vector<Pending> pending_;
+  std::vector<int> to_close_;
+
+  void add(int fd, uint32_t ev = EPOLLIN) {
+    epoll_event e{};
+    e.events = ev;
+    e.data.fd = fd;
+    epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &e);
+  }
+
+  void accept_all() {
+    while (true) {
+      const int fd = accept4(lfd_, nullptr, nullptr, SOCK_NONBLOCK);
+      if (fd < 0) return;
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      Conn c;
+      c.fd = fd;
+      conns_.emplace(fd, std::move(c));
+      add(fd);
+    }
+  }
+
+  void close_conn(int fd) {
+    if (conns_.erase(fd)) {
+      epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+      close(fd);
+    }
+  }
+
+  void on_readable(Conn& c) {
+    char buf[65536];
+    while (true) {
+      const ssize_t r = read(c.fd, buf, sizeof buf);
+      if (r > 0) {
+        c.in.append(buf, (size_t)r);
+        if (c.in.size() > (256u << 20)) { to_close_.push_back(c.fd); return; }
+        continue;
+      }
+      if (r == 0) { to_close_.push_back(c.fd); break; }
+      if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+      to_close_.push_back(c.fd);
+      return;
+    }
+    parse_requests(c);
+    if (c.out.size() > c.out_off) flush(c);   // immediate answers (errors, ping, 100-continue)
+  }
+
+  // Parse every complete request buffered on c (pipelining allowed).
+  void parse_requests(Conn& c) {
+    while (true) {
+      const size_t hend = c.in.find("\r\n\r\n");
+      if (hend == std::string::npos) {
+        if (c.in.size() > 65536) { respond(c, 431, "{\"error\":\"headers too large\"}", "", true); }
+        return;
+      }
+      const char* p = c.in.data();
+      const size_t sp1 = c.in.find(' ');
+      const size_t sp2 = sp1 == std::string::npos ? sp1 : c.in.find(' ', sp1 + 1);
+      const size_t eol = c.in.find("\r\n");
+      if (sp1 == std::string::npos || sp2 == std::string::npos || sp2 > eol) {
+        respond(c, 400, "{\"error\":\"bad request line\"}", "", true);
+        c.in.clear();
+        return;
+      }
+      const std::string method(p, sp1);
+      std::string path(p + sp1 + 1, sp2 - sp1 - 1);
+      const size_t qm = path.find('?');
+      if (qm != std::string::npos) path.resize(qm);
+      const bool http10 = c.in.compare(sp2 + 1, 8, "HTTP/1.0") == 0;
+      size_t clen = 0;
+      bool json = false, keep = !http10, expect100 = false, chunked = false;
+      std::string origin;
+      size_t ls = eol + 2;
+      while (ls < hend) {
+        const size_t le = c.in.find("\r\n", ls);
+        const size_t colon = c.in.find(':', ls);
+        if (colon != std::string::npos && colon < le) {
+          const char* k = p + ls;
+          const size_t kn = colon - ls;
+          size_t vs = colon + 1;
+          while (vs < le && (p[vs] == ' ' || p[vs] == '\t')) ++vs;
+          const std::string v(p + vs, le - vs);
+          if (ieq(k, kn, "content-length")) clen = (size_t)std::strtoull(v.c_str(), nullptr, 10);
+          else if (ieq(k, kn, "content-type")) {
+            std::string lv = v;
+            for (auto& ch : lv) ch = (char)std::tolower((unsigned char)ch);
+            json = lv.find("json") != std::string::npos;
+          } else if (ieq(k, kn, "connection")) {
+            std::string lv = v;
+            for (auto& ch : lv) ch = (char)std::tolower((unsigned char)ch);
+            if (lv.find("close") != std::string::npos) keep = false;
+            if (lv.find("keep-alive") != std::string::npos) keep = true;
+          } else if (ieq(k, kn, "expect")) {
+            expect100 = v.size() >= 3 && v.compare(0, 3, "100") == 0;
+          } else if (ieq(k, kn, "transfer-encoding")) {
+            chunked = true;
+          } else if (ieq(k, kn, "origin")) {
+            origin = v;
+          }
+        }
+        ls = le + 2;
+      }
+      if (chunked) {
+        respond(c, 411, "{\"error\":\"chunked bodies are not supported; send Content-Length\"}", origin, true);
+        c.in.clear();
+        return;
+      }
+      if (clen > (256u << 20)) {
+        respond(c, 413, "{\"error\":\"body too large\"}", origin, true);
+        c.in.clear();
+        return;
+      }
+      if (c.in.size() < hend + 4 + clen) {
+        if (expect100 && c.in.size() == hend + 4) {
+          if (c.npending > 0) run_batch();
+          c.out += "HTTP/1.1 100 Continue\r\n\r\n";
+          flush(c);
+        }
+        return;   // body not complete yet
+      }
+      std::string body = c.in.substr(hend + 4, clen);
+      c.in.erase(0, hend + 4 + clen);
+      st_.requests.fetch_add(1, std::memory_order_relaxed);
+      handle(c, method, path, body, json, keep, origin);
+      if (c.close_after) return;
+    }
+  }
+
+  bool cors_ok(const std::string& o) const {
+    if (o.empty()) return false;
+    for (const auto& e : cfg_.cors_exact)
+      if (e == o) return true;
+    const std::string suf = ".vercel.app";
+    return cfg_.cors_vercel && o.compare(0, 8, "https://") == 0 && o.size() > suf.size() + 8 &&
+           o.compare(o.size() - suf.size(), suf.size(), suf) == 0;
+  }
+
+  void respond(Conn& c, int code, const std::string& body, const std::string& origin, bool close_after) {
+    if (c.npending > 0) run_batch();   // HTTP/1.1 pipelining: answers leave in request order
+    const char* reason = code == 200 ? "OK" : code == 400 ? "Bad Request" : code == 404 ? "Not Found"
+                         : code == 405 ? "Method Not Allowed" : code == 411 ? "Length Required"
+                         : code == 413 ? "Payload Too Large" : code == 431 ? "Request Header Fields Too Large"
+                         : code == 503 ? "Service Unavailable" : "Error";
+    char head[256];
+    const int hn = std::snprintf(head, sizeof head,
+                                 "HTTP/1.1 %d %s\r\ncontent-type: application/json\r\ncontent-length: %zu\r\n",
+                                 code, reason, body.size());
+    c.out.append(head, (size_t)hn);
+    if (cors_ok(origin)) {
+      c.out += "access-control-allow-origin: ";
+      c.out += origin;
+      c.out += "\r\naccess-control-allow-credentials: true\r\nvary: Origin\r\n";
+    }
+    if (close_after) c.out += "connection: close\r\n";
+    c.out += "\r\n";
+    c.out += body;
+    if (close_after) c.close_after = true;
+    if (code >= 400) st_.errors.fetch_add(1, std::memory_order_relaxed);
+  }
+
+  void handle(Conn& c, const std::string& method, const std::string& path, const std::string& body,
+              bool json, bool keep, const std::string& origin) {
+    if (method == "OPTIONS") {
+      if (c.npending > 0) run_batch();
+      std::string h = "HTTP/1.1 200 OK\r\ncontent-length: 0\r\naccess-control-allow-methods: GET, POST, OPTIONS\r\n"
+                      "access-control-allow-headers: *\r\n";
+      if (cors_ok(origin)) h += "access-control-allow-origin: " + origin + "\r\naccess-control-allow-credentials: true\r\n";
+      c.out += h + "\r\n";
+      return;
+    }
+    if (path == "/api/ping" && method == "GET") {
+      respond(c, 200, "{\"ok\":true,\"service\":\"route-optimizer\"}", origin, !keep);
+      return;
+    }
+    const bool is_pe = path == "/api/predict_eta", is_p = path == "/predict";
+    if (!is_pe && !is_p) {
+      respond(c, 404, "{\"detail\":\"Not Found\"}", origin, !keep);
+      return;
+    }
+    if (method != "POST") {
+      respond(c, 405, "{\"detail\":\"Method Not Allowed\"}", origin, !keep);
+      return;
+    }
+    // body -> items
+    rtj::Value root;
+    bool parsed = false;
+    std::string perr;
+    if (json) {
+      try {
+        root = rtj::Parser(body.data(), body.size()).parse();
+        parsed = true;
+      } catch (const std::exception& e) {
+        perr = e.what();
+      }
+    }
+    Pending pd;
+    pd.fd = c.fd;
+    pd.keep_alive = keep;
+    pd.origin = origin;
+    std::vector<const rtj::Value*> items;
+    rtj::Value empty;
+    empty.kind = rtj::Value::Obj;
+    if (is_p && parsed && root.kind == rtj::Value::Arr) {
+      pd.batch = true;
+      for (const auto& v : root.arr) items.push_back(&v);
+    } else if (is_p && parsed && root.kind == rtj::Value::Obj && root.get("items") &&
+               root.get("items")->kind == rtj::Value::Arr) {
+      pd.batch = true;
+      for (const auto& v : root.get("items")->arr) items.push_back(&v);
+    } else if (is_p && json && !parsed && body.find_first_not_of(" \t\r\n") != std::string::npos &&
+               body[body.find_first_not_of(" \t\r\n")] == '[') {
+      std::string o = "{\"error\":\"";
+      for (char ch : perr) { if (ch == '"' || ch == '\\') o += '\\'; if ((unsigned char)ch >= 0x20) o += ch; }
+      respond(c, 400, o + "\"}", origin, !keep);
+      return;
+    } else {
+      items.push_back(parsed && root.kind == rtj::Value::Obj ? &root : &empty);   // silent -> {}
+    }
+    if (nrec_ + items.size() > (size_t)cap_) run_batch();   // flush before overflowing the buffer
+    if (items.size() > (size_t)cap_) {
+      respond(c, 413, "{\"error\":\"batch larger than the server's max_batch\"}", origin, !keep);
+      return;
+    }
+    const Stamp now = now_local();
+    pd.first = nrec_;
+    pd.count = items.size();
+    pd.stamps.resize(items.size());
+    pd.errs.resize(items.size());
+    for (size_t i = 0; i < items.size(); ++i) {
+      EtaRecord r{};
+      pd.errs[i] = rtc::pack_item(*items[i], now, r, pd.stamps[i]);
+      h_rec_[nrec_ + i] = r;
+    }
+    nrec_ += items.size();
+    if (!pd.batch && !pd.errs[0].empty()) {   // single request with bad input: answer now
+      nrec_ -= items.size();
+      std::string o = "{\"error\":\"invalid input: ";
+      for (char ch : pd.errs[0]) { if (ch == '"' || ch == '\\') o += '\\'; if ((unsigned char)ch >= 0x20) o += ch; }
+      respond(c, 400, o + "\"}", origin, !keep);
+      return;
+    }
+    ++c.npending;
+    pending_.push_back(std::move(pd));
+  }
+
+  void run_batch() {
+    if (pending_.empty()) return;
+    if (nrec_ > 0) {
+      hipError_t e = launch_eta_mlp3_fwd(d_rec_, d_out_, (int)nrec_, cfg_.blob, cfg_.H, cfg_.np,
+                                         cfg_.variant, cfg_.num_cus, stream_, false);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream_);
+      st_.launches.fetch_add(1, std::memory_order_relaxed);
+      if (e != hipSuccess) {
+        std::vector<Pending> failed;
+        failed.swap(pending_);
+        nrec_ = 0;
+        for (auto& pd : failed) {
+          auto it = conns_.find(pd.fd);
+          if (it == conns_.end()) continue;
+          --it->second.npending;
+          respond(it->second, 503, "{\"error\":\"model unavailable\"}", pd.origin, !pd.keep_alive);
+          flush(it->second);
+        }
+        return;
+      }
+    }
+    std::vector<Pending> done;
+    done.swap(pending_);                 // respond() below may re-enter run_batch: keep it empty
+    nrec_ = 0;                           // h_out_ stays valid until the next launch
+    for (auto& pd : done) {
+      auto it = conns_.find(pd.fd);
+      if (it == conns_.end()) continue;
+      --it->second.npending;
+      std::string o;
+      o.reserve(pd.count * 96 + 32);
+      long long ok = 0;
+      if (pd.batch) o += "{\"predictions\":[";
+      for (size_t i = 0; i < pd.count; ++i) {
+        if (i) o += ',';
+        rtc::format_one(o, (double)h_out_[pd.first + i], pd.stamps[i].secs, pd.stamps[i].us,
+                        pd.stamps[i].has_tz, pd.stamps[i].tz_sec, pd.errs[i]);
+        ok += pd.errs[i].empty();
+      }
+      if (pd.batch) o += "]}";
+      st_.predictions.fetch_add(ok, std::memory_order_relaxed);
+      respond(it->second, 200, o, pd.origin, !pd.keep_alive);
+      flush(it->second);
+    }
+  }
+
+  void flush(Conn& c) {
+    while (c.out_off < c.out.size()) {
+      const ssize_t w = write(c.fd, c.out.data() + c.out_off, c.out.size() - c.out_off);
+      if (w > 0) { c.out_off += (size_t)w; continue; }
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        epoll_event e{};
+        e.events = EPOLLIN | EPOLLOUT;
+        e.data.fd = c.fd;
+        epoll_ctl(ep_, EPOLL_CTL_MOD, c.fd, &e);
+        return;
+      }
+      to_close_.push_back(c.fd);
+      return;
+    }
+    c.out.clear();
+    c.out_off = 0;
+    epoll_event e{};
+    e.events = EPOLLIN;
+    e.data.fd = c.fd;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, c.fd, &e);
+    if (c.close_after) to_close_.push_back(c.fd);
+  }
+};
+
+struct Server {
+  ServerCfg cfg;
+  Stats stats;
+  std::atomic<bool> stop{false};
+  std::vector<std::unique_ptr<Reactor>> reactors;
+  std::vector<std::thread> threads;
+};
+
+std::mutex g_srv_mu;
+std::vector<Server*> g_servers;
+
+}  // namespace
+
+int64_t native_server_start(int port, int threads, int device, const void* blob, int H, const NormParams& np,
+                            int variant, int num_cus, int max_batch, const std::vector<std::string>& cors,
+                            bool cors_vercel, bool bind_any, std::string& err) {
+  auto* s = new Server();
+  s->cfg.port = port;
+  s->cfg.threads = threads < 1 ? 1 : threads;
+  s->cfg.device = device;
+  s->cfg.blob = blob;
+  s->cfg.H = H;
+  s->cfg.np = np;
+  s->cfg.variant = variant;
+  s->cfg.num_cus = num_cus;
+  s->cfg.max_batch = max_batch;
+  s->cfg.cors_exact = cors;
+  s->cfg.cors_vercel = cors_vercel;
+  for (int i = 0; i < s->cfg.threads; ++i) {
+    auto r = std::make_unique<Reactor>(s->cfg, s->stats, s->stop);
+    r->set_bind_any(bind_any);
+    if (!r->init(err)) {
+      delete s;
+      return -1;
+    }
+    s->reactors.push_back(std::move(r));
+  }
+  for (auto& r : s->reactors) s->threads.emplace_back([rp = r.get()]() { rp->run(); });
+  std::lock_guard<std::mutex> lk(g_srv_mu);
+  g_servers.push_back(s);
+  return (int64_t)g_servers.size() - 1;
+}
+
+void native_server_stop(int64_t h) {
+  Server* s = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_srv_mu);
+    if (h < 0 || h >= (int64_t)g_servers.size()) return;
+    s = g_servers[h];
+    g_servers[h] = nullptr;
+  }
+  if (!s) return;
+  s->stop.store(true);
+  for (auto& r : s->reactors) {
+    uint64_t one = 1;
+    (void)!write(r->wake_fd(), &one, 8);
+  }
+  for (auto& t : s->threads) t.join();
+  delete s;
+}
+
+void native_server_stats(int64_t h, long long out[4]) {
+  std::lock_guard<std::mutex> lk(g_srv_mu);
+  out[0] = out[1] = out[2] = out[3] = 0;
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return;
+  Server* s = g_servers[h];
+  out[0] = s->stats.requests.load();
+  out[1] = s->stats.predictions.load();
+  out[2] = s->stats.launches.load();
+  out[3] = s->stats.errors.load();
+}
+
+}  // namespace rt

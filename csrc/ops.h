@@ -77,6 +77,13 @@ hipError_t launch_greedy_cvrp(const double* D, const int* npts, const double* de
                               const double* cap, const double* maxd, int R, int NM, int* visit,
                               int* trip_of, int* ntrips, int* status, hipStream_t stream);
 
+// ---- native prediction front end : native_server.hip ----
+int64_t native_server_start(int port, int threads, int device, const void* blob, int H, const NormParams& np,
+                            int variant, int num_cus, int max_batch, const std::vector<std::string>& cors,
+                            bool cors_vercel, bool bind_any, std::string& err);
+void native_server_stop(int64_t h);
+void native_server_stats(int64_t h, long long out[4]);
+
 // ---- native collectives (rccl_ops) : comm.hip ----
 int comm_unique_id(char out[128]);
 int64_t comm_create(const char* uid, int rank, int world, int device, size_t oneshot_bytes, bool use_rccl,

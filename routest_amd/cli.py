@@ -36,8 +36,21 @@ def cmd_serve(a: argparse.Namespace) -> None:
         eta = EtaService(model_path=a.model, device=s.device, devices=s.devices, batch_max=s.batch_max,
                          timeout_us=s.batch_timeout_us, allow_pickle=os.environ.get("ROUTEST_ALLOW_PICKLE") == "1")
     app = create_app(build_services(s, eta=eta))
+    native_srv = None
+    if a.native_port and eta is not None and eta.backend == "hip":
+        from .models.mlp3 import EtaMLP
+        if isinstance(eta.model, EtaMLP):
+            from .serve.native_server import NativePredictServer
+            native_srv = NativePredictServer(eta.model, device=eta.devices[0].index, port=a.native_port,
+                                             threads=a.native_threads, cors_origins=s.cors_origins,
+                                             bind_any=a.host not in ("127.0.0.1", "localhost"))
+            print(json.dumps({"native_predict_port": native_srv.port}), flush=True)
     import uvicorn
-    uvicorn.run(app, host=a.host, port=a.port or s.port, log_level="warning", access_log=False)
+    try:
+        uvicorn.run(app, host=a.host, port=a.port or s.port, log_level="warning", access_log=False)
+    finally:
+        if native_srv is not None:
+            native_srv.close()
 
 
 def cmd_train(a: argparse.Namespace, rest) -> None:
@@ -85,6 +98,9 @@ def main(argv=None) -> None:
     s.add_argument("--provider", default="")
     s.add_argument("--store", default="")
     s.add_argument("--env-file", default=".env")
+    s.add_argument("--native-port", type=int, default=0,
+                   help="also serve /api/predict_eta and /predict from the native C++ front end on this port")
+    s.add_argument("--native-threads", type=int, default=2)
     t = sub.add_parser("train", help="train the ETA model (use torchrun for multi-GPU)")
     b = sub.add_parser("bench", help="run a benchmark")
     b.add_argument("what", choices=["serve", "train", "gcn", "route", "rccl", "http", "kernel"])

@@ -1,0 +1,59 @@
+"""Native HTTP front end for the prediction endpoints (``csrc/native_server.hip``).
+
+``POST /api/predict_eta`` and ``POST /predict`` are answered by C++ reactor threads — native JSON
+packing, one zero-copy fused-kernel launch per wake-up (natural batching across connections),
+CPython-exact response formatting — with no Python on the request path.  It runs next to the
+FastAPI app (which keeps every other endpoint) on its own port::
+
+    python -m routest_amd serve --synthetic-model --port 5000 --native-port 5001
+
+The reference answers this route through Flask (``RO/Flaskr/routes.py:365-383``); this front end
+exists because single-request latency is host-stack bound.
+"""
+from __future__ import annotations
+
+import socket
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ..ops._ext import native
+from ..ops.eta_mlp import EtaMlpKernel
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class NativePredictServer:
+    def __init__(self, model, device: int = 0, port: int = 0, threads: int = 2, max_batch: int = 1 << 18,
+                 cors_origins: Sequence[str] = ("http://localhost:3000", "http://127.0.0.1:3000"),
+                 cors_vercel: bool = True, bind_any: bool = False, variant: int = -1):
+        self.C = native(required=True)
+        self.kern = EtaMlpKernel(model, torch.device("cuda", device), variant=variant)   # owns the blob
+        self.port = port or free_port()
+        self.h: Optional[int] = self.C.native_server_start(
+            self.port, threads, self.kern.packed.blob, self.kern.hidden, list(self.kern.packed.norm),
+            variant, max_batch, list(cors_origins), cors_vercel, bind_any)
+
+    def stats(self) -> Dict[str, int]:
+        if self.h is None:
+            return {}
+        r, p, l, e = self.C.native_server_stats(self.h)
+        return {"requests": r, "predictions": p, "launches": l, "errors": e}
+
+    def close(self) -> None:
+        if self.h is not None:
+            self.C.native_server_stop(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False

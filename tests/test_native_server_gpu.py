@@ -1,0 +1,136 @@
+"""Native prediction front end (csrc/native_server.hip) vs the FastAPI app: same model, same
+requests -> byte-identical success bodies; protocol behaviour (keep-alive, pipelining,
+100-continue, CORS, errors, concurrency) over real sockets."""
+import http.client
+import json
+import socket
+import threading
+
+import pytest
+import torch
+from fastapi.testclient import TestClient
+
+pytestmark = pytest.mark.gpu
+
+BODY = {"summary": {"distance": 12345}, "pickup_time": "2025-08-25T08:30:00", "driver_age": 34,
+        "weather": "Sunny", "traffic": "Medium"}
+
+
+@pytest.fixture(scope="module")
+def stack():
+    from routest_amd.api.app import build_services, create_app
+    from routest_amd.config import load_settings
+    from routest_amd.serve.eta_service import EtaService, default_model
+    from routest_amd.serve.native_server import NativePredictServer
+    model = default_model(steps=30)
+    srv = NativePredictServer(model, device=0, threads=2)
+    s = load_settings(env={}, dotenv_path=None, devices=[0])
+    client = TestClient(create_app(build_services(s, eta=EtaService(model, devices=[0]), store=None)))
+    yield srv, client
+    srv.close()
+
+
+def _post(port, path, body, headers=None, conn=None):
+    c = conn or http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+    raw = body if isinstance(body, bytes) else json.dumps(body).encode()
+    c.request("POST", path, body=raw, headers=headers or {"Content-Type": "application/json"})
+    r = c.getresponse()
+    return r.status, r.read(), dict(r.getheaders())
+
+
+@pytest.mark.parametrize("path", ["/api/predict_eta", "/predict"])
+def test_single_matches_fastapi(stack, path):
+    srv, client = stack
+    for b in [BODY, {"summary": {"distance": 800}, "pickup_time": "2024-02-29T23:59:59.5+05:30", "traffic": "Jam"},
+              {"summary": {"distance": "2500"}, "pickup_time": "2025-01-01T00:00:00Z", "weather": "Hail"}]:
+        st, body, _ = _post(srv.port, path, b)
+        ref = client.post(path, json=b)
+        assert st == ref.status_code == 200
+        assert body == ref.content
+
+
+def test_batch_matches_fastapi(stack):
+    srv, client = stack
+    items = [{"summary": {"distance": 1000 + 37 * i}, "pickup_time": "2025-08-25T08:30:00",
+              "traffic": ["High", "Low", "Jam", "Medium", "x"][i % 5]} for i in range(3000)]
+    items[5] = {"summary": {"distance": "abc"}}
+    st, body, _ = _post(srv.port, "/predict", items)
+    ref = client.post("/predict", json=items)
+    assert st == ref.status_code == 200
+    assert body == ref.content
+
+
+def test_errors_and_routes(stack):
+    srv, _ = stack
+    st, body, _ = _post(srv.port, "/api/predict_eta", {"summary": {"distance": "abc"}})
+    assert st == 400 and json.loads(body)["error"].startswith("invalid input")
+    st, body, _ = _post(srv.port, "/predict", b"[1, 2", {"Content-Type": "application/json"})
+    assert st == 400 and "invalid JSON" in json.loads(body)["error"]
+    st, body, _ = _post(srv.port, "/api/predict_eta", b"hello", {"Content-Type": "text/plain"})
+    assert st == 200 and "eta_minutes_ml" in json.loads(body)        # silent -> {}
+    st, body, _ = _post(srv.port, "/nope", BODY)
+    assert st == 404
+    c = http.client.HTTPConnection("127.0.0.1", srv.port, timeout=10)
+    c.request("GET", "/api/ping")
+    r = c.getresponse()
+    assert r.status == 200 and json.loads(r.read()) == {"ok": True, "service": "route-optimizer"}
+
+
+def test_keepalive_pipelining_and_100_continue(stack):
+    srv, _ = stack
+    raw = json.dumps(BODY).encode()
+    req = (b"POST /api/predict_eta HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+           b"Content-Length: %d\r\n\r\n%s" % (len(raw), raw))
+    bad = b"GET /nope HTTP/1.1\r\nHost: x\r\n\r\n"
+    s = socket.create_connection(("127.0.0.1", srv.port), timeout=10)
+    s.sendall(req + bad + req)                   # pipelined: answers must come back in order
+    buf = b""
+    while buf.count(b"HTTP/1.1 ") < 3 or not buf.endswith(b"}"):
+        chunk = s.recv(65536)
+        assert chunk
+        buf += chunk
+    import re
+    codes = [int(m) for m in re.findall(rb"HTTP/1\.1 (\d{3}) ", buf)]
+    assert codes == [200, 404, 200]
+    # Expect: 100-continue, body sent after the interim response
+    s.sendall(b"POST /api/predict_eta HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+              b"Expect: 100-continue\r\nContent-Length: %d\r\n\r\n" % len(raw))
+    interim = s.recv(65536)
+    assert interim.startswith(b"HTTP/1.1 100 Continue")
+    s.sendall(raw)
+    final = s.recv(65536)
+    assert final.startswith(b"HTTP/1.1 200")
+    s.close()
+
+
+def test_cors(stack):
+    srv, _ = stack
+    _, _, h = _post(srv.port, "/api/predict_eta", BODY, {"Content-Type": "application/json",
+                                                         "Origin": "http://localhost:3000"})
+    assert h.get("access-control-allow-origin") == "http://localhost:3000"
+    _, _, h = _post(srv.port, "/api/predict_eta", BODY, {"Content-Type": "application/json",
+                                                         "Origin": "https://evil.example"})
+    assert "access-control-allow-origin" not in h
+
+
+def test_concurrent_clients_batch(stack):
+    srv, client = stack
+    ref = client.post("/api/predict_eta", json=BODY).content
+    errs = []
+    before = srv.stats()
+
+    def worker():
+        c = http.client.HTTPConnection("127.0.0.1", srv.port, timeout=10)
+        for _ in range(200):
+            st, body, _ = _post(srv.port, "/api/predict_eta", BODY, conn=c)
+            if st != 200 or body != ref:
+                errs.append((st, body))
+    th = [threading.Thread(target=worker) for _ in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs
+    after = srv.stats()
+    assert after["predictions"] - before["predictions"] == 3200
+    assert after["launches"] - before["launches"] <= 3200           # batching across connections
