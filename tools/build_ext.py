@@ -123,17 +123,29 @@ def build_sanitize(force: bool = False) -> str:
     return out
 
 
+def build_tools(force: bool = False) -> str:
+    """Host-only helper executables (build/native/loadgen: closed-loop HTTP load generator)."""
+    src = os.path.join(CSRC, "tools", "loadgen.cpp")
+    out = os.path.join(BUILD, "loadgen")
+    os.makedirs(BUILD, exist_ok=True)
+    if force or _newer(out, [src]):
+        _run(["g++", "-O2", "-std=c++17", "-pthread", src, "-o", out])
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
-    ap.add_argument("--only", choices=["C", "rt", "sanitize"], default=None)
+    ap.add_argument("--only", choices=["C", "rt", "sanitize", "tools"], default=None)
     ap.add_argument("--sanitize", action="store_true", help="also build the ASan/UBSan runtime harness")
     a = ap.parse_args()
     if a.only == "sanitize" or a.sanitize:
         print("built", build_sanitize(a.force))
         if a.only == "sanitize":
             return
+    if a.only in (None, "tools"):
+        print("built", build_tools(a.force))
     if a.only in (None, "rt"):
         print("built", build_rt(a.force, a.jobs))
     if a.only in (None, "C"):
