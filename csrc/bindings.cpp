@@ -407,11 +407,19 @@ torch::Tensor forest_predict(torch::Tensor records, torch::Tensor values, torch:
 }
 
 // ---------------------------------------------------------------- native predict server
-int64_t native_server_start(int64_t port, int64_t threads, torch::Tensor blob, int64_t H, std::vector<double> norm,
-                            int64_t variant, int64_t max_batch, std::vector<std::string> cors, bool cors_vercel,
-                            bool bind_any) {
-  check_dev(blob, "blob");
-  TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
+int64_t native_server_start(int64_t port, int64_t threads, std::vector<torch::Tensor> blobs, int64_t H,
+                            std::vector<double> norm, int64_t variant, int64_t max_batch,
+                            std::vector<std::string> cors, bool cors_vercel, bool bind_any) {
+  TORCH_CHECK(!blobs.empty(), "need one weight blob per GPU");
+  std::vector<int> devs, cus;
+  std::vector<const void*> ptrs;
+  for (auto& b : blobs) {
+    check_dev(b, "blob");
+    TORCH_CHECK((size_t)b.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
+    devs.push_back(b.device().index());
+    cus.push_back(num_cus(b.device().index()));
+    ptrs.push_back(b.data_ptr());
+  }
   TORCH_CHECK(norm.size() == 8, "norm must hold 4 scales + 4 shifts");
   TORCH_CHECK(max_batch >= 1 && max_batch <= (1 << 24), "max_batch out of range");
   rt::NormParams np;
@@ -420,9 +428,8 @@ int64_t native_server_start(int64_t port, int64_t threads, torch::Tensor blob, i
     np.shift[i] = (float)norm[4 + i];
   }
   std::string err;
-  const int dev = blob.device().index();
-  const int64_t h = rt::native_server_start((int)port, (int)threads, dev, blob.data_ptr(), (int)H, np, (int)variant,
-                                            num_cus(dev), (int)max_batch, cors, cors_vercel, bind_any, err);
+  const int64_t h = rt::native_server_start((int)port, (int)threads, devs, ptrs, cus, (int)H, np, (int)variant,
+                                            (int)max_batch, cors, cors_vercel, bind_any, err);
   TORCH_CHECK(h >= 0, "native server: ", err);
   return h;
 }

@@ -50,7 +50,7 @@ using rtc::Stamp;
 
 struct ServerCfg {
   int port = 0, threads = 1, device = 0, H = 256, variant = -1, num_cus = 256;
-  const void* blob = nullptr;
+  const void* blob = nullptr;          // this reactor's device + weight blob (one copy per GPU)
   NormParams np{};
   int max_batch = 1 << 20;
   std::vector<std::string> cors_exact;
@@ -102,6 +102,7 @@ inline bool ieq(const char* a, size_t n, const char* b) {
 class Reactor {
  public:
   Reactor(const ServerCfg& cfg, Stats& st, std::atomic<bool>& stop) : cfg_(cfg), st_(st), stop_(stop) {}
+  int device() const { return cfg_.device; }
 
   bool init(std::string& err) {
     lfd_ = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
@@ -164,7 +165,7 @@ class Reactor {
   }
 
  private:
-  const ServerCfg& cfg_;
+  const ServerCfg cfg_;                // per-reactor copy: device + blob of its GPU
   Stats& st_;
   std::atomic<bool>& stop_;
   bool bind_any_ = false;
@@ -505,23 +506,30 @@ std::vector<Server*> g_servers;
 
 }  // namespace
 
-int64_t native_server_start(int port, int threads, int device, const void* blob, int H, const NormParams& np,
-                            int variant, int num_cus, int max_batch, const std::vector<std::string>& cors,
+int64_t native_server_start(int port, int threads, const std::vector<int>& devices,
+                            const std::vector<const void*>& blobs, const std::vector<int>& num_cus, int H,
+                            const NormParams& np, int variant, int max_batch, const std::vector<std::string>& cors,
                             bool cors_vercel, bool bind_any, std::string& err) {
+  if (devices.empty() || devices.size() != blobs.size() || devices.size() != num_cus.size()) {
+    err = "devices/blobs mismatch";
+    return -1;
+  }
   auto* s = new Server();
   s->cfg.port = port;
   s->cfg.threads = threads < 1 ? 1 : threads;
-  s->cfg.device = device;
-  s->cfg.blob = blob;
   s->cfg.H = H;
   s->cfg.np = np;
   s->cfg.variant = variant;
-  s->cfg.num_cus = num_cus;
   s->cfg.max_batch = max_batch;
   s->cfg.cors_exact = cors;
   s->cfg.cors_vercel = cors_vercel;
   for (int i = 0; i < s->cfg.threads; ++i) {
-    auto r = std::make_unique<Reactor>(s->cfg, s->stats, s->stop);
+    ServerCfg rc = s->cfg;                       // reactors are spread round-robin over the GPUs
+    const size_t g = (size_t)i % devices.size();
+    rc.device = devices[g];
+    rc.blob = blobs[g];
+    rc.num_cus = num_cus[g];
+    auto r = std::make_unique<Reactor>(rc, s->stats, s->stop);
     r->set_bind_any(bind_any);
     if (!r->init(err)) {
       delete s;

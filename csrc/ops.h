@@ -78,8 +78,9 @@ hipError_t launch_greedy_cvrp(const double* D, const int* npts, const double* de
                               int* trip_of, int* ntrips, int* status, hipStream_t stream);
 
 // ---- native prediction front end : native_server.hip ----
-int64_t native_server_start(int port, int threads, int device, const void* blob, int H, const NormParams& np,
-                            int variant, int num_cus, int max_batch, const std::vector<std::string>& cors,
+int64_t native_server_start(int port, int threads, const std::vector<int>& devices,
+                            const std::vector<const void*>& blobs, const std::vector<int>& num_cus, int H,
+                            const NormParams& np, int variant, int max_batch, const std::vector<std::string>& cors,
                             bool cors_vercel, bool bind_any, std::string& err);
 void native_server_stop(int64_t h);
 void native_server_stats(int64_t h, long long out[4]);

@@ -41,7 +41,7 @@ def cmd_serve(a: argparse.Namespace) -> None:
         from .models.mlp3 import EtaMLP
         if isinstance(eta.model, EtaMLP):
             from .serve.native_server import NativePredictServer
-            native_srv = NativePredictServer(eta.model, device=eta.devices[0].index, port=a.native_port,
+            native_srv = NativePredictServer(eta.model, device=[d.index for d in eta.devices], port=a.native_port,
                                              threads=a.native_threads, cors_origins=s.cors_origins,
                                              bind_any=a.host not in ("127.0.0.1", "localhost"))
             print(json.dumps({"native_predict_port": native_srv.port}), flush=True)

@@ -30,14 +30,21 @@ def free_port() -> int:
 
 
 class NativePredictServer:
-    def __init__(self, model, device: int = 0, port: int = 0, threads: int = 2, max_batch: int = 1 << 18,
+    """``device``: one GPU index or a list — reactor threads are spread round-robin over the GPUs
+    (each GPU gets its own weight copy; use ``threads >= len(devices)``)."""
+
+    def __init__(self, model, device=0, port: int = 0, threads: int = 2, max_batch: int = 1 << 18,
                  cors_origins: Sequence[str] = ("http://localhost:3000", "http://127.0.0.1:3000"),
                  cors_vercel: bool = True, bind_any: bool = False, variant: int = -1):
         self.C = native(required=True)
-        self.kern = EtaMlpKernel(model, torch.device("cuda", device), variant=variant)   # owns the blob
+        devices = [device] if isinstance(device, int) else list(device)
+        threads = max(threads, len(devices))
+        # one packed weight blob per GPU; the kernels keep them alive for the server's lifetime
+        self.kerns = [EtaMlpKernel(model, torch.device("cuda", d), variant=variant) for d in devices]
+        k0 = self.kerns[0]
         self.port = port or free_port()
         self.h: Optional[int] = self.C.native_server_start(
-            self.port, threads, self.kern.packed.blob, self.kern.hidden, list(self.kern.packed.norm),
+            self.port, threads, [k.packed.blob for k in self.kerns], k0.hidden, list(k0.packed.norm),
             variant, max_batch, list(cors_origins), cors_vercel, bind_any)
 
     def stats(self) -> Dict[str, int]:
