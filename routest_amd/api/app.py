@@ -209,6 +209,15 @@ def _replay(body: bytes, tail=None):
     return receive
 
 
+async def _call(obj, fn, *args):
+    """Run ``fn`` inline when its owner is local CPU work (``obj.blocking`` False), otherwise in the
+    thread pool: a thread hop costs more than the sub-millisecond haversine optimizer or SQLite
+    insert it would wrap, while remote / GPU-synchronising calls must not block the event loop."""
+    if getattr(obj, "blocking", True):
+        return await run_in_threadpool(fn, *args)
+    return fn(*args)
+
+
 async def _json_body(request: Request, silent: bool):
     """Flask ``get_json()`` semantics: non-silent -> 415 on non-JSON content type, 400 on bad JSON;
     silent -> None on either."""
@@ -261,7 +270,7 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         data = await _json_body(request, silent=False)
         if isinstance(data, Response):
             return data
-        result = await run_in_threadpool(optimize_route, data, sv.provider, s.engine_name)
+        result = await _call(sv.provider, optimize_route, data, sv.provider, s.engine_name)
         if not result:
             return JSONResponse({"error": "no response acquired from the optimizer."}, 400)
         if isinstance(result, dict) and result.get("error") and not s.compat_request_route_200:
@@ -272,7 +281,7 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         payload = await _json_body(request, silent=True) or {}
         if not isinstance(payload, dict):
             payload = {}
-        result = await run_in_threadpool(optimize_route, payload, sv.provider, s.engine_name)
+        result = await _call(sv.provider, optimize_route, payload, sv.provider, s.engine_name)
         if isinstance(result, dict) and result.get("error"):
             return JSONResponse(result, 400)
         if payload.get("use_ml_eta"):
@@ -292,7 +301,7 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
                 props["eta_completion_time_ml"] = eta_iso
         if sv.store is not None:
             try:
-                rid = await run_in_threadpool(sv.store.persist_request_and_result, payload, result)
+                rid = await _call(sv.store, sv.store.persist_request_and_result, payload, result)
                 if rid:
                     result.setdefault("properties", {})["request_id"] = rid
                     result["properties"]["saved"] = True
@@ -459,7 +468,7 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
     async def locations():
         if sv.store is not None and hasattr(sv.store, "locations"):
             try:
-                return JSONResponse(await run_in_threadpool(sv.store.locations), 200)
+                return JSONResponse(await _call(sv.store, sv.store.locations), 200)
             except Exception as e:
                 return JSONResponse({"error": str(e)}, 500)
         from ..data.synth import seed_locations
@@ -485,7 +494,7 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         if sv.store is None:
             return _no_store()
         try:
-            items = await run_in_threadpool(sv.store.history, lim)
+            items = await _call(sv.store, sv.store.history, lim)
         except Exception as e:
             return JSONResponse({"error": f"history fetch failed: {e}"}, 500)
         return JSONResponse({"items": items}, 200)
@@ -495,7 +504,7 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         if sv.store is None:
             return JSONResponse({"error": "history disabled: SUPABASE not configured"}, 503)
         try:
-            d = await run_in_threadpool(sv.store.history_detail, req_id)
+            d = await _call(sv.store, sv.store.history_detail, req_id)
         except Exception as e:
             return JSONResponse({"error": f"history fetch failed: {e}"}, 500)
         if d is None:
@@ -507,7 +516,7 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         if sv.store is None:
             return JSONResponse({"error": "history disabled: SUPABASE not configured"}, 503)
         try:
-            await run_in_threadpool(sv.store.delete, req_id)
+            await _call(sv.store, sv.store.delete, req_id)
         except StoreUnavailable as e:
             return JSONResponse({"error": str(e)}, 500)
         except Exception as e:

@@ -200,6 +200,7 @@ class GraphProvider(HaversineProvider):
     """Directions along shortest paths of the road graph (durations from learned edge costs)."""
 
     name = "graph"
+    blocking = True        # GPU searches synchronise the device
 
     def __init__(self, g: RoadGraph, cost: np.ndarray, device=None):
         super().__init__()

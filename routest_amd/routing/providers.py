@@ -80,6 +80,7 @@ def _bearing_word(lat1, lon1, lat2, lon2) -> str:
 
 class HaversineProvider:
     name = "haversine"
+    blocking = False       # pure CPU, sub-millisecond: handlers call it inline (no thread hop)
 
     def __init__(self, circuity: float = 1.3, step_m: float = 150.0):
         self.circuity = circuity
@@ -104,9 +105,9 @@ class HaversineProvider:
             dist = float(haversine_m(lat1, lon1, lat2, lon2)) * self.circuity
             n = max(1, int(math.ceil(dist / self.step_m)))
             start_wp = len(geometry) - 1
-            for s in range(1, n + 1):
-                t = s / n
-                geometry.append([round(lon1 + (lon2 - lon1) * t, 6), round(lat1 + (lat2 - lat1) * t, 6)])
+            t = np.arange(1, n + 1, dtype=np.float64) / n          # densify in one vector op
+            pts = np.round(np.stack([lon1 + (lon2 - lon1) * t, lat1 + (lat2 - lat1) * t], axis=1), 6)
+            geometry.extend(pts.tolist())
             end_wp = len(geometry) - 1
             way_points.append(end_wp)
             dur = dist / speed
@@ -145,6 +146,7 @@ class ORSProvider:
     """The reference's remote calls (utils.py:55-62, 97-103, 151-156), same timeouts/errors."""
 
     name = "ors"
+    blocking = True        # remote HTTPS: handlers offload it to the thread pool
     BASE = "https://api.openrouteservice.org"
 
     def __init__(self, api_key: str, timeout: float = 30.0, session: Any = None):
