@@ -48,6 +48,21 @@ class Services:
     simulator: Simulator
     route_device: Optional[Any] = None
     started: float = field(default_factory=time.time)
+    scorer: Optional[Any] = None
+    _scorer_lock: Any = field(default_factory=lambda: __import__("threading").Lock())
+
+    def get_scorer(self):
+        """Candidate-route scorer (GCN on the road graph), built on first use: the provider's graph
+        when ``ROUTEST_PROVIDER=graph``, else a synthetic ``ROUTEST_GRAPH_NODES``-node graph."""
+        with self._scorer_lock:
+            if self.scorer is None:
+                from ..routing.scorer import RouteScorer
+                g = getattr(self.provider, "g", None)
+                if g is None:
+                    from ..data.graph import synth_road_graph
+                    g = synth_road_graph(self.settings.graph_nodes)
+                self.scorer = RouteScorer(g, device=self.route_device)
+            return self.scorer
 
 
 def build_services(settings: Optional[Settings] = None, eta: Optional[EtaService] = None,
@@ -321,6 +336,23 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
             return JSONResponse({"error": "expected a JSON array of route requests"}, 400)
         res = await run_in_threadpool(optimize_many, reqs, sv.provider, s.engine_name, sv.route_device)
         return JSONResponse({"results": res}, 200)
+
+    @app.post("/api/score_routes")
+    async def score_routes(request: Request):
+        """Rank candidate routes with the GCN road-graph scorer (HIP kernels on the GPU).
+        Body: {"routes": [[[lon, lat], ...] | {"coordinates": ...} | {"nodes": [...]} , ...]}."""
+        body = await _json_body(request, silent=False)
+        if isinstance(body, Response):
+            return body
+        routes = body.get("routes") if isinstance(body, dict) else body
+        if not isinstance(routes, list) or not routes:
+            return JSONResponse({"error": "expected {'routes': [route, ...]}"}, 400)
+        scorer = await run_in_threadpool(sv.get_scorer)
+        try:
+            res = await _call(scorer, scorer.score, routes)
+        except (ValueError, TypeError) as e:
+            return JSONResponse({"error": f"invalid route: {e}"}, 400)
+        return JSONResponse(res, 200)
 
     # ------------------------------------------------------------------ ETA
     async def _predict_one(body: Dict[str, Any]):

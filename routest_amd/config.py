@@ -70,6 +70,7 @@ class Settings:
     compat_history_500: bool = False     # ROUTEST_COMPAT_HISTORY_500 (Appendix B #6)
     sse_delta: bool = False              # ROUTEST_SSE_DELTA (Appendix B #7)
     fast_predict: bool = True            # ROUTEST_FAST_PREDICT: pure-ASGI native single-predict path
+    graph_nodes: int = 100_000           # ROUTEST_GRAPH_NODES: synthetic road graph for the route scorer
     sim_tick_min_s: float = 2.0          # ROUTEST_SIM_TICK_MIN (reference: U(2,5) s, utils.py:251)
     sim_tick_max_s: float = 5.0          # ROUTEST_SIM_TICK_MAX
     max_simulations: int = 256           # ROUTEST_MAX_SIMULATIONS (reference: unbounded threads)
@@ -142,6 +143,7 @@ def load_settings(env: Optional[Dict[str, str]] = None, dotenv_path: Optional[st
         compat_history_500=_as_bool(g("ROUTEST_COMPAT_HISTORY_500"), False),
         sse_delta=_as_bool(g("ROUTEST_SSE_DELTA"), False),
         fast_predict=_as_bool(g("ROUTEST_FAST_PREDICT"), True),
+        graph_nodes=_int("ROUTEST_GRAPH_NODES", 100_000),
         sim_tick_min_s=_float("ROUTEST_SIM_TICK_MIN", 2.0),
         sim_tick_max_s=_float("ROUTEST_SIM_TICK_MAX", 5.0),
         max_simulations=_int("ROUTEST_MAX_SIMULATIONS", 256),
