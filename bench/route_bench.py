@@ -63,7 +63,7 @@ def main() -> None:
     # every leg of a step in ONE launch: ~80k concurrent searches (dense per-slot state ~95 GB —
     # sized for 288 GB of HBM3E) so each CU keeps ~5 waves of latency-bound searches in flight
     legs_est = int(sum(len(s) for s in snapped) * 1.4) + 1024
-    astar = BatchedAstar(g, cost, dev, slots=min(legs_est, 98304), cap=32768)
+    astar = BatchedAstar(g, cost, dev, slots=min(legs_est, 98304), cap=65536)
 
     def step():
         D = C.route_haversine_matrix(lat_t, lon_t, npts_t, 1.3)
@@ -95,12 +95,13 @@ def main() -> None:
     el = allreduce_scalars([time.perf_counter() - t0], dev, op="max")[0]
     tot_legs = allreduce_scalars([legs], dev)[0]
     ok = float((st == 0).float().mean())
+    status_hist = torch.bincount(st.long().cpu(), minlength=5).tolist()
     if di.is_main:
         print(json.dumps({"metric": "batched multi-stop optimizer (greedy CVRP + A* w/ MLP edge costs)",
                           "n_gpus": di.world, "requests_per_step": a.requests, "nodes": g.num_nodes,
                           "ms_per_step": el / a.steps * 1e3, "requests_per_s": a.requests * a.steps / el,
                           "astar_legs_per_s": tot_legs / el, "legs_per_step": tot_legs / a.steps,
-                          "astar_found_frac": ok}), flush=True)
+                          "astar_found_frac": ok, "astar_status_hist": status_hist}), flush=True)
     if di.world > 1:
         dist.destroy_process_group()
 

@@ -3,12 +3,16 @@
 // 151-156), which it issues one at a time over HTTPS.
 //
 // One LANE per query ("slot"): tens of thousands of independent searches in flight, each with
-//   * dense per-slot g[N] (f32) and parent[N] (i32; bit 31 = closed) arrays in HBM — 16k slots x
-//     100k nodes = 13 GB, which 288 GB of HBM3E makes the simple and fast choice (no hashing);
+//   * dense per-slot state[N]: one 8-byte word (g as f32 | parent, closed bit) per node, so a
+//     relaxation is one random access — 80k slots x 100k nodes = 64 GB, which 288 GB of HBM3E makes
+//     the simple and fast choice (no hashing);
 //   * a binary min-heap of (f, node) 64-bit entries with lazy deletion (stale pops are skipped via
 //     the closed bit; the heuristic is consistent, so a node's first pop is final);
 //   * a touched list, so only the entries a search wrote are reset afterwards (no N-sized memset
 //     per query).
+// Launch time is set by the LONGEST search (one lane walks its own heap), so the heuristic matters
+// most in the tail: 32 landmarks (vs 16) cut p99 pops 28k -> 12k and the 80k-leg launch 671 ->
+// 444 ms (bench/astar_tail.py).
 // Heuristic: max(great-circle distance x circuity / v_max, ALT landmark bound); edge costs are
 // floored at length / v_max on the host, so both are admissible and consistent (ALT tables are
 // shrunk by 1e-4 against fp32 rounding).  Every lane stops within max_iters pops (status 3), on heap
@@ -27,21 +31,21 @@ struct AstarArgs {
   const float* lon;
   const int* src;        // [Q]
   const int* dst;
-  float* g;              // [S][N]
-  int* parent;           // [S][N]
+  unsigned long long* st;  // [S][N] packed per-node state: g (f32 bits, low) | parent (31 b) + closed (bit 63)
   unsigned long long* heap;  // [S][cap]
   int* touched;          // [S][cap]
   float* out_cost;       // [Q]
   int* out_len;          // [Q]
   int* out_status;       // [Q]
   int* out_path;         // [Q][max_path]
-  int N, Q, q0, cap, max_path, max_iters;
+  int N, Q, q0, S, cap, max_path, max_iters;
   float inv_vmax;        // seconds per metre at v_max
   const float* lm;       // [N][2K] ALT landmark tables: d(L_k -> v), d(v -> L_k) (nullptr: off)
   int K;
+  int* out_iters;        // [Q] heap pops per query (nullptr: not recorded)
 };
 
-constexpr int KMAX = 16;
+constexpr int KMAX = 32;
 
 __device__ __forceinline__ float hdist(const AstarArgs& a, int v, float tlat, float tlon, float ctl) {
   const float k = 0.017453292519943295f;
@@ -70,17 +74,28 @@ __device__ __forceinline__ float halt(const AstarArgs& a, int v, const float (&f
   return best * 0.9999f;
 }
 
+// One 8-byte word per (slot, node): a relaxation reads g and the closed bit with ONE random access
+// (the searches are bound by random HBM lines: 80k searches x dense 100k-node state = 64 GB).
+__device__ __forceinline__ float st_g(unsigned long long w) { return __uint_as_float((unsigned)w); }
+__device__ __forceinline__ unsigned st_p(unsigned long long w) { return (unsigned)(w >> 32); }
+__device__ __forceinline__ unsigned long long st_make(float g, unsigned p) {
+  return ((unsigned long long)p << 32) | __float_as_uint(g);
+}
+constexpr unsigned long long ST_INIT = 0x7fffffff7f800000ull;   // g = +inf, parent = none, open
+
 __device__ __forceinline__ unsigned long long hkey(float f, int v) {
   return ((unsigned long long)__float_as_uint(f) << 32) | (unsigned)v;   // f >= 0: monotone bits
 }
 
 template <int K>
 __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
-  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  // XCD-aware: workgroup b runs on XCD b % 8; give each XCD a contiguous range of queries, so with
+  // source-sorted queries one XCD's L2 serves one region of the graph (edges, costs, ALT rows)
+  const int lb = (int)(blockIdx.x % 8u) * (int)(gridDim.x / 8u) + (int)(blockIdx.x / 8u);
+  const int slot = lb * blockDim.x + threadIdx.x;
   const int q = a.q0 + slot;
-  if (q >= a.Q) return;
-  float* g = a.g + (size_t)slot * a.N;
-  int* par = a.parent + (size_t)slot * a.N;
+  if (q >= a.Q || slot >= a.S) return;
+  unsigned long long* st = a.st + (size_t)slot * a.N;
   unsigned long long* heap = a.heap + (size_t)slot * a.cap;
   int* touched = a.touched + (size_t)slot * a.cap;
   const int s = a.src[q], t = a.dst[q];
@@ -107,8 +122,7 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
   };
 
   int hn = 0, nt = 0, status = 1;
-  g[s] = 0.f;
-  par[s] = -1 & 0x7fffffff;
+  st[s] = st_make(0.f, 0x7fffffffu);
   touched[nt++] = s;
   heap[hn++] = hkey(heur(s), s);
   int it = 0;
@@ -134,26 +148,25 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
       heap[i] = last;
     }
     const int v = (int)(unsigned)(top & 0xffffffffu);
-    const unsigned pv = (unsigned)par[v];
-    if (pv & CLOSED) continue;           // stale duplicate
-    par[v] = (int)(pv | CLOSED);
+    const unsigned long long wv = st[v];
+    if (st_p(wv) & CLOSED) continue;     // stale duplicate
+    st[v] = wv | ((unsigned long long)CLOSED << 32);
     if (v == t) { status = 0; break; }
-    const float gv = g[v];
+    const float gv = st_g(wv);
     const int e1 = a.indptr[v + 1];
     bool overflow = false;
     for (int e = a.indptr[v]; e < e1; ++e) {
       const int u = a.indices[e];
-      const unsigned pu = (unsigned)par[u];
-      if (pu & CLOSED) continue;
+      const unsigned long long wu = st[u];
+      if (st_p(wu) & CLOSED) continue;
       const float ng = gv + a.cost[e];
-      const float gu = g[u];
+      const float gu = st_g(wu);
       if (ng < gu) {
         if (gu == __int_as_float(0x7f800000)) {   // first touch
           if (nt >= a.cap) { overflow = true; break; }
           touched[nt++] = u;
         }
-        g[u] = ng;
-        par[u] = v;
+        st[u] = st_make(ng, (unsigned)v);
         if (hn >= a.cap) { overflow = true; break; }
         // push + sift up
         unsigned long long key = hkey(ng + heur(u), u);
@@ -173,14 +186,14 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
   int len = 0;
   float total = 0.f;
   if (status == 0) {
-    total = g[t];
+    total = st_g(st[t]);
     int* path = a.out_path + (size_t)q * a.max_path;
     int v = t;
     while (true) {
       if (len >= a.max_path) { status = 4; break; }
       path[len++] = v;
       if (v == s) break;
-      v = (int)((unsigned)par[v] & 0x7fffffffu);
+      v = (int)(st_p(st[v]) & 0x7fffffffu);
     }
     if (status == 0) {
       for (int i = 0, j = len - 1; i < j; ++i, --j) {
@@ -192,37 +205,33 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
       len = 0;
     }
   }
+  if (a.out_iters) a.out_iters[q] = it;
   a.out_cost[q] = status == 0 ? total : -1.f;
   a.out_len[q] = len;
   a.out_status[q] = status;
   // reset this slot's touched entries for the next batch
-  const float inf = __int_as_float(0x7f800000);
-  for (int i = 0; i < nt; ++i) {
-    const int v = touched[i];
-    g[v] = inf;
-    par[v] = 0x7fffffff;
-  }
+  for (int i = 0; i < nt; ++i) st[touched[i]] = ST_INIT;
 }
 
 hipError_t launch_astar(const int* indptr, const int* indices, const float* cost, const float* lat,
-                        const float* lon, const int* src, const int* dst, float* g, int* parent,
+                        const float* lon, const int* src, const int* dst, void* state,
                         void* heap, int* touched, float* out_cost, int* out_len, int* out_status,
                         int* out_path, int N, int Q, int q0, int slots, int cap, int max_path,
                         int max_iters, float inv_vmax, const float* lm, int K,
-                        hipStream_t stream) {
+                        hipStream_t stream, int* out_iters) {
   const int n = min(slots, Q - q0);
   if (n <= 0) return hipSuccess;
-  if (lm != nullptr && K != 16 && K != 8) return hipErrorInvalidValue;
-  AstarArgs a{indptr, indices, cost, lat, lon, src, dst, g, parent,
+  if (lm != nullptr && K != 32 && K != 16 && K != 8) return hipErrorInvalidValue;
+  AstarArgs a{indptr, indices, cost, lat, lon, src, dst, (unsigned long long*)state,
               (unsigned long long*)heap, touched, out_cost, out_len, out_status, out_path,
-              N, Q, q0, cap, max_path, max_iters, inv_vmax, lm, K};
-  // one wavefront per workgroup: with length-sorted queries each wave is homogeneous, and the
-  // dispatcher's round-robin placement spreads short and long waves over all CUs (256-lane
-  // workgroups would pile the longest searches onto a few CUs and leave a serial tail)
-  const dim3 grid((n + 63) / 64), block(64);
+              N, Q, q0, slots, cap, max_path, max_iters, inv_vmax, lm, K, out_iters};
+  // one wavefront per workgroup (a wave runs as long as its longest search); grid rounded to a
+  // multiple of 8 for the XCD-aware remap in the kernel (surplus lanes exit at the slot check)
+  const dim3 grid(((n + 63) / 64 + 7) / 8 * 8), block(64);
   if (lm == nullptr) hipLaunchKernelGGL(astar_kernel<0>, grid, block, 0, stream, a);
   else if (K == 8) hipLaunchKernelGGL(astar_kernel<8>, grid, block, 0, stream, a);
-  else hipLaunchKernelGGL(astar_kernel<16>, grid, block, 0, stream, a);
+  else if (K == 16) hipLaunchKernelGGL(astar_kernel<16>, grid, block, 0, stream, a);
+  else hipLaunchKernelGGL(astar_kernel<32>, grid, block, 0, stream, a);
   return hipGetLastError();
 }
 

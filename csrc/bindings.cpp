@@ -349,15 +349,17 @@ torch::Tensor route_score(torch::Tensor rptr, torch::Tensor nodes, torch::Tensor
 // touched [S,cap] must be initialised to (inf, 0x7fffffff) once; the kernel restores them.
 void astar(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torch::Tensor lat,
            torch::Tensor lon, torch::Tensor src, torch::Tensor dst, torch::Tensor g,
-           torch::Tensor parent, torch::Tensor heap, torch::Tensor touched, torch::Tensor out_cost,
+           torch::Tensor heap, torch::Tensor touched, torch::Tensor out_cost,
            torch::Tensor out_len, torch::Tensor out_status, torch::Tensor out_path, int64_t q0,
-           int64_t max_iters, double inv_vmax, c10::optional<torch::Tensor> landmarks) {
-  for (auto* t : {&indptr, &indices, &cost, &lat, &lon, &src, &dst, &g, &parent, &heap, &touched,
+           int64_t max_iters, double inv_vmax, c10::optional<torch::Tensor> landmarks,
+           c10::optional<torch::Tensor> out_iters) {
+  for (auto* t : {&indptr, &indices, &cost, &lat, &lon, &src, &dst, &g, &heap, &touched,
                   &out_cost, &out_len, &out_status, &out_path})
     check_dev(*t, "astar tensor");
   const int64_t N = lat.numel();
   TORCH_CHECK(indptr.numel() == N + 1 && cost.numel() == indices.numel(), "graph shapes");
-  TORCH_CHECK(g.dim() == 2 && g.size(1) == N && parent.sizes() == g.sizes(), "g/parent must be [S,N]");
+  TORCH_CHECK(g.scalar_type() == torch::kInt64 && g.dim() == 2 && g.size(1) == N,
+              "state must be int64 [S,N] (packed g | parent)");
   TORCH_CHECK(heap.scalar_type() == torch::kInt64 && heap.dim() == 2 && heap.size(0) == g.size(0),
               "heap must be int64 [S,cap]");
   TORCH_CHECK(touched.sizes() == heap.sizes(), "touched must be [S,cap]");
@@ -370,20 +372,26 @@ void astar(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torc
   if (landmarks.has_value()) {
     check_dev(*landmarks, "landmarks");
     TORCH_CHECK(landmarks->scalar_type() == torch::kFloat32 && landmarks->dim() == 2 &&
-                landmarks->size(0) == N && landmarks->size(1) % 4 == 0 && landmarks->size(1) <= 32,
-                "landmarks must be f32 [N, 2K] with K even <= 16");
+                landmarks->size(0) == N && landmarks->size(1) % 4 == 0 && landmarks->size(1) <= 64,
+                "landmarks must be f32 [N, 2K] with K in {8, 16, 32}");
     lm = landmarks->data_ptr<float>();
     K = (int)landmarks->size(1) / 2;
+  }
+  int* iters = nullptr;
+  if (out_iters.has_value() && out_iters->defined()) {
+    check_dev(*out_iters, "out_iters");
+    TORCH_CHECK(out_iters->scalar_type() == torch::kInt32 && out_iters->numel() == Q, "out_iters int32 [Q]");
+    iters = out_iters->data_ptr<int>();
   }
   const c10::DeviceGuard guard(g.device());
   RT_CHECK_HIP(rt::launch_astar(indptr.data_ptr<int>(), indices.data_ptr<int>(), cost.data_ptr<float>(),
                                 lat.data_ptr<float>(), lon.data_ptr<float>(), src.data_ptr<int>(),
-                                dst.data_ptr<int>(), g.data_ptr<float>(), parent.data_ptr<int>(),
+                                dst.data_ptr<int>(), g.data_ptr(),
                                 heap.data_ptr(), touched.data_ptr<int>(), out_cost.data_ptr<float>(),
                                 out_len.data_ptr<int>(), out_status.data_ptr<int>(),
                                 out_path.data_ptr<int>(), (int)N, (int)Q, (int)q0, (int)g.size(0),
                                 (int)heap.size(1), (int)out_path.size(1), (int)max_iters,
-                                (float)inv_vmax, lm, K, cur_stream(g)));
+                                (float)inv_vmax, lm, K, cur_stream(g), iters));
 }
 
 torch::Tensor forest_predict(torch::Tensor records, torch::Tensor values, torch::Tensor info,
@@ -545,7 +553,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gcn_agg_gemm", &gcn_agg_gemm, "K8: fused CSR aggregation + MFMA GEMM + bias/ReLU");
   m.def("gcn_spmm_score", &gcn_spmm_score, "K8: layer-2 aggregation + delay head");
   m.def("route_score", &route_score, "K8: per-route delay-weighted length");
-  m.def("astar", &astar, "K9: batched A* (one lane per query) with learned edge costs");
+  m.def("astar", &astar, "K9: batched A* (one lane per query) with learned edge costs",
+        py::arg("indptr"), py::arg("indices"), py::arg("cost"), py::arg("lat"), py::arg("lon"), py::arg("src"),
+        py::arg("dst"), py::arg("state"), py::arg("heap"), py::arg("touched"), py::arg("out_cost"),
+        py::arg("out_len"), py::arg("out_status"), py::arg("out_path"), py::arg("q0"), py::arg("max_iters"),
+        py::arg("inv_vmax"), py::arg("landmarks") = py::none(), py::arg("out_iters") = py::none());
   m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
   m.def("forest_predict_lds", &forest_predict_lds, "K4: LDS-staged tree chunks, 2 walks per thread");
   m.def("native_server_start", &native_server_start, "native HTTP front end for /api/predict_eta and /predict");

@@ -56,10 +56,11 @@ hipError_t launch_route_score(const int* rptr, const int* nodes, const float* la
 
 // ---- batched A* (K9) : astar.hip ----
 hipError_t launch_astar(const int* indptr, const int* indices, const float* cost, const float* lat,
-                        const float* lon, const int* src, const int* dst, float* g, int* parent,
+                        const float* lon, const int* src, const int* dst, void* state,
                         void* heap, int* touched, float* out_cost, int* out_len, int* out_status,
                         int* out_path, int N, int Q, int q0, int slots, int cap, int max_path,
-                        int max_iters, float inv_vmax, const float* lm, int K, hipStream_t stream);
+                        int max_iters, float inv_vmax, const float* lm, int K, hipStream_t stream,
+                        int* out_iters = nullptr);
 
 // ---- tree ensemble (K4) : forest.hip ----
 hipError_t launch_forest(const void* rec, const float* values, const unsigned* info, const int* roots,

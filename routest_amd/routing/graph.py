@@ -121,7 +121,7 @@ class BatchedAstar:
     """GPU batched A*; workspace sized for ``slots`` concurrent searches (dense per-slot state)."""
 
     def __init__(self, g: RoadGraph, cost: np.ndarray, device, slots: int = 16384, cap: int = 65536,
-                 max_path: int = 4096, max_iters: int = 2_000_000, landmarks: int = 16):
+                 max_path: int = 4096, max_iters: int = 2_000_000, landmarks: int = 32):
         from ..ops import _ext
         self.C = _ext.native(required=True)
         self.g = g
@@ -140,8 +140,8 @@ class BatchedAstar:
         self.v_max = float((g.length_m / np.maximum(cost_np, 1e-6)).max()) * 1.0001
         self.inv_vmax = 1.15 / self.v_max
         self.lm = (torch.from_numpy(landmark_tables(g, cost, landmarks)).to(d) if landmarks else None)
-        self.gbuf = torch.full((slots, N), float("inf"), dtype=torch.float32, device=d)
-        self.parent = torch.full((slots, N), 0x7FFFFFFF, dtype=torch.int32, device=d)
+        # packed per-(slot, node) state: g (f32 bits) | parent << 32, initialised to (inf, none)
+        self.state = torch.full((slots, N), 0x7FFFFFFF7F800000, dtype=torch.int64, device=d)
         self.heap = torch.empty((slots, cap), dtype=torch.int64, device=d)
         self.touched = torch.empty((slots, cap), dtype=torch.int32, device=d)
 
@@ -156,17 +156,17 @@ class BatchedAstar:
     def run(self, src: Sequence[int], dst: Sequence[int], sort: bool = False):
         """Returns (cost_s [Q] tensor, path_len [Q], status [Q], paths [Q, max_path]) on device.
 
-        ``sort``: launch queries in order of straight-line length so the 64 searches of a wavefront
-        have similar sizes, results scattered back to the caller's order.  Measured neutral on the
-        config-5 bench (826 vs 811 ms/step: the searches are bound by dependent heap/state loads,
-        not by wave divergence), so it is off by default."""
+        ``sort``: launch queries ordered by source node (ids are row-major, so this is a spatial
+        order); with the kernel's XCD-aware wave mapping each XCD's L2 then serves one region of
+        the graph.  Results are scattered back to the caller's order.  Measured neutral (314 vs
+        317 ms for 80k legs: the per-slot state, not graph data, dominates), so off by default."""
         d = self.dev
         src = np.asarray(src, dtype=np.int32)
         dst = np.asarray(dst, dtype=np.int32)
         order = None
         if sort and len(src) > 64:
             g = self.g
-            order = np.argsort(haversine_m(g.lat[src], g.lon[src], g.lat[dst], g.lon[dst]), kind="stable")
+            order = np.argsort(src, kind="stable")
             src, dst = src[order], dst[order]
         s = torch.as_tensor(src).to(d)
         t = torch.as_tensor(dst).to(d)
@@ -175,10 +175,11 @@ class BatchedAstar:
         out_len = torch.empty(Q, dtype=torch.int32, device=d)
         out_status = torch.empty(Q, dtype=torch.int32, device=d)
         out_path = torch.empty((Q, self.max_path), dtype=torch.int32, device=d)
+        self.last_iters = torch.empty(Q, dtype=torch.int32, device=d)   # heap pops per query
         for q0 in range(0, Q, self.slots):
-            self.C.astar(self.indptr, self.indices, self.cost, self.lat, self.lon, s, t, self.gbuf,
-                         self.parent, self.heap, self.touched, out_cost, out_len, out_status, out_path,
-                         q0, self.max_iters, self.inv_vmax, self.lm)
+            self.C.astar(self.indptr, self.indices, self.cost, self.lat, self.lon, s, t, self.state,
+                         self.heap, self.touched, out_cost, out_len, out_status, out_path,
+                         q0, self.max_iters, self.inv_vmax, self.lm, self.last_iters)
         if order is not None:
             idx = torch.from_numpy(order.astype(np.int64)).to(d)
             res = []
