@@ -19,8 +19,8 @@ cost = edge_costs(g, default_model(hidden=256, steps=200), device="cuda:0")
 rng = np.random.default_rng(100)
 S = rng.integers(0, g.num_nodes, 80000).astype(np.int32)
 T = rng.integers(0, g.num_nodes, 80000).astype(np.int32)
-for K in (16, 32):
-    a = BatchedAstar(g, cost, "cuda:0", slots=80000, cap=65536, landmarks=K)
+for K, meth in ((32, "sectors"), (32, "farthest"), (16, "farthest")):
+    a = BatchedAstar(g, cost, "cuda:0", slots=80000, cap=65536, landmarks=K, landmark_method=meth)
     a.run(S[:1000], T[:1000])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -29,7 +29,7 @@ for K in (16, 32):
     el = time.perf_counter() - t0
     it = a.last_iters.cpu().numpy()
     pct = np.percentile(it, [50, 90, 99, 99.9, 100]).astype(int).tolist()
-    print(f"K={K}: {el * 1e3:.1f} ms, pops p50/p90/p99/p99.9/max = {pct}, status {np.bincount(st.cpu().numpy(), minlength=5).tolist()}",
+    print(f"K={K} {meth}: {el * 1e3:.1f} ms, pops p50/p90/p99/p99.9/max = {pct}, status {np.bincount(st.cpu().numpy(), minlength=5).tolist()}",
           flush=True)
     del a
     torch.cuda.empty_cache()

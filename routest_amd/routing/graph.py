@@ -90,21 +90,35 @@ def dijkstra_ref(g: RoadGraph, cost: np.ndarray, src: Sequence[int], dst: Sequen
     return out
 
 
-def landmark_tables(g: RoadGraph, cost: np.ndarray, k: int = 16, seed: int = 0) -> np.ndarray:
-    """ALT preprocessing: K landmarks spread around the periphery (by angle from the centre),
-    forward d(L -> v) and backward d(v -> L) shortest-path tables, interleaved per node as
-    [N][2K] = (fwd_k, fwd_k+1, bwd_k, bwd_k+1) float4 groups (csrc/astar.hip::halt)."""
+def landmark_tables(g: RoadGraph, cost: np.ndarray, k: int = 16, seed: int = 0,
+                    method: str = "sectors") -> np.ndarray:
+    """ALT preprocessing: K landmarks, forward d(L -> v) and backward d(v -> L) shortest-path
+    tables, interleaved per node as [N][2K] = (fwd_k, fwd_k+1, bwd_k, bwd_k+1) float4 groups
+    (csrc/astar.hip::halt).  ``sectors``: the outermost node of K angular sectors around the centre;
+    ``farthest``: greedy farthest-point selection in travel time (each new landmark maximises its
+    distance to the chosen set)."""
     from scipy.sparse import csr_matrix
     from scipy.sparse.csgraph import dijkstra
-    clat, clon = float(g.lat.mean()), float(g.lon.mean())
-    ang = np.arctan2(g.lat - clat, (g.lon - clon) * np.cos(np.radians(clat)))
-    rad = haversine_m(g.lat, g.lon, clat, clon)
-    lms = []
-    for i in range(k):
-        lo, hi = -np.pi + 2 * np.pi * i / k, -np.pi + 2 * np.pi * (i + 1) / k
-        sector = np.where((ang >= lo) & (ang < hi))[0]
-        lms.append(int(sector[np.argmax(rad[sector])]) if len(sector) else int(np.argmax(rad)))
     m = csr_matrix((np.asarray(cost, dtype=np.float64), g.indices, g.indptr), shape=(g.num_nodes,) * 2)
+    if method == "farthest":
+        rng = np.random.default_rng(seed)
+        start = int(rng.integers(0, g.num_nodes))
+        d0 = dijkstra(m, directed=True, indices=[start])[0]
+        lms = [int(np.argmax(np.where(np.isfinite(d0), d0, -1)))]
+        mind = dijkstra(m, directed=True, indices=lms)[0]
+        while len(lms) < k:
+            nxt = int(np.argmax(np.where(np.isfinite(mind), mind, -1)))
+            lms.append(nxt)
+            mind = np.minimum(mind, dijkstra(m, directed=True, indices=[nxt])[0])
+    else:
+        clat, clon = float(g.lat.mean()), float(g.lon.mean())
+        ang = np.arctan2(g.lat - clat, (g.lon - clon) * np.cos(np.radians(clat)))
+        rad = haversine_m(g.lat, g.lon, clat, clon)
+        lms = []
+        for i in range(k):
+            lo, hi = -np.pi + 2 * np.pi * i / k, -np.pi + 2 * np.pi * (i + 1) / k
+            sector = np.where((ang >= lo) & (ang < hi))[0]
+            lms.append(int(sector[np.argmax(rad[sector])]) if len(sector) else int(np.argmax(rad)))
     fwd = dijkstra(m, directed=True, indices=lms)
     bwd = dijkstra(m.T.tocsr(), directed=True, indices=lms)
     fwd = np.where(np.isfinite(fwd), fwd, 0.0).astype(np.float32)
@@ -121,7 +135,8 @@ class BatchedAstar:
     """GPU batched A*; workspace sized for ``slots`` concurrent searches (dense per-slot state)."""
 
     def __init__(self, g: RoadGraph, cost: np.ndarray, device, slots: int = 16384, cap: int = 65536,
-                 max_path: int = 4096, max_iters: int = 2_000_000, landmarks: int = 32):
+                 max_path: int = 4096, max_iters: int = 2_000_000, landmarks: int = 32,
+                 landmark_method: str = "farthest"):
         from ..ops import _ext
         self.C = _ext.native(required=True)
         self.g = g
@@ -139,7 +154,9 @@ class BatchedAstar:
         cost_np = np.asarray(cost, dtype=np.float64)
         self.v_max = float((g.length_m / np.maximum(cost_np, 1e-6)).max()) * 1.0001
         self.inv_vmax = 1.15 / self.v_max
-        self.lm = (torch.from_numpy(landmark_tables(g, cost, landmarks)).to(d) if landmarks else None)
+        self.landmark_method = landmark_method
+        self.lm = (torch.from_numpy(landmark_tables(g, cost, landmarks, method=landmark_method)).to(d)
+                   if landmarks else None)
         # packed per-(slot, node) state: g (f32 bits) | parent << 32, initialised to (inf, none)
         self.state = torch.full((slots, N), 0x7FFFFFFF7F800000, dtype=torch.int64, device=d)
         self.heap = torch.empty((slots, cap), dtype=torch.int64, device=d)
@@ -151,7 +168,8 @@ class BatchedAstar:
         self.v_max = float((self.g.length_m / np.maximum(cost.astype(np.float64), 1e-6)).max()) * 1.0001
         self.inv_vmax = 1.15 / self.v_max
         if self.lm is not None:
-            self.lm.copy_(torch.from_numpy(landmark_tables(self.g, cost, self.lm.shape[1] // 2)))
+            self.lm.copy_(torch.from_numpy(landmark_tables(self.g, cost, self.lm.shape[1] // 2,
+                                                           method=self.landmark_method)))
 
     def run(self, src: Sequence[int], dst: Sequence[int], sort: bool = False):
         """Returns (cost_s [Q] tensor, path_len [Q], status [Q], paths [Q, max_path]) on device.
