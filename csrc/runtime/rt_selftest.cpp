@@ -135,12 +135,48 @@ static void fuzz_float(std::mt19937_64& rng, int iters) {
   CHECK(timedelta_minutes_us(1.0 / 60000000.0 * 2.5) == 2, "half-even rounding");
 }
 
+// The batched /predict path splits a big array with split_top_array and packs / formats items on
+// parallel_chunks threads (rt.cpp); replay that shape here so TSan sees the real sharing pattern.
+static void threaded_pack_format(int n_items) {
+  std::string body = "[";
+  for (int i = 0; i < n_items; ++i) {
+    if (i) body += ',';
+    body += "{\"summary\":{\"distance\":" + std::to_string(1000 + i) +
+            "},\"pickup_time\":\"2025-08-25T08:30:00+02:00\",\"traffic\":\"High\"}";
+  }
+  body += "]";
+  std::vector<std::pair<size_t, size_t>> spans;
+  CHECK(split_top_array(body.data(), body.size(), spans) && (int)spans.size() == n_items, "split");
+  const Stamp now{1756110600, 0, false, 0, 0};
+  std::vector<EtaRecord> recs(spans.size());
+  std::vector<Stamp> st(spans.size());
+  std::vector<std::string> errs(spans.size());
+  parallel_chunks(spans.size(), 64, 8, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      rtj::Value v = rtj::Parser(body.data() + spans[i].first, spans[i].second - spans[i].first).parse();
+      errs[i] = pack_item(v, now, recs[i], st[i]);
+    }
+  });
+  std::vector<std::string> parts(8);
+  const size_t per = (spans.size() + 7) / 8;
+  parallel_chunks(8, 1, 8, [&](size_t klo, size_t khi) {
+    for (size_t k = klo; k < khi; ++k)
+      for (size_t i = k * per; i < std::min(spans.size(), (k + 1) * per); ++i)
+        format_one(parts[k], 12.5 + (double)i, st[i].secs, st[i].us, st[i].has_tz, st[i].tz_sec, errs[i]);
+  });
+  size_t ok = 0;
+  for (auto& e : errs) ok += e.empty();
+  CHECK(ok == spans.size(), "threaded pack errors");
+  CHECK(recs[n_items - 1].distance_m == (float)(1000 + n_items - 1), "threaded pack record");
+}
+
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? std::atoi(argv[1]) : 20000;
   std::mt19937_64 rng(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 1234);
   fuzz_json(rng, iters);
   fuzz_iso(rng, iters);
   fuzz_float(rng, iters);
+  threaded_pack_format(20000);
   std::printf("rt_selftest: %d iterations, %d failures\n", iters, g_fail);
   return g_fail ? 1 : 0;
 }

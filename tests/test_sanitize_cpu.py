@@ -11,6 +11,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_runtime_core_tsan_threaded_paths():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import build_ext
+    exe = build_ext.build_sanitize(kind="tsan")
+    r = subprocess.run([exe, "2000", "3"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "WARNING: ThreadSanitizer" not in r.stderr
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
 def test_runtime_core_asan_ubsan_fuzz():
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import build_ext

@@ -111,15 +111,18 @@ def build_rt(force: bool = False, jobs: int = 8) -> str:
     return out
 
 
-def build_sanitize(force: bool = False) -> str:
-    """Host-only ASan+UBSan build of the runtime core fuzz harness (no GPU code involved)."""
+def build_sanitize(force: bool = False, kind: str = "asan") -> str:
+    """Host-only sanitizer builds of the runtime core fuzz harness (no GPU code involved):
+    ``asan`` = AddressSanitizer + UBSan, ``tsan`` = ThreadSanitizer (parallel pack/format paths)."""
     rdir = os.path.join(CSRC, "runtime")
     src = os.path.join(rdir, "rt_selftest.cpp")
-    out = os.path.join(BUILD, "rt_selftest_asan")
+    out = os.path.join(BUILD, f"rt_selftest_{kind}")
     os.makedirs(BUILD, exist_ok=True)
+    flags = (["-fsanitize=address,undefined", "-fno-sanitize-recover=all"] if kind == "asan"
+             else ["-fsanitize=thread"])
     if force or _newer(out, [src] + glob.glob(os.path.join(rdir, "*.h"))):
-        _run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
-              "-fno-omit-frame-pointer", "-I", rdir, src, "-o", out])
+        _run(["g++", "-std=c++17", "-O1", "-g", *flags, "-fno-omit-frame-pointer", "-pthread", "-I", rdir, src,
+              "-o", out])
     return out
 
 
@@ -141,7 +144,8 @@ def main() -> None:
     ap.add_argument("--sanitize", action="store_true", help="also build the ASan/UBSan runtime harness")
     a = ap.parse_args()
     if a.only == "sanitize" or a.sanitize:
-        print("built", build_sanitize(a.force))
+        print("built", build_sanitize(a.force, "asan"))
+        print("built", build_sanitize(a.force, "tsan"))
         if a.only == "sanitize":
             return
     if a.only in (None, "tools"):
