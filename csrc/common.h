@@ -26,6 +26,32 @@ struct NormParams {
   float shift[4];
 };
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+
+// ReLU as an integer max on the fp32 bit pattern: negative floats (sign bit set) are negative
+// int32s, so max(bits, 0) is relu in ONE v_max_i32.  fmaxf(x, 0.f) costs two v_max_f32 on gfx950
+// (IEEE mode inserts a NaN-quieting self-max before every use), which made the MLP epilogues
+// VALU-bound.
+__device__ __forceinline__ float relu_f(float x) {
+  return __int_as_float(max(__float_as_int(x), 0));
+}
+
+// 8 fp32 -> relu -> bf16x8: convert pairs (v_cvt_pk_bf16_f32), then ReLU on the packed bf16 bit
+// patterns with v_pk_max_i16 (round-to-nearest preserves the sign, and -0 -> +0), i.e. 1
+// instruction per value instead of 2.5.  Bit-identical to (__bf16)fmaxf(x, 0).
+__device__ __forceinline__ void relu_cvt_bf16x8(const float* v, void* dst) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  i16x2* d = reinterpret_cast<i16x2*>(dst);
+  const i16x2 z = {0, 0};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x2 p = {v[2 * q], v[2 * q + 1]};
+    const bf16x2 t = __builtin_convertvector(p, bf16x2);
+    d[q] = __builtin_elementwise_max(__builtin_bit_cast(i16x2, t), z);
+  }
+}
+
 __device__ __forceinline__ f32x16 mfma32(const bf16x8 a, const bf16x8 b, const f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -58,7 +84,7 @@ __device__ __forceinline__ void featurize_f32(const int4 rc, const int h, const 
     int wd = (days + 2) % 7;
     if (wd < 0) wd += 7;
     const float hour = (float)(sod / 3600);
-    const float km = __int_as_float(rc.x) / 1000.f;
+    const float km = __int_as_float(rc.x) * 1e-3f;   // not '/': an IEEE divide is ~10 VALU ops
     const float age = __int_as_float(rc.y);
     const float wdn = (float)wd * np.scale[0] + np.shift[0];
     const float hrn = hour * np.scale[1] + np.shift[1];
@@ -93,7 +119,7 @@ __device__ __forceinline__ void featurize8_f32(const int2 rc, const int h, const
   } else {
     const float wdn = (float)((pk >> 16) & 7) * np.scale[0] + np.shift[0];
     const float hrn = (float)((pk >> 19) & 31) * np.scale[1] + np.shift[1];
-    const float kmn = (__int_as_float(rc.x) / 1000.f) * np.scale[2] + np.shift[2];
+    const float kmn = (__int_as_float(rc.x) * 1e-3f) * np.scale[2] + np.shift[2];
     const float agn = __half2float(__ushort_as_half((unsigned short)(pk & 0xffffu))) * np.scale[3] +
                       np.shift[3];
     const float kmh = (float)(__bf16)kmn;
@@ -114,6 +140,36 @@ __device__ __forceinline__ bf16x8 to_bf16x8(const float f[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = (__bf16)f[j];
   return v;
+}
+
+// One-hot pair (weather, traffic) straight as bf16 B-fragment bits for lane half h = 0:
+// bf16(1.0) = 0x3F80 in slot c of each 4-wide group; an unknown category (c >= 4) gives all
+// zeros, like the reference's dummies of an unseen value (RO/Flaskr/ml.py:35-48).
+__device__ __forceinline__ bf16x8 onehot_pair_bf16(unsigned w, unsigned t) {
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  u64x2 v;
+  v[0] = w < 4u ? (0x3F80ull << (16u * w)) : 0ull;
+  v[1] = t < 4u ? (0x3F80ull << (16u * t)) : 0ull;
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Branch-free B fragment of lane half h, bit-identical to to_bf16x8(featurize*_f32(..., h, ...)):
+// both halves compute both feature groups and select (a divergent branch runs the two halves'
+// paths one after the other anyway), and the one-hot group costs a few VALU ops instead of ~20.
+__device__ __forceinline__ bf16x8 featurize_bf16(const int4 rc, const int h, const NormParams& np) {
+  float f[8];
+  featurize_f32(rc, 1, np, f);
+  const bf16x8 nb = to_bf16x8(f);
+  const bf16x8 oh = onehot_pair_bf16((unsigned)rc.w & 0xffu, ((unsigned)rc.w >> 8) & 0xffu);
+  return h == 0 ? oh : nb;
+}
+__device__ __forceinline__ bf16x8 featurize8_bf16(const int2 rc, const int h, const NormParams& np) {
+  float f[8];
+  featurize8_f32(rc, 1, np, f);
+  const bf16x8 nb = to_bf16x8(f);
+  const unsigned pk = (unsigned)rc.y;
+  const bf16x8 oh = onehot_pair_bf16((pk >> 24) & 7u, (pk >> 27) & 7u);
+  return h == 0 ? oh : nb;
 }
 
 // Unnormalised R16 features (12 columns, reference order) of one record — the K1 standalone op.

@@ -76,9 +76,7 @@ __global__ __launch_bounds__(512, 2) void eta_mlp3_train_fwd_kernel(
     const int row = tile * 32 + r;
     const bool valid = row < B;
     const int4 rc = valid ? rec[row] : make_int4(0, 0, 0, 0);
-    float f[8];
-    featurize_f32(rc, h, np, f);
-    const bf16x8 xb = to_bf16x8(f);
+    const bf16x8 xb = featurize_bf16(rc, h, np);
     if (valid)  // slots 14, 15 hold 1.0 (the b1 hi/lo inputs): dW1k[:,14] == db1
       *reinterpret_cast<bf16x8*>(xf + (size_t)row * 16 + 8 * h) = xb;
 
@@ -107,7 +105,7 @@ __global__ __launch_bounds__(512, 2) void eta_mlp3_train_fwd_kernel(
         bf16x8 hv;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float v = fmaxf(acc[8 * s + j], 0.f);
+          const float v = relu_f(acc[8 * s + j]);
           ys += v * w3[8 * s + j];
           hv[j] = (__bf16)v;
           mk |= (v > 0.f ? 1u : 0u) << (8 * s + j);

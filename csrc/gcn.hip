@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void gcn_agg_gemm_kernel(
       for (int e = 0; e < 16; ++e) {
         const int v = base + (e & 3) + 8 * (e >> 2) + 4 * h;
         float o = acc[e] + b;
-        if (RELU) o = fmaxf(o, 0.f);
+        if (RELU) o = relu_f(o);
         if (v < row1) Y[(size_t)v * FOUT + n] = (__bf16)o;
       }
     }

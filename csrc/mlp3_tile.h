@@ -89,11 +89,11 @@ __device__ __forceinline__ void mlp3_layer1(const W1Frags<H>& w1, const bf16x8 x
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
     acc = mfma32(w1.f[mt], xb, acc);
+    float a[16];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) h1[2 * mt + s][j] = (__bf16)fmaxf(acc[8 * s + j], 0.f);
-    }
+    for (int e = 0; e < 16; ++e) a[e] = acc[e];
+    relu_cvt_bf16x8(a, &h1[2 * mt]);
+    relu_cvt_bf16x8(a + 8, &h1[2 * mt + 1]);
   }
 }
 
@@ -101,12 +101,17 @@ __device__ __forceinline__ void mlp3_layer1(const W1Frags<H>& w1, const bf16x8 x
 // boundaries (fragment f = mt*KS + ks; loads for f+1..f+4 are in flight while f feeds the MFMA),
 // so no MFMA waits on the LDS read issued just before it.  epi(mt, acc) consumes each finished
 // 32-row pre-activation tile z2^T[32mt..32mt+31][batch].
-template <int H, bool PIN = false, typename Epi>
+//
+// PIPE = true software-pipelines the epilogue: epi(mt - 1) is issued after the first MFMA group of
+// tile mt, so its VALU work (relu, dot with w3, ...) can fill the issue slots inside this wave's
+// own MFMA gaps instead of running while the SIMD's matrix core idles.
+template <int H, bool PIN = false, bool PIPE = false, typename Epi>
 __device__ __forceinline__ void mlp3_layer2(const Mlp3View<H>& w, const bf16x8 (&h1)[H / 16],
                                             int lane, int h, Epi&& epi) {
   constexpr int MT = H / 32, KS = H / 16, NF = MT * KS, D = 4;
   const bf16x8* wa = w.w2p + lane;
   bf16x8 r0 = wa[0 * 64], r1 = wa[1 * 64], r2 = wa[2 * 64], r3 = wa[3 * 64];
+  f32x16 prev;
 #pragma unroll 1
   for (int mt = 0; mt < MT; ++mt) {
     f32x16 acc = load_vec16(w.b2p, mt, h);
@@ -130,9 +135,14 @@ __device__ __forceinline__ void mlp3_layer2(const Mlp3View<H>& w, const bf16x8 (
         __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
       }
+      if constexpr (PIPE) {
+        if (ks == 0 && mt > 0) epi(mt - 1, prev);
+      }
     }
-    epi(mt, acc);
+    if constexpr (PIPE) prev = acc;
+    else epi(mt, acc);
   }
+  if constexpr (PIPE) epi(MT - 1, prev);
 }
 
 }  // namespace rt

@@ -17,13 +17,15 @@ from __future__ import annotations
 import asyncio
 import datetime as dt
 import json
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
 
 from fastapi import FastAPI, Request
 from fastapi.middleware.cors import CORSMiddleware
-from fastapi.responses import JSONResponse, PlainTextResponse, Response, StreamingResponse
+from fastapi.responses import (HTMLResponse, JSONResponse, PlainTextResponse, Response,
+                               StreamingResponse)
 from starlette.concurrency import run_in_threadpool
 
 from ..config import Settings, get_settings
@@ -554,5 +556,25 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         except Exception as e:
             return JSONResponse({"error": f"delete failed: {e}"}, 500)
         return Response(status_code=204)
+
+    # ------------------------------------------------------------------ built-in dashboard (F01-F09)
+    ui_cache: Dict[str, str] = {}
+
+    def _dashboard() -> HTMLResponse:
+        if "html" not in ui_cache:
+            with open(os.path.join(os.path.dirname(__file__), "static", "dashboard.html"), encoding="utf-8") as f:
+                ui_cache["html"] = f.read()
+        return HTMLResponse(ui_cache["html"])
+
+    @app.get("/ui", include_in_schema=False)
+    @app.get("/ui/", include_in_schema=False)
+    @app.get("/ui/history", include_in_schema=False)
+    @app.get("/ui/health", include_in_schema=False)
+    async def ui_page():
+        return _dashboard()
+
+    @app.get("/ui/history/{req_id}", include_in_schema=False)
+    async def ui_history_detail(req_id: str):
+        return _dashboard()
 
     return app

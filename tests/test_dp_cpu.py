@@ -1,4 +1,4 @@
-"""Data-parallel training logic on CPU with Gloo (world_size 2/4, torch.multiprocessing.spawn):
+"""Data-parallel training logic on CPU with Gloo (world_size 2/4/8, torch.multiprocessing.spawn):
 the flat-bucket all-reduce must give exactly the single-process large-batch gradient, all ranks
 must end with identical weights, and checkpoints must resume."""
 import os
@@ -55,7 +55,7 @@ def _grad_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_gradient_equals_large_batch(world):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_grad_worker, args=(world, _free_port(), d), nprocs=world, join=True)
