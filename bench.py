@@ -6,11 +6,14 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
 ``torch.distributed.run`` with one rank per GPU (RCCL backend).  Each rank scores a fixed
 per-GPU batch of packed synthetic trip records every step (weak scaling):
 
-    step = ONE fused featurize+MLP HIP launch (K1+K2) that reads the raw 16-byte request records
-           straight from pinned host memory and writes the predicted minutes straight back to
-           pinned host memory over PCIe (zero-copy: no copy-engine transfers; each wave prefetches
-           its next tile's records while computing the current one)
+    step = the records of B requests go host -> HBM on the copy engine (one DMA on its own
+           stream: large PCIe read TLPs, ~54 GB/s), then ONE fused featurize+MLP HIP launch
+           (K1+K2) scores them from HBM and writes the predicted minutes straight into pinned host
+           memory (zero-copy posted writes over the link's other direction).  Three slots are
+           pipelined, so the copy of step k+1 overlaps the kernel of step k.
 
+``--io zerocopy`` has the kernel read the records from pinned host memory itself (the PCIe read
+direction then runs ~64-byte requests and tops out ~20 % lower, profiles/zerocopy_probe_r1.jsonl);
 ``--io host`` instead pipelines copy-engine H2D / kernel / D2H over three HIP streams;
 ``--io device`` scores HBM-resident records (kernel-only; reported as an extra field too).  K steps are timed between a barrier +
 ``torch.cuda.synchronize()`` on both sides; the max over ranks is reported by rank 0 as ONE JSON
@@ -36,13 +39,15 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1 << 23, help="rows per GPU per step")
     ap.add_argument("--hidden", type=int, default=256)
-    ap.add_argument("--io", choices=["zerocopy", "host", "device"], default="zerocopy",
+    ap.add_argument("--io", choices=["zerocopy", "hybrid", "host", "device"], default="hybrid",
                     help="zerocopy: the kernel reads pinned host records and writes pinned host "
                          "predictions over PCIe; host: copy-engine H2D/D2H pipeline; device: "
                          "records already resident in HBM")
     ap.add_argument("--rec", type=int, choices=[8, 16], default=8,
                     help="wire record bytes per request (8: compact, 16: full with epoch seconds)")
     ap.add_argument("--variant", type=int, default=-1)
+    ap.add_argument("--h2d-streams", type=int, default=1,
+                    help="hybrid: split each step's record copy over this many copy streams")
     ap.add_argument("--p50", type=int, default=1, help="measure single-request p50 latency")
     ap.add_argument("--p50-requests", type=int, default=2000)
     return ap.parse_args()
@@ -99,6 +104,8 @@ def main() -> None:
     h2d_done = [torch.cuda.Event() for _ in range(nbuf)]
     comp_done = [torch.cuda.Event() for _ in range(nbuf)]
     d2h_done = [torch.cuda.Event() for _ in range(nbuf)]
+    h2d_extra = [torch.cuda.Stream(dev) for _ in range(max(0, a.h2d_streams - 1))]
+    h2d_parts = [[torch.cuda.Event() for _ in range(nbuf)] for _ in range(a.h2d_streams)]
     for i in range(nbuf):
         dev_rec[i].copy_(host_rec)
     torch.cuda.synchronize()
@@ -108,6 +115,21 @@ def main() -> None:
         if a.io == "zerocopy":
             with torch.cuda.stream(comp_s):
                 kern.forward_hostio(host_rec, host_out[k])
+        elif a.io == "hybrid":
+            # records in by DMA (large PCIe read TLPs), minutes out as the kernel's own posted
+            # writes over the other link direction
+            n = len(h2d_extra) + 1
+            for j, cs in enumerate([h2d_s] + h2d_extra):
+                lo, hi = B * j // n, B * (j + 1) // n
+                with torch.cuda.stream(cs):
+                    cs.wait_event(comp_done[k])         # slot k's records consumed
+                    dev_rec[k][lo:hi].copy_(host_rec[lo:hi], non_blocking=True)
+                    h2d_parts[j][k].record(cs)
+            with torch.cuda.stream(comp_s):
+                for j in range(n):
+                    comp_s.wait_event(h2d_parts[j][k])
+                kern.forward_hostio(dev_rec[k], host_out[k])
+                comp_done[k].record(comp_s)
         elif a.io == "host":
             with torch.cuda.stream(h2d_s):
                 h2d_s.wait_event(comp_done[k])          # slot k's records consumed

@@ -101,6 +101,35 @@ def test_mlp3_forward_zero_copy_host_io(variant, B):
     assert torch.equal(out, ref)
 
 
+def test_mlp3_forward_mixed_placement():
+    """Hybrid serving: HBM records (copy engine) + zero-copy minutes out, and the reverse."""
+    m = _model(256, 5)
+    k = EtaMlpKernel(m, torch.device("cuda:0"))
+    rec, _ = synth_records(100_003, 23)
+    dev = records_to_tensor(rec).cuda()
+    ref = k(dev).cpu()
+    out = torch.full((len(rec),), float("nan")).pin_memory()
+    k.forward_hostio(dev, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    dout = torch.full((len(rec),), float("nan"), device="cuda")
+    k.forward_hostio(dev.cpu().pin_memory(), dout)
+    torch.cuda.synchronize()
+    assert torch.equal(dout.cpu(), ref)
+    with pytest.raises(RuntimeError):
+        k.forward_hostio(dev.cpu(), out)           # pageable host memory is refused
+
+
+@pytest.mark.parametrize("variant", [5, 7, 8])
+def test_mlp3_forward_experimental_variants_match(variant):
+    m = _model(256, 6)
+    rec, _ = synth_records(200_001, 24)
+    rt = records_to_tensor(rec).cuda()
+    ref = EtaMlpKernel(m, torch.device("cuda:0"), variant=3)(rt)
+    got = EtaMlpKernel(m, torch.device("cuda:0"), variant=variant)(rt)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("variant", [0, 1, 3])
 def test_mlp3_forward_compact_records(variant):
     from routest_amd.models.features import compact_to_features, records_to_compact
