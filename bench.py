@@ -184,6 +184,7 @@ def main() -> None:
 
     p50_ms = p99_ms = None
     p50_fastapi_ms = None
+    p50_py_ms = None
     conc = None
     if a.p50 and rank == 0:
         # (1) headline p50: real HTTP/1.1 over loopback (keep-alive, http.client) to the native
@@ -191,45 +192,39 @@ def main() -> None:
         #     kernel on this GPU (zero-copy) -> C++ response formatting.  Same endpoint semantics
         #     as the FastAPI handler (byte-identical bodies, tests/test_native_server_gpu.py).
         import http.client
-        import threading
         from routest_amd.serve.native_server import NativePredictServer
         body = {"summary": {"distance": 12345}, "pickup_time": "2026-10-15T08:30:00",
                 "driver_age": 34, "weather": "Sunny", "traffic": "Medium"}
         raw = json.dumps(body).encode()
         hdr = {"Content-Type": "application/json"}
         with NativePredictServer(model, device=local_rank, threads=4) as srv:
+            # native closed-loop client (csrc/runtime/http_client.h): one keep-alive connection,
+            # one request in flight — the client adds ~1 us instead of http.client's ~30 us
+            from routest_amd.ops import _ext
+            rtm = _ext.runtime(required=True)
+            r1 = rtm.http_load(srv.port, 1, 30.0, "/api/predict_eta", raw.decode(), 1,
+                               a.p50_requests, 200)
+            assert r1["errors"] == 0 and r1["requests"] >= a.p50_requests, r1
+            lat = r1["latencies_us"]
+            p50_ms = float(lat[len(lat) // 2]) * 1e-3
+            p99_ms = float(lat[int(len(lat) * 0.99) - 1]) * 1e-3
+            # the same with Python's http.client (what a Python caller would see)
             conn = http.client.HTTPConnection("127.0.0.1", srv.port)
-            lat = []
-            for j in range(a.p50_requests + 200):
+            latp = []
+            for j in range(a.p50_requests // 2 + 200):
                 t1 = time.perf_counter()
                 conn.request("POST", "/api/predict_eta", body=raw, headers=hdr)
                 r = conn.getresponse()
                 r.read()
                 if j >= 200:
-                    lat.append(time.perf_counter() - t1)
+                    latp.append(time.perf_counter() - t1)
                 assert r.status == 200
-            lat.sort()
-            p50_ms = lat[len(lat) // 2] * 1e3
-            p99_ms = lat[int(len(lat) * 0.99) - 1] * 1e3
-            # concurrent single-item clients (separate connections; the reactors batch them)
-            done = []
-            stop_at = time.perf_counter() + 2.0
-
-            def client():
-                c = http.client.HTTPConnection("127.0.0.1", srv.port)
-                n = 0
-                while time.perf_counter() < stop_at:
-                    c.request("POST", "/api/predict_eta", body=raw, headers=hdr)
-                    c.getresponse().read()
-                    n += 1
-                done.append(n)
-            th = [threading.Thread(target=client) for _ in range(16)]
-            t1 = time.perf_counter()
-            for t_ in th:
-                t_.start()
-            for t_ in th:
-                t_.join()
-            conc = sum(done) / (time.perf_counter() - t1)
+            latp.sort()
+            p50_py_ms = latp[len(latp) // 2] * 1e3
+            # 16 concurrent single-item clients (separate connections; the reactors batch them)
+            r16 = rtm.http_load(srv.port, 16, 2.0, "/api/predict_eta", raw.decode(), 4, 0, 50)
+            assert r16["errors"] == 0, r16
+            conc = r16["requests"] / r16["seconds"]
 
         # (2) the FastAPI app in-process over ASGI (like the reference's Flask test-client figure)
         import asyncio
@@ -279,7 +274,8 @@ def main() -> None:
             "kernel_only_preds_per_s_per_gpu": kernel_preds_per_s,
             "p50_predict_ms": p50_ms,
             "p99_predict_ms": p99_ms,
-            "p50_path": "HTTP/1.1 loopback keep-alive POST /api/predict_eta -> native front end (C++ reactor, fused HIP kernel)",
+            "p50_path": "HTTP/1.1 loopback keep-alive POST /api/predict_eta -> native front end (C++ reactor, fused HIP kernel); native closed-loop client",
+            "p50_python_client_ms": p50_py_ms,
             "p50_fastapi_asgi_ms": p50_fastapi_ms,
             "http_concurrent16_req_per_s": conc,
             "finite": ok,

@@ -29,6 +29,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -53,6 +54,11 @@ struct ServerCfg {
   const void* blob = nullptr;          // this reactor's device + weight blob (one copy per GPU)
   NormParams np{};
   int max_batch = 1 << 20;
+  int persist_cap = 1024;              // rounds of up to this many rows use the resident scorer
+  double persist_idle_ms = 20.0;       // (0 = off); it exits after this long without a request
+  double persist_life_ms = 50.0;       // ... or after this long resident (then relaunched)
+  PersistentScorer* scorer = nullptr;  // one per GPU, shared by that GPU's reactors
+  std::mutex* scorer_mu = nullptr;
   std::vector<std::string> cors_exact;
   bool cors_vercel = true;
 };
@@ -76,7 +82,7 @@ struct Pending {
 };
 
 struct Stats {
-  std::atomic<long long> requests{0}, predictions{0}, launches{0}, errors{0};
+  std::atomic<long long> requests{0}, predictions{0}, launches{0}, errors{0}, resident{0}, fallbacks{0};
 };
 
 inline Stamp now_local() {
@@ -138,6 +144,7 @@ class Reactor {
     if (hipHostGetDevicePointer(&d_rec_, h_rec_, 0) != hipSuccess ||
         hipHostGetDevicePointer((void**)&d_out_, h_out_, 0) != hipSuccess)
       return;
+
     epoll_event evs[256];
     while (!stop_.load(std::memory_order_relaxed)) {
       const int n = epoll_wait(ep_, evs, 256, 100);
@@ -427,9 +434,31 @@ class Reactor {
   void run_batch() {
     if (pending_.empty()) return;
     if (nrec_ > 0) {
-      hipError_t e = launch_eta_mlp3_fwd(d_rec_, d_out_, (int)nrec_, cfg_.blob, cfg_.H, cfg_.np,
-                                         cfg_.variant, cfg_.num_cus, stream_, false);
-      if (e == hipSuccess) e = hipStreamSynchronize(stream_);
+      hipError_t e = hipErrorNotReady;
+      PersistentScorer* ps = cfg_.scorer;
+      if (ps != nullptr && (int)nrec_ <= pscore_cap(ps)) {
+        // small round: the resident kernel (no dispatch, weights already in LDS, no stream sync)
+        std::lock_guard<std::mutex> lk(*cfg_.scorer_mu);
+        if (!pscore_broken(ps)) {
+          std::memcpy(pscore_records(ps), h_rec_, nrec_ * sizeof(EtaRecord));
+          e = pscore_run(ps, (int)nrec_, 200.0);
+          if (e == hipSuccess) {
+            std::memcpy(h_out_, pscore_out(ps), nrec_ * sizeof(float));
+            st_.resident.fetch_add(1, std::memory_order_relaxed);
+          } else {
+            st_.fallbacks.fetch_add(1, std::memory_order_relaxed);
+          }
+        }
+      }
+      if (e != hipSuccess) {
+        if (ps != nullptr) {            // keep a hardware queue it may share free for this launch
+          std::lock_guard<std::mutex> lk(*cfg_.scorer_mu);
+          pscore_park(ps);
+        }
+        e = launch_eta_mlp3_fwd(d_rec_, d_out_, (int)nrec_, cfg_.blob, cfg_.H, cfg_.np, cfg_.variant,
+                                cfg_.num_cus, stream_, false);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream_);
+      }
       st_.launches.fetch_add(1, std::memory_order_relaxed);
       if (e != hipSuccess) {
         std::vector<Pending> failed;
@@ -499,6 +528,11 @@ struct Server {
   std::atomic<bool> stop{false};
   std::vector<std::unique_ptr<Reactor>> reactors;
   std::vector<std::thread> threads;
+  std::vector<PersistentScorer*> scorers;
+  std::vector<std::unique_ptr<std::mutex>> scorer_mus;
+  ~Server() {
+    for (PersistentScorer* p : scorers) pscore_destroy(p);   // stop + wait for the resident kernels
+  }
 };
 
 std::mutex g_srv_mu;
@@ -523,12 +557,27 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
   s->cfg.max_batch = max_batch;
   s->cfg.cors_exact = cors;
   s->cfg.cors_vercel = cors_vercel;
+  if (const char* v = std::getenv("ROUTEST_PERSIST_IDLE_MS")) s->cfg.persist_idle_ms = std::atof(v);
+  if (const char* v = std::getenv("ROUTEST_PERSIST_CAP")) s->cfg.persist_cap = std::atoi(v);
+  if (const char* v = std::getenv("ROUTEST_PERSIST_LIFE_MS")) s->cfg.persist_life_ms = std::atof(v);
+  if (s->cfg.persist_idle_ms > 0 && s->cfg.persist_cap > 0) {
+    for (size_t g = 0; g < devices.size(); ++g) {
+      hipError_t e = hipSuccess;
+      s->scorers.push_back(pscore_create(devices[g], blobs[g], H, np, s->cfg.persist_cap, s->cfg.persist_idle_ms,
+                                         s->cfg.persist_life_ms, &e));   // nullptr on failure: normal launches
+      s->scorer_mus.push_back(std::make_unique<std::mutex>());
+    }
+  }
   for (int i = 0; i < s->cfg.threads; ++i) {
     ServerCfg rc = s->cfg;                       // reactors are spread round-robin over the GPUs
     const size_t g = (size_t)i % devices.size();
     rc.device = devices[g];
     rc.blob = blobs[g];
     rc.num_cus = num_cus[g];
+    if (!s->scorers.empty()) {
+      rc.scorer = s->scorers[g];
+      rc.scorer_mu = s->scorer_mus[g].get();
+    }
     auto r = std::make_unique<Reactor>(rc, s->stats, s->stop);
     r->set_bind_any(bind_any);
     if (!r->init(err)) {
@@ -561,15 +610,17 @@ void native_server_stop(int64_t h) {
   delete s;
 }
 
-void native_server_stats(int64_t h, long long out[4]) {
+void native_server_stats(int64_t h, long long out[6]) {
   std::lock_guard<std::mutex> lk(g_srv_mu);
-  out[0] = out[1] = out[2] = out[3] = 0;
+  out[0] = out[1] = out[2] = out[3] = out[4] = out[5] = 0;
   if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return;
   Server* s = g_servers[h];
   out[0] = s->stats.requests.load();
   out[1] = s->stats.predictions.load();
   out[2] = s->stats.launches.load();
   out[3] = s->stats.errors.load();
+  out[4] = s->stats.resident.load();
+  out[5] = s->stats.fallbacks.load();
 }
 
 }  // namespace rt

@@ -78,13 +78,26 @@ hipError_t launch_greedy_cvrp(const double* D, const int* npts, const double* de
                               const double* cap, const double* maxd, int R, int NM, int* visit,
                               int* trip_of, int* ntrips, int* status, hipStream_t stream);
 
+// ---- persistent single-request scorer : persistent_serve.hip ----
+struct PersistentScorer;
+PersistentScorer* pscore_create(int device, const void* blob, int H, const NormParams& np, int cap,
+                                double idle_ms, double life_ms, hipError_t* err);
+void pscore_park(PersistentScorer* s);
+void* pscore_records(PersistentScorer* s);
+const float* pscore_out(PersistentScorer* s);
+int pscore_cap(PersistentScorer* s);
+bool pscore_broken(PersistentScorer* s);
+void pscore_stats(PersistentScorer* s, long long* launches, long long* served, long long* fallbacks);
+hipError_t pscore_run(PersistentScorer* s, int n, double timeout_ms);
+void pscore_destroy(PersistentScorer* s);
+
 // ---- native prediction front end : native_server.hip ----
 int64_t native_server_start(int port, int threads, const std::vector<int>& devices,
                             const std::vector<const void*>& blobs, const std::vector<int>& num_cus, int H,
                             const NormParams& np, int variant, int max_batch, const std::vector<std::string>& cors,
                             bool cors_vercel, bool bind_any, std::string& err);
 void native_server_stop(int64_t h);
-void native_server_stats(int64_t h, long long out[4]);
+void native_server_stats(int64_t h, long long out[6]);
 
 // ---- native collectives (rccl_ops) : comm.hip ----
 int comm_unique_id(char out[128]);

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "rt_core.h"
+#include "http_client.h"
 
 namespace py = pybind11;
 
@@ -317,8 +318,28 @@ py::tuple astar_batch(py::array_t<int32_t> indptr, py::array_t<int32_t> indices,
   return py::make_tuple(out, paths);
 }
 
+// Native closed-loop HTTP client (bench.py p50, load sweeps): returns the sorted latencies (us) and
+// counters; the GIL is released while the sockets run.
+py::dict py_http_load(int port, int connections, double seconds, const std::string& path, const std::string& body,
+                   int threads, long long max_requests, int warmup) {
+  rtc::LoadResult r;
+  {
+    py::gil_scoped_release nogil;
+    r = rtc::http_load(port, connections, seconds, path, body, threads, max_requests, warmup);
+  }
+  py::dict d;
+  d["seconds"] = r.seconds;
+  d["requests"] = r.requests;
+  d["errors"] = r.errors;
+  d["latencies_us"] = py::array_t<float>(r.lat_us.size(), r.lat_us.data());
+  return d;
+}
+
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "routest_amd CPU native runtime";
+  m.def("http_load", &py_http_load, py::arg("port"), py::arg("connections") = 1, py::arg("seconds") = 2.0,
+        py::arg("path") = "/api/predict_eta", py::arg("body") = "", py::arg("threads") = 1,
+        py::arg("max_requests") = 0, py::arg("warmup") = 0);
   m.def("pack_predict_batch", &pack_predict_batch, py::arg("body"), py::arg("now_secs"), py::arg("now_us"));
   m.def("format_predict_batch", &format_predict_batch);
   m.def("iso_parse", &iso_parse);

@@ -50,8 +50,11 @@ class NativePredictServer:
     def stats(self) -> Dict[str, int]:
         if self.h is None:
             return {}
-        r, p, l, e = self.C.native_server_stats(self.h)
-        return {"requests": r, "predictions": p, "launches": l, "errors": e}
+        r, p, l, e, res, fb = self.C.native_server_stats(self.h)
+        # resident: rounds scored by the persistent kernel (csrc/persistent_serve.hip);
+        # fallbacks: rounds it did not answer in time, re-scored by a normal launch
+        return {"requests": r, "predictions": p, "launches": l, "errors": e, "resident": res,
+                "fallbacks": fb}
 
     def close(self) -> None:
         if self.h is not None:

@@ -134,3 +134,37 @@ def test_concurrent_clients_batch(stack):
     after = srv.stats()
     assert after["predictions"] - before["predictions"] == 3200
     assert after["launches"] - before["launches"] <= 3200           # batching across connections
+
+
+def test_resident_scorer_serves_small_rounds(stack):
+    """Small rounds go to the persistent kernel (csrc/persistent_serve.hip), never falling back."""
+    srv, client = stack
+    before = srv.stats()
+    conn = http.client.HTTPConnection("127.0.0.1", srv.port, timeout=10)
+    ref = client.post("/api/predict_eta", json=BODY).content
+    for _ in range(50):
+        st, body, _ = _post(srv.port, "/api/predict_eta", BODY, conn=conn)
+        assert st == 200 and body == ref
+    after = srv.stats()
+    assert after["resident"] - before["resident"] >= 50
+    assert after["fallbacks"] == 0
+
+
+def test_resident_scorer_idle_exit_and_relaunch(monkeypatch):
+    """With a 2 ms idle timeout the resident kernel exits between requests; the next request
+    relaunches it and is still answered by it (no fallback)."""
+    import time
+    from routest_amd.serve.eta_service import default_model
+    from routest_amd.serve.native_server import NativePredictServer
+    monkeypatch.setenv("ROUTEST_PERSIST_IDLE_MS", "2")
+    model = default_model(steps=10)
+    with NativePredictServer(model, device=0, threads=1) as srv:
+        outs = []
+        for _ in range(5):
+            st, body, _ = _post(srv.port, "/api/predict_eta", BODY)
+            assert st == 200
+            outs.append(json.loads(body)["eta_minutes_ml"])
+            time.sleep(0.03)
+        stats = srv.stats()
+    assert len(set(outs)) == 1
+    assert stats["resident"] == 5 and stats["fallbacks"] == 0

@@ -131,7 +131,7 @@ def build_tools(force: bool = False) -> str:
     src = os.path.join(CSRC, "tools", "loadgen.cpp")
     out = os.path.join(BUILD, "loadgen")
     os.makedirs(BUILD, exist_ok=True)
-    if force or _newer(out, [src]):
+    if force or _newer(out, [src, os.path.join(CSRC, "runtime", "http_client.h")]):
         _run(["g++", "-O2", "-std=c++17", "-pthread", src, "-o", out])
     return out
 
