@@ -8,6 +8,8 @@
 #include <c10/core/DeviceGuard.h>
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "ops.h"
@@ -424,6 +426,55 @@ torch::Tensor forest_predict(torch::Tensor records, torch::Tensor values, torch:
   return out;
 }
 
+// ---------------------------------------------------------------- resident scorer (persistent_serve.hip)
+std::mutex g_ps_mu;
+std::vector<rt::PersistentScorer*> g_ps;
+
+rt::PersistentScorer* ps_get(int64_t h) {
+  std::lock_guard<std::mutex> lk(g_ps_mu);
+  TORCH_CHECK(h >= 0 && h < (int64_t)g_ps.size() && g_ps[h] != nullptr, "bad resident scorer handle");
+  return g_ps[h];
+}
+
+int64_t pscore_create(torch::Tensor blob, int64_t H, std::vector<double> norm, int64_t cap, double idle_ms,
+                      double life_ms) {
+  check_dev(blob, "blob");
+  TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
+  TORCH_CHECK(norm.size() == 8, "norm must hold 4 scales + 4 shifts");
+  rt::NormParams np;
+  for (int i = 0; i < 4; ++i) {
+    np.scale[i] = (float)norm[i];
+    np.shift[i] = (float)norm[4 + i];
+  }
+  hipError_t e = hipSuccess;
+  rt::PersistentScorer* p = rt::pscore_create((int)blob.device().index(), blob.data_ptr(), (int)H, np, (int)cap,
+                                              idle_ms, life_ms, &e);
+  TORCH_CHECK(p != nullptr, "resident scorer: ", hipGetErrorString(e));
+  std::lock_guard<std::mutex> lk(g_ps_mu);
+  g_ps.push_back(p);
+  return (int64_t)g_ps.size() - 1;
+}
+
+// rec: CPU int32 [n,4] (16-byte records), out: CPU f32 [n].  False when the scorer did not answer
+// (the caller then scores with a normal launch).  Not thread-safe per handle (callers hold a lock).
+bool pscore_score(int64_t h, torch::Tensor rec, torch::Tensor out) {
+  rt::PersistentScorer* p = ps_get(h);
+  TORCH_CHECK(!rec.is_cuda() && rec.is_contiguous() && rec.scalar_type() == torch::kInt32 && rec.dim() == 2 &&
+                  rec.size(1) == 4, "rec must be contiguous CPU int32 [n,4]");
+  TORCH_CHECK(!out.is_cuda() && out.is_contiguous() && out.scalar_type() == torch::kFloat32 &&
+                  out.numel() == rec.size(0), "out must be contiguous CPU f32 [n]");
+  const int n = (int)rec.size(0);
+  if (n > rt::pscore_cap(p) || rt::pscore_broken(p)) return false;
+  hipError_t e;
+  {
+    py::gil_scoped_release nogil;
+    std::memcpy(rt::pscore_records(p), rec.data_ptr(), (size_t)n * 16);
+    e = rt::pscore_run(p, n, 200.0);
+    if (e == hipSuccess) std::memcpy(out.data_ptr(), rt::pscore_out(p), (size_t)n * 4);
+  }
+  return e == hipSuccess;
+}
+
 // ---------------------------------------------------------------- native predict server
 int64_t native_server_start(int64_t port, int64_t threads, std::vector<torch::Tensor> blobs, int64_t H,
                             std::vector<double> norm, int64_t variant, int64_t max_batch,
@@ -570,6 +621,29 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("inv_vmax"), py::arg("landmarks") = py::none(), py::arg("out_iters") = py::none());
   m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
   m.def("forest_predict_lds", &forest_predict_lds, "K4: LDS-staged tree chunks, 2 walks per thread");
+  m.def("pscore_create", &pscore_create, "resident single-request scorer kernel on the blob's GPU");
+  m.def("pscore_score", &pscore_score, "score n <= cap records on the resident scorer (False: not answered)");
+  m.def("pscore_park", [](int64_t h) {
+    rt::PersistentScorer* p = ps_get(h);
+    py::gil_scoped_release nogil;
+    rt::pscore_park(p);
+  });
+  m.def("pscore_stats", [](int64_t h) {
+    long long l, s, f;
+    rt::pscore_stats(ps_get(h), &l, &s, &f);
+    return std::vector<int64_t>{l, s, f};
+  });
+  m.def("pscore_destroy", [](int64_t h) {
+    rt::PersistentScorer* p = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(g_ps_mu);
+      if (h < 0 || h >= (int64_t)g_ps.size()) return;
+      p = g_ps[h];
+      g_ps[h] = nullptr;
+    }
+    py::gil_scoped_release nogil;
+    rt::pscore_destroy(p);
+  });
   m.def("native_server_start", &native_server_start, "native HTTP front end for /api/predict_eta and /predict");
   m.def("native_server_stop", [](int64_t h) {
     py::gil_scoped_release nogil;

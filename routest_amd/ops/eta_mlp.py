@@ -221,3 +221,48 @@ class EtaMlpKernel:
                                             self.variant)
         with torch.no_grad():
             return self.model_cpu(featurize_torch(rec))
+
+
+class ResidentScorer:
+    """The resident single-request scorer (``csrc/persistent_serve.hip``) for one packed MLP: a
+    persistent 8-wave workgroup keeps the weights in LDS and takes rounds of up to ``cap``
+    16-byte records through a doorbell in pinned host memory — no kernel dispatch and no stream
+    synchronisation per request.  It exits after ``idle_ms`` without work or ``life_ms`` of
+    residency and is relaunched on demand.  :meth:`score` returns ``None`` when it did not answer
+    (the caller then launches the normal kernel); call :meth:`park` before large launches on the
+    same GPU."""
+
+    def __init__(self, kernel: "EtaMlpKernel", cap: int = 1024, idle_ms: float = 20.0,
+                 life_ms: float = 50.0):
+        self._C = kernel._C
+        self.cap = cap
+        self.h: Optional[int] = self._C.pscore_create(kernel.packed.blob, kernel.hidden,
+                                                      list(kernel.packed.norm), cap, idle_ms, life_ms)
+
+    def score(self, rec_i32: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+        n = rec_i32.shape[0]
+        if self.h is None or n > self.cap:
+            return None
+        out = torch.empty(n, dtype=torch.float32) if out is None else out
+        return out if self._C.pscore_score(self.h, rec_i32, out) else None
+
+    def park(self) -> None:
+        if self.h is not None:
+            self._C.pscore_park(self.h)
+
+    def stats(self) -> dict:
+        if self.h is None:
+            return {}
+        l, s, f = self._C.pscore_stats(self.h)
+        return {"launches": l, "served": s, "fallbacks": f}
+
+    def close(self) -> None:
+        if self.h is not None:
+            self._C.pscore_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -152,3 +152,37 @@ def test_mlp3_forward_compact_records(variant):
     k.forward_hostio(host, out)
     torch.cuda.synchronize()
     assert torch.equal(out, got)
+
+
+def test_resident_scorer_matches_kernel():
+    from routest_amd.ops.eta_mlp import ResidentScorer
+    m = _model(256, 7)
+    k = EtaMlpKernel(m, torch.device("cuda:0"))
+    rec, _ = synth_records(300, 25)
+    rt = records_to_tensor(rec)
+    ref = k(rt.cuda()).cpu()
+    rs = ResidentScorer(k, cap=256)
+    try:
+        assert rs.score(rt[:256]) is not None
+        assert torch.equal(rs.score(rt[:256]), ref[:256])
+        assert rs.score(rt) is None                       # above cap: caller launches normally
+        rs.park()                                         # exits; the next round relaunches it
+        assert torch.equal(rs.score(rt[100:101]), ref[100:101])
+        st = rs.stats()
+        assert st["served"] == 3 and st["fallbacks"] == 0 and st["launches"] == 2
+    finally:
+        rs.close()
+
+
+def test_gpu_runner_small_rounds_resident_large_rounds_launch():
+    from routest_amd.serve.batcher import GpuRunner
+    m = _model(256, 8)
+    k = EtaMlpKernel(m, torch.device("cuda:0"))
+    run = GpuRunner(k, torch.device("cuda:0"), 4096)
+    rec, _ = synth_records(3000, 26)
+    ref = k(records_to_tensor(rec).cuda()).cpu().numpy()
+    assert np.array_equal(run(rec[:7]), ref[:7])
+    assert np.array_equal(run(rec), ref)
+    assert np.array_equal(run(rec[5:6]), ref[5:6])
+    assert run.resident is not None and run.resident.stats()["served"] == 2
+    run.resident.close()
