@@ -6,8 +6,8 @@
 //   * dense per-slot state[N]: one 8-byte word (g as f32 | parent, closed bit) per node, so a
 //     relaxation is one random access — 80k slots x 100k nodes = 64 GB, which 288 GB of HBM3E makes
 //     the simple and fast choice (no hashing);
-//   * a binary min-heap of (f, node) 64-bit entries with lazy deletion (stale pops are skipped via
-//     the closed bit; the heuristic is consistent, so a node's first pop is final);
+//   * an 8-ary min-heap (LaneHeap) of (f, node) 64-bit entries with lazy deletion (stale pops are
+//     skipped via the closed bit; the heuristic is consistent, so a node's first pop is final);
 //   * a touched list, so only the entries a search wrote are reset afterwards (no N-sized memset
 //     per query).
 // Launch time is set by the LONGEST search (one lane walks its own heap), so the heuristic matters
@@ -18,6 +18,8 @@
 // shrunk by 1e-4 against fp32 rounding).  Every lane stops within max_iters pops (status 3), on heap
 // or touched-list overflow (status 2) or when the open set empties (status 1): the grid always
 // drains.  Paths are written target->source then reversed in place.
+#include <cstdlib>
+
 #include "common.h"
 #include "ops.h"
 
@@ -87,7 +89,80 @@ __device__ __forceinline__ unsigned long long hkey(float f, int v) {
   return ((unsigned long long)__float_as_uint(f) << 32) | (unsigned)v;   // f >= 0: monotone bits
 }
 
-template <int K>
+// D-ary min-heap of 64-bit (f, node) keys in this lane's HBM row.  Every pop/push is a chain of
+// DEPENDENT random loads (a lane walks its own heap), so the heap depth, not bandwidth, sets the
+// per-pop time.  With the storage shifted by D-1 the D children of a node are one aligned block
+// (D/2 independent 16-byte loads, one memory latency per level).  80k-leg launch
+// (bench/astar_tail.py): binary 378 ms, 4-ary 311-323 ms, 8-ary (default) 303 ms;
+// ROUTEST_ASTAR_ARITY=2|4|8 selects.
+template <int D>
+struct LaneHeap {
+  static constexpr int OFF = D == 8 ? 7 : (D == 4 ? 3 : 0);
+  unsigned long long* hp;
+  __device__ explicit LaneHeap(unsigned long long* row) : hp(row + OFF) {}
+  __device__ __forceinline__ void push(int& hn, unsigned long long key) {
+    int i = hn++;
+    while (i > 0) {
+      const int p = (i - 1) / D;
+      const unsigned long long pk = hp[p];
+      if (pk <= key) break;
+      hp[i] = pk;
+      i = p;
+    }
+    hp[i] = key;
+  }
+  __device__ __forceinline__ unsigned long long pop(int& hn) {
+    const unsigned long long top = hp[0];
+    const unsigned long long last = hp[--hn];
+    if (hn == 0) return top;
+    int i = 0;
+    while (true) {
+      const int c = D * i + 1;
+      if (c >= hn) break;
+      unsigned long long best;
+      int bi;
+      if constexpr (D == 4) {
+        const ulonglong2* blk = reinterpret_cast<const ulonglong2*>(hp + c);   // 32-byte aligned
+        const ulonglong2 x0 = blk[0], x1 = blk[1];
+        const unsigned long long v0 = x0.x;
+        const unsigned long long v1 = c + 1 < hn ? x0.y : ~0ull;
+        const unsigned long long v2 = c + 2 < hn ? x1.x : ~0ull;
+        const unsigned long long v3 = c + 3 < hn ? x1.y : ~0ull;
+        const bool b1 = v1 < v0, b3 = v3 < v2;
+        const unsigned long long m01 = b1 ? v1 : v0, m23 = b3 ? v3 : v2;
+        const int i01 = b1 ? c + 1 : c, i23 = b3 ? c + 3 : c + 2;
+        best = m23 < m01 ? m23 : m01;
+        bi = m23 < m01 ? i23 : i01;
+      } else if constexpr (D == 8) {
+        const ulonglong2* blk = reinterpret_cast<const ulonglong2*>(hp + c);   // 64-byte aligned
+        ulonglong2 x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = blk[q];
+        best = x[0].x;
+        bi = c;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+          const unsigned long long v = (j & 1) ? x[j >> 1].y : x[j >> 1].x;
+          if (c + j < hn && v < best) { best = v; bi = c + j; }
+        }
+      } else {
+        best = hp[c];
+        bi = c;
+        if (c + 1 < hn) {
+          const unsigned long long c2 = hp[c + 1];
+          if (c2 < best) { best = c2; ++bi; }
+        }
+      }
+      if (best >= last) break;
+      hp[i] = best;
+      i = bi;
+    }
+    hp[i] = last;
+    return top;
+  }
+};
+
+template <int K, int D>
 __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
   // XCD-aware: workgroup b runs on XCD b % 8; give each XCD a contiguous range of queries, so with
   // source-sorted queries one XCD's L2 serves one region of the graph (edges, costs, ALT rows)
@@ -122,31 +197,16 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
   };
 
   int hn = 0, nt = 0, status = 1;
+  const int capq = a.cap - 16;         // room for the shifted storage and a full child block
+  LaneHeap<D> hq(heap);
   st[s] = st_make(0.f, 0x7fffffffu);
   touched[nt++] = s;
-  heap[hn++] = hkey(heur(s), s);
+  hq.push(hn, hkey(heur(s), s));
   int it = 0;
   for (; hn > 0; ++it) {
     if (it >= a.max_iters) { status = 3; break; }
     // pop min
-    const unsigned long long top = heap[0];
-    const unsigned long long last = heap[--hn];
-    if (hn > 0) {
-      int i = 0;
-      while (true) {
-        int c = 2 * i + 1;
-        if (c >= hn) break;
-        unsigned long long cv = heap[c];
-        if (c + 1 < hn) {
-          const unsigned long long c2 = heap[c + 1];
-          if (c2 < cv) { cv = c2; ++c; }
-        }
-        if (cv >= last) break;
-        heap[i] = cv;
-        i = c;
-      }
-      heap[i] = last;
-    }
+    const unsigned long long top = hq.pop(hn);
     const int v = (int)(unsigned)(top & 0xffffffffu);
     const unsigned long long wv = st[v];
     if (st_p(wv) & CLOSED) continue;     // stale duplicate
@@ -163,22 +223,12 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
       const float gu = st_g(wu);
       if (ng < gu) {
         if (gu == __int_as_float(0x7f800000)) {   // first touch
-          if (nt >= a.cap) { overflow = true; break; }
+          if (nt >= capq) { overflow = true; break; }
           touched[nt++] = u;
         }
         st[u] = st_make(ng, (unsigned)v);
-        if (hn >= a.cap) { overflow = true; break; }
-        // push + sift up
-        unsigned long long key = hkey(ng + heur(u), u);
-        int i = hn++;
-        while (i > 0) {
-          const int p = (i - 1) >> 1;
-          const unsigned long long pk = heap[p];
-          if (pk <= key) break;
-          heap[i] = pk;
-          i = p;
-        }
-        heap[i] = key;
+        if (hn >= capq) { overflow = true; break; }
+        hq.push(hn, hkey(ng + heur(u), u));
       }
     }
     if (overflow) { status = 2; break; }
@@ -228,10 +278,28 @@ hipError_t launch_astar(const int* indptr, const int* indices, const float* cost
   // one wavefront per workgroup (a wave runs as long as its longest search); grid rounded to a
   // multiple of 8 for the XCD-aware remap in the kernel (surplus lanes exit at the slot check)
   const dim3 grid(((n + 63) / 64 + 7) / 8 * 8), block(64);
-  if (lm == nullptr) hipLaunchKernelGGL(astar_kernel<0>, grid, block, 0, stream, a);
-  else if (K == 8) hipLaunchKernelGGL(astar_kernel<8>, grid, block, 0, stream, a);
-  else if (K == 16) hipLaunchKernelGGL(astar_kernel<16>, grid, block, 0, stream, a);
-  else hipLaunchKernelGGL(astar_kernel<32>, grid, block, 0, stream, a);
+  static const int arity = [] {
+    const char* v = std::getenv("ROUTEST_ASTAR_ARITY");
+    const int d = v != nullptr ? std::atoi(v) : 8;
+    return (d == 2 || d == 4) ? d : 8;
+  }();
+  if (a.cap < 64) return hipErrorInvalidValue;
+  if (arity == 2) {
+    if (lm == nullptr) hipLaunchKernelGGL((astar_kernel<0, 2>), grid, block, 0, stream, a);
+    else if (K == 8) hipLaunchKernelGGL((astar_kernel<8, 2>), grid, block, 0, stream, a);
+    else if (K == 16) hipLaunchKernelGGL((astar_kernel<16, 2>), grid, block, 0, stream, a);
+    else hipLaunchKernelGGL((astar_kernel<32, 2>), grid, block, 0, stream, a);
+  } else if (arity == 8) {
+    if (lm == nullptr) hipLaunchKernelGGL((astar_kernel<0, 8>), grid, block, 0, stream, a);
+    else if (K == 8) hipLaunchKernelGGL((astar_kernel<8, 8>), grid, block, 0, stream, a);
+    else if (K == 16) hipLaunchKernelGGL((astar_kernel<16, 8>), grid, block, 0, stream, a);
+    else hipLaunchKernelGGL((astar_kernel<32, 8>), grid, block, 0, stream, a);
+  } else {
+    if (lm == nullptr) hipLaunchKernelGGL((astar_kernel<0, 4>), grid, block, 0, stream, a);
+    else if (K == 8) hipLaunchKernelGGL((astar_kernel<8, 4>), grid, block, 0, stream, a);
+    else if (K == 16) hipLaunchKernelGGL((astar_kernel<16, 4>), grid, block, 0, stream, a);
+    else hipLaunchKernelGGL((astar_kernel<32, 4>), grid, block, 0, stream, a);
+  }
   return hipGetLastError();
 }
 
