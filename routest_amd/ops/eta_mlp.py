@@ -238,6 +238,7 @@ class ResidentScorer:
         self.cap = cap
         self.h: Optional[int] = self._C.pscore_create(kernel.packed.blob, kernel.hidden,
                                                       list(kernel.packed.norm), cap, idle_ms, life_ms)
+        _RESIDENT.add(self)
 
     def score(self, rec_i32: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
         n = rec_i32.shape[0]
@@ -266,3 +267,19 @@ class ResidentScorer:
             self.close()
         except Exception:
             pass
+
+
+def _close_all_resident() -> None:  # pragma: no cover - exit path
+    """atexit: stop every live resident scorer before the HIP runtime is torn down."""
+    for o in list(_RESIDENT):
+        try:
+            o.close()
+        except Exception:
+            pass
+
+
+import atexit as _atexit  # noqa: E402
+import weakref as _weakref  # noqa: E402
+
+_RESIDENT: "_weakref.WeakSet[ResidentScorer]" = _weakref.WeakSet()
+_atexit.register(_close_all_resident)

@@ -72,6 +72,13 @@ class GpuRunner:
     def __repr__(self) -> str:
         return f"GpuRunner({self.device})"
 
+    def close(self) -> None:
+        """Stop the resident scorer kernel (and wait for it) while the HIP runtime is alive."""
+        with self.lock:
+            if self.resident is not None:
+                self.resident.close()
+                self.resident = None
+
     def __call__(self, rec: np.ndarray) -> np.ndarray:
         maybe_fail("gpu_fail")
         n = rec.shape[0]
@@ -307,3 +314,6 @@ class MicroBatcher:
         self.q.put(None)
         for t in self.threads:
             t.join(timeout=5)
+        for r in self.runners:
+            if hasattr(r, "close"):
+                r.close()
