@@ -327,6 +327,29 @@ void gcn_agg_gemm(torch::Tensor X, torch::Tensor indptr, torch::Tensor indices, 
                                        num_cus(X.device().index()), cur_stream(X)));
 }
 
+void gcn_l1_fused(torch::Tensor X, torch::Tensor indptr, torch::Tensor indices, torch::Tensor values,
+                  torch::Tensor w1frag, torch::Tensor b1, torch::Tensor w2frag, torch::Tensor Z, int64_t row0,
+                  int64_t row1) {
+  check_dev(X, "X");
+  check_dev(w1frag, "w1frag");
+  check_dev(w2frag, "w2frag");
+  check_dev(b1, "b1");
+  check_dev(Z, "Z");
+  check_csr(indptr, indices, values);
+  const int64_t fin = X.size(1), fhid = b1.numel(), fz = Z.size(1);
+  TORCH_CHECK(X.scalar_type() == torch::kBFloat16 && X.dim() == 2, "X bf16 [N,fin]");
+  TORCH_CHECK(Z.scalar_type() == torch::kBFloat16 && Z.dim() == 2 && Z.size(0) >= row1, "Z bf16 [N,fz]");
+  TORCH_CHECK(fin == 32 && fhid == 128 && fz == 32, "fused layer 1 is built for 32 -> 128 -> 32");
+  TORCH_CHECK(w1frag.numel() == fin * fhid && w2frag.numel() == fhid * fz, "weight fragments");
+  TORCH_CHECK(b1.scalar_type() == torch::kFloat32, "b1 f32");
+  TORCH_CHECK(0 <= row0 && row0 <= row1 && row1 <= X.size(0) && indptr.numel() >= row1 + 1, "rows");
+  const c10::DeviceGuard guard(X.device());
+  RT_CHECK_HIP(rt::launch_gcn_l1_fused(X.data_ptr(), indptr.data_ptr<int>(), indices.data_ptr<int>(),
+                                       values.data_ptr<float>(), w1frag.data_ptr(), b1.data_ptr<float>(),
+                                       w2frag.data_ptr(), Z.data_ptr(), (int)fin, (int)fhid, (int)fz, (int)row0,
+                                       (int)row1, num_cus(X.device().index()), cur_stream(X)));
+}
+
 void gcn_spmm_score(torch::Tensor Z, torch::Tensor indptr, torch::Tensor indices, torch::Tensor values,
                     torch::Tensor b2, torch::Tensor wo, double bo, torch::Tensor delay, int64_t row0,
                     int64_t row1) {
@@ -612,6 +635,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs");
   m.def("num_cus", [](int64_t dev) { return (int64_t)num_cus((int)dev); });
   m.def("gcn_agg_gemm", &gcn_agg_gemm, "K8: fused CSR aggregation + MFMA GEMM + bias/ReLU");
+  m.def("gcn_l1_fused", &gcn_l1_fused, "K8: fused aggregation + W1 GEMM + ReLU + W2 transform (H1 stays in LDS)");
   m.def("gcn_spmm_score", &gcn_spmm_score, "K8: layer-2 aggregation + delay head");
   m.def("route_score", &route_score, "K8: per-route delay-weighted length");
   m.def("astar", &astar, "K9: batched A* (one lane per query) with learned edge costs",

@@ -92,6 +92,120 @@ __global__ __launch_bounds__(256) void gcn_agg_gemm_kernel(
   }
 }
 
+// Fused layer 1 + layer-2 transform:  Z = relu((Â X) W1 + b1) W2  per 32-node wave tile.  H1 never
+// leaves the wave's LDS tile: the unfused pair wrote H1 (N x 128 bf16 = 25.6 MB at 100k nodes) and
+// read it back in a second launch.  H1 is rounded to bf16 in LDS exactly as the unfused path rounds
+// it in HBM, and both GEMMs keep the unfused k order, so Z is bit-identical.  Z leaves through the
+// LDS tile as 16-byte row chunks instead of one 2-byte store per accumulator register.
+template <int FIN, int FHID, int FZ>
+__global__ __launch_bounds__(256) void gcn_l1_fused_kernel(
+    const __bf16* __restrict__ X, const int* __restrict__ indptr, const int* __restrict__ indices,
+    const float* __restrict__ values, const bf16x8* __restrict__ w1frag, const float* __restrict__ b1,
+    const bf16x8* __restrict__ w2frag, __bf16* __restrict__ Z, int row0, int row1) {
+  constexpr int G = FIN / 8, RPP = 64 / G, KS1 = FIN / 16, NT1 = FHID / 32, KS2 = FHID / 16, NT2 = FZ / 32;
+  constexpr int LDA = FIN + 8, LDH = FHID + 8, LDZ = FZ + 8;
+  constexpr int TILE = 32 * (LDH > LDA ? LDH : LDA);
+  __shared__ __attribute__((aligned(16))) bf16x8 s_w1[NT1 * KS1 * 64];
+  __shared__ __attribute__((aligned(16))) bf16x8 s_w2[NT2 * KS2 * 64];
+  __shared__ __attribute__((aligned(16))) __bf16 s_t[4][TILE];
+  for (int i = threadIdx.x; i < NT1 * KS1 * 64; i += blockDim.x) s_w1[i] = w1frag[i];
+  for (int i = threadIdx.x; i < NT2 * KS2 * 64; i += blockDim.x) s_w2[i] = w2frag[i];
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  __bf16* tile = s_t[w];
+  const int ntiles = (row1 - row0 + 31) / 32;
+  float bias[NT1];
+#pragma unroll
+  for (int nt = 0; nt < NT1; ++nt) bias[nt] = b1[32 * nt + (lane & 31)];
+  const int lb = (int)(blockIdx.x % 8u) * (int)(gridDim.x / 8u) + (int)(blockIdx.x / 8u);
+  for (int t = lb * 4 + w; t < ntiles; t += gridDim.x * 4) {
+    const int base = row0 + t * 32;
+    // (1) aggregation Â X of the tile's 32 nodes -> A tile [32][LDA]
+#pragma unroll
+    for (int pass = 0; pass < 32 / RPP; ++pass) {
+      const int rr = pass * RPP + lane / G;
+      const int c = (lane % G) * 8;
+      const int v = base + rr;
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+      if (v < row1) {
+        const int e0 = indptr[v], e1 = indptr[v + 1];
+        for (int e = e0; e < e1; ++e) {
+          const int u = indices[e];
+          const float wv = values[e];
+          const bf16x8 x = *reinterpret_cast<const bf16x8*>(X + (size_t)u * FIN + c);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += wv * (float)x[j];
+        }
+      }
+      *reinterpret_cast<bf16x8*>(tile + rr * LDA + c) = to_bf16x8(acc);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    // (2) layer 1 GEMM (+bias, ReLU): accumulators keep the hidden unit on the lane
+    f32x16 h1[NT1];
+#pragma unroll
+    for (int nt = 0; nt < NT1; ++nt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) h1[nt][e] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + (lane & 31) * LDA + 16 * ks + 8 * h);
+        h1[nt] = mfma32(a, s_w1[(nt * KS1 + ks) * 64 + lane], h1[nt]);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();          // A tile consumed: the region now holds H1 [32][LDH]
+#pragma unroll
+    for (int nt = 0; nt < NT1; ++nt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rr = (e & 3) + 8 * (e >> 2) + 4 * h;
+        tile[rr * LDH + 32 * nt + (lane & 31)] = (__bf16)relu_f(h1[nt][e] + bias[nt]);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    // (3) transform Z = H1 W2
+    f32x16 z[NT2];
+#pragma unroll
+    for (int nt = 0; nt < NT2; ++nt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) z[nt][e] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS2; ++ks) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + (lane & 31) * LDH + 16 * ks + 8 * h);
+        z[nt] = mfma32(a, s_w2[(nt * KS2 + ks) * 64 + lane], z[nt]);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();          // H1 consumed: the region now holds Z [32][LDZ]
+#pragma unroll
+    for (int nt = 0; nt < NT2; ++nt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rr = (e & 3) + 8 * (e >> 2) + 4 * h;
+        tile[rr * LDZ + 32 * nt + (lane & 31)] = (__bf16)z[nt][e];
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    // (4) 16-byte row-chunk stores of the tile's Z rows
+    constexpr int CPR = FZ / 8;               // 16-byte chunks per row
+#pragma unroll
+    for (int q = lane; q < 32 * CPR; q += 64) {
+      const int rr = q / CPR, c8 = q % CPR;
+      if (base + rr < row1)
+        *reinterpret_cast<bf16x8*>(Z + (size_t)(base + rr) * FZ + 8 * c8) =
+            *reinterpret_cast<const bf16x8*>(tile + rr * LDZ + 8 * c8);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();          // tile free for the next aggregation
+  }
+}
+
 // delay[v] = 0.5 + softplus( sum_f (sum_u Â[v,u] Z[u,f] + b2[f]) * wo[f] + bo ),  F = 32 (4 lanes/row)
 __global__ __launch_bounds__(256) void gcn_spmm_score_kernel(
     const __bf16* __restrict__ Z, const int* __restrict__ indptr, const int* __restrict__ indices,
@@ -126,7 +240,9 @@ __global__ __launch_bounds__(256) void gcn_spmm_score_kernel(
   }
 }
 
-// score[r] = sum_i delay[v_i] * haversine(v_i, v_{i+1}) over route r's node list (one wave / route)
+// score[r] = sum_i delay[v_i] * haversine(v_i, v_{i+1}) over route r's node list (one wave / route).
+// Measured alternatives (bench/gcn_bench.py, 10k routes of 50-300 nodes): a 16-lane group per route
+// 18.3 us, loads of 4 segments per lane issued before computing 14.7 us, this form 13.7 us.
 __global__ __launch_bounds__(256) void route_score_kernel(const int* __restrict__ rptr,
                                                           const int* __restrict__ nodes,
                                                           const float* __restrict__ lat,
@@ -178,6 +294,21 @@ hipError_t launch_gcn_agg_gemm(const void* X, const int* indptr, const int* indi
   return hipErrorInvalidValue;
 }
 
+hipError_t launch_gcn_l1_fused(const void* X, const int* indptr, const int* indices, const float* values,
+                               const void* w1frag, const float* b1, const void* w2frag, void* Z, int fin,
+                               int fhid, int fz, int row0, int row1, int num_cus, hipStream_t stream) {
+  const int ntiles = (row1 - row0 + 31) / 32;
+  if (ntiles <= 0) return hipSuccess;
+  if (fin != 32 || fhid != 128 || fz != 32) return hipErrorInvalidValue;
+  int grid = (ntiles + 3) / 4;
+  if (grid > num_cus * 4) grid = num_cus * 4;
+  grid = (grid + 7) / 8 * 8;
+  hipLaunchKernelGGL((gcn_l1_fused_kernel<32, 128, 32>), dim3(grid), dim3(256), 0, stream, (const __bf16*)X,
+                     indptr, indices, values, (const bf16x8*)w1frag, b1, (const bf16x8*)w2frag, (__bf16*)Z, row0,
+                     row1);
+  return hipGetLastError();
+}
+
 hipError_t launch_gcn_spmm_score(const void* Z, const int* indptr, const int* indices,
                                  const float* values, const float* b2, const float* wo, float bo,
                                  float* delay, int row0, int row1, hipStream_t stream) {
@@ -193,8 +324,8 @@ hipError_t launch_route_score(const int* rptr, const int* nodes, const float* la
                               const float* lon, const float* delay, float* score, int R,
                               hipStream_t stream) {
   if (R <= 0) return hipSuccess;
-  hipLaunchKernelGGL(route_score_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, rptr, nodes, lat,
-                     lon, delay, score, R);
+  hipLaunchKernelGGL(route_score_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, rptr, nodes, lat, lon,
+                     delay, score, R);
   return hipGetLastError();
 }
 

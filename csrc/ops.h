@@ -47,6 +47,9 @@ hipError_t launch_gcn_agg_gemm(const void* X, const int* indptr, const int* indi
                                const float* values, const void* wfrag, const float* bias, void* Y,
                                int fin, int fout, bool agg, bool relu, int row0, int row1,
                                int num_cus, hipStream_t stream);
+hipError_t launch_gcn_l1_fused(const void* X, const int* indptr, const int* indices, const float* values,
+                               const void* w1frag, const float* b1, const void* w2frag, void* Z, int fin,
+                               int fhid, int fz, int row0, int row1, int num_cus, hipStream_t stream);
 hipError_t launch_gcn_spmm_score(const void* Z, const int* indptr, const int* indices,
                                  const float* values, const float* b2, const float* wo, float bo,
                                  float* delay, int row0, int row1, hipStream_t stream);

@@ -17,6 +17,8 @@ multi-GPU modes:
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -112,7 +114,11 @@ class GcnScorerHip:
             self.rows = (0, self.N)
             self.per = self.N
         npad = self.per * (world if mode == "partition" and world > 1 else 1)
-        self.H1 = torch.empty(npad, self.fhid, dtype=torch.bfloat16, device=d)
+        # fused layer 1 (csrc/gcn.hip gcn_l1_fused_kernel) for the 32 -> 128 -> 32 scorer;
+        # ROUTEST_GCN_FUSED=0 selects the two-launch path (H1 materialised in HBM)
+        self.fused = (self.X.shape[1], self.fhid, self.fz) == (32, 128, 32) and \
+            os.environ.get("ROUTEST_GCN_FUSED", "1") != "0"
+        self.H1 = None
         self.Z = torch.empty(npad, self.fz, dtype=torch.bfloat16, device=d)
         self.delay = torch.zeros(npad, dtype=torch.float32, device=d)
         self.lat = torch.from_numpy(g.lat.astype(np.float32)).to(d)
@@ -120,10 +126,17 @@ class GcnScorerHip:
 
     def node_delays(self) -> torch.Tensor:
         C, (r0, r1) = self.C, self.rows
-        C.gcn_agg_gemm(self.X, self.indptr, self.indices, self.values, self.w1, self.b1, self.H1,
-                       self.X.shape[1], self.fhid, True, True, r0, r1)
-        C.gcn_agg_gemm(self.H1, self.indptr, self.indices, self.values, self.w2, None, self.Z,
-                       self.fhid, self.fz, False, False, r0, r1)
+        if self.fused:
+            # aggregation + W1 + ReLU + W2 in one launch; H1 never leaves LDS
+            C.gcn_l1_fused(self.X, self.indptr, self.indices, self.values, self.w1, self.b1, self.w2,
+                           self.Z, r0, r1)
+        else:
+            if self.H1 is None:
+                self.H1 = torch.empty(self.Z.shape[0], self.fhid, dtype=torch.bfloat16, device=self.dev)
+            C.gcn_agg_gemm(self.X, self.indptr, self.indices, self.values, self.w1, self.b1, self.H1,
+                           self.X.shape[1], self.fhid, True, True, r0, r1)
+            C.gcn_agg_gemm(self.H1, self.indptr, self.indices, self.values, self.w2, None, self.Z,
+                           self.fhid, self.fz, False, False, r0, r1)
         if self.mode == "partition" and self.world > 1:
             import torch.distributed as dist
             own = self.Z[r0:r0 + self.per].clone()

@@ -52,8 +52,7 @@ def test_gcn_partition_rows_match_full():
         h.rows = (r * per, min(g.num_nodes, (r + 1) * per))
         C = h.C
         r0, r1 = h.rows
-        C.gcn_agg_gemm(h.X, h.indptr, h.indices, h.values, h.w1, h.b1, h.H1, 32, 128, True, True, r0, r1)
-        C.gcn_agg_gemm(h.H1, h.indptr, h.indices, h.values, h.w2, None, h.Z, 128, 32, False, False, r0, r1)
+        C.gcn_l1_fused(h.X, h.indptr, h.indices, h.values, h.w1, h.b1, h.w2, h.Z, r0, r1)
         zs.append(h.Z[r0:r1].clone())
         hs.append(h)
     Z = torch.cat(zs)
@@ -63,3 +62,22 @@ def test_gcn_partition_rows_match_full():
         h.C.gcn_spmm_score(h.Z, h.indptr, h.indices, h.values, h.b2, h.wo, h.bo, h.delay, r0, r1)
         parts.append(h.delay[r0:r1].cpu())
     torch.testing.assert_close(torch.cat(parts), full)
+
+
+@pytest.mark.parametrize("rows", [(0, 30_000), (1_000, 17_777)])
+def test_gcn_fused_layer1_bitwise_equals_two_launch_path(rows, monkeypatch):
+    """gcn_l1_fused_kernel keeps H1 in LDS; it must reproduce the two-launch path bit for bit."""
+    g = synth_road_graph(30_000, seed=5)
+    m = GcnScorer(seed=6)
+    fused = GcnScorerHip(m, g, torch.device("cuda:0"))
+    monkeypatch.setenv("ROUTEST_GCN_FUSED", "0")
+    split = GcnScorerHip(m, g, torch.device("cuda:0"))
+    assert fused.fused and not split.fused
+    r0, r1 = rows
+    fused.rows = split.rows = rows
+    fused.Z.zero_()
+    split.Z.zero_()
+    fused.node_delays()
+    split.node_delays()
+    assert torch.equal(fused.Z[r0:r1], split.Z[r0:r1])
+    assert torch.equal(fused.delay[r0:r1], split.delay[r0:r1])
