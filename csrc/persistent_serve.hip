@@ -40,6 +40,7 @@ struct alignas(64) ServeMailbox {
 };
 
 constexpr unsigned kOutSentinel = 0x7fa5a5a5u;   // signalling NaN payload (never produced)
+constexpr size_t kXchBytes = 4 * 4 * 64 * 16;     // single-tile mode: relu(z2) of 4 hidden tiles
 
 __device__ __forceinline__ unsigned sys_load_u32(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -88,6 +89,74 @@ __global__ __launch_bounds__(512, 1) void eta_mlp3_serve_kernel(ServeMailbox* mb
     __syncthreads();              // s_cmd is rewritten only after every wave has read it
     if (quit) break;
     const int ntiles = (n + 31) >> 5;
+    if (ntiles == 1) {
+      // one tile (n <= 32, the single-request case): split its layer 2 over the waves — wave w
+      // computes hidden tile mt = w (16 MFMAs instead of 128 in one wave) — and let wave 0 run the
+      // layer-3 dot over all tiles in the SAME order as the per-wave path, so the minutes are
+      // bit-identical to the normal kernel.  relu(z2) of 4 tiles at a time goes through LDS
+      // (16 KiB; the weight blob leaves ~21 KiB free).
+      constexpr int MT = H / 32;
+      const int row = r;
+      int4 rc = make_int4(0, 0, 0, 0);
+      if (row < n) {
+        const unsigned long long* p = reinterpret_cast<const unsigned long long*>(rec + row);
+        const unsigned long long lo = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long hi = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        rc = make_int4((int)lo, (int)(lo >> 32), (int)hi, (int)(hi >> 32));
+      }
+      f32x16 z;                                   // relu(z2) of hidden tile mt = wave
+      if (wave < MT) {
+        const bf16x8 xb = featurize_bf16(rc, h, np);
+        bf16x8 h1[KS];
+        mlp3_layer1<H>(w1, xb, h1);
+        const bf16x8* wa = w.w2p + lane + wave * KS * 64;
+        z = load_vec16(w.b2p, wave, h);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) z = mfma32(wa[ks * 64], h1[ks], z);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) z[i] = relu_f(z[i]);
+      }
+      f32x4* xch = reinterpret_cast<f32x4*>(smem + Mlp3Layout<H>::BLOB);   // [4 tiles][4][64 lanes]
+      f32x2 ys2 = {0.f, 0.f};
+      for (int g0 = 0; g0 < MT; g0 += 4) {
+        __syncthreads();
+        if (wave >= g0 && wave < g0 + 4 && wave < MT) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 v = {z[4 * q], z[4 * q + 1], z[4 * q + 2], z[4 * q + 3]};
+            xch[((wave - g0) * 4 + q) * 64 + lane] = v;
+          }
+        }
+        __syncthreads();
+        if (wave == 0) {
+          for (int mt = g0; mt < g0 + 4 && mt < MT; ++mt) {
+            const f32x16 w3 = load_vec16(w.w3p, mt, h);
+            f32x16 a;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const f32x4 v = xch[((mt - g0) * 4 + q) * 64 + lane];
+              a[4 * q] = v[0];
+              a[4 * q + 1] = v[1];
+              a[4 * q + 2] = v[2];
+              a[4 * q + 3] = v[3];
+            }
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+              const f32x2 a2 = {a[i], a[i + 1]};
+              const f32x2 w2 = {w3[i], w3[i + 1]};
+              ys2 = __builtin_elementwise_fma(a2, w2, ys2);
+            }
+          }
+        }
+      }
+      if (wave == 0) {
+        float ys = ys2[0] + ys2[1];
+        ys += __shfl_xor(ys, 32);
+        if (h == 0 && row < n)
+          __hip_atomic_store(out + row, __float_as_uint(ys + b3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      continue;
+    }
     for (int tile = wave; tile < ntiles; tile += 8) {
       const int row = tile * 32 + r;
       int4 rc = make_int4(0, 0, 0, 0);
@@ -146,11 +215,11 @@ static hipError_t launch_serve_h(PersistentScorer* s) {
   static bool attr_set[64] = {};
   if (!attr_set[s->device & 63]) {
     hipError_t e = hipFuncSetAttribute((const void*)eta_mlp3_serve_kernel<H>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::BLOB);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)(L::BLOB + kXchBytes));
     if (e != hipSuccess) return e;
     attr_set[s->device & 63] = true;
   }
-  hipLaunchKernelGGL(eta_mlp3_serve_kernel<H>, dim3(1), dim3(512), L::BLOB, s->stream, s->d_mb,
+  hipLaunchKernelGGL(eta_mlp3_serve_kernel<H>, dim3(1), dim3(512), L::BLOB + kXchBytes, s->stream, s->d_mb,
                      (const int4*)s->d_rec, s->d_out, s->cap, (const unsigned char*)s->blob, s->np,
                      s->seq, s->idle_ticks, s->life_ticks);
   return hipGetLastError();
