@@ -16,6 +16,8 @@
 //    (<= 144 accumulator VGPRs: two waves per SIMD); the staged B tile is shared by all 8 waves.
 //  * the fp32 partial of slice s is written to slab[s] in the caller's layout (the flat gradient
 //    bucket); wgrad_reduce_kernel sums the S slabs in a fixed order — deterministic, no atomics.
+#include <cstdlib>
+
 #include "common.h"
 #include "ops.h"
 
@@ -58,14 +60,14 @@ __device__ __forceinline__ int relu_mask_word(int a, int m) {
 
 // MASK: A_eff = A * (mask > 0) applied while staging (mask has A's shape, leading dim ldm) — fuses
 // the ReLU backward of the first layer into dW1 = dz1^T x, so dz1 is never materialised.
-template <int NT, bool MASK>
+template <int NT, bool MASK, int KB>
 __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict__ A, int lda, int M,
                                                        int Mout, const __bf16* __restrict__ Bm,
                                                        int ldb, int N, int K, int kslice,
                                                        float* __restrict__ slab, int ldo,
                                                        long long slab_stride,
                                                        const __bf16* __restrict__ mask, int ldm) {
-  constexpr int KB = 32, AW = 256, BW = 32 * NT;
+  constexpr int AW = 256, BW = 32 * NT;
   constexpr int ACH = AW / 8, BCH = BW / 8;           // 16-B chunks per staged row
   constexpr int TPB = 512;
   constexpr int APT = (KB * ACH + TPB - 1) / TPB;      // chunks per thread
@@ -224,26 +226,53 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
-size_t wgrad_lds_bytes(int NT) {
+size_t wgrad_lds_bytes(int NT, int KB) {
   auto pad = [](int cols) {
     int b = 2 * cols, r = b % 256;
     b += (r <= 64) ? (64 - r) : (256 - r + 64);
     return b;
   };
-  return (size_t)32 * pad(256) + (size_t)32 * pad(32 * NT);
+  return (size_t)KB * pad(256) + (size_t)KB * pad(32 * NT);
+}
+size_t wgrad_lds_bytes(int NT) { return wgrad_lds_bytes(NT, 32); }
+
+// rows staged per barrier: ROUTEST_WGRAD_KB = 32 | 64 | 128 (A/B knob)
+static int wgrad_kb() {
+  static const int kb = [] {
+    const char* v = std::getenv("ROUTEST_WGRAD_KB");
+    const int k = v ? std::atoi(v) : 32;
+    return (k == 64 || k == 128) ? k : 32;
+  }();
+  return kb;
+}
+
+template <int NT, bool MASK, int KB>
+static hipError_t launch_wgrad_kb(const void* A, int lda, int M, int Mout, const void* Bm, int ldb,
+                                  int N, int K, int S, float* slab, int ldo, long long slab_stride,
+                                  hipStream_t stream, const void* mask, int ldm) {
+  const int kslice = ((K + S - 1) / S + 31) / 32 * 32;
+  const int mblocks = (M + 255) / 256;
+  const size_t lds = wgrad_lds_bytes(NT, KB);
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)wgrad_kernel<NT, MASK, KB>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((wgrad_kernel<NT, MASK, KB>), dim3(S, mblocks), dim3(512), lds, stream,
+                     (const __bf16*)A, lda, M, Mout, (const __bf16*)Bm, ldb, N, K, kslice, slab, ldo,
+                     slab_stride, (const __bf16*)mask, ldm);
+  return hipGetLastError();
 }
 
 template <int NT, bool MASK = false>
 static hipError_t launch_wgrad_nt(const void* A, int lda, int M, int Mout, const void* Bm, int ldb,
                                   int N, int K, int S, float* slab, int ldo, long long slab_stride,
                                   hipStream_t stream, const void* mask = nullptr, int ldm = 0) {
-  const int kslice = ((K + S - 1) / S + 31) / 32 * 32;
-  const int mblocks = (M + 255) / 256;
-  const size_t lds = wgrad_lds_bytes(NT);
-  hipLaunchKernelGGL((wgrad_kernel<NT, MASK>), dim3(S, mblocks), dim3(512), lds, stream,
-                     (const __bf16*)A, lda, M, Mout, (const __bf16*)Bm, ldb, N, K, kslice, slab, ldo,
-                     slab_stride, (const __bf16*)mask, ldm);
-  return hipGetLastError();
+  switch (wgrad_kb()) {
+    case 128: return launch_wgrad_kb<NT, MASK, 128>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm);
+    case 64: return launch_wgrad_kb<NT, MASK, 64>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm);
+    default: return launch_wgrad_kb<NT, MASK, 32>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm);
+  }
 }
 
 hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm, int ldb, int N,

@@ -17,6 +17,7 @@ learned weights back into an :class:`EtaMLP` whose buffers carry the scaling.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -114,7 +115,8 @@ class FusedMlp3Trainer:
         self.dz2 = torch.empty(B, H, dtype=bf, device=d)
         self.dyb = torch.empty(B, 8, dtype=bf, device=d)
         ncu = self.C.num_cus(self.dev.index if self.dev.index is not None else 0)
-        self.S = max(1, min(ncu, B // 256))
+        rows = int(os.environ.get("ROUTEST_WGRAD_ROWS", "256"))     # batch rows per k-slice
+        self.S = max(1, min(ncu, B // rows))
         self.slab = torch.empty(self.S, self.G.numel(), dtype=torch.float32, device=d)
         self.use_hipblaslt_wgrad = False
         self.dh1 = torch.empty(B, H, dtype=bf, device=d)
