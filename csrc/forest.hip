@@ -64,7 +64,8 @@ __global__ __launch_bounds__(256) void forest_kernel(ForestArgs a) {
 // chunk's nodes into LDS ONCE, then streams all of its row tiles through it (featurize the tile's
 // records into the per-thread LDS feature rows, walk the chunk's trees, add the partial sum into
 // the output row, which this workgroup owns for every chunk).  Each thread walks two trees at a time
-// so the two dependent LDS-load chains overlap.  LDS: 96 KB nodes + 52 KB features.
+// so the two dependent LDS-load chains overlap (4 walks per thread measured 298 vs 326 M preds/s:
+// the union of four walks' depths per loop trip costs more than the extra overlap buys).  LDS: 96 KB nodes + 52 KB features.
 constexpr int FOREST_LDS_NODES = 12288;
 constexpr int FOREST_TPB = 1024;
 
