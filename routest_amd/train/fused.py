@@ -3,6 +3,7 @@
 Per step (all on the current HIP stream, no host synchronisation, HIP-graph capturable):
 
   eta_mlp3_train_fwd (HIP)  : featurize + 3 layers + MSE grad; writes xf, h1a, h2a, dz2, dy
+                            (hidden units in the hperm() order: 16-byte stores per lane)
   dh1 = dz2 @ W2            : hipBLASLt (bf16, fp32 accumulate)
   G[W2|b2] = dz2^T [h1|1]   : split-K wgrad HIP kernel (K = batch) -> fp32 slabs laid out like
   G[w3|b3] = dy^T  [h2|1]     the flat bucket, then ONE deterministic slab reduction into G
@@ -49,13 +50,22 @@ def unflatten_into(model: EtaMLP, flat: torch.Tensor) -> None:
         o += n
 
 
+def hperm(H: int) -> torch.Tensor:
+    """Stored hidden-unit order of the fused trainer's activations and gradient bucket (unit u at
+    column u with bits 2 and 3 swapped: one 16-byte store per lane, csrc/eta_mlp_train.hip)."""
+    u = torch.arange(H)
+    return (u & ~12) | ((u & 4) << 1) | ((u & 8) >> 1)
+
+
 def grads_from_bucket(G: torch.Tensor, H: int):
     """Python mirror of adamw_pack_kernel's bucket -> parameter-gradient mapping (tests)."""
     G = G.detach().float().cpu()
     ldg = H + 16
-    gW2a = G[:H * ldg].view(H, ldg)
-    gW3a = G[H * ldg:H * ldg + ldg]
-    gW1a = G[H * ldg + ldg:].view(H, 16)
+    pm = hperm(H)
+    cols = torch.cat([pm, torch.arange(H, ldg)])
+    gW2a = G[:H * ldg].view(H, ldg)[pm][:, cols]
+    gW3a = G[H * ldg:H * ldg + ldg][cols]
+    gW1a = G[H * ldg + ldg:].view(H, 16)[pm]
     gW1 = gW1a[:, :12].clone()
     gW1[:, 10] += gW1a[:, 12]
     gW1[:, 11] += gW1a[:, 13]
