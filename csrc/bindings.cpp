@@ -254,8 +254,9 @@ void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor
 
 // slab: f32 [S, stride]; the partial of k-slice s is written at slab[s, offset + m*ldo + n].
 void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N, torch::Tensor slab,
-           int64_t offset, int64_t ldo, c10::optional<torch::Tensor> mask) {
+           int64_t offset, int64_t ldo, c10::optional<torch::Tensor> mask, int64_t nout) {
   check_dev(A, "A");
+  if (nout < 0 || nout > N) nout = N;
   const void* mptr = nullptr;
   int ldm = 0;
   if (mask.has_value() && mask->defined()) {
@@ -276,12 +277,12 @@ void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N
   const int NT = (int)((N + 31) / 32);
   TORCH_CHECK(NT == 1 || NT == 2 || NT == 3 || NT == 5 || NT == 9, "unsupported N=", N);
   TORCH_CHECK(slab.scalar_type() == torch::kFloat32 && slab.dim() == 2, "slab must be f32 [S, stride]");
-  TORCH_CHECK(offset + (Mout - 1) * ldo + N <= slab.size(1), "slab region out of range");
+  TORCH_CHECK(offset + (Mout - 1) * ldo + nout <= slab.size(1), "slab region out of range");
   const c10::DeviceGuard guard(A.device());
   RT_CHECK_HIP(rt::launch_wgrad(A.data_ptr(), (int)A.size(1), (int)M, (int)Mout, Bm.data_ptr(),
                                 (int)Bm.size(1), (int)N, (int)A.size(0), (int)slab.size(0),
                                 slab.data_ptr<float>() + offset, (int)ldo, (long long)slab.size(1),
-                                cur_stream(A), mptr, ldm));
+                                cur_stream(A), mptr, ldm, (int)nout));
 }
 
 void wgrad_reduce(torch::Tensor slab, torch::Tensor G) {
@@ -631,7 +632,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp3_grad_bucket_floats", [](int64_t H) { return (int64_t)rt::mlp3_grad_bucket_floats((int)H); });
   m.def("wgrad", &wgrad, "split-K weight-gradient GEMM (K = batch) into fp32 slabs",
         py::arg("A"), py::arg("M"), py::arg("Mout"), py::arg("Bm"), py::arg("N"), py::arg("slab"),
-        py::arg("offset"), py::arg("ldo"), py::arg("mask") = py::none());
+        py::arg("offset"), py::arg("ldo"), py::arg("mask") = py::none(), py::arg("nout") = -1);
   m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs");
   m.def("num_cus", [](int64_t dev) { return (int64_t)num_cus((int)dev); });
   m.def("gcn_agg_gemm", &gcn_agg_gemm, "K8: fused CSR aggregation + MFMA GEMM + bias/ReLU");

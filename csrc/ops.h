@@ -37,7 +37,7 @@ hipError_t launch_adamw_pack(float* P, const float* G, float* M, float* V, void*
 // ---- weight-gradient GEMMs with K = batch : wgrad.hip ----
 hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm, int ldb, int N,
                         int K, int S, float* slab, int ldo, long long slab_stride, hipStream_t stream,
-                        const void* mask = nullptr, int ldm = 0);
+                        const void* mask = nullptr, int ldm = 0, int Nout = -1);
 hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, float* G, int n,
                                hipStream_t stream);
 size_t wgrad_lds_bytes(int NT);

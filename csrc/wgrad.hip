@@ -66,7 +66,8 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
                                                        int ldb, int N, int K, int kslice,
                                                        float* __restrict__ slab, int ldo,
                                                        long long slab_stride,
-                                                       const __bf16* __restrict__ mask, int ldm) {
+                                                       const __bf16* __restrict__ mask, int ldm,
+                                                       int Nout) {
   constexpr int AW = 256, BW = 32 * NT;
   constexpr int ACH = AW / 8, BCH = BW / 8;           // 16-B chunks per staged row
   constexpr int TPB = 512;
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int m = m_base + 32 * w + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (m < Mout && nn < N) out[(size_t)m * ldo + nn] = acc[n][e];
+      if (m < Mout && nn < Nout) out[(size_t)m * ldo + nn] = acc[n][e];
     }
   }
 }
@@ -249,7 +250,7 @@ static int wgrad_kb() {
 template <int NT, bool MASK, int KB>
 static hipError_t launch_wgrad_kb(const void* A, int lda, int M, int Mout, const void* Bm, int ldb,
                                   int N, int K, int S, float* slab, int ldo, long long slab_stride,
-                                  hipStream_t stream, const void* mask, int ldm) {
+                                  hipStream_t stream, const void* mask, int ldm, int Nout) {
   const int kslice = ((K + S - 1) / S + 31) / 32 * 32;
   const int mblocks = (M + 255) / 256;
   const size_t lds = wgrad_lds_bytes(NT, KB);
@@ -260,36 +261,39 @@ static hipError_t launch_wgrad_kb(const void* A, int lda, int M, int Mout, const
   }
   hipLaunchKernelGGL((wgrad_kernel<NT, MASK, KB>), dim3(S, mblocks), dim3(512), lds, stream,
                      (const __bf16*)A, lda, M, Mout, (const __bf16*)Bm, ldb, N, K, kslice, slab, ldo,
-                     slab_stride, (const __bf16*)mask, ldm);
+                     slab_stride, (const __bf16*)mask, ldm, Nout);
   return hipGetLastError();
 }
 
 template <int NT, bool MASK = false>
 static hipError_t launch_wgrad_nt(const void* A, int lda, int M, int Mout, const void* Bm, int ldb,
                                   int N, int K, int S, float* slab, int ldo, long long slab_stride,
-                                  hipStream_t stream, const void* mask = nullptr, int ldm = 0) {
+                                  hipStream_t stream, const void* mask = nullptr, int ldm = 0,
+                                  int Nout = -1) {
+  if (Nout < 0) Nout = N;
   switch (wgrad_kb()) {
-    case 128: return launch_wgrad_kb<NT, MASK, 128>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm);
-    case 64: return launch_wgrad_kb<NT, MASK, 64>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm);
-    default: return launch_wgrad_kb<NT, MASK, 32>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm);
+    case 128: return launch_wgrad_kb<NT, MASK, 128>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm, Nout);
+    case 64: return launch_wgrad_kb<NT, MASK, 64>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm, Nout);
+    default: return launch_wgrad_kb<NT, MASK, 32>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm, Nout);
   }
 }
 
 hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm, int ldb, int N,
                         int K, int S, float* slab, int ldo, long long slab_stride,
-                        hipStream_t stream, const void* mask, int ldm) {
+                        hipStream_t stream, const void* mask, int ldm, int Nout) {
   if (M % 8 || N % 8 || lda % 8 || ldb % 8) return hipErrorInvalidValue;
+  if (Nout < 0 || Nout > N) Nout = N;
   const int NT = (N + 31) / 32;
   if (mask != nullptr) {
     if (ldm % 8 || NT != 1) return hipErrorInvalidValue;   // the dW1 shape (N = 16)
-    return launch_wgrad_nt<1, true>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm);
+    return launch_wgrad_nt<1, true>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm, Nout);
   }
   switch (NT) {
-    case 1: return launch_wgrad_nt<1>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream);
-    case 2: return launch_wgrad_nt<2>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream);
-    case 3: return launch_wgrad_nt<3>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream);
-    case 5: return launch_wgrad_nt<5>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream);
-    case 9: return launch_wgrad_nt<9>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream);
+    case 1: return launch_wgrad_nt<1>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
+    case 2: return launch_wgrad_nt<2>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
+    case 3: return launch_wgrad_nt<3>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
+    case 5: return launch_wgrad_nt<5>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
+    case 9: return launch_wgrad_nt<9>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
     default: return hipErrorInvalidValue;
   }
 }

@@ -160,7 +160,9 @@ class FusedMlp3Trainer:
             return
         ldg = H + 16
         C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab, 0, ldg)
-        C.wgrad(self.dyb, 8, 1, self.h2a, ldg, self.slab, H * ldg, ldg)
+        # dW3|db3 = (h2a^T dy)^T: the unit axis (H+16) is the MFMA M side so all 8 waves of a
+        # workgroup work (dy as M = 8 rows left 7 of them idle); only column 0 of dy is real
+        C.wgrad(self.h2a, ldg, ldg, self.dyb, 8, self.slab, H * ldg, 1, None, 1)
         # dW1 = (dh1 * relu'(h1))^T x: the ReLU backward is applied while staging (no dz1 tensor)
         C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, H * ldg + ldg, 16, self.h1a)
         C.wgrad_reduce(self.slab, self.G)
