@@ -291,6 +291,236 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
   for (int i = 0; i < nt; ++i) st[touched[i]] = ST_INIT;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Tail stage: ONE WAVE per query, for the few searches that exhaust the lane kernel's pop budget.
+// The lane kernel's launch time is set by its longest search (a sequential chain of dependent HBM
+// loads, ~7.6 us per pop); here the 64 lanes of a wave expand a whole f-band at once:
+//
+//   near = open nodes with f = g + h < thr;  far = the other open nodes as (f, node) pairs
+//   repeat: every lane takes a near node, relaxes its edges with a 64-bit atomicMin on the packed
+//           (g << 32 | parent) word; an improved target goes to next-near if f < thr, else to far
+//   when near empties: best = g(t); if min f over far >= best the search is optimal (admissible
+//           h: every open node on a better path would have f < best); else thr = min f + delta and
+//           the far entries below it become the next near set (entries with f >= best are dropped)
+//
+// Label-correcting (a node is re-expanded when its g improves; stale duplicates are harmless), so
+// costs are exact.  Per-slot memory is the lane kernel's: the state row (read in the swapped
+// layout g << 32 | parent, for which the reset value ST_INIT is still "+inf"), the heap row split
+// into near A | near B | far, and the touched list.
+template <int K>
+__global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* __restrict__ qidx, int T,
+                                                        float delta, float* __restrict__ hcache) {
+  const int w = blockIdx.x;
+  if (w >= T || w >= a.S) return;
+  const int q = qidx[w];
+  const int lane = threadIdx.x;
+  unsigned long long* st = a.st + (size_t)w * a.N;
+  int* nearA = reinterpret_cast<int*>(a.heap + (size_t)w * a.cap);
+  const int NCAP = a.cap / 2;                       // ints per near list
+  int* nearB = nearA + NCAP;
+  unsigned long long* far = a.heap + (size_t)w * a.cap + a.cap / 2;
+  const int FCAP = a.cap / 2;                       // (f, node) entries
+  int* touched = a.touched + (size_t)w * a.cap;
+  // per-slot heuristic cache: h(v) costs a 256-byte landmark row, and this stage re-reads it for
+  // every relaxation and expansion (it was bandwidth-bound on those rows); the first toucher of a
+  // node stores h, everyone else reads 4 bytes (NaN = not yet stored -> compute it)
+  float* hc = hcache + (size_t)w * a.N;
+  __shared__ int s_next, s_far, s_touch, s_bad;
+  const int s = a.src[q], t = a.dst[q];
+  const float k = 0.017453292519943295f;
+  const float tlat = a.lat[t] * k, tlon = a.lon[t] * k, ctl = __cosf(tlat);
+  float ft[KMAX], bt[KMAX];
+  if constexpr (K > 0) {
+    const float4* row = reinterpret_cast<const float4*>(a.lm + (size_t)t * 2 * K);
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) {
+      const float4 x = row[i];
+      ft[2 * i] = x.x;
+      ft[2 * i + 1] = x.y;
+      bt[2 * i] = x.z;
+      bt[2 * i + 1] = x.w;
+    }
+  }
+  auto heur = [&](int v) {
+    float hv = hdist(a, v, tlat, tlon, ctl);
+    if constexpr (K > 0) hv = fmaxf(hv, halt<K>(a, v, ft, bt));
+    return hv;
+  };
+  // (the reset word ST_INIT reads as a NaN g in this layout: map it to +inf)
+  auto gof = [](unsigned long long x) {
+    return x == ST_INIT ? __int_as_float(0x7f800000) : __uint_as_float((unsigned)(x >> 32));
+  };
+  auto pack = [](float g, unsigned p) { return ((unsigned long long)__float_as_uint(g) << 32) | p; };
+
+  if (lane == 0) {
+    hc[s] = heur(s);
+    st[s] = pack(0.f, 0x7fffffffu);
+    touched[0] = s;
+    nearA[0] = s;
+    s_far = 0;
+    s_touch = 1;
+    s_bad = 0;
+  }
+  __syncthreads();
+  int* cur = nearA;
+  int* nxt = nearB;
+  int nnear = 1;
+  float thr = heur(s) + delta;
+  long long expanded = 0;
+  int status = 1;
+  while (true) {
+    while (nnear > 0) {
+      if (lane == 0) s_next = 0;
+      __syncthreads();
+      const float best = gof(st[t]);
+      for (int i = lane; i < nnear; i += 64) {
+        const int v = cur[i];
+        const float gv = gof(st[v]);
+        float hv = hc[v];
+        if (hv != hv) hv = heur(v);
+        if (!(gv + hv < best)) continue;                 // cannot lead to a better path
+        const int e1 = a.indptr[v + 1];
+        for (int e = a.indptr[v]; e < e1; ++e) {
+          const int u = a.indices[e];
+          const float ng = gv + a.cost[e];
+          const unsigned long long nw = pack(ng, (unsigned)v);
+          // plain load first: most relaxations do not improve, and a 64-bit atomic to HBM costs
+          // far more than a load (the stage was bound by them)
+          const unsigned long long seen = st[u];
+          if (nw >= seen) continue;
+          const unsigned long long old = atomicMin(st + u, nw);
+          if (nw >= old) continue;
+          float hu;
+          if (old == ST_INIT) {
+            const int ti = atomicAdd(&s_touch, 1);
+            if (ti < a.cap) touched[ti] = u;
+            else s_bad = 1;
+            hu = heur(u);
+            hc[u] = hu;
+          } else {
+            hu = hc[u];
+            if (hu != hu) hu = heur(u);
+          }
+          const float f = ng + hu;
+          if (f < thr) {
+            const int ni = atomicAdd(&s_next, 1);
+            if (ni < NCAP) nxt[ni] = u;
+            else s_bad = 1;
+          } else {
+            const int fi = atomicAdd(&s_far, 1);
+            if (fi < FCAP) far[fi] = pack(f, (unsigned)u);
+            else s_bad = 1;
+          }
+        }
+      }
+      expanded += nnear;
+      __syncthreads();
+      nnear = s_next < NCAP ? s_next : NCAP;
+      int* tmp = cur;
+      cur = nxt;
+      nxt = tmp;
+      if (s_bad) { status = 2; break; }
+      if (expanded > a.max_iters) { status = 3; break; }
+    }
+    if (status >= 2) break;
+    // near band exhausted: optimal if no open node can beat best; else open the next band
+    const float best = gof(st[t]);
+    const int nfar = s_far < FCAP ? s_far : FCAP;
+    float fmin = __int_as_float(0x7f800000);
+    for (int i = lane; i < nfar; i += 64) {
+      const float f = gof(far[i]);
+      if (f < best) fmin = fminf(fmin, f);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) fmin = fminf(fmin, __shfl_xor(fmin, o));
+    if (!(fmin < best)) break;                        // done: best is optimal (or +inf: unreachable)
+    thr = fmin + delta;
+    // split far in place: f < thr -> near (cur), f < best -> keep (compacted), else drop.  A chunk of
+    // 64 is read before any of its kept entries is written, and writes never pass reads.
+    if (lane == 0) {
+      s_next = 0;
+      s_far = 0;
+    }
+    __syncthreads();
+    for (int i0 = 0; i0 < nfar; i0 += 64) {
+      const int i = i0 + lane;
+      const unsigned long long x = i < nfar ? far[i] : ~0ull;
+      const float f = gof(x);
+      const bool to_near = i < nfar && f < thr;
+      const bool keep = i < nfar && !to_near && f < best;
+      const unsigned long long mk = __ballot(keep);
+      const int base = s_far;
+      __syncthreads();
+      if (keep) far[base + __popcll(mk & ((1ull << lane) - 1))] = x;
+      if (to_near) {
+        const int ni = atomicAdd(&s_next, 1);
+        if (ni < NCAP) cur[ni] = (int)(unsigned)(x & 0xffffffffu);
+        else s_bad = 1;
+      }
+      if (lane == 0) s_far = base + __popcll(mk);
+      __syncthreads();
+    }
+    nnear = s_next < NCAP ? s_next : NCAP;
+    if (s_bad) { status = 2; break; }
+  }
+  const float total = gof(st[t]);
+  int len = 0;
+  if (status < 2) status = total < __int_as_float(0x7f800000) ? 0 : 1;
+  if (lane == 0) {
+    if (status == 0) {
+      int* path = a.out_path + (size_t)q * a.max_path;
+      int v = t;
+      while (true) {
+        if (len >= a.max_path) { status = 4; break; }
+        path[len++] = v;
+        if (v == s) break;
+        v = (int)((unsigned)st[v] & 0x7fffffffu);
+      }
+      if (status == 0) {
+        for (int i = 0, j = len - 1; i < j; ++i, --j) {
+          const int tmp = path[i];
+          path[i] = path[j];
+          path[j] = tmp;
+        }
+      } else {
+        len = 0;
+      }
+    }
+    if (a.out_iters) a.out_iters[q] = (int)(expanded < 0x7fffffff ? expanded : 0x7fffffff);
+    a.out_cost[q] = status == 0 ? total : -1.f;
+    a.out_len[q] = len;
+    a.out_status[q] = status;
+  }
+  __syncthreads();
+  const int nt = s_touch < a.cap ? s_touch : a.cap;
+  for (int i = lane; i < nt; i += 64) {
+    const int v = touched[i];
+    st[v] = ST_INIT;
+    hc[v] = __int_as_float(-1);                      // NaN: not cached
+  }
+}
+
+hipError_t launch_astar_wave(const int* indptr, const int* indices, const float* cost, const float* lat,
+                             const float* lon, const int* src, const int* dst, void* state, void* heap,
+                             int* touched, float* out_cost, int* out_len, int* out_status, int* out_path,
+                             int N, int Q, int slots, int cap, int max_path, int max_iters, float inv_vmax,
+                             const float* lm, int K, const int* qidx, int T, float delta, float* hcache,
+                             int hrows, hipStream_t stream, int* out_iters) {
+  int n = T < slots ? T : slots;
+  if (n > hrows) n = hrows;
+  if (n <= 0) return hipSuccess;
+  if (lm != nullptr && K != 32 && K != 16 && K != 8) return hipErrorInvalidValue;
+  if (cap < 128) return hipErrorInvalidValue;
+  AstarArgs a{indptr, indices, cost, lat, lon, src, dst, (unsigned long long*)state,
+              (unsigned long long*)heap, touched, out_cost, out_len, out_status, out_path,
+              N, Q, 0, slots, cap, max_path, max_iters, inv_vmax, lm, K, out_iters};
+  if (lm == nullptr) hipLaunchKernelGGL(astar_wave_kernel<0>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, hcache);
+  else if (K == 8) hipLaunchKernelGGL(astar_wave_kernel<8>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, hcache);
+  else if (K == 16) hipLaunchKernelGGL(astar_wave_kernel<16>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, hcache);
+  else hipLaunchKernelGGL(astar_wave_kernel<32>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, hcache);
+  return hipGetLastError();
+}
+
 hipError_t launch_astar(const int* indptr, const int* indices, const float* cost, const float* lat,
                         const float* lon, const int* src, const int* dst, void* state,
                         void* heap, int* touched, float* out_cost, int* out_len, int* out_status,

@@ -388,7 +388,8 @@ void astar(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torc
            torch::Tensor heap, torch::Tensor touched, torch::Tensor out_cost,
            torch::Tensor out_len, torch::Tensor out_status, torch::Tensor out_path, int64_t q0,
            int64_t max_iters, double inv_vmax, c10::optional<torch::Tensor> landmarks,
-           c10::optional<torch::Tensor> out_iters) {
+           c10::optional<torch::Tensor> out_iters, c10::optional<torch::Tensor> qidx, double delta,
+           c10::optional<torch::Tensor> hcache) {
   for (auto* t : {&indptr, &indices, &cost, &lat, &lon, &src, &dst, &g, &heap, &touched,
                   &out_cost, &out_len, &out_status, &out_path})
     check_dev(*t, "astar tensor");
@@ -420,6 +421,26 @@ void astar(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torc
     iters = out_iters->data_ptr<int>();
   }
   const c10::DeviceGuard guard(g.device());
+  if (qidx.has_value() && qidx->defined()) {
+    // tail stage: one wave per listed query (slot = position in qidx, < S)
+    check_dev(*qidx, "qidx");
+    TORCH_CHECK(qidx->scalar_type() == torch::kInt32 && qidx->numel() <= g.size(0), "qidx int32 [T <= S]");
+    TORCH_CHECK(heap.size(1) >= 128, "heap row too small for the wave stage");
+    TORCH_CHECK(hcache.has_value() && hcache->defined(), "wave stage needs the heuristic cache");
+    check_dev(*hcache, "hcache");
+    TORCH_CHECK(hcache->scalar_type() == torch::kFloat32 && hcache->dim() == 2 && hcache->size(1) == N &&
+                qidx->numel() <= hcache->size(0), "hcache f32 [>= T, N]");
+    RT_CHECK_HIP(rt::launch_astar_wave(indptr.data_ptr<int>(), indices.data_ptr<int>(), cost.data_ptr<float>(),
+                                       lat.data_ptr<float>(), lon.data_ptr<float>(), src.data_ptr<int>(),
+                                       dst.data_ptr<int>(), g.data_ptr(), heap.data_ptr(), touched.data_ptr<int>(),
+                                       out_cost.data_ptr<float>(), out_len.data_ptr<int>(),
+                                       out_status.data_ptr<int>(), out_path.data_ptr<int>(), (int)N, (int)Q,
+                                       (int)g.size(0), (int)heap.size(1), (int)out_path.size(1), (int)max_iters,
+                                       (float)inv_vmax, lm, K, qidx->data_ptr<int>(), (int)qidx->numel(),
+                                       (float)delta, hcache->data_ptr<float>(), (int)hcache->size(0),
+                                       cur_stream(g), iters));
+    return;
+  }
   RT_CHECK_HIP(rt::launch_astar(indptr.data_ptr<int>(), indices.data_ptr<int>(), cost.data_ptr<float>(),
                                 lat.data_ptr<float>(), lon.data_ptr<float>(), src.data_ptr<int>(),
                                 dst.data_ptr<int>(), g.data_ptr(),
@@ -643,7 +664,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("indptr"), py::arg("indices"), py::arg("cost"), py::arg("lat"), py::arg("lon"), py::arg("src"),
         py::arg("dst"), py::arg("state"), py::arg("heap"), py::arg("touched"), py::arg("out_cost"),
         py::arg("out_len"), py::arg("out_status"), py::arg("out_path"), py::arg("q0"), py::arg("max_iters"),
-        py::arg("inv_vmax"), py::arg("landmarks") = py::none(), py::arg("out_iters") = py::none());
+        py::arg("inv_vmax"), py::arg("landmarks") = py::none(), py::arg("out_iters") = py::none(),
+        py::arg("qidx") = py::none(), py::arg("delta") = 60.0, py::arg("hcache") = py::none());
   m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
   m.def("forest_predict_lds", &forest_predict_lds, "K4: LDS-staged tree chunks, 2 walks per thread");
   m.def("pscore_create", &pscore_create, "resident single-request scorer kernel on the blob's GPU");

@@ -64,6 +64,12 @@ hipError_t launch_astar(const int* indptr, const int* indices, const float* cost
                         int* out_path, int N, int Q, int q0, int slots, int cap, int max_path,
                         int max_iters, float inv_vmax, const float* lm, int K, hipStream_t stream,
                         int* out_iters = nullptr);
+hipError_t launch_astar_wave(const int* indptr, const int* indices, const float* cost, const float* lat,
+                             const float* lon, const int* src, const int* dst, void* state, void* heap,
+                             int* touched, float* out_cost, int* out_len, int* out_status, int* out_path,
+                             int N, int Q, int slots, int cap, int max_path, int max_iters, float inv_vmax,
+                             const float* lm, int K, const int* qidx, int T, float delta, float* hcache,
+                             int hrows, hipStream_t stream, int* out_iters);
 
 // ---- tree ensemble (K4) : forest.hip ----
 hipError_t launch_forest(const void* rec, const float* values, const unsigned* info, const int* roots,

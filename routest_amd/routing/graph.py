@@ -13,6 +13,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import datetime as dt
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -147,6 +149,17 @@ class BatchedAstar:
         self.lat = torch.from_numpy(g.lat.astype(np.float32)).to(d)
         self.lon = torch.from_numpy(g.lon.astype(np.float32)).to(d)
         self.slots, self.cap, self.max_path, self.max_iters = slots, cap, max_path, max_iters
+        # two-stage search: the lane-per-query kernel gets `lane_pops` heap pops per query; the few
+        # searches still open then run one WAVE per query (f-band expansion, csrc/astar.hip
+        # astar_wave_kernel), so the launch is no longer as long as the single longest search.
+        # ROUTEST_ASTAR_LANE_POPS=0 disables the tail stage.
+        # 80k legs (bench/astar_stages.py): lane 1000 pops + waves 117 ms, 2000 + waves 124 ms,
+        # lane only 236 ms; the wave stage wants all of its queries resident at once (65k: 84 ms
+        # vs 100 ms in 16k chunks), hence up to 65536 wave slots (26 GB of heuristic cache)
+        self.lane_pops = int(os.environ.get("ROUTEST_ASTAR_LANE_POPS", "1000"))
+        self.wave_delta = float(os.environ.get("ROUTEST_ASTAR_DELTA", "10"))
+        self.wave_slots = min(slots, int(os.environ.get("ROUTEST_ASTAR_WAVE_SLOTS", "65536")))
+        self.hcache = None            # [wave_slots, N] f32 heuristic cache of the wave stage (NaN = empty)
         N = g.num_nodes
         # tightest admissible + consistent heuristic: every edge length is 1.15 x its great-circle
         # length (so any path >= 1.15 x the great-circle s-t distance) and every edge is traversed
@@ -163,6 +176,7 @@ class BatchedAstar:
         self.touched = torch.empty((slots, cap), dtype=torch.int32, device=d)
 
     def update_costs(self, cost: np.ndarray) -> None:
+        # (the wave stage's heuristic cache is per query and reset after each search: nothing to drop)
         cost = np.asarray(cost, dtype=np.float32)
         self.cost.copy_(torch.from_numpy(cost))
         self.v_max = float((self.g.length_m / np.maximum(cost.astype(np.float64), 1e-6)).max()) * 1.0001
@@ -194,10 +208,22 @@ class BatchedAstar:
         out_status = torch.empty(Q, dtype=torch.int32, device=d)
         out_path = torch.empty((Q, self.max_path), dtype=torch.int32, device=d)
         self.last_iters = torch.empty(Q, dtype=torch.int32, device=d)   # heap pops per query
+        lane_iters = min(self.max_iters, self.lane_pops) if self.lane_pops > 0 else self.max_iters
         for q0 in range(0, Q, self.slots):
             self.C.astar(self.indptr, self.indices, self.cost, self.lat, self.lon, s, t, self.state,
                          self.heap, self.touched, out_cost, out_len, out_status, out_path,
-                         q0, self.max_iters, self.inv_vmax, self.lm, self.last_iters)
+                         q0, lane_iters, self.inv_vmax, self.lm, self.last_iters)
+        if lane_iters < self.max_iters:
+            tail = (out_status == 3).nonzero().flatten().to(torch.int32)
+            self.last_tail = int(tail.numel())
+            if self.last_tail and self.hcache is None:
+                self.hcache = torch.full((self.wave_slots, self.g.num_nodes), float("nan"),
+                                         dtype=torch.float32, device=d)
+            for i0 in range(0, self.last_tail, self.wave_slots):
+                self.C.astar(self.indptr, self.indices, self.cost, self.lat, self.lon, s, t, self.state,
+                             self.heap, self.touched, out_cost, out_len, out_status, out_path,
+                             0, self.max_iters, self.inv_vmax, self.lm, self.last_iters,
+                             tail[i0:i0 + self.wave_slots].contiguous(), self.wave_delta, self.hcache)
         if order is not None:
             idx = torch.from_numpy(order.astype(np.int64)).to(d)
             res = []

@@ -49,3 +49,33 @@ def test_astar_optimal_costs_and_valid_paths(graph_and_cost):
     # workspace was restored: a second batch gives identical answers
     c2 = a.run(src, dst)[0].cpu().numpy()
     assert np.array_equal(c, c2)
+
+
+@pytest.mark.parametrize("lane_pops,delta", [(0, 60.0), (40, 60.0), (40, 5.0), (40, 600.0)])
+def test_wave_tail_stage_exact(graph_and_cost, monkeypatch, lane_pops, delta):
+    """Searches that exhaust the lane budget finish in the one-wave-per-query stage with the same
+    optimal costs (vs scipy Dijkstra) and valid paths; lane_pops=0 sends every query there."""
+    g, cost, _ = graph_and_cost
+    src, dst = synth_route_queries(g, 600, seed=2)
+    src[:3] = dst[:3]                                   # s == t queries too
+    monkeypatch.setenv("ROUTEST_ASTAR_LANE_POPS", str(lane_pops if lane_pops else 1))
+    monkeypatch.setenv("ROUTEST_ASTAR_DELTA", str(delta))
+    a = BatchedAstar(g, cost, "cuda:0", slots=1024, cap=65536)
+    c, n, st, p = a.run(src, dst)
+    assert a.last_tail > 300                            # most queries went through the wave stage
+    c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
+    assert (st == 0).all()
+    ref = dijkstra_ref(g, cost, src, dst)
+    np.testing.assert_allclose(c, ref, rtol=1e-4, atol=1e-3)
+    for i in range(0, len(src), 7):
+        path = p[i, :n[i]]
+        assert path[0] == src[i] and path[-1] == dst[i]
+        tot = 0.0
+        for u, v in zip(path[:-1], path[1:]):
+            nb = g.indices[g.indptr[u]:g.indptr[u + 1]]
+            k = np.where(nb == v)[0]
+            assert len(k) == 1
+            tot += cost[g.indptr[u] + k[0]]
+        assert abs(tot - c[i]) <= 1e-3 * max(1.0, c[i])
+    c2 = a.run(src, dst)[0].cpu().numpy()                 # workspace restored by both stages
+    assert np.array_equal(c, c2)
