@@ -379,37 +379,52 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
         float hv = hc[v];
         if (hv != hv) hv = heur(v);
         if (!(gv + hv < best)) continue;                 // cannot lead to a better path
-        const int e1 = a.indptr[v + 1];
-        for (int e = a.indptr[v]; e < e1; ++e) {
-          const int u = a.indices[e];
-          const float ng = gv + a.cost[e];
-          const unsigned long long nw = pack(ng, (unsigned)v);
-          // plain load first: most relaxations do not improve, and a 64-bit atomic to HBM costs
-          // far more than a load (the stage was bound by them)
-          const unsigned long long seen = st[u];
-          if (nw >= seen) continue;
-          const unsigned long long old = atomicMin(st + u, nw);
-          if (nw >= old) continue;
-          float hu;
-          if (old == ST_INIT) {
-            const int ti = atomicAdd(&s_touch, 1);
-            if (ti < a.cap) touched[ti] = u;
-            else s_bad = 1;
-            hu = heur(u);
-            hc[u] = hu;
-          } else {
-            hu = hc[u];
-            if (hu != hu) hu = heur(u);
+        const int e0 = a.indptr[v], e1 = a.indptr[v + 1];
+        for (int eb = e0; eb < e1; eb += RB) {
+          // same batching as the lane kernel: all (target, cost), then all target words, in flight
+          int uu[RB];
+          float cc[RB];
+          unsigned long long seen[RB];
+#pragma unroll
+          for (int j = 0; j < RB; ++j) {
+            const bool in = eb + j < e1;
+            uu[j] = in ? a.indices[eb + j] : v;
+            cc[j] = in ? a.cost[eb + j] : 0.f;
           }
-          const float f = ng + hu;
-          if (f < thr) {
-            const int ni = atomicAdd(&s_next, 1);
-            if (ni < NCAP) nxt[ni] = u;
-            else s_bad = 1;
-          } else {
-            const int fi = atomicAdd(&s_far, 1);
-            if (fi < FCAP) far[fi] = pack(f, (unsigned)u);
-            else s_bad = 1;
+#pragma unroll
+          for (int j = 0; j < RB; ++j) seen[j] = eb + j < e1 ? st[uu[j]] : 0ull;
+#pragma unroll
+          for (int j = 0; j < RB; ++j) {
+            if (eb + j >= e1) continue;
+            const int u = uu[j];
+            const float ng = gv + cc[j];
+            const unsigned long long nw = pack(ng, (unsigned)v);
+            // plain load first: most relaxations do not improve, and a 64-bit atomic to HBM costs
+            // far more than a load
+            if (nw >= seen[j]) continue;
+            const unsigned long long old = atomicMin(st + u, nw);
+            if (nw >= old) continue;
+            float hu;
+            if (old == ST_INIT) {
+              const int ti = atomicAdd(&s_touch, 1);
+              if (ti < a.cap) touched[ti] = u;
+              else s_bad = 1;
+              hu = heur(u);
+              hc[u] = hu;
+            } else {
+              hu = hc[u];
+              if (hu != hu) hu = heur(u);
+            }
+            const float f = ng + hu;
+            if (f < thr) {
+              const int ni = atomicAdd(&s_next, 1);
+              if (ni < NCAP) nxt[ni] = u;
+              else s_bad = 1;
+            } else {
+              const int fi = atomicAdd(&s_far, 1);
+              if (fi < FCAP) far[fi] = pack(f, (unsigned)u);
+              else s_bad = 1;
+            }
           }
         }
       }
