@@ -153,10 +153,11 @@ class BatchedAstar:
         # searches still open then run one WAVE per query (f-band expansion, csrc/astar.hip
         # astar_wave_kernel), so the launch is no longer as long as the single longest search.
         # ROUTEST_ASTAR_LANE_POPS=0 disables the tail stage.
-        # 80k legs (bench/astar_stages.py): lane 1000 pops + waves 117 ms, 2000 + waves 124 ms,
+        # 80k legs (bench/astar_tail.py, band 10 s): lane budget 2000 117 ms, 1000 112 ms, 500 105 ms,
+        # 250 108 ms, everything in the wave stage 101 ms (more wave work, fine for big batches);
         # lane only 236 ms; the wave stage wants all of its queries resident at once (65k: 84 ms
         # vs 100 ms in 16k chunks), hence up to 65536 wave slots (26 GB of heuristic cache)
-        self.lane_pops = int(os.environ.get("ROUTEST_ASTAR_LANE_POPS", "1000"))
+        self.lane_pops = int(os.environ.get("ROUTEST_ASTAR_LANE_POPS", "500"))
         self.wave_delta = float(os.environ.get("ROUTEST_ASTAR_DELTA", "10"))
         self.wave_slots = min(slots, int(os.environ.get("ROUTEST_ASTAR_WAVE_SLOTS", "65536")))
         self.hcache = None            # [wave_slots, N] f32 heuristic cache of the wave stage (NaN = empty)
