@@ -25,9 +25,12 @@ def test_edge_costs_kernel_vs_cpu(graph_and_cost):
     np.testing.assert_allclose(cg, cc, rtol=1e-2, atol=0.05)
 
 
-def test_astar_optimal_costs_and_valid_paths(graph_and_cost):
+@pytest.mark.parametrize("reorder", ["0", "1"])
+def test_astar_optimal_costs_and_valid_paths(graph_and_cost, monkeypatch, reorder):
+    """reorder=1: the searches run on the Morton-renumbered graph; paths come back in caller ids."""
     g, cost, _ = graph_and_cost
     src, dst = synth_route_queries(g, 2000, seed=1)
+    monkeypatch.setenv("ROUTEST_ASTAR_REORDER", reorder)
     a = BatchedAstar(g, cost, "cuda:0", slots=1024, cap=65536)
     c, n, st, p = a.run(src, dst)
     c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
