@@ -44,8 +44,9 @@ def parse_args():
                     help="zerocopy: the kernel reads pinned host records and writes pinned host "
                          "predictions over PCIe; host: copy-engine H2D/D2H pipeline; device: "
                          "records already resident in HBM")
-    ap.add_argument("--rec", type=int, choices=[8, 16], default=8,
-                    help="wire record bytes per request (8: compact, 16: full with epoch seconds)")
+    ap.add_argument("--rec", type=int, choices=[6, 8, 16], default=6,
+                    help="wire record bytes per request (6: bulk 48-bit, 8: compact, 16: full with "
+                         "epoch seconds) — routest_amd/models/features.py")
     ap.add_argument("--variant", type=int, default=-1)
     ap.add_argument("--h2d-streams", type=int, default=1,
                     help="hybrid: split each step's record copy over this many copy streams")
@@ -82,8 +83,9 @@ def main() -> None:
     from routest_amd.data.synth import synth_records
     from routest_amd.models.features import records_to_features
     from routest_amd.models.mlp3 import EtaMLP
-    from routest_amd.models.features import records_to_compact
-    from routest_amd.ops.eta_mlp import EtaMlpKernel, records8_to_tensor, records_to_tensor
+    from routest_amd.models.features import records_to_compact, records_to_compact6
+    from routest_amd.ops.eta_mlp import (EtaMlpKernel, records6_to_tensor, records8_to_tensor,
+                                         records_to_tensor)
 
     torch.manual_seed(1234)
     model = EtaMLP(a.hidden)
@@ -93,8 +95,9 @@ def main() -> None:
 
     B = a.batch
     rec, _ = synth_records(B, seed=100 + rank)
-    host_rec = (records8_to_tensor(records_to_compact(rec)) if a.rec == 8
-                else records_to_tensor(rec)).pin_memory()
+    host_rec = (records6_to_tensor(records_to_compact6(rec)) if a.rec == 6 else
+                records8_to_tensor(records_to_compact(rec)) if a.rec == 8 else
+                records_to_tensor(rec)).pin_memory()
     nbuf = 3
     dev_rec = [torch.empty_like(host_rec, device=dev) for _ in range(nbuf)]
     host_out = [torch.empty(B, dtype=torch.float32).pin_memory() for _ in range(nbuf)]

@@ -42,13 +42,22 @@ void check_dev(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
+// Record wire format from the tensor: int32 [B,4] = 16-byte, int32 [B,2] = 8-byte compact,
+// int16 [B,3] = 6-byte bulk records (routest_amd/models/features.py).
+static int record_bytes(const torch::Tensor& r) {
+  if (r.dim() == 2 && r.scalar_type() == torch::kInt32 && (r.size(1) == 4 || r.size(1) == 2))
+    return (int)r.size(1) * 4;
+  if (r.dim() == 2 && r.scalar_type() == torch::kInt16 && r.size(1) == 3) return 6;
+  TORCH_CHECK(false, "records must be int32 [B,4] (16-byte), int32 [B,2] (8-byte) or int16 [B,3] "
+              "(6-byte) records");
+  return 0;
+}
+
 torch::Tensor eta_mlp3_forward(torch::Tensor records, torch::Tensor blob, int64_t H,
                                std::vector<double> norm, int64_t variant) {
   check_dev(records, "records");
   check_dev(blob, "blob");
-  TORCH_CHECK(records.scalar_type() == torch::kInt32 && records.dim() == 2 &&
-                  (records.size(1) == 4 || records.size(1) == 2),
-              "records must be int32 [B,4] (16-byte records) or [B,2] (8-byte compact records)");
+  const int rb = record_bytes(records);
   TORCH_CHECK(blob.scalar_type() == torch::kUInt8, "blob must be uint8");
   TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H),
               "blob has ", blob.numel(), " bytes, expected ", rt::eta_mlp3_blob_bytes((int)H),
@@ -66,8 +75,7 @@ torch::Tensor eta_mlp3_forward(torch::Tensor records, torch::Tensor blob, int64_
   }
   RT_CHECK_HIP(rt::launch_eta_mlp3_fwd(records.data_ptr(), out.data_ptr<float>(), B,
                                        blob.data_ptr(), (int)H, np, (int)variant,
-                                       num_cus(records.device().index()), cur_stream(records),
-                                       records.size(1) == 2));
+                                       num_cus(records.device().index()), cur_stream(records), rb));
   return out;
 }
 
@@ -88,9 +96,7 @@ static void* kernel_ptr(const torch::Tensor& t, const char* name) {
 
 void eta_mlp3_forward_hostio(torch::Tensor records, torch::Tensor out, torch::Tensor blob, int64_t H,
                              std::vector<double> norm, int64_t variant) {
-  TORCH_CHECK(records.scalar_type() == torch::kInt32 && records.dim() == 2 &&
-                  (records.size(1) == 4 || records.size(1) == 2),
-              "records must be int32 [B,4] or [B,2]");
+  const int rb = record_bytes(records);
   TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.numel() == records.size(0), "out must be f32 [B]");
   check_dev(blob, "blob");
   TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
@@ -107,7 +113,7 @@ void eta_mlp3_forward_hostio(torch::Tensor records, torch::Tensor out, torch::Te
   }
   RT_CHECK_HIP(rt::launch_eta_mlp3_fwd(drec, (float*)dout, (int)records.size(0), blob.data_ptr(),
                                        (int)H, np, (int)variant, num_cus(blob.device().index()),
-                                       cur_stream(blob), records.size(1) == 2));
+                                       cur_stream(blob), rb));
 }
 
 torch::Tensor eta_featurize(torch::Tensor records) {

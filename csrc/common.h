@@ -172,6 +172,22 @@ __device__ __forceinline__ bf16x8 featurize8_bf16(const int2 rc, const int h, co
   return h == 0 ? oh : nb;
 }
 
+// 6-byte records (features.py RECORD6): one 48-bit word, lo = bits 0-31, hi = bits 32-47.
+// Same fragment as featurize8_bf16 (distance -> km exactly as q * 0.125 m * 1e-3).
+__device__ __forceinline__ bf16x8 featurize6_bf16(const unsigned lo, const unsigned hi, const int h,
+                                                  const NormParams& np) {
+  const float wdn = (float)((hi >> 2) & 7u) * np.scale[0] + np.shift[0];
+  const float hrn = (float)((hi >> 5) & 31u) * np.scale[1] + np.shift[1];
+  const float kmn = ((float)(lo & 0x7ffffffu) * (0.125f * 1e-3f)) * np.scale[2] + np.shift[2];
+  const float agn = (float)((lo >> 27) | ((hi & 3u) << 5)) * np.scale[3] + np.shift[3];
+  const float kmh = (float)(__bf16)kmn;
+  const float agh = (float)(__bf16)agn;
+  const float f[8] = {wdn, hrn, kmh, agh, kmn - kmh, agn - agh, 1.f, 1.f};
+  const bf16x8 nb = to_bf16x8(f);
+  const bf16x8 oh = onehot_pair_bf16((hi >> 10) & 7u, (hi >> 13) & 7u);
+  return h == 0 ? oh : nb;
+}
+
 // Unnormalised R16 features (12 columns, reference order) of one record — the K1 standalone op.
 __device__ __forceinline__ void featurize_raw12(const int4 rc, float f[12]) {
   const int w = rc.w & 0xff;

@@ -27,30 +27,51 @@
 
 namespace rt {
 
-// Record loads for the two wire formats (16-byte full record, 8-byte compact record).
-template <bool REC8>
+// Record loads for the three wire formats (16-byte full, 8-byte compact, 6-byte bulk record).
+// ``T`` is what a lane holds between the prefetching load and its use: raw loaded words only, so
+// the prefetch is never waited on before the tile that consumes it.
+template <int RB>
 struct RecT;
 template <>
-struct RecT<false> {
+struct RecT<16> {
   using T = int4;
   static __device__ __forceinline__ T zero() { return make_int4(0, 0, 0, 0); }
+  static __device__ __forceinline__ T load(const void* p, int i) { return ((const int4*)p)[i]; }
   static __device__ __forceinline__ bf16x8 feat(const T& r, int h, const NormParams& np) {
     return featurize_bf16(r, h, np);
   }
 };
 template <>
-struct RecT<true> {
+struct RecT<8> {
   using T = int2;
   static __device__ __forceinline__ T zero() { return make_int2(0, 0); }
+  static __device__ __forceinline__ T load(const void* p, int i) { return ((const int2*)p)[i]; }
   static __device__ __forceinline__ bf16x8 feat(const T& r, int h, const NormParams& np) {
     return featurize8_bf16(r, h, np);
   }
 };
+struct Rec6Words {
+  unsigned a, b, c;
+};
+template <>
+struct RecT<6> {
+  // 6-byte rows are only 2-byte aligned: three u16 loads (one VMEM triple per 32-row tile,
+  // ~4k MFMA cycles of work) rather than a dword load that would straddle rows
+  using T = Rec6Words;
+  static __device__ __forceinline__ T zero() { return {0u, 0u, 0u}; }
+  static __device__ __forceinline__ T load(const void* p, int i) {
+    const unsigned short* s = (const unsigned short*)p + 3 * (size_t)i;
+    return {s[0], s[1], s[2]};
+  }
+  static __device__ __forceinline__ bf16x8 feat(const T& r, int h, const NormParams& np) {
+    return featurize6_bf16(r.a | (r.b << 16), r.c, h, np);
+  }
+};
 
-template <int H, bool LDSW, int TPB, bool PIN = false, bool REC8 = false, bool PIPE = false,
+template <int H, bool LDSW, int TPB, bool PIN = false, int RB = 16, bool PIPE = false,
           bool PRIO = false>
 __global__ __launch_bounds__(TPB, LDSW ? TPB / 256 : 1) void eta_mlp3_fwd_kernel(
-    const typename RecT<REC8>::T* __restrict__ rec, float* __restrict__ out, int B,
+    const void* __restrict__ rec, float* __restrict__ out, int B,
     const unsigned char* __restrict__ blob, NormParams np) {
   constexpr int KS = H / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -79,14 +100,14 @@ __global__ __launch_bounds__(TPB, LDSW ? TPB / 256 : 1) void eta_mlp3_fwd_kernel
   // records are prefetched one tile ahead: with zero-copy I/O they come straight from pinned host
   // memory over PCIe, and the next tile's load then overlaps this tile's ~4k MFMA cycles
   int tile = blockIdx.x * wpb + (threadIdx.x >> 6);
-  using R = RecT<REC8>;
+  using R = RecT<RB>;
   typename R::T rc_next = R::zero();
-  if (tile < ntiles && tile * 32 + r < B) rc_next = rec[tile * 32 + r];
+  if (tile < ntiles && tile * 32 + r < B) rc_next = R::load(rec, tile * 32 + r);
   for (; tile < ntiles; tile += stride) {
     const int row = tile * 32 + r;
     const typename R::T rc = rc_next;
     const int nrow = (tile + stride) * 32 + r;
-    if (tile + stride < ntiles && nrow < B) rc_next = rec[nrow];
+    if (tile + stride < ntiles && nrow < B) rc_next = R::load(rec, nrow);
     const bf16x8 xb = R::feat(rc, h, np);
 
     bf16x8 h1[KS];
@@ -125,16 +146,15 @@ __global__ __launch_bounds__(256) void eta_featurize_kernel(const int4* __restri
 }
 
 // Persistent LDS-staged launch: one workgroup of T threads per CU (139 KiB of LDS at H = 256).
-template <int H, int T, bool PIN, bool REC8, bool PIPE = false, bool PRIO = false>
+template <int H, int T, bool PIN, int RB, bool PIPE = false, bool PRIO = false>
 static hipError_t launch_lds(const void* rec, float* out, int B, const void* blob,
                              const NormParams& np, int num_cus, hipStream_t stream) {
-  using RT = typename RecT<REC8>::T;
   using L = Mlp3Layout<H>;
   static bool attr_set[64] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (!attr_set[dev & 63]) {
-    hipError_t e = hipFuncSetAttribute((const void*)eta_mlp3_fwd_kernel<H, true, T, PIN, REC8, PIPE, PRIO>,
+    hipError_t e = hipFuncSetAttribute((const void*)eta_mlp3_fwd_kernel<H, true, T, PIN, RB, PIPE, PRIO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::BLOB);
     if (e != hipSuccess) return e;
     attr_set[dev & 63] = true;
@@ -142,15 +162,14 @@ static hipError_t launch_lds(const void* rec, float* out, int B, const void* blo
   const int ntiles = (B + 31) / 32;
   int grid = (ntiles + T / 64 - 1) / (T / 64);
   if (grid > num_cus) grid = num_cus;
-  hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, true, T, PIN, REC8, PIPE, PRIO>), dim3(grid), dim3(T), L::BLOB,
-                     stream, (const RT*)rec, out, B, (const unsigned char*)blob, np);
+  hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, true, T, PIN, RB, PIPE, PRIO>), dim3(grid), dim3(T), L::BLOB,
+                     stream, rec, out, B, (const unsigned char*)blob, np);
   return hipGetLastError();
 }
 
-template <int H, bool REC8>
+template <int H, int RB>
 static hipError_t launch_fwd_h(const void* rec, float* out, int B, const void* blob,
                                const NormParams& np, int variant, int num_cus, hipStream_t stream) {
-  using RT = typename RecT<REC8>::T;
   // variant: -1 auto, 0 global weights, LDS-staged: 1 = 512 thr, 2 = 768 thr, 3/4 = same + pinned
   // read/MFMA interleave (auto -> 3, the measured best), 5/6 = 3/4 + software-pipelined epilogue,
   // 7 = 5 + static priority for waves 4-7, 8 = 3 + priority
@@ -161,39 +180,42 @@ static hipError_t launch_fwd_h(const void* rec, float* out, int B, const void* b
   bool use_lds = lds_fits && (variant >= 1 || (variant < 0 && ntiles >= num_cus * 8 * 2));
   if (use_lds) {
     switch (variant) {
-      case 2: return launch_lds<H, 768, false, REC8>(rec, out, B, blob, np, num_cus, stream);
-      case 1: return launch_lds<H, 512, false, REC8>(rec, out, B, blob, np, num_cus, stream);
-      case 4: return launch_lds<H, 768, true, REC8>(rec, out, B, blob, np, num_cus, stream);
-      case 5: return launch_lds<H, 512, true, REC8, true>(rec, out, B, blob, np, num_cus, stream);
-      case 6: return launch_lds<H, 768, true, REC8, true>(rec, out, B, blob, np, num_cus, stream);
-      case 7: return launch_lds<H, 512, true, REC8, true, true>(rec, out, B, blob, np, num_cus, stream);
-      case 8: return launch_lds<H, 512, true, REC8, false, true>(rec, out, B, blob, np, num_cus, stream);
-      default: return launch_lds<H, 512, true, REC8>(rec, out, B, blob, np, num_cus, stream);
+      case 2: return launch_lds<H, 768, false, RB>(rec, out, B, blob, np, num_cus, stream);
+      case 1: return launch_lds<H, 512, false, RB>(rec, out, B, blob, np, num_cus, stream);
+      case 4: return launch_lds<H, 768, true, RB>(rec, out, B, blob, np, num_cus, stream);
+      case 5: return launch_lds<H, 512, true, RB, true>(rec, out, B, blob, np, num_cus, stream);
+      case 6: return launch_lds<H, 768, true, RB, true>(rec, out, B, blob, np, num_cus, stream);
+      case 7: return launch_lds<H, 512, true, RB, true, true>(rec, out, B, blob, np, num_cus, stream);
+      case 8: return launch_lds<H, 512, true, RB, false, true>(rec, out, B, blob, np, num_cus, stream);
+      default: return launch_lds<H, 512, true, RB>(rec, out, B, blob, np, num_cus, stream);
     }
   } else {
     // 4 waves per workgroup, one tile per wave
     int grid = (ntiles + 3) / 4;
-    hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, false, 256, false, REC8>), dim3(grid), dim3(256), 0,
-                       stream, (const RT*)rec, out, B, (const unsigned char*)blob, np);
+    hipLaunchKernelGGL((eta_mlp3_fwd_kernel<H, false, 256, false, RB>), dim3(grid), dim3(256), 0,
+                       stream, rec, out, B, (const unsigned char*)blob, np);
   }
   return hipGetLastError();
 }
 
+template <int RB>
+static hipError_t launch_fwd_rb(const void* rec, float* out, int B, const void* blob, int H,
+                                const NormParams& np, int variant, int num_cus, hipStream_t stream) {
+  switch (H) {
+    case 64: return launch_fwd_h<64, RB>(rec, out, B, blob, np, variant, num_cus, stream);
+    case 128: return launch_fwd_h<128, RB>(rec, out, B, blob, np, variant, num_cus, stream);
+    case 256: return launch_fwd_h<256, RB>(rec, out, B, blob, np, variant, num_cus, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 hipError_t launch_eta_mlp3_fwd(const void* rec, float* out, int B, const void* blob, int H,
                                const NormParams& np, int variant, int num_cus, hipStream_t stream,
-                               bool rec8) {
-  if (rec8) {
-    switch (H) {
-      case 64: return launch_fwd_h<64, true>(rec, out, B, blob, np, variant, num_cus, stream);
-      case 128: return launch_fwd_h<128, true>(rec, out, B, blob, np, variant, num_cus, stream);
-      case 256: return launch_fwd_h<256, true>(rec, out, B, blob, np, variant, num_cus, stream);
-      default: return hipErrorInvalidValue;
-    }
-  }
-  switch (H) {
-    case 64: return launch_fwd_h<64, false>(rec, out, B, blob, np, variant, num_cus, stream);
-    case 128: return launch_fwd_h<128, false>(rec, out, B, blob, np, variant, num_cus, stream);
-    case 256: return launch_fwd_h<256, false>(rec, out, B, blob, np, variant, num_cus, stream);
+                               int rec_bytes) {
+  switch (rec_bytes) {
+    case 16: return launch_fwd_rb<16>(rec, out, B, blob, H, np, variant, num_cus, stream);
+    case 8: return launch_fwd_rb<8>(rec, out, B, blob, H, np, variant, num_cus, stream);
+    case 6: return launch_fwd_rb<6>(rec, out, B, blob, H, np, variant, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }

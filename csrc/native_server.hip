@@ -456,7 +456,7 @@ class Reactor {
           pscore_park(ps);
         }
         e = launch_eta_mlp3_fwd(d_rec_, d_out_, (int)nrec_, cfg_.blob, cfg_.H, cfg_.np, cfg_.variant,
-                                cfg_.num_cus, stream_, false);
+                                cfg_.num_cus, stream_, 16);
         if (e == hipSuccess) e = hipStreamSynchronize(stream_);
       }
       st_.launches.fetch_add(1, std::memory_order_relaxed);

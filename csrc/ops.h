@@ -16,7 +16,7 @@ size_t eta_mlp3_blob_bytes(int H);
 // variant: -1 auto, 0 weights from global/L2, 1 weights staged in LDS (persistent grid)
 hipError_t launch_eta_mlp3_fwd(const void* rec, float* out, int B, const void* blob, int H,
                                const NormParams& np, int variant, int num_cus, hipStream_t stream,
-                               bool rec8 = false);
+                               int rec_bytes = 16);   // 16, 8 or 6-byte records
 hipError_t launch_eta_featurize(const void* rec, float* out, int B, hipStream_t stream);
 
 // ---- ETA MLP training (K3) : eta_mlp_train.hip ----

@@ -46,6 +46,15 @@ assert RECORD_DTYPE.itemsize == 16
 RECORD8_DTYPE = np.dtype([("distance_m", "<f4"), ("packed", "<u4")])
 assert RECORD8_DTYPE.itemsize == 8
 
+#: 6-byte bulk wire record (10 B per prediction with the f32 output): one little-endian 48-bit word
+#: stored as 3 x u16 — bits 0-26 distance in eighths of a metre (to 16,777 km; exact in f32 below
+#: 2,097 km), 27-33 driver age in whole years (0-127), 34-36 weekday, 37-41 hour, 42-44 weather,
+#: 45-47 traffic (code 7 = unknown -> all-zero one-hot).  Distance is kept to 1/8 m (ORS reports
+#: 0.1 m) and age to a year (the reference's column is an integer); both are finer than what the
+#: kernel's bf16 hi/lo operand split resolves after normalisation.
+RECORD6_WORDS = 3
+DIST6_MAX_Q = (1 << 27) - 1
+
 
 def weather_code(w: Any) -> int:
     return _W.get(w, UNKNOWN_CODE) if isinstance(w, str) else UNKNOWN_CODE
@@ -111,6 +120,43 @@ def records_to_compact(rec: np.ndarray) -> np.ndarray:
     t = np.where(t > 3, 7, t)
     out["packed"] = age | (wd << 16) | (hr << 19) | (w << 24) | (t << 27)
     return out
+
+
+def records_to_compact6(rec: np.ndarray) -> np.ndarray:
+    """16-byte records -> 6-byte bulk records, uint16 [B,3] (see RECORD6_WORDS)."""
+    rec = np.asarray(rec, dtype=RECORD_DTYPE)
+    q = np.clip(np.rint(rec["distance_m"].astype(np.float64) * 8.0), 0, DIST6_MAX_Q).astype(np.uint64)
+    age = np.clip(np.rint(rec["driver_age"].astype(np.float64)), 0, 127).astype(np.uint64)
+    secs = rec["wallclock_s"].astype(np.int64)
+    days = np.floor_divide(secs, 86400)
+    wd = ((days + KERNEL_EPOCH_WEEKDAY) % 7).astype(np.uint64)
+    hr = ((secs - days * 86400) // 3600).astype(np.uint64)
+    w = rec["weather"].astype(np.uint64)
+    t = rec["traffic"].astype(np.uint64)
+    w = np.where(w > 3, 7, w)
+    t = np.where(t > 3, 7, t)
+    word = q | (age << 27) | (wd << 34) | (hr << 37) | (w << 42) | (t << 45)
+    out = np.empty((rec.shape[0], RECORD6_WORDS), dtype=np.uint16)
+    for k in range(RECORD6_WORDS):
+        out[:, k] = (word >> (16 * k)) & 0xFFFF
+    return out
+
+
+def compact6_to_features(rec6: np.ndarray) -> np.ndarray:
+    """CPU reference of the K1 featurize kernel for 6-byte records."""
+    r = np.asarray(rec6, dtype=np.uint16).astype(np.uint64)
+    word = r[:, 0] | (r[:, 1] << 16) | (r[:, 2] << 32)
+    x = np.zeros((r.shape[0], NUM_FEATURES), dtype=np.float32)
+    w = (word >> 42) & 7
+    t = (word >> 45) & 7
+    for i in range(4):
+        x[:, i] = (w == i)
+        x[:, 4 + i] = (t == i)
+    x[:, 8] = (word >> 34) & 7
+    x[:, 9] = (word >> 37) & 31
+    x[:, 10] = (word & DIST6_MAX_Q).astype(np.float32) * np.float32(np.float32(0.125) * np.float32(1e-3))
+    x[:, 11] = (word >> 27) & 127
+    return x
 
 
 def compact_to_features(rec8: np.ndarray) -> np.ndarray:

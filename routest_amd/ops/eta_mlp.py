@@ -135,6 +135,24 @@ def records8_to_tensor(rec8: np.ndarray) -> torch.Tensor:
     return torch.from_numpy(rec8.view(np.int32).reshape(-1, 2))
 
 
+def records6_to_tensor(rec6: np.ndarray) -> torch.Tensor:
+    """uint16 [B,3] 6-byte records (features.records_to_compact6) -> int16 [B,3] tensor view."""
+    return torch.from_numpy(np.ascontiguousarray(rec6, dtype=np.uint16).view(np.int16))
+
+
+def featurize6_torch(rec6: torch.Tensor) -> torch.Tensor:
+    """PyTorch reference of K1 for 6-byte records: int16 [B,3] -> [B,12] fp32."""
+    r = rec6.to(torch.int64) & 0xFFFF
+    word = r[:, 0] | (r[:, 1] << 16) | (r[:, 2] << 32)
+    w = (word >> 42) & 7
+    t = (word >> 45) & 7
+    ar = torch.arange(4, device=rec6.device)
+    km = (word & ((1 << 27) - 1)).float() * (0.125 * 1e-3)
+    return torch.cat([(w[:, None] == ar[None]).float(), (t[:, None] == ar[None]).float(),
+                      ((word >> 34) & 7).float()[:, None], ((word >> 37) & 31).float()[:, None],
+                      km[:, None], ((word >> 27) & 127).float()[:, None]], 1)
+
+
 def featurize8_torch(rec8_i32: torch.Tensor) -> torch.Tensor:
     """PyTorch reference of K1 for compact records: int32 [B,2] -> [B,12] fp32."""
     dist = rec8_i32[:, 0].view(torch.float32)
@@ -152,6 +170,8 @@ def featurize_torch(rec_i32: torch.Tensor) -> torch.Tensor:
     """PyTorch reference of K1 on any device: int32 [B,4] (or compact [B,2]) -> [B,12] fp32."""
     if rec_i32.shape[1] == 2:
         return featurize8_torch(rec_i32)
+    if rec_i32.shape[1] == 3:
+        return featurize6_torch(rec_i32)
     r = rec_i32
     dist = r[:, 0].view(torch.float32) if r.dtype == torch.int32 else r[:, 0]
     age = r[:, 1].view(torch.float32)

@@ -154,6 +154,34 @@ def test_mlp3_forward_compact_records(variant):
     assert torch.equal(out, got)
 
 
+@pytest.mark.parametrize("variant", [0, 1, 3])
+def test_mlp3_forward_rec6_records(variant):
+    """6-byte bulk records: kernel == the fp32 model on the records' own features, on HBM and on
+    pinned host records (zero-copy), odd batch (the last row's 6 bytes end the buffer)."""
+    from routest_amd.models.features import compact6_to_features, records_to_compact6
+    from routest_amd.ops.eta_mlp import records6_to_tensor
+    m = _model(256, 5)
+    k = EtaMlpKernel(m, torch.device("cuda:0"), variant=variant)
+    rec, _ = synth_records(70_001, 23)
+    rec["weather"][:100] = 255
+    rec["traffic"][50:150] = 9
+    r6 = records_to_compact6(rec)
+    x6 = compact6_to_features(r6)
+    got = k(records6_to_tensor(r6).cuda()).cpu()
+    ref = m(torch.from_numpy(x6)).detach()
+    torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
+    # same predictions as the 8-byte path up to the record quantisation
+    from routest_amd.models.features import records_to_compact
+    from routest_amd.ops.eta_mlp import records8_to_tensor
+    g8 = k(records8_to_tensor(records_to_compact(rec)).cuda()).cpu()
+    assert (got - g8).abs().max().item() < 0.05
+    host = records6_to_tensor(r6).pin_memory()
+    out = torch.empty(len(r6)).pin_memory()
+    k.forward_hostio(host, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, got)
+
+
 def test_resident_scorer_matches_kernel():
     from routest_amd.ops.eta_mlp import ResidentScorer
     m = _model(256, 7)

@@ -127,3 +127,32 @@ def test_native_astar_matches_dijkstra():
     ref = dijkstra_ref(g, cost, s, t)
     np.testing.assert_allclose(got, ref, rtol=1e-4)
     assert all(p[0] == a and p[-1] == b for p, a, b in zip(paths, s, t))
+
+
+def test_compact6_records_roundtrip():
+    """6-byte bulk records (features.py RECORD6): features equal the 16-byte records' features for
+    1/8-metre distances and whole-year ages; the PyTorch reference of K1 agrees bitwise; out of
+    range values clamp and unknown categories give all-zero one-hots."""
+    import torch
+    from routest_amd.data.synth import synth_records
+    from routest_amd.models.features import (compact6_to_features, records_to_compact6,
+                                             records_to_features)
+    from routest_amd.ops.eta_mlp import featurize_torch, records6_to_tensor
+    rec, _ = synth_records(5000, seed=3)
+    rec["distance_m"] = np.rint(rec["distance_m"] * 8) / 8
+    rec["driver_age"] = np.rint(rec["driver_age"])
+    rec["weather"][:20] = 255
+    rec["traffic"][10:30] = 4
+    r6 = records_to_compact6(rec)
+    assert r6.dtype == np.uint16 and r6.shape == (5000, 3)
+    x6, x16 = compact6_to_features(r6), records_to_features(rec)
+    np.testing.assert_array_equal(x6[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11]],
+                                  x16[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11]])
+    np.testing.assert_allclose(x6[:, 10], x16[:, 10], rtol=1e-6)
+    assert torch.equal(featurize_torch(records6_to_tensor(r6)), torch.from_numpy(x6))
+    big = rec[:2].copy()
+    big["distance_m"] = [-5.0, 3e10]
+    big["driver_age"] = [-1.0, 500.0]
+    xb = compact6_to_features(records_to_compact6(big))
+    assert xb[0, 10] == 0 and abs(xb[1, 10] - ((1 << 27) - 1) * 0.125e-3) < 1e-2
+    assert xb[0, 11] == 0 and xb[1, 11] == 127
