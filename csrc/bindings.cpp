@@ -53,14 +53,31 @@ static int record_bytes(const torch::Tensor& r) {
   return 0;
 }
 
+// variant >= 16 selects the 16x16-MFMA kernel (blob16 layout): 16 -> 2, 17 -> 4, 18 -> 1 batch
+// halves per wave-tile (8 waves per CU), 19 -> 2 halves with 12 waves per CU; anything else the
+// 32x32 kernel (blob layout)
+static int fwd16_halves(int64_t variant) {
+  return variant == 16 ? 2 : variant == 17 ? 4 : variant == 18 ? 1 : variant == 19 ? 3 : 0;
+}
+static size_t fwd_blob_bytes(int64_t variant, int64_t H) {
+  return fwd16_halves(variant) ? rt::eta_mlp3_blob16_bytes((int)H) : rt::eta_mlp3_blob_bytes((int)H);
+}
+static hipError_t launch_fwd_any(const void* rec, float* out, int B, const void* blob, int64_t H,
+                                 const rt::NormParams& np, int64_t variant, int cus, hipStream_t st,
+                                 int rb) {
+  if (const int nh = fwd16_halves(variant))
+    return rt::launch_eta_mlp3_fwd16(rec, out, B, blob, (int)H, np, nh, cus, st, rb);
+  return rt::launch_eta_mlp3_fwd(rec, out, B, blob, (int)H, np, (int)variant, cus, st, rb);
+}
+
 torch::Tensor eta_mlp3_forward(torch::Tensor records, torch::Tensor blob, int64_t H,
                                std::vector<double> norm, int64_t variant) {
   check_dev(records, "records");
   check_dev(blob, "blob");
   const int rb = record_bytes(records);
   TORCH_CHECK(blob.scalar_type() == torch::kUInt8, "blob must be uint8");
-  TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H),
-              "blob has ", blob.numel(), " bytes, expected ", rt::eta_mlp3_blob_bytes((int)H),
+  TORCH_CHECK((size_t)blob.numel() == fwd_blob_bytes(variant, H),
+              "blob has ", blob.numel(), " bytes, expected ", fwd_blob_bytes(variant, H),
               " for H=", H);
   TORCH_CHECK(norm.size() == 8, "norm must hold 4 scales + 4 shifts");
   TORCH_CHECK(records.device() == blob.device(), "records/blob on different devices");
@@ -73,9 +90,8 @@ torch::Tensor eta_mlp3_forward(torch::Tensor records, torch::Tensor blob, int64_
     np.scale[i] = (float)norm[i];
     np.shift[i] = (float)norm[4 + i];
   }
-  RT_CHECK_HIP(rt::launch_eta_mlp3_fwd(records.data_ptr(), out.data_ptr<float>(), B,
-                                       blob.data_ptr(), (int)H, np, (int)variant,
-                                       num_cus(records.device().index()), cur_stream(records), rb));
+  RT_CHECK_HIP(launch_fwd_any(records.data_ptr(), out.data_ptr<float>(), B, blob.data_ptr(), H, np,
+                              variant, num_cus(records.device().index()), cur_stream(records), rb));
   return out;
 }
 
@@ -99,7 +115,7 @@ void eta_mlp3_forward_hostio(torch::Tensor records, torch::Tensor out, torch::Te
   const int rb = record_bytes(records);
   TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.numel() == records.size(0), "out must be f32 [B]");
   check_dev(blob, "blob");
-  TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
+  TORCH_CHECK((size_t)blob.numel() == fwd_blob_bytes(variant, H), "bad blob");
   TORCH_CHECK(norm.size() == 8, "norm must hold 4 scales + 4 shifts");
   for (const torch::Tensor* t : {&records, &out})
     TORCH_CHECK(!t->is_cuda() || t->device() == blob.device(), "GPU operands must be on the blob's device");
@@ -111,9 +127,8 @@ void eta_mlp3_forward_hostio(torch::Tensor records, torch::Tensor out, torch::Te
     np.scale[i] = (float)norm[i];
     np.shift[i] = (float)norm[4 + i];
   }
-  RT_CHECK_HIP(rt::launch_eta_mlp3_fwd(drec, (float*)dout, (int)records.size(0), blob.data_ptr(),
-                                       (int)H, np, (int)variant, num_cus(blob.device().index()),
-                                       cur_stream(blob), rb));
+  RT_CHECK_HIP(launch_fwd_any(drec, (float*)dout, (int)records.size(0), blob.data_ptr(), H, np,
+                              variant, num_cus(blob.device().index()), cur_stream(blob), rb));
 }
 
 torch::Tensor eta_featurize(torch::Tensor records) {
@@ -650,6 +665,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "zero-copy: fused kernel reads records / writes minutes in pinned host memory");
   m.def("eta_featurize", &eta_featurize, "K1: packed records -> R16 features [B,12] fp32");
   m.def("eta_mlp3_blob_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_blob_bytes((int)H); });
+  m.def("eta_mlp3_blob16_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_blob16_bytes((int)H); });
   m.def("route_haversine_matrix", &route_haversine_matrix, "K5: batched haversine matrices (f64)");
   m.def("route_greedy_cvrp", &route_greedy_cvrp, "K6: batched greedy multi-trip CVRP");
   m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad");

@@ -222,6 +222,227 @@ hipError_t launch_eta_mlp3_fwd(const void* rec, float* out, int B, const void* b
 
 size_t eta_mlp3_blob_bytes(int H) { return mlp3_blob_bytes(H); }
 
+// ---------------------------------------------------------------------------------------------
+// 16x16 MFMA form of K1+K2 (variant 16/17: NH = 2/4 batch halves of 16 rows per wave-tile).
+//
+// Same math as eta_mlp3_fwd_kernel, on v_mfma_f32_16x16x32_bf16 (layer 2) and
+// v_mfma_f32_16x16x16_bf16 (layer 1) instead of 32x32x16.  The reason is the clock, not the
+// cycle count: under the MI355X power limit, 16x16x32 MFMA loops hold a ~12-15 % higher clock
+// than 32x32x16 loops at equal cycles per FLOP (MI355X_MICROARCH.md, DVFS item 7).
+//   * layer 1: lane (j, kq) of the B operand holds features 4kq..4kq+3 of batch row j (the
+//     (kq & 1) half of the 32x32 kernel's lane-half kq >> 1); D of hidden tile t gives lane
+//     (j, g) hidden units 16t + 4g .. +3 of row j
+//   * the layer-2 B fragment of k-chunk c is [relu(D_2c) | relu(D_2c+1)] in bf16 — no shuffles;
+//     the host packs W2's columns in that (permuted) k order (ops/eta_mlp.py pack_mlp3_16)
+//   * each W2 A fragment read from LDS feeds NH MFMAs (NH batch halves), so NH = 2 moves the
+//     same LDS bytes per FLOP as the 32x32 kernel and NH = 4 half of them
+// Blob16: [ w2p: (H/16)x(H/32)x64 lanes x 8 bf16 | w1p: (H/16)x64 lanes x 4 bf16 | b2 (H f32) |
+//           w3 (H f32, target scale folded) | tail: b3, 0, 0, 0 ]
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <int H>
+struct Mlp3Layout16 {
+  static constexpr int MT = H / 16;   // 16-row hidden tiles
+  static constexpr int KC = H / 32;   // 32-deep k chunks
+  static constexpr size_t W2B = (size_t)H * H * 2;
+  static constexpr size_t W1B = (size_t)H * 16 * 2;
+  static constexpr size_t BLOB = W2B + W1B + 2 * (size_t)H * 4 + 16;
+};
+
+size_t eta_mlp3_blob16_bytes(int H) { return (size_t)2 * H * H + 40 * (size_t)H + 16; }
+
+// (pairwise: a 4-wide convertvector lowers to 4 single-element v_cvt_pk_bf16_f32 + 2 v_perm_b32)
+__device__ __forceinline__ bf16x4 relu_cvt_bf16x4(const f32x4 v) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const i16x2 z = {0, 0};
+  const bf16x2 lo = __builtin_convertvector(__builtin_shufflevector(v, v, 0, 1), bf16x2);
+  const bf16x2 hi = __builtin_convertvector(__builtin_shufflevector(v, v, 2, 3), bf16x2);
+  const i16x2 rl = __builtin_elementwise_max(__builtin_bit_cast(i16x2, lo), z);
+  const i16x2 rh = __builtin_elementwise_max(__builtin_bit_cast(i16x2, hi), z);
+  return __builtin_bit_cast(bf16x4, __builtin_shufflevector(rl, rh, 0, 1, 2, 3));
+}
+
+template <int H, int NH, int RB, int TPB = 512>
+__global__ __launch_bounds__(TPB, 1) void eta_mlp3_fwd16_kernel(const void* __restrict__ rec,
+                                                                 float* __restrict__ out, int B,
+                                                                 const unsigned char* __restrict__ blob,
+                                                                 NormParams np) {
+  using L = Mlp3Layout16<H>;
+  constexpr int MT = L::MT, KC = L::KC, NF = MT * KC, D = KC < 4 ? KC : 4, ROWS = 16 * NH;
+  static_assert(L::W1B >= D * 1024, "the ring's over-read must stay inside the blob");
+  (void)NF;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  {
+    const int4* src = reinterpret_cast<const int4*>(blob);
+    int4* dst = reinterpret_cast<int4*>(smem);
+    constexpr int N16 = (int)(L::BLOB / 16);
+    for (int i = threadIdx.x; i < N16; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+  }
+  const bf16x8* w2p = reinterpret_cast<const bf16x8*>(smem);
+  const i16x4* w1p = reinterpret_cast<const i16x4*>(smem + L::W2B);
+  const float* b2 = reinterpret_cast<const float*>(smem + L::W2B + L::W1B);
+  const float* w3 = b2 + H;
+  const float b3 = w3[H];
+
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 15;
+  const int kq = lane >> 4;
+  // layer-1 A fragments: kept in registers, or (NH = 4, where 4 halves of h1 already take
+  // 128 VGPRs) re-read from LDS per use
+  constexpr bool W1REG = NH < 4;
+  i16x4 w1[W1REG ? MT : 1];
+  if constexpr (W1REG) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) w1[t] = w1p[t * 64 + lane];
+  }
+
+  const int wpb = blockDim.x >> 6;
+  const int ntiles = (B + ROWS - 1) / ROWS;
+  const int stride = gridDim.x * wpb;
+  using R = RecT<RB>;
+  int tile = blockIdx.x * wpb + (threadIdx.x >> 6);
+  typename R::T rc_next[NH];
+#pragma unroll
+  for (int n = 0; n < NH; ++n) {
+    const int row = tile * ROWS + 16 * n + j;
+    rc_next[n] = (tile < ntiles && row < B) ? R::load(rec, row) : R::zero();
+  }
+  for (; tile < ntiles; tile += stride) {
+    bf16x8 h1[NH][KC];
+#pragma unroll
+    for (int n = 0; n < NH; ++n) {
+      const typename R::T rc = rc_next[n];
+      const int nrow = (tile + stride) * ROWS + 16 * n + j;
+      if (tile + stride < ntiles && nrow < B) rc_next[n] = R::load(rec, nrow);
+      const bf16x8 f8 = R::feat(rc, kq >> 1, np);
+      const i16x4 xb = (kq & 1) ? __builtin_bit_cast(i16x4, __builtin_shufflevector(f8, f8, 4, 5, 6, 7))
+                                : __builtin_bit_cast(i16x4, __builtin_shufflevector(f8, f8, 0, 1, 2, 3));
+      // layer 1 (bias folded into k = 14, 15)
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const i16x4 wa0 = W1REG ? w1[W1REG ? 2 * c : 0] : w1p[(2 * c) * 64 + lane];
+        const i16x4 wa1 = W1REG ? w1[W1REG ? 2 * c + 1 : 0] : w1p[(2 * c + 1) * 64 + lane];
+        const f32x4 d0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa0, xb, z, 0, 0, 0);
+        const f32x4 d1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa1, xb, z, 0, 0, 0);
+        const bf16x4 r0 = relu_cvt_bf16x4(d0), r1 = relu_cvt_bf16x4(d1);
+        h1[n][c] = __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    }
+    // layer 2 + fused layer 3; A fragments through a 4-deep prefetch ring across tiles
+    f32x2 ys[NH];
+#pragma unroll
+    for (int n = 0; n < NH; ++n) ys[n] = (f32x2){0.f, 0.f};
+    const bf16x8* wa = w2p + lane;
+    bf16x8 ring[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) ring[d] = wa[d * 64];
+#pragma unroll 1
+    for (int t = 0; t < MT; ++t) {
+      const f32x4 bias = *reinterpret_cast<const f32x4*>(b2 + 16 * t + 4 * kq);
+      f32x4 acc[NH];
+#pragma unroll
+      for (int n = 0; n < NH; ++n) acc[n] = bias;
+      const int base = t * KC;
+#pragma unroll
+      for (int c = 0; c < KC; c += D) {
+        bf16x8 a[D];
+        const int nf = base + c + D;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          a[d] = ring[d];
+          ring[d] = wa[(nf + d) * 64];   // past the last fragment: reads w1p (in the blob), unused
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+#pragma unroll
+          for (int n = 0; n < NH; ++n)
+            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[d], h1[n][c + d], acc[n], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, D * NH, 0);
+      }
+      const f32x4 w3v = *reinterpret_cast<const f32x4*>(w3 + 16 * t + 4 * kq);
+      // relu + dot with w3 straight into packed per-lane partial sums (4 v_max + 2 v_pk_fma)
+      const f32x2 w3lo = {w3v[0], w3v[1]}, w3hi = {w3v[2], w3v[3]};
+#pragma unroll
+      for (int n = 0; n < NH; ++n) {
+        const f32x2 lo = {relu_f(acc[n][0]), relu_f(acc[n][1])};
+        const f32x2 hi = {relu_f(acc[n][2]), relu_f(acc[n][3])};
+        ys[n] = __builtin_elementwise_fma(lo, w3lo, ys[n]);
+        ys[n] = __builtin_elementwise_fma(hi, w3hi, ys[n]);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NH; ++n) {
+      float y = ys[n][0] + ys[n][1];
+      y += __shfl_xor(y, 16);
+      y += __shfl_xor(y, 32);
+      const int row = tile * ROWS + 16 * n + j;
+      if (kq == 0 && row < B) out[row] = y + b3;
+    }
+  }
+}
+
+template <int H, int NH, int RB, int TPB = 512>
+static hipError_t launch_fwd16(const void* rec, float* out, int B, const void* blob,
+                               const NormParams& np, int num_cus, hipStream_t stream) {
+  using L = Mlp3Layout16<H>;
+  static bool attr_set[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!attr_set[dev & 63]) {
+    hipError_t e = hipFuncSetAttribute((const void*)eta_mlp3_fwd16_kernel<H, NH, RB, TPB>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::BLOB);
+    if (e != hipSuccess) return e;
+    attr_set[dev & 63] = true;
+  }
+  const int ntiles = (B + 16 * NH - 1) / (16 * NH);
+  if (ntiles == 0) return hipSuccess;
+  int grid = (ntiles + TPB / 64 - 1) / (TPB / 64);
+  if (grid > num_cus) grid = num_cus;
+  hipLaunchKernelGGL((eta_mlp3_fwd16_kernel<H, NH, RB, TPB>), dim3(grid), dim3(TPB), L::BLOB, stream,
+                     rec, out, B, (const unsigned char*)blob, np);
+  return hipGetLastError();
+}
+
+template <int H, int RB>
+static hipError_t launch_fwd16_nh(const void* rec, float* out, int B, const void* blob,
+                                  const NormParams& np, int nh, int num_cus, hipStream_t stream) {
+  switch (nh) {
+    case 1: return launch_fwd16<H, 1, RB>(rec, out, B, blob, np, num_cus, stream);
+    case 2: return launch_fwd16<H, 2, RB>(rec, out, B, blob, np, num_cus, stream);
+    case 4: return launch_fwd16<H, 4, RB>(rec, out, B, blob, np, num_cus, stream);
+    case 3: return launch_fwd16<H, 2, RB, 768>(rec, out, B, blob, np, num_cus, stream);   // 2 halves, 12 waves
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int RB>
+static hipError_t launch_fwd16_rb(const void* rec, float* out, int B, const void* blob, int H,
+                                  const NormParams& np, int nh, int num_cus, hipStream_t stream) {
+  switch (H) {
+    case 64: return launch_fwd16_nh<64, RB>(rec, out, B, blob, np, nh, num_cus, stream);
+    case 128: return launch_fwd16_nh<128, RB>(rec, out, B, blob, np, nh, num_cus, stream);
+    case 256: return launch_fwd16_nh<256, RB>(rec, out, B, blob, np, nh, num_cus, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_eta_mlp3_fwd16(const void* rec, float* out, int B, const void* blob16, int H,
+                                 const NormParams& np, int nh, int num_cus, hipStream_t stream,
+                                 int rec_bytes) {
+  switch (rec_bytes) {
+    case 16: return launch_fwd16_rb<16>(rec, out, B, blob16, H, np, nh, num_cus, stream);
+    case 8: return launch_fwd16_rb<8>(rec, out, B, blob16, H, np, nh, num_cus, stream);
+    case 6: return launch_fwd16_rb<6>(rec, out, B, blob16, H, np, nh, num_cus, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+
 hipError_t launch_eta_featurize(const void* rec, float* out, int B, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(eta_featurize_kernel, dim3((B + 255) / 256), dim3(256), 0, stream,

@@ -17,6 +17,11 @@ size_t eta_mlp3_blob_bytes(int H);
 hipError_t launch_eta_mlp3_fwd(const void* rec, float* out, int B, const void* blob, int H,
                                const NormParams& np, int variant, int num_cus, hipStream_t stream,
                                int rec_bytes = 16);   // 16, 8 or 6-byte records
+// 16x16-MFMA form (blob16 layout, ops/eta_mlp.py pack_mlp3_16); nh = 1, 2 or 4 batch halves
+size_t eta_mlp3_blob16_bytes(int H);
+hipError_t launch_eta_mlp3_fwd16(const void* rec, float* out, int B, const void* blob16, int H,
+                                 const NormParams& np, int nh, int num_cus, hipStream_t stream,
+                                 int rec_bytes);
 hipError_t launch_eta_featurize(const void* rec, float* out, int B, hipStream_t stream);
 
 // ---- ETA MLP training (K3) : eta_mlp_train.hip ----

@@ -123,6 +123,45 @@ def pack_mlp3(model: EtaMLP) -> PackedMLP3:
     return PackedMLP3(H, blob, scale + shift, b3, w1k, b1, W2.clone(), b2.clone(), w3)
 
 
+def blob16_bytes(H: int) -> int:
+    """[w2p16 | w1p16 | b2 | w3 | tail(b3,0,0,0)] — csrc/eta_mlp_fwd.hip Mlp3Layout16"""
+    return 2 * H * H + 40 * H + 16
+
+
+@torch.no_grad()
+def pack_mlp3_16(p: PackedMLP3) -> torch.Tensor:
+    """Weight blob of the 16x16-MFMA forward kernel (eta_mlp3_fwd16_kernel) from the fp32
+    kernel-view tensors of :func:`pack_mlp3` (same folded W1k / target-scaled w3 / b3)."""
+    H = p.hidden
+    MT, KC = H // 16, H // 32
+    lane = np.arange(64)
+    i = lane & 15
+    q = lane >> 4
+    v = np.arange(8)
+    # w2p16[t][c][l][v] = W2[16t + i][32c + (v < 4 ? 4q + v : 16 + 4q + v - 4)]
+    kslot = np.where(v < 4, 4 * q[:, None] + v[None, :], 16 + 4 * q[:, None] + (v[None, :] - 4))  # [64,8]
+    rows = 16 * np.arange(MT)[:, None, None, None] + i[None, None, :, None]
+    cols = 32 * np.arange(KC)[None, :, None, None] + kslot[None, None, :, :]
+    w2p = p.w2.numpy()[np.broadcast_to(rows, (MT, KC, 64, 8)), np.broadcast_to(cols, (MT, KC, 64, 8))]
+    # w1p16[t][l][v] = W1k[16t + i][4q + v]
+    v4 = np.arange(4)
+    rows1 = np.broadcast_to(16 * np.arange(MT)[:, None, None] + i[None, :, None], (MT, 64, 4))
+    cols1 = np.broadcast_to(4 * q[None, :, None] + v4[None, None, :], (MT, 64, 4))
+    w1p = p.w1k.numpy()[rows1, cols1]
+
+    def bf16_bytes(a: np.ndarray) -> np.ndarray:
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16)
+        return t.view(torch.int16).numpy().view(np.uint8).reshape(-1)
+
+    parts = [bf16_bytes(w2p), bf16_bytes(w1p),
+             p.b2.numpy().astype(np.float32).view(np.uint8).reshape(-1),
+             p.w3.numpy().astype(np.float32).view(np.uint8).reshape(-1),
+             np.array([p.b3, 0.0, 0.0, 0.0], dtype=np.float32).view(np.uint8)]
+    blob = torch.from_numpy(np.concatenate(parts).copy())
+    assert blob.numel() == blob16_bytes(H)
+    return blob
+
+
 def records_to_tensor(rec: np.ndarray) -> torch.Tensor:
     """numpy EtaRecord array -> int32 [B,4] tensor view (16-byte rows)."""
     rec = np.ascontiguousarray(rec, dtype=RECORD_DTYPE)
@@ -217,7 +256,12 @@ class EtaMlpKernel:
     """A packed MLP resident on one device; ``__call__(records_i32) -> minutes``.
 
     On a GPU device this ALWAYS runs the HIP kernel (raises if the extension is missing).
-    On CPU it runs the fp32 PyTorch model (the reference path)."""
+    On CPU it runs the fp32 PyTorch model (the reference path).
+
+    ``variant``: -1 auto, 0-8 the 32x32-MFMA kernel's variants (csrc/eta_mlp_fwd.hip
+    launch_fwd_h), 16/17/18 the 16x16-MFMA kernel with 2/4/1 batch halves per wave-tile (19: 2 halves at
+    12 waves per CU) (its own
+    weight blob, :func:`pack_mlp3_16`)."""
 
     def __init__(self, model: EtaMLP, device: Optional[torch.device] = None, variant: int = -1):
         self.device = torch.device(device) if device is not None else torch.device("cpu")
@@ -225,6 +269,12 @@ class EtaMlpKernel:
         self.packed = pack_mlp3(self.model_cpu).to(self.device)
         self.hidden = model.hidden
         self.variant = variant
+        # auto (-1): batches of >= AUTO16_MIN_ROWS rows run the 16x16-MFMA kernel with 4 batch
+        # halves per wave-tile (variant 17: +4-10 % over the 32x32 kernel's best variant on 16M
+        # rows, profiles/eta_fwd16_r1h.jsonl); smaller ones the 32x32 kernel's auto choice
+        self.blob16 = (pack_mlp3_16(pack_mlp3(self.model_cpu)).to(self.device)
+                       if self.device.type == "cuda" and (variant in (16, 17, 18, 19) or variant == -1)
+                       else None)
         self._C = _ext.native(required=True) if self.device.type == "cuda" else None
         if self.device.type == "cuda" and self.hidden not in (64, 128, 256):
             raise ValueError(f"HIP MLP kernel supports hidden in (64,128,256), got {self.hidden}")
@@ -232,13 +282,24 @@ class EtaMlpKernel:
     def forward_hostio(self, rec_pinned: torch.Tensor, out_pinned: torch.Tensor) -> None:
         """Zero-copy scoring: the kernel reads pinned host records and writes pinned host minutes
         directly over PCIe (asynchronous on the current stream; synchronize before reading)."""
-        self._C.eta_mlp3_forward_hostio(rec_pinned, out_pinned, self.packed.blob, self.hidden,
-                                        self.packed.norm, self.variant)
+        v = self._pick(rec_pinned.shape[0])
+        self._C.eta_mlp3_forward_hostio(rec_pinned, out_pinned, self._blob(v), self.hidden,
+                                        self.packed.norm, v)
+
+    AUTO16_MIN_ROWS = 1 << 17
+
+    def _pick(self, rows: int) -> int:
+        if self.variant == -1 and rows >= self.AUTO16_MIN_ROWS:
+            return 17
+        return self.variant
+
+    def _blob(self, variant: int) -> torch.Tensor:
+        return self.blob16 if variant in (16, 17, 18, 19) else self.packed.blob
 
     def __call__(self, rec: torch.Tensor) -> torch.Tensor:
         if self.device.type == "cuda":
-            return self._C.eta_mlp3_forward(rec, self.packed.blob, self.hidden, self.packed.norm,
-                                            self.variant)
+            v = self._pick(rec.shape[0])
+            return self._C.eta_mlp3_forward(rec, self._blob(v), self.hidden, self.packed.norm, v)
         with torch.no_grad():
             return self.model_cpu(featurize_torch(rec))
 

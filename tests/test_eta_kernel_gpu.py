@@ -41,7 +41,7 @@ def test_featurize_kernel_exact():
 
 
 @pytest.mark.parametrize("H", [64, 128, 256])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 16, 17, 18, 19])
 @pytest.mark.parametrize("B", [1, 31, 33, 1000, 70_001])
 def test_mlp3_forward_matches_fp32(H, variant, B):
     m = _model(H)
@@ -130,7 +130,7 @@ def test_mlp3_forward_experimental_variants_match(variant):
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3])
+@pytest.mark.parametrize("variant", [0, 1, 3, 16, 17])
 def test_mlp3_forward_compact_records(variant):
     from routest_amd.models.features import compact_to_features, records_to_compact
     from routest_amd.ops.eta_mlp import records8_to_tensor
@@ -154,7 +154,7 @@ def test_mlp3_forward_compact_records(variant):
     assert torch.equal(out, got)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3])
+@pytest.mark.parametrize("variant", [0, 1, 3, 16, 17, 18])
 def test_mlp3_forward_rec6_records(variant):
     """6-byte bulk records: kernel == the fp32 model on the records' own features, on HBM and on
     pinned host records (zero-copy), odd batch (the last row's 6 bytes end the buffer)."""
@@ -214,3 +214,20 @@ def test_gpu_runner_small_rounds_resident_large_rounds_launch():
     assert np.array_equal(run(rec[5:6]), ref[5:6])
     assert run.resident is not None and run.resident.stats()["served"] == 2
     run.resident.close()
+
+
+def test_auto_variant_switches_to_16x16_kernel():
+    """variant=-1: large batches run the 16x16-MFMA kernel (bitwise equal to variant 17), small
+    ones the 32x32 kernel; both within bf16 tolerance of the fp32 model."""
+    m = _model(256, 9)
+    auto = EtaMlpKernel(m, torch.device("cuda:0"))
+    k17 = EtaMlpKernel(m, torch.device("cuda:0"), variant=17)
+    k3 = EtaMlpKernel(m, torch.device("cuda:0"), variant=3)
+    rec, _ = synth_records(EtaMlpKernel.AUTO16_MIN_ROWS + 77, 31)
+    rt = records_to_tensor(rec).cuda()
+    assert torch.equal(auto(rt), k17(rt))
+    small = rt[:5000].contiguous()
+    assert torch.equal(auto(small), EtaMlpKernel(m, torch.device("cuda:0"), variant=0)(small)) or \
+        torch.equal(auto(small), k3(small))
+    ref = m(torch.from_numpy(records_to_features(rec))).detach()
+    torch.testing.assert_close(auto(rt).cpu(), ref, rtol=2e-2, atol=2e-2)
