@@ -375,14 +375,19 @@ __global__ __launch_bounds__(TPB, 1) void eta_mlp3_fwd16_kernel(const void* __re
         ys[n] = __builtin_elementwise_fma(hi, w3hi, ys[n]);
       }
     }
+    // after the two xor-reductions every lane holds the sums of its row j for all halves; lane
+    // group kq stores half n = kq, so one store instruction writes the tile's 16*NH rows as one
+    // contiguous run (256 B at NH = 4: full-size posted PCIe writes for zero-copy minutes out)
+    float mine = 0.f;
 #pragma unroll
     for (int n = 0; n < NH; ++n) {
       float y = ys[n][0] + ys[n][1];
       y += __shfl_xor(y, 16);
       y += __shfl_xor(y, 32);
-      const int row = tile * ROWS + 16 * n + j;
-      if (kq == 0 && row < B) out[row] = y + b3;
+      mine = (kq == n) ? y : mine;
     }
+    const int row = tile * ROWS + 16 * kq + j;
+    if (kq < NH && row < B) out[row] = mine + b3;
   }
 }
 
