@@ -2,9 +2,12 @@
 """Headline benchmark: ETA predictions/sec for the whole node (3-layer MLP, bf16 MFMA) plus the
 p50 latency of a single ``/predict`` request through the serving stack.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched by
-``torch.distributed.run`` with one rank per GPU (RCCL backend).  Each rank scores a fixed
-per-GPU batch of packed synthetic trip records every step (weak scaling):
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.  One rank per GPU over RCCL:
+either the caller launches the ranks (``torch.distributed.run``, WORLD_SIZE set — it must equal N,
+else exit 2), or, with WORLD_SIZE unset and N > 1, this script starts ``torch.distributed.run``
+itself as a CHILD process before anything touches the GPU and exits with its code (fails loudly if
+fewer than N GPUs are visible).  Each rank scores a fixed per-GPU batch of packed synthetic trip
+records every step (weak scaling):
 
     step = the records of B requests go host -> HBM on the copy engine (one DMA on its own
            stream: large PCIe read TLPs, ~54 GB/s), then ONE fused featurize+MLP HIP launch
@@ -52,23 +55,64 @@ def parse_args():
                     help="hybrid: split each step's record copy over this many copy streams")
     ap.add_argument("--p50", type=int, default=1, help="measure single-request p50 latency")
     ap.add_argument("--p50-requests", type=int, default=2000)
+    ap.add_argument("--rec16-steps", type=int, default=10,
+                    help="also time this many steps on full 16-byte records (extra JSON key)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(a, share: bool) -> int:
+    """Start N ranks (one per GPU) under ``torch.distributed.run`` as a child process.  Runs before
+    any HIP call in this process (``torch.cuda.device_count`` does not initialise the runtime), and
+    never execs: the parent only waits for the child and returns its exit code."""
+    import subprocess
+    if not share:
+        import torch
+        n_vis = torch.cuda.device_count()
+        if a.gpus > n_vis:
+            print(f"bench.py: --gpus {a.gpus} but only {n_vis} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main() -> None:
     a = parse_args()
+    # rehearsal mode for 1-GPU boxes: every rank on GPU 0, gloo rendezvous (RCCL refuses two ranks
+    # on one device).  The driver's N-GPU runs never set it: one rank per GPU over RCCL.  Tagged
+    # "shared_gpu" in the JSON so a rehearsal number cannot be read as a whole-node number.
+    share = os.environ.get("ROUTEST_BENCH_SHARE_GPU") == "1"
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a, share))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}", file=sys.stderr)
+        sys.exit(2)
+    if a.gpus < 1:
+        sys.exit(2)
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal mode for 1-GPU boxes: every rank on GPU 0, gloo rendezvous (RCCL refuses two ranks
-    # on one device).  The driver's N-GPU runs never set it: one rank per GPU over RCCL.
-    share = os.environ.get("ROUTEST_BENCH_SHARE_GPU") == "1"
     if share:
         local_rank = 0
+    elif local_rank >= torch.cuda.device_count():
+        print(f"bench.py: LOCAL_RANK {local_rank} has no GPU ({torch.cuda.device_count()} visible)",
+              file=sys.stderr)
+        sys.exit(2)
     if world > 1:
         torch.cuda.set_device(local_rank)
         if share:
@@ -95,96 +139,142 @@ def main() -> None:
 
     B = a.batch
     rec, _ = synth_records(B, seed=100 + rank)
-    host_rec = (records6_to_tensor(records_to_compact6(rec)) if a.rec == 6 else
-                records8_to_tensor(records_to_compact(rec)) if a.rec == 8 else
+
+    def wire(nbytes: int) -> torch.Tensor:
+        return (records6_to_tensor(records_to_compact6(rec)) if nbytes == 6 else
+                records8_to_tensor(records_to_compact(rec)) if nbytes == 8 else
                 records_to_tensor(rec)).pin_memory()
+
     nbuf = 3
-    dev_rec = [torch.empty_like(host_rec, device=dev) for _ in range(nbuf)]
-    host_out = [torch.empty(B, dtype=torch.float32).pin_memory() for _ in range(nbuf)]
-    dev_out = [None] * nbuf
     h2d_s = torch.cuda.Stream(dev)      # PCIe host->device
     comp_s = torch.cuda.Stream(dev)     # fused featurize+MLP kernel
     d2h_s = torch.cuda.Stream(dev)      # PCIe device->host (other direction, overlaps H2D)
-    h2d_done = [torch.cuda.Event() for _ in range(nbuf)]
-    comp_done = [torch.cuda.Event() for _ in range(nbuf)]
-    d2h_done = [torch.cuda.Event() for _ in range(nbuf)]
     h2d_extra = [torch.cuda.Stream(dev) for _ in range(max(0, a.h2d_streams - 1))]
-    h2d_parts = [[torch.cuda.Event() for _ in range(nbuf)] for _ in range(a.h2d_streams)]
-    for i in range(nbuf):
-        dev_rec[i].copy_(host_rec)
-    torch.cuda.synchronize()
+    host_out = [torch.empty(B, dtype=torch.float32).pin_memory() for _ in range(nbuf)]
 
-    def step(i: int) -> None:
-        k = i % nbuf
-        if a.io == "zerocopy":
-            with torch.cuda.stream(comp_s):
-                kern.forward_hostio(host_rec, host_out[k])
-        elif a.io == "hybrid":
-            # records in by DMA (large PCIe read TLPs), minutes out as the kernel's own posted
-            # writes over the other link direction
-            n = len(h2d_extra) + 1
-            for j, cs in enumerate([h2d_s] + h2d_extra):
-                lo, hi = B * j // n, B * (j + 1) // n
-                with torch.cuda.stream(cs):
-                    cs.wait_event(comp_done[k])         # slot k's records consumed
-                    dev_rec[k][lo:hi].copy_(host_rec[lo:hi], non_blocking=True)
-                    h2d_parts[j][k].record(cs)
-            with torch.cuda.stream(comp_s):
-                for j in range(n):
-                    comp_s.wait_event(h2d_parts[j][k])
-                kern.forward_hostio(dev_rec[k], host_out[k])
-                comp_done[k].record(comp_s)
-        elif a.io == "host":
-            with torch.cuda.stream(h2d_s):
-                h2d_s.wait_event(comp_done[k])          # slot k's records consumed
-                dev_rec[k].copy_(host_rec, non_blocking=True)
-                h2d_done[k].record(h2d_s)
-            with torch.cuda.stream(comp_s):
-                comp_s.wait_event(h2d_done[k])
-                comp_s.wait_event(d2h_done[k])          # slot k's previous output drained
-                dev_out[k] = kern(dev_rec[k])
-                comp_done[k].record(comp_s)
-            with torch.cuda.stream(d2h_s):
-                d2h_s.wait_event(comp_done[k])
-                host_out[k].copy_(dev_out[k], non_blocking=True)
-                d2h_done[k].record(d2h_s)
-        else:
-            with torch.cuda.stream(comp_s):
-                dev_out[k] = kern(dev_rec[k])
+    class Pipeline:
+        """Three slots of (records in HBM, minutes out); ``step(i)`` enqueues step i."""
 
-    for i in range(a.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(a.warmup + i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device="cpu" if share else dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        def __init__(self, host_rec: torch.Tensor):
+            self.host_rec = host_rec
+            self.dev_rec = [torch.empty_like(host_rec, device=dev) for _ in range(nbuf)]
+            self.dev_out = [None] * nbuf
+            self.h2d_done = [torch.cuda.Event() for _ in range(nbuf)]
+            self.comp_done = [torch.cuda.Event() for _ in range(nbuf)]
+            self.d2h_done = [torch.cuda.Event() for _ in range(nbuf)]
+            self.h2d_parts = [[torch.cuda.Event() for _ in range(nbuf)] for _ in range(a.h2d_streams)]
+            for i in range(nbuf):
+                self.dev_rec[i].copy_(host_rec)
+            torch.cuda.synchronize()
 
-    # sanity: predictions finite
-    chk = kern(dev_rec[0][:1024])
-    ok = bool(torch.isfinite(chk).all().item())
+        def step(self, i: int) -> None:
+            k = i % nbuf
+            host_rec, dev_rec, dev_out = self.host_rec, self.dev_rec, self.dev_out
+            comp_done = self.comp_done
+            if a.io == "zerocopy":
+                with torch.cuda.stream(comp_s):
+                    kern.forward_hostio(host_rec, host_out[k])
+            elif a.io == "hybrid":
+                # records in by DMA (large PCIe read TLPs), minutes out as the kernel's own posted
+                # writes over the other link direction
+                n = len(h2d_extra) + 1
+                for j, cs in enumerate([h2d_s] + h2d_extra):
+                    lo, hi = B * j // n, B * (j + 1) // n
+                    with torch.cuda.stream(cs):
+                        cs.wait_event(comp_done[k])         # slot k's records consumed
+                        dev_rec[k][lo:hi].copy_(host_rec[lo:hi], non_blocking=True)
+                        self.h2d_parts[j][k].record(cs)
+                with torch.cuda.stream(comp_s):
+                    for j in range(n):
+                        comp_s.wait_event(self.h2d_parts[j][k])
+                    kern.forward_hostio(dev_rec[k], host_out[k])
+                    comp_done[k].record(comp_s)
+            elif a.io == "host":
+                with torch.cuda.stream(h2d_s):
+                    h2d_s.wait_event(comp_done[k])          # slot k's records consumed
+                    dev_rec[k].copy_(host_rec, non_blocking=True)
+                    self.h2d_done[k].record(h2d_s)
+                with torch.cuda.stream(comp_s):
+                    comp_s.wait_event(self.h2d_done[k])
+                    comp_s.wait_event(self.d2h_done[k])     # slot k's previous output drained
+                    dev_out[k] = kern(dev_rec[k])
+                    comp_done[k].record(comp_s)
+                with torch.cuda.stream(d2h_s):
+                    d2h_s.wait_event(comp_done[k])
+                    host_out[k].copy_(dev_out[k], non_blocking=True)
+                    self.d2h_done[k].record(d2h_s)
+            else:
+                with torch.cuda.stream(comp_s):
+                    dev_out[k] = kern(dev_rec[k])
+
+        def timed(self, warmup: int, steps: int) -> float:
+            """``warmup`` untimed steps, then ``steps`` timed ones between barrier + synchronize
+            on both sides; returns the max over ranks of the elapsed seconds."""
+            for i in range(warmup):
+                self.step(i)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                self.step(warmup + i)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([el], device="cpu" if share else dev, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = float(t.item())
+            return el
+
+        def last_output(self, i: int) -> torch.Tensor:
+            k = i % nbuf
+            if a.io == "device":
+                return self.dev_out[k].float().cpu()
+            return host_out[k].clone()
+
+    pipe = Pipeline(wire(a.rec))
+    elapsed = pipe.timed(a.warmup, a.steps)
+
+    # verify the headline kernel's own output from the last timed step (not a separate small
+    # launch): every row finite, and a 64k-row slice against the fp32 model and the bf16 emulation
+    # of the kernel on the same (wire-format-decoded) features
+    from routest_amd.ops.eta_mlp import emulate_kernel, featurize_torch
+    got = pipe.last_output(a.warmup + a.steps - 1)
+    ok = bool(torch.isfinite(got).all().item())
+    nchk = min(B, 65536)
+    rec_chk = pipe.host_rec[:nchk]
+    with torch.no_grad():
+        ref32 = model.float().cpu()(featurize_torch(rec_chk)).reshape(-1)
+    emu = emulate_kernel(kern.packed.to("cpu"), rec_chk).reshape(-1)
+    spread = float((ref32 - ref32.mean()).abs().mean()) + 1e-6
+    err_fp32 = float((got[:nchk] - ref32).abs().max()) / spread
+    err_emu = float((got[:nchk] - emu).abs().max()) / spread
+    ok = ok and err_emu < 0.05 and err_fp32 < 0.25
 
     # device-only throughput of the fused kernel on the same batch (reported alongside)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
-        kern(dev_rec[0])
+        kern(pipe.dev_rec[0])
     ev0.record()
     for _ in range(30):
-        kern(dev_rec[0])
+        kern(pipe.dev_rec[0])
     ev1.record()
     torch.cuda.synchronize()
     kernel_preds_per_s = B * 30 / (ev0.elapsed_time(ev1) / 1e3)
+
+    # the same pipeline on full 16-byte records (epoch seconds: weekday/hour resolved by the
+    # kernel itself, float age and distance — no lossy packing), reported as an extra key
+    rec16_value = None
+    if a.rec != 16 and a.rec16_steps > 0:
+        del pipe
+        pipe16 = Pipeline(wire(16))
+        el16 = pipe16.timed(min(a.warmup, 3), a.rec16_steps)
+        rec16_value = B * a.rec16_steps * world / el16
+        del pipe16
 
     p50_ms = p99_ms = None
     p50_fastapi_ms = None
@@ -282,11 +372,21 @@ def main() -> None:
             "p50_python_client_ms": p50_py_ms,
             "p50_fastapi_asgi_ms": p50_fastapi_ms,
             "http_concurrent16_req_per_s": conc,
+            "preds_per_s_rec16": rec16_value,
+            "record_format": {6: "6 B packed: distance 1/8 m, integer age 0-127, host weekday/hour",
+                              8: "8 B compact: fp32 distance, fp16 age, host weekday/hour",
+                              16: "16 B full: fp32 distance, fp32 age, epoch seconds (kernel featurises)"}[a.rec],
+            "shared_gpu": bool(share and world > 1),
+            "check_max_err_vs_emulation": err_emu,
+            "check_max_err_vs_fp32": err_fp32,
             "finite": ok,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not ok:
+        print("bench.py: output check failed", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

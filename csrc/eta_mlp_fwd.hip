@@ -106,8 +106,12 @@ __global__ __launch_bounds__(TPB, LDSW ? TPB / 256 : 1) void eta_mlp3_fwd_kernel
   for (; tile < ntiles; tile += stride) {
     const int row = tile * 32 + r;
     const typename R::T rc = rc_next;
-    const int nrow = (tile + stride) * 32 + r;
-    if (tile + stride < ntiles && nrow < B) rc_next = R::load(rec, nrow);
+    // next-row index formed only once tile + stride < ntiles: (tile + stride) * 32 < B + 32 then
+    // cannot overflow int (bindings.cpp bounds B)
+    if (tile + stride < ntiles) {
+      const int nrow = (tile + stride) * 32 + r;
+      if (nrow < B) rc_next = R::load(rec, nrow);
+    }
     const bf16x8 xb = R::feat(rc, h, np);
 
     bf16x8 h1[KS];
@@ -314,8 +318,10 @@ __global__ __launch_bounds__(TPB, 1) void eta_mlp3_fwd16_kernel(const void* __re
 #pragma unroll
     for (int n = 0; n < NH; ++n) {
       const typename R::T rc = rc_next[n];
-      const int nrow = (tile + stride) * ROWS + 16 * n + j;
-      if (tile + stride < ntiles && nrow < B) rc_next[n] = R::load(rec, nrow);
+      if (tile + stride < ntiles) {   // (tile + stride) * ROWS < B + ROWS: no int overflow
+        const int nrow = (tile + stride) * ROWS + 16 * n + j;
+        if (nrow < B) rc_next[n] = R::load(rec, nrow);
+      }
       const bf16x8 f8 = R::feat(rc, kq >> 1, np);
       const i16x4 xb = (kq & 1) ? __builtin_bit_cast(i16x4, __builtin_shufflevector(f8, f8, 4, 5, 6, 7))
                                 : __builtin_bit_cast(i16x4, __builtin_shufflevector(f8, f8, 0, 1, 2, 3));

@@ -28,3 +28,32 @@ def test_bench_json_line(io):
     assert d["dtype"] == "bf16" and d["finite"] is True
     assert d["config"]["global_batch"] == 262144 and d["config"]["io"] == io
     assert abs(d["value"] - 262144 * 3 / (d["ms_per_step"] * 3 / 1e3)) / d["value"] < 1e-6
+
+
+def test_bench_spawns_ranks_itself_shared_gpu():
+    """``python bench.py --gpus 2`` (no WORLD_SIZE) launches the 2 ranks itself; on the 1-GPU box
+    both share GPU 0 (gloo rendezvous) and the line says so."""
+    env = dict(os.environ, ROUTEST_BENCH_SHARE_GPU="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1", "--batch", "262144", "--p50", "0", "--rec16-steps", "2"],
+                       capture_output=True, text=True, timeout=115, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["shared_gpu"] is True and d["finite"] is True
+    assert d["config"]["global_batch"] == 2 * 262144
+    assert d["preds_per_s_rec16"] > 1e8
+
+
+def test_bench_fails_loud_on_too_many_gpus():
+    import torch
+    n = torch.cuda.device_count()
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("ROUTEST_BENCH_SHARE_GPU", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n + 1),
+                        "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=60, cwd=ROOT, env=env)
+    assert r.returncode == 2 and "visible" in r.stderr
