@@ -18,12 +18,15 @@ def main() -> None:
     ap.add_argument("--variants", default="0,1")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--rec", type=int, default=16, choices=[6, 8, 16], help="wire record bytes")
     a = ap.parse_args()
     import torch
     from routest_amd.data.synth import synth_records
     from routest_amd.models.features import records_to_features
     from routest_amd.models.mlp3 import EtaMLP
-    from routest_amd.ops.eta_mlp import EtaMlpKernel, records_to_tensor
+    from routest_amd.models.features import records_to_compact, records_to_compact6
+    from routest_amd.ops.eta_mlp import (EtaMlpKernel, records6_to_tensor, records8_to_tensor,
+                                         records_to_tensor)
 
     dev = torch.device("cuda:0")
     res = {}
@@ -36,7 +39,9 @@ def main() -> None:
         flop_per_row = 2 * (16 * H + H * H + H)
         for B in [int(x) for x in a.batches.split(",")]:
             rec, _ = synth_records(B, 2)
-            rt = records_to_tensor(rec).to(dev)
+            rt = (records6_to_tensor(records_to_compact6(rec)) if a.rec == 6 else
+                  records8_to_tensor(records_to_compact(rec)) if a.rec == 8 else
+                  records_to_tensor(rec)).to(dev)
             times = {v: [] for v in kerns}
             for _ in range(a.rounds):
                 for v, k in kerns.items():
@@ -51,7 +56,7 @@ def main() -> None:
                     times[v].append(s.elapsed_time(e) / a.iters * 1e3)
             for v, ts in times.items():
                 us = min(ts)
-                row = {"H": H, "B": B, "variant": v, "us": round(us, 2),
+                row = {"H": H, "B": B, "rec": a.rec, "variant": v, "us": round(us, 2),
                        "preds_per_s": B / us * 1e6, "tflops": flop_per_row * B / us / 1e6}
                 print(json.dumps(row), flush=True)
                 res[f"{H}/{B}/{v}"] = row

@@ -57,7 +57,8 @@ static int record_bytes(const torch::Tensor& r) {
 // halves per wave-tile (8 waves per CU), 19 -> 2 halves with 12 waves per CU; anything else the
 // 32x32 kernel (blob layout)
 static int fwd16_halves(int64_t variant) {
-  return variant == 16 ? 2 : variant == 17 ? 4 : variant == 18 ? 1 : variant == 19 ? 3 : 0;
+  return variant == 16 ? 2 : variant == 17 ? 4 : variant == 18 ? 1 : variant == 19 ? 3
+       : variant == 20 ? 5 : variant == 21 ? 6 : variant == 22 ? 7 : 0;
 }
 static size_t fwd_blob_bytes(int64_t variant, int64_t H) {
   return fwd16_halves(variant) ? rt::eta_mlp3_blob16_bytes((int)H) : rt::eta_mlp3_blob_bytes((int)H);
@@ -613,6 +614,28 @@ void comm_all_reduce(int64_t h, torch::Tensor t, int64_t algo) {
   TORCH_CHECK(e == hipSuccess, "comm_all_reduce: ", err.empty() ? hipGetErrorString(e) : err);
 }
 
+// one-shot all-gather (op 0) / broadcast (op 2) over the IPC-mapped peer buffers; any dtype
+void comm_oneshot(int64_t h, int64_t op, torch::Tensor in, torch::Tensor out, int64_t root) {
+  check_dev(in, "input");
+  check_dev(out, "output");
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous(), "one-shot: contiguous tensors only");
+  TORCH_CHECK(in.scalar_type() == out.scalar_type(), "dtype mismatch");
+  const c10::DeviceGuard guard(in.device());
+  std::string err;
+  const size_t bytes = (size_t)in.numel() * in.element_size();
+  const int world = rt::comm_world(h);
+  TORCH_CHECK(world >= 1, "bad comm handle");
+  hipError_t e;
+  if (op == 0) {
+    TORCH_CHECK(out.numel() == in.numel() * world, "all_gather: out must hold world x input");
+    e = rt::comm_all_gather_oneshot(h, in.data_ptr(), out.data_ptr(), bytes, cur_stream(in), err);
+  } else {
+    TORCH_CHECK(in.data_ptr() == out.data_ptr(), "one-shot broadcast is in place");
+    e = rt::comm_broadcast_oneshot(h, in.data_ptr(), bytes, (int)root, cur_stream(in), err);
+  }
+  TORCH_CHECK(e == hipSuccess, "comm_oneshot: ", err.empty() ? hipGetErrorString(e) : err);
+}
+
 int dtype_code(const torch::Tensor& t) {
   if (t.scalar_type() == torch::kFloat32) return 0;
   if (t.scalar_type() == torch::kBFloat16) return 1;
@@ -729,6 +752,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_open_peers", &comm_open_peers, "map every peer's one-shot buffers (xGMI)");
   m.def("comm_all_reduce", &comm_all_reduce, "in-place SUM all-reduce on the current stream (0=rccl, 1=oneshot)");
   m.def("comm_collective", &comm_collective, "RCCL all_gather(0)/reduce_scatter(1)/broadcast(2)/all_reduce(3)");
+  m.def("comm_oneshot", &comm_oneshot, "one-shot IPC all_gather(0)/broadcast(2) on the current stream");
   m.def("comm_error", [](int64_t h) { return (int64_t)rt::comm_error(h); });
   m.def("comm_destroy", [](int64_t h) { rt::comm_destroy(h); });
   m.def("rccl_version", []() { return (int64_t)rt::comm_rccl_version(); });

@@ -12,6 +12,11 @@
 //                once, not the 2 a ring uses) and sums them in fixed rank order — so every rank
 //                gets a bit-identical result.  Three small kernels, no host round trip.
 //
+// The same stage/signal/wait protocol also gives a one-shot ALL-GATHER (every rank stages its own
+// shard, then copies all W shards straight out of the peers' buffers into its output, rank order)
+// and a one-shot BROADCAST (only the root stages; everyone copies the root's buffer).  Collectives
+// of any kind share the parity buffers and the epoch counter: every rank issues the same sequence.
+//
 // Buffers are double-buffered by epoch parity: a rank can only start epoch e+2 (reusing parity
 // e&1) after every peer signalled e+1, i.e. after every peer finished reading epoch e.  The
 // epoch counter lives in device memory so a captured graph replays correctly.  All waits are
@@ -98,24 +103,30 @@ struct ReduceArgs {
   int world;
 };
 
-__global__ __launch_bounds__(256) void wait_reduce_kernel(ReduceArgs a) {
-  const unsigned e = *a.epoch;
+// Every block waits until all ``world`` peers announced epoch ``e`` (bounded; sets *err and returns
+// false on a timeout so the kernel exits instead of hanging the GPU).
+__device__ bool wait_peers(Signals* my_sig, unsigned e, int world, int* err) {
   __shared__ int ok;
   if (threadIdx.x == 0) ok = 1;
   __syncthreads();
-  if ((int)threadIdx.x < a.world) {
+  if ((int)threadIdx.x < world) {
     const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(&a.my_sig->flags[threadIdx.x], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+    while (__hip_atomic_load(&my_sig->flags[threadIdx.x], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
       if (wall_clock64() - t0 > WAIT_TICKS) {
         ok = 0;                       // benign same-value race between waiting lanes
-        atomicExch(a.err, 1);
+        atomicExch(err, 1);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
   }
   __syncthreads();
-  if (!ok) return;
+  return ok != 0;
+}
+
+__global__ __launch_bounds__(256) void wait_reduce_kernel(ReduceArgs a) {
+  const unsigned e = *a.epoch;
+  if (!wait_peers(a.my_sig, e, a.world, a.err)) return;
   const float4* const* src = (e & 1u) ? a.peer1 : a.peer0;
   using v4 = float __attribute__((ext_vector_type(4)));
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < a.n4; i += (size_t)gridDim.x * blockDim.x) {
@@ -123,6 +134,33 @@ __global__ __launch_bounds__(256) void wait_reduce_kernel(ReduceArgs a) {
     for (int r = 1; r < a.world; ++r)          // fixed rank order: identical result on every rank
       s += __builtin_nontemporal_load((const v4*)&src[r][i]);
     *(v4*)&a.out[i] = s;
+  }
+}
+
+struct GatherArgs {
+  const int4* peer0[MAXW];
+  const int4* peer1[MAXW];
+  Signals* my_sig;
+  const unsigned* epoch;
+  int* err;
+  int4* out;
+  size_t n16;      // 16-byte words per shard
+  int world;
+  int first, count;   // copy shards [first, first + count): all-gather 0..W, broadcast root..root+1
+};
+
+// One-shot all-gather / broadcast: after the wait, out[(r - first) * n16 + k] = shard_r[k], read
+// directly from rank r's staged buffer over its xGMI link (all peers' links in flight at once).
+__global__ __launch_bounds__(256) void wait_gather_kernel(GatherArgs a) {
+  const unsigned e = *a.epoch;
+  if (!wait_peers(a.my_sig, e, a.world, a.err)) return;
+  const int4* const* src = (e & 1u) ? a.peer1 : a.peer0;
+  using v4 = int __attribute__((ext_vector_type(4)));
+  const size_t total = a.n16 * (size_t)a.count;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = i / a.n16;
+    const size_t k = i - r * a.n16;
+    *(v4*)&a.out[i] = __builtin_nontemporal_load((const v4*)&src[a.first + r][k]);
   }
 }
 
@@ -264,6 +302,68 @@ hipError_t comm_all_reduce_f32(int64_t h, float* data, size_t n, int algo, hipSt
   return hipSuccess;
 }
 
+namespace {
+// stage (optional) + signal + wait/copy for the one-shot gather family
+hipError_t oneshot_gather(CommState* c, const void* in, void* out, size_t bytes, int first, int count,
+                          bool stage, hipStream_t stream) {
+  const size_t n16 = bytes / 16;
+  if (stage)
+    hipLaunchKernelGGL(stage_kernel, dim3(grid_for(n16, 512)), dim3(256), 0, stream, (const float4*)in,
+                       (float4*)c->buf, (float4*)(c->buf + c->cap), n16, (const unsigned*)c->epoch);
+  SignalArgs sa{};
+  for (int r = 0; r < c->world; ++r) sa.peer_sig[r] = c->peer_sig[r];
+  sa.epoch = c->epoch;
+  sa.rank = c->rank;
+  sa.world = c->world;
+  hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, stream, sa);
+  GatherArgs ga{};
+  for (int r = 0; r < c->world; ++r) {
+    ga.peer0[r] = (const int4*)c->peer_buf[r];
+    ga.peer1[r] = (const int4*)(c->peer_buf[r] + c->cap);
+  }
+  ga.my_sig = c->sig;
+  ga.epoch = c->epoch;
+  ga.err = c->err;
+  ga.out = (int4*)out;
+  ga.n16 = n16;
+  ga.world = c->world;
+  ga.first = first;
+  ga.count = count;
+  hipLaunchKernelGGL(wait_gather_kernel, dim3(grid_for(n16 * count, 256)), dim3(256), 0, stream, ga);
+  return hipGetLastError();
+}
+
+bool oneshot_ok(const CommState* c, const void* a, const void* b, size_t bytes, std::string& errmsg) {
+  if (!c->peers_open) { errmsg = "one-shot peers not opened"; return false; }
+  if (bytes > c->cap || (bytes & 15) || ((uintptr_t)a & 15) || ((uintptr_t)b & 15)) {
+    errmsg = "one-shot needs 16-byte multiples/alignment and bytes <= capacity";
+    return false;
+  }
+  return true;
+}
+}  // namespace
+
+hipError_t comm_all_gather_oneshot(int64_t h, const void* in, void* out, size_t bytes_per_rank,
+                                   hipStream_t stream, std::string& errmsg) {
+  CommState* c = get(h);
+  if (!c) { errmsg = "bad comm handle"; return hipErrorInvalidValue; }
+  if (c->world == 1) return hipMemcpyAsync(out, in, bytes_per_rank, hipMemcpyDeviceToDevice, stream);
+  if (!oneshot_ok(c, in, out, bytes_per_rank, errmsg)) return hipErrorInvalidValue;
+  return oneshot_gather(c, in, out, bytes_per_rank, 0, c->world, true, stream);
+}
+
+hipError_t comm_broadcast_oneshot(int64_t h, void* data, size_t bytes, int root, hipStream_t stream,
+                                  std::string& errmsg) {
+  CommState* c = get(h);
+  if (!c) { errmsg = "bad comm handle"; return hipErrorInvalidValue; }
+  if (c->world == 1) return hipSuccess;
+  if (root < 0 || root >= c->world) { errmsg = "bad root"; return hipErrorInvalidValue; }
+  if (!oneshot_ok(c, data, data, bytes, errmsg)) return hipErrorInvalidValue;
+  // the root copies its own staged bytes back onto themselves (same values): harmless, and keeps
+  // one code path
+  return oneshot_gather(c, data, data, bytes, root, 1, c->rank == root, stream);
+}
+
 int comm_nccl_call(int64_t h, int op, const void* in, void* out, size_t count, int dtype, int root,
                    hipStream_t stream, std::string& errmsg) {
   CommState* c = get(h);
@@ -310,6 +410,11 @@ void comm_destroy(int64_t h) {
   if (c->epoch) (void)hipFree(c->epoch);
   if (c->has_nccl) ncclCommDestroy(c->nccl);
   delete c;
+}
+
+int comm_world(int64_t h) {
+  CommState* c = get(h);
+  return c ? c->world : -1;
 }
 
 int comm_rccl_version() {

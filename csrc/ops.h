@@ -124,7 +124,12 @@ hipError_t comm_all_reduce_f32(int64_t h, float* data, size_t n, int algo, hipSt
                                std::string& errmsg);
 int comm_nccl_call(int64_t h, int op, const void* in, void* out, size_t count, int dtype, int root,
                    hipStream_t stream, std::string& errmsg);
+hipError_t comm_all_gather_oneshot(int64_t h, const void* in, void* out, size_t bytes_per_rank,
+                                   hipStream_t stream, std::string& errmsg);
+hipError_t comm_broadcast_oneshot(int64_t h, void* data, size_t bytes, int root, hipStream_t stream,
+                                  std::string& errmsg);
 int comm_error(int64_t h);
+int comm_world(int64_t h);
 void comm_destroy(int64_t h);
 int comm_rccl_version();
 

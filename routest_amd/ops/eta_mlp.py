@@ -252,6 +252,12 @@ def emulate_kernel(p: PackedMLP3, rec_i32: torch.Tensor) -> torch.Tensor:
     return h2 @ p.w3.to(dev) + p.b3
 
 
+# variants of the 16x16-MFMA kernel (csrc/eta_mlp_fwd.hip eta_mlp3_fwd16_kernel; bindings.cpp
+# fwd16_halves): 16/17/18 = 2/4/1 batch halves, 19 = 2 halves at 12 waves/CU, 20 = 4 halves with
+# a scalar-FMA layer-3 epilogue, 21 = 20 software-pipelined across hidden tiles, 22 = 21 with 2 halves
+FWD16_VARIANTS = (16, 17, 18, 19, 20, 21, 22)
+
+
 class EtaMlpKernel:
     """A packed MLP resident on one device; ``__call__(records_i32) -> minutes``.
 
@@ -273,7 +279,7 @@ class EtaMlpKernel:
         # halves per wave-tile (variant 17: +4-10 % over the 32x32 kernel's best variant on 16M
         # rows, profiles/eta_fwd16_r1h.jsonl); smaller ones the 32x32 kernel's auto choice
         self.blob16 = (pack_mlp3_16(pack_mlp3(self.model_cpu)).to(self.device)
-                       if self.device.type == "cuda" and (variant in (16, 17, 18, 19) or variant == -1)
+                       if self.device.type == "cuda" and (variant in FWD16_VARIANTS or variant == -1)
                        else None)
         self._C = _ext.native(required=True) if self.device.type == "cuda" else None
         if self.device.type == "cuda" and self.hidden not in (64, 128, 256):
@@ -294,7 +300,7 @@ class EtaMlpKernel:
         return self.variant
 
     def _blob(self, variant: int) -> torch.Tensor:
-        return self.blob16 if variant in (16, 17, 18, 19) else self.packed.blob
+        return self.blob16 if variant in FWD16_VARIANTS else self.packed.blob
 
     def __call__(self, rec: torch.Tensor) -> torch.Tensor:
         if self.device.type == "cuda":

@@ -41,7 +41,7 @@ def test_featurize_kernel_exact():
 
 
 @pytest.mark.parametrize("H", [64, 128, 256])
-@pytest.mark.parametrize("variant", [0, 1, 16, 17, 18, 19])
+@pytest.mark.parametrize("variant", [0, 1, 16, 17, 18, 19, 20, 21, 22])
 @pytest.mark.parametrize("B", [1, 31, 33, 1000, 70_001])
 def test_mlp3_forward_matches_fp32(H, variant, B):
     m = _model(H)
@@ -154,7 +154,7 @@ def test_mlp3_forward_compact_records(variant):
     assert torch.equal(out, got)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 16, 17, 18])
+@pytest.mark.parametrize("variant", [0, 1, 3, 16, 17, 18, 20, 21, 22])
 def test_mlp3_forward_rec6_records(variant):
     """6-byte bulk records: kernel == the fp32 model on the records' own features, on HBM and on
     pinned host records (zero-copy), odd batch (the last row's 6 bytes end the buffer)."""
