@@ -60,59 +60,20 @@ def parse_args():
     return ap.parse_args()
 
 
-def _free_port() -> int:
-    import socket
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        return so.getsockname()[1]
-
-
-def launch_ranks(a, share: bool) -> int:
-    """Start N ranks (one per GPU) under ``torch.distributed.run`` as a child process.  Runs before
-    any HIP call in this process (``torch.cuda.device_count`` does not initialise the runtime), and
-    never execs: the parent only waits for the child and returns its exit code."""
-    import subprocess
-    if not share:
-        import torch
-        n_vis = torch.cuda.device_count()
-        if a.gpus > n_vis:
-            print(f"bench.py: --gpus {a.gpus} but only {n_vis} GPU(s) visible", file=sys.stderr)
-            return 2
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
-           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
-    env = dict(os.environ)
-    env.setdefault("OMP_NUM_THREADS", "4")
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.call(cmd, env=env)
-
-
 def main() -> None:
     a = parse_args()
     # rehearsal mode for 1-GPU boxes: every rank on GPU 0, gloo rendezvous (RCCL refuses two ranks
     # on one device).  The driver's N-GPU runs never set it: one rank per GPU over RCCL.  Tagged
     # "shared_gpu" in the JSON so a rehearsal number cannot be read as a whole-node number.
-    share = os.environ.get("ROUTEST_BENCH_SHARE_GPU") == "1"
-    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
-        sys.exit(launch_ranks(a, share))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != a.gpus:
-        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}", file=sys.stderr)
-        sys.exit(2)
-    if a.gpus < 1:
-        sys.exit(2)
+    from routest_amd.parallel.launch import ensure_ranks, share_gpu
+    share = share_gpu()
+    world = ensure_ranks(a.gpus, __file__)    # may run the ranks as a child and exit
     import numpy as np
     import torch
     import torch.distributed as dist
 
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if share:
-        local_rank = 0
-    elif local_rank >= torch.cuda.device_count():
-        print(f"bench.py: LOCAL_RANK {local_rank} has no GPU ({torch.cuda.device_count()} visible)",
-              file=sys.stderr)
-        sys.exit(2)
+    local_rank = 0 if share else int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local_rank)
         if share:

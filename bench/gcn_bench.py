@@ -22,9 +22,16 @@ def main() -> None:
     ap.add_argument("--nodes", type=int, default=100_000)
     ap.add_argument("--routes", type=int, default=10_000)
     ap.add_argument("--mode", default="partition")
+    ap.add_argument("--comm", default="device", choices=["device", "dist"],
+                    help="partition gathers: native DeviceComm (one-shot IPC / RCCL on the stream) "
+                         "or torch.distributed")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU; without torchrun this script launches them itself")
     a = ap.parse_args()
+    from routest_amd.parallel.launch import ensure_ranks, share_gpu
+    ensure_ranks(a.gpus, __file__)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -36,7 +43,11 @@ def main() -> None:
     dev = di.device
     g = synth_road_graph(a.nodes, seed=0)
     m = GcnScorer(seed=0)
-    hip = GcnScorerHip(m, g, dev, mode=a.mode, rank=di.rank, world=di.world)
+    comm = None
+    if a.mode == "partition" and di.world > 1 and a.comm == "device":
+        from routest_amd.parallel.comm import DeviceComm
+        comm = DeviceComm(dev, use_rccl=not share_gpu(), oneshot_bytes=32 << 20)
+    hip = GcnScorerHip(m, g, dev, mode=a.mode, rank=di.rank, world=di.world, comm=comm)
     rng = np.random.default_rng(di.rank)
     routes = []
     for _ in range(a.routes // di.world):
@@ -65,7 +76,8 @@ def main() -> None:
     barrier(dev)
     el = allreduce_scalars([time.perf_counter() - t0], dev, op="max")[0]
     if di.is_main:
-        print(json.dumps({"metric": "GCN route scorer", "n_gpus": di.world, "mode": a.mode, "nodes": g.num_nodes,
+        print(json.dumps({"metric": "GCN route scorer", "n_gpus": di.world, "mode": a.mode, "comm": a.comm if comm is not None else "none",
+                          "shared_gpu": share_gpu() and di.world > 1, "nodes": g.num_nodes,
                           "edges": g.num_edges, "routes_per_step": a.routes, "ms_per_step": el / a.steps * 1e3,
                           "routes_per_s": a.routes * a.steps / el,
                           "node_updates_per_s": g.num_nodes * a.steps / el}), flush=True)

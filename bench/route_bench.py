@@ -24,7 +24,11 @@ def main() -> None:
     ap.add_argument("--nodes", type=int, default=100_000)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU; without torchrun this script launches them itself")
     a = ap.parse_args()
+    from routest_amd.parallel.launch import ensure_ranks, share_gpu
+    ensure_ranks(a.gpus, __file__)
     import numpy as np
     import torch
     import torch.distributed as dist

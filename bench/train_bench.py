@@ -39,7 +39,11 @@ def main() -> None:
     ap.add_argument("--trace", default="", help="write a Chrome trace of 3 extra steps per mode (prefix)")
     ap.add_argument("--comm", default="torch", choices=["torch", "rccl", "oneshot", "auto"],
                     help="gradient all-reduce for the fused modes: ProcessGroup, or native (csrc/comm.hip)")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU; without torchrun this script launches them itself")
     a = ap.parse_args()
+    from routest_amd.parallel.launch import ensure_ranks, share_gpu
+    ensure_ranks(a.gpus, __file__)
     import torch
     import torch.distributed as dist
     from routest_amd.data.synth import synth_records, synth_trips
@@ -58,7 +62,7 @@ def main() -> None:
     comm = None
     if a.comm != "torch" and di.world > 1:
         from routest_amd.parallel.comm import DeviceComm
-        comm = DeviceComm(dev)
+        comm = DeviceComm(dev, use_rccl=not share_gpu())
         comm_algo = a.comm
     results = {}
     for mode in a.modes.split(","):
@@ -117,7 +121,8 @@ def main() -> None:
         results[mode] = {"ms_per_step": el / a.steps * 1e3,
                          "samples_per_s": B * di.world * a.steps / el}
     if di.is_main:
-        print(json.dumps({"metric": "ETA MLP DP training samples/s", "n_gpus": di.world, "comm": a.comm,
+        print(json.dumps({"metric": "ETA MLP DP training samples/s", "n_gpus": di.world,
+                          "shared_gpu": share_gpu() and di.world > 1, "comm": a.comm,
                           "batch_per_gpu": B, "hidden": a.hidden, "results": results}), flush=True)
     if di.world > 1:
         dist.destroy_process_group()

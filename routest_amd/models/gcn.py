@@ -13,7 +13,10 @@ multi-GPU modes:
   the candidate routes are sharded.
 * ``partition``: rank r computes layer 1 and the layer-2 transform for its contiguous node range
   only, then ONE ``all_gather`` of Z (N x 32 bf16 = 6.4 MB at 100k nodes, 0.8 MB per rank) before
-  the layer-2 aggregation, and one all_gather of the delays (0.4 MB).
+  the layer-2 aggregation, and one all_gather of the delays (0.4 MB).  With a
+  :class:`~routest_amd.parallel.comm.DeviceComm` both gathers are issued in place on the current
+  stream (one-shot IPC over xGMI when the shard fits its buffers, else RCCL); without one they go
+  through ``torch.distributed.all_gather_into_tensor``.
 """
 from __future__ import annotations
 
@@ -86,14 +89,14 @@ def routes_to_csr(routes: Sequence[Sequence[int]]):
 
 class GcnScorerHip:
     def __init__(self, model: GcnScorer, g: RoadGraph, device: torch.device, mode: str = "replicate",
-                 rank: int = 0, world: int = 1, group=None):
+                 rank: int = 0, world: int = 1, group=None, comm=None):
         from ..ops import _ext
         self.C = _ext.native(required=True)
         self.dev = d = torch.device(device)
         self.g = g
         self.N = g.num_nodes
         self.mode = mode
-        self.rank, self.world, self.group = rank, world, group
+        self.rank, self.world, self.group, self.comm = rank, world, group, comm
         self.X = torch.from_numpy(g.features).to(torch.bfloat16).to(d)
         self.indptr = torch.from_numpy(g.gcn_indptr).to(d)
         self.indices = torch.from_numpy(g.gcn_indices).to(d)
@@ -107,7 +110,9 @@ class GcnScorerHip:
         self.fhid = model.W1.shape[1]
         self.fz = model.W2.shape[1]
         if mode == "partition" and world > 1:
-            per = (self.N + world - 1) // world
+            # shard rows rounded up to 4 nodes: every shard of Z and of the delays starts 16-byte
+            # aligned and is a 16-byte multiple (one-shot all-gather requirement)
+            per = ((self.N + world - 1) // world + 3) // 4 * 4
             self.rows = (rank * per, min(self.N, (rank + 1) * per))
             self.per = per
         else:
@@ -138,16 +143,22 @@ class GcnScorerHip:
             C.gcn_agg_gemm(self.H1, self.indptr, self.indices, self.values, self.w2, None, self.Z,
                            self.fhid, self.fz, False, False, r0, r1)
         if self.mode == "partition" and self.world > 1:
-            import torch.distributed as dist
-            own = self.Z[r0:r0 + self.per].clone()
-            dist.all_gather_into_tensor(self.Z, own, group=self.group)
+            self._gather(self.Z)
         C.gcn_spmm_score(self.Z, self.indptr, self.indices, self.values, self.b2, self.wo, self.bo,
                          self.delay, r0, r1)
         if self.mode == "partition" and self.world > 1:
-            import torch.distributed as dist
-            own = self.delay[r0:r0 + self.per].clone()
-            dist.all_gather_into_tensor(self.delay, own, group=self.group)
+            self._gather(self.delay)
         return self.delay[:self.N]
+
+    def _gather(self, full: torch.Tensor) -> None:
+        """In-place all-gather of this rank's row shard of ``full`` (rows [rank*per, (rank+1)*per))."""
+        r0 = self.rank * self.per
+        own = full[r0:r0 + self.per]
+        if self.comm is not None:
+            self.comm.all_gather(own, full)
+        else:
+            import torch.distributed as dist
+            dist.all_gather_into_tensor(full, own.clone(), group=self.group)
 
     def score_routes(self, rptr: torch.Tensor, nodes: torch.Tensor) -> torch.Tensor:
         return self.C.route_score(rptr, nodes, self.lat, self.lon, self.delay)

@@ -85,9 +85,26 @@ class DeviceComm:
             self.C.comm_collective(self.h, 3, t, t, 0)
         return t
 
-    def all_gather(self, inp: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-        assert out.numel() == inp.numel() * self.world
-        self.C.comm_collective(self.h, 0, inp, out, 0)
+    def _oneshot_fits(self, t: torch.Tensor) -> bool:
+        nb = t.numel() * t.element_size()
+        return (self.oneshot and t.is_contiguous() and nb % 16 == 0 and nb <= self.oneshot_bytes
+                and t.data_ptr() % 16 == 0)
+
+    def all_gather(self, inp: torch.Tensor, out: torch.Tensor, algo: str = "auto") -> torch.Tensor:
+        """``out`` = the W inputs concatenated in rank order, on the current stream.  "oneshot":
+        every rank stages its shard and reads all peers' shards straight over xGMI (one hop, any
+        dtype); "rccl": ncclAllGather."""
+        assert out.numel() == inp.numel() * self.world and out.dtype == inp.dtype
+        if self.world == 1:
+            out.view(-1).copy_(inp.view(-1))
+            return out
+        maybe_fail("rccl_timeout")
+        if algo == "auto":
+            algo = "oneshot" if self._oneshot_fits(inp) and out.data_ptr() % 16 == 0 else "rccl"
+        if algo == "oneshot":
+            self.C.comm_oneshot(self.h, 0, inp, out, 0)
+        else:
+            self.C.comm_collective(self.h, 0, inp, out, 0)
         return out
 
     def reduce_scatter(self, inp: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -95,10 +112,21 @@ class DeviceComm:
         self.C.comm_collective(self.h, 1, inp, out, 0)
         return out
 
-    def broadcast(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+    def broadcast(self, t: torch.Tensor, root: int = 0, algo: str = "auto") -> torch.Tensor:
         if self.world > 1:
-            self.C.comm_collective(self.h, 2, t, t, root)
+            if algo == "auto":
+                algo = "oneshot" if self._oneshot_fits(t) else "rccl"
+            if algo == "oneshot":
+                self.C.comm_oneshot(self.h, 2, t, t, root)
+            else:
+                self.C.comm_collective(self.h, 2, t, t, root)
         return t
+
+    def ready(self) -> dict:
+        """Readiness summary for /api/health: which paths are usable and no pending wait error."""
+        return {"world": self.world, "rank": self.rank, "rccl": bool(self.use_rccl),
+                "oneshot": bool(self.oneshot), "error": bool(self.C.comm_error(self.h))
+                if self.h is not None else True}
 
     def check(self) -> None:
         """Raise if a one-shot wait timed out (a peer never arrived) — call after a sync."""

@@ -41,8 +41,12 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 300.0) ->
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
-    device = torch.device("cuda", local) if use_gpu else torch.device("cpu")
+    # 1-GPU rehearsal (parallel/launch.py): every rank on GPU 0, gloo rendezvous
+    share = os.environ.get("ROUTEST_BENCH_SHARE_GPU") == "1"
+    use_gpu = torch.cuda.is_available() and (backend != "gloo" or share)
+    device = torch.device("cuda", 0 if share else local) if use_gpu else torch.device("cpu")
+    if share:
+        backend = "gloo"
     if use_gpu:
         torch.cuda.set_device(device)
     if world <= 1:
@@ -85,8 +89,12 @@ def broadcast_flat(buf: torch.Tensor, src: int = 0, group=None) -> torch.Tensor:
     return buf
 
 
+def _gloo() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_backend() == "gloo"
+
+
 def allreduce_scalars(vals: Sequence[float], device: torch.device, op: str = "sum") -> List[float]:
-    t = torch.tensor(list(vals), dtype=torch.float64, device=device)
+    t = torch.tensor(list(vals), dtype=torch.float64, device="cpu" if _gloo() else device)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
                                "min": dist.ReduceOp.MIN}[op])
@@ -95,7 +103,7 @@ def allreduce_scalars(vals: Sequence[float], device: torch.device, op: str = "su
 
 def barrier(device: Optional[torch.device] = None) -> None:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        if device is not None and device.type == "cuda":
+        if device is not None and device.type == "cuda" and not _gloo():
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()

@@ -40,11 +40,22 @@ log = get_logger("batcher")
 Runner = Callable[[np.ndarray], np.ndarray]
 
 
+# Per-device state shared by every GpuRunner on that device: ONE resident scorer (a persistent
+# kernel that never yields its hardware queue while it lives) and the lock that orders its use
+# against the other runners' launches.  A second resident scorer on the same GPU, or a launch
+# queued behind a live one, would stall up to the scorer's lifetime per batch.
+_DEV_LOCKS: dict = {}
+_DEV_RESIDENT: dict = {}
+_DEV_GUARD = threading.Lock()
+
+
 class GpuRunner:
     """Runs a fused ETA kernel on one GPU with pinned staging buffers and a private stream.
 
     Kernels exposing ``forward_hostio`` (the MLP) run zero-copy; others (the tree ensemble) go
-    through an explicit H2D copy, the kernel, and a D2H copy on the same stream."""
+    through an explicit H2D copy, the kernel, and a D2H copy on the same stream.  Several runners
+    may share a device: the first one owns the device's resident scorer, and every runner parks it
+    (under the device lock) before enqueueing a launch."""
 
     def __init__(self, kernel, device: torch.device, batch_max: int):
         self.kernel = kernel
@@ -60,22 +71,32 @@ class GpuRunner:
         self.h_rec_np = self.h_rec.numpy().view(np.uint8).reshape(batch_max, 16).view(RECORD_DTYPE).reshape(-1)
         self.h_out_np = self.h_out.numpy()
         self.lock = threading.Lock()
+        idx = self.device.index if self.device.index is not None else 0
+        self._dev_key = idx
         # small batches go to the resident scorer kernel (no dispatch, no stream sync per request)
         self.resident = None
-        if self.zero_copy and os.environ.get("ROUTEST_RESIDENT", "1") != "0":
-            try:
-                from ..ops.eta_mlp import ResidentScorer
-                self.resident = ResidentScorer(kernel, cap=min(1024, batch_max))
-            except Exception as e:  # pragma: no cover - falls back to launches
-                log.warning("resident scorer unavailable on %s: %r", self.device, e)
+        with _DEV_GUARD:
+            self.dev_lock = _DEV_LOCKS.setdefault(idx, threading.Lock())
+            own = (self.zero_copy and os.environ.get("ROUTEST_RESIDENT", "1") != "0"
+                   and getattr(_DEV_RESIDENT.get(idx), "h", None) is None)
+            if own:
+                try:
+                    from ..ops.eta_mlp import ResidentScorer
+                    self.resident = ResidentScorer(kernel, cap=min(1024, batch_max))
+                    _DEV_RESIDENT[idx] = self.resident
+                except Exception as e:  # pragma: no cover - falls back to launches
+                    log.warning("resident scorer unavailable on %s: %r", self.device, e)
 
     def __repr__(self) -> str:
         return f"GpuRunner({self.device})"
 
     def close(self) -> None:
         """Stop the resident scorer kernel (and wait for it) while the HIP runtime is alive."""
-        with self.lock:
+        with self.lock, self.dev_lock:
             if self.resident is not None:
+                with _DEV_GUARD:
+                    if _DEV_RESIDENT.get(self._dev_key) is self.resident:
+                        del _DEV_RESIDENT[self._dev_key]
                 self.resident.close()
                 self.resident = None
 
@@ -84,23 +105,25 @@ class GpuRunner:
         n = rec.shape[0]
         out = np.empty(n, dtype=np.float32)
         if self.resident is not None and n <= self.resident.cap:
-            with self.lock:
+            with self.lock, self.dev_lock:
                 r = self.resident.score(torch.from_numpy(np.ascontiguousarray(rec).view(np.int32).reshape(n, 4)),
                                         torch.from_numpy(out))
             if r is not None:
                 return out
         with self.lock, torch.cuda.device(self.device), torch.cuda.stream(self.stream):
-            if self.resident is not None:
-                self.resident.park()      # keep a hardware queue it may share free for this launch
             for s in range(0, n, self.batch_max):
                 m = min(self.batch_max, n - s)
                 self.h_rec_np[:m] = rec[s:s + m]
-                if self.zero_copy:
-                    self.kernel.forward_hostio(self.h_rec[:m], self.h_out[:m])
-                else:
-                    self.d_rec[:m].copy_(self.h_rec[:m], non_blocking=True)
-                    y = self.kernel(self.d_rec[:m])
-                    self.h_out[:m].copy_(y, non_blocking=True)
+                with self.dev_lock:
+                    res = _DEV_RESIDENT.get(self._dev_key)
+                    if res is not None:
+                        res.park()        # keep a hardware queue it may share free for this launch
+                    if self.zero_copy:
+                        self.kernel.forward_hostio(self.h_rec[:m], self.h_out[:m])
+                    else:
+                        self.d_rec[:m].copy_(self.h_rec[:m], non_blocking=True)
+                        y = self.kernel(self.d_rec[:m])
+                        self.h_out[:m].copy_(y, non_blocking=True)
                 self.stream.synchronize()
                 out[s:s + m] = self.h_out_np[:m]
         return out
