@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Optimizer on the request path: C concurrent multi-stop POST /api/optimize_route requests (2-10
+stops each) through the FastAPI app in-process (ASGI, no sockets) with the cross-request GPU
+batcher, vs the per-request path.  Reports req/s and p50/p99 latency per mode.
+
+    python bench/route_http_bench.py [--provider haversine|graph] [--concurrency 1000] [--rounds 3]
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--provider", default="haversine", choices=["haversine", "graph"])
+    ap.add_argument("--nodes", type=int, default=100_000)
+    ap.add_argument("--concurrency", type=int, default=1000)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--batch-max", type=int, default=1024)
+    ap.add_argument("--timeout-us", type=int, default=2000)
+    a = ap.parse_args()
+    import httpx
+    import numpy as np
+    import torch
+    from routest_amd.api.app import build_services, create_app
+    from routest_amd.config import load_settings
+    from routest_amd.serve.eta_service import EtaService
+    from routest_amd.routing.providers import HaversineProvider
+
+    dev = torch.device("cuda:0")
+    if a.provider == "graph":
+        from routest_amd.data.graph import synth_road_graph
+        from routest_amd.routing.graph import GraphProvider, edge_costs
+        from routest_amd.serve.eta_service import default_model
+        g = synth_road_graph(a.nodes, seed=0)
+        prov = GraphProvider(g, edge_costs(g, default_model(hidden=256, steps=100), device=dev), device=dev)
+        lat, lon = g.lat, g.lon
+    else:
+        prov = HaversineProvider()
+        rng = np.random.default_rng(0)
+        lat, lon = 14.55 + rng.normal(0, 0.05, 20000), 121.03 + rng.normal(0, 0.05, 20000)
+    rng = np.random.default_rng(1)
+    reqs = []
+    for i in range(a.concurrency):
+        idx = rng.integers(0, len(lat), int(rng.integers(3, 12)))
+        reqs.append({"source_point": {"lat": float(lat[idx[0]]), "lon": float(lon[idx[0]])},
+                     "destination_points": [{"lat": float(lat[j]), "lon": float(lon[j]), "payload": 1}
+                                            for j in idx[1:]],
+                     "driver_details": {"driver_name": f"v{i}", "vehicle_type": "car",
+                                        "vehicle_capacity": 4, "maximum_distance": 1e7}})
+    out = {"metric": "optimize_route req/s (concurrent HTTP, in-process ASGI)", "provider": a.provider,
+           "concurrency": a.concurrency, "stops": "2-10 per request"}
+    for mode in ("batched", "per_request"):
+        s = load_settings(env={}, dotenv_path=None, devices=[0],
+                          route_batch="1" if mode == "batched" else "0", route_gpu_min_stops=1, route_batch_max=a.batch_max,
+                          route_batch_timeout_us=a.timeout_us, warm_scorer=False)
+        sv = build_services(s, eta=EtaService(None, device="cpu"), provider=prov, store=None)
+        app = create_app(sv)
+
+        async def one(c, r):
+            t = time.perf_counter()
+            resp = await c.post("/api/optimize_route", json=r)
+            assert resp.status_code == 200, resp.text[:300]
+            return time.perf_counter() - t
+
+        async def go():
+            async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://b",
+                                         timeout=600) as c:
+                await asyncio.gather(*[one(c, r) for r in reqs[:64]])          # warm-up
+                best = None
+                for _ in range(a.rounds):
+                    t0 = time.perf_counter()
+                    lat_s = await asyncio.gather(*[one(c, r) for r in reqs])
+                    el = time.perf_counter() - t0
+                    if best is None or el < best[0]:
+                        best = (el, sorted(lat_s))
+                return best
+        el, ls = asyncio.run(go())
+        out[mode] = {"req_per_s": len(reqs) / el, "wall_s": el, "p50_ms": ls[len(ls) // 2] * 1e3,
+                     "p99_ms": ls[int(len(ls) * 0.99) - 1] * 1e3,
+                     "flushes": sum(sv.route_batcher.flushes) if sv.route_batcher else None}
+        sv.close()
+        print(json.dumps({mode: out[mode]}), flush=True)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -122,7 +122,7 @@ def main() -> None:
                          "samples_per_s": B * di.world * a.steps / el}
     if di.is_main:
         print(json.dumps({"metric": "ETA MLP DP training samples/s", "n_gpus": di.world,
-                          "shared_gpu": share_gpu() and di.world > 1, "comm": a.comm,
+                          "shared_gpu": share_gpu() and di.world > 1,
                           "batch_per_gpu": B, "hidden": a.hidden, "results": results}), flush=True)
     if di.world > 1:
         dist.destroy_process_group()

@@ -71,6 +71,12 @@ class Settings:
     sse_delta: bool = False              # ROUTEST_SSE_DELTA (Appendix B #7)
     fast_predict: bool = True            # ROUTEST_FAST_PREDICT: pure-ASGI native single-predict path
     graph_nodes: int = 100_000           # ROUTEST_GRAPH_NODES: synthetic road graph for the route scorer
+    route_batch: str = "auto"            # ROUTEST_ROUTE_BATCH: auto (on with a GPU) | 1 | 0
+    route_batch_max: int = 1024          # ROUTEST_ROUTE_BATCH_MAX: requests per optimizer flush
+    route_batch_timeout_us: int = 500    # ROUTEST_ROUTE_BATCH_TIMEOUT_US
+    route_gpu_min_stops: int = 32        # ROUTEST_ROUTE_GPU_MIN_STOPS: haversine requests with fewer
+                                         # destinations stay inline (profiles/route_http_r2.jsonl)
+    warm_scorer: bool = True             # ROUTEST_WARM_SCORER: build the GCN scorer at startup
     sim_tick_min_s: float = 2.0          # ROUTEST_SIM_TICK_MIN (reference: U(2,5) s, utils.py:251)
     sim_tick_max_s: float = 5.0          # ROUTEST_SIM_TICK_MAX
     max_simulations: int = 256           # ROUTEST_MAX_SIMULATIONS (reference: unbounded threads)
@@ -144,6 +150,11 @@ def load_settings(env: Optional[Dict[str, str]] = None, dotenv_path: Optional[st
         sse_delta=_as_bool(g("ROUTEST_SSE_DELTA"), False),
         fast_predict=_as_bool(g("ROUTEST_FAST_PREDICT"), True),
         graph_nodes=_int("ROUTEST_GRAPH_NODES", 100_000),
+        route_batch=(g("ROUTEST_ROUTE_BATCH") or "auto").lower(),
+        route_batch_max=_int("ROUTEST_ROUTE_BATCH_MAX", 1024),
+        route_batch_timeout_us=_int("ROUTEST_ROUTE_BATCH_TIMEOUT_US", 500),
+        route_gpu_min_stops=_int("ROUTEST_ROUTE_GPU_MIN_STOPS", 32),
+        warm_scorer=_as_bool(g("ROUTEST_WARM_SCORER"), True),
         sim_tick_min_s=_float("ROUTEST_SIM_TICK_MIN", 2.0),
         sim_tick_max_s=_float("ROUTEST_SIM_TICK_MAX", 5.0),
         max_simulations=_int("ROUTEST_MAX_SIMULATIONS", 256),

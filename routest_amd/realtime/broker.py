@@ -23,6 +23,7 @@ import time
 from typing import Any, Dict, List, Optional, Set, Tuple
 
 from ..utils.logging import get_logger
+from ..utils.metrics import REGISTRY
 from ..utils.timeutil import parse_iso
 
 log = get_logger("realtime")
@@ -64,6 +65,7 @@ class MemoryBroker:
         self._lock = threading.Lock()
         self.max_queue = max_queue
         self.published = 0
+        self.dropped = 0         # messages not queued because a subscriber was max_queue behind
 
     def publish(self, data: Any, channel: str = "sse", type_: Optional[str] = None) -> int:
         msg = sse_message(data, type_)
@@ -71,9 +73,15 @@ class MemoryBroker:
             subs = list(self._subs.get(str(channel), ()))
             self.published += 1
         for loop, q in subs:
-            def _put(q=q, msg=msg):
+            def _put(q=q, msg=msg, channel=channel):
                 if q.qsize() < self.max_queue:
                     q.put_nowait(msg)
+                else:
+                    self.dropped += 1
+                    REGISTRY.sse_dropped.inc()
+                    if self.dropped & (self.dropped - 1) == 0:   # log at 1, 2, 4, 8, ... drops
+                        log.warning("SSE subscriber on channel %r is %d messages behind: dropped "
+                                    "(%d dropped so far)", channel, self.max_queue, self.dropped)
             try:
                 loop.call_soon_threadsafe(_put)
             except RuntimeError:  # loop closed

@@ -4,8 +4,8 @@
 tensors, then on a GPU runs ONE K5 launch (all haversine matrices) and ONE K6 launch (all greedy
 trip constructions, a wavefront per request); on CPU it runs the numpy/Python reference.  The
 result per request is the trips list (index lists into ``[source]+destinations``) or an
-:class:`InfeasibleStops` instance.  Requests can also be sharded round-robin over several GPUs
-(no collective needed).
+:class:`InfeasibleStops` instance.  Sharding over several GPUs is done by
+:class:`routing.route_batcher.RouteBatcher` (one worker thread per device, no collective).
 """
 from __future__ import annotations
 
@@ -103,17 +103,3 @@ def batched_trips(requests: Sequence[Dict[str, Any]], circuity: float = 1.3,
     if device is not None and torch.device(device).type == "cuda":
         return batched_trips_device(*packed, circuity=circuity, device=device)
     return batched_trips_cpu(*packed, circuity=circuity)
-
-
-def batched_trips_multi_gpu(requests: Sequence[Dict[str, Any]], circuity: float = 1.3,
-                            devices: Sequence[int] = (0,)) -> List[TripsOrError]:
-    """Shard requests round-robin over GPUs; launches on each device are asynchronous."""
-    shards = [list(range(k, len(requests), len(devices))) for k in range(len(devices))]
-    results: List[Optional[TripsOrError]] = [None] * len(requests)
-    for dev, idx in zip(devices, shards):
-        if not idx:
-            continue
-        res = batched_trips([requests[i] for i in idx], circuity, torch.device("cuda", dev))
-        for i, r in zip(idx, res):
-            results[i] = r
-    return results  # type: ignore[return-value]

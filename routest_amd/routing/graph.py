@@ -23,7 +23,7 @@ import torch
 
 from ..data.graph import RoadGraph, synth_road_graph
 from ..models.features import RECORD_DTYPE, pack_record
-from .providers import HaversineProvider, PROFILE_SPEED_MPS, _bbox, haversine_m
+from .providers import HaversineProvider, PROFILE_SPEED_MPS, ProviderError, _bbox, haversine_m
 
 V_MAX_MPS = 130 / 3.6
 CLASS_FACTOR = np.array([1.15, 1.0, 0.85, 0.65], dtype=np.float32)   # residential .. highway
@@ -317,6 +317,8 @@ class GraphProvider(HaversineProvider):
         self.device = device
         self._astar = None
         self._csr = None
+        import threading
+        self._lock = threading.Lock()
 
     @classmethod
     def synthetic(cls, num_nodes: int = 100_000, eta_model=None, device=None) -> "GraphProvider":
@@ -328,9 +330,11 @@ class GraphProvider(HaversineProvider):
 
     def _shortest(self, pairs: List[Tuple[int, int]]) -> List[Tuple[float, List[int]]]:
         if self.device is not None and torch.device(self.device).type == "cuda":
-            if self._astar is None:
-                self._astar = BatchedAstar(self.g, self.cost, self.device, slots=1024, cap=65536)
-            return self._astar.paths([p[0] for p in pairs], [p[1] for p in pairs])
+            # one search workspace per provider: concurrent handler threads take turns
+            with self._lock:
+                if self._astar is None:
+                    self._astar = BatchedAstar(self.g, self.cost, self.device, slots=1024, cap=65536)
+                return self._astar.paths([p[0] for p in pairs], [p[1] for p in pairs])
         from scipy.sparse import csr_matrix
         from scipy.sparse.csgraph import dijkstra
         if self._csr is None:
@@ -348,9 +352,19 @@ class GraphProvider(HaversineProvider):
             out.append((float(dist[t]), path[::-1]))
         return out
 
-    def directions(self, coords: List[List[float]], profile: str) -> Dict[str, Any]:
+    def leg_pairs(self, coords: List[List[float]]):
+        """Snap [[lon, lat], ...] to graph nodes; returns (nodes, consecutive (s, t) node pairs)."""
         nodes = self.g.nearest_nodes([c[1] for c in coords], [c[0] for c in coords])
-        legs = self._shortest([(int(nodes[k]), int(nodes[k + 1])) for k in range(len(nodes) - 1)])
+        return nodes, [(int(nodes[k]), int(nodes[k + 1])) for k in range(len(nodes) - 1)]
+
+    def directions(self, coords: List[List[float]], profile: str) -> Dict[str, Any]:
+        nodes, pairs = self.leg_pairs(coords)
+        return self.feature_from_legs(coords, nodes, self._shortest(pairs), profile)
+
+    def feature_from_legs(self, coords: List[List[float]], nodes, legs, profile: str) -> Dict[str, Any]:
+        """ORS-shaped Feature from per-leg (seconds, node path) results.  A leg the search did not
+        find (disconnected stops, or a search that hit its pop/heap limits) is an explicit
+        :class:`ProviderError`, never a silent straight line."""
         speed_scale = PROFILE_SPEED_MPS["driving-car"] / PROFILE_SPEED_MPS.get(profile, PROFILE_SPEED_MPS["driving-car"])
         geometry: List[List[float]] = [[float(coords[0][0]), float(coords[0][1])]]
         segments, way_points = [], [0]
@@ -358,14 +372,14 @@ class GraphProvider(HaversineProvider):
         for k, (sec, path) in enumerate(legs):
             start = len(geometry) - 1
             if not path:
-                path = [int(nodes[k]), int(nodes[k + 1])]
-                sec = float(haversine_m(self.g.lat[path[0]], self.g.lon[path[0]], self.g.lat[path[1]],
-                                        self.g.lon[path[1]]) / PROFILE_SPEED_MPS["driving-car"])
+                raise ProviderError(f"no road path found between waypoints {k} and {k + 1} "
+                                    f"(graph nodes {int(nodes[k])} -> {int(nodes[k + 1])})")
             p = np.asarray(path)
             dist = float(haversine_m(self.g.lat[p[:-1]], self.g.lon[p[:-1]], self.g.lat[p[1:]],
                                      self.g.lon[p[1:]]).sum() * 1.15) if len(p) > 1 else 0.0
-            for v in path:
-                geometry.append([round(float(self.g.lon[v]), 6), round(float(self.g.lat[v]), 6)])
+            # node coordinates of the whole leg in one vector op (6 decimals, like ORS)
+            geometry.extend(np.round(np.stack([self.g.lon[p], self.g.lat[p]], axis=1)
+                                     .astype(np.float64), 6).tolist())
             geometry.append([float(coords[k + 1][0]), float(coords[k + 1][1])])
             end = len(geometry) - 1
             way_points.append(end)

@@ -1,0 +1,243 @@
+"""Cross-request micro-batching for ``/api/optimize_route``, ``/route`` and ``/api/request_route``.
+
+The reference optimises one request at a time: an ORS matrix call, a Python greedy loop, then one
+ORS directions call per trip (``RO/Flaskr/utils.py:85-193``, ``RO/Flaskr/routes.py:89-127``).
+Here concurrent requests queue up and one worker per GPU flushes them together
+(``batch_max`` requests or ``timeout_us`` after the first arrival):
+
+1. every multi-stop request of the flush goes through ONE K5 launch (all haversine matrices) and
+   ONE K6 launch (all greedy multi-trip constructions, a wavefront per request) —
+   :func:`routing.batched.batched_trips`;
+2. with the road-graph provider, every leg of every trip (and every point-to-point request) of
+   the flush is snapped to graph nodes in one KD-tree query and searched by ONE batched A* launch
+   (K9, :class:`routing.graph.BatchedAstar` on the worker's own GPU); duplicate legs are searched
+   once;
+3. the GeoJSON Features are assembled on the host by the same code as the per-request path
+   (:func:`routing.optimizer.optimize_route` with the precomputed trips and a provider view that
+   answers ``directions`` from the precomputed legs), so responses are identical to it.  The
+   assembly runs back on the caller's thread (the event loop for HTTP requests): the worker thread
+   only runs the short GPU phases, so it does not fight the request handlers for the GIL.
+
+Several GPUs: one worker thread per device pulling from the same queue (no
+collective); each worker's launches and host syncs touch only its own device, so flushes on
+different GPUs overlap.  A leg the search does not find is an explicit error response.
+"""
+from __future__ import annotations
+
+import asyncio
+import concurrent.futures as cf
+import queue
+import threading
+import time
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from ..utils.logging import get_logger
+from ..utils.metrics import REGISTRY
+from .batched import batched_trips
+from .greedy import InfeasibleStops
+from .optimizer import optimize_route
+from .providers import ProviderError
+
+log = get_logger("route_batcher")
+
+
+def _valid_points(r: Any) -> bool:
+    return (isinstance(r, dict) and isinstance(r.get("destination_points"), list)
+            and len(r["destination_points"]) > 0 and isinstance(r.get("source_point"), dict)
+            and "lat" in r["source_point"] and "lon" in r["source_point"]
+            and all(isinstance(p, dict) and "lat" in p and "lon" in p for p in r["destination_points"]))
+
+
+class _LegView:
+    """Provider view for the host-side assembly of one flush: ``directions`` answers from the legs
+    searched in the batch's single A* launch; everything else delegates to the real provider."""
+
+    def __init__(self, base, legs: Dict[tuple, tuple]):
+        self.base = base
+        self.legs = legs
+        self.name = base.name
+
+    def matrix(self, points, profile):
+        return self.base.matrix(points, profile)
+
+    def directions(self, coords, profile):
+        nodes, pairs = self.base.leg_pairs(coords)
+        return self.base.feature_from_legs(coords, nodes, [self.legs[p] for p in pairs], profile)
+
+
+class RouteBatcher:
+    def __init__(self, provider, engine: str = "backend:mi355x", devices: Sequence[Any] = (None,),
+                 batch_max: int = 1024, timeout_us: int = 500, astar_slots: int = 8192):
+        self.provider = provider
+        self.engine = engine
+        self.devices = list(devices) or [None]
+        self.batch_max = batch_max
+        self.timeout_s = timeout_us / 1e6
+        self.astar_slots = astar_slots
+        self._astar: Dict[Any, Any] = {}
+        self._astar_lock = threading.Lock()
+        self.q: "queue.SimpleQueue[Optional[tuple]]" = queue.SimpleQueue()
+        self.flushes = [0] * len(self.devices)
+        self.threads = [threading.Thread(target=self._worker, args=(d, i), name=f"route-batch-{i}",
+                                         daemon=True) for i, d in enumerate(self.devices)]
+        for t in self.threads:
+            t.start()
+
+    # ------------------------------------------------------------------ batch function
+    def _astar_for(self, device):
+        from .graph import BatchedAstar
+        key = str(device)
+        with self._astar_lock:
+            a = self._astar.get(key)
+            if a is None:
+                a = BatchedAstar(self.provider.g, self.provider.cost, device, slots=self.astar_slots)
+                self._astar[key] = a
+            return a
+
+    def _graph_legs(self, payloads: List[Any], trips: Dict[int, Any], device) -> Dict[tuple, tuple]:
+        """Every leg of the flush -> {(s, t): (seconds, node path)} from ONE batched search."""
+        prov = self.provider
+        coord_lists: List[List[List[float]]] = []
+        for k, r in enumerate(payloads):
+            if not _valid_points(r):
+                continue
+            pts = [r["source_point"]] + list(r["destination_points"])
+            if len(pts) == 2:
+                coord_lists.append([[pts[0]["lon"], pts[0]["lat"]], [pts[1]["lon"], pts[1]["lat"]]])
+            elif isinstance(trips.get(k), list):
+                for trip in trips[k]:
+                    coord_lists.append([[pts[i]["lon"], pts[i]["lat"]] for i in trip])
+        if not coord_lists:
+            return {}
+        flat = np.array([c for cl in coord_lists for c in cl], dtype=np.float64)
+        nodes = prov.g.nearest_nodes(flat[:, 1], flat[:, 0])
+        pairs = set()
+        o = 0
+        for cl in coord_lists:
+            n = nodes[o:o + len(cl)]
+            pairs.update((int(n[i]), int(n[i + 1])) for i in range(len(cl) - 1))
+            o += len(cl)
+        pairs = sorted(pairs)
+        if device is not None and getattr(device, "type", str(device)).startswith("cuda"):
+            res = self._astar_for(device).paths([p[0] for p in pairs], [p[1] for p in pairs])
+        else:
+            res = prov._shortest(pairs)
+        return dict(zip(pairs, res))
+
+    def plan_batch(self, payloads: Sequence[Any], device=None) -> List[tuple]:
+        """The GPU phases of a flush: per request ``(trips or InfeasibleStops or None, view)``."""
+        payloads = list(payloads)
+        name = getattr(self.provider, "name", "")
+        trips: Dict[int, Any] = {}
+        multi = [k for k, r in enumerate(payloads) if _valid_points(r) and len(r["destination_points"]) > 1]
+        if multi and name in ("haversine", "graph"):
+            res = batched_trips([payloads[k] for k in multi], circuity=self.provider.circuity,
+                                device=device)
+            trips = dict(zip(multi, res))
+        view = self.provider
+        if name == "graph":
+            try:
+                view = _LegView(self.provider, self._graph_legs(payloads, trips, device))
+            except ProviderError as e:
+                return [(e, None) for _ in payloads]
+        return [(trips.get(k), view) for k in range(len(payloads))]
+
+    def assemble(self, payload: Any, plan: tuple) -> Dict[str, Any]:
+        """Host side of one request: GeoJSON Feature (or error) from its planned trips/legs."""
+        t, view = plan
+        if isinstance(t, (InfeasibleStops, ProviderError)):
+            return {"error": str(t)}
+        return optimize_route(payload, view, self.engine, trips=t)
+
+    def run_batch(self, payloads: Sequence[Any], device=None) -> List[Dict[str, Any]]:
+        """Optimise a list of request payloads together (plan + assembly; also callable directly,
+        e.g. ``/api/optimize_routes_batch``)."""
+        payloads = list(payloads)
+        return [self.assemble(p, pl) for p, pl in zip(payloads, self.plan_batch(payloads, device))]
+
+    # ------------------------------------------------------------------ queue side
+    def submit_nowait(self, payload: Any, loop: Optional[asyncio.AbstractEventLoop] = None):
+        fut = loop.create_future() if loop is not None else cf.Future()
+        self.q.put((payload, fut, loop, time.perf_counter()))
+        return fut
+
+    async def submit(self, payload: Any) -> Dict[str, Any]:
+        plan = await self.submit_nowait(payload, asyncio.get_running_loop())
+        return self.assemble(payload, plan)
+
+    def optimize_sync(self, payload: Any, timeout: float = 60.0) -> Dict[str, Any]:
+        return self.assemble(payload, self.submit_nowait(payload).result(timeout))
+
+    @staticmethod
+    def _resolve(fut, loop, value=None, exc: Optional[BaseException] = None) -> None:
+        def _set():
+            if fut.done():
+                return
+            if exc is not None:
+                fut.set_exception(exc)
+            else:
+                fut.set_result(value)
+        if loop is not None:
+            try:
+                loop.call_soon_threadsafe(_set)
+            except RuntimeError:
+                pass
+        else:
+            _set()
+
+    def _collect(self, first) -> list:
+        batch = [first]
+        deadline = first[3] + self.timeout_s
+        while len(batch) < self.batch_max:
+            try:
+                it = self.q.get_nowait()
+            except queue.Empty:
+                rem = deadline - time.perf_counter()
+                if rem <= 0:
+                    break
+                try:
+                    it = self.q.get(timeout=rem)
+                except queue.Empty:
+                    break
+            batch.append(it)
+            if it is None:
+                break
+        return batch
+
+    def _worker(self, device, idx: int) -> None:
+        import torch
+        while True:
+            first = self.q.get()
+            if first is None:
+                self.q.put(None)
+                return
+            batch = self._collect(first)
+            stop = batch[-1] is None
+            if stop:
+                batch.pop()
+            t0 = time.perf_counter()
+            try:
+                if device is not None and getattr(device, "type", "") == "cuda":
+                    with torch.cuda.device(device):
+                        res = self.plan_batch([b[0] for b in batch], device)
+                else:
+                    res = self.plan_batch([b[0] for b in batch], device)
+                for (_, fut, loop, _), r in zip(batch, res):
+                    self._resolve(fut, loop, r)
+            except BaseException as e:  # noqa: BLE001 - fail the flush's requests, keep serving
+                log.error("route flush of %d failed on %s: %r", len(batch), device, e)
+                for _, fut, loop, _ in batch:
+                    self._resolve(fut, loop, exc=e)
+            self.flushes[idx] += 1
+            REGISTRY.route_batch.observe(len(batch))
+            REGISTRY.route_flush_time.observe(time.perf_counter() - t0)
+            if stop:
+                self.q.put(None)
+                return
+
+    def close(self) -> None:
+        self.q.put(None)
+        for t in self.threads:
+            t.join(timeout=10)

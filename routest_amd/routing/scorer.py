@@ -63,6 +63,11 @@ class RouteScorer:
         keep[1:] = ids[1:] != ids[:-1]
         return ids[keep].astype(int).tolist()
 
+    def warm(self) -> None:
+        """Startup warm-up: KD-tree for coordinate snapping + node delays (GPU: done in __init__)."""
+        self.g.nearest_nodes([float(self.g.lat[0])], [float(self.g.lon[0])])
+        self.node_delays()
+
     # ------------------------------------------------------------------ scoring
     def node_delays(self) -> np.ndarray:
         if self._hip is not None:

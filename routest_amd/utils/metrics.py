@@ -97,11 +97,17 @@ class Registry:
 
         self.device_failures = Counter("routest_device_failures_total", "batches that raised on a device")
         self.slow_batches = Counter("routest_slow_batches_total", "batches slower than the watchdog limit")
+        self.route_batch = Histogram("routest_route_batch_size", "route requests per optimizer flush",
+                                     [1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 4096])
+        self.route_flush_time = Histogram("routest_route_flush_seconds", "optimizer flush time (K5+K6+K9 + assembly)",
+                                          [1e-4, 5e-4, 1e-3, 5e-3, 1e-2, 5e-2, 0.1, 0.5, 1.0])
+        self.sse_dropped = Counter("routest_sse_dropped_total", "SSE messages dropped for slow subscribers")
 
     def render(self) -> str:
         lines: List[str] = []
         for m in (self.requests, self.preds, self.latency, self.batch, self.queue_wait, self.gpu_time,
-                  self.device_failures, self.slow_batches):
+                  self.device_failures, self.slow_batches, self.route_batch, self.route_flush_time,
+                  self.sse_dropped):
             lines.extend(m.render())
         lines.extend(_device_gauges())
         return "\n".join(lines) + "\n"

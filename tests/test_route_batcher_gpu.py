@@ -1,0 +1,87 @@
+"""The GPU optimizer on the request path: >= 1k concurrent multi-stop HTTP requests through
+/api/optimize_route with the cross-request batcher (K5 + K6 per flush; with the road-graph
+provider ONE batched A* launch per flush) answer exactly what the per-request path answers."""
+import asyncio
+
+import numpy as np
+import pytest
+import torch
+
+from routest_amd.routing.optimizer import optimize_route
+
+pytestmark = pytest.mark.gpu
+
+
+def _reqs_on(lat, lon, n, seed, kmax=10):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        idx = rng.integers(0, len(lat), int(rng.integers(2, kmax + 1)))
+        out.append({"source_point": {"lat": float(lat[idx[0]]), "lon": float(lon[idx[0]])},
+                    "destination_points": [{"lat": float(lat[j]), "lon": float(lon[j]),
+                                            "payload": int(rng.integers(1, 3))} for j in idx[1:]],
+                    "driver_details": {"driver_name": f"v{i}", "vehicle_type": "car",
+                                       "vehicle_capacity": int(rng.integers(2, 8)),
+                                       "maximum_distance": float(rng.choice([20000, 1e7]))}})
+    return out
+
+
+def _serve(provider, reqs):
+    import httpx
+    from routest_amd.api.app import build_services, create_app
+    from routest_amd.config import load_settings
+    from routest_amd.serve.eta_service import EtaService
+    s = load_settings(env={}, dotenv_path=None, devices=[0], route_batch="auto", route_gpu_min_stops=1,
+                      route_batch_max=512, route_batch_timeout_us=2000, warm_scorer=False)
+    sv = build_services(s, eta=EtaService(None, device="cpu"), provider=provider, store=None)
+    assert sv.route_batcher is not None and sv.route_batcher.devices[0].type == "cuda"
+    app = create_app(sv)
+
+    async def go():
+        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://t",
+                                     timeout=120) as c:
+            return await asyncio.gather(*[c.post("/api/optimize_route", json=r) for r in reqs])
+    try:
+        rs = asyncio.run(go())
+        flushes = sum(sv.route_batcher.flushes)
+    finally:
+        sv.close()
+    return [r.json() for r in rs], [r.status_code for r in rs], flushes, s.engine_name
+
+
+def test_http_1k_concurrent_haversine_gpu_batched():
+    from routest_amd.routing.providers import HaversineProvider
+    rng = np.random.default_rng(0)
+    lat = 14.55 + rng.normal(0, 0.05, 5000)
+    lon = 121.03 + rng.normal(0, 0.05, 5000)
+    reqs = _reqs_on(lat, lon, 1200, 1)
+    prov = HaversineProvider()
+    got, codes, flushes, eng = _serve(prov, reqs)
+    assert flushes < len(reqs) / 4            # requests were batched
+    for g, c, r in zip(got, codes, reqs):
+        ref = optimize_route(r, prov, eng)
+        assert g == ref and c == (400 if "error" in ref else 200)
+
+
+def test_http_1k_concurrent_graph_provider_one_astar_launch_per_flush():
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider, edge_costs
+    from routest_amd.serve.eta_service import default_model
+    g = synth_road_graph(20_000, seed=4)
+    dev = torch.device("cuda:0")
+    cost = edge_costs(g, default_model(hidden=64, steps=50), device=dev)
+    prov = GraphProvider(g, cost, device=dev)
+    reqs = _reqs_on(g.lat, g.lon, 1000, 2, kmax=6)
+    got, codes, flushes, eng = _serve(prov, reqs)
+    assert flushes < len(reqs) / 4
+    ref_prov = GraphProvider(g, cost, device=dev)           # per-request path: one A* launch per trip
+    mism = 0
+    for gg, c, r in zip(got, codes, reqs):
+        ref = optimize_route(r, ref_prov, eng)
+        assert c == (400 if "error" in ref else 200)
+        if gg != ref:
+            mism += 1
+            # same search problem: equal cost; a tie may pick another equal-cost node path
+            assert abs(gg["properties"]["summary"]["duration"] - ref["properties"]["summary"]["duration"]) \
+                <= 1e-3 * max(1.0, ref["properties"]["summary"]["duration"])
+    assert mism <= len(reqs) // 100
