@@ -55,6 +55,38 @@ def _check_gpu(sv: Any) -> Dict[str, Any]:
         return {"status": "error", "latency_ms": int((time.time() - t0) * 1000), "error": str(e)[:200]}
 
 
+def _check_collectives(sv: Any) -> Dict[str, Any]:
+    """RCCL / collective readiness (SURVEY R10 "RCCL ready"): the RCCL library our native comm
+    links (torch's bundled librccl), the torch.distributed state of this process, and any native
+    DeviceComm the services hold (one-shot buffers mapped, no pending peer-wait error)."""
+    t0 = time.time()
+    try:
+        import torch
+        import torch.distributed as dist
+        out: Dict[str, Any] = {"rccl_available": bool(dist.is_available() and dist.is_nccl_available())}
+        from ..ops import _ext
+        C = _ext.native(required=False)
+        if C is not None and torch.cuda.is_available():
+            out["rccl_version"] = int(C.rccl_version())
+        init = dist.is_available() and dist.is_initialized()
+        out["dist_initialized"] = bool(init)
+        if init:
+            out["backend"] = dist.get_backend()
+            out["world_size"] = dist.get_world_size()
+            out["rank"] = dist.get_rank()
+        comm = getattr(sv, "comm", None)
+        status = "ok" if out["rccl_available"] else "skipped"
+        if comm is not None:
+            out["device_comm"] = comm.ready()
+            if out["device_comm"].get("error"):
+                status = "degraded"
+        out["status"] = status
+        out["latency_ms"] = int((time.time() - t0) * 1000)
+        return out
+    except Exception as e:
+        return {"status": "error", "latency_ms": int((time.time() - t0) * 1000), "error": str(e)[:200]}
+
+
 def health_payload(sv: Any) -> Dict[str, Any]:
     s = sv.settings
     redis_res = sv.broker.ping()
@@ -64,15 +96,17 @@ def health_payload(sv: Any) -> Dict[str, Any]:
     else:
         db_res = sv.store.ping()
     gpu_res = _check_gpu(sv)
+    coll_res = _check_collectives(sv)
     model = sv.eta.describe()
     model_res = {"status": ("degraded" if model.get("degraded") else "ok") if sv.eta.batcher is not None
                  else "skipped", **model}
-    parts = (redis_res["status"], engine_res["status"], db_res["status"], gpu_res["status"], model_res["status"])
+    parts = (redis_res["status"], engine_res["status"], db_res["status"], gpu_res["status"], model_res["status"],
+             coll_res["status"])
     overall = "degraded" if any(p in ("error", "degraded") for p in parts) else "ok"
     return {
         "backend": True,
         "checks": {"engine": engine_res, "redis": redis_res, "supabase": db_res, "gpu": gpu_res,
-                   "model": model_res},
+                   "model": model_res, "collectives": coll_res},
         "db": db_res["status"] == "ok",
         "osrm": engine_res["status"] in ("ok", "degraded"),
         "redis": redis_res["status"] == "ok",

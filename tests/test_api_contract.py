@@ -190,6 +190,9 @@ def test_health_always_200(client):
     assert {"backend", "checks", "db", "osrm", "redis", "tiles", "status", "version"} <= set(j)
     assert {"engine", "redis", "supabase"} <= set(j["checks"])
     assert j["status"] in ("ok", "degraded")
+    # R10 "RCCL ready": collective readiness next to the gpu/model checks
+    coll = j["checks"]["collectives"]
+    assert coll["status"] in ("ok", "skipped") and "rccl_available" in coll and "dist_initialized" in coll
 
 
 def test_history_without_store():
