@@ -34,8 +34,9 @@ def test_astar_optimal_costs_and_valid_paths(graph_and_cost, monkeypatch, reorde
     a = BatchedAstar(g, cost, "cuda:0", slots=1024, cap=65536)
     c, n, st, p = a.run(src, dst)
     c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
-    assert (st == 0).mean() > 0.99
     ref = dijkstra_ref(g, cost, src, dst)
+    assert np.isfinite(ref).all()            # every query is connected on this graph ...
+    assert (st == 0).all(), np.unique(st, return_counts=True)    # ... and every search finds it
     ok = st == 0
     np.testing.assert_allclose(c[ok], ref[ok], rtol=1e-4)
     # each path is a real edge sequence from src to dst whose cost sums to the reported cost

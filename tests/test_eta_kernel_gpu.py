@@ -231,3 +231,43 @@ def test_auto_variant_switches_to_16x16_kernel():
         torch.equal(auto(small), k3(small))
     ref = m(torch.from_numpy(records_to_features(rec))).detach()
     torch.testing.assert_close(auto(rt).cpu(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.fixture(scope="module")
+def trained256():
+    """An EtaMLP(256) trained in fp32 (autograd, on the GPU) so that its outputs vary with the
+    inputs: random-init outputs sit near y_mean, where a loose rtol hides large relative errors."""
+    torch.manual_seed(5)
+    m = EtaMLP(256)
+    rec, y = synth_records(1 << 16, 41)
+    x = torch.from_numpy(records_to_features(rec))
+    m.fit_normalization(x.numpy(), y)
+    md = m.to("cuda:0")
+    xd, yd = x.to("cuda:0"), torch.from_numpy(y).to("cuda:0")
+    yn = (yd - md.y_mean) / md.y_std
+    opt = torch.optim.Adam(md.parameters(), lr=2e-3)
+    for s in range(400):
+        k = (s % 16) * 4096
+        loss = torch.nn.functional.mse_loss(md.forward_normalized(xd[k:k + 4096]), yn[k:k + 4096])
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    return md.cpu().eval()
+
+
+@pytest.mark.parametrize("variant", [0, 3, 17, 20])
+def test_forward_trained_model_relative_to_spread(trained256, variant):
+    """K1+K2 vs the fp32 model on a TRAINED model, with the error measured against the spread of
+    the predictions (y - mean y), not against y itself: bf16 operands and fp32 accumulation keep
+    the worst row within 3 % and the mean within 0.5 % of the mean |y - mean y|."""
+    rec, _ = synth_records(200_003, 42)
+    rt = records_to_tensor(rec)
+    k = EtaMlpKernel(trained256, torch.device("cuda:0"), variant=variant)
+    got = k(rt.cuda()).cpu()
+    with torch.no_grad():
+        ref = trained256(torch.from_numpy(records_to_features(rec))).reshape(-1)
+    spread = (ref - ref.mean()).abs().mean()
+    assert spread > 5.0                      # the trained model's outputs really vary
+    err = (got - ref).abs() / spread
+    assert float(err.max()) < 0.03, float(err.max())
+    assert float(err.mean()) < 0.005, float(err.mean())

@@ -115,3 +115,21 @@ def test_http_concurrent_requests_through_batcher():
             assert r.json() == ref
         else:
             assert r.status_code == 200 and r.json() == ref
+
+
+def test_unfound_leg_is_an_explicit_error():
+    """A leg the search did not find is an error response, never a silent straight line."""
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider
+    g = synth_road_graph(2000, seed=6)
+    prov = GraphProvider(g, np.ones(g.num_edges, dtype=np.float32))
+    prov._shortest = lambda pairs: [(float("nan"), [])] * len(pairs)
+    req = {"source_point": {"lat": float(g.lat[0]), "lon": float(g.lon[0])},
+           "destination_points": [{"lat": float(g.lat[500]), "lon": float(g.lon[500])}]}
+    out = optimize_route(req, prov)
+    assert "error" in out and "no road path" in out["error"]
+    rb = RouteBatcher(prov, devices=[None])
+    try:
+        assert "no road path" in rb.run_batch([req])[0]["error"]
+    finally:
+        rb.close()
