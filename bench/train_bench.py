@@ -4,7 +4,7 @@
     python bench/train_bench.py                        # 1 GPU
     torchrun --nproc-per-node 8 bench/train_bench.py   # 8 GPUs, RCCL all-reduce over xGMI
 
-Modes: ``fused`` (HIP kernels, eager launches), ``graph`` (the whole fused step incl. the RCCL
+Modes: ``fused`` (HIP kernels only, eager launches), ``graph`` (the whole fused step incl. the RCCL
 all-reduce captured in one HIP graph), ``autograd`` (PyTorch eager bf16-autocast baseline with the
 same flat-bucket all-reduce).  Each mode: W warmup steps, then K timed steps between barriers.
 """
@@ -35,7 +35,7 @@ def main() -> None:
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--modes", default="fused,graph,hipblaslt,autograd")
+    ap.add_argument("--modes", default="fused,graph,autograd")
     ap.add_argument("--trace", default="", help="write a Chrome trace of 3 extra steps per mode (prefix)")
     ap.add_argument("--comm", default="torch", choices=["torch", "rccl", "oneshot", "auto"],
                     help="gradient all-reduce for the fused modes: ProcessGroup, or native (csrc/comm.hip)")
@@ -69,11 +69,10 @@ def main() -> None:
         m = EtaMLP(a.hidden)
         m.fit_normalization(xs, ys)
         yn = ((torch.from_numpy(y) - m.y_mean) / m.y_std).float().to(dev)
-        if mode in ("fused", "graph", "hipblaslt"):
+        if mode in ("fused", "graph"):
             tr = FusedMlp3Trainer(m, dev, B, B * di.world, lr=1e-3, allreduce=di.world > 1, comm=comm)
             if comm is not None and comm_algo != "auto":
                 tr.comm = _Pinned(comm, comm_algo)
-            tr.use_hipblaslt_wgrad = mode == "hipblaslt"
             step = lambda: tr.step(rt, yn)  # noqa: E731
             if mode == "graph":
                 s = torch.cuda.Stream()

@@ -132,6 +132,130 @@ void eta_mlp3_forward_hostio(torch::Tensor records, torch::Tensor out, torch::Te
                               variant, num_cus(blob.device().index()), cur_stream(blob), rb));
 }
 
+// ---------------------------------------------------------------- wide MLPs (mlp_big.hip)
+void check_bf16(const torch::Tensor& t, const char* name, int64_t rows, int64_t cols);
+
+static rt::NormParams norm_params(const std::vector<double>& norm) {
+  TORCH_CHECK(norm.size() == 8, "norm must hold 4 scales + 4 shifts");
+  rt::NormParams np;
+  for (int i = 0; i < 4; ++i) {
+    np.scale[i] = (float)norm[i];
+    np.shift[i] = (float)norm[4 + i];
+  }
+  return np;
+}
+
+// records may be pinned host memory (zero-copy) or on the GPU; h1 (and xf) on the GPU.
+void big_layer1(torch::Tensor records, torch::Tensor w1p, int64_t H, std::vector<double> norm,
+                torch::Tensor h1, c10::optional<torch::Tensor> xf) {
+  const int rb = record_bytes(records);
+  const int64_t B = records.size(0);
+  check_dev(w1p, "w1p");
+  check_dev(h1, "h1");
+  TORCH_CHECK(H % 32 == 0 && H >= 32, "H must be a multiple of 32");
+  TORCH_CHECK(w1p.scalar_type() == torch::kBFloat16 && w1p.numel() == H * 16, "w1p bf16 [H*16]");
+  TORCH_CHECK(h1.scalar_type() == torch::kBFloat16 && h1.dim() == 2 && h1.size(0) >= B && h1.size(1) >= H &&
+              h1.size(1) % 8 == 0, "h1 must be bf16 [>=B, >=H] (ld % 8 == 0)");
+  void* xfp = nullptr;
+  if (xf.has_value() && xf->defined()) {
+    check_bf16(*xf, "xf", B, 16);
+    xfp = xf->data_ptr();
+  }
+  TORCH_CHECK(B < (1LL << 31) - 64, "batch too large");
+  const c10::DeviceGuard guard(h1.device());
+  RT_CHECK_HIP(rt::launch_big_layer1(kernel_ptr(records, "records"), rb, (int)B, w1p.data_ptr(), (int)H,
+                                     norm_params(norm), h1.data_ptr(), (int)h1.size(1), xfp, cur_stream(h1)));
+}
+
+// epi 0: ypart = relu(W X^T + b2) . w3 per 64-unit block; 1: + h2 stored into out; 2: out = W X^T
+void gemm_nt(int64_t epi, torch::Tensor W, torch::Tensor X, int64_t N, int64_t M, int64_t K,
+             c10::optional<torch::Tensor> b2, c10::optional<torch::Tensor> w3,
+             c10::optional<torch::Tensor> ypart, c10::optional<torch::Tensor> out) {
+  check_dev(W, "W");
+  check_dev(X, "X");
+  TORCH_CHECK(W.scalar_type() == torch::kBFloat16 && X.scalar_type() == torch::kBFloat16, "bf16 W/X");
+  TORCH_CHECK(W.dim() == 2 && X.dim() == 2 && W.size(0) >= N && W.size(1) >= K && X.size(0) >= M &&
+              X.size(1) >= K, "operand shapes");
+  TORCH_CHECK(N % 128 == 0 && K % 32 == 0, "N % 128 == 0 and K % 32 == 0 required");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "epi in 0..2");
+  const float* b2p = nullptr;
+  const float* w3p = nullptr;
+  float* yp = nullptr;
+  void* op = nullptr;
+  int ldo = 0;
+  if (epi <= 1) {
+    TORCH_CHECK(b2.has_value() && w3.has_value() && ypart.has_value(), "b2, w3, ypart required");
+    for (auto* t : {&*b2, &*w3}) {
+      check_dev(*t, "vec");
+      TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->numel() >= N, "b2/w3 f32 [N]");
+    }
+    check_dev(*ypart, "ypart");
+    TORCH_CHECK(ypart->scalar_type() == torch::kFloat32 && ypart->numel() >= M * (N / 64), "ypart f32 [M, N/64]");
+    b2p = b2->data_ptr<float>();
+    w3p = w3->data_ptr<float>();
+    yp = ypart->data_ptr<float>();
+  }
+  if (epi >= 1) {
+    TORCH_CHECK(out.has_value(), "out required");
+    check_dev(*out, "out");
+    TORCH_CHECK(out->scalar_type() == torch::kBFloat16 && out->dim() == 2 && out->size(0) >= M &&
+                out->size(1) >= N && out->size(1) % 8 == 0, "out bf16 [>=M, >=N]");
+    op = out->data_ptr();
+    ldo = (int)out->size(1);
+  }
+  TORCH_CHECK(M < (1LL << 31) - 256, "M too large");
+  const c10::DeviceGuard guard(W.device());
+  RT_CHECK_HIP(rt::launch_gemm_nt((int)epi, W.data_ptr(), (int)W.size(1), X.data_ptr(), (int)X.size(1),
+                                  (int)N, (int)M, (int)K, b2p, w3p, yp, op, ldo, cur_stream(W)));
+}
+
+// y (f32 [B], GPU or pinned host) = sum of ypart rows + b3; training outputs optional
+void big_yreduce(torch::Tensor ypart, int64_t nparts, double b3, c10::optional<torch::Tensor> y,
+                 c10::optional<torch::Tensor> target, double gscale, c10::optional<torch::Tensor> dy,
+                 c10::optional<torch::Tensor> dyb, c10::optional<torch::Tensor> sq_err) {
+  check_dev(ypart, "ypart");
+  TORCH_CHECK(ypart.scalar_type() == torch::kFloat32 && nparts > 0 && ypart.numel() % nparts == 0, "ypart");
+  const int64_t B = ypart.numel() / nparts;
+  float* yp = nullptr;
+  if (y.has_value() && y->defined()) {
+    TORCH_CHECK(y->scalar_type() == torch::kFloat32 && y->numel() >= B, "y f32 [B]");
+    yp = (float*)kernel_ptr(*y, "y");
+  }
+  const float* tp = nullptr;
+  float* dyp = nullptr;
+  void* dybp = nullptr;
+  float* sqp = nullptr;
+  if (target.has_value() && target->defined()) {
+    TORCH_CHECK(dy.has_value() && dyb.has_value() && sq_err.has_value(), "training outputs required");
+    check_dev(*target, "target");
+    check_dev(*dy, "dy");
+    check_dev(*sq_err, "sq_err");
+    TORCH_CHECK(target->numel() >= B && dy->numel() >= B && sq_err->numel() >= B, "training vectors [B]");
+    check_bf16(*dyb, "dyb", B, 8);
+    tp = target->data_ptr<float>();
+    dyp = dy->data_ptr<float>();
+    dybp = dyb->data_ptr();
+    sqp = sq_err->data_ptr<float>();
+  }
+  const c10::DeviceGuard guard(ypart.device());
+  RT_CHECK_HIP(rt::launch_big_yreduce(ypart.data_ptr<float>(), (int)nparts, (int)B, (float)b3, yp, tp,
+                                      (float)gscale, dyp, dybp, sqp, cur_stream(ypart)));
+}
+
+void big_dz2(torch::Tensor h2a, torch::Tensor dy, torch::Tensor w3, int64_t H, torch::Tensor dz2) {
+  check_dev(h2a, "h2a");
+  check_dev(dy, "dy");
+  check_dev(w3, "w3");
+  const int64_t B = dz2.size(0);
+  check_bf16(dz2, "dz2", B, H);
+  TORCH_CHECK(h2a.scalar_type() == torch::kBFloat16 && h2a.dim() == 2 && h2a.size(0) >= B &&
+              h2a.size(1) >= H && H % 8 == 0, "h2a bf16 [B, >=H]");
+  TORCH_CHECK(dy.numel() >= B && w3.numel() >= H, "dy [B], w3 [H]");
+  const c10::DeviceGuard guard(h2a.device());
+  RT_CHECK_HIP(rt::launch_big_dz2(h2a.data_ptr(), (int)h2a.size(1), dy.data_ptr<float>(),
+                                  w3.data_ptr<float>(), (int)B, (int)H, dz2.data_ptr(), cur_stream(h2a)));
+}
+
 torch::Tensor eta_featurize(torch::Tensor records) {
   check_dev(records, "records");
   TORCH_CHECK(records.scalar_type() == torch::kInt32 && records.dim() == 2 && records.size(1) == 4,
@@ -207,8 +331,8 @@ void check_bf16(const torch::Tensor& t, const char* name, int64_t rows, int64_t 
 // Writes every output in place (static buffers: the step is HIP-graph capturable).
 void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tensor blob, int64_t H,
                         std::vector<double> norm, double gscale, torch::Tensor xf,
-                        torch::Tensor h1a, torch::Tensor h2a, torch::Tensor dz2, torch::Tensor dyb,
-                        torch::Tensor loss_tiles, torch::Tensor step_ctr) {
+                        torch::Tensor h1a, torch::Tensor h2a, torch::Tensor dz2, torch::Tensor dh1,
+                        torch::Tensor dyb, torch::Tensor sq_err, torch::Tensor step_ctr) {
   check_dev(records, "records");
   check_dev(target, "target");
   check_dev(blob, "blob");
@@ -216,42 +340,29 @@ void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tens
               "records must be int32 [B,4]");
   const int64_t B = records.size(0);
   TORCH_CHECK(target.scalar_type() == torch::kFloat32 && target.numel() == B, "target must be f32 [B]");
+  TORCH_CHECK(H == 64 || H == 128 || H == 256, "fused trainer: H in (64, 128, 256)");
   TORCH_CHECK(blob.scalar_type() == torch::kUInt8 &&
-              (size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
+              (size_t)blob.numel() == rt::eta_mlp3_train_blob_bytes((int)H), "bad training blob");
   check_bf16(xf, "xf", B, 16);
   check_bf16(h1a, "h1a", B, H + 16);
   check_bf16(h2a, "h2a", B, H + 16);
   check_bf16(dz2, "dz2", B, H);
+  check_bf16(dh1, "dh1", B, H);
   check_bf16(dyb, "dyb", B, 8);
-  check_dev(loss_tiles, "loss_tiles");
-  TORCH_CHECK(loss_tiles.scalar_type() == torch::kFloat32 && loss_tiles.numel() >= (B + 31) / 32,
-              "loss_tiles must be f32 [ceil(B/32)]");
+  check_dev(sq_err, "sq_err");
+  TORCH_CHECK(sq_err.scalar_type() == torch::kFloat32 && sq_err.numel() >= B, "sq_err must be f32 [B]");
   check_dev(step_ctr, "step_ctr");
   TORCH_CHECK(step_ctr.scalar_type() == torch::kInt32 && step_ctr.numel() >= 1, "step_ctr i32");
   const c10::DeviceGuard guard(records.device());
   RT_CHECK_HIP(rt::launch_eta_mlp3_train_fwd(
       records.data_ptr(), target.data_ptr<float>(), (int)B, blob.data_ptr(), (int)H,
       norm_from(norm), (float)gscale, xf.data_ptr(), h1a.data_ptr(), h2a.data_ptr(),
-      dz2.data_ptr(), dyb.data_ptr(), loss_tiles.data_ptr<float>(), step_ctr.data_ptr<int>(),
+      dz2.data_ptr(), dh1.data_ptr(), dyb.data_ptr(), sq_err.data_ptr<float>(), step_ctr.data_ptr<int>(),
       num_cus(records.device().index()), cur_stream(records)));
 }
 
-void relu_bwd(torch::Tensor dh1, torch::Tensor h1a, torch::Tensor dz1) {
-  check_dev(dh1, "dh1");
-  check_dev(h1a, "h1a");
-  check_dev(dz1, "dz1");
-  TORCH_CHECK(dh1.dim() == 2 && dh1.sizes() == dz1.sizes(), "dh1/dz1 shape");
-  const int64_t B = dh1.size(0), H = dh1.size(1);
-  TORCH_CHECK(H % 8 == 0 && h1a.size(0) == B && h1a.size(1) >= H, "h1a shape");
-  TORCH_CHECK(dh1.scalar_type() == torch::kBFloat16 && h1a.scalar_type() == torch::kBFloat16 &&
-              dz1.scalar_type() == torch::kBFloat16, "bf16 tensors expected");
-  const c10::DeviceGuard guard(dh1.device());
-  RT_CHECK_HIP(rt::launch_relu_bwd(dh1.data_ptr(), h1a.data_ptr(), (int)h1a.size(1),
-                                   dz1.data_ptr(), (int)B, (int)H, cur_stream(dh1)));
-}
-
 void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor V,
-                torch::Tensor blob, torch::Tensor w2bf, torch::Tensor step, int64_t H, double lr,
+                torch::Tensor blob, torch::Tensor step, int64_t H, double lr,
                 double beta1, double beta2, double eps, double wd, int64_t warmup,
                 int64_t total_steps, double min_lr_ratio, bool update) {
   const int64_t N = rt::mlp3_num_params((int)H);
@@ -262,12 +373,14 @@ void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor
   check_dev(G, "G");
   TORCH_CHECK(G.scalar_type() == torch::kFloat32 && G.numel() == rt::mlp3_grad_bucket_floats((int)H),
               "G must be the flat f32 gradient bucket");
-  TORCH_CHECK((size_t)blob.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
-  check_bf16(w2bf, "w2bf", H, H);
+  TORCH_CHECK(H == 64 || H == 128 || H == 256, "fused trainer: H in (64, 128, 256)");
+  check_dev(blob, "blob");
+  TORCH_CHECK(blob.scalar_type() == torch::kUInt8 &&
+              (size_t)blob.numel() == rt::eta_mlp3_train_blob_bytes((int)H), "bad training blob");
   check_dev(step, "step");
   const c10::DeviceGuard guard(P.device());
   RT_CHECK_HIP(rt::launch_adamw_pack(P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(),
-                                     V.data_ptr<float>(), blob.data_ptr(), w2bf.data_ptr(),
+                                     V.data_ptr<float>(), blob.data_ptr(),
                                      step.data_ptr<int>(), (int)H, (float)lr, (float)beta1,
                                      (float)beta2, (float)eps, (float)wd, (int)warmup,
                                      (int)total_steps, (float)min_lr_ratio, update ? 1 : 0,
@@ -276,7 +389,8 @@ void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor
 
 // slab: f32 [S, stride]; the partial of k-slice s is written at slab[s, offset + m*ldo + n].
 void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N, torch::Tensor slab,
-           int64_t offset, int64_t ldo, c10::optional<torch::Tensor> mask, int64_t nout) {
+           int64_t offset, int64_t ldo, c10::optional<torch::Tensor> mask, int64_t nout,
+           bool mask_hperm) {
   check_dev(A, "A");
   if (nout < 0 || nout > N) nout = N;
   const void* mptr = nullptr;
@@ -304,7 +418,7 @@ void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N
   RT_CHECK_HIP(rt::launch_wgrad(A.data_ptr(), (int)A.size(1), (int)M, (int)Mout, Bm.data_ptr(),
                                 (int)Bm.size(1), (int)N, (int)A.size(0), (int)slab.size(0),
                                 slab.data_ptr<float>() + offset, (int)ldo, (long long)slab.size(1),
-                                cur_stream(A), mptr, ldm, (int)nout));
+                                cur_stream(A), mptr, ldm, (int)nout, mask_hperm));
 }
 
 void wgrad_reduce(torch::Tensor slab, torch::Tensor G) {
@@ -691,14 +805,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("eta_mlp3_blob16_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_blob16_bytes((int)H); });
   m.def("route_haversine_matrix", &route_haversine_matrix, "K5: batched haversine matrices (f64)");
   m.def("route_greedy_cvrp", &route_greedy_cvrp, "K6: batched greedy multi-trip CVRP");
-  m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad");
-  m.def("relu_bwd", &relu_bwd, "dz1 = dh1 * (h1 > 0)");
-  m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + MFMA fragment re-pack");
+  m.def("big_layer1", &big_layer1, "wide MLP: featurize + layer 1 -> h1 (hperm order)",
+        py::arg("records"), py::arg("w1p"), py::arg("H"), py::arg("norm"), py::arg("h1"),
+        py::arg("xf") = py::none());
+  m.def("gemm_nt", &gemm_nt, "wide MLP layer GEMM Z^T = W X^T with fused epilogues (0 y-partials, 1 +h2, 2 store)",
+        py::arg("epi"), py::arg("W"), py::arg("X"), py::arg("N"), py::arg("M"), py::arg("K"),
+        py::arg("b2") = py::none(), py::arg("w3") = py::none(), py::arg("ypart") = py::none(),
+        py::arg("out") = py::none());
+  m.def("big_yreduce", &big_yreduce, "y = sum of partials + b3 (+ dy, dy operand, squared error)",
+        py::arg("ypart"), py::arg("nparts"), py::arg("b3"), py::arg("y") = py::none(),
+        py::arg("target") = py::none(), py::arg("gscale") = 0.0, py::arg("dy") = py::none(),
+        py::arg("dyb") = py::none(), py::arg("sq_err") = py::none());
+  m.def("big_dz2", &big_dz2, "dz2 = dy * w3 * relu'(z2) from h2a (hperm order)");
+  m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad + input gradient (dz2, dh1 = dz2 W2)");
+  m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + training-blob re-pack");
+  m.def("eta_mlp3_train_blob_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_train_blob_bytes((int)H); });
   m.def("mlp3_num_params", [](int64_t H) { return (int64_t)rt::mlp3_num_params((int)H); });
   m.def("mlp3_grad_bucket_floats", [](int64_t H) { return (int64_t)rt::mlp3_grad_bucket_floats((int)H); });
   m.def("wgrad", &wgrad, "split-K weight-gradient GEMM (K = batch) into fp32 slabs",
         py::arg("A"), py::arg("M"), py::arg("Mout"), py::arg("Bm"), py::arg("N"), py::arg("slab"),
-        py::arg("offset"), py::arg("ldo"), py::arg("mask") = py::none(), py::arg("nout") = -1);
+        py::arg("offset"), py::arg("ldo"), py::arg("mask") = py::none(), py::arg("nout") = -1, py::arg("mask_hperm") = false);
   m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs");
   m.def("num_cus", [](int64_t dev) { return (int64_t)num_cus((int)dev); });
   m.def("gcn_agg_gemm", &gcn_agg_gemm, "K8: fused CSR aggregation + MFMA GEMM + bias/ReLU");

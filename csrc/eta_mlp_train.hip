@@ -4,27 +4,46 @@
 //
 // One training step on a rank (routest_amd/train/fused.py::FusedMlp3Trainer):
 //   1. eta_mlp3_train_fwd_kernel (this file): featurize + layer 1 + layer 2 + layer 3 + MSE
-//      gradient in ONE launch, same wave/tile structure and LDS-staged weight blob as inference.
-//      Because dL/dz2 = dy * w3 * relu'(z2) needs only the ReLU mask, dz2 is produced in-register
-//      the moment y (hence dy) is known — no second pass.  Emits, bf16 row-major:
+//      gradient + the input gradient dh1 = dz2 W2 in ONE launch (relu'(z1) is applied by the dW1
+//      wgrad kernel while it stages dh1: wgrad.hip MASK, mask columns in the hperm order).  Because dL/dz2 = dy * w3 * relu'(z2) needs only the ReLU mask, dz2 is produced
+//      in-register the moment y (hence dy) is known, and it IS the B operand of the dgrad MFMAs
+//      (accumulator layout == next-MFMA B layout, common.h); W2 is read a second time from the
+//      same LDS image through the hardware-transposed ds_read_b64_tr_b16 as the A operand W2^T,
+//      and h1 (still in registers) gives relu'(z1).  No library GEMM, no dh1 round trip through
+//      HBM.  Emits, bf16 row-major:
 //        xf  [B,16]   the exact bf16 features the MFMA consumed, slot 14 := 1 (bias-grad column)
 //        h1a [B,H+16] relu(z1) with column H := 1   (dW2 | db2 = dz2^T h1a)
 //        h2a [B,H+16] relu(z2) with column H := 1   (dW3 | db3 = dy^T h2a)
-//        dz2 [B,H], dy [B,8] (col 0; pre-scaled by 2 / global_batch), per-tile squared errors.
-//   2. dh1 = dz2 W2 on hipBLASLt (a plain [B,H]x[H,H] GEMM); the three weight-gradient GEMMs
-//      (K = batch) on the split-K wgrad kernel (wgrad.hip) + one deterministic slab reduction.
-//   3. relu_bwd_kernel: dz1 = dh1 * (h1 > 0).
-//   4. ONE flat fp32 gradient bucket -> one RCCL all-reduce over xGMI.
-//   5. adamw_pack_kernel: AdamW on the flat fp32 master params, writing back the bf16 fragment
-//      blob the next forward stages into LDS (and a row-major bf16 W2 for step 2) — no host work,
-//      no sync, so the whole step is capturable in a HIP graph.
+//        dz2 [B,H], dh1 [B,H] (natural unit order), dy [B,8] (col 0; pre-scaled by
+//        2 / global_batch), per-row squared errors.
+//      The kernel never reads back what it stored: a load waits for every older store of the wave
+//      (vmcnt counts both in order), which serialised each tile on its own store stream when the
+//      relu'(z1) mask was read back from h1a here (83 us vs 31 us for the whole kernel at 65k rows).
+//   2. the three weight-gradient GEMMs (K = batch) on the split-K wgrad kernel (wgrad.hip) + one
+//      deterministic slab reduction.
+//   3. ONE flat fp32 gradient bucket -> one RCCL all-reduce over xGMI.
+//   4. adamw_pack_kernel: AdamW on the flat fp32 master params, writing back the training blob the
+//      next forward stages into LDS — no host work, no sync, so the whole step is capturable in a
+//      HIP graph.
+//
+// Training blob (TrainLayout): [ w2img | w1p | b1p | b2p | w3p | tail ] where w2img holds W2
+// row-major in 512-byte rows (row = output unit o, natural order; column c = input unit hperm(c),
+// the stored activation order) with 16-byte chunk k of row R at chunk k ^ w2swz(R).  That one
+// image serves both operand reads conflict-free (bank rule, cdna_hip_programming.md §2 /
+// MI355X_MICROARCH.md §LDS):
+//   * layer 2, A = W2: lane (r, h) of tile (mt, ks) reads row 32mt + r, columns 16ks + 8h .. +7
+//     with ONE ds_read_b128 (w2swz is a bijection of R mod 16: each 16-lane group hits 16 slots);
+//   * dgrad, A = W2^T: ds_read_b64_tr_b16 over 4-row x 16-column blocks (rows 16ks + 4h + q and
+//     16ks + 8 + 4h + q, columns 32mi + 16g .. +15): w2swz moves the 4 rows of a block to 4
+//     different groups of 4 slots, so a 32-lane half touches 64 distinct banks.
+// The rest of the blob is the inference layout (mlp3_tile.h): w1p, b1p, b2p, w3p, tail.
 #include "mlp3_tile.h"
 #include "ops.h"
 
 namespace rt {
 
 // Stored hidden-unit order of the saved activations h1a / h2a / dz2 (and of the gradient bucket
-// and w2bf built from them): element j of fragment ks on lane half h is hidden unit
+// built from them): element j of fragment ks on lane half h is hidden unit
 // u = 16ks + 8(j>>2) + 4h + (j&3); storing it at column c = 16ks + 8h + j (= u with bits 2 and 3
 // swapped, an involution) makes each lane's 8 values ONE contiguous 16-byte store instead of two
 // 8-byte ones — the forward's activation writes went 42 -> 29 us at 65k rows.  adamw_pack_kernel
@@ -32,40 +51,74 @@ namespace rt {
 __host__ __device__ __forceinline__ int hperm(int u) { return (u & ~12) | ((u & 4) << 1) | ((u & 8) >> 1); }
 
 template <int H>
-__device__ __forceinline__ void store_act(__bf16* base_row, const bf16x8 (&a)[H / 16], int h) {
-#pragma unroll
-  for (int ks = 0; ks < H / 16; ++ks) *reinterpret_cast<bf16x8*>(base_row + 16 * ks + 8 * h) = a[ks];
+struct TrainLayout {
+  static constexpr int ROWB = 512;                       // bytes per W2 image row (256 slots)
+  static constexpr size_t W2B = (size_t)H * ROWB;
+  static constexpr size_t W1B = (size_t)H * 16 * 2;
+  static constexpr size_t VB = (size_t)H * 4;
+  static constexpr size_t BLOB = W2B + W1B + 3 * VB + 16;
+};
+
+size_t eta_mlp3_train_blob_bytes(int H) { return (size_t)H * 512 + 44 * (size_t)H + 16; }
+
+__host__ __device__ __forceinline__ int w2swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+// byte offset of image element (row, col) (col = stored column, i.e. input unit hperm(col))
+__host__ __device__ __forceinline__ int w2off(int row, int col) {
+  return row * 512 + (((col >> 3) ^ w2swz(row)) << 4) + 2 * (col & 7);
 }
 
-// 8 waves per workgroup (2 per SIMD; <= 256 VGPRs incl. register-resident W1 fragments).
-template <int H>
-constexpr int train_tpb() { return 512; }
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ bf16x8 join4(const s16x4 lo, const s16x4 hi) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// 8 waves per workgroup, 2 per SIMD (<= 256 VGPRs each).
+constexpr int TRAIN_TPB = 512;
 
 template <int H>
-__global__ __launch_bounds__(512, 2) void eta_mlp3_train_fwd_kernel(
+__global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     const int4* __restrict__ rec, const float* __restrict__ target, int B,
     const unsigned char* __restrict__ blob, NormParams np, float gscale, __bf16* __restrict__ xf,
     __bf16* __restrict__ h1a, __bf16* __restrict__ h2a, __bf16* __restrict__ dz2,
-    __bf16* __restrict__ dyb, float* __restrict__ loss_tiles, int* __restrict__ step_ctr) {
-  constexpr int MT = H / 32, KS = H / 16, LDA = H + 16;
+    __bf16* __restrict__ dh1, __bf16* __restrict__ dyb, float* __restrict__ sq_err,
+    int* __restrict__ step_ctr) {
+  using L = TrainLayout<H>;
+  constexpr int MT = H / 32, KS = H / 16, LDA = H + 16, D = KS < 4 ? KS : 4;
   // device-side optimizer step counter (read by adamw_pack_kernel later on the same stream), so a
   // captured HIP graph replays with correct bias corrections / LR schedule
   if (step_ctr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *step_ctr += 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  stage_blob<H>(blob, smem);
-  const Mlp3View<H> w(smem);
-  const float b3 = w.tail[0];
-  W1Frags<H> w1;
-  w1.load(w, threadIdx.x & 63);
+  {
+    const int4* src = reinterpret_cast<const int4*>(blob);
+    int4* dst = reinterpret_cast<int4*>(smem);
+    constexpr int N16 = (int)(L::BLOB / 16);
+    for (int i = threadIdx.x; i < N16; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+  }
+  const unsigned char* img = smem;
+  const bf16x8* w1p = reinterpret_cast<const bf16x8*>(smem + L::W2B);
+  const f32x4* b2p = reinterpret_cast<const f32x4*>(smem + L::W2B + L::W1B) + H / 4;
+  const f32x4* w3p = b2p + H / 4;
+  const float b3 = reinterpret_cast<const float*>(w3p + H / 4)[0];
 
   const int lane = threadIdx.x & 63;
-  const int h = lane >> 5;
-  const int r = lane & 31;
   const int wpb = blockDim.x >> 6;
   const int ntiles = (B + 31) >> 5;
   const int stride = gridDim.x * wpb;
 
   for (int tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntiles; tile += stride) {
+    // nothing is hoisted out of the tile loop: the LDS-resident weights (W1 fragments, biases)
+    // and the lane-derived LDS addresses are re-derived per tile.  Hoisted, they exceed the
+    // 256-VGPR budget and get spilled, and a scratch reload issued after the activation stores
+    // waits for all of them (vmcnt is in order) — which stalled every tile on its own stores.
+    __asm__ volatile("" ::: "memory");
+    int lv = lane;
+    __asm__ volatile("" : "+v"(lv));
+    const int r = lv & 31, h = lv >> 5;
     const int row = tile * 32 + r;
     const bool valid = row < B;
     const int4 rc = valid ? rec[row] : make_int4(0, 0, 0, 0);
@@ -73,12 +126,25 @@ __global__ __launch_bounds__(512, 2) void eta_mlp3_train_fwd_kernel(
     if (valid)  // slots 14, 15 hold 1.0 (the b1 hi/lo inputs): dW1k[:,14] == db1
       *reinterpret_cast<bf16x8*>(xf + (size_t)row * 16 + 8 * h) = xb;
 
+    // layer 1 (A fragments re-read from LDS per tile: no registers held across tiles)
     bf16x8 h1[KS];
-    mlp3_layer1<H>(w1, xb, h1);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      acc = mfma32(w1p[mt * 64 + lane], xb, acc);
+      float a[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) a[e] = acc[e];
+      relu_cvt_bf16x8(a, &h1[2 * mt]);
+      relu_cvt_bf16x8(a + 8, &h1[2 * mt + 1]);
+    }
     __bf16* h1row = h1a + (size_t)row * LDA;
     __bf16* h2row = h2a + (size_t)row * LDA;
     if (valid) {
-      store_act<H>(h1row, h1, h);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf16x8*>(h1row + 16 * ks + 8 * h) = h1[ks];
       bf16x8 tailv;
 #pragma unroll
       for (int j = 0; j < 8; ++j) tailv[j] = (__bf16)0.f;
@@ -88,28 +154,58 @@ __global__ __launch_bounds__(512, 2) void eta_mlp3_train_fwd_kernel(
     }
 
     // layer 2 + layer 3; relu(z2) goes straight to memory, only its mask stays in registers
-    unsigned long long mask_lo = 0, mask_hi = 0;   // 16 mask bits per 32-row hidden tile
+    unsigned long long mask_lo = 0, mask_hi = 0;   // 16 relu'(z2) bits per hidden tile
     float ys = 0.f;
-    mlp3_layer2<H>(w, h1, lane, h, [&](int mt, const f32x16& acc) {
-      const f32x16 w3 = load_vec16(w.w3p, mt, h);
-      unsigned mk = 0;
+    {
+      // addresses as lane bases + immediates (a run-time or fully hoisted w2off() per fragment
+      // costs VGPRs the compiler then spills — and a scratch reload after the activation stores
+      // would wait for all of them, vmcnt being in order): chunk (2ks + h) ^ w2swz(r) only
+      // depends on ks & 7, ks >> 3 adds 256 B
+      const int sw = w2swz(r);
+      const unsigned char* lrow = img + r * 512;
+      constexpr int NX = KS < 8 ? KS : 8;      // distinct ks & 7 patterns
+      int xk[NX];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 hv;
+      for (int k = 0; k < NX; ++k) xk[k] = 16 * ((2 * k + h) ^ sw);
+#pragma unroll 1
+      for (int mt = 0; mt < MT; ++mt) {
+        f32x16 acc = load_vec16(b2p, mt, h);
+        const unsigned char* pm = lrow + mt * 16384;
+        auto frag = [&](int ks) {
+          return *reinterpret_cast<const bf16x8*>(pm + xk[ks & 7] + 256 * (ks >> 3));
+        };
+        bf16x8 ring[D];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = relu_f(acc[8 * s + j]);
-          ys += v * w3[8 * s + j];
-          hv[j] = (__bf16)v;
-          mk |= (v > 0.f ? 1u : 0u) << (8 * s + j);
+        for (int d = 0; d < D; ++d) ring[d] = frag(d);
+#pragma unroll
+        for (int ks = 0; ks < KS; ks += D) {
+          bf16x8 a[D];
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            a[d] = ring[d];
+            if (ks + D + d < KS) ring[d] = frag(ks + D + d);
+          }
+#pragma unroll
+          for (int d = 0; d < D; ++d) acc = mfma32(a[d], h1[ks + d], acc);
         }
-        if (valid) {
-          *reinterpret_cast<bf16x8*>(h2row + 16 * (2 * mt + s) + 8 * h) = hv;   // hperm order
+        const f32x16 w3 = load_vec16(w3p, mt, h);
+        unsigned mk = 0;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 hv;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float v = relu_f(acc[8 * s + j]);
+            ys = __builtin_fmaf(v, w3[8 * s + j], ys);
+            hv[j] = (__bf16)v;
+            mk |= (v > 0.f ? 1u : 0u) << (8 * s + j);
+          }
+          if (valid) *reinterpret_cast<bf16x8*>(h2row + 16 * (2 * mt + s) + 8 * h) = hv;  // hperm order
         }
+        if (mt < 4) mask_lo |= (unsigned long long)mk << (16 * mt);
+        else mask_hi |= (unsigned long long)mk << (16 * (mt - 4));
       }
-      if (mt < 4) mask_lo |= (unsigned long long)mk << (16 * mt);
-      else mask_hi |= (unsigned long long)mk << (16 * (mt - 4));
-    });
+    }
     ys += __shfl_xor(ys, 32);
     const float y = ys + b3;
     const float diff = valid ? (y - target[row]) : 0.f;
@@ -121,47 +217,80 @@ __global__ __launch_bounds__(512, 2) void eta_mlp3_train_fwd_kernel(
       dv[0] = (__bf16)dy;
       *reinterpret_cast<bf16x8*>(dyb + (size_t)row * 8) = dv;
     }
-    // per-tile squared error (h = 0 half only), wave reduction
-    float l = (h == 0) ? diff * diff : 0.f;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) l += __shfl_xor(l, o);
-    if (lane == 0) loss_tiles[tile] = l;
+    // per-row squared error (no cross-lane reduction: its shuffle addresses were the values the
+    // compiler spilled, and every reload after the activation stores waited for all of them)
+    if (valid && h == 0) sq_err[row] = diff * diff;
 
-    // dz2 = dy * w3 * relu'(z2), in fragment order, stored row-major
+    // dz2 = dy * w3 * relu'(z2): fragment 2mt + s element j is accumulator register 8s + j of
+    // hidden tile mt, i.e. exactly the B-operand k order of the dgrad MFMAs below
+    bf16x8 dz2f[KS];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const f32x16 w3 = load_vec16(w3p, mt, h);
+      const unsigned mk = (unsigned)((mt < 4 ? mask_lo >> (16 * mt) : mask_hi >> (16 * (mt - 4))) & 0xffffu);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 d;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          d[j] = (__bf16)(((mk >> (8 * s + j)) & 1u) ? dy * w3[8 * s + j] : 0.f);
+        dz2f[2 * mt + s] = d;
+      }
+    }
     if (valid) {
       __bf16* drow = dz2 + (size_t)row * H;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf16x8*>(drow + 16 * ks + 8 * h) = dz2f[ks];
+    }
+
+    // dgrad: dh1^T tile mi = W2^T[stored cols 32mi.., :] dz2^T.  Accumulator register e is
+    // stored column c = 32mi + (e&3) + 8(e>>2) + 4h, i.e. input unit hperm(c) =
+    // 32mi + 16(e>>3) + 8h + (e&7): dh1 is written in NATURAL unit order, two 16-byte runs per lane.
+    {
+      __bf16* zrow = dh1 + (size_t)row * H;
+      // transposed-read addresses (w2_tr_frag) as two lane bases per tile mi + immediates:
+      // row 16ks + 8t + 4h + q -> +8192 ks; chunk (4mi + 2(g&1) + (p>>1)) ^ (4q + 2t + h)
+      const int g1 = (lv >> 4) & 1, p = lv & 3, q = (lv >> 2) & 3;
+      const unsigned char* rb = img + (4 * h + q) * 512 + 8 * (p & 1);
 #pragma unroll 1
-      for (int mt = 0; mt < MT; ++mt) {
-        const f32x16 w3 = load_vec16(w.w3p, mt, h);
-        const unsigned mk = (unsigned)((mt < 4 ? mask_lo >> (16 * mt) : mask_hi >> (16 * (mt - 4))) & 0xffffu);
+      for (int mi = 0; mi < MT; ++mi) {
+        const int cc = 4 * (mi & 3) + 2 * g1 + (p >> 1);
+        const unsigned char* b0 = rb + 16 * (cc ^ (4 * q + h)) + 256 * (mi >> 2);
+        const unsigned char* b1 = rb + 4096 + 16 * (cc ^ (4 * q + 2 + h)) + 256 * (mi >> 2);
+        auto frag = [&](int ks) {
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(const_cast<unsigned char*>(b0) + 8192 * ks));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(const_cast<unsigned char*>(b1) + 8192 * ks));
+          return join4(lo, hi);
+        };
+        f32x16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+        bf16x8 ring[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) ring[d] = frag(d);
+#pragma unroll
+        for (int ks = 0; ks < KS; ks += D) {
+          bf16x8 a[D];
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            a[d] = ring[d];
+            if (ks + D + d < KS) ring[d] = frag(ks + D + d);
+          }
+#pragma unroll
+          for (int d = 0; d < D; ++d) acc = mfma32(a[d], dz2f[ks + d], acc);
+        }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          bf16x8 d;
+          bf16x8 o;
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            d[j] = (__bf16)(((mk >> (8 * s + j)) & 1u) ? dy * w3[8 * s + j] : 0.f);
-          *reinterpret_cast<bf16x8*>(drow + 16 * (2 * mt + s) + 8 * h) = d;     // hperm order
+          for (int j = 0; j < 8; ++j) o[j] = (__bf16)acc[8 * s + j];
+          if (valid) *reinterpret_cast<bf16x8*>(zrow + 32 * mi + 16 * s + 8 * h) = o;   // natural order
         }
       }
     }
   }
-}
-
-// dz1[b][o] = dh1[b][o] * (h1a[b][o] > 0), 8 bf16 per thread.
-__global__ __launch_bounds__(256) void relu_bwd_kernel(const __bf16* __restrict__ dh1,
-                                                       const __bf16* __restrict__ h1a, int lda,
-                                                       __bf16* __restrict__ dz1, int B, int H) {
-  const long long i8 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int per_row = H / 8;
-  if (i8 >= (long long)B * per_row) return;
-  const long long b = i8 / per_row;
-  const int c = (int)(i8 - b * per_row) * 8;
-  const bf16x8 g = *reinterpret_cast<const bf16x8*>(dh1 + b * H + c);
-  const bf16x8 a = *reinterpret_cast<const bf16x8*>(h1a + b * lda + c);
-  bf16x8 o;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (float)a[j] > 0.f ? g[j] : (__bf16)0.f;
-  *reinterpret_cast<bf16x8*>(dz1 + b * H + c) = o;
 }
 
 // Flat parameter layout (fp32 master): W1[H][12] | b1[H] | W2[H][H] | b2[H] | w3[H] | b3
@@ -189,17 +318,15 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
                                                          const float* __restrict__ G,
                                                          float* __restrict__ M, float* __restrict__ V,
                                                          unsigned char* __restrict__ blob,
-                                                         __bf16* __restrict__ w2bf,
                                                          const int* __restrict__ step, AdamWArgs a) {
-  using L = Mlp3Layout<H>;
-  constexpr int KS = H / 16;
+  using L = TrainLayout<H>;
   constexpr int OFF_B1 = 12 * H, OFF_W2 = 13 * H, OFF_B2 = 13 * H + H * H, OFF_W3 = OFF_B2 + H,
                 OFF_B3 = OFF_W3 + H, N = OFF_B3 + 1;
   constexpr int LDG = H + 16;
   const float* gW2a = G;
   const float* gW3a = G + H * LDG;
   const float* gW1a = gW3a + LDG;
-  __bf16* w2p = reinterpret_cast<__bf16*>(blob);
+  unsigned char* w2img = blob;
   __bf16* w1p = reinterpret_cast<__bf16*>(blob + L::W2B);
   float* b1p = reinterpret_cast<float*>(blob + L::W2B + L::W1B);
   float* b2p = b1p + H;
@@ -214,14 +341,13 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
   if (e < OFF_B1) {
     o = e / 12;
     i = e - o * 12;
-    const int po = hperm(o);
-    g = gW1a[po * 16 + i];
-    if (i == 10) g += gW1a[po * 16 + 12];
-    if (i == 11) g += gW1a[po * 16 + 13];
+    g = gW1a[o * 16 + i];                 // dW1 rows in natural unit order (dh1 is stored so)
+    if (i == 10) g += gW1a[o * 16 + 12];
+    if (i == 11) g += gW1a[o * 16 + 13];
     decay = true;
   } else if (e < OFF_W2) {
     o = e - OFF_B1;
-    g = gW1a[hperm(o) * 16 + 14];
+    g = gW1a[o * 16 + 14];
   } else if (e < OFF_B2) {
     const int k = e - OFF_W2;
     o = k / H;
@@ -263,13 +389,7 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
     if (i == 10) put(12);
     if (i == 11) put(13);
   } else if (e >= OFF_W2 && e < OFF_B2) {
-    const int mt = o >> 5, rr = o & 31;
-    const int ks = i >> 4, c = i & 15;
-    const int hh = (c >> 2) & 1;
-    const int j = 4 * (c >> 3) + (c & 3);
-    const int ln = rr + 32 * hh;
-    w2p[((size_t)((mt * KS + ks) * 64 + ln)) * 8 + j] = (__bf16)p;
-    w2bf[(size_t)hperm(o) * H + hperm(i)] = (__bf16)p;   // rows/cols in the stored (hperm) order
+    *reinterpret_cast<__bf16*>(w2img + w2off(o, hperm(i))) = (__bf16)p;   // rows natural, cols hperm
   } else if (e < OFF_B3) {
     const int mt = o >> 5, rr = o & 31;
     const int hh = (rr >> 2) & 1;
@@ -291,9 +411,9 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
 template <int H>
 static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B, const void* blob,
                                      const NormParams& np, float gscale, void* xf, void* h1a,
-                                     void* h2a, void* dz2, void* dyb, float* loss_tiles,
+                                     void* h2a, void* dz2, void* dh1, void* dyb, float* sq_err,
                                      int* step_ctr, int num_cus, hipStream_t stream) {
-  using L = Mlp3Layout<H>;
+  using L = TrainLayout<H>;
   static bool attr_set[64] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -304,43 +424,34 @@ static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B
     attr_set[dev & 63] = true;
   }
   const int ntiles = (B + 31) / 32;
-  constexpr int TPB = train_tpb<H>();
+  constexpr int TPB = TRAIN_TPB;
   int grid = (ntiles + TPB / 64 - 1) / (TPB / 64);
   if (grid > num_cus) grid = num_cus;
   if (grid < 1) return hipSuccess;
   hipLaunchKernelGGL(eta_mlp3_train_fwd_kernel<H>, dim3(grid), dim3(TPB), L::BLOB, stream,
                      (const int4*)rec, target, B, (const unsigned char*)blob, np, gscale,
-                     (__bf16*)xf, (__bf16*)h1a, (__bf16*)h2a, (__bf16*)dz2, (__bf16*)dyb,
-                     loss_tiles, step_ctr);
+                     (__bf16*)xf, (__bf16*)h1a, (__bf16*)h2a, (__bf16*)dz2, (__bf16*)dh1,
+                     (__bf16*)dyb, sq_err, step_ctr);
   return hipGetLastError();
 }
 
 hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B, const void* blob,
                                      int H, const NormParams& np, float gscale, void* xf,
-                                     void* h1a, void* h2a, void* dz2, void* dyb,
-                                     float* loss_tiles, int* step_ctr, int num_cus,
+                                     void* h1a, void* h2a, void* dz2, void* dh1, void* dyb,
+                                     float* sq_err, int* step_ctr, int num_cus,
                                      hipStream_t stream) {
   switch (H) {
-    case 64: return launch_train_fwd_h<64>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dyb, loss_tiles, step_ctr, num_cus, stream);
-    case 128: return launch_train_fwd_h<128>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dyb, loss_tiles, step_ctr, num_cus, stream);
-    case 256: return launch_train_fwd_h<256>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dyb, loss_tiles, step_ctr, num_cus, stream);
+    case 64: return launch_train_fwd_h<64>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dh1, dyb, sq_err, step_ctr, num_cus, stream);
+    case 128: return launch_train_fwd_h<128>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dh1, dyb, sq_err, step_ctr, num_cus, stream);
+    case 256: return launch_train_fwd_h<256>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dh1, dyb, sq_err, step_ctr, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
-}
-
-hipError_t launch_relu_bwd(const void* dh1, const void* h1a, int lda, void* dz1, int B, int H,
-                           hipStream_t stream) {
-  const long long n = (long long)B * (H / 8);
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                     (const __bf16*)dh1, (const __bf16*)h1a, lda, (__bf16*)dz1, B, H);
-  return hipGetLastError();
 }
 
 int mlp3_num_params(int H) { return H * H + 15 * H + 1; }
 int mlp3_grad_bucket_floats(int H) { return H * (H + 16) + (H + 16) + 16 * H; }
 
-hipError_t launch_adamw_pack(float* P, const float* G, float* M, float* V, void* blob, void* w2bf,
+hipError_t launch_adamw_pack(float* P, const float* G, float* M, float* V, void* blob,
                              const int* step, int H, float lr, float beta1, float beta2, float eps,
                              float wd, int warmup, int total_steps, float min_lr_ratio, int update,
                              hipStream_t stream) {
@@ -348,9 +459,9 @@ hipError_t launch_adamw_pack(float* P, const float* G, float* M, float* V, void*
   const int N = mlp3_num_params(H);
   const dim3 grid((N + 255) / 256), block(256);
   switch (H) {
-    case 64: hipLaunchKernelGGL(adamw_pack_kernel<64>, grid, block, 0, stream, P, G, M, V, (unsigned char*)blob, (__bf16*)w2bf, step, a); break;
-    case 128: hipLaunchKernelGGL(adamw_pack_kernel<128>, grid, block, 0, stream, P, G, M, V, (unsigned char*)blob, (__bf16*)w2bf, step, a); break;
-    case 256: hipLaunchKernelGGL(adamw_pack_kernel<256>, grid, block, 0, stream, P, G, M, V, (unsigned char*)blob, (__bf16*)w2bf, step, a); break;
+    case 64: hipLaunchKernelGGL(adamw_pack_kernel<64>, grid, block, 0, stream, P, G, M, V, (unsigned char*)blob, step, a); break;
+    case 128: hipLaunchKernelGGL(adamw_pack_kernel<128>, grid, block, 0, stream, P, G, M, V, (unsigned char*)blob, step, a); break;
+    case 256: hipLaunchKernelGGL(adamw_pack_kernel<256>, grid, block, 0, stream, P, G, M, V, (unsigned char*)blob, step, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

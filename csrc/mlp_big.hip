@@ -1,0 +1,339 @@
+// Wide ETA MLPs (H = 512, 1024): the layer-2 GEMM no longer fits LDS, so W2 streams from L2
+// through double-buffered LDS tiles (the "L2-streamed" path; SURVEY C1 sizes the DP bucket for
+// H = 1024; the reference artifact is a 2.44 MB model, RO/xgb_eta_model.pkl:1-3).
+//
+//   big_layer1_kernel  : records -> featurize -> layer 1 (MFMA 32x32x16, W1k fragments from L2)
+//                        -> h1 bf16 [B, ld] in the hperm() unit order (16-byte stores); training
+//                        also writes xf and the h1a ones-column.
+//   gemm_nt_kernel     : D = W^T-side GEMM  Z^T[n][m] = sum_k W[n][k] X[m][k]  (both operands
+//                        row-major with K contiguous, bf16, fp32 accumulate), 128 x 128 tiles,
+//                        4 waves of 64 x 64, K in 32-deep stages through LDS (16-byte row reads,
+//                        XOR-swizzled chunks: conflict-free), batch on the lane so every epilogue
+//                        reduction over hidden units stays in-lane:
+//      EPI_Y    (inference): relu(z + b2) . w3 -> per-(row, 64-unit block) partial sums
+//      EPI_H2Y  (training) : same + relu(z + b2) stored bf16 (hperm order) into h2a
+//      EPI_STORE(dgrad)    : z stored bf16 (hperm order)
+//   big_yreduce_kernel : y = sum of partials + b3 (inference) | + dy, dy operand, squared error
+//                        (training)
+//   big_dz2_kernel     : dz2 = dy * w3 * relu'(z2) from h2a (training)
+//
+// Weight layouts (host: routest_amd/ops/mlp_big.py; training: adamw_pack_big_kernel):
+//   w1p [H/32][64 lanes][8] bf16 (as mlp3_tile.h), w2k [H][H] bf16 row-major with K columns in
+//   hperm order (w2k[n][c] = W2[n][hperm(c)]), w2t [H][H] bf16 row-major = W2^T with K (output
+//   unit) columns in hperm order (training only), b2 / w3 f32 in natural order.
+#include "common.h"
+#include "ops.h"
+
+namespace rt {
+
+namespace {
+
+__host__ __device__ __forceinline__ int hp(int u) { return (u & ~12) | ((u & 4) << 1) | ((u & 8) >> 1); }
+
+template <int RB>
+struct BigRec;
+template <>
+struct BigRec<16> {
+  static __device__ __forceinline__ bf16x8 feat(const void* p, int row, int h, const NormParams& np) {
+    return featurize_bf16(reinterpret_cast<const int4*>(p)[row], h, np);
+  }
+};
+template <>
+struct BigRec<8> {
+  static __device__ __forceinline__ bf16x8 feat(const void* p, int row, int h, const NormParams& np) {
+    return featurize8_bf16(reinterpret_cast<const int2*>(p)[row], h, np);
+  }
+};
+template <>
+struct BigRec<6> {
+  static __device__ __forceinline__ bf16x8 feat(const void* p, int row, int h, const NormParams& np) {
+    const unsigned short* s = reinterpret_cast<const unsigned short*>(p) + 3 * (size_t)row;
+    return featurize6_bf16((unsigned)s[0] | ((unsigned)s[1] << 16), s[2], h, np);
+  }
+};
+
+// One wave per 32-row tile: lane (r, h) featurizes row r's half h, H/32 MFMAs, relu, bf16,
+// stored as 16-byte chunks at hperm positions 16ks + 8h (= the MFMA B-fragment order).
+template <int RB>
+__global__ __launch_bounds__(256) void big_layer1_kernel(const void* __restrict__ rec, int B,
+                                                         const bf16x8* __restrict__ w1p, int H,
+                                                         NormParams np, __bf16* __restrict__ h1,
+                                                         int ld, __bf16* __restrict__ xf) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = tile * 32 + r;
+  if (tile * 32 >= B) return;                                   // whole wave leaves together
+  const bool valid = row < B;
+  bf16x8 xb;
+  if (valid) {
+    xb = BigRec<RB>::feat(rec, row, h, np);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xb[j] = (__bf16)0.f;
+  }
+  if (xf != nullptr && valid) *reinterpret_cast<bf16x8*>(xf + (size_t)row * 16 + 8 * h) = xb;
+  __bf16* out = h1 + (size_t)row * ld;
+  for (int mt = 0; mt < H / 32; ++mt) {
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    acc = mfma32(w1p[mt * 64 + lane], xb, acc);
+    float a[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) a[e] = acc[e];
+    bf16x8 v0, v1;
+    relu_cvt_bf16x8(a, &v0);
+    relu_cvt_bf16x8(a + 8, &v1);
+    if (valid) {
+      *reinterpret_cast<bf16x8*>(out + 32 * mt + 8 * h) = v0;
+      *reinterpret_cast<bf16x8*>(out + 32 * mt + 16 + 8 * h) = v1;
+    }
+  }
+  if (xf != nullptr && valid && ld > H) {                       // h1a ones-column (db2 input)
+    bf16x8 t;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = (__bf16)0.f;
+    if (h == 0) t[0] = (__bf16)1.f;
+    *reinterpret_cast<bf16x8*>(out + H + 8 * h) = t;
+  }
+}
+
+constexpr int GT = 128;          // tile rows (units) and columns (batch rows)
+constexpr int GK = 32;           // K per LDS stage
+constexpr int EPI_Y = 0, EPI_H2Y = 1, EPI_STORE = 2;
+
+// LDS tile: 128 rows x 64 bytes; 16-byte chunk c of row r at slot c ^ ((r >> 2) & 3) — the 16
+// rows a ds_read_b128 lane group reads (lanes {0-3,12-15,20-27} etc.) hit 16 distinct slots.
+__device__ __forceinline__ int toff(int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 3)) << 4); }
+
+struct GemmArgs {
+  const __bf16* W;   // [N][ldw]  MFMA A side (output units)
+  const __bf16* X;   // [M][ldx]  MFMA B side (batch rows)
+  int ldw, ldx, N, M, K;
+  const float* b2;   // EPI_Y / EPI_H2Y: bias per unit (natural order)
+  const float* w3;   //                 layer-3 weights per unit
+  float* ypart;      //                 [M][N/64] partial dots
+  __bf16* out;       // EPI_H2Y: h2a, EPI_STORE: output; [M][ldo], unit n at hperm position
+  int ldo;
+  int tiles_n;       // N / 128
+};
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char sm[2][2][GT * GK * 2];   // [stage][W|X]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // XCD-aware tile order: hardware round-robins consecutive workgroups over the 8 XCDs; remap
+  // so that the tiles_n column blocks of one batch tile run on ONE XCD (its X tile stays in that
+  // XCD's L2) — only when the grid divides evenly
+  int bid = blockIdx.x;
+  const int nb = gridDim.x;
+  if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
+  const int tn = bid % a.tiles_n, tm = bid / a.tiles_n;
+  const int n0 = tn * GT, m0 = tm * GT;
+  const int wn = w & 1, wm = w >> 1;        // wave: units [64wn, +64) x batch [64wm, +64)
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // global -> register staging: each thread moves 2 chunks of W and 2 of X per stage (rows of
+  // X past M are clamped to row M-1: their products land in columns that are never stored)
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  i32x4 rw[2], rx[2];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * u, r = c >> 2, ch = c & 3;
+      rw[u] = *reinterpret_cast<const i32x4*>(a.W + (size_t)(n0 + r) * a.ldw + k0 + 8 * ch);
+      const int mr = min(m0 + r, a.M - 1);
+      rx[u] = *reinterpret_cast<const i32x4*>(a.X + (size_t)mr * a.ldx + k0 + 8 * ch);
+    }
+  };
+  auto lstore = [&](int s) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * u, r = c >> 2, ch = c & 3;
+      *reinterpret_cast<i32x4*>(&sm[s][0][toff(r, ch)]) = rw[u];
+      *reinterpret_cast<i32x4*>(&sm[s][1][toff(r, ch)]) = rx[u];
+    }
+  };
+  const int nk = a.K / GK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int s = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * GK);          // in flight under this stage's MFMAs
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = 2 * ks + (lane >> 5);
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        fa[i] = *reinterpret_cast<const bf16x8*>(&sm[s][0][toff(64 * wn + 32 * i + (lane & 31), ch)]);
+        fb[i] = *reinterpret_cast<const bf16x8*>(&sm[s][1][toff(64 * wm + 32 * i + (lane & 31), ch)]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) {
+      lstore(s ^ 1);                                   // the other buffer: consumed last stage
+      __syncthreads();
+    }
+  }
+
+  // epilogue: acc[i][j] = Z^T[units 64wn + 32i + (e&3) + 8(e>>2) + 4h][batch 64wm + 32j + (l&31)]
+  const int h = lane >> 5, col = lane & 31;
+  if constexpr (EPI == EPI_STORE) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m = m0 + 64 * wm + 32 * j + col;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ub = n0 + 64 * wn + 32 * i;
+        // registers 0-7 are units ub + 4h + {0..3}, ub + 8 + 4h + {0..3}: hperm positions
+        // ub + 8h + {0..7}; registers 8-15 the same +16
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 o;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] = (__bf16)acc[i][j][8 * s2 + q];
+          *reinterpret_cast<bf16x8*>(a.out + (size_t)m * a.ldo + ub + 16 * s2 + 8 * h) = o;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m = m0 + 64 * wm + 32 * j + col;
+      float ys = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ub = n0 + 64 * wn + 32 * i;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 o;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int e = 8 * s2 + q;
+            const int u = ub + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const float v = relu_f(acc[i][j][e] + a.b2[u]);
+            ys = __builtin_fmaf(v, a.w3[u], ys);
+            o[q] = (__bf16)v;
+          }
+          if constexpr (EPI == EPI_H2Y) {
+            if (m < a.M) *reinterpret_cast<bf16x8*>(a.out + (size_t)m * a.ldo + ub + 16 * s2 + 8 * h) = o;
+          }
+        }
+      }
+      ys += __shfl_xor(ys, 32);
+      if (h == 0 && m < a.M) a.ypart[(size_t)m * (a.N / 64) + (n0 >> 6) + wn] = ys;
+    }
+  }
+}
+
+// y = sum_j ypart[m][j] + b3 (fixed order: deterministic).  Training (target != null): dy, the
+// bf16 dy operand [B,8] (col 0), squared error.
+__global__ __launch_bounds__(256) void big_yreduce_kernel(const float* __restrict__ ypart, int nparts,
+                                                          int B, float b3, float* __restrict__ y,
+                                                          const float* __restrict__ target,
+                                                          float gscale, float* __restrict__ dy,
+                                                          __bf16* __restrict__ dyb,
+                                                          float* __restrict__ sq_err) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= B) return;
+  const float* p = ypart + (size_t)m * nparts;
+  float s = 0.f;
+  for (int j = 0; j < nparts; ++j) s += p[j];
+  const float yy = s + b3;
+  if (y != nullptr) y[m] = yy;
+  if (target != nullptr) {
+    const float diff = yy - target[m];
+    const float d = gscale * diff;
+    dy[m] = d;
+    sq_err[m] = diff * diff;
+    bf16x8 dv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dv[j] = (__bf16)0.f;
+    dv[0] = (__bf16)d;
+    *reinterpret_cast<bf16x8*>(dyb + (size_t)m * 8) = dv;
+  }
+}
+
+// dz2[m][c] = dy[m] * w3[hperm(c)] * (h2a[m][c] > 0), 8 columns per thread (hperm order both).
+__global__ __launch_bounds__(256) void big_dz2_kernel(const __bf16* __restrict__ h2a, int lda,
+                                                      const float* __restrict__ dy,
+                                                      const float* __restrict__ w3, int B, int H,
+                                                      __bf16* __restrict__ dz2) {
+  const long long i8 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = H / 8;
+  if (i8 >= (long long)B * per) return;
+  const long long m = i8 / per;
+  const int c = (int)(i8 - m * per) * 8;
+  const bf16x8 hv = *reinterpret_cast<const bf16x8*>(h2a + m * lda + c);
+  const float d = dy[m];
+  bf16x8 o;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = (__bf16)(((float)hv[q] > 0.f) ? d * w3[hp(c + q)] : 0.f);
+  *reinterpret_cast<bf16x8*>(dz2 + m * H + c) = o;
+}
+
+}  // namespace
+
+hipError_t launch_big_layer1(const void* rec, int rec_bytes, int B, const void* w1p, int H,
+                             const NormParams& np, void* h1, int ld, void* xf, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  if (H % 32 || ld % 8) return hipErrorInvalidValue;
+  const int tiles = (B + 31) / 32;
+  const dim3 grid((tiles + 3) / 4), block(256);
+  switch (rec_bytes) {
+    case 16: hipLaunchKernelGGL(big_layer1_kernel<16>, grid, block, 0, stream, rec, B, (const bf16x8*)w1p, H, np, (__bf16*)h1, ld, (__bf16*)xf); break;
+    case 8: hipLaunchKernelGGL(big_layer1_kernel<8>, grid, block, 0, stream, rec, B, (const bf16x8*)w1p, H, np, (__bf16*)h1, ld, (__bf16*)xf); break;
+    case 6: hipLaunchKernelGGL(big_layer1_kernel<6>, grid, block, 0, stream, rec, B, (const bf16x8*)w1p, H, np, (__bf16*)h1, ld, (__bf16*)xf); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm_nt(int epi, const void* W, int ldw, const void* X, int ldx, int N, int M,
+                          int K, const float* b2, const float* w3, float* ypart, void* out,
+                          int ldo, hipStream_t stream) {
+  if (M <= 0) return hipSuccess;
+  if (N % GT || K % GK || ldw % 8 || ldx % 8 || (out != nullptr && ldo % 8)) return hipErrorInvalidValue;
+  GemmArgs a{(const __bf16*)W, (const __bf16*)X, ldw, ldx, N, M, K, b2, w3, ypart, (__bf16*)out, ldo, N / GT};
+  const dim3 grid((unsigned)((N / GT) * ((M + GT - 1) / GT))), block(256);
+  switch (epi) {
+    case EPI_Y: hipLaunchKernelGGL(gemm_nt_kernel<EPI_Y>, grid, block, 0, stream, a); break;
+    case EPI_H2Y: hipLaunchKernelGGL(gemm_nt_kernel<EPI_H2Y>, grid, block, 0, stream, a); break;
+    case EPI_STORE: hipLaunchKernelGGL(gemm_nt_kernel<EPI_STORE>, grid, block, 0, stream, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_big_yreduce(const float* ypart, int nparts, int B, float b3, float* y,
+                              const float* target, float gscale, float* dy, void* dyb, float* sq_err,
+                              hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(big_yreduce_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, ypart, nparts, B,
+                     b3, y, target, gscale, dy, (__bf16*)dyb, sq_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_big_dz2(const void* h2a, int lda, const float* dy, const float* w3, int B, int H,
+                          void* dz2, hipStream_t stream) {
+  const long long n = (long long)B * (H / 8);
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(big_dz2_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     (const __bf16*)h2a, lda, dy, w3, B, H, (__bf16*)dz2);
+  return hipGetLastError();
+}
+
+}  // namespace rt

@@ -27,22 +27,34 @@ hipError_t launch_eta_featurize(const void* rec, float* out, int B, hipStream_t 
 // ---- ETA MLP training (K3) : eta_mlp_train.hip ----
 hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B, const void* blob,
                                      int H, const NormParams& np, float gscale, void* xf,
-                                     void* h1a, void* h2a, void* dz2, void* dyb,
-                                     float* loss_tiles, int* step_ctr, int num_cus,
+                                     void* h1a, void* h2a, void* dz2, void* dz1, void* dyb,
+                                     float* sq_err, int* step_ctr, int num_cus,
                                      hipStream_t stream);
-hipError_t launch_relu_bwd(const void* dh1, const void* h1a, int lda, void* dz1, int B, int H,
-                           hipStream_t stream);
+size_t eta_mlp3_train_blob_bytes(int H);
 int mlp3_num_params(int H);
 int mlp3_grad_bucket_floats(int H);
-hipError_t launch_adamw_pack(float* P, const float* G, float* M, float* V, void* blob, void* w2bf,
+hipError_t launch_adamw_pack(float* P, const float* G, float* M, float* V, void* blob,
                              const int* step, int H, float lr, float beta1, float beta2, float eps,
                              float wd, int warmup, int total_steps, float min_lr_ratio, int update,
                              hipStream_t stream);
 
+// ---- wide MLPs (H = 512, 1024): mlp_big.hip ----
+hipError_t launch_big_layer1(const void* rec, int rec_bytes, int B, const void* w1p, int H,
+                             const NormParams& np, void* h1, int ld, void* xf, hipStream_t stream);
+hipError_t launch_gemm_nt(int epi, const void* W, int ldw, const void* X, int ldx, int N, int M,
+                          int K, const float* b2, const float* w3, float* ypart, void* out,
+                          int ldo, hipStream_t stream);
+hipError_t launch_big_yreduce(const float* ypart, int nparts, int B, float b3, float* y,
+                              const float* target, float gscale, float* dy, void* dyb, float* sq_err,
+                              hipStream_t stream);
+hipError_t launch_big_dz2(const void* h2a, int lda, const float* dy, const float* w3, int B, int H,
+                          void* dz2, hipStream_t stream);
+
 // ---- weight-gradient GEMMs with K = batch : wgrad.hip ----
 hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm, int ldb, int N,
                         int K, int S, float* slab, int ldo, long long slab_stride, hipStream_t stream,
-                        const void* mask = nullptr, int ldm = 0, int Nout = -1);
+                        const void* mask = nullptr, int ldm = 0, int Nout = -1,
+                        bool mask_hperm = false);
 hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, float* G, int n,
                                hipStream_t stream);
 size_t wgrad_lds_bytes(int NT);

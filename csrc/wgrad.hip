@@ -60,7 +60,10 @@ __device__ __forceinline__ int relu_mask_word(int a, int m) {
 
 // MASK: A_eff = A * (mask > 0) applied while staging (mask has A's shape, leading dim ldm) — fuses
 // the ReLU backward of the first layer into dW1 = dz1^T x, so dz1 is never materialised.
-template <int NT, bool MASK, int KB>
+// MPERM: the mask's columns are in the trainer's hperm() unit order (h1a) while A's are natural
+// (dh1): the 8 mask values of A columns m..m+7 (m % 8 == 0) are the two 8-byte runs at
+// p0 = (m & ~15) + 4 * ((m >> 3) & 1) and p0 + 8.
+template <int NT, bool MASK, int KB, bool MPERM = false>
 __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict__ A, int lda, int M,
                                                        int Mout, const __bf16* __restrict__ Bm,
                                                        int ldb, int N, int K, int kslice,
@@ -100,7 +103,15 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
                   ? *reinterpret_cast<const int4*>(A + (size_t)k * lda + m) : make_int4(0, 0, 0, 0);
       if constexpr (MASK) {
         if (c < KB * ACH && k < k_end && m < M) {
-          const int4 mk = *reinterpret_cast<const int4*>(mask + (size_t)k * ldm + m);
+          int4 mk;
+          if constexpr (MPERM) {
+            const __bf16* mp = mask + (size_t)k * ldm + (m & ~15) + 4 * ((m >> 3) & 1);
+            const int2 lo = *reinterpret_cast<const int2*>(mp);
+            const int2 hi = *reinterpret_cast<const int2*>(mp + 8);
+            mk = make_int4(lo.x, lo.y, hi.x, hi.y);
+          } else {
+            mk = *reinterpret_cast<const int4*>(mask + (size_t)k * ldm + m);
+          }
           ra[u].x = relu_mask_word(ra[u].x, mk.x);
           ra[u].y = relu_mask_word(ra[u].y, mk.y);
           ra[u].z = relu_mask_word(ra[u].z, mk.z);
@@ -247,7 +258,7 @@ static int wgrad_kb() {
   return kb;
 }
 
-template <int NT, bool MASK, int KB>
+template <int NT, bool MASK, int KB, bool MPERM = false>
 static hipError_t launch_wgrad_kb(const void* A, int lda, int M, int Mout, const void* Bm, int ldb,
                                   int N, int K, int S, float* slab, int ldo, long long slab_stride,
                                   hipStream_t stream, const void* mask, int ldm, int Nout) {
@@ -255,11 +266,11 @@ static hipError_t launch_wgrad_kb(const void* A, int lda, int M, int Mout, const
   const int mblocks = (M + 255) / 256;
   const size_t lds = wgrad_lds_bytes(NT, KB);
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)wgrad_kernel<NT, MASK, KB>,
+    hipError_t e = hipFuncSetAttribute((const void*)wgrad_kernel<NT, MASK, KB, MPERM>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((wgrad_kernel<NT, MASK, KB>), dim3(S, mblocks), dim3(512), lds, stream,
+  hipLaunchKernelGGL((wgrad_kernel<NT, MASK, KB, MPERM>), dim3(S, mblocks), dim3(512), lds, stream,
                      (const __bf16*)A, lda, M, Mout, (const __bf16*)Bm, ldb, N, K, kslice, slab, ldo,
                      slab_stride, (const __bf16*)mask, ldm, Nout);
   return hipGetLastError();
@@ -280,12 +291,17 @@ static hipError_t launch_wgrad_nt(const void* A, int lda, int M, int Mout, const
 
 hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm, int ldb, int N,
                         int K, int S, float* slab, int ldo, long long slab_stride,
-                        hipStream_t stream, const void* mask, int ldm, int Nout) {
+                        hipStream_t stream, const void* mask, int ldm, int Nout, bool mask_hperm) {
   if (M % 8 || N % 8 || lda % 8 || ldb % 8) return hipErrorInvalidValue;
   if (Nout < 0 || Nout > N) Nout = N;
   const int NT = (N + 31) / 32;
   if (mask != nullptr) {
     if (ldm % 8 || NT != 1) return hipErrorInvalidValue;   // the dW1 shape (N = 16)
+    if (mask_hperm) {
+      if (M % 16) return hipErrorInvalidValue;
+      return launch_wgrad_kb<1, true, 32, true>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride,
+                                                stream, mask, ldm, Nout);
+    }
     return launch_wgrad_nt<1, true>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, mask, ldm, Nout);
   }
   switch (NT) {

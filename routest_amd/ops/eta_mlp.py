@@ -261,8 +261,9 @@ FWD16_VARIANTS = (16, 17, 18, 19, 20, 21, 22)
 class EtaMlpKernel:
     """A packed MLP resident on one device; ``__call__(records_i32) -> minutes``.
 
-    On a GPU device this ALWAYS runs the HIP kernel (raises if the extension is missing).
-    On CPU it runs the fp32 PyTorch model (the reference path).
+    On a GPU device this ALWAYS runs the HIP kernel (raises if the extension is missing): the
+    fused K1+K2 kernel for hidden <= 256, the L2-streamed wide path (ops/mlp_big.py) for 512 and
+    1024.  On CPU it runs the fp32 PyTorch model (the reference path).
 
     ``variant``: -1 auto, 0-8 the 32x32-MFMA kernel's variants (csrc/eta_mlp_fwd.hip
     launch_fwd_h), 16/17/18 the 16x16-MFMA kernel with 2/4/1 batch halves per wave-tile (19: 2 halves at
@@ -272,6 +273,20 @@ class EtaMlpKernel:
     def __init__(self, model: EtaMLP, device: Optional[torch.device] = None, variant: int = -1):
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.model_cpu = model.float().cpu().eval()
+        self._big = None
+        if self.device.type == "cuda" and model.hidden > 256:
+            # wide MLPs: W2 no longer fits LDS -> the L2-streamed path (ops/mlp_big.py)
+            from .mlp_big import BIG_HIDDEN, EtaMlpBigKernel
+            if model.hidden not in BIG_HIDDEN:
+                raise ValueError(f"HIP MLP kernels support hidden in (64, 128, 256, 512, 1024), "
+                                 f"got {model.hidden}")
+            self._big = EtaMlpBigKernel(self.model_cpu, self.device)
+            self.hidden = model.hidden
+            self.variant = variant
+            self.packed = pack_mlp3(self.model_cpu)
+            self.blob16 = None
+            self._C = self._big._C
+            return
         self.packed = pack_mlp3(self.model_cpu).to(self.device)
         self.hidden = model.hidden
         self.variant = variant
@@ -288,6 +303,8 @@ class EtaMlpKernel:
     def forward_hostio(self, rec_pinned: torch.Tensor, out_pinned: torch.Tensor) -> None:
         """Zero-copy scoring: the kernel reads pinned host records and writes pinned host minutes
         directly over PCIe (asynchronous on the current stream; synchronize before reading)."""
+        if self._big is not None:
+            return self._big.forward_hostio(rec_pinned, out_pinned)
         v = self._pick(rec_pinned.shape[0])
         self._C.eta_mlp3_forward_hostio(rec_pinned, out_pinned, self._blob(v), self.hidden,
                                         self.packed.norm, v)
@@ -303,6 +320,8 @@ class EtaMlpKernel:
         return self.blob16 if variant in FWD16_VARIANTS else self.packed.blob
 
     def __call__(self, rec: torch.Tensor) -> torch.Tensor:
+        if self._big is not None:
+            return self._big(rec)
         if self.device.type == "cuda":
             v = self._pick(rec.shape[0])
             return self._C.eta_mlp3_forward(rec, self._blob(v), self.hidden, self.packed.norm, v)

@@ -2,15 +2,17 @@
 
 Per step (all on the current HIP stream, no host synchronisation, HIP-graph capturable):
 
-  eta_mlp3_train_fwd (HIP)  : featurize + 3 layers + MSE grad; writes xf, h1a, h2a, dz2, dy
-                            (hidden units in the hperm() order: 16-byte stores per lane)
-  dh1 = dz2 @ W2            : hipBLASLt (bf16, fp32 accumulate)
+  eta_mlp3_train_fwd (HIP)  : featurize + 3 layers + MSE grad + the input gradient
+                            dh1 = dz2 W2 (MFMA on the transposed LDS image of W2); writes xf,
+                            h1a, h2a, dz2, dh1, dy (h1a/h2a/dz2 in the hperm() unit order, dh1 in
+                            natural order: 16-byte stores)
   G[W2|b2] = dz2^T [h1|1]   : split-K wgrad HIP kernel (K = batch) -> fp32 slabs laid out like
   G[w3|b3] = dy^T  [h2|1]     the flat bucket, then ONE deterministic slab reduction into G
   G[W1k|b1] = dz1^T [xf]    with dz1 = dh1 * (h1 > 0) applied inside the wgrad kernel's A staging
-                            (ReLU backward fused: dz1 is never written; xf slot 14 == 1)
+                            (mask read from h1a through the hperm order; xf slot 14 == 1)
   all_reduce(G)             : ONE RCCL collective (SUM; dy was pre-scaled by 2/global_batch)
-  adamw_pack (HIP)          : AdamW on fp32 master params + re-pack of the bf16 MFMA blob
+  adamw_pack (HIP)          : AdamW on fp32 master params + re-pack of the training blob
+No library GEMM runs in the step (csrc/eta_mlp_train.hip).
 
 Training runs in normalised-target space (y' = (y - y_mean)/y_std); :meth:`to_model` writes the
 learned weights back into an :class:`EtaMLP` whose buffers carry the scaling.
@@ -21,11 +23,12 @@ import math
 import os
 from typing import Optional
 
+import numpy as np
 import torch
 
 from ..models.mlp3 import EtaMLP
 from ..ops import _ext
-from ..ops.eta_mlp import blob_bytes
+
 from ..parallel.dp import allreduce_flat
 
 
@@ -65,7 +68,7 @@ def grads_from_bucket(G: torch.Tensor, H: int):
     cols = torch.cat([pm, torch.arange(H, ldg)])
     gW2a = G[:H * ldg].view(H, ldg)[pm][:, cols]
     gW3a = G[H * ldg:H * ldg + ldg][cols]
-    gW1a = G[H * ldg + ldg:].view(H, 16)[pm]
+    gW1a = G[H * ldg + ldg:].view(H, 16)          # natural unit order (dz1 is stored so)
     gW1 = gW1a[:, :12].clone()
     gW1[:, 10] += gW1a[:, 12]
     gW1[:, 11] += gW1a[:, 13]
@@ -74,11 +77,29 @@ def grads_from_bucket(G: torch.Tensor, H: int):
             "l3.bias": gW3a[H:H + 1].clone()}
 
 
-def _mm_f32(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> None:
-    try:
-        torch.mm(a, b, out_dtype=torch.float32, out=out)
-    except (RuntimeError, TypeError):
-        out.copy_(torch.mm(a, b))
+def _w2off(row: np.ndarray, col: np.ndarray) -> np.ndarray:
+    """Byte offset of stored element (row, col) of the training blob's W2 image (eta_mlp_train.hip
+    w2off: 512-byte rows, 16-byte chunk k of row R at chunk k ^ w2swz(R))."""
+    swz = ((row & 3) << 2) | ((row >> 2) & 3)
+    return row * 512 + (((col >> 3) ^ swz) << 4) + 2 * (col & 7)
+
+
+@torch.no_grad()
+def pack_train_blob(model: EtaMLP) -> torch.Tensor:
+    """Host mirror of adamw_pack_kernel(update=False): the training blob of ``model`` — the W2
+    image (rows = output units, stored column c = input unit hperm(c)) followed by the inference
+    blob's w1p | b1p | b2p | w3p | tail (target scale as in the model's buffers)."""
+    from ..ops.eta_mlp import pack_mlp3
+    H = model.hidden
+    inf = pack_mlp3(model).blob.numpy()
+    W2 = model.l2.weight.detach().float().cpu().to(torch.bfloat16).view(torch.int16).numpy()
+    img = np.zeros(H * 512, dtype=np.uint8)
+    o, c = np.meshgrid(np.arange(H), np.arange(H), indexing="ij")
+    src = W2[o, hperm(H).numpy()[c]]          # stored column c holds input unit hperm(c)
+    off = _w2off(o, c)
+    img.view(np.int16)[(off // 2).reshape(-1)] = src.reshape(-1)
+    tail = inf[2 * H * H:]                   # w1p | b1p | b2p | w3p | tail of the inference blob
+    return torch.from_numpy(np.concatenate([img, tail]))
 
 
 class FusedMlp3Trainer:
@@ -115,8 +136,7 @@ class FusedMlp3Trainer:
         self.gW2a = self.G[:H * ldg].view(H, ldg)
         self.gW3a = self.G[H * ldg:H * ldg + ldg].view(1, ldg)
         self.gW1a = self.G[H * ldg + ldg:].view(H, 16)
-        self.blob = torch.zeros(blob_bytes(H), dtype=torch.uint8, device=d)
-        self.w2bf = torch.empty(H, H, dtype=bf, device=d)
+        self.blob = torch.zeros(self.C.eta_mlp3_train_blob_bytes(H), dtype=torch.uint8, device=d)
         self.step_ctr = torch.zeros(1, dtype=torch.int32, device=d)
         B = batch_local
         self.xf = torch.empty(B, 16, dtype=bf, device=d)
@@ -128,15 +148,14 @@ class FusedMlp3Trainer:
         rows = int(os.environ.get("ROUTEST_WGRAD_ROWS", "256"))     # batch rows per k-slice
         self.S = max(1, min(ncu, B // rows))
         self.slab = torch.empty(self.S, self.G.numel(), dtype=torch.float32, device=d)
-        self.use_hipblaslt_wgrad = False
         self.dh1 = torch.empty(B, H, dtype=bf, device=d)
-        self.dz1 = None                # only the hipBLASLt A/B path materialises dz1
-        self.loss_tiles = torch.zeros((B + 31) // 32, dtype=torch.float32, device=d)
+        self.sq_err = torch.zeros(B, dtype=torch.float32, device=d)      # per-row squared errors
+        self.loss_tiles = self.sq_err                                      # (older name)
         self._pack(update=False)
 
     def _pack(self, update: bool) -> None:
         h = self.hp
-        self.C.adamw_pack(self.P, self.G, self.M, self.V, self.blob, self.w2bf, self.step_ctr, self.H,
+        self.C.adamw_pack(self.P, self.G, self.M, self.V, self.blob, self.step_ctr, self.H,
                           h["lr"], h["beta1"], h["beta2"], h["eps"], h["wd"], h["warmup"],
                           h["total_steps"], h["min_lr_ratio"], update)
 
@@ -147,38 +166,30 @@ class FusedMlp3Trainer:
         """Fills the flat gradient bucket G (local contribution, pre-scaled for the global mean)."""
         C, H = self.C, self.H
         C.eta_mlp3_train_fwd(rec, tgt_norm, self.blob, H, self.norm, 2.0 / self.global_batch,
-                             self.xf, self.h1a, self.h2a, self.dz2, self.dyb, self.loss_tiles,
-                             self.step_ctr)
-        torch.mm(self.dz2, self.w2bf, out=self.dh1)
-        if self.use_hipblaslt_wgrad:  # library baseline, kept for A/B measurements
-            if self.dz1 is None:
-                self.dz1 = torch.empty_like(self.dh1)
-            C.relu_bwd(self.dh1, self.h1a, self.dz1)
-            _mm_f32(self.dz2.t(), self.h1a, self.gW2a)
-            _mm_f32(self.dyb[:, :1].t(), self.h2a, self.gW3a)
-            _mm_f32(self.dz1.t(), self.xf, self.gW1a)
-            return
+                             self.xf, self.h1a, self.h2a, self.dz2, self.dh1, self.dyb,
+                             self.sq_err, self.step_ctr)
         ldg = H + 16
         C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab, 0, ldg)
         # dW3|db3 = (h2a^T dy)^T: the unit axis (H+16) is the MFMA M side so all 8 waves of a
         # workgroup work (dy as M = 8 rows left 7 of them idle); only column 0 of dy is real
         C.wgrad(self.h2a, ldg, ldg, self.dyb, 8, self.slab, H * ldg, 1, None, 1)
-        # dW1 = (dh1 * relu'(h1))^T x: the ReLU backward is applied while staging (no dz1 tensor)
-        C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, H * ldg + ldg, 16, self.h1a)
+        # dW1 = (dh1 * relu'(h1))^T x: the ReLU backward is applied while staging (no dz1 tensor);
+        # dh1 is in natural unit order, its mask h1a in the hperm order
+        C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, H * ldg + ldg, 16, self.h1a, mask_hperm=True)
         C.wgrad_reduce(self.slab, self.G)
 
     def step(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> torch.Tensor:
-        """One optimizer step; returns the device tensor of per-tile squared errors (no sync)."""
+        """One optimizer step; returns the device tensor of per-row squared errors (no sync)."""
         self.forward_backward(rec, tgt_norm)
         if self.comm is not None:
             self.comm.all_reduce(self.G)
         elif self.allreduce:
             allreduce_flat(self.G, average=False)
         self._pack(update=True)
-        return self.loss_tiles
+        return self.sq_err
 
     def local_mse(self) -> float:
-        return float(self.loss_tiles.sum().item()) / self.B
+        return float(self.sq_err.sum().item()) / self.B
 
     @torch.no_grad()
     def to_model(self) -> EtaMLP:

@@ -1,0 +1,106 @@
+"""Wide MLPs (H = 512, 1024) on the L2-streamed path (csrc/mlp_big.hip) vs the PyTorch emulation
+of its numerics and the fp32 model."""
+import numpy as np
+import pytest
+import torch
+
+from routest_amd.data.synth import synth_records
+from routest_amd.models.features import records_to_features
+from routest_amd.models.mlp3 import EtaMLP
+from routest_amd.ops.eta_mlp import EtaMlpKernel, featurize_torch, records_to_tensor
+from routest_amd.ops.mlp_big import emulate_big, hperm
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _model(H, seed=0):
+    torch.manual_seed(seed)
+    m = EtaMLP(H)
+    rec, y = synth_records(8192, seed)
+    m.fit_normalization(records_to_features(rec), y)
+    return m
+
+
+@pytest.mark.parametrize("H", [512, 1024])
+@pytest.mark.parametrize("B", [1, 127, 1000, 70_001])
+def test_big_forward_matches_emulation_and_fp32(H, B):
+    m = _model(H, 1)
+    k = EtaMlpKernel(m, DEV)
+    assert k._big is not None
+    rec, _ = synth_records(B, 3)
+    rt = records_to_tensor(rec)
+    got = k(rt.to(DEV)).cpu()
+    emu = emulate_big(k._big.packed, rt).reshape(-1)
+    with torch.no_grad():
+        ref = m(featurize_torch(rt)).reshape(-1)
+    spread = max(float((ref - ref.mean()).abs().mean()), 1e-3) if B > 1 else 1.0
+    assert torch.isfinite(got).all()
+    assert float((got - emu).abs().max()) / spread < 5e-3          # accumulation order only
+    torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("H", [512, 1024])
+def test_big_forward_trained_model(H):
+    """Trained (fp32 autograd) wide model: error relative to the prediction spread."""
+    torch.manual_seed(7)
+    m = EtaMLP(H)
+    rec, y = synth_records(1 << 15, 8)
+    x = torch.from_numpy(records_to_features(rec))
+    m.fit_normalization(x.numpy(), y)
+    md = m.to(DEV)
+    xd, yd = x.to(DEV), torch.from_numpy(y).to(DEV)
+    yn = (yd - md.y_mean) / md.y_std
+    opt = torch.optim.Adam(md.parameters(), lr=1e-3)
+    for s in range(200):
+        k0 = (s % 8) * 4096
+        loss = torch.nn.functional.mse_loss(md.forward_normalized(xd[k0:k0 + 4096]), yn[k0:k0 + 4096])
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    m = md.cpu().eval()
+    erec, _ = synth_records(100_000, 9)
+    got = EtaMlpKernel(m, DEV)(records_to_tensor(erec).to(DEV)).cpu()
+    with torch.no_grad():
+        ref = m(torch.from_numpy(records_to_features(erec))).reshape(-1)
+    spread = (ref - ref.mean()).abs().mean()
+    assert spread > 5.0
+    err = (got - ref).abs() / spread
+    assert float(err.max()) < 0.04 and float(err.mean()) < 0.006, (float(err.max()), float(err.mean()))
+
+
+def test_big_forward_zero_copy_and_wire_formats():
+    from routest_amd.models.features import records_to_compact6
+    from routest_amd.ops.eta_mlp import records6_to_tensor
+    m = _model(512, 2)
+    k = EtaMlpKernel(m, DEV)
+    rec, _ = synth_records(50_001, 4)
+    rt = records_to_tensor(rec)
+    ref = k(rt.to(DEV)).cpu()
+    host = rt.pin_memory()
+    out = torch.full((len(rec),), float("nan")).pin_memory()
+    k.forward_hostio(host, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    r6 = records6_to_tensor(records_to_compact6(rec))
+    got6 = k(r6.to(DEV)).cpu()
+    assert (got6 - ref).abs().max() < 0.1                  # 6-byte record quantisation only
+
+
+@pytest.mark.parametrize("M", [128, 1000, 4097])
+def test_gemm_nt_store_epilogue(M):
+    """EPI_STORE: out[m][hperm(n)] = sum_k W[n][k] X[m][k] (the dgrad GEMM of the wide trainer)."""
+    from routest_amd.ops import _ext
+    C = _ext.native()
+    g = torch.Generator().manual_seed(M)
+    N, K = 256, 512
+    W = torch.randn(N, K, generator=g).to(torch.bfloat16)
+    X = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    out = torch.zeros(M, N + 16, dtype=torch.bfloat16, device=DEV)
+    C.gemm_nt(2, W.to(DEV), X.to(DEV), N, M, K, out=out)
+    torch.cuda.synchronize()
+    ref = (X.float() @ W.float().T)                    # [M, N] natural unit order
+    got = torch.empty(M, N)
+    got[:, hperm(N)] = out[:, :N].float().cpu()        # stored position c holds unit hperm(c)
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=0.15)
+    assert (out[:, N:] == 0).all()
