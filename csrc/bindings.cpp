@@ -212,7 +212,8 @@ void gemm_nt(int64_t epi, torch::Tensor W, torch::Tensor X, int64_t N, int64_t M
 // y (f32 [B], GPU or pinned host) = sum of ypart rows + b3; training outputs optional
 void big_yreduce(torch::Tensor ypart, int64_t nparts, double b3, c10::optional<torch::Tensor> y,
                  c10::optional<torch::Tensor> target, double gscale, c10::optional<torch::Tensor> dy,
-                 c10::optional<torch::Tensor> dyb, c10::optional<torch::Tensor> sq_err) {
+                 c10::optional<torch::Tensor> dyb, c10::optional<torch::Tensor> sq_err,
+                 c10::optional<torch::Tensor> b3_dev) {
   check_dev(ypart, "ypart");
   TORCH_CHECK(ypart.scalar_type() == torch::kFloat32 && nparts > 0 && ypart.numel() % nparts == 0, "ypart");
   const int64_t B = ypart.numel() / nparts;
@@ -237,9 +238,45 @@ void big_yreduce(torch::Tensor ypart, int64_t nparts, double b3, c10::optional<t
     dybp = dyb->data_ptr();
     sqp = sq_err->data_ptr<float>();
   }
+  const float* b3p = nullptr;
+  if (b3_dev.has_value() && b3_dev->defined()) {
+    check_dev(*b3_dev, "b3");
+    TORCH_CHECK(b3_dev->scalar_type() == torch::kFloat32 && b3_dev->numel() >= 1, "b3 f32 [1]");
+    b3p = b3_dev->data_ptr<float>();
+  }
   const c10::DeviceGuard guard(ypart.device());
-  RT_CHECK_HIP(rt::launch_big_yreduce(ypart.data_ptr<float>(), (int)nparts, (int)B, (float)b3, yp, tp,
+  RT_CHECK_HIP(rt::launch_big_yreduce(ypart.data_ptr<float>(), (int)nparts, (int)B, (float)b3, b3p, yp, tp,
                                       (float)gscale, dyp, dybp, sqp, cur_stream(ypart)));
+}
+
+void adamw_pack_big(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor V,
+                    torch::Tensor w1p, torch::Tensor w2k, torch::Tensor w2t, torch::Tensor b2,
+                    torch::Tensor w3, torch::Tensor b3, torch::Tensor step, int64_t H, double lr,
+                    double beta1, double beta2, double eps, double wd, int64_t warmup,
+                    int64_t total_steps, double min_lr_ratio, bool update) {
+  const int64_t N = H * H + 15 * H + 1;
+  for (auto* t : {&P, &M, &V}) {
+    check_dev(*t, "adam state");
+    TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->numel() == N, "P/M/V f32 [", N, "]");
+  }
+  check_dev(G, "G");
+  TORCH_CHECK(G.scalar_type() == torch::kFloat32 && G.numel() == rt::mlp3_grad_bucket_floats((int)H), "G bucket");
+  check_bf16(w1p, "w1p", H, 16);
+  check_bf16(w2k, "w2k", H, H);
+  check_bf16(w2t, "w2t", H, H);
+  for (auto* t : {&b2, &w3, &b3}) {
+    check_dev(*t, "vec");
+    TORCH_CHECK(t->scalar_type() == torch::kFloat32, "f32 vectors");
+  }
+  TORCH_CHECK(b2.numel() == H && w3.numel() == H && b3.numel() >= 1, "b2/w3 [H], b3 [1]");
+  check_dev(step, "step");
+  const c10::DeviceGuard guard(P.device());
+  RT_CHECK_HIP(rt::launch_adamw_pack_big(P.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(),
+                                         V.data_ptr<float>(), w1p.data_ptr(), w2k.data_ptr(), w2t.data_ptr(),
+                                         b2.data_ptr<float>(), w3.data_ptr<float>(), b3.data_ptr<float>(),
+                                         step.data_ptr<int>(), (int)H, (float)lr, (float)beta1, (float)beta2,
+                                         (float)eps, (float)wd, (int)warmup, (int)total_steps,
+                                         (float)min_lr_ratio, update ? 1 : 0, cur_stream(P)));
 }
 
 void big_dz2(torch::Tensor h2a, torch::Tensor dy, torch::Tensor w3, int64_t H, torch::Tensor dz2) {
@@ -403,20 +440,23 @@ void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N
     mptr = mask->data_ptr();
     ldm = (int)mask->size(1);
   }
-  check_dev(Bm, "Bm");
+  // Bm may be a column block of a wider row-major matrix (the wide trainer's N-blocked dW2)
+  TORCH_CHECK(Bm.is_cuda() && Bm.dim() == 2 && Bm.stride(1) == 1 && Bm.stride(0) % 8 == 0 &&
+                  (reinterpret_cast<uintptr_t>(Bm.data_ptr()) & 15) == 0,
+              "Bm must be a row-major (column-sliced allowed) GPU tensor, 16-byte aligned");
   check_dev(slab, "slab");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && Bm.scalar_type() == torch::kBFloat16, "bf16 A/Bm");
   TORCH_CHECK(A.dim() == 2 && Bm.dim() == 2 && A.size(0) == Bm.size(0), "A/Bm must be [K, *]");
   TORCH_CHECK(M <= A.size(1) && N <= Bm.size(1) && Mout <= M, "M/N exceed operand widths");
-  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && A.size(1) % 8 == 0 && Bm.size(1) % 8 == 0,
+  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && A.size(1) % 8 == 0,
               "M, N and leading dims must be multiples of 8");
   const int NT = (int)((N + 31) / 32);
-  TORCH_CHECK(NT == 1 || NT == 2 || NT == 3 || NT == 5 || NT == 9, "unsupported N=", N);
+  TORCH_CHECK(NT >= 1 && NT <= 9, "unsupported N=", N, " (at most 288 columns per call)");
   TORCH_CHECK(slab.scalar_type() == torch::kFloat32 && slab.dim() == 2, "slab must be f32 [S, stride]");
   TORCH_CHECK(offset + (Mout - 1) * ldo + nout <= slab.size(1), "slab region out of range");
   const c10::DeviceGuard guard(A.device());
   RT_CHECK_HIP(rt::launch_wgrad(A.data_ptr(), (int)A.size(1), (int)M, (int)Mout, Bm.data_ptr(),
-                                (int)Bm.size(1), (int)N, (int)A.size(0), (int)slab.size(0),
+                                (int)Bm.stride(0), (int)N, (int)A.size(0), (int)slab.size(0),
                                 slab.data_ptr<float>() + offset, (int)ldo, (long long)slab.size(1),
                                 cur_stream(A), mptr, ldm, (int)nout, mask_hperm));
 }
@@ -815,7 +855,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("big_yreduce", &big_yreduce, "y = sum of partials + b3 (+ dy, dy operand, squared error)",
         py::arg("ypart"), py::arg("nparts"), py::arg("b3"), py::arg("y") = py::none(),
         py::arg("target") = py::none(), py::arg("gscale") = 0.0, py::arg("dy") = py::none(),
-        py::arg("dyb") = py::none(), py::arg("sq_err") = py::none());
+        py::arg("dyb") = py::none(), py::arg("sq_err") = py::none(), py::arg("b3_dev") = py::none());
+  m.def("adamw_pack_big", &adamw_pack_big, "wide trainer: AdamW + re-pack of w1p / w2k / w2t / b2 / w3 / b3");
   m.def("big_dz2", &big_dz2, "dz2 = dy * w3 * relu'(z2) from h2a (hperm order)");
   m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad + input gradient (dz2, dh1 = dz2 W2)");
   m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + training-blob re-pack");

@@ -242,7 +242,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 // y = sum_j ypart[m][j] + b3 (fixed order: deterministic).  Training (target != null): dy, the
 // bf16 dy operand [B,8] (col 0), squared error.
 __global__ __launch_bounds__(256) void big_yreduce_kernel(const float* __restrict__ ypart, int nparts,
-                                                          int B, float b3, float* __restrict__ y,
+                                                          int B, float b3, const float* __restrict__ b3p,
+                                                          float* __restrict__ y,
                                                           const float* __restrict__ target,
                                                           float gscale, float* __restrict__ dy,
                                                           __bf16* __restrict__ dyb,
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(256) void big_yreduce_kernel(const float* __restric
   const float* p = ypart + (size_t)m * nparts;
   float s = 0.f;
   for (int j = 0; j < nparts; ++j) s += p[j];
-  const float yy = s + b3;
+  const float yy = s + (b3p != nullptr ? *b3p : b3);     // training: b3 lives on the device
   if (y != nullptr) y[m] = yy;
   if (target != nullptr) {
     const float diff = yy - target[m];
@@ -285,7 +286,119 @@ __global__ __launch_bounds__(256) void big_dz2_kernel(const __bf16* __restrict__
   *reinterpret_cast<bf16x8*>(dz2 + m * H + c) = o;
 }
 
+struct AdamWBigArgs {
+  float lr, beta1, beta2, eps, wd;
+  int warmup, total_steps;
+  float min_lr_ratio;
+  int update, H;
+};
+
+__device__ __forceinline__ float sched_lr_big(const AdamWBigArgs& a, int t) {
+  float lr = a.lr;
+  if (a.warmup > 0 && t < a.warmup) lr *= (float)t / (float)a.warmup;
+  if (a.total_steps > 0 && t > a.warmup) {
+    const float prog = fminf(1.f, (float)(t - a.warmup) / fmaxf(1.f, (float)(a.total_steps - a.warmup)));
+    lr *= a.min_lr_ratio + (1.f - a.min_lr_ratio) * 0.5f * (1.f + cosf(3.14159265f * prog));
+  }
+  return lr;
+}
+
+// AdamW on the flat fp32 master params (W1[H][12] | b1 | W2[H][H] | b2 | w3 | b3) + re-pack of
+// the wide trainer's operands: w1p fragments (b1 as bf16 hi/lo in k = 14, 15), w2k[o][hp(i)],
+// w2t[i][hp(o)] (bf16), b2 / w3 / b3 f32.  Gradient bucket rows/columns are hperm positions
+// (gW2a[hp(o)][hp(i)], gW3a[hp(o)], gW1a[hp(o)][16]): every activation is stored in that order.
+__global__ __launch_bounds__(256) void adamw_pack_big_kernel(float* __restrict__ P, const float* __restrict__ G,
+                                                             float* __restrict__ M, float* __restrict__ V,
+                                                             __bf16* __restrict__ w1p, __bf16* __restrict__ w2k,
+                                                             __bf16* __restrict__ w2t, float* __restrict__ b2,
+                                                             float* __restrict__ w3, float* __restrict__ b3,
+                                                             const int* __restrict__ step, AdamWBigArgs a) {
+  const int H = a.H, LDG = H + 16;
+  const long long OFF_B1 = 12LL * H, OFF_W2 = 13LL * H, OFF_B2 = OFF_W2 + (long long)H * H,
+                  OFF_W3 = OFF_B2 + H, OFF_B3 = OFF_W3 + H, N = OFF_B3 + 1;
+  const float* gW2a = G;
+  const float* gW3a = G + (long long)H * LDG;
+  const float* gW1a = gW3a + LDG;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N) return;
+  float g;
+  bool decay = false;
+  int o = 0, i = 0;
+  if (e < OFF_B1) {
+    o = (int)(e / 12);
+    i = (int)(e - 12LL * o);
+    g = gW1a[hp(o) * 16 + i];
+    if (i == 10) g += gW1a[hp(o) * 16 + 12];
+    if (i == 11) g += gW1a[hp(o) * 16 + 13];
+    decay = true;
+  } else if (e < OFF_W2) {
+    o = (int)(e - OFF_B1);
+    g = gW1a[hp(o) * 16 + 14];
+  } else if (e < OFF_B2) {
+    const long long k = e - OFF_W2;
+    o = (int)(k / H);
+    i = (int)(k - (long long)o * H);
+    g = gW2a[(long long)hp(o) * LDG + hp(i)];
+    decay = true;
+  } else if (e < OFF_W3) {
+    o = (int)(e - OFF_B2);
+    g = gW2a[(long long)hp(o) * LDG + H];
+  } else if (e < OFF_B3) {
+    o = (int)(e - OFF_W3);
+    g = gW3a[hp(o)];
+    decay = true;
+  } else {
+    g = gW3a[H];
+  }
+  float p = P[e];
+  if (a.update) {
+    const int t = *step > 0 ? *step : 1;
+    const float lr = sched_lr_big(a, t);
+    const float bc1 = 1.f - powf(a.beta1, (float)t);
+    const float bc2 = 1.f - powf(a.beta2, (float)t);
+    if (decay) p -= lr * a.wd * p;
+    const float m = a.beta1 * M[e] + (1.f - a.beta1) * g;
+    const float v = a.beta2 * V[e] + (1.f - a.beta2) * g * g;
+    M[e] = m;
+    V[e] = v;
+    p -= lr * (m / bc1) / (sqrtf(v / bc2) + a.eps);
+    P[e] = p;
+  }
+  if (e < OFF_B1) {
+    const int mt = o >> 5, rr = o & 31;
+    auto put = [&](int kappa) { w1p[((size_t)(mt * 64 + rr + 32 * (kappa >> 3))) * 8 + (kappa & 7)] = (__bf16)p; };
+    put(i);
+    if (i == 10) put(12);
+    if (i == 11) put(13);
+  } else if (e < OFF_W2) {
+    const int mt = o >> 5, rr = o & 31;
+    const __bf16 hi = (__bf16)p;
+    w1p[((size_t)(mt * 64 + rr + 32)) * 8 + 6] = hi;
+    w1p[((size_t)(mt * 64 + rr + 32)) * 8 + 7] = (__bf16)(p - (float)hi);
+  } else if (e < OFF_B2) {
+    w2k[(size_t)o * H + hp(i)] = (__bf16)p;
+    w2t[(size_t)i * H + hp(o)] = (__bf16)p;
+  } else if (e < OFF_W3) {
+    b2[o] = p;
+  } else if (e < OFF_B3) {
+    w3[o] = p;
+  } else {
+    b3[0] = p;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_adamw_pack_big(float* P, const float* G, float* M, float* V, void* w1p, void* w2k,
+                                 void* w2t, float* b2, float* w3, float* b3, const int* step, int H,
+                                 float lr, float beta1, float beta2, float eps, float wd, int warmup,
+                                 int total_steps, float min_lr_ratio, int update, hipStream_t stream) {
+  AdamWBigArgs a{lr, beta1, beta2, eps, wd, warmup, total_steps, min_lr_ratio, update, H};
+  const long long N = (long long)H * H + 15LL * H + 1;
+  hipLaunchKernelGGL(adamw_pack_big_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, stream,
+                     P, G, M, V, (__bf16*)w1p, (__bf16*)w2k, (__bf16*)w2t, b2, w3, b3, step, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_big_layer1(const void* rec, int rec_bytes, int B, const void* w1p, int H,
                              const NormParams& np, void* h1, int ld, void* xf, hipStream_t stream) {
@@ -318,12 +431,12 @@ hipError_t launch_gemm_nt(int epi, const void* W, int ldw, const void* X, int ld
   return hipGetLastError();
 }
 
-hipError_t launch_big_yreduce(const float* ypart, int nparts, int B, float b3, float* y,
-                              const float* target, float gscale, float* dy, void* dyb, float* sq_err,
-                              hipStream_t stream) {
+hipError_t launch_big_yreduce(const float* ypart, int nparts, int B, float b3, const float* b3p,
+                              float* y, const float* target, float gscale, float* dy, void* dyb,
+                              float* sq_err, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(big_yreduce_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, ypart, nparts, B,
-                     b3, y, target, gscale, dy, (__bf16*)dyb, sq_err);
+                     b3, b3p, y, target, gscale, dy, (__bf16*)dyb, sq_err);
   return hipGetLastError();
 }
 

@@ -44,9 +44,13 @@ hipError_t launch_big_layer1(const void* rec, int rec_bytes, int B, const void* 
 hipError_t launch_gemm_nt(int epi, const void* W, int ldw, const void* X, int ldx, int N, int M,
                           int K, const float* b2, const float* w3, float* ypart, void* out,
                           int ldo, hipStream_t stream);
-hipError_t launch_big_yreduce(const float* ypart, int nparts, int B, float b3, float* y,
-                              const float* target, float gscale, float* dy, void* dyb, float* sq_err,
-                              hipStream_t stream);
+hipError_t launch_big_yreduce(const float* ypart, int nparts, int B, float b3, const float* b3p,
+                              float* y, const float* target, float gscale, float* dy, void* dyb,
+                              float* sq_err, hipStream_t stream);
+hipError_t launch_adamw_pack_big(float* P, const float* G, float* M, float* V, void* w1p, void* w2k,
+                                 void* w2t, float* b2, float* w3, float* b3, const int* step, int H,
+                                 float lr, float beta1, float beta2, float eps, float wd, int warmup,
+                                 int total_steps, float min_lr_ratio, int update, hipStream_t stream);
 hipError_t launch_big_dz2(const void* h2a, int lda, const float* dy, const float* w3, int B, int H,
                           void* dz2, hipStream_t stream);
 

@@ -308,7 +308,11 @@ hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm,
     case 1: return launch_wgrad_nt<1>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
     case 2: return launch_wgrad_nt<2>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
     case 3: return launch_wgrad_nt<3>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
+    case 4: return launch_wgrad_nt<4>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
     case 5: return launch_wgrad_nt<5>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
+    case 6: return launch_wgrad_nt<6>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
+    case 7: return launch_wgrad_nt<7>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
+    case 8: return launch_wgrad_nt<8>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
     case 9: return launch_wgrad_nt<9>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
     default: return hipErrorInvalidValue;
   }

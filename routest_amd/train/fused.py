@@ -68,7 +68,9 @@ def grads_from_bucket(G: torch.Tensor, H: int):
     cols = torch.cat([pm, torch.arange(H, ldg)])
     gW2a = G[:H * ldg].view(H, ldg)[pm][:, cols]
     gW3a = G[H * ldg:H * ldg + ldg][cols]
-    gW1a = G[H * ldg + ldg:].view(H, 16)          # natural unit order (dz1 is stored so)
+    gW1a = G[H * ldg + ldg:].view(H, 16)          # natural unit order (dh1 is stored so) ...
+    if H > 256:
+        gW1a = gW1a[pm]                            # ... the wide trainer keeps hperm rows
     gW1 = gW1a[:, :12].clone()
     gW1[:, 10] += gW1a[:, 12]
     gW1[:, 11] += gW1a[:, 13]
@@ -103,12 +105,21 @@ def pack_train_blob(model: EtaMLP) -> torch.Tensor:
 
 
 class FusedMlp3Trainer:
+    """One rank of data-parallel training on the hand-written kernels.  H in (64, 128, 256) runs
+    the fused LDS-resident step below; H in (512, 1024) is dispatched to
+    :class:`FusedMlp3TrainerBig` (L2-streamed GEMMs, csrc/mlp_big.hip)."""
+
+    def __new__(cls, model: EtaMLP, *args, **kw):
+        if cls is FusedMlp3Trainer and model.hidden in (512, 1024):
+            return super().__new__(FusedMlp3TrainerBig)
+        return super().__new__(cls)
+
     def __init__(self, model: EtaMLP, device: torch.device, batch_local: int, global_batch: int,
                  lr: float = 2e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  warmup: int = 0, total_steps: int = 0, min_lr_ratio: float = 0.1,
                  allreduce: bool = True, comm=None):
-        if model.hidden not in (64, 128, 256):
-            raise ValueError("fused trainer supports hidden in (64, 128, 256)")
+        if model.hidden not in self.SUPPORTED:
+            raise ValueError(f"{type(self).__name__} supports hidden in {self.SUPPORTED}")
         self.C = _ext.native(required=True)
         self.model = model
         self.H = H = model.hidden
@@ -136,22 +147,35 @@ class FusedMlp3Trainer:
         self.gW2a = self.G[:H * ldg].view(H, ldg)
         self.gW3a = self.G[H * ldg:H * ldg + ldg].view(1, ldg)
         self.gW1a = self.G[H * ldg + ldg:].view(H, 16)
-        self.blob = torch.zeros(self.C.eta_mlp3_train_blob_bytes(H), dtype=torch.uint8, device=d)
         self.step_ctr = torch.zeros(1, dtype=torch.int32, device=d)
-        B = batch_local
+        self._alloc(batch_local)
+        self._pack(update=False)
+
+    SUPPORTED = (64, 128, 256)
+
+    def _slices(self, B: int, cap_bytes: int = 0) -> int:
+        """Split-K slices of the wgrad kernels: one per CU (256 batch rows each), bounded by
+        ``cap_bytes`` of fp32 slabs."""
+        ncu = self.C.num_cus(self.dev.index if self.dev.index is not None else 0)
+        rows = int(os.environ.get("ROUTEST_WGRAD_ROWS", "256"))     # batch rows per k-slice
+        S = max(1, min(ncu, B // rows))
+        if cap_bytes:
+            S = max(1, min(S, cap_bytes // (4 * self.G.numel())))
+        return S
+
+    def _alloc(self, B: int) -> None:
+        d, H, bf = self.dev, self.H, torch.bfloat16
+        self.blob = torch.zeros(self.C.eta_mlp3_train_blob_bytes(H), dtype=torch.uint8, device=d)
         self.xf = torch.empty(B, 16, dtype=bf, device=d)
         self.h1a = torch.empty(B, H + 16, dtype=bf, device=d)
         self.h2a = torch.empty(B, H + 16, dtype=bf, device=d)
         self.dz2 = torch.empty(B, H, dtype=bf, device=d)
         self.dyb = torch.empty(B, 8, dtype=bf, device=d)
-        ncu = self.C.num_cus(self.dev.index if self.dev.index is not None else 0)
-        rows = int(os.environ.get("ROUTEST_WGRAD_ROWS", "256"))     # batch rows per k-slice
-        self.S = max(1, min(ncu, B // rows))
+        self.S = self._slices(B)
         self.slab = torch.empty(self.S, self.G.numel(), dtype=torch.float32, device=d)
         self.dh1 = torch.empty(B, H, dtype=bf, device=d)
         self.sq_err = torch.zeros(B, dtype=torch.float32, device=d)      # per-row squared errors
         self.loss_tiles = self.sq_err                                      # (older name)
-        self._pack(update=False)
 
     def _pack(self, update: bool) -> None:
         h = self.hp
@@ -208,6 +232,77 @@ class FusedMlp3Trainer:
     def set_params(self, flat: torch.Tensor) -> None:
         self.P.copy_(flat.to(self.dev))
         self._pack(update=False)
+
+
+class FusedMlp3TrainerBig(FusedMlp3Trainer):
+    """Wide MLPs (H = 512, 1024): W2 is 0.5 / 2 MiB, so it no longer lives in LDS.  Per step, all
+    on the current stream (no host sync, HIP-graph capturable):
+
+      big_layer1        : featurize + layer 1 -> xf, h1a (hperm order, ones column)
+      gemm_nt(H2Y)      : z2 = W2 h1 (W2 streamed from L2 through LDS tiles) -> h2a = relu(z2 + b2)
+                          + per-64-unit partials of h2 . w3
+      big_yreduce       : y, dy (scaled 2/global_batch), the dy operand, squared errors
+      big_dz2           : dz2 = dy w3 relu'(z2)
+      gemm_nt(STORE)    : dh1 = dz2 W2 (W2^T operand, kept by the optimizer kernel)
+      wgrad x 3 + reduce: dW2|db2 (column blocks of <= 288), dW3|db3, dW1 (relu'(h1) fused)
+      all_reduce(G)     : one collective on the flat bucket (C1: 4.3 MB at H = 1024)
+      adamw_pack_big    : AdamW + re-pack of w1p / w2k / w2t / b2 / w3 / b3
+    """
+
+    SUPPORTED = (512, 1024)
+
+    def _alloc(self, B: int) -> None:
+        d, H, bf = self.dev, self.H, torch.bfloat16
+        ldg = H + 16
+        self.w1p = torch.zeros(H * 16, dtype=bf, device=d)
+        self.w2k = torch.zeros(H, H, dtype=bf, device=d)
+        self.w2t = torch.zeros(H, H, dtype=bf, device=d)
+        self.b2v = torch.zeros(H, dtype=torch.float32, device=d)
+        self.w3v = torch.zeros(H, dtype=torch.float32, device=d)
+        self.b3v = torch.zeros(1, dtype=torch.float32, device=d)
+        self.xf = torch.empty(B, 16, dtype=bf, device=d)
+        self.h1a = torch.empty(B, ldg, dtype=bf, device=d)
+        self.h2a = torch.zeros(B, ldg, dtype=bf, device=d)
+        self.h2a[:, H] = 1.0                 # ones column (db3 input); kernels never write it
+        self.dz2 = torch.empty(B, H, dtype=bf, device=d)
+        self.dh1 = torch.empty(B, H, dtype=bf, device=d)
+        self.dyb = torch.empty(B, 8, dtype=bf, device=d)
+        self.dy = torch.empty(B, dtype=torch.float32, device=d)
+        self.ypart = torch.empty(B, H // 64, dtype=torch.float32, device=d)
+        self.sq_err = torch.zeros(B, dtype=torch.float32, device=d)
+        self.loss_tiles = self.sq_err
+        # k-slices: one slab per slice holds the whole bucket (4.3 MB at H = 1024): cap at 96 MB
+        self.S = self._slices(B, cap_bytes=96 << 20)
+        self.slab = torch.empty(self.S, self.G.numel(), dtype=torch.float32, device=d)
+
+    def _pack(self, update: bool) -> None:
+        h = self.hp
+        self.C.adamw_pack_big(self.P, self.G, self.M, self.V, self.w1p, self.w2k, self.w2t, self.b2v,
+                              self.w3v, self.b3v, self.step_ctr, self.H, h["lr"], h["beta1"],
+                              h["beta2"], h["eps"], h["wd"], h["warmup"], h["total_steps"],
+                              h["min_lr_ratio"], update)
+
+    def forward_backward(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> None:
+        C, H, B = self.C, self.H, rec.shape[0]
+        ldg = H + 16
+        assert B == self.B, "wide trainer: batch must equal batch_local"
+        self.step_ctr.add_(1)
+        C.big_layer1(rec, self.w1p, H, self.norm, self.h1a, self.xf)
+        C.gemm_nt(1, self.w2k, self.h1a, H, B, H, b2=self.b2v, w3=self.w3v, ypart=self.ypart,
+                  out=self.h2a)
+        C.big_yreduce(self.ypart.reshape(-1), H // 64, 0.0, target=tgt_norm,
+                      gscale=2.0 / self.global_batch, dy=self.dy, dyb=self.dyb, sq_err=self.sq_err,
+                      b3_dev=self.b3v)
+        C.big_dz2(self.h2a, self.dy, self.w3v, H, self.dz2)
+        C.gemm_nt(2, self.w2t, self.dz2, H, B, H, out=self.dh1)
+        # dW2|db2 = dz2^T [h1|1] in column blocks of <= 288 (9 MFMA n-tiles per wgrad launch)
+        for c0 in range(0, ldg, 288):
+            nb = min(288, ldg - c0)
+            C.wgrad(self.dz2, H, H, self.h1a[:, c0:c0 + nb], nb, self.slab, c0, ldg)
+        C.wgrad(self.h2a, ldg, ldg, self.dyb, 8, self.slab, H * ldg, 1, None, 1)
+        # dW1 = (dh1 * relu'(h1))^T x: dh1 and its mask h1a are both in the hperm order here
+        C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, H * ldg + ldg, 16, self.h1a)
+        C.wgrad_reduce(self.slab, self.G)
 
 
 def lr_at(step: int, lr: float, warmup: int, total: int, min_ratio: float) -> float:
