@@ -368,7 +368,7 @@ void check_bf16(const torch::Tensor& t, const char* name, int64_t rows, int64_t 
 // Writes every output in place (static buffers: the step is HIP-graph capturable).
 void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tensor blob, int64_t H,
                         std::vector<double> norm, double gscale, torch::Tensor xf,
-                        torch::Tensor h1a, torch::Tensor h2a, torch::Tensor dz2, torch::Tensor dh1,
+                        torch::Tensor h1a, torch::Tensor h2a, torch::Tensor dz2, torch::Tensor dz1,
                         torch::Tensor dyb, torch::Tensor sq_err, torch::Tensor step_ctr) {
   check_dev(records, "records");
   check_dev(target, "target");
@@ -384,7 +384,7 @@ void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tens
   check_bf16(h1a, "h1a", B, H + 16);
   check_bf16(h2a, "h2a", B, H + 16);
   check_bf16(dz2, "dz2", B, H);
-  check_bf16(dh1, "dh1", B, H);
+  check_bf16(dz1, "dz1", B, H);
   check_bf16(dyb, "dyb", B, 8);
   check_dev(sq_err, "sq_err");
   TORCH_CHECK(sq_err.scalar_type() == torch::kFloat32 && sq_err.numel() >= B, "sq_err must be f32 [B]");
@@ -394,7 +394,7 @@ void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tens
   RT_CHECK_HIP(rt::launch_eta_mlp3_train_fwd(
       records.data_ptr(), target.data_ptr<float>(), (int)B, blob.data_ptr(), (int)H,
       norm_from(norm), (float)gscale, xf.data_ptr(), h1a.data_ptr(), h2a.data_ptr(),
-      dz2.data_ptr(), dh1.data_ptr(), dyb.data_ptr(), sq_err.data_ptr<float>(), step_ctr.data_ptr<int>(),
+      dz2.data_ptr(), dz1.data_ptr(), dyb.data_ptr(), sq_err.data_ptr<float>(), step_ctr.data_ptr<int>(),
       num_cus(records.device().index()), cur_stream(records)));
 }
 
@@ -858,7 +858,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dyb") = py::none(), py::arg("sq_err") = py::none(), py::arg("b3_dev") = py::none());
   m.def("adamw_pack_big", &adamw_pack_big, "wide trainer: AdamW + re-pack of w1p / w2k / w2t / b2 / w3 / b3");
   m.def("big_dz2", &big_dz2, "dz2 = dy * w3 * relu'(z2) from h2a (hperm order)");
-  m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad + input gradient (dz2, dh1 = dz2 W2)");
+  m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad + input-gradient path (dz2, dz1)");
   m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + training-blob re-pack");
   m.def("eta_mlp3_train_blob_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_train_blob_bytes((int)H); });
   m.def("mlp3_num_params", [](int64_t H) { return (int64_t)rt::mlp3_num_params((int)H); });

@@ -4,21 +4,22 @@
 //
 // One training step on a rank (routest_amd/train/fused.py::FusedMlp3Trainer):
 //   1. eta_mlp3_train_fwd_kernel (this file): featurize + layer 1 + layer 2 + layer 3 + MSE
-//      gradient + the input gradient dh1 = dz2 W2 in ONE launch (relu'(z1) is applied by the dW1
-//      wgrad kernel while it stages dh1: wgrad.hip MASK, mask columns in the hperm order).  Because dL/dz2 = dy * w3 * relu'(z2) needs only the ReLU mask, dz2 is produced
-//      in-register the moment y (hence dy) is known, and it IS the B operand of the dgrad MFMAs
-//      (accumulator layout == next-MFMA B layout, common.h); W2 is read a second time from the
-//      same LDS image through the hardware-transposed ds_read_b64_tr_b16 as the A operand W2^T,
-//      and h1 (still in registers) gives relu'(z1).  No library GEMM, no dh1 round trip through
-//      HBM.  Emits, bf16 row-major:
+//      gradient + the whole input-gradient path dz2 -> dh1 = dz2 W2 -> dz1 = dh1 * relu'(z1) in
+//      ONE launch.  Because dL/dz2 = dy * w3 * relu'(z2) needs only the ReLU mask, dz2 is
+//      produced in-register the moment y (hence dy) is known, and it IS the B operand of the dgrad
+//      MFMAs (accumulator layout == next-MFMA B layout, common.h); W2 is read a second time from
+//      the same LDS image through the hardware-transposed ds_read_b64_tr_b16 as the A operand
+//      W2^T; h1, still in registers, gives relu'(z1).  No library GEMM, no dh1 round trip.
+//      Emits, bf16 row-major:
 //        xf  [B,16]   the exact bf16 features the MFMA consumed, slot 14 := 1 (bias-grad column)
 //        h1a [B,H+16] relu(z1) with column H := 1   (dW2 | db2 = dz2^T h1a)
 //        h2a [B,H+16] relu(z2) with column H := 1   (dW3 | db3 = dy^T h2a)
-//        dz2 [B,H], dh1 [B,H] (natural unit order), dy [B,8] (col 0; pre-scaled by
-//        2 / global_batch), per-row squared errors.
-//      The kernel never reads back what it stored: a load waits for every older store of the wave
-//      (vmcnt counts both in order), which serialised each tile on its own store stream when the
-//      relu'(z1) mask was read back from h1a here (83 us vs 31 us for the whole kernel at 65k rows).
+//        dz2 [B,H], dz1 [B,H], dy [B,8] (col 0; pre-scaled by 2 / global_batch), per-row
+//        squared errors.
+//      The kernel never reads back what it stored (a load waits for every older store of the
+//      wave: vmcnt counts both, in order), and nothing it needs per tile is hoisted out of the
+//      tile loop (hoisted, it exceeds the VGPR budget and every spill reload after the stores
+//      stalls the same way).
 //   2. the three weight-gradient GEMMs (K = batch) on the split-K wgrad kernel (wgrad.hip) + one
 //      deterministic slab reduction.
 //   3. ONE flat fp32 gradient bucket -> one RCCL all-reduce over xGMI.
@@ -27,22 +28,24 @@
 //      HIP graph.
 //
 // Training blob (TrainLayout): [ w2img | w1p | b1p | b2p | w3p | tail ] where w2img holds W2
-// row-major in 512-byte rows (row = output unit o, natural order; column c = input unit hperm(c),
-// the stored activation order) with 16-byte chunk k of row R at chunk k ^ w2swz(R).  That one
-// image serves both operand reads conflict-free (bank rule, cdna_hip_programming.md §2 /
-// MI355X_MICROARCH.md §LDS):
-//   * layer 2, A = W2: lane (r, h) of tile (mt, ks) reads row 32mt + r, columns 16ks + 8h .. +7
-//     with ONE ds_read_b128 (w2swz is a bijection of R mod 16: each 16-lane group hits 16 slots);
+// row-major in 512-byte rows (natural unit order both ways) with 8-byte chunk k of row R at chunk
+// k ^ w2swz(R).  That one image serves both operand reads conflict-free (bank rule,
+// cdna_hip_programming.md §2 / MI355X_MICROARCH.md §LDS):
+//   * layer 2, A = W2: lane (r, h) of tile (mt, ks) reads row 32mt + r, units 16ks + 4h .. +3 and
+//     16ks + 8 + 4h .. +3 (the permuted k order of the h1 B fragments) with two ds_read_b64:
+//     w2swz is a bijection of R mod 32, so a 32-lane half hits 64 distinct banks;
 //   * dgrad, A = W2^T: ds_read_b64_tr_b16 over 4-row x 16-column blocks (rows 16ks + 4h + q and
 //     16ks + 8 + 4h + q, columns 32mi + 16g .. +15): w2swz moves the 4 rows of a block to 4
-//     different groups of 4 slots, so a 32-lane half touches 64 distinct banks.
+//     different 8-chunk groups, so a 32-lane half touches 64 distinct banks.
+// Natural column order is what makes relu'(z1) lane-local: dgrad accumulator register e of lane
+// half h is unit 32mi + 8(e>>2) + 4h + (e&3), element e&7 of the lane's own h1 fragment.
 // The rest of the blob is the inference layout (mlp3_tile.h): w1p, b1p, b2p, w3p, tail.
 #include "mlp3_tile.h"
 #include "ops.h"
 
 namespace rt {
 
-// Stored hidden-unit order of the saved activations h1a / h2a / dz2 (and of the gradient bucket
+// Stored hidden-unit order of the saved activations h1a / h2a / dz2 / dz1 (and of the gradient bucket
 // built from them): element j of fragment ks on lane half h is hidden unit
 // u = 16ks + 8(j>>2) + 4h + (j&3); storing it at column c = 16ks + 8h + j (= u with bits 2 and 3
 // swapped, an involution) makes each lane's 8 values ONE contiguous 16-byte store instead of two
@@ -61,10 +64,10 @@ struct TrainLayout {
 
 size_t eta_mlp3_train_blob_bytes(int H) { return (size_t)H * 512 + 44 * (size_t)H + 16; }
 
-__host__ __device__ __forceinline__ int w2swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
-// byte offset of image element (row, col) (col = stored column, i.e. input unit hperm(col))
+__host__ __device__ __forceinline__ int w2swz(int row) { return ((row & 3) << 3) | ((row >> 2) & 7); }
+// byte offset of W2[row][col] in the image (natural order both ways; 8-byte chunks swizzled)
 __host__ __device__ __forceinline__ int w2off(int row, int col) {
-  return row * 512 + (((col >> 3) ^ w2swz(row)) << 4) + 2 * (col & 7);
+  return row * 512 + (((col >> 2) ^ w2swz(row)) << 3) + 2 * (col & 3);
 }
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -84,7 +87,7 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     const int4* __restrict__ rec, const float* __restrict__ target, int B,
     const unsigned char* __restrict__ blob, NormParams np, float gscale, __bf16* __restrict__ xf,
     __bf16* __restrict__ h1a, __bf16* __restrict__ h2a, __bf16* __restrict__ dz2,
-    __bf16* __restrict__ dh1, __bf16* __restrict__ dyb, float* __restrict__ sq_err,
+    __bf16* __restrict__ dz1, __bf16* __restrict__ dyb, float* __restrict__ sq_err,
     int* __restrict__ step_ctr) {
   using L = TrainLayout<H>;
   constexpr int MT = H / 32, KS = H / 16, LDA = H + 16, D = KS < 4 ? KS : 4;
@@ -163,16 +166,21 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       // depends on ks & 7, ks >> 3 adds 256 B
       const int sw = w2swz(r);
       const unsigned char* lrow = img + r * 512;
-      constexpr int NX = KS < 8 ? KS : 8;      // distinct ks & 7 patterns
-      int xk[NX];
+      constexpr int NX = KS < 8 ? KS : 8;      // distinct ks & 7 patterns (ks >> 3 adds 256 B)
+      int xk[NX][2];
 #pragma unroll
-      for (int k = 0; k < NX; ++k) xk[k] = 16 * ((2 * k + h) ^ sw);
+      for (int k = 0; k < NX; ++k)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) xk[k][t] = 8 * ((4 * k + 2 * t + h) ^ sw);
 #pragma unroll 1
       for (int mt = 0; mt < MT; ++mt) {
         f32x16 acc = load_vec16(b2p, mt, h);
         const unsigned char* pm = lrow + mt * 16384;
+        // units 16ks + 4h + 0..3 and 16ks + 8 + 4h + 0..3: the permuted k order of h1
         auto frag = [&](int ks) {
-          return *reinterpret_cast<const bf16x8*>(pm + xk[ks & 7] + 256 * (ks >> 3));
+          const s16x4 lo = *reinterpret_cast<const s16x4*>(pm + xk[ks & 7][0] + 256 * (ks >> 3));
+          const s16x4 hi = *reinterpret_cast<const s16x4*>(pm + xk[ks & 7][1] + 256 * (ks >> 3));
+          return join4(lo, hi);
         };
         bf16x8 ring[D];
 #pragma unroll
@@ -243,25 +251,27 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf16x8*>(drow + 16 * ks + 8 * h) = dz2f[ks];
     }
 
-    // dgrad: dh1^T tile mi = W2^T[stored cols 32mi.., :] dz2^T.  Accumulator register e is
-    // stored column c = 32mi + (e&3) + 8(e>>2) + 4h, i.e. input unit hperm(c) =
-    // 32mi + 16(e>>3) + 8h + (e&7): dh1 is written in NATURAL unit order, two 16-byte runs per lane.
+    // dgrad: dh1^T tile mi = W2^T[32mi.., :] dz2^T, then dz1 = dh1 * relu'(z1).  Accumulator
+    // register e is input unit 32mi + 8(e>>2) + 4h + (e&3): exactly element e&7 of this lane's own
+    // h1 fragment 2mi + (e>>3), so relu'(z1) is a lane-local select on the packed bf16 output, and
+    // dz1 lands at hperm positions 32mi + 16(e>>3) + 8h + (e&7) — two 16-byte stores like h1a.
+    // The mi loop is unrolled so that h1 is indexed statically (kept in registers, never re-read
+    // from memory: a load would wait for every older store of the wave).
     {
-      __bf16* zrow = dh1 + (size_t)row * H;
-      // transposed-read addresses (w2_tr_frag) as two lane bases per tile mi + immediates:
-      // row 16ks + 8t + 4h + q -> +8192 ks; chunk (4mi + 2(g&1) + (p>>1)) ^ (4q + 2t + h)
+      __bf16* zrow = dz1 + (size_t)row * H;
+      // transposed reads: rows 16ks + 8t + 4h + q, columns 32mi + 16(g&1) + 4p (8-byte chunk
+      // 8mi + 4(g&1) + p) -> chunk ^ ((q << 3) | (4(ks&1) + 2t + h))
       const int g1 = (lv >> 4) & 1, p = lv & 3, q = (lv >> 2) & 3;
-      const unsigned char* rb = img + (4 * h + q) * 512 + 8 * (p & 1);
-#pragma unroll 1
+      const unsigned char* rb = img + (4 * h + q) * 512;
+#pragma unroll
       for (int mi = 0; mi < MT; ++mi) {
-        const int cc = 4 * (mi & 3) + 2 * g1 + (p >> 1);
-        const unsigned char* b0 = rb + 16 * (cc ^ (4 * q + h)) + 256 * (mi >> 2);
-        const unsigned char* b1 = rb + 4096 + 16 * (cc ^ (4 * q + 2 + h)) + 256 * (mi >> 2);
+        const int ck = 8 * mi + 4 * g1 + p;
         auto frag = [&](int ks) {
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4*)(const_cast<unsigned char*>(b0) + 8192 * ks));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4*)(const_cast<unsigned char*>(b1) + 8192 * ks));
+          const int kx = 4 * (ks & 1) + h;
+          const unsigned char* r0 = rb + 8192 * ks + 8 * (ck ^ ((q << 3) | kx));
+          const unsigned char* r1 = rb + 8192 * ks + 4096 + 8 * (ck ^ ((q << 3) | (kx + 2)));
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<unsigned char*>(r0)));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<unsigned char*>(r1)));
           return join4(lo, hi);
         };
         f32x16 acc;
@@ -283,10 +293,14 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          bf16x8 o;
+          // relu'(z1) from h1 (>= 0: nonzero bits <=> z1 > 0) as a select on the bf16 output
+          const bf16x8 hm = h1[2 * mi + s];
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          const s16x8 hb = __builtin_bit_cast(s16x8, hm);
+          bf16x8 ov;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = (__bf16)acc[8 * s + j];
-          if (valid) *reinterpret_cast<bf16x8*>(zrow + 32 * mi + 16 * s + 8 * h) = o;   // natural order
+          for (int j = 0; j < 8; ++j) ov[j] = hb[j] != 0 ? (__bf16)acc[8 * s + j] : (__bf16)0.f;
+          if (valid) *reinterpret_cast<bf16x8*>(zrow + 32 * mi + 16 * s + 8 * h) = ov;   // hperm order
         }
       }
     }
@@ -341,13 +355,13 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
   if (e < OFF_B1) {
     o = e / 12;
     i = e - o * 12;
-    g = gW1a[o * 16 + i];                 // dW1 rows in natural unit order (dh1 is stored so)
-    if (i == 10) g += gW1a[o * 16 + 12];
-    if (i == 11) g += gW1a[o * 16 + 13];
+    g = gW1a[hperm(o) * 16 + i];          // dW1 rows at hperm positions (dz1 is stored so)
+    if (i == 10) g += gW1a[hperm(o) * 16 + 12];
+    if (i == 11) g += gW1a[hperm(o) * 16 + 13];
     decay = true;
   } else if (e < OFF_W2) {
     o = e - OFF_B1;
-    g = gW1a[o * 16 + 14];
+    g = gW1a[hperm(o) * 16 + 14];
   } else if (e < OFF_B2) {
     const int k = e - OFF_W2;
     o = k / H;
@@ -389,7 +403,7 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
     if (i == 10) put(12);
     if (i == 11) put(13);
   } else if (e >= OFF_W2 && e < OFF_B2) {
-    *reinterpret_cast<__bf16*>(w2img + w2off(o, hperm(i))) = (__bf16)p;   // rows natural, cols hperm
+    *reinterpret_cast<__bf16*>(w2img + w2off(o, i)) = (__bf16)p;   // natural order, swizzled chunks
   } else if (e < OFF_B3) {
     const int mt = o >> 5, rr = o & 31;
     const int hh = (rr >> 2) & 1;
@@ -411,7 +425,7 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
 template <int H>
 static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B, const void* blob,
                                      const NormParams& np, float gscale, void* xf, void* h1a,
-                                     void* h2a, void* dz2, void* dh1, void* dyb, float* sq_err,
+                                     void* h2a, void* dz2, void* dz1, void* dyb, float* sq_err,
                                      int* step_ctr, int num_cus, hipStream_t stream) {
   using L = TrainLayout<H>;
   static bool attr_set[64] = {};
@@ -430,20 +444,20 @@ static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B
   if (grid < 1) return hipSuccess;
   hipLaunchKernelGGL(eta_mlp3_train_fwd_kernel<H>, dim3(grid), dim3(TPB), L::BLOB, stream,
                      (const int4*)rec, target, B, (const unsigned char*)blob, np, gscale,
-                     (__bf16*)xf, (__bf16*)h1a, (__bf16*)h2a, (__bf16*)dz2, (__bf16*)dh1,
+                     (__bf16*)xf, (__bf16*)h1a, (__bf16*)h2a, (__bf16*)dz2, (__bf16*)dz1,
                      (__bf16*)dyb, sq_err, step_ctr);
   return hipGetLastError();
 }
 
 hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B, const void* blob,
                                      int H, const NormParams& np, float gscale, void* xf,
-                                     void* h1a, void* h2a, void* dz2, void* dh1, void* dyb,
+                                     void* h1a, void* h2a, void* dz2, void* dz1, void* dyb,
                                      float* sq_err, int* step_ctr, int num_cus,
                                      hipStream_t stream) {
   switch (H) {
-    case 64: return launch_train_fwd_h<64>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dh1, dyb, sq_err, step_ctr, num_cus, stream);
-    case 128: return launch_train_fwd_h<128>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dh1, dyb, sq_err, step_ctr, num_cus, stream);
-    case 256: return launch_train_fwd_h<256>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dh1, dyb, sq_err, step_ctr, num_cus, stream);
+    case 64: return launch_train_fwd_h<64>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
+    case 128: return launch_train_fwd_h<128>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
+    case 256: return launch_train_fwd_h<256>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }

@@ -2,14 +2,13 @@
 
 Per step (all on the current HIP stream, no host synchronisation, HIP-graph capturable):
 
-  eta_mlp3_train_fwd (HIP)  : featurize + 3 layers + MSE grad + the input gradient
-                            dh1 = dz2 W2 (MFMA on the transposed LDS image of W2); writes xf,
-                            h1a, h2a, dz2, dh1, dy (h1a/h2a/dz2 in the hperm() unit order, dh1 in
-                            natural order: 16-byte stores)
+  eta_mlp3_train_fwd (HIP)  : featurize + 3 layers + MSE grad + the input-gradient path
+                            dz2 -> dh1 = dz2 W2 (MFMA on the transposed LDS image of W2) ->
+                            dz1 = dh1 * relu'(z1) (h1 still in registers); writes xf, h1a, h2a,
+                            dz2, dz1, dy (activations in the hperm() unit order: 16-byte stores)
   G[W2|b2] = dz2^T [h1|1]   : split-K wgrad HIP kernel (K = batch) -> fp32 slabs laid out like
   G[w3|b3] = dy^T  [h2|1]     the flat bucket, then ONE deterministic slab reduction into G
-  G[W1k|b1] = dz1^T [xf]    with dz1 = dh1 * (h1 > 0) applied inside the wgrad kernel's A staging
-                            (mask read from h1a through the hperm order; xf slot 14 == 1)
+  G[W1k|b1] = dz1^T [xf]    (xf slot 14 == 1)
   all_reduce(G)             : ONE RCCL collective (SUM; dy was pre-scaled by 2/global_batch)
   adamw_pack (HIP)          : AdamW on fp32 master params + re-pack of the training blob
 No library GEMM runs in the step (csrc/eta_mlp_train.hip).
@@ -68,9 +67,7 @@ def grads_from_bucket(G: torch.Tensor, H: int):
     cols = torch.cat([pm, torch.arange(H, ldg)])
     gW2a = G[:H * ldg].view(H, ldg)[pm][:, cols]
     gW3a = G[H * ldg:H * ldg + ldg][cols]
-    gW1a = G[H * ldg + ldg:].view(H, 16)          # natural unit order (dh1 is stored so) ...
-    if H > 256:
-        gW1a = gW1a[pm]                            # ... the wide trainer keeps hperm rows
+    gW1a = G[H * ldg + ldg:].view(H, 16)[pm]
     gW1 = gW1a[:, :12].clone()
     gW1[:, 10] += gW1a[:, 12]
     gW1[:, 11] += gW1a[:, 13]
@@ -80,24 +77,24 @@ def grads_from_bucket(G: torch.Tensor, H: int):
 
 
 def _w2off(row: np.ndarray, col: np.ndarray) -> np.ndarray:
-    """Byte offset of stored element (row, col) of the training blob's W2 image (eta_mlp_train.hip
-    w2off: 512-byte rows, 16-byte chunk k of row R at chunk k ^ w2swz(R))."""
-    swz = ((row & 3) << 2) | ((row >> 2) & 3)
-    return row * 512 + (((col >> 3) ^ swz) << 4) + 2 * (col & 7)
+    """Byte offset of W2[row][col] in the training blob's W2 image (eta_mlp_train.hip w2off:
+    512-byte rows, 8-byte chunk k of row R at chunk k ^ w2swz(R))."""
+    swz = ((row & 3) << 3) | ((row >> 2) & 7)
+    return row * 512 + (((col >> 2) ^ swz) << 3) + 2 * (col & 3)
 
 
 @torch.no_grad()
 def pack_train_blob(model: EtaMLP) -> torch.Tensor:
     """Host mirror of adamw_pack_kernel(update=False): the training blob of ``model`` — the W2
-    image (rows = output units, stored column c = input unit hperm(c)) followed by the inference
-    blob's w1p | b1p | b2p | w3p | tail (target scale as in the model's buffers)."""
+    image (natural order, swizzled 8-byte chunks) followed by the inference blob's
+    w1p | b1p | b2p | w3p | tail (target scale as in the model's buffers)."""
     from ..ops.eta_mlp import pack_mlp3
     H = model.hidden
     inf = pack_mlp3(model).blob.numpy()
     W2 = model.l2.weight.detach().float().cpu().to(torch.bfloat16).view(torch.int16).numpy()
     img = np.zeros(H * 512, dtype=np.uint8)
     o, c = np.meshgrid(np.arange(H), np.arange(H), indexing="ij")
-    src = W2[o, hperm(H).numpy()[c]]          # stored column c holds input unit hperm(c)
+    src = W2[o, c]
     off = _w2off(o, c)
     img.view(np.int16)[(off // 2).reshape(-1)] = src.reshape(-1)
     tail = inf[2 * H * H:]                   # w1p | b1p | b2p | w3p | tail of the inference blob
@@ -173,7 +170,7 @@ class FusedMlp3Trainer:
         self.dyb = torch.empty(B, 8, dtype=bf, device=d)
         self.S = self._slices(B)
         self.slab = torch.empty(self.S, self.G.numel(), dtype=torch.float32, device=d)
-        self.dh1 = torch.empty(B, H, dtype=bf, device=d)
+        self.dz1 = torch.empty(B, H, dtype=bf, device=d)
         self.sq_err = torch.zeros(B, dtype=torch.float32, device=d)      # per-row squared errors
         self.loss_tiles = self.sq_err                                      # (older name)
 
@@ -190,16 +187,15 @@ class FusedMlp3Trainer:
         """Fills the flat gradient bucket G (local contribution, pre-scaled for the global mean)."""
         C, H = self.C, self.H
         C.eta_mlp3_train_fwd(rec, tgt_norm, self.blob, H, self.norm, 2.0 / self.global_batch,
-                             self.xf, self.h1a, self.h2a, self.dz2, self.dh1, self.dyb,
+                             self.xf, self.h1a, self.h2a, self.dz2, self.dz1, self.dyb,
                              self.sq_err, self.step_ctr)
         ldg = H + 16
         C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab, 0, ldg)
         # dW3|db3 = (h2a^T dy)^T: the unit axis (H+16) is the MFMA M side so all 8 waves of a
         # workgroup work (dy as M = 8 rows left 7 of them idle); only column 0 of dy is real
         C.wgrad(self.h2a, ldg, ldg, self.dyb, 8, self.slab, H * ldg, 1, None, 1)
-        # dW1 = (dh1 * relu'(h1))^T x: the ReLU backward is applied while staging (no dz1 tensor);
-        # dh1 is in natural unit order, its mask h1a in the hperm order
-        C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, H * ldg + ldg, 16, self.h1a, mask_hperm=True)
+        # dW1 = dz1^T x (relu'(z1) applied by the forward kernel)
+        C.wgrad(self.dz1, H, H, self.xf, 16, self.slab, H * ldg + ldg, 16)
         C.wgrad_reduce(self.slab, self.G)
 
     def step(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> torch.Tensor:
