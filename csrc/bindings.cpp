@@ -454,7 +454,7 @@ void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor
 // slab: f32 [S, stride]; the partial of k-slice s is written at slab[s, offset + m*ldo + n].
 void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N, torch::Tensor slab,
            int64_t offset, int64_t ldo, c10::optional<torch::Tensor> mask, int64_t nout,
-           bool mask_hperm) {
+           bool mask_hperm, int64_t nsplit) {
   check_dev(A, "A");
   if (nout < 0 || nout > N) nout = N;
   const void* mptr = nullptr;
@@ -480,23 +480,36 @@ void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N
   const int NT = (int)((N + 31) / 32);
   TORCH_CHECK(NT >= 1 && NT <= 9, "unsupported N=", N, " (at most 288 columns per call)");
   TORCH_CHECK(slab.scalar_type() == torch::kFloat32 && slab.dim() == 2, "slab must be f32 [S, stride]");
+  TORCH_CHECK(nsplit >= 1 && (nsplit == 1 || !mptr), "nsplit >= 1 (1 with a mask)");
   TORCH_CHECK(offset + (Mout - 1) * ldo + nout <= slab.size(1), "slab region out of range");
   const c10::DeviceGuard guard(A.device());
   RT_CHECK_HIP(rt::launch_wgrad(A.data_ptr(), (int)A.size(1), (int)M, (int)Mout, Bm.data_ptr(),
                                 (int)Bm.stride(0), (int)N, (int)A.size(0), (int)slab.size(0),
                                 slab.data_ptr<float>() + offset, (int)ldo, (long long)slab.size(1),
-                                cur_stream(A), mptr, ldm, (int)nout, mask_hperm));
+                                cur_stream(A), mptr, ldm, (int)nout, mask_hperm, (int)nsplit));
 }
 
-void wgrad_reduce(torch::Tensor slab, torch::Tensor G) {
-  check_dev(slab, "slab");
-  check_dev(G, "G");
-  TORCH_CHECK(slab.scalar_type() == torch::kFloat32 && G.scalar_type() == torch::kFloat32, "f32");
-  TORCH_CHECK(slab.dim() == 2 && slab.size(1) >= G.numel(), "slab/G shape");
+void wgrad_reduce(torch::Tensor slab, torch::Tensor G, c10::optional<torch::Tensor> slab1,
+                  c10::optional<torch::Tensor> G1) {
+  auto chk = [](const torch::Tensor& sl, const torch::Tensor& g) {
+    check_dev(sl, "slab");
+    check_dev(g, "G");
+    TORCH_CHECK(sl.scalar_type() == torch::kFloat32 && g.scalar_type() == torch::kFloat32, "f32");
+    TORCH_CHECK(sl.dim() == 2 && sl.size(1) >= g.numel(), "slab/G shape");
+  };
+  chk(slab, G);
+  const bool two = slab1.has_value() && slab1->defined();
+  TORCH_CHECK(two == (G1.has_value() && G1->defined()), "slab1 and G1 go together");
+  if (two) {
+    chk(*slab1, *G1);
+    TORCH_CHECK(slab1->device() == G.device() && G1->device() == G.device(), "one device");
+  }
   const c10::DeviceGuard guard(G.device());
-  RT_CHECK_HIP(rt::launch_wgrad_reduce(slab.data_ptr<float>(), (int)slab.size(0),
-                                       (long long)slab.size(1), G.data_ptr<float>(), (int)G.numel(),
-                                       cur_stream(G)));
+  RT_CHECK_HIP(rt::launch_wgrad_reduce(
+      slab.data_ptr<float>(), (int)slab.size(0), (long long)slab.size(1), G.data_ptr<float>(),
+      (int)G.numel(), cur_stream(G), two ? slab1->data_ptr<float>() : nullptr,
+      two ? (int)slab1->size(0) : 0, two ? (long long)slab1->size(1) : 0,
+      two ? G1->data_ptr<float>() : nullptr, two ? (int)G1->numel() : 0));
 }
 
 void check_csr(const torch::Tensor& indptr, const torch::Tensor& indices, const torch::Tensor& values) {
@@ -894,8 +907,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp3_grad_bucket_floats", [](int64_t H) { return (int64_t)rt::mlp3_grad_bucket_floats((int)H); });
   m.def("wgrad", &wgrad, "split-K weight-gradient GEMM (K = batch) into fp32 slabs",
         py::arg("A"), py::arg("M"), py::arg("Mout"), py::arg("Bm"), py::arg("N"), py::arg("slab"),
-        py::arg("offset"), py::arg("ldo"), py::arg("mask") = py::none(), py::arg("nout") = -1, py::arg("mask_hperm") = false);
-  m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs");
+        py::arg("offset"), py::arg("ldo"), py::arg("mask") = py::none(), py::arg("nout") = -1, py::arg("mask_hperm") = false,
+        py::arg("nsplit") = 1);
+  m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs (optionally a second region)",
+        py::arg("slab"), py::arg("G"), py::arg("slab1") = py::none(), py::arg("G1") = py::none());
   m.def("num_cus", [](int64_t dev) { return (int64_t)num_cus((int)dev); });
   m.def("gcn_agg_gemm", &gcn_agg_gemm, "K8: fused CSR aggregation + MFMA GEMM + bias/ReLU");
   m.def("gcn_l1_fused", &gcn_l1_fused, "K8: fused aggregation + W1 GEMM + ReLU + W2 transform (H1 stays in LDS)");

@@ -58,9 +58,10 @@ hipError_t launch_big_dz2(const void* h2a, int lda, const float* dy, const float
 hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm, int ldb, int N,
                         int K, int S, float* slab, int ldo, long long slab_stride, hipStream_t stream,
                         const void* mask = nullptr, int ldm = 0, int Nout = -1,
-                        bool mask_hperm = false);
+                        bool mask_hperm = false, int nsplit = 1);
 hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, float* G, int n,
-                               hipStream_t stream);
+                               hipStream_t stream, const float* slab1 = nullptr, int S1 = 0,
+                               long long slab_stride1 = 0, float* G1 = nullptr, int n1 = 0);
 size_t wgrad_lds_bytes(int NT);
 
 // ---- GCN route scorer (K8) : gcn.hip ----

@@ -4,8 +4,12 @@
 // (measured: 236 us for dW2 in a 465 us training step, profiles/train_step_hipblaslt.csv), because
 // they are really a streaming reduction over the batch.  This kernel is built for that shape:
 //
-//  * grid = (S k-slices, M/256 m-blocks); every workgroup streams ITS slice of batch rows exactly
-//    once from HBM, so all CUs pull bandwidth (a few large K-slices would leave the chip idle).
+//  * grid = (S k-slices, M/256 m-blocks, n-blocks of 32*NT columns); every workgroup streams ITS
+//    slice of batch rows once, so all CUs pull bandwidth (a few large K-slices would leave the chip
+//    idle).  With n-blocks, the nb workgroups of one slice share its A rows through L2 (same XCD
+//    when S*mblocks % 8 == 0: their ids differ by multiples of it) and the slice can be nb x longer
+//    for the same grid
+//    — nb x fewer fp32 slabs to write and reduce.
 //  * 32-row stages of A (256 cols) and Bm (32*NT cols) go through LDS with a row stride padded to
 //    64 (mod 256) bytes, so each ds_read_b64_tr_b16 (hardware transpose: a lane receives 4
 //    consecutive ROWS of its column) is bank-conflict-free; two such reads form the 8-deep k
@@ -83,6 +87,12 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int m_base = blockIdx.y * AW;
+  // n-block z: columns [n0, n0 + 32*NT) of Bm / the output (several workgroups per k-slice, so a
+  // slice can cover more batch rows for the same grid: fewer fp32 slabs to write and reduce)
+  const int n0 = blockIdx.z * BW;
+  Bm += n0;
+  N -= n0;
+  Nout -= n0;
   const int k_begin = blockIdx.x * kslice;
   const int k_end = min(K, k_begin + kslice);
 
@@ -169,7 +179,7 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
     }
   }
   // partial of this k-slice -> slab[blockIdx.x]
-  float* out = slab + (long long)blockIdx.x * slab_stride;
+  float* out = slab + (long long)blockIdx.x * slab_stride + n0;
   const int h = lane >> 5, col = lane & 31;
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
@@ -190,12 +200,26 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
 // the previous one-thread-per-column version ran 73 workgroups and 256 dependent loads per thread.
 constexpr int RED_SL = 16, RED_COLS = 16;
 
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, int S,
-                                                           long long slab_stride,
-                                                           float* __restrict__ G, int n) {
+// Two independent segments (slab regions with their own slice counts) in one launch: blocks
+// [0, nb0) reduce segment 0, the rest segment 1.
+struct RedSeg {
+  const float* slab;
+  long long slab_stride;
+  float* G;
+  int S, n;
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(RedSeg s0, RedSeg s1, int nb0) {
+  const bool second = (int)blockIdx.x >= nb0;
+  const RedSeg sg = second ? s1 : s0;
+  const float* __restrict__ slab = sg.slab;
+  const long long slab_stride = sg.slab_stride;
+  float* __restrict__ G = sg.G;
+  const int S = sg.S, n = sg.n;
+  const int blk = second ? (int)blockIdx.x - nb0 : (int)blockIdx.x;
   __shared__ float4 part[RED_SL][RED_COLS + 1];
   const int c = threadIdx.x & (RED_COLS - 1), sl = threadIdx.x / RED_COLS;
-  const int e = (blockIdx.x * RED_COLS + c) * 4;
+  const int e = (blk * RED_COLS + c) * 4;
   const bool vec = (slab_stride % 4) == 0 && e + 4 <= n;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e < n) {
@@ -248,11 +272,12 @@ size_t wgrad_lds_bytes(int NT, int KB) {
 }
 size_t wgrad_lds_bytes(int NT) { return wgrad_lds_bytes(NT, 32); }
 
-// rows staged per barrier: ROUTEST_WGRAD_KB = 32 | 64 | 128 (A/B knob)
+// rows staged per barrier: ROUTEST_WGRAD_KB = 32 | 64 (default: 2x the bytes in flight per CU,
+// wgrad<3> 23.7 -> 20.9 us, profiles/train_wgrad_ab_r2.md) | 128
 static int wgrad_kb() {
   static const int kb = [] {
     const char* v = std::getenv("ROUTEST_WGRAD_KB");
-    const int k = v ? std::atoi(v) : 32;
+    const int k = v ? std::atoi(v) : 64;
     return (k == 64 || k == 128) ? k : 32;
   }();
   return kb;
@@ -264,13 +289,14 @@ static hipError_t launch_wgrad_kb(const void* A, int lda, int M, int Mout, const
                                   hipStream_t stream, const void* mask, int ldm, int Nout) {
   const int kslice = ((K + S - 1) / S + 31) / 32 * 32;
   const int mblocks = (M + 255) / 256;
+  const int nblocks = (N + 32 * NT - 1) / (32 * NT);
   const size_t lds = wgrad_lds_bytes(NT, KB);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)wgrad_kernel<NT, MASK, KB, MPERM>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((wgrad_kernel<NT, MASK, KB, MPERM>), dim3(S, mblocks), dim3(512), lds, stream,
+  hipLaunchKernelGGL((wgrad_kernel<NT, MASK, KB, MPERM>), dim3(S, mblocks, nblocks), dim3(512), lds, stream,
                      (const __bf16*)A, lda, M, Mout, (const __bf16*)Bm, ldb, N, K, kslice, slab, ldo,
                      slab_stride, (const __bf16*)mask, ldm, Nout);
   return hipGetLastError();
@@ -291,12 +317,14 @@ static hipError_t launch_wgrad_nt(const void* A, int lda, int M, int Mout, const
 
 hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm, int ldb, int N,
                         int K, int S, float* slab, int ldo, long long slab_stride,
-                        hipStream_t stream, const void* mask, int ldm, int Nout, bool mask_hperm) {
+                        hipStream_t stream, const void* mask, int ldm, int Nout, bool mask_hperm,
+                        int nsplit) {
   if (M % 8 || N % 8 || lda % 8 || ldb % 8) return hipErrorInvalidValue;
   if (Nout < 0 || Nout > N) Nout = N;
-  const int NT = (N + 31) / 32;
+  if (nsplit < 1) nsplit = 1;
+  const int NT = ((N + 31) / 32 + nsplit - 1) / nsplit;     // n-tiles per workgroup
   if (mask != nullptr) {
-    if (ldm % 8 || NT != 1) return hipErrorInvalidValue;   // the dW1 shape (N = 16)
+    if (ldm % 8 || NT != 1 || N > 32) return hipErrorInvalidValue;   // the dW1 shape (N = 16)
     if (mask_hperm) {
       if (M % 16) return hipErrorInvalidValue;
       return launch_wgrad_kb<1, true, 32, true>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride,
@@ -319,9 +347,14 @@ hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm,
 }
 
 hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, float* G, int n,
-                               hipStream_t stream) {
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((n + 4 * RED_COLS - 1) / (4 * RED_COLS)), dim3(256), 0, stream, slab,
-                     S, slab_stride, G, n);
+                               hipStream_t stream, const float* slab1, int S1,
+                               long long slab_stride1, float* G1, int n1) {
+  const RedSeg s0{slab, slab_stride, G, S, n};
+  const RedSeg s1{slab1, slab_stride1, G1, S1, slab1 ? n1 : 0};
+  const int nb0 = (n + 4 * RED_COLS - 1) / (4 * RED_COLS);
+  const int nb1 = (s1.n + 4 * RED_COLS - 1) / (4 * RED_COLS);
+  if (nb0 + nb1 == 0) return hipSuccess;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb0 + nb1), dim3(256), 0, stream, s0, s1, nb0);
   return hipGetLastError();
 }
 

@@ -168,8 +168,19 @@ class FusedMlp3Trainer:
         self.h2a = torch.empty(B, H + 16, dtype=bf, device=d)
         self.dz2 = torch.empty(B, H, dtype=bf, device=d)
         self.dyb = torch.empty(B, 8, dtype=bf, device=d)
+        # dW2|db2 (the big block): nsplit column blocks per k-slice, so each slice covers nsplit x
+        # more batch rows for the same ~one-workgroup-per-CU grid -> nsplit x fewer fp32 slabs.
+        # dW3|db3 and dW1 (small outputs, operands as big as dW2's) keep one slice per CU.
+        ldg = H + 16
+        self.nsplit = int(os.environ.get("ROUTEST_WGRAD_NSPLIT", "3"))
         self.S = self._slices(B)
-        self.slab = torch.empty(self.S, self.G.numel(), dtype=torch.float32, device=d)
+        ntt = (ldg + 31) // 32
+        nt = -(-ntt // max(1, self.nsplit))
+        nblk = -(-ntt // nt)                       # n-blocks the kernel actually launches
+        # the nblk workgroups of a slice share its dz2 rows through one XCD's L2 when S2 % 8 == 0
+        self.S2 = max(1, (self.S // nblk) // 8 * 8 or self.S // nblk)
+        self.slab2 = torch.empty(self.S2, H * ldg, dtype=torch.float32, device=d)
+        self.slab = torch.empty(self.S, self.G.numel() - H * ldg, dtype=torch.float32, device=d)
         self.dz1 = torch.empty(B, H, dtype=bf, device=d)
         self.sq_err = torch.zeros(B, dtype=torch.float32, device=d)      # per-row squared errors
         self.loss_tiles = self.sq_err                                      # (older name)
@@ -190,13 +201,13 @@ class FusedMlp3Trainer:
                              self.xf, self.h1a, self.h2a, self.dz2, self.dz1, self.dyb,
                              self.sq_err, self.step_ctr)
         ldg = H + 16
-        C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab, 0, ldg)
+        C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit)
         # dW3|db3 = (h2a^T dy)^T: the unit axis (H+16) is the MFMA M side so all 8 waves of a
         # workgroup work (dy as M = 8 rows left 7 of them idle); only column 0 of dy is real
-        C.wgrad(self.h2a, ldg, ldg, self.dyb, 8, self.slab, H * ldg, 1, None, 1)
+        C.wgrad(self.h2a, ldg, ldg, self.dyb, 8, self.slab, 0, 1, None, 1)
         # dW1 = dz1^T x (relu'(z1) applied by the forward kernel)
-        C.wgrad(self.dz1, H, H, self.xf, 16, self.slab, H * ldg + ldg, 16)
-        C.wgrad_reduce(self.slab, self.G)
+        C.wgrad(self.dz1, H, H, self.xf, 16, self.slab, ldg, 16)
+        C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg:])
 
     def step(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> torch.Tensor:
         """One optimizer step; returns the device tensor of per-row squared errors (no sync)."""
