@@ -205,6 +205,18 @@ def main() -> None:
     torch.cuda.synchronize()
     elapsed = pipe.timed(a.warmup, a.steps)
 
+    # whole-node runs: what the xGMI links delivered, measured on the same ranks right after the
+    # timed region (RCCL all-reduce / all-gather sweep; extra JSON key, outside the timing)
+    coll = None
+    if world > 1 and not share and os.environ.get("ROUTEST_BENCH_COLLECTIVES", "1") != "0":
+        # RCCL only (the process group bench.py already holds): nothing here can leave one rank
+        # waiting on a set-up step another rank skipped
+        from routest_amd.parallel.collective_probe import sweep
+        try:
+            coll = sweep(dev)
+        except Exception as e:  # noqa: BLE001 - the headline line must still print
+            coll = [{"error": repr(e)[:200]}]
+
     # the link bound: the record DMA alone, same bytes, same stream (what the step cannot beat)
     h2d_only_ms = None
     if a.io == "hybrid":
@@ -357,6 +369,7 @@ def main() -> None:
                               8: "8 B compact: fp32 distance, fp16 age, host weekday/hour",
                               16: "16 B full: fp32 distance, fp32 age, epoch seconds (kernel featurises)"}[a.rec],
             "shared_gpu": bool(share and world > 1),
+            "collectives": coll,
             "check_max_err_vs_emulation": err_emu,
             "check_max_err_vs_fp32": err_fp32,
             "finite": ok,
