@@ -5,6 +5,7 @@
 //   big_layer1_kernel  : records -> featurize -> layer 1 (MFMA 32x32x16, W1k fragments from L2)
 //                        -> h1 bf16 [B, ld] in the hperm() unit order (16-byte stores); training
 //                        also writes xf and the h1a ones-column.
+//   gemm256_kernel     : the default for N % 256 == 0, K % 64 == 0 (see its comment below);
 //   gemm_nt_kernel     : D = W^T-side GEMM  Z^T[n][m] = sum_k W[n][k] X[m][k]  (both operands
 //                        row-major with K contiguous, bf16, fp32 accumulate), 128 x 128 tiles,
 //                        4 waves of 64 x 64, K in 32-deep stages through LDS (16-byte row reads,
@@ -21,6 +22,8 @@
 //   w1p [H/32][64 lanes][8] bf16 (as mlp3_tile.h), w2k [H][H] bf16 row-major with K columns in
 //   hperm order (w2k[n][c] = W2[n][hperm(c)]), w2t [H][H] bf16 row-major = W2^T with K (output
 //   unit) columns in hperm order (training only), b2 / w3 f32 in natural order.
+#include <cstdlib>
+
 #include "common.h"
 #include "ops.h"
 
@@ -239,6 +242,144 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// gemm256_kernel: the same three products on 256 x 256 tiles (units x batch rows), 8 waves of
+// 128 x 64 on mfma_f32_16x16x32_bf16 (32 accumulators of 4 = 128 VGPRs), K in 64-deep stages.
+// Both operand tiles go global -> LDS with global_load_lds_dwordx4 (no VGPR staging, no ds_write
+// pass): each wave-instruction writes 1 KB of the LDS image lane-linearly, so the XOR swizzle is
+// applied to the per-lane GLOBAL address — row r's 16-byte chunk c lives at slot c ^ ((r >> 1) & 7)
+// of its 128-byte LDS row, which makes each 16-lane group of a ds_read_b128 fragment read (16
+// consecutive rows, one chunk) hit 16 distinct 16-byte bank groups.  Two stages (128 KB LDS, one
+// workgroup per CU): the loads of stage k+1 are in flight under stage k's 64 MFMAs per wave.
+// Workgroups are remapped XCD-aware (bijective for any grid) so the N/256 unit tiles of one
+// batch-row block run on one XCD and share its X tile through that XCD's L2.
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int G2T = 256, G2K = 64;
+constexpr int G2_STAGE = 2 * G2T * G2K * 2;          // A + B tile bytes per stage (64 KB)
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm2[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int bid = blockIdx.x;
+  {
+    const int nb = gridDim.x, xcd = bid & 7, q = nb >> 3, r = nb & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int tn = bid % a.tiles_n, tm = bid / a.tiles_n;
+  const int n0 = tn * G2T, m0 = tm * G2T;
+  const int wu = w & 1, wr = w >> 1;                 // units [128wu, +128) x rows [64wr, +64)
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // staging: thread t moves chunk q*512 + t of each tile (q = 0..3): row q*64 + (t >> 3), LDS
+  // slot t & 7, global chunk (t & 7) ^ ((t >> 4) & 7) — the same for every q
+  const int srow = tid >> 3, schunk = (tid & 7) ^ ((tid >> 4) & 7);
+  const __bf16* ga = a.W + (size_t)(n0 + srow) * a.ldw + 8 * schunk;
+  const __bf16* gb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) gb[q] = a.X + (size_t)min(m0 + 64 * q + srow, a.M - 1) * a.ldx + 8 * schunk;
+  typedef __attribute__((address_space(3))) void lds_void;
+  auto issue = [&](int kt, int s) {
+    unsigned char* st = sm2 + s * G2_STAGE;
+    const int k0 = kt * G2K;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      __builtin_amdgcn_global_load_lds((const void*)(ga + (size_t)(64 * q) * a.ldw + k0),
+                                       (lds_void*)(st + (q * 8 + w) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gb[q] + k0),
+                                       (lds_void*)(st + G2T * G2K * 2 + (q * 8 + w) * 1024), 16, 0, 0);
+    }
+  };
+
+  // fragment offsets: row 16i + (lane & 15) of the wave's block, k chunk 4ks + (lane >> 4)
+  const int fr = lane & 15, sw = (lane >> 1) & 7;
+  const int offa = (128 * wu + fr) * 128, offb = G2T * G2K * 2 + (64 * wr + fr) * 128;
+  const int nk = a.K / G2K;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int s = kt & 1;
+    if (kt + 1 < nk) issue(kt + 1, s ^ 1);
+    const unsigned char* st = sm2 + s * G2_STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int co = ((4 * ks + (lane >> 4)) ^ sw) << 4;
+      bf16x8 fa[8], fb[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(st + offa + i * 2048 + co);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(st + offb + j * 2048 + co);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stage k+1 landed
+    __syncthreads();                                    // ... and stage k fully read
+  }
+
+  // epilogue: acc[i][j] element e = Z^T[unit n0 + 128wu + 16i + 4g + e][row m0 + 64wr + 16j + fr]
+  // (g = lane >> 4); hperm swaps unit bits 2, 3: stored position 16i + 4 swap2(g) + e
+  const int g = lane >> 4, gp = ((g & 1) << 1) | (g >> 1);
+  const int ub = n0 + 128 * wu;
+  if constexpr (EPI == EPI_STORE) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + 64 * wr + 16 * j + fr;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (__bf16)acc[i][j][e];
+        *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + ub + 16 * i + 4 * gp) = o;
+      }
+    }
+  } else {
+    f32x4 bv[8], wv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bv[i] = *reinterpret_cast<const f32x4*>(a.b2 + ub + 16 * i + 4 * g);
+      wv[i] = *reinterpret_cast<const f32x4*>(a.w3 + ub + 16 * i + 4 * g);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + 64 * wr + 16 * j + fr;
+      float ys[2] = {0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = relu_f(acc[i][j][e] + bv[i][e]);
+          ys[i >> 2] = __builtin_fmaf(v, wv[i][e], ys[i >> 2]);
+          o[e] = (__bf16)v;
+        }
+        if constexpr (EPI == EPI_H2Y) {
+          if (m < a.M) *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + ub + 16 * i + 4 * gp) = o;
+        }
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        ys[hh] += __shfl_xor(ys[hh], 16);
+        ys[hh] += __shfl_xor(ys[hh], 32);
+      }
+      if (g == 0 && m < a.M) {
+        float* yp = a.ypart + (size_t)m * (a.N / 64) + (ub >> 6);
+        yp[0] = ys[0];
+        yp[1] = ys[1];
+      }
+    }
+  }
+}
+
 // y = sum_j ypart[m][j] + b3 (fixed order: deterministic).  Training (target != null): dy, the
 // bf16 dy operand [B,8] (col 0), squared error.
 __global__ __launch_bounds__(256) void big_yreduce_kernel(const float* __restrict__ ypart, int nparts,
@@ -415,11 +556,46 @@ hipError_t launch_big_layer1(const void* rec, int rec_bytes, int B, const void* 
   return hipGetLastError();
 }
 
-hipError_t launch_gemm_nt(int epi, const void* W, int ldw, const void* X, int ldx, int N, int M,
+// 256 (default where the shape allows) or 128: ROUTEST_GEMM_TILE A/B knob
+static int gemm_tile() {
+  static const int t = [] {
+    const char* v = std::getenv("ROUTEST_GEMM_TILE");
+    return (v && std::atoi(v) == 128) ? 128 : 256;
+  }();
+  return t;
+}
+
+template <int EPI>
+static hipError_t launch_g256(const GemmArgs& a, dim3 grid, dim3 block, int lds, hipStream_t stream) {
+  static bool attr[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!attr[dev & 63]) {
+    const hipError_t e = hipFuncSetAttribute((const void*)gemm256_kernel<EPI>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr[dev & 63] = true;
+  }
+  hipLaunchKernelGGL(gemm256_kernel<EPI>, grid, block, lds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm_nt(int epi,const void* W, int ldw, const void* X, int ldx, int N, int M,
                           int K, const float* b2, const float* w3, float* ypart, void* out,
                           int ldo, hipStream_t stream) {
   if (M <= 0) return hipSuccess;
   if (N % GT || K % GK || ldw % 8 || ldx % 8 || (out != nullptr && ldo % 8)) return hipErrorInvalidValue;
+  if (N % G2T == 0 && K % G2K == 0 && gemm_tile() == 256) {
+    GemmArgs a{(const __bf16*)W, (const __bf16*)X, ldw, ldx, N, M, K, b2, w3, ypart, (__bf16*)out, ldo, N / G2T};
+    const dim3 grid((unsigned)((N / G2T) * ((M + G2T - 1) / G2T))), block(512);
+    const int lds = 2 * G2_STAGE;
+    switch (epi) {
+      case EPI_Y: return launch_g256<EPI_Y>(a, grid, block, lds, stream);
+      case EPI_H2Y: return launch_g256<EPI_H2Y>(a, grid, block, lds, stream);
+      case EPI_STORE: return launch_g256<EPI_STORE>(a, grid, block, lds, stream);
+      default: return hipErrorInvalidValue;
+    }
+  }
   GemmArgs a{(const __bf16*)W, (const __bf16*)X, ldw, ldx, N, M, K, b2, w3, ypart, (__bf16*)out, ldo, N / GT};
   const dim3 grid((unsigned)((N / GT) * ((M + GT - 1) / GT))), block(256);
   switch (epi) {
