@@ -173,6 +173,26 @@ static rt::NormParams norm_params(const std::vector<double>& norm) {
 }
 
 // records may be pinned host memory (zero-copy) or on the GPU; h1 (and xf) on the GPU.
+// wide-MLP inference in one launch: records -> layer 1 -> layer 2 -> relu.w3 partials (mlp_big.hip)
+void big_fused(torch::Tensor records, torch::Tensor w1q, torch::Tensor w2f, torch::Tensor b2,
+               torch::Tensor w3, int64_t H, std::vector<double> norm, torch::Tensor ypart) {
+  const int rb = record_bytes(records);
+  for (auto* t : {&w1q, &w2f, &b2, &w3, &ypart}) check_dev(*t, "big_fused operand");
+  TORCH_CHECK(H % 256 == 0, "big_fused needs H % 256 == 0");
+  TORCH_CHECK(w1q.scalar_type() == torch::kBFloat16 && w1q.numel() == H * 16, "w1q must be bf16 [H*16]");
+  TORCH_CHECK(w2f.scalar_type() == torch::kBFloat16 && w2f.numel() == H * H, "w2f must be bf16 [H, H]");
+  TORCH_CHECK(b2.scalar_type() == torch::kFloat32 && b2.numel() == H && w3.scalar_type() == torch::kFloat32 &&
+                  w3.numel() == H, "b2 / w3 must be f32 [H]");
+  TORCH_CHECK(ypart.scalar_type() == torch::kFloat32 && ypart.numel() >= records.size(0) * (H / 64),
+              "ypart must be f32 [B, H/64]");
+  TORCH_CHECK(!records.is_cuda() || records.device() == w2f.device(), "records on the weights' device");
+  TORCH_CHECK(records.size(0) < (1LL << 31) - 256, "batch too large");
+  const c10::DeviceGuard guard(w2f.device());
+  RT_CHECK_HIP(rt::launch_big_fused(kernel_ptr(records, "records"), rb, (int)records.size(0), w1q.data_ptr(), w2f.data_ptr(),
+                                    (int)H, norm_params(norm), b2.data_ptr<float>(), w3.data_ptr<float>(),
+                                    ypart.data_ptr<float>(), cur_stream(w2f)));
+}
+
 void big_layer1(torch::Tensor records, torch::Tensor w1p, int64_t H, std::vector<double> norm,
                 torch::Tensor h1, c10::optional<torch::Tensor> xf) {
   const int rb = record_bytes(records);
@@ -890,6 +910,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("big_layer1", &big_layer1, "wide MLP: featurize + layer 1 -> h1 (hperm order)",
         py::arg("records"), py::arg("w1p"), py::arg("H"), py::arg("norm"), py::arg("h1"),
         py::arg("xf") = py::none());
+  m.def("big_fused", &big_fused, "wide MLP inference: featurize + layer 1 + layer 2 + relu.w3 partials, one launch");
   m.def("gemm_nt", &gemm_nt, "wide MLP layer GEMM Z^T = W X^T with fused epilogues (0 y-partials, 1 +h2, 2 store)",
         py::arg("epi"), py::arg("W"), py::arg("X"), py::arg("N"), py::arg("M"), py::arg("K"),
         py::arg("b2") = py::none(), py::arg("w3") = py::none(), py::arg("ypart") = py::none(),

@@ -380,6 +380,150 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// mlp_big_fused_kernel (inference): records -> featurize -> layer 1 -> layer 2 -> relu.w3 partials
+// in ONE launch, so h1 never goes to HBM (at H = 1024 that is 2 KB per row written by a layer-1
+// kernel and read back by the GEMM: 23 % of the unfused time).  Tiles and waves as gemm256_kernel
+// (256 units x 256 rows, 8 waves of 128 x 64); only W2 is staged (global_load_lds, 2 x 32 KB).
+// Each wave computes the B fragments of its own 64 rows per 64-deep K stage on MFMA:
+//   h1^T block = W1k[16 units][16] . x^T[16][16 rows]   (mfma_f32_16x16x16bf16_1k, K = 16: the 12
+//   features + hi/lo-split inputs + the two constant-1 slots that carry b1)
+// lane (g = l >> 4, row l & 15) gets units 4g .. 4g+3 of the block; two blocks s = 0, 1 of a
+// 32-unit chunk, relu'd and packed, are exactly one 16x16x32 B fragment when the chunk's K order
+// is p = 8g + 4s + j  <->  unit 16s + 4g + j — the host packs W2's columns in that order (w2f).
+// x^T stays in 8 VGPRs for the whole tile (featurized once); W1k fragments (w1q) sit in LDS.
+struct FusedArgs {
+  const void* rec;
+  int B, H;
+  const __bf16* w1q;   // [H/16][64 lanes][4]: W1k[16ub + (l & 15)][4(l >> 4) + j]
+  const __bf16* w2f;   // [H][H] row-major, K columns in the chunk order above
+  const float* b2;
+  const float* w3;
+  float* ypart;        // [B][H/64]
+  int tiles_n;
+  NormParams np;
+};
+
+typedef short s16x4v __attribute__((ext_vector_type(4)));
+
+template <int RB>
+__global__ __launch_bounds__(512, 1) void mlp_big_fused_kernel(FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm3[];   // [2 x 32 KB W2 | w1q]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int bid = blockIdx.x;
+  {
+    const int nb = gridDim.x, xcd = bid & 7, q = nb >> 3, r = nb & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int tn = bid % a.tiles_n, tm = bid / a.tiles_n;
+  const int n0 = tn * G2T, m0 = tm * G2T;
+  const int wu = w & 1, wr = w >> 1;
+  const int g = lane >> 4, fr = lane & 15;
+  constexpr int ABYTES = G2T * G2K * 2;              // one W2 stage
+  unsigned char* w1s = sm3 + 2 * ABYTES;
+
+  // W2 stage 0 in flight first, then W1k fragments into LDS (plain 16-byte copies) and the
+  // features of the wave's 64 rows (x^T fragments: features 4g .. 4g+3 of row 16jr + fr)
+  const int srow = tid >> 3, schunk = (tid & 7) ^ ((tid >> 4) & 7);
+  const __bf16* ga = a.w2f + (size_t)(n0 + srow) * a.H + 8 * schunk;
+  typedef __attribute__((address_space(3))) void lds_void;
+  auto issue = [&](int kt, int s) {
+    unsigned char* st = sm3 + s * ABYTES;
+    const int k0 = kt * G2K;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)(ga + (size_t)(64 * q) * a.H + k0),
+                                       (lds_void*)(st + (q * 8 + w) * 1024), 16, 0, 0);
+  };
+  {
+    const int n16 = a.H * 16 * 2 / 16;               // w1q bytes / 16
+    const int4* src = reinterpret_cast<const int4*>(a.w1q);
+    int4* dst = reinterpret_cast<int4*>(w1s);
+    for (int i = tid; i < n16; i += 512) dst[i] = src[i];
+  }
+  s16x4v xk[4];
+#pragma unroll
+  for (int jr = 0; jr < 4; ++jr) {
+    const int row = min(m0 + 64 * wr + 16 * jr + fr, a.B - 1);
+    const bf16x8 f8 = BigRec<RB>::feat(a.rec, row, g >> 1, a.np);
+    const bf16x4 x4 = (g & 1) ? __builtin_shufflevector(f8, f8, 4, 5, 6, 7)
+                              : __builtin_shufflevector(f8, f8, 0, 1, 2, 3);
+    xk[jr] = __builtin_bit_cast(s16x4v, x4);
+  }
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int sw = (lane >> 1) & 7;
+  const int offa = (128 * wu + fr) * 128;
+  const int nk = a.H / G2K;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int s = kt & 1;
+    if (kt + 1 < nk) issue(kt + 1, s ^ 1);
+    const unsigned char* st = sm3 + s * ABYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // layer 1 for units kt*64 + 32ks .. +31 (two 16-unit blocks) x the wave's 4 row blocks
+      const int ub = kt * 4 + 2 * ks;
+      const s16x4v w10 = *reinterpret_cast<const s16x4v*>(w1s + ((ub * 64 + lane) << 3));
+      const s16x4v w11 = *reinterpret_cast<const s16x4v*>(w1s + (((ub + 1) * 64 + lane) << 3));
+      bf16x8 fb[4];
+#pragma unroll
+      for (int jr = 0; jr < 4; ++jr) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w10, xk[jr], z, 0, 0, 0);
+        const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w11, xk[jr], z, 0, 0, 0);
+        float t[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+        relu_cvt_bf16x8(t, &fb[jr]);
+      }
+      const int co = ((4 * ks + g) ^ sw) << 4;
+      bf16x8 fa[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(st + offa + i * 2048 + co);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue (as gemm256_kernel EPI_Y): relu(z + b2) . w3 per (row, 64-unit block)
+  const int ub0 = n0 + 128 * wu;
+  f32x4 bv[8], wv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    bv[i] = *reinterpret_cast<const f32x4*>(a.b2 + ub0 + 16 * i + 4 * g);
+    wv[i] = *reinterpret_cast<const f32x4*>(a.w3 + ub0 + 16 * i + 4 * g);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + 64 * wr + 16 * j + fr;
+    float ys[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ys[i >> 2] = __builtin_fmaf(relu_f(acc[i][j][e] + bv[i][e]), wv[i][e], ys[i >> 2]);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      ys[hh] += __shfl_xor(ys[hh], 16);
+      ys[hh] += __shfl_xor(ys[hh], 32);
+    }
+    if (g == 0 && m < a.B) {
+      float* yp = a.ypart + (size_t)m * (a.H / 64) + (ub0 >> 6);
+      yp[0] = ys[0];
+      yp[1] = ys[1];
+    }
+  }
+}
+
 // y = sum_j ypart[m][j] + b3 (fixed order: deterministic).  Training (target != null): dy, the
 // bf16 dy operand [B,8] (col 0), squared error.
 __global__ __launch_bounds__(256) void big_yreduce_kernel(const float* __restrict__ ypart, int nparts,
@@ -605,6 +749,36 @@ hipError_t launch_gemm_nt(int epi,const void* W, int ldw, const void* X, int ldx
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+hipError_t launch_big_fused(const void* rec, int rec_bytes, int B, const void* w1q, const void* w2f,
+                            int H, const NormParams& np, const float* b2, const float* w3,
+                            float* ypart, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  if (H % G2T) return hipErrorInvalidValue;
+  FusedArgs a{rec, B, H, (const __bf16*)w1q, (const __bf16*)w2f, b2, w3, ypart, H / G2T, np};
+  const dim3 grid((unsigned)((H / G2T) * ((B + G2T - 1) / G2T))), block(512);
+  const int lds = 2 * G2T * G2K * 2 + H * 32;
+  auto go = [&](auto kern) -> hipError_t {
+    static bool attr[64] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (!attr[dev & 63]) {
+      // sized once for the largest H (1024): 64 KB of W2 stages + 32 KB of W1k fragments
+      const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               2 * G2T * G2K * 2 + 1024 * 32);
+      if (e != hipSuccess) return e;
+      attr[dev & 63] = true;
+    }
+    hipLaunchKernelGGL(kern, grid, block, lds, stream, a);
+    return hipGetLastError();
+  };
+  switch (rec_bytes) {
+    case 16: return go(mlp_big_fused_kernel<16>);
+    case 8: return go(mlp_big_fused_kernel<8>);
+    case 6: return go(mlp_big_fused_kernel<6>);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_big_yreduce(const float* ypart, int nparts, int B, float b3, const float* b3p,

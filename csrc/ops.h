@@ -44,6 +44,9 @@ hipError_t launch_big_layer1(const void* rec, int rec_bytes, int B, const void* 
 hipError_t launch_gemm_nt(int epi, const void* W, int ldw, const void* X, int ldx, int N, int M,
                           int K, const float* b2, const float* w3, float* ypart, void* out,
                           int ldo, hipStream_t stream);
+hipError_t launch_big_fused(const void* rec, int rec_bytes, int B, const void* w1q, const void* w2f,
+                            int H, const NormParams& np, const float* b2, const float* w3,
+                            float* ypart, hipStream_t stream);
 hipError_t launch_big_yreduce(const float* ypart, int nparts, int B, float b3, const float* b3p,
                               float* y, const float* target, float gscale, float* dy, void* dyb,
                               float* sq_err, hipStream_t stream);

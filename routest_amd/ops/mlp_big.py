@@ -14,6 +14,7 @@ the target scale folded into w3 / b3.  :func:`emulate_big` mirrors the numerics 
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import numpy as np
@@ -28,6 +29,14 @@ BIG_HIDDEN = (512, 1024)
 def hperm(H: int) -> torch.Tensor:
     u = torch.arange(H)
     return (u & ~12) | ((u & 4) << 1) | ((u & 8) >> 1)
+
+
+def fused_korder(H: int) -> torch.Tensor:
+    """Unit feeding K position c of the fused kernel's layer-2 operand: within each 32-chunk,
+    p = 8g + 4s + j holds unit 16s + 4g + j."""
+    c = torch.arange(H)
+    p = c & 31
+    return (c & ~31) + 16 * ((p >> 2) & 1) + 4 * (p >> 3) + (p & 3)
 
 
 class PackedBig:
@@ -50,6 +59,14 @@ class PackedBig:
         self.w3 = p.w3.float().contiguous().to(device)
         self.w1k = p.w1k                                                          # fp32, for emulation
         self.w2 = p.w2
+        # fused inference kernel (mlp_big_fused_kernel): W1k as 16x16x16 A fragments
+        # w1q[ub][l][j] = W1k[16ub + (l & 15)][4(l >> 4) + j], and W2 with each 32-column K chunk in
+        # the order p = 8g + 4s + j <-> unit 16s + 4g + j (the layer-1 MFMA output packing)
+        lane = torch.arange(64)
+        rows = 16 * torch.arange(H // 16)[:, None, None] + (lane & 15)[None, :, None]
+        cols = 4 * (lane >> 4)[None, :, None] + torch.arange(4)[None, None, :]
+        self.w1q = p.w1k[rows, cols].to(torch.bfloat16).contiguous().to(device)
+        self.w2f = p.w2[:, fused_korder(H)].to(torch.bfloat16).contiguous().to(device)
 
 
 class EtaMlpBigKernel:
@@ -62,6 +79,7 @@ class EtaMlpBigKernel:
         self.packed = PackedBig(model.float().cpu().eval(), self.device)
         self.chunk = chunk_rows
         self._ws = None
+        self._yp = None
 
     def _workspace(self, rows: int):
         H = self.hidden
@@ -70,15 +88,29 @@ class EtaMlpBigKernel:
                         torch.empty(rows, H // 64, dtype=torch.float32, device=self.device))
         return self._ws
 
+    # one launch (featurize + both layers, h1 never in HBM) when H % 256 == 0; ROUTEST_BIG_FUSED=0
+    # selects the three-launch path (layer-1 kernel -> h1 in HBM -> GEMM)
+    FUSED = os.environ.get("ROUTEST_BIG_FUSED", "1") != "0"
+
     def _run(self, rec: torch.Tensor, out: torch.Tensor) -> None:
         C, p, H = self._C, self.packed, self.hidden
         B = rec.shape[0]
+        fused = self.FUSED and H % 256 == 0
         for s in range(0, B, self.chunk):
             n = min(self.chunk, B - s)
-            h1, yp = self._workspace(n)
-            C.big_layer1(rec[s:s + n], p.w1p, H, p.norm, h1[:n])
-            C.gemm_nt(0, p.w2k, h1, H, n, H, b2=p.b2, w3=p.w3, ypart=yp)
+            if fused:
+                yp = self._ypart(n)
+                C.big_fused(rec[s:s + n], p.w1q, p.w2f, p.b2, p.w3, H, p.norm, yp)
+            else:
+                h1, yp = self._workspace(n)
+                C.big_layer1(rec[s:s + n], p.w1p, H, p.norm, h1[:n])
+                C.gemm_nt(0, p.w2k, h1, H, n, H, b2=p.b2, w3=p.w3, ypart=yp)
             C.big_yreduce(yp[:n].reshape(-1), H // 64, p.b3, y=out[s:s + n])
+
+    def _ypart(self, rows: int) -> torch.Tensor:
+        if self._yp is None or self._yp.shape[0] < rows:
+            self._yp = torch.empty(rows, self.hidden // 64, dtype=torch.float32, device=self.device)
+        return self._yp
 
     def __call__(self, rec: torch.Tensor) -> torch.Tensor:
         out = torch.empty(rec.shape[0], dtype=torch.float32, device=self.device)

@@ -104,3 +104,29 @@ def test_gemm_nt_store_epilogue(M):
     got[:, hperm(N)] = out[:, :N].float().cpu()        # stored position c holds unit hperm(c)
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=0.15)
     assert (out[:, N:] == 0).all()
+
+
+@pytest.mark.parametrize("H", [512, 1024])
+@pytest.mark.parametrize("rb", [16, 6])
+def test_big_fused_equals_three_launch_path(H, rb):
+    """The one-launch kernel (layer 1 computed in-register per K stage, h1 never in HBM) against
+    the layer-1 kernel -> h1 -> GEMM path: same bf16 h1, same fp32 accumulation order per 32-k
+    chunk up to the K permutation, so the two agree to accumulation-order rounding."""
+    from routest_amd.models.features import records_to_compact6
+    from routest_amd.ops.eta_mlp import records6_to_tensor
+    from routest_amd.ops.mlp_big import EtaMlpBigKernel
+    m = _model(H, 5)
+    k = EtaMlpBigKernel(m, DEV)
+    rec, _ = synth_records(33_333, 6)
+    rt = records_to_tensor(rec) if rb == 16 else records6_to_tensor(records_to_compact6(rec))
+    rd = rt.to(DEV)
+    try:
+        EtaMlpBigKernel.FUSED = False
+        ref = k(rd).cpu()
+        EtaMlpBigKernel.FUSED = True
+        got = k(rd).cpu()
+    finally:
+        EtaMlpBigKernel.FUSED = True
+    spread = float((ref - ref.mean()).abs().mean())
+    assert torch.isfinite(got).all()
+    assert float((got - ref).abs().max()) / spread < 2e-3
