@@ -406,9 +406,9 @@ struct FusedArgs {
 
 typedef short s16x4v __attribute__((ext_vector_type(4)));
 
-template <int RB>
+template <int RB, int NS>
 __global__ __launch_bounds__(512, 1) void mlp_big_fused_kernel(FusedArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char sm3[];   // [2 x 32 KB W2 | w1q]
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm3[];   // [NS x 32 KB W2 | w1q]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int bid = blockIdx.x;
   {
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(512, 1) void mlp_big_fused_kernel(FusedArgs a) {
   const int wu = w & 1, wr = w >> 1;
   const int g = lane >> 4, fr = lane & 15;
   constexpr int ABYTES = G2T * G2K * 2;              // one W2 stage
-  unsigned char* w1s = sm3 + 2 * ABYTES;
+  unsigned char* w1s = sm3 + NS * ABYTES;
 
   // W2 stage 0 in flight first, then W1k fragments into LDS (plain 16-byte copies) and the
   // features of the wave's 64 rows (x^T fragments: features 4g .. 4g+3 of row 16jr + fr)
@@ -450,9 +450,28 @@ __global__ __launch_bounds__(512, 1) void mlp_big_fused_kernel(FusedArgs a) {
                               : __builtin_shufflevector(f8, f8, 0, 1, 2, 3);
     xk[jr] = __builtin_bit_cast(s16x4v, x4);
   }
+  // the features are finished (and their record loads retired) BEFORE the first W2 DMA: a use
+  // of an ordinary load's result below a global_load_lds makes the compiler drain every
+  // outstanding DMA with vmcnt(0)
+#pragma unroll
+  for (int jr = 0; jr < 4; ++jr) asm volatile("" : "+v"(xk[jr]) :: "memory");
+  const int nk = a.H / G2K;
   issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if constexpr (NS == 3) {
+    // stage 1 stays in flight across the first barrier: counted vmcnt + raw s_barrier (a
+    // __syncthreads() fence would drain every outstanding global_load_lds)
+    if (nk > 1) {
+      issue(1, 1);
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -461,10 +480,10 @@ __global__ __launch_bounds__(512, 1) void mlp_big_fused_kernel(FusedArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int sw = (lane >> 1) & 7;
   const int offa = (128 * wu + fr) * 128;
-  const int nk = a.H / G2K;
   for (int kt = 0; kt < nk; ++kt) {
-    const int s = kt & 1;
-    if (kt + 1 < nk) issue(kt + 1, s ^ 1);
+    const int s = kt % NS;
+    // the buffer refilled here was last read in iteration kt - 1, which every wave has left
+    if (kt + NS - 1 < nk) issue(kt + NS - 1, (kt + NS - 1) % NS);
     const unsigned char* st = sm3 + s * ABYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -491,8 +510,16 @@ __global__ __launch_bounds__(512, 1) void mlp_big_fused_kernel(FusedArgs a) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (NS == 3) {
+      // stage kt + 1 landed (stage kt + 2, if issued, stays in flight), then everyone is past kt
+      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
   // epilogue (as gemm256_kernel EPI_Y): relu(z + b2) . w3 per (row, 64-unit block)
@@ -751,6 +778,17 @@ hipError_t launch_gemm_nt(int epi,const void* W, int ldw, const void* X, int ldx
   return hipGetLastError();
 }
 
+// W2 stages in the fused kernel: 2 (default) or 3 (ROUTEST_BIG_STAGES=3: one stage kept in flight
+// across each raw s_barrier with a counted vmcnt — measured 4-8 % SLOWER here,
+// profiles/mlp_big_gemm256_r2.md: with 2 waves per SIMD the other wave already covers the DMA)
+static int big_stages() {
+  static const int n = [] {
+    const char* v = std::getenv("ROUTEST_BIG_STAGES");
+    return (v && std::atoi(v) == 3) ? 3 : 2;
+  }();
+  return n;
+}
+
 hipError_t launch_big_fused(const void* rec, int rec_bytes, int B, const void* w1q, const void* w2f,
                             int H, const NormParams& np, const float* b2, const float* w3,
                             float* ypart, hipStream_t stream) {
@@ -758,25 +796,29 @@ hipError_t launch_big_fused(const void* rec, int rec_bytes, int B, const void* w
   if (H % G2T) return hipErrorInvalidValue;
   FusedArgs a{rec, B, H, (const __bf16*)w1q, (const __bf16*)w2f, b2, w3, ypart, H / G2T, np};
   const dim3 grid((unsigned)((H / G2T) * ((B + G2T - 1) / G2T))), block(512);
-  const int lds = 2 * G2T * G2K * 2 + H * 32;
+  const int ns = big_stages();
+  const int lds = ns * G2T * G2K * 2 + H * 32;
   auto go = [&](auto kern) -> hipError_t {
     static bool attr[64] = {};
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (!attr[dev & 63]) {
-      // sized once for the largest H (1024): 64 KB of W2 stages + 32 KB of W1k fragments
+      // sized once for the largest H (1024): 3 x 32 KB of W2 stages + 32 KB of W1k fragments
       const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               2 * G2T * G2K * 2 + 1024 * 32);
+                                               3 * G2T * G2K * 2 + 1024 * 32);
       if (e != hipSuccess) return e;
       attr[dev & 63] = true;
     }
     hipLaunchKernelGGL(kern, grid, block, lds, stream, a);
     return hipGetLastError();
   };
-  switch (rec_bytes) {
-    case 16: return go(mlp_big_fused_kernel<16>);
-    case 8: return go(mlp_big_fused_kernel<8>);
-    case 6: return go(mlp_big_fused_kernel<6>);
+  switch (rec_bytes * 10 + ns) {
+    case 163: return go(mlp_big_fused_kernel<16, 3>);
+    case 83: return go(mlp_big_fused_kernel<8, 3>);
+    case 63: return go(mlp_big_fused_kernel<6, 3>);
+    case 162: return go(mlp_big_fused_kernel<16, 2>);
+    case 82: return go(mlp_big_fused_kernel<8, 2>);
+    case 62: return go(mlp_big_fused_kernel<6, 2>);
     default: return hipErrorInvalidValue;
   }
 }
