@@ -497,8 +497,9 @@ void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N
   TORCH_CHECK(M <= A.size(1) && N <= Bm.size(1) && Mout <= M, "M/N exceed operand widths");
   TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && A.size(1) % 8 == 0,
               "M, N and leading dims must be multiples of 8");
-  const int NT = (int)((N + 31) / 32);
-  TORCH_CHECK(NT >= 1 && NT <= 9, "unsupported N=", N, " (at most 288 columns per call)");
+  const int NT = (int)(((N + 31) / 32 + std::max<int64_t>(nsplit, 1) - 1) / std::max<int64_t>(nsplit, 1));
+  TORCH_CHECK(NT >= 1 && NT <= 9, "unsupported N=", N, " with nsplit=", nsplit,
+              " (at most 288 columns per n-block)");
   TORCH_CHECK(slab.scalar_type() == torch::kFloat32 && slab.dim() == 2, "slab must be f32 [S, stride]");
   TORCH_CHECK(nsplit >= 1 && (nsplit == 1 || !mptr), "nsplit >= 1 (1 with a mask)");
   TORCH_CHECK(offset + (Mout - 1) * ldo + nout <= slab.size(1), "slab region out of range");

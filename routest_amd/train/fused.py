@@ -278,9 +278,19 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
         self.ypart = torch.empty(B, H // 64, dtype=torch.float32, device=d)
         self.sq_err = torch.zeros(B, dtype=torch.float32, device=d)
         self.loss_tiles = self.sq_err
-        # k-slices: one slab per slice holds the whole bucket (4.3 MB at H = 1024): cap at 96 MB
-        self.S = self._slices(B, cap_bytes=96 << 20)
-        self.slab = torch.empty(self.S, self.G.numel(), dtype=torch.float32, device=d)
+        # dW2|db2 ([H, H+16], 4.3 MB at H = 1024) in ONE wgrad launch: ceil(tiles / 9) n-blocks x
+        # H/256 m-blocks per k-slice, and only as many k-slices as fill ~one workgroup per CU —
+        # 16 slices at H = 1024 (68 MB of slabs) instead of a whole-bucket slab per 256 rows
+        ntt = (ldg + 31) // 32
+        self.nsplit2 = -(-ntt // 9)
+        nt = -(-ntt // self.nsplit2)
+        nblk = -(-ntt // nt)
+        ncu = self.C.num_cus(d.index if d.index is not None else 0)
+        self.S2 = max(1, min(B // 256, ncu // (nblk * (H // 256))))
+        self.slab2 = torch.empty(self.S2, H * ldg, dtype=torch.float32, device=d)
+        # dW3|db3 and dW1 (small outputs): one k-slice per CU
+        self.S = self._slices(B)
+        self.slab = torch.empty(self.S, self.G.numel() - H * ldg, dtype=torch.float32, device=d)
 
     def _pack(self, update: bool) -> None:
         h = self.hp
@@ -302,14 +312,12 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
                       b3_dev=self.b3v)
         C.big_dz2(self.h2a, self.dy, self.w3v, H, self.dz2)
         C.gemm_nt(2, self.w2t, self.dz2, H, B, H, out=self.dh1)
-        # dW2|db2 = dz2^T [h1|1] in column blocks of <= 288 (9 MFMA n-tiles per wgrad launch)
-        for c0 in range(0, ldg, 288):
-            nb = min(288, ldg - c0)
-            C.wgrad(self.dz2, H, H, self.h1a[:, c0:c0 + nb], nb, self.slab, c0, ldg)
-        C.wgrad(self.h2a, ldg, ldg, self.dyb, 8, self.slab, H * ldg, 1, None, 1)
+        # dW2|db2 = dz2^T [h1|1]: one launch, n-blocks of <= 288 columns in the grid
+        C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit2)
+        C.wgrad(self.h2a, ldg, ldg, self.dyb, 8, self.slab, 0, 1, None, 1)
         # dW1 = (dh1 * relu'(h1))^T x: dh1 and its mask h1a are both in the hperm order here
-        C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, H * ldg + ldg, 16, self.h1a)
-        C.wgrad_reduce(self.slab, self.G)
+        C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, ldg, 16, self.h1a)
+        C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg:])
 
 
 def lr_at(step: int, lr: float, warmup: int, total: int, min_ratio: float) -> float:
