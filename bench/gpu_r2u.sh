@@ -1,0 +1,10 @@
+# training forward: blob staged with global_load_lds — tests, bench, stats
+ROOT=$GRAFT_REPO_ROOT
+cd $ROOT
+O=$ROOT/gpurun_out/r2u; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_train_gpu.py tests/test_multirank_gpu.py -k "train or fused or dp or wgrad" -x -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || exit 1
+timeout -k 10 120 python -u bench/train_bench.py --steps 200 --warmup 20 --modes fused,graph > $O/train.log 2>&1 || exit 2
+timeout -k 10 120 python -u bench/train_bench.py --steps 200 --warmup 20 --modes fused,graph >> $O/train.log 2>&1 || exit 2
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o train --output-format csv -- python3 $ROOT/bench/train_bench.py --steps 20 --warmup 5 --modes fused > $O/prof.log 2>&1 || exit 4
+echo done

@@ -277,13 +277,7 @@ __global__ __launch_bounds__(TPB, 1) void eta_mlp3_fwd16_kernel(const void* __re
   static_assert(L::W1B >= D * 1024, "the ring's over-read must stay inside the blob");
   (void)NF;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  {
-    const int4* src = reinterpret_cast<const int4*>(blob);
-    int4* dst = reinterpret_cast<int4*>(smem);
-    constexpr int N16 = (int)(L::BLOB / 16);
-    for (int i = threadIdx.x; i < N16; i += blockDim.x) dst[i] = src[i];
-    __syncthreads();
-  }
+  lds_fill_block(smem, blob, (int)L::BLOB);
   const bf16x8* w2p = reinterpret_cast<const bf16x8*>(smem);
   const i16x4* w1p = reinterpret_cast<const i16x4*>(smem + L::W2B);
   const float* b2 = reinterpret_cast<const float*>(smem + L::W2B + L::W1B);

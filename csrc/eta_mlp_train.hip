@@ -40,6 +40,7 @@
 // Natural column order is what makes relu'(z1) lane-local: dgrad accumulator register e of lane
 // half h is unit 32mi + 8(e>>2) + 4h + (e&3), element e&7 of the lane's own h1 fragment.
 // The rest of the blob is the inference layout (mlp3_tile.h): w1p, b1p, b2p, w3p, tail.
+#include "lds_fill.h"
 #include "mlp3_tile.h"
 #include "ops.h"
 
@@ -95,13 +96,7 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
   // captured HIP graph replays with correct bias corrections / LR schedule
   if (step_ctr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *step_ctr += 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  {
-    const int4* src = reinterpret_cast<const int4*>(blob);
-    int4* dst = reinterpret_cast<int4*>(smem);
-    constexpr int N16 = (int)(L::BLOB / 16);
-    for (int i = threadIdx.x; i < N16; i += blockDim.x) dst[i] = src[i];
-    __syncthreads();
-  }
+  lds_fill_block(smem, blob, (int)L::BLOB);
   const unsigned char* img = smem;
   const bf16x8* w1p = reinterpret_cast<const bf16x8*>(smem + L::W2B);
   const f32x4* b2p = reinterpret_cast<const f32x4*>(smem + L::W2B + L::W1B) + H / 4;
@@ -236,13 +231,23 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     for (int mt = 0; mt < MT; ++mt) {
       const f32x16 w3 = load_vec16(w3p, mt, h);
       const unsigned mk = (unsigned)((mt < 4 ? mask_lo >> (16 * mt) : mask_hi >> (16 * (mt - 4))) & 0xffffu);
+      // per output pair: two products, one v_cvt_pk_bf16_f32, and the pair's two mask bits
+      // sign-extended (v_bfe_i32) into a 0xFFFF / 0xFFFF0000 mask
+      typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+      typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        bf16x8 d;
+        u32x4v dw;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          d[j] = (__bf16)(((mk >> (8 * s + j)) & 1u) ? dy * w3[8 * s + j] : 0.f);
-        dz2f[2 * mt + s] = d;
+        for (int q2 = 0; q2 < 4; ++q2) {
+          const int b = 8 * s + 2 * q2;
+          const f32x2 pr = {dy * w3[b], dy * w3[b + 1]};
+          const unsigned cw = __builtin_bit_cast(unsigned, __builtin_convertvector(pr, bf16x2v));
+          const unsigned lo = (unsigned)(((int)(mk << (31 - b))) >> 31);
+          const unsigned hi = (unsigned)(((int)(mk << (30 - b))) >> 31);
+          dw[q2] = cw & ((lo & 0xFFFFu) | (hi & 0xFFFF0000u));
+        }
+        dz2f[2 * mt + s] = __builtin_bit_cast(bf16x8, dw);
       }
     }
     if (valid) {
@@ -261,15 +266,23 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       __bf16* zrow = dz1 + (size_t)row * H;
       // transposed reads: rows 16ks + 8t + 4h + q, columns 32mi + 16(g&1) + 4p (8-byte chunk
       // 8mi + 4(g&1) + p) -> chunk ^ ((q << 3) | (4(ks&1) + 2t + h))
+      // = 64 (mi ^ q) + 8 ((4(g&1) + p) ^ (4(ks&1) + 2t + h)): the lane part of the second term
+      // takes four values (ks parity x t), so four lane bases + a per-mi offset + immediates
+      // replace a full address computation per read
       const int g1 = (lv >> 4) & 1, p = lv & 3, q = (lv >> 2) & 3;
+      const int lx = 4 * g1 + p;
       const unsigned char* rb = img + (4 * h + q) * 512;
+      const unsigned char* bp[2][2];
+#pragma unroll
+      for (int par = 0; par < 2; ++par)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) bp[par][t] = rb + 4096 * t + 8 * (lx ^ (4 * par + 2 * t + h));
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi) {
-        const int ck = 8 * mi + 4 * g1 + p;
+        const int om = 64 * (mi ^ q);
         auto frag = [&](int ks) {
-          const int kx = 4 * (ks & 1) + h;
-          const unsigned char* r0 = rb + 8192 * ks + 8 * (ck ^ ((q << 3) | kx));
-          const unsigned char* r1 = rb + 8192 * ks + 4096 + 8 * (ck ^ ((q << 3) | (kx + 2)));
+          const unsigned char* r0 = bp[ks & 1][0] + om + 8192 * ks;
+          const unsigned char* r1 = bp[ks & 1][1] + om + 8192 * ks;
           const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<unsigned char*>(r0)));
           const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<unsigned char*>(r1)));
           return join4(lo, hi);
@@ -293,13 +306,23 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          // relu'(z1) from h1 (>= 0: nonzero bits <=> z1 > 0) as a select on the bf16 output
-          const bf16x8 hm = h1[2 * mi + s];
-          typedef short s16x8 __attribute__((ext_vector_type(8)));
-          const s16x8 hb = __builtin_bit_cast(s16x8, hm);
-          bf16x8 ov;
+          // relu'(z1) from h1 as a packed mask: h1 halves are non-negative bf16 bit patterns
+          // (0 .. 0x7F80), so x + 0x7FFF has bit 15 set iff x != 0 (iff z1 > 0) and no carry
+          // crosses into the other half; an arithmetic >> 15 per half spreads it to 0xFFFF.
+          // Per pair of outputs: one v_cvt_pk_bf16_f32, one add, one v_pk_ashrrev_i16, one and.
+          typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+          typedef short s16x2v __attribute__((ext_vector_type(2)));
+          typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+          const u32x4v hw = __builtin_bit_cast(u32x4v, h1[2 * mi + s]);
+          u32x4v ow;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) ov[j] = hb[j] != 0 ? (__bf16)acc[8 * s + j] : (__bf16)0.f;
+          for (int q2 = 0; q2 < 4; ++q2) {
+            const f32x2 pr = {acc[8 * s + 2 * q2], acc[8 * s + 2 * q2 + 1]};
+            const unsigned cw = __builtin_bit_cast(unsigned, __builtin_convertvector(pr, bf16x2v));
+            const s16x2v m = __builtin_bit_cast(s16x2v, hw[q2] + 0x7FFF7FFFu) >> (s16x2v){15, 15};
+            ow[q2] = cw & __builtin_bit_cast(unsigned, m);
+          }
+          const bf16x8 ov = __builtin_bit_cast(bf16x8, ow);
           if (valid) *reinterpret_cast<bf16x8*>(zrow + 32 * mi + 16 * s + 8 * h) = ov;   // hperm order
         }
       }

@@ -13,6 +13,7 @@
 // (row = node, k = feature) of mfma_f32_32x32x16_bf16.  W is staged into LDS once per workgroup in
 // B-fragment order (lane-linear 16-B reads).  The accumulator has the output feature on the lane,
 // so the bias is a per-lane scalar and each result register is one node's 32 contiguous outputs.
+#include "lds_fill.h"
 #include "common.h"
 #include "ops.h"
 
@@ -27,8 +28,8 @@ __global__ __launch_bounds__(256) void gcn_agg_gemm_kernel(
   constexpr int LDT = FIN + 8;  // padded LDS row (bf16 elements): conflict-free ds_read_b128
   __shared__ __attribute__((aligned(16))) bf16x8 s_w[NT * KS * 64];
   __shared__ __attribute__((aligned(16))) __bf16 s_t[4][32 * LDT];
-  for (int i = threadIdx.x; i < NT * KS * 64; i += blockDim.x) s_w[i] = wfrag[i];
-  __syncthreads();
+  lds_fill_block(reinterpret_cast<unsigned char*>(s_w), reinterpret_cast<const unsigned char*>(wfrag),
+                 NT * KS * 64 * 16);
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   __bf16* tile = s_t[w];
@@ -108,9 +109,10 @@ __global__ __launch_bounds__(256) void gcn_l1_fused_kernel(
   __shared__ __attribute__((aligned(16))) bf16x8 s_w1[NT1 * KS1 * 64];
   __shared__ __attribute__((aligned(16))) bf16x8 s_w2[NT2 * KS2 * 64];
   __shared__ __attribute__((aligned(16))) __bf16 s_t[4][TILE];
-  for (int i = threadIdx.x; i < NT1 * KS1 * 64; i += blockDim.x) s_w1[i] = w1frag[i];
-  for (int i = threadIdx.x; i < NT2 * KS2 * 64; i += blockDim.x) s_w2[i] = w2frag[i];
-  __syncthreads();
+  lds_fill_block(reinterpret_cast<unsigned char*>(s_w1), reinterpret_cast<const unsigned char*>(w1frag),
+                 NT1 * KS1 * 64 * 16);
+  lds_fill_block(reinterpret_cast<unsigned char*>(s_w2), reinterpret_cast<const unsigned char*>(w2frag),
+                 NT2 * KS2 * 64 * 16);
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   __bf16* tile = s_t[w];

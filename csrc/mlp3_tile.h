@@ -6,6 +6,7 @@
 //   [ w2p: (H/32)x(H/16)x64 lanes x 8 bf16 | w1p: (H/32)x64x8 bf16 | b1p | b2p | w3p (H f32 each,
 //     accumulator-register order) | tail: b3, 0, 0, 0 (f32) ]
 #pragma once
+#include "lds_fill.h"
 #include "common.h"
 
 namespace rt {
@@ -46,11 +47,7 @@ struct Mlp3View {
 template <int H>
 __device__ __forceinline__ void stage_blob(const unsigned char* __restrict__ blob, unsigned char* smem) {
   using L = Mlp3Layout<H>;
-  const int4* src = reinterpret_cast<const int4*>(blob);
-  int4* dst = reinterpret_cast<int4*>(smem);
-  constexpr int N16 = (int)(L::BLOB / 16);
-  for (int i = threadIdx.x; i < N16; i += blockDim.x) dst[i] = src[i];
-  __syncthreads();
+  lds_fill_block(smem, blob, (int)L::BLOB);
 }
 
 // 16 accumulator-order floats of a per-hidden vector for tile mt, lane half h.
