@@ -271,3 +271,28 @@ def test_forward_trained_model_relative_to_spread(trained256, variant):
     err = (got - ref).abs() / spread
     assert float(err.max()) < 0.03, float(err.max())
     assert float(err.mean()) < 0.005, float(err.mean())
+
+
+@pytest.mark.parametrize("huge", [True, False])
+def test_registered_host_buffers_zero_copy_and_dma(huge):
+    """_C.pinned_host_empty (2 MiB-aligned mapping, optional THP, hipHostRegister'ed) works both
+    as a copy-engine source and as the kernel's zero-copy input / output."""
+    from routest_amd.ops import _ext
+    C = _ext.native(required=True)
+    m = _model(256, 7)
+    k = EtaMlpKernel(m, torch.device("cuda:0"))
+    rec, _ = synth_records(70_001, 29)
+    src = records_to_tensor(rec)
+    host = C.pinned_host_empty(src.numel() * 4, huge).view(torch.int32).view(src.shape)
+    host.copy_(src)
+    assert host.is_pinned()
+    out = C.pinned_host_empty(len(rec) * 4, huge).view(torch.float32)
+    out.fill_(float("nan"))
+    ref = k(src.cuda()).cpu()
+    k.forward_hostio(host, out)                        # zero-copy records in, minutes out
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    dev = torch.empty_like(src, device="cuda")
+    dev.copy_(host, non_blocking=True)                 # DMA from the registered buffer
+    torch.cuda.synchronize()
+    assert torch.equal(dev.cpu(), src)
