@@ -57,6 +57,10 @@ def parse_args():
     ap.add_argument("--p50-requests", type=int, default=2000)
     ap.add_argument("--rec16-steps", type=int, default=10,
                     help="also time this many steps on full 16-byte records (extra JSON key)")
+    ap.add_argument("--train-steps", type=int, default=30,
+                    help="also time this many data-parallel training steps of the same MLP on the "
+                         "same ranks (64k rows per GPU, one flat-bucket RCCL all-reduce per step; "
+                         "extra JSON key 'dp_training')")
     return ap.parse_args()
 
 
@@ -177,14 +181,22 @@ def main() -> None:
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
+            # per-step completion times (an event on the compute stream after each step; event
+            # records are asynchronous and cost nothing on the timed path)
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+            evs[0].record(comp_s)
             t0 = time.perf_counter()
             for i in range(steps):
                 self.step(warmup + i)
+                evs[i + 1].record(comp_s)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
+            d = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(1, steps))
+            self.step_ms = ({"p50": d[len(d) // 2], "p90": d[int(len(d) * 0.9)], "min": d[0], "max": d[-1]}
+                            if d else None)
             if world > 1:
                 t = torch.tensor([el], device="cpu" if share else dev, dtype=torch.float64)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -204,6 +216,7 @@ def main() -> None:
         kern(pipe.dev_rec[0])
     torch.cuda.synchronize()
     elapsed = pipe.timed(a.warmup, a.steps)
+    step_dist = pipe.step_ms          # intervals between consecutive steps' kernel completions
 
     # whole-node runs: what the xGMI links delivered, measured on the same ranks right after the
     # timed region (RCCL all-reduce / all-gather sweep; extra JSON key, outside the timing)
@@ -265,6 +278,46 @@ def main() -> None:
         el16 = pipe16.timed(min(a.warmup, 3), a.rec16_steps)
         rec16_value = B * a.rec16_steps * world / el16
         del pipe16
+
+    # config 3 on the same ranks: the fused DP training step (forward + MSE gradient + dgrad in
+    # one kernel, split-K weight gradients, one flat-bucket all-reduce, fused AdamW + re-pack)
+    train_res = None
+    if a.train_steps > 0:
+        from routest_amd.train.fused import FusedMlp3Trainer
+        tB = 65536
+        torch.manual_seed(4321)                 # identical initial parameters on every rank
+        tmodel = EtaMLP(a.hidden)
+        tmodel.fit_normalization(records_to_features(norm_rec), norm_y)
+        trec, ty = synth_records(tB, seed=300 + rank)
+        trt = records_to_tensor(trec).to(dev)
+        tr = FusedMlp3Trainer(tmodel, dev, tB, tB * world, lr=1e-3, allreduce=world > 1)
+        yn = tr.normalize_targets(torch.from_numpy(ty).to(dev))
+        for _ in range(5):
+            tr.step(trt, yn)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.train_steps):
+            tr.step(trt, yn)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tel = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([tel], device="cpu" if share else dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tel = float(t.item())
+        loss = float(tr.sq_err.sum().item()) / tB
+        train_res = {"samples_per_s": tB * world * a.train_steps / tel,
+                     "ms_per_step": tel / a.train_steps * 1e3, "batch_per_gpu": tB,
+                     "global_batch": tB * world, "steps": a.train_steps,
+                     "allreduce": ("none" if world == 1 else "gloo (shared GPU)" if share
+                                   else "RCCL, one flat fp32 bucket"),
+                     "final_local_mse_normalized": loss}
+        del tr, trt
 
     p50_ms = p99_ms = None
     p50_fastapi_ms = None
@@ -357,6 +410,7 @@ def main() -> None:
                        "io": a.io, "record_bytes": a.rec, "numa_node": numa},
             "kernel_only_preds_per_s_per_gpu": kernel_preds_per_s,
             "h2d_copy_only_ms": h2d_only_ms,
+            "step_ms_distribution": step_dist,
             "step_vs_h2d_copy_only": (h2d_only_ms / (elapsed / a.steps * 1e3)) if h2d_only_ms else None,
             "p50_predict_ms": p50_ms,
             "p99_predict_ms": p99_ms,
@@ -370,6 +424,7 @@ def main() -> None:
                               16: "16 B full: fp32 distance, fp32 age, epoch seconds (kernel featurises)"}[a.rec],
             "shared_gpu": bool(share and world > 1),
             "collectives": coll,
+            "dp_training": train_res,
             "check_max_err_vs_emulation": err_emu,
             "check_max_err_vs_fp32": err_fp32,
             "finite": ok,
