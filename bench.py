@@ -57,6 +57,10 @@ def parse_args():
     ap.add_argument("--p50-requests", type=int, default=2000)
     ap.add_argument("--rec16-steps", type=int, default=10,
                     help="also time this many steps on full 16-byte records (extra JSON key)")
+    ap.add_argument("--gcn-steps", type=int, default=30,
+                    help="also time this many steps of the GCN route scorer (100k-node graph, 10k "
+                         "routes per step over all ranks), replicated and row-partitioned with an "
+                         "RCCL all-gather (extra JSON key 'gcn'; skipped on a shared GPU)")
     ap.add_argument("--train-steps", type=int, default=30,
                     help="also time this many data-parallel training steps of the same MLP on the "
                          "same ranks (64k rows per GPU, one flat-bucket RCCL all-reduce per step; "
@@ -319,6 +323,56 @@ def main() -> None:
                      "final_local_mse_normalized": loss}
         del tr, trt
 
+    # config 4 on the same ranks: the 2-layer GCN scorer, graph replicated on every GPU (no
+    # collective) and row-partitioned (each rank runs 1/N of the nodes, RCCL all-gather of Z)
+    gcn_res = None
+    if a.gcn_steps > 0 and not (share and world > 1):
+        from routest_amd.data.graph import synth_road_graph
+        from routest_amd.models.gcn import GcnScorer, GcnScorerHip, routes_to_csr
+        g = synth_road_graph(100_000, seed=0)
+        gm = GcnScorer(seed=0)
+        rng = np.random.default_rng(rank)
+        nroutes = 10_000 // world
+        walks = []
+        for _ in range(nroutes):
+            v = int(rng.integers(0, g.num_nodes))
+            path = [v]
+            for _ in range(int(rng.integers(50, 300))):
+                nb = g.indices[g.indptr[v]:g.indptr[v + 1]]
+                v = int(nb[rng.integers(0, len(nb))])
+                path.append(v)
+            walks.append(path)
+        ptr, nodes = routes_to_csr(walks)
+        ptr_t, nodes_t = torch.from_numpy(ptr).to(dev), torch.from_numpy(nodes).to(dev)
+        gcn_res = {"nodes": g.num_nodes, "edges": g.num_edges, "routes_per_step": nroutes * world}
+        for mode in (["replicate", "partition"] if world > 1 else ["replicate"]):
+            hip = GcnScorerHip(gm, g, dev, mode=mode, rank=rank, world=world)
+
+            def gstep():
+                hip.node_delays()
+                return hip.score_routes(ptr_t, nodes_t)
+            for _ in range(5):
+                gstep()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.gcn_steps):
+                gstep()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            gel = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([gel], device=dev, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                gel = float(t.item())
+            gcn_res[mode] = {"ms_per_step": gel / a.gcn_steps * 1e3,
+                             "routes_per_s": nroutes * world * a.gcn_steps / gel}
+            del hip
+
     p50_ms = p99_ms = None
     p50_fastapi_ms = None
     p50_py_ms = None
@@ -425,6 +479,7 @@ def main() -> None:
             "shared_gpu": bool(share and world > 1),
             "collectives": coll,
             "dp_training": train_res,
+            "gcn": gcn_res,
             "check_max_err_vs_emulation": err_emu,
             "check_max_err_vs_fp32": err_fp32,
             "finite": ok,
