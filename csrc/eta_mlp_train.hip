@@ -167,14 +167,27 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       for (int k = 0; k < NX; ++k)
 #pragma unroll
         for (int t = 0; t < 2; ++t) xk[k][t] = 8 * ((4 * k + 2 * t + h) ^ sw);
+      // the ks >= 8 half gets its own (opaque) offsets: with pm + xk + 256 the compiler merges the
+      // reads of ks and ks + 8 into one ds_read2_b64 (offsets 0 / 256 B), which conflicts with
+      // itself — 7.5 bank-conflict cycles per instruction (tools/probes/lds_pattern_probe.hip);
+      // two plain ds_read_b64 of the same swizzle are conflict-free
+      int xk8[NX][2];
+#pragma unroll
+      for (int k = 0; k < NX; ++k)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          xk8[k][t] = xk[k][t] + 256;
+          __asm__ volatile("" : "+v"(xk8[k][t]));
+        }
 #pragma unroll 1
       for (int mt = 0; mt < MT; ++mt) {
         f32x16 acc = load_vec16(b2p, mt, h);
         const unsigned char* pm = lrow + mt * 16384;
         // units 16ks + 4h + 0..3 and 16ks + 8 + 4h + 0..3: the permuted k order of h1
         auto frag = [&](int ks) {
-          const s16x4 lo = *reinterpret_cast<const s16x4*>(pm + xk[ks & 7][0] + 256 * (ks >> 3));
-          const s16x4 hi = *reinterpret_cast<const s16x4*>(pm + xk[ks & 7][1] + 256 * (ks >> 3));
+          const int* xo = (ks >> 3) ? xk8[ks & 7] : xk[ks & 7];
+          const s16x4 lo = *reinterpret_cast<const s16x4*>(pm + xo[0]);
+          const s16x4 hi = *reinterpret_cast<const s16x4*>(pm + xo[1]);
           return join4(lo, hi);
         };
         bf16x8 ring[D];

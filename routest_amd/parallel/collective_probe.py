@@ -38,14 +38,13 @@ def _time(fn, iters: int, warm: int = 3) -> float:
 
 
 def sweep(device: torch.device, sizes: Sequence[int] = DEFAULT_SIZES,
-          native: Optional[object] = None, budget_s: float = 5.0) -> List[Dict]:
-    """All ranks call this together; returns the same rows on every rank."""
+          native: Optional[object] = None) -> List[Dict]:
+    """All ranks call this together with the same arguments; every decision below depends on
+    those arguments only (never on local timing), so no rank can leave the others waiting in a
+    collective.  Returns the same rows on every rank (times are the max over ranks)."""
     n = dist.get_world_size()
     rows: List[Dict] = []
-    t_start = time.perf_counter()
     for nbytes in sizes:
-        if time.perf_counter() - t_start > budget_s:
-            break
         iters = 20 if nbytes <= (4 << 20) else 5
         numel = (nbytes // 4 + 3) // 4 * 4
         x = torch.ones(numel, device=device)
