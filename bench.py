@@ -256,7 +256,7 @@ def main() -> None:
     rec_chk = pipe.host_rec[:nchk]
     with torch.no_grad():
         ref32 = model.float().cpu()(featurize_torch(rec_chk)).reshape(-1)
-    emu = emulate_kernel(kern.packed.to("cpu"), rec_chk).reshape(-1)
+    emu = emulate_kernel(kern.packed.to("cpu"), rec_chk, kern._pick(B)).reshape(-1)
     spread = float((ref32 - ref32.mean()).abs().mean()) + 1e-6
     err_fp32 = float((got[:nchk] - ref32).abs().max()) / spread
     err_emu = float((got[:nchk] - emu).abs().max()) / spread

@@ -60,7 +60,7 @@ static int record_bytes(const torch::Tensor& r) {
 // 32x32 kernel (blob layout)
 static int fwd16_halves(int64_t variant) {
   return variant == 16 ? 2 : variant == 17 ? 4 : variant == 18 ? 1 : variant == 19 ? 3
-       : variant == 20 ? 5 : variant == 21 ? 6 : variant == 22 ? 7 : 0;
+       : variant == 20 ? 5 : variant == 21 ? 6 : variant == 22 ? 7 : variant == 23 ? 8 : 0;
 }
 static size_t fwd_blob_bytes(int64_t variant, int64_t H) {
   return fwd16_halves(variant) ? rt::eta_mlp3_blob16_bytes((int)H) : rt::eta_mlp3_blob_bytes((int)H);

@@ -241,7 +241,8 @@ size_t eta_mlp3_blob_bytes(int H) { return mlp3_blob_bytes(H); }
 //   * each W2 A fragment read from LDS feeds NH MFMAs (NH batch halves), so NH = 2 moves the
 //     same LDS bytes per FLOP as the 32x32 kernel and NH = 4 half of them
 // Blob16: [ w2p: (H/16)x(H/32)x64 lanes x 8 bf16 | w1p: (H/16)x64 lanes x 4 bf16 | b2 (H f32) |
-//           w3 (H f32, target scale folded) | tail: b3, 0, 0, 0 ]
+//           w3 (H f32, target scale folded) | tail: b3, 0, 0, 0 |
+//           w3f: (H/32)x64 lanes x 8 bf16 — w3 as the A operand of a layer-3 MFMA (EPI = 3) ]
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
@@ -251,10 +252,11 @@ struct Mlp3Layout16 {
   static constexpr int KC = H / 32;   // 32-deep k chunks
   static constexpr size_t W2B = (size_t)H * H * 2;
   static constexpr size_t W1B = (size_t)H * 16 * 2;
-  static constexpr size_t BLOB = W2B + W1B + 2 * (size_t)H * 4 + 16;
+  static constexpr size_t W3F = (size_t)H * 32;          // layer-3 A fragments (EPI = 3)
+  static constexpr size_t BLOB = W2B + W1B + 2 * (size_t)H * 4 + 16 + W3F;
 };
 
-size_t eta_mlp3_blob16_bytes(int H) { return (size_t)2 * H * H + 40 * (size_t)H + 16; }
+size_t eta_mlp3_blob16_bytes(int H) { return (size_t)2 * H * H + 72 * (size_t)H + 16; }
 
 // (pairwise: a 4-wide convertvector lowers to 4 single-element v_cvt_pk_bf16_f32 + 2 v_perm_b32)
 __device__ __forceinline__ bf16x4 relu_cvt_bf16x4(const f32x4 v) {
@@ -283,6 +285,7 @@ __global__ __launch_bounds__(TPB, 1) void eta_mlp3_fwd16_kernel(const void* __re
   const float* b2 = reinterpret_cast<const float*>(smem + L::W2B + L::W1B);
   const float* w3 = b2 + H;
   const float b3 = w3[H];
+  const bf16x8* w3f = reinterpret_cast<const bf16x8*>(smem + L::W2B + L::W1B + 8 * (size_t)H + 16);
 
   const int lane = threadIdx.x & 63;
   const int j = lane & 15;
@@ -344,18 +347,29 @@ __global__ __launch_bounds__(TPB, 1) void eta_mlp3_fwd16_kernel(const void* __re
     //          slot, MI355X_MICROARCH.md "price of one filler").
     // EPI = 2: scalar, and software-pipelined: hidden tile t-1's relu/dot is interleaved one VALU
     //          per MFMA gap into tile t's MFMA chain instead of stalling on t's last MFMA.
+    // EPI = 3: layer 3 on MFMA: relu(z2) of hidden tiles 2tp, 2tp+1 packed to bf16 (2 VALU per
+    //          output pair) is the B operand (k = 32 units, the w2p k order) of one 16x16x32 MFMA
+    //          whose A operand is w3 broadcast over the 16 rows (w3f); every lane then holds its
+    //          row's y — no w3 FMAs and no cross-lane reduction.
     constexpr int NC = KC / D;            // prefetch chunks per hidden tile
     f32x4 accp[NH];
 #pragma unroll
     for (int n = 0; n < NH; ++n) accp[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
     f32x4 w3p = {0.f, 0.f, 0.f, 0.f};
+    f32x4 y3[EPI == 3 ? NH : 1];
+    bf16x4 hprev[EPI == 3 ? NH : 1];
+    if constexpr (EPI == 3) {
+#pragma unroll
+      for (int n = 0; n < NH; ++n) y3[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
     auto epi = [&](const f32x4& a, const f32x4& w, float (&y)[2]) {
       y[0] = __builtin_fmaf(relu_f(a[0]), w[0], y[0]);
       y[1] = __builtin_fmaf(relu_f(a[1]), w[1], y[1]);
       y[0] = __builtin_fmaf(relu_f(a[2]), w[2], y[0]);
       y[1] = __builtin_fmaf(relu_f(a[3]), w[3], y[1]);
     };
-#pragma unroll 1
+    constexpr int TUNROLL = EPI == 3 ? 2 : 1;   // EPI 3: tile parity static in each copy
+#pragma unroll TUNROLL
     for (int t = 0; t < MT; ++t) {
       const f32x4 bias = *reinterpret_cast<const f32x4*>(b2 + 16 * t + 4 * kq);
       f32x4 acc[NH];
@@ -394,6 +408,21 @@ __global__ __launch_bounds__(TPB, 1) void eta_mlp3_fwd16_kernel(const void* __re
           __builtin_amdgcn_sched_group_barrier(0x008, D * NH, 0);
         }
       }
+      if constexpr (EPI == 3) {
+        if (t & 1) {
+          const bf16x8 wf = w3f[(t >> 1) * 64 + lane];
+#pragma unroll
+          for (int n = 0; n < NH; ++n) {
+            const bf16x4 hc = relu_cvt_bf16x4(acc[n]);
+            const bf16x8 hb = __builtin_shufflevector(hprev[n], hc, 0, 1, 2, 3, 4, 5, 6, 7);
+            y3[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hb, y3[n], 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int n = 0; n < NH; ++n) hprev[n] = relu_cvt_bf16x4(acc[n]);
+        }
+        continue;
+      }
       const f32x4 w3v = *reinterpret_cast<const f32x4*>(w3 + 16 * t + 4 * kq);
       if constexpr (EPI == 2) {
 #pragma unroll
@@ -427,9 +456,14 @@ __global__ __launch_bounds__(TPB, 1) void eta_mlp3_fwd16_kernel(const void* __re
     float mine = 0.f;
 #pragma unroll
     for (int n = 0; n < NH; ++n) {
-      float y = ys[n][0] + ys[n][1];
-      y += __shfl_xor(y, 16);
-      y += __shfl_xor(y, 32);
+      float y;
+      if constexpr (EPI == 3) {
+        y = y3[n][0];                    // C[m][row]: the same y in every m (w3 broadcast)
+      } else {
+        y = ys[n][0] + ys[n][1];
+        y += __shfl_xor(y, 16);
+        y += __shfl_xor(y, 32);
+      }
       mine = (kq == n) ? y : mine;
     }
     const int row = tile * ROWS + 16 * kq + j;
@@ -470,6 +504,7 @@ static hipError_t launch_fwd16_nh(const void* rec, float* out, int B, const void
     case 5: return launch_fwd16<H, 4, RB, 512, 1>(rec, out, B, blob, np, num_cus, stream);  // scalar-FMA epilogue
     case 6: return launch_fwd16<H, 4, RB, 512, 2>(rec, out, B, blob, np, num_cus, stream);  // + pipelined
     case 7: return launch_fwd16<H, 2, RB, 512, 2>(rec, out, B, blob, np, num_cus, stream);
+    case 8: return launch_fwd16<H, 4, RB, 512, 3>(rec, out, B, blob, np, num_cus, stream);  // layer 3 on MFMA
     default: return hipErrorInvalidValue;
   }
 }

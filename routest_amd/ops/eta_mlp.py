@@ -124,8 +124,8 @@ def pack_mlp3(model: EtaMLP) -> PackedMLP3:
 
 
 def blob16_bytes(H: int) -> int:
-    """[w2p16 | w1p16 | b2 | w3 | tail(b3,0,0,0)] — csrc/eta_mlp_fwd.hip Mlp3Layout16"""
-    return 2 * H * H + 40 * H + 16
+    """[w2p16 | w1p16 | b2 | w3 | tail(b3,0,0,0) | w3f] — csrc/eta_mlp_fwd.hip Mlp3Layout16"""
+    return 2 * H * H + 72 * H + 16
 
 
 @torch.no_grad()
@@ -153,10 +153,14 @@ def pack_mlp3_16(p: PackedMLP3) -> torch.Tensor:
         t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16)
         return t.view(torch.int16).numpy().view(np.uint8).reshape(-1)
 
+    # w3f[tp][l][v] = w3[32tp + kslot[l][v]]: w3 as the (row-broadcast) A operand of the layer-3
+    # MFMA of variant 23, in the same k order as the relu(z2) pairs of hidden tiles 2tp, 2tp+1
+    w3f = p.w3.numpy()[32 * np.arange(H // 32)[:, None, None] + kslot[None, :, :]]
     parts = [bf16_bytes(w2p), bf16_bytes(w1p),
              p.b2.numpy().astype(np.float32).view(np.uint8).reshape(-1),
              p.w3.numpy().astype(np.float32).view(np.uint8).reshape(-1),
-             np.array([p.b3, 0.0, 0.0, 0.0], dtype=np.float32).view(np.uint8)]
+             np.array([p.b3, 0.0, 0.0, 0.0], dtype=np.float32).view(np.uint8),
+             bf16_bytes(w3f)]
     blob = torch.from_numpy(np.concatenate(parts).copy())
     assert blob.numel() == blob16_bytes(H)
     return blob
@@ -228,8 +232,9 @@ def featurize_torch(rec_i32: torch.Tensor) -> torch.Tensor:
                       age[:, None]], 1)
 
 
-def emulate_kernel(p: PackedMLP3, rec_i32: torch.Tensor) -> torch.Tensor:
-    """Bit-faithful-ish PyTorch emulation of the kernel numerics (bf16 operands, fp32 acc)."""
+def emulate_kernel(p: PackedMLP3, rec_i32: torch.Tensor, variant: int = -1) -> torch.Tensor:
+    """Bit-faithful-ish PyTorch emulation of the kernel numerics (bf16 operands, fp32 acc);
+    variant 23 runs layer 3 on MFMA, so relu(z2) and w3 are bf16 there."""
     x = featurize_torch(rec_i32)
     dev = x.device
     sc = torch.tensor(p.norm[:4], device=dev)
@@ -249,13 +254,17 @@ def emulate_kernel(p: PackedMLP3, rec_i32: torch.Tensor) -> torch.Tensor:
     bf = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
     h1 = torch.relu(bf(f) @ bf(p.w1k.to(dev)).T)
     h2 = torch.relu(bf(h1) @ bf(p.w2.to(dev)).T + p.b2.to(dev))
+    if variant in MFMA_L3_VARIANTS:
+        return bf(h2) @ bf(p.w3.to(dev)) + p.b3
     return h2 @ p.w3.to(dev) + p.b3
 
 
 # variants of the 16x16-MFMA kernel (csrc/eta_mlp_fwd.hip eta_mlp3_fwd16_kernel; bindings.cpp
 # fwd16_halves): 16/17/18 = 2/4/1 batch halves, 19 = 2 halves at 12 waves/CU, 20 = 4 halves with
-# a scalar-FMA layer-3 epilogue, 21 = 20 software-pipelined across hidden tiles, 22 = 21 with 2 halves
-FWD16_VARIANTS = (16, 17, 18, 19, 20, 21, 22)
+# a scalar-FMA layer-3 epilogue, 21 = 20 software-pipelined across hidden tiles, 22 = 21 with 2 halves,
+# 23 = 4 halves with layer 3 on MFMA (relu(z2) and w3 in bf16)
+FWD16_VARIANTS = (16, 17, 18, 19, 20, 21, 22, 23)
+MFMA_L3_VARIANTS = (23,)
 
 
 class EtaMlpKernel:
@@ -310,10 +319,14 @@ class EtaMlpKernel:
                                         self.packed.norm, v)
 
     AUTO16_MIN_ROWS = 1 << 17
+    # large batches: 4 batch halves per wave-tile, scalar-FMA fp32 layer 3 (variant 20: 1-2 %
+    # ahead of the packed-FMA 17, profiles/eta_fwd16_epilogue_ab_r2.jsonl; variant 23, layer 3 on
+    # MFMA, is 2.5 % faster still but rounds relu(z2) and w3 to bf16, profiles/eta_fwd16_pmc_r2.md)
+    AUTO16_VARIANT = 20
 
     def _pick(self, rows: int) -> int:
         if self.variant == -1 and rows >= self.AUTO16_MIN_ROWS:
-            return 17
+            return self.AUTO16_VARIANT
         return self.variant
 
     def _blob(self, variant: int) -> torch.Tensor:

@@ -41,7 +41,7 @@ def test_featurize_kernel_exact():
 
 
 @pytest.mark.parametrize("H", [64, 128, 256])
-@pytest.mark.parametrize("variant", [0, 1, 16, 17, 18, 19, 20, 21, 22])
+@pytest.mark.parametrize("variant", [0, 1, 16, 17, 18, 19, 20, 21, 22, 23])
 @pytest.mark.parametrize("B", [1, 31, 33, 1000, 70_001])
 def test_mlp3_forward_matches_fp32(H, variant, B):
     m = _model(H)
@@ -52,7 +52,7 @@ def test_mlp3_forward_matches_fp32(H, variant, B):
     torch.cuda.synchronize()
     got = got.cpu()
     ref = m(torch.from_numpy(records_to_features(rec))).detach()
-    emu = emulate_kernel(k.packed.to("cpu"), rt)
+    emu = emulate_kernel(k.packed.to("cpu"), rt, variant)
     assert got.shape == (B,)
     assert torch.isfinite(got).all()
     # vs the kernel-numerics emulation: only accumulation order differs
@@ -154,7 +154,7 @@ def test_mlp3_forward_compact_records(variant):
     assert torch.equal(out, got)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 16, 17, 18, 20, 21, 22])
+@pytest.mark.parametrize("variant", [0, 1, 3, 16, 17, 18, 20, 21, 22, 23])
 def test_mlp3_forward_rec6_records(variant):
     """6-byte bulk records: kernel == the fp32 model on the records' own features, on HBM and on
     pinned host records (zero-copy), odd batch (the last row's 6 bytes end the buffer)."""
@@ -217,11 +217,11 @@ def test_gpu_runner_small_rounds_resident_large_rounds_launch():
 
 
 def test_auto_variant_switches_to_16x16_kernel():
-    """variant=-1: large batches run the 16x16-MFMA kernel (bitwise equal to variant 17), small
-    ones the 32x32 kernel; both within bf16 tolerance of the fp32 model."""
+    """variant=-1: large batches run the 16x16-MFMA kernel (bitwise equal to its auto variant),
+    small ones the 32x32 kernel; both within bf16 tolerance of the fp32 model."""
     m = _model(256, 9)
     auto = EtaMlpKernel(m, torch.device("cuda:0"))
-    k17 = EtaMlpKernel(m, torch.device("cuda:0"), variant=17)
+    k17 = EtaMlpKernel(m, torch.device("cuda:0"), variant=EtaMlpKernel.AUTO16_VARIANT)
     k3 = EtaMlpKernel(m, torch.device("cuda:0"), variant=3)
     rec, _ = synth_records(EtaMlpKernel.AUTO16_MIN_ROWS + 77, 31)
     rt = records_to_tensor(rec).cuda()
@@ -255,7 +255,7 @@ def trained256():
     return md.cpu().eval()
 
 
-@pytest.mark.parametrize("variant", [0, 3, 17, 20])
+@pytest.mark.parametrize("variant", [0, 3, 17, 20, 23])
 def test_forward_trained_model_relative_to_spread(trained256, variant):
     """K1+K2 vs the fp32 model on a TRAINED model, with the error measured against the spread of
     the predictions (y - mean y), not against y itself: bf16 operands and fp32 accumulation keep
