@@ -326,6 +326,29 @@ void adamw_pack_big(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Te
                                          (float)min_lr_ratio, update ? 1 : 0, cur_stream(P)));
 }
 
+// wide trainer: dy / dyb / sq_err from the relu.w3 partials + dz2 from h2a + step counter (one launch)
+void big_dz2y(torch::Tensor ypart, int64_t nparts, torch::Tensor b3_dev, torch::Tensor target, double gscale,
+              torch::Tensor dy, torch::Tensor dyb, torch::Tensor sq_err, torch::Tensor h2a,
+              torch::Tensor w3, int64_t H, torch::Tensor dz2, torch::Tensor step_ctr) {
+  for (auto* t : {&ypart, &b3_dev, &target, &dy, &sq_err, &h2a, &w3, &step_ctr}) check_dev(*t, "big_dz2y operand");
+  const int64_t B = dz2.size(0);
+  check_bf16(dz2, "dz2", B, H);
+  check_bf16(dyb, "dyb", B, 8);
+  TORCH_CHECK(ypart.scalar_type() == torch::kFloat32 && nparts > 0 && nparts <= 64 &&
+                  ypart.numel() >= B * nparts, "ypart f32 [B, nparts <= 64]");
+  TORCH_CHECK(target.numel() >= B && dy.numel() >= B && sq_err.numel() >= B && w3.numel() >= H &&
+                  b3_dev.numel() >= 1, "training vectors");
+  TORCH_CHECK(h2a.scalar_type() == torch::kBFloat16 && h2a.dim() == 2 && h2a.size(0) >= B &&
+                  h2a.size(1) >= H && H % 8 == 0, "h2a bf16 [B, >=H]");
+  TORCH_CHECK(step_ctr.scalar_type() == torch::kInt32, "step_ctr i32");
+  const c10::DeviceGuard guard(h2a.device());
+  RT_CHECK_HIP(rt::launch_big_dz2y(ypart.data_ptr<float>(), (int)nparts, (int)B, (int)H, b3_dev.data_ptr<float>(),
+                                   target.data_ptr<float>(), (float)gscale, dy.data_ptr<float>(), dyb.data_ptr(),
+                                   sq_err.data_ptr<float>(), h2a.data_ptr(), (int)h2a.size(1),
+                                   w3.data_ptr<float>(), dz2.data_ptr(), step_ctr.data_ptr<int>(),
+                                   cur_stream(h2a)));
+}
+
 void big_dz2(torch::Tensor h2a, torch::Tensor dy, torch::Tensor w3, int64_t H, torch::Tensor dz2) {
   check_dev(h2a, "h2a");
   check_dev(dy, "dy");
@@ -921,6 +944,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("target") = py::none(), py::arg("gscale") = 0.0, py::arg("dy") = py::none(),
         py::arg("dyb") = py::none(), py::arg("sq_err") = py::none(), py::arg("b3_dev") = py::none());
   m.def("adamw_pack_big", &adamw_pack_big, "wide trainer: AdamW + re-pack of w1p / w2k / w2t / b2 / w3 / b3");
+  m.def("big_dz2y", &big_dz2y, "wide trainer: dy, dyb, squared error, dz2 and the step counter in one launch");
   m.def("big_dz2", &big_dz2, "dz2 = dy * w3 * relu'(z2) from h2a (hperm order)");
   m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad + input-gradient path (dz2, dz1)");
   m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + training-blob re-pack");

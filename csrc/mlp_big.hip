@@ -17,6 +17,7 @@
 //   big_yreduce_kernel : y = sum of partials + b3 (inference) | + dy, dy operand, squared error
 //                        (training)
 //   big_dz2_kernel     : dz2 = dy * w3 * relu'(z2) from h2a (training)
+//   big_dz2y_kernel    : training: big_yreduce + big_dz2 + the step counter in one launch
 //
 // Weight layouts (host: routest_amd/ops/mlp_big.py; training: adamw_pack_big_kernel):
 //   w1p [H/32][64 lanes][8] bf16 (as mlp3_tile.h), w2k [H][H] bf16 row-major with K columns in
@@ -598,6 +599,45 @@ __global__ __launch_bounds__(256) void big_dz2_kernel(const __bf16* __restrict__
   *reinterpret_cast<bf16x8*>(dz2 + m * H + c) = o;
 }
 
+// Training: dy (+ its bf16 operand row, squared error) and dz2 for one row per wave, in one
+// launch (was big_yreduce + big_dz2 + a step-counter increment): lanes < nparts fetch the row's
+// relu.w3 partials, a butterfly sums them, and the wave then writes the row's H dz2 values
+// (8 per lane per pass).  Block 0 advances the device step counter for adamw_pack_big.
+__global__ __launch_bounds__(256) void big_dz2y_kernel(const float* __restrict__ ypart, int nparts,
+                                                       int B, int H, const float* __restrict__ b3p,
+                                                       const float* __restrict__ target, float gscale,
+                                                       float* __restrict__ dy, __bf16* __restrict__ dyb,
+                                                       float* __restrict__ sq_err,
+                                                       const __bf16* __restrict__ h2a, int lda,
+                                                       const float* __restrict__ w3,
+                                                       __bf16* __restrict__ dz2, int* __restrict__ step_ctr) {
+  if (step_ctr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *step_ctr += 1;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= B) return;                                       // whole wave leaves together
+  float s = lane < nparts ? ypart[(size_t)m * nparts + lane] : 0.f;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  const float diff = s + b3p[0] - target[m];
+  const float d = gscale * diff;
+  if (lane == 0) {
+    dy[m] = d;
+    sq_err[m] = diff * diff;
+    bf16x8 dv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dv[j] = (__bf16)0.f;
+    dv[0] = (__bf16)d;
+    *reinterpret_cast<bf16x8*>(dyb + (size_t)m * 8) = dv;
+  }
+  for (int c = 8 * lane; c < H; c += 512) {
+    const bf16x8 hv = *reinterpret_cast<const bf16x8*>(h2a + (size_t)m * lda + c);
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = (__bf16)(((float)hv[q] > 0.f) ? d * w3[hp(c + q)] : 0.f);
+    *reinterpret_cast<bf16x8*>(dz2 + (size_t)m * H + c) = o;
+  }
+}
+
 struct AdamWBigArgs {
   float lr, beta1, beta2, eps, wd;
   int warmup, total_steps;
@@ -619,19 +659,21 @@ __device__ __forceinline__ float sched_lr_big(const AdamWBigArgs& a, int t) {
 // the wide trainer's operands: w1p fragments (b1 as bf16 hi/lo in k = 14, 15), w2k[o][hp(i)],
 // w2t[i][hp(o)] (bf16), b2 / w3 / b3 f32.  Gradient bucket rows/columns are hperm positions
 // (gW2a[hp(o)][hp(i)], gW3a[hp(o)], gW1a[hp(o)][16]): every activation is stored in that order.
-__global__ __launch_bounds__(256) void adamw_pack_big_kernel(float* __restrict__ P, const float* __restrict__ G,
-                                                             float* __restrict__ M, float* __restrict__ V,
-                                                             __bf16* __restrict__ w1p, __bf16* __restrict__ w2k,
-                                                             __bf16* __restrict__ w2t, float* __restrict__ b2,
-                                                             float* __restrict__ w3, float* __restrict__ b3,
-                                                             const int* __restrict__ step, AdamWBigArgs a) {
+__device__ __forceinline__ void adamw_big_elem(long long ep, float* __restrict__ P, const float* __restrict__ G,
+                                               float* __restrict__ M, float* __restrict__ V,
+                                               __bf16* __restrict__ w1p, __bf16* __restrict__ w2k,
+                                               __bf16* __restrict__ w2t, float* __restrict__ b2,
+                                               float* __restrict__ w3, float* __restrict__ b3,
+                                               const int* __restrict__ step, const AdamWBigArgs& a) {
   const int H = a.H, LDG = H + 16;
   const long long OFF_B1 = 12LL * H, OFF_W2 = 13LL * H, OFF_B2 = OFF_W2 + (long long)H * H,
                   OFF_W3 = OFF_B2 + H, OFF_B3 = OFF_W3 + H, N = OFF_B3 + 1;
   const float* gW2a = G;
   const float* gW3a = G + (long long)H * LDG;
   const float* gW1a = gW3a + LDG;
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  // the W2 block (H*H of the N parameters) is handled by adamw_w2_tile_kernel; this grid covers
+  // the rest: index e' < OFF_W2 maps to itself, the others skip the W2 range
+  const long long e = ep < OFF_W2 ? ep : ep + (long long)H * H;
   if (e >= N) return;
   float g;
   bool decay = false;
@@ -699,6 +741,58 @@ __global__ __launch_bounds__(256) void adamw_pack_big_kernel(float* __restrict__
   }
 }
 
+// Wide AdamW + re-pack in ONE launch.  Blocks [0, (H/32)^2) take the W2 block in 32 x 32 tiles:
+// P / M / V and the w2k rows are written coalesced as before, and the transposed copy w2t goes
+// through an LDS tile so its rows are written coalesced too (one element per thread scattered
+// 2-byte writes H*2 bytes apart).  The remaining blocks take the other 15H + 1 parameters one per
+// thread (adamw_big_elem).
+__global__ __launch_bounds__(256) void adamw_pack_big_kernel(float* __restrict__ P, const float* __restrict__ G,
+                                                             float* __restrict__ M, float* __restrict__ V,
+                                                             __bf16* __restrict__ w1p, __bf16* __restrict__ w2k,
+                                                             __bf16* __restrict__ w2t, float* __restrict__ b2,
+                                                             float* __restrict__ w3, float* __restrict__ b3,
+                                                             const int* __restrict__ step, AdamWBigArgs a) {
+  __shared__ __bf16 T[32][34];
+  const int H = a.H, LDG = H + 16, tpr = H / 32, ntiles = tpr * tpr;
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= ntiles) {
+    const long long ep = (long long)(blockIdx.x - ntiles) * blockDim.x + tid;
+    if (ep < 15LL * H + 1) adamw_big_elem(ep, P, G, M, V, w1p, w2k, w2t, b2, w3, b3, step, a);
+    return;
+  }
+  const long long OFF_W2 = 13LL * H;
+  const int o0 = (blockIdx.x / tpr) * 32, i0 = (blockIdx.x % tpr) * 32;
+  const int t = *step > 0 ? *step : 1;
+  const float lr = sched_lr_big(a, t);
+  const float bc1 = 1.f - powf(a.beta1, (float)t);
+  const float bc2 = 1.f - powf(a.beta2, (float)t);
+#pragma unroll
+  for (int idx = tid; idx < 1024; idx += 256) {
+    const int oo = idx >> 5, ii = idx & 31, o = o0 + oo, i = i0 + ii;
+    const long long e = OFF_W2 + (long long)o * H + i;
+    float p = P[e];
+    if (a.update) {
+      const float g = G[(long long)hp(o) * LDG + hp(i)];
+      p -= lr * a.wd * p;
+      const float m = a.beta1 * M[e] + (1.f - a.beta1) * g;
+      const float v = a.beta2 * V[e] + (1.f - a.beta2) * g * g;
+      M[e] = m;
+      V[e] = v;
+      p -= lr * (m / bc1) / (sqrtf(v / bc2) + a.eps);
+      P[e] = p;
+    }
+    const __bf16 pb = (__bf16)p;
+    w2k[(size_t)o * H + hp(i)] = pb;
+    T[ii][oo] = pb;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int idx = tid; idx < 1024; idx += 256) {
+    const int ii = idx >> 5, oo = idx & 31;
+    w2t[(size_t)(i0 + ii) * H + o0 + hp(oo)] = T[ii][oo];
+  }
+}
+
 }  // namespace
 
 hipError_t launch_adamw_pack_big(float* P, const float* G, float* M, float* V, void* w1p, void* w2k,
@@ -706,8 +800,10 @@ hipError_t launch_adamw_pack_big(float* P, const float* G, float* M, float* V, v
                                  float lr, float beta1, float beta2, float eps, float wd, int warmup,
                                  int total_steps, float min_lr_ratio, int update, hipStream_t stream) {
   AdamWBigArgs a{lr, beta1, beta2, eps, wd, warmup, total_steps, min_lr_ratio, update, H};
-  const long long N = (long long)H * H + 15LL * H + 1;
-  hipLaunchKernelGGL(adamw_pack_big_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, stream,
+  if (H % 32) return hipErrorInvalidValue;
+  const long long Nrest = 15LL * H + 1;                 // everything but the W2 block
+  const unsigned nb = (unsigned)((H / 32) * (H / 32) + (Nrest + 255) / 256);
+  hipLaunchKernelGGL(adamw_pack_big_kernel, dim3(nb), dim3(256), 0, stream,
                      P, G, M, V, (__bf16*)w1p, (__bf16*)w2k, (__bf16*)w2t, b2, w3, b3, step, a);
   return hipGetLastError();
 }
@@ -829,6 +925,18 @@ hipError_t launch_big_yreduce(const float* ypart, int nparts, int B, float b3, c
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(big_yreduce_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, ypart, nparts, B,
                      b3, b3p, y, target, gscale, dy, (__bf16*)dyb, sq_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_big_dz2y(const float* ypart, int nparts, int B, int H, const float* b3p,
+                           const float* target, float gscale, float* dy, void* dyb, float* sq_err,
+                           const void* h2a, int lda, const float* w3, void* dz2, int* step_ctr,
+                           hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  if (H % 8 || nparts > 64 || lda % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(big_dz2y_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, ypart, nparts, B, H, b3p,
+                     target, gscale, dy, (__bf16*)dyb, sq_err, (const __bf16*)h2a, lda, w3, (__bf16*)dz2,
+                     step_ctr);
   return hipGetLastError();
 }
 

@@ -54,6 +54,10 @@ hipError_t launch_adamw_pack_big(float* P, const float* G, float* M, float* V, v
                                  void* w2t, float* b2, float* w3, float* b3, const int* step, int H,
                                  float lr, float beta1, float beta2, float eps, float wd, int warmup,
                                  int total_steps, float min_lr_ratio, int update, hipStream_t stream);
+hipError_t launch_big_dz2y(const float* ypart, int nparts, int B, int H, const float* b3p,
+                           const float* target, float gscale, float* dy, void* dyb, float* sq_err,
+                           const void* h2a, int lda, const float* w3, void* dz2, int* step_ctr,
+                           hipStream_t stream);
 hipError_t launch_big_dz2(const void* h2a, int lda, const float* dy, const float* w3, int B, int H,
                           void* dz2, hipStream_t stream);
 

@@ -303,14 +303,12 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
         C, H, B = self.C, self.H, rec.shape[0]
         ldg = H + 16
         assert B == self.B, "wide trainer: batch must equal batch_local"
-        self.step_ctr.add_(1)
         C.big_layer1(rec, self.w1p, H, self.norm, self.h1a, self.xf)
         C.gemm_nt(1, self.w2k, self.h1a, H, B, H, b2=self.b2v, w3=self.w3v, ypart=self.ypart,
                   out=self.h2a)
-        C.big_yreduce(self.ypart.reshape(-1), H // 64, 0.0, target=tgt_norm,
-                      gscale=2.0 / self.global_batch, dy=self.dy, dyb=self.dyb, sq_err=self.sq_err,
-                      b3_dev=self.b3v)
-        C.big_dz2(self.h2a, self.dy, self.w3v, H, self.dz2)
+        # dy / dyb / squared error + dz2 + the device step counter: one launch
+        C.big_dz2y(self.ypart, H // 64, self.b3v, tgt_norm, 2.0 / self.global_batch, self.dy,
+                   self.dyb, self.sq_err, self.h2a, self.w3v, H, self.dz2, self.step_ctr)
         C.gemm_nt(2, self.w2t, self.dz2, H, B, H, out=self.dh1)
         # dW2|db2 = dz2^T [h1|1]: one launch, n-blocks of <= 288 columns in the grid
         C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit2)
