@@ -438,7 +438,7 @@ void check_bf16(const torch::Tensor& t, const char* name, int64_t rows, int64_t 
 // Writes every output in place (static buffers: the step is HIP-graph capturable).
 void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tensor blob, int64_t H,
                         std::vector<double> norm, double gscale, torch::Tensor xf,
-                        torch::Tensor h1a, torch::Tensor h2a, torch::Tensor dz2, torch::Tensor dz1,
+                        torch::Tensor h1a, torch::Tensor w3slab, torch::Tensor dz2, torch::Tensor dz1,
                         torch::Tensor dyb, torch::Tensor sq_err, torch::Tensor step_ctr) {
   check_dev(records, "records");
   check_dev(target, "target");
@@ -452,7 +452,11 @@ void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tens
               (size_t)blob.numel() == rt::eta_mlp3_train_blob_bytes((int)H), "bad training blob");
   check_bf16(xf, "xf", B, 16);
   check_bf16(h1a, "h1a", B, H + 16);
-  check_bf16(h2a, "h2a", B, H + 16);
+  check_dev(w3slab, "w3slab");
+  const int grid = rt::train_fwd_grid((int)B, num_cus(records.device().index()));
+  TORCH_CHECK(w3slab.scalar_type() == torch::kFloat32 && w3slab.is_contiguous() && w3slab.dim() == 2 &&
+                  w3slab.size(0) == grid && w3slab.size(1) == H + 16,
+              "w3slab must be f32 [train_fwd_grid(B), H + 16] = [", grid, ", ", H + 16, "]");
   check_bf16(dz2, "dz2", B, H);
   check_bf16(dz1, "dz1", B, H);
   check_bf16(dyb, "dyb", B, 8);
@@ -463,7 +467,7 @@ void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tens
   const c10::DeviceGuard guard(records.device());
   RT_CHECK_HIP(rt::launch_eta_mlp3_train_fwd(
       records.data_ptr(), target.data_ptr<float>(), (int)B, blob.data_ptr(), (int)H,
-      norm_from(norm), (float)gscale, xf.data_ptr(), h1a.data_ptr(), h2a.data_ptr(),
+      norm_from(norm), (float)gscale, xf.data_ptr(), h1a.data_ptr(), w3slab.data_ptr<float>(),
       dz2.data_ptr(), dz1.data_ptr(), dyb.data_ptr(), sq_err.data_ptr<float>(), step_ctr.data_ptr<int>(),
       num_cus(records.device().index()), cur_stream(records)));
 }
@@ -534,26 +538,32 @@ void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N
 }
 
 void wgrad_reduce(torch::Tensor slab, torch::Tensor G, c10::optional<torch::Tensor> slab1,
-                  c10::optional<torch::Tensor> G1) {
-  auto chk = [](const torch::Tensor& sl, const torch::Tensor& g) {
+                  c10::optional<torch::Tensor> G1, c10::optional<torch::Tensor> slab2,
+                  c10::optional<torch::Tensor> G2) {
+  auto chk = [&](const torch::Tensor& sl, const torch::Tensor& g) {
     check_dev(sl, "slab");
     check_dev(g, "G");
     TORCH_CHECK(sl.scalar_type() == torch::kFloat32 && g.scalar_type() == torch::kFloat32, "f32");
-    TORCH_CHECK(sl.dim() == 2 && sl.size(1) >= g.numel(), "slab/G shape");
+    TORCH_CHECK(sl.dim() == 2 && sl.size(1) >= g.numel() && sl.is_contiguous() && g.is_contiguous(),
+                "slab/G shape");
+    TORCH_CHECK(sl.device() == G.device() && g.device() == G.device(), "one device");
   };
   chk(slab, G);
   const bool two = slab1.has_value() && slab1->defined();
   TORCH_CHECK(two == (G1.has_value() && G1->defined()), "slab1 and G1 go together");
-  if (two) {
-    chk(*slab1, *G1);
-    TORCH_CHECK(slab1->device() == G.device() && G1->device() == G.device(), "one device");
-  }
+  const bool three = slab2.has_value() && slab2->defined();
+  TORCH_CHECK(three == (G2.has_value() && G2->defined()), "slab2 and G2 go together");
+  if (two) chk(*slab1, *G1);
+  if (three) chk(*slab2, *G2);
   const c10::DeviceGuard guard(G.device());
   RT_CHECK_HIP(rt::launch_wgrad_reduce(
       slab.data_ptr<float>(), (int)slab.size(0), (long long)slab.size(1), G.data_ptr<float>(),
       (int)G.numel(), cur_stream(G), two ? slab1->data_ptr<float>() : nullptr,
       two ? (int)slab1->size(0) : 0, two ? (long long)slab1->size(1) : 0,
-      two ? G1->data_ptr<float>() : nullptr, two ? (int)G1->numel() : 0));
+      two ? G1->data_ptr<float>() : nullptr, two ? (int)G1->numel() : 0,
+      three ? slab2->data_ptr<float>() : nullptr, three ? (int)slab2->size(0) : 0,
+      three ? (long long)slab2->size(1) : 0, three ? G2->data_ptr<float>() : nullptr,
+      three ? (int)G2->numel() : 0));
 }
 
 void check_csr(const torch::Tensor& indptr, const torch::Tensor& indices, const torch::Tensor& values) {
@@ -955,8 +965,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A"), py::arg("M"), py::arg("Mout"), py::arg("Bm"), py::arg("N"), py::arg("slab"),
         py::arg("offset"), py::arg("ldo"), py::arg("mask") = py::none(), py::arg("nout") = -1, py::arg("mask_hperm") = false,
         py::arg("nsplit") = 1);
-  m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs (optionally a second region)",
-        py::arg("slab"), py::arg("G"), py::arg("slab1") = py::none(), py::arg("G1") = py::none());
+  m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs (optionally a second and third region)",
+        py::arg("slab"), py::arg("G"), py::arg("slab1") = py::none(), py::arg("G1") = py::none(),
+        py::arg("slab2") = py::none(), py::arg("G2") = py::none());
+  m.def("train_fwd_grid", [](int64_t B, int64_t dev) { return (int64_t)rt::train_fwd_grid((int)B, num_cus((int)dev)); },
+        "workgroups of the training forward = rows of its dW3 slab");
   m.def("num_cus", [](int64_t dev) { return (int64_t)num_cus((int)dev); });
   m.def("gcn_agg_gemm", &gcn_agg_gemm, "K8: fused CSR aggregation + MFMA GEMM + bias/ReLU");
   m.def("gcn_l1_fused", &gcn_l1_fused, "K8: fused aggregation + W1 GEMM + ReLU + W2 transform (H1 stays in LDS)");

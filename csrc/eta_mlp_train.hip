@@ -83,11 +83,26 @@ __device__ __forceinline__ bf16x8 join4(const s16x4 lo, const s16x4 hi) {
 // 8 waves per workgroup, 2 per SIMD (<= 256 VGPRs each).
 constexpr int TRAIN_TPB = 512;
 
+// One halving step of a reduce-scatter over the 32 lanes of each half-wave: pairs (k, k + N/2)
+// of v[0 .. N); a lane keeps the member whose index bit matches its lane bit X and adds the
+// partner lane's copy of it (ds_swizzle bit mode: xor X within 32 lanes).  Leaves v[0 .. N/2).
+template <int X, int N, int NV>
+__device__ __forceinline__ void rs32_step(float (&v)[NV], int lane) {
+  const bool up = (lane & X) != 0;
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) {
+    const float a = v[k], b = v[k + N / 2];
+    const float send = up ? a : b;
+    const float keep = up ? b : a;
+    v[k] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), (X << 10) | 0x1f));
+  }
+}
+
 template <int H>
 __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     const int4* __restrict__ rec, const float* __restrict__ target, int B,
     const unsigned char* __restrict__ blob, NormParams np, float gscale, __bf16* __restrict__ xf,
-    __bf16* __restrict__ h1a, __bf16* __restrict__ h2a, __bf16* __restrict__ dz2,
+    __bf16* __restrict__ h1a, float* __restrict__ w3slab, __bf16* __restrict__ dz2,
     __bf16* __restrict__ dz1, __bf16* __restrict__ dyb, float* __restrict__ sq_err,
     int* __restrict__ step_ctr) {
   using L = TrainLayout<H>;
@@ -107,6 +122,10 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
   const int wpb = blockDim.x >> 6;
   const int ntiles = (B + 31) >> 5;
   const int stride = gridDim.x * wpb;
+  // this wave's dW3 | db3 partial accumulates in LDS past the blob (nothing carried in registers
+  // across tiles): [wpb][LDA] f32, one row per wave until the final barrier
+  float* const w3part = reinterpret_cast<float*>(smem + L::BLOB) + (threadIdx.x >> 6) * LDA;
+  for (int c = lane; c < LDA; c += 64) w3part[c] = 0.f;
 
   for (int tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntiles; tile += stride) {
     // nothing is hoisted out of the tile loop: the LDS-resident weights (W1 fragments, biases)
@@ -139,7 +158,6 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       relu_cvt_bf16x8(a + 8, &h1[2 * mt + 1]);
     }
     __bf16* h1row = h1a + (size_t)row * LDA;
-    __bf16* h2row = h2a + (size_t)row * LDA;
     if (valid) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf16x8*>(h1row + 16 * ks + 8 * h) = h1[ks];
@@ -148,12 +166,16 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       for (int j = 0; j < 8; ++j) tailv[j] = (__bf16)0.f;
       if (h == 0) tailv[0] = (__bf16)1.f;
       *reinterpret_cast<bf16x8*>(h1row + H + 8 * h) = tailv;
-      *reinterpret_cast<bf16x8*>(h2row + H + 8 * h) = tailv;
     }
 
-    // layer 2 + layer 3; relu(z2) goes straight to memory, only its mask stays in registers
+    // layer 2 + layer 3 in TWO passes over the hidden tiles, relu(z2) never stored: pass 1 only
+    // forms y (hence dy); pass 2 recomputes z2 per tile for the relu'(z2) mask and the dW3 | db3
+    // partial.  The second 128 MFMAs per tile cost less than writing h2a (35.6 MB at 64k rows)
+    // and reading it back in a split-K GEMM; keeping relu(z2) in registers instead (64 VGPRs next
+    // to h1's 64) spilled.
     unsigned long long mask_lo = 0, mask_hi = 0;   // 16 relu'(z2) bits per hidden tile
     float ys = 0.f;
+    float dy, diff;
     {
       // addresses as lane bases + immediates (a run-time or fully hoisted w2off() per fragment
       // costs VGPRs the compiler then spills — and a scratch reload after the activation stores
@@ -179,8 +201,7 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
           xk8[k][t] = xk[k][t] + 256;
           __asm__ volatile("" : "+v"(xk8[k][t]));
         }
-#pragma unroll 1
-      for (int mt = 0; mt < MT; ++mt) {
+      auto layer2 = [&](int mt) {
         f32x16 acc = load_vec16(b2p, mt, h);
         const unsigned char* pm = lrow + mt * 16384;
         // units 16ks + 4h + 0..3 and 16ks + 8 + 4h + 0..3: the permuted k order of h1
@@ -204,28 +225,56 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
 #pragma unroll
           for (int d = 0; d < D; ++d) acc = mfma32(a[d], h1[ks + d], acc);
         }
+        return acc;
+      };
+      // pass 1: y
+#pragma unroll 1
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x16 acc = layer2(mt);
         const f32x16 w3 = load_vec16(w3p, mt, h);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) ys = __builtin_fmaf(relu_f(acc[e]), w3[e], ys);
+      }
+      ys += __shfl_xor(ys, 32);
+      const float y = ys + b3;
+      diff = valid ? (y - target[row]) : 0.f;
+      dy = gscale * diff;
+      // pass 2: relu'(z2) bits and the dW3 partial sum_r bf16(dy_r) bf16(relu(z2[r, c])) (the
+      // operands the split-K GEMM over h2a used).  The 32 rows of a lane half sit on 32 lanes:
+      // the row sum of a hidden tile's 16 values per lane is a reduce-scatter over lane bits
+      // 4..1 (ds_swizzle xor, no LDS traffic) plus a final xor-1 add; lane (r, h) then holds the
+      // tile-sum of value i = r >> 1, stored column 16 (2mt + (i >> 3)) + 8h + (i & 7).
+      // Rows past B carry dy = 0.
+      const float dyr = (float)(__bf16)dy;
+#pragma unroll 1
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x16 acc = layer2(mt);
         unsigned mk = 0;
+        float v[16];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          bf16x8 hv;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float v = relu_f(acc[8 * s + j]);
-            ys = __builtin_fmaf(v, w3[8 * s + j], ys);
-            hv[j] = (__bf16)v;
-            mk |= (v > 0.f ? 1u : 0u) << (8 * s + j);
-          }
-          if (valid) *reinterpret_cast<bf16x8*>(h2row + 16 * (2 * mt + s) + 8 * h) = hv;  // hperm order
+        for (int e = 0; e < 16; ++e) {
+          const float x = relu_f(acc[e]);
+          mk |= (x > 0.f ? 1u : 0u) << e;
+          v[e] = dyr * (float)(__bf16)x;
+        }
+        rs32_step<16, 16>(v, lv);
+        rs32_step<8, 8>(v, lv);
+        rs32_step<4, 4>(v, lv);
+        rs32_step<2, 2>(v, lv);
+        const float t = v[0] + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v[0]), (1 << 10) | 0x1f));
+        if ((lv & 1) == 0) {
+          const int i = r >> 1;
+          w3part[32 * mt + 16 * (i >> 3) + 8 * h + (i & 7)] += t;
         }
         if (mt < 4) mask_lo |= (unsigned long long)mk << (16 * mt);
         else mask_hi |= (unsigned long long)mk << (16 * (mt - 4));
       }
+      // db3 = sum of bf16(dy) over the rows (lanes of half 0 hold each row once)
+      float d = h == 0 ? dyr : 0.f;
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) d += __shfl_xor(d, o);
+      if (lv == 0) w3part[H] += d;
     }
-    ys += __shfl_xor(ys, 32);
-    const float y = ys + b3;
-    const float diff = valid ? (y - target[row]) : 0.f;
-    const float dy = gscale * diff;
     if (valid && h == 0) {  // dy as an [B,8] bf16 operand (cols 1..7 zero) for the wgrad kernel
       bf16x8 dv;
 #pragma unroll
@@ -340,6 +389,16 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
         }
       }
     }
+  }
+
+  // workgroup dW3 | db3 partial: the waves' rows summed in wave order (deterministic), one fp32
+  // row of w3slab per workgroup; wgrad_reduce sums the rows into the bucket
+  __syncthreads();
+  const float* part = reinterpret_cast<const float*>(smem + L::BLOB);
+  for (int c = threadIdx.x; c < LDA; c += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < wpb; ++k) acc += part[k * LDA + c];
+    w3slab[(size_t)blockIdx.x * LDA + c] = acc;
   }
 }
 
@@ -458,42 +517,51 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
   }
 }
 
+// workgroups of the training forward (= rows of its dW3 slab): one per 8 row tiles, at most one
+// per CU (the blob fills the LDS)
+int train_fwd_grid(int B, int num_cus) {
+  const int ntiles = (B + 31) / 32;
+  const int g = (ntiles + TRAIN_TPB / 64 - 1) / (TRAIN_TPB / 64);
+  return g < num_cus ? g : num_cus;
+}
+
 template <int H>
 static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B, const void* blob,
                                      const NormParams& np, float gscale, void* xf, void* h1a,
-                                     void* h2a, void* dz2, void* dz1, void* dyb, float* sq_err,
+                                     float* w3slab, void* dz2, void* dz1, void* dyb, float* sq_err,
                                      int* step_ctr, int num_cus, hipStream_t stream) {
   using L = TrainLayout<H>;
+  constexpr int TPB = TRAIN_TPB;
+  // the blob + the waves' dW3 partials [TPB / 64][H + 16] f32
+  constexpr size_t LDS = L::BLOB + (size_t)(TPB / 64) * (H + 16) * 4;
+  static_assert(LDS <= 160 * 1024, "training kernel LDS budget");
   static bool attr_set[64] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (!attr_set[dev & 63]) {
     hipError_t e = hipFuncSetAttribute((const void*)eta_mlp3_train_fwd_kernel<H>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::BLOB);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
     if (e != hipSuccess) return e;
     attr_set[dev & 63] = true;
   }
-  const int ntiles = (B + 31) / 32;
-  constexpr int TPB = TRAIN_TPB;
-  int grid = (ntiles + TPB / 64 - 1) / (TPB / 64);
-  if (grid > num_cus) grid = num_cus;
+  const int grid = train_fwd_grid(B, num_cus);
   if (grid < 1) return hipSuccess;
-  hipLaunchKernelGGL(eta_mlp3_train_fwd_kernel<H>, dim3(grid), dim3(TPB), L::BLOB, stream,
+  hipLaunchKernelGGL(eta_mlp3_train_fwd_kernel<H>, dim3(grid), dim3(TPB), LDS, stream,
                      (const int4*)rec, target, B, (const unsigned char*)blob, np, gscale,
-                     (__bf16*)xf, (__bf16*)h1a, (__bf16*)h2a, (__bf16*)dz2, (__bf16*)dz1,
+                     (__bf16*)xf, (__bf16*)h1a, w3slab, (__bf16*)dz2, (__bf16*)dz1,
                      (__bf16*)dyb, sq_err, step_ctr);
   return hipGetLastError();
 }
 
 hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B, const void* blob,
                                      int H, const NormParams& np, float gscale, void* xf,
-                                     void* h1a, void* h2a, void* dz2, void* dz1, void* dyb,
+                                     void* h1a, float* w3slab, void* dz2, void* dz1, void* dyb,
                                      float* sq_err, int* step_ctr, int num_cus,
                                      hipStream_t stream) {
   switch (H) {
-    case 64: return launch_train_fwd_h<64>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
-    case 128: return launch_train_fwd_h<128>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
-    case 256: return launch_train_fwd_h<256>(rec, target, B, blob, np, gscale, xf, h1a, h2a, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
+    case 64: return launch_train_fwd_h<64>(rec, target, B, blob, np, gscale, xf, h1a, w3slab, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
+    case 128: return launch_train_fwd_h<128>(rec, target, B, blob, np, gscale, xf, h1a, w3slab, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
+    case 256: return launch_train_fwd_h<256>(rec, target, B, blob, np, gscale, xf, h1a, w3slab, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }

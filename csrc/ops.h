@@ -27,9 +27,10 @@ hipError_t launch_eta_featurize(const void* rec, float* out, int B, hipStream_t 
 // ---- ETA MLP training (K3) : eta_mlp_train.hip ----
 hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B, const void* blob,
                                      int H, const NormParams& np, float gscale, void* xf,
-                                     void* h1a, void* h2a, void* dz2, void* dz1, void* dyb,
+                                     void* h1a, float* w3slab, void* dz2, void* dz1, void* dyb,
                                      float* sq_err, int* step_ctr, int num_cus,
                                      hipStream_t stream);
+int train_fwd_grid(int B, int num_cus);   // workgroups = rows of the dW3 slab
 size_t eta_mlp3_train_blob_bytes(int H);
 int mlp3_num_params(int H);
 int mlp3_grad_bucket_floats(int H);
@@ -68,7 +69,9 @@ hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm,
                         bool mask_hperm = false, int nsplit = 1);
 hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, float* G, int n,
                                hipStream_t stream, const float* slab1 = nullptr, int S1 = 0,
-                               long long slab_stride1 = 0, float* G1 = nullptr, int n1 = 0);
+                               long long slab_stride1 = 0, float* G1 = nullptr, int n1 = 0,
+                               const float* slab2 = nullptr, int S2 = 0, long long slab_stride2 = 0,
+                               float* G2 = nullptr, int n2 = 0);
 size_t wgrad_lds_bytes(int NT);
 
 // ---- GCN route scorer (K8) : gcn.hip ----

@@ -200,8 +200,8 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
 // the previous one-thread-per-column version ran 73 workgroups and 256 dependent loads per thread.
 constexpr int RED_SL = 16, RED_COLS = 16;
 
-// Two independent segments (slab regions with their own slice counts) in one launch: blocks
-// [0, nb0) reduce segment 0, the rest segment 1.
+// Up to three independent segments (slab regions with their own slice counts) in one launch:
+// blocks [0, nb0) reduce segment 0, [nb0, nb01) segment 1, the rest segment 2.
 struct RedSeg {
   const float* slab;
   long long slab_stride;
@@ -209,14 +209,16 @@ struct RedSeg {
   int S, n;
 };
 
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(RedSeg s0, RedSeg s1, int nb0) {
-  const bool second = (int)blockIdx.x >= nb0;
-  const RedSeg sg = second ? s1 : s0;
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(RedSeg s0, RedSeg s1, RedSeg s2, int nb0,
+                                                           int nb01) {
+  const int bx = (int)blockIdx.x;
+  const int seg = bx < nb0 ? 0 : (bx < nb01 ? 1 : 2);
+  const RedSeg sg = seg == 0 ? s0 : (seg == 1 ? s1 : s2);
   const float* __restrict__ slab = sg.slab;
   const long long slab_stride = sg.slab_stride;
   float* __restrict__ G = sg.G;
   const int S = sg.S, n = sg.n;
-  const int blk = second ? (int)blockIdx.x - nb0 : (int)blockIdx.x;
+  const int blk = bx - (seg == 0 ? 0 : (seg == 1 ? nb0 : nb01));
   __shared__ float4 part[RED_SL][RED_COLS + 1];
   const int c = threadIdx.x & (RED_COLS - 1), sl = threadIdx.x / RED_COLS;
   const int e = (blk * RED_COLS + c) * 4;
@@ -348,13 +350,17 @@ hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm,
 
 hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, float* G, int n,
                                hipStream_t stream, const float* slab1, int S1,
-                               long long slab_stride1, float* G1, int n1) {
+                               long long slab_stride1, float* G1, int n1, const float* slab2, int S2,
+                               long long slab_stride2, float* G2, int n2) {
   const RedSeg s0{slab, slab_stride, G, S, n};
   const RedSeg s1{slab1, slab_stride1, G1, S1, slab1 ? n1 : 0};
+  const RedSeg s2{slab2, slab_stride2, G2, S2, slab2 ? n2 : 0};
   const int nb0 = (n + 4 * RED_COLS - 1) / (4 * RED_COLS);
   const int nb1 = (s1.n + 4 * RED_COLS - 1) / (4 * RED_COLS);
-  if (nb0 + nb1 == 0) return hipSuccess;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb0 + nb1), dim3(256), 0, stream, s0, s1, nb0);
+  const int nb2 = (s2.n + 4 * RED_COLS - 1) / (4 * RED_COLS);
+  if (nb0 + nb1 + nb2 == 0) return hipSuccess;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb0 + nb1 + nb2), dim3(256), 0, stream, s0, s1, s2, nb0,
+                     nb0 + nb1);
   return hipGetLastError();
 }
 

@@ -4,11 +4,13 @@ Per step (all on the current HIP stream, no host synchronisation, HIP-graph capt
 
   eta_mlp3_train_fwd (HIP)  : featurize + 3 layers + MSE grad + the input-gradient path
                             dz2 -> dh1 = dz2 W2 (MFMA on the transposed LDS image of W2) ->
-                            dz1 = dh1 * relu'(z1) (h1 still in registers); writes xf, h1a, h2a,
+                            dz1 = dh1 * relu'(z1) (h1 still in registers); writes xf, h1a,
                             dz2, dz1, dy (activations in the hperm() unit order: 16-byte stores)
+                            and G[w3|b3] = dy^T [h2|1] as one fp32 row per workgroup: relu(z2)
+                            stays in registers, reduce-scattered over the rows (ds_swizzle)
   G[W2|b2] = dz2^T [h1|1]   : split-K wgrad HIP kernel (K = batch) -> fp32 slabs laid out like
-  G[w3|b3] = dy^T  [h2|1]     the flat bucket, then ONE deterministic slab reduction into G
-  G[W1k|b1] = dz1^T [xf]    (xf slot 14 == 1)
+  G[W1k|b1] = dz1^T [xf]      the flat bucket (xf slot 14 == 1), then ONE deterministic reduction
+                            of the three slab regions into G
   all_reduce(G)             : ONE RCCL collective (SUM; dy was pre-scaled by 2/global_batch)
   adamw_pack (HIP)          : AdamW on fp32 master params + re-pack of the training blob
 No library GEMM runs in the step (csrc/eta_mlp_train.hip).
@@ -165,7 +167,6 @@ class FusedMlp3Trainer:
         self.blob = torch.zeros(self.C.eta_mlp3_train_blob_bytes(H), dtype=torch.uint8, device=d)
         self.xf = torch.empty(B, 16, dtype=bf, device=d)
         self.h1a = torch.empty(B, H + 16, dtype=bf, device=d)
-        self.h2a = torch.empty(B, H + 16, dtype=bf, device=d)
         self.dz2 = torch.empty(B, H, dtype=bf, device=d)
         self.dyb = torch.empty(B, 8, dtype=bf, device=d)
         # dW2|db2 (the big block): nsplit column blocks per k-slice, so each slice covers nsplit x
@@ -180,7 +181,11 @@ class FusedMlp3Trainer:
         # the nblk workgroups of a slice share its dz2 rows through one XCD's L2 when S2 % 8 == 0
         self.S2 = max(1, (self.S // nblk) // 8 * 8 or self.S // nblk)
         self.slab2 = torch.empty(self.S2, H * ldg, dtype=torch.float32, device=d)
-        self.slab = torch.empty(self.S, self.G.numel() - H * ldg, dtype=torch.float32, device=d)
+        # dW1 slabs; dW3|db3 arrives as one row per forward workgroup (w3slab): relu(z2) never
+        # leaves the forward kernel's registers
+        self.slab = torch.empty(self.S, H * 16, dtype=torch.float32, device=d)
+        self.w3slab = torch.empty(self.C.train_fwd_grid(B, d.index or 0), ldg, dtype=torch.float32,
+                                  device=d)
         self.dz1 = torch.empty(B, H, dtype=bf, device=d)
         self.sq_err = torch.zeros(B, dtype=torch.float32, device=d)      # per-row squared errors
         self.loss_tiles = self.sq_err                                      # (older name)
@@ -198,16 +203,14 @@ class FusedMlp3Trainer:
         """Fills the flat gradient bucket G (local contribution, pre-scaled for the global mean)."""
         C, H = self.C, self.H
         C.eta_mlp3_train_fwd(rec, tgt_norm, self.blob, H, self.norm, 2.0 / self.global_batch,
-                             self.xf, self.h1a, self.h2a, self.dz2, self.dz1, self.dyb,
+                             self.xf, self.h1a, self.w3slab, self.dz2, self.dz1, self.dyb,
                              self.sq_err, self.step_ctr)
         ldg = H + 16
         C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit)
-        # dW3|db3 = (h2a^T dy)^T: the unit axis (H+16) is the MFMA M side so all 8 waves of a
-        # workgroup work (dy as M = 8 rows left 7 of them idle); only column 0 of dy is real
-        C.wgrad(self.h2a, ldg, ldg, self.dyb, 8, self.slab, 0, 1, None, 1)
         # dW1 = dz1^T x (relu'(z1) applied by the forward kernel)
-        C.wgrad(self.dz1, H, H, self.xf, 16, self.slab, ldg, 16)
-        C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg:])
+        C.wgrad(self.dz1, H, H, self.xf, 16, self.slab, 0, 16)
+        C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg + ldg:],
+                       self.w3slab, self.G[H * ldg:H * ldg + ldg])
 
     def step(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> torch.Tensor:
         """One optimizer step; returns the device tensor of per-row squared errors (no sync)."""

@@ -41,8 +41,8 @@ def test_initial_pack_matches_host_pack(H):
     assert torch.equal(tr.blob.cpu(), ref)
 
 
-@pytest.mark.parametrize("H", [64, 256])
-@pytest.mark.parametrize("B", [1000, 8192])
+@pytest.mark.parametrize("H", [64, 128, 256])
+@pytest.mark.parametrize("B", [1000, 8192, 70000])
 def test_fused_gradients_match_autograd(H, B):
     m = _model(H)
     rt, yn = _batch(B, m)
