@@ -636,18 +636,20 @@ void gcn_spmm_score(torch::Tensor Z, torch::Tensor indptr, torch::Tensor indices
                                          (int)row0, (int)row1, cur_stream(Z)));
 }
 
-torch::Tensor route_score(torch::Tensor rptr, torch::Tensor nodes, torch::Tensor lat, torch::Tensor lon,
-                          torch::Tensor delay) {
-  for (auto* t : {&rptr, &nodes, &lat, &lon, &delay}) check_dev(*t, "route_score input");
-  TORCH_CHECK(rptr.scalar_type() == torch::kInt32 && nodes.scalar_type() == torch::kInt32, "i32 routes");
-  TORCH_CHECK(lat.scalar_type() == torch::kFloat32 && lon.scalar_type() == torch::kFloat32 &&
-              delay.scalar_type() == torch::kFloat32, "f32 lat/lon/delay");
+// latlon: f32 [N, 2] (degrees), delay: f32 [>= N]; node ids outside [0, N) add nothing
+torch::Tensor route_score(torch::Tensor rptr, torch::Tensor nodes, torch::Tensor latlon, torch::Tensor delay) {
+  for (auto* t : {&rptr, &nodes, &latlon, &delay}) check_dev(*t, "route_score input");
+  TORCH_CHECK(rptr.scalar_type() == torch::kInt32 && nodes.scalar_type() == torch::kInt32 &&
+                  rptr.is_contiguous() && nodes.is_contiguous(), "i32 routes");
+  TORCH_CHECK(latlon.scalar_type() == torch::kFloat32 && latlon.dim() == 2 && latlon.size(1) == 2 &&
+                  latlon.is_contiguous(), "latlon must be f32 [N, 2]");
+  TORCH_CHECK(delay.scalar_type() == torch::kFloat32 && delay.numel() >= latlon.size(0), "delay f32 [>= N]");
   const c10::DeviceGuard guard(rptr.device());
   const int R = (int)rptr.numel() - 1;
   auto score = torch::empty({R}, delay.options());
-  RT_CHECK_HIP(rt::launch_route_score(rptr.data_ptr<int>(), nodes.data_ptr<int>(), lat.data_ptr<float>(),
-                                      lon.data_ptr<float>(), delay.data_ptr<float>(),
-                                      score.data_ptr<float>(), R, cur_stream(rptr)));
+  RT_CHECK_HIP(rt::launch_route_score(rptr.data_ptr<int>(), nodes.data_ptr<int>(), latlon.data_ptr<float>(),
+                                      delay.data_ptr<float>(), score.data_ptr<float>(), R,
+                                      (int)latlon.size(0), cur_stream(rptr)));
   return score;
 }
 

@@ -19,6 +19,79 @@
 
 namespace rt {
 
+// acc[0..8) += sum over CSR entries e0..e1 of values[e] * X[indices[e]][c .. c+8), in entry order
+// (the same fp32 sums as a plain loop).  Entries go in batches of RB: all index/weight loads of a
+// batch, then all RB feature-row loads, are in flight together — one memory round trip per level
+// and batch instead of two dependent loads per edge (road-graph rows hold 3-9 entries).  Batch
+// slots past e1 load row 0 (a valid address) and are masked out of the sum.
+template <int RB>
+__device__ __forceinline__ void csr_gather8(const __bf16* __restrict__ X, int F, int c,
+                                            const int* __restrict__ indices,
+                                            const float* __restrict__ values, int e0, int e1,
+                                            float (&acc)[8]) {
+  for (int eb = e0; eb < e1; eb += RB) {
+    int u[RB];
+    float wv[RB];
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const bool in = eb + j < e1;
+      u[j] = in ? indices[eb + j] : 0;
+      wv[j] = in ? values[eb + j] : 0.f;
+    }
+    bf16x8 x[RB];
+#pragma unroll
+    for (int j = 0; j < RB; ++j) x[j] = *reinterpret_cast<const bf16x8*>(X + (size_t)u[j] * F + c);
+#pragma unroll
+    for (int j = 0; j < RB; ++j)
+      if (eb + j < e1) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += wv[j] * (float)x[j][k];
+      }
+  }
+}
+
+// The same for NP rows per lane at once (row p: entries e0[p]..e1[p], sums into acc[p]): batch b of
+// every row is loaded together, so the NP rows share each round trip.
+template <int RB, int NP>
+__device__ __forceinline__ void csr_gather8_rows(const __bf16* __restrict__ X, int F, int c,
+                                                 const int* __restrict__ indices,
+                                                 const float* __restrict__ values,
+                                                 const int (&e0)[NP], const int (&e1)[NP],
+                                                 float (&acc)[NP][8]) {
+  int nb = 0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int n = (e1[p] - e0[p] + RB - 1) / RB;
+    nb = n > nb ? n : nb;
+  }
+  for (int b = 0; b < nb; ++b) {
+    int u[NP][RB];
+    float wv[NP][RB];
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int j = 0; j < RB; ++j) {
+        const int e = e0[p] + b * RB + j;
+        const bool in = e < e1[p];
+        u[p][j] = in ? indices[e] : 0;
+        wv[p][j] = in ? values[e] : 0.f;
+      }
+    bf16x8 x[NP][RB];
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int j = 0; j < RB; ++j) x[p][j] = *reinterpret_cast<const bf16x8*>(X + (size_t)u[p][j] * F + c);
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int j = 0; j < RB; ++j)
+        if (e0[p] + b * RB + j < e1[p]) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[p][k] += wv[p][j] * (float)x[p][j][k];
+        }
+  }
+}
+
 template <int FIN, int FOUT, bool AGG, bool RELU>
 __global__ __launch_bounds__(256) void gcn_agg_gemm_kernel(
     const __bf16* __restrict__ X, const int* __restrict__ indptr, const int* __restrict__ indices,
@@ -51,14 +124,7 @@ __global__ __launch_bounds__(256) void gcn_agg_gemm_kernel(
       for (int j = 0; j < 8; ++j) acc[j] = 0.f;
       if (v < row1) {
         if constexpr (AGG) {
-          const int e0 = indptr[v], e1 = indptr[v + 1];
-          for (int e = e0; e < e1; ++e) {
-            const int u = indices[e];
-            const float wv = values[e];
-            const bf16x8 x = *reinterpret_cast<const bf16x8*>(X + (size_t)u * FIN + c);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[j] += wv * (float)x[j];
-          }
+          csr_gather8<8>(X, FIN, c, indices, values, indptr[v], indptr[v + 1], acc);
         } else {
           const bf16x8 x = *reinterpret_cast<const bf16x8*>(X + (size_t)v * FIN + c);
 #pragma unroll
@@ -123,26 +189,25 @@ __global__ __launch_bounds__(256) void gcn_l1_fused_kernel(
   const int lb = (int)(blockIdx.x % 8u) * (int)(gridDim.x / 8u) + (int)(blockIdx.x / 8u);
   for (int t = lb * 4 + w; t < ntiles; t += gridDim.x * 4) {
     const int base = row0 + t * 32;
-    // (1) aggregation Â X of the tile's 32 nodes -> A tile [32][LDA]
-#pragma unroll
-    for (int pass = 0; pass < 32 / RPP; ++pass) {
-      const int rr = pass * RPP + lane / G;
+    // (1) aggregation Â X of the tile's 32 nodes -> A tile [32][LDA]: every lane gathers its rows of
+    // all passes together (one round trip per CSR level for the whole tile)
+    {
+      constexpr int NP = 32 / RPP;
       const int c = (lane % G) * 8;
-      const int v = base + rr;
-      float acc[8];
+      int e0[NP], e1[NP];
+      float acc[NP][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-      if (v < row1) {
-        const int e0 = indptr[v], e1 = indptr[v + 1];
-        for (int e = e0; e < e1; ++e) {
-          const int u = indices[e];
-          const float wv = values[e];
-          const bf16x8 x = *reinterpret_cast<const bf16x8*>(X + (size_t)u * FIN + c);
+      for (int p = 0; p < NP; ++p) {
+        const int v = base + p * RPP + lane / G;
+        e0[p] = v < row1 ? indptr[v] : 0;
+        e1[p] = v < row1 ? indptr[v + 1] : 0;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] += wv * (float)x[j];
-        }
+        for (int j = 0; j < 8; ++j) acc[p][j] = 0.f;
       }
-      *reinterpret_cast<bf16x8*>(tile + rr * LDA + c) = to_bf16x8(acc);
+      csr_gather8_rows<8, NP>(X, FIN, c, indices, values, e0, e1, acc);
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        *reinterpret_cast<bf16x8*>(tile + (p * RPP + lane / G) * LDA + c) = to_bf16x8(acc[p]);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
@@ -222,14 +287,7 @@ __global__ __launch_bounds__(256) void gcn_spmm_score_kernel(
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    const int e0 = indptr[v], e1 = indptr[v + 1];
-    for (int e = e0; e < e1; ++e) {
-      const int u = indices[e];
-      const float wv = values[e];
-      const bf16x8 z = *reinterpret_cast<const bf16x8*>(Z + (size_t)u * F + c);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += wv * (float)z[j];
-    }
+    csr_gather8<8>(Z, F, c, indices, values, indptr[v], indptr[v + 1], acc);
 #pragma unroll
     for (int j = 0; j < 8; ++j) part += (acc[j] + b2[c + j]) * wo[c + j];
   }
@@ -243,28 +301,39 @@ __global__ __launch_bounds__(256) void gcn_spmm_score_kernel(
 }
 
 // score[r] = sum_i delay[v_i] * haversine(v_i, v_{i+1}) over route r's node list (one wave / route).
-// Measured alternatives (bench/gcn_bench.py, 10k routes of 50-300 nodes): a 16-lane group per route
-// 18.3 us, loads of 4 segments per lane issued before computing 14.7 us, this form 13.7 us.
+// The kernel is bound by the texture path's gather rate (each wave-load of 64 random node ids
+// touches up to 64 cache lines), not by latency: issuing 4 segments' loads ahead was slower.  So
+// each node is gathered ONCE: lane l of a 64-node window loads node i = i0 + l (lat/lon as one
+// 8-byte pair, its delay), and takes v_{i+1}'s position from lane l + 1 (ds_bpermute); windows
+// advance by 63 nodes.  2 gathers per segment instead of 5 (lat, lon of both ends + delay).
+// Node ids outside [0, N) contribute nothing.
 __global__ __launch_bounds__(256) void route_score_kernel(const int* __restrict__ rptr,
                                                           const int* __restrict__ nodes,
-                                                          const float* __restrict__ lat,
-                                                          const float* __restrict__ lon,
+                                                          const float2* __restrict__ latlon,
                                                           const float* __restrict__ delay,
-                                                          float* __restrict__ score, int R) {
+                                                          float* __restrict__ score, int R, int N) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= R) return;
   const int p0 = rptr[r], p1 = rptr[r + 1];
   float s = 0.f;
   const float k = 0.017453292519943295f;
-  for (int i = p0 + lane; i < p1 - 1; i += 64) {
-    const int a = nodes[i], b = nodes[i + 1];
-    const float la1 = lat[a] * k, la2 = lat[b] * k;
-    const float dphi = la2 - la1, dl = (lon[b] - lon[a]) * k;
-    const float s1 = __sinf(0.5f * dphi), s2 = __sinf(0.5f * dl);
-    const float hv = s1 * s1 + __cosf(la1) * __cosf(la2) * s2 * s2;
-    const float d = 2.f * 6371000.f * asinf(sqrtf(fminf(1.f, fmaxf(0.f, hv))));
-    s += delay[a] * d;
+  for (int i0 = p0; i0 < p1 - 1; i0 += 63) {
+    const int i = i0 + lane;
+    const int a = i < p1 ? nodes[i] : -1;
+    const bool ok = a >= 0 && a < N;
+    const float2 ll = ok ? latlon[a] : make_float2(0.f, 0.f);
+    const float dv = ok ? delay[a] : 0.f;
+    const float lat2 = __shfl_down(ll.x, 1), lon2 = __shfl_down(ll.y, 1);
+    const int b = __shfl_down(a, 1);
+    if (lane < 63 && i + 1 < p1 && ok && b >= 0 && b < N) {
+      const float la1 = ll.x * k, la2 = lat2 * k;
+      const float dphi = la2 - la1, dl = (lon2 - ll.y) * k;
+      const float s1 = __sinf(0.5f * dphi), s2 = __sinf(0.5f * dl);
+      const float hv = s1 * s1 + __cosf(la1) * __cosf(la2) * s2 * s2;
+      const float d = 2.f * 6371000.f * asinf(sqrtf(fminf(1.f, fmaxf(0.f, hv))));
+      s += dv * d;
+    }
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
@@ -322,12 +391,11 @@ hipError_t launch_gcn_spmm_score(const void* Z, const int* indptr, const int* in
   return hipGetLastError();
 }
 
-hipError_t launch_route_score(const int* rptr, const int* nodes, const float* lat,
-                              const float* lon, const float* delay, float* score, int R,
-                              hipStream_t stream) {
+hipError_t launch_route_score(const int* rptr, const int* nodes, const float* latlon,
+                              const float* delay, float* score, int R, int N, hipStream_t stream) {
   if (R <= 0) return hipSuccess;
-  hipLaunchKernelGGL(route_score_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, rptr, nodes, lat, lon,
-                     delay, score, R);
+  hipLaunchKernelGGL(route_score_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, rptr, nodes,
+                     (const float2*)latlon, delay, score, R, N);
   return hipGetLastError();
 }
 

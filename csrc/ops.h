@@ -85,9 +85,8 @@ hipError_t launch_gcn_l1_fused(const void* X, const int* indptr, const int* indi
 hipError_t launch_gcn_spmm_score(const void* Z, const int* indptr, const int* indices,
                                  const float* values, const float* b2, const float* wo, float bo,
                                  float* delay, int row0, int row1, hipStream_t stream);
-hipError_t launch_route_score(const int* rptr, const int* nodes, const float* lat,
-                              const float* lon, const float* delay, float* score, int R,
-                              hipStream_t stream);
+hipError_t launch_route_score(const int* rptr, const int* nodes, const float* latlon,
+                              const float* delay, float* score, int R, int N, hipStream_t stream);
 
 // ---- batched A* (K9) : astar.hip ----
 hipError_t launch_astar(const int* indptr, const int* indices, const float* cost, const float* lat,

@@ -128,6 +128,8 @@ class GcnScorerHip:
         self.delay = torch.zeros(npad, dtype=torch.float32, device=d)
         self.lat = torch.from_numpy(g.lat.astype(np.float32)).to(d)
         self.lon = torch.from_numpy(g.lon.astype(np.float32)).to(d)
+        # one 8-byte gather per route node in route_score_kernel
+        self.latlon = torch.stack([self.lat, self.lon], 1).contiguous()
 
     def node_delays(self) -> torch.Tensor:
         C, (r0, r1) = self.C, self.rows
@@ -161,4 +163,4 @@ class GcnScorerHip:
             dist.all_gather_into_tensor(full, own.clone(), group=self.group)
 
     def score_routes(self, rptr: torch.Tensor, nodes: torch.Tensor) -> torch.Tensor:
-        return self.C.route_score(rptr, nodes, self.lat, self.lon, self.delay)
+        return self.C.route_score(rptr, nodes, self.latlon, self.delay)

@@ -81,3 +81,28 @@ def test_gcn_fused_layer1_bitwise_equals_two_launch_path(rows, monkeypatch):
     split.node_delays()
     assert torch.equal(fused.Z[r0:r1], split.Z[r0:r1])
     assert torch.equal(fused.delay[r0:r1], split.delay[r0:r1])
+
+
+def test_route_score_windows_and_bad_ids():
+    """route_score_kernel walks 64-node windows advancing by 63 (the next node's position comes from
+    the neighbouring lane): lengths around the window edges, 0/1-node routes, and node ids outside
+    [0, N) (their segments add nothing)."""
+    g = synth_road_graph(5_000, seed=5)
+    m = GcnScorer(seed=6)
+    hip = GcnScorerHip(m, g, torch.device("cuda:0"))
+    delay = hip.node_delays().cpu().numpy()
+    routes = [w[:L] for w, L in zip(_random_walks(g, 9, seed=7, lo=300, hi=301),
+                                    [0, 1, 2, 63, 64, 65, 126, 127, 128])]
+    bad = list(_random_walks(g, 1, seed=8, lo=100, hi=101)[0])
+    bad[10], bad[50] = -1, g.num_nodes + 3
+    routes.append(bad)
+    ptr, nodes = routes_to_csr(routes)
+    got = hip.score_routes(torch.from_numpy(ptr).cuda(), torch.from_numpy(nodes).cuda()).cpu().numpy()
+    good = [r for r in routes[:-1]]
+    ref = list(score_routes_ref(g, delay, good))
+    # the bad route: sum of the segments whose two ends are valid nodes
+    segs = [[bad[i], bad[i + 1]] for i in range(len(bad) - 1)
+            if 0 <= bad[i] < g.num_nodes and 0 <= bad[i + 1] < g.num_nodes]
+    ref.append(sum(score_routes_ref(g, delay, segs)))
+    np.testing.assert_allclose(got, np.array(ref, dtype=np.float64), rtol=1e-3, atol=1e-3)
+    assert got[0] == 0.0 and got[1] == 0.0
