@@ -222,18 +222,6 @@ def main() -> None:
     elapsed = pipe.timed(a.warmup, a.steps)
     step_dist = pipe.step_ms          # intervals between consecutive steps' kernel completions
 
-    # whole-node runs: what the xGMI links delivered, measured on the same ranks right after the
-    # timed region (RCCL all-reduce / all-gather sweep; extra JSON key, outside the timing)
-    coll = None
-    if world > 1 and not share and os.environ.get("ROUTEST_BENCH_COLLECTIVES", "1") != "0":
-        # RCCL only (the process group bench.py already holds): nothing here can leave one rank
-        # waiting on a set-up step another rank skipped
-        from routest_amd.parallel.collective_probe import sweep
-        try:
-            coll = sweep(dev)
-        except Exception as e:  # noqa: BLE001 - the headline line must still print
-            coll = [{"error": repr(e)[:200]}]
-
     # the link bound: the record DMA alone, same bytes, same stream (what the step cannot beat)
     h2d_only_ms = None
     if a.io == "hybrid":
@@ -285,8 +273,15 @@ def main() -> None:
 
     # config 3 on the same ranks: the fused DP training step (forward + MSE gradient + dgrad in
     # one kernel, split-K weight gradients, one flat-bucket all-reduce, fused AdamW + re-pack)
-    train_res = None
-    if a.train_steps > 0:
+    def agree(ok_local: bool) -> bool:
+        """True only if every rank says so (one collective every rank reaches)."""
+        if world == 1:
+            return ok_local
+        t = torch.tensor([0.0 if ok_local else 1.0], device="cpu" if share else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()) == 0.0
+
+    def train_probe(comm=None):
         from routest_amd.train.fused import FusedMlp3Trainer
         tB = 65536
         torch.manual_seed(4321)                 # identical initial parameters on every rank
@@ -294,11 +289,13 @@ def main() -> None:
         tmodel.fit_normalization(records_to_features(norm_rec), norm_y)
         trec, ty = synth_records(tB, seed=300 + rank)
         trt = records_to_tensor(trec).to(dev)
-        tr = FusedMlp3Trainer(tmodel, dev, tB, tB * world, lr=1e-3, allreduce=world > 1)
+        tr = FusedMlp3Trainer(tmodel, dev, tB, tB * world, lr=1e-3, allreduce=world > 1, comm=comm)
         yn = tr.normalize_targets(torch.from_numpy(ty).to(dev))
         for _ in range(5):
             tr.step(trt, yn)
         torch.cuda.synchronize()
+        if comm is not None and not agree(not comm.C.comm_error(comm.h)):
+            return {"error": "one-shot all-reduce: a peer wait timed out during warmup"}
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -315,13 +312,57 @@ def main() -> None:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             tel = float(t.item())
         loss = float(tr.sq_err.sum().item()) / tB
-        train_res = {"samples_per_s": tB * world * a.train_steps / tel,
-                     "ms_per_step": tel / a.train_steps * 1e3, "batch_per_gpu": tB,
-                     "global_batch": tB * world, "steps": a.train_steps,
-                     "allreduce": ("none" if world == 1 else "gloo (shared GPU)" if share
-                                   else "RCCL, one flat fp32 bucket"),
-                     "final_local_mse_normalized": loss}
+        res = {"samples_per_s": tB * world * a.train_steps / tel,
+               "ms_per_step": tel / a.train_steps * 1e3, "batch_per_gpu": tB,
+               "global_batch": tB * world, "steps": a.train_steps,
+               "allreduce": ("none" if world == 1 else "gloo (shared GPU)" if share and comm is None
+                             else "RCCL, one flat fp32 bucket" if comm is None else
+                             "one-shot over IPC-mapped peer HBM (csrc/comm.hip), one flat fp32 bucket"),
+               "final_local_mse_normalized": loss}
+        if comm is not None:
+            res["comm_error"] = not agree(not comm.C.comm_error(comm.h))
+            # every rank must hold the same parameters after the identical reduced updates
+            ph = torch.tensor([float(tr.P.double().sum())], device="cpu" if share else dev,
+                              dtype=torch.float64)
+            lo, hi = ph.clone(), ph.clone()
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            res["params_identical_across_ranks"] = bool(float(lo.item()) == float(hi.item()))
         del tr, trt
+        return res
+
+    train_res = train_probe() if a.train_steps > 0 else None
+
+    # the same training step with the native one-shot all-reduce (one hop over all 7 xGMI links at
+    # once, instead of RCCL's latency-bound ring at this 296 KB bucket).  Set-up failures and peer
+    # timeouts are agreed on by every rank before anything else runs, so no rank is left waiting.
+    train_os_res = None
+    devcomm = None
+    if a.train_steps > 0 and world > 1 and os.environ.get("ROUTEST_BENCH_ONESHOT", "1") != "0":
+        from routest_amd.parallel.comm import DeviceComm
+        err = None
+        try:
+            devcomm = DeviceComm(dev, use_rccl=False)
+            ok = devcomm.oneshot
+        except Exception as e:  # noqa: BLE001 - reported, never fatal for the headline
+            ok, err = False, repr(e)[:200]
+        if agree(ok):
+            train_os_res = train_probe(devcomm)
+        else:
+            train_os_res = {"error": err or "one-shot set-up failed on a peer rank"}
+            devcomm = None
+
+    # whole-node runs: what the xGMI links delivered, measured on the same ranks right after the
+    # timed region (RCCL all-reduce / all-gather sweep; extra JSON key, outside the timing)
+    coll = None
+    if world > 1 and not share and os.environ.get("ROUTEST_BENCH_COLLECTIVES", "1") != "0":
+        # RCCL only (the process group bench.py already holds): nothing here can leave one rank
+        # waiting on a set-up step another rank skipped
+        from routest_amd.parallel.collective_probe import sweep
+        try:
+            coll = sweep(dev, native=devcomm)
+        except Exception as e:  # noqa: BLE001 - the headline line must still print
+            coll = [{"error": repr(e)[:200]}]
 
     # config 4 on the same ranks: the 2-layer GCN scorer, graph replicated on every GPU (no
     # collective) and row-partitioned (each rank runs 1/N of the nodes, RCCL all-gather of Z)
@@ -345,8 +386,12 @@ def main() -> None:
         ptr, nodes = routes_to_csr(walks)
         ptr_t, nodes_t = torch.from_numpy(ptr).to(dev), torch.from_numpy(nodes).to(dev)
         gcn_res = {"nodes": g.num_nodes, "edges": g.num_edges, "routes_per_step": nroutes * world}
-        for mode in (["replicate", "partition"] if world > 1 else ["replicate"]):
-            hip = GcnScorerHip(gm, g, dev, mode=mode, rank=rank, world=world)
+        modes = ["replicate"] + (["partition"] if world > 1 else [])
+        if world > 1 and devcomm is not None:
+            modes.append("partition_oneshot")     # Z gathered over IPC-mapped peer HBM in one hop
+        for mode in modes:
+            hip = GcnScorerHip(gm, g, dev, mode=mode.split("_")[0], rank=rank, world=world,
+                               comm=devcomm if mode.endswith("oneshot") else None)
 
             def gstep():
                 hip.node_delays()
@@ -479,12 +524,16 @@ def main() -> None:
             "shared_gpu": bool(share and world > 1),
             "collectives": coll,
             "dp_training": train_res,
+            "dp_training_oneshot": train_os_res,
             "gcn": gcn_res,
             "check_max_err_vs_emulation": err_emu,
             "check_max_err_vs_fp32": err_fp32,
             "finite": ok,
         }
         print(json.dumps(out), flush=True)
+    if devcomm is not None:
+        torch.cuda.synchronize()
+        devcomm.close()
     if world > 1:
         dist.destroy_process_group()
     if not ok:
