@@ -65,6 +65,12 @@ def parse_args():
                     help="also time this many data-parallel training steps of the same MLP on the "
                          "same ranks (64k rows per GPU, one flat-bucket RCCL all-reduce per step; "
                          "extra JSON key 'dp_training')")
+    ap.add_argument("--route-requests", type=int, default=10_000,
+                    help="config 5: concurrent multi-stop requests per step over all ranks")
+    ap.add_argument("--route-steps", type=int, default=3,
+                    help="also time this many steps of the batched route optimizer (K5 + K6 + one "
+                         "A* launch over MLP edge costs; extra JSON key 'route_optimizer'; skipped "
+                         "on a shared GPU)")
     return ap.parse_args()
 
 
@@ -367,6 +373,7 @@ def main() -> None:
     # config 4 on the same ranks: the 2-layer GCN scorer, graph replicated on every GPU (no
     # collective) and row-partitioned (each rank runs 1/N of the nodes, RCCL all-gather of Z)
     gcn_res = None
+    g = None
     if a.gcn_steps > 0 and not (share and world > 1):
         from routest_amd.data.graph import synth_road_graph
         from routest_amd.models.gcn import GcnScorer, GcnScorerHip, routes_to_csr
@@ -417,6 +424,49 @@ def main() -> None:
             gcn_res[mode] = {"ms_per_step": gel / a.gcn_steps * 1e3,
                              "routes_per_s": nroutes * world * a.gcn_steps / gel}
             del hip
+
+    # config 5 on the same ranks: 10k concurrent multi-stop requests sharded over the ranks, each
+    # step K5 + K6 for all of a rank's requests, then every trip leg in ONE batched A* launch over
+    # MLP-learned edge times (no collective; timing max over ranks)
+    route_res = None
+    if a.route_steps > 0 and not (share and world > 1):
+        from routest_amd.data.graph import synth_road_graph
+        from routest_amd.routing.bulk import BulkRouteStep
+        from routest_amd.routing.graph import edge_costs
+        from routest_amd.serve.eta_service import default_model
+        if g is None:
+            g = synth_road_graph(100_000, seed=0)
+        torch.manual_seed(0)
+        cost = edge_costs(g, default_model(hidden=a.hidden, steps=200), device=dev)
+        bulk = BulkRouteStep(g, cost, dev, a.route_requests // world, seed=100 + rank)
+        bulk.step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        legs, unfound = 0, 0
+        for _ in range(a.route_steps):
+            nl, _, st, _ = bulk.step()
+            legs += nl
+            unfound += (st != 0).sum()          # device-side count, read once after the loop
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        rel = time.perf_counter() - t0
+        unfound = int(unfound)
+        if world > 1:
+            t = torch.tensor([rel], device=dev, dtype=torch.float64)
+            tl = torch.tensor([float(legs), float(unfound)], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tl)
+            rel, legs, unfound = float(t[0]), int(tl[0]), int(tl[1])
+        R = a.route_requests // world * world
+        route_res = {"requests_per_step": R, "steps": a.route_steps,
+                     "ms_per_step": rel / a.route_steps * 1e3,
+                     "requests_per_s": R * a.route_steps / rel,
+                     "astar_legs_per_s": legs / rel, "astar_unfound_legs": unfound,
+                     "graph_nodes": g.num_nodes}
+        del bulk
 
     p50_ms = p99_ms = None
     p50_fastapi_ms = None
@@ -526,6 +576,7 @@ def main() -> None:
             "dp_training": train_res,
             "dp_training_oneshot": train_os_res,
             "gcn": gcn_res,
+            "route_optimizer": route_res,
             "check_max_err_vs_emulation": err_emu,
             "check_max_err_vs_fp32": err_fp32,
             "finite": ok,

@@ -29,61 +29,25 @@ def main() -> None:
     a = ap.parse_args()
     from routest_amd.parallel.launch import ensure_ranks, share_gpu
     ensure_ranks(a.gpus, __file__)
-    import numpy as np
     import torch
     import torch.distributed as dist
     from routest_amd.data.graph import synth_road_graph
-    from routest_amd.ops import _ext
     from routest_amd.parallel.dp import allreduce_scalars, barrier, init_distributed
-    from routest_amd.routing.batched import pack_requests
-    from routest_amd.routing.graph import BatchedAstar, edge_costs
+    from routest_amd.routing.bulk import BulkRouteStep
+    from routest_amd.routing.graph import edge_costs
     from routest_amd.serve.eta_service import default_model
 
     di = init_distributed()
     dev = di.device
-    C = _ext.native()
     g = synth_road_graph(a.nodes, seed=0)
     torch.manual_seed(0)
     cost = edge_costs(g, default_model(hidden=256, steps=200), device=dev)
-    rng = np.random.default_rng(100 + di.rank)
     R = a.requests // di.world
-    reqs, snapped = [], []
-    for _ in range(R):
-        n = int(rng.integers(2, 11))
-        nodes = rng.integers(0, g.num_nodes, n + 1)
-        reqs.append({"source_point": {"lat": float(g.lat[nodes[0]]), "lon": float(g.lon[nodes[0]])},
-                     "destination_points": [{"lat": float(g.lat[v]), "lon": float(g.lon[v]),
-                                             "payload": int(rng.integers(1, 4))} for v in nodes[1:]],
-                     "driver_details": {"vehicle_capacity": 8, "maximum_distance": 150_000}})
-        snapped.append(nodes.astype(np.int32))
-    lat, lon, dem, npts, cap, maxd = pack_requests(reqs)
-    T = lambda x, dt=torch.float64: torch.as_tensor(x, dtype=dt).to(dev)  # noqa: E731
-    lat_t, lon_t, dem_t, npts_t, cap_t, maxd_t = T(lat), T(lon), T(dem), T(npts, torch.int32), T(cap), T(maxd)
-    NM = lat.shape[1]
-    snap = np.full((R, NM), -1, dtype=np.int32)
-    for k, s in enumerate(snapped):
-        snap[k, :len(s)] = s
-    snap_t = torch.from_numpy(snap).to(dev)
-    # every leg of a step in ONE launch: ~80k concurrent searches (dense per-slot state ~95 GB —
-    # sized for 288 GB of HBM3E) so each CU keeps ~5 waves of latency-bound searches in flight
-    legs_est = int(sum(len(s) for s in snapped) * 1.4) + 1024
-    astar = BatchedAstar(g, cost, dev, slots=min(legs_est, 98304), cap=65536)
+    bulk = BulkRouteStep(g, cost, dev, R, seed=100 + di.rank)
 
     def step():
-        D = C.route_haversine_matrix(lat_t, lon_t, npts_t, 1.3)
-        visit, trip_of, ntrips, status = C.route_greedy_cvrp(D, npts_t, dem_t, cap_t, maxd_t)
-        # legs: depot -> first stop, stop -> stop within a trip, last stop -> depot  (device-side)
-        valid = visit >= 0
-        prev_same = torch.zeros_like(valid)
-        prev_same[:, 1:] = valid[:, 1:] & (trip_of[:, 1:] == trip_of[:, :-1])
-        next_same = torch.zeros_like(valid)
-        next_same[:, :-1] = valid[:, :-1] & (trip_of[:, :-1] == trip_of[:, 1:])
-        vnode = torch.gather(snap_t, 1, visit.clamp_min(0).long())
-        prev_node = torch.where(prev_same, torch.roll(vnode, 1, 1), snap_t[:, :1].expand_as(vnode))
-        src = torch.cat([prev_node[valid], vnode[valid & ~next_same]])
-        dst = torch.cat([vnode[valid], snap_t[:, :1].expand_as(vnode)[valid & ~next_same]])
-        c, n, st, _ = astar.run(src.cpu().numpy(), dst.cpu().numpy())
-        return int(src.numel()), c, st
+        nl, c, st, _ = bulk.step()
+        return nl, c, st
 
     for _ in range(a.warmup):
         step()

@@ -1,0 +1,79 @@
+"""Config 5 step: R concurrent multi-stop requests on one device, end to end on the GPU.
+
+Per step, for all R requests of this rank (each: depot + 2..10 stops snapped to road-graph nodes):
+
+  K5 haversine matrices + K6 greedy multi-trip CVRP     (one launch each, all requests)
+  -> every trip leg (consecutive stops, depot returns) as one A* query  (K9, one launch)
+  -> per-leg costs from the learned edge times (the ETA MLP over edge features, ``edge_costs``)
+
+The legs are derived on the device from K6's visit order; only the (src, dst) node lists cross to
+the host once for the A* launch.  Used by ``bench/route_bench.py`` and the ``route_optimizer`` key of
+``bench.py`` (requests sharded over ranks, no collective: SURVEY §2.7 C6 / §2.8 P2).  Replaces the
+reference's per-request remote ORS matrix + greedy loop + per-trip directions
+(``/root/reference/backend/route_optimizer_twx2/Flaskr/utils.py:85-193``).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..ops import _ext
+from .batched import pack_requests
+from .graph import BatchedAstar
+
+
+class BulkRouteStep:
+    def __init__(self, g, cost: np.ndarray, device, requests: int, seed: int = 100,
+                 max_slots: int = 98304, astar: Optional[BatchedAstar] = None):
+        self.C = _ext.native(required=True)
+        self.dev = d = torch.device(device)
+        rng = np.random.default_rng(seed)
+        reqs, snapped = [], []
+        for _ in range(requests):
+            n = int(rng.integers(2, 11))
+            nodes = rng.integers(0, g.num_nodes, n + 1)
+            reqs.append({"source_point": {"lat": float(g.lat[nodes[0]]), "lon": float(g.lon[nodes[0]])},
+                         "destination_points": [{"lat": float(g.lat[v]), "lon": float(g.lon[v]),
+                                                 "payload": int(rng.integers(1, 4))} for v in nodes[1:]],
+                         "driver_details": {"vehicle_capacity": 8, "maximum_distance": 150_000}})
+            snapped.append(nodes.astype(np.int32))
+        lat, lon, dem, npts, cap, maxd = pack_requests(reqs)
+        T = lambda x, dt=torch.float64: torch.as_tensor(x, dtype=dt).to(d)  # noqa: E731
+        self.lat, self.lon, self.dem = T(lat), T(lon), T(dem)
+        self.npts, self.cap, self.maxd = T(npts, torch.int32), T(cap), T(maxd)
+        snap = np.full((requests, lat.shape[1]), -1, dtype=np.int32)
+        for k, s in enumerate(snapped):
+            snap[k, :len(s)] = s
+        self.snap = torch.from_numpy(snap).to(d)
+        self.requests = requests
+        # every leg of a step in ONE launch (~80k concurrent searches on one GPU: the dense per-slot
+        # state is sized for 288 GB of HBM3E) so each CU keeps several waves of searches in flight
+        legs_est = int(sum(len(s) for s in snapped) * 1.4) + 1024
+        self.astar = astar or BatchedAstar(g, cost, d, slots=min(legs_est, max_slots), cap=65536)
+
+    def legs(self):
+        """K5 + K6 for every request, then the trip legs as (src, dst) node tensors on the device."""
+        C = self.C
+        D = C.route_haversine_matrix(self.lat, self.lon, self.npts, 1.3)
+        visit, trip_of, ntrips, status = C.route_greedy_cvrp(D, self.npts, self.dem, self.cap, self.maxd)
+        snap = self.snap
+        valid = visit >= 0
+        prev_same = torch.zeros_like(valid)
+        prev_same[:, 1:] = valid[:, 1:] & (trip_of[:, 1:] == trip_of[:, :-1])
+        next_same = torch.zeros_like(valid)
+        next_same[:, :-1] = valid[:, :-1] & (trip_of[:, :-1] == trip_of[:, 1:])
+        vnode = torch.gather(snap, 1, visit.clamp_min(0).long())
+        depot = snap[:, :1].expand_as(vnode)
+        prev_node = torch.where(prev_same, torch.roll(vnode, 1, 1), depot)
+        last = valid & ~next_same
+        src = torch.cat([prev_node[valid], vnode[last]])
+        dst = torch.cat([vnode[valid], depot[last]])
+        return src, dst, status
+
+    def step(self):
+        """One whole step; returns (legs, per-leg cost [s], per-leg A* status, per-request K6 status)."""
+        src, dst, status = self.legs()
+        c, _, st, _ = self.astar.run(src.cpu().numpy(), dst.cpu().numpy())
+        return int(src.numel()), c, st, status

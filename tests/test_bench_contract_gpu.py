@@ -16,7 +16,7 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
 @pytest.mark.parametrize("io", ["hybrid", "zerocopy"])
 def test_bench_json_line(io):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--batch", "262144", "--io", io, "--p50", "0"],
+                        "--batch", "262144", "--io", io, "--p50", "0", "--route-steps", "0"],
                        capture_output=True, text=True, timeout=110, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -46,6 +46,24 @@ def test_bench_spawns_ranks_itself_shared_gpu():
     assert d["config"]["global_batch"] == 2 * 262144
     # two ranks time-sharing one GPU through gloo barriers: a sanity floor, not a rate claim
     assert d["preds_per_s_rec16"] > 1e7
+    # the DP-training probe on the native one-shot all-reduce: every rank ends on the same params
+    os_ = d["dp_training_oneshot"]
+    assert os_ and "error" not in os_, os_
+    assert os_["params_identical_across_ranks"] is True and os_["comm_error"] is False
+    assert abs(os_["final_local_mse_normalized"] - d["dp_training"]["final_local_mse_normalized"]) < 1e-3
+
+
+def test_bench_route_optimizer_probe():
+    """Config 5 inside bench.py: K5 + K6 + one batched A* launch per step, every leg found."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--batch", "262144", "--p50", "0", "--rec16-steps", "0", "--train-steps", "0",
+                        "--gcn-steps", "0", "--route-requests", "2000", "--route-steps", "2"],
+                       capture_output=True, text=True, timeout=115, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    ro = d["route_optimizer"]
+    assert ro["requests_per_step"] == 2000 and ro["steps"] == 2
+    assert ro["astar_unfound_legs"] == 0 and ro["requests_per_s"] > 1e3
 
 
 def test_bench_fails_loud_on_too_many_gpus():
