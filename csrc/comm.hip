@@ -10,7 +10,8 @@
 //                peer's signal array (remote store over xGMI), waits for all W flags, then reads
 //                the W buffers directly over the point-to-point xGMI links (all 7 links busy at
 //                once, not the 2 a ring uses) and sums them in fixed rank order — so every rank
-//                gets a bit-identical result.  Three small kernels, no host round trip.
+//                gets a bit-identical result.  Two small kernels (stage+signal, wait+reduce), no
+//                host round trip.
 //
 // The same stage/signal/wait protocol also gives a one-shot ALL-GATHER (every rank stages its own
 // shard, then copies all W shards straight out of the peers' buffers into its output, rank order)
@@ -52,6 +53,7 @@ struct CommState {
   char* buf = nullptr;                  // [2][cap], uncached, IPC-exported
   Signals* sig = nullptr;               // uncached, IPC-exported
   unsigned* epoch = nullptr;            // local device counter
+  unsigned* arrive = nullptr;           // stage_signal_kernel's block tickets (reset by the last)
   int* err = nullptr;                   // local device error word
   char* peer_buf[MAXW] = {};
   Signals* peer_sig[MAXW] = {};
@@ -68,28 +70,40 @@ CommState* get(int64_t h) {
 }
 
 // ---------------------------------------------------------------------------- kernels
-__global__ void stage_kernel(const float4* __restrict__ src, float4* base0, float4* base1, size_t n4,
-                             const unsigned* epoch) {
-  float4* dst = ((*epoch + 1u) & 1u) ? base1 : base0;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
-    dst[i] = src[i];
-}
-
 struct SignalArgs {
   Signals* peer_sig[MAXW];
   unsigned* epoch;
   int rank, world;
 };
 
-__global__ void signal_kernel(SignalArgs a) {
-  const int r = threadIdx.x;
+// Stage + signal in ONE launch (one dependent kernel boundary fewer per collective): every block
+// copies its share of the bucket into the parity buffer, fences at system scope and takes a ticket;
+// the block that takes the last ticket raises this rank's flag in every peer's signal array and
+// advances the epoch.  ``src == nullptr`` skips the copy (broadcast from a non-root rank).
+__global__ __launch_bounds__(256) void stage_signal_kernel(const float4* __restrict__ src, float4* base0,
+                                                           float4* base1, size_t n4, SignalArgs a,
+                                                           unsigned* arrive) {
   const unsigned e = *a.epoch + 1u;
-  if (r < a.world) {
-    // release at system scope: the staged bucket is visible to peers before the flag
-    __hip_atomic_store(&a.peer_sig[r]->flags[a.rank], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (src) {
+    float4* dst = (e & 1u) ? base1 : base0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
+      dst[i] = src[i];
   }
+  __atomic_thread_fence(__ATOMIC_RELEASE);   // (system scope) this thread's staged stores
   __syncthreads();
-  if (r == 0) *a.epoch = e;
+  __shared__ unsigned ticket;
+  if (threadIdx.x == 0)
+    ticket = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (ticket != gridDim.x - 1) return;
+  const int r = threadIdx.x;
+  if (r < a.world)
+    __hip_atomic_store(&a.peer_sig[r]->flags[a.rank], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+  if (r == 0) {
+    __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *a.epoch = e;
+  }
 }
 
 struct ReduceArgs {
@@ -207,6 +221,7 @@ int64_t comm_create(const char* uid, int rank, int world, int device, size_t one
       return -1;
     }
     c->err = (int*)(c->epoch + 4);
+    c->arrive = c->epoch + 8;
     (void)hipMemset(c->sig, 0, sizeof(Signals));
     (void)hipMemset(c->epoch, 0, 64);
     (void)hipDeviceSynchronize();
@@ -272,14 +287,13 @@ hipError_t comm_all_reduce_f32(int64_t h, float* data, size_t n, int algo, hipSt
       p0[r] = (const float4*)c->peer_buf[r];
       p1[r] = (const float4*)(c->peer_buf[r] + c->cap);
     }
-    hipLaunchKernelGGL(stage_kernel, dim3(grid_for(n4, 512)), dim3(256), 0, stream, (const float4*)data,
-                       (float4*)c->buf, (float4*)(c->buf + c->cap), n4, (const unsigned*)c->epoch);
     SignalArgs sa{};
     for (int r = 0; r < c->world; ++r) sa.peer_sig[r] = c->peer_sig[r];
     sa.epoch = c->epoch;
     sa.rank = c->rank;
     sa.world = c->world;
-    hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, stream, sa);
+    hipLaunchKernelGGL(stage_signal_kernel, dim3(grid_for(n4, 512)), dim3(256), 0, stream,
+                       (const float4*)data, (float4*)c->buf, (float4*)(c->buf + c->cap), n4, sa, c->arrive);
     ReduceArgs ra{};
     for (int r = 0; r < c->world; ++r) {
       ra.peer0[r] = p0[r];
@@ -307,15 +321,14 @@ namespace {
 hipError_t oneshot_gather(CommState* c, const void* in, void* out, size_t bytes, int first, int count,
                           bool stage, hipStream_t stream) {
   const size_t n16 = bytes / 16;
-  if (stage)
-    hipLaunchKernelGGL(stage_kernel, dim3(grid_for(n16, 512)), dim3(256), 0, stream, (const float4*)in,
-                       (float4*)c->buf, (float4*)(c->buf + c->cap), n16, (const unsigned*)c->epoch);
   SignalArgs sa{};
   for (int r = 0; r < c->world; ++r) sa.peer_sig[r] = c->peer_sig[r];
   sa.epoch = c->epoch;
   sa.rank = c->rank;
   sa.world = c->world;
-  hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, stream, sa);
+  hipLaunchKernelGGL(stage_signal_kernel, dim3(stage ? grid_for(n16, 512) : 1), dim3(256), 0, stream,
+                     stage ? (const float4*)in : nullptr, (float4*)c->buf, (float4*)(c->buf + c->cap), n16,
+                     sa, c->arrive);
   GatherArgs ga{};
   for (int r = 0; r < c->world; ++r) {
     ga.peer0[r] = (const int4*)c->peer_buf[r];
