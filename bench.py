@@ -65,6 +65,9 @@ def parse_args():
                     help="also time this many data-parallel training steps of the same MLP on the "
                          "same ranks (64k rows per GPU, one flat-bucket RCCL all-reduce per step; "
                          "extra JSON key 'dp_training')")
+    ap.add_argument("--train-batch-large", type=int, default=1 << 20,
+                    help="also time the DP training probe at this many rows per GPU (extra JSON key "
+                         "'dp_training_large_batch'; 0 skips)")
     ap.add_argument("--route-requests", type=int, default=10_000,
                     help="config 5: concurrent multi-stop requests per step over all ranks")
     ap.add_argument("--route-steps", type=int, default=3,
@@ -287,9 +290,8 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item()) == 0.0
 
-    def train_probe(comm=None):
+    def train_probe(comm=None, tB: int = 65536):
         from routest_amd.train.fused import FusedMlp3Trainer
-        tB = 65536
         torch.manual_seed(4321)                 # identical initial parameters on every rank
         tmodel = EtaMLP(a.hidden)
         tmodel.fit_normalization(records_to_features(norm_rec), norm_y)
@@ -338,6 +340,10 @@ def main() -> None:
         return res
 
     train_res = train_probe() if a.train_steps > 0 else None
+    # the same step at 1M rows per GPU (16 MB of records — HBM is never the limit): the fixed
+    # per-step costs (slab reduction, AdamW, launch gaps, the all-reduce) amortised over 16x the rows
+    train_big_res = (train_probe(tB=a.train_batch_large)
+                     if a.train_steps > 0 and a.train_batch_large > 0 else None)
 
     # the same training step with the native one-shot all-reduce (one hop over all 7 xGMI links at
     # once, instead of RCCL's latency-bound ring at this 296 KB bucket).  Set-up failures and peer
@@ -575,6 +581,7 @@ def main() -> None:
             "collectives": coll,
             "dp_training": train_res,
             "dp_training_oneshot": train_os_res,
+            "dp_training_large_batch": train_big_res,
             "gcn": gcn_res,
             "route_optimizer": route_res,
             "check_max_err_vs_emulation": err_emu,
