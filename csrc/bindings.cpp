@@ -537,6 +537,42 @@ void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N
                                 cur_stream(A), mptr, ldm, (int)nout, mask_hperm, (int)nsplit));
 }
 
+// dW2|db2 (segment 0, nsplit0 n-blocks per k-slice) and dW1 (segment 1, N <= 32) in ONE launch:
+// each segment's fp32 partials go to row s of its own slab (whole rows, offset 0)
+void wgrad_dual(torch::Tensor A0, int64_t M0, torch::Tensor B0, int64_t N0, torch::Tensor slab0, int64_t ldo0,
+                int64_t nsplit0, torch::Tensor A1, int64_t M1, torch::Tensor B1, int64_t N1, torch::Tensor slab1,
+                int64_t ldo1) {
+  auto chk = [](const torch::Tensor& A, int64_t M, const torch::Tensor& Bm, int64_t N, const torch::Tensor& slab,
+                int64_t ldo) {
+    check_dev(A, "A");
+    check_dev(Bm, "Bm");
+    check_dev(slab, "slab");
+    TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && Bm.scalar_type() == torch::kBFloat16, "bf16 A/Bm");
+    TORCH_CHECK(A.dim() == 2 && Bm.dim() == 2 && A.size(0) == Bm.size(0) && A.is_contiguous() &&
+                    Bm.is_contiguous(), "A/Bm must be contiguous [K, *]");
+    TORCH_CHECK(M <= A.size(1) && N <= Bm.size(1) && M % 8 == 0 && N % 8 == 0 && A.size(1) % 8 == 0 &&
+                    Bm.size(1) % 8 == 0, "M/N: multiples of 8 within the operand widths");
+    TORCH_CHECK(slab.scalar_type() == torch::kFloat32 && slab.dim() == 2 && slab.is_contiguous() &&
+                    (M - 1) * ldo + N <= slab.size(1), "slab must be f32 [S, >= (M-1)*ldo+N]");
+  };
+  chk(A0, M0, B0, N0, slab0, ldo0);
+  chk(A1, M1, B1, N1, slab1, ldo1);
+  TORCH_CHECK(A0.size(0) == A1.size(0), "both segments reduce over the same batch");
+  TORCH_CHECK(N1 <= 32, "segment 1 takes N <= 32");
+  TORCH_CHECK(A0.device() == A1.device() && slab0.device() == A0.device() && slab1.device() == A0.device(),
+              "one device");
+  const int nsp = (int)std::max<int64_t>(nsplit0, 1);
+  const int NT0 = (int)((N0 + 31) / 32 + nsp - 1) / nsp;
+  TORCH_CHECK(NT0 >= 1 && NT0 <= 9, "at most 288 columns per n-block");
+  const c10::DeviceGuard guard(A0.device());
+  RT_CHECK_HIP(rt::launch_wgrad_dual(A0.data_ptr(), (int)A0.size(1), (int)M0, (int)M0, B0.data_ptr(),
+                                     (int)B0.size(1), (int)N0, (int)A0.size(0), (int)slab0.size(0),
+                                     slab0.data_ptr<float>(), (int)ldo0, (long long)slab0.size(1), (int)N0, nsp,
+                                     A1.data_ptr(), (int)A1.size(1), (int)M1, (int)M1, B1.data_ptr(),
+                                     (int)B1.size(1), (int)N1, (int)slab1.size(0), slab1.data_ptr<float>(),
+                                     (int)ldo1, (long long)slab1.size(1), (int)N1, cur_stream(A0)));
+}
+
 void wgrad_reduce(torch::Tensor slab, torch::Tensor G, c10::optional<torch::Tensor> slab1,
                   c10::optional<torch::Tensor> G1, c10::optional<torch::Tensor> slab2,
                   c10::optional<torch::Tensor> G2) {
@@ -967,6 +1003,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A"), py::arg("M"), py::arg("Mout"), py::arg("Bm"), py::arg("N"), py::arg("slab"),
         py::arg("offset"), py::arg("ldo"), py::arg("mask") = py::none(), py::arg("nout") = -1, py::arg("mask_hperm") = false,
         py::arg("nsplit") = 1);
+  m.def("wgrad_dual", &wgrad_dual, "two split-K weight-gradient GEMMs (dW2|db2 and dW1) in one launch");
   m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs (optionally a second and third region)",
         py::arg("slab"), py::arg("G"), py::arg("slab1") = py::none(), py::arg("G1") = py::none(),
         py::arg("slab2") = py::none(), py::arg("G2") = py::none());

@@ -73,6 +73,12 @@ hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, 
                                const float* slab2 = nullptr, int S2 = 0, long long slab_stride2 = 0,
                                float* G2 = nullptr, int n2 = 0);
 size_t wgrad_lds_bytes(int NT);
+// two independent wgrad GEMMs (segment 1: N <= 32) in one launch, same K
+hipError_t launch_wgrad_dual(const void* A0, int lda0, int M0, int Mout0, const void* B0, int ldb0,
+                             int N0, int K, int S0, float* slab0, int ldo0, long long stride0, int Nout0,
+                             int nsplit0, const void* A1, int lda1, int M1, int Mout1, const void* B1,
+                             int ldb1, int N1, int S1, float* slab1, int ldo1, long long stride1,
+                             int Nout1, hipStream_t stream);
 
 // ---- GCN route scorer (K8) : gcn.hip ----
 hipError_t launch_gcn_agg_gemm(const void* X, const int* indptr, const int* indices,

@@ -21,6 +21,7 @@
 //  * the fp32 partial of slice s is written to slab[s] in the caller's layout (the flat gradient
 //    bucket); wgrad_reduce_kernel sums the S slabs in a fixed order — deterministic, no atomics.
 #include <cstdlib>
+#include <utility>
 
 #include "common.h"
 #include "ops.h"
@@ -67,14 +68,15 @@ __device__ __forceinline__ int relu_mask_word(int a, int m) {
 // MPERM: the mask's columns are in the trainer's hperm() unit order (h1a) while A's are natural
 // (dh1): the 8 mask values of A columns m..m+7 (m % 8 == 0) are the two 8-byte runs at
 // p0 = (m & ~15) + 4 * ((m >> 3) & 1) and p0 + 8.
-template <int NT, bool MASK, int KB, bool MPERM = false>
-__global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict__ A, int lda, int M,
-                                                       int Mout, const __bf16* __restrict__ Bm,
-                                                       int ldb, int N, int K, int kslice,
-                                                       float* __restrict__ slab, int ldo,
-                                                       long long slab_stride,
-                                                       const __bf16* __restrict__ mask, int ldm,
-                                                       int Nout) {
+// The body of one workgroup (k-slice bx, m-block by, n-block bz); the kernels below map their
+// block ids onto it.
+template <int NT, bool MASK, int KB, bool MPERM>
+__device__ __forceinline__ void wgrad_body(const int bx, const int by, const int bz,
+                                           const __bf16* __restrict__ A, int lda, int M, int Mout,
+                                           const __bf16* __restrict__ Bm, int ldb, int N, int K,
+                                           int kslice, float* __restrict__ slab, int ldo,
+                                           long long slab_stride, const __bf16* __restrict__ mask,
+                                           int ldm, int Nout) {
   constexpr int AW = 256, BW = 32 * NT;
   constexpr int ACH = AW / 8, BCH = BW / 8;           // 16-B chunks per staged row
   constexpr int TPB = 512;
@@ -86,14 +88,14 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
   __bf16* sB = sA + KB * sa;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int m_base = blockIdx.y * AW;
+  const int m_base = by * AW;
   // n-block z: columns [n0, n0 + 32*NT) of Bm / the output (several workgroups per k-slice, so a
   // slice can cover more batch rows for the same grid: fewer fp32 slabs to write and reduce)
-  const int n0 = blockIdx.z * BW;
+  const int n0 = bz * BW;
   Bm += n0;
   N -= n0;
   Nout -= n0;
-  const int k_begin = blockIdx.x * kslice;
+  const int k_begin = bx * kslice;
   const int k_end = min(K, k_begin + kslice);
 
   f32x16 acc[NT];
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
     }
   }
   // partial of this k-slice -> slab[blockIdx.x]
-  float* out = slab + (long long)blockIdx.x * slab_stride + n0;
+  float* out = slab + (long long)bx * slab_stride + n0;
   const int h = lane >> 5, col = lane & 31;
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
@@ -189,6 +191,48 @@ __global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict_
       const int m = m_base + 32 * w + (e & 3) + 8 * (e >> 2) + 4 * h;
       if (m < Mout && nn < Nout) out[(size_t)m * ldo + nn] = acc[n][e];
     }
+  }
+}
+
+template <int NT, bool MASK, int KB, bool MPERM = false>
+__global__ __launch_bounds__(512, 2) void wgrad_kernel(const __bf16* __restrict__ A, int lda, int M,
+                                                       int Mout, const __bf16* __restrict__ Bm,
+                                                       int ldb, int N, int K, int kslice,
+                                                       float* __restrict__ slab, int ldo,
+                                                       long long slab_stride,
+                                                       const __bf16* __restrict__ mask, int ldm,
+                                                       int Nout) {
+  wgrad_body<NT, MASK, KB, MPERM>(blockIdx.x, blockIdx.y, blockIdx.z, A, lda, M, Mout, Bm, ldb, N, K,
+                                  kslice, slab, ldo, slab_stride, mask, ldm, Nout);
+}
+
+// Two independent weight-gradient GEMMs in ONE launch (the small trainer's dW2|db2 with NT0 n-tiles
+// per workgroup, and dW1 with one): blocks [0, nb0) run segment 0 in the 3-D order of a plain launch
+// (k-slice fastest, so a slice's n-blocks still land on one XCD), the rest segment 1.  The two
+// grids (~240 + 256 workgroups) fit the 512 workgroup slots of the chip together, so dW1 streams
+// its operands while dW2 runs instead of after it, and one dependent launch boundary goes away.
+struct WgSeg {
+  const __bf16* A;
+  const __bf16* Bm;
+  float* slab;
+  long long slab_stride;
+  int lda, M, Mout, ldb, N, K, kslice, ldo, Nout, S, mblocks;
+};
+
+template <int NT0, int KB>
+__global__ __launch_bounds__(512, 2) void wgrad_dual_kernel(WgSeg s0, WgSeg s1, int nb0) {
+  int b = (int)blockIdx.x;
+  if (b < nb0) {
+    const int x = b % s0.S, r = b / s0.S;
+    wgrad_body<NT0, false, KB, false>(x, r % s0.mblocks, r / s0.mblocks, s0.A, s0.lda, s0.M, s0.Mout,
+                                      s0.Bm, s0.ldb, s0.N, s0.K, s0.kslice, s0.slab, s0.ldo,
+                                      s0.slab_stride, nullptr, 0, s0.Nout);
+  } else {
+    b -= nb0;
+    const int x = b % s1.S, r = b / s1.S;
+    wgrad_body<1, false, KB, false>(x, r % s1.mblocks, r / s1.mblocks, s1.A, s1.lda, s1.M, s1.Mout,
+                                    s1.Bm, s1.ldb, s1.N, s1.K, s1.kslice, s1.slab, s1.ldo,
+                                    s1.slab_stride, nullptr, 0, s1.Nout);
   }
 }
 
@@ -344,6 +388,54 @@ hipError_t launch_wgrad(const void* A, int lda, int M, int Mout, const void* Bm,
     case 7: return launch_wgrad_nt<7>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
     case 8: return launch_wgrad_nt<8>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
     case 9: return launch_wgrad_nt<9>(A, lda, M, Mout, Bm, ldb, N, K, S, slab, ldo, slab_stride, stream, nullptr, 0, Nout);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int NT0, int KB>
+static hipError_t launch_dual_kb(const WgSeg& s0, const WgSeg& s1, int nb0, int nb1, hipStream_t stream) {
+  const size_t lds = wgrad_lds_bytes(NT0, KB);     // >= the NT = 1 segment's
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)wgrad_dual_kernel<NT0, KB>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((wgrad_dual_kernel<NT0, KB>), dim3(nb0 + nb1), dim3(512), lds, stream, s0, s1, nb0);
+  return hipGetLastError();
+}
+
+hipError_t launch_wgrad_dual(const void* A0, int lda0, int M0, int Mout0, const void* B0, int ldb0,
+                             int N0, int K, int S0, float* slab0, int ldo0, long long stride0, int Nout0,
+                             int nsplit0, const void* A1, int lda1, int M1, int Mout1, const void* B1,
+                             int ldb1, int N1, int S1, float* slab1, int ldo1, long long stride1,
+                             int Nout1, hipStream_t stream) {
+  if (M0 % 8 || N0 % 8 || lda0 % 8 || ldb0 % 8 || M1 % 8 || N1 % 8 || lda1 % 8 || ldb1 % 8 || N1 > 32 ||
+      S0 < 1 || S1 < 1)
+    return hipErrorInvalidValue;
+  if (nsplit0 < 1) nsplit0 = 1;
+  const int NT0 = ((N0 + 31) / 32 + nsplit0 - 1) / nsplit0;
+  auto seg = [&](const void* A, int lda, int M, int Mout, const void* Bm, int ldb, int N, int S, float* slab,
+                 int ldo, long long stride, int Nout, int NT) {
+    WgSeg g{};
+    g.A = (const __bf16*)A;
+    g.Bm = (const __bf16*)Bm;
+    g.slab = slab;
+    g.slab_stride = stride;
+    g.lda = lda; g.M = M; g.Mout = Mout; g.ldb = ldb; g.N = N; g.K = K; g.ldo = ldo;
+    g.Nout = (Nout < 0 || Nout > N) ? N : Nout;
+    g.kslice = ((K + S - 1) / S + 31) / 32 * 32;
+    g.S = S;
+    g.mblocks = (M + 255) / 256;
+    return std::make_pair(g, S * g.mblocks * ((N + 32 * NT - 1) / (32 * NT)));
+  };
+  const auto p0 = seg(A0, lda0, M0, Mout0, B0, ldb0, N0, S0, slab0, ldo0, stride0, Nout0, NT0);
+  const auto p1 = seg(A1, lda1, M1, Mout1, B1, ldb1, N1, S1, slab1, ldo1, stride1, Nout1, 1);
+  const bool kb64 = wgrad_kb() != 32;
+  switch (NT0) {
+#define RT_DUAL(nt) case nt: return kb64 ? launch_dual_kb<nt, 64>(p0.first, p1.first, p0.second, p1.second, stream) \
+                                         : launch_dual_kb<nt, 32>(p0.first, p1.first, p0.second, p1.second, stream);
+    RT_DUAL(1) RT_DUAL(2) RT_DUAL(3) RT_DUAL(4) RT_DUAL(5) RT_DUAL(6) RT_DUAL(7) RT_DUAL(8) RT_DUAL(9)
+#undef RT_DUAL
     default: return hipErrorInvalidValue;
   }
 }

@@ -114,6 +114,10 @@ class GpuRunner:
             for s in range(0, n, self.batch_max):
                 m = min(self.batch_max, n - s)
                 self.h_rec_np[:m] = rec[s:s + m]
+                # the device lock is held until this launch has COMPLETED: released right after
+                # the enqueue, another runner on the device could relaunch the resident scorer
+                # while this kernel still waits for the CU / hardware queue the scorer takes —
+                # and a scorer kept busy by a steady stream of small batches can hold it for good
                 with self.dev_lock:
                     res = _DEV_RESIDENT.get(self._dev_key)
                     if res is not None:
@@ -124,7 +128,7 @@ class GpuRunner:
                         self.d_rec[:m].copy_(self.h_rec[:m], non_blocking=True)
                         y = self.kernel(self.d_rec[:m])
                         self.h_out[:m].copy_(y, non_blocking=True)
-                self.stream.synchronize()
+                    self.stream.synchronize()
                 out[s:s + m] = self.h_out_np[:m]
         return out
 

@@ -174,6 +174,7 @@ class FusedMlp3Trainer:
         # dW3|db3 and dW1 (small outputs, operands as big as dW2's) keep one slice per CU.
         ldg = H + 16
         self.nsplit = int(os.environ.get("ROUTEST_WGRAD_NSPLIT", "3"))
+        self.dual = os.environ.get("ROUTEST_WGRAD_DUAL", "1") != "0"
         self.S = self._slices(B)
         ntt = (ldg + 31) // 32
         nt = -(-ntt // max(1, self.nsplit))
@@ -206,9 +207,14 @@ class FusedMlp3Trainer:
                              self.xf, self.h1a, self.w3slab, self.dz2, self.dz1, self.dyb,
                              self.sq_err, self.step_ctr)
         ldg = H + 16
-        C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit)
-        # dW1 = dz1^T x (relu'(z1) applied by the forward kernel)
-        C.wgrad(self.dz1, H, H, self.xf, 16, self.slab, 0, 16)
+        if self.dual:
+            # dW2|db2 and dW1 = dz1^T x in ONE launch: the two grids share the chip
+            C.wgrad_dual(self.dz2, H, self.h1a, ldg, self.slab2, ldg, self.nsplit,
+                         self.dz1, H, self.xf, 16, self.slab, 16)
+        else:
+            C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit)
+            # dW1 = dz1^T x (relu'(z1) applied by the forward kernel)
+            C.wgrad(self.dz1, H, H, self.xf, 16, self.slab, 0, 16)
         C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg + ldg:],
                        self.w3slab, self.G[H * ldg:H * ldg + ldg])
 
