@@ -58,6 +58,17 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 300.0) ->
         kw = {"backend": be, "timeout": dt.timedelta(seconds=timeout_s)}
         if be == "nccl":
             kw["device_id"] = device
+        restart = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0)
+        if restart > 0 and "MASTER_PORT" in os.environ:
+            # a `torchrun --max-restarts` relaunch with a static rendezvous re-uses the agent's store:
+            # the previous attempt's connection keys are still in it (a rank can read a dead peer's
+            # address and fail connectFullMesh), so every attempt gets its own key prefix
+            agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+            base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                                 is_master=(not agent and rank == 0),
+                                 timeout=dt.timedelta(seconds=timeout_s), multi_tenant=not agent)
+            kw.update(store=dist.PrefixStore(f"routest/attempt_{restart}", base), rank=rank,
+                      world_size=world)
         dist.init_process_group(**kw)
     return DistInfo(dist.get_rank(), dist.get_world_size(), local, be, device)
 

@@ -27,6 +27,7 @@ from ..models.features import features_to_records, records_to_features
 from ..models.mlp3 import EtaMLP, LinearETA
 from ..ops.eta_mlp import featurize_torch, records_to_tensor
 from ..parallel.dp import DistInfo, FlatGrads, allreduce_scalars, barrier, broadcast_flat, init_distributed
+from ..utils.faults import fault_step
 from ..utils.logging import get_logger
 from .fused import FusedMlp3Trainer, flatten_params, lr_at, unflatten_into
 
@@ -54,6 +55,7 @@ class TrainConfig:
     eval_rows: int = 65536
     dist_backend: str = ""         # "" = nccl on GPU, gloo on CPU
     comm: str = "torch"            # gradient all-reduce: torch (ProcessGroup) | rccl | oneshot (native, fused backend)
+    max_steps: int = 0             # > 0: train until this ABSOLUTE step (elastic relaunches resume and stop here)
 
 
 def train_linear(cfg: TrainConfig) -> LinearETA:
@@ -241,10 +243,15 @@ class Trainer:
         logf = open(cfg.log_path, "a") if (cfg.log_path and self.di.is_main) else None
         t0 = time.perf_counter()
         last_t, last_s = t0, self.start_step
-        end = self.start_step + cfg.steps
+        end = cfg.max_steps if cfg.max_steps > 0 else self.start_step + cfg.steps
+        crash_at = fault_step("rank_crash")
+        first_attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") == "0"
         for step in range(self.start_step, end):
             lt = self.train_step(step)
             s1 = step + 1
+            if crash_at == s1 and first_attempt and self.di.rank == self.di.world - 1:
+                log.error("injected fault: rank %d exits hard at step %d", self.di.rank, s1)
+                os._exit(13)
             if (cfg.log_every and s1 % cfg.log_every == 0) or s1 == end:
                 loss_sum = float(lt.sum().item())
                 tot = allreduce_scalars([loss_sum], dev)[0] / self.global_batch
@@ -265,8 +272,8 @@ class Trainer:
         wall = time.perf_counter() - t0
         self.save(end)
         ev = self.evaluate()
-        out = {"steps": cfg.steps, "wall_s": wall, "global_batch": self.global_batch,
-               "samples_per_s": cfg.steps * self.global_batch / wall, "world": self.di.world,
+        out = {"steps": end - self.start_step, "start_step": self.start_step, "end_step": end, "wall_s": wall, "global_batch": self.global_batch,
+               "samples_per_s": (end - self.start_step) * self.global_batch / wall, "world": self.di.world,
                "backend": self.backend, **ev, "history": self.history[-3:]}
         if logf:
             logf.write(json.dumps({k: v for k, v in out.items() if k != "history"}) + "\n")

@@ -1,6 +1,8 @@
 """Fault-injection hooks.  ``ROUTEST_FAULT`` is a comma list of
-``provider_timeout``, ``gpu_fail``, ``rccl_timeout``, ``store_fail``; tests flip them with
-:func:`set_faults` instead of the env var."""
+``provider_timeout``, ``gpu_fail``, ``rccl_timeout``, ``store_fail`` and ``rank_crash@<step>`` (the
+last rank of a training job dies hard at that step on the job's FIRST attempt, so a
+``torchrun --max-restarts`` relaunch resumes from the last checkpoint and finishes); tests flip them
+with :func:`set_faults` instead of the env var."""
 from __future__ import annotations
 
 import os
@@ -38,3 +40,14 @@ def clear_faults() -> None:
 def maybe_fail(name: str) -> None:
     if name in active_faults():
         raise InjectedFault(f"injected fault: {name}")
+
+
+def fault_step(name: str) -> Optional[int]:
+    """``name@N`` in the active faults -> N (else None)."""
+    for f in active_faults():
+        if f.startswith(name + "@"):
+            try:
+                return int(f.split("@", 1)[1])
+            except ValueError:
+                return None
+    return None
