@@ -128,7 +128,7 @@ class Trainer:
     # ---------------------------------------------------------------- backends
     def _setup_backend(self) -> None:
         cfg = self.cfg
-        total = self.start_step + cfg.steps
+        total = cfg.max_steps if cfg.max_steps > 0 else self.start_step + cfg.steps
         if self.backend == "fused":
             self.fused = FusedMlp3Trainer(self.model, self.di.device, cfg.batch_local, self.global_batch,
                                           lr=cfg.lr, weight_decay=cfg.weight_decay, warmup=cfg.warmup,

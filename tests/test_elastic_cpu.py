@@ -9,6 +9,8 @@ import subprocess
 import sys
 import tempfile
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -20,16 +22,17 @@ def _port() -> int:
     return p
 
 
-def test_torchrun_max_restarts_resumes_after_rank_crash():
+def _run(backend: str, extra_env=None):
     with tempfile.TemporaryDirectory() as d:
         ck = os.path.join(d, "ckpt")
-        env = dict(os.environ, ROUTEST_FAULT="rank_crash@25", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+        env = dict(os.environ, ROUTEST_FAULT="rank_crash@25", PYTHONPATH=ROOT, OMP_NUM_THREADS="2",
+                   **(extra_env or {}))
         env.pop("WORLD_SIZE", None)
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
                "--max-restarts", "1", "--master-addr", "127.0.0.1", "--master-port", str(_port()),
                "-m", "routest_amd.train", "--hidden", "64", "--batch-local", "512", "--steps", "40",
                "--max-steps", "40", "--rows-per-rank", "4096", "--eval-rows", "1024", "--log-every", "10",
-               "--ckpt-dir", ck, "--ckpt-every", "10", "--backend", "autograd", "--dist-backend", "gloo",
+               "--ckpt-dir", ck, "--ckpt-every", "10", "--backend", backend, "--dist-backend", "gloo",
                "--warmup", "5"]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=d, env=env)
         assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-8000:])
@@ -39,3 +42,14 @@ def test_torchrun_max_restarts_resumes_after_rank_crash():
         assert res["start_step"] == 20 and res["end_step"] == 40 and res["world"] == 2
         with open(os.path.join(ck, "trainer_state.json")) as f:
             assert json.load(f)["step"] == 40
+
+
+def test_torchrun_max_restarts_resumes_after_rank_crash():
+    _run("autograd")
+
+
+@pytest.mark.gpu
+def test_torchrun_max_restarts_fused_hip_trainer_shared_gpu():
+    """The same on the fused HIP trainer: both ranks on GPU 0 (gloo), the relaunch restores the
+    flat fp32 params and the AdamW moments into the kernels' buffers and finishes."""
+    _run("fused", {"ROUTEST_BENCH_SHARE_GPU": "1"})
