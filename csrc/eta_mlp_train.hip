@@ -83,21 +83,6 @@ __device__ __forceinline__ bf16x8 join4(const s16x4 lo, const s16x4 hi) {
 // 8 waves per workgroup, 2 per SIMD (<= 256 VGPRs each).
 constexpr int TRAIN_TPB = 512;
 
-// One halving step of a reduce-scatter over the 32 lanes of each half-wave: pairs (k, k + N/2)
-// of v[0 .. N); a lane keeps the member whose index bit matches its lane bit X and adds the
-// partner lane's copy of it (ds_swizzle bit mode: xor X within 32 lanes).  Leaves v[0 .. N/2).
-template <int X, int N, int NV>
-__device__ __forceinline__ void rs32_step(float (&v)[NV], int lane) {
-  const bool up = (lane & X) != 0;
-#pragma unroll
-  for (int k = 0; k < N / 2; ++k) {
-    const float a = v[k], b = v[k + N / 2];
-    const float send = up ? a : b;
-    const float keep = up ? b : a;
-    v[k] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), (X << 10) | 0x1f));
-  }
-}
-
 template <int H>
 __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     const int4* __restrict__ rec, const float* __restrict__ target, int B,
@@ -125,6 +110,8 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
   // this wave's dW3 | db3 partial accumulates in LDS past the blob (nothing carried in registers
   // across tiles): [wpb][LDA] f32, one row per wave until the final barrier
   float* const w3part = reinterpret_cast<float*>(smem + L::BLOB) + (threadIdx.x >> 6) * LDA;
+  // per-wave 32-float scratch past the partials: the tile's dy values, broadcast to the lanes
+  float* const dyscr = reinterpret_cast<float*>(smem + L::BLOB) + wpb * LDA + (threadIdx.x >> 6) * 32;
   for (int c = lane; c < LDA; c += 64) w3part[c] = 0.f;
 
   for (int tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntiles; tile += stride) {
@@ -227,47 +214,80 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
         }
         return acc;
       };
-      // pass 1: y
+      // pass 1: y and the relu'(z2) bits (accumulator layout: units in registers, rows on lanes)
 #pragma unroll 1
       for (int mt = 0; mt < MT; ++mt) {
         const f32x16 acc = layer2(mt);
         const f32x16 w3 = load_vec16(w3p, mt, h);
+        unsigned mk = 0;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) ys = __builtin_fmaf(relu_f(acc[e]), w3[e], ys);
+        for (int e = 0; e < 16; ++e) {
+          ys = __builtin_fmaf(relu_f(acc[e]), w3[e], ys);
+          mk |= (acc[e] > 0.f ? 1u : 0u) << e;
+        }
+        if (mt < 4) mask_lo |= (unsigned long long)mk << (16 * mt);
+        else mask_hi |= (unsigned long long)mk << (16 * (mt - 4));
       }
       ys += __shfl_xor(ys, 32);
       const float y = ys + b3;
       diff = valid ? (y - target[row]) : 0.f;
       dy = gscale * diff;
-      // pass 2: relu'(z2) bits and the dW3 partial sum_r bf16(dy_r) bf16(relu(z2[r, c])) (the
-      // operands the split-K GEMM over h2a used).  The 32 rows of a lane half sit on 32 lanes:
-      // the row sum of a hidden tile's 16 values per lane is a reduce-scatter over lane bits
-      // 4..1 (ds_swizzle xor, no LDS traffic) plus a final xor-1 add; lane (r, h) then holds the
-      // tile-sum of value i = r >> 1, stored column 16 (2mt + (i >> 3)) + 8h + (i & 7).
-      // Rows past B carry dy = 0.
+      // pass 2: the dW3 partial sum_r bf16(dy_r) bf16(relu(z2[r, c])) (the operands the split-K
+      // GEMM over h2a used) on the TRANSPOSED tile: the same two operands with their MFMA roles
+      // swapped (h1 as A, the W2 row fragment as B) give z2^T — hidden unit 32mt + r on the lanes,
+      // the tile's rows 8(e>>2) + 4h + (e&3) in the registers — so the row sum is 16 in-lane FMAs
+      // and ONE cross-half add per hidden tile instead of a 5-step lane reduce-scatter.  The rows'
+      // dy reach the lanes through a 128-byte LDS broadcast; rows past B carry dy = 0.
       const float dyr = (float)(__bf16)dy;
+      float* const dys = dyscr;                      // this wave's 32-float scratch
+      if (h == 0) dys[r] = dyr;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float dyv[16];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const f32x4 t = reinterpret_cast<const f32x4*>(dys)[2 * q4 + h];   // rows 8q4 + 4h .. +3
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dyv[4 * q4 + j] = t[j];
+      }
+      const float* b2f = reinterpret_cast<const float*>(b2p);
+      const int bpos = 2 * ((r >> 2) & 1) * 8 + 4 * (r >> 3) + (r & 3);   // b2 of unit 32mt + r
 #pragma unroll 1
       for (int mt = 0; mt < MT; ++mt) {
-        const f32x16 acc = layer2(mt);
-        unsigned mk = 0;
-        float v[16];
+        f32x16 acc;
+        const float bias = b2f[mt * 32 + bpos];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const float x = relu_f(acc[e]);
-          mk |= (x > 0.f ? 1u : 0u) << e;
-          v[e] = dyr * (float)(__bf16)x;
+        for (int e = 0; e < 16; ++e) acc[e] = bias;
+        const unsigned char* pm = lrow + mt * 16384;
+        auto fragw = [&](int ks) {
+          const int* xo = (ks >> 3) ? xk8[ks & 7] : xk[ks & 7];
+          const s16x4 lo = *reinterpret_cast<const s16x4*>(pm + xo[0]);
+          const s16x4 hi = *reinterpret_cast<const s16x4*>(pm + xo[1]);
+          return join4(lo, hi);
+        };
+        bf16x8 ring[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) ring[d] = fragw(d);
+#pragma unroll
+        for (int ks = 0; ks < KS; ks += D) {
+          bf16x8 a[D];
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            a[d] = ring[d];
+            if (ks + D + d < KS) ring[d] = fragw(ks + D + d);
+          }
+#pragma unroll
+          for (int d = 0; d < D; ++d) acc = mfma32(h1[ks + d], a[d], acc);
         }
-        rs32_step<16, 16>(v, lv);
-        rs32_step<8, 8>(v, lv);
-        rs32_step<4, 4>(v, lv);
-        rs32_step<2, 2>(v, lv);
-        const float t = v[0] + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v[0]), (1 << 10) | 0x1f));
-        if ((lv & 1) == 0) {
-          const int i = r >> 1;
-          w3part[32 * mt + 16 * (i >> 3) + 8 * h + (i & 7)] += t;
+        float t = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) t = __builtin_fmaf(dyv[e], (float)(__bf16)relu_f(acc[e]), t);
+        t += __shfl_xor(t, 32);
+        if (h == 0) {
+          const int u = 32 * mt + r;                 // stored column: hperm(u) = u with bits 2, 3 swapped
+          w3part[(u & ~12) | ((u & 4) << 1) | ((u & 8) >> 1)] += t;
         }
-        if (mt < 4) mask_lo |= (unsigned long long)mk << (16 * mt);
-        else mask_hi |= (unsigned long long)mk << (16 * (mt - 4));
       }
       // db3 = sum of bf16(dy) over the rows (lanes of half 0 hold each row once)
       float d = h == 0 ? dyr : 0.f;
@@ -532,8 +552,8 @@ static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B
                                      int* step_ctr, int num_cus, hipStream_t stream) {
   using L = TrainLayout<H>;
   constexpr int TPB = TRAIN_TPB;
-  // the blob + the waves' dW3 partials [TPB / 64][H + 16] f32
-  constexpr size_t LDS = L::BLOB + (size_t)(TPB / 64) * (H + 16) * 4;
+  // the blob + the waves' dW3 partials [TPB / 64][H + 16] f32 + their dy scratch [TPB / 64][32]
+  constexpr size_t LDS = L::BLOB + (size_t)(TPB / 64) * (H + 16 + 32) * 4;
   static_assert(LDS <= 160 * 1024, "training kernel LDS budget");
   static bool attr_set[64] = {};
   int dev = 0;
