@@ -35,6 +35,7 @@ import numpy as np
 
 from ..utils.logging import get_logger
 from ..utils.metrics import REGISTRY
+from ..utils.queues import get_until
 from .batched import batched_trips
 from .greedy import InfeasibleStops
 from .optimizer import optimize_route
@@ -192,15 +193,9 @@ class RouteBatcher:
         deadline = first[3] + self.timeout_s
         while len(batch) < self.batch_max:
             try:
-                it = self.q.get_nowait()
+                it = get_until(self.q, deadline)         # (not q.get(timeout=...): see utils/queues.py)
             except queue.Empty:
-                rem = deadline - time.perf_counter()
-                if rem <= 0:
-                    break
-                try:
-                    it = self.q.get(timeout=rem)
-                except queue.Empty:
-                    break
+                break
             batch.append(it)
             if it is None:
                 break

@@ -34,6 +34,7 @@ from ..models.features import RECORD_DTYPE
 from ..utils.faults import maybe_fail
 from ..utils.logging import get_logger
 from ..utils.metrics import REGISTRY
+from ..utils.queues import get_until
 
 log = get_logger("batcher")
 
@@ -235,11 +236,8 @@ class MicroBatcher:
                 pass
             if self._last_batch <= 1 and len(batch) == 1:
                 break
-            rem = deadline - time.perf_counter()
-            if rem <= 0:
-                break
             try:
-                it = self.q.get(timeout=rem)
+                it = get_until(self.q, deadline)     # (not q.get(timeout=...): see utils/queues.py)
             except queue.Empty:
                 break
             batch.append(it)

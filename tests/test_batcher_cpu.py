@@ -128,3 +128,49 @@ def test_inline_when_idle_and_queue_under_load():
         assert sum(calls[1:]) == 32
     finally:
         b.close()
+
+
+def test_two_consumers_never_strand_requests():
+    """Two workers on one queue, bursts of concurrent requests: every request is answered.  With
+    CPython's timed SimpleQueue.get a worker whose wake-up item was taken by the other worker
+    re-waited without a timeout and held its partial batch until the next put (utils/queues.py);
+    this lost requests within ~10 bursts."""
+    import concurrent.futures as cf
+    import time
+
+    from routest_amd.data.synth import synth_records
+
+    class Slow:
+        rows = 0
+
+        def __call__(self, rec):
+            time.sleep(0.0002)
+            Slow.rows += len(rec)
+            return np.arange(len(rec), dtype=np.float32)
+
+    rec, _ = synth_records(6000, 1)
+    for _ in range(20):
+        Slow.rows = 0
+        mb = MicroBatcher([Slow(), Slow()], batch_max=512, timeout_us=300, inline_when_idle=False)
+        try:
+            with cf.ThreadPoolExecutor(16) as ex:
+                futs = [ex.submit(mb.predict_sync, rec[i].item(), 5.0) for i in range(len(rec))]
+                for f in futs:
+                    f.result(10)
+        finally:
+            mb.close()
+        assert Slow.rows == len(rec)
+
+
+def test_get_until_deadline():
+    import queue
+    import time
+
+    from routest_amd.utils.queues import get_until
+    q = queue.SimpleQueue()
+    t0 = time.perf_counter()
+    with pytest.raises(queue.Empty):
+        get_until(q, t0 + 0.002)
+    assert time.perf_counter() - t0 < 0.5
+    q.put(7)
+    assert get_until(q, time.perf_counter() + 1.0) == 7
