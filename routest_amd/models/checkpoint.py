@@ -46,20 +46,29 @@ def save_checkpoint(path: str, model: Any, optimizer_state: Optional[Dict[str, t
         sd = {k: v.contiguous() for k, v in model.state_dict().items()}
     if extra_config:
         cfg.update(extra_config)
-    tmp = path + "/.tmp_model.safetensors"
-    save_file(sd, tmp)
-    os.replace(tmp, os.path.join(path, "model.safetensors"))
+    # every file is written under a temporary name first and only then renamed into place, in one
+    # tight sequence ending with trainer_state.json (the resume step) and config.json: a rank killed
+    # while saving (torchrun tears the job down when a peer dies) leaves the previous checkpoint's
+    # files intact instead of a half-written one
+    staged = []
+    tmp = os.path.join(path, ".tmp_opt.safetensors")
     if optimizer_state is not None:
-        tmp = path + "/.tmp_opt.safetensors"
         save_file({k: v.detach().cpu().contiguous() for k, v in optimizer_state.items()}, tmp)
-        os.replace(tmp, os.path.join(path, "optimizer.safetensors"))
+        staged.append((tmp, os.path.join(path, "optimizer.safetensors")))
+    tmp = os.path.join(path, ".tmp_model.safetensors")
+    save_file(sd, tmp)
+    staged.append((tmp, os.path.join(path, "model.safetensors")))
     if trainer_state is not None:
-        with open(os.path.join(path, "trainer_state.json.tmp"), "w") as f:
+        tmp = os.path.join(path, ".tmp_trainer_state.json")
+        with open(tmp, "w") as f:
             json.dump(trainer_state, f)
-        os.replace(os.path.join(path, "trainer_state.json.tmp"), os.path.join(path, "trainer_state.json"))
-    with open(os.path.join(path, "config.json.tmp"), "w") as f:
+        staged.append((tmp, os.path.join(path, "trainer_state.json")))
+    tmp = os.path.join(path, ".tmp_config.json")
+    with open(tmp, "w") as f:
         json.dump(cfg, f, indent=1)
-    os.replace(os.path.join(path, "config.json.tmp"), os.path.join(path, "config.json"))
+    staged.append((tmp, os.path.join(path, "config.json")))
+    for src, dst in staged:
+        os.replace(src, dst)
 
 
 def load_checkpoint(path: str) -> Tuple[Any, Dict[str, Any]]:
