@@ -2,7 +2,7 @@
 ROOT=$GRAFT_REPO_ROOT
 cd $ROOT
 O=$ROOT/gpurun_out/r2av; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_elastic_cpu.py -x -v -m gpu --timeout 280 --timeout-method thread > $O/pytest_elastic.log 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_elastic.py -x -v -m gpu --timeout 280 --timeout-method thread > $O/pytest_elastic.log 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp
 G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_INSTS_VMEM GRBM_GUI_ACTIVE"
 G2="SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES"
