@@ -88,12 +88,15 @@ class RouteBatcher:
 
     # ------------------------------------------------------------------ batch function
     def _astar_for(self, device):
+        """The device's A* workspace and the lock that serialises its searches (two workers on one
+        device would otherwise run on the same per-slot state rows at once)."""
         from .graph import BatchedAstar
         key = str(device)
         with self._astar_lock:
             a = self._astar.get(key)
             if a is None:
-                a = BatchedAstar(self.provider.g, self.provider.cost, device, slots=self.astar_slots)
+                a = (BatchedAstar(self.provider.g, self.provider.cost, device, slots=self.astar_slots),
+                     threading.Lock())
                 self._astar[key] = a
             return a
 
@@ -122,7 +125,9 @@ class RouteBatcher:
             o += len(cl)
         pairs = sorted(pairs)
         if device is not None and getattr(device, "type", str(device)).startswith("cuda"):
-            res = self._astar_for(device).paths([p[0] for p in pairs], [p[1] for p in pairs])
+            astar, lock = self._astar_for(device)
+            with lock:
+                res = astar.paths([p[0] for p in pairs], [p[1] for p in pairs])
         else:
             res = prov._shortest(pairs)
         return dict(zip(pairs, res))
