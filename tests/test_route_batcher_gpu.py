@@ -85,3 +85,38 @@ def test_http_1k_concurrent_graph_provider_one_astar_launch_per_flush():
             assert abs(gg["properties"]["summary"]["duration"] - ref["properties"]["summary"]["duration"]) \
                 <= 1e-3 * max(1.0, ref["properties"]["summary"]["duration"])
     assert mism <= len(reqs) // 100
+
+
+def test_two_workers_one_device_graph_provider_stress():
+    """Two flush workers on ONE GPU (shared A* workspace, one request queue): bursts of concurrent
+    requests are all answered and equal the per-request path (regression for the stranded-batch
+    queue wait and the unlocked shared A* workspace)."""
+    import concurrent.futures as cf
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider, edge_costs
+    from routest_amd.routing.route_batcher import RouteBatcher
+    from routest_amd.serve.eta_service import default_model
+    g = synth_road_graph(20_000, seed=5)
+    dev = torch.device("cuda:0")
+    cost = edge_costs(g, default_model(hidden=64, steps=50), device=dev)
+    prov = GraphProvider(g, cost, device=dev)
+    ref_prov = GraphProvider(g, cost, device=dev)
+    eng = "backend:mi355x"
+    rb = RouteBatcher(prov, engine=eng, devices=[dev, dev], batch_max=128, timeout_us=300, astar_slots=2048)
+    try:
+        for rnd in range(3):
+            reqs = _reqs_on(g.lat, g.lon, 400, 10 + rnd, kmax=5)
+            with cf.ThreadPoolExecutor(16) as ex:
+                got = list(ex.map(lambda r: rb.optimize_sync(r, timeout=60.0), reqs))
+            mism = 0
+            for gg, r in zip(got, reqs):
+                ref = optimize_route(r, ref_prov, eng)
+                assert ("error" in gg) == ("error" in ref)
+                if gg != ref:
+                    mism += 1       # a tie may pick another equal-cost node path: same duration
+                    assert abs(gg["properties"]["summary"]["duration"] - ref["properties"]["summary"]["duration"]) \
+                        <= 1e-3 * max(1.0, ref["properties"]["summary"]["duration"])
+            assert mism <= len(reqs) // 50
+        assert sum(rb.flushes) < 3 * 400 / 2
+    finally:
+        rb.close()
