@@ -1,0 +1,150 @@
+#!/usr/bin/env python3
+"""Mixed-traffic soak of the whole FastAPI app in-process (ASGI): concurrent clients hit
+/api/predict_eta, /predict (batched), /api/optimize_route (ML ETA on, persisted to SQLite),
+/route, /api/history, /api/history/<id>, DELETE, /api/health and /metrics for ``--seconds``, on
+the GPU services when a GPU is visible (micro-batched ETA kernel, cross-request route batcher with
+the road-graph provider and batched A*).  Every response is checked against its endpoint's
+contract; exits non-zero on any unexpected status, malformed body or exception.
+
+    python tools/app_soak.py --seconds 30 --clients 64
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=20.0)
+    ap.add_argument("--clients", type=int, default=64)
+    ap.add_argument("--graph-nodes", type=int, default=20000)
+    a = ap.parse_args()
+    import httpx
+    import numpy as np
+    import torch
+
+    from routest_amd.api.app import build_services, create_app
+    from routest_amd.config import load_settings
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider, edge_costs
+    from routest_amd.serve.eta_service import EtaService, default_model
+    from routest_amd.store.store import SQLiteStore
+
+    gpu = torch.cuda.is_available()
+    dev = torch.device("cuda:0") if gpu else None
+    model = default_model(seed=0, hidden=256, steps=100)
+    g = synth_road_graph(a.graph_nodes, seed=7)
+    cost = edge_costs(g, model, device=dev)
+    prov = GraphProvider(g, cost, device=dev)
+    s = load_settings(env={}, dotenv_path=None, devices=[0] if gpu else [], device="cuda:0" if gpu else "cpu",
+                      route_batch="auto" if gpu else "0", route_gpu_min_stops=1, warm_scorer=False)
+    tmp = tempfile.mkdtemp()
+    store = SQLiteStore(os.path.join(tmp, "soak.db"))
+    eta = EtaService(model, devices=[0]) if gpu else EtaService(model, device="cpu")
+    sv = build_services(s, eta=eta, provider=prov, store=store)
+    app = create_app(sv)
+    rng = random.Random(1)
+    lat, lon = g.lat, g.lon
+
+    def route_req(k):
+        idx = [rng.randrange(len(lat)) for _ in range(k + 1)]
+        return {"source_point": {"lat": float(lat[idx[0]]), "lon": float(lon[idx[0]])},
+                "destination_points": [{"lat": float(lat[i]), "lon": float(lon[i]), "payload": 1} for i in idx[1:]],
+                "driver_details": {"driver_name": f"d{rng.randrange(1000)}", "vehicle_type": "car",
+                                   "vehicle_capacity": 9999, "maximum_distance": 1e7, "driver_age": 30},
+                "use_ml_eta": True, "context": {"weather": "Rainy", "traffic": "High"}}
+
+    def eta_req():
+        return {"summary": {"distance": rng.uniform(500, 40000)}, "pickup_time": "2026-10-15T08:30:00",
+                "driver_age": rng.randint(18, 70), "weather": rng.choice(["Sunny", "Rainy", "Foggy", "Stormy"]),
+                "traffic": rng.choice(["Low", "Medium", "High"])}
+
+    stats = {"requests": 0, "errors": [], "by_ep": {}}
+    ids = []
+
+    def bad(ep, msg):
+        if len(stats["errors"]) < 20:
+            stats["errors"].append(f"{ep}: {msg}")
+
+    async def client(c: httpx.AsyncClient, deadline: float):
+        while time.perf_counter() < deadline:
+            op = rng.random()
+            try:
+                if op < 0.35:
+                    ep = "predict_eta"
+                    r = await c.post("/api/predict_eta", json=eta_req())
+                    ok = r.status_code == 200 and "eta_minutes_ml" in r.json()
+                elif op < 0.45:
+                    ep = "predict_batch"
+                    r = await c.post("/predict", json={"items": [eta_req() for _ in range(rng.randint(1, 64))]})
+                    ok = r.status_code == 200
+                elif op < 0.70:
+                    ep = "optimize_route"
+                    r = await c.post("/api/optimize_route", json=route_req(rng.randint(1, 6)))
+                    body = r.json()
+                    ok = r.status_code in (200, 400) and (("error" in body) == (r.status_code == 400))
+                    if r.status_code == 200 and body.get("properties", {}).get("request_id"):
+                        ids.append(body["properties"]["request_id"])
+                elif op < 0.80:
+                    ep = "route"
+                    r = await c.post("/route", json=route_req(1))
+                    ok = r.status_code in (200, 400)
+                elif op < 0.88:
+                    ep = "history"
+                    r = await c.get("/api/history")
+                    ok = r.status_code == 200 and isinstance(r.json(), (list, dict))
+                elif op < 0.93 and ids:
+                    ep = "history_id"
+                    r = await c.get(f"/api/history/{rng.choice(ids)}")
+                    ok = r.status_code in (200, 404)
+                elif op < 0.95 and ids:
+                    ep = "delete"
+                    r = await c.delete(f"/api/history/{ids.pop()}")
+                    ok = r.status_code in (200, 204, 404)
+                elif op < 0.98:
+                    ep = "health"
+                    r = await c.get("/api/health")
+                    ok = r.status_code == 200 and "status" in r.json()
+                else:
+                    ep = "metrics"
+                    r = await c.get("/metrics")
+                    ok = r.status_code == 200
+            except Exception as e:  # noqa: BLE001
+                ep, ok, r = "exception", False, None
+                bad(ep, repr(e)[:200])
+            stats["requests"] += 1
+            stats["by_ep"][ep] = stats["by_ep"].get(ep, 0) + 1
+            if not ok and r is not None:
+                bad(ep, f"status {r.status_code} body {r.text[:200]}")
+
+    async def run():
+        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://soak",
+                                     timeout=60) as c:
+            deadline = time.perf_counter() + a.seconds
+            await asyncio.gather(*[client(c, deadline) for _ in range(a.clients)])
+
+    t0 = time.perf_counter()
+    rb = sv.route_batcher
+    try:
+        asyncio.run(run())
+    finally:
+        sv.close()
+    el = time.perf_counter() - t0
+    out = {"gpu": gpu, "seconds": round(el, 1), "clients": a.clients, "requests": stats["requests"],
+           "req_per_s": round(stats["requests"] / el, 1), "by_endpoint": stats["by_ep"],
+           "errors": stats["errors"], "route_flushes": sum(rb.flushes) if rb is not None else None}
+    print(json.dumps(out), flush=True)
+    return 0 if not stats["errors"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
