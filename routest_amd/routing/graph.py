@@ -282,6 +282,7 @@ class BatchedAstar:
                              self.heap, self.touched, out_cost, out_len, out_status, out_path,
                              0, self.max_iters, self.inv_vmax, self.lm, self.last_iters,
                              tail[i0:i0 + self.wave_slots].contiguous(), self.wave_delta, self.hcache)
+        self._exact_fallback(s, t, out_cost, out_len, out_status, out_path)
         if self.perm_t is not None:
             # back to the caller's node ids (entries past path_len are undefined: mask them to -1)
             valid = torch.arange(self.max_path, device=d, dtype=torch.int32)[None, :] < out_len[:, None]
@@ -296,6 +297,44 @@ class BatchedAstar:
                 res.append(y)
             return tuple(res)
         return out_cost, out_len, out_status, out_path
+
+    # searches that ran out of per-slot list capacity (status 2) or of the iteration cap (3) are
+    # finished exactly on the host (scipy Dijkstra over the same costs), at most this many per launch
+    FALLBACK_MAX = 1024
+
+    def _exact_fallback(self, s, t, out_cost, out_len, out_status, out_path) -> None:
+        bad = ((out_status == 2) | (out_status == 3)).nonzero().flatten()
+        self.last_fallbacks = int(bad.numel())
+        if not self.last_fallbacks or self.last_fallbacks > self.FALLBACK_MAX:
+            return
+        from scipy.sparse import csr_matrix
+        from scipy.sparse.csgraph import dijkstra
+        if getattr(self, "_csr", None) is None:
+            # the device-order graph (node ids as the kernel sees them)
+            self._csr = csr_matrix((self.cost.double().cpu().numpy(), self.indices.cpu().numpy(),
+                                    self.indptr.cpu().numpy()), shape=(self.g.num_nodes,) * 2)
+        qi = bad.cpu().numpy()
+        ss, tt = s[bad].cpu().numpy(), t[bad].cpu().numpy()
+        uniq, inv = np.unique(ss, return_inverse=True)
+        dist, pred = dijkstra(self._csr, directed=True, indices=uniq, return_predecessors=True)
+        cost_h, len_h, st_h = out_cost[bad].cpu(), out_len[bad].cpu(), out_status[bad].cpu()
+        for j, (q, sv, tv) in enumerate(zip(qi, ss, tt)):
+            row = inv[j]
+            if not np.isfinite(dist[row, tv]):
+                cost_h[j], len_h[j], st_h[j] = -1.0, 0, 1
+                continue
+            path = [int(tv)]
+            while path[-1] != sv:
+                path.append(int(pred[row, path[-1]]))
+            if len(path) > self.max_path:
+                cost_h[j], len_h[j], st_h[j] = -1.0, 0, 4
+                continue
+            path.reverse()
+            out_path[int(q), :len(path)] = torch.tensor(path, dtype=torch.int32, device=out_path.device)
+            cost_h[j], len_h[j], st_h[j] = float(dist[row, tv]), len(path), 0
+        out_cost[bad] = cost_h.to(out_cost.device)
+        out_len[bad] = len_h.to(out_len.device)
+        out_status[bad] = st_h.to(out_status.device)
 
     def paths(self, src, dst) -> List[Tuple[float, List[int]]]:
         c, n, st, p = self.run(src, dst)

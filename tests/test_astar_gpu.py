@@ -37,6 +37,7 @@ def test_astar_optimal_costs_and_valid_paths(graph_and_cost, monkeypatch, reorde
     ref = dijkstra_ref(g, cost, src, dst)
     assert np.isfinite(ref).all()            # every query is connected on this graph ...
     assert (st == 0).all(), np.unique(st, return_counts=True)    # ... and every search finds it
+    assert a.last_fallbacks == 0             # ... on the GPU (no host fallback involved)
     ok = st == 0
     np.testing.assert_allclose(c[ok], ref[ok], rtol=1e-4)
     # each path is a real edge sequence from src to dst whose cost sums to the reported cost
@@ -83,3 +84,18 @@ def test_wave_tail_stage_exact(graph_and_cost, monkeypatch, lane_pops, delta):
         assert abs(tot - c[i]) <= 1e-3 * max(1.0, c[i])
     c2 = a.run(src, dst)[0].cpu().numpy()                 # workspace restored by both stages
     assert np.array_equal(c, c2)
+
+
+def test_overflowed_searches_finish_exactly_on_host(graph_and_cost):
+    """With per-slot lists far too small (cap 128) most searches overflow on the GPU (status 2);
+    they are finished by the exact host fallback, so every leg is found at the optimal cost."""
+    g, cost, _ = graph_and_cost
+    src, dst = synth_route_queries(g, 300, seed=3)
+    a = BatchedAstar(g, cost, "cuda:0", slots=512, cap=128)
+    c, n, st, p = a.run(src, dst)
+    assert a.last_fallbacks > 0
+    c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
+    assert (st == 0).all(), np.unique(st, return_counts=True)
+    np.testing.assert_allclose(c, dijkstra_ref(g, cost, src, dst), rtol=1e-4)
+    for i in range(0, 300, 37):
+        assert p[i, 0] == src[i] and p[i, n[i] - 1] == dst[i]
