@@ -360,6 +360,11 @@ def main() -> None:
             ok, err = False, repr(e)[:200]
         if agree(ok):
             train_os_res = train_probe(devcomm)
+            if "error" in train_os_res or train_os_res.get("comm_error"):
+                # (agreed on by every rank inside train_probe): no further one-shot use
+                torch.cuda.synchronize()
+                devcomm.close()
+                devcomm = None
         else:
             train_os_res = {"error": err or "one-shot set-up failed on a peer rank"}
             devcomm = None
@@ -368,8 +373,9 @@ def main() -> None:
     # timed region (RCCL all-reduce / all-gather sweep; extra JSON key, outside the timing)
     coll = None
     if world > 1 and not share and os.environ.get("ROUTEST_BENCH_COLLECTIVES", "1") != "0":
-        # RCCL only (the process group bench.py already holds): nothing here can leave one rank
-        # waiting on a set-up step another rank skipped
+        # RCCL on the process group bench.py already holds, plus the one-shot all-reduce when its
+        # set-up and training probe succeeded on every rank: every decision here depends only on
+        # state all ranks agreed on, so no rank can be left waiting on a step another one skipped
         from routest_amd.parallel.collective_probe import sweep
         try:
             coll = sweep(dev, native=devcomm)
