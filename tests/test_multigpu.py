@@ -179,7 +179,7 @@ def test_bench_launches_all_gpus():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "3",
                         "--warmup", "1", "--batch", "1048576", "--p50", "0", "--rec16-steps", "2",
                         "--route-requests", "2000", "--route-steps", "1"],
-                       capture_output=True, text=True, timeout=220, cwd=ROOT, env=env)
+                       capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
