@@ -47,9 +47,11 @@ def parse_args():
                     help="zerocopy: the kernel reads pinned host records and writes pinned host "
                          "predictions over PCIe; host: copy-engine H2D/D2H pipeline; device: "
                          "records already resident in HBM")
-    ap.add_argument("--rec", type=int, choices=[6, 8, 16], default=6,
-                    help="wire record bytes per request (6: bulk 48-bit, 8: compact, 16: full with "
-                         "epoch seconds) — routest_amd/models/features.py")
+    ap.add_argument("--rec", type=int, choices=[6, 8, 16], default=8,
+                    help="wire record bytes per request (8: the serving format — the native front "
+                         "end and the batcher send it for every batch it represents exactly; 16: "
+                         "full record with epoch seconds; 6: lossy bulk research format) — "
+                         "routest_amd/models/features.py")
     ap.add_argument("--variant", type=int, default=-1)
     ap.add_argument("--h2d-streams", type=int, default=1,
                     help="hybrid: split each step's record copy over this many copy streams")
@@ -105,7 +107,7 @@ def main() -> None:
     from routest_amd.data.synth import synth_records
     from routest_amd.models.features import records_to_features
     from routest_amd.models.mlp3 import EtaMLP
-    from routest_amd.models.features import records_to_compact, records_to_compact6
+    from routest_amd.models.features import records_to_compact6, records_to_wire8
     from routest_amd.ops.eta_mlp import (EtaMlpKernel, records6_to_tensor, records8_to_tensor,
                                          records_to_tensor)
 
@@ -119,8 +121,15 @@ def main() -> None:
     rec, _ = synth_records(B, seed=100 + rank)
 
     def wire(nbytes: int) -> torch.Tensor:
+        if nbytes == 8:
+            # the same exactness-guarded packer the service runs (features.records_to_wire8 ==
+            # csrc/runtime/rt_core.h pack_wire8): pickup hours since the batch's base Monday, the
+            # kernel derives weekday/hour; the synthetic pickups carry minutes/seconds like real
+            # ISO timestamps and integer ages, so the whole batch is representable
+            r8 = records_to_wire8(rec)
+            assert r8 is not None, "synthetic batch not representable as 8-byte wire records"
+            return records8_to_tensor(r8).pin_memory()
         return (records6_to_tensor(records_to_compact6(rec)) if nbytes == 6 else
-                records8_to_tensor(records_to_compact(rec)) if nbytes == 8 else
                 records_to_tensor(rec)).pin_memory()
 
     nbuf = 3
@@ -248,6 +257,10 @@ def main() -> None:
     # of the kernel on the same (wire-format-decoded) features
     from routest_amd.ops.eta_mlp import emulate_kernel, featurize_torch
     got = pipe.last_output(a.warmup + a.steps - 1)
+    from routest_amd.utils.faults import active_faults
+    if "bench_corrupt_output" in active_faults():     # test hook: the check must catch this
+        got[0] = float("nan")
+        got[1:64] += 1e3
     ok = bool(torch.isfinite(got).all().item())
     nchk = min(B, 65536)
     rec_chk = pipe.host_rec[:nchk]
@@ -355,10 +368,11 @@ def main() -> None:
         err = None
         try:
             devcomm = DeviceComm(dev, use_rccl=False)
-            ok = devcomm.oneshot
+            os_ok = devcomm.oneshot
         except Exception as e:  # noqa: BLE001 - reported, never fatal for the headline
-            ok, err = False, repr(e)[:200]
-        if agree(ok):
+            os_ok, err = False, repr(e)[:200]
+        # (os_ok, not ok: `ok` holds the headline output check reported as "finite" / exit 3)
+        if agree(os_ok):
             train_os_res = train_probe(devcomm)
             if "error" in train_os_res or train_os_res.get("comm_error"):
                 # (agreed on by every rank inside train_probe): no further one-shot use
@@ -584,8 +598,10 @@ def main() -> None:
             "p50_fastapi_asgi_ms": p50_fastapi_ms,
             "http_concurrent16_req_per_s": conc,
             "preds_per_s_rec16": rec16_value,
-            "record_format": {6: "6 B packed: distance 1/8 m, integer age 0-127, host weekday/hour",
-                              8: "8 B compact: fp32 distance, fp16 age, host weekday/hour",
+            "record_format": {6: "6 B packed (lossy research format): distance 1/8 m, integer age 0-127, host weekday/hour",
+                              8: "8 B wire record = the serving format (native front end, batcher): fp32 distance, "
+                                 "fp16 age (exactness-guarded, else 16 B), pickup hours since the batch's base "
+                                 "Monday; weekday/hour featurised by the kernel; bit-identical predictions to 16 B",
                               16: "16 B full: fp32 distance, fp32 age, epoch seconds (kernel featurises)"}[a.rec],
             "shared_gpu": bool(share and world > 1),
             "collectives": coll,

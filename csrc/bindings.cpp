@@ -1051,9 +1051,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     rt::native_server_stop(h);
   });
   m.def("native_server_stats", [](int64_t h) {
-    long long v[6];
-    rt::native_server_stats(h, v);
-    return std::vector<int64_t>{v[0], v[1], v[2], v[3], v[4], v[5]};
+    const auto v = rt::native_server_stats(h);
+    return std::vector<int64_t>(v.begin(), v.end());
   });
   m.def("comm_unique_id", &comm_unique_id, "RCCL unique id (128 bytes) for comm_create");
   m.def("comm_create", &comm_create, "own RCCL communicator + one-shot IPC buffers");

@@ -103,22 +103,35 @@ __device__ __forceinline__ void featurize_f32(const int4 rc, const int h, const 
   }
 }
 
-// Compact 8-byte record (features.py::RECORD8_DTYPE): x = distance_m bits, y = fp16 age |
-// weekday << 16 | hour << 19 | weather << 24 | traffic << 27.  Same lane-half feature split.
+// 8-byte wire record (features.py::RECORD8_DTYPE): x = distance_m bits, y = fp16 age | hours << 16 |
+// weather << 26 | traffic << 29, where `hours` counts wall-clock hours from 00:00 of the batch's
+// base Monday.  The featurisation of the time happens here: weekday = (hours / 24) % 7 and hour =
+// hours % 24, as multiply-shifts that are exact over the 10-bit range (hours < 1024, days < 43;
+// checked exhaustively in tests/test_runtime_cpu.py).
+__device__ __forceinline__ void wire8_time(const unsigned pk, float& wd, float& hr) {
+  const unsigned hrs = (pk >> 16) & 1023u;
+  const unsigned day = (hrs * 2731u) >> 16;                 // hrs / 24
+  const unsigned wdi = day - ((day * 9363u) >> 16) * 7u;    // day % 7
+  wd = (float)wdi;
+  hr = (float)(hrs - day * 24u);
+}
+
 __device__ __forceinline__ void featurize8_f32(const int2 rc, const int h, const NormParams& np,
                                                float f[8]) {
   const unsigned pk = (unsigned)rc.y;
   if (h == 0) {
-    const int w = (pk >> 24) & 7;
-    const int t = (pk >> 27) & 7;
+    const int w = (pk >> 26) & 7;
+    const int t = (pk >> 29) & 7;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       f[j] = (w == j) ? 1.f : 0.f;
       f[4 + j] = (t == j) ? 1.f : 0.f;
     }
   } else {
-    const float wdn = (float)((pk >> 16) & 7) * np.scale[0] + np.shift[0];
-    const float hrn = (float)((pk >> 19) & 31) * np.scale[1] + np.shift[1];
+    float wd, hr;
+    wire8_time(pk, wd, hr);
+    const float wdn = wd * np.scale[0] + np.shift[0];
+    const float hrn = hr * np.scale[1] + np.shift[1];
     const float kmn = (__int_as_float(rc.x) * 1e-3f) * np.scale[2] + np.shift[2];
     const float agn = __half2float(__ushort_as_half((unsigned short)(pk & 0xffffu))) * np.scale[3] +
                       np.shift[3];
@@ -168,7 +181,7 @@ __device__ __forceinline__ bf16x8 featurize8_bf16(const int2 rc, const int h, co
   featurize8_f32(rc, 1, np, f);
   const bf16x8 nb = to_bf16x8(f);
   const unsigned pk = (unsigned)rc.y;
-  const bf16x8 oh = onehot_pair_bf16((pk >> 24) & 7u, (pk >> 27) & 7u);
+  const bf16x8 oh = onehot_pair_bf16((pk >> 26) & 7u, (pk >> 29) & 7u);
   return h == 0 ? oh : nb;
 }
 

@@ -82,7 +82,8 @@ struct Pending {
 };
 
 struct Stats {
-  std::atomic<long long> requests{0}, predictions{0}, launches{0}, errors{0}, resident{0}, fallbacks{0};
+  std::atomic<long long> requests{0}, predictions{0}, launches{0}, errors{0}, resident{0}, fallbacks{0},
+      wire8{0};
 };
 
 inline Stamp now_local() {
@@ -139,9 +140,11 @@ class Reactor {
     if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return;
     cap_ = cfg_.max_batch;
     if (hipHostMalloc((void**)&h_rec_, (size_t)cap_ * 16, hipHostMallocMapped) != hipSuccess ||
+        hipHostMalloc((void**)&h_rec8_, (size_t)cap_ * 8, hipHostMallocMapped) != hipSuccess ||
         hipHostMalloc((void**)&h_out_, (size_t)cap_ * 4, hipHostMallocMapped) != hipSuccess)
       return;
     if (hipHostGetDevicePointer(&d_rec_, h_rec_, 0) != hipSuccess ||
+        hipHostGetDevicePointer(&d_rec8_, h_rec8_, 0) != hipSuccess ||
         hipHostGetDevicePointer((void**)&d_out_, h_out_, 0) != hipSuccess)
       return;
 
@@ -167,6 +170,7 @@ class Reactor {
     close(ep_);
     close(wake_);
     (void)hipHostFree(h_rec_);
+    (void)hipHostFree(h_rec8_);
     (void)hipHostFree(h_out_);
     (void)hipStreamDestroy(stream_);
   }
@@ -179,8 +183,10 @@ class Reactor {
   int lfd_ = -1, ep_ = -1, wake_ = -1;
   hipStream_t stream_{};
   EtaRecord* h_rec_ = nullptr;
+  rtc::Wire8* h_rec8_ = nullptr;       // the same round as 8-byte wire records, when exact
   float* h_out_ = nullptr;
   void* d_rec_ = nullptr;
+  void* d_rec8_ = nullptr;
   float* d_out_ = nullptr;
   int cap_ = 0;
   size_t nrec_ = 0;
@@ -455,8 +461,12 @@ class Reactor {
           std::lock_guard<std::mutex> lk(*cfg_.scorer_mu);
           pscore_park(ps);
         }
-        e = launch_eta_mlp3_fwd(d_rec_, d_out_, (int)nrec_, cfg_.blob, cfg_.H, cfg_.np, cfg_.variant,
-                                cfg_.num_cus, stream_, 16);
+        // the kernel reads the records over PCIe (zero-copy): send 8-byte wire records whenever
+        // the round is exactly representable (csrc/runtime/rt_core.h pack_wire8), else 16-byte
+        const bool w8 = rtc::pack_wire8(h_rec_, nrec_, h_rec8_);
+        if (w8) st_.wire8.fetch_add(1, std::memory_order_relaxed);
+        e = launch_eta_mlp3_fwd(w8 ? d_rec8_ : d_rec_, d_out_, (int)nrec_, cfg_.blob, cfg_.H, cfg_.np,
+                                cfg_.variant, cfg_.num_cus, stream_, w8 ? 8 : 16);
         if (e == hipSuccess) e = hipStreamSynchronize(stream_);
       }
       st_.launches.fetch_add(1, std::memory_order_relaxed);
@@ -610,17 +620,13 @@ void native_server_stop(int64_t h) {
   delete s;
 }
 
-void native_server_stats(int64_t h, long long out[6]) {
+std::vector<long long> native_server_stats(int64_t h) {
   std::lock_guard<std::mutex> lk(g_srv_mu);
-  out[0] = out[1] = out[2] = out[3] = out[4] = out[5] = 0;
-  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return;
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(7, 0);
   Server* s = g_servers[h];
-  out[0] = s->stats.requests.load();
-  out[1] = s->stats.predictions.load();
-  out[2] = s->stats.launches.load();
-  out[3] = s->stats.errors.load();
-  out[4] = s->stats.resident.load();
-  out[5] = s->stats.fallbacks.load();
+  return {s->stats.requests.load(), s->stats.predictions.load(), s->stats.launches.load(),
+          s->stats.errors.load(), s->stats.resident.load(), s->stats.fallbacks.load(),
+          s->stats.wire8.load()};
 }
 
 }  // namespace rt

@@ -143,7 +143,7 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
                             const NormParams& np, int variant, int max_batch, const std::vector<std::string>& cors,
                             bool cors_vercel, bool bind_any, std::string& err);
 void native_server_stop(int64_t h);
-void native_server_stats(int64_t h, long long out[6]);
+std::vector<long long> native_server_stats(int64_t h);
 
 // ---- native collectives (rccl_ops) : comm.hip ----
 int comm_unique_id(char out[128]);

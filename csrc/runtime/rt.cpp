@@ -133,6 +133,22 @@ py::tuple pack_predict_batch(py::bytes body, int64_t now_secs, int32_t now_us) {
   return py::make_tuple(rec, secs, us, tz, errs, is_batch);
 }
 
+// uint8 [N,16] EtaRecords -> uint8 [N,8] wire8 records, or None if the batch is not exactly
+// representable (the native front end's guard, rt_core.h pack_wire8).
+py::object pack_wire8_py(py::array_t<uint8_t, py::array::c_style> rec) {
+  if (rec.ndim() != 2 || rec.shape(1) != 16) throw std::invalid_argument("records must be uint8 [N,16]");
+  const size_t n = (size_t)rec.shape(0);
+  py::array_t<uint8_t> out({(py::ssize_t)n, (py::ssize_t)8});
+  bool ok;
+  {
+    py::gil_scoped_release nogil;
+    ok = pack_wire8(reinterpret_cast<const EtaRecord*>(rec.data()), n,
+                    reinterpret_cast<Wire8*>(out.mutable_data()));
+  }
+  if (!ok) return py::none();
+  return std::move(out);
+}
+
 // minutes + stamps -> the reference's response JSON (batch: {"predictions": [...]}).
 py::bytes format_predict_batch(py::array_t<float, py::array::c_style | py::array::forcecast> minutes,
                                py::array_t<int64_t> secs, py::array_t<int32_t> us,
@@ -342,6 +358,7 @@ PYBIND11_MODULE(_rt, m) {
         py::arg("max_requests") = 0, py::arg("warmup") = 0);
   m.def("pack_predict_batch", &pack_predict_batch, py::arg("body"), py::arg("now_secs"), py::arg("now_us"));
   m.def("format_predict_batch", &format_predict_batch);
+  m.def("pack_wire8", &pack_wire8_py);
   m.def("iso_parse", &iso_parse);
   m.def("iso_add_minutes", &iso_add_minutes);
   m.def("py_float_repr", &py_float_repr);

@@ -298,6 +298,65 @@ struct EtaRecord {
 #pragma pack(pop)
 static_assert(sizeof(EtaRecord) == 16, "record layout");
 
+// 8-byte wire record (routest_amd/models/features.py RECORD8_DTYPE, csrc/common.h featurize8_f32):
+// distance_m (f32) | fp16(age) | hours since the batch's base Monday << 16 | weather << 26 |
+// traffic << 29.  Used for every batch it represents exactly (halves the PCIe bytes per request).
+#pragma pack(push, 1)
+struct Wire8 {
+  float distance_m;
+  uint32_t packed;
+};
+#pragma pack(pop)
+static_assert(sizeof(Wire8) == 8, "wire8 layout");
+
+// f32 -> fp16 bits, only if the value is exactly representable (no rounding anywhere).
+inline bool f16_exact(float v, uint16_t& h) {
+  uint32_t b;
+  std::memcpy(&b, &v, 4);
+  const uint16_t sign = (uint16_t)((b >> 16) & 0x8000u);
+  const int exp = (int)((b >> 23) & 0xffu);
+  const uint32_t man = b & 0x7fffffu;
+  if (exp == 0 && man == 0) { h = sign; return true; }
+  if (exp == 0 || exp == 255) return false;             // f32 subnormal / inf / nan
+  const int e = exp - 127;
+  if (e > 15) return false;
+  if (e >= -14) {                                        // normal half
+    if (man & 0x1fffu) return false;
+    h = (uint16_t)(sign | (uint16_t)((e + 15) << 10) | (uint16_t)(man >> 13));
+    return true;
+  }
+  const int s = -(e + 1);                                // subnormal half: m = full >> s
+  if (s > 24) return false;
+  const uint32_t full = man | 0x800000u;
+  if (full & ((1u << s) - 1u)) return false;
+  h = (uint16_t)(sign | (uint16_t)(full >> s));
+  return true;
+}
+
+inline int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+// Pack n 16-byte records as wire8 into `out`; false (out untouched beyond n) if any record is not
+// exactly representable.  The base is 00:00 of the Monday on or before the earliest pickup (the
+// records' epoch 2020-01-01 is a Wednesday: day d has weekday (d + 2) % 7).
+inline bool pack_wire8(const EtaRecord* r, size_t n, Wire8* out) {
+  if (n == 0) return true;
+  int64_t hmin = INT64_MAX;
+  for (size_t i = 0; i < n; ++i) hmin = std::min(hmin, floor_div(r[i].wallclock_s, 3600));
+  const int64_t d0 = floor_div(hmin, 24);
+  const int64_t base = (d0 - ((d0 + 2) % 7 + 7) % 7) * 24;
+  for (size_t i = 0; i < n; ++i) {
+    uint16_t a;
+    if (!f16_exact(r[i].driver_age, a)) return false;
+    const int64_t hrs = floor_div(r[i].wallclock_s, 3600) - base;
+    if (hrs < 0 || hrs >= 1024) return false;
+    const uint32_t w = r[i].weather > 3 ? 7u : r[i].weather;
+    const uint32_t t = r[i].traffic > 3 ? 7u : r[i].traffic;
+    out[i].distance_m = r[i].distance_m;
+    out[i].packed = (uint32_t)a | ((uint32_t)hrs << 16) | (w << 26) | (t << 29);
+  }
+  return true;
+}
+
 // One /predict item -> record (+stamp) or error text.
 inline std::string pack_item(const rtj::Value& it, const Stamp& now, EtaRecord& r, Stamp& st) {
   if (it.kind != rtj::Value::Obj) return "item must be a JSON object";

@@ -100,8 +100,12 @@ def synth_trips(n: int, seed: int = 0, noise: float = 0.05) -> Tuple[np.ndarray,
 
 
 def synth_records(n: int, seed: int = 0, noise: float = 0.05) -> Tuple[np.ndarray, np.ndarray]:
+    """Packed 16-byte records; pickups carry a random minute/second inside their hour, like real
+    ISO timestamps (only weekday and hour reach the model)."""
     x, y = synth_trips(n, seed, noise)
-    return features_to_records(x, base_day=2200), y
+    rec = features_to_records(x, base_day=2200)
+    rec["wallclock_s"] += np.random.default_rng(seed + 7).integers(0, 3600, n).astype(np.int32)
+    return rec, y
 
 
 def write_trips_csv(path: str, n: int = 1000, seed: int = 0) -> None:

@@ -1,16 +1,26 @@
 """On-disk model format + compatibility loaders.
 
-Native checkpoint = a directory::
+Native checkpoint = a directory holding versioned snapshots and one pointer::
 
-    config.json          {"arch": "mlp3"|"linear", "hidden", "feature_columns", "target",
-                          "dtype", "version", "framework": "routest_amd"}
-    model.safetensors    weights + normalisation buffers
-    optimizer.safetensors / trainer_state.json   (training resume, optional)
+    <path>/LATEST                   text: name of the current snapshot directory (e.g. step_00000120)
+    <path>/step_00000120/
+        config.json                 {"arch": "mlp3"|"linear", "hidden", "feature_columns", "target",
+                                     "dtype", "version", "framework": "routest_amd", "step"}
+        model.safetensors           weights + normalisation buffers
+        optimizer.safetensors       flat AdamW moments (training resume, optional)
+        trainer_state.json          {"step", "config", "world"} (training resume, optional)
+
+A save writes a complete snapshot into a private staging directory, fsyncs every file and the
+directory, renames it to ``step_N`` and only then swaps ``LATEST`` with ONE ``os.replace`` (fsynced
+as well).  A rank killed at any point leaves either the previous snapshot or the new one as
+``LATEST`` — never new weights beside an old step counter (round-2 ADVICE: the per-file renames
+could mix them).  The two most recent snapshots are kept.  A flat legacy directory
+(``config.json`` + ``model.safetensors`` directly inside) still loads.
 
 Compatibility:
-* :class:`EtaPredictor` is a picklable wrapper exposing ``.predict(pandas.DataFrame[12 R16 cols])``
-  -> minutes, so the *reference* Flask service can load a routest_amd model unchanged through
-  ``ETA_MODEL_PATH`` (``RO/Flaskr/ml.py:6-21,53``).
+* :func:`export_predictor_pickle` (``models/export.py``) writes a by-value pickle exposing
+  ``.predict(pandas.DataFrame[12 R16 cols])`` -> minutes that the *reference* Flask service loads
+  unchanged through ``ETA_MODEL_PATH`` with numpy + pandas only (``RO/Flaskr/ml.py:6-21,53``).
 * :func:`load_any` also accepts a pickle exposing ``.predict(DataFrame)`` (e.g. the reference's
   ``XGBRegressor``; needs ``xgboost``, which is not installed here) — only when the caller opts in
   (``allow_pickle=True``), since unpickling executes code — and an XGBoost JSON model dump
@@ -21,23 +31,68 @@ from __future__ import annotations
 
 import json
 import os
+import shutil
 from typing import Any, Dict, Optional, Tuple
 
-import numpy as np
 import torch
 from safetensors.torch import load_file, save_file
 
-from .features import FEATURE_COLUMNS, dataframe_to_features
+from .export import EtaPredictor, export_predictor_pickle, make_predictor  # noqa: F401 (re-export)
+from .features import FEATURE_COLUMNS
 from .mlp3 import EtaMLP, LinearETA
 
-FORMAT_VERSION = 1
+FORMAT_VERSION = 2
+LATEST = "LATEST"
+KEEP = 2
+
+
+def _fsync_file(p: str) -> None:
+    fd = os.open(p, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
+def _fsync_dir(p: str) -> None:
+    try:
+        fd = os.open(p, os.O_RDONLY | os.O_DIRECTORY)
+    except OSError:
+        return
+    try:
+        os.fsync(fd)
+    except OSError:
+        pass
+    finally:
+        os.close(fd)
+
+
+def resolve_checkpoint(path: str) -> Optional[str]:
+    """The snapshot directory ``path`` currently designates, or None if there is none."""
+    ptr = os.path.join(path, LATEST)
+    if os.path.isfile(ptr):
+        with open(ptr) as f:
+            name = f.read().strip()
+        d = os.path.join(path, name)
+        if name and os.path.basename(name) == name and os.path.isfile(os.path.join(d, "config.json")):
+            return d
+        raise ValueError(f"checkpoint pointer {ptr} names a missing snapshot {name!r}")
+    if os.path.isfile(os.path.join(path, "config.json")):
+        return path                                   # flat legacy layout
+    return None
+
+
+def checkpoint_exists(path: Optional[str]) -> bool:
+    return bool(path) and os.path.isdir(path) and resolve_checkpoint(path) is not None
 
 
 def save_checkpoint(path: str, model: Any, optimizer_state: Optional[Dict[str, torch.Tensor]] = None,
-                    trainer_state: Optional[Dict[str, Any]] = None, extra_config: Optional[dict] = None) -> None:
+                    trainer_state: Optional[Dict[str, Any]] = None, extra_config: Optional[dict] = None) -> str:
+    """Write one complete snapshot and atomically make it ``LATEST``; returns its directory."""
     os.makedirs(path, exist_ok=True)
+    step = int((trainer_state or {}).get("step", 0))
     cfg = {"arch": model.arch, "feature_columns": FEATURE_COLUMNS, "target": "eta_minutes",
-           "version": FORMAT_VERSION, "framework": "routest_amd",
+           "version": FORMAT_VERSION, "framework": "routest_amd", "step": step,
            "dtype": "bf16-kernel/fp32-master" if model.arch == "mlp3" else "fp64"}
     if model.arch == "mlp3":
         cfg["hidden"] = model.hidden
@@ -46,37 +101,70 @@ def save_checkpoint(path: str, model: Any, optimizer_state: Optional[Dict[str, t
         sd = {k: v.contiguous() for k, v in model.state_dict().items()}
     if extra_config:
         cfg.update(extra_config)
-    # every file is written under a temporary name first and only then renamed into place, in one
-    # tight sequence ending with trainer_state.json (the resume step) and config.json: a rank killed
-    # while saving (torchrun tears the job down when a peer dies) leaves the previous checkpoint's
-    # files intact instead of a half-written one
-    staged = []
-    tmp = os.path.join(path, ".tmp_opt.safetensors")
+    stage = os.path.join(path, f".staging_{os.getpid()}_{step}")
+    shutil.rmtree(stage, ignore_errors=True)
+    os.makedirs(stage)
+    files = []
     if optimizer_state is not None:
-        save_file({k: v.detach().cpu().contiguous() for k, v in optimizer_state.items()}, tmp)
-        staged.append((tmp, os.path.join(path, "optimizer.safetensors")))
-    tmp = os.path.join(path, ".tmp_model.safetensors")
-    save_file(sd, tmp)
-    staged.append((tmp, os.path.join(path, "model.safetensors")))
+        p = os.path.join(stage, "optimizer.safetensors")
+        save_file({k: v.detach().cpu().contiguous() for k, v in optimizer_state.items()}, p)
+        files.append(p)
+    p = os.path.join(stage, "model.safetensors")
+    save_file(sd, p)
+    files.append(p)
     if trainer_state is not None:
-        tmp = os.path.join(path, ".tmp_trainer_state.json")
-        with open(tmp, "w") as f:
+        p = os.path.join(stage, "trainer_state.json")
+        with open(p, "w") as f:
             json.dump(trainer_state, f)
-        staged.append((tmp, os.path.join(path, "trainer_state.json")))
-    tmp = os.path.join(path, ".tmp_config.json")
-    with open(tmp, "w") as f:
+        files.append(p)
+    p = os.path.join(stage, "config.json")
+    with open(p, "w") as f:
         json.dump(cfg, f, indent=1)
-    staged.append((tmp, os.path.join(path, "config.json")))
-    for src, dst in staged:
-        os.replace(src, dst)
+    files.append(p)
+    for p in files:
+        _fsync_file(p)
+    _fsync_dir(stage)
+    name = f"step_{step:08d}"
+    final = os.path.join(path, name)
+    if os.path.exists(final):
+        # re-save of the same step: if LATEST points at it, point LATEST at the staging copy while
+        # the old one is moved away, so the pointer never names a missing directory
+        old = os.path.join(path, f".old_{os.getpid()}_{name}")
+        shutil.rmtree(old, ignore_errors=True)
+        os.replace(final, old)
+        os.replace(stage, final)
+        shutil.rmtree(old, ignore_errors=True)
+    else:
+        os.replace(stage, final)
+    _fsync_dir(path)
+    tmp = os.path.join(path, f".{LATEST}.{os.getpid()}")
+    with open(tmp, "w") as f:
+        f.write(name + "\n")
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, os.path.join(path, LATEST))       # the commit point
+    _fsync_dir(path)
+    _prune(path, keep_name=name)
+    return final
+
+
+def _prune(path: str, keep_name: str) -> None:
+    snaps = sorted(d for d in os.listdir(path) if d.startswith("step_") and
+                   os.path.isdir(os.path.join(path, d)))
+    drop = [d for d in snaps[:-KEEP] if d != keep_name]
+    for d in drop:
+        shutil.rmtree(os.path.join(path, d), ignore_errors=True)
 
 
 def load_checkpoint(path: str) -> Tuple[Any, Dict[str, Any]]:
-    with open(os.path.join(path, "config.json")) as f:
+    d = resolve_checkpoint(path)
+    if d is None:
+        raise FileNotFoundError(f"no checkpoint in {path!r}")
+    with open(os.path.join(d, "config.json")) as f:
         cfg = json.load(f)
     if cfg.get("feature_columns", FEATURE_COLUMNS) != FEATURE_COLUMNS:
         raise ValueError("checkpoint feature schema differs from R16")
-    sd = load_file(os.path.join(path, "model.safetensors"))
+    sd = load_file(os.path.join(d, "model.safetensors"))
     if cfg["arch"] == "mlp3":
         m = EtaMLP(int(cfg["hidden"]))
         m.load_state_dict(sd)
@@ -90,66 +178,18 @@ def load_checkpoint(path: str) -> Tuple[Any, Dict[str, Any]]:
 
 
 def load_training_state(path: str) -> Tuple[Optional[Dict[str, torch.Tensor]], Optional[Dict[str, Any]]]:
+    d = resolve_checkpoint(path)
     opt = ts = None
-    p = os.path.join(path, "optimizer.safetensors")
+    if d is None:
+        return opt, ts
+    p = os.path.join(d, "optimizer.safetensors")
     if os.path.exists(p):
         opt = load_file(p)
-    p = os.path.join(path, "trainer_state.json")
+    p = os.path.join(d, "trainer_state.json")
     if os.path.exists(p):
         with open(p) as f:
             ts = json.load(f)
     return opt, ts
-
-
-class EtaPredictor:
-    """Picklable ``.predict(DataFrame) -> minutes`` wrapper (reference-loader compatible)."""
-
-    def __init__(self, model: Any):
-        self.arch = model.arch
-        if self.arch == "mlp3":
-            self.hidden = model.hidden
-            self.state = {k: v.detach().float().cpu().numpy() for k, v in model.state_dict().items()}
-        else:
-            self.hidden = 0
-            self.state = {k: v.numpy() for k, v in model.state_dict().items()}
-        self._model = None
-
-    def __getstate__(self):
-        d = dict(self.__dict__)
-        d["_model"] = None
-        return d
-
-    def _get(self):
-        if self._model is None:
-            if self.arch == "mlp3":
-                m = EtaMLP(self.hidden)
-                m.load_state_dict({k: torch.from_numpy(v) for k, v in self.state.items()})
-                self._model = m.eval()
-            else:
-                m = LinearETA()
-                m.load_state_dict({k: torch.from_numpy(v) for k, v in self.state.items()})
-                self._model = m
-        return self._model
-
-    def predict_features(self, x: np.ndarray) -> np.ndarray:
-        m = self._get()
-        if self.arch == "mlp3":
-            with torch.no_grad():
-                return m(torch.as_tensor(np.asarray(x, dtype=np.float32))).numpy()
-        return m.predict_features(x)
-
-    def predict(self, df: Any) -> np.ndarray:
-        if hasattr(df, "columns"):
-            x = dataframe_to_features(df)
-        else:
-            x = np.asarray(df, dtype=np.float32)
-        return self.predict_features(x)
-
-
-def export_predictor_pickle(model: Any, path: str) -> None:
-    import pickle
-    with open(path, "wb") as f:
-        pickle.dump(EtaPredictor(model), f)
 
 
 def load_any(path: str, allow_pickle: bool = False) -> Any:

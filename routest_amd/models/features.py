@@ -18,7 +18,7 @@ on the GPU)::
 from __future__ import annotations
 
 import datetime as dt
-from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple  # noqa: F401
 
 import numpy as np
 
@@ -40,12 +40,21 @@ RECORD_DTYPE = np.dtype([("distance_m", "<f4"), ("driver_age", "<f4"), ("wallclo
                          ("weather", "u1"), ("traffic", "u1"), ("pad", "<u2")])
 assert RECORD_DTYPE.itemsize == 16
 
-#: Compact 8-byte wire record for bulk / PCIe-bound scoring (12 B per prediction with the f32
-#: output instead of 20):  word0 = distance_m (f32);  word1 = fp16(driver_age) | weekday << 16 |
-#: hour << 19 | weather << 24 | traffic << 27   (category code 7 = unknown -> all-zero one-hot).
+#: Compact 8-byte wire record (12 B per prediction with the f32 output instead of 20), used by the
+#: native front end, the Python batcher and bench.py alike for every batch it represents EXACTLY:
+#:   word0 = distance_m (f32, the same value as the 16-byte record's)
+#:   word1 = fp16(driver_age) | hours << 16 | weather << 26 | traffic << 29
+#: ``hours`` (10 bits) is the pickup's wall-clock hour counted from 00:00 of the Monday that starts
+#: the batch's earliest pickup week (the per-batch base, kept by the host for the response).  The
+#: kernel derives weekday = (hours / 24) % 7 and hour = hours % 24 itself — hour is the finest unit
+#: any R16 feature reads, so the record is lossless for the model.  Category code 7 = unknown
+#: (all-zero one-hot).  :func:`records_to_wire8` returns None when a batch cannot be represented
+#: exactly (an age that fp16 does not hold, or pickups spanning more than 1024 hours from the
+#: base); callers then send the 16-byte records.
 RECORD8_DTYPE = np.dtype([("distance_m", "<f4"), ("packed", "<u4")])
 assert RECORD8_DTYPE.itemsize == 8
-
+WIRE8_HOURS = 1 << 10
+#: 2020-01-01 (the records' wall-clock epoch) is a Wednesday: day d has weekday (d + 2) % 7
 #: 6-byte bulk wire record (10 B per prediction with the f32 output): one little-endian 48-bit word
 #: stored as 3 x u16 — bits 0-26 distance in eighths of a metre (to 16,777 km; exact in f32 below
 #: 2,097 km), 27-33 driver age in whole years (0-127), 34-36 weekday, 37-41 hour, 42-44 weather,
@@ -104,21 +113,43 @@ def pack_records(rows: Sequence[Dict[str, Any]]) -> np.ndarray:
     return out
 
 
-def records_to_compact(rec: np.ndarray) -> np.ndarray:
-    """16-byte records -> 8-byte compact records (weekday/hour resolved on the host)."""
+def wire8_base_hour(wallclock_s: np.ndarray) -> int:
+    """Per-batch base: 00:00 of the Monday on or before the earliest pickup (hours since epoch)."""
+    h0 = int(np.floor_divide(np.asarray(wallclock_s, dtype=np.int64).min(), 3600))
+    d0 = h0 // 24
+    monday = d0 - (d0 + KERNEL_EPOCH_WEEKDAY) % 7
+    return monday * 24
+
+
+def records_to_wire8(rec: np.ndarray) -> Optional[np.ndarray]:
+    """16-byte records -> 8-byte wire records, or None if the batch does not fit exactly."""
     rec = np.asarray(rec, dtype=RECORD_DTYPE)
     out = np.empty(rec.shape[0], dtype=RECORD8_DTYPE)
-    out["distance_m"] = rec["distance_m"]
-    secs = rec["wallclock_s"].astype(np.int64)
-    days = np.floor_divide(secs, 86400)
-    wd = ((days + KERNEL_EPOCH_WEEKDAY) % 7).astype(np.uint32)
-    hr = ((secs - days * 86400) // 3600).astype(np.uint32)
-    age = rec["driver_age"].astype(np.float16).view(np.uint16).astype(np.uint32)
+    if rec.shape[0] == 0:
+        return out
+    age = rec["driver_age"]
+    age16 = age.astype(np.float16)
+    if not np.array_equal(age16.astype(np.float32).view(np.uint32), age.view(np.uint32)):
+        return None
+    hrs = np.floor_divide(rec["wallclock_s"].astype(np.int64), 3600) - wire8_base_hour(rec["wallclock_s"])
+    if hrs.max() >= WIRE8_HOURS:
+        return None
     w = rec["weather"].astype(np.uint32)
     t = rec["traffic"].astype(np.uint32)
     w = np.where(w > 3, 7, w)
     t = np.where(t > 3, 7, t)
-    out["packed"] = age | (wd << 16) | (hr << 19) | (w << 24) | (t << 27)
+    out["distance_m"] = rec["distance_m"]
+    out["packed"] = (age16.view(np.uint16).astype(np.uint32) | (hrs.astype(np.uint32) << 16)
+                     | (w << 26) | (t << 29))
+    return out
+
+
+def records_to_compact(rec: np.ndarray) -> np.ndarray:
+    """:func:`records_to_wire8`, raising if the batch is not exactly representable."""
+    out = records_to_wire8(rec)
+    if out is None:
+        raise ValueError("batch not representable as 8-byte wire records (age not fp16-exact or "
+                         "pickups span >= 1024 hours)")
     return out
 
 
@@ -160,17 +191,18 @@ def compact6_to_features(rec6: np.ndarray) -> np.ndarray:
 
 
 def compact_to_features(rec8: np.ndarray) -> np.ndarray:
-    """CPU reference of the K1 featurize kernel for compact records."""
+    """CPU reference of the K1 featurize kernel for 8-byte wire records."""
     rec8 = np.asarray(rec8, dtype=RECORD8_DTYPE)
     pk = rec8["packed"].astype(np.uint32)
     x = np.zeros((rec8.shape[0], NUM_FEATURES), dtype=np.float32)
-    w = (pk >> 24) & 7
-    t = (pk >> 27) & 7
+    w = (pk >> 26) & 7
+    t = (pk >> 29) & 7
     for i in range(4):
         x[:, i] = (w == i)
         x[:, 4 + i] = (t == i)
-    x[:, 8] = (pk >> 16) & 7
-    x[:, 9] = (pk >> 19) & 31
+    hrs = (pk >> 16) & (WIRE8_HOURS - 1)
+    x[:, 8] = (hrs // 24) % 7
+    x[:, 9] = hrs % 24
     x[:, 10] = rec8["distance_m"].astype(np.float32) / np.float32(1000.0)
     x[:, 11] = (pk & 0xFFFF).astype(np.uint16).view(np.float16).astype(np.float32)
     return x

@@ -197,15 +197,16 @@ def featurize6_torch(rec6: torch.Tensor) -> torch.Tensor:
 
 
 def featurize8_torch(rec8_i32: torch.Tensor) -> torch.Tensor:
-    """PyTorch reference of K1 for compact records: int32 [B,2] -> [B,12] fp32."""
+    """PyTorch reference of K1 for 8-byte wire records: int32 [B,2] -> [B,12] fp32."""
     dist = rec8_i32[:, 0].view(torch.float32)
     pk = rec8_i32[:, 1].to(torch.int64) & 0xFFFFFFFF
     age = (pk & 0xFFFF).to(torch.int16).view(torch.float16).float()
-    w = (pk >> 24) & 7
-    t = (pk >> 27) & 7
+    w = (pk >> 26) & 7
+    t = (pk >> 29) & 7
+    hrs = (pk >> 16) & 1023
     ar = torch.arange(4, device=rec8_i32.device)
     return torch.cat([(w[:, None] == ar[None]).float(), (t[:, None] == ar[None]).float(),
-                      ((pk >> 16) & 7).float()[:, None], ((pk >> 19) & 31).float()[:, None],
+                      ((hrs // 24) % 7).float()[:, None], (hrs % 24).float()[:, None],
                       (dist / 1000.0)[:, None], age[:, None]], 1)
 
 

@@ -65,13 +65,26 @@ class DeviceComm:
             self.oneshot = True
 
     # ------------------------------------------------------------------ collectives
+    # The auto choice between one-shot and RCCL depends ONLY on what every rank agrees on (dtype,
+    # element count, world, the one-shot capacity) — never on a rank's local view offset or
+    # strides (round-2 ADVICE, comm.py:70): if ranks picked differently, one would enter the epoch
+    # protocol while another called RCCL and both would wait forever.  A locally misaligned or
+    # strided tensor is staged through an aligned contiguous copy instead, with the same result.
     def pick(self, t: torch.Tensor, algo: str = "auto") -> str:
         if algo != "auto":
             return algo
         if (self.oneshot and t.dtype == torch.float32 and t.numel() % 4 == 0
-                and t.numel() * 4 <= self.oneshot_bytes and t.data_ptr() % 16 == 0):
+                and t.numel() * 4 <= self.oneshot_bytes):
             return "oneshot"
         return "rccl"
+
+    def _oneshot_size_ok(self, t: torch.Tensor) -> bool:
+        nb = t.numel() * t.element_size()
+        return self.oneshot and nb % 16 == 0 and nb <= self.oneshot_bytes
+
+    @staticmethod
+    def _aligned(t: torch.Tensor) -> bool:
+        return t.is_contiguous() and t.data_ptr() % 16 == 0
 
     def all_reduce(self, t: torch.Tensor, algo: str = "auto") -> torch.Tensor:
         """In-place SUM on the current stream (no host sync; graph-capturable)."""
@@ -79,16 +92,16 @@ class DeviceComm:
             return t
         maybe_fail("rccl_timeout")
         a = self.pick(t, algo)
+        if a == "oneshot" and not self._aligned(t):
+            tmp = t.contiguous().clone()
+            self.C.comm_all_reduce(self.h, tmp, ALGOS[a])
+            t.copy_(tmp)
+            return t
         if a == "oneshot" or t.dtype == torch.float32:
             self.C.comm_all_reduce(self.h, t, ALGOS[a])
         else:
             self.C.comm_collective(self.h, 3, t, t, 0)
         return t
-
-    def _oneshot_fits(self, t: torch.Tensor) -> bool:
-        nb = t.numel() * t.element_size()
-        return (self.oneshot and t.is_contiguous() and nb % 16 == 0 and nb <= self.oneshot_bytes
-                and t.data_ptr() % 16 == 0)
 
     def all_gather(self, inp: torch.Tensor, out: torch.Tensor, algo: str = "auto") -> torch.Tensor:
         """``out`` = the W inputs concatenated in rank order, on the current stream.  "oneshot":
@@ -100,11 +113,15 @@ class DeviceComm:
             return out
         maybe_fail("rccl_timeout")
         if algo == "auto":
-            algo = "oneshot" if self._oneshot_fits(inp) and out.data_ptr() % 16 == 0 else "rccl"
+            algo = "oneshot" if self._oneshot_size_ok(inp) else "rccl"
+        src = inp if self._aligned(inp) else inp.contiguous().clone()
+        dst = out if self._aligned(out) else torch.empty(out.shape, dtype=out.dtype, device=out.device)
         if algo == "oneshot":
-            self.C.comm_oneshot(self.h, 0, inp, out, 0)
+            self.C.comm_oneshot(self.h, 0, src, dst, 0)
         else:
-            self.C.comm_collective(self.h, 0, inp, out, 0)
+            self.C.comm_collective(self.h, 0, src, dst, 0)
+        if dst is not out:
+            out.copy_(dst)
         return out
 
     def reduce_scatter(self, inp: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -115,11 +132,14 @@ class DeviceComm:
     def broadcast(self, t: torch.Tensor, root: int = 0, algo: str = "auto") -> torch.Tensor:
         if self.world > 1:
             if algo == "auto":
-                algo = "oneshot" if self._oneshot_fits(t) else "rccl"
+                algo = "oneshot" if self._oneshot_size_ok(t) else "rccl"
+            buf = t if self._aligned(t) else t.contiguous().clone()
             if algo == "oneshot":
-                self.C.comm_oneshot(self.h, 2, t, t, root)
+                self.C.comm_oneshot(self.h, 2, buf, buf, root)
             else:
-                self.C.comm_collective(self.h, 2, t, t, root)
+                self.C.comm_collective(self.h, 2, buf, buf, root)
+            if buf is not t:
+                t.copy_(buf)
         return t
 
     def ready(self) -> dict:

@@ -236,6 +236,7 @@ class BatchedAstar:
         # (the wave stage's heuristic cache is per query and reset after each search: nothing to drop)
         cost = np.asarray(cost, dtype=np.float32)
         self.cost.copy_(torch.from_numpy(self._edges(cost)))
+        self._csr = None          # the host fallback's CSR was built from the old costs
         self.v_max = float((self.g.length_m / np.maximum(cost.astype(np.float64), 1e-6)).max()) * 1.0001
         self.inv_vmax = 1.15 / self.v_max
         if self.lm is not None:

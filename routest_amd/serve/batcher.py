@@ -30,7 +30,7 @@ from typing import Callable, List, Optional, Sequence
 import numpy as np
 import torch
 
-from ..models.features import RECORD_DTYPE
+from ..models.features import RECORD8_DTYPE, RECORD_DTYPE, records_to_wire8
 from ..utils.faults import maybe_fail
 from ..utils.logging import get_logger
 from ..utils.metrics import REGISTRY
@@ -66,27 +66,48 @@ class GpuRunner:
         with torch.cuda.device(self.device):
             self.stream = torch.cuda.Stream(self.device)
             self.h_rec = torch.empty((batch_max, 4), dtype=torch.int32).pin_memory()
+            # the same rows as 8-byte wire records (features.py RECORD8) when a batch fits exactly:
+            # the zero-copy kernel then reads half the PCIe bytes
+            self.h_rec8 = (torch.empty((batch_max, 2), dtype=torch.int32).pin_memory()
+                           if self.zero_copy else None)
             self.h_out = torch.empty(batch_max, dtype=torch.float32).pin_memory()
             self.d_rec = None if self.zero_copy else torch.empty((batch_max, 4), dtype=torch.int32,
                                                                  device=self.device)
         self.h_rec_np = self.h_rec.numpy().view(np.uint8).reshape(batch_max, 16).view(RECORD_DTYPE).reshape(-1)
+        self.h_rec8_np = (self.h_rec8.numpy().view(np.uint8).reshape(batch_max, 8).view(RECORD8_DTYPE).reshape(-1)
+                          if self.h_rec8 is not None else None)
+        self.wire8_launches = 0
         self.h_out_np = self.h_out.numpy()
         self.lock = threading.Lock()
         idx = self.device.index if self.device.index is not None else 0
         self._dev_key = idx
         # small batches go to the resident scorer kernel (no dispatch, no stream sync per request)
         self.resident = None
+        self._resident_ok = self.zero_copy and os.environ.get("ROUTEST_RESIDENT", "1") != "0"
         with _DEV_GUARD:
             self.dev_lock = _DEV_LOCKS.setdefault(idx, threading.Lock())
-            own = (self.zero_copy and os.environ.get("ROUTEST_RESIDENT", "1") != "0"
-                   and getattr(_DEV_RESIDENT.get(idx), "h", None) is None)
-            if own:
-                try:
-                    from ..ops.eta_mlp import ResidentScorer
-                    self.resident = ResidentScorer(kernel, cap=min(1024, batch_max))
-                    _DEV_RESIDENT[idx] = self.resident
-                except Exception as e:  # pragma: no cover - falls back to launches
-                    log.warning("resident scorer unavailable on %s: %r", self.device, e)
+        self._try_own_resident()
+
+    def _try_own_resident(self) -> None:
+        """Take the device's resident scorer if no live runner owns it.  Called at construction
+        and again (cheaply) before small batches, so a runner built while another one owned the
+        scorer — e.g. a reload that builds the new service before closing the old — takes over
+        once the owner closes (round-2 ADVICE, batcher.py:541) instead of launching forever."""
+        if not self._resident_ok or self.resident is not None:
+            return
+        with _DEV_GUARD:
+            if getattr(_DEV_RESIDENT.get(self._dev_key), "h", None) is not None:
+                return
+            try:
+                from ..ops.eta_mlp import ResidentScorer
+                self.resident = ResidentScorer(self.kernel, cap=min(1024, self.batch_max))
+                _DEV_RESIDENT[self._dev_key] = self.resident
+            except Exception as e:  # pragma: no cover - falls back to launches
+                log.warning("resident scorer unavailable on %s: %r", self.device, e)
+                self._resident_ok = False
+
+    def owns_resident(self) -> bool:
+        return self.resident is not None and getattr(self.resident, "h", None) is not None
 
     def __repr__(self) -> str:
         return f"GpuRunner({self.device})"
@@ -105,6 +126,8 @@ class GpuRunner:
         maybe_fail("gpu_fail")
         n = rec.shape[0]
         out = np.empty(n, dtype=np.float32)
+        if self.resident is None and self._resident_ok and n <= 1024:
+            self._try_own_resident()
         if self.resident is not None and n <= self.resident.cap:
             with self.lock, self.dev_lock:
                 r = self.resident.score(torch.from_numpy(np.ascontiguousarray(rec).view(np.int32).reshape(n, 4)),
@@ -114,7 +137,12 @@ class GpuRunner:
         with self.lock, torch.cuda.device(self.device), torch.cuda.stream(self.stream):
             for s in range(0, n, self.batch_max):
                 m = min(self.batch_max, n - s)
-                self.h_rec_np[:m] = rec[s:s + m]
+                r8 = records_to_wire8(rec[s:s + m]) if self.h_rec8 is not None and m >= 64 else None
+                if r8 is not None:
+                    self.h_rec8_np[:m] = r8
+                    self.wire8_launches += 1
+                else:
+                    self.h_rec_np[:m] = rec[s:s + m]
                 # the device lock is held until this launch has COMPLETED: released right after
                 # the enqueue, another runner on the device could relaunch the resident scorer
                 # while this kernel still waits for the CU / hardware queue the scorer takes —
@@ -124,7 +152,8 @@ class GpuRunner:
                     if res is not None:
                         res.park()        # keep a hardware queue it may share free for this launch
                     if self.zero_copy:
-                        self.kernel.forward_hostio(self.h_rec[:m], self.h_out[:m])
+                        self.kernel.forward_hostio(self.h_rec8[:m] if r8 is not None else self.h_rec[:m],
+                                                   self.h_out[:m])
                     else:
                         self.d_rec[:m].copy_(self.h_rec[:m], non_blocking=True)
                         y = self.kernel(self.d_rec[:m])

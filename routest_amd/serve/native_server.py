@@ -50,11 +50,12 @@ class NativePredictServer:
     def stats(self) -> Dict[str, int]:
         if self.h is None:
             return {}
-        r, p, l, e, res, fb = self.C.native_server_stats(self.h)
+        v = self.C.native_server_stats(self.h)
         # resident: rounds scored by the persistent kernel (csrc/persistent_serve.hip);
-        # fallbacks: rounds it did not answer in time, re-scored by a normal launch
-        return {"requests": r, "predictions": p, "launches": l, "errors": e, "resident": res,
-                "fallbacks": fb}
+        # fallbacks: rounds it did not answer in time, re-scored by a normal launch;
+        # wire8: launches that read 8-byte wire records (features.py RECORD8) instead of 16-byte
+        names = ("requests", "predictions", "launches", "errors", "resident", "fallbacks", "wire8")
+        return dict(zip(names, v))
 
     def close(self) -> None:
         if self.h is not None:

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from ..data.synth import read_trips_csv, synth_records, synth_trips
-from ..models.checkpoint import load_checkpoint, load_training_state, save_checkpoint
+from ..models.checkpoint import checkpoint_exists, load_checkpoint, load_training_state, save_checkpoint
 from ..models.features import features_to_records, records_to_features
 from ..models.mlp3 import EtaMLP, LinearETA
 from ..ops.eta_mlp import featurize_torch, records_to_tensor
@@ -190,7 +190,7 @@ class Trainer:
     def _maybe_resume(self) -> bool:
         self._opt_state = None
         d = self.cfg.ckpt_dir
-        if not d or not os.path.exists(os.path.join(d, "config.json")):
+        if not checkpoint_exists(d):
             return False
         model, _ = load_checkpoint(d)
         opt, ts = load_training_state(d)

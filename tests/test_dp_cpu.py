@@ -92,7 +92,8 @@ def test_dp_training_ranks_in_sync_and_resume():
         assert torch.equal(r0["p"], r1["p"])
         h = r0["res"]["history"]
         assert h[-1]["mse_norm"] < 1.0
-        assert os.path.exists(os.path.join(ck, "optimizer.safetensors"))
+        from routest_amd.models.checkpoint import resolve_checkpoint
+        assert os.path.exists(os.path.join(resolve_checkpoint(ck), "optimizer.safetensors"))
         # resume: continues from step 30 for 10 more steps
         mp.spawn(_train_worker, args=(world, _free_port(), d, 10, ck), nprocs=world, join=True)
         r0b = torch.load(os.path.join(d, "r0.pt"), weights_only=False)

@@ -40,8 +40,9 @@ def _run(backend: str, extra_env=None):
         assert "exits hard at step 25" in r.stderr, r.stderr[-3000:]
         res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
         assert res["start_step"] == 20 and res["end_step"] == 40 and res["world"] == 2
-        with open(os.path.join(ck, "trainer_state.json")) as f:
-            assert json.load(f)["step"] == 40
+        from routest_amd.models.checkpoint import load_training_state
+        _, ts = load_training_state(ck)
+        assert ts["step"] == 40
 
 
 def test_torchrun_max_restarts_resumes_after_rank_crash():

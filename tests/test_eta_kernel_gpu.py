@@ -130,21 +130,26 @@ def test_mlp3_forward_experimental_variants_match(variant):
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 16, 17])
+@pytest.mark.parametrize("variant", [0, 1, 3, 16, 17, 20, 23])
 def test_mlp3_forward_compact_records(variant):
-    from routest_amd.models.features import compact_to_features, records_to_compact
+    """8-byte wire records (the serving format): the kernel featurises weekday/hour from the hour
+    count itself and its output is BIT-identical to the same kernel on the 16-byte records, on HBM
+    and on pinned host records (zero-copy)."""
+    from routest_amd.models.features import compact_to_features, records_to_wire8
     from routest_amd.ops.eta_mlp import records8_to_tensor
     m = _model(256, 4)
     k = EtaMlpKernel(m, torch.device("cuda:0"), variant=variant)
     rec, _ = synth_records(70_001, 22)
     rec["weather"][:100] = 255
-    rec["driver_age"][100:200] = 33.7
-    r8 = records_to_compact(rec)
+    rec["driver_age"][100:200] = 33.5
+    r8 = records_to_wire8(rec)
+    assert r8 is not None
     x8 = compact_to_features(r8)
     x16 = records_to_features(rec)
-    assert np.array_equal(x8[:, :11], x16[:, :11])
-    assert np.allclose(x8[:, 11], x16[:, 11], atol=0.02)
+    assert np.array_equal(x8, x16)
     got = k(records8_to_tensor(r8).cuda()).cpu()
+    g16 = k(records_to_tensor(rec).cuda()).cpu()
+    assert torch.equal(got, g16)
     ref = m(torch.from_numpy(x8)).detach()
     torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
     host = records8_to_tensor(r8).pin_memory()

@@ -20,5 +20,6 @@ def test_train_notebook_runs(tmp_path, monkeypatch):
         if cell["cell_type"] == "code":
             src = "".join(cell["source"]).replace("os.path.abspath('..')", repr(root))
             exec(compile(src, "train_eta.ipynb", "exec"), g)
-    assert (nbdir / "out" / "mlp3_ckpt" / "config.json").exists()
+    from routest_amd.models.checkpoint import checkpoint_exists
+    assert checkpoint_exists(str(nbdir / "out" / "mlp3_ckpt"))
     assert (nbdir / "out" / "train_log.jsonl").exists()
