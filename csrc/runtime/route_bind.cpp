@@ -1,0 +1,202 @@
+// routest_amd._rt bindings of the native route assembler (csrc/runtime/route_core.h).
+//
+//  * haversine_m / path_length_m / NodeGrid: the libm-dependent values of the Python providers
+//    (routing/providers.py, routing/graph.py, data/graph.py) come from these, so the Python path
+//    and the native front end (csrc/native_server.hip) produce identical bits.
+//  * route_optimize_cpu: the whole haversine-provider request on the CPU in C++ (parse, matrix,
+//    R21 greedy, directions, assembly) -> (status, body) or None (fallback to Python) — the CPU
+//    reference the GPU service is tested against, and a fast path for GPU-less deployments.
+//  * route_assemble_graph: graph-provider assembly from given trips + searched legs (tests).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <map>
+#include <memory>
+
+#include "route_core.h"
+
+namespace py = pybind11;
+
+namespace {
+
+using rtr::Value;
+
+double py_haversine(double lat1, double lon1, double lat2, double lon2) {
+  return rtr::haversine_m(lat1, lon1, lat2, lon2);
+}
+
+double py_path_length(py::array_t<double, py::array::c_style | py::array::forcecast> lat,
+                      py::array_t<double, py::array::c_style | py::array::forcecast> lon,
+                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> path) {
+  const int64_t n = lat.shape(0);
+  const int32_t* p = path.data();
+  for (py::ssize_t i = 0; i < path.shape(0); ++i)
+    if (p[i] < 0 || p[i] >= n) throw std::out_of_range("path node out of range");
+  return rtr::path_length_m(lat.data(), lon.data(), p, (size_t)path.shape(0));
+}
+
+py::array_t<double> py_haversine_matrix(py::array_t<double, py::array::c_style | py::array::forcecast> lat,
+                                        py::array_t<double, py::array::c_style | py::array::forcecast> lon,
+                                        double circuity) {
+  const py::ssize_t n = lat.shape(0);
+  py::array_t<double> D({n, n});
+  double* d = D.mutable_data();
+  const double* la = lat.data();
+  const double* lo = lon.data();
+  for (py::ssize_t i = 0; i < n; ++i)
+    for (py::ssize_t j = 0; j < n; ++j)
+      d[i * n + j] = i == j ? 0.0 : rtr::haversine_m(la[i], lo[i], la[j], lo[j]) * circuity;
+  return D;
+}
+
+class PyNodeGrid {
+ public:
+  PyNodeGrid(py::array_t<double, py::array::c_style | py::array::forcecast> lat,
+             py::array_t<double, py::array::c_style | py::array::forcecast> lon, double c)
+      : c_(c) {
+    if (lat.shape(0) != lon.shape(0) || lat.shape(0) == 0) throw std::invalid_argument("lat/lon mismatch");
+    g_.build(lat.data(), lon.data(), (size_t)lat.shape(0), c);
+  }
+  py::array_t<int32_t> nearest(py::array_t<double, py::array::c_style | py::array::forcecast> lats,
+                               py::array_t<double, py::array::c_style | py::array::forcecast> lons) const {
+    const py::ssize_t n = lats.shape(0);
+    py::array_t<int32_t> out(n);
+    int32_t* o = out.mutable_data();
+    const double* la = lats.data();
+    const double* lo = lons.data();
+    {
+      py::gil_scoped_release nogil;
+      for (py::ssize_t i = 0; i < n; ++i) o[i] = g_.nearest(la[i], lo[i], c_);
+    }
+    return out;
+  }
+
+ private:
+  rtr::NodeGrid g_;
+  double c_;
+};
+
+py::bytes to_bytes(const std::string& s) { return py::bytes(s); }
+
+// Finish an assembled request as the FastAPI handler answers it (no ETA, no persistence).
+std::pair<int, std::string> finish_plain(const rtr::Assembled& a, bool request_route_compat, bool is_request_route) {
+  if (!a.error.empty()) {
+    const int st = (is_request_route && request_route_compat) ? 200 : 400;
+    return {st, rtr::error_body(a.error)};
+  }
+  return {200, a.body + "}}"};
+}
+
+py::object route_optimize_cpu(py::bytes body, bool json_ok, const std::string& engine, double circuity,
+                              double step_m, bool is_request_route, bool compat200) {
+  const std::string b = body;
+  Value root;
+  bool parsed = false;
+  if (json_ok && !b.empty()) {
+    try {
+      root = rtj::Parser(b.data(), b.size()).parse();
+      parsed = true;
+    } catch (const std::exception&) {
+    }
+  }
+  if (is_request_route && (!json_ok || (!parsed && !b.empty()))) return py::none();   // 415 / 400: Python
+  Value empty;
+  empty.kind = Value::Obj;
+  const Value* rootp = parsed ? &root : (is_request_route ? nullptr : &empty);
+  if (!is_request_route && parsed && root.kind != Value::Obj) rootp = &empty;   // silent: non-dict -> {}
+  rtr::RouteReq r = rtr::parse_route_request(rootp);
+  if (r.fallback) return py::none();
+  rtr::Plan plan;
+  if (r.error.empty() && r.dst.size() > 1) {
+    const int n1 = (int)r.dst.size() + 1;
+    std::vector<double> lat(n1), lon(n1), dem(n1, 0.0), D((size_t)n1 * n1, 0.0);
+    lat[0] = r.src.lat;
+    lon[0] = r.src.lon;
+    for (int i = 1; i < n1; ++i) {
+      lat[i] = r.dst[i - 1].lat;
+      lon[i] = r.dst[i - 1].lon;
+      dem[i] = r.dst[i - 1].demand;
+    }
+    for (int i = 0; i < n1; ++i)
+      for (int j = 0; j < n1; ++j)
+        D[(size_t)i * n1 + j] = i == j ? 0.0 : rtr::haversine_m(lat[i], lon[i], lat[j], lon[j]) * circuity;
+    plan.infeasible = !rtr::greedy_trips(D, n1, dem, r.cap, r.maxd, plan.trips, plan.infeasible_stops);
+  }
+  std::vector<std::vector<std::pair<double, double>>> calls;
+  rtr::directions_calls(r, plan, calls);
+  std::vector<rtr::Dir> dirs(calls.size());
+  for (size_t k = 0; k < calls.size(); ++k)
+    rtr::haversine_directions(calls[k], r.profile, circuity, step_m, dirs[k]);
+  rtr::Assembled a;
+  if (!rtr::assemble(r, plan, dirs, engine, a)) return py::none();
+  auto res = finish_plain(a, compat200, is_request_route);
+  return py::make_tuple(res.first, to_bytes(res.second));
+}
+
+// Graph-provider assembly with given trips and searched legs: `trips` per request as index lists
+// (None for point-to-point), `legs` {(s, t): (seconds, [nodes])} (missing / empty = not found).
+py::object route_assemble_graph(py::bytes body, const std::string& engine,
+                                py::array_t<double, py::array::c_style | py::array::forcecast> glat,
+                                py::array_t<double, py::array::c_style | py::array::forcecast> glon,
+                                py::array_t<int32_t, py::array::c_style | py::array::forcecast> nodes_of_calls,
+                                py::object trips_obj, py::dict legs_obj) {
+  const std::string b = body;
+  Value root = rtj::Parser(b.data(), b.size()).parse();
+  rtr::RouteReq r = rtr::parse_route_request(&root);
+  if (r.fallback) return py::none();
+  rtr::Plan plan;
+  if (!trips_obj.is_none()) plan.trips = trips_obj.cast<std::vector<std::vector<int>>>();
+  std::vector<std::vector<std::pair<double, double>>> calls;
+  rtr::directions_calls(r, plan, calls);
+  // legs table
+  std::map<std::pair<int, int>, std::pair<rtr::Leg, std::vector<int32_t>>> table;
+  for (auto kv : legs_obj) {
+    auto key = kv.first.cast<std::pair<int, int>>();
+    auto val = kv.second.cast<std::pair<double, std::vector<int32_t>>>();
+    auto& e = table[key];
+    e.second = val.second;
+    e.first.sec = (float)val.first;
+    e.first.len = (int)e.second.size();
+    e.first.path = e.second.data();
+  }
+  const int32_t* nodes = nodes_of_calls.data();
+  std::vector<rtr::Dir> dirs(calls.size());
+  size_t off = 0;
+  rtr::Leg missing;
+  for (size_t k = 0; k < calls.size(); ++k) {
+    std::vector<const rtr::Leg*> legs;
+    for (size_t i = 0; i + 1 < calls[k].size(); ++i) {
+      auto it = table.find({nodes[off + i], nodes[off + i + 1]});
+      legs.push_back(it == table.end() ? &missing : &it->second.first);
+    }
+    const std::string e = rtr::graph_directions(calls[k], nodes + off, legs, r.profile, glat.data(), glon.data(), dirs[k]);
+    off += calls[k].size();
+    if (!e.empty()) {
+      r.error = e;
+      break;
+    }
+  }
+  rtr::Assembled a;
+  if (!rtr::assemble(r, plan, dirs, engine, a)) return py::none();
+  auto res = finish_plain(a, true, false);
+  return py::make_tuple(res.first, to_bytes(res.second));
+}
+
+}  // namespace
+
+void bind_route(py::module& m) {
+  m.def("haversine_m", &py_haversine);
+  m.def("path_length_m", &py_path_length);
+  m.def("haversine_matrix", &py_haversine_matrix);
+  py::class_<PyNodeGrid>(m, "NodeGrid")
+      .def(py::init<py::array_t<double, py::array::c_style | py::array::forcecast>,
+                    py::array_t<double, py::array::c_style | py::array::forcecast>, double>())
+      .def("nearest", &PyNodeGrid::nearest);
+  m.def("route_optimize_cpu", &route_optimize_cpu, py::arg("body"), py::arg("json_ok") = true,
+        py::arg("engine") = "backend:mi355x", py::arg("circuity") = 1.3, py::arg("step_m") = 150.0,
+        py::arg("is_request_route") = false, py::arg("compat200") = true);
+  m.def("route_assemble_graph", &route_assemble_graph);
+  m.def("py_round", &rtr::py_round);
+  m.def("bearing_word", [](double a, double b, double c, double d) { return std::string(rtr::bearing_word(a, b, c, d)); });
+}

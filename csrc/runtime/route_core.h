@@ -1,0 +1,789 @@
+// Native route assembly (host C++, no GPU): the reference's optimize_route response built without
+// Python, byte-identical to the FastAPI handler's JSONResponse (routest_amd/routing/optimizer.py,
+// providers.py, graph.py; reference RO/Flaskr/utils.py:10-201, RO/Flaskr/routes.py:29-50,89-127).
+//
+//  * Python-exact numerics: builtin round(x, n) (correctly rounded, half-even on exact ties),
+//    numpy.round(x, 6) (rint(x * 1e6) / 1e6), float // and %, repr(float) (rt_core.h), and the
+//    transcendental helpers (haversine, path length) that the Python providers call through
+//    routest_amd._rt so both paths share one implementation of every libm-dependent value.
+//  * A JSON writer with json.dumps(ensure_ascii=False, separators=(",", ":"), allow_nan=False)
+//    semantics, so request fields echoed back (source, destinations, driver_name) keep Python's
+//    int/float/str rendering and key order.
+//  * RouteReq: the request fields with the reference's defaults and coercions.  Anything whose
+//    Python semantics are not reproduced exactly here (a string where a number is expected, a
+//    non-dict driver_details, ...) is marked `fallback` and the caller hands the request to the
+//    Python app instead (csrc/native_server.hip proxies it), which owns those error semantics.
+//  * Feature assembly for the haversine provider (densified straight lines) and the road-graph
+//    provider (node paths from the batched A*), multi-trip concatenation, annotation.
+//
+// Compile with -ffp-contract=off (tools/build_ext.py): every expression must round like Python's.
+#pragma once
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "json_lite.h"
+#include "rt_core.h"
+
+namespace rtr {
+
+using rtj::Value;
+
+constexpr double EARTH_R = 6371000.0;
+constexpr double PY_PI = 3.141592653589793238462643383279502884;
+
+// ------------------------------------------------------------------ Python-exact numerics
+// builtin round(x, nd): the correctly rounded decimal string, parsed back (CPython double_round).
+inline double py_round(double x, int nd) {
+  if (!std::isfinite(x)) return x;
+  char b[64];
+  std::snprintf(b, sizeof b, "%.*f", nd, x);
+  return std::strtod(b, nullptr);
+}
+// numpy.round(x, 6) on float64: multiply, rint (half-even), true_divide
+inline double np_round6(double x) { return std::nearbyint(x * 1e6) / 1e6; }
+
+inline double py_mod(double vx, double wx) {
+  double mod = std::fmod(vx, wx);
+  if (mod != 0.0) {
+    if ((wx < 0) != (mod < 0)) mod += wx;
+  } else {
+    mod = std::copysign(0.0, wx);
+  }
+  return mod;
+}
+inline double py_floordiv(double vx, double wx) {
+  double mod = std::fmod(vx, wx);
+  double div = (vx - mod) / wx;
+  if (mod != 0.0) {
+    if ((wx < 0) != (mod < 0)) div -= 1.0;
+  }
+  double fd;
+  if (div != 0.0) {
+    fd = std::floor(div);
+    if (div - fd > 0.5) fd += 1.0;
+  } else {
+    fd = std::copysign(0.0, vx / wx);
+  }
+  return fd;
+}
+
+// numpy haversine_m (routing/providers.py) for scalars; the Python providers call this very
+// function through routest_amd._rt, so both paths produce the same bits.
+inline double haversine_m(double lat1, double lon1, double lat2, double lon2) {
+  const double k = PY_PI / 180.0;
+  const double p1 = lat1 * k, p2 = lat2 * k;
+  const double dphi = p2 - p1;
+  const double dl = lon2 * k - lon1 * k;
+  const double s1 = std::sin(dphi / 2), s2 = std::sin(dl / 2);
+  double a = s1 * s1 + std::cos(p1) * std::cos(p2) * (s2 * s2);
+  a = a < 0.0 ? 0.0 : (a > 1.0 ? 1.0 : a);
+  return (2 * EARTH_R) * std::asin(std::sqrt(a));
+}
+
+// sum over consecutive nodes of the haversine length (sequential order), graph.py feature_from_legs
+inline double path_length_m(const double* lat, const double* lon, const int32_t* p, size_t n) {
+  double s = 0.0;
+  for (size_t i = 0; i + 1 < n; ++i) s += haversine_m(lat[p[i]], lon[p[i]], lat[p[i + 1]], lon[p[i + 1]]);
+  return s;
+}
+
+// providers.py _bearing_word (math.* == libm, like CPython's math module)
+inline const char* bearing_word(double lat1, double lon1, double lat2, double lon2) {
+  static const char* const W[8] = {"north", "northeast", "east", "southeast", "south", "southwest",
+                                   "west", "northwest"};
+  const double d2r = PY_PI / 180.0, r2d = 180.0 / PY_PI;
+  const double y = std::sin((lon2 - lon1) * d2r) * std::cos(lat2 * d2r);
+  const double x = std::cos(lat1 * d2r) * std::sin(lat2 * d2r) -
+                   std::sin(lat1 * d2r) * std::cos(lat2 * d2r) * std::cos((lon2 - lon1) * d2r);
+  const double b = py_mod(std::atan2(y, x) * r2d + 360.0, 360.0);
+  long long i = (long long)py_floordiv(b + 22.5, 45.0);
+  i %= 8;
+  if (i < 0) i += 8;
+  return W[i];
+}
+
+// ------------------------------------------------------------------ JSON writer (json.dumps)
+inline void put_int(std::string& o, long long v) {
+  char b[24];
+  const auto r = std::to_chars(b, b + sizeof b, v);
+  o.append(b, r.ptr);
+}
+// repr of a float that is numpy.round(x, 6) output: the decimal itself (shortest round-trip), laid
+// out like repr; values below 1e-4 in magnitude take repr's exponent form via append_pyfloat
+inline void put_coord(std::string& o, double v) {
+  const double a = std::fabs(v);
+  if (!(a >= 1e-4 && a < 1e15)) { rtc::append_pyfloat(o, v); return; }
+  long long k = (long long)std::nearbyint(v * 1e6);
+  if ((double)k / 1e6 != v) { rtc::append_pyfloat(o, v); return; }   // not a 6-decimal value
+  if (k < 0) { o += '-'; k = -k; }
+  put_int(o, k / 1000000);
+  long long f = k % 1000000;
+  o += '.';
+  if (f == 0) { o += '0'; return; }
+  char d[6];
+  for (int i = 5; i >= 0; --i) { d[i] = (char)('0' + f % 10); f /= 10; }
+  int n = 6;
+  while (n > 1 && d[n - 1] == '0') --n;
+  o.append(d, n);
+}
+inline void put_float(std::string& o, double v) { rtc::append_pyfloat(o, v); }
+
+// json.dumps(str, ensure_ascii=False)
+inline void put_str(std::string& o, const std::string& s) {
+  o += '"';
+  for (unsigned char c : s) {
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\n': o += "\\n"; break;
+      case '\r': o += "\\r"; break;
+      case '\t': o += "\\t"; break;
+      case '\b': o += "\\b"; break;
+      case '\f': o += "\\f"; break;
+      default:
+        if (c < 0x20) {
+          char b[8];
+          std::snprintf(b, sizeof b, "\\u%04x", c);
+          o += b;
+        } else {
+          o += (char)c;
+        }
+    }
+  }
+  o += '"';
+}
+
+// A parsed JSON value re-serialised like json.dumps of its Python object.  Returns false where the
+// Python rendering is not reproduced (NaN/inf: allow_nan=False raises; an integer token beyond
+// the double's exact range is kept from its token text).
+inline bool put_value(std::string& o, const Value& v) {
+  switch (v.kind) {
+    case Value::Null: o += "null"; return true;
+    case Value::Bool: o += v.b ? "true" : "false"; return true;
+    case Value::Str: put_str(o, v.str); return true;
+    case Value::Num:
+      if (!std::isfinite(v.num)) return false;
+      if (v.is_int) {
+        if (std::fabs(v.num) < 9.0e15) { put_int(o, (long long)v.num); return true; }
+        return false;
+      }
+      put_float(o, v.num);
+      return true;
+    case Value::Arr: {
+      o += '[';
+      for (size_t i = 0; i < v.arr.size(); ++i) {
+        if (i) o += ',';
+        if (!put_value(o, v.arr[i])) return false;
+      }
+      o += ']';
+      return true;
+    }
+    case Value::Obj: {
+      o += '{';
+      for (size_t i = 0; i < v.obj.size(); ++i) {
+        if (i) o += ',';
+        put_str(o, v.obj[i].first);
+        o += ':';
+        if (!put_value(o, v.obj[i].second)) return false;
+      }
+      o += '}';
+      return true;
+    }
+  }
+  return false;
+}
+
+// ------------------------------------------------------------------ request model
+enum Profile { CAR = 0, HGV, CYCLING, ROADBIKE, FOOT };
+inline const char* profile_name(int p) {
+  static const char* const N[5] = {"driving-car", "driving-hgv", "cycling-regular", "cycling-road", "foot-walking"};
+  return N[p];
+}
+inline double profile_speed(int p) {   // providers.py PROFILE_SPEED_MPS
+  switch (p) {
+    case HGV: return 24 / 3.6;
+    case CYCLING: return 15 / 3.6;
+    case ROADBIKE: return 22 / 3.6;
+    case FOOT: return 5 / 3.6;
+    default: return 30 / 3.6;
+  }
+}
+
+inline bool is_num(const Value* v) { return v && v->kind == Value::Num; }
+
+struct Pt {
+  const Value* raw = nullptr;     // the point object (echoed back)
+  double lat = 0, lon = 0;        // float(p["lat"]), float(p["lon"])
+  double demand = 0;              // _float(p.get("payload", 0), 0.0)
+};
+
+struct RouteReq {
+  bool fallback = false;          // hand to the Python app
+  std::string error;              // optimize_route's {"error": ...} (set instead of a route)
+  const Value* root = nullptr;
+  Pt src;
+  std::vector<Pt> dst;
+  std::string vehicle_type = "car";
+  int profile = CAR;
+  const Value* driver_name = nullptr;      // driver.get("driver_name") (nullptr -> null)
+  double cap = 9e12, maxd = 9e12;          // multi-stop: _float semantics
+  // point-to-point feasibility: `payload > cap` (TypeError -> skipped) and _float(maximum_distance)
+  int p2p_cmp = 0;                         // 1: compare p2p_payload > p2p_cap, 0: skip
+  double p2p_payload = 0, p2p_cap = 0;
+  // use_ml_eta
+  bool use_ml_eta = false;
+  bool eta_ok = false;                     // driver_age coerced (else no ETA fields)
+  double eta_age = 30.0;
+  uint8_t eta_weather = 2, eta_traffic = 2;
+};
+
+// _float(v, default): float(v) for numbers, default for None / missing / list / dict; strings and
+// bools are converted by Python in ways not mirrored here -> fallback
+inline bool coerce_float(const Value* v, double dflt, double& out) {
+  if (!v || v->kind == Value::Null || v->kind == Value::Arr || v->kind == Value::Obj) { out = dflt; return true; }
+  if (v->kind == Value::Num) { out = v->num; return std::isfinite(v->num) || true; }
+  return false;
+}
+
+inline int code_of(const Value* v, const char* const names[4], const char* dflt) {
+  return rtc::code_of(v, names, dflt);
+}
+
+// Parse the optimize_route payload (silent: non-dict -> {}).  `body_ok` is false when the body
+// was not JSON (silent handlers treat it as {}).
+inline RouteReq parse_route_request(const Value* root) {
+  RouteReq r;
+  r.root = root;
+  const Value* dp = (root && root->kind == Value::Obj) ? root->get("destination_points") : nullptr;
+  if (!root || root->kind != Value::Obj || !dp || !dp->truthy()) {
+    r.error = "no destination points specified.";
+    return r;
+  }
+  const Value* drv = root->get("driver_details");
+  if (drv && drv->truthy() && drv->kind != Value::Obj) { r.fallback = true; return r; }
+  if (drv && !drv->truthy()) drv = nullptr;
+  // vehicle_type: (driver.get("vehicle_type") or "car"); str -> lower().strip()
+  const Value* vt = drv ? drv->get("vehicle_type") : nullptr;
+  if (vt && vt->truthy()) {
+    if (vt->kind == Value::Str) {
+      std::string s;
+      for (unsigned char c : vt->str) {
+        if (c >= 0x80 || (c < 0x20 && !(c == '\t' || c == '\n' || c == '\r' || c == 0x0b || c == 0x0c))) {
+          r.fallback = true;           // Unicode lower()/strip() not mirrored
+          return r;
+        }
+        s += (char)((c >= 'A' && c <= 'Z') ? c + 32 : c);
+      }
+      const char* ws = " \t\n\r\x0b\x0c";
+      const size_t b = s.find_first_not_of(ws);
+      s = b == std::string::npos ? std::string() : s.substr(b, s.find_last_not_of(ws) - b + 1);
+      r.vehicle_type = s;
+    } else {
+      r.vehicle_type = "car";
+    }
+  }
+  const std::string& v = r.vehicle_type;
+  r.profile = v == "truck" || v == "hgv" ? HGV : v == "bike" ? CYCLING : v == "roadbike" ? ROADBIKE
+            : v == "foot" ? FOOT : CAR;
+  const Value* src = root->get("source_point");
+  if (!src || src->kind != Value::Obj || !src->get("lat") || !src->get("lon")) {
+    r.error = "source_point with lat/lon is required.";
+    return r;
+  }
+  if (dp->kind != Value::Arr) { r.fallback = true; return r; }
+  auto take = [&](const Value* p, Pt& out) -> bool {
+    if (!p || p->kind != Value::Obj) return false;
+    const Value* la = p->get("lat");
+    const Value* lo = p->get("lon");
+    if (!is_num(la) || !is_num(lo) || !std::isfinite(la->num) || !std::isfinite(lo->num)) return false;
+    out.raw = p;
+    out.lat = la->num;
+    out.lon = lo->num;
+    return true;
+  };
+  if (!take(src, r.src)) { r.fallback = true; return r; }
+  r.dst.resize(dp->arr.size());
+  for (size_t i = 0; i < dp->arr.size(); ++i) {
+    if (!take(&dp->arr[i], r.dst[i])) { r.fallback = true; return r; }
+    double d;
+    if (!coerce_float(dp->arr[i].get("payload"), 0.0, d)) { r.fallback = true; return r; }
+    r.dst[i].demand = d;
+  }
+  r.driver_name = drv ? drv->get("driver_name") : nullptr;
+  if (r.dst.size() == 1) {
+    // point_to_point: payload = dest.get("payload", 0); cap = driver.get("vehicle_capacity", 999999)
+    const Value* pl = r.dst[0].raw->get("payload");
+    const Value* cp = drv ? drv->get("vehicle_capacity") : nullptr;
+    const double plv = pl ? (is_num(pl) ? pl->num : NAN) : 0.0;
+    const double cpv = cp ? (is_num(cp) ? cp->num : NAN) : 999999.0;
+    const bool pl_null = pl && pl->kind == Value::Null, cp_null = cp && cp->kind == Value::Null;
+    if ((pl && !is_num(pl) && !pl_null) || (cp && !is_num(cp) && !cp_null)) {
+      // str > str compares, list > list compares, bool is an int: not mirrored
+      if ((pl && (pl->kind == Value::Obj)) || (cp && (cp->kind == Value::Obj))) {
+        r.p2p_cmp = 0;                 // dict comparisons raise TypeError -> skipped
+      } else {
+        r.fallback = true;
+        return r;
+      }
+    } else if (pl_null || cp_null) {
+      r.p2p_cmp = 0;                   // None > x raises TypeError -> skipped
+    } else {
+      r.p2p_cmp = 1;
+      r.p2p_payload = plv;
+      r.p2p_cap = cpv;
+    }
+    if (!coerce_float(drv ? drv->get("maximum_distance") : nullptr, 9e12, r.maxd)) { r.fallback = true; return r; }
+  } else {
+    if (!coerce_float(drv ? drv->get("vehicle_capacity") : nullptr, 9e12, r.cap) ||
+        !coerce_float(drv ? drv->get("maximum_distance") : nullptr, 9e12, r.maxd)) {
+      r.fallback = true;
+      return r;
+    }
+  }
+  // use_ml_eta (routes.py:97-116): context must be a dict (or falsy), driver_age float-coercible
+  const Value* ue = root->get("use_ml_eta");
+  r.use_ml_eta = ue && ue->truthy();
+  if (r.use_ml_eta) {
+    const Value* ctx = root->get("context");
+    if (ctx && ctx->truthy() && ctx->kind != Value::Obj) { r.fallback = true; return r; }
+    if (ctx && !ctx->truthy()) ctx = nullptr;
+    r.eta_weather = (uint8_t)code_of(ctx ? ctx->get("weather") : nullptr, rtc::WEATHERS, "Sunny");
+    r.eta_traffic = (uint8_t)code_of(ctx ? ctx->get("traffic") : nullptr, rtc::TRAFFICS, "Low");
+    const Value* ag = drv ? drv->get("driver_age") : nullptr;
+    if (!ag) { r.eta_ok = true; r.eta_age = 30.0; }
+    else if (is_num(ag) && std::isfinite(ag->num)) { r.eta_ok = true; r.eta_age = ag->num == 0.0 ? 30.0 : ag->num; }
+    else if (ag->kind == Value::Null || ag->kind == Value::Arr || ag->kind == Value::Obj) { r.eta_ok = false; }
+    else { r.fallback = true; return r; }   // str / bool: float() semantics not mirrored
+  }
+  return r;
+}
+
+// ------------------------------------------------------------------ feature assembly
+// One provider directions() result (an ORS-shaped Feature), kept as the pieces the multi-trip
+// concatenation needs: coordinates, segments JSON, rounded summary.
+struct Dir {
+  std::vector<double> xy;     // lon, lat pairs (geometry coordinates)
+  std::vector<uint8_t> raw;   // per point: 1 = an input coordinate (repr), 0 = rounded node/interp
+  std::string segments;       // JSON elements (no brackets), comma-joined
+  std::vector<long long> way_points;
+  double dist = 0, dur = 0;   // round(tot, 1)
+};
+
+inline void put_xy(std::string& o, double x, double y, bool raw) {
+  o += '[';
+  if (raw) put_float(o, x); else put_coord(o, x);
+  o += ',';
+  if (raw) put_float(o, y); else put_coord(o, y);
+  o += ']';
+}
+
+inline void step_pair(std::string& seg, double d_r, double t_r, int k, int nlegs, const char* instr1,
+                      long long start, long long end) {
+  seg += "{\"distance\":"; put_float(seg, d_r);
+  seg += ",\"duration\":"; put_float(seg, t_r);
+  seg += ",\"steps\":[{\"distance\":"; put_float(seg, d_r);
+  seg += ",\"duration\":"; put_float(seg, t_r);
+  seg += ",\"type\":"; put_int(seg, k == 0 ? 11 : 1);
+  seg += ",\"instruction\":"; put_str(seg, instr1);
+  seg += ",\"name\":\"-\",\"way_points\":["; put_int(seg, start); seg += ','; put_int(seg, end);
+  seg += "]},{\"distance\":0.0,\"duration\":0.0,\"type\":10,\"instruction\":";
+  if (k == nlegs - 1) {
+    put_str(seg, "Arrive at your destination");
+  } else {
+    std::string w = "Arrive at waypoint ";
+    put_int(w, k + 1);
+    put_str(seg, w);
+  }
+  seg += ",\"name\":\"-\",\"way_points\":["; put_int(seg, end); seg += ','; put_int(seg, end);
+  seg += "]}]}";
+}
+
+// HaversineProvider.directions over waypoints (lon, lat) — providers.py
+inline void haversine_directions(const std::vector<std::pair<double, double>>& c, int profile,
+                                 double circuity, double step_m, Dir& out) {
+  const double speed = profile_speed(profile);
+  out.xy.assign({c[0].first, c[0].second});
+  out.raw.assign({1});
+  out.way_points.assign({0});
+  out.segments.clear();
+  double tot_d = 0.0;
+  const int nlegs = (int)c.size() - 1;
+  for (int k = 0; k < nlegs; ++k) {
+    const double lon1 = c[k].first, lat1 = c[k].second, lon2 = c[k + 1].first, lat2 = c[k + 1].second;
+    const double dist = haversine_m(lat1, lon1, lat2, lon2) * circuity;
+    const long long n = std::max(1LL, (long long)std::ceil(dist / step_m));
+    const long long start_wp = (long long)out.raw.size() - 1;
+    const double dlon = lon2 - lon1, dlat = lat2 - lat1;
+    for (long long i = 1; i <= n; ++i) {
+      const double t = (double)i / (double)n;
+      out.xy.push_back(np_round6(lon1 + dlon * t));
+      out.xy.push_back(np_round6(lat1 + dlat * t));
+      out.raw.push_back(0);
+    }
+    const long long end_wp = (long long)out.raw.size() - 1;
+    out.way_points.push_back(end_wp);
+    const double dur = dist / speed;
+    const double d_r = py_round(dist, 1), t_r = py_round(dur, 1);
+    if (k) out.segments += ',';
+    std::string instr = "Head ";
+    instr += bearing_word(lat1, lon1, lat2, lon2);
+    step_pair(out.segments, d_r, t_r, k, nlegs, instr.c_str(), start_wp, end_wp);
+    tot_d += dist;
+  }
+  out.dist = py_round(tot_d, 1);
+  out.dur = py_round(tot_d / speed, 1);
+}
+
+// One searched leg: seconds (the f32 A* cost) and the node path.
+struct Leg {
+  float sec = 0.f;
+  const int32_t* path = nullptr;
+  int len = 0;                    // 0 = not found
+};
+
+// GraphProvider.feature_from_legs — graph.py.  Returns "" or the ProviderError text.
+inline std::string graph_directions(const std::vector<std::pair<double, double>>& c, const int32_t* nodes,
+                                    const std::vector<const Leg*>& legs, int profile, const double* glat,
+                                    const double* glon, Dir& out) {
+  const double speed_scale = profile_speed(CAR) / profile_speed(profile);
+  out.xy.assign({c[0].first, c[0].second});
+  out.raw.assign({1});
+  out.way_points.assign({0});
+  out.segments.clear();
+  double tot_d = 0.0, tot_t = 0.0;
+  const int nlegs = (int)legs.size();
+  for (int k = 0; k < nlegs; ++k) {
+    const long long start = (long long)out.raw.size() - 1;
+    const Leg& L = *legs[k];
+    if (L.len <= 0) {
+      std::string e = "no road path found between waypoints ";
+      put_int(e, k); e += " and "; put_int(e, k + 1); e += " (graph nodes ";
+      put_int(e, nodes[k]); e += " -> "; put_int(e, nodes[k + 1]); e += ")";
+      return e;
+    }
+    const double dist = L.len > 1 ? path_length_m(glat, glon, L.path, (size_t)L.len) * 1.15 : 0.0;
+    for (int i = 0; i < L.len; ++i) {
+      out.xy.push_back(np_round6(glon[L.path[i]]));
+      out.xy.push_back(np_round6(glat[L.path[i]]));
+      out.raw.push_back(0);
+    }
+    out.xy.push_back(c[k + 1].first);
+    out.xy.push_back(c[k + 1].second);
+    out.raw.push_back(1);
+    const long long end = (long long)out.raw.size() - 1;
+    out.way_points.push_back(end);
+    const double dur = (double)L.sec * speed_scale;
+    if (k) out.segments += ',';
+    step_pair(out.segments, py_round(dist, 1), py_round(dur, 1), k, nlegs, "Follow the road network", start, end);
+    tot_d += dist;
+    tot_t += dur;
+  }
+  out.dist = py_round(tot_d, 1);
+  out.dur = py_round(tot_t, 1);
+  return "";
+}
+
+inline void put_bbox(std::string& o, const std::vector<double>& xy) {
+  double mnx = xy[0], mny = xy[1], mxx = xy[0], mxy = xy[1];
+  for (size_t i = 2; i + 1 < xy.size(); i += 2) {   // Python min()/max(): first extreme wins
+    if (xy[i] < mnx) mnx = xy[i];
+    if (xy[i] > mxx) mxx = xy[i];
+    if (xy[i + 1] < mny) mny = xy[i + 1];
+    if (xy[i + 1] > mxy) mxy = xy[i + 1];
+  }
+  o += '[';
+  put_float(o, mnx); o += ','; put_float(o, mny); o += ','; put_float(o, mxx); o += ','; put_float(o, mxy);
+  o += ']';
+}
+
+inline void put_coords(std::string& o, const std::vector<double>& xy, const std::vector<uint8_t>& raw) {
+  o += '[';
+  for (size_t i = 0; i < raw.size(); ++i) {
+    if (i) o += ',';
+    put_xy(o, xy[2 * i], xy[2 * i + 1], raw[i] != 0);
+  }
+  o += ']';
+}
+
+// Trailing annotation (_annotate, optimizer.py): vehicle_type, driver_name, engine.
+inline bool put_annotation(std::string& o, const RouteReq& r, const std::string& engine) {
+  o += ",\"vehicle_type\":";
+  put_str(o, r.vehicle_type);
+  o += ",\"driver_name\":";
+  if (r.driver_name) { if (!put_value(o, *r.driver_name)) return false; }
+  else o += "null";
+  o += ",\"engine\":";
+  put_str(o, engine);
+  return true;
+}
+
+// optimized_order / error text of an infeasible greedy (greedy.py InfeasibleStops)
+inline std::string infeasible_msg(const std::vector<int>& stops) {
+  std::string m = "infeasible stop(s) (payload exceeds vehicle capacity or round trip exceeds "
+                  "maximum_distance): destination indices [";
+  for (size_t i = 0; i < stops.size(); ++i) {
+    if (i) m += ", ";
+    put_int(m, stops[i]);
+  }
+  m += ']';
+  return m;
+}
+
+inline std::string error_body(const std::string& msg) {
+  std::string o = "{\"error\":";
+  put_str(o, msg);
+  o += '}';
+  return o;
+}
+
+// Point-to-point feasibility after routing (optimizer.py point_to_point): "" if feasible
+inline std::string p2p_errors(const RouteReq& r, double dist_m) {
+  std::string e;
+  if (r.p2p_cmp && r.p2p_payload > r.p2p_cap) e = "payload exceeds vehicle capacity";
+  if (dist_m > r.maxd) {
+    if (!e.empty()) e += " | ";
+    e += "route distance exceeds maximum_distance";
+  }
+  return e;
+}
+
+// ------------------------------------------------------------------ whole-request assembly
+// A planned request: the greedy trips (multi-stop) or the infeasible stops.
+struct Plan {
+  bool infeasible = false;
+  std::vector<int> infeasible_stops;          // 0-based destination indices, greedy.py order
+  std::vector<std::vector<int>> trips;        // index lists into [source] + destinations
+};
+
+// The directions calls optimize_route makes, as waypoint lists [(lon, lat), ...]:
+// point-to-point -> [source, dest]; multi-stop -> one list per trip.
+inline void directions_calls(const RouteReq& r, const Plan& p,
+                             std::vector<std::vector<std::pair<double, double>>>& calls) {
+  calls.clear();
+  if (!r.error.empty() || r.fallback || p.infeasible) return;
+  if (r.dst.size() == 1) {
+    calls.push_back({{r.src.lon, r.src.lat}, {r.dst[0].lon, r.dst[0].lat}});
+    return;
+  }
+  for (const auto& t : p.trips) {
+    std::vector<std::pair<double, double>> c;
+    c.reserve(t.size());
+    for (int i : t) c.emplace_back(i == 0 ? r.src.lon : r.dst[i - 1].lon, i == 0 ? r.src.lat : r.dst[i - 1].lat);
+    calls.push_back(std::move(c));
+  }
+}
+
+// The assembled response (properties left open so ETA / persistence fields can follow) and the
+// pieces the persistence rows reuse.
+struct Assembled {
+  bool ok = false;
+  std::string error;                          // optimize_route {"error": ...}
+  std::string body;                           // Feature JSON up to the open properties object
+  std::string coords;                         // geometry.coordinates JSON
+  std::string segments;                       // properties.segments JSON
+  std::string order;                          // optimized_order JSON
+  double dist = 0, dur = 0;                   // properties.summary distance / duration
+};
+
+// Assemble from the directions results `dirs` (one per directions_calls entry).
+inline bool assemble(const RouteReq& r, const Plan& p, const std::vector<Dir>& dirs,
+                     const std::string& engine, Assembled& a) {
+  a = Assembled();
+  if (!r.error.empty()) { a.error = r.error; return true; }
+  if (p.infeasible) { a.error = infeasible_msg(p.infeasible_stops); return true; }
+  std::string& o = a.body;
+  if (r.dst.size() == 1) {
+    const Dir& d = dirs[0];
+    const std::string e = p2p_errors(r, d.dist);
+    if (!e.empty()) { a.error = e; return true; }
+    put_coords(a.coords, d.xy, d.raw);
+    a.segments = "[" + d.segments + "]";
+    a.order = "[0]";
+    a.dist = d.dist;
+    a.dur = d.dur;
+    o += "{\"type\":\"Feature\",\"bbox\":";
+    put_bbox(o, d.xy);
+    o += ",\"geometry\":{\"type\":\"LineString\",\"coordinates\":";
+    o += a.coords;
+    o += "},\"properties\":{\"segments\":";
+    o += a.segments;
+    o += ",\"summary\":{\"distance\":"; put_float(o, d.dist);
+    o += ",\"duration\":"; put_float(o, d.dur);
+    o += "},\"way_points\":[";
+    for (size_t i = 0; i < d.way_points.size(); ++i) { if (i) o += ','; put_int(o, d.way_points[i]); }
+    o += "],\"optimized_order\":[0],\"source\":";
+    if (!put_value(o, *r.src.raw)) return false;
+    o += ",\"destinations\":[";
+    if (!put_value(o, *r.dst[0].raw)) return false;
+    o += ']';
+  } else {
+    std::vector<double> xy;
+    std::vector<uint8_t> raw;
+    double tot_d = 0.0, tot_t = 0.0;
+    for (const Dir& d : dirs) {
+      xy.insert(xy.end(), d.xy.begin(), d.xy.end());
+      raw.insert(raw.end(), d.raw.begin(), d.raw.end());
+      tot_d += d.dist;
+      tot_t += d.dur;
+    }
+    put_coords(a.coords, xy, raw);
+    a.segments = "[";
+    bool first = true;
+    for (const Dir& d : dirs) {
+      if (d.segments.empty()) continue;
+      if (!first) a.segments += ',';
+      first = false;
+      a.segments += d.segments;
+    }
+    a.segments += ']';
+    a.order = "[";
+    first = true;
+    for (const auto& t : p.trips)
+      for (size_t i = 1; i + 1 < t.size(); ++i) {
+        if (!first) a.order += ',';
+        first = false;
+        put_int(a.order, t[i] - 1);
+      }
+    a.order += ']';
+    a.dist = tot_d;
+    a.dur = tot_t;
+    o += "{\"bbox\":";
+    put_bbox(o, xy);
+    o += ",\"type\":\"Feature\",\"geometry\":{\"type\":\"LineString\",\"coordinates\":";
+    o += a.coords;
+    o += "},\"properties\":{\"source\":";
+    if (!put_value(o, *r.src.raw)) return false;
+    o += ",\"destinations\":";
+    if (!put_value(o, *r.root->get("destination_points"))) return false;
+    o += ",\"optimized_order\":";
+    o += a.order;
+    o += ",\"segments\":";
+    o += a.segments;
+    o += ",\"summary\":{\"distance\":"; put_float(o, tot_d);
+    o += ",\"duration\":"; put_float(o, tot_t);
+    o += ",\"trips\":"; put_int(o, (long long)p.trips.size());
+    o += '}';
+  }
+  if (!put_annotation(o, r, engine)) return false;
+  a.ok = true;
+  return true;
+}
+
+// ------------------------------------------------------------------ CPU greedy (greedy.py)
+// Returns trips as index lists into [depot] + stops, or the infeasible stops (0-based dest idx).
+inline bool greedy_trips(const std::vector<double>& d, int n1, const std::vector<double>& dem, double cap,
+                         double maxd, std::vector<std::vector<int>>& trips, std::vector<int>& infeasible) {
+  const int n = n1 - 1;
+  std::vector<int> order(n);
+  for (int i = 0; i < n; ++i) order[i] = i + 1;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return d[a] < d[b]; });
+  std::vector<char> vis(n1, 0);
+  int remaining = n;
+  trips.clear();
+  while (remaining) {
+    std::vector<int> trip{0};
+    double load = 0.0, tdist = 0.0;
+    int cur = 0;
+    for (int idx : order) {
+      if (vis[idx]) continue;
+      const double dm = dem[idx];
+      if ((load + dm) <= cap && (tdist + d[(size_t)cur * n1 + idx] + d[(size_t)idx * n1]) <= maxd) {
+        trip.push_back(idx);
+        load += dm;
+        tdist += d[(size_t)cur * n1 + idx];
+        cur = idx;
+      }
+    }
+    if (trip.size() == 1) {
+      infeasible.clear();
+      for (int i : order)
+        if (!vis[i]) infeasible.push_back(i - 1);
+      return false;
+    }
+    for (size_t i = 1; i < trip.size(); ++i) vis[trip[i]] = 1;
+    remaining -= (int)trip.size() - 1;
+    trip.push_back(0);
+    trips.push_back(std::move(trip));
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ nearest-node snapping
+// Exact nearest neighbour on (lat, lon * c) — the metric of RoadGraph.nearest_nodes (a KD-tree
+// over the same scaled coordinates) — with a uniform bucket grid.  Ties go to the lower node id.
+struct NodeGrid {
+  std::vector<double> y, x;              // lat, lon * c
+  double y0 = 0, x0 = 0, cell = 1;
+  int ny = 1, nx = 1;
+  std::vector<int32_t> start, items;
+
+  void build(const double* lat, const double* lon, size_t n, double c) {
+    y.resize(n);
+    x.resize(n);
+    double y1 = -1e300, x1 = -1e300;
+    y0 = x0 = 1e300;
+    for (size_t i = 0; i < n; ++i) {
+      y[i] = lat[i];
+      x[i] = lon[i] * c;
+      y0 = std::min(y0, y[i]); x0 = std::min(x0, x[i]);
+      y1 = std::max(y1, y[i]); x1 = std::max(x1, x[i]);
+    }
+    const double area = std::max((y1 - y0) * (x1 - x0), 1e-18);
+    cell = std::max(std::sqrt(area / std::max<double>(1.0, (double)n / 2.0)), 1e-9);
+    ny = std::max(1, (int)((y1 - y0) / cell) + 1);
+    nx = std::max(1, (int)((x1 - x0) / cell) + 1);
+    std::vector<int32_t> cnt((size_t)ny * nx + 1, 0);
+    for (size_t i = 0; i < n; ++i) ++cnt[cell_of(y[i], x[i]) + 1];
+    for (size_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
+    start = cnt;
+    items.resize(n);
+    std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+    for (size_t i = 0; i < n; ++i) items[fill[cell_of(y[i], x[i])]++] = (int32_t)i;
+  }
+  size_t cell_of(double yy, double xx) const {
+    int iy = (int)std::floor((yy - y0) / cell), ix = (int)std::floor((xx - x0) / cell);
+    iy = std::min(std::max(iy, 0), ny - 1);
+    ix = std::min(std::max(ix, 0), nx - 1);
+    return (size_t)iy * nx + ix;
+  }
+  int32_t nearest(double lat, double lon, double c) const {
+    const double qy = lat, qx = lon * c;
+    double best = INFINITY;
+    int32_t bi = -1;
+    auto consider = [&](int32_t i) {
+      const double dy = y[i] - qy, dx = x[i] - qx;
+      const double d2 = dy * dy + dx * dx;
+      if (d2 < best || (d2 == best && i < bi)) { best = d2; bi = i; }
+    };
+    // start at the query's cell clamped into the grid: a node in a cell r + 1 or more index steps
+    // away (Chebyshev) from it is at least r cells from the query, inside or outside the grid
+    double fcy = std::floor((qy - y0) / cell), fcx = std::floor((qx - x0) / cell);
+    fcy = std::min(std::max(fcy, 0.0), (double)(ny - 1));
+    fcx = std::min(std::max(fcx, 0.0), (double)(nx - 1));
+    const int cy = (int)fcy, cx = (int)fcx;
+    for (int r = 0;; ++r) {
+      // ring r around (cy, cx), clamped to the grid
+      for (int iy = cy - r; iy <= cy + r; ++iy) {
+        if (iy < 0 || iy >= ny) continue;
+        const bool edge_row = (iy == cy - r || iy == cy + r);
+        for (int ix = cx - r; ix <= cx + r; ix += (edge_row ? 1 : std::max(1, 2 * r))) {
+          if (ix < 0 || ix >= nx) continue;
+          const size_t k = (size_t)iy * nx + ix;
+          for (int32_t j = start[k]; j < start[k + 1]; ++j) consider(items[j]);
+        }
+      }
+      // a node in ring r + 1 or beyond is at least r cells (Chebyshev) from the query's cell
+      const double m = (double)r * cell;
+      if (bi >= 0 && best <= m * m) return bi;
+      if (r > ny + nx + 4) return bi;
+    }
+  }
+};
+
+}  // namespace rtr

@@ -351,8 +351,11 @@ py::dict py_http_load(int port, int connections, double seconds, const std::stri
   return d;
 }
 
+void bind_route(py::module& m);   // route_bind.cpp
+
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "routest_amd CPU native runtime";
+  bind_route(m);
   m.def("http_load", &py_http_load, py::arg("port"), py::arg("connections") = 1, py::arg("seconds") = 2.0,
         py::arg("path") = "/api/predict_eta", py::arg("body") = "", py::arg("threads") = 1,
         py::arg("max_requests") = 0, py::arg("warmup") = 0);

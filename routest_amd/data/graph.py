@@ -50,16 +50,37 @@ class RoadGraph:
     def degree(self) -> np.ndarray:
         return np.diff(self.indptr)
 
+    #: snapping metric: Euclidean on (lat, lon * cos(14.6 deg)) — Metro Manila's latitude
+    SNAP_C = float(np.cos(np.radians(14.6)))
+
+    def _snapper(self):
+        """Exact nearest node: the native bucket grid (csrc/runtime/route_core.h NodeGrid, the same
+        code the native front end snaps with) when the C++ runtime is present, else a KD-tree."""
+        s = getattr(self, "_snap", None)
+        if s is None:
+            try:
+                from ..ops._ext import runtime
+                rt = runtime(required=False)
+            except Exception:  # pragma: no cover
+                rt = None
+            if rt is not None:
+                s = ("grid", rt.NodeGrid(self.lat.astype(np.float64), self.lon.astype(np.float64), self.SNAP_C))
+            else:
+                from scipy.spatial import cKDTree
+                s = ("kd", cKDTree(np.stack([self.lat, self.lon * self.SNAP_C], 1)))
+            self._snap = s
+        return s
+
     def nearest_node(self, lat: float, lon: float) -> int:
-        from scipy.spatial import cKDTree
-        if getattr(self, "_tree", None) is None:
-            self._tree = cKDTree(np.stack([self.lat, self.lon * np.cos(np.radians(14.6))], 1))
-        _, i = self._tree.query([lat, lon * np.cos(np.radians(14.6))])
-        return int(i)
+        return int(self.nearest_nodes([lat], [lon])[0])
 
     def nearest_nodes(self, lats, lons) -> np.ndarray:
-        self.nearest_node(float(self.lat[0]), float(self.lon[0]))
-        _, i = self._tree.query(np.stack([np.asarray(lats), np.asarray(lons) * np.cos(np.radians(14.6))], 1))
+        kind, s = self._snapper()
+        la = np.asarray(lats, dtype=np.float64).reshape(-1)
+        lo = np.asarray(lons, dtype=np.float64).reshape(-1)
+        if kind == "grid":
+            return s.nearest(la, lo)
+        _, i = s.query(np.stack([la, lo * self.SNAP_C], 1))
         return i.astype(np.int32)
 
     def save(self, path: str) -> None:

@@ -344,6 +344,16 @@ class BatchedAstar:
                 for i in range(len(c))]
 
 
+def _path_length(g: RoadGraph, p: np.ndarray) -> float:
+    """Sum of the great-circle lengths along a node path: the native route assembler's function
+    (csrc/runtime/route_core.h path_length_m) when the C++ runtime is present, so the Python path
+    and the native front end produce identical bits."""
+    from .providers import _RT
+    if _RT is not None:
+        return _RT.path_length_m(g.lat, g.lon, np.asarray(p, dtype=np.int32))
+    return float(haversine_m(g.lat[p[:-1]], g.lon[p[:-1]], g.lat[p[1:]], g.lon[p[1:]]).sum())
+
+
 class GraphProvider(HaversineProvider):
     """Directions along shortest paths of the road graph (durations from learned edge costs)."""
 
@@ -415,8 +425,7 @@ class GraphProvider(HaversineProvider):
                 raise ProviderError(f"no road path found between waypoints {k} and {k + 1} "
                                     f"(graph nodes {int(nodes[k])} -> {int(nodes[k + 1])})")
             p = np.asarray(path)
-            dist = float(haversine_m(self.g.lat[p[:-1]], self.g.lon[p[:-1]], self.g.lat[p[1:]],
-                                     self.g.lon[p[1:]]).sum() * 1.15) if len(p) > 1 else 0.0
+            dist = _path_length(self.g, p) * 1.15 if len(p) > 1 else 0.0
             # node coordinates of the whole leg in one vector op (6 decimals, like ORS)
             geometry.extend(np.round(np.stack([self.g.lon[p], self.g.lat[p]], axis=1)
                                      .astype(np.float64), 6).tolist())

@@ -63,9 +63,31 @@ def haversine_m(lat1, lon1, lat2, lon2):
     return 2 * EARTH_R * np.arcsin(np.sqrt(np.clip(a, 0.0, 1.0)))
 
 
+def _native_rt():
+    try:
+        from ..ops._ext import runtime
+        return runtime(required=False)
+    except Exception:  # pragma: no cover
+        return None
+
+
+_RT = _native_rt()
+
+
+def haversine_scalar(lat1: float, lon1: float, lat2: float, lon2: float) -> float:
+    """One great-circle distance.  With the C++ runtime present this is the native route
+    assembler's own function (csrc/runtime/route_core.h), so the Python path and the native front
+    end produce identical bits; numpy's vectorised sin/cos may differ from libm in the last ulp."""
+    if _RT is not None:
+        return _RT.haversine_m(float(lat1), float(lon1), float(lat2), float(lon2))
+    return float(haversine_m(lat1, lon1, lat2, lon2))
+
+
 def haversine_matrix(lats: Sequence[float], lons: Sequence[float], circuity: float = 1.0) -> np.ndarray:
     la = np.asarray(lats, dtype=np.float64)
     lo = np.asarray(lons, dtype=np.float64)
+    if _RT is not None and la.shape[0] <= 4096:
+        return _RT.haversine_matrix(la, lo, float(circuity))
     return haversine_m(la[:, None], lo[:, None], la[None, :], lo[None, :]) * circuity
 
 
@@ -102,7 +124,7 @@ class HaversineProvider:
         for k in range(len(coords) - 1):
             lon1, lat1 = float(coords[k][0]), float(coords[k][1])
             lon2, lat2 = float(coords[k + 1][0]), float(coords[k + 1][1])
-            dist = float(haversine_m(lat1, lon1, lat2, lon2)) * self.circuity
+            dist = haversine_scalar(lat1, lon1, lat2, lon2) * self.circuity
             n = max(1, int(math.ceil(dist / self.step_m)))
             start_wp = len(geometry) - 1
             t = np.arange(1, n + 1, dtype=np.float64) / n          # densify in one vector op

@@ -57,13 +57,15 @@ def _run(cmd: List[str]) -> None:
 
 
 NO_SLP = {"eta_mlp_fwd.hip"}
+# host code that must round exactly like Python (csrc/runtime/route_core.h): no FMA contraction
+NO_CONTRACT = {"native_server.hip", "route_service.hip"}
 
 
 def build_C(force: bool = False, jobs: int = 8) -> str:
     inc, libdir, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     os.makedirs(BUILD, exist_ok=True)
-    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "runtime", "*.h"))
     hip_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}"]
@@ -77,6 +79,8 @@ def build_C(force: bool = False, jobs: int = 8) -> str:
             # otherwise re-pack scalar f32 FMAs beside MFMAs into v_pk_fma_f32, which costs ~5x its
             # issue slot there (MI355X_MICROARCH.md, "price of one filler")
             extra = ["-fno-slp-vectorize"] if os.path.basename(src) in NO_SLP else []
+            if os.path.basename(src) in NO_CONTRACT:
+                extra.append("-ffp-contract=off")
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common, *extra, "-munsafe-fp-atomics",
                               "-I", CSRC, "-I", os.path.join(ROCM, "include"), "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
@@ -113,6 +117,7 @@ def build_rt(force: bool = False, jobs: int = 8) -> str:
         return ""
     if force or _newer(out, srcs + headers):
         _run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-pthread",
+              "-ffp-contract=off",
               "-I", pybind11.get_include(), "-I", py_inc, "-I", os.path.join(CSRC, "runtime"),
               *srcs, "-o", out])
     return out
