@@ -1,7 +1,15 @@
 #!/usr/bin/env python3
 """Optimizer on the request path: C concurrent multi-stop POST /api/optimize_route requests (2-10
-stops each) through the FastAPI app in-process (ASGI, no sockets) with the cross-request GPU
-batcher, vs the per-request path.  Reports req/s and p50/p99 latency per mode.
+stops each).
+
+* ``native`` (default first): real HTTP over loopback to the serving stack's main port — the native
+  front end + route service (csrc/native_server.hip, csrc/route_service.hip: cross-request
+  batching, K5 + K6, the batched A*, C++ GeoJSON assembly) — driven by the native closed-loop
+  client with C connections, 1k distinct request bodies cycled;
+* ``batched`` / ``per_request``: the FastAPI app in-process (ASGI, no sockets) with and without the
+  Python cross-request batcher;
+  (``per_request`` with the haversine provider is the inline CPU optimizer).
+Reports req/s and p50/p99 latency per mode.
 
     python bench/route_http_bench.py [--provider haversine|graph] [--concurrency 1000] [--rounds 3]
 """
@@ -25,7 +33,12 @@ def main() -> None:
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--batch-max", type=int, default=1024)
     ap.add_argument("--timeout-us", type=int, default=2000)
+    ap.add_argument("--modes", default="native,batched,per_request")
+    ap.add_argument("--seconds", type=float, default=8.0, help="native mode: load duration")
+    ap.add_argument("--threads", type=int, default=8, help="native mode: front-end reactor threads")
+    ap.add_argument("--client-threads", type=int, default=8)
     a = ap.parse_args()
+    modes = a.modes.split(",")
     import httpx
     import numpy as np
     import torch
@@ -46,6 +59,7 @@ def main() -> None:
         prov = HaversineProvider()
         rng = np.random.default_rng(0)
         lat, lon = 14.55 + rng.normal(0, 0.05, 20000), 121.03 + rng.normal(0, 0.05, 20000)
+        g = None
     rng = np.random.default_rng(1)
     reqs = []
     for i in range(a.concurrency):
@@ -55,9 +69,38 @@ def main() -> None:
                                             for j in idx[1:]],
                      "driver_details": {"driver_name": f"v{i}", "vehicle_type": "car",
                                         "vehicle_capacity": 4, "maximum_distance": 1e7}})
-    out = {"metric": "optimize_route req/s (concurrent HTTP, in-process ASGI)", "provider": a.provider,
+    out = {"metric": "optimize_route req/s (concurrent HTTP)", "provider": a.provider,
            "concurrency": a.concurrency, "stops": "2-10 per request"}
-    for mode in ("batched", "per_request"):
+    if "native" in modes:
+        from routest_amd.ops import _ext
+        from routest_amd.serve.eta_service import default_model
+        from routest_amd.serve.frontend import ServingStack
+        rt = _ext.runtime(required=True)
+        s = load_settings(env={}, dotenv_path=None, devices=[0], route_batch="0", warm_scorer=False)
+        model = default_model(steps=30)
+        sv = build_services(s, eta=EtaService(model, devices=[0]), provider=prov, store=None)
+        app = create_app(sv)
+        with ServingStack(sv, app, model, [0], threads=a.threads, batch_max=a.batch_max,
+                          timeout_us=min(a.timeout_us, 1000)) as st:
+            bodies = [json.dumps(r) for r in reqs]
+            paths = ["/api/optimize_route"] * len(bodies)
+            rt.http_load_multi(st.port, min(64, a.concurrency), 2.0, paths, bodies, a.client_threads)   # warm-up
+            f0 = st.front.stats()
+            r = rt.http_load_multi(st.port, a.concurrency, a.seconds, paths, bodies, a.client_threads, 0, 1)
+            f1 = st.front.stats()
+            lat_us = r["latencies_us"]
+            out["native"] = {"req_per_s": r["requests"] / r["seconds"], "errors": int(r["errors"]),
+                             "p50_ms": float(lat_us[len(lat_us) // 2]) / 1e3 if len(lat_us) else None,
+                             "p99_ms": float(lat_us[int(len(lat_us) * 0.99) - 1]) / 1e3 if len(lat_us) else None,
+                             "response_MB_per_s": r["bytes"] / r["seconds"] / 1e6,
+                             "flushes": f1["route_flushes"] - f0["route_flushes"],
+                             "legs_searched": f1["route_legs"] - f0["route_legs"],
+                             "legs_on_host": f1["route_host_legs"] - f0["route_host_legs"],
+                             "fallbacks_to_python": f1["route_service_fallbacks"] - f0["route_service_fallbacks"],
+                             "front_threads": a.threads, "client": "native closed-loop (csrc/runtime/http_client.h)",
+                             "path": "HTTP/1.1 loopback -> native front end main port -> route service"}
+        print(json.dumps({"native": out["native"]}), flush=True)
+    for mode in [m for m in modes if m in ("batched", "per_request")]:
         s = load_settings(env={}, dotenv_path=None, devices=[0],
                           route_batch="1" if mode == "batched" else "0", route_gpu_min_stops=1, route_batch_max=a.batch_max,
                           route_batch_timeout_us=a.timeout_us, warm_scorer=False)
@@ -85,7 +128,8 @@ def main() -> None:
         el, ls = asyncio.run(go())
         out[mode] = {"req_per_s": len(reqs) / el, "wall_s": el, "p50_ms": ls[len(ls) // 2] * 1e3,
                      "p99_ms": ls[int(len(ls) * 0.99) - 1] * 1e3,
-                     "flushes": sum(sv.route_batcher.flushes) if sv.route_batcher else None}
+                     "flushes": sum(sv.route_batcher.flushes) if sv.route_batcher else None,
+                     "path": "in-process ASGI (no sockets)"}
         sv.close()
         print(json.dumps({mode: out[mode]}), flush=True)
     print(json.dumps(out), flush=True)

@@ -16,6 +16,7 @@
 
 #include "ops.h"
 #include "common.h"
+#include "route_service.h"
 
 namespace {
 
@@ -829,9 +830,74 @@ bool pscore_score(int64_t h, torch::Tensor rec, torch::Tensor out) {
 }
 
 // ---------------------------------------------------------------- native predict server
+// One route service config per GPU from a Python dict (routest_amd/serve/native_server.py
+// route_config): scalars, host arrays (CPU tensors) and device tensors the caller keeps alive.
+static rt::RouteServiceCfg route_cfg_from(const py::dict& d, int device, const void* eta_blob, int H,
+                                          const rt::NormParams& np, int variant, int cus) {
+  rt::RouteServiceCfg c;
+  auto has = [&](const char* k) { return d.contains(k) && !d[k].is_none(); };
+  auto tptr = [&](const char* k, bool cuda) -> void* {
+    if (!has(k)) return nullptr;
+    torch::Tensor t = d[k].cast<torch::Tensor>();
+    TORCH_CHECK(t.is_contiguous(), "route config tensor ", k, " must be contiguous");
+    TORCH_CHECK(t.is_cuda() == cuda, "route config tensor ", k, cuda ? " must be on the GPU" : " must be on the CPU");
+    if (cuda) TORCH_CHECK(t.device().index() == device, "route config tensor ", k, " on the wrong GPU");
+    return t.data_ptr();
+  };
+  c.device = device;
+  c.provider = d["provider"].cast<std::string>() == "graph" ? 1 : 0;
+  if (has("circuity")) c.circuity = d["circuity"].cast<double>();
+  if (has("step_m")) c.step_m = d["step_m"].cast<double>();
+  if (has("engine")) c.engine = d["engine"].cast<std::string>();
+  if (has("compat200")) c.compat200 = d["compat200"].cast<bool>();
+  if (has("batch_max")) c.batch_max = d["batch_max"].cast<int>();
+  if (has("timeout_us")) c.timeout_us = d["timeout_us"].cast<double>();
+  if (has("sqlite_path")) c.sqlite_path = d["sqlite_path"].cast<std::string>();
+  if (c.provider == 1) {
+    c.glat = (const double*)tptr("glat", false);
+    c.glon = (const double*)tptr("glon", false);
+    c.h_indptr = (const int*)tptr("h_indptr", false);
+    c.h_indices = (const int*)tptr("h_indices", false);
+    c.h_cost = (const float*)tptr("h_cost", false);
+    c.indptr = (const int*)tptr("indptr", true);
+    c.indices = (const int*)tptr("indices", true);
+    c.cost = (const float*)tptr("cost", true);
+    c.lat32 = (const float*)tptr("lat32", true);
+    c.lon32 = (const float*)tptr("lon32", true);
+    c.lm = (const float*)tptr("lm", true);
+    c.state = tptr("state", true);
+    c.heap = tptr("heap", true);
+    c.touched = (int*)tptr("touched", true);
+    c.hcache = (float*)tptr("hcache", true);
+    c.N = d["N"].cast<int>();
+    c.K = has("K") ? d["K"].cast<int>() : 0;
+    c.snap_c = d["snap_c"].cast<double>();
+    c.slots = d["slots"].cast<int>();
+    c.cap = d["cap"].cast<int>();
+    c.max_path = d["max_path"].cast<int>();
+    c.max_iters = d["max_iters"].cast<int>();
+    c.lane_pops = d["lane_pops"].cast<int>();
+    c.wave_slots = d["wave_slots"].cast<int>();
+    c.inv_vmax = d["inv_vmax"].cast<float>();
+    c.wave_delta = d["wave_delta"].cast<float>();
+    TORCH_CHECK(c.glat && c.glon && c.indptr && c.indices && c.cost && c.lat32 && c.lon32 && c.state && c.heap &&
+                    c.touched && c.N > 0 && c.slots > 0 && c.cap >= 128 && c.max_path > 0,
+                "graph route config incomplete");
+    TORCH_CHECK(c.lm == nullptr || c.K == 8 || c.K == 16 || c.K == 32, "landmarks K must be 8, 16 or 32");
+    TORCH_CHECK(c.hcache == nullptr || c.wave_slots > 0, "wave stage needs wave_slots");
+  }
+  c.eta_blob = eta_blob;
+  c.H = H;
+  c.np = np;
+  c.variant = variant;
+  c.num_cus = cus;
+  return c;
+}
+
 int64_t native_server_start(int64_t port, int64_t threads, std::vector<torch::Tensor> blobs, int64_t H,
                             std::vector<double> norm, int64_t variant, int64_t max_batch,
-                            std::vector<std::string> cors, bool cors_vercel, bool bind_any) {
+                            std::vector<std::string> cors, bool cors_vercel, bool bind_any,
+                            int64_t upstream_port, py::list routes) {
   TORCH_CHECK(!blobs.empty(), "need one weight blob per GPU");
   std::vector<int> devs, cus;
   std::vector<const void*> ptrs;
@@ -844,14 +910,19 @@ int64_t native_server_start(int64_t port, int64_t threads, std::vector<torch::Te
   }
   TORCH_CHECK(norm.size() == 8, "norm must hold 4 scales + 4 shifts");
   TORCH_CHECK(max_batch >= 1 && max_batch <= (1 << 24), "max_batch out of range");
+  TORCH_CHECK(routes.empty() || routes.size() == blobs.size(), "one route config per GPU (or none)");
   rt::NormParams np;
   for (int i = 0; i < 4; ++i) {
     np.scale[i] = (float)norm[i];
     np.shift[i] = (float)norm[4 + i];
   }
+  std::vector<rt::RouteServiceCfg> rcfg;
+  for (size_t g = 0; g < routes.size(); ++g)
+    rcfg.push_back(route_cfg_from(routes[g].cast<py::dict>(), devs[g], ptrs[g], (int)H, np, (int)variant, cus[g]));
   std::string err;
   const int64_t h = rt::native_server_start((int)port, (int)threads, devs, ptrs, cus, (int)H, np, (int)variant,
-                                            (int)max_batch, cors, cors_vercel, bind_any, err);
+                                            (int)max_batch, cors, cors_vercel, bind_any, (int)upstream_port, rcfg,
+                                            err);
   TORCH_CHECK(h >= 0, "native server: ", err);
   return h;
 }
@@ -1045,7 +1116,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     py::gil_scoped_release nogil;
     rt::pscore_destroy(p);
   });
-  m.def("native_server_start", &native_server_start, "native HTTP front end for /api/predict_eta and /predict");
+  m.def("native_server_start", &native_server_start, "native HTTP front end (predictions, routes, relay)",
+        py::arg("port"), py::arg("threads"), py::arg("blobs"), py::arg("H"), py::arg("norm"), py::arg("variant"),
+        py::arg("max_batch"), py::arg("cors"), py::arg("cors_vercel"), py::arg("bind_any"),
+        py::arg("upstream_port") = 0, py::arg("routes") = py::list());
   m.def("native_server_stop", [](int64_t h) {
     py::gil_scoped_release nogil;
     rt::native_server_stop(h);

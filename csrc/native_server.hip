@@ -1,6 +1,17 @@
-// Native prediction front end: HTTP/1.1 server for POST /api/predict_eta and POST /predict with
-// no Python on the request path (SURVEY §7.5 hard part 2: "p50 is dominated by the host stack";
-// the reference serves this route through Flask, RO/Flaskr/routes.py:365-383).
+// Native front end: HTTP/1.1 server for the API's hot routes with no Python on the request path
+// (SURVEY §7.5 hard part 2: "p50 is dominated by the host stack"; the reference serves these
+// through Flask, RO/Flaskr/routes.py:29-50,89-127,365-383), and — when given an upstream port — the
+// service's MAIN port: every other request is relayed unchanged to the Python (ASGI) app.
+//
+//  * POST /api/predict_eta, /predict: answered in the reactor (below).
+//  * POST /api/optimize_route, /route, /api/request_route: parsed requests go to the GPU's route
+//    service (csrc/route_service.hip: K5 + K6 + batched A* + native assembly, byte-identical to
+//    the FastAPI handler); the connection is parked until its job comes back through the
+//    reactor's eventfd.  A request whose semantics the native path does not mirror comes back as
+//    a fallback and is relayed to the Python app.
+//  * anything else: relayed to the upstream ASGI server over a per-connection keep-alive
+//    connection; a streamed (chunked) answer such as the SSE feed turns the connection into a
+//    byte tunnel for the rest of its life.
 //
 // Design (one process, MI355X-first):
 //  * R reactor threads, each with its own SO_REUSEPORT listening socket (the kernel spreads
@@ -15,7 +26,7 @@
 //    on /api/predict_eta reads as {} (Flask get_json(silent=True)); a JSON array (or {"items": []})
 //    on /predict is a batch answered as {"predictions": [...]}; per-item errors -> 400 for single
 //    requests, {"error": ...} entries in batches.  GET /api/ping is answered natively; everything
-//    else is 404 (the full API stays on the uvicorn port).
+//    else is relayed to the upstream app (404 when the front end runs without one).
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -40,6 +51,7 @@
 
 #include "common.h"
 #include "ops.h"
+#include "route_service.h"
 #include "runtime/rt_core.h"
 
 namespace rt {
@@ -61,14 +73,35 @@ struct ServerCfg {
   std::mutex* scorer_mu = nullptr;
   std::vector<std::string> cors_exact;
   bool cors_vercel = true;
+  int upstream_port = 0;               // Python app for everything not answered natively (0 = none)
+  RouteService* routes = nullptr;      // this reactor's GPU's route service (nullptr = relay routes)
 };
 
 struct Conn {
   int fd = -1;
+  uint64_t gen = 0;      // distinguishes a reused fd from the connection a late job belongs to
   std::string in, out;
   size_t out_off = 0;
   bool close_after = false;
   int npending = 0;      // requests of this connection waiting for the batch launch
+  bool async = false;    // a route job or a relayed request is in flight: answers stay in order
+  // relay to the upstream app
+  int up = -1;
+  std::string up_out, up_in;
+  size_t up_off = 0;
+  bool up_head = false;  // the relayed request was HEAD (no response body)
+  bool tunnel = false;   // streamed upstream answer: bytes flow both ways unparsed from now on
+};
+
+// A route job's reactor-side context.
+class Reactor;
+struct JobTag {
+  Reactor* reactor;
+  int fd;
+  uint64_t gen;
+  bool keep_alive;
+  std::string origin;
+  std::string raw;       // the whole HTTP request, for the relay if the job falls back
 };
 
 // One parsed prediction request waiting for the batch launch.
@@ -83,7 +116,7 @@ struct Pending {
 
 struct Stats {
   std::atomic<long long> requests{0}, predictions{0}, launches{0}, errors{0}, resident{0}, fallbacks{0},
-      wire8{0};
+      wire8{0}, route_requests{0}, route_fallbacks{0}, relayed{0};
 };
 
 inline Stamp now_local() {
@@ -121,7 +154,7 @@ class Reactor {
     a.sin_port = htons((uint16_t)cfg_.port);
     a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
     if (bind_any_) a.sin_addr.s_addr = htonl(INADDR_ANY);
-    if (bind(lfd_, (sockaddr*)&a, sizeof a) != 0 || listen(lfd_, 1024) != 0) {
+    if (bind(lfd_, (sockaddr*)&a, sizeof a) != 0 || listen(lfd_, 4096) != 0) {
       err = std::string("bind/listen: ") + std::strerror(errno);
       return false;
     }
@@ -133,7 +166,18 @@ class Reactor {
   }
 
   void set_bind_any(bool v) { bind_any_ = v; }
+  void set_routes(RouteService* r) { cfg_.routes = r; }
   int wake_fd() const { return wake_; }
+
+  // called on the route service's worker thread
+  void job_done(RouteJob* j) {
+    {
+      std::lock_guard<std::mutex> lk(done_mu_);
+      done_.push_back(j);
+    }
+    uint64_t one = 1;
+    (void)!write(wake_, &one, 8);
+  }
 
   void run() {
     if (hipSetDevice(cfg_.device) != hipSuccess) return;
@@ -149,12 +193,18 @@ class Reactor {
       return;
 
     epoll_event evs[256];
-    while (!stop_.load(std::memory_order_relaxed)) {
+    while (!stop_.load(std::memory_order_relaxed) || inflight_ > 0) {
       const int n = epoll_wait(ep_, evs, 256, 100);
       for (int i = 0; i < n; ++i) {
         const int fd = evs[i].data.fd;
-        if (fd == lfd_) { accept_all(); continue; }
-        if (fd == wake_) { uint64_t v; (void)!read(wake_, &v, 8); continue; }
+        if (fd == lfd_) { if (!stop_.load(std::memory_order_relaxed)) accept_all(); continue; }
+        if (fd == wake_) { uint64_t v; (void)!read(wake_, &v, 8); drain_done(); continue; }
+        auto ui = up2c_.find(fd);
+        if (ui != up2c_.end()) {
+          auto ci = conns_.find(ui->second);
+          if (ci != conns_.end()) on_upstream(ci->second, evs[i].events);
+          continue;
+        }
         auto it = conns_.find(fd);
         if (it == conns_.end()) continue;
         if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) on_readable(it->second);
@@ -163,8 +213,12 @@ class Reactor {
       run_batch();
       for (int fd : to_close_) close_conn(fd);
       to_close_.clear();
+      if (stop_.load(std::memory_order_relaxed) && n == 0) drain_done();
     }
-    for (auto& kv : conns_) close(kv.first);
+    for (auto& kv : conns_) {
+      if (kv.second.up >= 0) close(kv.second.up);
+      close(kv.first);
+    }
     conns_.clear();
     close(lfd_);
     close(ep_);
@@ -176,7 +230,7 @@ class Reactor {
   }
 
  private:
-  const ServerCfg cfg_;                // per-reactor copy: device + blob of its GPU
+  ServerCfg cfg_;                      // per-reactor copy: device + blob of its GPU
   Stats& st_;
   std::atomic<bool>& stop_;
   bool bind_any_ = false;
@@ -190,9 +244,14 @@ class Reactor {
   float* d_out_ = nullptr;
   int cap_ = 0;
   size_t nrec_ = 0;
+  uint64_t next_gen_ = 1;
   std::unordered_map<int, Conn> conns_;
+  std::unordered_map<int, int> up2c_;  // upstream fd -> client fd
   std::vector<Pending> pending_;
   std::vector<int> to_close_;
+  std::mutex done_mu_;
+  std::vector<RouteJob*> done_;
+  int inflight_ = 0;                   // route jobs submitted and not yet drained
 
   void add(int fd, uint32_t ev = EPOLLIN) {
     epoll_event e{};
@@ -209,20 +268,28 @@ class Reactor {
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
       Conn c;
       c.fd = fd;
-      conns_.emplace(fd, std::move(c));
+      c.gen = next_gen_++;
+      conns_[fd] = std::move(c);
       add(fd);
     }
   }
 
   void close_conn(int fd) {
-    if (conns_.erase(fd)) {
-      epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
-      close(fd);
+    auto it = conns_.find(fd);
+    if (it == conns_.end()) return;
+    if (it->second.up >= 0) {
+      epoll_ctl(ep_, EPOLL_CTL_DEL, it->second.up, nullptr);
+      up2c_.erase(it->second.up);
+      close(it->second.up);
     }
+    conns_.erase(it);
+    epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+    close(fd);
   }
 
   void on_readable(Conn& c) {
     char buf[65536];
+    bool eof = false;
     while (true) {
       const ssize_t r = read(c.fd, buf, sizeof buf);
       if (r > 0) {
@@ -230,18 +297,33 @@ class Reactor {
         if (c.in.size() > (256u << 20)) { to_close_.push_back(c.fd); return; }
         continue;
       }
-      if (r == 0) { to_close_.push_back(c.fd); break; }
+      if (r == 0) { eof = true; break; }
       if (errno == EAGAIN || errno == EWOULDBLOCK) break;
       to_close_.push_back(c.fd);
       return;
     }
-    parse_requests(c);
+    if (c.tunnel) {                    // streamed upstream answer: forward the client's bytes raw
+      c.up_out += c.in;
+      c.in.clear();
+      flush_up(c);
+      if (eof) to_close_.push_back(c.fd);
+      return;
+    }
+    if (eof) {
+      // half-closed client: answer what is already complete, then close
+      if (!c.async) parse_requests(c);
+      if (c.async) { c.close_after = true; return; }
+      if (c.out.size() > c.out_off) flush(c);
+      to_close_.push_back(c.fd);
+      return;
+    }
+    if (!c.async) parse_requests(c);
     if (c.out.size() > c.out_off) flush(c);   // immediate answers (errors, ping, 100-continue)
   }
 
-  // Parse every complete request buffered on c (pipelining allowed).
+  // Parse every complete request buffered on c (pipelining allowed); stops at an async request.
   void parse_requests(Conn& c) {
-    while (true) {
+    while (!c.async && !c.tunnel) {
       const size_t hend = c.in.find("\r\n\r\n");
       if (hend == std::string::npos) {
         if (c.in.size() > 65536) { respond(c, 431, "{\"error\":\"headers too large\"}", "", true); }
@@ -295,6 +377,10 @@ class Reactor {
         ls = le + 2;
       }
       if (chunked) {
+        if (cfg_.upstream_port > 0) {      // the Python app decodes chunked bodies: relay raw
+          start_tunnel(c);
+          return;
+        }
         respond(c, 411, "{\"error\":\"chunked bodies are not supported; send Content-Length\"}", origin, true);
         c.in.clear();
         return;
@@ -312,10 +398,11 @@ class Reactor {
         }
         return;   // body not complete yet
       }
+      std::string raw = c.in.substr(0, hend + 4 + clen);
       std::string body = c.in.substr(hend + 4, clen);
       c.in.erase(0, hend + 4 + clen);
       st_.requests.fetch_add(1, std::memory_order_relaxed);
-      handle(c, method, path, body, json, keep, origin);
+      handle(c, method, path, body, json, keep, origin, raw);
       if (c.close_after) return;
     }
   }
@@ -334,7 +421,7 @@ class Reactor {
     const char* reason = code == 200 ? "OK" : code == 400 ? "Bad Request" : code == 404 ? "Not Found"
                          : code == 405 ? "Method Not Allowed" : code == 411 ? "Length Required"
                          : code == 413 ? "Payload Too Large" : code == 431 ? "Request Header Fields Too Large"
-                         : code == 503 ? "Service Unavailable" : "Error";
+                         : code == 502 ? "Bad Gateway" : code == 503 ? "Service Unavailable" : "Error";
     char head[256];
     const int hn = std::snprintf(head, sizeof head,
                                  "HTTP/1.1 %d %s\r\ncontent-type: application/json\r\ncontent-length: %zu\r\n",
@@ -353,7 +440,7 @@ class Reactor {
   }
 
   void handle(Conn& c, const std::string& method, const std::string& path, const std::string& body,
-              bool json, bool keep, const std::string& origin) {
+              bool json, bool keep, const std::string& origin, std::string& raw) {
     if (method == "OPTIONS") {
       if (c.npending > 0) run_batch();
       std::string h = "HTTP/1.1 200 OK\r\ncontent-length: 0\r\naccess-control-allow-methods: GET, POST, OPTIONS\r\n"
@@ -366,13 +453,29 @@ class Reactor {
       respond(c, 200, "{\"ok\":true,\"service\":\"route-optimizer\"}", origin, !keep);
       return;
     }
-    const bool is_pe = path == "/api/predict_eta", is_p = path == "/predict";
-    if (!is_pe && !is_p) {
-      respond(c, 404, "{\"detail\":\"Not Found\"}", origin, !keep);
+    const bool is_opt = path == "/api/optimize_route" || path == "/route", is_req = path == "/api/request_route";
+    if ((is_opt || is_req) && method == "POST" && cfg_.routes != nullptr) {
+      if (c.npending > 0) run_batch();           // earlier predictions of this connection first
+      auto* tag = new JobTag{this, c.fd, c.gen, keep, origin, std::move(raw)};
+      auto* j = new RouteJob();
+      j->body = body;
+      j->json_ok = json;
+      j->request_route = is_req;
+      j->tag = tag;
+      c.async = true;
+      ++inflight_;
+      st_.route_requests.fetch_add(1, std::memory_order_relaxed);
+      cfg_.routes->submit(j);
       return;
     }
-    if (method != "POST") {
-      respond(c, 405, "{\"detail\":\"Method Not Allowed\"}", origin, !keep);
+    const bool is_pe = path == "/api/predict_eta", is_p = path == "/predict";
+    if (!(is_pe || is_p) || method != "POST") {
+      if (cfg_.upstream_port > 0) {
+        relay(c, raw, method == "HEAD");
+        return;
+      }
+      if (!is_pe && !is_p) respond(c, 404, "{\"detail\":\"Not Found\"}", origin, !keep);
+      else respond(c, 405, "{\"detail\":\"Method Not Allowed\"}", origin, !keep);
       return;
     }
     // body -> items
@@ -435,6 +538,224 @@ class Reactor {
     }
     ++c.npending;
     pending_.push_back(std::move(pd));
+  }
+
+  // ---------------------------------------------------------------- route jobs coming back
+  void drain_done() {
+    std::vector<RouteJob*> jobs;
+    {
+      std::lock_guard<std::mutex> lk(done_mu_);
+      jobs.swap(done_);
+    }
+    for (RouteJob* j : jobs) {
+      --inflight_;
+      JobTag* t = static_cast<JobTag*>(j->tag);
+      auto it = conns_.find(t->fd);
+      if (it != conns_.end() && it->second.gen == t->gen) {
+        Conn& c = it->second;
+        c.async = false;
+        if (j->fallback) {
+          st_.route_fallbacks.fetch_add(1, std::memory_order_relaxed);
+          if (cfg_.upstream_port > 0) {
+            relay(c, t->raw, false);
+          } else {
+            respond(c, 503, "{\"error\":\"request not supported by the native route path\"}", t->origin,
+                    !t->keep_alive);
+          }
+        } else {
+          respond(c, j->status, j->out, t->origin, !t->keep_alive);
+        }
+        if (!c.async) {
+          flush(c);
+          if (!c.close_after && !c.tunnel) {
+            parse_requests(c);                 // requests that arrived while the job ran
+            if (c.out.size() > c.out_off) flush(c);
+          }
+        }
+      }
+      delete t;
+      delete j;
+    }
+  }
+
+  // ---------------------------------------------------------------- relay to the Python app
+  bool connect_up(Conn& c) {
+    if (c.up >= 0) return true;
+    const int u = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+    if (u < 0) return false;
+    int one = 1;
+    setsockopt(u, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)cfg_.upstream_port);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (connect(u, (sockaddr*)&a, sizeof a) != 0 && errno != EINPROGRESS) {
+      close(u);
+      return false;
+    }
+    c.up = u;
+    c.up_in.clear();
+    c.up_out.clear();
+    c.up_off = 0;
+    up2c_[u] = c.fd;
+    add(u, EPOLLIN | EPOLLOUT);
+    return true;
+  }
+
+  void relay(Conn& c, const std::string& raw, bool head) {
+    if (c.npending > 0) run_batch();
+    flush(c);
+    if (!connect_up(c)) {
+      respond(c, 502, "{\"error\":\"upstream app unavailable\"}", "", true);
+      flush(c);
+      return;
+    }
+    st_.relayed.fetch_add(1, std::memory_order_relaxed);
+    c.up_out += raw;
+    c.up_head = head;
+    c.async = true;
+    flush_up(c);
+  }
+
+  // chunked request bodies (and anything after them) go to the app as raw bytes
+  void start_tunnel(Conn& c) {
+    if (c.npending > 0) run_batch();
+    flush(c);
+    if (!connect_up(c)) {
+      respond(c, 502, "{\"error\":\"upstream app unavailable\"}", "", true);
+      flush(c);
+      return;
+    }
+    c.tunnel = true;
+    c.up_out += c.in;
+    c.in.clear();
+    flush_up(c);
+  }
+
+  void flush_up(Conn& c) {
+    if (c.up < 0) return;
+    while (c.up_off < c.up_out.size()) {
+      const ssize_t w = write(c.up, c.up_out.data() + c.up_off, c.up_out.size() - c.up_off);
+      if (w > 0) { c.up_off += (size_t)w; continue; }
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == ENOTCONN)) return;   // EPOLLOUT resumes
+      upstream_closed(c);
+      return;
+    }
+    c.up_out.clear();
+    c.up_off = 0;
+  }
+
+  void upstream_closed(Conn& c) {
+    if (c.up < 0) return;
+    epoll_ctl(ep_, EPOLL_CTL_DEL, c.up, nullptr);
+    up2c_.erase(c.up);
+    close(c.up);
+    c.up = -1;
+    if (c.tunnel) {                    // the stream ended: deliver what is left, then close
+      if (!c.up_in.empty()) { c.out += c.up_in; c.up_in.clear(); }
+      c.close_after = true;
+      flush(c);
+      return;
+    }
+    if (c.async) {                     // no (complete) answer came back
+      if (!c.up_in.empty() && c.up_in.find("\r\n\r\n") != std::string::npos && !c.up_in.empty()) {
+        c.out += c.up_in;              // read-until-close body
+        c.up_in.clear();
+        c.close_after = true;
+      } else {
+        c.async = false;
+        respond(c, 502, "{\"error\":\"upstream app closed the connection\"}", "", true);
+      }
+      flush(c);
+    }
+  }
+
+  void on_upstream(Conn& c, uint32_t events) {
+    if (events & EPOLLOUT) {
+      flush_up(c);
+      if (c.up >= 0 && c.up_out.empty()) {
+        epoll_event e{};
+        e.events = EPOLLIN;
+        e.data.fd = c.up;
+        epoll_ctl(ep_, EPOLL_CTL_MOD, c.up, &e);
+      }
+    }
+    if (c.up < 0 || !(events & (EPOLLIN | EPOLLHUP | EPOLLERR))) return;
+    char buf[65536];
+    bool eof = false;
+    while (true) {
+      const ssize_t r = read(c.up, buf, sizeof buf);
+      if (r > 0) { c.up_in.append(buf, (size_t)r); continue; }
+      if (r == 0) { eof = true; break; }
+      if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+      eof = true;
+      break;
+    }
+    if (c.tunnel) {
+      c.out += c.up_in;
+      c.up_in.clear();
+      flush(c);
+    } else {
+      parse_upstream(c);
+    }
+    if (eof) upstream_closed(c);
+  }
+
+  // one relayed response: status line + headers + (content-length | chunked -> tunnel | none)
+  void parse_upstream(Conn& c) {
+    while (c.async && !c.up_in.empty()) {
+      const size_t hend = c.up_in.find("\r\n\r\n");
+      if (hend == std::string::npos) return;
+      int code = 0;
+      if (c.up_in.size() > 12) code = std::atoi(c.up_in.c_str() + 9);
+      if (code >= 100 && code < 200) {         // interim (100 Continue): the client had its own
+        c.up_in.erase(0, hend + 4);
+        continue;
+      }
+      size_t clen = 0;
+      bool has_len = false, chunked = false;
+      size_t ls = c.up_in.find("\r\n") + 2;
+      while (ls < hend) {
+        const size_t le = c.up_in.find("\r\n", ls);
+        const size_t colon = c.up_in.find(':', ls);
+        if (colon != std::string::npos && colon < le) {
+          const char* k = c.up_in.data() + ls;
+          const size_t kn = colon - ls;
+          size_t vs = colon + 1;
+          while (vs < le && c.up_in[vs] == ' ') ++vs;
+          if (ieq(k, kn, "content-length")) {
+            clen = (size_t)std::strtoull(c.up_in.c_str() + vs, nullptr, 10);
+            has_len = true;
+          } else if (ieq(k, kn, "transfer-encoding")) {
+            chunked = true;
+          }
+        }
+        ls = le + 2;
+      }
+      const bool no_body = c.up_head || code == 204 || code == 304;
+      if (chunked && !no_body) {       // streamed answer (SSE): tunnel from here on
+        c.tunnel = true;
+        c.async = false;
+        c.out += c.up_in;
+        c.up_in.clear();
+        c.up_out += c.in;              // anything the client already sent follows raw
+        c.in.clear();
+        flush_up(c);
+        flush(c);
+        return;
+      }
+      if (!has_len && !no_body) return;          // body until close (upstream_closed delivers it)
+      const size_t total = hend + 4 + (no_body ? 0 : clen);
+      if (c.up_in.size() < total) return;
+      c.out.append(c.up_in, 0, total);
+      c.up_in.erase(0, total);
+      c.async = false;
+      flush(c);
+      if (!c.close_after) {
+        parse_requests(c);                       // requests that arrived meanwhile
+        if (c.out.size() > c.out_off) flush(c);
+      }
+    }
   }
 
   void run_batch() {
@@ -528,7 +849,7 @@ class Reactor {
     e.events = EPOLLIN;
     e.data.fd = c.fd;
     epoll_ctl(ep_, EPOLL_CTL_MOD, c.fd, &e);
-    if (c.close_after) to_close_.push_back(c.fd);
+    if (c.close_after && !c.async) to_close_.push_back(c.fd);
   }
 };
 
@@ -540,7 +861,9 @@ struct Server {
   std::vector<std::thread> threads;
   std::vector<PersistentScorer*> scorers;
   std::vector<std::unique_ptr<std::mutex>> scorer_mus;
+  std::vector<std::unique_ptr<RouteService>> routes;      // one per GPU
   ~Server() {
+    routes.clear();                                          // joins the route workers
     for (PersistentScorer* p : scorers) pscore_destroy(p);   // stop + wait for the resident kernels
   }
 };
@@ -553,9 +876,11 @@ std::vector<Server*> g_servers;
 int64_t native_server_start(int port, int threads, const std::vector<int>& devices,
                             const std::vector<const void*>& blobs, const std::vector<int>& num_cus, int H,
                             const NormParams& np, int variant, int max_batch, const std::vector<std::string>& cors,
-                            bool cors_vercel, bool bind_any, std::string& err) {
-  if (devices.empty() || devices.size() != blobs.size() || devices.size() != num_cus.size()) {
-    err = "devices/blobs mismatch";
+                            bool cors_vercel, bool bind_any, int upstream_port,
+                            const std::vector<RouteServiceCfg>& routes, std::string& err) {
+  if (devices.empty() || devices.size() != blobs.size() || devices.size() != num_cus.size() ||
+      (!routes.empty() && routes.size() != devices.size())) {
+    err = "devices/blobs/routes mismatch";
     return -1;
   }
   auto* s = new Server();
@@ -567,6 +892,7 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
   s->cfg.max_batch = max_batch;
   s->cfg.cors_exact = cors;
   s->cfg.cors_vercel = cors_vercel;
+  s->cfg.upstream_port = upstream_port;
   if (const char* v = std::getenv("ROUTEST_PERSIST_IDLE_MS")) s->cfg.persist_idle_ms = std::atof(v);
   if (const char* v = std::getenv("ROUTEST_PERSIST_CAP")) s->cfg.persist_cap = std::atoi(v);
   if (const char* v = std::getenv("ROUTEST_PERSIST_LIFE_MS")) s->cfg.persist_life_ms = std::atof(v);
@@ -596,6 +922,19 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
     }
     s->reactors.push_back(std::move(r));
   }
+  // one route service per GPU; a finished job goes back to the reactor that parsed it
+  for (size_t g = 0; g < routes.size(); ++g) {
+    RouteServiceCfg rc = routes[g];
+    if (!s->scorers.empty()) {
+      rc.scorer = s->scorers[g];
+      rc.scorer_mu = s->scorer_mus[g].get();
+    }
+    s->routes.push_back(std::make_unique<RouteService>(rc, [](RouteJob* j) {
+      static_cast<JobTag*>(j->tag)->reactor->job_done(j);
+    }));
+  }
+  if (!s->routes.empty())
+    for (int i = 0; i < s->cfg.threads; ++i) s->reactors[i]->set_routes(s->routes[(size_t)i % devices.size()].get());
   for (auto& r : s->reactors) s->threads.emplace_back([rp = r.get()]() { rp->run(); });
   std::lock_guard<std::mutex> lk(g_srv_mu);
   g_servers.push_back(s);
@@ -622,11 +961,19 @@ void native_server_stop(int64_t h) {
 
 std::vector<long long> native_server_stats(int64_t h) {
   std::lock_guard<std::mutex> lk(g_srv_mu);
-  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(7, 0);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(16, 0);
   Server* s = g_servers[h];
-  return {s->stats.requests.load(), s->stats.predictions.load(), s->stats.launches.load(),
-          s->stats.errors.load(), s->stats.resident.load(), s->stats.fallbacks.load(),
-          s->stats.wire8.load()};
+  std::vector<long long> v = {s->stats.requests.load(), s->stats.predictions.load(), s->stats.launches.load(),
+                              s->stats.errors.load(), s->stats.resident.load(), s->stats.fallbacks.load(),
+                              s->stats.wire8.load(), s->stats.route_requests.load(),
+                              s->stats.route_fallbacks.load(), s->stats.relayed.load()};
+  std::vector<long long> rs(6, 0);
+  for (auto& r : s->routes) {
+    const auto x = r->stats();
+    for (size_t i = 0; i < rs.size(); ++i) rs[i] += x[i];
+  }
+  v.insert(v.end(), rs.begin(), rs.end());
+  return v;
 }
 
 }  // namespace rt

@@ -137,11 +137,13 @@ void pscore_stats(PersistentScorer* s, long long* launches, long long* served, l
 hipError_t pscore_run(PersistentScorer* s, int n, double timeout_ms);
 void pscore_destroy(PersistentScorer* s);
 
-// ---- native prediction front end : native_server.hip ----
+// ---- native front end (predictions, routes, relay to the Python app) : native_server.hip ----
+struct RouteServiceCfg;   // route_service.h
 int64_t native_server_start(int port, int threads, const std::vector<int>& devices,
                             const std::vector<const void*>& blobs, const std::vector<int>& num_cus, int H,
                             const NormParams& np, int variant, int max_batch, const std::vector<std::string>& cors,
-                            bool cors_vercel, bool bind_any, std::string& err);
+                            bool cors_vercel, bool bind_any, int upstream_port,
+                            const std::vector<RouteServiceCfg>& routes, std::string& err);
 void native_server_stop(int64_t h);
 std::vector<long long> native_server_stats(int64_t h);
 

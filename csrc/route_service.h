@@ -1,0 +1,95 @@
+// Native route service (csrc/route_service.hip): request/response types shared with the native
+// front end (csrc/native_server.hip).
+#pragma once
+#include <cmath>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "runtime/route_core.h"
+
+#include <mutex>
+
+namespace rt {
+
+struct PersistentScorer;
+
+struct RouteServiceCfg {
+  int device = 0;
+  int provider = 0;                       // 0 haversine, 1 road graph (A*)
+  double circuity = 1.3, step_m = 150.0;  // HaversineProvider (routing/providers.py)
+  std::string engine = "backend:mi355x";
+  bool compat200 = true;                  // /api/request_route answers errors with 200 (reference)
+  int batch_max = 1024;
+  double timeout_us = 500.0;
+  // road graph, host side (assembly, snapping, exact fallback)
+  const double* glat = nullptr;
+  const double* glon = nullptr;
+  int N = 0;
+  double snap_c = 1.0;
+  const int* h_indptr = nullptr;
+  const int* h_indices = nullptr;
+  const float* h_cost = nullptr;
+  // road graph, device side (routing/graph.py BatchedAstar's tensors)
+  const int* indptr = nullptr;
+  const int* indices = nullptr;
+  const float* cost = nullptr;
+  const float* lat32 = nullptr;
+  const float* lon32 = nullptr;
+  const float* lm = nullptr;
+  int K = 0;
+  void* state = nullptr;
+  void* heap = nullptr;
+  int* touched = nullptr;
+  float* hcache = nullptr;
+  int slots = 0, cap = 0, max_path = 4096, max_iters = 2000000, lane_pops = 500, wave_slots = 0;
+  float inv_vmax = 0.f, wave_delta = 10.f;
+  // ETA model for use_ml_eta (the fused K1+K2 kernel's 32x32 weight blob on this device)
+  const void* eta_blob = nullptr;
+  int H = 0, variant = -1, num_cus = 256;
+  NormParams np{};
+  // persistence: SQLite database path/URI of the Python store ("" = none)
+  std::string sqlite_path;
+  // the GPU's resident single-request scorer (persistent_serve.hip): parked before each flush's
+  // launches so they never queue behind it on a shared hardware queue
+  PersistentScorer* scorer = nullptr;
+  std::mutex* scorer_mu = nullptr;
+};
+
+// One request handed from a reactor to the service and back.
+struct RouteJob {
+  std::string body;                 // request body
+  bool json_ok = true;              // content-type is JSON
+  bool request_route = false;       // /api/request_route (non-silent JSON, never persisted)
+  void* tag = nullptr;              // reactor-owned context
+  // result: fallback (hand to the Python app) or status + bytes
+  bool fallback = false;
+  int status = 0;
+  std::string out;
+  // internal
+  rtj::Value root;
+  rtr::RouteReq req;
+  rtr::Plan plan;
+  std::vector<std::vector<std::pair<double, double>>> calls;
+  std::vector<int32_t> nodes;
+  rtr::Assembled asmb;
+  float eta_min = NAN;
+  std::string eta_iso, request_id;
+  rtc::Stamp now;
+};
+
+class RouteService {
+ public:
+  RouteService(const RouteServiceCfg& cfg, std::function<void(RouteJob*)> done);
+  ~RouteService();
+  void submit(RouteJob* j);
+  // jobs, flushes, fallbacks, legs searched, legs finished on the host, rows persisted
+  std::vector<long long> stats() const;
+
+ private:
+  struct Impl;
+  Impl* p_;
+};
+
+}  // namespace rt

@@ -1,0 +1,705 @@
+// Native route service: /api/optimize_route, /route and /api/request_route answered without Python
+// (reference RO/Flaskr/routes.py:29-50,89-127 -> RO/Flaskr/utils.py:10-201; Python equivalent
+// routest_amd/routing/route_batcher.py + optimizer.py + api/app.py _optimize).
+//
+// One worker thread per GPU pulls the requests the native front end's reactors parsed off their
+// sockets, and flushes them together (batch_max requests or timeout_us after the first):
+//   1. parse + validate every request (csrc/runtime/route_core.h RouteReq; unusual inputs are
+//      handed back for the Python app);
+//   2. ONE K5 + ONE K6 launch for every multi-stop request of the flush (csrc/route_kernels.hip);
+//      only the trips and, for infeasible requests, the depot row of D come back to the host;
+//   3. road-graph provider: every waypoint snapped (NodeGrid), the flush's unique legs searched by
+//      the batched A* (csrc/astar.hip: lane stage, then one wave per long search, exact host
+//      Dijkstra for the rare search that exhausts both), and the found paths COMPACTED on the GPU
+//      into one flat array before the copy-out (a leg row is max_path ints; a path is ~200);
+//   4. responses assembled on a thread pool (route_core.h: byte-identical to the FastAPI handler);
+//   5. use_ml_eta: one fused featurize+MLP launch (K1+K2) for the flush's ETA records;
+//   6. persistence of /api/optimize_route results: one SQLite transaction per flush into the same
+//      database file the Python store reads (reference routes.py:119-125, best effort);
+//   7. completed jobs go back to their reactors (eventfd wake-up), which write the bytes.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <queue>
+#include <random>
+#include <thread>
+#include <unordered_map>
+
+#include "common.h"
+#include "ops.h"
+#include "route_service.h"
+#include "runtime/sqlite_lite.h"
+
+namespace rt {
+
+namespace {
+
+// one block per found path: copy its nodes from the (Q, max_path) rows into the flat array
+__global__ void compact_paths_kernel(const int* __restrict__ rows, int max_path, const int* __restrict__ len,
+                                     const int* __restrict__ status, const long long* __restrict__ off, int Q,
+                                     int* __restrict__ flat) {
+  const int q = blockIdx.x;
+  if (q >= Q || status[q] != 0) return;
+  const int n = min(len[q], max_path);
+  const long long o = off[q];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) flat[o + i] = rows[(size_t)q * max_path + i];
+}
+
+template <class T>
+struct DevBuf {
+  T* d = nullptr;
+  size_t n = 0;
+  hipError_t need(size_t k) {
+    if (k <= n) return hipSuccess;
+    const size_t m = std::max(k, n * 3 / 2);
+    if (d) (void)hipFree(d);
+    d = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc((void**)&d, m * sizeof(T));
+    if (e == hipSuccess) n = m;
+    return e;
+  }
+  ~DevBuf() { if (d) (void)hipFree(d); }
+};
+template <class T>
+struct HostBuf {
+  T* h = nullptr;
+  size_t n = 0;
+  hipError_t need(size_t k) {
+    if (k <= n) return hipSuccess;
+    const size_t m = std::max(k, n * 3 / 2);
+    if (h) (void)hipHostFree(h);
+    h = nullptr;
+    n = 0;
+    hipError_t e = hipHostMalloc((void**)&h, m * sizeof(T), hipHostMallocDefault);
+    if (e == hipSuccess) n = m;
+    return e;
+  }
+  ~HostBuf() { if (h) (void)hipHostFree(h); }
+};
+
+inline rtc::Stamp local_now() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  struct tm lt;
+  time_t t = ts.tv_sec;
+  localtime_r(&t, &lt);
+  rtc::Stamp s;
+  s.secs = rtc::days_from_civil(lt.tm_year + 1900, (unsigned)lt.tm_mon + 1, (unsigned)lt.tm_mday) * 86400 +
+           lt.tm_hour * 3600 + lt.tm_min * 60 + lt.tm_sec;
+  s.us = (int32_t)(ts.tv_nsec / 1000);
+  return s;
+}
+
+// datetime.now(timezone.utc).isoformat() (store.py _now_iso)
+inline std::string utc_now_iso() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  rtc::Stamp tz;
+  tz.has_tz = true;
+  tz.tz_sec = 0;
+  return rtc::isoformat((int64_t)ts.tv_sec, ts.tv_nsec / 1000, tz);
+}
+
+struct Uuid4 {
+  std::mt19937_64 g{std::random_device{}() ^ ((uint64_t)std::random_device{}() << 32)};
+  std::string next() {
+    uint64_t a = g(), b = g();
+    a = (a & 0xFFFFFFFFFFFF0FFFULL) | 0x0000000000004000ULL;   // version 4
+    b = (b & 0x3FFFFFFFFFFFFFFFULL) | 0x8000000000000000ULL;   // variant 10
+    char s[37];
+    std::snprintf(s, sizeof s, "%08x-%04x-%04x-%04x-%012llx", (unsigned)(a >> 32), (unsigned)((a >> 16) & 0xFFFF),
+                  (unsigned)(a & 0xFFFF), (unsigned)(b >> 48), (unsigned long long)(b & 0xFFFFFFFFFFFFULL));
+    return s;
+  }
+};
+
+// Exact host search for the rare leg both GPU stages gave up on (graph.py _exact_fallback):
+// Dijkstra from s stopping when t is settled.
+bool host_dijkstra(const int* indptr, const int* indices, const float* cost, int N, int s, int t, int max_path,
+                   float& out_cost, std::vector<int32_t>& path) {
+  std::vector<double> dist((size_t)N, INFINITY);
+  std::vector<int32_t> par((size_t)N, -1);
+  using QE = std::pair<double, int>;
+  std::priority_queue<QE, std::vector<QE>, std::greater<QE>> pq;
+  dist[s] = 0.0;
+  pq.push({0.0, s});
+  while (!pq.empty()) {
+    auto [d, v] = pq.top();
+    pq.pop();
+    if (d > dist[v]) continue;
+    if (v == t) break;
+    for (int e = indptr[v]; e < indptr[v + 1]; ++e) {
+      const int w = indices[e];
+      const double nd = d + (double)cost[e];
+      if (nd < dist[w]) {
+        dist[w] = nd;
+        par[w] = v;
+        pq.push({nd, w});
+      }
+    }
+  }
+  if (!std::isfinite(dist[t])) return false;
+  path.clear();
+  for (int v = t; v != -1; v = par[v]) {
+    path.push_back(v);
+    if ((int)path.size() > max_path) return false;
+    if (v == s) break;
+  }
+  std::reverse(path.begin(), path.end());
+  out_cost = (float)dist[t];
+  return true;
+}
+
+}  // namespace
+
+struct RouteService::Impl {
+  RouteServiceCfg cfg;
+  std::function<void(RouteJob*)> done;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<RouteJob*> q;
+  bool stop = false;
+  std::thread th;
+  hipStream_t stream{};
+  rtr::NodeGrid grid;
+  // statistics
+  std::atomic<long long> n_jobs{0}, n_flushes{0}, n_fallback{0}, n_legs{0}, n_host_legs{0}, n_persisted{0};
+  // K5 / K6 buffers
+  HostBuf<double> h_lat, h_lon, h_dem, h_cap, h_maxd, h_row0;
+  HostBuf<int> h_npts, h_visit, h_trip, h_ntrips, h_status;
+  DevBuf<double> d_lat, d_lon, d_dem, d_cap, d_maxd, d_D;
+  DevBuf<int> d_npts, d_visit, d_trip, d_ntrips, d_status;
+  // A* buffers
+  HostBuf<int> h_src, h_dst, h_len, h_st, h_qidx, h_flat;
+  HostBuf<float> h_cost;
+  HostBuf<long long> h_off;
+  DevBuf<int> d_src, d_dst, d_len, d_st, d_path, d_qidx, d_flat, d_iters;
+  DevBuf<float> d_cost;
+  DevBuf<long long> d_off;
+  // ETA
+  HostBuf<rtc::EtaRecord> h_rec;
+  HostBuf<float> h_eta;
+  DevBuf<rtc::EtaRecord> d_rec;
+  DevBuf<float> d_eta;
+  // store
+  rtsql::Api sql;
+  void* db = nullptr;
+  void* st_req = nullptr;
+  void* st_res = nullptr;
+  Uuid4 uuid;
+
+  void open_store() {
+    if (cfg.sqlite_path.empty()) return;
+    std::string err;
+    if (!sql.load(err)) return;
+    if (sql.open_v2(cfg.sqlite_path.c_str(), &db, rtsql::OPEN_READWRITE | rtsql::OPEN_URI | rtsql::OPEN_NOMUTEX,
+                    nullptr) != rtsql::OK) {
+      if (db) sql.close(db);
+      db = nullptr;
+      return;
+    }
+    sql.busy_timeout(db, 10000);
+    sql.exec(db, "PRAGMA journal_mode=WAL", nullptr, nullptr, nullptr);
+    sql.exec(db, "PRAGMA foreign_keys=ON", nullptr, nullptr, nullptr);
+    const char* q1 = "INSERT INTO route_requests(id,origin_id,stops,request_time,status,engine,vehicle_id,driver_age)"
+                     " VALUES(?,?,?,?,?,?,?,?)";
+    const char* q2 = "INSERT INTO route_results(id,request_id,optimized_order,total_distance,total_duration,legs,"
+                     "geometry,eta_minutes_ml,eta_completion_time_ml,created_at) VALUES(?,?,?,?,?,?,?,?,?,?)";
+    if (sql.prepare_v2(db, q1, -1, &st_req, nullptr) != rtsql::OK ||
+        sql.prepare_v2(db, q2, -1, &st_res, nullptr) != rtsql::OK) {
+      if (st_req) sql.finalize(st_req);
+      if (st_res) sql.finalize(st_res);
+      st_req = st_res = nullptr;
+      sql.close(db);
+      db = nullptr;
+    }
+  }
+
+  // bind a JSON value like Python's sqlite3 adapter binds the corresponding object; false for
+  // objects sqlite3 cannot bind (list / dict raise -> the persist fails, best effort)
+  bool bind_value(void* st, int i, const rtj::Value* v) {
+    if (!v || v->kind == rtj::Value::Null) return sql.bind_null(st, i) == rtsql::OK;
+    switch (v->kind) {
+      case rtj::Value::Bool: return sql.bind_int64(st, i, v->b ? 1 : 0) == rtsql::OK;
+      case rtj::Value::Str: return sql.bind_text(st, i, v->str.data(), (int)v->str.size(), rtsql::TRANSIENT) == rtsql::OK;
+      case rtj::Value::Num:
+        if (v->is_int && std::fabs(v->num) < 9.0e15) return sql.bind_int64(st, i, (long long)v->num) == rtsql::OK;
+        return sql.bind_double(st, i, v->num) == rtsql::OK;
+      default: return false;
+    }
+  }
+  bool bind_text(void* st, int i, const std::string& s) {
+    return sql.bind_text(st, i, s.data(), (int)s.size(), rtsql::TRANSIENT) == rtsql::OK;
+  }
+
+  // store.py build_rows + SQLiteStore.persist_request_and_result for one job; "" on failure
+  std::string persist_one(RouteJob* j, const std::string& now) {
+    const rtj::Value* root = j->req.root;
+    const rtj::Value* meta = root->get("meta");
+    if (meta && meta->truthy() && meta->kind != rtj::Value::Obj) return "";   // .get on a non-dict
+    if (meta && !meta->truthy()) meta = nullptr;
+    const rtj::Value* drv = root->get("driver_details");
+    if (drv && !drv->truthy()) drv = nullptr;
+    std::string stops = "{\"destination_ids\":";
+    const rtj::Value* ids = meta ? meta->get("destination_ids") : nullptr;
+    if (ids && ids->truthy()) { if (!rtr::put_value(stops, *ids)) return ""; }
+    else stops += "[]";
+    stops += ",\"destination_points\":";
+    if (!rtr::put_value(stops, *root->get("destination_points"))) return "";
+    stops += '}';
+    const std::string rid = uuid.next();
+    const rtr::Assembled& a = j->asmb;
+    sql.reset(st_req);
+    sql.clear_bindings(st_req);
+    const rtj::Value* ue = root->get("use_ml_eta");
+    bool ok = bind_text(st_req, 1, rid) && bind_value(st_req, 2, meta ? meta->get("origin_id") : nullptr) &&
+              bind_text(st_req, 3, stops) && bind_text(st_req, 4, now) && bind_text(st_req, 5, "completed") &&
+              bind_text(st_req, 6, (ue && ue->truthy()) ? "ml" : "default") &&
+              bind_value(st_req, 7, drv ? drv->get("driver_name") : nullptr) &&
+              bind_value(st_req, 8, drv ? drv->get("driver_age") : nullptr);
+    if (!ok || sql.step(st_req) != rtsql::DONE) return "";
+    sql.reset(st_res);
+    sql.clear_bindings(st_res);
+    std::string geom = "{\"type\":\"LineString\",\"coordinates\":";
+    geom += a.coords;
+    geom += '}';
+    ok = bind_text(st_res, 1, uuid.next()) && bind_text(st_res, 2, rid) && bind_text(st_res, 3, a.order) &&
+         sql.bind_double(st_res, 4, rtr::py_round(a.dist, 2)) == rtsql::OK &&
+         sql.bind_double(st_res, 5, rtr::py_round(a.dur, 2)) == rtsql::OK && bind_text(st_res, 6, a.segments) &&
+         bind_text(st_res, 7, geom);
+    if (ok && !j->eta_iso.empty()) {
+      ok = sql.bind_double(st_res, 8, (double)j->eta_min) == rtsql::OK && bind_text(st_res, 9, j->eta_iso);
+    } else if (ok) {
+      ok = sql.bind_null(st_res, 8) == rtsql::OK && sql.bind_null(st_res, 9) == rtsql::OK;
+    }
+    ok = ok && bind_text(st_res, 10, now);
+    if (!ok || sql.step(st_res) != rtsql::DONE) return "";
+    return rid;
+  }
+
+  void run() {
+    if (hipSetDevice(cfg.device) != hipSuccess) return;
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return;
+    open_store();
+    std::vector<RouteJob*> batch;
+    while (true) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return stop || !q.empty(); });
+        if (stop && q.empty()) break;
+        // collect: up to batch_max, or timeout_us after the first arrival
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds((long long)cfg.timeout_us);
+        while ((int)q.size() < cfg.batch_max && !stop) {
+          if (cv.wait_until(lk, deadline) == std::cv_status::timeout) break;
+        }
+        const size_t take = std::min<size_t>(q.size(), (size_t)cfg.batch_max);
+        batch.assign(q.begin(), q.begin() + take);
+        q.erase(q.begin(), q.begin() + take);
+      }
+      process(batch);
+      n_flushes.fetch_add(1, std::memory_order_relaxed);
+      for (RouteJob* j : batch) done(j);
+      batch.clear();
+    }
+    if (st_req) sql.finalize(st_req);
+    if (st_res) sql.finalize(st_res);
+    if (db) sql.close(db);
+    (void)hipStreamDestroy(stream);
+  }
+
+  void fail_all(std::vector<RouteJob*>& jobs, const char* msg) {
+    for (RouteJob* j : jobs) {
+      if (j->fallback || j->status) continue;
+      j->status = 503;
+      j->out = rtr::error_body(msg);
+    }
+  }
+
+  bool plan_multi(std::vector<RouteJob*>& jobs) {
+    std::vector<RouteJob*> m;
+    for (RouteJob* j : jobs)
+      if (!j->fallback && j->req.error.empty() && j->req.dst.size() > 1) m.push_back(j);
+    if (m.empty()) return true;
+    const int R = (int)m.size();
+    int NM = 1;
+    for (RouteJob* j : m) NM = std::max(NM, (int)j->req.dst.size() + 1);
+    if (NM > 4096) {   // beyond the greedy kernel's LDS scan: CPU greedy for those (never in the UI)
+      for (RouteJob* j : m) j->fallback = true;
+      return true;
+    }
+    const size_t RN = (size_t)R * NM;
+    if (h_lat.need(RN) || h_lon.need(RN) || h_dem.need(RN) || h_npts.need(R) || h_cap.need(R) || h_maxd.need(R) ||
+        h_visit.need(RN) || h_trip.need(RN) || h_ntrips.need(R) || h_status.need(R) || h_row0.need(RN) ||
+        d_lat.need(RN) || d_lon.need(RN) || d_dem.need(RN) || d_npts.need(R) || d_cap.need(R) || d_maxd.need(R) ||
+        d_D.need(RN * NM) || d_visit.need(RN) || d_trip.need(RN) || d_ntrips.need(R) || d_status.need(R))
+      return false;
+    for (int k = 0; k < R; ++k) {
+      const rtr::RouteReq& r = m[k]->req;
+      const int n = (int)r.dst.size() + 1;
+      double* la = h_lat.h + (size_t)k * NM;
+      double* lo = h_lon.h + (size_t)k * NM;
+      double* de = h_dem.h + (size_t)k * NM;
+      std::fill(la, la + NM, 0.0);
+      std::fill(lo, lo + NM, 0.0);
+      std::fill(de, de + NM, 0.0);
+      la[0] = r.src.lat;
+      lo[0] = r.src.lon;
+      for (int i = 1; i < n; ++i) {
+        la[i] = r.dst[i - 1].lat;
+        lo[i] = r.dst[i - 1].lon;
+        de[i] = r.dst[i - 1].demand;
+      }
+      h_npts.h[k] = n;
+      h_cap.h[k] = r.cap;
+      h_maxd.h[k] = r.maxd;
+    }
+    hipError_t e = hipSuccess;
+    auto cp = [&](void* d, const void* h, size_t b) {
+      if (e == hipSuccess) e = hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, stream);
+    };
+    cp(d_lat.d, h_lat.h, RN * 8);
+    cp(d_lon.d, h_lon.h, RN * 8);
+    cp(d_dem.d, h_dem.h, RN * 8);
+    cp(d_npts.d, h_npts.h, (size_t)R * 4);
+    cp(d_cap.d, h_cap.h, (size_t)R * 8);
+    cp(d_maxd.d, h_maxd.h, (size_t)R * 8);
+    if (e == hipSuccess) e = launch_haversine_matrix(d_lat.d, d_lon.d, d_npts.d, R, NM, cfg.circuity, d_D.d, stream);
+    if (e == hipSuccess)
+      e = launch_greedy_cvrp(d_D.d, d_npts.d, d_dem.d, d_cap.d, d_maxd.d, R, NM, d_visit.d, d_trip.d, d_ntrips.d,
+                             d_status.d, stream);
+    auto back = [&](void* h, const void* d, size_t b) {
+      if (e == hipSuccess) e = hipMemcpyAsync(h, d, b, hipMemcpyDeviceToHost, stream);
+    };
+    back(h_visit.h, d_visit.d, RN * 4);
+    back(h_trip.h, d_trip.d, RN * 4);
+    back(h_ntrips.h, d_ntrips.d, (size_t)R * 4);
+    back(h_status.h, d_status.d, (size_t)R * 4);
+    // the depot row of every D (the infeasible-stop order key) — the matrices stay on the GPU
+    if (e == hipSuccess)
+      e = hipMemcpy2DAsync(h_row0.h, (size_t)NM * 8, d_D.d, (size_t)NM * NM * 8, (size_t)NM * 8, (size_t)R,
+                           hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return false;
+    for (int k = 0; k < R; ++k) {
+      rtr::Plan& p = m[k]->plan;
+      const int n = h_npts.h[k];
+      const int* vis = h_visit.h + (size_t)k * NM;
+      const int* tof = h_trip.h + (size_t)k * NM;
+      if (h_status.h[k] != 0) {           // batched.py _unpack: unplaced stops by depot distance
+        std::vector<char> placed(n, 0);
+        for (int i = 0; i < NM && vis[i] >= 0; ++i) placed[vis[i]] = 1;
+        std::vector<int> rest;
+        for (int i = 1; i < n; ++i)
+          if (!placed[i]) rest.push_back(i);
+        const double* d0 = h_row0.h + (size_t)k * NM;
+        std::stable_sort(rest.begin(), rest.end(), [&](int a, int b) { return d0[a] < d0[b]; });
+        p.infeasible = true;
+        for (int i : rest) p.infeasible_stops.push_back(i - 1);
+        continue;
+      }
+      p.trips.assign(h_ntrips.h[k], std::vector<int>{0});
+      for (int i = 0; i < NM && vis[i] >= 0; ++i) p.trips[tof[i]].push_back(vis[i]);
+      for (auto& t : p.trips) t.push_back(0);
+    }
+    return true;
+  }
+
+  // graph provider: snap, search every unique leg of the flush once, fill `legs` / `leg_of`
+  std::vector<rtr::Leg> legs;
+  std::vector<std::vector<int32_t>> host_paths;
+  std::unordered_map<uint64_t, int> leg_index;
+
+  bool search_legs(std::vector<RouteJob*>& jobs) {
+    legs.clear();
+    host_paths.clear();
+    leg_index.clear();
+    std::vector<RouteJob*> g;
+    for (RouteJob* j : jobs)
+      if (!j->fallback && !j->calls.empty()) g.push_back(j);
+    rtc::parallel_chunks(g.size(), 64, 16, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        RouteJob* j = g[i];
+        j->nodes.clear();
+        for (const auto& c : j->calls)
+          for (const auto& pt : c) j->nodes.push_back(grid.nearest(pt.second, pt.first, cfg.snap_c));
+      }
+    });
+    std::vector<std::pair<int, int>> pairs;
+    for (RouteJob* j : g) {
+      size_t off = 0;
+      for (const auto& c : j->calls) {
+        for (size_t i = 0; i + 1 < c.size(); ++i) {
+          const uint64_t key = ((uint64_t)(uint32_t)j->nodes[off + i] << 32) | (uint32_t)j->nodes[off + i + 1];
+          if (leg_index.emplace(key, (int)pairs.size()).second) pairs.emplace_back(j->nodes[off + i], j->nodes[off + i + 1]);
+        }
+        off += c.size();
+      }
+    }
+    const int Q = (int)pairs.size();
+    legs.assign(Q, rtr::Leg());
+    if (Q == 0) return true;
+    n_legs.fetch_add(Q, std::memory_order_relaxed);
+    const int MP = cfg.max_path;
+    if (h_src.need(Q) || h_dst.need(Q) || h_len.need(Q) || h_st.need(Q) || h_cost.need(Q) || h_off.need(Q) ||
+        h_qidx.need(Q) || d_src.need(Q) || d_dst.need(Q) || d_len.need(Q) || d_st.need(Q) || d_cost.need(Q) ||
+        d_off.need(Q) || d_qidx.need(Q) || d_iters.need(Q) || d_path.need((size_t)Q * MP))
+      return false;
+    for (int i = 0; i < Q; ++i) {
+      h_src.h[i] = pairs[i].first;
+      h_dst.h[i] = pairs[i].second;
+    }
+    hipError_t e = hipMemcpyAsync(d_src.d, h_src.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_dst.d, h_dst.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
+    const int lane_iters = cfg.lane_pops > 0 ? std::min(cfg.max_iters, cfg.lane_pops) : cfg.max_iters;
+    for (int q0 = 0; q0 < Q && e == hipSuccess; q0 += cfg.slots)
+      e = launch_astar(cfg.indptr, cfg.indices, cfg.cost, cfg.lat32, cfg.lon32, d_src.d, d_dst.d, cfg.state, cfg.heap,
+                       cfg.touched, d_cost.d, d_len.d, d_st.d, d_path.d, cfg.N, Q, q0, cfg.slots, cfg.cap, MP,
+                       lane_iters, cfg.inv_vmax, cfg.lm, cfg.K, stream, d_iters.d);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return false;
+    if (lane_iters < cfg.max_iters && cfg.hcache != nullptr) {
+      int T = 0;
+      for (int i = 0; i < Q; ++i)
+        if (h_st.h[i] == 3) h_qidx.h[T++] = i;
+      if (T > 0) {
+        e = hipMemcpyAsync(d_qidx.d, h_qidx.h, (size_t)T * 4, hipMemcpyHostToDevice, stream);
+        for (int i0 = 0; i0 < T && e == hipSuccess; i0 += cfg.wave_slots)
+          e = launch_astar_wave(cfg.indptr, cfg.indices, cfg.cost, cfg.lat32, cfg.lon32, d_src.d, d_dst.d, cfg.state,
+                                cfg.heap, cfg.touched, d_cost.d, d_len.d, d_st.d, d_path.d, cfg.N, Q, cfg.slots,
+                                cfg.cap, MP, cfg.max_iters, cfg.inv_vmax, cfg.lm, cfg.K, d_qidx.d + i0,
+                                std::min(cfg.wave_slots, T - i0), cfg.wave_delta, cfg.hcache, cfg.wave_slots, stream,
+                                d_iters.d);
+      }
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_len.h, d_len.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_cost.h, d_cost.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return false;
+    long long total = 0;
+    for (int i = 0; i < Q; ++i) {
+      h_off.h[i] = total;
+      if (h_st.h[i] == 0) total += std::min(h_len.h[i], MP);
+    }
+    if (total > 0) {
+      if (h_flat.need((size_t)total) || d_flat.need((size_t)total)) return false;
+      e = hipMemcpyAsync(d_off.d, h_off.h, (size_t)Q * 8, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(compact_paths_kernel, dim3(Q), dim3(256), 0, stream, d_path.d, MP, d_len.d, d_st.d, d_off.d,
+                           Q, d_flat.d);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess) e = hipMemcpyAsync(h_flat.h, d_flat.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return false;
+    }
+    // searches both GPU stages gave up on (status 2 / 3): exact on the host, like graph.py
+    int nbad = 0;
+    for (int i = 0; i < Q; ++i) nbad += (h_st.h[i] == 2 || h_st.h[i] == 3);
+    host_paths.resize(Q);
+    for (int i = 0; i < Q; ++i) {
+      rtr::Leg& L = legs[i];
+      if (h_st.h[i] == 0) {
+        L.sec = h_cost.h[i];
+        L.len = std::min(h_len.h[i], MP);
+        L.path = h_flat.h + h_off.h[i];
+      } else if ((h_st.h[i] == 2 || h_st.h[i] == 3) && nbad <= 1024 && cfg.h_indptr != nullptr) {
+        float c;
+        if (host_dijkstra(cfg.h_indptr, cfg.h_indices, cfg.h_cost, cfg.N, pairs[i].first, pairs[i].second, MP, c,
+                          host_paths[i])) {
+          L.sec = c;
+          L.len = (int)host_paths[i].size();
+          L.path = host_paths[i].data();
+          n_host_legs.fetch_add(1, std::memory_order_relaxed);
+        }
+      }
+    }
+    return true;
+  }
+
+  void assemble_all(std::vector<RouteJob*>& jobs) {
+    rtc::parallel_chunks(jobs.size(), 8, 16, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        RouteJob* j = jobs[i];
+        if (j->fallback || j->status) continue;
+        std::vector<rtr::Dir> dirs(j->calls.size());
+        std::string perr;
+        size_t off = 0;
+        for (size_t k = 0; k < j->calls.size() && perr.empty(); ++k) {
+          if (cfg.provider == 0) {
+            rtr::haversine_directions(j->calls[k], j->req.profile, cfg.circuity, cfg.step_m, dirs[k]);
+          } else {
+            std::vector<const rtr::Leg*> lp;
+            for (size_t t = 0; t + 1 < j->calls[k].size(); ++t) {
+              const uint64_t key = ((uint64_t)(uint32_t)j->nodes[off + t] << 32) | (uint32_t)j->nodes[off + t + 1];
+              lp.push_back(&legs[leg_index.at(key)]);
+            }
+            perr = rtr::graph_directions(j->calls[k], j->nodes.data() + off, lp, j->req.profile, cfg.glat, cfg.glon,
+                                         dirs[k]);
+            off += j->calls[k].size();
+          }
+        }
+        if (!perr.empty()) j->req.error = perr;
+        if (!rtr::assemble(j->req, j->plan, dirs, cfg.engine, j->asmb)) j->fallback = true;
+      }
+    });
+  }
+
+  bool run_eta(std::vector<RouteJob*>& jobs) {
+    std::vector<RouteJob*> m;
+    for (RouteJob* j : jobs)
+      if (!j->fallback && !j->status && j->asmb.ok && j->req.use_ml_eta && j->req.eta_ok) m.push_back(j);
+    if (m.empty() || cfg.eta_blob == nullptr) return true;
+    const int n = (int)m.size();
+    if (h_rec.need(n) || h_eta.need(n) || d_rec.need(n) || d_eta.need(n)) return false;
+    const rtc::Stamp now = local_now();
+    for (int k = 0; k < n; ++k) {
+      RouteJob* j = m[k];
+      j->now = now;
+      rtc::EtaRecord& r = h_rec.h[k];
+      r.distance_m = (float)j->asmb.dist;
+      r.driver_age = (float)j->req.eta_age;
+      r.wallclock_s = (int32_t)(now.secs - rtc::EPOCH2020_DAYS * 86400);
+      r.weather = j->req.eta_weather;
+      r.traffic = j->req.eta_traffic;
+      r.pad = 0;
+    }
+    hipError_t e = hipMemcpyAsync(d_rec.d, h_rec.h, (size_t)n * 16, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess)
+      e = launch_eta_mlp3_fwd(d_rec.d, d_eta.d, n, cfg.eta_blob, cfg.H, cfg.np, cfg.variant, cfg.num_cus, stream, 16);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_eta.h, d_eta.d, (size_t)n * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return false;
+    for (int k = 0; k < n; ++k) {
+      RouteJob* j = m[k];
+      const double mins = (double)h_eta.h[k];
+      // EtaService.finish: pickup + timedelta(minutes) — raises (-> no ETA fields) when out of range
+      if (!std::isfinite(mins) || std::fabs(mins) > 1.4e9) continue;
+      std::string tmp;
+      rtc::format_one(tmp, mins, now.secs, now.us, false, 0, "");
+      // {"eta_minutes_ml":X,"eta_completion_time_ml":"..."}: keep the iso text
+      const size_t a = tmp.find("\"eta_completion_time_ml\":\"");
+      if (a == std::string::npos) continue;
+      const size_t b0 = a + 26;
+      j->eta_iso = tmp.substr(b0, tmp.size() - 2 - b0);
+      j->eta_min = h_eta.h[k];
+    }
+    return true;
+  }
+
+  void process(std::vector<RouteJob*>& jobs) {
+    n_jobs.fetch_add((long long)jobs.size(), std::memory_order_relaxed);
+    // 1. parse
+    rtc::parallel_chunks(jobs.size(), 32, 16, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        RouteJob* j = jobs[i];
+        bool parsed = false;
+        if (j->json_ok && !j->body.empty()) {
+          try {
+            j->root = rtj::Parser(j->body.data(), j->body.size()).parse();
+            parsed = true;
+          } catch (const std::exception&) {
+          }
+        }
+        if (j->request_route && (!j->json_ok || (!parsed && !j->body.empty()))) { j->fallback = true; continue; }
+        static const rtj::Value empty = [] { rtj::Value v; v.kind = rtj::Value::Obj; return v; }();
+        const rtj::Value* rootp = parsed ? &j->root : (j->request_route ? nullptr : &empty);
+        if (!j->request_route && parsed && j->root.kind != rtj::Value::Obj) rootp = &empty;
+        j->req = rtr::parse_route_request(rootp);
+        if (j->req.fallback) j->fallback = true;
+      }
+    });
+    if (cfg.scorer != nullptr && cfg.scorer_mu != nullptr) {
+      std::lock_guard<std::mutex> lk(*cfg.scorer_mu);
+      pscore_park(cfg.scorer);
+    }
+    // 2. trips (K5 + K6)
+    if (!plan_multi(jobs)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); return; }
+    for (RouteJob* j : jobs)
+      if (!j->fallback) rtr::directions_calls(j->req, j->plan, j->calls);
+    // 3. legs (graph provider)
+    if (cfg.provider == 1 && !search_legs(jobs)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); return; }
+    // 4. assembly
+    assemble_all(jobs);
+    // 5. ETA
+    if (!run_eta(jobs)) {
+      for (RouteJob* j : jobs) j->eta_iso.clear();
+    }
+    // 6. persistence (optimize_route / route only; request_route never persists)
+    std::vector<RouteJob*> save;
+    for (RouteJob* j : jobs)
+      if (!j->fallback && !j->status && j->asmb.ok && !j->request_route) save.push_back(j);
+    if (db && !save.empty()) {
+      const std::string now = utc_now_iso();
+      for (RouteJob* j : save) {
+        // one transaction per request, like SQLiteStore (a failed insert rolls back its own rows)
+        sql.exec(db, "BEGIN", nullptr, nullptr, nullptr);
+        j->request_id = persist_one(j, now);
+        sql.exec(db, j->request_id.empty() ? "ROLLBACK" : "COMMIT", nullptr, nullptr, nullptr);
+        if (!j->request_id.empty()) n_persisted.fetch_add(1, std::memory_order_relaxed);
+      }
+    }
+    // 7. response bytes
+    for (RouteJob* j : jobs) {
+      if (j->fallback) { n_fallback.fetch_add(1, std::memory_order_relaxed); continue; }
+      if (j->status) continue;
+      if (!j->asmb.ok) {
+        j->status = (j->request_route && cfg.compat200) ? 200 : 400;
+        j->out = rtr::error_body(j->asmb.error.empty() ? j->req.error : j->asmb.error);
+        continue;
+      }
+      j->status = 200;
+      j->out = std::move(j->asmb.body);
+      if (!j->eta_iso.empty()) {
+        j->out += ",\"eta_minutes_ml\":";
+        rtr::put_float(j->out, (double)j->eta_min);
+        j->out += ",\"eta_completion_time_ml\":";
+        rtr::put_str(j->out, j->eta_iso);
+      }
+      if (!j->request_id.empty()) {
+        j->out += ",\"request_id\":";
+        rtr::put_str(j->out, j->request_id);
+        j->out += ",\"saved\":true";
+      }
+      j->out += "}}";
+    }
+  }
+};
+
+RouteService::RouteService(const RouteServiceCfg& cfg, std::function<void(RouteJob*)> done) : p_(new Impl) {
+  p_->cfg = cfg;
+  p_->done = std::move(done);
+  if (cfg.provider == 1 && cfg.glat != nullptr) p_->grid.build(cfg.glat, cfg.glon, (size_t)cfg.N, cfg.snap_c);
+  p_->th = std::thread([this] { p_->run(); });
+}
+
+RouteService::~RouteService() {
+  {
+    std::lock_guard<std::mutex> lk(p_->mu);
+    p_->stop = true;
+  }
+  p_->cv.notify_all();
+  if (p_->th.joinable()) p_->th.join();
+  delete p_;
+}
+
+void RouteService::submit(RouteJob* j) {
+  {
+    std::lock_guard<std::mutex> lk(p_->mu);
+    p_->q.push_back(j);
+  }
+  p_->cv.notify_one();
+}
+
+std::vector<long long> RouteService::stats() const {
+  return {p_->n_jobs.load(), p_->n_flushes.load(), p_->n_fallback.load(), p_->n_legs.load(),
+          p_->n_host_legs.load(), p_->n_persisted.load()};
+}
+
+}  // namespace rt

@@ -23,19 +23,24 @@ namespace rtc {
 
 struct LoadResult {
   double seconds = 0;
-  long long requests = 0, errors = 0;
+  long long requests = 0, errors = 0, bytes = 0;
   std::vector<float> lat_us;   // sorted per-request latencies
   double pct(double p) const {
     return lat_us.empty() ? 0.0 : (double)lat_us[std::min(lat_us.size() - 1, (size_t)(p * lat_us.size()))];
   }
 };
 
+inline std::string post_request(const std::string& path, const std::string& body) {
+  return "POST " + path + " HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: application/json\r\n" +
+         "Content-Length: " + std::to_string(body.size()) + "\r\n\r\n" + body;
+}
+
 // nconn connections over nthreads epoll loops; runs until `seconds` elapse or `max_requests`
-// responses (0 = unlimited) have arrived.  The first `warmup` responses per connection are not
+// responses (0 = unlimited) have arrived.  Every new request takes the next of `reqs` (whole HTTP
+// requests, cycled by a shared counter).  The first `warmup` responses per connection are not
 // recorded.
-inline LoadResult http_load(int port, int nconn, double seconds, const std::string& path,
-                            const std::string& body, int nthreads, long long max_requests = 0,
-                            int warmup = 0) {
+inline LoadResult http_load_multi(int port, int nconn, double seconds, const std::vector<std::string>& reqs,
+                                  int nthreads, long long max_requests = 0, int warmup = 0) {
   using Clock = std::chrono::steady_clock;
   struct C {
     int fd = -1;
@@ -44,9 +49,16 @@ inline LoadResult http_load(int port, int nconn, double seconds, const std::stri
     int seen = 0;
   };
   nthreads = std::max(1, std::min(nthreads, std::max(1, nconn)));
-  const std::string req = "POST " + path + " HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: application/json\r\n" +
-                          "Content-Length: " + std::to_string(body.size()) + "\r\n\r\n" + body;
-  std::atomic<long long> total{0}, errors{0};
+  std::atomic<long long> total{0}, errors{0}, bytes{0}, next{0};
+  auto send_next = [&](int fd) {
+    const std::string& req = reqs[(size_t)(next.fetch_add(1, std::memory_order_relaxed) % (long long)reqs.size())];
+    size_t off = 0;
+    while (off < req.size()) {
+      const ssize_t w = write(fd, req.data() + off, req.size() - off);
+      if (w <= 0) { errors++; return; }
+      off += (size_t)w;
+    }
+  };
   std::vector<std::vector<float>> lat(nthreads);
   const auto t_end = Clock::now() + std::chrono::microseconds((long long)(seconds * 1e6));
   auto done = [&](Clock::time_point now) {
@@ -71,7 +83,7 @@ inline LoadResult http_load(int port, int nconn, double seconds, const std::stri
       e.data.u32 = (uint32_t)i;
       epoll_ctl(ep, EPOLL_CTL_ADD, fd, &e);
       cs[i].t0 = Clock::now();
-      if (write(fd, req.data(), req.size()) != (ssize_t)req.size()) errors++;
+      send_next(fd);
     }
     std::vector<float>& L = lat[tid];
     epoll_event evs[512];
@@ -93,6 +105,7 @@ inline LoadResult http_load(int port, int nconn, double seconds, const std::stri
           if (cl != std::string::npos && cl < h) clen = std::strtoull(c.in.c_str() + cl + 15, nullptr, 10);
           if (c.in.size() < h + 4 + clen) break;
           if (c.in.compare(0, 12, "HTTP/1.1 200") != 0) errors++;
+          bytes += (long long)(h + 4 + clen);
           c.in.erase(0, h + 4 + clen);
           const auto now = Clock::now();
           if (c.seen++ >= warmup) {
@@ -101,7 +114,7 @@ inline LoadResult http_load(int port, int nconn, double seconds, const std::stri
           }
           if (!done(now)) {
             c.t0 = Clock::now();
-            if (write(c.fd, req.data(), req.size()) != (ssize_t)req.size()) errors++;
+            send_next(c.fd);
           }
         }
       }
@@ -120,7 +133,14 @@ inline LoadResult http_load(int port, int nconn, double seconds, const std::stri
   std::sort(res.lat_us.begin(), res.lat_us.end());
   res.requests = total.load();
   res.errors = errors.load();
+  res.bytes = bytes.load();
   return res;
+}
+
+inline LoadResult http_load(int port, int nconn, double seconds, const std::string& path,
+                            const std::string& body, int nthreads, long long max_requests = 0,
+                            int warmup = 0) {
+  return http_load_multi(port, nconn, seconds, {post_request(path, body)}, nthreads, max_requests, warmup);
 }
 
 }  // namespace rtc

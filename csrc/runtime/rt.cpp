@@ -353,12 +353,36 @@ py::dict py_http_load(int port, int connections, double seconds, const std::stri
 
 void bind_route(py::module& m);   // route_bind.cpp
 
+// The same over many different requests (path, body), cycled — e.g. 1k distinct route requests.
+py::dict py_http_load_multi(int port, int connections, double seconds, const std::vector<std::string>& paths,
+                            const std::vector<std::string>& bodies, int threads, long long max_requests,
+                            int warmup) {
+  if (paths.size() != bodies.size() || paths.empty()) throw std::invalid_argument("paths/bodies mismatch");
+  std::vector<std::string> reqs;
+  for (size_t i = 0; i < paths.size(); ++i) reqs.push_back(rtc::post_request(paths[i], bodies[i]));
+  rtc::LoadResult r;
+  {
+    py::gil_scoped_release nogil;
+    r = rtc::http_load_multi(port, connections, seconds, reqs, threads, max_requests, warmup);
+  }
+  py::dict d;
+  d["seconds"] = r.seconds;
+  d["requests"] = r.requests;
+  d["errors"] = r.errors;
+  d["bytes"] = r.bytes;
+  d["latencies_us"] = py::array_t<float>(r.lat_us.size(), r.lat_us.data());
+  return d;
+}
+
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "routest_amd CPU native runtime";
   bind_route(m);
   m.def("http_load", &py_http_load, py::arg("port"), py::arg("connections") = 1, py::arg("seconds") = 2.0,
         py::arg("path") = "/api/predict_eta", py::arg("body") = "", py::arg("threads") = 1,
         py::arg("max_requests") = 0, py::arg("warmup") = 0);
+  m.def("http_load_multi", &py_http_load_multi, py::arg("port"), py::arg("connections"), py::arg("seconds"),
+        py::arg("paths"), py::arg("bodies"), py::arg("threads") = 4, py::arg("max_requests") = 0,
+        py::arg("warmup") = 0);
   m.def("pack_predict_batch", &pack_predict_batch, py::arg("body"), py::arg("now_secs"), py::arg("now_us"));
   m.def("format_predict_batch", &format_predict_batch);
   m.def("pack_wire8", &pack_wire8_py);

@@ -1,0 +1,66 @@
+// Minimal run-time binding of the system SQLite library (libsqlite3.so.0, the same library Python's
+// sqlite3 module uses; the image ships no sqlite3.h).  The native route service writes the
+// reference's two persistence rows (RO/Flaskr/routes.py:134-182; routest_amd/store/store.py
+// SQLiteStore) into the same database file the Python store reads, in WAL mode with a busy timeout
+// so both connections interleave safely.
+#pragma once
+#include <dlfcn.h>
+
+#include <cstdint>
+#include <string>
+
+namespace rtsql {
+
+struct Api {
+  void* h = nullptr;
+  int (*open_v2)(const char*, void**, int, const char*) = nullptr;
+  int (*close)(void*) = nullptr;
+  int (*busy_timeout)(void*, int) = nullptr;
+  int (*exec)(void*, const char*, void*, void*, char**) = nullptr;
+  int (*prepare_v2)(void*, const char*, int, void**, const char**) = nullptr;
+  int (*bind_text)(void*, int, const char*, int, void (*)(void*)) = nullptr;
+  int (*bind_double)(void*, int, double) = nullptr;
+  int (*bind_int64)(void*, int, long long) = nullptr;
+  int (*bind_null)(void*, int) = nullptr;
+  int (*step)(void*) = nullptr;
+  int (*reset)(void*) = nullptr;
+  int (*clear_bindings)(void*) = nullptr;
+  int (*finalize)(void*) = nullptr;
+  const char* (*errmsg)(void*) = nullptr;
+  void (*free_)(void*) = nullptr;
+
+  bool load(std::string& err) {
+    if (h) return true;
+    h = dlopen("libsqlite3.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("libsqlite3.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) { err = "libsqlite3 not found"; return false; }
+    bool ok = true;
+    auto sym = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      ok = ok && fn != nullptr;
+    };
+    sym(open_v2, "sqlite3_open_v2");
+    sym(close, "sqlite3_close");
+    sym(busy_timeout, "sqlite3_busy_timeout");
+    sym(exec, "sqlite3_exec");
+    sym(prepare_v2, "sqlite3_prepare_v2");
+    sym(bind_text, "sqlite3_bind_text");
+    sym(bind_double, "sqlite3_bind_double");
+    sym(bind_int64, "sqlite3_bind_int64");
+    sym(bind_null, "sqlite3_bind_null");
+    sym(step, "sqlite3_step");
+    sym(reset, "sqlite3_reset");
+    sym(clear_bindings, "sqlite3_clear_bindings");
+    sym(finalize, "sqlite3_finalize");
+    sym(errmsg, "sqlite3_errmsg");
+    sym(free_, "sqlite3_free");
+    if (!ok) err = "libsqlite3: missing symbols";
+    return ok;
+  }
+};
+
+constexpr int OK = 0, ROW = 100, DONE = 101;
+constexpr int OPEN_READWRITE = 0x2, OPEN_CREATE = 0x4, OPEN_URI = 0x40, OPEN_NOMUTEX = 0x8000;
+inline void (*const TRANSIENT)(void*) = reinterpret_cast<void (*)(void*)>(-1);
+
+}  // namespace rtsql

@@ -35,19 +35,37 @@ def cmd_serve(a: argparse.Namespace) -> None:
     elif a.model:
         eta = EtaService(model_path=a.model, device=s.device, devices=s.devices, batch_max=s.batch_max,
                          timeout_us=s.batch_timeout_us, allow_pickle=os.environ.get("ROUTEST_ALLOW_PICKLE") == "1")
-    app = create_app(build_services(s, eta=eta))
+    sv = build_services(s, eta=eta)
+    app = create_app(sv)
+    port = a.port or s.port
+    from .models.mlp3 import EtaMLP
+    native_ok = (eta is not None and eta.backend == "hip" and isinstance(eta.model, EtaMLP)
+                 and eta.model.hidden in (64, 128, 256))
+    if a.front == "native" and native_ok:
+        # the native front end owns the main port; the FastAPI app answers what it relays
+        from .serve.frontend import ServingStack
+        stack = ServingStack(sv, app, eta.model, [d.index for d in eta.devices], port=port,
+                             threads=a.native_threads, bind_any=a.host not in ("127.0.0.1", "localhost"))
+        print(json.dumps({"port": stack.port, "front": "native", "app_port": stack.app_server.port,
+                          "native_routes": bool(stack.front.routes)}), flush=True)
+        import threading
+        try:
+            threading.Event().wait()
+        except KeyboardInterrupt:
+            pass
+        finally:
+            stack.close()
+        return
     native_srv = None
-    if a.native_port and eta is not None and eta.backend == "hip":
-        from .models.mlp3 import EtaMLP
-        if isinstance(eta.model, EtaMLP):
-            from .serve.native_server import NativePredictServer
-            native_srv = NativePredictServer(eta.model, device=[d.index for d in eta.devices], port=a.native_port,
-                                             threads=a.native_threads, cors_origins=s.cors_origins,
-                                             bind_any=a.host not in ("127.0.0.1", "localhost"))
-            print(json.dumps({"native_predict_port": native_srv.port}), flush=True)
+    if a.native_port and native_ok:
+        from .serve.native_server import NativePredictServer
+        native_srv = NativePredictServer(eta.model, device=[d.index for d in eta.devices], port=a.native_port,
+                                         threads=a.native_threads, cors_origins=s.cors_origins,
+                                         bind_any=a.host not in ("127.0.0.1", "localhost"))
+        print(json.dumps({"native_predict_port": native_srv.port}), flush=True)
     import uvicorn
     try:
-        uvicorn.run(app, host=a.host, port=a.port or s.port, log_level="warning", access_log=False)
+        uvicorn.run(app, host=a.host, port=port, log_level="warning", access_log=False)
     finally:
         if native_srv is not None:
             native_srv.close()
@@ -98,9 +116,12 @@ def main(argv=None) -> None:
     s.add_argument("--provider", default="")
     s.add_argument("--store", default="")
     s.add_argument("--env-file", default=".env")
+    s.add_argument("--front", choices=["native", "python"], default="native",
+                   help="native: the C++ front end owns the main port (predictions and routes natively, "
+                        "everything else relayed to the FastAPI app); python: uvicorn on the main port")
     s.add_argument("--native-port", type=int, default=0,
-                   help="also serve /api/predict_eta and /predict from the native C++ front end on this port")
-    s.add_argument("--native-threads", type=int, default=2)
+                   help="(--front python) also serve /api/predict_eta and /predict natively on this port")
+    s.add_argument("--native-threads", type=int, default=8)
     t = sub.add_parser("train", help="train the ETA model (use torchrun for multi-GPU)")
     b = sub.add_parser("bench", help="run a benchmark")
     b.add_argument("what", choices=["serve", "train", "gcn", "route", "rccl", "http", "kernel"])

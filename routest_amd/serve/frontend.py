@@ -1,0 +1,123 @@
+"""Assemble the serving stack: the native front end on the main port, the FastAPI app behind it.
+
+    client ──HTTP──> native front end (C++ reactors, csrc/native_server.hip)  :5000
+                       ├─ /api/predict_eta, /predict ........ fused K1+K2 kernel
+                       ├─ /api/optimize_route, /route,
+                       │  /api/request_route ................ native route service per GPU
+                       │                                       (K5 + K6 + batched A* + C++ GeoJSON)
+                       └─ everything else, and requests the native paths do not mirror
+                                                 ──relay──> FastAPI app (uvicorn)  127.0.0.1:<private>
+
+The reference serves all of it from one Flask process (``RO/app.py:8``, gunicorn in
+``RO/requirements.txt:10``).  Here the request paths that carry the traffic never enter Python,
+and the Python app keeps the long tail (history, health, SSE, admin, scorer) with identical
+semantics — byte-identical bodies on the shared routes (tests/test_frontend_gpu.py).
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import Any, List, Optional, Sequence
+
+from ..utils.logging import get_logger
+
+log = get_logger("frontend")
+
+
+class AppServer:
+    """uvicorn serving ``app`` on 127.0.0.1:``port`` from a background thread (the relay target)."""
+
+    def __init__(self, app, port: int = 0, host: str = "127.0.0.1", log_level: str = "warning"):
+        import uvicorn
+        from .native_server import free_port
+        self.port = port or free_port()
+        self.server = uvicorn.Server(uvicorn.Config(app, host=host, port=self.port, log_level=log_level,
+                                                    access_log=False, lifespan="on"))
+        self.thread = threading.Thread(target=self.server.run, name="uvicorn-app", daemon=True)
+        self.thread.start()
+        t0 = time.time()
+        while not self.server.started:
+            if not self.thread.is_alive() or time.time() - t0 > 60:
+                raise RuntimeError("the FastAPI app server did not start")
+            time.sleep(0.01)
+
+    def close(self) -> None:
+        self.server.should_exit = True
+        self.thread.join(timeout=15)
+
+
+def native_route_reason(sv) -> Optional[str]:
+    """None if the native route service can answer this app's route requests, else why not."""
+    name = getattr(sv.provider, "name", "")
+    if name not in ("haversine", "graph"):
+        return f"provider {name!r} (remote calls) stays in Python"
+    st = sv.store
+    if st is not None and getattr(st, "kind", "") != "sqlite":
+        return f"store {getattr(st, 'kind', type(st).__name__)!r} is written by the Python app only"
+    if name == "graph" and getattr(sv.provider, "device", None) is None:
+        return "road-graph provider without a GPU"
+    return None
+
+
+def route_configs(sv, devices: Sequence[int], batch_max: int = 1024, timeout_us: int = 500) -> List[dict]:
+    """One native route service config per GPU (serve/native_server.py route_config)."""
+    import torch
+    from .native_server import route_config
+    s = sv.settings
+    out = []
+    for d in devices:
+        astar = None
+        if getattr(sv.provider, "name", "") == "graph":
+            from ..routing.graph import BatchedAstar
+            astar = BatchedAstar(sv.provider.g, sv.provider.cost, torch.device("cuda", d),
+                                 slots=int(getattr(s, "route_astar_slots", 8192)))
+        out.append(route_config(sv.provider, d, engine=s.engine_name, compat200=s.compat_request_route_200,
+                                batch_max=batch_max, timeout_us=timeout_us, store=sv.store, astar=astar))
+    return out
+
+
+def start_front_end(sv, model, devices: Sequence[int], port: int = 0, upstream_port: int = 0,
+                    threads: int = 8, bind_any: bool = False, routes: bool = True,
+                    batch_max: Optional[int] = None, timeout_us: Optional[int] = None,
+                    cors_origins: Optional[Sequence[str]] = None):
+    """Start the native front end for ``sv``'s app (relaying to ``upstream_port``)."""
+    from .native_server import NativePredictServer
+    s = sv.settings
+    cfgs: List[dict] = []
+    if routes:
+        why = native_route_reason(sv)
+        if why is None:
+            cfgs = route_configs(sv, devices, batch_max or s.route_batch_max,
+                                 timeout_us if timeout_us is not None else s.route_batch_timeout_us)
+        else:
+            log.info("route requests relayed to the Python app: %s", why)
+    srv = NativePredictServer(model, device=list(devices), port=port, threads=max(threads, len(devices)),
+                              cors_origins=cors_origins if cors_origins is not None else s.cors_origins,
+                              bind_any=bind_any, upstream_port=upstream_port, routes=cfgs)
+    return srv
+
+
+class ServingStack:
+    """FastAPI app on a private port + the native front end on ``port`` (tests, benches, serve)."""
+
+    def __init__(self, sv, app, model, devices: Sequence[int], port: int = 0, threads: int = 8,
+                 bind_any: bool = False, routes: bool = True, **kw: Any):
+        self.app_server = AppServer(app)
+        try:
+            self.front = start_front_end(sv, model, devices, port=port, upstream_port=self.app_server.port,
+                                         threads=threads, bind_any=bind_any, routes=routes, **kw)
+        except BaseException:
+            self.app_server.close()
+            raise
+        self.port = self.front.port
+
+    def close(self) -> None:
+        self.front.close()
+        self.app_server.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False

@@ -1,14 +1,19 @@
-"""Native HTTP front end for the prediction endpoints (``csrc/native_server.hip``).
+"""Native HTTP front end (``csrc/native_server.hip``): the service's main port.
 
-``POST /api/predict_eta`` and ``POST /predict`` are answered by C++ reactor threads — native JSON
-packing, one zero-copy fused-kernel launch per wake-up (natural batching across connections),
-CPython-exact response formatting — with no Python on the request path.  It runs next to the
-FastAPI app (which keeps every other endpoint) on its own port::
+* ``POST /api/predict_eta`` and ``POST /predict`` are answered by C++ reactor threads — native
+  JSON packing, one zero-copy fused-kernel launch per wake-up (natural batching across
+  connections), CPython-exact response formatting.
+* ``POST /api/optimize_route``, ``/route`` and ``/api/request_route`` go to one native route service
+  per GPU (``csrc/route_service.hip``: cross-request batching, K5 + K6, the batched A*, C++ GeoJSON
+  assembly byte-identical to the FastAPI handler, ``use_ml_eta`` on the fused MLP kernel, SQLite
+  persistence into the Python store's database).
+* Everything else — and any request whose semantics the native path does not mirror — is relayed
+  to the FastAPI app listening on a private loopback port (``upstream_port``); a streamed answer
+  (the SSE feed) turns its connection into a byte tunnel.
 
-    python -m routest_amd serve --synthetic-model --port 5000 --native-port 5001
-
-The reference answers this route through Flask (``RO/Flaskr/routes.py:365-383``); this front end
-exists because single-request latency is host-stack bound.
+No Python runs on the native request paths.  ``python -m routest_amd serve`` puts this front end
+on the main port (5000) with uvicorn behind it; the reference serves every route through Flask
+(``RO/Flaskr/routes.py``), and single-request latency is host-stack bound.
 """
 from __future__ import annotations
 
@@ -35,9 +40,11 @@ class NativePredictServer:
 
     def __init__(self, model, device=0, port: int = 0, threads: int = 2, max_batch: int = 1 << 18,
                  cors_origins: Sequence[str] = ("http://localhost:3000", "http://127.0.0.1:3000"),
-                 cors_vercel: bool = True, bind_any: bool = False, variant: int = -1):
+                 cors_vercel: bool = True, bind_any: bool = False, variant: int = -1,
+                 upstream_port: int = 0, routes: Optional[List[dict]] = None):
         self.C = native(required=True)
         devices = [device] if isinstance(device, int) else list(device)
+        self.routes = list(routes or [])      # keeps the route configs' tensors alive
         threads = max(threads, len(devices))
         # one packed weight blob per GPU; the kernels keep them alive for the server's lifetime
         self.kerns = [EtaMlpKernel(model, torch.device("cuda", d), variant=variant) for d in devices]
@@ -45,7 +52,7 @@ class NativePredictServer:
         self.port = port or free_port()
         self.h: Optional[int] = self.C.native_server_start(
             self.port, threads, [k.packed.blob for k in self.kerns], k0.hidden, list(k0.packed.norm),
-            variant, max_batch, list(cors_origins), cors_vercel, bind_any)
+            variant, max_batch, list(cors_origins), cors_vercel, bind_any, int(upstream_port), self.routes)
 
     def stats(self) -> Dict[str, int]:
         if self.h is None:
@@ -53,8 +60,12 @@ class NativePredictServer:
         v = self.C.native_server_stats(self.h)
         # resident: rounds scored by the persistent kernel (csrc/persistent_serve.hip);
         # fallbacks: rounds it did not answer in time, re-scored by a normal launch;
-        # wire8: launches that read 8-byte wire records (features.py RECORD8) instead of 16-byte
-        names = ("requests", "predictions", "launches", "errors", "resident", "fallbacks", "wire8")
+        # wire8: launches that read 8-byte wire records (features.py RECORD8) instead of 16-byte;
+        # route_*: the native route service (jobs, flushes, jobs handed to Python, unique legs
+        # searched, legs finished on the host, rows persisted); relayed: requests sent to the app
+        names = ("requests", "predictions", "launches", "errors", "resident", "fallbacks", "wire8",
+                 "route_requests", "route_fallbacks", "relayed", "route_jobs", "route_flushes",
+                 "route_service_fallbacks", "route_legs", "route_host_legs", "route_persisted")
         return dict(zip(names, v))
 
     def close(self) -> None:
@@ -68,3 +79,45 @@ class NativePredictServer:
     def __exit__(self, *exc):
         self.close()
         return False
+
+
+def route_config(provider, device, *, engine: str = "backend:mi355x", compat200: bool = True,
+                 batch_max: int = 1024, timeout_us: int = 500, store=None, astar=None) -> dict:
+    """The native route service's configuration for one GPU (``csrc/route_service.h``).
+
+    ``provider``: the app's HaversineProvider or GraphProvider.  For the road graph, ``astar`` is a
+    :class:`~routest_amd.routing.graph.BatchedAstar` on ``device`` whose device tensors the service
+    searches with (the caller keeps it alive; its wave-stage heuristic cache is allocated here).
+    ``store``: the app's store — an :class:`SQLiteStore` is written natively (same database file);
+    any other store kind is not mirrored, so route requests are then relayed to the Python app
+    (the caller passes no route configs)."""
+    name = getattr(provider, "name", "")
+    cfg = {"provider": "graph" if name == "graph" else "haversine", "engine": engine,
+           "compat200": bool(compat200), "batch_max": int(batch_max), "timeout_us": float(timeout_us),
+           "circuity": float(getattr(provider, "circuity", 1.3)), "step_m": float(getattr(provider, "step_m", 150.0)),
+           "sqlite_path": getattr(store, "sqlite_uri", "") if store is not None else ""}
+    if name == "graph":
+        import numpy as np
+        a = astar
+        if a is None or a.perm is not None:
+            raise ValueError("graph routes need a BatchedAstar without node reordering")
+        if a.hcache is None and a.lane_pops > 0:
+            a.hcache = torch.full((a.wave_slots, a.g.num_nodes), float("nan"), dtype=torch.float32, device=a.dev)
+        g = a.g
+        cfg.update({
+            "glat": torch.from_numpy(np.ascontiguousarray(g.lat, dtype=np.float64)),
+            "glon": torch.from_numpy(np.ascontiguousarray(g.lon, dtype=np.float64)),
+            "h_indptr": torch.from_numpy(np.ascontiguousarray(g.indptr, dtype=np.int32)),
+            "h_indices": torch.from_numpy(np.ascontiguousarray(g.indices, dtype=np.int32)),
+            "h_cost": a.cost.detach().cpu().contiguous(),
+            "indptr": a.indptr, "indices": a.indices, "cost": a.cost, "lat32": a.lat, "lon32": a.lon,
+            "lm": a.lm, "K": (a.lm.shape[1] // 2) if a.lm is not None else 0,
+            "state": a.state, "heap": a.heap, "touched": a.touched, "hcache": a.hcache,
+            "N": int(g.num_nodes), "snap_c": float(g.SNAP_C), "slots": int(a.slots), "cap": int(a.cap),
+            "max_path": int(a.max_path), "max_iters": int(a.max_iters), "lane_pops": int(a.lane_pops),
+            "wave_slots": int(a.wave_slots), "inv_vmax": float(a.inv_vmax), "wave_delta": float(a.wave_delta),
+            "_astar": a})
+    return cfg
+
+
+NativeFrontEnd = NativePredictServer

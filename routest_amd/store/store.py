@@ -14,9 +14,12 @@ driver_age}``, ``route_results.{geometry, eta_minutes_ml, eta_completion_time_ml
 """
 from __future__ import annotations
 
+import atexit
 import datetime as dt
 import json
+import os
 import sqlite3
+import tempfile
 import threading
 import time
 import uuid
@@ -62,6 +65,23 @@ CREATE INDEX IF NOT EXISTS route_results_req ON route_results(request_id);
 
 class StoreUnavailable(RuntimeError):
     pass
+
+
+_EPHEMERAL: List[str] = []
+
+
+def _remove_db(path: str) -> None:
+    for suffix in ("", "-wal", "-shm"):
+        try:
+            os.remove(path + suffix)
+        except OSError:
+            pass
+
+
+@atexit.register
+def _cleanup_ephemeral() -> None:  # pragma: no cover - exit path
+    for p in _EPHEMERAL:
+        _remove_db(p)
 
 
 def _now_iso() -> str:
@@ -114,16 +134,39 @@ class SQLiteStore:
     kind = "sqlite"
 
     def __init__(self, path: str = ":memory:", seed: bool = True):
+        # ":memory:" (the default, nothing survives a restart) is backed by a private temporary
+        # file deleted at exit, so the native route service (csrc/route_service.hip) can write the
+        # same database through its own connection; WAL + a busy timeout interleave the two
+        self.ephemeral = path == ":memory:"
+        if self.ephemeral:
+            fd, path = tempfile.mkstemp(prefix="routest-store-", suffix=".db")
+            os.close(fd)
+            _EPHEMERAL.append(path)
         self.path = path
         self._lock = threading.Lock()
-        self._db = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
+        self._db = sqlite3.connect(path, check_same_thread=False, isolation_level=None, timeout=10.0)
         self._db.row_factory = sqlite3.Row
         self._db.execute("PRAGMA foreign_keys=ON")
-        if path != ":memory:":
-            self._db.execute("PRAGMA journal_mode=WAL")
+        self._db.execute("PRAGMA journal_mode=WAL")
+        if self.ephemeral:
+            self._db.execute("PRAGMA synchronous=OFF")
         self._db.executescript(SCHEMA)
         if seed:
             self.seed_locations()
+
+    @property
+    def sqlite_uri(self) -> str:
+        """Database file for other connections (the native route service)."""
+        return os.path.abspath(self.path)
+
+    def close(self) -> None:
+        with self._lock:
+            try:
+                self._db.close()
+            except Exception:  # pragma: no cover
+                pass
+        if self.ephemeral:
+            _remove_db(self.path)
 
     # ---- locations (L03, F10, L04) ----
     def seed_locations(self) -> None:

@@ -1,0 +1,221 @@
+"""The serving stack on a GPU: native front end on the main port, FastAPI app behind it.
+
+* /api/optimize_route, /route, /api/request_route answered by the native route service
+  (csrc/route_service.hip) are byte-identical to the Python app's answers for the same request —
+  haversine provider (K5 + K6) and road-graph provider (K5 + K6 + the batched A*);
+* use_ml_eta adds the fused MLP kernel's ETA; results are persisted into the Python store's
+  database and readable through the relayed /api/history routes;
+* everything else is relayed to the app unchanged (health, history, locations, 404s, the SSE feed
+  as a byte tunnel), and requests the native path does not mirror are answered by the app.
+Reference: RO/Flaskr/routes.py:29-50,89-127,185-279; RO/Flaskr/utils.py:10-201."""
+import http.client
+import json
+import re
+import socket
+import threading
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _req(port, method, path, body=None, headers=None, conn=None):
+    c = conn or http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+    raw = None if body is None else (body if isinstance(body, bytes) else json.dumps(body).encode())
+    h = {"Content-Type": "application/json"} if raw is not None else {}
+    h.update(headers or {})
+    c.request(method, path, body=raw, headers=h)
+    r = c.getresponse()
+    return r.status, r.read(), dict(r.getheaders())
+
+
+def _payloads(n, lat, lon, seed=0, max_stops=10):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        idx = rng.integers(0, len(lat), int(rng.integers(2, max_stops + 2)))
+        p = {"source_point": {"lat": float(lat[idx[0]]), "lon": float(lon[idx[0]])},
+             "destination_points": [{"lat": float(lat[j]), "lon": float(lon[j]), "payload": int(rng.integers(0, 3))}
+                                    for j in idx[1:]],
+             "driver_details": {"driver_name": f"drv{i}", "vehicle_type": ["car", "truck", "bike"][i % 3],
+                                "vehicle_capacity": 4, "maximum_distance": 1e7},
+             "meta": {"origin_id": None, "destination_ids": [f"d{j}" for j in idx[1:]]}}
+        if i % 9 == 0:
+            p["destination_points"] = p["destination_points"][:1]       # point-to-point
+        if i % 13 == 0:
+            p["driver_details"]["vehicle_capacity"] = 0                 # infeasible stops
+        out.append(p)
+    return out
+
+
+_RID = re.compile(rb',"request_id":"[0-9a-f-]{36}","saved":true')
+
+
+def _strip_rid(b: bytes) -> bytes:
+    return _RID.sub(b"", b)
+
+
+def _stack(provider, store, route_min_stops=1):
+    from routest_amd.api.app import build_services, create_app
+    from routest_amd.config import load_settings
+    from routest_amd.serve.eta_service import EtaService, default_model
+    from routest_amd.serve.frontend import ServingStack
+    model = default_model(steps=30)
+    s = load_settings(env={}, dotenv_path=None, devices=[0], route_batch="1", route_gpu_min_stops=route_min_stops,
+                      warm_scorer=False)
+    sv = build_services(s, eta=EtaService(model, devices=[0]), provider=provider, store=store)
+    app = create_app(sv)
+    return ServingStack(sv, app, model, [0], threads=4, timeout_us=300), sv
+
+
+@pytest.fixture(scope="module")
+def hav():
+    from routest_amd.routing.providers import HaversineProvider
+    from routest_amd.store.store import SQLiteStore
+    st, sv = _stack(HaversineProvider(), SQLiteStore(":memory:"))
+    assert st.front.routes, "native routes not enabled"
+    yield st, sv
+    st.close()
+
+
+def test_haversine_routes_byte_identical(hav):
+    st, sv = hav
+    rng = np.random.default_rng(7)
+    lat, lon = 14.55 + rng.normal(0, 0.04, 500), 121.02 + rng.normal(0, 0.04, 500)
+    pays = _payloads(150, lat, lon, seed=1)
+    for path in ("/api/optimize_route", "/route", "/api/request_route"):
+        for p in pays[:60]:
+            a = _req(st.port, "POST", path, p)
+            b = _req(st.app_server.port, "POST", path, p)
+            assert a[0] == b[0], (path, p, a[1][:300], b[1][:300])
+            assert _strip_rid(a[1]) == _strip_rid(b[1]), (path, p)
+    stats = st.front.stats()
+    assert stats["route_jobs"] >= 180 and stats["route_service_fallbacks"] == 0, stats
+
+
+def test_concurrent_requests_batched_and_identical(hav):
+    st, sv = hav
+    rng = np.random.default_rng(9)
+    lat, lon = 14.55 + rng.normal(0, 0.05, 800), 121.02 + rng.normal(0, 0.05, 800)
+    pays = _payloads(200, lat, lon, seed=3)
+    want = [_req(st.app_server.port, "POST", "/api/request_route", p) for p in pays]
+    f0 = st.front.stats()["route_flushes"]
+    got = [None] * len(pays)
+
+    def worker(k):
+        c = http.client.HTTPConnection("127.0.0.1", st.port, timeout=60)
+        for i in range(k, len(pays), 16):
+            got[i] = _req(st.port, "POST", "/api/request_route", pays[i], conn=c)
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for g, w in zip(got, want):
+        assert g[0] == w[0] and g[1] == w[1]
+    assert st.front.stats()["route_flushes"] - f0 < len(pays)     # requests shared flushes
+
+
+def test_ml_eta_and_persistence(hav):
+    st, sv = hav
+    p = {"source_point": {"lat": 14.5836, "lon": 121.0409},
+         "destination_points": [{"lat": 14.5352, "lon": 120.9822, "payload": 1},
+                                {"lat": 14.6556, "lon": 121.0313, "payload": 1}],
+         "driver_details": {"driver_name": "Juan", "vehicle_type": "car", "vehicle_capacity": 9999,
+                            "maximum_distance": 100000, "driver_age": 41},
+         "meta": {"origin_id": "o-1", "destination_ids": ["a", "b"], "vehicle_id": "Juan"},
+         "use_ml_eta": True, "context": {"weather": "Sunny", "traffic": "Medium"}}
+    code, body, _ = _req(st.port, "POST", "/api/optimize_route", p)
+    assert code == 200
+    d = json.loads(body)
+    ref = json.loads(_req(st.app_server.port, "POST", "/api/optimize_route", p)[1])
+    pr, rr = d["properties"], ref["properties"]
+    assert abs(pr["eta_minutes_ml"] - rr["eta_minutes_ml"]) <= 1e-3 * abs(rr["eta_minutes_ml"]) + 1e-4
+    assert pr["eta_completion_time_ml"][:10] == rr["eta_completion_time_ml"][:10]
+    assert pr["saved"] is True and re.fullmatch(r"[0-9a-f-]{36}", pr["request_id"])
+    # the native row is readable through the relayed history routes (Python store, same database)
+    code, hb, _ = _req(st.port, "GET", f"/api/history/{pr['request_id']}")
+    assert code == 200
+    h = json.loads(hb)
+    assert h["request"]["engine"] == "ml" and h["request"]["vehicle_id"] == "Juan" and h["request"]["driver_age"] == 41
+    assert h["request"]["stops"]["destination_ids"] == ["a", "b"] and h["request"]["origin_id"] == "o-1"
+    assert h["result"]["geometry"] == d["geometry"] and h["result"]["legs"] == pr["segments"]
+    assert h["result"]["optimized_order"] == pr["optimized_order"]
+    assert h["result"]["total_distance"] == round(pr["summary"]["distance"], 2)
+    assert h["result"]["eta_minutes_ml"] == pr["eta_minutes_ml"]
+    items = json.loads(_req(st.port, "GET", "/api/history?limit=5")[1])["items"]
+    assert items[0]["request_id"] == pr["request_id"] and items[0]["engine"] == "ml"
+    assert _req(st.port, "DELETE", f"/api/history/{pr['request_id']}")[0] == 204
+    assert _req(st.port, "GET", f"/api/history/{pr['request_id']}")[0] == 404
+
+
+@pytest.mark.parametrize("method,path,body", [
+    ("GET", "/api/health", None), ("GET", "/api/locations", None), ("GET", "/api/history?limit=3", None),
+    ("GET", "/no/such/route", None), ("GET", "/api/optimize_route", None),
+    ("POST", "/api/request_route", b"{bad json"),
+    ("POST", "/api/optimize_route", {"source_point": {"lat": "14.5", "lon": 121.0},
+                                     "destination_points": [{"lat": 14.6, "lon": 121.0}]}),
+    ("POST", "/api/update_tracker", {}),
+])
+def test_relayed_requests_match_the_app(hav, method, path, body):
+    st, sv = hav
+    a = _req(st.port, method, path, body)
+    b = _req(st.app_server.port, method, path, body)
+    assert a[0] == b[0]
+    if path != "/api/health":                    # (latency fields differ run to run)
+        assert a[1] == b[1]
+    else:
+        assert set(json.loads(a[1])) == set(json.loads(b[1]))
+
+
+def test_sse_feed_tunnels_through_the_front_end(hav):
+    st, sv = hav
+    s = socket.create_connection(("127.0.0.1", st.port), timeout=20)
+    s.sendall(b"GET /api/realtime_feed?channel=drvX HTTP/1.1\r\nHost: x\r\n\r\n")
+    buf = b""
+    while b": connected" not in buf:
+        buf += s.recv(4096)
+    assert b"text/event-stream" in buf
+    tick = {"route_id": "drvX", "route": [[121.0, 14.5], [121.1, 14.6]], "destinations": [],
+            "duration": 600, "distance": 5000, "driver_name": "drvX", "vehicle_type": "car",
+            "pickup_time": "2025-08-25T08:30:00"}
+    assert _req(st.port, "POST", "/api/update_tracker", tick)[0] == 200
+    t0 = time.time()
+    while b"data:" not in buf and time.time() - t0 < 10:
+        buf += s.recv(65536)
+    s.close()
+    msg = json.loads(buf.split(b"data:", 1)[1].split(b"\n\n", 1)[0])
+    assert msg["assigned_driver"] == "drvX" and msg["overall_travel_distance"] == 5000
+
+
+def test_predict_on_main_port_matches_app(hav):
+    st, sv = hav
+    b = {"summary": {"distance": 12345}, "pickup_time": "2025-08-25T08:30:00", "driver_age": 34}
+    a = _req(st.port, "POST", "/api/predict_eta", b)
+    r = _req(st.app_server.port, "POST", "/api/predict_eta", b)
+    assert a[0] == r[0] == 200 and a[1] == r[1]
+
+
+def test_graph_provider_routes_byte_identical():
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider, edge_costs
+    from routest_amd.serve.eta_service import default_model
+    import torch
+    g = synth_road_graph(20_000, seed=2)
+    prov = GraphProvider(g, edge_costs(g, default_model(hidden=64, steps=50), device=torch.device("cuda", 0)),
+                         device=torch.device("cuda", 0))
+    st, sv = _stack(prov, None)
+    try:
+        assert st.front.routes and st.front.routes[0]["provider"] == "graph"
+        pays = _payloads(60, g.lat, g.lon, seed=11, max_stops=6)
+        for path in ("/api/optimize_route", "/api/request_route"):
+            for p in pays:
+                a = _req(st.port, "POST", path, p)
+                b = _req(st.app_server.port, "POST", path, p)
+                assert a[0] == b[0] and a[1] == b[1], (path, p, a[1][:300], b[1][:300])
+        stats = st.front.stats()
+        assert stats["route_legs"] > 0 and stats["route_service_fallbacks"] == 0, stats
+    finally:
+        st.close()
