@@ -97,6 +97,8 @@ def main() -> None:
                              "legs_searched": f1["route_legs"] - f0["route_legs"],
                              "legs_on_host": f1["route_host_legs"] - f0["route_host_legs"],
                              "fallbacks_to_python": f1["route_service_fallbacks"] - f0["route_service_fallbacks"],
+                             "stage_ms_per_flush": {k[9:]: (f1[k] - f0[k]) / 1e3 / max(1, f1["route_flushes"] - f0["route_flushes"])
+                                                    for k in f1 if k.startswith("route_us_")},
                              "front_threads": a.threads, "client": "native closed-loop (csrc/runtime/http_client.h)",
                              "path": "HTTP/1.1 loopback -> native front end main port -> route service"}
         print(json.dumps({"native": out["native"]}), flush=True)

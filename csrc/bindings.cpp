@@ -877,6 +877,7 @@ static rt::RouteServiceCfg route_cfg_from(const py::dict& d, int device, const v
     c.max_path = d["max_path"].cast<int>();
     c.max_iters = d["max_iters"].cast<int>();
     c.lane_pops = d["lane_pops"].cast<int>();
+    if (has("wave_only_below")) c.wave_only_below = d["wave_only_below"].cast<int>();
     c.wave_slots = d["wave_slots"].cast<int>();
     c.inv_vmax = d["inv_vmax"].cast<float>();
     c.wave_delta = d["wave_delta"].cast<float>();

@@ -967,7 +967,7 @@ std::vector<long long> native_server_stats(int64_t h) {
                               s->stats.errors.load(), s->stats.resident.load(), s->stats.fallbacks.load(),
                               s->stats.wire8.load(), s->stats.route_requests.load(),
                               s->stats.route_fallbacks.load(), s->stats.relayed.load()};
-  std::vector<long long> rs(6, 0);
+  std::vector<long long> rs(14, 0);
   for (auto& r : s->routes) {
     const auto x = r->stats();
     for (size_t i = 0; i < rs.size(); ++i) rs[i] += x[i];

@@ -44,6 +44,7 @@ struct RouteServiceCfg {
   int* touched = nullptr;
   float* hcache = nullptr;
   int slots = 0, cap = 0, max_path = 4096, max_iters = 2000000, lane_pops = 500, wave_slots = 0;
+  int wave_only_below = 32768;            // fewer unique legs than this: every search in the wave stage
   float inv_vmax = 0.f, wave_delta = 10.f;
   // ETA model for use_ml_eta (the fused K1+K2 kernel's 32x32 weight blob on this device)
   const void* eta_blob = nullptr;

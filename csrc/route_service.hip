@@ -157,6 +157,20 @@ bool host_dijkstra(const int* indptr, const int* indices, const float* cost, int
 
 }  // namespace
 
+// One flush in flight between the two stages: its jobs and the legs its responses are built from.
+struct Batch {
+  std::vector<RouteJob*> jobs;
+  std::vector<rtr::Leg> legs;
+  std::vector<std::vector<int32_t>> host_paths;
+  std::vector<int32_t> flat;                 // found paths, compacted (Leg::path points in here)
+  std::unordered_map<uint64_t, int> leg_index;
+  bool failed = false;
+};
+
+inline double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 struct RouteService::Impl {
   RouteServiceCfg cfg;
   std::function<void(RouteJob*)> done;
@@ -164,11 +178,19 @@ struct RouteService::Impl {
   std::condition_variable cv;
   std::deque<RouteJob*> q;
   bool stop = false;
-  std::thread th;
-  hipStream_t stream{};
+  std::thread th, th_asm;
+  hipStream_t stream{}, stream_asm{};
   rtr::NodeGrid grid;
+  // GPU stage -> assembly stage hand-off (at most 2 flushes waiting: the GPU runs ahead by one)
+  std::mutex amu;
+  std::condition_variable acv;
+  std::deque<Batch*> aq;
+  bool gpu_done = false;
   // statistics
   std::atomic<long long> n_jobs{0}, n_flushes{0}, n_fallback{0}, n_legs{0}, n_host_legs{0}, n_persisted{0};
+  // stage times (us): parse, trips (K5+K6), snap, A*, copy-out, assembly, ETA, persistence
+  std::atomic<long long> t_stage[8] = {};
+  void add_t(int k, double t0) { t_stage[k].fetch_add((long long)(now_us() - t0), std::memory_order_relaxed); }
   // K5 / K6 buffers
   HostBuf<double> h_lat, h_lon, h_dem, h_cap, h_maxd, h_row0;
   HostBuf<int> h_npts, h_visit, h_trip, h_ntrips, h_status;
@@ -285,31 +307,60 @@ struct RouteService::Impl {
   void run() {
     if (hipSetDevice(cfg.device) != hipSuccess) return;
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return;
-    open_store();
-    std::vector<RouteJob*> batch;
+    th_asm = std::thread([this] { asm_loop(); });
     while (true) {
+      auto* b = new Batch();
       {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return stop || !q.empty(); });
-        if (stop && q.empty()) break;
+        if (stop && q.empty()) { delete b; break; }
         // collect: up to batch_max, or timeout_us after the first arrival
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds((long long)cfg.timeout_us);
         while ((int)q.size() < cfg.batch_max && !stop) {
           if (cv.wait_until(lk, deadline) == std::cv_status::timeout) break;
         }
         const size_t take = std::min<size_t>(q.size(), (size_t)cfg.batch_max);
-        batch.assign(q.begin(), q.begin() + take);
+        b->jobs.assign(q.begin(), q.begin() + take);
         q.erase(q.begin(), q.begin() + take);
       }
-      process(batch);
+      gpu_stage(*b);
+      std::unique_lock<std::mutex> lk(amu);
+      acv.wait(lk, [&] { return aq.size() < 2; });
+      aq.push_back(b);
+      acv.notify_all();
+    }
+    {
+      std::lock_guard<std::mutex> lk(amu);
+      gpu_done = true;
+    }
+    acv.notify_all();
+    th_asm.join();
+    (void)hipStreamDestroy(stream);
+  }
+
+  void asm_loop() {
+    if (hipSetDevice(cfg.device) != hipSuccess) return;
+    if (hipStreamCreateWithFlags(&stream_asm, hipStreamNonBlocking) != hipSuccess) return;
+    open_store();
+    while (true) {
+      Batch* b = nullptr;
+      {
+        std::unique_lock<std::mutex> lk(amu);
+        acv.wait(lk, [&] { return gpu_done || !aq.empty(); });
+        if (aq.empty()) break;
+        b = aq.front();
+        aq.pop_front();
+        acv.notify_all();
+      }
+      asm_stage(*b);
       n_flushes.fetch_add(1, std::memory_order_relaxed);
-      for (RouteJob* j : batch) done(j);
-      batch.clear();
+      for (RouteJob* j : b->jobs) done(j);
+      delete b;
     }
     if (st_req) sql.finalize(st_req);
     if (st_res) sql.finalize(st_res);
     if (db) sql.close(db);
-    (void)hipStreamDestroy(stream);
+    (void)hipStreamDestroy(stream_asm);
   }
 
   void fail_all(std::vector<RouteJob*>& jobs, const char* msg) {
@@ -409,15 +460,13 @@ struct RouteService::Impl {
     return true;
   }
 
-  // graph provider: snap, search every unique leg of the flush once, fill `legs` / `leg_of`
-  std::vector<rtr::Leg> legs;
-  std::vector<std::vector<int32_t>> host_paths;
-  std::unordered_map<uint64_t, int> leg_index;
-
-  bool search_legs(std::vector<RouteJob*>& jobs) {
-    legs.clear();
-    host_paths.clear();
-    leg_index.clear();
+  // graph provider: snap, search every unique leg of the flush once, fill the batch's legs
+  bool search_legs(Batch& b) {
+    std::vector<RouteJob*>& jobs = b.jobs;
+    std::vector<rtr::Leg>& legs = b.legs;
+    std::vector<std::vector<int32_t>>& host_paths = b.host_paths;
+    std::unordered_map<uint64_t, int>& leg_index = b.leg_index;
+    double t0 = now_us();
     std::vector<RouteJob*> g;
     for (RouteJob* j : jobs)
       if (!j->fallback && !j->calls.empty()) g.push_back(j);
@@ -429,6 +478,8 @@ struct RouteService::Impl {
           for (const auto& pt : c) j->nodes.push_back(grid.nearest(pt.second, pt.first, cfg.snap_c));
       }
     });
+    add_t(2, t0);
+    t0 = now_us();
     std::vector<std::pair<int, int>> pairs;
     for (RouteJob* j : g) {
       size_t off = 0;
@@ -455,7 +506,10 @@ struct RouteService::Impl {
     }
     hipError_t e = hipMemcpyAsync(d_src.d, h_src.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(d_dst.d, h_dst.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
-    const int lane_iters = cfg.lane_pops > 0 ? std::min(cfg.max_iters, cfg.lane_pops) : cfg.max_iters;
+    // lane stage budget; interactive flushes (few thousand legs) go straight to the wave stage
+    // (routing/graph.py BatchedAstar.run applies the same rule)
+    int lane_iters = cfg.lane_pops > 0 ? std::min(cfg.max_iters, cfg.lane_pops) : cfg.max_iters;
+    if (cfg.lane_pops > 0 && Q < cfg.wave_only_below) lane_iters = 1;
     for (int q0 = 0; q0 < Q && e == hipSuccess; q0 += cfg.slots)
       e = launch_astar(cfg.indptr, cfg.indices, cfg.cost, cfg.lat32, cfg.lon32, d_src.d, d_dst.d, cfg.state, cfg.heap,
                        cfg.touched, d_cost.d, d_len.d, d_st.d, d_path.d, cfg.N, Q, q0, cfg.slots, cfg.cap, MP,
@@ -478,6 +532,9 @@ struct RouteService::Impl {
       }
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    add_t(3, t0);
+    t0 = now_us();
     if (e == hipSuccess) e = hipMemcpyAsync(h_len.h, d_len.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h_cost.h, d_cost.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
@@ -498,7 +555,9 @@ struct RouteService::Impl {
       if (e == hipSuccess) e = hipMemcpyAsync(h_flat.h, d_flat.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
       if (e == hipSuccess) e = hipStreamSynchronize(stream);
       if (e != hipSuccess) return false;
+      b.flat.assign(h_flat.h, h_flat.h + total);     // the next flush reuses the pinned buffer
     }
+    add_t(4, t0);
     // searches both GPU stages gave up on (status 2 / 3): exact on the host, like graph.py
     int nbad = 0;
     for (int i = 0; i < Q; ++i) nbad += (h_st.h[i] == 2 || h_st.h[i] == 3);
@@ -508,7 +567,7 @@ struct RouteService::Impl {
       if (h_st.h[i] == 0) {
         L.sec = h_cost.h[i];
         L.len = std::min(h_len.h[i], MP);
-        L.path = h_flat.h + h_off.h[i];
+        L.path = b.flat.data() + h_off.h[i];
       } else if ((h_st.h[i] == 2 || h_st.h[i] == 3) && nbad <= 1024 && cfg.h_indptr != nullptr) {
         float c;
         if (host_dijkstra(cfg.h_indptr, cfg.h_indices, cfg.h_cost, cfg.N, pairs[i].first, pairs[i].second, MP, c,
@@ -523,7 +582,10 @@ struct RouteService::Impl {
     return true;
   }
 
-  void assemble_all(std::vector<RouteJob*>& jobs) {
+  void assemble_all(Batch& b) {
+    std::vector<RouteJob*>& jobs = b.jobs;
+    const std::vector<rtr::Leg>& legs = b.legs;
+    const std::unordered_map<uint64_t, int>& leg_index = b.leg_index;
     rtc::parallel_chunks(jobs.size(), 8, 16, [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         RouteJob* j = jobs[i];
@@ -570,11 +632,11 @@ struct RouteService::Impl {
       r.traffic = j->req.eta_traffic;
       r.pad = 0;
     }
-    hipError_t e = hipMemcpyAsync(d_rec.d, h_rec.h, (size_t)n * 16, hipMemcpyHostToDevice, stream);
+    hipError_t e = hipMemcpyAsync(d_rec.d, h_rec.h, (size_t)n * 16, hipMemcpyHostToDevice, stream_asm);
     if (e == hipSuccess)
-      e = launch_eta_mlp3_fwd(d_rec.d, d_eta.d, n, cfg.eta_blob, cfg.H, cfg.np, cfg.variant, cfg.num_cus, stream, 16);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_eta.h, d_eta.d, (size_t)n * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      e = launch_eta_mlp3_fwd(d_rec.d, d_eta.d, n, cfg.eta_blob, cfg.H, cfg.np, cfg.variant, cfg.num_cus, stream_asm, 16);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_eta.h, d_eta.d, (size_t)n * 4, hipMemcpyDeviceToHost, stream_asm);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream_asm);
     if (e != hipSuccess) return false;
     for (int k = 0; k < n; ++k) {
       RouteJob* j = m[k];
@@ -593,9 +655,11 @@ struct RouteService::Impl {
     return true;
   }
 
-  void process(std::vector<RouteJob*>& jobs) {
+  // GPU stage: parse, trips (K5 + K6), snapping + the batched A* (graph provider)
+  void gpu_stage(Batch& b) {
+    std::vector<RouteJob*>& jobs = b.jobs;
     n_jobs.fetch_add((long long)jobs.size(), std::memory_order_relaxed);
-    // 1. parse
+    double t0 = now_us();
     rtc::parallel_chunks(jobs.size(), 32, 16, [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         RouteJob* j = jobs[i];
@@ -615,23 +679,33 @@ struct RouteService::Impl {
         if (j->req.fallback) j->fallback = true;
       }
     });
+    add_t(0, t0);
     if (cfg.scorer != nullptr && cfg.scorer_mu != nullptr) {
       std::lock_guard<std::mutex> lk(*cfg.scorer_mu);
       pscore_park(cfg.scorer);
     }
-    // 2. trips (K5 + K6)
-    if (!plan_multi(jobs)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); return; }
+    t0 = now_us();
+    if (!plan_multi(jobs)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); b.failed = true; return; }
+    add_t(1, t0);
     for (RouteJob* j : jobs)
       if (!j->fallback) rtr::directions_calls(j->req, j->plan, j->calls);
-    // 3. legs (graph provider)
-    if (cfg.provider == 1 && !search_legs(jobs)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); return; }
-    // 4. assembly
-    assemble_all(jobs);
-    // 5. ETA
+    if (cfg.provider == 1 && !search_legs(b)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); b.failed = true; }
+  }
+
+  // assembly stage: GeoJSON, ETA, persistence, response bytes
+  void asm_stage(Batch& b) {
+    std::vector<RouteJob*>& jobs = b.jobs;
+    if (b.failed) return;
+    double t0 = now_us();
+    assemble_all(b);
+    add_t(5, t0);
+    t0 = now_us();
     if (!run_eta(jobs)) {
       for (RouteJob* j : jobs) j->eta_iso.clear();
     }
-    // 6. persistence (optimize_route / route only; request_route never persists)
+    add_t(6, t0);
+    t0 = now_us();
+    // persistence (optimize_route / route only; request_route never persists)
     std::vector<RouteJob*> save;
     for (RouteJob* j : jobs)
       if (!j->fallback && !j->status && j->asmb.ok && !j->request_route) save.push_back(j);
@@ -645,7 +719,7 @@ struct RouteService::Impl {
         if (!j->request_id.empty()) n_persisted.fetch_add(1, std::memory_order_relaxed);
       }
     }
-    // 7. response bytes
+    add_t(7, t0);
     for (RouteJob* j : jobs) {
       if (j->fallback) { n_fallback.fetch_add(1, std::memory_order_relaxed); continue; }
       if (j->status) continue;
@@ -698,8 +772,10 @@ void RouteService::submit(RouteJob* j) {
 }
 
 std::vector<long long> RouteService::stats() const {
-  return {p_->n_jobs.load(), p_->n_flushes.load(), p_->n_fallback.load(), p_->n_legs.load(),
-          p_->n_host_legs.load(), p_->n_persisted.load()};
+  std::vector<long long> v = {p_->n_jobs.load(), p_->n_flushes.load(), p_->n_fallback.load(), p_->n_legs.load(),
+                              p_->n_host_legs.load(), p_->n_persisted.load()};
+  for (int k = 0; k < 8; ++k) v.push_back(p_->t_stage[k].load());
+  return v;
 }
 
 }  // namespace rt

@@ -207,6 +207,11 @@ class BatchedAstar:
         # lane only 236 ms; the wave stage wants all of its queries resident at once (65k: 84 ms
         # vs 100 ms in 16k chunks), hence up to 65536 wave slots (26 GB of heuristic cache)
         self.lane_pops = int(os.environ.get("ROUTEST_ASTAR_LANE_POPS", "500"))
+        # interactive batches (a few thousand legs per flush: ~60 lane waves would leave most of the
+        # 256 CUs idle) go straight to the wave stage: one 64-lane wave per search fills the chip.
+        # Measured on the native route path at 1k concurrency (profiles/route_http_r3.jsonl): lane
+        # budget 500 -> 19.3k req/s, 100 -> 24.1k, 1 (all wave) -> 26.2k, 2000 -> 10.3k.
+        self.wave_only_below = int(os.environ.get("ROUTEST_ASTAR_WAVE_ONLY_BELOW", "32768"))
         self.wave_delta = float(os.environ.get("ROUTEST_ASTAR_DELTA", "10"))
         self.wave_slots = min(slots, int(os.environ.get("ROUTEST_ASTAR_WAVE_SLOTS", "65536")))
         self.hcache = None            # [wave_slots, N] f32 heuristic cache of the wave stage (NaN = empty)
@@ -268,6 +273,8 @@ class BatchedAstar:
         out_path = torch.empty((Q, self.max_path), dtype=torch.int32, device=d)
         self.last_iters = torch.empty(Q, dtype=torch.int32, device=d)   # heap pops per query
         lane_iters = min(self.max_iters, self.lane_pops) if self.lane_pops > 0 else self.max_iters
+        if self.lane_pops > 0 and Q < self.wave_only_below:
+            lane_iters = 1                   # (csrc/route_service.hip applies the same rule)
         for q0 in range(0, Q, self.slots):
             self.C.astar(self.indptr, self.indices, self.cost, self.lat, self.lon, s, t, self.state,
                          self.heap, self.touched, out_cost, out_len, out_status, out_path,

@@ -65,7 +65,10 @@ class NativePredictServer:
         # searched, legs finished on the host, rows persisted); relayed: requests sent to the app
         names = ("requests", "predictions", "launches", "errors", "resident", "fallbacks", "wire8",
                  "route_requests", "route_fallbacks", "relayed", "route_jobs", "route_flushes",
-                 "route_service_fallbacks", "route_legs", "route_host_legs", "route_persisted")
+                 "route_service_fallbacks", "route_legs", "route_host_legs", "route_persisted",
+                 # accumulated stage times of the route service (us)
+                 "route_us_parse", "route_us_trips", "route_us_snap", "route_us_astar", "route_us_copyout",
+                 "route_us_assemble", "route_us_eta", "route_us_persist")
         return dict(zip(names, v))
 
     def close(self) -> None:
@@ -115,6 +118,7 @@ def route_config(provider, device, *, engine: str = "backend:mi355x", compat200:
             "state": a.state, "heap": a.heap, "touched": a.touched, "hcache": a.hcache,
             "N": int(g.num_nodes), "snap_c": float(g.SNAP_C), "slots": int(a.slots), "cap": int(a.cap),
             "max_path": int(a.max_path), "max_iters": int(a.max_iters), "lane_pops": int(a.lane_pops),
+            "wave_only_below": int(a.wave_only_below),
             "wave_slots": int(a.wave_slots), "inv_vmax": float(a.inv_vmax), "wave_delta": float(a.wave_delta),
             "_astar": a})
     return cfg
