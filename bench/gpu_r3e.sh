@@ -8,4 +8,6 @@ timeout -k 10 400 python -u bench/route_http_bench.py --provider graph > $O/rout
 tail -1 $O/route_graph.log
 timeout -k 10 300 python -u bench/route_http_bench.py --provider haversine > $O/route_hav.log 2>&1 || { tail -40 $O/route_hav.log; exit 2; }
 tail -1 $O/route_hav.log
+timeout -k 10 300 python -u tools/app_soak.py --stack --seconds 20 --clients 128 > $O/soak_stack.log 2>&1 || { tail -20 $O/soak_stack.log; exit 4; }
+tail -1 $O/soak_stack.log
 echo done

@@ -24,6 +24,8 @@ namespace rtc {
 struct LoadResult {
   double seconds = 0;
   long long requests = 0, errors = 0, bytes = 0;
+  // per request kind: responses by status code (http_load_mixed)
+  std::vector<std::vector<std::pair<int, long long>>> status_by_kind;
   std::vector<float> lat_us;   // sorted per-request latencies
   double pct(double p) const {
     return lat_us.empty() ? 0.0 : (double)lat_us[std::min(lat_us.size() - 1, (size_t)(p * lat_us.size()))];
@@ -134,6 +136,113 @@ inline LoadResult http_load_multi(int port, int nconn, double seconds, const std
   res.requests = total.load();
   res.errors = errors.load();
   res.bytes = bytes.load();
+  return res;
+}
+
+// Mixed traffic: raw HTTP requests `reqs` (any method) with a kind id each, picked round-robin by
+// a shared counter; every response's status code is tallied per kind (contract checks happen in
+// the caller).  Responses are framed by Content-Length (none = empty body, e.g. 204).
+inline LoadResult http_load_mixed(int port, int nconn, double seconds, const std::vector<std::string>& reqs,
+                                  const std::vector<int>& kinds, int nkinds, int nthreads) {
+  using Clock = std::chrono::steady_clock;
+  struct C {
+    int fd = -1;
+    std::string in;
+    Clock::time_point t0;
+    int kind = 0;
+  };
+  nthreads = std::max(1, std::min(nthreads, std::max(1, nconn)));
+  std::atomic<long long> total{0}, errors{0}, bytes{0}, next{0};
+  std::vector<std::vector<std::vector<long long>>> counts(nthreads, std::vector<std::vector<long long>>(nkinds, std::vector<long long>(600, 0)));
+  std::vector<std::vector<float>> lat(nthreads);
+  const auto t_end = Clock::now() + std::chrono::microseconds((long long)(seconds * 1e6));
+  auto send_next = [&](C& c) {
+    const size_t k = (size_t)(next.fetch_add(1, std::memory_order_relaxed) % (long long)reqs.size());
+    c.kind = kinds[k];
+    const std::string& req = reqs[k];
+    size_t off = 0;
+    while (off < req.size()) {
+      const ssize_t w = write(c.fd, req.data() + off, req.size() - off);
+      if (w <= 0) { errors++; return; }
+      off += (size_t)w;
+    }
+  };
+  auto worker = [&](int tid) {
+    const int mine = nconn / nthreads + (tid < nconn % nthreads);
+    const int ep = epoll_create1(0);
+    std::vector<C> cs(mine);
+    for (int i = 0; i < mine; ++i) {
+      int fd = socket(AF_INET, SOCK_STREAM, 0);
+      sockaddr_in a{};
+      a.sin_family = AF_INET;
+      a.sin_port = htons((uint16_t)port);
+      a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+      if (connect(fd, (sockaddr*)&a, sizeof a) != 0) { errors++; close(fd); continue; }
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      cs[i].fd = fd;
+      epoll_event e{};
+      e.events = EPOLLIN;
+      e.data.u32 = (uint32_t)i;
+      epoll_ctl(ep, EPOLL_CTL_ADD, fd, &e);
+      cs[i].t0 = Clock::now();
+      send_next(cs[i]);
+    }
+    epoll_event evs[512];
+    std::vector<char> buf(1 << 16);
+    bool stop = false;
+    while (!stop && Clock::now() < t_end) {
+      const int n = epoll_wait(ep, evs, 512, 50);
+      for (int k = 0; k < n; ++k) {
+        C& c = cs[evs[k].data.u32];
+        const ssize_t r = read(c.fd, buf.data(), buf.size());
+        if (r <= 0) { errors++; stop = true; break; }
+        c.in.append(buf.data(), (size_t)r);
+        while (true) {
+          const size_t h = c.in.find("\r\n\r\n");
+          if (h == std::string::npos) break;
+          size_t clen = 0;
+          for (const char* key : {"content-length:", "Content-Length:"}) {
+            const size_t cl = c.in.find(key);
+            if (cl != std::string::npos && cl < h) { clen = std::strtoull(c.in.c_str() + cl + 15, nullptr, 10); break; }
+          }
+          if (c.in.size() < h + 4 + clen) break;
+          const int code = c.in.size() > 12 ? std::atoi(c.in.c_str() + 9) : 0;
+          counts[tid][c.kind][(code >= 0 && code < 600) ? code : 0]++;
+          bytes += (long long)(h + 4 + clen);
+          c.in.erase(0, h + 4 + clen);
+          const auto now = Clock::now();
+          lat[tid].push_back((float)std::chrono::duration<double, std::micro>(now - c.t0).count());
+          total++;
+          if (now < t_end) {
+            c.t0 = Clock::now();
+            send_next(c);
+          }
+        }
+      }
+    }
+    for (auto& c : cs)
+      if (c.fd >= 0) close(c.fd);
+    close(ep);
+  };
+  const auto t0 = Clock::now();
+  std::vector<std::thread> th;
+  for (int i = 0; i < nthreads; ++i) th.emplace_back(worker, i);
+  for (auto& t : th) t.join();
+  LoadResult res;
+  res.seconds = std::chrono::duration<double>(Clock::now() - t0).count();
+  for (auto& v : lat) res.lat_us.insert(res.lat_us.end(), v.begin(), v.end());
+  std::sort(res.lat_us.begin(), res.lat_us.end());
+  res.requests = total.load();
+  res.errors = errors.load();
+  res.bytes = bytes.load();
+  res.status_by_kind.resize(nkinds);
+  for (int k = 0; k < nkinds; ++k)
+    for (int code = 0; code < 600; ++code) {
+      long long c = 0;
+      for (int t = 0; t < nthreads; ++t) c += counts[t][k][code];
+      if (c) res.status_by_kind[k].emplace_back(code, c);
+    }
   return res;
 }
 

@@ -374,6 +374,33 @@ py::dict py_http_load_multi(int port, int connections, double seconds, const std
   return d;
 }
 
+// Mixed raw requests (any method) with per-kind status tallies — tools/app_soak.py --stack.
+py::dict py_http_load_mixed(int port, int connections, double seconds, const std::vector<py::bytes>& raw,
+                            const std::vector<int>& kinds, int nkinds, int threads) {
+  if (raw.size() != kinds.size() || raw.empty()) throw std::invalid_argument("raw/kinds mismatch");
+  std::vector<std::string> reqs;
+  for (const auto& b : raw) reqs.push_back(std::string(b));
+  rtc::LoadResult r;
+  {
+    py::gil_scoped_release nogil;
+    r = rtc::http_load_mixed(port, connections, seconds, reqs, kinds, nkinds, threads);
+  }
+  py::dict d;
+  d["seconds"] = r.seconds;
+  d["requests"] = r.requests;
+  d["errors"] = r.errors;
+  d["bytes"] = r.bytes;
+  d["latencies_us"] = py::array_t<float>(r.lat_us.size(), r.lat_us.data());
+  py::list by;
+  for (const auto& v : r.status_by_kind) {
+    py::dict k;
+    for (const auto& pc : v) k[py::int_(pc.first)] = pc.second;
+    by.append(k);
+  }
+  d["status_by_kind"] = by;
+  return d;
+}
+
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "routest_amd CPU native runtime";
   bind_route(m);
@@ -383,6 +410,8 @@ PYBIND11_MODULE(_rt, m) {
   m.def("http_load_multi", &py_http_load_multi, py::arg("port"), py::arg("connections"), py::arg("seconds"),
         py::arg("paths"), py::arg("bodies"), py::arg("threads") = 4, py::arg("max_requests") = 0,
         py::arg("warmup") = 0);
+  m.def("http_load_mixed", &py_http_load_mixed, py::arg("port"), py::arg("connections"), py::arg("seconds"),
+        py::arg("raw"), py::arg("kinds"), py::arg("nkinds"), py::arg("threads") = 4);
   m.def("pack_predict_batch", &pack_predict_batch, py::arg("body"), py::arg("now_secs"), py::arg("now_us"));
   m.def("format_predict_batch", &format_predict_batch);
   m.def("pack_wire8", &pack_wire8_py);
