@@ -829,6 +829,42 @@ bool pscore_score(int64_t h, torch::Tensor rec, torch::Tensor out) {
   return e == hipSuccess;
 }
 
+// ---------------------------------------------------------------- GCN scorer training (gcn_train.hip)
+// One backward pass of the scorer over the rows [r0, r1) (all nodes' dy): writes the flat fp32
+// gradient [W1 | b1 | W2 | b2 | wo | bo] and the squared-error sum of those rows.
+void gcn_train_bwd(torch::Tensor X, torch::Tensor Z, torch::Tensor indptr, torch::Tensor indices,
+                   torch::Tensor values, torch::Tensor w1frag, torch::Tensor b1, torch::Tensor W2,
+                   torch::Tensor b2, torch::Tensor wo, torch::Tensor bo, torch::Tensor target, int64_t r0,
+                   int64_t r1, torch::Tensor dy, torch::Tensor slab1, torch::Tensor slab2, torch::Tensor grad,
+                   torch::Tensor loss) {
+  for (auto* t : {&X, &Z, &indptr, &indices, &values, &w1frag, &b1, &W2, &b2, &wo, &bo, &target, &dy, &slab1,
+                  &slab2, &grad, &loss})
+    check_dev(*t, "gcn_train_bwd tensor");
+  const int64_t N = X.size(0);
+  TORCH_CHECK(X.scalar_type() == torch::kBFloat16 && X.dim() == 2 && X.size(1) == 32, "X bf16 [N,32]");
+  TORCH_CHECK(Z.scalar_type() == torch::kBFloat16 && Z.dim() == 2 && Z.size(0) >= N && Z.size(1) == 32, "Z bf16 [N,32]");
+  TORCH_CHECK(indptr.numel() == N + 1 && indices.numel() == values.numel(), "CSR shapes");
+  TORCH_CHECK(w1frag.scalar_type() == torch::kBFloat16 && w1frag.numel() == 32 * 128, "w1frag bf16 [32*128]");
+  TORCH_CHECK(b1.numel() == 128 && W2.numel() == 128 * 32 && b2.numel() == 32 && wo.numel() == 32 && bo.numel() == 1,
+              "parameter shapes");
+  for (auto* t : {&b1, &W2, &b2, &wo, &bo, &target, &dy, &slab1, &slab2, &grad, &loss})
+    TORCH_CHECK(t->scalar_type() == torch::kFloat32, "fp32 operands");
+  TORCH_CHECK(target.numel() == N && dy.numel() >= N, "target / dy [N]");
+  TORCH_CHECK(0 <= r0 && r0 <= r1 && r1 <= N, "row range");
+  TORCH_CHECK(slab1.dim() == 2 && slab1.size(1) == 32 * 128 + 256 && slab1.size(0) >= 8, "slab1 [>=8, 4352]");
+  TORCH_CHECK(slab2.dim() == 2 && slab2.size(1) == 34 && slab2.size(0) >= rt::gcn_train_slab2_rows((int)N),
+              "slab2 [rows, 34]");
+  TORCH_CHECK(grad.numel() == rt::gcn_grad_numel() && loss.numel() >= 1, "grad [8385], loss [1]");
+  const c10::DeviceGuard guard(X.device());
+  RT_CHECK_HIP(rt::launch_gcn_train_bwd(X.data_ptr(), Z.data_ptr(), indptr.data_ptr<int>(), indices.data_ptr<int>(),
+                                        values.data_ptr<float>(), w1frag.data_ptr(), b1.data_ptr<float>(),
+                                        W2.data_ptr<float>(), b2.data_ptr<float>(), wo.data_ptr<float>(),
+                                        bo.data_ptr<float>(), target.data_ptr<float>(), (int)N, (int)r0, (int)r1,
+                                        dy.data_ptr<float>(), slab1.data_ptr<float>(), (int)slab1.size(0),
+                                        slab2.data_ptr<float>(), grad.data_ptr<float>(), loss.data_ptr<float>(),
+                                        num_cus(X.device().index()), cur_stream(X)));
+}
+
 // ---------------------------------------------------------------- native predict server
 // One route service config per GPU from a Python dict (routest_amd/serve/native_server.py
 // route_config): scalars, host arrays (CPU tensors) and device tensors the caller keeps alive.
@@ -1117,6 +1153,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     py::gil_scoped_release nogil;
     rt::pscore_destroy(p);
   });
+  m.def("gcn_train_bwd", &gcn_train_bwd, "GCN scorer backward over a row range -> flat gradient + loss");
+  m.def("gcn_grad_numel", []() { return (int64_t)rt::gcn_grad_numel(); });
+  m.def("gcn_train_slab2_rows", [](int64_t n) { return (int64_t)rt::gcn_train_slab2_rows((int)n); });
   m.def("native_server_start", &native_server_start, "native HTTP front end (predictions, routes, relay)",
         py::arg("port"), py::arg("threads"), py::arg("blobs"), py::arg("H"), py::arg("norm"), py::arg("variant"),
         py::arg("max_batch"), py::arg("cors"), py::arg("cors_vercel"), py::arg("bind_any"),

@@ -94,6 +94,15 @@ hipError_t launch_gcn_spmm_score(const void* Z, const int* indptr, const int* in
 hipError_t launch_route_score(const int* rptr, const int* nodes, const float* latlon,
                               const float* delay, float* score, int R, int N, hipStream_t stream);
 
+// ---- GCN scorer training (K8 backward) : gcn_train.hip ----
+int gcn_grad_numel();
+int gcn_train_slab2_rows(int N);
+hipError_t launch_gcn_train_bwd(const void* X, const void* Z, const int* indptr, const int* indices,
+                                const float* values, const void* w1frag, const float* b1, const float* W2,
+                                const float* b2, const float* wo, const float* bo, const float* target, int N,
+                                int r0, int r1, float* dy, float* slab1, int slab1_rows, float* slab2,
+                                float* grad, float* loss, int num_cus, hipStream_t stream);
+
 // ---- batched A* (K9) : astar.hip ----
 hipError_t launch_astar(const int* indptr, const int* indices, const float* cost, const float* lat,
                         const float* lon, const int* src, const int* dst, void* state,

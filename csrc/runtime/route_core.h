@@ -267,6 +267,9 @@ inline RouteReq parse_route_request(const Value* root) {
   }
   const Value* drv = root->get("driver_details");
   if (drv && drv->truthy() && drv->kind != Value::Obj) { r.fallback = true; return r; }
+  // candidate routes ranked by the GCN scorer: answered by the Python app (routing/alternatives.py)
+  const Value* alt = root->get("alternatives");
+  if (alt && alt->truthy()) { r.fallback = true; return r; }
   if (drv && !drv->truthy()) drv = nullptr;
   // vehicle_type: (driver.get("vehicle_type") or "car"); str -> lower().strip()
   const Value* vt = drv ? drv->get("vehicle_type") : nullptr;

@@ -56,16 +56,47 @@ class Services:
 
     def get_scorer(self):
         """Candidate-route scorer (GCN on the road graph), built on first use: the provider's graph
-        when ``ROUTEST_PROVIDER=graph``, else a synthetic ``ROUTEST_GRAPH_NODES``-node graph."""
+        when ``ROUTEST_PROVIDER=graph``, else a synthetic ``ROUTEST_GRAPH_NODES``-node graph.  It is
+        trained (``ROUTEST_SCORER_TRAIN_STEPS``; HIP backward on a GPU, models/gcn_train.py) on the
+        graph's learned edge times — the provider's, or the ETA model's over the synthetic graph."""
         with self._scorer_lock:
             if self.scorer is None:
                 from ..routing.scorer import RouteScorer
                 g = getattr(self.provider, "g", None)
+                cost = getattr(self.provider, "cost", None) if g is not None else None
                 if g is None:
                     from ..data.graph import synth_road_graph
                     g = synth_road_graph(self.settings.graph_nodes)
-                self.scorer = RouteScorer(g, device=self.route_device)
+                model, info = None, None
+                steps = int(self.settings.scorer_train_steps)
+                if steps > 0:
+                    if cost is None:
+                        from ..models.mlp3 import EtaMLP
+                        from ..routing.graph import edge_costs
+                        m = getattr(self.eta, "model", None)
+                        if isinstance(m, EtaMLP):
+                            cost = edge_costs(g, m, device=self.route_device)
+                        else:
+                            from ..data.graph import CLASS_SPEED_KMH
+                            cost = (g.length_m / (CLASS_SPEED_KMH[g.road_class] / 3.6)).astype("float32")
+                    from ..models.gcn_train import train
+                    model, info = train(g, cost, steps=steps, lr=5e-3, device=self.route_device, log_every=steps)
+                self.scorer = RouteScorer(g, model=model, device=self.route_device)
+                self.scorer.training = info
             return self.scorer
+
+    def graph_search(self):
+        """(src, dst) -> [(seconds, node path)] on the provider's graph: the route batcher's batched
+        A* workspace on the GPU (under its lock), else host Dijkstra."""
+        rb, dev = self.route_batcher, self.route_device
+        if rb is not None and dev is not None:
+            astar, lock = rb._astar_for(dev)
+
+            def search(src, dst):
+                with lock:
+                    return astar.paths(src, dst)
+            return search
+        return lambda src, dst: self.provider._shortest(list(zip(src, dst)))
 
     def warm_scorer_async(self) -> None:
         """Build the scorer (graph + GCN + first node-delay pass) on a background thread at
@@ -329,12 +360,23 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
                 return await sv.route_batcher.submit(payload)
         return await _call(sv.provider, optimize_route, payload, sv.provider, s.engine_name)
 
+    async def _route(payload):
+        """One optimizer answer: ranked alternatives when the request asks for them (graph
+        provider, routing/alternatives.py), else the batched / inline optimizer."""
+        alt = payload.get("alternatives") if isinstance(payload, dict) else None
+        if alt and not isinstance(alt, bool) and isinstance(alt, (int, float)) and alt >= 2:
+            from ..routing.alternatives import optimize_with_alternatives
+            scorer = await run_in_threadpool(sv.get_scorer)
+            return await run_in_threadpool(optimize_with_alternatives, payload, sv.provider, scorer,
+                                           sv.graph_search(), s.engine_name, int(alt))
+        return await _optimize_one(payload)
+
     @app.post("/api/request_route")
     async def request_route(request: Request):
         data = await _json_body(request, silent=False)
         if isinstance(data, Response):
             return data
-        result = await _optimize_one(data)
+        result = await _route(data)
         if not result:
             return JSONResponse({"error": "no response acquired from the optimizer."}, 400)
         if isinstance(result, dict) and result.get("error") and not s.compat_request_route_200:
@@ -345,7 +387,7 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         payload = await _json_body(request, silent=True) or {}
         if not isinstance(payload, dict):
             payload = {}
-        result = await _optimize_one(payload)
+        result = await _route(payload)
         if isinstance(result, dict) and result.get("error"):
             return JSONResponse(result, 400)
         if payload.get("use_ml_eta"):

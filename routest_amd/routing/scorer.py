@@ -36,6 +36,7 @@ class RouteScorer:
             self._hip = GcnScorerHip(self.model, g, self.device)
             self._hip.node_delays()
         self.engine = "gcn-hip" if self._hip is not None else "gcn-cpu"
+        self.training: Optional[Dict[str, Any]] = None     # set when trained (models/gcn_train.py)
 
     @classmethod
     def synthetic(cls, num_nodes: int = 100_000, device=None) -> "RouteScorer":
@@ -93,4 +94,4 @@ class RouteScorer:
             scores = score_routes_ref(self.g, self.node_delays(), node_lists)
         best = int(np.argmin(scores)) if len(scores) else None
         return {"scores": [float(x) for x in scores], "best": best, "engine": self.engine,
-                "nodes_per_route": [len(n) for n in node_lists]}
+                "trained": self.training is not None, "nodes_per_route": [len(n) for n in node_lists]}

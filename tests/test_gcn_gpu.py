@@ -38,6 +38,28 @@ def test_gcn_delays_and_route_scores(n):
     np.testing.assert_allclose(sc, score_routes_ref(g, got, routes), rtol=1e-3)
 
 
+def test_gcn_trained_delays_relative_to_spread():
+    """On a TRAINED scorer (outputs spread over the delay range, not sitting at the softplus floor
+    like a random init): kernel delays vs the fp32 reference, max error relative to the mean
+    absolute deviation of the reference (the K2 criterion), and route-score ranks."""
+    from routest_amd.models.gcn_train import train
+    from routest_amd.routing.graph import edge_costs
+    from routest_amd.serve.eta_service import default_model
+    from scipy.stats import spearmanr
+    g = synth_road_graph(20_000, seed=8)
+    cost = edge_costs(g, default_model(hidden=64, steps=60), device=torch.device("cuda", 0))
+    m, _ = train(g, cost, steps=150, lr=5e-3, device="cuda:0")
+    with torch.no_grad():
+        ref = m(GcnScorer.adjacency(g), torch.from_numpy(g.features)).numpy()
+    spread = float(np.abs(ref - ref.mean()).mean())
+    assert spread > 0.1, spread                      # a real spread of delay factors
+    got = GcnScorerHip(m, g, torch.device("cuda:0")).node_delays().cpu().numpy()
+    assert float(np.abs(got - ref).max()) / spread < 0.05
+    routes = _random_walks(g, 400, seed=3)
+    a, b = score_routes_ref(g, got, routes), score_routes_ref(g, ref, routes)
+    assert spearmanr(a, b).correlation > 0.999
+
+
 def test_gcn_partition_rows_match_full():
     g = synth_road_graph(20_000, seed=3)
     m = GcnScorer(seed=4)
