@@ -72,6 +72,8 @@ def parse_args():
                          "'dp_training_large_batch'; 0 skips)")
     ap.add_argument("--route-requests", type=int, default=10_000,
                     help="config 5: concurrent multi-stop requests per step over all ranks")
+    ap.add_argument("--route-http-seconds", type=float, default=4.0,
+                    help="route_optimizer.http: seconds of 1k-concurrency optimize_route load on the main port")
     ap.add_argument("--route-steps", type=int, default=3,
                     help="also time this many steps of the batched route optimizer (K5 + K6 + one "
                          "A* launch over MLP edge costs; extra JSON key 'route_optimizer'; skipped "
@@ -455,6 +457,7 @@ def main() -> None:
     # step K5 + K6 for all of a rank's requests, then every trip leg in ONE batched A* launch over
     # MLP-learned edge times (no collective; timing max over ranks)
     route_res = None
+    route_cost = None
     if a.route_steps > 0 and not (share and world > 1):
         from routest_amd.data.graph import synth_road_graph
         from routest_amd.routing.bulk import BulkRouteStep
@@ -464,6 +467,7 @@ def main() -> None:
             g = synth_road_graph(100_000, seed=0)
         torch.manual_seed(0)
         cost = edge_costs(g, default_model(hidden=a.hidden, steps=200), device=dev)
+        route_cost = cost
         bulk = BulkRouteStep(g, cost, dev, a.route_requests // world, seed=100 + rank)
         bulk.step()
         torch.cuda.synchronize()
@@ -499,17 +503,30 @@ def main() -> None:
     p50_py_ms = None
     conc = None
     if a.p50 and rank == 0:
-        # (1) headline p50: real HTTP/1.1 over loopback (keep-alive, http.client) to the native
-        #     prediction front end (csrc/native_server.hip): socket -> C++ JSON pack -> fused HIP
-        #     kernel on this GPU (zero-copy) -> C++ response formatting.  Same endpoint semantics
-        #     as the FastAPI handler (byte-identical bodies, tests/test_native_server_gpu.py).
+        # (1) headline p50 on the MAIN port of the stack `routest serve` runs (serve/frontend.py
+        #     ServingStack): real HTTP/1.1 over loopback (keep-alive) to the native front end
+        #     (csrc/native_server.hip): socket -> C++ JSON pack -> fused HIP kernel on this GPU
+        #     (zero-copy) -> C++ response formatting; the FastAPI app sits behind it for the long
+        #     tail.  Same endpoint semantics as the FastAPI handler (byte-identical bodies,
+        #     tests/test_frontend_gpu.py).  With the road graph of config 5 loaded, the same port
+        #     also serves the route_optimizer HTTP variant below.
         import http.client
-        from routest_amd.serve.native_server import NativePredictServer
+        from routest_amd.api.app import build_services, create_app
+        from routest_amd.config import load_settings
+        from routest_amd.serve.eta_service import EtaService
+        from routest_amd.serve.frontend import ServingStack
+        from routest_amd.serve.loadgen import native_route_load, route_payloads
         body = {"summary": {"distance": 12345}, "pickup_time": "2026-10-15T08:30:00",
                 "driver_age": 34, "weather": "Sunny", "traffic": "Medium"}
         raw = json.dumps(body).encode()
         hdr = {"Content-Type": "application/json"}
-        with NativePredictServer(model, device=local_rank, threads=4) as srv:
+        prov = None
+        if g is not None and route_cost is not None:
+            from routest_amd.routing.graph import GraphProvider
+            prov = GraphProvider(g, route_cost, device=dev)
+        ss = load_settings(env={}, dotenv_path=None, devices=[local_rank], warm_scorer=False)
+        sv = build_services(ss, eta=EtaService(model, devices=[local_rank]), provider=prov, store=None)
+        with ServingStack(sv, create_app(sv), model, [local_rank], threads=8) as srv:
             # native closed-loop client (csrc/runtime/http_client.h): one keep-alive connection,
             # one request in flight — the client adds ~1 us instead of http.client's ~30 us
             from routest_amd.ops import _ext
@@ -537,6 +554,12 @@ def main() -> None:
             r16 = rtm.http_load(srv.port, 16, 2.0, "/api/predict_eta", raw.decode(), 4, 0, 50)
             assert r16["errors"] == 0, r16
             conc = r16["requests"] / r16["seconds"]
+            # config 5 as a service: 1k concurrent multi-stop optimize_route requests on the same
+            # port — K5 + K6 + batched A* + path copy-out + C++ GeoJSON + response bytes
+            if prov is not None and route_res is not None and srv.front.routes:
+                route_res["http"] = native_route_load(srv, route_payloads(g.lat, g.lon, 1000, seed=1), 1000,
+                                                      a.route_http_seconds)
+        sv.eta.close()
 
         # (2) the FastAPI app in-process over ASGI (like the reference's Flask test-client figure)
         import asyncio
@@ -593,7 +616,9 @@ def main() -> None:
             "step_vs_h2d_copy_only": (h2d_only_ms / (elapsed / a.steps * 1e3)) if h2d_only_ms else None,
             "p50_predict_ms": p50_ms,
             "p99_predict_ms": p99_ms,
-            "p50_path": "HTTP/1.1 loopback keep-alive POST /api/predict_eta -> native front end (C++ reactor, fused HIP kernel); native closed-loop client",
+            "p50_path": "main port of the serving stack (`routest serve`: native front end + FastAPI app behind it): "
+                        "HTTP/1.1 loopback keep-alive POST /api/predict_eta -> C++ reactor -> fused HIP kernel; "
+                        "native closed-loop client",
             "p50_python_client_ms": p50_py_ms,
             "p50_fastapi_asgi_ms": p50_fastapi_ms,
             "http_concurrent16_req_per_s": conc,

@@ -60,47 +60,21 @@ def main() -> None:
         rng = np.random.default_rng(0)
         lat, lon = 14.55 + rng.normal(0, 0.05, 20000), 121.03 + rng.normal(0, 0.05, 20000)
         g = None
-    rng = np.random.default_rng(1)
-    reqs = []
-    for i in range(a.concurrency):
-        idx = rng.integers(0, len(lat), int(rng.integers(3, 12)))
-        reqs.append({"source_point": {"lat": float(lat[idx[0]]), "lon": float(lon[idx[0]])},
-                     "destination_points": [{"lat": float(lat[j]), "lon": float(lon[j]), "payload": 1}
-                                            for j in idx[1:]],
-                     "driver_details": {"driver_name": f"v{i}", "vehicle_type": "car",
-                                        "vehicle_capacity": 4, "maximum_distance": 1e7}})
+    from routest_amd.serve.loadgen import native_route_load, route_payloads
+    reqs = route_payloads(lat, lon, a.concurrency, seed=1)
     out = {"metric": "optimize_route req/s (concurrent HTTP)", "provider": a.provider,
            "concurrency": a.concurrency, "stops": "2-10 per request"}
     if "native" in modes:
-        from routest_amd.ops import _ext
         from routest_amd.serve.eta_service import default_model
         from routest_amd.serve.frontend import ServingStack
-        rt = _ext.runtime(required=True)
         s = load_settings(env={}, dotenv_path=None, devices=[0], route_batch="0", warm_scorer=False)
         model = default_model(steps=30)
         sv = build_services(s, eta=EtaService(model, devices=[0]), provider=prov, store=None)
         app = create_app(sv)
         with ServingStack(sv, app, model, [0], threads=a.threads, batch_max=a.batch_max,
                           timeout_us=min(a.timeout_us, 1000)) as st:
-            bodies = [json.dumps(r) for r in reqs]
-            paths = ["/api/optimize_route"] * len(bodies)
-            rt.http_load_multi(st.port, min(64, a.concurrency), 2.0, paths, bodies, a.client_threads)   # warm-up
-            f0 = st.front.stats()
-            r = rt.http_load_multi(st.port, a.concurrency, a.seconds, paths, bodies, a.client_threads, 0, 1)
-            f1 = st.front.stats()
-            lat_us = r["latencies_us"]
-            out["native"] = {"req_per_s": r["requests"] / r["seconds"], "errors": int(r["errors"]),
-                             "p50_ms": float(lat_us[len(lat_us) // 2]) / 1e3 if len(lat_us) else None,
-                             "p99_ms": float(lat_us[int(len(lat_us) * 0.99) - 1]) / 1e3 if len(lat_us) else None,
-                             "response_MB_per_s": r["bytes"] / r["seconds"] / 1e6,
-                             "flushes": f1["route_flushes"] - f0["route_flushes"],
-                             "legs_searched": f1["route_legs"] - f0["route_legs"],
-                             "legs_on_host": f1["route_host_legs"] - f0["route_host_legs"],
-                             "fallbacks_to_python": f1["route_service_fallbacks"] - f0["route_service_fallbacks"],
-                             "stage_ms_per_flush": {k[9:]: (f1[k] - f0[k]) / 1e3 / max(1, f1["route_flushes"] - f0["route_flushes"])
-                                                    for k in f1 if k.startswith("route_us_")},
-                             "front_threads": a.threads, "client": "native closed-loop (csrc/runtime/http_client.h)",
-                             "path": "HTTP/1.1 loopback -> native front end main port -> route service"}
+            out["native"] = native_route_load(st, reqs, a.concurrency, a.seconds, a.client_threads)
+            out["native"]["front_threads"] = a.threads
         print(json.dumps({"native": out["native"]}), flush=True)
     for mode in [m for m in modes if m in ("batched", "per_request")]:
         s = load_settings(env={}, dotenv_path=None, devices=[0],

@@ -2,28 +2,47 @@
 // Conceptually replaces the reference's per-trip ORS directions calls (RO/Flaskr/utils.py:55-62,
 // 151-156), which it issues one at a time over HTTPS.
 //
-// One LANE per query ("slot"): tens of thousands of independent searches in flight, each with
-//   * dense per-slot state[N]: one 8-byte word (g as f32 | parent, closed bit) per node, so a
-//     relaxation is one random access — 80k slots x 100k nodes = 64 GB, which 288 GB of HBM3E makes
-//     the simple and fast choice (no hashing);
-//   * an 8-ary min-heap (LaneHeap) of (f, node) 64-bit entries with lazy deletion (stale pops are
-//     skipped via the closed bit; the heuristic is consistent, so a node's first pop is final);
-//   * a touched list, so only the entries a search wrote are reset afterwards (no N-sized memset
-//     per query).
-// Launch time is set by the LONGEST search (one lane walks its own heap), so the heuristic matters
-// most in the tail: 32 landmarks (vs 16) cut p99 pops 28k -> 12k and the 80k-leg launch 671 ->
-// 444 ms (bench/astar_tail.py).
-// Heuristic: max(great-circle distance x circuity / v_max, ALT landmark bound); edge costs are
-// floored at length / v_max on the host, so both are admissible and consistent (ALT tables are
-// shrunk by 1e-4 against fp32 rounding).  Every lane stops within max_iters pops (status 3), on heap
-// or touched-list overflow (status 2) or when the open set empties (status 1): the grid always
-// drains.  Paths are written target->source then reversed in place.
+// Per-search state is SPARSE: every search owns an open-addressing hash table of 16-byte entries
+//   { key = node id, h = cached heuristic (NaN: not computed yet), w = g (f32) << 32 | closed | parent slot }
+// sized to what the search may touch, not to the graph — workspace is O(slots x table), independent
+// of N, so a 1M-node graph serves as many concurrent searches as a 10k-node one (the round-2 design
+// kept a dense [slots, N] state plus a [slots, N] heuristic cache: 153 GB for 80k searches on a
+// 100k-node graph, and no 1M-node graph fit at all).  Linear probing with a hash that is the identity
+// on the low bits: ids that are neighbours in the graph (row-major grids, Morton-ordered OSM) land in
+// neighbouring entries, so a second probe is almost always the same 128-byte line.  Parent pointers
+// are table slots, so the path walk needs no probing; the reset list holds slots as well.
+//
+// Three tiers, each an AstarWs (tables + heap rows + reset lists), run by astar_search():
+//   lane  — one LANE per query, an 8-ary lane heap (LaneHeap), `lane_pops` pops in small tables
+//           (a few thousand entries): most legs finish here;
+//   wave  — one WAVE per remaining query (table/heap overflow or pop budget spent), expanding a whole
+//           f-band at once (label-correcting, exact) in medium tables; the launch is no longer as
+//           long as the single longest search;
+//   big   — searches that overflowed a medium table rerun in a few very large tables (>= 2N entries:
+//           they cannot overflow);
+// only searches that exceed max_iters fall back to the host.  Small batches (interactive flushes)
+// skip the lane tier: one 64-lane wave per search fills the chip.
+// Heuristic: max(great-circle distance x circuity / v_max, ALT landmark bound); edge costs are floored
+// at length / v_max on the host, so both are admissible and consistent (ALT tables are shrunk by 1e-4
+// against fp32 rounding).  Every search stops within max_iters pops (status 3), on overflow (2) or
+// when the open set empties (1): the grid always drains.
+#include <chrono>
 #include <cstdlib>
 
 #include "common.h"
 #include "ops.h"
 
 namespace rt {
+
+struct __align__(16) AEnt {
+  unsigned key;              // node id, EMPTY = free
+  float h;                   // cached heuristic, NaN = not computed
+  unsigned long long w;      // g (f32 bits) << 32 | closed (bit 31) | parent slot (31 b)
+};
+constexpr unsigned EMPTY = 0xffffffffu;
+constexpr unsigned long long W_INIT = ~0ull;    // the all-ones reset pattern: g unset (reads as +inf)
+constexpr unsigned NOPAR = 0x7fffffffu;
+constexpr unsigned CLOSEDB = 0x80000000u;
 
 struct AstarArgs {
   const int* indptr;
@@ -33,23 +52,22 @@ struct AstarArgs {
   const float* lon;
   const int* src;        // [Q]
   const int* dst;
-  unsigned long long* st;  // [S][N] packed per-node state: g (f32 bits, low) | parent (31 b) + closed (bit 63)
-  unsigned long long* heap;  // [S][cap]
-  int* touched;          // [S][cap]
+  AEnt* tab;             // [S][1 << tbits] per-search hash tables (all-ones when idle)
+  unsigned long long* heap;  // [S][cap] lane heap / wave near+far lists
+  int* touched;          // [S][(1 << tbits) / 2] table slots a search wrote (reset list)
   float* out_cost;       // [Q]
   int* out_len;          // [Q]
   int* out_status;       // [Q]
   int* out_path;         // [Q][max_path]
-  int N, Q, q0, S, cap, max_path, max_iters;
+  int N, Q, q0, S, cap, tbits, max_path, max_iters;
   float inv_vmax;        // seconds per metre at v_max
   const float* lm;       // [N][2K] ALT landmark tables: d(L_k -> v), d(v -> L_k) (nullptr: off)
   int K;
-  int* out_iters;        // [Q] heap pops per query (nullptr: not recorded)
+  int* out_iters;        // [Q] pops (lane) / expansions (wave) per query (nullptr: not recorded)
 };
 
 constexpr int KMAX = 32;
-// edges relaxed per batch of independent loads (road-graph degrees are 2-6, mostly 4-5); 80k-leg
-// launch: RB 4 236 ms, 6 243 ms, 8 259 ms; evaluating the batch's heuristics together was neutral
+// edges relaxed per batch of independent loads (road-graph degrees are 2-6, mostly 4-5)
 constexpr int RB = 4;
 
 __device__ __forceinline__ float hdist(const AstarArgs& a, int v, float tlat, float tlon, float ctl) {
@@ -79,15 +97,46 @@ __device__ __forceinline__ float halt(const AstarArgs& a, int v, const float (&f
   return best * 0.9999f;
 }
 
-// One 8-byte word per (slot, node): a relaxation reads g and the closed bit with ONE random access
-// (the searches are bound by random HBM lines: 80k searches x dense 100k-node state = 64 GB).
-__device__ __forceinline__ float st_g(unsigned long long w) { return __uint_as_float((unsigned)w); }
-__device__ __forceinline__ unsigned st_p(unsigned long long w) { return (unsigned)(w >> 32); }
-__device__ __forceinline__ unsigned long long st_make(float g, unsigned p) {
-  return ((unsigned long long)p << 32) | __float_as_uint(g);
+template <int K>
+__device__ __forceinline__ void load_target_lm(const AstarArgs& a, int t, float (&ft)[KMAX], float (&bt)[KMAX]) {
+  if constexpr (K > 0) {
+    const float4* row = reinterpret_cast<const float4*>(a.lm + (size_t)t * 2 * K);
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) {
+      const float4 x = row[i];
+      ft[2 * i] = x.x;
+      ft[2 * i + 1] = x.y;
+      bt[2 * i] = x.z;
+      bt[2 * i + 1] = x.w;
+    }
+  }
 }
-constexpr unsigned long long ST_INIT = 0x7fffffff7f800000ull;   // g = +inf, parent = none, open
 
+// identity on the low bits, high bits mixed in (see the header comment)
+__device__ __forceinline__ unsigned hslot(unsigned u, int tbits) {
+  return (u ^ ((u >> tbits) * 0x9E3779B1u)) & ((1u << tbits) - 1u);
+}
+__device__ __forceinline__ AEnt ld_ent(const AEnt* p) {
+  const uint4 x = *reinterpret_cast<const uint4*>(p);
+  AEnt e;
+  e.key = x.x;
+  e.h = __uint_as_float(x.y);
+  e.w = ((unsigned long long)x.w << 32) | x.z;
+  return e;
+}
+__device__ __forceinline__ void st_ent(AEnt* p, unsigned key, float h, unsigned long long w) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(key, __float_as_uint(h), (unsigned)w, (unsigned)(w >> 32));
+}
+__device__ __forceinline__ void clr_ent(AEnt* p) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(~0u, ~0u, ~0u, ~0u);
+}
+__device__ __forceinline__ float w_g(unsigned long long w) {
+  return w == W_INIT ? __int_as_float(0x7f800000) : __uint_as_float((unsigned)(w >> 32));
+}
+__device__ __forceinline__ unsigned w_par(unsigned long long w) { return (unsigned)w & NOPAR; }
+__device__ __forceinline__ unsigned long long w_make(float g, unsigned par) {
+  return ((unsigned long long)__float_as_uint(g) << 32) | par;
+}
 __device__ __forceinline__ unsigned long long hkey(float f, int v) {
   return ((unsigned long long)__float_as_uint(f) << 32) | (unsigned)v;   // f >= 0: monotone bits
 }
@@ -165,34 +214,47 @@ struct LaneHeap {
   }
 };
 
+// Walk parent slots from t's slot pt to s; writes the path source-first.  Returns the length, or -1
+// when it does not fit max_path.
+__device__ __forceinline__ int write_path(const AstarArgs& a, const AEnt* tab, unsigned pt, int s, int q) {
+  int* path = a.out_path + (size_t)q * a.max_path;
+  int len = 0;
+  unsigned p = pt;
+  while (true) {
+    if (len >= a.max_path) return -1;
+    const AEnt e = ld_ent(tab + p);
+    path[len++] = (int)e.key;
+    if ((int)e.key == s) break;
+    p = w_par(e.w);
+  }
+  for (int i = 0, j = len - 1; i < j; ++i, --j) {
+    const int tmp = path[i];
+    path[i] = path[j];
+    path[j] = tmp;
+  }
+  return len;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Lane tier: one lane per query, a private table (no atomics), lazy-deletion heap of (f, node).
 template <int K, int D>
-__global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
-  // XCD-aware: workgroup b runs on XCD b % 8; give each XCD a contiguous range of queries, so with
-  // source-sorted queries one XCD's L2 serves one region of the graph (edges, costs, ALT rows)
+__global__ __launch_bounds__(64) void astar_kernel(AstarArgs a) {
+  // XCD-aware: workgroup b runs on XCD b % 8; give each XCD a contiguous range of queries
   const int lb = (int)(blockIdx.x % 8u) * (int)(gridDim.x / 8u) + (int)(blockIdx.x / 8u);
   const int slot = lb * blockDim.x + threadIdx.x;
   const int q = a.q0 + slot;
   if (q >= a.Q || slot >= a.S) return;
-  unsigned long long* st = a.st + (size_t)slot * a.N;
+  const int tb = a.tbits;
+  const unsigned mask = (1u << tb) - 1u;
+  const int tcap = 1 << (tb - 1);
+  AEnt* tab = a.tab + ((size_t)slot << tb);
   unsigned long long* heap = a.heap + (size_t)slot * a.cap;
-  int* touched = a.touched + (size_t)slot * a.cap;
+  int* touched = a.touched + (size_t)slot * tcap;
   const int s = a.src[q], t = a.dst[q];
   const float k = 0.017453292519943295f;
   const float tlat = a.lat[t] * k, tlon = a.lon[t] * k, ctl = __cosf(tlat);
-  const unsigned CLOSED = 0x80000000u;
-
   float ft[KMAX], bt[KMAX];  // landmark distances of the target (registers: K is a constant)
-  if constexpr (K > 0) {
-    const float4* row = reinterpret_cast<const float4*>(a.lm + (size_t)t * 2 * K);
-#pragma unroll
-    for (int q = 0; q < K / 2; ++q) {
-      const float4 x = row[q];
-      ft[2 * q] = x.x;
-      ft[2 * q + 1] = x.y;
-      bt[2 * q] = x.z;
-      bt[2 * q + 1] = x.w;
-    }
-  }
+  load_target_lm<K>(a, t, ft, bt);
   auto heur = [&](int v) {
     float hv = hdist(a, v, tlat, tlon, ctl);
     if constexpr (K > 0) hv = fmaxf(hv, halt<K>(a, v, ft, bt));
@@ -202,30 +264,42 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
   int hn = 0, nt = 0, status = 1;
   const int capq = a.cap - 16;         // room for the shifted storage and a full child block
   LaneHeap<D> hq(heap);
-  st[s] = st_make(0.f, 0x7fffffffu);
-  touched[nt++] = s;
-  hq.push(hn, hkey(heur(s), s));
+  {
+    const unsigned ps = hslot((unsigned)s, tb);     // the table is empty
+    const float hs = heur(s);
+    st_ent(tab + ps, (unsigned)s, hs, w_make(0.f, NOPAR));
+    touched[nt++] = (int)ps;
+    hq.push(hn, hkey(hs, s));
+  }
+  unsigned pt = 0;
   int it = 0;
   for (; hn > 0; ++it) {
     if (it >= a.max_iters) { status = 3; break; }
-    // pop min: the popped node's own loads (state word, CSR row bounds) are issued BEFORE the
+    // pop min: the popped node's own loads (table entry, CSR row bounds) are issued BEFORE the
     // sift-down, so their latency overlaps the heap's dependent chain
     const unsigned long long top = hq.top();
     const int v = (int)(unsigned)(top & 0xffffffffu);
-    const unsigned long long wv = st[v];
+    unsigned pv = hslot((unsigned)v, tb);
+    AEnt ev = ld_ent(tab + pv);
     const int e0 = a.indptr[v], e1 = a.indptr[v + 1];
     hq.pop(hn);
-    if (st_p(wv) & CLOSED) continue;     // stale duplicate
-    st[v] = wv | ((unsigned long long)CLOSED << 32);
-    if (v == t) { status = 0; break; }
-    const float gv = st_g(wv);
+    for (unsigned n = 0; ev.key != (unsigned)v && n < mask; ++n) {   // a pushed node is in the table
+      pv = (pv + 1) & mask;
+      ev = ld_ent(tab + pv);
+    }
+    if (ev.key != (unsigned)v) { status = 2; break; }
+    if ((unsigned)ev.w & CLOSEDB) continue;         // stale duplicate
+    tab[pv].w = ev.w | CLOSEDB;
+    if (v == t) { status = 0; pt = pv; break; }
+    const float gv = w_g(ev.w);
     bool overflow = false;
-    // relax in chunks of RB edges: all (target, cost) loads, then all target state loads, are
+    // relax in chunks of RB edges: all (target, cost) loads, then all first-probe entry loads, are
     // issued together — two round trips per chunk instead of two per edge
     for (int eb = e0; eb < e1 && !overflow; eb += RB) {
       int uu[RB];
       float cc[RB];
-      unsigned long long wu[RB];
+      unsigned pp[RB];
+      AEnt ee[RB];
 #pragma unroll
       for (int j = 0; j < RB; ++j) {
         const bool in = eb + j < e1;
@@ -233,29 +307,45 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
         cc[j] = in ? a.cost[eb + j] : 0.f;
       }
 #pragma unroll
-      for (int j = 0; j < RB; ++j) wu[j] = eb + j < e1 ? st[uu[j]] : (ST_INIT | ((unsigned long long)CLOSED << 32));
+      for (int j = 0; j < RB; ++j) {
+        pp[j] = hslot((unsigned)uu[j], tb);
+        if (eb + j < e1) ee[j] = ld_ent(tab + pp[j]);
+      }
 #pragma unroll
       for (int j = 0; j < RB; ++j) {
-        if (eb + j >= e1 || (st_p(wu[j]) & CLOSED)) continue;
-        const int u = uu[j];
-        const float ng = gv + cc[j];
-        float gu = st_g(wu[j]);
-        bool fresh = gu == __int_as_float(0x7f800000);
+        if (eb + j >= e1) continue;
+        const unsigned u = (unsigned)uu[j];
+        unsigned p = pp[j];
+        AEnt e = ee[j];
+        // an earlier edge of this chunk may have written this entry (same target, or an insert
+        // into the slot this probe started at): re-read it
+        bool stale = false;
 #pragma unroll
-        for (int i = 0; i < j; ++i)             // a repeated target within the chunk: its state
-          if (uu[i] == u && eb + i < e1) {      // word may have been updated by edge i
-            const unsigned long long w2 = st[u];
-            gu = st_g(w2);
-            fresh = gu == __int_as_float(0x7f800000);
-          }
-        if (ng < gu) {
-          if (fresh) {                          // first touch
-            if (nt >= capq) { overflow = true; break; }
-            touched[nt++] = u;
-          }
-          st[u] = st_make(ng, (unsigned)v);
+        for (int i = 0; i < j; ++i) {
+          if (eb + i >= e1) continue;
+          if ((unsigned)uu[i] == u) { p = pp[i]; stale = true; }
+          else if (pp[i] == p) stale = true;
+        }
+        if (stale) e = ld_ent(tab + p);
+        // (an empty entry is always reachable: inserts stop at half the table)
+        for (unsigned n = 0; e.key != u && e.key != EMPTY && n < mask; ++n) {
+          p = (p + 1) & mask;
+          e = ld_ent(tab + p);
+        }
+        if (e.key != u && e.key != EMPTY) { overflow = true; break; }
+        pp[j] = p;
+        const float ng = gv + cc[j];
+        if (e.key == EMPTY) {                       // first touch
+          if (nt >= tcap || hn >= capq) { overflow = true; break; }
+          const float hu = heur((int)u);
+          st_ent(tab + p, u, hu, w_make(ng, pv));
+          touched[nt++] = (int)p;
+          hq.push(hn, hkey(ng + hu, (int)u));
+        } else {
+          if (((unsigned)e.w & CLOSEDB) || !(ng < w_g(e.w))) continue;
           if (hn >= capq) { overflow = true; break; }
-          hq.push(hn, hkey(ng + heur(u), u));
+          tab[p].w = w_make(ng, pv);
+          hq.push(hn, hkey(ng + e.h, (int)u));
         }
       }
     }
@@ -264,37 +354,20 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
   int len = 0;
   float total = 0.f;
   if (status == 0) {
-    total = st_g(st[t]);
-    int* path = a.out_path + (size_t)q * a.max_path;
-    int v = t;
-    while (true) {
-      if (len >= a.max_path) { status = 4; break; }
-      path[len++] = v;
-      if (v == s) break;
-      v = (int)(st_p(st[v]) & 0x7fffffffu);
-    }
-    if (status == 0) {
-      for (int i = 0, j = len - 1; i < j; ++i, --j) {
-        const int tmp = path[i];
-        path[i] = path[j];
-        path[j] = tmp;
-      }
-    } else {
-      len = 0;
-    }
+    total = w_g(tab[pt].w);
+    len = write_path(a, tab, pt, s, q);
+    if (len < 0) { status = 4; len = 0; }
   }
   if (a.out_iters) a.out_iters[q] = it;
   a.out_cost[q] = status == 0 ? total : -1.f;
   a.out_len[q] = len;
   a.out_status[q] = status;
-  // reset this slot's touched entries for the next batch
-  for (int i = 0; i < nt; ++i) st[touched[i]] = ST_INIT;
+  // reset the entries this search wrote (the table is all-ones again for the next query)
+  for (int i = 0; i < nt; ++i) clr_ent(tab + touched[i]);
 }
 
 // ---------------------------------------------------------------------------------------------
-// Tail stage: ONE WAVE per query, for the few searches that exhaust the lane kernel's pop budget.
-// The lane kernel's launch time is set by its longest search (a sequential chain of dependent HBM
-// loads, ~7.6 us per pop); here the 64 lanes of a wave expand a whole f-band at once:
+// Wave tier: ONE WAVE per query.  The 64 lanes of a wave expand a whole f-band at once:
 //
 //   near = open nodes with f = g + h < thr;  far = the other open nodes as (f, node) pairs
 //   repeat: every lane takes a near node, relaxes its edges with a 64-bit atomicMin on the packed
@@ -304,58 +377,77 @@ __global__ __launch_bounds__(256) void astar_kernel(AstarArgs a) {
 //           the far entries below it become the next near set (entries with f >= best are dropped)
 //
 // Label-correcting (a node is re-expanded when its g improves; stale duplicates are harmless), so
-// costs are exact.  Per-slot memory is the lane kernel's: the state row (read in the swapped
-// layout g << 32 | parent, for which the reset value ST_INIT is still "+inf"), the heap row split
-// into near A | near B | far, and the touched list.
+// costs are exact.  The table is shared by the wave's lanes: a key is claimed with atomicCAS (the
+// claimer records the slot for the reset), the state word is lowered with atomicMin, and plain
+// loads only ever see older (larger) words, which at worst cost a redundant atomic.  The heap row
+// holds near A | near B | far.
 template <int K>
 __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* __restrict__ qidx, int T,
-                                                        float delta, float* __restrict__ hcache) {
+                                                        float delta) {
   const int w = blockIdx.x;
   if (w >= T || w >= a.S) return;
-  const int q = qidx[w];
+  const int q = qidx != nullptr ? qidx[w] : a.q0 + w;
   const int lane = threadIdx.x;
-  unsigned long long* st = a.st + (size_t)w * a.N;
+  const int tb = a.tbits;
+  const int TS = 1 << tb;
+  const unsigned mask = (unsigned)TS - 1u;
+  const int tcap = TS / 2;
+  AEnt* tab = a.tab + ((size_t)w << tb);
   int* nearA = reinterpret_cast<int*>(a.heap + (size_t)w * a.cap);
   const int NCAP = a.cap / 2;                       // ints per near list
   int* nearB = nearA + NCAP;
   unsigned long long* far = a.heap + (size_t)w * a.cap + a.cap / 2;
   const int FCAP = a.cap / 2;                       // (f, node) entries
-  int* touched = a.touched + (size_t)w * a.cap;
-  // per-slot heuristic cache: h(v) costs a 256-byte landmark row, and this stage re-reads it for
-  // every relaxation and expansion (it was bandwidth-bound on those rows); the first toucher of a
-  // node stores h, everyone else reads 4 bytes (NaN = not yet stored -> compute it)
-  float* hc = hcache + (size_t)w * a.N;
+  int* touched = a.touched + (size_t)w * tcap;
   __shared__ int s_next, s_far, s_touch, s_bad;
   const int s = a.src[q], t = a.dst[q];
   const float k = 0.017453292519943295f;
   const float tlat = a.lat[t] * k, tlon = a.lon[t] * k, ctl = __cosf(tlat);
   float ft[KMAX], bt[KMAX];
-  if constexpr (K > 0) {
-    const float4* row = reinterpret_cast<const float4*>(a.lm + (size_t)t * 2 * K);
-#pragma unroll
-    for (int i = 0; i < K / 2; ++i) {
-      const float4 x = row[i];
-      ft[2 * i] = x.x;
-      ft[2 * i + 1] = x.y;
-      bt[2 * i] = x.z;
-      bt[2 * i + 1] = x.w;
-    }
-  }
+  load_target_lm<K>(a, t, ft, bt);
   auto heur = [&](int v) {
     float hv = hdist(a, v, tlat, tlon, ctl);
     if constexpr (K > 0) hv = fmaxf(hv, halt<K>(a, v, ft, bt));
     return hv;
   };
-  // (the reset word ST_INIT reads as a NaN g in this layout: map it to +inf)
-  auto gof = [](unsigned long long x) {
-    return x == ST_INIT ? __int_as_float(0x7f800000) : __uint_as_float((unsigned)(x >> 32));
+  auto bad = [&]() { return *reinterpret_cast<volatile int*>(&s_bad) != 0; };
+  // slot of u, or -1 if absent (probes are bounded: the table is never more than half full
+  // unless the search overflowed, and then at most TS probes)
+  auto find = [&](unsigned u) -> int {
+    unsigned p = hslot(u, tb);
+    for (int n = 0; n < TS; ++n) {
+      const unsigned key = __hip_atomic_load(&tab[p].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (key == u) return (int)p;
+      if (key == EMPTY) return -1;
+      p = (p + 1) & mask;
+    }
+    return -1;
   };
-  auto pack = [](float g, unsigned p) { return ((unsigned long long)__float_as_uint(g) << 32) | p; };
+  // find-or-insert u starting at slot p; -1 when the table is full
+  auto acquire = [&](unsigned u, unsigned p, bool& claimed) -> int {
+    claimed = false;
+    for (int n = 0; n < TS; ++n) {
+      const unsigned key = __hip_atomic_load(&tab[p].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (key == u) return (int)p;
+      if (key == EMPTY) {
+        const unsigned old = atomicCAS(&tab[p].key, EMPTY, u);
+        if (old == EMPTY) { claimed = true; return (int)p; }
+        if (old == u) return (int)p;
+      }
+      p = (p + 1) & mask;
+    }
+    return -1;
+  };
+  int pt = -1;                                      // t's slot once inserted (slots never move)
+  auto gbest = [&]() -> float {
+    if (pt < 0) pt = find((unsigned)t);
+    return pt < 0 ? __int_as_float(0x7f800000) : w_g(tab[pt].w);
+  };
 
   if (lane == 0) {
-    hc[s] = heur(s);
-    st[s] = pack(0.f, 0x7fffffffu);
-    touched[0] = s;
+    const unsigned ps = hslot((unsigned)s, tb);
+    st_ent(tab + ps, (unsigned)s, heur(s), w_make(0.f, NOPAR));
+    touched[0] = (int)ps;
     nearA[0] = s;
     s_far = 0;
     s_touch = 1;
@@ -372,18 +464,22 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
     while (nnear > 0) {
       if (lane == 0) s_next = 0;
       __syncthreads();
-      const float best = gof(st[t]);
+      const float best = gbest();
       for (int i = lane; i < nnear; i += 64) {
+        if (bad()) break;
         const int v = cur[i];
-        const float gv = gof(st[v]);
-        float hv = hc[v];
-        if (hv != hv) hv = heur(v);
+        const int pv = find((unsigned)v);
+        if (pv < 0) continue;
+        const AEnt ev = ld_ent(tab + pv);
+        const float gv = w_g(ev.w);
+        const float hv = ev.h == ev.h ? ev.h : heur(v);
         if (!(gv + hv < best)) continue;                 // cannot lead to a better path
         const int e0 = a.indptr[v], e1 = a.indptr[v + 1];
         for (int eb = e0; eb < e1; eb += RB) {
-          // same batching as the lane kernel: all (target, cost), then all target words, in flight
+          // same batching as the lane tier: all (target, cost), then all first-probe entries
           int uu[RB];
           float cc[RB];
+          unsigned pp[RB];
           unsigned long long seen[RB];
 #pragma unroll
           for (int j = 0; j < RB; ++j) {
@@ -392,28 +488,38 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
             cc[j] = in ? a.cost[eb + j] : 0.f;
           }
 #pragma unroll
-          for (int j = 0; j < RB; ++j) seen[j] = eb + j < e1 ? st[uu[j]] : 0ull;
+          for (int j = 0; j < RB; ++j) {
+            pp[j] = hslot((unsigned)uu[j], tb);
+            seen[j] = 0ull;
+            if (eb + j < e1) {
+              const AEnt x = ld_ent(tab + pp[j]);
+              // known entry: its word; empty or another key: unknown (take the atomic path)
+              seen[j] = x.key == (unsigned)uu[j] ? x.w : W_INIT;
+            }
+          }
 #pragma unroll
           for (int j = 0; j < RB; ++j) {
             if (eb + j >= e1) continue;
             const int u = uu[j];
             const float ng = gv + cc[j];
-            const unsigned long long nw = pack(ng, (unsigned)v);
-            // plain load first: most relaxations do not improve, and a 64-bit atomic to HBM costs
-            // far more than a load
+            const unsigned long long nw = w_make(ng, (unsigned)pv);
+            // plain load first: most relaxations do not improve, and a 64-bit atomic costs far
+            // more than a load
             if (nw >= seen[j]) continue;
-            const unsigned long long old = atomicMin(st + u, nw);
-            if (nw >= old) continue;
-            float hu;
-            if (old == ST_INIT) {
+            bool claimed;
+            const int p = acquire((unsigned)u, pp[j], claimed);
+            if (p < 0) { s_bad = 1; break; }
+            if (claimed) {
               const int ti = atomicAdd(&s_touch, 1);
-              if (ti < a.cap) touched[ti] = u;
-              else s_bad = 1;
+              if (ti < tcap) touched[ti] = p;
+              else s_bad = 1;                        // (the reset then clears the whole table)
+            }
+            const unsigned long long old = atomicMin(&tab[p].w, nw);
+            if (nw >= old) continue;
+            float hu = tab[p].h;
+            if (hu != hu) {
               hu = heur(u);
-              hc[u] = hu;
-            } else {
-              hu = hc[u];
-              if (hu != hu) hu = heur(u);
+              tab[p].h = hu;
             }
             const float f = ng + hu;
             if (f < thr) {
@@ -422,7 +528,7 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
               else s_bad = 1;
             } else {
               const int fi = atomicAdd(&s_far, 1);
-              if (fi < FCAP) far[fi] = pack(f, (unsigned)u);
+              if (fi < FCAP) far[fi] = hkey(f, u);
               else s_bad = 1;
             }
           }
@@ -439,11 +545,11 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
     }
     if (status >= 2) break;
     // near band exhausted: optimal if no open node can beat best; else open the next band
-    const float best = gof(st[t]);
+    const float best = gbest();
     const int nfar = s_far < FCAP ? s_far : FCAP;
     float fmin = __int_as_float(0x7f800000);
     for (int i = lane; i < nfar; i += 64) {
-      const float f = gof(far[i]);
+      const float f = __uint_as_float((unsigned)(far[i] >> 32));
       if (f < best) fmin = fminf(fmin, f);
     }
 #pragma unroll
@@ -460,7 +566,7 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
     for (int i0 = 0; i0 < nfar; i0 += 64) {
       const int i = i0 + lane;
       const unsigned long long x = i < nfar ? far[i] : ~0ull;
-      const float f = gof(x);
+      const float f = __uint_as_float((unsigned)(x >> 32));
       const bool to_near = i < nfar && f < thr;
       const bool keep = i < nfar && !to_near && f < best;
       const unsigned long long mk = __ballot(keep);
@@ -478,28 +584,15 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
     nnear = s_next < NCAP ? s_next : NCAP;
     if (s_bad) { status = 2; break; }
   }
-  const float total = gof(st[t]);
-  int len = 0;
-  if (status < 2) status = total < __int_as_float(0x7f800000) ? 0 : 1;
+  __syncthreads();
   if (lane == 0) {
+    const int ptt = find((unsigned)t);
+    const float total = ptt < 0 ? __int_as_float(0x7f800000) : w_g(tab[ptt].w);
+    int len = 0;
+    if (status < 2) status = total < __int_as_float(0x7f800000) ? 0 : 1;
     if (status == 0) {
-      int* path = a.out_path + (size_t)q * a.max_path;
-      int v = t;
-      while (true) {
-        if (len >= a.max_path) { status = 4; break; }
-        path[len++] = v;
-        if (v == s) break;
-        v = (int)((unsigned)st[v] & 0x7fffffffu);
-      }
-      if (status == 0) {
-        for (int i = 0, j = len - 1; i < j; ++i, --j) {
-          const int tmp = path[i];
-          path[i] = path[j];
-          path[j] = tmp;
-        }
-      } else {
-        len = 0;
-      }
+      len = write_path(a, tab, (unsigned)ptt, s, q);
+      if (len < 0) { status = 4; len = 0; }
     }
     if (a.out_iters) a.out_iters[q] = (int)(expanded < 0x7fffffff ? expanded : 0x7fffffff);
     a.out_cost[q] = status == 0 ? total : -1.f;
@@ -507,47 +600,64 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
     a.out_status[q] = status;
   }
   __syncthreads();
-  const int nt = s_touch < a.cap ? s_touch : a.cap;
-  for (int i = lane; i < nt; i += 64) {
-    const int v = touched[i];
-    st[v] = ST_INIT;
-    hc[v] = __int_as_float(-1);                      // NaN: not cached
+  const int nt = s_touch;
+  if (nt <= tcap) {
+    for (int i = lane; i < nt; i += 64) clr_ent(tab + touched[i]);
+  } else {                                            // claims past the reset list: clear everything
+    for (int i = lane; i < TS; i += 64) clr_ent(tab + i);
   }
 }
 
-hipError_t launch_astar_wave(const int* indptr, const int* indices, const float* cost, const float* lat,
-                             const float* lon, const int* src, const int* dst, void* state, void* heap,
-                             int* touched, float* out_cost, int* out_len, int* out_status, int* out_path,
-                             int N, int Q, int slots, int cap, int max_path, int max_iters, float inv_vmax,
-                             const float* lm, int K, const int* qidx, int T, float delta, float* hcache,
-                             int hrows, hipStream_t stream, int* out_iters) {
-  int n = T < slots ? T : slots;
-  if (n > hrows) n = hrows;
-  if (n <= 0) return hipSuccess;
-  if (lm != nullptr && K != 32 && K != 16 && K != 8) return hipErrorInvalidValue;
-  if (cap < 128) return hipErrorInvalidValue;
-  AstarArgs a{indptr, indices, cost, lat, lon, src, dst, (unsigned long long*)state,
-              (unsigned long long*)heap, touched, out_cost, out_len, out_status, out_path,
-              N, Q, 0, slots, cap, max_path, max_iters, inv_vmax, lm, K, out_iters};
-  if (lm == nullptr) hipLaunchKernelGGL(astar_wave_kernel<0>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, hcache);
-  else if (K == 8) hipLaunchKernelGGL(astar_wave_kernel<8>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, hcache);
-  else if (K == 16) hipLaunchKernelGGL(astar_wave_kernel<16>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, hcache);
-  else hipLaunchKernelGGL(astar_wave_kernel<32>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, hcache);
-  return hipGetLastError();
+// Ordered compaction: qidx = [i for i in range(Q) if (1 << status[i]) & want], count = len (one block;
+// the order is the query order, so tier slots — and results under exact ties — are deterministic).
+__global__ __launch_bounds__(1024) void astar_select_kernel(const int* __restrict__ status, int Q, int want,
+                                                            int* __restrict__ qidx, int* __restrict__ count) {
+  __shared__ int wsum[16];
+  __shared__ int base;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  for (int i0 = 0; i0 < Q; i0 += 1024) {
+    const int i = i0 + (int)threadIdx.x;
+    const int sv = i < Q ? status[i] : -1;
+    const bool f = sv >= 0 && sv < 31 && ((want >> sv) & 1);
+    const unsigned long long m = __ballot(f);
+    if (lane == 0) wsum[wv] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int k = 0; k < wv; ++k) off += wsum[k];
+    if (f) qidx[off + __popcll(m & ((1ull << lane) - 1))] = i;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int sum = 0;
+      for (int k = 0; k < 16; ++k) sum += wsum[k];
+      base += sum;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *count = base;
 }
 
-hipError_t launch_astar(const int* indptr, const int* indices, const float* cost, const float* lat,
-                        const float* lon, const int* src, const int* dst, void* state,
-                        void* heap, int* touched, float* out_cost, int* out_len, int* out_status,
-                        int* out_path, int N, int Q, int q0, int slots, int cap, int max_path,
-                        int max_iters, float inv_vmax, const float* lm, int K,
-                        hipStream_t stream, int* out_iters) {
-  const int n = min(slots, Q - q0);
+static AstarArgs make_args(const AstarGraphDev& g, const int* src, const int* dst, int Q, int q0,
+                           const AstarWs& ws, const AstarOut& o, int max_iters) {
+  return AstarArgs{g.indptr, g.indices, g.cost, g.lat, g.lon, src, dst, (AEnt*)ws.tab,
+                   (unsigned long long*)ws.heap, ws.touched, o.cost, o.len, o.status, o.path,
+                   g.N, Q, q0, ws.slots, ws.cap, ws.tbits, o.max_path, max_iters, g.inv_vmax, g.lm, g.K,
+                   o.iters};
+}
+
+bool astar_ws_ok(const AstarWs& ws, bool wave) {
+  return ws.tab != nullptr && ws.heap != nullptr && ws.touched != nullptr && ws.slots > 0 && ws.tbits >= 6 &&
+         ws.tbits <= 30 && ws.cap >= (wave ? 128 : 64) && ws.cap % 8 == 0;
+}
+
+hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* dst, int Q, int q0,
+                             const AstarWs& ws, const AstarOut& o, int max_iters, hipStream_t stream) {
+  const int n = min(ws.slots, Q - q0);
   if (n <= 0) return hipSuccess;
-  if (lm != nullptr && K != 32 && K != 16 && K != 8) return hipErrorInvalidValue;
-  AstarArgs a{indptr, indices, cost, lat, lon, src, dst, (unsigned long long*)state,
-              (unsigned long long*)heap, touched, out_cost, out_len, out_status, out_path,
-              N, Q, q0, slots, cap, max_path, max_iters, inv_vmax, lm, K, out_iters};
+  if (g.lm != nullptr && g.K != 32 && g.K != 16 && g.K != 8) return hipErrorInvalidValue;
+  if (!astar_ws_ok(ws, false)) return hipErrorInvalidValue;
+  const AstarArgs a = make_args(g, src, dst, Q, q0, ws, o, max_iters);
   // one wavefront per workgroup (a wave runs as long as its longest search); grid rounded to a
   // multiple of 8 for the XCD-aware remap in the kernel (surplus lanes exit at the slot check)
   const dim3 grid(((n + 63) / 64 + 7) / 8 * 8), block(64);
@@ -556,24 +666,99 @@ hipError_t launch_astar(const int* indptr, const int* indices, const float* cost
     const int d = v != nullptr ? std::atoi(v) : 8;
     return (d == 2 || d == 4) ? d : 8;
   }();
-  if (a.cap < 64) return hipErrorInvalidValue;
-  if (arity == 2) {
-    if (lm == nullptr) hipLaunchKernelGGL((astar_kernel<0, 2>), grid, block, 0, stream, a);
-    else if (K == 8) hipLaunchKernelGGL((astar_kernel<8, 2>), grid, block, 0, stream, a);
-    else if (K == 16) hipLaunchKernelGGL((astar_kernel<16, 2>), grid, block, 0, stream, a);
-    else hipLaunchKernelGGL((astar_kernel<32, 2>), grid, block, 0, stream, a);
-  } else if (arity == 8) {
-    if (lm == nullptr) hipLaunchKernelGGL((astar_kernel<0, 8>), grid, block, 0, stream, a);
-    else if (K == 8) hipLaunchKernelGGL((astar_kernel<8, 8>), grid, block, 0, stream, a);
-    else if (K == 16) hipLaunchKernelGGL((astar_kernel<16, 8>), grid, block, 0, stream, a);
-    else hipLaunchKernelGGL((astar_kernel<32, 8>), grid, block, 0, stream, a);
-  } else {
-    if (lm == nullptr) hipLaunchKernelGGL((astar_kernel<0, 4>), grid, block, 0, stream, a);
-    else if (K == 8) hipLaunchKernelGGL((astar_kernel<8, 4>), grid, block, 0, stream, a);
-    else if (K == 16) hipLaunchKernelGGL((astar_kernel<16, 4>), grid, block, 0, stream, a);
-    else hipLaunchKernelGGL((astar_kernel<32, 4>), grid, block, 0, stream, a);
-  }
+#define RT_ASTAR_LANE(D)                                                                          \
+  do {                                                                                            \
+    if (g.lm == nullptr) hipLaunchKernelGGL((astar_kernel<0, D>), grid, block, 0, stream, a);     \
+    else if (g.K == 8) hipLaunchKernelGGL((astar_kernel<8, D>), grid, block, 0, stream, a);       \
+    else if (g.K == 16) hipLaunchKernelGGL((astar_kernel<16, D>), grid, block, 0, stream, a);     \
+    else hipLaunchKernelGGL((astar_kernel<32, D>), grid, block, 0, stream, a);                    \
+  } while (0)
+  if (arity == 2) RT_ASTAR_LANE(2);
+  else if (arity == 4) RT_ASTAR_LANE(4);
+  else RT_ASTAR_LANE(8);
+#undef RT_ASTAR_LANE
   return hipGetLastError();
+}
+
+hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* dst, int Q, const int* qidx,
+                             int q0, int T, const AstarWs& ws, const AstarOut& o, int max_iters, float delta,
+                             hipStream_t stream) {
+  const int n = T < ws.slots ? T : ws.slots;
+  if (n <= 0) return hipSuccess;
+  if (g.lm != nullptr && g.K != 32 && g.K != 16 && g.K != 8) return hipErrorInvalidValue;
+  if (!astar_ws_ok(ws, true)) return hipErrorInvalidValue;
+  if (qidx == nullptr && q0 + n > Q) return hipErrorInvalidValue;
+  const AstarArgs a = make_args(g, src, dst, Q, q0, ws, o, max_iters);
+  if (g.lm == nullptr) hipLaunchKernelGGL(astar_wave_kernel<0>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta);
+  else if (g.K == 8) hipLaunchKernelGGL(astar_wave_kernel<8>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta);
+  else if (g.K == 16) hipLaunchKernelGGL(astar_wave_kernel<16>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta);
+  else hipLaunchKernelGGL(astar_wave_kernel<32>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta);
+  return hipGetLastError();
+}
+
+static double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// select (1 << status) & want into scratch[0..Q), count -> scratch[Q]; returns the count on the host
+static hipError_t select_count(const int* status, int Q, int want, int* scratch, hipStream_t stream, int& count) {
+  hipLaunchKernelGGL(astar_select_kernel, dim3(1), dim3(1024), 0, stream, status, Q, want, scratch, scratch + Q);
+  hipError_t e = hipGetLastError();
+  int h = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&h, scratch + Q, sizeof(int), hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  count = h;
+  return e;
+}
+
+hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, int Q, const AstarWs* lane,
+                        const AstarWs* wave, const AstarWs* big, const AstarOut& o, const AstarPlan& pl,
+                        int* scratch, hipStream_t stream, AstarRunStats* st) {
+  AstarRunStats z{};
+  AstarRunStats& S = st != nullptr ? *st : z;
+  S = AstarRunStats{};
+  if (Q <= 0) return hipSuccess;
+  auto t0 = std::chrono::steady_clock::now();
+  hipError_t e = hipSuccess;
+  const bool use_wave = wave != nullptr && pl.lane_pops > 0;
+  const bool use_lane = lane != nullptr && (!use_wave || Q >= pl.wave_only_below);
+  if (!use_lane && !use_wave) return hipErrorInvalidValue;
+  const int* qidx = nullptr;
+  int T = 0;
+  if (use_lane) {
+    const int iters = use_wave ? std::min(pl.max_iters, pl.lane_pops) : pl.max_iters;
+    for (int q0 = 0; q0 < Q && e == hipSuccess; q0 += lane->slots)
+      e = launch_astar_lane(g, src, dst, Q, q0, *lane, o, iters, stream);
+    S.lane = Q;
+    if (e == hipSuccess && use_wave) {
+      // pop budget spent (3) or the small table/heap overflowed (2): continue in the wave tier
+      e = select_count(o.status, Q, (1 << 2) | (1 << 3), scratch, stream, T);
+      qidx = scratch;
+    }
+    S.lane_ms = ms_since(t0);
+  } else {
+    T = Q;                                          // every query, identity order
+  }
+  t0 = std::chrono::steady_clock::now();
+  if (use_wave) {
+    S.wave = T;
+    for (int i0 = 0; i0 < T && e == hipSuccess; i0 += wave->slots)
+      e = launch_astar_wave(g, src, dst, Q, qidx != nullptr ? qidx + i0 : nullptr, i0, std::min(wave->slots, T - i0),
+                            *wave, o, pl.max_iters, pl.delta, stream);
+  }
+  if (e == hipSuccess && big != nullptr) {
+    int E = 0;
+    e = select_count(o.status, Q, 1 << 2, scratch, stream, E);
+    S.wave_ms = ms_since(t0);
+    t0 = std::chrono::steady_clock::now();
+    S.escalated = E;
+    for (int i0 = 0; i0 < E && e == hipSuccess; i0 += big->slots)
+      e = launch_astar_wave(g, src, dst, Q, scratch + i0, 0, std::min(big->slots, E - i0), *big, o, pl.max_iters,
+                            pl.delta, stream);
+    if (E > 0 && e == hipSuccess) e = hipStreamSynchronize(stream);
+    S.big_ms = ms_since(t0);
+  }
+  return e;
 }
 
 }  // namespace rt

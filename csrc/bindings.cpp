@@ -690,74 +690,103 @@ torch::Tensor route_score(torch::Tensor rptr, torch::Tensor nodes, torch::Tensor
   return score;
 }
 
-// Runs queries [q0, q0 + slots) of (src, dst); workspace g/parent [S,N], heap [S,cap] (int64),
-// touched [S,cap] must be initialised to (inf, 0x7fffffff) once; the kernel restores them.
-void astar(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torch::Tensor lat,
-           torch::Tensor lon, torch::Tensor src, torch::Tensor dst, torch::Tensor g,
-           torch::Tensor heap, torch::Tensor touched, torch::Tensor out_cost,
-           torch::Tensor out_len, torch::Tensor out_status, torch::Tensor out_path, int64_t q0,
-           int64_t max_iters, double inv_vmax, c10::optional<torch::Tensor> landmarks,
-           c10::optional<torch::Tensor> out_iters, c10::optional<torch::Tensor> qidx, double delta,
-           c10::optional<torch::Tensor> hcache) {
-  for (auto* t : {&indptr, &indices, &cost, &lat, &lon, &src, &dst, &g, &heap, &touched,
-                  &out_cost, &out_len, &out_status, &out_path})
+// One tier's workspace from (tab int64 [S, 2 << (tbits-1) ... i.e. 2 * TS], heap int64 [S, cap],
+// touched int32 [S, TS / 2]) — routing/graph.py AstarTier.  None -> tier off.
+static bool ws_from(const py::object& o, rt::AstarWs& ws, const torch::Device& dev) {
+  if (o.is_none()) return false;
+  auto t = o.cast<std::tuple<torch::Tensor, torch::Tensor, torch::Tensor>>();
+  torch::Tensor tab = std::get<0>(t), heap = std::get<1>(t), touched = std::get<2>(t);
+  for (auto* x : {&tab, &heap, &touched}) check_dev(*x, "astar workspace");
+  TORCH_CHECK(tab.device() == dev && heap.device() == dev && touched.device() == dev, "workspace on another GPU");
+  TORCH_CHECK(tab.scalar_type() == torch::kInt64 && tab.dim() == 2 && heap.scalar_type() == torch::kInt64 &&
+                  heap.dim() == 2 && touched.scalar_type() == torch::kInt32 && touched.dim() == 2,
+              "workspace dtypes: tab int64 [S, 2*TS], heap int64 [S, cap], touched int32 [S, TS/2]");
+  const int64_t TS = tab.size(1) / 2;
+  TORCH_CHECK(TS >= 64 && (TS & (TS - 1)) == 0 && tab.size(1) == 2 * TS, "table size must be a power of two");
+  TORCH_CHECK(heap.size(0) == tab.size(0) && touched.size(0) == tab.size(0) && touched.size(1) == TS / 2,
+              "workspace rows");
+  ws.tab = tab.data_ptr();
+  ws.heap = heap.data_ptr();
+  ws.touched = touched.data_ptr<int>();
+  ws.slots = (int)tab.size(0);
+  ws.cap = (int)heap.size(1);
+  int tb = 0;
+  while ((int64_t(1) << tb) < TS) ++tb;
+  ws.tbits = tb;
+  return true;
+}
+
+// The tiered batched A* (csrc/astar.hip astar_search).  Returns [lane queries, wave queries,
+// escalated queries, lane ms, wave ms, big ms].
+std::vector<double> astar_search(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torch::Tensor lat,
+                                 torch::Tensor lon, double inv_vmax, c10::optional<torch::Tensor> landmarks,
+                                 torch::Tensor src, torch::Tensor dst, py::object lane, py::object wave,
+                                 py::object big, torch::Tensor out_cost, torch::Tensor out_len,
+                                 torch::Tensor out_status, torch::Tensor out_path,
+                                 c10::optional<torch::Tensor> out_iters, torch::Tensor scratch, int64_t max_iters,
+                                 int64_t lane_pops, int64_t wave_only_below, double delta) {
+  for (auto* t : {&indptr, &indices, &cost, &lat, &lon, &src, &dst, &out_cost, &out_len, &out_status, &out_path,
+                  &scratch})
     check_dev(*t, "astar tensor");
   const int64_t N = lat.numel();
-  TORCH_CHECK(indptr.numel() == N + 1 && cost.numel() == indices.numel(), "graph shapes");
-  TORCH_CHECK(g.scalar_type() == torch::kInt64 && g.dim() == 2 && g.size(1) == N,
-              "state must be int64 [S,N] (packed g | parent)");
-  TORCH_CHECK(heap.scalar_type() == torch::kInt64 && heap.dim() == 2 && heap.size(0) == g.size(0),
-              "heap must be int64 [S,cap]");
-  TORCH_CHECK(touched.sizes() == heap.sizes(), "touched must be [S,cap]");
+  TORCH_CHECK(indptr.numel() == N + 1 && cost.numel() == indices.numel() && lon.numel() == N, "graph shapes");
+  TORCH_CHECK(indptr.scalar_type() == torch::kInt32 && indices.scalar_type() == torch::kInt32 &&
+                  cost.scalar_type() == torch::kFloat32 && lat.scalar_type() == torch::kFloat32 &&
+                  lon.scalar_type() == torch::kFloat32 && src.scalar_type() == torch::kInt32 &&
+                  dst.scalar_type() == torch::kInt32,
+              "graph dtypes");
   const int64_t Q = src.numel();
-  TORCH_CHECK(dst.numel() == Q && out_cost.numel() == Q && out_len.numel() == Q &&
-              out_status.numel() == Q && out_path.dim() == 2 && out_path.size(0) == Q, "outputs [Q]");
-  TORCH_CHECK(0 <= q0 && q0 <= Q, "q0");
-  const float* lm = nullptr;
-  int K = 0;
-  if (landmarks.has_value()) {
+  TORCH_CHECK(dst.numel() == Q && out_cost.numel() == Q && out_len.numel() == Q && out_status.numel() == Q &&
+                  out_path.dim() == 2 && out_path.size(0) == Q && out_status.scalar_type() == torch::kInt32 &&
+                  out_len.scalar_type() == torch::kInt32 && out_path.scalar_type() == torch::kInt32 &&
+                  out_cost.scalar_type() == torch::kFloat32,
+              "outputs [Q]");
+  TORCH_CHECK(scratch.scalar_type() == torch::kInt32 && scratch.numel() >= Q + 1, "scratch int32 [Q + 1]");
+  rt::AstarGraphDev g;
+  g.indptr = indptr.data_ptr<int>();
+  g.indices = indices.data_ptr<int>();
+  g.cost = cost.data_ptr<float>();
+  g.lat = lat.data_ptr<float>();
+  g.lon = lon.data_ptr<float>();
+  g.N = (int)N;
+  g.inv_vmax = (float)inv_vmax;
+  if (landmarks.has_value() && landmarks->defined()) {
     check_dev(*landmarks, "landmarks");
-    TORCH_CHECK(landmarks->scalar_type() == torch::kFloat32 && landmarks->dim() == 2 &&
-                landmarks->size(0) == N && landmarks->size(1) % 4 == 0 && landmarks->size(1) <= 64,
+    TORCH_CHECK(landmarks->scalar_type() == torch::kFloat32 && landmarks->dim() == 2 && landmarks->size(0) == N &&
+                    (landmarks->size(1) == 16 || landmarks->size(1) == 32 || landmarks->size(1) == 64),
                 "landmarks must be f32 [N, 2K] with K in {8, 16, 32}");
-    lm = landmarks->data_ptr<float>();
-    K = (int)landmarks->size(1) / 2;
+    g.lm = landmarks->data_ptr<float>();
+    g.K = (int)landmarks->size(1) / 2;
   }
-  int* iters = nullptr;
+  rt::AstarOut o;
+  o.cost = out_cost.data_ptr<float>();
+  o.len = out_len.data_ptr<int>();
+  o.status = out_status.data_ptr<int>();
+  o.path = out_path.data_ptr<int>();
+  o.max_path = (int)out_path.size(1);
   if (out_iters.has_value() && out_iters->defined()) {
     check_dev(*out_iters, "out_iters");
     TORCH_CHECK(out_iters->scalar_type() == torch::kInt32 && out_iters->numel() == Q, "out_iters int32 [Q]");
-    iters = out_iters->data_ptr<int>();
+    o.iters = out_iters->data_ptr<int>();
   }
-  const c10::DeviceGuard guard(g.device());
-  if (qidx.has_value() && qidx->defined()) {
-    // tail stage: one wave per listed query (slot = position in qidx, < S)
-    check_dev(*qidx, "qidx");
-    TORCH_CHECK(qidx->scalar_type() == torch::kInt32 && qidx->numel() <= g.size(0), "qidx int32 [T <= S]");
-    TORCH_CHECK(heap.size(1) >= 128, "heap row too small for the wave stage");
-    TORCH_CHECK(hcache.has_value() && hcache->defined(), "wave stage needs the heuristic cache");
-    check_dev(*hcache, "hcache");
-    TORCH_CHECK(hcache->scalar_type() == torch::kFloat32 && hcache->dim() == 2 && hcache->size(1) == N &&
-                qidx->numel() <= hcache->size(0), "hcache f32 [>= T, N]");
-    RT_CHECK_HIP(rt::launch_astar_wave(indptr.data_ptr<int>(), indices.data_ptr<int>(), cost.data_ptr<float>(),
-                                       lat.data_ptr<float>(), lon.data_ptr<float>(), src.data_ptr<int>(),
-                                       dst.data_ptr<int>(), g.data_ptr(), heap.data_ptr(), touched.data_ptr<int>(),
-                                       out_cost.data_ptr<float>(), out_len.data_ptr<int>(),
-                                       out_status.data_ptr<int>(), out_path.data_ptr<int>(), (int)N, (int)Q,
-                                       (int)g.size(0), (int)heap.size(1), (int)out_path.size(1), (int)max_iters,
-                                       (float)inv_vmax, lm, K, qidx->data_ptr<int>(), (int)qidx->numel(),
-                                       (float)delta, hcache->data_ptr<float>(), (int)hcache->size(0),
-                                       cur_stream(g), iters));
-    return;
-  }
-  RT_CHECK_HIP(rt::launch_astar(indptr.data_ptr<int>(), indices.data_ptr<int>(), cost.data_ptr<float>(),
-                                lat.data_ptr<float>(), lon.data_ptr<float>(), src.data_ptr<int>(),
-                                dst.data_ptr<int>(), g.data_ptr(),
-                                heap.data_ptr(), touched.data_ptr<int>(), out_cost.data_ptr<float>(),
-                                out_len.data_ptr<int>(), out_status.data_ptr<int>(),
-                                out_path.data_ptr<int>(), (int)N, (int)Q, (int)q0, (int)g.size(0),
-                                (int)heap.size(1), (int)out_path.size(1), (int)max_iters,
-                                (float)inv_vmax, lm, K, cur_stream(g), iters));
+  rt::AstarWs wl, ww, wb;
+  const bool hl = ws_from(lane, wl, lat.device()), hw = ws_from(wave, ww, lat.device()),
+             hb = ws_from(big, wb, lat.device());
+  TORCH_CHECK(hl || hw, "need a lane or a wave tier");
+  TORCH_CHECK((!hl || rt::astar_ws_ok(wl, false)) && (!hw || rt::astar_ws_ok(ww, true)) &&
+                  (!hb || rt::astar_ws_ok(wb, true)),
+              "A* workspace too small (wave tiers need cap >= 128, cap % 8 == 0)");
+  rt::AstarPlan pl;
+  pl.max_iters = (int)max_iters;
+  pl.lane_pops = (int)lane_pops;
+  pl.wave_only_below = (int)wave_only_below;
+  pl.delta = (float)delta;
+  rt::AstarRunStats st;
+  const c10::DeviceGuard guard(lat.device());
+  RT_CHECK_HIP(rt::astar_search(g, src.data_ptr<int>(), dst.data_ptr<int>(), (int)Q, hl ? &wl : nullptr,
+                                hw ? &ww : nullptr, hb ? &wb : nullptr, o, pl, scratch.data_ptr<int>(),
+                                cur_stream(lat), &st));
+  return {(double)st.lane, (double)st.wave, (double)st.escalated, st.lane_ms, st.wave_ms, st.big_ms};
 }
 
 torch::Tensor forest_predict(torch::Tensor records, torch::Tensor values, torch::Tensor info,
@@ -901,27 +930,27 @@ static rt::RouteServiceCfg route_cfg_from(const py::dict& d, int device, const v
     c.lat32 = (const float*)tptr("lat32", true);
     c.lon32 = (const float*)tptr("lon32", true);
     c.lm = (const float*)tptr("lm", true);
-    c.state = tptr("state", true);
-    c.heap = tptr("heap", true);
-    c.touched = (int*)tptr("touched", true);
-    c.hcache = (float*)tptr("hcache", true);
+    const torch::Device dev(torch::kCUDA, device);
+    ws_from(d.contains("lane_ws") ? py::object(d["lane_ws"]) : py::object(py::none()), c.lane_ws, dev);
+    ws_from(d.contains("wave_ws") ? py::object(d["wave_ws"]) : py::object(py::none()), c.wave_ws, dev);
+    ws_from(d.contains("big_ws") ? py::object(d["big_ws"]) : py::object(py::none()), c.big_ws, dev);
     c.N = d["N"].cast<int>();
     c.K = has("K") ? d["K"].cast<int>() : 0;
     c.snap_c = d["snap_c"].cast<double>();
-    c.slots = d["slots"].cast<int>();
-    c.cap = d["cap"].cast<int>();
     c.max_path = d["max_path"].cast<int>();
     c.max_iters = d["max_iters"].cast<int>();
     c.lane_pops = d["lane_pops"].cast<int>();
     if (has("wave_only_below")) c.wave_only_below = d["wave_only_below"].cast<int>();
-    c.wave_slots = d["wave_slots"].cast<int>();
     c.inv_vmax = d["inv_vmax"].cast<float>();
     c.wave_delta = d["wave_delta"].cast<float>();
-    TORCH_CHECK(c.glat && c.glon && c.indptr && c.indices && c.cost && c.lat32 && c.lon32 && c.state && c.heap &&
-                    c.touched && c.N > 0 && c.slots > 0 && c.cap >= 128 && c.max_path > 0,
+    TORCH_CHECK(c.glat && c.glon && c.indptr && c.indices && c.cost && c.lat32 && c.lon32 &&
+                    (c.lane_ws.slots > 0 || c.wave_ws.slots > 0) && c.N > 0 && c.max_path > 0,
                 "graph route config incomplete");
     TORCH_CHECK(c.lm == nullptr || c.K == 8 || c.K == 16 || c.K == 32, "landmarks K must be 8, 16 or 32");
-    TORCH_CHECK(c.hcache == nullptr || c.wave_slots > 0, "wave stage needs wave_slots");
+    TORCH_CHECK((c.lane_ws.slots == 0 || rt::astar_ws_ok(c.lane_ws, false)) &&
+                    (c.wave_ws.slots == 0 || rt::astar_ws_ok(c.wave_ws, true)) &&
+                    (c.big_ws.slots == 0 || rt::astar_ws_ok(c.big_ws, true)),
+                "A* workspace too small");
   }
   c.eta_blob = eta_blob;
   c.H = H;
@@ -1122,12 +1151,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gcn_l1_fused", &gcn_l1_fused, "K8: fused aggregation + W1 GEMM + ReLU + W2 transform (H1 stays in LDS)");
   m.def("gcn_spmm_score", &gcn_spmm_score, "K8: layer-2 aggregation + delay head");
   m.def("route_score", &route_score, "K8: per-route delay-weighted length");
-  m.def("astar", &astar, "K9: batched A* (one lane per query) with learned edge costs",
-        py::arg("indptr"), py::arg("indices"), py::arg("cost"), py::arg("lat"), py::arg("lon"), py::arg("src"),
-        py::arg("dst"), py::arg("state"), py::arg("heap"), py::arg("touched"), py::arg("out_cost"),
-        py::arg("out_len"), py::arg("out_status"), py::arg("out_path"), py::arg("q0"), py::arg("max_iters"),
-        py::arg("inv_vmax"), py::arg("landmarks") = py::none(), py::arg("out_iters") = py::none(),
-        py::arg("qidx") = py::none(), py::arg("delta") = 60.0, py::arg("hcache") = py::none());
+  m.def("astar_search", &astar_search, "K9: tiered batched A* (lane -> wave -> big tier) with learned edge costs",
+        py::arg("indptr"), py::arg("indices"), py::arg("cost"), py::arg("lat"), py::arg("lon"), py::arg("inv_vmax"),
+        py::arg("landmarks"), py::arg("src"), py::arg("dst"), py::arg("lane"), py::arg("wave"), py::arg("big"),
+        py::arg("out_cost"), py::arg("out_len"), py::arg("out_status"), py::arg("out_path"), py::arg("out_iters"),
+        py::arg("scratch"), py::arg("max_iters"), py::arg("lane_pops"), py::arg("wave_only_below"),
+        py::arg("delta"));
   m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
   m.def("forest_predict_lds", &forest_predict_lds, "K4: LDS-staged tree chunks, 2 walks per thread");
   m.def("pscore_create", &pscore_create, "resident single-request scorer kernel on the blob's GPU");

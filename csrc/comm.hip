@@ -260,9 +260,24 @@ int comm_open_peers(int64_t h, const std::vector<std::string>& handles, std::str
     std::memcpy(&hb, handles[r].data(), sizeof hb);
     std::memcpy(&hs, handles[r].data() + sizeof hb, sizeof hs);
     hipError_t e1 = hipIpcOpenMemHandle((void**)&c->peer_buf[r], hb, hipIpcMemLazyEnablePeerAccess);
-    hipError_t e2 = hipIpcOpenMemHandle((void**)&c->peer_sig[r], hs, hipIpcMemLazyEnablePeerAccess);
+    hipError_t e2 = e1 == hipSuccess
+                        ? hipIpcOpenMemHandle((void**)&c->peer_sig[r], hs, hipIpcMemLazyEnablePeerAccess)
+                        : hipSuccess;
     if (e1 != hipSuccess || e2 != hipSuccess) {
       errmsg = std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e1 != hipSuccess ? e1 : e2);
+      // undo what this call mapped, and clear the thread's sticky last-error so the caller's next
+      // HIP call (the agreed fallback path) does not report this failure as its own
+      if (e1 == hipSuccess) (void)hipIpcCloseMemHandle(c->peer_buf[r]);
+      c->peer_buf[r] = nullptr;
+      c->peer_sig[r] = nullptr;
+      for (int q = 0; q < r; ++q) {
+        if (q == c->rank) continue;
+        if (c->peer_buf[q]) (void)hipIpcCloseMemHandle(c->peer_buf[q]);
+        if (c->peer_sig[q]) (void)hipIpcCloseMemHandle(c->peer_sig[q]);
+        c->peer_buf[q] = nullptr;
+        c->peer_sig[q] = nullptr;
+      }
+      (void)hipGetLastError();
       return -1;
     }
   }

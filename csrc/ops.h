@@ -104,18 +104,55 @@ hipError_t launch_gcn_train_bwd(const void* X, const void* Z, const int* indptr,
                                 float* grad, float* loss, int num_cus, hipStream_t stream);
 
 // ---- batched A* (K9) : astar.hip ----
-hipError_t launch_astar(const int* indptr, const int* indices, const float* cost, const float* lat,
-                        const float* lon, const int* src, const int* dst, void* state,
-                        void* heap, int* touched, float* out_cost, int* out_len, int* out_status,
-                        int* out_path, int N, int Q, int q0, int slots, int cap, int max_path,
-                        int max_iters, float inv_vmax, const float* lm, int K, hipStream_t stream,
-                        int* out_iters = nullptr);
-hipError_t launch_astar_wave(const int* indptr, const int* indices, const float* cost, const float* lat,
-                             const float* lon, const int* src, const int* dst, void* state, void* heap,
-                             int* touched, float* out_cost, int* out_len, int* out_status, int* out_path,
-                             int N, int Q, int slots, int cap, int max_path, int max_iters, float inv_vmax,
-                             const float* lm, int K, const int* qidx, int T, float delta, float* hcache,
-                             int hrows, hipStream_t stream, int* out_iters);
+// Device graph (CSR + coordinates + ALT tables) as the kernels read it.
+struct AstarGraphDev {
+  const int* indptr = nullptr;
+  const int* indices = nullptr;
+  const float* cost = nullptr;
+  const float* lat = nullptr;
+  const float* lon = nullptr;
+  int N = 0;
+  float inv_vmax = 0.f;
+  const float* lm = nullptr;   // [N][2K] or nullptr
+  int K = 0;
+};
+// One tier's workspace: `slots` searches, each with a hash table of 1 << tbits 16-byte entries
+// (all-ones when idle), a heap row of `cap` u64 and a reset list of (1 << tbits) / 2 ints.
+struct AstarWs {
+  void* tab = nullptr;
+  void* heap = nullptr;
+  int* touched = nullptr;
+  int slots = 0, cap = 0, tbits = 0;
+};
+struct AstarOut {
+  float* cost = nullptr;
+  int* len = nullptr;
+  int* status = nullptr;    // 0 found, 1 unreachable, 2 overflow, 3 max_iters, 4 path > max_path
+  int* path = nullptr;      // [Q][max_path]
+  int max_path = 0;
+  int* iters = nullptr;     // [Q] or nullptr
+};
+struct AstarPlan {
+  int max_iters = 2000000;
+  int lane_pops = 500;          // <= 0: lane tier only, run to max_iters
+  int wave_only_below = 32768;  // fewer queries than this: skip the lane tier
+  float delta = 10.f;           // wave tier f-band width (seconds)
+};
+struct AstarRunStats {
+  int lane = 0, wave = 0, escalated = 0;
+  double lane_ms = 0, wave_ms = 0, big_ms = 0;
+};
+bool astar_ws_ok(const AstarWs& ws, bool wave);
+hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* dst, int Q, int q0,
+                             const AstarWs& ws, const AstarOut& o, int max_iters, hipStream_t stream);
+hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* dst, int Q, const int* qidx,
+                             int q0, int T, const AstarWs& ws, const AstarOut& o, int max_iters, float delta,
+                             hipStream_t stream);
+// The tiered search (lane -> wave -> big); any tier pointer may be null.  scratch: Q + 1 device ints.
+// Searches left with status 2/3 are the caller's (host Dijkstra).
+hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, int Q, const AstarWs* lane,
+                        const AstarWs* wave, const AstarWs* big, const AstarOut& o, const AstarPlan& pl,
+                        int* scratch, hipStream_t stream, AstarRunStats* st);
 
 // ---- tree ensemble (K4) : forest.hip ----
 hipError_t launch_forest(const void* rec, const float* values, const unsigned* info, const int* roots,

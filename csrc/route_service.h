@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "common.h"
+#include "ops.h"
 #include "runtime/route_core.h"
 
 #include <mutex>
@@ -39,12 +40,9 @@ struct RouteServiceCfg {
   const float* lon32 = nullptr;
   const float* lm = nullptr;
   int K = 0;
-  void* state = nullptr;
-  void* heap = nullptr;
-  int* touched = nullptr;
-  float* hcache = nullptr;
-  int slots = 0, cap = 0, max_path = 4096, max_iters = 2000000, lane_pops = 500, wave_slots = 0;
-  int wave_only_below = 32768;            // fewer unique legs than this: every search in the wave stage
+  AstarWs lane_ws, wave_ws, big_ws;       // the tiers' workspaces (csrc/astar.hip); slots == 0: off
+  int max_path = 4096, max_iters = 2000000, lane_pops = 500;
+  int wave_only_below = 32768;            // fewer unique legs than this: every search in the wave tier
   float inv_vmax = 0.f, wave_delta = 10.f;
   // ETA model for use_ml_eta (the fused K1+K2 kernel's 32x32 weight blob on this device)
   const void* eta_blob = nullptr;

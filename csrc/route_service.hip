@@ -187,7 +187,8 @@ struct RouteService::Impl {
   std::deque<Batch*> aq;
   bool gpu_done = false;
   // statistics
-  std::atomic<long long> n_jobs{0}, n_flushes{0}, n_fallback{0}, n_legs{0}, n_host_legs{0}, n_persisted{0};
+  std::atomic<long long> n_jobs{0}, n_flushes{0}, n_fallback{0}, n_legs{0}, n_host_legs{0}, n_persisted{0},
+      n_escalated{0};
   // stage times (us): parse, trips (K5+K6), snap, A*, copy-out, assembly, ETA, persistence
   std::atomic<long long> t_stage[8] = {};
   void add_t(int k, double t0) { t_stage[k].fetch_add((long long)(now_us() - t0), std::memory_order_relaxed); }
@@ -498,7 +499,7 @@ struct RouteService::Impl {
     const int MP = cfg.max_path;
     if (h_src.need(Q) || h_dst.need(Q) || h_len.need(Q) || h_st.need(Q) || h_cost.need(Q) || h_off.need(Q) ||
         h_qidx.need(Q) || d_src.need(Q) || d_dst.need(Q) || d_len.need(Q) || d_st.need(Q) || d_cost.need(Q) ||
-        d_off.need(Q) || d_qidx.need(Q) || d_iters.need(Q) || d_path.need((size_t)Q * MP))
+        d_off.need(Q) || d_qidx.need(Q + 1) || d_iters.need(Q) || d_path.need((size_t)Q * MP))
       return false;
     for (int i = 0; i < Q; ++i) {
       h_src.h[i] = pairs[i].first;
@@ -506,31 +507,36 @@ struct RouteService::Impl {
     }
     hipError_t e = hipMemcpyAsync(d_src.d, h_src.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(d_dst.d, h_dst.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
-    // lane stage budget; interactive flushes (few thousand legs) go straight to the wave stage
-    // (routing/graph.py BatchedAstar.run applies the same rule)
-    int lane_iters = cfg.lane_pops > 0 ? std::min(cfg.max_iters, cfg.lane_pops) : cfg.max_iters;
-    if (cfg.lane_pops > 0 && Q < cfg.wave_only_below) lane_iters = 1;
-    for (int q0 = 0; q0 < Q && e == hipSuccess; q0 += cfg.slots)
-      e = launch_astar(cfg.indptr, cfg.indices, cfg.cost, cfg.lat32, cfg.lon32, d_src.d, d_dst.d, cfg.state, cfg.heap,
-                       cfg.touched, d_cost.d, d_len.d, d_st.d, d_path.d, cfg.N, Q, q0, cfg.slots, cfg.cap, MP,
-                       lane_iters, cfg.inv_vmax, cfg.lm, cfg.K, stream, d_iters.d);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
-    if (e != hipSuccess) return false;
-    if (lane_iters < cfg.max_iters && cfg.hcache != nullptr) {
-      int T = 0;
-      for (int i = 0; i < Q; ++i)
-        if (h_st.h[i] == 3) h_qidx.h[T++] = i;
-      if (T > 0) {
-        e = hipMemcpyAsync(d_qidx.d, h_qidx.h, (size_t)T * 4, hipMemcpyHostToDevice, stream);
-        for (int i0 = 0; i0 < T && e == hipSuccess; i0 += cfg.wave_slots)
-          e = launch_astar_wave(cfg.indptr, cfg.indices, cfg.cost, cfg.lat32, cfg.lon32, d_src.d, d_dst.d, cfg.state,
-                                cfg.heap, cfg.touched, d_cost.d, d_len.d, d_st.d, d_path.d, cfg.N, Q, cfg.slots,
-                                cfg.cap, MP, cfg.max_iters, cfg.inv_vmax, cfg.lm, cfg.K, d_qidx.d + i0,
-                                std::min(cfg.wave_slots, T - i0), cfg.wave_delta, cfg.hcache, cfg.wave_slots, stream,
-                                d_iters.d);
-      }
-    }
+    // the tiered search (csrc/astar.hip): interactive flushes (few thousand legs) skip the lane tier
+    // (routing/graph.py BatchedAstar.run calls the same function)
+    AstarGraphDev gd;
+    gd.indptr = cfg.indptr;
+    gd.indices = cfg.indices;
+    gd.cost = cfg.cost;
+    gd.lat = cfg.lat32;
+    gd.lon = cfg.lon32;
+    gd.N = cfg.N;
+    gd.inv_vmax = cfg.inv_vmax;
+    gd.lm = cfg.lm;
+    gd.K = cfg.K;
+    AstarOut ao;
+    ao.cost = d_cost.d;
+    ao.len = d_len.d;
+    ao.status = d_st.d;
+    ao.path = d_path.d;
+    ao.max_path = MP;
+    ao.iters = d_iters.d;
+    AstarPlan pl;
+    pl.max_iters = cfg.max_iters;
+    pl.lane_pops = cfg.lane_pops;
+    pl.wave_only_below = cfg.wave_only_below;
+    pl.delta = cfg.wave_delta;
+    AstarRunStats rs;
+    if (e == hipSuccess)
+      e = astar_search(gd, d_src.d, d_dst.d, Q, cfg.lane_ws.slots > 0 ? &cfg.lane_ws : nullptr,
+                       cfg.wave_ws.slots > 0 ? &cfg.wave_ws : nullptr, cfg.big_ws.slots > 0 ? &cfg.big_ws : nullptr,
+                       ao, pl, d_qidx.d, stream, &rs);
+    n_escalated.fetch_add(rs.escalated, std::memory_order_relaxed);
     if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     add_t(3, t0);
@@ -775,6 +781,7 @@ std::vector<long long> RouteService::stats() const {
   std::vector<long long> v = {p_->n_jobs.load(), p_->n_flushes.load(), p_->n_fallback.load(), p_->n_legs.load(),
                               p_->n_host_legs.load(), p_->n_persisted.load()};
   for (int k = 0; k < 8; ++k) v.push_back(p_->t_stage[k].load());
+  v.push_back(p_->n_escalated.load());     // A* searches rerun in the big tier
   return v;
 }
 

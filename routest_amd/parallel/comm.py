@@ -25,7 +25,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops._ext import native
-from ..utils.faults import maybe_fail
+from ..utils.faults import fault_step, maybe_fail
 
 ALGOS = {"rccl": 0, "oneshot": 1}
 
@@ -56,13 +56,38 @@ class DeviceComm:
             self.h = self.C.comm_create(uid, self.rank, self.world, self.device.index, self.oneshot_bytes, use_rccl)
         self.use_rccl = use_rccl
         self.oneshot = False
+        self.oneshot_error: Optional[str] = None
         if self.oneshot_bytes:
             mine = self.C.comm_ipc_handles(self.h)
             allh: List[Optional[bytes]] = [None] * self.world
             dist.all_gather_object(allh, mine, group=group)
-            with torch.cuda.device(self.device):
-                self.C.comm_open_peers(self.h, allh)
-            self.oneshot = True
+            if fault_step("ipc_open") == self.rank:
+                # test hook: hand this rank's hipIpcOpenMemHandle calls corrupted handles, so the
+                # real HIP call fails here (and only here)
+                allh = [h if r == self.rank else bytes(len(h)) for r, h in enumerate(allh)]
+            ok = True
+            try:
+                with torch.cuda.device(self.device):
+                    self.C.comm_open_peers(self.h, allh)
+            except RuntimeError as e:
+                ok, self.oneshot_error = False, str(e)[:300]
+            # one decision for every rank: one-shot only if EVERY rank mapped every peer.  A rank
+            # that enabled it while another fell back would wait forever in the epoch protocol.
+            flags: List[Optional[bool]] = [None] * self.world
+            dist.all_gather_object(flags, ok, group=group)
+            self.oneshot = all(bool(f) for f in flags)
+            if not self.oneshot and self.oneshot_error is None:
+                bad = [r for r, f in enumerate(flags) if not f]
+                self.oneshot_error = f"rank(s) {bad} could not open the peer IPC handles"
+
+    def _pg_host(self, t: torch.Tensor) -> bool:
+        """gloo groups reduce host tensors: stage device tensors through the CPU."""
+        return t.is_cuda and dist.get_backend(self.group) == "gloo"
+
+    @property
+    def fallback(self) -> str:
+        """The path used when one-shot does not apply: RCCL from C++, else the process group."""
+        return "rccl" if self.use_rccl else "pg"
 
     # ------------------------------------------------------------------ collectives
     # The auto choice between one-shot and RCCL depends ONLY on what every rank agrees on (dtype,
@@ -76,7 +101,7 @@ class DeviceComm:
         if (self.oneshot and t.dtype == torch.float32 and t.numel() % 4 == 0
                 and t.numel() * 4 <= self.oneshot_bytes):
             return "oneshot"
-        return "rccl"
+        return self.fallback
 
     def _oneshot_size_ok(self, t: torch.Tensor) -> bool:
         nb = t.numel() * t.element_size()
@@ -92,6 +117,12 @@ class DeviceComm:
             return t
         maybe_fail("rccl_timeout")
         a = self.pick(t, algo)
+        if a == "pg":                   # (host-synchronous; not graph-capturable)
+            h = t.cpu() if self._pg_host(t) else t
+            dist.all_reduce(h, group=self.group)
+            if h is not t:
+                t.copy_(h)
+            return t
         if a == "oneshot" and not self._aligned(t):
             tmp = t.contiguous().clone()
             self.C.comm_all_reduce(self.h, tmp, ALGOS[a])
@@ -113,7 +144,13 @@ class DeviceComm:
             return out
         maybe_fail("rccl_timeout")
         if algo == "auto":
-            algo = "oneshot" if self._oneshot_size_ok(inp) else "rccl"
+            algo = "oneshot" if self._oneshot_size_ok(inp) else self.fallback
+        if algo == "pg":
+            x = inp.contiguous().cpu() if self._pg_host(inp) else inp.contiguous()
+            parts = [torch.empty_like(x) for _ in range(self.world)]
+            dist.all_gather(parts, x, group=self.group)
+            out.view(-1).copy_(torch.cat([p.view(-1) for p in parts]))
+            return out
         src = inp if self._aligned(inp) else inp.contiguous().clone()
         dst = out if self._aligned(out) else torch.empty(out.shape, dtype=out.dtype, device=out.device)
         if algo == "oneshot":
@@ -126,13 +163,24 @@ class DeviceComm:
 
     def reduce_scatter(self, inp: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         assert inp.numel() == out.numel() * self.world
+        if self.world > 1 and not self.use_rccl:
+            tmp = inp.contiguous().cpu() if self._pg_host(inp) else inp.contiguous().clone()
+            dist.all_reduce(tmp, group=self.group)
+            out.view(-1).copy_(tmp.view(-1)[self.rank * out.numel():(self.rank + 1) * out.numel()])
+            return out
         self.C.comm_collective(self.h, 1, inp, out, 0)
         return out
 
     def broadcast(self, t: torch.Tensor, root: int = 0, algo: str = "auto") -> torch.Tensor:
         if self.world > 1:
             if algo == "auto":
-                algo = "oneshot" if self._oneshot_size_ok(t) else "rccl"
+                algo = "oneshot" if self._oneshot_size_ok(t) else self.fallback
+            if algo == "pg":
+                h = t.cpu() if self._pg_host(t) else t
+                dist.broadcast(h, src=root, group=self.group)     # (global rank == group rank here)
+                if h is not t:
+                    t.copy_(h)
+                return t
             buf = t if self._aligned(t) else t.contiguous().clone()
             if algo == "oneshot":
                 self.C.comm_oneshot(self.h, 2, buf, buf, root)
@@ -145,7 +193,7 @@ class DeviceComm:
     def ready(self) -> dict:
         """Readiness summary for /api/health: which paths are usable and no pending wait error."""
         return {"world": self.world, "rank": self.rank, "rccl": bool(self.use_rccl),
-                "oneshot": bool(self.oneshot), "error": bool(self.C.comm_error(self.h))
+                "oneshot": bool(self.oneshot), "oneshot_error": self.oneshot_error, "error": bool(self.C.comm_error(self.h))
                 if self.h is not None else True}
 
     def check(self) -> None:

@@ -26,14 +26,32 @@ from .graph import BatchedAstar
 
 class BulkRouteStep:
     def __init__(self, g, cost: np.ndarray, device, requests: int, seed: int = 100,
-                 max_slots: int = 98304, astar: Optional[BatchedAstar] = None):
+                 max_slots: int = 98304, astar: Optional[BatchedAstar] = None,
+                 radius_km: Optional[float] = None):
         self.C = _ext.native(required=True)
         self.dev = d = torch.device(device)
         rng = np.random.default_rng(seed)
         reqs, snapped = [], []
-        for _ in range(requests):
-            n = int(rng.integers(2, 11))
-            nodes = rng.integers(0, g.num_nodes, n + 1)
+        # radius_km: every request's depot and stops lie within that distance of a random centre
+        # (a delivery area, snapped to the nearest road nodes); None: uniform over the whole graph
+        local = None
+        if radius_km:
+            ns = rng.integers(2, 11, requests)
+            c = rng.integers(0, g.num_nodes, requests)
+            tot = int((ns + 1).sum())
+            rc = np.repeat(c, ns + 1)
+            r = radius_km * np.sqrt(rng.random(tot))
+            th = rng.random(tot) * 2 * np.pi
+            plat = g.lat[rc] + r * np.cos(th) / 111.195
+            plon = g.lon[rc] + r * np.sin(th) / (111.195 * np.cos(np.radians(g.lat[rc])))
+            local = np.split(np.asarray(g.nearest_nodes(plat, plon), dtype=np.int64), np.cumsum(ns + 1)[:-1])
+        for k in range(requests):
+            if local is not None:
+                nodes = local[k]
+                n = len(nodes) - 1
+            else:
+                n = int(rng.integers(2, 11))
+                nodes = rng.integers(0, g.num_nodes, n + 1)
             reqs.append({"source_point": {"lat": float(g.lat[nodes[0]]), "lon": float(g.lon[nodes[0]])},
                          "destination_points": [{"lat": float(g.lat[v]), "lon": float(g.lon[v]),
                                                  "payload": int(rng.integers(1, 4))} for v in nodes[1:]],
@@ -48,10 +66,12 @@ class BulkRouteStep:
             snap[k, :len(s)] = s
         self.snap = torch.from_numpy(snap).to(d)
         self.requests = requests
-        # every leg of a step in ONE launch (~80k concurrent searches on one GPU: the dense per-slot
-        # state is sized for 288 GB of HBM3E) so each CU keeps several waves of searches in flight
+        # every leg of a step in ONE lane-tier launch (~80k concurrent searches on one GPU) and the
+        # searches left after the pop budget in one or a few wave-tier launches, so each CU keeps
+        # several waves of searches in flight (sparse per-search tables: ~19 GB + 35 GB of HBM3E)
         legs_est = int(sum(len(s) for s in snapped) * 1.4) + 1024
-        self.astar = astar or BatchedAstar(g, cost, d, slots=min(legs_est, max_slots), cap=65536)
+        slots = min(legs_est, max_slots)
+        self.astar = astar or BatchedAstar(g, cost, d, slots=slots, wave_slots=min(slots, 49152))
 
     def legs(self):
         """K5 + K6 for every request, then the trip legs as (src, dst) node tensors on the device."""

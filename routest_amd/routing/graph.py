@@ -167,23 +167,57 @@ def landmark_tables(g: RoadGraph, cost: np.ndarray, k: int = 16, seed: int = 0,
     return out.reshape(g.num_nodes, 2 * k)
 
 
-class BatchedAstar:
-    """GPU batched A*; workspace sized for ``slots`` concurrent searches (dense per-slot state)."""
+def _pow2_bits(n: int) -> int:
+    return max(1, int(np.ceil(np.log2(max(2, n)))))
 
-    def __init__(self, g: RoadGraph, cost: np.ndarray, device, slots: int = 16384, cap: int = 65536,
+
+class AstarTier:
+    """One tier's workspace (csrc/astar.hip AstarWs): ``slots`` concurrent searches, each with a hash
+    table of ``2**tbits`` 16-byte entries (all-ones when idle), a heap row of ``cap`` u64 (the lane
+    heap, or the wave tier's near/near/far lists) and a reset list of ``2**(tbits-1)`` slots.  A search
+    may touch at most half its table; past that it overflows to the next tier."""
+
+    def __init__(self, slots: int, cap: int, tbits: int, device):
+        self.slots, self.cap, self.tbits = int(slots), int(cap), int(tbits)
+        ts = 1 << self.tbits
+        self.tab = torch.full((self.slots, 2 * ts), -1, dtype=torch.int64, device=device)
+        self.heap = torch.empty((self.slots, self.cap), dtype=torch.int64, device=device)
+        self.touched = torch.empty((self.slots, ts // 2), dtype=torch.int32, device=device)
+
+    def ws(self):
+        return (self.tab, self.heap, self.touched)
+
+    @property
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.ws())
+
+    @staticmethod
+    def bytes_per_slot(cap: int, tbits: int) -> int:
+        return 16 * (1 << tbits) + 8 * cap + 4 * (1 << (tbits - 1))
+
+
+class BatchedAstar:
+    """GPU batched A* (csrc/astar.hip): three tiers of sparse per-search state.
+
+    * lane tier — ``slots`` searches, one lane each, ``lane_pops`` heap pops in small tables;
+    * wave tier — ``wave_slots`` searches, one 64-lane wave each, tables of ``2 * cap`` entries
+      (a search may touch ``cap`` nodes);
+    * big tier — ``big_slots`` searches with tables of >= 2N entries for what overflowed the wave tier.
+
+    Workspace is ``slots x ~176 KB + wave_slots x 44 cap + big_slots x (16-48 MB)`` — independent of
+    the graph size up to the big tier (the round-2 kernel kept a dense [slots, N] state)."""
+
+    def __init__(self, g: RoadGraph, cost: np.ndarray, device, slots: int = 16384, cap: int = 16384,
                  max_path: int = 4096, max_iters: int = 2_000_000, landmarks: int = 32,
-                 landmark_method: str = "farthest"):
+                 landmark_method: str = "farthest", wave_slots: Optional[int] = None,
+                 big_slots: Optional[int] = None):
         from ..ops import _ext
         self.C = _ext.native(required=True)
         self.g = g
         self.dev = d = torch.device(device)
         # internal node order: Z-order (Morton) over (lat, lon), so that nodes close on the map are
-        # close in memory and a 2-D neighbourhood of a search shares cache lines of the per-slot
-        # state / CSR / coordinates (ids of synthetic graphs are row-major: the node north of v
-        # is a whole grid row away).  Queries are mapped in, paths mapped back out.
-        # Measured neutral on the 100k-node graph (80k legs: 105.1-105.6 ms reordered vs 105.2 ms;
-        # the searches are bound by dependent-load latency, not cache-line reuse), so opt-in:
-        # ROUTEST_ASTAR_REORDER=1.
+        # close in memory.  Measured neutral on the 100k-node graph with the dense state (80k legs:
+        # 105.1-105.6 ms reordered vs 105.2 ms), so opt-in: ROUTEST_ASTAR_REORDER=1.
         self.reorder = os.environ.get("ROUTEST_ASTAR_REORDER", "0") == "1"
         if self.reorder:
             self.perm, self.inv, indptr, indices, self.edge_perm = permute_csr(
@@ -198,24 +232,40 @@ class BatchedAstar:
         self.lat = torch.from_numpy(self._nodes(g.lat.astype(np.float32))).to(d)
         self.lon = torch.from_numpy(self._nodes(g.lon.astype(np.float32))).to(d)
         self.slots, self.cap, self.max_path, self.max_iters = slots, cap, max_path, max_iters
-        # two-stage search: the lane-per-query kernel gets `lane_pops` heap pops per query; the few
-        # searches still open then run one WAVE per query (f-band expansion, csrc/astar.hip
-        # astar_wave_kernel), so the launch is no longer as long as the single longest search.
-        # ROUTEST_ASTAR_LANE_POPS=0 disables the tail stage.
-        # 80k legs (bench/astar_tail.py, band 10 s): lane budget 2000 117 ms, 1000 112 ms, 500 105 ms,
-        # 250 108 ms, everything in the wave stage 101 ms (more wave work, fine for big batches);
-        # lane only 236 ms; the wave stage wants all of its queries resident at once (65k: 84 ms
-        # vs 100 ms in 16k chunks), hence up to 65536 wave slots (26 GB of heuristic cache)
+        # lane tier budget: the lane-per-query kernel gets `lane_pops` heap pops per query; the
+        # searches still open then run one WAVE per query (f-band expansion), so the launch is no
+        # longer as long as the single longest search.  ROUTEST_ASTAR_LANE_POPS=0: lane tier only.
+        # 80k legs (bench/astar_tail.py, band 10 s, dense state): budget 2000 117 ms, 1000 112 ms,
+        # 500 105 ms, 250 108 ms, everything in the wave stage 101 ms; lane only 236 ms.
         self.lane_pops = int(os.environ.get("ROUTEST_ASTAR_LANE_POPS", "500"))
         # interactive batches (a few thousand legs per flush: ~60 lane waves would leave most of the
-        # 256 CUs idle) go straight to the wave stage: one 64-lane wave per search fills the chip.
+        # 256 CUs idle) go straight to the wave tier: one 64-lane wave per search fills the chip.
         # Measured on the native route path at 1k concurrency (profiles/route_http_r3.jsonl): lane
         # budget 500 -> 19.3k req/s, 100 -> 24.1k, 1 (all wave) -> 26.2k, 2000 -> 10.3k.
         self.wave_only_below = int(os.environ.get("ROUTEST_ASTAR_WAVE_ONLY_BELOW", "32768"))
         self.wave_delta = float(os.environ.get("ROUTEST_ASTAR_DELTA", "10"))
-        self.wave_slots = min(slots, int(os.environ.get("ROUTEST_ASTAR_WAVE_SLOTS", "65536")))
-        self.hcache = None            # [wave_slots, N] f32 heuristic cache of the wave stage (NaN = empty)
+        if wave_slots is None:
+            wave_slots = int(os.environ.get("ROUTEST_ASTAR_WAVE_SLOTS", "16384"))
+        self.wave_slots = max(1, min(slots, int(wave_slots)))
         N = g.num_nodes
+        if big_slots is None:
+            big_slots = int(os.environ.get("ROUTEST_ASTAR_BIG_SLOTS", "64"))
+        # tiers: cap rounded to a multiple of 8, tables twice the touch capacity
+        cap = max(128, (int(cap) + 7) // 8 * 8)
+        wave_tbits = _pow2_bits(2 * cap)
+        if self.lane_pops > 0:
+            lane_tbits = min(wave_tbits, max(8, _pow2_bits(16 * self.lane_pops)))
+            lane_cap = max(64, 1 << (lane_tbits - 1))
+            self.lane_tier = AstarTier(slots, lane_cap, lane_tbits, d)
+            self.wave_tier = AstarTier(self.wave_slots, cap, wave_tbits, d)
+        else:
+            self.lane_tier = AstarTier(slots, cap, wave_tbits, d)
+            self.wave_tier = None
+        big_tbits = min(24, max(wave_tbits + 1, _pow2_bits(2 * N)))
+        self.big_tier = (AstarTier(big_slots, max(cap, min(1 << 20, 1 << _pow2_bits(N // 2))), big_tbits, d)
+                         if big_slots > 0 else None)
+        self.scratch = torch.empty(1, dtype=torch.int32, device=d)
+        self.last_stats = {}
         # tightest admissible + consistent heuristic: every edge length is 1.15 x its great-circle
         # length (so any path >= 1.15 x the great-circle s-t distance) and every edge is traversed
         # no faster than the fastest edge of the graph
@@ -226,10 +276,11 @@ class BatchedAstar:
         self.lm = (torch.from_numpy(self._nodes(landmark_tables(g, cost, landmarks,
                                                                 method=landmark_method))).to(d)
                    if landmarks else None)
-        # packed per-(slot, node) state: g (f32 bits) | parent << 32, initialised to (inf, none)
-        self.state = torch.full((slots, N), 0x7FFFFFFF7F800000, dtype=torch.int64, device=d)
-        self.heap = torch.empty((slots, cap), dtype=torch.int64, device=d)
-        self.touched = torch.empty((slots, cap), dtype=torch.int32, device=d)
+
+    @property
+    def workspace_bytes(self) -> int:
+        """Device bytes of the search workspace (all tiers; graph and landmark tables excluded)."""
+        return sum(t.nbytes for t in (self.lane_tier, self.wave_tier, self.big_tier) if t is not None)
 
     def _nodes(self, a: np.ndarray) -> np.ndarray:
         return np.ascontiguousarray(a[self.perm]) if self.perm is not None else a
@@ -238,7 +289,7 @@ class BatchedAstar:
         return np.ascontiguousarray(a[self.edge_perm]) if self.edge_perm is not None else a
 
     def update_costs(self, cost: np.ndarray) -> None:
-        # (the wave stage's heuristic cache is per query and reset after each search: nothing to drop)
+        # (heuristics are cached per search in its table and reset after it: nothing to drop)
         cost = np.asarray(cost, dtype=np.float32)
         self.cost.copy_(torch.from_numpy(self._edges(cost)))
         self._csr = None          # the host fallback's CSR was built from the old costs
@@ -271,25 +322,17 @@ class BatchedAstar:
         out_len = torch.empty(Q, dtype=torch.int32, device=d)
         out_status = torch.empty(Q, dtype=torch.int32, device=d)
         out_path = torch.empty((Q, self.max_path), dtype=torch.int32, device=d)
-        self.last_iters = torch.empty(Q, dtype=torch.int32, device=d)   # heap pops per query
-        lane_iters = min(self.max_iters, self.lane_pops) if self.lane_pops > 0 else self.max_iters
-        if self.lane_pops > 0 and Q < self.wave_only_below:
-            lane_iters = 1                   # (csrc/route_service.hip applies the same rule)
-        for q0 in range(0, Q, self.slots):
-            self.C.astar(self.indptr, self.indices, self.cost, self.lat, self.lon, s, t, self.state,
-                         self.heap, self.touched, out_cost, out_len, out_status, out_path,
-                         q0, lane_iters, self.inv_vmax, self.lm, self.last_iters)
-        if lane_iters < self.max_iters:
-            tail = (out_status == 3).nonzero().flatten().to(torch.int32)
-            self.last_tail = int(tail.numel())
-            if self.last_tail and self.hcache is None:
-                self.hcache = torch.full((self.wave_slots, self.g.num_nodes), float("nan"),
-                                         dtype=torch.float32, device=d)
-            for i0 in range(0, self.last_tail, self.wave_slots):
-                self.C.astar(self.indptr, self.indices, self.cost, self.lat, self.lon, s, t, self.state,
-                             self.heap, self.touched, out_cost, out_len, out_status, out_path,
-                             0, self.max_iters, self.inv_vmax, self.lm, self.last_iters,
-                             tail[i0:i0 + self.wave_slots].contiguous(), self.wave_delta, self.hcache)
+        self.last_iters = torch.empty(Q, dtype=torch.int32, device=d)   # pops / expansions per query
+        if self.scratch.numel() < Q + 1:
+            self.scratch = torch.empty(Q + 1, dtype=torch.int32, device=d)
+        st = self.C.astar_search(self.indptr, self.indices, self.cost, self.lat, self.lon, self.inv_vmax, self.lm,
+                                 s, t, self.lane_tier.ws(), self.wave_tier.ws() if self.wave_tier else None,
+                                 self.big_tier.ws() if self.big_tier else None, out_cost, out_len, out_status,
+                                 out_path, self.last_iters, self.scratch, self.max_iters, self.lane_pops,
+                                 self.wave_only_below, self.wave_delta)
+        self.last_stats = dict(zip(("lane", "wave", "escalated", "lane_ms", "wave_ms", "big_ms"), st))
+        self.last_tail = int(st[1])
+        self.last_escalated = int(st[2])
         self._exact_fallback(s, t, out_cost, out_len, out_status, out_path)
         if self.perm_t is not None:
             # back to the caller's node ids (entries past path_len are undefined: mask them to -1)
@@ -390,7 +433,7 @@ class GraphProvider(HaversineProvider):
             # one search workspace per provider: concurrent handler threads take turns
             with self._lock:
                 if self._astar is None:
-                    self._astar = BatchedAstar(self.g, self.cost, self.device, slots=1024, cap=65536)
+                    self._astar = BatchedAstar(self.g, self.cost, self.device, slots=1024)
                 return self._astar.paths([p[0] for p in pairs], [p[1] for p in pairs])
         from scipy.sparse import csr_matrix
         from scipy.sparse.csgraph import dijkstra

@@ -68,7 +68,9 @@ class NativePredictServer:
                  "route_service_fallbacks", "route_legs", "route_host_legs", "route_persisted",
                  # accumulated stage times of the route service (us)
                  "route_us_parse", "route_us_trips", "route_us_snap", "route_us_astar", "route_us_copyout",
-                 "route_us_assemble", "route_us_eta", "route_us_persist")
+                 "route_us_assemble", "route_us_eta", "route_us_persist",
+                 # A* searches that overflowed a wave-tier table and were rerun in the big tier
+                 "route_astar_escalated")
         return dict(zip(names, v))
 
     def close(self) -> None:
@@ -90,7 +92,7 @@ def route_config(provider, device, *, engine: str = "backend:mi355x", compat200:
 
     ``provider``: the app's HaversineProvider or GraphProvider.  For the road graph, ``astar`` is a
     :class:`~routest_amd.routing.graph.BatchedAstar` on ``device`` whose device tensors the service
-    searches with (the caller keeps it alive; its wave-stage heuristic cache is allocated here).
+    searches with (its three workspace tiers; the caller keeps it alive).
     ``store``: the app's store — an :class:`SQLiteStore` is written natively (same database file);
     any other store kind is not mirrored, so route requests are then relayed to the Python app
     (the caller passes no route configs)."""
@@ -104,8 +106,6 @@ def route_config(provider, device, *, engine: str = "backend:mi355x", compat200:
         a = astar
         if a is None or a.perm is not None:
             raise ValueError("graph routes need a BatchedAstar without node reordering")
-        if a.hcache is None and a.lane_pops > 0:
-            a.hcache = torch.full((a.wave_slots, a.g.num_nodes), float("nan"), dtype=torch.float32, device=a.dev)
         g = a.g
         cfg.update({
             "glat": torch.from_numpy(np.ascontiguousarray(g.lat, dtype=np.float64)),
@@ -115,11 +115,12 @@ def route_config(provider, device, *, engine: str = "backend:mi355x", compat200:
             "h_cost": a.cost.detach().cpu().contiguous(),
             "indptr": a.indptr, "indices": a.indices, "cost": a.cost, "lat32": a.lat, "lon32": a.lon,
             "lm": a.lm, "K": (a.lm.shape[1] // 2) if a.lm is not None else 0,
-            "state": a.state, "heap": a.heap, "touched": a.touched, "hcache": a.hcache,
-            "N": int(g.num_nodes), "snap_c": float(g.SNAP_C), "slots": int(a.slots), "cap": int(a.cap),
+            "lane_ws": a.lane_tier.ws(), "wave_ws": a.wave_tier.ws() if a.wave_tier else None,
+            "big_ws": a.big_tier.ws() if a.big_tier else None,
+            "N": int(g.num_nodes), "snap_c": float(g.SNAP_C),
             "max_path": int(a.max_path), "max_iters": int(a.max_iters), "lane_pops": int(a.lane_pops),
             "wave_only_below": int(a.wave_only_below),
-            "wave_slots": int(a.wave_slots), "inv_vmax": float(a.inv_vmax), "wave_delta": float(a.wave_delta),
+            "inv_vmax": float(a.inv_vmax), "wave_delta": float(a.wave_delta),
             "_astar": a})
     return cfg
 

@@ -31,7 +31,7 @@ def test_astar_optimal_costs_and_valid_paths(graph_and_cost, monkeypatch, reorde
     g, cost, _ = graph_and_cost
     src, dst = synth_route_queries(g, 2000, seed=1)
     monkeypatch.setenv("ROUTEST_ASTAR_REORDER", reorder)
-    a = BatchedAstar(g, cost, "cuda:0", slots=1024, cap=65536)
+    a = BatchedAstar(g, cost, "cuda:0", slots=1024)
     c, n, st, p = a.run(src, dst)
     c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
     ref = dijkstra_ref(g, cost, src, dst)
@@ -65,7 +65,7 @@ def test_wave_tail_stage_exact(graph_and_cost, monkeypatch, lane_pops, delta):
     src[:3] = dst[:3]                                   # s == t queries too
     monkeypatch.setenv("ROUTEST_ASTAR_LANE_POPS", str(lane_pops if lane_pops else 1))
     monkeypatch.setenv("ROUTEST_ASTAR_DELTA", str(delta))
-    a = BatchedAstar(g, cost, "cuda:0", slots=1024, cap=65536)
+    a = BatchedAstar(g, cost, "cuda:0", slots=1024)
     c, n, st, p = a.run(src, dst)
     assert a.last_tail > 300                            # most queries went through the wave stage
     c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
@@ -86,12 +86,29 @@ def test_wave_tail_stage_exact(graph_and_cost, monkeypatch, lane_pops, delta):
     assert np.array_equal(c, c2)
 
 
-def test_overflowed_searches_finish_exactly_on_host(graph_and_cost):
-    """With per-slot lists far too small (cap 128) most searches overflow on the GPU (status 2);
-    they are finished by the exact host fallback, so every leg is found at the optimal cost."""
+def test_overflowed_searches_escalate_to_the_big_tier(graph_and_cost):
+    """With wave-tier tables far too small (cap 128: a search may touch 128 nodes) most searches
+    overflow (status 2) and are rerun in the big tier, whose tables hold every node — still on the
+    GPU, at the optimal cost."""
     g, cost, _ = graph_and_cost
     src, dst = synth_route_queries(g, 300, seed=3)
     a = BatchedAstar(g, cost, "cuda:0", slots=512, cap=128)
+    c, n, st, p = a.run(src, dst)
+    assert a.last_escalated > 100 and a.last_fallbacks == 0, a.last_stats
+    c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
+    assert (st == 0).all(), np.unique(st, return_counts=True)
+    np.testing.assert_allclose(c, dijkstra_ref(g, cost, src, dst), rtol=1e-4)
+    for i in range(0, 300, 37):
+        assert p[i, 0] == src[i] and p[i, n[i] - 1] == dst[i]
+    c2 = a.run(src, dst)[0].cpu().numpy()               # every tier restored its tables
+    assert np.array_equal(c, c2)
+
+
+def test_overflowed_searches_finish_exactly_on_host(graph_and_cost):
+    """Without a big tier the overflowed searches are finished by the exact host fallback."""
+    g, cost, _ = graph_and_cost
+    src, dst = synth_route_queries(g, 300, seed=3)
+    a = BatchedAstar(g, cost, "cuda:0", slots=512, cap=128, big_slots=0)
     c, n, st, p = a.run(src, dst)
     assert a.last_fallbacks > 0
     c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
@@ -99,3 +116,30 @@ def test_overflowed_searches_finish_exactly_on_host(graph_and_cost):
     np.testing.assert_allclose(c, dijkstra_ref(g, cost, src, dst), rtol=1e-4)
     for i in range(0, 300, 37):
         assert p[i, 0] == src[i] and p[i, n[i] - 1] == dst[i]
+
+
+def test_lane_tier_overflow_continues_in_the_wave_tier(graph_and_cost, monkeypatch):
+    """Big batches run the lane tier first; its small tables overflow on long legs (status 2) and
+    those searches continue in the wave tier like the ones whose pop budget ran out."""
+    g, cost, _ = graph_and_cost
+    src, dst = synth_route_queries(g, 1500, seed=4)
+    monkeypatch.setenv("ROUTEST_ASTAR_WAVE_ONLY_BELOW", "0")       # force the lane tier
+    monkeypatch.setenv("ROUTEST_ASTAR_LANE_POPS", "2000")          # long budget, small tables overflow
+    a = BatchedAstar(g, cost, "cuda:0", slots=1024)
+    a.lane_tier = type(a.lane_tier)(1024, 64, 7, a.dev)            # 128-entry tables: overflow early
+    c, n, st, p = a.run(src, dst)
+    assert a.last_stats["lane"] == 1500 and a.last_tail > 500, a.last_stats
+    st = st.cpu().numpy()
+    assert (st == 0).all()
+    np.testing.assert_allclose(c.cpu().numpy(), dijkstra_ref(g, cost, src, dst), rtol=1e-4)
+
+
+def test_workspace_is_independent_of_graph_size(graph_and_cost):
+    """Sparse per-search state: the lane and wave tiers do not grow with N (only the big tier's
+    tables are sized from the graph)."""
+    g, cost, _ = graph_and_cost
+    a = BatchedAstar(g, cost, "cuda:0", slots=1024, big_slots=0)
+    small = synth_road_graph(5_000, seed=1)
+    b = BatchedAstar(small, edge_costs(small, default_model(hidden=64, steps=5), device="cuda:0"), "cuda:0",
+                     slots=1024, big_slots=0)
+    assert a.workspace_bytes == b.workspace_bytes

@@ -115,6 +115,37 @@ def test_oneshot_allgather_broadcast(world):
     _spawn(_gather_worker, world)
 
 
+# ----------------------------------------------------------------------------- IPC open failure
+def _ipc_fail_worker(rank, world):
+    # rank 1's hipIpcOpenMemHandle calls get corrupted handles (parallel/comm.py test hook), so the
+    # real HIP call fails on that rank only
+    os.environ["ROUTEST_FAULT"] = "ipc_open@1"
+    from routest_amd.parallel.comm import DeviceComm
+    c = DeviceComm(torch.device("cuda", 0), use_rccl=False, oneshot_bytes=1 << 20)
+    v = torch.full((1024,), float(rank + 1), device="cuda")
+    algo = c.pick(v)
+    c.all_reduce(v)                                       # the agreed fallback path
+    g = torch.empty(2 * 256, device="cuda")
+    c.all_gather(torch.full((256,), float(rank), device="cuda"), g)
+    torch.cuda.synchronize()
+    out = (c.oneshot, algo, c.oneshot_error, float(v[0]), g.cpu().tolist())
+    c.close()
+    return out
+
+
+def test_ipc_open_failure_on_one_rank_is_one_decision_for_all():
+    """hipIpcOpenMemHandle fails on rank 1 only: every rank disables the one-shot path (the same
+    decision everywhere — a rank that kept it would wait forever for its peer) and the collectives
+    run on the fallback (RCCL when the comm has it; here, both ranks on one GPU, the gloo group)."""
+    res = _spawn(_ipc_fail_worker, 2)
+    assert [r[0] for r in res] == [False, False]
+    assert [r[1] for r in res] == ["pg", "pg"]
+    assert "hipIpcOpenMemHandle" in res[1][2], res[1][2]
+    assert "rank(s) [1]" in res[0][2], res[0][2]
+    assert all(r[3] == 3.0 for r in res)
+    assert all(r[4] == [0.0] * 256 + [1.0] * 256 for r in res)
+
+
 # ----------------------------------------------------------------------------- GCN partition
 def _gcn_worker(rank, world, n):
     from routest_amd.data.graph import synth_road_graph
