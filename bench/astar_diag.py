@@ -16,7 +16,7 @@ from routest_amd.serve.eta_service import default_model  # noqa: E402
 g = synth_road_graph(100_000)
 cost = edge_costs(g, default_model(hidden=64, steps=60), "cuda:0")
 S, T = synth_route_queries(g, 80000, seed=5, min_km=1, max_km=25)
-a = BatchedAstar(g, cost, "cuda:0", slots=80000, wave_slots=49152)
+a = BatchedAstar(g, cost, "cuda:0", slots=80000, wave_slots=32768, arena_gb=16)
 for sort in (False, True, False, True):
     a.run(S[:1000], T[:1000], sort=sort)
     torch.cuda.synchronize()

@@ -33,7 +33,8 @@ def main():
     ap.add_argument("--radius-km", type=float, default=8.0)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--slots", type=int, default=65536)
-    ap.add_argument("--wave-slots", type=int, default=16384)
+    ap.add_argument("--wave-slots", type=int, default=32768)
+    ap.add_argument("--arena-gb", type=float, default=16.0)
     ap.add_argument("--check", type=int, default=12)
     args = ap.parse_args()
     d = torch.device("cuda", 0)
@@ -44,13 +45,15 @@ def main():
     torch.cuda.synchronize()
     base = torch.cuda.memory_allocated(d)
     t0 = time.time()
-    astar = BatchedAstar(g, cost, d, slots=args.slots, wave_slots=args.wave_slots)
+    astar = BatchedAstar(g, cost, d, slots=args.slots, wave_slots=args.wave_slots, arena_gb=args.arena_gb)
     print(f"A* ready in {time.time() - t0:.1f} s (landmarks included)", flush=True)
     step = BulkRouteStep(g, cost, d, args.requests, astar=astar, radius_km=args.radius_km or None)
     torch.cuda.synchronize()
     torch.cuda.reset_peak_memory_stats(d)
+    t1 = time.perf_counter()
     legs, c, st, _ = step.step()                       # warm-up
     torch.cuda.synchronize()
+    print(f"warm-up step: {legs} legs in {time.perf_counter() - t1:.2f} s, tiers {astar.last_stats}", flush=True)
     times, tiers = [], []
     for _ in range(args.steps):
         t1 = time.perf_counter()
@@ -58,6 +61,7 @@ def main():
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t1)
         tiers.append(dict(astar.last_stats, fallbacks=astar.last_fallbacks))
+        print(f"step: {times[-1] * 1e3:.1f} ms, tiers {tiers[-1]}", flush=True)
     peak = torch.cuda.max_memory_allocated(d)
     stc = np.bincount(st.cpu().numpy(), minlength=5).tolist()
     # exactness on a sample of legs (scipy Dijkstra per source)

@@ -20,7 +20,7 @@ rng = np.random.default_rng(100)
 S = rng.integers(0, g.num_nodes, 80000).astype(np.int32)
 T = rng.integers(0, g.num_nodes, 80000).astype(np.int32)
 for K, meth in ((32, "farthest"),):
-    a = BatchedAstar(g, cost, "cuda:0", slots=80000, wave_slots=49152, landmarks=K, landmark_method=meth)
+    a = BatchedAstar(g, cost, "cuda:0", slots=80000, wave_slots=32768, arena_gb=16, landmarks=K, landmark_method=meth)
     a.run(S[:1000], T[:1000])
     torch.cuda.synchronize()
     t0 = time.perf_counter()

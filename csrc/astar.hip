@@ -7,10 +7,9 @@
 // sized to what the search may touch, not to the graph — workspace is O(slots x table), independent
 // of N, so a 1M-node graph serves as many concurrent searches as a 10k-node one (the round-2 design
 // kept a dense [slots, N] state plus a [slots, N] heuristic cache: 153 GB for 80k searches on a
-// 100k-node graph, and no 1M-node graph fit at all).  Linear probing with a hash that is the identity
-// on the low bits: ids that are neighbours in the graph (row-major grids, Morton-ordered OSM) land in
-// neighbouring entries, so a second probe is almost always the same 128-byte line.  Parent pointers
-// are table slots, so the path walk needs no probing; the reset list holds slots as well.
+// 100k-node graph, and no 1M-node graph fit at all).  Linear probing over a multiplicative hash
+// (hslot); a relaxation's first probe is issued with the edge loads, like the dense word was.
+// Parent pointers are table slots, so the path walk needs no probing; the reset list holds slots.
 //
 // Three tiers, each an AstarWs (tables + heap rows + reset lists), run by astar_search():
 //   lane  — one LANE per query, an 8-ary lane heap (LaneHeap), `lane_pops` pops in small tables
@@ -66,6 +65,13 @@ struct AstarArgs {
   int* out_iters;        // [Q] pops (lane) / expansions (wave) per query (nullptr: not recorded)
 };
 
+// Growth arena of the wave tier (all-ones when idle; the bump counter is reset before each launch)
+struct AstarArena {
+  AEnt* base;
+  unsigned long long n;      // entries
+  unsigned long long* ctr;   // bump pointer (entries)
+};
+
 constexpr int KMAX = 32;
 // edges relaxed per batch of independent loads (road-graph degrees are 2-6, mostly 4-5)
 constexpr int RB = 4;
@@ -112,10 +118,17 @@ __device__ __forceinline__ void load_target_lm(const AstarArgs& a, int t, float 
   }
 }
 
-// identity on the low bits, high bits mixed in (see the header comment)
+// Block hashing: the 8 ids of a group (u >> 3) share one 128-byte block of 8 entries, at offset u & 7,
+// and the block is chosen by Fibonacci (multiplicative) hashing of the group; a collision moves to the
+// next block at the same offset (probe stride 8).  So ids that are neighbours in the graph (row-major
+// grids, Morton-ordered OSM) share cache lines like the dense state did, while blocks are scattered
+// uniformly: each of the 8 offset columns is an ordinary linear-probing table over random blocks
+// (expected probes <= 2.5 at the half-full limit).  Hashing that keeps whole id RUNS contiguous
+// (identity on the low bits) clustered under wrap-around collisions and ran the wave tier 30x slower.
 __device__ __forceinline__ unsigned hslot(unsigned u, int tbits) {
-  return (u ^ ((u >> tbits) * 0x9E3779B1u)) & ((1u << tbits) - 1u);
+  return (((u >> 3) * 0x9E3779B1u) >> (35 - tbits) << 3) | (u & 7u);
 }
+constexpr unsigned PSTEP = 8;                       // probe stride (one block)
 __device__ __forceinline__ AEnt ld_ent(const AEnt* p) {
   const uint4 x = *reinterpret_cast<const uint4*>(p);
   AEnt e;
@@ -283,8 +296,8 @@ __global__ __launch_bounds__(64) void astar_kernel(AstarArgs a) {
     AEnt ev = ld_ent(tab + pv);
     const int e0 = a.indptr[v], e1 = a.indptr[v + 1];
     hq.pop(hn);
-    for (unsigned n = 0; ev.key != (unsigned)v && n < mask; ++n) {   // a pushed node is in the table
-      pv = (pv + 1) & mask;
+    for (unsigned n = 0; ev.key != (unsigned)v && n < (mask >> 3); ++n) {   // a pushed node is in the table
+      pv = (pv + PSTEP) & mask;
       ev = ld_ent(tab + pv);
     }
     if (ev.key != (unsigned)v) { status = 2; break; }
@@ -328,8 +341,8 @@ __global__ __launch_bounds__(64) void astar_kernel(AstarArgs a) {
         }
         if (stale) e = ld_ent(tab + p);
         // (an empty entry is always reachable: inserts stop at half the table)
-        for (unsigned n = 0; e.key != u && e.key != EMPTY && n < mask; ++n) {
-          p = (p + 1) & mask;
+        for (unsigned n = 0; e.key != u && e.key != EMPTY && n < (mask >> 3); ++n) {
+          p = (p + PSTEP) & mask;
           e = ld_ent(tab + p);
         }
         if (e.key != u && e.key != EMPTY) { overflow = true; break; }
@@ -381,25 +394,34 @@ __global__ __launch_bounds__(64) void astar_kernel(AstarArgs a) {
 // claimer records the slot for the reset), the state word is lowered with atomicMin, and plain
 // loads only ever see older (larger) words, which at worst cost a redundant atomic.  The heap row
 // holds near A | near B | far.
+// (waves_per_eu 4: the compiler fits the kernel in 102 VGPRs instead of 136 with no scratch, so four
+// searches per SIMD are resident instead of three; the tier is bound by dependent-load latency)
 template <int K>
-__global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* __restrict__ qidx, int T,
-                                                        float delta) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void astar_wave_kernel(AstarArgs a, const int* __restrict__ qidx, int T,
+                                                        float delta, AstarArena ar) {
   const int w = blockIdx.x;
   if (w >= T || w >= a.S) return;
   const int q = qidx != nullptr ? qidx[w] : a.q0 + w;
   const int lane = threadIdx.x;
-  const int tb = a.tbits;
-  const int TS = 1 << tb;
-  const unsigned mask = (unsigned)TS - 1u;
-  const int tcap = TS / 2;
+  // the search's table: the slot's own region first; GROWN (2x per step) into the arena when it
+  // fills up — memory follows the search instead of a fixed worst case per slot
+  int tb = a.tbits;
+  unsigned mask = (1u << tb) - 1u;
+  int tcap = 1 << (tb - 1);
   AEnt* tab = a.tab + ((size_t)w << tb);
-  int* nearA = reinterpret_cast<int*>(a.heap + (size_t)w * a.cap);
-  const int NCAP = a.cap / 2;                       // ints per near list
-  int* nearB = nearA + NCAP;
-  unsigned long long* far = a.heap + (size_t)w * a.cap + a.cap / 2;
-  const int FCAP = a.cap / 2;                       // (f, node) entries
   int* touched = a.touched + (size_t)w * tcap;
+  bool in_arena = false;
+  // the f-band lists (near A | near B | far) start in the slot's heap row and, like the table, move
+  // into larger arena buffers when a band would not fit
+  int* nearA = reinterpret_cast<int*>(a.heap + (size_t)w * a.cap);
+  int ncapA = a.cap / 2, ncapB = a.cap / 2;         // ints per near list
+  bool narA = false, narB = false;
+  int* nearB = nearA + a.cap / 2;
+  unsigned long long* far = a.heap + (size_t)w * a.cap + a.cap / 2;
+  int FCAP = a.cap / 2;                             // (f, node) entries
+  bool farena = false;
   __shared__ int s_next, s_far, s_touch, s_bad;
+  __shared__ unsigned long long s_off;
   const int s = a.src[q], t = a.dst[q];
   const float k = 0.017453292519943295f;
   const float tlat = a.lat[t] * k, tlon = a.lon[t] * k, ctl = __cosf(tlat);
@@ -411,22 +433,22 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
     return hv;
   };
   auto bad = [&]() { return *reinterpret_cast<volatile int*>(&s_bad) != 0; };
-  // slot of u, or -1 if absent (probes are bounded: the table is never more than half full
-  // unless the search overflowed, and then at most TS probes)
+  // slot of u, or -1 if absent (bounded: an empty entry is always reachable below the grow
+  // threshold; past an overflow at most TS / 8 probes per offset column)
   auto find = [&](unsigned u) -> int {
     unsigned p = hslot(u, tb);
-    for (int n = 0; n < TS; ++n) {
+    for (unsigned n = 0; n <= (mask >> 3); ++n) {
       const unsigned key = __hip_atomic_load(&tab[p].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (key == u) return (int)p;
       if (key == EMPTY) return -1;
-      p = (p + 1) & mask;
+      p = (p + PSTEP) & mask;
     }
     return -1;
   };
-  // find-or-insert u starting at slot p; -1 when the table is full
+  // find-or-insert u starting at slot p; -1 when its offset column is full
   auto acquire = [&](unsigned u, unsigned p, bool& claimed) -> int {
     claimed = false;
-    for (int n = 0; n < TS; ++n) {
+    for (unsigned n = 0; n <= (mask >> 3); ++n) {
       const unsigned key = __hip_atomic_load(&tab[p].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (key == u) return (int)p;
       if (key == EMPTY) {
@@ -434,14 +456,109 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
         if (old == EMPTY) { claimed = true; return (int)p; }
         if (old == u) return (int)p;
       }
-      p = (p + 1) & mask;
+      p = (p + PSTEP) & mask;
     }
     return -1;
   };
-  int pt = -1;                                      // t's slot once inserted (slots never move)
+  int pt = -1;                                      // t's slot once inserted (until the table grows)
   auto gbest = [&]() -> float {
     if (pt < 0) pt = find((unsigned)t);
     return pt < 0 ? __int_as_float(0x7f800000) : w_g(tab[pt].w);
+  };
+  // Arena allocation of `units` 16-byte entries (all lanes, uniform control flow); nullptr when
+  // the arena is exhausted.  Everything allocated is restored to all-ones before the search ends.
+  auto alloc = [&](unsigned long long units) -> AEnt* {
+    __syncthreads();
+    if (lane == 0) {
+      const unsigned long long off = atomicAdd(ar.ctr, units);
+      s_off = off + units <= ar.n ? off : ~0ull;
+    }
+    __syncthreads();
+    return s_off == ~0ull ? nullptr : ar.base + s_off;
+  };
+  auto fill_ones = [&](void* p, long long bytes) {     // bytes % 16 == 0
+    uint4* q = reinterpret_cast<uint4*>(p);
+    for (long long i = lane; i < bytes / 16; i += 64) q[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  };
+  // a near list able to take `need` ints (its content is dead at the call)
+  auto ensure_near = [&](int*& lst, int& cap, bool& inar, int need) -> bool {
+    if (need <= cap) return true;
+    int nc = cap * 2;
+    while (nc < need) nc *= 2;
+    nc = (nc + 3) & ~3;
+    AEnt* p = alloc((unsigned long long)nc / 4);
+    if (p == nullptr) return false;
+    if (inar) fill_ones(lst, (long long)cap * 4);
+    lst = reinterpret_cast<int*>(p);
+    cap = nc;
+    inar = true;
+    __syncthreads();
+    return true;
+  };
+  auto ensure_far = [&](int need) -> bool {
+    if (need <= FCAP) return true;
+    int nc = FCAP * 2;
+    while (nc < need) nc *= 2;
+    nc = (nc + 1) & ~1;
+    AEnt* p = alloc((unsigned long long)nc / 2);
+    if (p == nullptr) return false;
+    unsigned long long* nf = reinterpret_cast<unsigned long long*>(p);
+    const int nfar = s_far < FCAP ? s_far : FCAP;
+    for (int i = lane; i < nfar; i += 64) nf[i] = far[i];
+    __syncthreads();
+    if (farena) fill_ones(far, (long long)FCAP * 8);
+    far = nf;
+    FCAP = nc;
+    farena = true;
+    __syncthreads();
+    return true;
+  };
+  // Grow 2x into the arena (all lanes, at a point where no lane is inside a pass).  Entries are
+  // re-inserted, the old slot -> new slot map is kept in the dead table's key fields to rewrite the
+  // parent pointers, and the old table (and old reset list, if it was an arena one) is restored to
+  // all-ones.  Returns false when the arena is exhausted (the search then overflows to the big tier).
+  auto grow = [&]() -> bool {
+    const int nb = tb + 1;
+    const unsigned long long tsz = 1ull << nb, lsz = (tsz / 2 * 4 + 15) / 16;   // table + reset list
+    AEnt* ntab = alloc(tsz + lsz);
+    if (ntab == nullptr) return false;
+    int* ntouch = reinterpret_cast<int*>(ntab + tsz);
+    const unsigned nmask = (unsigned)tsz - 1u;
+    const int nt = s_touch < tcap ? s_touch : tcap;
+    for (int i = lane; i < nt; i += 64) {
+      const int o = touched[i];
+      const AEnt e = ld_ent(tab + o);
+      unsigned p = hslot(e.key, nb);
+      for (unsigned n = 0; n <= (nmask >> 3); ++n) {
+        if (atomicCAS(&ntab[p].key, EMPTY, e.key) == EMPTY) break;
+        p = (p + PSTEP) & nmask;
+      }
+      ntab[p].h = e.h;
+      ntab[p].w = e.w;
+      ntouch[i] = (int)p;
+      tab[o].key = p;                               // old -> new slot (the old table is dead)
+    }
+    __syncthreads();
+    for (int i = lane; i < nt; i += 64) {
+      const int p = ntouch[i];
+      const unsigned long long e = ntab[p].w;
+      const unsigned par = w_par(e);
+      if (par != NOPAR) ntab[p].w = (e & ~(unsigned long long)NOPAR) | tab[par].key;
+    }
+    __syncthreads();
+    for (int i = lane; i < nt; i += 64) {
+      clr_ent(tab + touched[i]);
+      if (in_arena) touched[i] = -1;
+    }
+    __syncthreads();
+    tab = ntab;
+    touched = ntouch;
+    tb = nb;
+    mask = nmask;
+    tcap = (int)(tsz / 2);
+    in_arena = true;
+    pt = -1;
+    return true;
   };
 
   if (lane == 0) {
@@ -454,23 +571,46 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
     s_bad = 0;
   }
   __syncthreads();
-  int* cur = nearA;
-  int* nxt = nearB;
+  // cur / nxt alias the two near lists (A, B) and swap every pass
+  bool curA = true;
   int nnear = 1;
   float thr = heur(s) + delta;
   long long expanded = 0;
   int status = 1;
   while (true) {
     while (nnear > 0) {
+      // keep the table at most half full after a pass (a pass inserts at most ~6 entries per
+      // expanded node), growing 2x at a time while the arena lasts
+      while (s_touch + 8 * nnear > tcap && ar.base != nullptr && tb + 1 <= 26) {
+        if (!grow()) break;
+      }
+      if (ar.base != nullptr) {             // room for this pass's pushes (<= 8 per expansion)
+        if (curA) ensure_near(nearB, ncapB, narB, 8 * nnear);
+        else ensure_near(nearA, ncapA, narA, 8 * nnear);
+        ensure_far(s_far + 8 * nnear);
+      }
+      int* cur = curA ? nearA : nearB;
+      int* nxt = curA ? nearB : nearA;
+      const int ncap_nxt = curA ? ncapB : ncapA;
       if (lane == 0) s_next = 0;
       __syncthreads();
       const float best = gbest();
       for (int i = lane; i < nnear; i += 64) {
         if (bad()) break;
         const int v = cur[i];
-        const int pv = find((unsigned)v);
+        // probe with whole-entry loads: the hit is the entry (no second dependent load)
+        int pv = -1;
+        AEnt ev;
+        {
+          unsigned p = hslot((unsigned)v, tb);
+          for (unsigned n = 0; n <= (mask >> 3); ++n) {
+            ev = ld_ent(tab + p);
+            if (ev.key == (unsigned)v) { pv = (int)p; break; }
+            if (ev.key == EMPTY) break;
+            p = (p + PSTEP) & mask;
+          }
+        }
         if (pv < 0) continue;
-        const AEnt ev = ld_ent(tab + pv);
         const float gv = w_g(ev.w);
         const float hv = ev.h == ev.h ? ev.h : heur(v);
         if (!(gv + hv < best)) continue;                 // cannot lead to a better path
@@ -481,6 +621,7 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
           float cc[RB];
           unsigned pp[RB];
           unsigned long long seen[RB];
+          bool hit[RB];
 #pragma unroll
           for (int j = 0; j < RB; ++j) {
             const bool in = eb + j < e1;
@@ -491,10 +632,12 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
           for (int j = 0; j < RB; ++j) {
             pp[j] = hslot((unsigned)uu[j], tb);
             seen[j] = 0ull;
+            hit[j] = false;
             if (eb + j < e1) {
               const AEnt x = ld_ent(tab + pp[j]);
-              // known entry: its word; empty or another key: unknown (take the atomic path)
-              seen[j] = x.key == (unsigned)uu[j] ? x.w : W_INIT;
+              // known entry: its word and slot; empty or another key: unknown (probe + claim)
+              hit[j] = x.key == (unsigned)uu[j];
+              seen[j] = hit[j] ? x.w : W_INIT;
             }
           }
 #pragma unroll
@@ -506,8 +649,8 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
             // plain load first: most relaxations do not improve, and a 64-bit atomic costs far
             // more than a load
             if (nw >= seen[j]) continue;
-            bool claimed;
-            const int p = acquire((unsigned)u, pp[j], claimed);
+            bool claimed = false;
+            const int p = hit[j] ? (int)pp[j] : acquire((unsigned)u, pp[j], claimed);
             if (p < 0) { s_bad = 1; break; }
             if (claimed) {
               const int ti = atomicAdd(&s_touch, 1);
@@ -524,7 +667,7 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
             const float f = ng + hu;
             if (f < thr) {
               const int ni = atomicAdd(&s_next, 1);
-              if (ni < NCAP) nxt[ni] = u;
+              if (ni < ncap_nxt) nxt[ni] = u;
               else s_bad = 1;
             } else {
               const int fi = atomicAdd(&s_far, 1);
@@ -536,10 +679,8 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
       }
       expanded += nnear;
       __syncthreads();
-      nnear = s_next < NCAP ? s_next : NCAP;
-      int* tmp = cur;
-      cur = nxt;
-      nxt = tmp;
+      nnear = s_next < ncap_nxt ? s_next : ncap_nxt;
+      curA = !curA;
       if (s_bad) { status = 2; break; }
       if (expanded > a.max_iters) { status = 3; break; }
     }
@@ -558,6 +699,13 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
     thr = fmin + delta;
     // split far in place: f < thr -> near (cur), f < best -> keep (compacted), else drop.  A chunk of
     // 64 is read before any of its kept entries is written, and writes never pass reads.
+    // the split refills cur (its content is dead): make room for every far entry
+    if (ar.base != nullptr) {
+      if (curA) ensure_near(nearA, ncapA, narA, nfar);
+      else ensure_near(nearB, ncapB, narB, nfar);
+    }
+    int* cur = curA ? nearA : nearB;
+    const int ncap_cur = curA ? ncapA : ncapB;
     if (lane == 0) {
       s_next = 0;
       s_far = 0;
@@ -575,13 +723,13 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
       if (keep) far[base + __popcll(mk & ((1ull << lane) - 1))] = x;
       if (to_near) {
         const int ni = atomicAdd(&s_next, 1);
-        if (ni < NCAP) cur[ni] = (int)(unsigned)(x & 0xffffffffu);
+        if (ni < ncap_cur) cur[ni] = (int)(unsigned)(x & 0xffffffffu);
         else s_bad = 1;
       }
       if (lane == 0) s_far = base + __popcll(mk);
       __syncthreads();
     }
-    nnear = s_next < NCAP ? s_next : NCAP;
+    nnear = s_next < ncap_cur ? s_next : ncap_cur;
     if (s_bad) { status = 2; break; }
   }
   __syncthreads();
@@ -602,10 +750,18 @@ __global__ __launch_bounds__(64) void astar_wave_kernel(AstarArgs a, const int* 
   __syncthreads();
   const int nt = s_touch;
   if (nt <= tcap) {
-    for (int i = lane; i < nt; i += 64) clr_ent(tab + touched[i]);
+    for (int i = lane; i < nt; i += 64) {
+      clr_ent(tab + touched[i]);
+      if (in_arena) touched[i] = -1;
+    }
   } else {                                            // claims past the reset list: clear everything
-    for (int i = lane; i < TS; i += 64) clr_ent(tab + i);
+    for (int i = lane; i <= (int)mask; i += 64) clr_ent(tab + i);
+    if (in_arena)
+      for (int i = lane; i < tcap; i += 64) touched[i] = -1;
   }
+  if (narA) fill_ones(nearA, (long long)ncapA * 4);
+  if (narB) fill_ones(nearB, (long long)ncapB * 4);
+  if (farena) fill_ones(far, (long long)FCAP * 8);
 }
 
 // Ordered compaction: qidx = [i for i in range(Q) if (1 << status[i]) & want], count = len (one block;
@@ -682,17 +838,24 @@ hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* 
 
 hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* dst, int Q, const int* qidx,
                              int q0, int T, const AstarWs& ws, const AstarOut& o, int max_iters, float delta,
-                             hipStream_t stream) {
+                             hipStream_t stream, const AstarArenaBuf* arena) {
   const int n = T < ws.slots ? T : ws.slots;
   if (n <= 0) return hipSuccess;
   if (g.lm != nullptr && g.K != 32 && g.K != 16 && g.K != 8) return hipErrorInvalidValue;
   if (!astar_ws_ok(ws, true)) return hipErrorInvalidValue;
   if (qidx == nullptr && q0 + n > Q) return hipErrorInvalidValue;
   const AstarArgs a = make_args(g, src, dst, Q, q0, ws, o, max_iters);
-  if (g.lm == nullptr) hipLaunchKernelGGL(astar_wave_kernel<0>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta);
-  else if (g.K == 8) hipLaunchKernelGGL(astar_wave_kernel<8>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta);
-  else if (g.K == 16) hipLaunchKernelGGL(astar_wave_kernel<16>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta);
-  else hipLaunchKernelGGL(astar_wave_kernel<32>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta);
+  AstarArena ar{nullptr, 0, nullptr};
+  if (arena != nullptr && arena->base != nullptr && arena->ctr != nullptr && arena->entries > 0) {
+    // every search of the previous launch restored what it used: start the bump pointer over
+    hipError_t e = hipMemsetAsync(arena->ctr, 0, sizeof(unsigned long long), stream);
+    if (e != hipSuccess) return e;
+    ar = AstarArena{(AEnt*)arena->base, arena->entries, arena->ctr};
+  }
+  if (g.lm == nullptr) hipLaunchKernelGGL(astar_wave_kernel<0>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, ar);
+  else if (g.K == 8) hipLaunchKernelGGL(astar_wave_kernel<8>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, ar);
+  else if (g.K == 16) hipLaunchKernelGGL(astar_wave_kernel<16>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, ar);
+  else hipLaunchKernelGGL(astar_wave_kernel<32>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, ar);
   return hipGetLastError();
 }
 
@@ -713,7 +876,7 @@ static hipError_t select_count(const int* status, int Q, int want, int* scratch,
 
 hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, int Q, const AstarWs* lane,
                         const AstarWs* wave, const AstarWs* big, const AstarOut& o, const AstarPlan& pl,
-                        int* scratch, hipStream_t stream, AstarRunStats* st) {
+                        int* scratch, hipStream_t stream, AstarRunStats* st, const AstarArenaBuf* arena) {
   AstarRunStats z{};
   AstarRunStats& S = st != nullptr ? *st : z;
   S = AstarRunStats{};
@@ -744,7 +907,7 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
     S.wave = T;
     for (int i0 = 0; i0 < T && e == hipSuccess; i0 += wave->slots)
       e = launch_astar_wave(g, src, dst, Q, qidx != nullptr ? qidx + i0 : nullptr, i0, std::min(wave->slots, T - i0),
-                            *wave, o, pl.max_iters, pl.delta, stream);
+                            *wave, o, pl.max_iters, pl.delta, stream, arena);
   }
   if (e == hipSuccess && big != nullptr) {
     int E = 0;
@@ -754,7 +917,7 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
     S.escalated = E;
     for (int i0 = 0; i0 < E && e == hipSuccess; i0 += big->slots)
       e = launch_astar_wave(g, src, dst, Q, scratch + i0, 0, std::min(big->slots, E - i0), *big, o, pl.max_iters,
-                            pl.delta, stream);
+                            pl.delta, stream, arena);
     if (E > 0 && e == hipSuccess) e = hipStreamSynchronize(stream);
     S.big_ms = ms_since(t0);
   }

@@ -438,9 +438,9 @@ void check_bf16(const torch::Tensor& t, const char* name, int64_t rows, int64_t 
 
 // Writes every output in place (static buffers: the step is HIP-graph capturable).
 void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tensor blob, int64_t H,
-                        std::vector<double> norm, double gscale, torch::Tensor xf,
-                        torch::Tensor h1a, torch::Tensor w3slab, torch::Tensor dz2, torch::Tensor dz1,
-                        torch::Tensor dyb, torch::Tensor sq_err, torch::Tensor step_ctr) {
+                        std::vector<double> norm, double gscale, torch::Tensor xf, torch::Tensor w3slab,
+                        torch::Tensor dz2t, torch::Tensor dh1t, torch::Tensor dyb, torch::Tensor sq_err,
+                        torch::Tensor step_ctr) {
   check_dev(records, "records");
   check_dev(target, "target");
   check_dev(blob, "blob");
@@ -452,14 +452,17 @@ void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tens
   TORCH_CHECK(blob.scalar_type() == torch::kUInt8 &&
               (size_t)blob.numel() == rt::eta_mlp3_train_blob_bytes((int)H), "bad training blob");
   check_bf16(xf, "xf", B, 16);
-  check_bf16(h1a, "h1a", B, H + 16);
   check_dev(w3slab, "w3slab");
   const int grid = rt::train_fwd_grid((int)B, num_cus(records.device().index()));
   TORCH_CHECK(w3slab.scalar_type() == torch::kFloat32 && w3slab.is_contiguous() && w3slab.dim() == 2 &&
                   w3slab.size(0) == grid && w3slab.size(1) == H + 16,
               "w3slab must be f32 [train_fwd_grid(B), H + 16] = [", grid, ", ", H + 16, "]");
-  check_bf16(dz2, "dz2", B, H);
-  check_bf16(dz1, "dz1", B, H);
+  const int64_t tiles = (B + 31) / 32;
+  for (auto* t : {&dz2t, &dh1t}) {
+    check_dev(*t, "dz2t/dh1t");
+    TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->is_contiguous() && t->numel() == tiles * 32 * H,
+                "dz2t / dh1t must be bf16 with ceil(B/32) * 32 * H elements");
+  }
   check_bf16(dyb, "dyb", B, 8);
   check_dev(sq_err, "sq_err");
   TORCH_CHECK(sq_err.scalar_type() == torch::kFloat32 && sq_err.numel() >= B, "sq_err must be f32 [B]");
@@ -468,9 +471,32 @@ void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tens
   const c10::DeviceGuard guard(records.device());
   RT_CHECK_HIP(rt::launch_eta_mlp3_train_fwd(
       records.data_ptr(), target.data_ptr<float>(), (int)B, blob.data_ptr(), (int)H,
-      norm_from(norm), (float)gscale, xf.data_ptr(), h1a.data_ptr(), w3slab.data_ptr<float>(),
-      dz2.data_ptr(), dz1.data_ptr(), dyb.data_ptr(), sq_err.data_ptr<float>(), step_ctr.data_ptr<int>(),
-      num_cus(records.device().index()), cur_stream(records)));
+      norm_from(norm), (float)gscale, xf.data_ptr(), w3slab.data_ptr<float>(), dz2t.data_ptr(), dh1t.data_ptr(),
+      dyb.data_ptr(), sq_err.data_ptr<float>(), step_ctr.data_ptr<int>(), num_cus(records.device().index()),
+      cur_stream(records)));
+}
+
+// dW2|db2 and dW1 partial sums per k-slice from the forward's dz2^T / dh1^T (train_wgrad_kernel)
+void train_wgrad(torch::Tensor xf, int64_t B, torch::Tensor blob, int64_t H, torch::Tensor dz2t, torch::Tensor dh1t,
+                 torch::Tensor slab2, torch::Tensor slab1) {
+  for (auto* t : {&xf, &blob, &dz2t, &dh1t, &slab2, &slab1}) check_dev(*t, "train_wgrad tensor");
+  TORCH_CHECK(H == 64 || H == 128 || H == 256, "H in (64, 128, 256)");
+  check_bf16(xf, "xf", B, 16);
+  const int64_t tiles = (B + 31) / 32;
+  TORCH_CHECK(dz2t.numel() == tiles * 32 * H && dh1t.numel() == tiles * 32 * H &&
+                  dz2t.scalar_type() == torch::kBFloat16 && dh1t.scalar_type() == torch::kBFloat16,
+              "dz2t / dh1t shapes");
+  TORCH_CHECK(blob.scalar_type() == torch::kUInt8 && (size_t)blob.numel() == rt::eta_mlp3_train_blob_bytes((int)H),
+              "bad training blob");
+  const int64_t S = slab2.size(0);
+  TORCH_CHECK(slab2.scalar_type() == torch::kFloat32 && slab2.dim() == 2 && slab2.size(1) == H * (H + 16) &&
+                  slab1.scalar_type() == torch::kFloat32 && slab1.dim() == 2 && slab1.size(0) == S &&
+                  slab1.size(1) == H * 16 && S >= 1,
+              "slab2 f32 [S, H*(H+16)], slab1 f32 [S, H*16]");
+  const c10::DeviceGuard guard(xf.device());
+  RT_CHECK_HIP(rt::launch_train_wgrad(xf.data_ptr(), (int)B, blob.data_ptr(), (int)H, dz2t.data_ptr(),
+                                      dh1t.data_ptr(), slab2.data_ptr<float>(), slab1.data_ptr<float>(), (int)S,
+                                      cur_stream(xf)));
 }
 
 void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor V,
@@ -724,7 +750,8 @@ std::vector<double> astar_search(torch::Tensor indptr, torch::Tensor indices, to
                                  py::object big, torch::Tensor out_cost, torch::Tensor out_len,
                                  torch::Tensor out_status, torch::Tensor out_path,
                                  c10::optional<torch::Tensor> out_iters, torch::Tensor scratch, int64_t max_iters,
-                                 int64_t lane_pops, int64_t wave_only_below, double delta) {
+                                 int64_t lane_pops, int64_t wave_only_below, double delta,
+                                 c10::optional<torch::Tensor> arena, c10::optional<torch::Tensor> arena_ctr) {
   for (auto* t : {&indptr, &indices, &cost, &lat, &lon, &src, &dst, &out_cost, &out_len, &out_status, &out_path,
                   &scratch})
     check_dev(*t, "astar tensor");
@@ -782,10 +809,22 @@ std::vector<double> astar_search(torch::Tensor indptr, torch::Tensor indices, to
   pl.wave_only_below = (int)wave_only_below;
   pl.delta = (float)delta;
   rt::AstarRunStats st;
+  rt::AstarArenaBuf ab;
+  if (arena.has_value() && arena->defined()) {
+    TORCH_CHECK(arena_ctr.has_value() && arena_ctr->defined(), "arena needs its counter");
+    check_dev(*arena, "arena");
+    check_dev(*arena_ctr, "arena_ctr");
+    TORCH_CHECK(arena->scalar_type() == torch::kInt64 && arena->is_contiguous() && arena->numel() % 2 == 0 &&
+                    arena_ctr->scalar_type() == torch::kInt64 && arena_ctr->numel() >= 1,
+                "arena int64 [2n] (all-ones), counter int64 [1]");
+    ab.base = arena->data_ptr();
+    ab.entries = (unsigned long long)(arena->numel() / 2);
+    ab.ctr = (unsigned long long*)arena_ctr->data_ptr();
+  }
   const c10::DeviceGuard guard(lat.device());
   RT_CHECK_HIP(rt::astar_search(g, src.data_ptr<int>(), dst.data_ptr<int>(), (int)Q, hl ? &wl : nullptr,
                                 hw ? &ww : nullptr, hb ? &wb : nullptr, o, pl, scratch.data_ptr<int>(),
-                                cur_stream(lat), &st));
+                                cur_stream(lat), &st, ab.base ? &ab : nullptr));
   return {(double)st.lane, (double)st.wave, (double)st.escalated, st.lane_ms, st.wave_ms, st.big_ms};
 }
 
@@ -934,6 +973,14 @@ static rt::RouteServiceCfg route_cfg_from(const py::dict& d, int device, const v
     ws_from(d.contains("lane_ws") ? py::object(d["lane_ws"]) : py::object(py::none()), c.lane_ws, dev);
     ws_from(d.contains("wave_ws") ? py::object(d["wave_ws"]) : py::object(py::none()), c.wave_ws, dev);
     ws_from(d.contains("big_ws") ? py::object(d["big_ws"]) : py::object(py::none()), c.big_ws, dev);
+    if (has("arena")) {
+      torch::Tensor ar = d["arena"].cast<torch::Tensor>(), ctr = d["arena_ctr"].cast<torch::Tensor>();
+      TORCH_CHECK(ar.is_cuda() && ar.device().index() == device && ar.scalar_type() == torch::kInt64 &&
+                      ctr.is_cuda() && ctr.scalar_type() == torch::kInt64, "route config arena");
+      c.arena.base = ar.data_ptr();
+      c.arena.entries = (unsigned long long)(ar.numel() / 2);
+      c.arena.ctr = (unsigned long long*)ctr.data_ptr();
+    }
     c.N = d["N"].cast<int>();
     c.K = has("K") ? d["K"].cast<int>() : 0;
     c.snap_c = d["snap_c"].cast<double>();
@@ -1131,7 +1178,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw_pack_big", &adamw_pack_big, "wide trainer: AdamW + re-pack of w1p / w2k / w2t / b2 / w3 / b3");
   m.def("big_dz2y", &big_dz2y, "wide trainer: dy, dyb, squared error, dz2 and the step counter in one launch");
   m.def("big_dz2", &big_dz2, "dz2 = dy * w3 * relu'(z2) from h2a (hperm order)");
-  m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad + input-gradient path (dz2, dz1)");
+  m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad + input-gradient path (dz2^T, dh1^T)");
+  m.def("train_wgrad", &train_wgrad, "K3: dW2|db2 and dW1 split-K partials, register-resident (train_wgrad_kernel)");
+  m.def("train_wgrad_slices", [](int64_t B, int64_t device) { return (int64_t)rt::train_wgrad_slices((int)B, num_cus((int)device)); });
   m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + training-blob re-pack");
   m.def("eta_mlp3_train_blob_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_train_blob_bytes((int)H); });
   m.def("mlp3_num_params", [](int64_t H) { return (int64_t)rt::mlp3_num_params((int)H); });
@@ -1156,7 +1205,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("landmarks"), py::arg("src"), py::arg("dst"), py::arg("lane"), py::arg("wave"), py::arg("big"),
         py::arg("out_cost"), py::arg("out_len"), py::arg("out_status"), py::arg("out_path"), py::arg("out_iters"),
         py::arg("scratch"), py::arg("max_iters"), py::arg("lane_pops"), py::arg("wave_only_below"),
-        py::arg("delta"));
+        py::arg("delta"), py::arg("arena") = py::none(), py::arg("arena_ctr") = py::none());
   m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
   m.def("forest_predict_lds", &forest_predict_lds, "K4: LDS-staged tree chunks, 2 walks per thread");
   m.def("pscore_create", &pscore_create, "resident single-request scorer kernel on the blob's GPU");

@@ -40,6 +40,8 @@
 // Natural column order is what makes relu'(z1) lane-local: dgrad accumulator register e of lane
 // half h is unit 32mi + 8(e>>2) + 4h + (e&3), element e&7 of the lane's own h1 fragment.
 // The rest of the blob is the inference layout (mlp3_tile.h): w1p, b1p, b2p, w3p, tail.
+#include <cstdlib>
+
 #include "lds_fill.h"
 #include "mlp3_tile.h"
 #include "ops.h"
@@ -87,9 +89,8 @@ template <int H>
 __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     const int4* __restrict__ rec, const float* __restrict__ target, int B,
     const unsigned char* __restrict__ blob, NormParams np, float gscale, __bf16* __restrict__ xf,
-    __bf16* __restrict__ h1a, float* __restrict__ w3slab, __bf16* __restrict__ dz2,
-    __bf16* __restrict__ dz1, __bf16* __restrict__ dyb, float* __restrict__ sq_err,
-    int* __restrict__ step_ctr) {
+    float* __restrict__ w3slab, bf16x8* __restrict__ dz2t, bf16x8* __restrict__ dh1t,
+    __bf16* __restrict__ dyb, float* __restrict__ sq_err, int* __restrict__ step_ctr) {
   using L = TrainLayout<H>;
   constexpr int MT = H / 32, KS = H / 16, LDA = H + 16, D = KS < 4 ? KS : 4;
   // device-side optimizer step counter (read by adamw_pack_kernel later on the same stream), so a
@@ -97,7 +98,12 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
   if (step_ctr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *step_ctr += 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   lds_fill_block(smem, blob, (int)L::BLOB);
-  const unsigned char* img = smem;
+  // the W2 image as an absolute LDS address: dynamic LDS starts at 0 in this kernel (it has no
+  // static __shared__ data), and a literal base lets every fragment read use its lane register as
+  // the address with the rest in the instruction's offset field (through the extern array's base,
+  // which is a link-time symbol, the compiler inserted a v_add of that base before each read)
+  typedef __attribute__((address_space(3))) const unsigned char lds_u8;
+  lds_u8* img = (lds_u8*)(uintptr_t)0;
   const bf16x8* w1p = reinterpret_cast<const bf16x8*>(smem + L::W2B);
   const f32x4* b2p = reinterpret_cast<const f32x4*>(smem + L::W2B + L::W1B) + H / 4;
   const f32x4* w3p = b2p + H / 4;
@@ -144,16 +150,7 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       relu_cvt_bf16x8(a, &h1[2 * mt]);
       relu_cvt_bf16x8(a + 8, &h1[2 * mt + 1]);
     }
-    __bf16* h1row = h1a + (size_t)row * LDA;
-    if (valid) {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf16x8*>(h1row + 16 * ks + 8 * h) = h1[ks];
-      bf16x8 tailv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) tailv[j] = (__bf16)0.f;
-      if (h == 0) tailv[0] = (__bf16)1.f;
-      *reinterpret_cast<bf16x8*>(h1row + H + 8 * h) = tailv;
-    }
+    // (h1 is not stored: train_wgrad_kernel recomputes it from xf on the same MFMA)
 
     // layer 2 + layer 3 in TWO passes over the hidden tiles, relu(z2) never stored: pass 1 only
     // forms y (hence dy); pass 2 recomputes z2 per tile for the relu'(z2) mask and the dW3 | db3
@@ -169,7 +166,7 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       // would wait for all of them, vmcnt being in order): chunk (2ks + h) ^ w2swz(r) only
       // depends on ks & 7, ks >> 3 adds 256 B
       const int sw = w2swz(r);
-      const unsigned char* lrow = img + r * 512;
+      lds_u8* lrow = img + r * 512;
       constexpr int NX = KS < 8 ? KS : 8;      // distinct ks & 7 patterns (ks >> 3 adds 256 B)
       int xk[NX][2];
 #pragma unroll
@@ -190,12 +187,12 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
         }
       auto layer2 = [&](int mt) {
         f32x16 acc = load_vec16(b2p, mt, h);
-        const unsigned char* pm = lrow + mt * 16384;
+        lds_u8* pm = lrow + mt * 16384;
         // units 16ks + 4h + 0..3 and 16ks + 8 + 4h + 0..3: the permuted k order of h1
         auto frag = [&](int ks) {
           const int* xo = (ks >> 3) ? xk8[ks & 7] : xk[ks & 7];
-          const s16x4 lo = *reinterpret_cast<const s16x4*>(pm + xo[0]);
-          const s16x4 hi = *reinterpret_cast<const s16x4*>(pm + xo[1]);
+          const s16x4 lo = *reinterpret_cast<const lds_s16x4*>(pm + xo[0]);
+          const s16x4 hi = *reinterpret_cast<const lds_s16x4*>(pm + xo[1]);
           return join4(lo, hi);
         };
         bf16x8 ring[D];
@@ -238,9 +235,8 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       // the tile's rows 8(e>>2) + 4h + (e&3) in the registers — so the row sum is 16 in-lane FMAs
       // and ONE cross-half add per hidden tile instead of a 5-step lane reduce-scatter.  The rows'
       // dy reach the lanes through a 128-byte LDS broadcast; rows past B carry dy = 0.
-      const float dyr = (float)(__bf16)dy;
       float* const dys = dyscr;                      // this wave's 32-float scratch
-      if (h == 0) dys[r] = dyr;
+      if (h == 0) dys[r] = dy;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -252,18 +248,18 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
         for (int j = 0; j < 4; ++j) dyv[4 * q4 + j] = t[j];
       }
       const float* b2f = reinterpret_cast<const float*>(b2p);
-      const int bpos = 2 * ((r >> 2) & 1) * 8 + 4 * (r >> 3) + (r & 3);   // b2 of unit 32mt + r
+      const int bpos = 2 * ((r >> 2) & 1) * 8 + 4 * (r >> 3) + (r & 3);   // b2 / w3 of unit 32mt + r
 #pragma unroll 1
       for (int mt = 0; mt < MT; ++mt) {
         f32x16 acc;
         const float bias = b2f[mt * 32 + bpos];
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[e] = bias;
-        const unsigned char* pm = lrow + mt * 16384;
+        lds_u8* pm = lrow + mt * 16384;
         auto fragw = [&](int ks) {
           const int* xo = (ks >> 3) ? xk8[ks & 7] : xk[ks & 7];
-          const s16x4 lo = *reinterpret_cast<const s16x4*>(pm + xo[0]);
-          const s16x4 hi = *reinterpret_cast<const s16x4*>(pm + xo[1]);
+          const s16x4 lo = *reinterpret_cast<const lds_s16x4*>(pm + xo[0]);
+          const s16x4 hi = *reinterpret_cast<const lds_s16x4*>(pm + xo[1]);
           return join4(lo, hi);
         };
         bf16x8 ring[D];
@@ -289,8 +285,8 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
           w3part[(u & ~12) | ((u & 4) << 1) | ((u & 8) >> 1)] += t;
         }
       }
-      // db3 = sum of bf16(dy) over the rows (lanes of half 0 hold each row once)
-      float d = h == 0 ? dyr : 0.f;
+      // db3 = sum of dy over the rows (lanes of half 0 hold each row once)
+      float d = h == 0 ? dy : 0.f;
 #pragma unroll
       for (int o = 16; o >= 1; o >>= 1) d += __shfl_xor(d, o);
       if (lv == 0) w3part[H] += d;
@@ -332,20 +328,47 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
         dz2f[2 * mt + s] = __builtin_bit_cast(bf16x8, dw);
       }
     }
-    if (valid) {
-      __bf16* drow = dz2 + (size_t)row * H;
+    // dz2^T for the weight-gradient kernel: each hidden tile transposed by TWO MFMAs against a
+    // permuted identity (B[k][n] = 1 iff fragment k of this lane half holds unit n), which turns the
+    // rows-on-lanes fragments into units-on-lanes / rows-in-registers — exact (every product is
+    // x * 1) — and stored in the MFMA operand order: chunk (tile, K-step s, unit, lane half h)
+    {
+      bf16x8 eye0, eye1;
+      const int n = lv & 31;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf16x8*>(drow + 16 * ks + 8 * h) = dz2f[ks];
+      for (int j = 0; j < 8; ++j) {
+        const int u0 = (j & 3) + 8 * (j >> 2) + 4 * h;          // unit offset of k = 8h + j, K-step 0
+        eye0[j] = (__bf16)(u0 == n ? 1.f : 0.f);
+        eye1[j] = (__bf16)(u0 + 16 == n ? 1.f : 0.f);
+      }
+      f32x16 zero;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) zero[e] = 0.f;
+      typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+      typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        f32x16 tt = mfma32(dz2f[2 * mt], eye0, zero);
+        tt = mfma32(dz2f[2 * mt + 1], eye1, tt);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          u32x4v ow;
+#pragma unroll
+          for (int q2 = 0; q2 < 4; ++q2) {
+            const f32x2 pr = {tt[8 * s2 + 2 * q2], tt[8 * s2 + 2 * q2 + 1]};
+            ow[q2] = __builtin_bit_cast(unsigned, __builtin_convertvector(pr, bf16x2v));
+          }
+          dz2t[(((size_t)tile * 2 + s2) * H + 32 * mt + n) * 2 + h] = __builtin_bit_cast(bf16x8, ow);
+        }
+      }
     }
 
-    // dgrad: dh1^T tile mi = W2^T[32mi.., :] dz2^T, then dz1 = dh1 * relu'(z1).  Accumulator
-    // register e is input unit 32mi + 8(e>>2) + 4h + (e&3): exactly element e&7 of this lane's own
-    // h1 fragment 2mi + (e>>3), so relu'(z1) is a lane-local select on the packed bf16 output, and
-    // dz1 lands at hperm positions 32mi + 16(e>>3) + 8h + (e&7) — two 16-byte stores like h1a.
-    // The mi loop is unrolled so that h1 is indexed statically (kept in registers, never re-read
-    // from memory: a load would wait for every older store of the wave).
+    // dgrad: dh1 = dz2 W2 on the TRANSPOSED tile — dz2 as the A operand (rows on the lanes) and
+    // the W2^T fragment as B — so the accumulator holds input unit 32mi + (l&31) on the lane and the
+    // tile's rows in the registers, in the MFMA k order.  That is the dW1 GEMM's A layout: stored
+    // like dz2^T (one 16-byte chunk per K-step and lane half), it is read by train_wgrad_kernel
+    // without any transpose; relu'(z1) is applied there, from the h1^T tile it recomputes anyway.
     {
-      __bf16* zrow = dz1 + (size_t)row * H;
       // transposed reads: rows 16ks + 8t + 4h + q, columns 32mi + 16(g&1) + 4p (8-byte chunk
       // 8mi + 4(g&1) + p) -> chunk ^ ((q << 3) | (4(ks&1) + 2t + h))
       // = 64 (mi ^ q) + 8 ((4(g&1) + p) ^ (4(ks&1) + 2t + h)): the lane part of the second term
@@ -353,8 +376,8 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       // replace a full address computation per read
       const int g1 = (lv >> 4) & 1, p = lv & 3, q = (lv >> 2) & 3;
       const int lx = 4 * g1 + p;
-      const unsigned char* rb = img + (4 * h + q) * 512;
-      const unsigned char* bp[2][2];
+      lds_u8* rb = img + (4 * h + q) * 512;
+      lds_u8* bp[2][2];
 #pragma unroll
       for (int par = 0; par < 2; ++par)
 #pragma unroll
@@ -363,10 +386,10 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       for (int mi = 0; mi < MT; ++mi) {
         const int om = 64 * (mi ^ q);
         auto frag = [&](int ks) {
-          const unsigned char* r0 = bp[ks & 1][0] + om + 8192 * ks;
-          const unsigned char* r1 = bp[ks & 1][1] + om + 8192 * ks;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<unsigned char*>(r0)));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<unsigned char*>(r1)));
+          lds_u8* r0 = bp[ks & 1][0] + om + 8192 * ks;
+          lds_u8* r1 = bp[ks & 1][1] + om + 8192 * ks;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)r0);
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)r1);
           return join4(lo, hi);
         };
         f32x16 acc;
@@ -384,28 +407,19 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
             if (ks + D + d < KS) ring[d] = frag(ks + D + d);
           }
 #pragma unroll
-          for (int d = 0; d < D; ++d) acc = mfma32(a[d], dz2f[ks + d], acc);
+          for (int d = 0; d < D; ++d) acc = mfma32(dz2f[ks + d], a[d], acc);
         }
+        typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+        typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          // relu'(z1) from h1 as a packed mask: h1 halves are non-negative bf16 bit patterns
-          // (0 .. 0x7F80), so x + 0x7FFF has bit 15 set iff x != 0 (iff z1 > 0) and no carry
-          // crosses into the other half; an arithmetic >> 15 per half spreads it to 0xFFFF.
-          // Per pair of outputs: one v_cvt_pk_bf16_f32, one add, one v_pk_ashrrev_i16, one and.
-          typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-          typedef short s16x2v __attribute__((ext_vector_type(2)));
-          typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-          const u32x4v hw = __builtin_bit_cast(u32x4v, h1[2 * mi + s]);
+        for (int s2 = 0; s2 < 2; ++s2) {
           u32x4v ow;
 #pragma unroll
           for (int q2 = 0; q2 < 4; ++q2) {
-            const f32x2 pr = {acc[8 * s + 2 * q2], acc[8 * s + 2 * q2 + 1]};
-            const unsigned cw = __builtin_bit_cast(unsigned, __builtin_convertvector(pr, bf16x2v));
-            const s16x2v m = __builtin_bit_cast(s16x2v, hw[q2] + 0x7FFF7FFFu) >> (s16x2v){15, 15};
-            ow[q2] = cw & __builtin_bit_cast(unsigned, m);
+            const f32x2 pr = {acc[8 * s2 + 2 * q2], acc[8 * s2 + 2 * q2 + 1]};
+            ow[q2] = __builtin_bit_cast(unsigned, __builtin_convertvector(pr, bf16x2v));
           }
-          const bf16x8 ov = __builtin_bit_cast(bf16x8, ow);
-          if (valid) *reinterpret_cast<bf16x8*>(zrow + 32 * mi + 16 * s + 8 * h) = ov;   // hperm order
+          dh1t[(((size_t)tile * 2 + s2) * H + 32 * mi + (lv & 31)) * 2 + h] = __builtin_bit_cast(bf16x8, ow);
         }
       }
     }
@@ -420,6 +434,152 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     for (int k = 0; k < wpb; ++k) acc += part[k * LDA + c];
     w3slab[(size_t)blockIdx.x * LDA + c] = acc;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradients dW2 | db2 = dz2^T [h1 | 1] and dW1 = (dh1 * relu'(z1))^T x, K = batch, with
+// NO LDS and no barriers: one workgroup per k-slice, wave w owning output rows 32w .. 32w + 31 of
+// both products and its accumulators (9 + 1 tiles of 32x32 at H = 256: 160 VGPRs) in registers for
+// the whole slice.  Per 32-row tile a wave
+//   * loads its dz2^T / dh1^T fragments — one 16-byte load per K-step, the forward stored them in
+//     the MFMA operand order — and the tile's 32-byte feature rows;
+//   * recomputes h1 = relu(W1k x) for every n-tile on the layer-1 MFMA with the operands swapped
+//     (x as A, the forward's w1p fragment as B), which yields h1^T with the units on the lanes and
+//     the rows in the registers: exactly the B operand of dW2 (K = rows), and, for n-tile w, the
+//     relu'(z1) mask of dh1^T in its own layout;
+//   * transposes x by one MFMA against an identity fragment for dW1's B operand;
+//   * issues 2 MFMAs per output tile (K = 32 rows).
+// The B operand [h1 | 1] never exists in memory (the old path stored h1a, 544 B/row, and read it
+// back with dz2 through LDS-staged transposed reads).  Partial sums of slice s go to slab[s] in the
+// bucket layout (hperm rows and columns, train/fused.py) and wgrad_reduce sums them in a fixed
+// order.
+template <int H>
+__global__ __launch_bounds__(H / 32 * 64, 1) void train_wgrad_kernel(
+    const __bf16* __restrict__ xf, int B, const unsigned char* __restrict__ blob,
+    const bf16x8* __restrict__ dz2t, const bf16x8* __restrict__ dh1t, int tiles_per_slice,
+    float* __restrict__ slab2, float* __restrict__ slab1) {
+  using L = TrainLayout<H>;
+  constexpr int MT = H / 32, LDG = H + 16;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 31, h = lane >> 5;
+  const int ntiles = (B + 31) >> 5;
+  const int t0 = blockIdx.x * tiles_per_slice;
+  const int t1 = min(ntiles, t0 + tiles_per_slice);
+  // the layer-1 fragments (the same for every wave) in LDS, not in 32 VGPRs per wave
+  __shared__ bf16x8 s_w1[MT * 64];
+  const bf16x8* w1p = reinterpret_cast<const bf16x8*>(blob + L::W2B);
+  for (int i = threadIdx.x; i < MT * 64; i += blockDim.x) s_w1[i] = w1p[i];
+  __syncthreads();
+  bf16x8 eye;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) eye[j] = (__bf16)(8 * h + j == col ? 1.f : 0.f);   // B (k = 8h + j, n = col)
+  f32x16 acc2[MT], acc1;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    acc1[e] = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < MT; ++nt) acc2[nt][e] = 0.f;
+  }
+  float db2 = 0.f;                     // sum of this lane's dz2 values (unit 32w + col)
+  f32x16 zero;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) zero[e] = 0.f;
+  typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+  auto pack = [](const f32x16& v, int s, bool relu) {
+    u32x4v o;
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2) {
+      float x0 = v[8 * s + 2 * q2], x1 = v[8 * s + 2 * q2 + 1];
+      if (relu) {
+        x0 = relu_f(x0);
+        x1 = relu_f(x1);
+      }
+      const f32x2 pr = {x0, x1};
+      o[q2] = __builtin_bit_cast(unsigned, __builtin_convertvector(pr, bf16x2v));
+    }
+    return __builtin_bit_cast(bf16x8, o);
+  };
+  // fragments of one 32-row tile: x (A of the layer-1 / identity MFMAs), dz2^T and dh1^T (A of
+  // the two products, one 16-byte load per K-step); the next tile's are in flight while this one
+  // computes (the loads are the only latency in the loop)
+  struct Frags {
+    bf16x8 x, a0, a1, g0, g1;
+  };
+  // buffer loads: 32-bit offsets against wave-uniform descriptors (no 64-bit address per load, which
+  // left the kernel short of VGPRs), and the hardware range check zero-fills the rows past B
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)xf, 0, B * 32, 0x00020000);
+  const int tb = ntiles * 32 * H * 2;                  // bytes of dz2t / dh1t
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)dz2t, 0, tb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)dh1t, 0, tb, 0x00020000);
+  auto load = [&](int tile) {
+    Frags f;
+    f.x = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, (tile * 32 + col) * 32 + 16 * h, 0, 0));
+    const int c0 = ((tile * 2 * H + 32 * w + col) * 2 + h) * 16, c1 = c0 + H * 2 * 16;
+    f.a0 = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, c0, 0, 0));
+    f.a1 = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, c1, 0, 0));
+    f.g0 = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rg, c0, 0, 0));
+    f.g1 = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rg, c1, 0, 0));
+    return f;
+  };
+  Frags cur;
+  if (t0 < t1) cur = load(t0);
+  for (int tile = t0; tile < t1; ++tile) {
+    Frags nxt = cur;
+    if (tile + 1 < t1) nxt = load(tile + 1);
+    // db2 = sum over rows of dz2 (VALU on the A fragments; no MFMA tile for one column)
+    {
+      const u32x4v p0 = __builtin_bit_cast(u32x4v, cur.a0), p1 = __builtin_bit_cast(u32x4v, cur.a1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        db2 += __uint_as_float(p0[q] << 16) + __uint_as_float(p0[q] & 0xFFFF0000u);
+        db2 += __uint_as_float(p1[q] << 16) + __uint_as_float(p1[q] & 0xFFFF0000u);
+      }
+    }
+    bf16x8 g0 = cur.g0, g1 = cur.g1;
+#pragma unroll
+    for (int nt = 0; nt < MT; ++nt) {
+      const f32x16 hz = mfma32(cur.x, s_w1[nt * 64 + lane], zero);   // h1^T pre-activation, units 32nt + col
+      acc2[nt] = mfma32(cur.a0, pack(hz, 0, true), acc2[nt]);
+      acc2[nt] = mfma32(cur.a1, pack(hz, 1, true), acc2[nt]);
+      if (nt == w) {                                    // relu'(z1) for this wave's dW1 rows
+        u32x4v m0 = __builtin_bit_cast(u32x4v, g0), m1 = __builtin_bit_cast(u32x4v, g1);
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+          const unsigned k0 = (hz[2 * q2] > 0.f ? 0xFFFFu : 0u) | (hz[2 * q2 + 1] > 0.f ? 0xFFFF0000u : 0u);
+          const unsigned k1 = (hz[8 + 2 * q2] > 0.f ? 0xFFFFu : 0u) | (hz[8 + 2 * q2 + 1] > 0.f ? 0xFFFF0000u : 0u);
+          m0[q2] &= k0;
+          m1[q2] &= k1;
+        }
+        g0 = __builtin_bit_cast(bf16x8, m0);
+        g1 = __builtin_bit_cast(bf16x8, m1);
+      }
+    }
+    // x^T: D[row][f] with the feature on the lane and the rows in the registers
+    const f32x16 xt = mfma32(cur.x, eye, zero);
+    acc1 = mfma32(g0, pack(xt, 0, false), acc1);
+    acc1 = mfma32(g1, pack(xt, 1, false), acc1);
+    cur = nxt;
+  }
+  // D[m][n]: lane -> n = col, register e -> m = (e&3) + 8(e>>2) + 4h; rows / columns to the bucket's
+  // hperm order (the stored unit order of every other gradient path)
+  float* o2 = slab2 + (size_t)blockIdx.x * H * LDG;
+  float* o1 = slab1 + (size_t)blockIdx.x * H * 16;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int m = 32 * w + (e & 3) + 8 * (e >> 2) + 4 * h;
+    const int mr = hperm(m);
+#pragma unroll
+    for (int nt = 0; nt < MT; ++nt) o2[(size_t)mr * LDG + hperm(32 * nt + col)] = acc2[nt][e];
+    if (col < 16) o1[(size_t)mr * 16 + col] = acc1[e];
+  }
+  // db2 column (and the zero columns H+1 .. H+15): both lane halves hold rows of unit 32w + col
+  db2 += __shfl_xor(db2, 32);
+  const int ur = hperm(32 * w + col);
+  if (h == 0) o2[(size_t)ur * LDG + H] = db2;
+  else
+#pragma unroll
+    for (int c = 1; c < 16; ++c) o2[(size_t)ur * LDG + H + c] = 0.f;
 }
 
 // Flat parameter layout (fp32 master): W1[H][12] | b1[H] | W2[H][H] | b2[H] | w3[H] | b3
@@ -547,9 +707,9 @@ int train_fwd_grid(int B, int num_cus) {
 
 template <int H>
 static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B, const void* blob,
-                                     const NormParams& np, float gscale, void* xf, void* h1a,
-                                     float* w3slab, void* dz2, void* dz1, void* dyb, float* sq_err,
-                                     int* step_ctr, int num_cus, hipStream_t stream) {
+                                     const NormParams& np, float gscale, void* xf, float* w3slab, void* dz2t,
+                                     void* dh1t, void* dyb, float* sq_err, int* step_ctr, int num_cus,
+                                     hipStream_t stream) {
   using L = TrainLayout<H>;
   constexpr int TPB = TRAIN_TPB;
   // the blob + the waves' dW3 partials [TPB / 64][H + 16] f32 + their dy scratch [TPB / 64][32]
@@ -562,26 +722,65 @@ static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B
     hipError_t e = hipFuncSetAttribute((const void*)eta_mlp3_train_fwd_kernel<H>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
     if (e != hipSuccess) return e;
+    // the kernel addresses its W2 image at absolute LDS address 0: only valid without static LDS
+    hipFuncAttributes fa;
+    e = hipFuncGetAttributes(&fa, (const void*)eta_mlp3_train_fwd_kernel<H>);
+    if (e != hipSuccess) return e;
+    if (fa.sharedSizeBytes != 0) return hipErrorInvalidConfiguration;
     attr_set[dev & 63] = true;
   }
   const int grid = train_fwd_grid(B, num_cus);
   if (grid < 1) return hipSuccess;
   hipLaunchKernelGGL(eta_mlp3_train_fwd_kernel<H>, dim3(grid), dim3(TPB), LDS, stream,
                      (const int4*)rec, target, B, (const unsigned char*)blob, np, gscale,
-                     (__bf16*)xf, (__bf16*)h1a, w3slab, (__bf16*)dz2, (__bf16*)dz1,
-                     (__bf16*)dyb, sq_err, step_ctr);
+                     (__bf16*)xf, w3slab, (bf16x8*)dz2t, (bf16x8*)dh1t, (__bf16*)dyb, sq_err, step_ctr);
   return hipGetLastError();
 }
 
 hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B, const void* blob,
                                      int H, const NormParams& np, float gscale, void* xf,
-                                     void* h1a, float* w3slab, void* dz2, void* dz1, void* dyb,
+                                     float* w3slab, void* dz2t, void* dh1t, void* dyb,
                                      float* sq_err, int* step_ctr, int num_cus,
                                      hipStream_t stream) {
   switch (H) {
-    case 64: return launch_train_fwd_h<64>(rec, target, B, blob, np, gscale, xf, h1a, w3slab, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
-    case 128: return launch_train_fwd_h<128>(rec, target, B, blob, np, gscale, xf, h1a, w3slab, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
-    case 256: return launch_train_fwd_h<256>(rec, target, B, blob, np, gscale, xf, h1a, w3slab, dz2, dz1, dyb, sq_err, step_ctr, num_cus, stream);
+    case 64: return launch_train_fwd_h<64>(rec, target, B, blob, np, gscale, xf, w3slab, dz2t, dh1t, dyb, sq_err, step_ctr, num_cus, stream);
+    case 128: return launch_train_fwd_h<128>(rec, target, B, blob, np, gscale, xf, w3slab, dz2t, dh1t, dyb, sq_err, step_ctr, num_cus, stream);
+    case 256: return launch_train_fwd_h<256>(rec, target, B, blob, np, gscale, xf, w3slab, dz2t, dh1t, dyb, sq_err, step_ctr, num_cus, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// k-slices of train_wgrad_kernel: one workgroup per CU at most (its waves hold ~170 VGPRs of
+// accumulators and fragments), each slice a whole number of 32-row tiles
+int train_wgrad_slices(int B, int num_cus) {
+  static const int min_tiles = [] {
+    const char* v = std::getenv("ROUTEST_TRAIN_WGRAD_TILES");
+    const int t = v ? std::atoi(v) : 4;
+    return t < 1 ? 1 : t;
+  }();
+  const int ntiles = (B + 31) / 32;
+  int S = ntiles / min_tiles;          // >= min_tiles 32-row tiles per slice (the slab write amortised)
+  if (S > num_cus) S = num_cus;
+  return S < 1 ? 1 : S;
+}
+
+template <int H>
+static hipError_t launch_train_wgrad_h(const void* xf, int B, const void* blob, const void* dz2t, const void* dh1t,
+                                       float* slab2, float* slab1, int S, hipStream_t stream) {
+  const int ntiles = (B + 31) / 32;
+  const int tps = (ntiles + S - 1) / S;
+  hipLaunchKernelGGL(train_wgrad_kernel<H>, dim3(S), dim3(H / 32 * 64), 0, stream, (const __bf16*)xf, B,
+                     (const unsigned char*)blob, (const bf16x8*)dz2t, (const bf16x8*)dh1t, tps, slab2, slab1);
+  return hipGetLastError();
+}
+
+hipError_t launch_train_wgrad(const void* xf, int B, const void* blob, int H, const void* dz2t, const void* dh1t,
+                              float* slab2, float* slab1, int S, hipStream_t stream) {
+  if (S < 1) return hipErrorInvalidValue;
+  switch (H) {
+    case 64: return launch_train_wgrad_h<64>(xf, B, blob, dz2t, dh1t, slab2, slab1, S, stream);
+    case 128: return launch_train_wgrad_h<128>(xf, B, blob, dz2t, dh1t, slab2, slab1, S, stream);
+    case 256: return launch_train_wgrad_h<256>(xf, B, blob, dz2t, dh1t, slab2, slab1, S, stream);
     default: return hipErrorInvalidValue;
   }
 }

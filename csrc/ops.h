@@ -25,12 +25,18 @@ hipError_t launch_eta_mlp3_fwd16(const void* rec, float* out, int B, const void*
 hipError_t launch_eta_featurize(const void* rec, float* out, int B, hipStream_t stream);
 
 // ---- ETA MLP training (K3) : eta_mlp_train.hip ----
+// forward + MSE gradient + dgrad; writes xf [B,16], dz2^T and dh1^T in the MFMA operand order
+// ([ceil(B/32)][H][4] x 16 bytes each), dy, squared errors and the dW3 slab
 hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B, const void* blob,
                                      int H, const NormParams& np, float gscale, void* xf,
-                                     void* h1a, float* w3slab, void* dz2, void* dz1, void* dyb,
+                                     float* w3slab, void* dz2t, void* dh1t, void* dyb,
                                      float* sq_err, int* step_ctr, int num_cus,
                                      hipStream_t stream);
 int train_fwd_grid(int B, int num_cus);   // workgroups = rows of the dW3 slab
+// dW2|db2 and dW1 partials per k-slice (slab2 [S][H][H+16], slab1 [S][H][16], bucket order)
+hipError_t launch_train_wgrad(const void* xf, int B, const void* blob, int H, const void* dz2t, const void* dh1t,
+                              float* slab2, float* slab1, int S, hipStream_t stream);
+int train_wgrad_slices(int B, int num_cus);
 size_t eta_mlp3_train_blob_bytes(int H);
 int mlp3_num_params(int H);
 int mlp3_grad_bucket_floats(int H);
@@ -124,6 +130,13 @@ struct AstarWs {
   int* touched = nullptr;
   int slots = 0, cap = 0, tbits = 0;
 };
+// Growth arena of the wave/big tiers: `entries` 16-byte entries, all-ones when idle, and an 8-byte
+// device bump counter (the launcher resets it before every wave launch).
+struct AstarArenaBuf {
+  void* base = nullptr;
+  unsigned long long entries = 0;
+  unsigned long long* ctr = nullptr;
+};
 struct AstarOut {
   float* cost = nullptr;
   int* len = nullptr;
@@ -147,12 +160,13 @@ hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* 
                              const AstarWs& ws, const AstarOut& o, int max_iters, hipStream_t stream);
 hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* dst, int Q, const int* qidx,
                              int q0, int T, const AstarWs& ws, const AstarOut& o, int max_iters, float delta,
-                             hipStream_t stream);
+                             hipStream_t stream, const AstarArenaBuf* arena = nullptr);
 // The tiered search (lane -> wave -> big); any tier pointer may be null.  scratch: Q + 1 device ints.
 // Searches left with status 2/3 are the caller's (host Dijkstra).
 hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, int Q, const AstarWs* lane,
                         const AstarWs* wave, const AstarWs* big, const AstarOut& o, const AstarPlan& pl,
-                        int* scratch, hipStream_t stream, AstarRunStats* st);
+                        int* scratch, hipStream_t stream, AstarRunStats* st,
+                        const AstarArenaBuf* arena = nullptr);
 
 // ---- tree ensemble (K4) : forest.hip ----
 hipError_t launch_forest(const void* rec, const float* values, const unsigned* info, const int* roots,

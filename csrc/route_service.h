@@ -41,6 +41,7 @@ struct RouteServiceCfg {
   const float* lm = nullptr;
   int K = 0;
   AstarWs lane_ws, wave_ws, big_ws;       // the tiers' workspaces (csrc/astar.hip); slots == 0: off
+  AstarArenaBuf arena;                    // growth arena of the wave/big tiers (optional)
   int max_path = 4096, max_iters = 2000000, lane_pops = 500;
   int wave_only_below = 32768;            // fewer unique legs than this: every search in the wave tier
   float inv_vmax = 0.f, wave_delta = 10.f;

@@ -535,7 +535,7 @@ struct RouteService::Impl {
     if (e == hipSuccess)
       e = astar_search(gd, d_src.d, d_dst.d, Q, cfg.lane_ws.slots > 0 ? &cfg.lane_ws : nullptr,
                        cfg.wave_ws.slots > 0 ? &cfg.wave_ws : nullptr, cfg.big_ws.slots > 0 ? &cfg.big_ws : nullptr,
-                       ao, pl, d_qidx.d, stream, &rs);
+                       ao, pl, d_qidx.d, stream, &rs, cfg.arena.base ? &cfg.arena : nullptr);
     n_escalated.fetch_add(rs.escalated, std::memory_order_relaxed);
     if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);

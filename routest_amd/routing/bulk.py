@@ -68,10 +68,10 @@ class BulkRouteStep:
         self.requests = requests
         # every leg of a step in ONE lane-tier launch (~80k concurrent searches on one GPU) and the
         # searches left after the pop budget in one or a few wave-tier launches, so each CU keeps
-        # several waves of searches in flight (sparse per-search tables: ~19 GB + 35 GB of HBM3E)
+        # several waves of searches in flight (sparse per-search tables: ~33 GB of HBM3E in all)
         legs_est = int(sum(len(s) for s in snapped) * 1.4) + 1024
         slots = min(legs_est, max_slots)
-        self.astar = astar or BatchedAstar(g, cost, d, slots=slots, wave_slots=min(slots, 49152))
+        self.astar = astar or BatchedAstar(g, cost, d, slots=slots, wave_slots=min(slots, 32768), arena_gb=16)
 
     def legs(self):
         """K5 + K6 for every request, then the trip legs as (src, dst) node tensors on the device."""

@@ -200,17 +200,19 @@ class BatchedAstar:
     """GPU batched A* (csrc/astar.hip): three tiers of sparse per-search state.
 
     * lane tier — ``slots`` searches, one lane each, ``lane_pops`` heap pops in small tables;
-    * wave tier — ``wave_slots`` searches, one 64-lane wave each, tables of ``2 * cap`` entries
-      (a search may touch ``cap`` nodes);
+    * wave tier — ``wave_slots`` searches, one 64-lane wave each, tables of 2**13 entries that grow
+      2x at a time into a shared arena (``arena_gb`` / ``ROUTEST_ASTAR_ARENA_GB``, default 4); ``cap`` bounds the
+      f-band lists of a search;
     * big tier — ``big_slots`` searches with tables of >= 2N entries for what overflowed the wave tier.
 
-    Workspace is ``slots x ~176 KB + wave_slots x 44 cap + big_slots x (16-48 MB)`` — independent of
-    the graph size up to the big tier (the round-2 kernel kept a dense [slots, N] state)."""
+    Workspace is ``slots x ~176 KB + wave_slots x (128 KB + 8 cap) + arena + big_slots x (5-40 MB)``
+    — independent of the graph size up to the big tier (the round-2 kernel kept a dense [slots, N]
+    state)."""
 
     def __init__(self, g: RoadGraph, cost: np.ndarray, device, slots: int = 16384, cap: int = 16384,
                  max_path: int = 4096, max_iters: int = 2_000_000, landmarks: int = 32,
                  landmark_method: str = "farthest", wave_slots: Optional[int] = None,
-                 big_slots: Optional[int] = None):
+                 big_slots: Optional[int] = None, arena_gb: Optional[float] = None):
         from ..ops import _ext
         self.C = _ext.native(required=True)
         self.g = g
@@ -248,22 +250,37 @@ class BatchedAstar:
             wave_slots = int(os.environ.get("ROUTEST_ASTAR_WAVE_SLOTS", "16384"))
         self.wave_slots = max(1, min(slots, int(wave_slots)))
         N = g.num_nodes
+        big_tbits = min(24, max(_pow2_bits(2 * max(128, (int(cap) + 7) // 8 * 8)) + 1, _pow2_bits(2 * N)))
+        big_cap = max(int(cap), min(1 << 20, 1 << _pow2_bits(N // 2)))
         if big_slots is None:
-            big_slots = int(os.environ.get("ROUTEST_ASTAR_BIG_SLOTS", "64"))
-        # tiers: cap rounded to a multiple of 8, tables twice the touch capacity
+            # as many big-tier searches as ~4 GiB of tables hold (1M nodes: ~100), at most 128
+            per = AstarTier.bytes_per_slot(big_cap, big_tbits)
+            big_slots = int(os.environ.get("ROUTEST_ASTAR_BIG_SLOTS", str(max(16, min(128, (4 << 30) // per)))))
+        # tiers: cap (the wave tier's near/far lists per search) rounded to a multiple of 8; wave
+        # tables start at 2**wave_tbits entries and grow 2x at a time into a shared arena, so their
+        # memory follows the searches instead of a fixed worst case per slot
         cap = max(128, (int(cap) + 7) // 8 * 8)
-        wave_tbits = _pow2_bits(2 * cap)
+        wave_tbits = min(int(os.environ.get("ROUTEST_ASTAR_WAVE_TBITS", "13")), _pow2_bits(2 * cap))
         if self.lane_pops > 0:
-            lane_tbits = min(wave_tbits, max(8, _pow2_bits(16 * self.lane_pops)))
+            lane_tbits = max(8, _pow2_bits(8 * self.lane_pops))
             lane_cap = max(64, 1 << (lane_tbits - 1))
             self.lane_tier = AstarTier(slots, lane_cap, lane_tbits, d)
             self.wave_tier = AstarTier(self.wave_slots, cap, wave_tbits, d)
         else:
-            self.lane_tier = AstarTier(slots, cap, wave_tbits, d)
+            self.lane_tier = AstarTier(slots, cap, _pow2_bits(2 * cap), d)
             self.wave_tier = None
-        big_tbits = min(24, max(wave_tbits + 1, _pow2_bits(2 * N)))
-        self.big_tier = (AstarTier(big_slots, max(cap, min(1 << 20, 1 << _pow2_bits(N // 2))), big_tbits, d)
-                         if big_slots > 0 else None)
+        if arena_gb is None:
+            arena_gb = float(os.environ.get("ROUTEST_ASTAR_ARENA_GB", "4"))
+        self.arena = (torch.full((int(arena_gb * (1 << 30)) // 16 * 2,), -1, dtype=torch.int64, device=d)
+                      if arena_gb > 0 else None)
+        self.arena_ctr = torch.zeros(1, dtype=torch.int64, device=d)
+        big_tbits = min(24, max(_pow2_bits(2 * cap) + 1, _pow2_bits(2 * N)))
+        big_cap = max(cap, min(1 << 20, 1 << _pow2_bits(N // 2)))
+        if big_slots is None:
+            # as many big-tier searches as ~4 GiB of tables hold (1M nodes: ~100), at most 128
+            per = AstarTier.bytes_per_slot(big_cap, big_tbits)
+            big_slots = int(os.environ.get("ROUTEST_ASTAR_BIG_SLOTS", str(max(16, min(128, (4 << 30) // per)))))
+        self.big_tier = AstarTier(big_slots, big_cap, big_tbits, d) if big_slots > 0 else None
         self.scratch = torch.empty(1, dtype=torch.int32, device=d)
         self.last_stats = {}
         # tightest admissible + consistent heuristic: every edge length is 1.15 x its great-circle
@@ -280,7 +297,8 @@ class BatchedAstar:
     @property
     def workspace_bytes(self) -> int:
         """Device bytes of the search workspace (all tiers; graph and landmark tables excluded)."""
-        return sum(t.nbytes for t in (self.lane_tier, self.wave_tier, self.big_tier) if t is not None)
+        return (sum(t.nbytes for t in (self.lane_tier, self.wave_tier, self.big_tier) if t is not None)
+                + (self.arena.numel() * 8 if self.arena is not None else 0))
 
     def _nodes(self, a: np.ndarray) -> np.ndarray:
         return np.ascontiguousarray(a[self.perm]) if self.perm is not None else a
@@ -329,7 +347,7 @@ class BatchedAstar:
                                  s, t, self.lane_tier.ws(), self.wave_tier.ws() if self.wave_tier else None,
                                  self.big_tier.ws() if self.big_tier else None, out_cost, out_len, out_status,
                                  out_path, self.last_iters, self.scratch, self.max_iters, self.lane_pops,
-                                 self.wave_only_below, self.wave_delta)
+                                 self.wave_only_below, self.wave_delta, self.arena, self.arena_ctr)
         self.last_stats = dict(zip(("lane", "wave", "escalated", "lane_ms", "wave_ms", "big_ms"), st))
         self.last_tail = int(st[1])
         self.last_escalated = int(st[2])

@@ -117,6 +117,7 @@ def route_config(provider, device, *, engine: str = "backend:mi355x", compat200:
             "lm": a.lm, "K": (a.lm.shape[1] // 2) if a.lm is not None else 0,
             "lane_ws": a.lane_tier.ws(), "wave_ws": a.wave_tier.ws() if a.wave_tier else None,
             "big_ws": a.big_tier.ws() if a.big_tier else None,
+            "arena": a.arena, "arena_ctr": a.arena_ctr if a.arena is not None else None,
             "N": int(g.num_nodes), "snap_c": float(g.SNAP_C),
             "max_path": int(a.max_path), "max_iters": int(a.max_iters), "lane_pops": int(a.lane_pops),
             "wave_only_below": int(a.wave_only_below),

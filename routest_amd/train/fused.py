@@ -3,14 +3,15 @@
 Per step (all on the current HIP stream, no host synchronisation, HIP-graph capturable):
 
   eta_mlp3_train_fwd (HIP)  : featurize + 3 layers + MSE grad + the input-gradient path
-                            dz2 -> dh1 = dz2 W2 (MFMA on the transposed LDS image of W2) ->
-                            dz1 = dh1 * relu'(z1) (h1 still in registers); writes xf, h1a,
-                            dz2, dz1, dy (activations in the hperm() unit order: 16-byte stores)
-                            and G[w3|b3] = dy^T [h2|1] as one fp32 row per workgroup: relu(z2)
-                            stays in registers, reduce-scattered over the rows (ds_swizzle)
-  G[W2|b2] = dz2^T [h1|1]   : split-K wgrad HIP kernel (K = batch) -> fp32 slabs laid out like
-  G[W1k|b1] = dz1^T [xf]      the flat bucket (xf slot 14 == 1), then ONE deterministic reduction
-                            of the three slab regions into G
+                            dh1 = dz2 W2 (MFMA on the transposed LDS image of W2); writes xf,
+                            dy, and dz2^T / dh1^T in the MFMA operand order of the weight-gradient
+                            kernel, plus G[w3|b3] = dy^T [h2|1] as one fp32 row per workgroup
+                            (relu(z2) never leaves the registers)
+  G[W2|b2], G[W1k|b1]       : train_wgrad (HIP, K = batch, no LDS): each wave holds its rows of
+                            dW2|db2 and dW1 in registers over a k-slice, recomputing [h1|1] from
+                            xf on the layer-1 MFMA (h1 is never stored) and applying relu'(z1) to
+                            dh1^T there; fp32 slabs in the bucket layout, then ONE deterministic
+                            reduction of the three slab regions into G
   all_reduce(G)             : ONE RCCL collective (SUM; dy was pre-scaled by 2/global_batch)
   adamw_pack (HIP)          : AdamW on fp32 master params + re-pack of the training blob
 No library GEMM runs in the step (csrc/eta_mlp_train.hip).
@@ -166,28 +167,20 @@ class FusedMlp3Trainer:
         d, H, bf = self.dev, self.H, torch.bfloat16
         self.blob = torch.zeros(self.C.eta_mlp3_train_blob_bytes(H), dtype=torch.uint8, device=d)
         self.xf = torch.empty(B, 16, dtype=bf, device=d)
-        self.h1a = torch.empty(B, H + 16, dtype=bf, device=d)
-        self.dz2 = torch.empty(B, H, dtype=bf, device=d)
+        # dz2^T and dh1^T in the MFMA operand order of train_wgrad_kernel (per 32-row tile and unit,
+        # 32 rows in the k order): nothing else of the activations leaves the forward kernel
+        tiles = (B + 31) // 32
+        self.dz2t = torch.empty(tiles * 32 * H, dtype=bf, device=d)
+        self.dh1t = torch.empty(tiles * 32 * H, dtype=bf, device=d)
         self.dyb = torch.empty(B, 8, dtype=bf, device=d)
-        # dW2|db2 (the big block): nsplit column blocks per k-slice, so each slice covers nsplit x
-        # more batch rows for the same ~one-workgroup-per-CU grid -> nsplit x fewer fp32 slabs.
-        # dW3|db3 and dW1 (small outputs, operands as big as dW2's) keep one slice per CU.
         ldg = H + 16
-        self.nsplit = int(os.environ.get("ROUTEST_WGRAD_NSPLIT", "3"))
-        self.dual = os.environ.get("ROUTEST_WGRAD_DUAL", "1") != "0"
-        self.S = self._slices(B)
-        ntt = (ldg + 31) // 32
-        nt = -(-ntt // max(1, self.nsplit))
-        nblk = -(-ntt // nt)                       # n-blocks the kernel actually launches
-        # the nblk workgroups of a slice share its dz2 rows through one XCD's L2 when S2 % 8 == 0
-        self.S2 = max(1, (self.S // nblk) // 8 * 8 or self.S // nblk)
-        self.slab2 = torch.empty(self.S2, H * ldg, dtype=torch.float32, device=d)
-        # dW1 slabs; dW3|db3 arrives as one row per forward workgroup (w3slab): relu(z2) never
-        # leaves the forward kernel's registers
+        # k-slices of the weight-gradient kernel (one workgroup per CU at most): dW2|db2 and dW1
+        # partials per slice; dW3|db3 arrives as one row per forward workgroup (w3slab)
+        self.S = self.C.train_wgrad_slices(B, d.index or 0)
+        self.slab2 = torch.empty(self.S, H * ldg, dtype=torch.float32, device=d)
         self.slab = torch.empty(self.S, H * 16, dtype=torch.float32, device=d)
         self.w3slab = torch.empty(self.C.train_fwd_grid(B, d.index or 0), ldg, dtype=torch.float32,
                                   device=d)
-        self.dz1 = torch.empty(B, H, dtype=bf, device=d)
         self.sq_err = torch.zeros(B, dtype=torch.float32, device=d)      # per-row squared errors
         self.loss_tiles = self.sq_err                                      # (older name)
 
@@ -204,17 +197,9 @@ class FusedMlp3Trainer:
         """Fills the flat gradient bucket G (local contribution, pre-scaled for the global mean)."""
         C, H = self.C, self.H
         C.eta_mlp3_train_fwd(rec, tgt_norm, self.blob, H, self.norm, 2.0 / self.global_batch,
-                             self.xf, self.h1a, self.w3slab, self.dz2, self.dz1, self.dyb,
-                             self.sq_err, self.step_ctr)
+                             self.xf, self.w3slab, self.dz2t, self.dh1t, self.dyb, self.sq_err, self.step_ctr)
         ldg = H + 16
-        if self.dual:
-            # dW2|db2 and dW1 = dz1^T x in ONE launch: the two grids share the chip
-            C.wgrad_dual(self.dz2, H, self.h1a, ldg, self.slab2, ldg, self.nsplit,
-                         self.dz1, H, self.xf, 16, self.slab, 16)
-        else:
-            C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit)
-            # dW1 = dz1^T x (relu'(z1) applied by the forward kernel)
-            C.wgrad(self.dz1, H, H, self.xf, 16, self.slab, 0, 16)
+        C.train_wgrad(self.xf, rec.shape[0], self.blob, H, self.dz2t, self.dh1t, self.slab2, self.slab)
         C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg + ldg:],
                        self.w3slab, self.G[H * ldg:H * ldg + ldg])
 

@@ -86,13 +86,26 @@ def test_wave_tail_stage_exact(graph_and_cost, monkeypatch, lane_pops, delta):
     assert np.array_equal(c, c2)
 
 
-def test_overflowed_searches_escalate_to_the_big_tier(graph_and_cost):
-    """With wave-tier tables far too small (cap 128: a search may touch 128 nodes) most searches
-    overflow (status 2) and are rerun in the big tier, whose tables hold every node — still on the
-    GPU, at the optimal cost."""
+def test_small_lists_grow_into_the_arena(graph_and_cost):
+    """cap 128 (64-entry f-band lists, 256-entry tables): the wave tier moves its lists and tables
+    into arena buffers as the searches grow, so nothing overflows to the big tier or the host."""
     g, cost, _ = graph_and_cost
     src, dst = synth_route_queries(g, 300, seed=3)
     a = BatchedAstar(g, cost, "cuda:0", slots=512, cap=128)
+    c, n, st, p = a.run(src, dst)
+    assert a.last_escalated == 0 and a.last_fallbacks == 0, a.last_stats
+    assert (st.cpu().numpy() == 0).all()
+    np.testing.assert_allclose(c.cpu().numpy(), dijkstra_ref(g, cost, src, dst), rtol=1e-4)
+    assert bool((a.arena == -1).all())                   # lists and tables restored to all-ones
+
+
+def test_overflowed_searches_escalate_to_the_big_tier(graph_and_cost):
+    """Without the arena, wave-tier lists far too small (cap 128) overflow (status 2) and the
+    searches are rerun in the big tier, whose tables hold every node — still on the GPU, at the
+    optimal cost."""
+    g, cost, _ = graph_and_cost
+    src, dst = synth_route_queries(g, 300, seed=3)
+    a = BatchedAstar(g, cost, "cuda:0", slots=512, cap=128, arena_gb=0)
     c, n, st, p = a.run(src, dst)
     assert a.last_escalated > 100 and a.last_fallbacks == 0, a.last_stats
     c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
@@ -105,10 +118,11 @@ def test_overflowed_searches_escalate_to_the_big_tier(graph_and_cost):
 
 
 def test_overflowed_searches_finish_exactly_on_host(graph_and_cost):
-    """Without a big tier the overflowed searches are finished by the exact host fallback."""
+    """Without an arena or a big tier the overflowed searches are finished by the exact host
+    fallback."""
     g, cost, _ = graph_and_cost
     src, dst = synth_route_queries(g, 300, seed=3)
-    a = BatchedAstar(g, cost, "cuda:0", slots=512, cap=128, big_slots=0)
+    a = BatchedAstar(g, cost, "cuda:0", slots=512, cap=128, big_slots=0, arena_gb=0)
     c, n, st, p = a.run(src, dst)
     assert a.last_fallbacks > 0
     c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
@@ -132,6 +146,35 @@ def test_lane_tier_overflow_continues_in_the_wave_tier(graph_and_cost, monkeypat
     st = st.cpu().numpy()
     assert (st == 0).all()
     np.testing.assert_allclose(c.cpu().numpy(), dijkstra_ref(g, cost, src, dst), rtol=1e-4)
+
+
+def test_wave_tables_grow_into_the_arena_exactly(graph_and_cost, monkeypatch):
+    """Wave-tier tables that start at 64 entries grow 4x at a time into the shared arena (parent
+    pointers rewritten at every rehash): every search still finishes on the GPU at the optimal cost,
+    and the arena is restored (a second run gives identical answers)."""
+    g, cost, _ = graph_and_cost
+    src, dst = synth_route_queries(g, 800, seed=6)
+    monkeypatch.setenv("ROUTEST_ASTAR_WAVE_TBITS", "6")
+    a = BatchedAstar(g, cost, "cuda:0", slots=1024)
+    assert a.wave_tier.tbits == 6
+    c, n, st, p = a.run(src, dst)
+    assert a.last_escalated == 0 and a.last_fallbacks == 0, a.last_stats
+    c, n, st, p = c.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy(), p.cpu().numpy()
+    assert (st == 0).all()
+    np.testing.assert_allclose(c, dijkstra_ref(g, cost, src, dst), rtol=1e-4, atol=1e-3)
+    for i in range(0, len(src), 41):
+        path = p[i, :n[i]]
+        assert path[0] == src[i] and path[-1] == dst[i]
+        tot = 0.0
+        for u, v in zip(path[:-1], path[1:]):
+            nb = g.indices[g.indptr[u]:g.indptr[u + 1]]
+            k = np.where(nb == v)[0]
+            assert len(k) == 1
+            tot += cost[g.indptr[u] + k[0]]
+        assert abs(tot - c[i]) <= 1e-3 * max(1.0, c[i])
+    assert bool((a.arena == -1).all())                   # every grown table restored to all-ones
+    c2 = a.run(src, dst)[0].cpu().numpy()
+    assert np.array_equal(c, c2)
 
 
 def test_workspace_is_independent_of_graph_size(graph_and_cost):
