@@ -439,8 +439,7 @@ void check_bf16(const torch::Tensor& t, const char* name, int64_t rows, int64_t 
 // Writes every output in place (static buffers: the step is HIP-graph capturable).
 void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tensor blob, int64_t H,
                         std::vector<double> norm, double gscale, torch::Tensor xf, torch::Tensor w3slab,
-                        torch::Tensor dz2t, torch::Tensor dh1t, torch::Tensor dyb, torch::Tensor sq_err,
-                        torch::Tensor step_ctr) {
+                        torch::Tensor dz2r, torch::Tensor sq_err, torch::Tensor step_ctr) {
   check_dev(records, "records");
   check_dev(target, "target");
   check_dev(blob, "blob");
@@ -451,19 +450,16 @@ void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tens
   TORCH_CHECK(H == 64 || H == 128 || H == 256, "fused trainer: H in (64, 128, 256)");
   TORCH_CHECK(blob.scalar_type() == torch::kUInt8 &&
               (size_t)blob.numel() == rt::eta_mlp3_train_blob_bytes((int)H), "bad training blob");
-  check_bf16(xf, "xf", B, 16);
+  const int64_t tiles = (B + 31) / 32;
+  check_bf16(xf, "xf", tiles * 32, 16);
   check_dev(w3slab, "w3slab");
   const int grid = rt::train_fwd_grid((int)B, num_cus(records.device().index()));
   TORCH_CHECK(w3slab.scalar_type() == torch::kFloat32 && w3slab.is_contiguous() && w3slab.dim() == 2 &&
                   w3slab.size(0) == grid && w3slab.size(1) == H + 16,
               "w3slab must be f32 [train_fwd_grid(B), H + 16] = [", grid, ", ", H + 16, "]");
-  const int64_t tiles = (B + 31) / 32;
-  for (auto* t : {&dz2t, &dh1t}) {
-    check_dev(*t, "dz2t/dh1t");
-    TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->is_contiguous() && t->numel() == tiles * 32 * H,
-                "dz2t / dh1t must be bf16 with ceil(B/32) * 32 * H elements");
-  }
-  check_bf16(dyb, "dyb", B, 8);
+  check_dev(dz2r, "dz2r");
+  TORCH_CHECK(dz2r.scalar_type() == torch::kBFloat16 && dz2r.is_contiguous() && dz2r.numel() == tiles * 32 * H,
+              "dz2r must be bf16 with ceil(B/32) * 32 * H elements");
   check_dev(sq_err, "sq_err");
   TORCH_CHECK(sq_err.scalar_type() == torch::kFloat32 && sq_err.numel() >= B, "sq_err must be f32 [B]");
   check_dev(step_ctr, "step_ctr");
@@ -471,32 +467,31 @@ void eta_mlp3_train_fwd(torch::Tensor records, torch::Tensor target, torch::Tens
   const c10::DeviceGuard guard(records.device());
   RT_CHECK_HIP(rt::launch_eta_mlp3_train_fwd(
       records.data_ptr(), target.data_ptr<float>(), (int)B, blob.data_ptr(), (int)H,
-      norm_from(norm), (float)gscale, xf.data_ptr(), w3slab.data_ptr<float>(), dz2t.data_ptr(), dh1t.data_ptr(),
-      dyb.data_ptr(), sq_err.data_ptr<float>(), step_ctr.data_ptr<int>(), num_cus(records.device().index()),
+      norm_from(norm), (float)gscale, xf.data_ptr(), w3slab.data_ptr<float>(), dz2r.data_ptr(),
+      sq_err.data_ptr<float>(), step_ctr.data_ptr<int>(), num_cus(records.device().index()),
       cur_stream(records)));
 }
 
-// dW2|db2 and dW1 partial sums per k-slice from the forward's dz2^T / dh1^T (train_wgrad_kernel)
-void train_wgrad(torch::Tensor xf, int64_t B, torch::Tensor blob, int64_t H, torch::Tensor dz2t, torch::Tensor dh1t,
-                 torch::Tensor slab2, torch::Tensor slab1) {
-  for (auto* t : {&xf, &blob, &dz2t, &dh1t, &slab2, &slab1}) check_dev(*t, "train_wgrad tensor");
+// dgrad + relu'(z1) + dW2|db2 and dW1 partial sums per k-slice from the forward's dz2 fragments
+// (train_bwd_kernel)
+void train_bwd(torch::Tensor xf, int64_t B, torch::Tensor blob, int64_t H, torch::Tensor dz2r,
+               torch::Tensor slab2, torch::Tensor slab1) {
+  for (auto* t : {&xf, &blob, &dz2r, &slab2, &slab1}) check_dev(*t, "train_bwd tensor");
   TORCH_CHECK(H == 64 || H == 128 || H == 256, "H in (64, 128, 256)");
-  check_bf16(xf, "xf", B, 16);
   const int64_t tiles = (B + 31) / 32;
-  TORCH_CHECK(dz2t.numel() == tiles * 32 * H && dh1t.numel() == tiles * 32 * H &&
-                  dz2t.scalar_type() == torch::kBFloat16 && dh1t.scalar_type() == torch::kBFloat16,
-              "dz2t / dh1t shapes");
+  check_bf16(xf, "xf", tiles * 32, 16);
+  TORCH_CHECK(dz2r.numel() == tiles * 32 * H && dz2r.scalar_type() == torch::kBFloat16 && dz2r.is_contiguous(),
+              "dz2r shape");
   TORCH_CHECK(blob.scalar_type() == torch::kUInt8 && (size_t)blob.numel() == rt::eta_mlp3_train_blob_bytes((int)H),
               "bad training blob");
   const int64_t S = slab2.size(0);
   TORCH_CHECK(slab2.scalar_type() == torch::kFloat32 && slab2.dim() == 2 && slab2.size(1) == H * (H + 16) &&
                   slab1.scalar_type() == torch::kFloat32 && slab1.dim() == 2 && slab1.size(0) == S &&
-                  slab1.size(1) == H * 16 && S >= 1,
-              "slab2 f32 [S, H*(H+16)], slab1 f32 [S, H*16]");
+                  slab1.size(1) == H * 16 && S >= 1 && S <= tiles,
+              "slab2 f32 [S, H*(H+16)], slab1 f32 [S, H*16], 1 <= S <= ceil(B/32)");
   const c10::DeviceGuard guard(xf.device());
-  RT_CHECK_HIP(rt::launch_train_wgrad(xf.data_ptr(), (int)B, blob.data_ptr(), (int)H, dz2t.data_ptr(),
-                                      dh1t.data_ptr(), slab2.data_ptr<float>(), slab1.data_ptr<float>(), (int)S,
-                                      cur_stream(xf)));
+  RT_CHECK_HIP(rt::launch_train_bwd(xf.data_ptr(), (int)B, blob.data_ptr(), (int)H, dz2r.data_ptr(),
+                                    slab2.data_ptr<float>(), slab1.data_ptr<float>(), (int)S, cur_stream(xf)));
 }
 
 void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor V,
@@ -1178,8 +1173,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw_pack_big", &adamw_pack_big, "wide trainer: AdamW + re-pack of w1p / w2k / w2t / b2 / w3 / b3");
   m.def("big_dz2y", &big_dz2y, "wide trainer: dy, dyb, squared error, dz2 and the step counter in one launch");
   m.def("big_dz2", &big_dz2, "dz2 = dy * w3 * relu'(z2) from h2a (hperm order)");
-  m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward + MSE grad + input-gradient path (dz2^T, dh1^T)");
-  m.def("train_wgrad", &train_wgrad, "K3: dW2|db2 and dW1 split-K partials, register-resident (train_wgrad_kernel)");
+  m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward (one pass over layer 2) + MSE grad + dW3 partial -> dz2 fragments");
+  m.def("train_bwd", &train_bwd, "K3: dgrad + relu'(z1) + dW2|db2 and dW1 split-K partials in one kernel (train_bwd_kernel)");
   m.def("train_wgrad_slices", [](int64_t B, int64_t device) { return (int64_t)rt::train_wgrad_slices((int)B, num_cus((int)device)); });
   m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + training-blob re-pack");
   m.def("eta_mlp3_train_blob_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_train_blob_bytes((int)H); });

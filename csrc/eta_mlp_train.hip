@@ -62,10 +62,25 @@ struct TrainLayout {
   static constexpr size_t W2B = (size_t)H * ROWB;
   static constexpr size_t W1B = (size_t)H * 16 * 2;
   static constexpr size_t VB = (size_t)H * 4;
-  static constexpr size_t BLOB = W2B + W1B + 3 * VB + 16;
+  static constexpr size_t BLOB = W2B + W1B + 3 * VB + 16;   // what the forward stages into LDS
+  static constexpr size_t W2F = (size_t)H * H * 2;             // + train_bwd_kernel's W2 B fragments
 };
 
-size_t eta_mlp3_train_blob_bytes(int H) { return (size_t)H * 512 + 44 * (size_t)H + 16; }
+size_t eta_mlp3_train_blob_bytes(int H) { return (size_t)H * 512 + 44 * (size_t)H + 16 + (size_t)H * H * 2; }
+
+// W2 B-fragment image of train_bwd_kernel (past the forward's blob): fragment (nb, ks), lane
+// (n, h), element j = W2[u2][u1] with u1 = 32nb + n and u2 = 16ks + 8(j>>2) + 4h + (j&3) — the k
+// order of the forward's dz2 fragments.  Returns the bf16 index.
+// XOR swizzle of the 16-byte chunks of row r in the dz2 tile image (512-byte rows at H = 256):
+// 16 consecutive rows' chunk c land on 16 different bank groups (row reads) and the 4 rows x 64 bytes
+// of a transposed read's 32-lane half on 16 different ones (cdna_hip_programming.md T10 (b))
+__host__ __device__ __forceinline__ int dz2swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+__host__ __device__ __forceinline__ size_t w2frag_index(int u2, int u1, int KS) {
+  const int nb = u1 >> 5, n = u1 & 31, ks = u2 >> 4, r = u2 & 15;
+  const int hh = (r >> 2) & 1, j = 4 * (r >> 3) + (r & 3);
+  return (((size_t)nb * KS + ks) * 64 + n + 32 * hh) * 8 + j;
+}
 
 __host__ __device__ __forceinline__ int w2swz(int row) { return ((row & 3) << 3) | ((row >> 2) & 7); }
 // byte offset of W2[row][col] in the image (natural order both ways; 8-byte chunks swizzled)
@@ -89,8 +104,8 @@ template <int H>
 __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     const int4* __restrict__ rec, const float* __restrict__ target, int B,
     const unsigned char* __restrict__ blob, NormParams np, float gscale, __bf16* __restrict__ xf,
-    float* __restrict__ w3slab, bf16x8* __restrict__ dz2t, bf16x8* __restrict__ dh1t,
-    __bf16* __restrict__ dyb, float* __restrict__ sq_err, int* __restrict__ step_ctr) {
+    float* __restrict__ w3slab, bf16x8* __restrict__ dz2r, float* __restrict__ sq_err,
+    int* __restrict__ step_ctr) {
   using L = TrainLayout<H>;
   constexpr int MT = H / 32, KS = H / 16, LDA = H + 16, D = KS < 4 ? KS : 4;
   // device-side optimizer step counter (read by adamw_pack_kernel later on the same stream), so a
@@ -107,7 +122,6 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
   const bf16x8* w1p = reinterpret_cast<const bf16x8*>(smem + L::W2B);
   const f32x4* b2p = reinterpret_cast<const f32x4*>(smem + L::W2B + L::W1B) + H / 4;
   const f32x4* w3p = b2p + H / 4;
-  const float b3 = reinterpret_cast<const float*>(w3p + H / 4)[0];
 
   const int lane = threadIdx.x & 63;
   const int wpb = blockDim.x >> 6;
@@ -136,35 +150,16 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     if (valid)  // slots 14, 15 hold 1.0 (the b1 hi/lo inputs): dW1k[:,14] == db1
       *reinterpret_cast<bf16x8*>(xf + (size_t)row * 16 + 8 * h) = xb;
 
-    // layer 1 (A fragments re-read from LDS per tile: no registers held across tiles)
-    bf16x8 h1[KS];
+    // layers 1 and 2 streamed over k: all MT layer-2 accumulators stay live (the MFMAs of one k-step
+    // are MT independent chains), and layer-1 tile m1 is computed right before the two k-steps that
+    // consume it, so only 2 h1 fragments are ever live (the round-2 order held all of h1: 64 VGPRs)
+    f32x16 acc[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      f32x16 acc;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-      acc = mfma32(w1p[mt * 64 + lane], xb, acc);
-      float a[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) a[e] = acc[e];
-      relu_cvt_bf16x8(a, &h1[2 * mt]);
-      relu_cvt_bf16x8(a + 8, &h1[2 * mt + 1]);
-    }
-    // (h1 is not stored: train_wgrad_kernel recomputes it from xf on the same MFMA)
-
-    // layer 2 + layer 3 in TWO passes over the hidden tiles, relu(z2) never stored: pass 1 only
-    // forms y (hence dy); pass 2 recomputes z2 per tile for the relu'(z2) mask and the dW3 | db3
-    // partial.  The second 128 MFMAs per tile cost less than writing h2a (35.6 MB at 64k rows)
-    // and reading it back in a split-K GEMM; keeping relu(z2) in registers instead (64 VGPRs next
-    // to h1's 64) spilled.
-    unsigned long long mask_lo = 0, mask_hi = 0;   // 16 relu'(z2) bits per hidden tile
-    float ys = 0.f;
-    float dy, diff;
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = load_vec16(b2p, mt, h);
     {
-      // addresses as lane bases + immediates (a run-time or fully hoisted w2off() per fragment
-      // costs VGPRs the compiler then spills — and a scratch reload after the activation stores
-      // would wait for all of them, vmcnt being in order): chunk (2ks + h) ^ w2swz(r) only
-      // depends on ks & 7, ks >> 3 adds 256 B
+      // W2 fragment addresses as lane bases + immediates (a run-time or fully hoisted w2off() per
+      // fragment costs VGPRs the compiler then spills): chunk (2ks + h) ^ w2swz(r) only depends on
+      // ks & 7, ks >> 3 adds 256 B
       const int sw = w2swz(r);
       lds_u8* lrow = img + r * 512;
       constexpr int NX = KS < 8 ? KS : 8;      // distinct ks & 7 patterns (ks >> 3 adds 256 B)
@@ -185,56 +180,72 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
           xk8[k][t] = xk[k][t] + 256;
           __asm__ volatile("" : "+v"(xk8[k][t]));
         }
-      auto layer2 = [&](int mt) {
-        f32x16 acc = load_vec16(b2p, mt, h);
+      // units 16ks + 4h + 0..3 and 16ks + 8 + 4h + 0..3 of hidden tile mt: the permuted k order of h1
+      auto frag = [&](int mt, int ks) {
         lds_u8* pm = lrow + mt * 16384;
-        // units 16ks + 4h + 0..3 and 16ks + 8 + 4h + 0..3: the permuted k order of h1
-        auto frag = [&](int ks) {
-          const int* xo = (ks >> 3) ? xk8[ks & 7] : xk[ks & 7];
-          const s16x4 lo = *reinterpret_cast<const lds_s16x4*>(pm + xo[0]);
-          const s16x4 hi = *reinterpret_cast<const lds_s16x4*>(pm + xo[1]);
-          return join4(lo, hi);
-        };
-        bf16x8 ring[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) ring[d] = frag(d);
-#pragma unroll
-        for (int ks = 0; ks < KS; ks += D) {
-          bf16x8 a[D];
-#pragma unroll
-          for (int d = 0; d < D; ++d) {
-            a[d] = ring[d];
-            if (ks + D + d < KS) ring[d] = frag(ks + D + d);
-          }
-#pragma unroll
-          for (int d = 0; d < D; ++d) acc = mfma32(a[d], h1[ks + d], acc);
-        }
-        return acc;
+        const int* xo = (ks >> 3) ? xk8[ks & 7] : xk[ks & 7];
+        const s16x4 lo = *reinterpret_cast<const lds_s16x4*>(pm + xo[0]);
+        const s16x4 hi = *reinterpret_cast<const lds_s16x4*>(pm + xo[1]);
+        return join4(lo, hi);
       };
-      // pass 1: y and the relu'(z2) bits (accumulator layout: units in registers, rows on lanes)
-#pragma unroll 1
-      for (int mt = 0; mt < MT; ++mt) {
-        const f32x16 acc = layer2(mt);
-        const f32x16 w3 = load_vec16(w3p, mt, h);
-        unsigned mk = 0;
+      f32x16 zero;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          ys = __builtin_fmaf(relu_f(acc[e]), w3[e], ys);
-          mk |= (acc[e] > 0.f ? 1u : 0u) << e;
-        }
-        if (mt < 4) mask_lo |= (unsigned long long)mk << (16 * mt);
-        else mask_hi |= (unsigned long long)mk << (16 * (mt - 4));
+      for (int e = 0; e < 16; ++e) zero[e] = 0.f;
+#pragma unroll
+      for (int m1 = 0; m1 < MT; ++m1) {
+        __asm__ volatile("" ::: "memory");     // one layer-1 tile's reads at a time
+        const f32x16 z = mfma32(w1p[m1 * 64 + lane], xb, zero);
+        float zf[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) zf[e] = z[e];
+        bf16x8 hk[2];
+        relu_cvt_bf16x8(zf, &hk[0]);
+        relu_cvt_bf16x8(zf + 8, &hk[1]);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma32(frag(mt, 2 * m1 + s2), hk[s2], acc[mt]);
       }
-      ys += __shfl_xor(ys, 32);
-      const float y = ys + b3;
-      diff = valid ? (y - target[row]) : 0.f;
-      dy = gscale * diff;
-      // pass 2: the dW3 partial sum_r bf16(dy_r) bf16(relu(z2[r, c])) (the operands the split-K
-      // GEMM over h2a used) on the TRANSPOSED tile: the same two operands with their MFMA roles
-      // swapped (h1 as A, the W2 row fragment as B) give z2^T — hidden unit 32mt + r on the lanes,
-      // the tile's rows 8(e>>2) + 4h + (e&3) in the registers — so the row sum is 16 in-lane FMAs
-      // and ONE cross-half add per hidden tile instead of a 5-step lane reduce-scatter.  The rows'
-      // dy reach the lanes through a 128-byte LDS broadcast; rows past B carry dy = 0.
+    }
+    // (h1 is not stored: train_bwd_kernel recomputes it from xf on the same MFMA)
+    // y (hence dy), the relu'(z2) bits and relu(z2) itself packed to bf16 in registers (h2p, the
+    // same k order as the dz2 fragments below); accumulator layout: units in registers, rows on lanes
+    bf16x8 h2p[KS];
+    unsigned long long mask_lo = 0, mask_hi = 0;   // 16 relu'(z2) bits per hidden tile
+    float ys = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const f32x16 w3 = load_vec16(w3p, mt, h);
+      unsigned mk = 0;
+      float a[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        ys = __builtin_fmaf(relu_f(acc[mt][e]), w3[e], ys);
+        mk |= (acc[mt][e] > 0.f ? 1u : 0u) << e;
+        a[e] = acc[mt][e];
+      }
+      relu_cvt_bf16x8(a, &h2p[2 * mt]);
+      relu_cvt_bf16x8(a + 8, &h2p[2 * mt + 1]);
+      if (mt < 4) mask_lo |= (unsigned long long)mk << (16 * mt);
+      else mask_hi |= (unsigned long long)mk << (16 * (mt - 4));
+    }
+    const float b3 = reinterpret_cast<const float*>(w3p + H / 4)[0];   // (per tile: not held in a VGPR)
+    ys += __shfl_xor(ys, 32);
+    const float y = ys + b3;
+    const float diff = valid ? (y - target[row]) : 0.f;
+    const float dy = gscale * diff;
+    // per-row squared error (no cross-lane reduction: its shuffle addresses were the values the
+    // compiler spilled)
+    if (valid && h == 0) sq_err[row] = diff * diff;
+
+    // dW3 | db3 partial sum_r dy_r relu(z2[r, c]) on the TRANSPOSED tile: relu(z2) is exactly
+    // transposed by TWO MFMAs per hidden tile against a permuted identity (B[k][n] = 1 iff element k
+    // of this lane half holds unit n; every product is x * 1), which puts hidden unit 32mt + n on the
+    // lanes and the tile's rows 8(e>>2) + 4h + (e&3) in the registers — so the row sum is 16 in-lane
+    // FMAs and ONE cross-half add per hidden tile.  (Round 2 recomputed z2^T with 128 more MFMAs per
+    // tile because relu(z2) did not fit next to the dgrad's operands; the dgrad now runs in
+    // train_bwd_kernel.)  The rows' dy reach the lanes through a 128-byte LDS broadcast.
+    {
       float* const dys = dyscr;                      // this wave's 32-float scratch
       if (h == 0) dys[r] = dy;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -247,43 +258,25 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) dyv[4 * q4 + j] = t[j];
       }
-      const float* b2f = reinterpret_cast<const float*>(b2p);
-      const int bpos = 2 * ((r >> 2) & 1) * 8 + 4 * (r >> 3) + (r & 3);   // b2 / w3 of unit 32mt + r
-#pragma unroll 1
+      bf16x8 eye0, eye1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int u0 = (j & 3) + 8 * (j >> 2) + 4 * h;          // unit offset of k = 8h + j, K-step 0
+        eye0[j] = (__bf16)(u0 == r ? 1.f : 0.f);
+        eye1[j] = (__bf16)(u0 + 16 == r ? 1.f : 0.f);
+      }
+      f32x16 zero;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) zero[e] = 0.f;
+#pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        f32x16 acc;
-        const float bias = b2f[mt * 32 + bpos];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = bias;
-        lds_u8* pm = lrow + mt * 16384;
-        auto fragw = [&](int ks) {
-          const int* xo = (ks >> 3) ? xk8[ks & 7] : xk[ks & 7];
-          const s16x4 lo = *reinterpret_cast<const lds_s16x4*>(pm + xo[0]);
-          const s16x4 hi = *reinterpret_cast<const lds_s16x4*>(pm + xo[1]);
-          return join4(lo, hi);
-        };
-        bf16x8 ring[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) ring[d] = fragw(d);
-#pragma unroll
-        for (int ks = 0; ks < KS; ks += D) {
-          bf16x8 a[D];
-#pragma unroll
-          for (int d = 0; d < D; ++d) {
-            a[d] = ring[d];
-            if (ks + D + d < KS) ring[d] = fragw(ks + D + d);
-          }
-#pragma unroll
-          for (int d = 0; d < D; ++d) acc = mfma32(h1[ks + d], a[d], acc);
-        }
+        f32x16 tt = mfma32(h2p[2 * mt], eye0, zero);
+        tt = mfma32(h2p[2 * mt + 1], eye1, tt);
         float t = 0.f;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) t = __builtin_fmaf(dyv[e], (float)(__bf16)relu_f(acc[e]), t);
+        for (int e = 0; e < 16; ++e) t = __builtin_fmaf(dyv[e], tt[e], t);
         t += __shfl_xor(t, 32);
-        if (h == 0) {
-          const int u = 32 * mt + r;                 // stored column: hperm(u) = u with bits 2, 3 swapped
-          w3part[(u & ~12) | ((u & 4) << 1) | ((u & 8) >> 1)] += t;
-        }
+        if (h == 0) w3part[hperm(32 * mt + r)] += t;
       }
       // db3 = sum of dy over the rows (lanes of half 0 hold each row once)
       float d = h == 0 ? dy : 0.f;
@@ -291,135 +284,38 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
       for (int o = 16; o >= 1; o >>= 1) d += __shfl_xor(d, o);
       if (lv == 0) w3part[H] += d;
     }
-    if (valid && h == 0) {  // dy as an [B,8] bf16 operand (cols 1..7 zero) for the wgrad kernel
-      bf16x8 dv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dv[j] = (__bf16)0.f;
-      dv[0] = (__bf16)dy;
-      *reinterpret_cast<bf16x8*>(dyb + (size_t)row * 8) = dv;
-    }
-    // per-row squared error (no cross-lane reduction: its shuffle addresses were the values the
-    // compiler spilled, and every reload after the activation stores waited for all of them)
-    if (valid && h == 0) sq_err[row] = diff * diff;
 
     // dz2 = dy * w3 * relu'(z2): fragment 2mt + s element j is accumulator register 8s + j of
-    // hidden tile mt, i.e. exactly the B-operand k order of the dgrad MFMAs below
-    bf16x8 dz2f[KS];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const f32x16 w3 = load_vec16(w3p, mt, h);
-      const unsigned mk = (unsigned)((mt < 4 ? mask_lo >> (16 * mt) : mask_hi >> (16 * (mt - 4))) & 0xffffu);
-      // per output pair: two products, one v_cvt_pk_bf16_f32, and the pair's two mask bits
-      // sign-extended (v_bfe_i32) into a 0xFFFF / 0xFFFF0000 mask
-      typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-      typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        u32x4v dw;
-#pragma unroll
-        for (int q2 = 0; q2 < 4; ++q2) {
-          const int b = 8 * s + 2 * q2;
-          const f32x2 pr = {dy * w3[b], dy * w3[b + 1]};
-          const unsigned cw = __builtin_bit_cast(unsigned, __builtin_convertvector(pr, bf16x2v));
-          const unsigned lo = (unsigned)(((int)(mk << (31 - b))) >> 31);
-          const unsigned hi = (unsigned)(((int)(mk << (30 - b))) >> 31);
-          dw[q2] = cw & ((lo & 0xFFFFu) | (hi & 0xFFFF0000u));
-        }
-        dz2f[2 * mt + s] = __builtin_bit_cast(bf16x8, dw);
-      }
-    }
-    // dz2^T for the weight-gradient kernel: each hidden tile transposed by TWO MFMAs against a
-    // permuted identity (B[k][n] = 1 iff fragment k of this lane half holds unit n), which turns the
-    // rows-on-lanes fragments into units-on-lanes / rows-in-registers — exact (every product is
-    // x * 1) — and stored in the MFMA operand order: chunk (tile, K-step s, unit, lane half h)
+    // hidden tile mt, i.e. hidden units 16ks + 8(j>>2) + 4h + (j&3) (ks = 2mt + s) — contiguous in the
+    // hperm column order.  Stored as a row-major [32 rows][H hperm columns] tile image, one 16-byte
+    // chunk per lane and fragment at chunk (2ks + h) ^ dz2swz(row): train_bwd_kernel copies the image
+    // into LDS as it is and reads it both row-wise (ds_read_b128, the dgrad's A operand) and
+    // transposed (ds_read_b64_tr_b16, dW2's A operand), conflict-free both ways.  Rows past B carry
+    // dy = 0.
     {
-      bf16x8 eye0, eye1;
-      const int n = lv & 31;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int u0 = (j & 3) + 8 * (j >> 2) + 4 * h;          // unit offset of k = 8h + j, K-step 0
-        eye0[j] = (__bf16)(u0 == n ? 1.f : 0.f);
-        eye1[j] = (__bf16)(u0 + 16 == n ? 1.f : 0.f);
-      }
-      f32x16 zero;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) zero[e] = 0.f;
-      typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
       typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+      typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+      bf16x8* const out = dz2r + (size_t)tile * KS * 64 + r * (KS * 2);
+      const int fz = dz2swz(r) & (2 * KS - 1);     // (within the row for H < 256)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        f32x16 tt = mfma32(dz2f[2 * mt], eye0, zero);
-        tt = mfma32(dz2f[2 * mt + 1], eye1, tt);
+        const f32x16 w3 = load_vec16(w3p, mt, h);
+        const unsigned mk = (unsigned)((mt < 4 ? mask_lo >> (16 * mt) : mask_hi >> (16 * (mt - 4))) & 0xffffu);
+        // per output pair: two products, one v_cvt_pk_bf16_f32, and the pair's two mask bits
+        // sign-extended (v_bfe_i32) into a 0xFFFF / 0xFFFF0000 mask
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          u32x4v ow;
-#pragma unroll
-          for (int q2 = 0; q2 < 4; ++q2) {
-            const f32x2 pr = {tt[8 * s2 + 2 * q2], tt[8 * s2 + 2 * q2 + 1]};
-            ow[q2] = __builtin_bit_cast(unsigned, __builtin_convertvector(pr, bf16x2v));
-          }
-          dz2t[(((size_t)tile * 2 + s2) * H + 32 * mt + n) * 2 + h] = __builtin_bit_cast(bf16x8, ow);
-        }
-      }
-    }
-
-    // dgrad: dh1 = dz2 W2 on the TRANSPOSED tile — dz2 as the A operand (rows on the lanes) and
-    // the W2^T fragment as B — so the accumulator holds input unit 32mi + (l&31) on the lane and the
-    // tile's rows in the registers, in the MFMA k order.  That is the dW1 GEMM's A layout: stored
-    // like dz2^T (one 16-byte chunk per K-step and lane half), it is read by train_wgrad_kernel
-    // without any transpose; relu'(z1) is applied there, from the h1^T tile it recomputes anyway.
-    {
-      // transposed reads: rows 16ks + 8t + 4h + q, columns 32mi + 16(g&1) + 4p (8-byte chunk
-      // 8mi + 4(g&1) + p) -> chunk ^ ((q << 3) | (4(ks&1) + 2t + h))
-      // = 64 (mi ^ q) + 8 ((4(g&1) + p) ^ (4(ks&1) + 2t + h)): the lane part of the second term
-      // takes four values (ks parity x t), so four lane bases + a per-mi offset + immediates
-      // replace a full address computation per read
-      const int g1 = (lv >> 4) & 1, p = lv & 3, q = (lv >> 2) & 3;
-      const int lx = 4 * g1 + p;
-      lds_u8* rb = img + (4 * h + q) * 512;
-      lds_u8* bp[2][2];
-#pragma unroll
-      for (int par = 0; par < 2; ++par)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) bp[par][t] = rb + 4096 * t + 8 * (lx ^ (4 * par + 2 * t + h));
-#pragma unroll
-      for (int mi = 0; mi < MT; ++mi) {
-        const int om = 64 * (mi ^ q);
-        auto frag = [&](int ks) {
-          lds_u8* r0 = bp[ks & 1][0] + om + 8192 * ks;
-          lds_u8* r1 = bp[ks & 1][1] + om + 8192 * ks;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)r0);
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)r1);
-          return join4(lo, hi);
-        };
-        f32x16 acc;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-        bf16x8 ring[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) ring[d] = frag(d);
-#pragma unroll
-        for (int ks = 0; ks < KS; ks += D) {
-          bf16x8 a[D];
-#pragma unroll
-          for (int d = 0; d < D; ++d) {
-            a[d] = ring[d];
-            if (ks + D + d < KS) ring[d] = frag(ks + D + d);
-          }
-#pragma unroll
-          for (int d = 0; d < D; ++d) acc = mfma32(dz2f[ks + d], a[d], acc);
-        }
-        typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-        typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          u32x4v ow;
+        for (int s = 0; s < 2; ++s) {
+          u32x4v dw;
 #pragma unroll
           for (int q2 = 0; q2 < 4; ++q2) {
-            const f32x2 pr = {acc[8 * s2 + 2 * q2], acc[8 * s2 + 2 * q2 + 1]};
-            ow[q2] = __builtin_bit_cast(unsigned, __builtin_convertvector(pr, bf16x2v));
+            const int b = 8 * s + 2 * q2;
+            const f32x2 pr = {dy * w3[b], dy * w3[b + 1]};
+            const unsigned cw = __builtin_bit_cast(unsigned, __builtin_convertvector(pr, bf16x2v));
+            const unsigned lo = (unsigned)(((int)(mk << (31 - b))) >> 31);
+            const unsigned hi = (unsigned)(((int)(mk << (30 - b))) >> 31);
+            dw[q2] = cw & ((lo & 0xFFFFu) | (hi & 0xFFFF0000u));
           }
-          dh1t[(((size_t)tile * 2 + s2) * H + 32 * mi + (lv & 31)) * 2 + h] = __builtin_bit_cast(bf16x8, ow);
+          out[(2 * (2 * mt + s) + h) ^ fz] = __builtin_bit_cast(bf16x8, dw);
         }
       }
     }
@@ -437,52 +333,106 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Weight gradients dW2 | db2 = dz2^T [h1 | 1] and dW1 = (dh1 * relu'(z1))^T x, K = batch, with
-// NO LDS and no barriers: one workgroup per k-slice, wave w owning output rows 32w .. 32w + 31 of
-// both products and its accumulators (9 + 1 tiles of 32x32 at H = 256: 160 VGPRs) in registers for
-// the whole slice.  Per 32-row tile a wave
-//   * loads its dz2^T / dh1^T fragments — one 16-byte load per K-step, the forward stored them in
-//     the MFMA operand order — and the tile's 32-byte feature rows;
-//   * recomputes h1 = relu(W1k x) for every n-tile on the layer-1 MFMA with the operands swapped
-//     (x as A, the forward's w1p fragment as B), which yields h1^T with the units on the lanes and
-//     the rows in the registers: exactly the B operand of dW2 (K = rows), and, for n-tile w, the
-//     relu'(z1) mask of dh1^T in its own layout;
-//   * transposes x by one MFMA against an identity fragment for dW1's B operand;
-//   * issues 2 MFMAs per output tile (K = 32 rows).
-// The B operand [h1 | 1] never exists in memory (the old path stored h1a, 544 B/row, and read it
-// back with dz2 through LDS-staged transposed reads).  Partial sums of slice s go to slab[s] in the
-// bucket layout (hperm rows and columns, train/fused.py) and wgrad_reduce sums them in a fixed
-// order.
+// The whole backward below dz2 in ONE kernel: dh1 = dz2 W2 (dgrad), dz1 = dh1 * relu'(z1),
+// dW2 | db2 = dz2^T [h1 | 1] and dW1 = dz1^T x, K = batch, split over k-slices (one workgroup per
+// CU, each a contiguous run of 32-row tiles).  Inputs per row: the forward's dz2 fragments
+// (512 B) and the 32-byte feature row — half the bytes of the round-2 pair dz2^T + dh1^T, and
+// the forward no longer runs the dgrad or any transpose.
+//
+// One wave per SIMD (4 waves at H = 256, 512 registers each); wave w owns the hidden units
+// u1 = 64w .. 64w + 63 of h1 (two 32-unit n-blocks), so per 32-row tile it:
+//   * recomputes h1^T for its two n-blocks on the layer-1 MFMA (x as A, the w1p fragment as B:
+//     units on the lanes, rows in the registers = the dW2 B operand, and relu'(z1) in the layout
+//     of its own dh1^T tile) — no redundant layer-1 work across waves;
+//   * runs the dgrad with dz2 as the A operand (rows on the lanes, as the forward stored it) and
+//     W2's column block as B, read from an LDS image of W2 in B-fragment order (ds_read_b128,
+//     conflict-free): D = dh1 with the units on the lanes and the rows in the registers, i.e. dh1^T
+//     in the dW1 A layout;
+//   * transposes every dz2 fragment pair exactly (MFMA against a permuted identity, as the forward
+//     does for relu(z2)) into dz2^T, the dW2 A operand, and accumulates dW2 for all 256 z2 units x
+//     its 64 h1 units: 16 accumulator tiles = 256 registers, resident for the whole slice;
+//   * transposes x once for dW1's B operand.
+// 87 MFMAs per wave and tile, no LDS writes: the dz2 tile (16 KB) is double-buffered in LDS by
+// global_load_lds issued one tile ahead (every wave reads all of it), x rows arrive by plain loads
+// one tile ahead, and one barrier per tile separates the stages.  LDS = W2 image (H*H*2 B) + two dz2
+// tiles (2 * H * 64 B): exactly 160 KB at H = 256.
+// Partial sums of slice s go to slab[s] in the bucket layout (hperm rows and columns,
+// train/fused.py); wgrad_reduce sums them in a fixed order (deterministic).
 template <int H>
-__global__ __launch_bounds__(H / 32 * 64, 1) void train_wgrad_kernel(
+__global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     const __bf16* __restrict__ xf, int B, const unsigned char* __restrict__ blob,
-    const bf16x8* __restrict__ dz2t, const bf16x8* __restrict__ dh1t, int tiles_per_slice,
-    float* __restrict__ slab2, float* __restrict__ slab1) {
+    const bf16x8* __restrict__ dz2r, int tiles_per_slice, float* __restrict__ slab2, float* __restrict__ slab1) {
   using L = TrainLayout<H>;
-  constexpr int MT = H / 32, LDG = H + 16;
+  constexpr int MT = H / 32, KS = H / 16, LDG = H + 16, RBF = KS * 64;
+  typedef __attribute__((address_space(3))) void lds_void_t;
+  typedef __attribute__((address_space(3))) const unsigned char lds_u8c;
+  typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16x8* const w2s = reinterpret_cast<bf16x8*>(smem);      // [H/32][KS][64] B fragments
+  bf16x8* const rb = w2s + MT * RBF;                         // [2][KS][64] dz2 fragments
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 31, h = lane >> 5;
+  const int nw = blockDim.x >> 6;
   const int ntiles = (B + 31) >> 5;
   const int t0 = blockIdx.x * tiles_per_slice;
   const int t1 = min(ntiles, t0 + tiles_per_slice);
-  // the layer-1 fragments (the same for every wave) in LDS, not in 32 VGPRs per wave
-  __shared__ bf16x8 s_w1[MT * 64];
+
+  // the W2 B-fragment image (kept by adamw_pack_kernel past the forward's blob) into LDS, and the
+  // first dz2 tile behind it
+  const unsigned char* w2g = blob + L::BLOB;
+  for (int c = w; c < (int)(MT * RBF / 64); c += nw)
+    __builtin_amdgcn_global_load_lds((const void*)(w2g + (size_t)c * 1024 + 16 * lane),
+                                     (lds_void_t*)(w2s + c * 64), 16, 0, 0);
+  auto stage = [&](int tile, int buf) {
+    const bf16x8* src = dz2r + (size_t)tile * RBF;
+    for (int c = w; c < KS; c += nw)
+      __builtin_amdgcn_global_load_lds((const void*)(src + c * 64 + lane), (lds_void_t*)(rb + buf * RBF + c * 64),
+                                       16, 0, 0);
+  };
+  const bf16x8* xg = reinterpret_cast<const bf16x8*>(xf);    // row r, half h = chunk 2r + h
+  bf16x8 xn;
+  if (t0 < t1) {
+    stage(t0, 0);
+    xn = xg[(size_t)t0 * 64 + 2 * col + h];
+  }
   const bf16x8* w1p = reinterpret_cast<const bf16x8*>(blob + L::W2B);
-  for (int i = threadIdx.x; i < MT * 64; i += blockDim.x) s_w1[i] = w1p[i];
-  __syncthreads();
+  // this wave's two W2 B-fragment blocks in the LDS image (absolute addresses: lane base + immediates)
+  const unsigned wb0[2] = {(unsigned)(((2 * w) * KS * 64 + lane) * 16), (unsigned)(((2 * w + 1) * KS * 64 + lane) * 16)};
+  bf16x8 w1f[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) w1f[i] = w1p[(2 * w + i) * 64 + lane];
   bf16x8 eye;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) eye[j] = (__bf16)(8 * h + j == col ? 1.f : 0.f);   // B (k = 8h + j, n = col)
-  f32x16 acc2[MT], acc1;
+  for (int j = 0; j < 8; ++j) eye[j] = (__bf16)(8 * h + j == col ? 1.f : 0.f);   // x^T: B (k = 8h + j, n = col)
+  // Addresses into a dz2 tile image ([32 rows][2KS chunks of 16 B], chunk c of row r at
+  // c ^ dz2swz(r)): the swizzled fields and the compile-time parts occupy disjoint bits, so every read
+  // is ONE lane base XOR a constant (checked exhaustively for H = 64/128/256 on the host):
+  //   row read of k-step ks (the dgrad's A operand, chunk 2ks + h of row col):
+  //       R0 ^ (32 (ks & 7) + 256 (ks >> 3))
+  //   transposed read t of k-step s2 of hidden tile mt (dW2's A operand: rows 16s2 + 8t + 4(lane>>5)
+  //   + 0..3, image columns 32mt + 16((lane>>4)&1) + 0..15):
+  //       C0 ^ (64 (mt & 3) + 32 t + 8t RB2 + 256 (mt >> 2) + 16 RB2 s2)
+  // and the buffer's base is OR-ed in (its bits lie above).  Two VGPRs instead of a 16-entry table.
+  constexpr int RB2 = 2 * KS * 16;                          // bytes per image row
+  constexpr int CM = 2 * KS - 1;                            // chunk mask (H < 256: fewer chunks)
+  const unsigned R0 = col * RB2 + 16 * ((h ^ dz2swz(col)) & CM);
+  unsigned C0;
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int row = 4 * (g >> 1) + q, chunk = 2 * (g & 1) + (p >> 1);
+    C0 = row * RB2 + 16 * ((chunk ^ dz2swz(row)) & CM) + 8 * (p & 1);
+  }
+  f32x16 acc2[MT][2], acc1[2], zero;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    acc1[e] = 0.f;
+    zero[e] = 0.f;
 #pragma unroll
-    for (int nt = 0; nt < MT; ++nt) acc2[nt][e] = 0.f;
+    for (int i = 0; i < 2; ++i) {
+      acc1[i][e] = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc2[mt][i][e] = 0.f;
+    }
   }
-  float db2 = 0.f;                     // sum of this lane's dz2 values (unit 32w + col)
-  f32x16 zero;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) zero[e] = 0.f;
+  float db2[2] = {0.f, 0.f};           // sums of dz2 over the rows, units 32(2w + i) + col
   typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
   typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
   auto pack = [](const f32x16& v, int s, bool relu) {
@@ -499,67 +449,113 @@ __global__ __launch_bounds__(H / 32 * 64, 1) void train_wgrad_kernel(
     }
     return __builtin_bit_cast(bf16x8, o);
   };
-  // fragments of one 32-row tile: x (A of the layer-1 / identity MFMAs), dz2^T and dh1^T (A of
-  // the two products, one 16-byte load per K-step); the next tile's are in flight while this one
-  // computes (the loads are the only latency in the loop)
-  struct Frags {
-    bf16x8 x, a0, a1, g0, g1;
-  };
-  // buffer loads: 32-bit offsets against wave-uniform descriptors (no 64-bit address per load, which
-  // left the kernel short of VGPRs), and the hardware range check zero-fills the rows past B
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)xf, 0, B * 32, 0x00020000);
-  const int tb = ntiles * 32 * H * 2;                  // bytes of dz2t / dh1t
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)dz2t, 0, tb, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)dh1t, 0, tb, 0x00020000);
-  auto load = [&](int tile) {
-    Frags f;
-    f.x = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, (tile * 32 + col) * 32 + 16 * h, 0, 0));
-    const int c0 = ((tile * 2 * H + 32 * w + col) * 2 + h) * 16, c1 = c0 + H * 2 * 16;
-    f.a0 = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, c0, 0, 0));
-    f.a1 = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, c1, 0, 0));
-    f.g0 = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rg, c0, 0, 0));
-    f.g1 = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rg, c1, 0, 0));
-    return f;
-  };
-  Frags cur;
-  if (t0 < t1) cur = load(t0);
+
   for (int tile = t0; tile < t1; ++tile) {
-    Frags nxt = cur;
-    if (tile + 1 < t1) nxt = load(tile + 1);
-    // db2 = sum over rows of dz2 (VALU on the A fragments; no MFMA tile for one column)
-    {
-      const u32x4v p0 = __builtin_bit_cast(u32x4v, cur.a0), p1 = __builtin_bit_cast(u32x4v, cur.a1);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        db2 += __uint_as_float(p0[q] << 16) + __uint_as_float(p0[q] & 0xFFFF0000u);
-        db2 += __uint_as_float(p1[q] << 16) + __uint_as_float(p1[q] & 0xFFFF0000u);
-      }
+    const int buf = (tile - t0) & 1;
+    // this wave's share of the tile (and, on the first pass, of the W2 image) has landed; after the
+    // barrier every wave's share has, and every wave has finished reading the other buffer
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const bf16x8 x = xn;
+    if (tile + 1 < t1) {
+      stage(tile + 1, buf ^ 1);
+      xn = xg[(size_t)(tile + 1) * 64 + 2 * col + h];
     }
-    bf16x8 g0 = cur.g0, g1 = cur.g1;
+    // the tile image as an absolute LDS address (dynamic LDS starts at 0: no static __shared__ here),
+    // so every read is a lane base + an immediate offset
+    // layer 1 for the two n-blocks: h1^T (units on the lanes, rows in the registers)
+    bf16x8 h1t[2][2];
+    unsigned m1[2];                    // relu'(z1) bits in the accumulator-register order
 #pragma unroll
-    for (int nt = 0; nt < MT; ++nt) {
-      const f32x16 hz = mfma32(cur.x, s_w1[nt * 64 + lane], zero);   // h1^T pre-activation, units 32nt + col
-      acc2[nt] = mfma32(cur.a0, pack(hz, 0, true), acc2[nt]);
-      acc2[nt] = mfma32(cur.a1, pack(hz, 1, true), acc2[nt]);
-      if (nt == w) {                                    // relu'(z1) for this wave's dW1 rows
-        u32x4v m0 = __builtin_bit_cast(u32x4v, g0), m1 = __builtin_bit_cast(u32x4v, g1);
+    for (int i = 0; i < 2; ++i) {
+      const f32x16 hz = mfma32(x, w1f[i], zero);
+      h1t[i][0] = pack(hz, 0, true);
+      h1t[i][1] = pack(hz, 1, true);
+      unsigned mk = 0;
 #pragma unroll
-        for (int q2 = 0; q2 < 4; ++q2) {
-          const unsigned k0 = (hz[2 * q2] > 0.f ? 0xFFFFu : 0u) | (hz[2 * q2 + 1] > 0.f ? 0xFFFF0000u : 0u);
-          const unsigned k1 = (hz[8 + 2 * q2] > 0.f ? 0xFFFFu : 0u) | (hz[8 + 2 * q2 + 1] > 0.f ? 0xFFFF0000u : 0u);
-          m0[q2] &= k0;
-          m1[q2] &= k1;
+      for (int e = 0; e < 16; ++e) mk |= (hz[e] > 0.f ? 1u : 0u) << e;
+      m1[i] = mk;
+    }
+    f32x16 accd[2] = {zero, zero};
+    // dz2 fragments of hidden tile mt — the dgrad's row-read pair and dW2's two transposed k-steps —
+    // are read one hidden tile ahead, the tile's 4 W2 B fragments at its start (the dW2 MFMAs run
+    // while they arrive).  The bases pass through an empty asm per hidden tile, so the XORs are
+    // formed where they are used instead of all being hoisted into live registers, and the memory
+    // clobber keeps later tiles' reads from being hoisted to the top (both spilled).
+    const unsigned tb0 = (unsigned)(MT * RBF * 16 + buf * RBF * 16);
+    unsigned rbase = tb0 | R0, tbase = tb0 | C0;
+    struct AFrags {
+      bf16x8 a0, a1, t[2];
+    };
+    auto lda = [&](int mt) {
+      AFrags f;
+      f.a0 = *(const lds_bf16x8*)(uintptr_t)(rbase ^ (32u * ((2 * mt) & 7) + 256u * ((2 * mt) >> 3)));
+      f.a1 = *(const lds_bf16x8*)(uintptr_t)(rbase ^ (32u * ((2 * mt + 1) & 7) + 256u * ((2 * mt + 1) >> 3)));
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const unsigned k0 = 64u * (mt & 3) + 256u * (mt >> 2) + 16u * RB2 * s2;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(tbase ^ k0));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(tbase ^ (k0 + 32u + 8u * RB2)));
+        f.t[s2] = join4(lo, hi);
+      }
+      return f;
+    };
+    AFrags cur = lda(0);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      asm volatile("" : "+v"(rbase), "+v"(tbase));
+      bf16x8 wv[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const lds_u8c* wf = (const lds_u8c*)(uintptr_t)(wb0[i] + 2048u * mt);
+        wv[i][0] = *reinterpret_cast<const lds_bf16x8*>(wf);
+        wv[i][1] = *reinterpret_cast<const lds_bf16x8*>(wf + 1024);
+      }
+      AFrags nxt = cur;
+      if (mt + 1 < MT) nxt = lda(mt + 1);
+      asm volatile("" ::: "memory");
+      // dW2: dz2^T of hidden tile mt (lane m: the unit in image column 32mt + m, rows in the k order
+      // of h1t) x h1^T
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        acc2[mt][i] = mfma32(cur.t[0], h1t[i][0], acc2[mt][i]);
+        acc2[mt][i] = mfma32(cur.t[1], h1t[i][1], acc2[mt][i]);
+      }
+      // dgrad: dh1^T(u1 block) += dz2 (rows on lanes) x W2[:, block]
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        accd[i] = mfma32(cur.a0, wv[i][0], accd[i]);
+        accd[i] = mfma32(cur.a1, wv[i][1], accd[i]);
+      }
+      if ((mt >> 1) == w) {            // db2 of this wave's own two z2 tiles (wave-uniform)
+        const u32x4v q0 = __builtin_bit_cast(u32x4v, cur.t[0]), q1 = __builtin_bit_cast(u32x4v, cur.t[1]);
+        float sacc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sacc += __uint_as_float(q0[q] << 16) + __uint_as_float(q0[q] & 0xFFFF0000u);
+          sacc += __uint_as_float(q1[q] << 16) + __uint_as_float(q1[q] & 0xFFFF0000u);
         }
-        g0 = __builtin_bit_cast(bf16x8, m0);
-        g1 = __builtin_bit_cast(bf16x8, m1);
+        db2[mt & 1] += sacc;
       }
+      cur = nxt;
     }
-    // x^T: D[row][f] with the feature on the lane and the rows in the registers
-    const f32x16 xt = mfma32(cur.x, eye, zero);
-    acc1 = mfma32(g0, pack(xt, 0, false), acc1);
-    acc1 = mfma32(g1, pack(xt, 1, false), acc1);
-    cur = nxt;
+    // dW1 += (dh1 * relu'(z1))^T x: x^T as the B operand (features on the lanes)
+    const f32x16 xt = mfma32(x, eye, zero);
+    const bf16x8 xb0 = pack(xt, 0, false), xb1 = pack(xt, 1, false);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      u32x4v g0 = __builtin_bit_cast(u32x4v, pack(accd[i], 0, false));
+      u32x4v g1 = __builtin_bit_cast(u32x4v, pack(accd[i], 1, false));
+#pragma unroll
+      for (int q2 = 0; q2 < 4; ++q2) {
+        const unsigned b0 = m1[i] >> (2 * q2), b1 = m1[i] >> (8 + 2 * q2);
+        g0[q2] &= ((b0 & 1u) ? 0xFFFFu : 0u) | ((b0 & 2u) ? 0xFFFF0000u : 0u);
+        g1[q2] &= ((b1 & 1u) ? 0xFFFFu : 0u) | ((b1 & 2u) ? 0xFFFF0000u : 0u);
+      }
+      acc1[i] = mfma32(__builtin_bit_cast(bf16x8, g0), xb0, acc1[i]);
+      acc1[i] = mfma32(__builtin_bit_cast(bf16x8, g1), xb1, acc1[i]);
+    }
   }
   // D[m][n]: lane -> n = col, register e -> m = (e&3) + 8(e>>2) + 4h; rows / columns to the bucket's
   // hperm order (the stored unit order of every other gradient path)
@@ -567,19 +563,27 @@ __global__ __launch_bounds__(H / 32 * 64, 1) void train_wgrad_kernel(
   float* o1 = slab1 + (size_t)blockIdx.x * H * 16;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const int m = 32 * w + (e & 3) + 8 * (e >> 2) + 4 * h;
-    const int mr = hperm(m);
+    const int mo = (e & 3) + 8 * (e >> 2) + 4 * h;
 #pragma unroll
-    for (int nt = 0; nt < MT; ++nt) o2[(size_t)mr * LDG + hperm(32 * nt + col)] = acc2[nt][e];
-    if (col < 16) o1[(size_t)mr * 16 + col] = acc1[e];
+    for (int i = 0; i < 2; ++i) {
+      const int nc = hperm(32 * (2 * w + i) + col);
+#pragma unroll
+      // (dW2's A rows came out of the hperm-ordered image: D row 32mt + mo IS bucket row 32mt + mo)
+      for (int mt = 0; mt < MT; ++mt) o2[(size_t)(32 * mt + mo) * LDG + nc] = acc2[mt][i][e];
+      if (col < 16) o1[(size_t)hperm(32 * (2 * w + i) + mo) * 16 + col] = acc1[i][e];
+    }
   }
-  // db2 column (and the zero columns H+1 .. H+15): both lane halves hold rows of unit 32w + col
-  db2 += __shfl_xor(db2, 32);
-  const int ur = hperm(32 * w + col);
-  if (h == 0) o2[(size_t)ur * LDG + H] = db2;
-  else
+  // db2 column (and the zero columns H+1 .. H+15): both lane halves hold rows of image column
+  // 32(2w+i) + col
 #pragma unroll
-    for (int c = 1; c < 16; ++c) o2[(size_t)ur * LDG + H + c] = 0.f;
+  for (int i = 0; i < 2; ++i) {
+    const float d = db2[i] + __shfl_xor(db2[i], 32);
+    const int ur = 32 * (2 * w + i) + col;          // (image column = bucket row, as above)
+    if (h == 0) o2[(size_t)ur * LDG + H] = d;
+    else
+#pragma unroll
+      for (int c = 1; c < 16; ++c) o2[(size_t)ur * LDG + H + c] = 0.f;
+  }
 }
 
 // Flat parameter layout (fp32 master): W1[H][12] | b1[H] | W2[H][H] | b2[H] | w3[H] | b3
@@ -679,6 +683,7 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
     if (i == 11) put(13);
   } else if (e >= OFF_W2 && e < OFF_B2) {
     *reinterpret_cast<__bf16*>(w2img + w2off(o, i)) = (__bf16)p;   // natural order, swizzled chunks
+    reinterpret_cast<__bf16*>(blob + L::BLOB)[w2frag_index(o, i, H / 16)] = (__bf16)p;
   } else if (e < OFF_B3) {
     const int mt = o >> 5, rr = o & 31;
     const int hh = (rr >> 2) & 1;
@@ -707,8 +712,8 @@ int train_fwd_grid(int B, int num_cus) {
 
 template <int H>
 static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B, const void* blob,
-                                     const NormParams& np, float gscale, void* xf, float* w3slab, void* dz2t,
-                                     void* dh1t, void* dyb, float* sq_err, int* step_ctr, int num_cus,
+                                     const NormParams& np, float gscale, void* xf, float* w3slab, void* dz2r,
+                                     float* sq_err, int* step_ctr, int num_cus,
                                      hipStream_t stream) {
   using L = TrainLayout<H>;
   constexpr int TPB = TRAIN_TPB;
@@ -733,54 +738,66 @@ static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B
   if (grid < 1) return hipSuccess;
   hipLaunchKernelGGL(eta_mlp3_train_fwd_kernel<H>, dim3(grid), dim3(TPB), LDS, stream,
                      (const int4*)rec, target, B, (const unsigned char*)blob, np, gscale,
-                     (__bf16*)xf, w3slab, (bf16x8*)dz2t, (bf16x8*)dh1t, (__bf16*)dyb, sq_err, step_ctr);
+                     (__bf16*)xf, w3slab, (bf16x8*)dz2r, sq_err, step_ctr);
   return hipGetLastError();
 }
 
 hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B, const void* blob,
                                      int H, const NormParams& np, float gscale, void* xf,
-                                     float* w3slab, void* dz2t, void* dh1t, void* dyb,
+                                     float* w3slab, void* dz2r,
                                      float* sq_err, int* step_ctr, int num_cus,
                                      hipStream_t stream) {
   switch (H) {
-    case 64: return launch_train_fwd_h<64>(rec, target, B, blob, np, gscale, xf, w3slab, dz2t, dh1t, dyb, sq_err, step_ctr, num_cus, stream);
-    case 128: return launch_train_fwd_h<128>(rec, target, B, blob, np, gscale, xf, w3slab, dz2t, dh1t, dyb, sq_err, step_ctr, num_cus, stream);
-    case 256: return launch_train_fwd_h<256>(rec, target, B, blob, np, gscale, xf, w3slab, dz2t, dh1t, dyb, sq_err, step_ctr, num_cus, stream);
+    case 64: return launch_train_fwd_h<64>(rec, target, B, blob, np, gscale, xf, w3slab, dz2r, sq_err, step_ctr, num_cus, stream);
+    case 128: return launch_train_fwd_h<128>(rec, target, B, blob, np, gscale, xf, w3slab, dz2r, sq_err, step_ctr, num_cus, stream);
+    case 256: return launch_train_fwd_h<256>(rec, target, B, blob, np, gscale, xf, w3slab, dz2r, sq_err, step_ctr, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }
 
-// k-slices of train_wgrad_kernel: one workgroup per CU at most (its waves hold ~170 VGPRs of
-// accumulators and fragments), each slice a whole number of 32-row tiles
+// k-slices of train_bwd_kernel: one workgroup per CU at most (its LDS is the whole 160 KB at
+// H = 256), each slice a whole number of 32-row tiles, >= ROUTEST_TRAIN_WGRAD_TILES (default 8) of
+// them so the W2 staging and the slab write are amortised
 int train_wgrad_slices(int B, int num_cus) {
   static const int min_tiles = [] {
     const char* v = std::getenv("ROUTEST_TRAIN_WGRAD_TILES");
-    const int t = v ? std::atoi(v) : 4;
+    const int t = v ? std::atoi(v) : 8;
     return t < 1 ? 1 : t;
   }();
   const int ntiles = (B + 31) / 32;
-  int S = ntiles / min_tiles;          // >= min_tiles 32-row tiles per slice (the slab write amortised)
+  int S = ntiles / min_tiles;
   if (S > num_cus) S = num_cus;
   return S < 1 ? 1 : S;
 }
 
 template <int H>
-static hipError_t launch_train_wgrad_h(const void* xf, int B, const void* blob, const void* dz2t, const void* dh1t,
-                                       float* slab2, float* slab1, int S, hipStream_t stream) {
+static hipError_t launch_train_bwd_h(const void* xf, int B, const void* blob, const void* dz2r, float* slab2,
+                                     float* slab1, int S, hipStream_t stream) {
+  constexpr size_t LDS = (size_t)H * H * 2 + (size_t)2 * H * 64;
+  static_assert(LDS <= 160 * 1024, "train_bwd_kernel LDS budget");
+  static bool attr_set[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!attr_set[dev & 63]) {
+    hipError_t e = hipFuncSetAttribute((const void*)train_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)LDS);
+    if (e != hipSuccess) return e;
+    attr_set[dev & 63] = true;
+  }
   const int ntiles = (B + 31) / 32;
   const int tps = (ntiles + S - 1) / S;
-  hipLaunchKernelGGL(train_wgrad_kernel<H>, dim3(S), dim3(H / 32 * 64), 0, stream, (const __bf16*)xf, B,
-                     (const unsigned char*)blob, (const bf16x8*)dz2t, (const bf16x8*)dh1t, tps, slab2, slab1);
+  hipLaunchKernelGGL(train_bwd_kernel<H>, dim3(S), dim3(H), LDS, stream, (const __bf16*)xf, B,
+                     (const unsigned char*)blob, (const bf16x8*)dz2r, tps, slab2, slab1);
   return hipGetLastError();
 }
 
-hipError_t launch_train_wgrad(const void* xf, int B, const void* blob, int H, const void* dz2t, const void* dh1t,
-                              float* slab2, float* slab1, int S, hipStream_t stream) {
+hipError_t launch_train_bwd(const void* xf, int B, const void* blob, int H, const void* dz2r, float* slab2,
+                            float* slab1, int S, hipStream_t stream) {
   if (S < 1) return hipErrorInvalidValue;
   switch (H) {
-    case 64: return launch_train_wgrad_h<64>(xf, B, blob, dz2t, dh1t, slab2, slab1, S, stream);
-    case 128: return launch_train_wgrad_h<128>(xf, B, blob, dz2t, dh1t, slab2, slab1, S, stream);
-    case 256: return launch_train_wgrad_h<256>(xf, B, blob, dz2t, dh1t, slab2, slab1, S, stream);
+    case 64: return launch_train_bwd_h<64>(xf, B, blob, dz2r, slab2, slab1, S, stream);
+    case 128: return launch_train_bwd_h<128>(xf, B, blob, dz2r, slab2, slab1, S, stream);
+    case 256: return launch_train_bwd_h<256>(xf, B, blob, dz2r, slab2, slab1, S, stream);
     default: return hipErrorInvalidValue;
   }
 }

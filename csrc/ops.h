@@ -25,17 +25,18 @@ hipError_t launch_eta_mlp3_fwd16(const void* rec, float* out, int B, const void*
 hipError_t launch_eta_featurize(const void* rec, float* out, int B, hipStream_t stream);
 
 // ---- ETA MLP training (K3) : eta_mlp_train.hip ----
-// forward + MSE gradient + dgrad; writes xf [B,16], dz2^T and dh1^T in the MFMA operand order
-// ([ceil(B/32)][H][4] x 16 bytes each), dy, squared errors and the dW3 slab
+// forward + MSE gradient in one pass over layer 2; writes xf [ceil(B/32)*32, 16] (rows past B
+// untouched), the dz2 fragments ([ceil(B/32)][H/16][64] x 16 bytes, train_bwd_kernel's A-operand
+// order), squared errors and the dW3 slab
 hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B, const void* blob,
                                      int H, const NormParams& np, float gscale, void* xf,
-                                     float* w3slab, void* dz2t, void* dh1t, void* dyb,
-                                     float* sq_err, int* step_ctr, int num_cus,
+                                     float* w3slab, void* dz2r, float* sq_err, int* step_ctr, int num_cus,
                                      hipStream_t stream);
 int train_fwd_grid(int B, int num_cus);   // workgroups = rows of the dW3 slab
-// dW2|db2 and dW1 partials per k-slice (slab2 [S][H][H+16], slab1 [S][H][16], bucket order)
-hipError_t launch_train_wgrad(const void* xf, int B, const void* blob, int H, const void* dz2t, const void* dh1t,
-                              float* slab2, float* slab1, int S, hipStream_t stream);
+// dgrad + relu'(z1) + dW2|db2 and dW1 partials per k-slice (slab2 [S][H][H+16], slab1 [S][H][16],
+// bucket order); xf must hold ceil(B/32)*32 rows (zeros past B)
+hipError_t launch_train_bwd(const void* xf, int B, const void* blob, int H, const void* dz2r, float* slab2,
+                            float* slab1, int S, hipStream_t stream);
 int train_wgrad_slices(int B, int num_cus);
 size_t eta_mlp3_train_blob_bytes(int H);
 int mlp3_num_params(int H);

@@ -2,16 +2,15 @@
 
 Per step (all on the current HIP stream, no host synchronisation, HIP-graph capturable):
 
-  eta_mlp3_train_fwd (HIP)  : featurize + 3 layers + MSE grad + the input-gradient path
-                            dh1 = dz2 W2 (MFMA on the transposed LDS image of W2); writes xf,
-                            dy, and dz2^T / dh1^T in the MFMA operand order of the weight-gradient
-                            kernel, plus G[w3|b3] = dy^T [h2|1] as one fp32 row per workgroup
-                            (relu(z2) never leaves the registers)
-  G[W2|b2], G[W1k|b1]       : train_wgrad (HIP, K = batch, no LDS): each wave holds its rows of
-                            dW2|db2 and dW1 in registers over a k-slice, recomputing [h1|1] from
-                            xf on the layer-1 MFMA (h1 is never stored) and applying relu'(z1) to
-                            dh1^T there; fp32 slabs in the bucket layout, then ONE deterministic
-                            reduction of the three slab regions into G
+  eta_mlp3_train_fwd (HIP)  : featurize + layer 1 + ONE pass over layer 2 (relu(z2) kept packed
+                            in registers) + layer 3 + MSE grad; G[w3|b3] = dy^T [h2|1] as one fp32
+                            row per workgroup (relu(z2) transposed exactly on the MFMA); writes xf
+                            and the dz2 fragments (512 B/row) in train_bwd's A-operand order
+  G[W2|b2], G[W1k|b1]       : train_bwd (HIP, K = batch): dgrad dh1 = dz2 W2 against an LDS image
+                            of W2, relu'(z1) from h1 recomputed on the layer-1 MFMA (h1 is never
+                            stored), dW2|db2 and dW1 register-resident over a k-slice; fp32 slabs
+                            in the bucket layout, then ONE deterministic reduction of the three
+                            slab regions into G
   all_reduce(G)             : ONE RCCL collective (SUM; dy was pre-scaled by 2/global_batch)
   adamw_pack (HIP)          : AdamW on fp32 master params + re-pack of the training blob
 No library GEMM runs in the step (csrc/eta_mlp_train.hip).
@@ -87,10 +86,20 @@ def _w2off(row: np.ndarray, col: np.ndarray) -> np.ndarray:
 
 
 @torch.no_grad()
+def _w2frag_index(u2: np.ndarray, u1: np.ndarray, H: int) -> np.ndarray:
+    """bf16 index of W2[u2][u1] in train_bwd_kernel's B-fragment image (eta_mlp_train.hip
+    w2frag_index): fragment (u1 // 32, u2 // 16), lane u1 % 32 + 32 h, element j."""
+    KS = H // 16
+    nb, n, ks, r = u1 >> 5, u1 & 31, u2 >> 4, u2 & 15
+    hh, j = (r >> 2) & 1, 4 * (r >> 3) + (r & 3)
+    return ((nb * KS + ks) * 64 + n + 32 * hh) * 8 + j
+
+
 def pack_train_blob(model: EtaMLP) -> torch.Tensor:
     """Host mirror of adamw_pack_kernel(update=False): the training blob of ``model`` — the W2
     image (natural order, swizzled 8-byte chunks) followed by the inference blob's
-    w1p | b1p | b2p | w3p | tail (target scale as in the model's buffers)."""
+    w1p | b1p | b2p | w3p | tail (target scale as in the model's buffers), then the backward's
+    W2 B-fragment image."""
     from ..ops.eta_mlp import pack_mlp3
     H = model.hidden
     inf = pack_mlp3(model).blob.numpy()
@@ -101,7 +110,9 @@ def pack_train_blob(model: EtaMLP) -> torch.Tensor:
     off = _w2off(o, c)
     img.view(np.int16)[(off // 2).reshape(-1)] = src.reshape(-1)
     tail = inf[2 * H * H:]                   # w1p | b1p | b2p | w3p | tail of the inference blob
-    return torch.from_numpy(np.concatenate([img, tail]))
+    frag = np.zeros(H * H, dtype=np.int16)
+    frag[_w2frag_index(o, c, H).reshape(-1)] = src.reshape(-1)
+    return torch.from_numpy(np.concatenate([img, tail, frag.view(np.uint8)]))
 
 
 class FusedMlp3Trainer:
@@ -166,16 +177,16 @@ class FusedMlp3Trainer:
     def _alloc(self, B: int) -> None:
         d, H, bf = self.dev, self.H, torch.bfloat16
         self.blob = torch.zeros(self.C.eta_mlp3_train_blob_bytes(H), dtype=torch.uint8, device=d)
-        self.xf = torch.empty(B, 16, dtype=bf, device=d)
-        # dz2^T and dh1^T in the MFMA operand order of train_wgrad_kernel (per 32-row tile and unit,
-        # 32 rows in the k order): nothing else of the activations leaves the forward kernel
         tiles = (B + 31) // 32
-        self.dz2t = torch.empty(tiles * 32 * H, dtype=bf, device=d)
-        self.dh1t = torch.empty(tiles * 32 * H, dtype=bf, device=d)
-        self.dyb = torch.empty(B, 8, dtype=bf, device=d)
+        # feature rows padded to whole 32-row tiles; the pad rows stay zero (the forward only
+        # writes rows < B), so the backward's tail tile contributes nothing
+        self.xf = torch.zeros(tiles * 32, 16, dtype=bf, device=d)
+        # dz2 fragments in train_bwd's A-operand order (per 32-row tile: H/16 x 64 lanes x 16 B):
+        # with xf, all the activations that leave the forward kernel
+        self.dz2r = torch.empty(tiles * 32 * H, dtype=bf, device=d)
         ldg = H + 16
-        # k-slices of the weight-gradient kernel (one workgroup per CU at most): dW2|db2 and dW1
-        # partials per slice; dW3|db3 arrives as one row per forward workgroup (w3slab)
+        # k-slices of the backward kernel (one workgroup per CU at most): dW2|db2 and dW1 partials
+        # per slice; dW3|db3 arrives as one row per forward workgroup (w3slab)
         self.S = self.C.train_wgrad_slices(B, d.index or 0)
         self.slab2 = torch.empty(self.S, H * ldg, dtype=torch.float32, device=d)
         self.slab = torch.empty(self.S, H * 16, dtype=torch.float32, device=d)
@@ -197,9 +208,9 @@ class FusedMlp3Trainer:
         """Fills the flat gradient bucket G (local contribution, pre-scaled for the global mean)."""
         C, H = self.C, self.H
         C.eta_mlp3_train_fwd(rec, tgt_norm, self.blob, H, self.norm, 2.0 / self.global_batch,
-                             self.xf, self.w3slab, self.dz2t, self.dh1t, self.dyb, self.sq_err, self.step_ctr)
+                             self.xf, self.w3slab, self.dz2r, self.sq_err, self.step_ctr)
         ldg = H + 16
-        C.train_wgrad(self.xf, rec.shape[0], self.blob, H, self.dz2t, self.dh1t, self.slab2, self.slab)
+        C.train_bwd(self.xf, rec.shape[0], self.blob, H, self.dz2r, self.slab2, self.slab)
         C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg + ldg:],
                        self.w3slab, self.G[H * ldg:H * ldg + ldg])
 
