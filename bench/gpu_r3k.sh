@@ -1,6 +1,6 @@
 # round 3: PMC passes for the v3 training kernels (train_bwd_kernel, single-pass forward) at 1M rows
 ROOT=$GRAFT_REPO_ROOT
-O=$ROOT/gpurun_out/r3k; mkdir -p $O
+O=$ROOT/gpurun_out/${TAG:-r3k}; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_INSTS_VMEM GRBM_GUI_ACTIVE SQ_INSTS_SALU"
 G2="SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA"

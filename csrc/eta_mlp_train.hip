@@ -134,6 +134,29 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
   float* const dyscr = reinterpret_cast<float*>(smem + L::BLOB) + wpb * LDA + (threadIdx.x >> 6) * 32;
   for (int c = lane; c < LDA; c += 64) w3part[c] = 0.f;
 
+  // The next tile's records and targets are copied into LDS (global_load_lds) at the top of the
+  // current tile, BEFORE its stores, and read back after a counted wait: a register load issued after
+  // the stores waits for all of them (vmcnt is in order), and a register prefetch carried across the
+  // loop got a vmcnt(0) from the compiler at the loop head — either way the store latency was exposed
+  // once per tile (PMC r3k2: waves waiting 53% of their cycles).  Per wave: [2][32] records (16 B) +
+  // [2][32] targets past the dy scratch; zeroed first so rows past B only ever see finite values.
+  typedef __attribute__((address_space(3))) void lds_void_t;
+  unsigned char* const pfb = smem + L::BLOB + (size_t)wpb * (LDA + 32) * 4 + (size_t)(threadIdx.x >> 6) * 1280;
+  for (int i = lane; i < 80; i += 64) reinterpret_cast<int4*>(pfb)[i] = make_int4(0, 0, 0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // the zeros land before any DMA write
+  auto prefetch = [&](int t, int pb) {      // pb: buffer 0/1; all lanes call, lanes < 32 load
+    const int rw = t * 32 + lane;
+    if (lane < 32 && rw < B) {
+      __builtin_amdgcn_global_load_lds((const void*)(rec + rw), (lds_void_t*)(pfb + pb * 512), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(target + rw), (lds_void_t*)(pfb + 1024 + pb * 128), 4, 0, 0);
+    }
+  };
+  int pbuf = 0;
+  {
+    const int tile0 = blockIdx.x * wpb + (threadIdx.x >> 6);
+    if (tile0 < ntiles) prefetch(tile0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   for (int tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntiles; tile += stride) {
     // nothing is hoisted out of the tile loop: the LDS-resident weights (W1 fragments, biases)
     // and the lane-derived LDS addresses are re-derived per tile.  Hoisted, they exceed the
@@ -145,7 +168,19 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     const int r = lv & 31, h = lv >> 5;
     const int row = tile * 32 + r;
     const bool valid = row < B;
-    const int4 rc = valid ? rec[row] : make_int4(0, 0, 0, 0);
+    // this tile's copy was issued at the top of the previous tile, followed by that tile's KS + 2
+    // stores (the dz2 chunks, the xf row, the squared error: a tile always has a valid row 0).  The
+    // LDS reads are inline asm: through plain loads the compiler adds its own vmcnt(0) for the DMA
+    int4 rc;
+    float tgt;
+    {
+      const unsigned a_rc = (unsigned)(uintptr_t)(pfb + pbuf * 512) + 16u * r;
+      const unsigned a_tg = (unsigned)(uintptr_t)(pfb + 1024 + pbuf * 128) + 4u * r;
+      asm volatile("s_waitcnt vmcnt(%2)\n\tds_read_b128 %0, %3\n\tds_read_b32 %1, %4\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(rc), "=&v"(tgt) : "n"(KS + 2), "v"(a_rc), "v"(a_tg) : "memory");
+    }
+    if (tile + stride < ntiles) prefetch(tile + stride, pbuf ^ 1);
+    pbuf ^= 1;
     const bf16x8 xb = featurize_bf16(rc, h, np);
     if (valid)  // slots 14, 15 hold 1.0 (the b1 hi/lo inputs): dW1k[:,14] == db1
       *reinterpret_cast<bf16x8*>(xf + (size_t)row * 16 + 8 * h) = xb;
@@ -180,9 +215,19 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
           xk8[k][t] = xk[k][t] + 256;
           __asm__ volatile("" : "+v"(xk8[k][t]));
         }
+      // per-hidden-tile row bases, opaque: with lrow + mt * 16384 visible the compiler paired the reads
+      // of two hidden tiles into ds_read2st64_b64, which conflicts with itself (1.5 conflict cycles
+      // per LDS instruction, PMC r3k2)
+      lds_u8* pmv[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        uintptr_t v = (uintptr_t)(lrow + mt * 16384);
+        __asm__ volatile("" : "+v"(v));
+        pmv[mt] = (lds_u8*)v;
+      }
       // units 16ks + 4h + 0..3 and 16ks + 8 + 4h + 0..3 of hidden tile mt: the permuted k order of h1
       auto frag = [&](int mt, int ks) {
-        lds_u8* pm = lrow + mt * 16384;
+        lds_u8* pm = pmv[mt];
         const int* xo = (ks >> 3) ? xk8[ks & 7] : xk[ks & 7];
         const s16x4 lo = *reinterpret_cast<const lds_s16x4*>(pm + xo[0]);
         const s16x4 hi = *reinterpret_cast<const lds_s16x4*>(pm + xo[1]);
@@ -232,7 +277,7 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     const float b3 = reinterpret_cast<const float*>(w3p + H / 4)[0];   // (per tile: not held in a VGPR)
     ys += __shfl_xor(ys, 32);
     const float y = ys + b3;
-    const float diff = valid ? (y - target[row]) : 0.f;
+    const float diff = valid ? (y - tgt) : 0.f;
     const float dy = gscale * diff;
     // per-row squared error (no cross-lane reduction: its shuffle addresses were the values the
     // compiler spilled)
@@ -330,6 +375,25 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     for (int k = 0; k < wpb; ++k) acc += part[k * LDA + c];
     w3slab[(size_t)blockIdx.x * LDA + c] = acc;
   }
+}
+
+// acc += a x b with the accumulator pinned to AGPRs.  train_bwd_kernel's 256 dW2 accumulators fill
+// the AGPR file; through the builtin, the register allocator parked them in VGPRs and copied every
+// tile in and out of AGPRs around each MFMA (32 v_accvgpr moves per MFMA pair).  Only other MFMAs
+// of the same shape read these registers inside the loop (SrcC = the previous D: no wait states);
+// the epilogue reads them after the loop has ended.
+__device__ __forceinline__ void mfma32_acc(f32x16& acc, const bf16x8 a, const bf16x8 b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+// the same with a VGPR accumulator (the dgrad's, which VALU reads after the loop: the reader must
+// first pass mfma_drain, the hazard recognizer does not see inline asm)
+__device__ __forceinline__ void mfma32_vacc(f32x16& acc, const bf16x8 a, const bf16x8 b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+// 24 wait states after the last inline-asm MFMA that wrote x, y, before VALU reads them (an XDL write
+// followed by a VALU read of the same VGPRs needs up to 18); the operands tie the order
+__device__ __forceinline__ void mfma_drain(f32x16& x, f32x16& y) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(x), "+v"(y));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -501,33 +565,42 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
       }
       return f;
     };
-    AFrags cur = lda(0);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      asm volatile("" : "+v"(rbase), "+v"(tbase));
-      bf16x8 wv[2][2];
+    auto ldw = [&](int mt, bf16x8 (&wv)[2][2]) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const lds_u8c* wf = (const lds_u8c*)(uintptr_t)(wb0[i] + 2048u * mt);
         wv[i][0] = *reinterpret_cast<const lds_bf16x8*>(wf);
         wv[i][1] = *reinterpret_cast<const lds_bf16x8*>(wf + 1024);
       }
+    };
+    AFrags cur = lda(0);
+    bf16x8 wc[2][2];
+    ldw(0, wc);
+    // VALU-written MFMA operands (h1t, the zeroed accd) get their wait states before the first
+    // inline-asm MFMA reads them
+    asm volatile("s_nop 4" : "+v"(h1t[0][0]), "+v"(h1t[0][1]), "+v"(h1t[1][0]), "+v"(h1t[1][1]),
+                 "+v"(accd[0]), "+v"(accd[1]));
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      asm volatile("" : "+v"(rbase), "+v"(tbase));
       AFrags nxt = cur;
-      if (mt + 1 < MT) nxt = lda(mt + 1);
+      bf16x8 wn[2][2];
+      if (mt + 1 < MT) {
+        nxt = lda(mt + 1);
+        ldw(mt + 1, wn);
+      }
       asm volatile("" ::: "memory");
-      // dW2: dz2^T of hidden tile mt (lane m: the unit in image column 32mt + m, rows in the k order
-      // of h1t) x h1^T
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        acc2[mt][i] = mfma32(cur.t[0], h1t[i][0], acc2[mt][i]);
-        acc2[mt][i] = mfma32(cur.t[1], h1t[i][1], acc2[mt][i]);
-      }
-      // dgrad: dh1^T(u1 block) += dz2 (rows on lanes) x W2[:, block]
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        accd[i] = mfma32(cur.a0, wv[i][0], accd[i]);
-        accd[i] = mfma32(cur.a1, wv[i][1], accd[i]);
-      }
+      // four independent accumulation chains interleaved (a dependent MFMA waits for its
+      // predecessor's result): dW2 = dz2^T (lane m: the unit in image column 32mt + m, rows in the k
+      // order of h1t) x h1^T, and the dgrad dh1^T(u1 block) += dz2 (rows on lanes) x W2[:, block]
+      mfma32_acc(acc2[mt][0], cur.t[0], h1t[0][0]);
+      mfma32_acc(acc2[mt][1], cur.t[0], h1t[1][0]);
+      mfma32_vacc(accd[0], cur.a0, wc[0][0]);
+      mfma32_vacc(accd[1], cur.a0, wc[1][0]);
+      mfma32_acc(acc2[mt][0], cur.t[1], h1t[0][1]);
+      mfma32_acc(acc2[mt][1], cur.t[1], h1t[1][1]);
+      mfma32_vacc(accd[0], cur.a1, wc[0][1]);
+      mfma32_vacc(accd[1], cur.a1, wc[1][1]);
       if ((mt >> 1) == w) {            // db2 of this wave's own two z2 tiles (wave-uniform)
         const u32x4v q0 = __builtin_bit_cast(u32x4v, cur.t[0]), q1 = __builtin_bit_cast(u32x4v, cur.t[1]);
         float sacc = 0.f;
@@ -539,7 +612,15 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
         db2[mt & 1] += sacc;
       }
       cur = nxt;
+      if (mt + 1 < MT) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          wc[i][0] = wn[i][0];
+          wc[i][1] = wn[i][1];
+        }
+      }
     }
+    mfma_drain(accd[0], accd[1]);
     // dW1 += (dh1 * relu'(z1))^T x: x^T as the B operand (features on the lanes)
     const f32x16 xt = mfma32(x, eye, zero);
     const bf16x8 xb0 = pack(xt, 0, false), xb1 = pack(xt, 1, false);
@@ -557,6 +638,9 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
       acc1[i] = mfma32(__builtin_bit_cast(bf16x8, g1), xb1, acc1[i]);
     }
   }
+  // the last dW2 MFMAs were issued through inline asm, which the hazard recognizer does not see: give
+  // them their 16 passes before the epilogue reads the accumulators
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   // D[m][n]: lane -> n = col, register e -> m = (e&3) + 8(e>>2) + 4h; rows / columns to the bucket's
   // hperm order (the stored unit order of every other gradient path)
   float* o2 = slab2 + (size_t)blockIdx.x * H * LDG;
@@ -718,7 +802,7 @@ static hipError_t launch_train_fwd_h(const void* rec, const float* target, int B
   using L = TrainLayout<H>;
   constexpr int TPB = TRAIN_TPB;
   // the blob + the waves' dW3 partials [TPB / 64][H + 16] f32 + their dy scratch [TPB / 64][32]
-  constexpr size_t LDS = L::BLOB + (size_t)(TPB / 64) * (H + 16 + 32) * 4;
+  constexpr size_t LDS = L::BLOB + (size_t)(TPB / 64) * ((H + 16 + 32) * 4 + 1280);
   static_assert(LDS <= 160 * 1024, "training kernel LDS budget");
   static bool attr_set[64] = {};
   int dev = 0;

@@ -59,6 +59,10 @@ def _run(cmd: List[str]) -> None:
 NO_SLP = {"eta_mlp_fwd.hip"}
 # host code that must round exactly like Python (csrc/runtime/route_core.h): no FMA contraction
 NO_CONTRACT = {"native_server.hip", "route_service.hip"}
+# builtin MFMAs write VGPRs: train_bwd_kernel pins its 256 dW2 accumulators to the AGPRs (inline-asm
+# MFMAs), and with the default heuristic the builtin MFMAs beside them also took AGPR destinations,
+# which made the allocator park accumulator tiles in VGPRs and copy them around every MFMA
+MFMA_VGPR = {"eta_mlp_train.hip"}
 
 
 def build_C(force: bool = False, jobs: int = 8) -> str:
@@ -81,6 +85,8 @@ def build_C(force: bool = False, jobs: int = 8) -> str:
             extra = ["-fno-slp-vectorize"] if os.path.basename(src) in NO_SLP else []
             if os.path.basename(src) in NO_CONTRACT:
                 extra.append("-ffp-contract=off")
+            if os.path.basename(src) in MFMA_VGPR:
+                extra += ["-mllvm", "-amdgpu-mfma-vgpr-form"]
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common, *extra, "-munsafe-fp-atomics",
                               "-I", CSRC, "-I", os.path.join(ROCM, "include"), "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
