@@ -437,8 +437,14 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 31, h = lane >> 5;
   const int nw = blockDim.x >> 6;
   const int ntiles = (B + 31) >> 5;
-  const int t0 = blockIdx.x * tiles_per_slice;
-  const int t1 = min(ntiles, t0 + tiles_per_slice);
+  // slice s takes tiles s, s + S, s + 2S, ... in DESCENDING order: the forward wrote the tiles in
+  // rounds of increasing index, so every slice starts on the most recently written tiles, which are
+  // still in the 256 MB last-level cache, instead of half the slices streaming the oldest from HBM
+  const int S = gridDim.x;
+  const int nmine = blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / S + 1 : 0;
+  auto tile_at = [&](int i) { return (int)blockIdx.x + (nmine - 1 - i) * S; };
+  (void)tiles_per_slice;
+  const int t0 = 0, t1 = nmine;                              // loop positions
 
   // the W2 B-fragment image (kept by adamw_pack_kernel past the forward's blob) into LDS, and the
   // first dz2 tile behind it
@@ -446,17 +452,24 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
   for (int c = w; c < (int)(MT * RBF / 64); c += nw)
     __builtin_amdgcn_global_load_lds((const void*)(w2g + (size_t)c * 1024 + 16 * lane),
                                      (lds_void_t*)(w2s + c * 64), 16, 0, 0);
+  // the per-tile dz2 copy is issued through inline asm: issued with the builtin, the compiler tracks
+  // it as a pending LDS write and put a vmcnt(0) before the first LDS read of the CURRENT tile — the
+  // next tile's copy was then waited for right after it was issued (the loop-top vmcnt(0) + barrier
+  // is what orders it)
   auto stage = [&](int tile, int buf) {
     const bf16x8* src = dz2r + (size_t)tile * RBF;
-    for (int c = w; c < KS; c += nw)
-      __builtin_amdgcn_global_load_lds((const void*)(src + c * 64 + lane), (lds_void_t*)(rb + buf * RBF + c * 64),
-                                       16, 0, 0);
+    for (int c = w; c < KS; c += nw) {
+      const unsigned ldst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(rb + buf * RBF + c * 64));
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src + c * 64 + lane), "s"(ldst) : "memory");
+    }
   };
   const bf16x8* xg = reinterpret_cast<const bf16x8*>(xf);    // row r, half h = chunk 2r + h
   bf16x8 xn;
   if (t0 < t1) {
-    stage(t0, 0);
-    xn = xg[(size_t)t0 * 64 + 2 * col + h];
+    stage(tile_at(t0), 0);
+    xn = xg[(size_t)tile_at(t0) * 64 + 2 * col + h];
   }
   const bf16x8* w1p = reinterpret_cast<const bf16x8*>(blob + L::W2B);
   // this wave's two W2 B-fragment blocks in the LDS image (absolute addresses: lane base + immediates)
@@ -514,17 +527,19 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     return __builtin_bit_cast(bf16x8, o);
   };
 
-  for (int tile = t0; tile < t1; ++tile) {
-    const int buf = (tile - t0) & 1;
+  for (int it = t0; it < t1; ++it) {
+    const int buf = (it - t0) & 1;
     // this wave's share of the tile (and, on the first pass, of the W2 image) has landed; after the
     // barrier every wave's share has, and every wave has finished reading the other buffer
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (xn passes through the wait as an asm operand: read as a plain load result, the compiler put a
+    // vmcnt(0) after the NEXT tile's loads below and serialised the whole prefetch)
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(xn) :: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const bf16x8 x = xn;
-    if (tile + 1 < t1) {
-      stage(tile + 1, buf ^ 1);
-      xn = xg[(size_t)(tile + 1) * 64 + 2 * col + h];
+    if (it + 1 < t1) {
+      stage(tile_at(it + 1), buf ^ 1);
+      xn = xg[(size_t)tile_at(it + 1) * 64 + 2 * col + h];
     }
     // the tile image as an absolute LDS address (dynamic LDS starts at 0: no static __shared__ here),
     // so every read is a lane base + an immediate offset
