@@ -3,44 +3,35 @@
 // all: notebooks/.gitkeep; its feature schema is RO/Flaskr/ml.py:35-51.)
 //
 // One training step on a rank (routest_amd/train/fused.py::FusedMlp3Trainer):
-//   1. eta_mlp3_train_fwd_kernel (this file): featurize + layer 1 + layer 2 + layer 3 + MSE
-//      gradient + the whole input-gradient path dz2 -> dh1 = dz2 W2 -> dz1 = dh1 * relu'(z1) in
-//      ONE launch.  Because dL/dz2 = dy * w3 * relu'(z2) needs only the ReLU mask, dz2 is
-//      produced in-register the moment y (hence dy) is known, and it IS the B operand of the dgrad
-//      MFMAs (accumulator layout == next-MFMA B layout, common.h); W2 is read a second time from
-//      the same LDS image through the hardware-transposed ds_read_b64_tr_b16 as the A operand
-//      W2^T; h1, still in registers, gives relu'(z1).  No library GEMM, no dh1 round trip.
-//      Emits, bf16 row-major:
-//        xf  [B,16]   the exact bf16 features the MFMA consumed, slot 14 := 1 (bias-grad column)
-//        h1a [B,H+16] relu(z1) with column H := 1   (dW2 | db2 = dz2^T h1a)
-//        h2a [B,H+16] relu(z2) with column H := 1   (dW3 | db3 = dy^T h2a)
-//        dz2 [B,H], dz1 [B,H], dy [B,8] (col 0; pre-scaled by 2 / global_batch), per-row
-//        squared errors.
-//      The kernel never reads back what it stored (a load waits for every older store of the
-//      wave: vmcnt counts both, in order), and nothing it needs per tile is hoisted out of the
-//      tile loop (hoisted, it exceeds the VGPR budget and every spill reload after the stores
-//      stalls the same way).
-//   2. the three weight-gradient GEMMs (K = batch) on the split-K wgrad kernel (wgrad.hip) + one
-//      deterministic slab reduction.
+//   1. eta_mlp3_train_fwd_kernel: featurize + layer 1 + ONE pass over layer 2 + layer 3 + MSE
+//      gradient.  Layers 1 and 2 stream over k with all hidden-tile accumulators live; relu(z2) is
+//      kept packed to bf16 in registers, so the dW3 | db3 partial needs only an exact MFMA transpose
+//      per hidden tile (no second layer-2 pass).  dL/dz2 = dy * w3 * relu'(z2) is formed in-register
+//      once y (hence dy) is known.  Emits xf [B,16] (the exact bf16 features, slot 14 := 1), the dz2
+//      tile images (512 B per row, [32 rows][H hperm columns] with a XOR chunk swizzle), the per-row
+//      squared errors and one dW3 | db3 row per workgroup.  Records and targets of the next tile are
+//      copied into LDS before the tile's stores (vmcnt is in order: a load issued after the stores
+//      waits for all of them).
+//   2. train_bwd_kernel: dgrad dh1 = dz2 W2 against an LDS image of W2 in B-fragment order,
+//      relu'(z1) from h1 recomputed on the layer-1 MFMA, dW2 | db2 from the dz2 tile read transposed
+//      (ds_read_b64_tr_b16) and dW1 — one kernel, split-K over the batch, then one deterministic
+//      slab reduction (wgrad_reduce).  Nothing but dz2 and xf crosses HBM between the two kernels
+//      (round 2 moved dz2^T + dh1^T, 1 KB per row, and ran the dgrad in the forward).
 //   3. ONE flat fp32 gradient bucket -> one RCCL all-reduce over xGMI.
 //   4. adamw_pack_kernel: AdamW on the flat fp32 master params, writing back the training blob the
-//      next forward stages into LDS — no host work, no sync, so the whole step is capturable in a
-//      HIP graph.
+//      next forward stages into LDS and the backward's W2 fragment image — no host work, no sync, so
+//      the whole step is capturable in a HIP graph.
 //
-// Training blob (TrainLayout): [ w2img | w1p | b1p | b2p | w3p | tail ] where w2img holds W2
-// row-major in 512-byte rows (natural unit order both ways) with 8-byte chunk k of row R at chunk
-// k ^ w2swz(R).  That one image serves both operand reads conflict-free (bank rule,
-// cdna_hip_programming.md §2 / MI355X_MICROARCH.md §LDS):
-//   * layer 2, A = W2: lane (r, h) of tile (mt, ks) reads row 32mt + r, units 16ks + 4h .. +3 and
-//     16ks + 8 + 4h .. +3 (the permuted k order of the h1 B fragments) with two ds_read_b64:
-//     w2swz is a bijection of R mod 32, so a 32-lane half hits 64 distinct banks;
-//   * dgrad, A = W2^T: ds_read_b64_tr_b16 over 4-row x 16-column blocks (rows 16ks + 4h + q and
-//     16ks + 8 + 4h + q, columns 32mi + 16g .. +15): w2swz moves the 4 rows of a block to 4
-//     different 8-chunk groups, so a 32-lane half touches 64 distinct banks.
-// Natural column order is what makes relu'(z1) lane-local: dgrad accumulator register e of lane
-// half h is unit 32mi + 8(e>>2) + 4h + (e&3), element e&7 of the lane's own h1 fragment.
-// The rest of the blob is the inference layout (mlp3_tile.h): w1p, b1p, b2p, w3p, tail.
+// Training blob (TrainLayout): [ w2img | w1p | b1p | b2p | w3p | tail | w2frag ] where w2img holds
+// W2 row-major in 512-byte rows (natural unit order both ways) with 8-byte chunk k of row R at chunk
+// k ^ w2swz(R): layer 2's A operand, lane (r, h) of tile (mt, ks) reads row 32mt + r, units
+// 16ks + 4h .. +3 and 16ks + 8 + 4h .. +3 (the permuted k order of the h1 B fragments) with two
+// ds_read_b64 — w2swz is a bijection of R mod 32, so a 32-lane half hits 64 distinct banks (bank rule,
+// cdna_hip_programming.md §2 / MI355X_MICROARCH.md §LDS).  w1p .. tail is the inference layout
+// (mlp3_tile.h); w2frag (w2frag_index) is the backward's B-fragment image, lane-linear per fragment.
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "lds_fill.h"
 #include "mlp3_tile.h"
@@ -399,33 +390,50 @@ __device__ __forceinline__ void mfma_drain(f32x16& x, f32x16& y) {
 // ---------------------------------------------------------------------------------------------
 // The whole backward below dz2 in ONE kernel: dh1 = dz2 W2 (dgrad), dz1 = dh1 * relu'(z1),
 // dW2 | db2 = dz2^T [h1 | 1] and dW1 = dz1^T x, K = batch, split over k-slices (one workgroup per
-// CU, each a contiguous run of 32-row tiles).  Inputs per row: the forward's dz2 fragments
-// (512 B) and the 32-byte feature row — half the bytes of the round-2 pair dz2^T + dh1^T, and
-// the forward no longer runs the dgrad or any transpose.
+// CU; slice s takes every S-th 32-row tile, newest first, so it starts on tiles the forward wrote
+// last, still in the last-level cache).  Inputs per row: the forward's dz2 tile image (512 B) and the
+// 32-byte feature row — half the bytes of the round-2 pair dz2^T + dh1^T, and the forward no longer
+// runs the dgrad or any transpose.
 //
 // One wave per SIMD (4 waves at H = 256, 512 registers each); wave w owns the hidden units
 // u1 = 64w .. 64w + 63 of h1 (two 32-unit n-blocks), so per 32-row tile it:
 //   * recomputes h1^T for its two n-blocks on the layer-1 MFMA (x as A, the w1p fragment as B:
 //     units on the lanes, rows in the registers = the dW2 B operand, and relu'(z1) in the layout
 //     of its own dh1^T tile) — no redundant layer-1 work across waves;
-//   * runs the dgrad with dz2 as the A operand (rows on the lanes, as the forward stored it) and
+//   * runs the dgrad with dz2 as the A operand (row reads of the tile image: rows on the lanes) and
 //     W2's column block as B, read from an LDS image of W2 in B-fragment order (ds_read_b128,
 //     conflict-free): D = dh1 with the units on the lanes and the rows in the registers, i.e. dh1^T
 //     in the dW1 A layout;
-//   * transposes every dz2 fragment pair exactly (MFMA against a permuted identity, as the forward
-//     does for relu(z2)) into dz2^T, the dW2 A operand, and accumulates dW2 for all 256 z2 units x
-//     its 64 h1 units: 16 accumulator tiles = 256 registers, resident for the whole slice;
+//   * reads the same tile image transposed (ds_read_b64_tr_b16) as dz2^T, the dW2 A operand, and
+//     accumulates dW2 for all 256 z2 units x its 64 h1 units: 16 accumulator tiles = 256 AGPRs,
+//     resident for the whole slice (inline-asm MFMAs pin them; the builtin MFMAs beside them are
+//     compiled in VGPR form, tools/build_ext.py MFMA_VGPR);
 //   * transposes x once for dW1's B operand.
-// 87 MFMAs per wave and tile, no LDS writes: the dz2 tile (16 KB) is double-buffered in LDS by
-// global_load_lds issued one tile ahead (every wave reads all of it), x rows arrive by plain loads
-// one tile ahead, and one barrier per tile separates the stages.  LDS = W2 image (H*H*2 B) + two dz2
-// tiles (2 * H * 64 B): exactly 160 KB at H = 256.
+// 71 MFMAs per wave and tile, no LDS writes: the dz2 tile (16 KB) is double-buffered in LDS by
+// global_load_lds issued one tile ahead through inline asm (issued with the builtin, the compiler's
+// LDS-DMA tracking put a vmcnt(0) before the first read of the CURRENT tile and serialised the
+// prefetch), x rows arrive by plain loads one tile ahead, and one barrier per tile separates the
+// stages; within a tile the fragments of hidden tile mt + 1 are read while mt's 8 MFMAs (four
+// interleaved accumulation chains) run.  LDS = W2 image (H*H*2 B) + two dz2 tiles (2 * H * 64 B):
+// exactly 160 KB at H = 256.  Measured at 1M rows: 377 us (profiles/train_kernel_stats_1m_r3_v3.csv).
 // Partial sums of slice s go to slab[s] in the bucket layout (hperm rows and columns,
 // train/fused.py); wgrad_reduce sums them in a fixed order (deterministic).
-template <int H>
+// PROF (ROUTEST_TRAIN_BWD_PROF=1, diagnostics only): s_memtime per tile segment — [0] the loop-top
+// wait + barrier, [1] staging issue + layer 1, [2] the hidden-tile loop, [3] dW1 — summed per wave
+// into prof[wave][4] (scalar registers: the timed code keeps its VGPR allocation)
+template <int H, int PROF = 0>
 __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     const __bf16* __restrict__ xf, int B, const unsigned char* __restrict__ blob,
-    const bf16x8* __restrict__ dz2r, int tiles_per_slice, float* __restrict__ slab2, float* __restrict__ slab1) {
+    const bf16x8* __restrict__ dz2r, float* __restrict__ slab2, float* __restrict__ slab1,
+    unsigned long long* __restrict__ prof = nullptr) {
+  unsigned long long pt[4] = {0, 0, 0, 0}, tprev = 0;
+  auto mark = [&](int seg) {
+    if constexpr (PROF) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (seg >= 0) pt[seg] += t - tprev;
+      tprev = t;
+    }
+  };
   using L = TrainLayout<H>;
   constexpr int MT = H / 32, KS = H / 16, LDG = H + 16, RBF = KS * 64;
   typedef __attribute__((address_space(3))) void lds_void_t;
@@ -443,7 +451,6 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
   const int S = gridDim.x;
   const int nmine = blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / S + 1 : 0;
   auto tile_at = [&](int i) { return (int)blockIdx.x + (nmine - 1 - i) * S; };
-  (void)tiles_per_slice;
   const int t0 = 0, t1 = nmine;                              // loop positions
 
   // the W2 B-fragment image (kept by adamw_pack_kernel past the forward's blob) into LDS, and the
@@ -529,6 +536,7 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
 
   for (int it = t0; it < t1; ++it) {
     const int buf = (it - t0) & 1;
+    mark(-1);
     // this wave's share of the tile (and, on the first pass, of the W2 image) has landed; after the
     // barrier every wave's share has, and every wave has finished reading the other buffer
     // (xn passes through the wait as an asm operand: read as a plain load result, the compiler put a
@@ -536,6 +544,7 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(xn) :: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    mark(0);
     const bf16x8 x = xn;
     if (it + 1 < t1) {
       stage(tile_at(it + 1), buf ^ 1);
@@ -545,18 +554,20 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     // so every read is a lane base + an immediate offset
     // layer 1 for the two n-blocks: h1^T (units on the lanes, rows in the registers)
     bf16x8 h1t[2][2];
-    unsigned m1[2];                    // relu'(z1) bits in the accumulator-register order
+    // (relu on the packed bf16 pairs, v_pk_max_i16 — and relu'(z1) is read back off the same packed
+    // values below: one wave per SIMD issues VALU at 4 cycles, and the per-element compare/select
+    // mask this replaces was ~150 VALU per tile)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const f32x16 hz = mfma32(x, w1f[i], zero);
-      h1t[i][0] = pack(hz, 0, true);
-      h1t[i][1] = pack(hz, 1, true);
-      unsigned mk = 0;
+      float zf[16];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) mk |= (hz[e] > 0.f ? 1u : 0u) << e;
-      m1[i] = mk;
+      for (int e = 0; e < 16; ++e) zf[e] = hz[e];
+      relu_cvt_bf16x8(zf, &h1t[i][0]);
+      relu_cvt_bf16x8(zf + 8, &h1t[i][1]);
     }
     f32x16 accd[2] = {zero, zero};
+    mark(1);
     // dz2 fragments of hidden tile mt — the dgrad's row-read pair and dW2's two transposed k-steps —
     // are read one hidden tile ahead, the tile's 4 W2 B fragments at its start (the dW2 MFMAs run
     // while they arrive).  The bases pass through an empty asm per hidden tile, so the XORs are
@@ -600,7 +611,7 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
       asm volatile("" : "+v"(rbase), "+v"(tbase));
       AFrags nxt = cur;
       bf16x8 wn[2][2];
-      if (mt + 1 < MT) {
+      if (mt + 1 < MT && PROF < 2) {
         nxt = lda(mt + 1);
         ldw(mt + 1, wn);
       }
@@ -608,14 +619,22 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
       // four independent accumulation chains interleaved (a dependent MFMA waits for its
       // predecessor's result): dW2 = dz2^T (lane m: the unit in image column 32mt + m, rows in the k
       // order of h1t) x h1^T, and the dgrad dh1^T(u1 block) += dz2 (rows on lanes) x W2[:, block]
-      mfma32_acc(acc2[mt][0], cur.t[0], h1t[0][0]);
-      mfma32_acc(acc2[mt][1], cur.t[0], h1t[1][0]);
-      mfma32_vacc(accd[0], cur.a0, wc[0][0]);
-      mfma32_vacc(accd[1], cur.a0, wc[1][0]);
-      mfma32_acc(acc2[mt][0], cur.t[1], h1t[0][1]);
-      mfma32_acc(acc2[mt][1], cur.t[1], h1t[1][1]);
-      mfma32_vacc(accd[0], cur.a1, wc[0][1]);
-      mfma32_vacc(accd[1], cur.a1, wc[1][1]);
+      if (PROF != 4) {
+        mfma32_acc(acc2[mt][0], cur.t[0], h1t[0][0]);
+        mfma32_acc(acc2[mt][1], cur.t[0], h1t[1][0]);
+      }
+      if (PROF != 3) {
+        mfma32_vacc(accd[0], cur.a0, wc[0][0]);
+        mfma32_vacc(accd[1], cur.a0, wc[1][0]);
+      }
+      if (PROF != 4) {
+        mfma32_acc(acc2[mt][0], cur.t[1], h1t[0][1]);
+        mfma32_acc(acc2[mt][1], cur.t[1], h1t[1][1]);
+      }
+      if (PROF != 3) {
+        mfma32_vacc(accd[0], cur.a1, wc[0][1]);
+        mfma32_vacc(accd[1], cur.a1, wc[1][1]);
+      }
       if ((mt >> 1) == w) {            // db2 of this wave's own two z2 tiles (wave-uniform)
         const u32x4v q0 = __builtin_bit_cast(u32x4v, cur.t[0]), q1 = __builtin_bit_cast(u32x4v, cur.t[1]);
         float sacc = 0.f;
@@ -626,8 +645,8 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
         }
         db2[mt & 1] += sacc;
       }
-      cur = nxt;
-      if (mt + 1 < MT) {
+      if (PROF < 2) cur = nxt;
+      if (mt + 1 < MT && PROF < 2) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           wc[i][0] = wn[i][0];
@@ -636,22 +655,38 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
       }
     }
     mfma_drain(accd[0], accd[1]);
+    mark(2);
     // dW1 += (dh1 * relu'(z1))^T x: x^T as the B operand (features on the lanes)
     const f32x16 xt = mfma32(x, eye, zero);
     const bf16x8 xb0 = pack(xt, 0, false), xb1 = pack(xt, 1, false);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      // dz1 = dh1 * relu'(z1): a bf16 half survives where h1 = relu(z1) is nonzero.  Per packed pair
+      // (h1 halves in [0, 0x7F80]): x = (w + 0x7FFF7FFF) & 0x80008000 flags the nonzero halves (no
+      // carry crosses a half) and (x << 1) - (x >> 15) widens each flag to 0xFFFF
       u32x4v g0 = __builtin_bit_cast(u32x4v, pack(accd[i], 0, false));
       u32x4v g1 = __builtin_bit_cast(u32x4v, pack(accd[i], 1, false));
+      const u32x4v hw0 = __builtin_bit_cast(u32x4v, h1t[i][0]), hw1 = __builtin_bit_cast(u32x4v, h1t[i][1]);
+      auto nzmask = [](unsigned wv) {
+        const unsigned xv = (wv + 0x7FFF7FFFu) & 0x80008000u;
+        return (xv << 1) - (xv >> 15);
+      };
 #pragma unroll
       for (int q2 = 0; q2 < 4; ++q2) {
-        const unsigned b0 = m1[i] >> (2 * q2), b1 = m1[i] >> (8 + 2 * q2);
-        g0[q2] &= ((b0 & 1u) ? 0xFFFFu : 0u) | ((b0 & 2u) ? 0xFFFF0000u : 0u);
-        g1[q2] &= ((b1 & 1u) ? 0xFFFFu : 0u) | ((b1 & 2u) ? 0xFFFF0000u : 0u);
+        g0[q2] &= nzmask(hw0[q2]);
+        g1[q2] &= nzmask(hw1[q2]);
       }
       acc1[i] = mfma32(__builtin_bit_cast(bf16x8, g0), xb0, acc1[i]);
       acc1[i] = mfma32(__builtin_bit_cast(bf16x8, g1), xb1, acc1[i]);
     }
+    if constexpr (PROF) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      mark(3);
+    }
+  }
+  if constexpr (PROF) {
+    if (lane == 0 && prof != nullptr)
+      for (int k = 0; k < 4; ++k) prof[((size_t)blockIdx.x * nw + w) * 4 + k] = pt[k];
   }
   // the last dW2 MFMAs were issued through inline asm, which the hazard recognizer does not see: give
   // them their 16 passes before the epilogue reads the accumulators
@@ -883,10 +918,50 @@ static hipError_t launch_train_bwd_h(const void* xf, int B, const void* blob, co
     if (e != hipSuccess) return e;
     attr_set[dev & 63] = true;
   }
-  const int ntiles = (B + 31) / 32;
-  const int tps = (ntiles + S - 1) / S;
+  static const bool prof = [] {
+    const char* v = std::getenv("ROUTEST_TRAIN_BWD_PROF");
+    return v != nullptr && std::atoi(v) != 0;
+  }();
+  if (prof) {   // diagnostics: per-segment s_memtime sums, printed per launch (synchronises)
+    static bool attr_p = false;
+    if (!attr_p) {
+      hipError_t e = hipFuncSetAttribute((const void*)train_bwd_kernel<H, 1>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
+      if (e != hipSuccess) return e;
+      attr_p = true;
+    }
+    const int nwv = H / 64;
+    unsigned long long* d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof(unsigned long long) * 4 * S * nwv);
+    if (e != hipSuccess) return e;
+    static const int pmode = std::atoi(std::getenv("ROUTEST_TRAIN_BWD_PROF"));
+#define RT_BWD_PMODE(P)                                                                                   \
+    if (pmode == P) {                                                                                       \
+      (void)hipFuncSetAttribute((const void*)train_bwd_kernel<H, P>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                (int)LDS);                                                                  \
+      hipLaunchKernelGGL((train_bwd_kernel<H, P>), dim3(S), dim3(H), LDS, stream, (const __bf16*)xf, B,    \
+                         (const unsigned char*)blob, (const bf16x8*)dz2r, slab2, slab1, d);                \
+    } else
+    RT_BWD_PMODE(2) RT_BWD_PMODE(3) RT_BWD_PMODE(4) {
+#undef RT_BWD_PMODE
+      hipLaunchKernelGGL((train_bwd_kernel<H, 1>), dim3(S), dim3(H), LDS, stream, (const __bf16*)xf, B,
+                         (const unsigned char*)blob, (const bf16x8*)dz2r, slab2, slab1, d);
+    }
+    std::vector<unsigned long long> h((size_t)4 * S * nwv);
+    e = hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return e;
+    double sum[4] = {0, 0, 0, 0};
+    for (size_t i = 0; i < h.size(); ++i) sum[i % 4] += (double)h[i];
+    const double tiles = (double)((B + 31) / 32) / S;
+    std::fprintf(stderr, "[train_bwd prof] per wave-tile (s_memtime ticks): top %.0f  stage+layer1 %.0f  hidden-tile loop %.0f  dW1 %.0f  (tiles/slice %.1f)\n",
+                 sum[0] / (S * nwv) / tiles, sum[1] / (S * nwv) / tiles, sum[2] / (S * nwv) / tiles,
+                 sum[3] / (S * nwv) / tiles, tiles);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(train_bwd_kernel<H>, dim3(S), dim3(H), LDS, stream, (const __bf16*)xf, B,
-                     (const unsigned char*)blob, (const bf16x8*)dz2r, tps, slab2, slab1);
+                     (const unsigned char*)blob, (const bf16x8*)dz2r, slab2, slab1, nullptr);
   return hipGetLastError();
 }
 
