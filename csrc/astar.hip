@@ -25,6 +25,7 @@
 // at length / v_max on the host, so both are admissible and consistent (ALT tables are shrunk by 1e-4
 // against fp32 rounding).  Every search stops within max_iters pops (status 3), on overflow (2) or
 // when the open set empties (1): the grid always drains.
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 
@@ -909,10 +910,38 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
       e = launch_astar_wave(g, src, dst, Q, qidx != nullptr ? qidx + i0 : nullptr, i0, std::min(wave->slots, T - i0),
                             *wave, o, pl.max_iters, pl.delta, stream, arena);
   }
+  // Searches that overflowed because one launch's searches shared the growth arena: rerun them in
+  // the wave tier a chunk at a time (the arena restarts per launch), so each can grow into
+  // ROUTEST_ASTAR_RETRY_ENTRIES (default 2^20) entries — on a 1M-node graph thousands of local legs
+  // overflowed a 32k-search launch's share, and the few big-tier slots then ran them ~100 at a time
+  // for seconds (profiles/astar_scale_1m_r3n.jsonl).  Only what overflows again goes to the big tier.
+  bool wave_timed = false;
+  if (e == hipSuccess && use_wave && arena != nullptr && arena->base != nullptr && arena->entries > 0) {
+    static const unsigned long long per = [] {
+      const char* v = std::getenv("ROUTEST_ASTAR_RETRY_ENTRIES");
+      const long long x = v ? std::atoll(v) : (1ll << 20);
+      return (unsigned long long)(x < 4096 ? 4096 : x);
+    }();
+    int R = 0;
+    e = select_count(o.status, Q, 1 << 2, scratch, stream, R);
+    S.wave_ms = ms_since(t0);
+    wave_timed = true;
+    t0 = std::chrono::steady_clock::now();
+    S.retried = R;
+    if (R > 0) {
+      const unsigned long long c = arena->entries / per;
+      const int chunk = (int)std::max<unsigned long long>(64, std::min<unsigned long long>((unsigned long long)wave->slots, c));
+      for (int i0 = 0; i0 < R && e == hipSuccess; i0 += chunk)
+        e = launch_astar_wave(g, src, dst, Q, scratch + i0, 0, std::min(chunk, R - i0), *wave, o, pl.max_iters,
+                              pl.delta, stream, arena);
+    }
+    S.retry_ms = ms_since(t0);
+    t0 = std::chrono::steady_clock::now();
+  }
   if (e == hipSuccess && big != nullptr) {
     int E = 0;
     e = select_count(o.status, Q, 1 << 2, scratch, stream, E);
-    S.wave_ms = ms_since(t0);
+    if (!wave_timed) S.wave_ms = ms_since(t0);
     t0 = std::chrono::steady_clock::now();
     S.escalated = E;
     for (int i0 = 0; i0 < E && e == hipSuccess; i0 += big->slots)

@@ -738,7 +738,7 @@ static bool ws_from(const py::object& o, rt::AstarWs& ws, const torch::Device& d
 }
 
 // The tiered batched A* (csrc/astar.hip astar_search).  Returns [lane queries, wave queries,
-// escalated queries, lane ms, wave ms, big ms].
+// escalated queries, lane ms, wave ms, big ms, retried queries, retry ms].
 std::vector<double> astar_search(torch::Tensor indptr, torch::Tensor indices, torch::Tensor cost, torch::Tensor lat,
                                  torch::Tensor lon, double inv_vmax, c10::optional<torch::Tensor> landmarks,
                                  torch::Tensor src, torch::Tensor dst, py::object lane, py::object wave,
@@ -820,7 +820,8 @@ std::vector<double> astar_search(torch::Tensor indptr, torch::Tensor indices, to
   RT_CHECK_HIP(rt::astar_search(g, src.data_ptr<int>(), dst.data_ptr<int>(), (int)Q, hl ? &wl : nullptr,
                                 hw ? &ww : nullptr, hb ? &wb : nullptr, o, pl, scratch.data_ptr<int>(),
                                 cur_stream(lat), &st, ab.base ? &ab : nullptr));
-  return {(double)st.lane, (double)st.wave, (double)st.escalated, st.lane_ms, st.wave_ms, st.big_ms};
+  return {(double)st.lane, (double)st.wave, (double)st.escalated, st.lane_ms, st.wave_ms, st.big_ms,
+          (double)st.retried, st.retry_ms};
 }
 
 torch::Tensor forest_predict(torch::Tensor records, torch::Tensor values, torch::Tensor info,

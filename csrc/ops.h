@@ -155,6 +155,8 @@ struct AstarPlan {
 struct AstarRunStats {
   int lane = 0, wave = 0, escalated = 0;
   double lane_ms = 0, wave_ms = 0, big_ms = 0;
+  int retried = 0;              // wave-tier overflows rerun a few at a time (larger arena share)
+  double retry_ms = 0;
 };
 bool astar_ws_ok(const AstarWs& ws, bool wave);
 hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* dst, int Q, int q0,

@@ -348,7 +348,8 @@ class BatchedAstar:
                                  self.big_tier.ws() if self.big_tier else None, out_cost, out_len, out_status,
                                  out_path, self.last_iters, self.scratch, self.max_iters, self.lane_pops,
                                  self.wave_only_below, self.wave_delta, self.arena, self.arena_ctr)
-        self.last_stats = dict(zip(("lane", "wave", "escalated", "lane_ms", "wave_ms", "big_ms"), st))
+        self.last_stats = dict(zip(("lane", "wave", "escalated", "lane_ms", "wave_ms", "big_ms", "retried",
+                                    "retry_ms"), st))
         self.last_tail = int(st[1])
         self.last_escalated = int(st[2])
         self._exact_fallback(s, t, out_cost, out_len, out_status, out_path)

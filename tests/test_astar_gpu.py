@@ -117,6 +117,21 @@ def test_overflowed_searches_escalate_to_the_big_tier(graph_and_cost):
     assert np.array_equal(c, c2)
 
 
+def test_arena_overflows_are_retried_in_chunks(graph_and_cost):
+    """A growth arena far too small for one launch's searches (2 MB for 300 concurrent searches):
+    the searches that overflowed are rerun in the wave tier a chunk at a time (each chunk gets the
+    whole, reset arena) before anything reaches the big tier — optimal costs, arena restored."""
+    g, cost, _ = graph_and_cost
+    src, dst = synth_route_queries(g, 300, seed=3)
+    a = BatchedAstar(g, cost, "cuda:0", slots=512, cap=128, arena_gb=0.002)
+    c, n, st, p = a.run(src, dst)
+    assert a.last_stats["retried"] > 0 and a.last_fallbacks == 0, a.last_stats
+    assert a.last_escalated <= a.last_stats["retried"]
+    assert (st.cpu().numpy() == 0).all()
+    np.testing.assert_allclose(c.cpu().numpy(), dijkstra_ref(g, cost, src, dst), rtol=1e-4)
+    assert bool((a.arena == -1).all())
+
+
 def test_overflowed_searches_finish_exactly_on_host(graph_and_cost):
     """Without an arena or a big tier the overflowed searches are finished by the exact host
     fallback."""
