@@ -14,6 +14,7 @@ reference's per-request remote ORS matrix + greedy loop + per-trip directions
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import numpy as np
@@ -71,7 +72,14 @@ class BulkRouteStep:
         # several waves of searches in flight (sparse per-search tables: ~33 GB of HBM3E in all)
         legs_est = int(sum(len(s) for s in snapped) * 1.4) + 1024
         slots = min(legs_est, max_slots)
-        self.astar = astar or BatchedAstar(g, cost, d, slots=slots, wave_slots=min(slots, 32768), arena_gb=16)
+        # the searches left after the lane tier's pop budget (~56k of 80k here) in ONE wave-tier launch
+        # with 2^14-entry starting tables (fewer growth steps): 163 -> 142 ms per 10k-request step
+        # on the 100k-node graph (bench/gpu_r3q.sh, profiles/route_tiering_ab_r3q.jsonl).  Workspace:
+        # lane tier ~8 GB, wave tier ~26 GB, big tier ~4 GB, growth arena 16 GB (of 288 GB HBM3E)
+        ws = int(os.environ.get("ROUTEST_BULK_WAVE_SLOTS", "65536"))
+        tb = int(os.environ.get("ROUTEST_BULK_WAVE_TBITS", "14"))
+        self.astar = astar or BatchedAstar(g, cost, d, slots=slots, wave_slots=min(slots, ws), arena_gb=16,
+                                           wave_tbits=tb)
 
     def legs(self):
         """K5 + K6 for every request, then the trip legs as (src, dst) node tensors on the device."""

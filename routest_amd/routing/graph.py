@@ -212,7 +212,8 @@ class BatchedAstar:
     def __init__(self, g: RoadGraph, cost: np.ndarray, device, slots: int = 16384, cap: int = 16384,
                  max_path: int = 4096, max_iters: int = 2_000_000, landmarks: int = 32,
                  landmark_method: str = "farthest", wave_slots: Optional[int] = None,
-                 big_slots: Optional[int] = None, arena_gb: Optional[float] = None):
+                 big_slots: Optional[int] = None, arena_gb: Optional[float] = None,
+                 wave_tbits: Optional[int] = None):
         from ..ops import _ext
         self.C = _ext.native(required=True)
         self.g = g
@@ -260,7 +261,9 @@ class BatchedAstar:
         # tables start at 2**wave_tbits entries and grow 2x at a time into a shared arena, so their
         # memory follows the searches instead of a fixed worst case per slot
         cap = max(128, (int(cap) + 7) // 8 * 8)
-        wave_tbits = min(int(os.environ.get("ROUTEST_ASTAR_WAVE_TBITS", "13")), _pow2_bits(2 * cap))
+        if wave_tbits is None:
+            wave_tbits = int(os.environ.get("ROUTEST_ASTAR_WAVE_TBITS", "13"))
+        wave_tbits = min(int(wave_tbits), _pow2_bits(2 * cap))
         if self.lane_pops > 0:
             lane_tbits = max(8, _pow2_bits(8 * self.lane_pops))
             lane_cap = max(64, 1 << (lane_tbits - 1))
