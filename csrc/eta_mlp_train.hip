@@ -923,12 +923,12 @@ static hipError_t launch_train_bwd_h(const void* xf, int B, const void* blob, co
     return v != nullptr && std::atoi(v) != 0;
   }();
   if (prof) {   // diagnostics: per-segment s_memtime sums, printed per launch (synchronises)
-    static bool attr_p = false;
-    if (!attr_p) {
+    static bool attr_p[64] = {};
+    if (!attr_p[dev & 63]) {
       hipError_t e = hipFuncSetAttribute((const void*)train_bwd_kernel<H, 1>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
       if (e != hipSuccess) return e;
-      attr_p = true;
+      attr_p[dev & 63] = true;
     }
     const int nwv = H / 64;
     unsigned long long* d = nullptr;
