@@ -74,6 +74,9 @@ struct AstarArena {
 };
 
 constexpr int KMAX = 32;
+// diagnostics: the wave tier records f-band passes instead of expansions in out_iters
+__constant__ int c_count_passes = 0;
+__device__ __forceinline__ bool count_passes_flag() { return c_count_passes != 0; }
 // edges relaxed per batch of independent loads (road-graph degrees are 2-6, mostly 4-5)
 constexpr int RB = 4;
 
@@ -577,6 +580,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   int nnear = 1;
   float thr = heur(s) + delta;
   long long expanded = 0;
+  int passes = 0;                                   // f-band passes (diagnostics: ROUTEST_ASTAR_COUNT_PASSES)
   int status = 1;
   while (true) {
     while (nnear > 0) {
@@ -679,6 +683,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         }
       }
       expanded += nnear;
+      ++passes;
       __syncthreads();
       nnear = s_next < ncap_nxt ? s_next : ncap_nxt;
       curA = !curA;
@@ -743,7 +748,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       len = write_path(a, tab, (unsigned)ptt, s, q);
       if (len < 0) { status = 4; len = 0; }
     }
-    if (a.out_iters) a.out_iters[q] = (int)(expanded < 0x7fffffff ? expanded : 0x7fffffff);
+    if (a.out_iters)
+      a.out_iters[q] = count_passes_flag() ? passes : (int)(expanded < 0x7fffffff ? expanded : 0x7fffffff);
     a.out_cost[q] = status == 0 ? total : -1.f;
     a.out_len[q] = len;
     a.out_status[q] = status;
@@ -846,6 +852,20 @@ hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* 
   if (!astar_ws_ok(ws, true)) return hipErrorInvalidValue;
   if (qidx == nullptr && q0 + n > Q) return hipErrorInvalidValue;
   const AstarArgs a = make_args(g, src, dst, Q, q0, ws, o, max_iters);
+  static const int count_passes = [] {
+    const char* v = std::getenv("ROUTEST_ASTAR_COUNT_PASSES");
+    return v != nullptr && std::atoi(v) != 0 ? 1 : 0;
+  }();
+  if (count_passes) {
+    static bool set[64] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (!set[dev & 63]) {
+      hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_count_passes), &count_passes, sizeof(int));
+      if (e != hipSuccess) return e;
+      set[dev & 63] = true;
+    }
+  }
   AstarArena ar{nullptr, 0, nullptr};
   if (arena != nullptr && arena->base != nullptr && arena->ctr != nullptr && arena->entries > 0) {
     // every search of the previous launch restored what it used: start the bump pointer over
