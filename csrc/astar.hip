@@ -801,6 +801,86 @@ __global__ __launch_bounds__(1024) void astar_select_kernel(const int* __restric
   if (threadIdx.x == 0) *count = base;
 }
 
+// The same compaction for the wave tier, ordered LONGEST FIRST: a stable counting sort on NBK buckets
+// of log2(great-circle src-dst distance), descending.  One launch holds more searches than the chip
+// has wave slots, and a search's f-band passes grow with the leg's length (bench/astar_passes.py:
+// p50 235, max 1508 passes), so a long leg dispatched late ran alone at the end of the launch; issuing
+// long legs first lets the short ones fill in behind them (longest-processing-time-first).  Stable
+// within a bucket and independent of timing, so slots and tie results stay deterministic.
+constexpr int NBK = 32;
+__device__ __forceinline__ int lpt_bucket(const float* lat, const float* lon, int s, int t) {
+  const float k = 0.017453292519943295f;
+  const float la = lat[s] * k, lb = lat[t] * k;
+  const float s1 = __sinf(0.5f * (lb - la)), s2 = __sinf(0.5f * (lon[t] - lon[s]) * k);
+  const float hv = s1 * s1 + __cosf(la) * __cosf(lb) * s2 * s2;
+  const float d = 2.f * 6371000.f * asinf(sqrtf(fminf(1.f, fmaxf(0.f, hv))));   // metres
+  // two buckets per octave above 100 m, longest legs in bucket 0
+  const int b = d > 100.f ? (int)(2.f * __log2f(d * 0.01f)) : 0;
+  return NBK - 1 - (b < 0 ? 0 : (b > NBK - 1 ? NBK - 1 : b));
+}
+
+__global__ __launch_bounds__(1024) void astar_select_lpt_kernel(const int* __restrict__ status, int Q, int want,
+                                                                const int* __restrict__ src,
+                                                                const int* __restrict__ dst,
+                                                                const float* __restrict__ lat,
+                                                                const float* __restrict__ lon,
+                                                                int* __restrict__ qidx, int* __restrict__ count) {
+  __shared__ int hist[NBK];            // per-bucket counts, then running output offsets
+  __shared__ int wcnt[16][NBK];        // this chunk's per-wave bucket counts
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x < NBK) hist[threadIdx.x] = 0;
+  __syncthreads();
+  auto bucket_of = [&](int i) {
+    const int sv = i < Q ? status[i] : -1;
+    const bool f = sv >= 0 && sv < 31 && ((want >> sv) & 1);
+    return f ? lpt_bucket(lat, lon, src[i], dst[i]) : -1;
+  };
+  for (int i0 = 0; i0 < Q; i0 += 1024) {
+    const int b = bucket_of(i0 + (int)threadIdx.x);
+    if (b >= 0) atomicAdd(&hist[b], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int k = 0; k < NBK; ++k) {
+      const int c = hist[k];
+      hist[k] = run;
+      run += c;
+    }
+    *count = run;
+  }
+  __syncthreads();
+  for (int i0 = 0; i0 < Q; i0 += 1024) {
+    const int i = i0 + (int)threadIdx.x;
+    const int b = bucket_of(i);
+    for (int k = lane; k < NBK; k += 64) wcnt[wv][k] = 0;
+    // lanes of this wave with the same bucket, one ballot per distinct bucket present
+    unsigned long long same = 0;
+    unsigned long long todo = __ballot(b >= 0);
+    while (todo) {
+      const int l0 = __ffsll((long long)todo) - 1;
+      const int b0 = __shfl(b, l0);
+      const unsigned long long m = __ballot(b == b0);
+      if (b == b0) same = m;
+      if (lane == l0) wcnt[wv][b0] = __popcll(m);
+      todo &= ~m;
+    }
+    __syncthreads();
+    if (b >= 0) {
+      int off = hist[b] + __popcll(same & ((1ull << lane) - 1));
+      for (int k = 0; k < wv; ++k) off += wcnt[k][b];
+      qidx[off] = i;
+    }
+    __syncthreads();
+    if (threadIdx.x < NBK) {
+      int s = 0;
+      for (int k = 0; k < 16; ++k) s += wcnt[k][threadIdx.x];
+      hist[threadIdx.x] += s;
+    }
+    __syncthreads();
+  }
+}
+
 static AstarArgs make_args(const AstarGraphDev& g, const int* src, const int* dst, int Q, int q0,
                            const AstarWs& ws, const AstarOut& o, int max_iters) {
   return AstarArgs{g.indptr, g.indices, g.cost, g.lat, g.lon, src, dst, (AEnt*)ws.tab,
@@ -895,6 +975,18 @@ static hipError_t select_count(const int* status, int Q, int want, int* scratch,
   return e;
 }
 
+static hipError_t select_count_lpt(const AstarGraphDev& g, const int* src, const int* dst, const int* status, int Q,
+                                   int want, int* scratch, hipStream_t stream, int& count) {
+  hipLaunchKernelGGL(astar_select_lpt_kernel, dim3(1), dim3(1024), 0, stream, status, Q, want, src, dst, g.lat, g.lon,
+                     scratch, scratch + Q);
+  hipError_t e = hipGetLastError();
+  int h = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&h, scratch + Q, sizeof(int), hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  count = h;
+  return e;
+}
+
 hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, int Q, const AstarWs* lane,
                         const AstarWs* wave, const AstarWs* big, const AstarOut& o, const AstarPlan& pl,
                         int* scratch, hipStream_t stream, AstarRunStats* st, const AstarArenaBuf* arena) {
@@ -915,8 +1007,14 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
       e = launch_astar_lane(g, src, dst, Q, q0, *lane, o, iters, stream);
     S.lane = Q;
     if (e == hipSuccess && use_wave) {
-      // pop budget spent (3) or the small table/heap overflowed (2): continue in the wave tier
-      e = select_count(o.status, Q, (1 << 2) | (1 << 3), scratch, stream, T);
+      // pop budget spent (3) or the small table/heap overflowed (2): continue in the wave tier,
+      // longest legs first (ROUTEST_ASTAR_LPT=0: query order)
+      static const bool lpt = [] {
+        const char* v = std::getenv("ROUTEST_ASTAR_LPT");
+        return v == nullptr || std::atoi(v) != 0;
+      }();
+      if (lpt) e = select_count_lpt(g, src, dst, o.status, Q, (1 << 2) | (1 << 3), scratch, stream, T);
+      else e = select_count(o.status, Q, (1 << 2) | (1 << 3), scratch, stream, T);
       qidx = scratch;
     }
     S.lane_ms = ms_since(t0);
