@@ -255,12 +255,12 @@ __device__ __forceinline__ int write_path(const AstarArgs& a, const AEnt* tab, u
 // ---------------------------------------------------------------------------------------------
 // Lane tier: one lane per query, a private table (no atomics), lazy-deletion heap of (f, node).
 template <int K, int D>
-__global__ __launch_bounds__(64) void astar_kernel(AstarArgs a) {
+__global__ __launch_bounds__(64) void astar_kernel(AstarArgs a, const int* __restrict__ qidx, int n) {
   // XCD-aware: workgroup b runs on XCD b % 8; give each XCD a contiguous range of queries
   const int lb = (int)(blockIdx.x % 8u) * (int)(gridDim.x / 8u) + (int)(blockIdx.x / 8u);
   const int slot = lb * blockDim.x + threadIdx.x;
-  const int q = a.q0 + slot;
-  if (q >= a.Q || slot >= a.S) return;
+  if (slot >= a.S || slot >= n) return;
+  const int q = qidx != nullptr ? qidx[slot] : a.q0 + slot;
   const int tb = a.tbits;
   const unsigned mask = (1u << tb) - 1u;
   const int tcap = 1 << (tb - 1);
@@ -881,6 +881,50 @@ __global__ __launch_bounds__(1024) void astar_select_lpt_kernel(const int* __res
   }
 }
 
+// Lane/wave split by leg length: legs longer than `thr_m` (great circle) would spend the lane tier's
+// whole pop budget and then start over in the wave tier, so they skip the lane tier (status 3 = "pop
+// budget spent" routes them to the wave tier's selection); the short ones are compacted, in query
+// order, into qidx for the lane tier.
+__global__ __launch_bounds__(1024) void astar_split_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                           const float* __restrict__ lat,
+                                                           const float* __restrict__ lon, int Q, float thr_m,
+                                                           int* __restrict__ status, int* __restrict__ qidx,
+                                                           int* __restrict__ count) {
+  __shared__ int wsum[16];
+  __shared__ int base;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const float k = 0.017453292519943295f;
+  for (int i0 = 0; i0 < Q; i0 += 1024) {
+    const int i = i0 + (int)threadIdx.x;
+    bool f = false;
+    if (i < Q) {
+      const int s = src[i], t = dst[i];
+      const float la = lat[s] * k, lb = lat[t] * k;
+      const float s1 = __sinf(0.5f * (lb - la)), s2 = __sinf(0.5f * (lon[t] - lon[s]) * k);
+      const float hv = s1 * s1 + __cosf(la) * __cosf(lb) * s2 * s2;
+      const float d = 2.f * 6371000.f * asinf(sqrtf(fminf(1.f, fmaxf(0.f, hv))));
+      f = d <= thr_m;
+      if (!f) status[i] = 3;
+    }
+    const unsigned long long m = __ballot(f);
+    if (lane == 0) wsum[wv] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int j = 0; j < wv; ++j) off += wsum[j];
+    if (f) qidx[off + __popcll(m & ((1ull << lane) - 1))] = i;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int sum = 0;
+      for (int j = 0; j < 16; ++j) sum += wsum[j];
+      base += sum;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *count = base;
+}
+
 static AstarArgs make_args(const AstarGraphDev& g, const int* src, const int* dst, int Q, int q0,
                            const AstarWs& ws, const AstarOut& o, int max_iters) {
   return AstarArgs{g.indptr, g.indices, g.cost, g.lat, g.lon, src, dst, (AEnt*)ws.tab,
@@ -895,8 +939,9 @@ bool astar_ws_ok(const AstarWs& ws, bool wave) {
 }
 
 hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* dst, int Q, int q0,
-                             const AstarWs& ws, const AstarOut& o, int max_iters, hipStream_t stream) {
-  const int n = min(ws.slots, Q - q0);
+                             const AstarWs& ws, const AstarOut& o, int max_iters, hipStream_t stream,
+                             const int* qidx, int nq) {
+  const int n = min(ws.slots, qidx != nullptr ? nq : Q - q0);
   if (n <= 0) return hipSuccess;
   if (g.lm != nullptr && g.K != 32 && g.K != 16 && g.K != 8) return hipErrorInvalidValue;
   if (!astar_ws_ok(ws, false)) return hipErrorInvalidValue;
@@ -911,10 +956,10 @@ hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* 
   }();
 #define RT_ASTAR_LANE(D)                                                                          \
   do {                                                                                            \
-    if (g.lm == nullptr) hipLaunchKernelGGL((astar_kernel<0, D>), grid, block, 0, stream, a);     \
-    else if (g.K == 8) hipLaunchKernelGGL((astar_kernel<8, D>), grid, block, 0, stream, a);       \
-    else if (g.K == 16) hipLaunchKernelGGL((astar_kernel<16, D>), grid, block, 0, stream, a);     \
-    else hipLaunchKernelGGL((astar_kernel<32, D>), grid, block, 0, stream, a);                    \
+    if (g.lm == nullptr) hipLaunchKernelGGL((astar_kernel<0, D>), grid, block, 0, stream, a, qidx, n);     \
+    else if (g.K == 8) hipLaunchKernelGGL((astar_kernel<8, D>), grid, block, 0, stream, a, qidx, n);       \
+    else if (g.K == 16) hipLaunchKernelGGL((astar_kernel<16, D>), grid, block, 0, stream, a, qidx, n);     \
+    else hipLaunchKernelGGL((astar_kernel<32, D>), grid, block, 0, stream, a, qidx, n);                    \
   } while (0)
   if (arity == 2) RT_ASTAR_LANE(2);
   else if (arity == 4) RT_ASTAR_LANE(4);
@@ -1003,9 +1048,27 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
   int T = 0;
   if (use_lane) {
     const int iters = use_wave ? std::min(pl.max_iters, pl.lane_pops) : pl.max_iters;
-    for (int q0 = 0; q0 < Q && e == hipSuccess; q0 += lane->slots)
-      e = launch_astar_lane(g, src, dst, Q, q0, *lane, o, iters, stream);
-    S.lane = Q;
+    // legs longer than ROUTEST_ASTAR_LANE_MAX_M metres (great circle; 0 = no split) skip the lane tier
+    float lane_max_m = pl.lane_max_m;
+    if (lane_max_m < 0.f) {
+      const char* v = std::getenv("ROUTEST_ASTAR_LANE_MAX_M");
+      lane_max_m = v != nullptr ? (float)std::atof(v) : 0.f;
+    }
+    if (use_wave && lane_max_m > 0.f) {
+      int L = 0;
+      hipLaunchKernelGGL(astar_split_kernel, dim3(1), dim3(1024), 0, stream, src, dst, g.lat, g.lon, Q, lane_max_m,
+                         o.status, scratch, scratch + Q);
+      e = hipGetLastError();
+      if (e == hipSuccess) e = hipMemcpyAsync(&L, scratch + Q, sizeof(int), hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      for (int q0 = 0; q0 < L && e == hipSuccess; q0 += lane->slots)
+        e = launch_astar_lane(g, src, dst, Q, 0, *lane, o, iters, stream, scratch + q0, std::min(lane->slots, L - q0));
+      S.lane = L;
+    } else {
+      for (int q0 = 0; q0 < Q && e == hipSuccess; q0 += lane->slots)
+        e = launch_astar_lane(g, src, dst, Q, q0, *lane, o, iters, stream);
+      S.lane = Q;
+    }
     if (e == hipSuccess && use_wave) {
       // pop budget spent (3) or the small table/heap overflowed (2): continue in the wave tier,
       // longest legs first (ROUTEST_ASTAR_LPT=0: query order)

@@ -746,7 +746,8 @@ std::vector<double> astar_search(torch::Tensor indptr, torch::Tensor indices, to
                                  torch::Tensor out_status, torch::Tensor out_path,
                                  c10::optional<torch::Tensor> out_iters, torch::Tensor scratch, int64_t max_iters,
                                  int64_t lane_pops, int64_t wave_only_below, double delta,
-                                 c10::optional<torch::Tensor> arena, c10::optional<torch::Tensor> arena_ctr) {
+                                 c10::optional<torch::Tensor> arena, c10::optional<torch::Tensor> arena_ctr,
+                                 double lane_max_m) {
   for (auto* t : {&indptr, &indices, &cost, &lat, &lon, &src, &dst, &out_cost, &out_len, &out_status, &out_path,
                   &scratch})
     check_dev(*t, "astar tensor");
@@ -803,6 +804,7 @@ std::vector<double> astar_search(torch::Tensor indptr, torch::Tensor indices, to
   pl.lane_pops = (int)lane_pops;
   pl.wave_only_below = (int)wave_only_below;
   pl.delta = (float)delta;
+  pl.lane_max_m = (float)lane_max_m;
   rt::AstarRunStats st;
   rt::AstarArenaBuf ab;
   if (arena.has_value() && arena->defined()) {
@@ -986,6 +988,7 @@ static rt::RouteServiceCfg route_cfg_from(const py::dict& d, int device, const v
     if (has("wave_only_below")) c.wave_only_below = d["wave_only_below"].cast<int>();
     c.inv_vmax = d["inv_vmax"].cast<float>();
     c.wave_delta = d["wave_delta"].cast<float>();
+    if (has("lane_max_m")) c.lane_max_m = d["lane_max_m"].cast<float>();
     TORCH_CHECK(c.glat && c.glon && c.indptr && c.indices && c.cost && c.lat32 && c.lon32 &&
                     (c.lane_ws.slots > 0 || c.wave_ws.slots > 0) && c.N > 0 && c.max_path > 0,
                 "graph route config incomplete");
@@ -1201,7 +1204,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("landmarks"), py::arg("src"), py::arg("dst"), py::arg("lane"), py::arg("wave"), py::arg("big"),
         py::arg("out_cost"), py::arg("out_len"), py::arg("out_status"), py::arg("out_path"), py::arg("out_iters"),
         py::arg("scratch"), py::arg("max_iters"), py::arg("lane_pops"), py::arg("wave_only_below"),
-        py::arg("delta"), py::arg("arena") = py::none(), py::arg("arena_ctr") = py::none());
+        py::arg("delta"), py::arg("arena") = py::none(), py::arg("arena_ctr") = py::none(),
+        py::arg("lane_max_m") = -1.0);
   m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
   m.def("forest_predict_lds", &forest_predict_lds, "K4: LDS-staged tree chunks, 2 walks per thread");
   m.def("pscore_create", &pscore_create, "resident single-request scorer kernel on the blob's GPU");

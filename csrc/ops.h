@@ -151,6 +151,8 @@ struct AstarPlan {
   int lane_pops = 500;          // <= 0: lane tier only, run to max_iters
   int wave_only_below = 32768;  // fewer queries than this: skip the lane tier
   float delta = 10.f;           // wave tier f-band width (seconds)
+  float lane_max_m = -1.f;      // legs longer than this (great circle, m) skip the lane tier; 0: none;
+                                // < 0: ROUTEST_ASTAR_LANE_MAX_M, read per search (default 0)
 };
 struct AstarRunStats {
   int lane = 0, wave = 0, escalated = 0;
@@ -160,7 +162,8 @@ struct AstarRunStats {
 };
 bool astar_ws_ok(const AstarWs& ws, bool wave);
 hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* dst, int Q, int q0,
-                             const AstarWs& ws, const AstarOut& o, int max_iters, hipStream_t stream);
+                             const AstarWs& ws, const AstarOut& o, int max_iters, hipStream_t stream,
+                             const int* qidx = nullptr, int nq = 0);   // qidx: run queries qidx[0..nq)
 hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* dst, int Q, const int* qidx,
                              int q0, int T, const AstarWs& ws, const AstarOut& o, int max_iters, float delta,
                              hipStream_t stream, const AstarArenaBuf* arena = nullptr);

@@ -44,7 +44,7 @@ struct RouteServiceCfg {
   AstarArenaBuf arena;                    // growth arena of the wave/big tiers (optional)
   int max_path = 4096, max_iters = 2000000, lane_pops = 500;
   int wave_only_below = 32768;            // fewer unique legs than this: every search in the wave tier
-  float inv_vmax = 0.f, wave_delta = 10.f;
+  float inv_vmax = 0.f, wave_delta = 10.f, lane_max_m = -1.f;
   // ETA model for use_ml_eta (the fused K1+K2 kernel's 32x32 weight blob on this device)
   const void* eta_blob = nullptr;
   int H = 0, variant = -1, num_cus = 256;

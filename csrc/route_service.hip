@@ -531,6 +531,7 @@ struct RouteService::Impl {
     pl.lane_pops = cfg.lane_pops;
     pl.wave_only_below = cfg.wave_only_below;
     pl.delta = cfg.wave_delta;
+    pl.lane_max_m = cfg.lane_max_m;
     AstarRunStats rs;
     if (e == hipSuccess)
       e = astar_search(gd, d_src.d, d_dst.d, Q, cfg.lane_ws.slots > 0 ? &cfg.lane_ws : nullptr,

@@ -167,6 +167,20 @@ def landmark_tables(g: RoadGraph, cost: np.ndarray, k: int = 16, seed: int = 0,
     return out.reshape(g.num_nodes, 2 * k)
 
 
+def median_edge_m(g: RoadGraph, sample: int = 1 << 16) -> float:
+    """Median great-circle edge length (metres) over an evenly strided sample of the edges."""
+    ip = np.asarray(g.indptr)
+    ix = np.asarray(g.indices)
+    if ix.size == 0:
+        return 0.0
+    e = np.arange(0, ix.size, max(1, ix.size // sample))
+    u = np.searchsorted(ip, e, side="right") - 1
+    v = ix[e]
+    la, lb = np.radians(g.lat[u]), np.radians(g.lat[v])
+    hv = np.sin(0.5 * (lb - la)) ** 2 + np.cos(la) * np.cos(lb) * np.sin(0.5 * np.radians(g.lon[v] - g.lon[u])) ** 2
+    return float(np.median(2 * 6371000.0 * np.arcsin(np.sqrt(np.clip(hv, 0.0, 1.0)))))
+
+
 def _pow2_bits(n: int) -> int:
     return max(1, int(np.ceil(np.log2(max(2, n)))))
 
@@ -247,6 +261,11 @@ class BatchedAstar:
         # budget 500 -> 19.3k req/s, 100 -> 24.1k, 1 (all wave) -> 26.2k, 2000 -> 10.3k.
         self.wave_only_below = int(os.environ.get("ROUTEST_ASTAR_WAVE_ONLY_BELOW", "32768"))
         self.wave_delta = float(os.environ.get("ROUTEST_ASTAR_DELTA", "10"))
+        # legs longer than ~8 median edges (great circle) would spend the lane tier's whole pop budget
+        # and start over in the wave tier: they skip the lane tier.  Route step, 100k-node graph
+        # (profiles/astar_lane_split_ab_r3x.jsonl): no split 131.7 ms, 1000 m 124.6 ms, 4000 m 129.3 ms
+        env_m = os.environ.get("ROUTEST_ASTAR_LANE_MAX_M")
+        self.lane_max_m = float(env_m) if env_m is not None else 8.0 * median_edge_m(g)
         if wave_slots is None:
             wave_slots = int(os.environ.get("ROUTEST_ASTAR_WAVE_SLOTS", "16384"))
         self.wave_slots = max(1, min(slots, int(wave_slots)))
@@ -350,7 +369,8 @@ class BatchedAstar:
                                  s, t, self.lane_tier.ws(), self.wave_tier.ws() if self.wave_tier else None,
                                  self.big_tier.ws() if self.big_tier else None, out_cost, out_len, out_status,
                                  out_path, self.last_iters, self.scratch, self.max_iters, self.lane_pops,
-                                 self.wave_only_below, self.wave_delta, self.arena, self.arena_ctr)
+                                 self.wave_only_below, self.wave_delta, self.arena, self.arena_ctr,
+                                 lane_max_m=self.lane_max_m)
         self.last_stats = dict(zip(("lane", "wave", "escalated", "lane_ms", "wave_ms", "big_ms", "retried",
                                     "retry_ms"), st))
         self.last_tail = int(st[1])

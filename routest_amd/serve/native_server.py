@@ -122,6 +122,7 @@ def route_config(provider, device, *, engine: str = "backend:mi355x", compat200:
             "max_path": int(a.max_path), "max_iters": int(a.max_iters), "lane_pops": int(a.lane_pops),
             "wave_only_below": int(a.wave_only_below),
             "inv_vmax": float(a.inv_vmax), "wave_delta": float(a.wave_delta),
+            "lane_max_m": float(a.lane_max_m),
             "_astar": a})
     return cfg
 

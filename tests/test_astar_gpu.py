@@ -154,12 +154,35 @@ def test_lane_tier_overflow_continues_in_the_wave_tier(graph_and_cost, monkeypat
     src, dst = synth_route_queries(g, 1500, seed=4)
     monkeypatch.setenv("ROUTEST_ASTAR_WAVE_ONLY_BELOW", "0")       # force the lane tier
     monkeypatch.setenv("ROUTEST_ASTAR_LANE_POPS", "2000")          # long budget, small tables overflow
+    monkeypatch.setenv("ROUTEST_ASTAR_LANE_MAX_M", "0")            # every leg starts in the lane tier
     a = BatchedAstar(g, cost, "cuda:0", slots=1024)
     a.lane_tier = type(a.lane_tier)(1024, 64, 7, a.dev)            # 128-entry tables: overflow early
     c, n, st, p = a.run(src, dst)
     assert a.last_stats["lane"] == 1500 and a.last_tail > 500, a.last_stats
     st = st.cpu().numpy()
     assert (st == 0).all()
+    np.testing.assert_allclose(c.cpu().numpy(), dijkstra_ref(g, cost, src, dst), rtol=1e-4)
+
+
+def test_long_legs_skip_the_lane_tier_exactly(graph_and_cost, monkeypatch):
+    """ROUTEST_ASTAR_LANE_MAX_M: legs longer than the threshold (great circle) go straight to the wave
+    tier, which takes them longest first; the short ones run the lane tier from a compacted index
+    list.  Every cost stays optimal and exactly the short legs ran the lane tier."""
+    g, cost, _ = graph_and_cost
+    src, dst = synth_route_queries(g, 1500, seed=5)
+    la, lb = np.radians(g.lat[src]), np.radians(g.lat[dst])
+    dl = np.radians(g.lon[dst] - g.lon[src])
+    hv = np.sin(0.5 * (lb - la)) ** 2 + np.cos(la) * np.cos(lb) * np.sin(0.5 * dl) ** 2
+    d = 2 * 6371000.0 * np.arcsin(np.sqrt(np.clip(hv, 0, 1)))
+    thr = float(np.median(d))
+    monkeypatch.setenv("ROUTEST_ASTAR_WAVE_ONLY_BELOW", "0")       # force the lane tier
+    monkeypatch.setenv("ROUTEST_ASTAR_LANE_MAX_M", str(thr))
+    a = BatchedAstar(g, cost, "cuda:0", slots=1024)
+    c, n, st, p = a.run(src, dst)
+    short = int((d <= thr * (1 - 1e-4)).sum())
+    assert short <= a.last_stats["lane"] <= int((d <= thr * (1 + 1e-4)).sum()), (a.last_stats, short)
+    assert a.last_stats["lane"] < 1500
+    assert (st.cpu().numpy() == 0).all()
     np.testing.assert_allclose(c.cpu().numpy(), dijkstra_ref(g, cost, src, dst), rtol=1e-4)
 
 
