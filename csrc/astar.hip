@@ -1072,10 +1072,23 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
     if (e == hipSuccess && use_wave) {
       // pop budget spent (3) or the small table/heap overflowed (2): continue in the wave tier,
       // longest legs first (ROUTEST_ASTAR_LPT=0: query order)
-      static const bool lpt = [] {
+      // Only when the growth arena holds every resident wave-tier search at the largest table it can
+      // reach (2N entries): long searches first means the longest ones grow at the same time, and on
+      // a 1M-node graph that exhausted the arena and sent 18k searches to the chunked retry (1M-node
+      // local step 739 -> 1630 ms; 100k-node route step 150 -> 124.6 ms with it,
+      // profiles/astar_lpt_arena_ab_r3aa.jsonl).  ROUTEST_ASTAR_LPT=0 | 1 forces it off | on.
+      static const int lpt_env = [] {
         const char* v = std::getenv("ROUTEST_ASTAR_LPT");
-        return v == nullptr || std::atoi(v) != 0;
+        return v == nullptr ? -1 : (std::atoi(v) != 0 ? 1 : 0);
       }();
+      bool lpt = lpt_env == 1;
+      if (lpt_env < 0 && arena != nullptr && arena->base != nullptr) {
+        int dev = 0, cus = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const unsigned long long resident = (unsigned long long)cus * 16ull;   // 4 SIMDs x 4 waves
+        lpt = arena->entries >= resident * 2ull * (unsigned long long)g.N;
+      }
       if (lpt) e = select_count_lpt(g, src, dst, o.status, Q, (1 << 2) | (1 << 3), scratch, stream, T);
       else e = select_count(o.status, Q, (1 << 2) | (1 << 3), scratch, stream, T);
       qidx = scratch;
