@@ -330,7 +330,8 @@ void adamw_pack_big(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Te
 // wide trainer: dy / dyb / sq_err from the relu.w3 partials + dz2 from h2a + step counter (one launch)
 void big_dz2y(torch::Tensor ypart, int64_t nparts, torch::Tensor b3_dev, torch::Tensor target, double gscale,
               torch::Tensor dy, torch::Tensor dyb, torch::Tensor sq_err, torch::Tensor h2a,
-              torch::Tensor w3, int64_t H, torch::Tensor dz2, torch::Tensor step_ctr) {
+              torch::Tensor w3, int64_t H, torch::Tensor dz2, torch::Tensor step_ctr,
+              c10::optional<torch::Tensor> slab) {
   for (auto* t : {&ypart, &b3_dev, &target, &dy, &sq_err, &h2a, &w3, &step_ctr}) check_dev(*t, "big_dz2y operand");
   const int64_t B = dz2.size(0);
   check_bf16(dz2, "dz2", B, H);
@@ -343,6 +344,21 @@ void big_dz2y(torch::Tensor ypart, int64_t nparts, torch::Tensor b3_dev, torch::
                   h2a.size(1) >= H && H % 8 == 0, "h2a bf16 [B, >=H]");
   TORCH_CHECK(step_ctr.scalar_type() == torch::kInt32, "step_ctr i32");
   const c10::DeviceGuard guard(h2a.device());
+  if (slab.has_value() && slab->defined()) {
+    // dW3 | db3 partials folded in: slab[s][0 .. H+16) for s < S, summed by wgrad_reduce
+    check_dev(*slab, "slab");
+    TORCH_CHECK(slab->scalar_type() == torch::kFloat32 && slab->dim() == 2 && slab->is_contiguous() &&
+                    slab->size(1) >= H + 16 && slab->size(0) >= 1 && slab->size(0) <= B,
+                "slab f32 [S <= B, >= H + 16]");
+    TORCH_CHECK(H == 512 || H == 1024, "fused dW3 path: H = 512 or 1024");
+    RT_CHECK_HIP(rt::launch_big_dz2y_w3(ypart.data_ptr<float>(), (int)nparts, (int)B, (int)H, b3_dev.data_ptr<float>(),
+                                        target.data_ptr<float>(), (float)gscale, dy.data_ptr<float>(), dyb.data_ptr(),
+                                        sq_err.data_ptr<float>(), h2a.data_ptr(), (int)h2a.size(1),
+                                        w3.data_ptr<float>(), dz2.data_ptr(), step_ctr.data_ptr<int>(),
+                                        slab->data_ptr<float>(), (long long)slab->size(1), (int)slab->size(0),
+                                        cur_stream(h2a)));
+    return;
+  }
   RT_CHECK_HIP(rt::launch_big_dz2y(ypart.data_ptr<float>(), (int)nparts, (int)B, (int)H, b3_dev.data_ptr<float>(),
                                    target.data_ptr<float>(), (float)gscale, dy.data_ptr<float>(), dyb.data_ptr(),
                                    sq_err.data_ptr<float>(), h2a.data_ptr(), (int)h2a.size(1),
@@ -1175,7 +1191,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("target") = py::none(), py::arg("gscale") = 0.0, py::arg("dy") = py::none(),
         py::arg("dyb") = py::none(), py::arg("sq_err") = py::none(), py::arg("b3_dev") = py::none());
   m.def("adamw_pack_big", &adamw_pack_big, "wide trainer: AdamW + re-pack of w1p / w2k / w2t / b2 / w3 / b3");
-  m.def("big_dz2y", &big_dz2y, "wide trainer: dy, dyb, squared error, dz2 and the step counter in one launch");
+  m.def("big_dz2y", &big_dz2y,
+        "wide trainer: dy, dyb, squared error, dz2 and the step counter in one launch (+ dW3|db3 slab rows)",
+        py::arg("ypart"), py::arg("nparts"), py::arg("b3"), py::arg("target"), py::arg("gscale"), py::arg("dy"),
+        py::arg("dyb"), py::arg("sq_err"), py::arg("h2a"), py::arg("w3"), py::arg("H"), py::arg("dz2"),
+        py::arg("step_ctr"), py::arg("slab") = py::none());
   m.def("big_dz2", &big_dz2, "dz2 = dy * w3 * relu'(z2) from h2a (hperm order)");
   m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward (one pass over layer 2) + MSE grad + dW3 partial -> dz2 fragments");
   m.def("train_bwd", &train_bwd, "K3: dgrad + relu'(z1) + dW2|db2 and dW1 split-K partials in one kernel (train_bwd_kernel)");

@@ -638,6 +638,110 @@ __global__ __launch_bounds__(256) void big_dz2y_kernel(const float* __restrict__
   }
 }
 
+// The same step with dW3 | db3 folded in (was a separate wgrad launch that streamed h2a a second
+// time): S workgroups of 16 waves, one split-K slice each, write slab[s][0 .. H+16) = sum over the
+// slice's rows of dy * [relu(z2) | 1 | 0...] — the layout wgrad_reduce already sums.  A lane keeps its
+// 8 (H = 512) or 16 (H = 1024) columns' w3 values and dW3 partials in registers for all its rows;
+// rows go two at a time so each wave has two independent load chains in flight; the row loop never
+// re-reads w3 (the round-2 kernel gathered w3[hperm(c)] per element, 8 loads per 16-byte output).
+template <int KC>
+__global__ __launch_bounds__(1024) void big_dz2y_w3_kernel(const float* __restrict__ ypart, int nparts, int B,
+                                                           const float* __restrict__ b3p,
+                                                           const float* __restrict__ target, float gscale,
+                                                           float* __restrict__ dy, __bf16* __restrict__ dyb,
+                                                           float* __restrict__ sq_err,
+                                                           const __bf16* __restrict__ h2a, int lda,
+                                                           const float* __restrict__ w3,
+                                                           __bf16* __restrict__ dz2, int* __restrict__ step_ctr,
+                                                           float* __restrict__ slab, long long slab_ld, int S) {
+  constexpr int H = 512 * KC;
+  __shared__ float red[16][H];
+  __shared__ float dred[16];
+  if (step_ctr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *step_ctr += 1;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int s = blockIdx.x;
+  const int r0 = (int)((long long)s * B / S), r1 = (int)((long long)(s + 1) * B / S);
+  float w3r[KC][8], acc[KC][8];
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      w3r[k][q] = w3[hp(8 * lane + 512 * k + q)];
+      acc[k][q] = 0.f;
+    }
+  const float b3 = b3p[0];
+  float dsum = 0.f;
+  auto row_dy = [&](int m) {
+    float t = lane < nparts ? ypart[(size_t)m * nparts + lane] : 0.f;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+    const float diff = t + b3 - target[m];
+    const float d = gscale * diff;
+    if (lane == 0) {
+      dy[m] = d;
+      sq_err[m] = diff * diff;
+      bf16x8 dv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dv[j] = (__bf16)0.f;
+      dv[0] = (__bf16)d;
+      *reinterpret_cast<bf16x8*>(dyb + (size_t)m * 8) = dv;
+    }
+    return d;
+  };
+  auto row_out = [&](int m, float d, const bf16x8 (&hv)[KC]) {
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      bf16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float h = (float)hv[k][q];                 // relu(z2) >= 0
+        o[q] = (__bf16)(h > 0.f ? d * w3r[k][q] : 0.f);
+        acc[k][q] = __builtin_fmaf(d, h, acc[k][q]);
+      }
+      *reinterpret_cast<bf16x8*>(dz2 + (size_t)m * H + 8 * lane + 512 * k) = o;
+    }
+    dsum += d;
+  };
+  int m = r0 + wv;
+  for (; m + 16 < r1; m += 32) {                         // rows m and m + 16 together
+    bf16x8 ha[KC], hb[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      ha[k] = *reinterpret_cast<const bf16x8*>(h2a + (size_t)m * lda + 8 * lane + 512 * k);
+      hb[k] = *reinterpret_cast<const bf16x8*>(h2a + (size_t)(m + 16) * lda + 8 * lane + 512 * k);
+    }
+    const float da = row_dy(m), db = row_dy(m + 16);
+    row_out(m, da, ha);
+    row_out(m + 16, db, hb);
+  }
+  if (m < r1) {
+    bf16x8 ha[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+      ha[k] = *reinterpret_cast<const bf16x8*>(h2a + (size_t)m * lda + 8 * lane + 512 * k);
+    row_out(m, row_dy(m), ha);
+  }
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[wv][8 * lane + 512 * k + q] = acc[k][q];
+  if (lane == 0) dred[wv] = dsum;
+  __syncthreads();
+  float* out = slab + (long long)s * slab_ld;
+  for (int c = threadIdx.x; c < H; c += 1024) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][c];
+    out[c] = t;
+  }
+  if (threadIdx.x < 16) {                                // db3 (the ones column), zero padding
+    float t = 0.f;
+    if (threadIdx.x == 0)
+      for (int w = 0; w < 16; ++w) t += dred[w];
+    out[H + threadIdx.x] = t;
+  }
+}
+
 struct AdamWBigArgs {
   float lr, beta1, beta2, eps, wd;
   int warmup, total_steps;
@@ -937,6 +1041,22 @@ hipError_t launch_big_dz2y(const float* ypart, int nparts, int B, int H, const f
   hipLaunchKernelGGL(big_dz2y_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, ypart, nparts, B, H, b3p,
                      target, gscale, dy, (__bf16*)dyb, sq_err, (const __bf16*)h2a, lda, w3, (__bf16*)dz2,
                      step_ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_big_dz2y_w3(const float* ypart, int nparts, int B, int H, const float* b3p,
+                              const float* target, float gscale, float* dy, void* dyb, float* sq_err,
+                              const void* h2a, int lda, const float* w3, void* dz2, int* step_ctr, float* slab,
+                              long long slab_ld, int S, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  if ((H != 512 && H != 1024) || nparts > 64 || lda % 8 || S < 1 || S > B || slab_ld < H + 16)
+    return hipErrorInvalidValue;
+#define RT_DZ2Y_W3(KCV)                                                                                        \
+  hipLaunchKernelGGL(big_dz2y_w3_kernel<KCV>, dim3(S), dim3(1024), 0, stream, ypart, nparts, B, b3p, target, gscale, \
+                     dy, (__bf16*)dyb, sq_err, (const __bf16*)h2a, lda, w3, (__bf16*)dz2, step_ctr, slab, slab_ld, S)
+  if (H == 512) RT_DZ2Y_W3(1);
+  else RT_DZ2Y_W3(2);
+#undef RT_DZ2Y_W3
   return hipGetLastError();
 }
 

@@ -66,6 +66,11 @@ hipError_t launch_big_dz2y(const float* ypart, int nparts, int B, int H, const f
                            const float* target, float gscale, float* dy, void* dyb, float* sq_err,
                            const void* h2a, int lda, const float* w3, void* dz2, int* step_ctr,
                            hipStream_t stream);
+// + dW3 | db3: slab[s][0 .. H+16) for s < S (H = 512 or 1024)
+hipError_t launch_big_dz2y_w3(const float* ypart, int nparts, int B, int H, const float* b3p,
+                              const float* target, float gscale, float* dy, void* dyb, float* sq_err,
+                              const void* h2a, int lda, const float* w3, void* dz2, int* step_ctr, float* slab,
+                              long long slab_ld, int S, hipStream_t stream);
 hipError_t launch_big_dz2(const void* h2a, int lda, const float* dy, const float* w3, int B, int H,
                           void* dz2, hipStream_t stream);
 

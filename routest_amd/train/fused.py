@@ -253,10 +253,10 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
       big_layer1        : featurize + layer 1 -> xf, h1a (hperm order, ones column)
       gemm_nt(H2Y)      : z2 = W2 h1 (W2 streamed from L2 through LDS tiles) -> h2a = relu(z2 + b2)
                           + per-64-unit partials of h2 . w3
-      big_yreduce       : y, dy (scaled 2/global_batch), the dy operand, squared errors
-      big_dz2           : dz2 = dy w3 relu'(z2)
+      big_dz2y          : y, dy (scaled 2/global_batch), squared errors, dz2 = dy w3 relu'(z2) and
+                          the dW3|db3 split-K slab rows, h2a streamed once
       gemm_nt(STORE)    : dh1 = dz2 W2 (W2^T operand, kept by the optimizer kernel)
-      wgrad x 3 + reduce: dW2|db2 (column blocks of <= 288), dW3|db3, dW1 (relu'(h1) fused)
+      wgrad x 2 + reduce: dW2|db2 (column blocks of <= 288), dW1 (relu'(h1) fused)
       all_reduce(G)     : one collective on the flat bucket (C1: 4.3 MB at H = 1024)
       adamw_pack_big    : AdamW + re-pack of w1p / w2k / w2t / b2 / w3 / b3
     """
@@ -312,12 +312,12 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
         C.gemm_nt(1, self.w2k, self.h1a, H, B, H, b2=self.b2v, w3=self.w3v, ypart=self.ypart,
                   out=self.h2a)
         # dy / dyb / squared error + dz2 + the device step counter: one launch
+        # ... and dW3|db3 = [h2|1]^T dy into the slab's first H + 16 columns (h2a streamed once)
         C.big_dz2y(self.ypart, H // 64, self.b3v, tgt_norm, 2.0 / self.global_batch, self.dy,
-                   self.dyb, self.sq_err, self.h2a, self.w3v, H, self.dz2, self.step_ctr)
+                   self.dyb, self.sq_err, self.h2a, self.w3v, H, self.dz2, self.step_ctr, self.slab)
         C.gemm_nt(2, self.w2t, self.dz2, H, B, H, out=self.dh1)
         # dW2|db2 = dz2^T [h1|1]: one launch, n-blocks of <= 288 columns in the grid
         C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit2)
-        C.wgrad(self.h2a, ldg, ldg, self.dyb, 8, self.slab, 0, 1, None, 1)
         # dW1 = (dh1 * relu'(h1))^T x: dh1 and its mask h1a are both in the hperm order here
         C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, ldg, 16, self.h1a)
         C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg:])
