@@ -400,13 +400,14 @@ __global__ __launch_bounds__(64) void astar_kernel(AstarArgs a, const int* __res
 // holds near A | near B | far.
 // (waves_per_eu 4: the compiler fits the kernel in 102 VGPRs instead of 136 with no scratch, so four
 // searches per SIMD are resident instead of three; the tier is bound by dependent-load latency)
-template <int K>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void astar_wave_kernel(AstarArgs a, const int* __restrict__ qidx, int T,
+template <int K, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4, 8))) void astar_wave_kernel(AstarArgs a, const int* __restrict__ qidx, int T,
                                                         float delta, AstarArena ar) {
   const int w = blockIdx.x;
   if (w >= T || w >= a.S) return;
   const int q = qidx != nullptr ? qidx[w] : a.q0 + w;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x;                     // thread of the search's workgroup (NW waves)
+  constexpr int NT = 64 * NW;
   // the search's table: the slot's own region first; GROWN (2x per step) into the arena when it
   // fills up — memory follows the search instead of a fixed worst case per slot
   int tb = a.tbits;
@@ -425,6 +426,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   int FCAP = a.cap / 2;                             // (f, node) entries
   bool farena = false;
   __shared__ int s_next, s_far, s_touch, s_bad;
+  __shared__ float s_red[NW];
+  __shared__ int s_wcnt[NW];
   __shared__ unsigned long long s_off;
   const int s = a.src[q], t = a.dst[q];
   const float k = 0.017453292519943295f;
@@ -482,7 +485,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   };
   auto fill_ones = [&](void* p, long long bytes) {     // bytes % 16 == 0
     uint4* q = reinterpret_cast<uint4*>(p);
-    for (long long i = lane; i < bytes / 16; i += 64) q[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    for (long long i = lane; i < bytes / 16; i += NT) q[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
   };
   // a near list able to take `need` ints (its content is dead at the call)
   auto ensure_near = [&](int*& lst, int& cap, bool& inar, int need) -> bool {
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     if (p == nullptr) return false;
     unsigned long long* nf = reinterpret_cast<unsigned long long*>(p);
     const int nfar = s_far < FCAP ? s_far : FCAP;
-    for (int i = lane; i < nfar; i += 64) nf[i] = far[i];
+    for (int i = lane; i < nfar; i += NT) nf[i] = far[i];
     __syncthreads();
     if (farena) fill_ones(far, (long long)FCAP * 8);
     far = nf;
@@ -529,7 +532,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     int* ntouch = reinterpret_cast<int*>(ntab + tsz);
     const unsigned nmask = (unsigned)tsz - 1u;
     const int nt = s_touch < tcap ? s_touch : tcap;
-    for (int i = lane; i < nt; i += 64) {
+    for (int i = lane; i < nt; i += NT) {
       const int o = touched[i];
       const AEnt e = ld_ent(tab + o);
       unsigned p = hslot(e.key, nb);
@@ -543,14 +546,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       tab[o].key = p;                               // old -> new slot (the old table is dead)
     }
     __syncthreads();
-    for (int i = lane; i < nt; i += 64) {
+    for (int i = lane; i < nt; i += NT) {
       const int p = ntouch[i];
       const unsigned long long e = ntab[p].w;
       const unsigned par = w_par(e);
       if (par != NOPAR) ntab[p].w = (e & ~(unsigned long long)NOPAR) | tab[par].key;
     }
     __syncthreads();
-    for (int i = lane; i < nt; i += 64) {
+    for (int i = lane; i < nt; i += NT) {
       clr_ent(tab + touched[i]);
       if (in_arena) touched[i] = -1;
     }
@@ -600,7 +603,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       if (lane == 0) s_next = 0;
       __syncthreads();
       const float best = gbest();
-      for (int i = lane; i < nnear; i += 64) {
+      for (int i = lane; i < nnear; i += NT) {
         if (bad()) break;
         const int v = cur[i];
         // probe with whole-entry loads: the hit is the entry (no second dependent load)
@@ -695,12 +698,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const float best = gbest();
     const int nfar = s_far < FCAP ? s_far : FCAP;
     float fmin = __int_as_float(0x7f800000);
-    for (int i = lane; i < nfar; i += 64) {
+    for (int i = lane; i < nfar; i += NT) {
       const float f = __uint_as_float((unsigned)(far[i] >> 32));
       if (f < best) fmin = fminf(fmin, f);
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) fmin = fminf(fmin, __shfl_xor(fmin, o));
+    if constexpr (NW > 1) {
+      if ((lane & 63) == 0) s_red[lane >> 6] = fmin;
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < NW; ++w) fmin = fminf(fmin, s_red[w]);
+      __syncthreads();
+    }
     if (!(fmin < best)) break;                        // done: best is optimal (or +inf: unreachable)
     thr = fmin + delta;
     // split far in place: f < thr -> near (cur), f < best -> keep (compacted), else drop.  A chunk of
@@ -717,22 +727,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       s_far = 0;
     }
     __syncthreads();
-    for (int i0 = 0; i0 < nfar; i0 += 64) {
+    for (int i0 = 0; i0 < nfar; i0 += NT) {
       const int i = i0 + lane;
       const unsigned long long x = i < nfar ? far[i] : ~0ull;
       const float f = __uint_as_float((unsigned)(x >> 32));
       const bool to_near = i < nfar && f < thr;
       const bool keep = i < nfar && !to_near && f < best;
       const unsigned long long mk = __ballot(keep);
-      const int base = s_far;
+      int base = s_far;
+      int total = __popcll(mk);
+      if constexpr (NW > 1) {                       // kept entries in (wave, lane) order
+        if ((lane & 63) == 0) s_wcnt[lane >> 6] = total;
+        __syncthreads();
+        total = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const int c = s_wcnt[w];
+          if (w < (lane >> 6)) base += c;
+          total += c;
+        }
+      }
       __syncthreads();
-      if (keep) far[base + __popcll(mk & ((1ull << lane) - 1))] = x;
+      if (keep) far[base + __popcll(mk & ((1ull << (lane & 63)) - 1))] = x;
       if (to_near) {
         const int ni = atomicAdd(&s_next, 1);
         if (ni < ncap_cur) cur[ni] = (int)(unsigned)(x & 0xffffffffu);
         else s_bad = 1;
       }
-      if (lane == 0) s_far = base + __popcll(mk);
+      if (lane == 0) s_far = base + total;
       __syncthreads();
     }
     nnear = s_next < ncap_cur ? s_next : ncap_cur;
@@ -757,14 +779,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   __syncthreads();
   const int nt = s_touch;
   if (nt <= tcap) {
-    for (int i = lane; i < nt; i += 64) {
+    for (int i = lane; i < nt; i += NT) {
       clr_ent(tab + touched[i]);
       if (in_arena) touched[i] = -1;
     }
   } else {                                            // claims past the reset list: clear everything
-    for (int i = lane; i <= (int)mask; i += 64) clr_ent(tab + i);
+    for (int i = lane; i <= (int)mask; i += NT) clr_ent(tab + i);
     if (in_arena)
-      for (int i = lane; i < tcap; i += 64) touched[i] = -1;
+      for (int i = lane; i < tcap; i += NT) touched[i] = -1;
   }
   if (narA) fill_ones(nearA, (long long)ncapA * 4);
   if (narB) fill_ones(nearB, (long long)ncapB * 4);
@@ -970,7 +992,7 @@ hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* 
 
 hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* dst, int Q, const int* qidx,
                              int q0, int T, const AstarWs& ws, const AstarOut& o, int max_iters, float delta,
-                             hipStream_t stream, const AstarArenaBuf* arena) {
+                             hipStream_t stream, const AstarArenaBuf* arena, int nw) {
   const int n = T < ws.slots ? T : ws.slots;
   if (n <= 0) return hipSuccess;
   if (g.lm != nullptr && g.K != 32 && g.K != 16 && g.K != 8) return hipErrorInvalidValue;
@@ -998,10 +1020,17 @@ hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* 
     if (e != hipSuccess) return e;
     ar = AstarArena{(AEnt*)arena->base, arena->entries, arena->ctr};
   }
-  if (g.lm == nullptr) hipLaunchKernelGGL(astar_wave_kernel<0>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, ar);
-  else if (g.K == 8) hipLaunchKernelGGL(astar_wave_kernel<8>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, ar);
-  else if (g.K == 16) hipLaunchKernelGGL(astar_wave_kernel<16>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, ar);
-  else hipLaunchKernelGGL(astar_wave_kernel<32>, dim3(n), dim3(64), 0, stream, a, qidx, n, delta, ar);
+#define RT_ASTAR_WAVE(NWV)                                                                                   \
+  do {                                                                                                       \
+    const dim3 blk(64 * NWV);                                                                                \
+    if (g.lm == nullptr) hipLaunchKernelGGL((astar_wave_kernel<0, NWV>), dim3(n), blk, 0, stream, a, qidx, n, delta, ar); \
+    else if (g.K == 8) hipLaunchKernelGGL((astar_wave_kernel<8, NWV>), dim3(n), blk, 0, stream, a, qidx, n, delta, ar);  \
+    else if (g.K == 16) hipLaunchKernelGGL((astar_wave_kernel<16, NWV>), dim3(n), blk, 0, stream, a, qidx, n, delta, ar); \
+    else hipLaunchKernelGGL((astar_wave_kernel<32, NWV>), dim3(n), blk, 0, stream, a, qidx, n, delta, ar);             \
+  } while (0)
+  if (nw >= 4) RT_ASTAR_WAVE(4);
+  else RT_ASTAR_WAVE(1);
+#undef RT_ASTAR_WAVE
   return hipGetLastError();
 }
 
@@ -1110,6 +1139,12 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
   // overflowed a 32k-search launch's share, and the few big-tier slots then ran them ~100 at a time
   // for seconds (profiles/astar_scale_1m_r3n.jsonl).  Only what overflows again goes to the big tier.
   bool wave_timed = false;
+  // the reruns and the big tier hold the LARGE searches (f-bands of thousands of nodes): a workgroup
+  // of ROUTEST_ASTAR_RETRY_WAVES (default 4, or 1) waves per search instead of one wave
+  static const int big_nw = [] {
+    const char* v = std::getenv("ROUTEST_ASTAR_RETRY_WAVES");
+    return v != nullptr && std::atoi(v) == 1 ? 1 : 4;
+  }();
   if (e == hipSuccess && use_wave && arena != nullptr && arena->base != nullptr && arena->entries > 0) {
     static const unsigned long long per = [] {
       const char* v = std::getenv("ROUTEST_ASTAR_RETRY_ENTRIES");
@@ -1127,7 +1162,7 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
       const int chunk = (int)std::max<unsigned long long>(64, std::min<unsigned long long>((unsigned long long)wave->slots, c));
       for (int i0 = 0; i0 < R && e == hipSuccess; i0 += chunk)
         e = launch_astar_wave(g, src, dst, Q, scratch + i0, 0, std::min(chunk, R - i0), *wave, o, pl.max_iters,
-                              pl.delta, stream, arena);
+                              pl.delta, stream, arena, big_nw);
     }
     S.retry_ms = ms_since(t0);
     t0 = std::chrono::steady_clock::now();
@@ -1140,7 +1175,7 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
     S.escalated = E;
     for (int i0 = 0; i0 < E && e == hipSuccess; i0 += big->slots)
       e = launch_astar_wave(g, src, dst, Q, scratch + i0, 0, std::min(big->slots, E - i0), *big, o, pl.max_iters,
-                            pl.delta, stream, arena);
+                            pl.delta, stream, arena, big_nw);
     if (E > 0 && e == hipSuccess) e = hipStreamSynchronize(stream);
     S.big_ms = ms_since(t0);
   }

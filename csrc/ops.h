@@ -171,7 +171,8 @@ hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* 
                              const int* qidx = nullptr, int nq = 0);   // qidx: run queries qidx[0..nq)
 hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* dst, int Q, const int* qidx,
                              int q0, int T, const AstarWs& ws, const AstarOut& o, int max_iters, float delta,
-                             hipStream_t stream, const AstarArenaBuf* arena = nullptr);
+                             hipStream_t stream, const AstarArenaBuf* arena = nullptr,
+                             int nw = 1);   // nw: waves per search (1 or 4)
 // The tiered search (lane -> wave -> big); any tier pointer may be null.  scratch: Q + 1 device ints.
 // Searches left with status 2/3 are the caller's (host Dijkstra).
 hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, int Q, const AstarWs* lane,
