@@ -1028,7 +1028,9 @@ hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* 
     else if (g.K == 16) hipLaunchKernelGGL((astar_wave_kernel<16, NWV>), dim3(n), blk, 0, stream, a, qidx, n, delta, ar); \
     else hipLaunchKernelGGL((astar_wave_kernel<32, NWV>), dim3(n), blk, 0, stream, a, qidx, n, delta, ar);             \
   } while (0)
-  if (nw >= 4) RT_ASTAR_WAVE(4);
+  if (nw >= 8) RT_ASTAR_WAVE(8);
+  else if (nw >= 4) RT_ASTAR_WAVE(4);
+  else if (nw >= 2) RT_ASTAR_WAVE(2);
   else RT_ASTAR_WAVE(1);
 #undef RT_ASTAR_WAVE
   return hipGetLastError();
@@ -1129,9 +1131,13 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
   t0 = std::chrono::steady_clock::now();
   if (use_wave) {
     S.wave = T;
+    static const int wave_nw = [] {                 // waves per search in the main wave-tier launch
+      const char* v = std::getenv("ROUTEST_ASTAR_WAVE_WAVES");
+      return v != nullptr ? std::atoi(v) : 1;
+    }();
     for (int i0 = 0; i0 < T && e == hipSuccess; i0 += wave->slots)
       e = launch_astar_wave(g, src, dst, Q, qidx != nullptr ? qidx + i0 : nullptr, i0, std::min(wave->slots, T - i0),
-                            *wave, o, pl.max_iters, pl.delta, stream, arena);
+                            *wave, o, pl.max_iters, pl.delta, stream, arena, wave_nw);
   }
   // Searches that overflowed because one launch's searches shared the growth arena: rerun them in
   // the wave tier a chunk at a time (the arena restarts per launch), so each can grow into
@@ -1140,10 +1146,10 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
   // for seconds (profiles/astar_scale_1m_r3n.jsonl).  Only what overflows again goes to the big tier.
   bool wave_timed = false;
   // the reruns and the big tier hold the LARGE searches (f-bands of thousands of nodes): a workgroup
-  // of ROUTEST_ASTAR_RETRY_WAVES (default 4, or 1) waves per search instead of one wave
+  // of ROUTEST_ASTAR_RETRY_WAVES (default 4; 1, 2, 8) waves per search instead of one wave
   static const int big_nw = [] {
     const char* v = std::getenv("ROUTEST_ASTAR_RETRY_WAVES");
-    return v != nullptr && std::atoi(v) == 1 ? 1 : 4;
+    return v != nullptr ? std::atoi(v) : 4;
   }();
   if (e == hipSuccess && use_wave && arena != nullptr && arena->base != nullptr && arena->entries > 0) {
     static const unsigned long long per = [] {

@@ -172,7 +172,7 @@ hipError_t launch_astar_lane(const AstarGraphDev& g, const int* src, const int* 
 hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* dst, int Q, const int* qidx,
                              int q0, int T, const AstarWs& ws, const AstarOut& o, int max_iters, float delta,
                              hipStream_t stream, const AstarArenaBuf* arena = nullptr,
-                             int nw = 1);   // nw: waves per search (1 or 4)
+                             int nw = 1);   // nw: waves per search (1, 2, 4 or 8)
 // The tiered search (lane -> wave -> big); any tier pointer may be null.  scratch: Q + 1 device ints.
 // Searches left with status 2/3 are the caller's (host Dijkstra).
 hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, int Q, const AstarWs* lane,
