@@ -72,11 +72,12 @@ class BulkRouteStep:
         # several waves of searches in flight (sparse per-search tables: ~33 GB of HBM3E in all)
         legs_est = int(sum(len(s) for s in snapped) * 1.4) + 1024
         slots = min(legs_est, max_slots)
-        # the searches left after the lane tier's pop budget (~56k of 80k here) in ONE wave-tier launch
-        # with 2^14-entry starting tables (fewer growth steps): 163 -> 142 ms per 10k-request step
-        # on the 100k-node graph (bench/gpu_r3q.sh, profiles/route_tiering_ab_r3q.jsonl).  Workspace:
-        # lane tier ~8 GB, wave tier ~26 GB, big tier ~4 GB, growth arena 16 GB (of 288 GB HBM3E)
-        ws = int(os.environ.get("ROUTEST_BULK_WAVE_SLOTS", "65536"))
+        # every search the lane tier leaves (with the length split: ~65k+ of 80k here) in ONE wave-tier
+        # launch with 2^14-entry starting tables (fewer growth steps): 163 -> 142 ms per 10k-request
+        # step on the 100k-node graph (profiles/route_tiering_ab_r3q.jsonl); 98304 slots instead of
+        # 65536 once the long legs skip the lane tier: 124.2 -> 119.6 ms (route_wave_slots_ab_r3aj.jsonl).
+        # Workspace: lane tier ~8 GB, wave tier ~39 GB, big tier ~4 GB, growth arena 16 GB (of 288 GB)
+        ws = int(os.environ.get("ROUTEST_BULK_WAVE_SLOTS", "98304"))
         tb = int(os.environ.get("ROUTEST_BULK_WAVE_TBITS", "14"))
         self.astar = astar or BatchedAstar(g, cost, d, slots=slots, wave_slots=min(slots, ws), arena_gb=16,
                                            wave_tbits=tb)
