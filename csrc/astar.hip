@@ -384,7 +384,8 @@ __global__ __launch_bounds__(64) void astar_kernel(AstarArgs a, const int* __res
 }
 
 // ---------------------------------------------------------------------------------------------
-// Wave tier: ONE WAVE per query.  The 64 lanes of a wave expand a whole f-band at once:
+// Wave tier: one WORKGROUP of NW waves (NW = 1, 2, 4 or 8; AstarPlan::wave_nw / retry_nw) per query.
+// Its 64 * NW lanes expand a whole f-band at once:
 //
 //   near = open nodes with f = g + h < thr;  far = the other open nodes as (f, node) pairs
 //   repeat: every lane takes a near node, relaxes its edges with a 64-bit atomicMin on the packed
@@ -600,6 +601,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4, 8)))
       int* cur = curA ? nearA : nearB;
       int* nxt = curA ? nearB : nearA;
       const int ncap_nxt = curA ? ncapB : ncapA;
+      // every wave has read s_next (nnear) after the previous pass's / far split's barrier before
+      // lane 0 clears it: without this barrier a fast wave 0 could zero it while a slower wave was
+      // still about to read it, and the waves' band loops (and their barriers) would diverge
+      if constexpr (NW > 1) __syncthreads();
       if (lane == 0) s_next = 0;
       __syncthreads();
       const float best = gbest();
@@ -1028,10 +1033,11 @@ hipError_t launch_astar_wave(const AstarGraphDev& g, const int* src, const int* 
     else if (g.K == 16) hipLaunchKernelGGL((astar_wave_kernel<16, NWV>), dim3(n), blk, 0, stream, a, qidx, n, delta, ar); \
     else hipLaunchKernelGGL((astar_wave_kernel<32, NWV>), dim3(n), blk, 0, stream, a, qidx, n, delta, ar);             \
   } while (0)
-  if (nw >= 8) RT_ASTAR_WAVE(8);
-  else if (nw >= 4) RT_ASTAR_WAVE(4);
-  else if (nw >= 2) RT_ASTAR_WAVE(2);
-  else RT_ASTAR_WAVE(1);
+  if (nw == 8) RT_ASTAR_WAVE(8);
+  else if (nw == 4) RT_ASTAR_WAVE(4);
+  else if (nw == 2) RT_ASTAR_WAVE(2);
+  else if (nw == 1) RT_ASTAR_WAVE(1);
+  else return hipErrorInvalidValue;
 #undef RT_ASTAR_WAVE
   return hipGetLastError();
 }
@@ -1072,6 +1078,17 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
   if (Q <= 0) return hipSuccess;
   auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipSuccess;
+  // waves per search: the plan's value, else the environment (read per call, so tests can switch
+  // them); only 1, 2, 4 and 8 have kernel instantiations — anything else is an error, not a rounding
+  auto waves = [](int v, const char* env, int dflt) {
+    if (v != 0) return v;
+    const char* s = std::getenv(env);
+    return s != nullptr ? std::atoi(s) : dflt;
+  };
+  const int wave_nw = waves(pl.wave_nw, "ROUTEST_ASTAR_WAVE_WAVES", 1);
+  const int big_nw = waves(pl.retry_nw, "ROUTEST_ASTAR_RETRY_WAVES", 4);
+  auto nw_ok = [](int v) { return v == 1 || v == 2 || v == 4 || v == 8; };
+  if (!nw_ok(wave_nw) || !nw_ok(big_nw)) return hipErrorInvalidValue;
   const bool use_wave = wave != nullptr && pl.lane_pops > 0;
   const bool use_lane = lane != nullptr && (!use_wave || Q >= pl.wave_only_below);
   if (!use_lane && !use_wave) return hipErrorInvalidValue;
@@ -1117,7 +1134,8 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
         int dev = 0, cus = 256;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const unsigned long long resident = (unsigned long long)cus * 16ull;   // 4 SIMDs x 4 waves
+        // resident searches: 4 SIMDs x 4 waves per CU, nw waves per search
+        const unsigned long long resident = (unsigned long long)cus * 16ull / (unsigned long long)wave_nw;
         lpt = arena->entries >= resident * 2ull * (unsigned long long)g.N;
       }
       if (lpt) e = select_count_lpt(g, src, dst, o.status, Q, (1 << 2) | (1 << 3), scratch, stream, T);
@@ -1131,10 +1149,6 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
   t0 = std::chrono::steady_clock::now();
   if (use_wave) {
     S.wave = T;
-    static const int wave_nw = [] {                 // waves per search in the main wave-tier launch
-      const char* v = std::getenv("ROUTEST_ASTAR_WAVE_WAVES");
-      return v != nullptr ? std::atoi(v) : 1;
-    }();
     for (int i0 = 0; i0 < T && e == hipSuccess; i0 += wave->slots)
       e = launch_astar_wave(g, src, dst, Q, qidx != nullptr ? qidx + i0 : nullptr, i0, std::min(wave->slots, T - i0),
                             *wave, o, pl.max_iters, pl.delta, stream, arena, wave_nw);
@@ -1147,10 +1161,6 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
   bool wave_timed = false;
   // the reruns and the big tier hold the LARGE searches (f-bands of thousands of nodes): a workgroup
   // of ROUTEST_ASTAR_RETRY_WAVES (default 4; 1, 2, 8) waves per search instead of one wave
-  static const int big_nw = [] {
-    const char* v = std::getenv("ROUTEST_ASTAR_RETRY_WAVES");
-    return v != nullptr ? std::atoi(v) : 4;
-  }();
   if (e == hipSuccess && use_wave && arena != nullptr && arena->base != nullptr && arena->entries > 0) {
     static const unsigned long long per = [] {
       const char* v = std::getenv("ROUTEST_ASTAR_RETRY_ENTRIES");

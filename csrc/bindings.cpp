@@ -763,7 +763,7 @@ std::vector<double> astar_search(torch::Tensor indptr, torch::Tensor indices, to
                                  c10::optional<torch::Tensor> out_iters, torch::Tensor scratch, int64_t max_iters,
                                  int64_t lane_pops, int64_t wave_only_below, double delta,
                                  c10::optional<torch::Tensor> arena, c10::optional<torch::Tensor> arena_ctr,
-                                 double lane_max_m) {
+                                 double lane_max_m, int64_t wave_nw, int64_t retry_nw) {
   for (auto* t : {&indptr, &indices, &cost, &lat, &lon, &src, &dst, &out_cost, &out_len, &out_status, &out_path,
                   &scratch})
     check_dev(*t, "astar tensor");
@@ -821,6 +821,10 @@ std::vector<double> astar_search(torch::Tensor indptr, torch::Tensor indices, to
   pl.wave_only_below = (int)wave_only_below;
   pl.delta = (float)delta;
   pl.lane_max_m = (float)lane_max_m;
+  pl.wave_nw = (int)wave_nw;
+  pl.retry_nw = (int)retry_nw;
+  TORCH_CHECK(wave_nw == 0 || wave_nw == 1 || wave_nw == 2 || wave_nw == 4 || wave_nw == 8, "wave_nw in {0,1,2,4,8}");
+  TORCH_CHECK(retry_nw == 0 || retry_nw == 1 || retry_nw == 2 || retry_nw == 4 || retry_nw == 8, "retry_nw in {0,1,2,4,8}");
   rt::AstarRunStats st;
   rt::AstarArenaBuf ab;
   if (arena.has_value() && arena->defined()) {
@@ -1225,7 +1229,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_cost"), py::arg("out_len"), py::arg("out_status"), py::arg("out_path"), py::arg("out_iters"),
         py::arg("scratch"), py::arg("max_iters"), py::arg("lane_pops"), py::arg("wave_only_below"),
         py::arg("delta"), py::arg("arena") = py::none(), py::arg("arena_ctr") = py::none(),
-        py::arg("lane_max_m") = -1.0);
+        py::arg("lane_max_m") = -1.0, py::arg("wave_nw") = 0, py::arg("retry_nw") = 0);
   m.def("forest_predict", &forest_predict, "K4: fused featurize + tree-ensemble inference");
   m.def("forest_predict_lds", &forest_predict_lds, "K4: LDS-staged tree chunks, 2 walks per thread");
   m.def("pscore_create", &pscore_create, "resident single-request scorer kernel on the blob's GPU");

@@ -158,6 +158,10 @@ struct AstarPlan {
   float delta = 10.f;           // wave tier f-band width (seconds)
   float lane_max_m = -1.f;      // legs longer than this (great circle, m) skip the lane tier; 0: none;
                                 // < 0: ROUTEST_ASTAR_LANE_MAX_M, read per search (default 0)
+  int wave_nw = 0;              // waves per search in the main wave-tier launch (1, 2, 4, 8);
+                                // 0: ROUTEST_ASTAR_WAVE_WAVES, read per search (default 1)
+  int retry_nw = 0;             // waves per search in the arena reruns and the big tier;
+                                // 0: ROUTEST_ASTAR_RETRY_WAVES, read per search (default 4)
 };
 struct AstarRunStats {
   int lane = 0, wave = 0, escalated = 0;

@@ -11,8 +11,10 @@ Native checkpoint = a directory holding versioned snapshots and one pointer::
         trainer_state.json          {"step", "config", "world"} (training resume, optional)
 
 A save writes a complete snapshot into a private staging directory, fsyncs every file and the
-directory, renames it to ``step_N`` and only then swaps ``LATEST`` with ONE ``os.replace`` (fsynced
-as well).  A rank killed at any point leaves either the previous snapshot or the new one as
+directory, renames it to ``step_N`` (``step_N.<pid>_<ns>`` when that step already has a snapshot,
+so a re-save never moves the directory ``LATEST`` names) and only then swaps ``LATEST`` with ONE
+``os.replace`` (fsynced as well).  Staging directories of saves whose process died are removed by
+the next save.  A rank killed at any point leaves either the previous snapshot or the new one as
 ``LATEST`` — never new weights beside an old step counter (round-2 ADVICE: the per-file renames
 could mix them).  The two most recent snapshots are kept.  A flat legacy directory
 (``config.json`` + ``model.safetensors`` directly inside) still loads.
@@ -31,7 +33,9 @@ from __future__ import annotations
 
 import json
 import os
+import re
 import shutil
+import time
 from typing import Any, Dict, Optional, Tuple
 
 import torch
@@ -44,6 +48,8 @@ from .mlp3 import EtaMLP, LinearETA
 FORMAT_VERSION = 2
 LATEST = "LATEST"
 KEEP = 2
+_SNAP_RE = re.compile(r"^step_(\d+)(\.\d+_\d+)?$")
+_TMP_RE = re.compile(r"^\.(?:staging|old)_(\d+)_")
 
 
 def _fsync_file(p: str) -> None:
@@ -101,6 +107,7 @@ def save_checkpoint(path: str, model: Any, optimizer_state: Optional[Dict[str, t
         sd = {k: v.contiguous() for k, v in model.state_dict().items()}
     if extra_config:
         cfg.update(extra_config)
+    _clean_stale(path)
     stage = os.path.join(path, f".staging_{os.getpid()}_{step}")
     shutil.rmtree(stage, ignore_errors=True)
     os.makedirs(stage)
@@ -125,17 +132,13 @@ def save_checkpoint(path: str, model: Any, optimizer_state: Optional[Dict[str, t
         _fsync_file(p)
     _fsync_dir(stage)
     name = f"step_{step:08d}"
+    if os.path.exists(os.path.join(path, name)):
+        # re-save of a step that already has a snapshot: the new copy gets a name of its own and
+        # the LATEST swap below stays the ONLY commit point (a crash at any moment leaves LATEST on
+        # a complete snapshot); the superseded copy is removed only after the swap
+        name = f"{name}.{os.getpid()}_{time.time_ns()}"
     final = os.path.join(path, name)
-    if os.path.exists(final):
-        # re-save of the same step: if LATEST points at it, point LATEST at the staging copy while
-        # the old one is moved away, so the pointer never names a missing directory
-        old = os.path.join(path, f".old_{os.getpid()}_{name}")
-        shutil.rmtree(old, ignore_errors=True)
-        os.replace(final, old)
-        os.replace(stage, final)
-        shutil.rmtree(old, ignore_errors=True)
-    else:
-        os.replace(stage, final)
+    os.replace(stage, final)
     _fsync_dir(path)
     tmp = os.path.join(path, f".{LATEST}.{os.getpid()}")
     with open(tmp, "w") as f:
@@ -148,12 +151,53 @@ def save_checkpoint(path: str, model: Any, optimizer_state: Optional[Dict[str, t
     return final
 
 
+def _snap_step(d: str) -> Optional[int]:
+    m = _SNAP_RE.match(d)
+    return int(m.group(1)) if m else None
+
+
+def _pid_alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    return True
+
+
+def _clean_stale(path: str) -> None:
+    """Remove staging / superseded directories left by saves that died mid-write (their writer
+    process is gone); a live writer's directories are left alone."""
+    for d in os.listdir(path):
+        m = _TMP_RE.match(d)
+        if m and int(m.group(1)) != os.getpid() and not _pid_alive(int(m.group(1))):
+            shutil.rmtree(os.path.join(path, d), ignore_errors=True)
+
+
 def _prune(path: str, keep_name: str) -> None:
-    snaps = sorted(d for d in os.listdir(path) if d.startswith("step_") and
-                   os.path.isdir(os.path.join(path, d)))
-    drop = [d for d in snaps[:-KEEP] if d != keep_name]
-    for d in drop:
-        shutil.rmtree(os.path.join(path, d), ignore_errors=True)
+    """Keep the snapshots of the KEEP most recent steps (one copy per step: the LATEST one for its
+    step, else the newest) and never ``keep_name``."""
+    by_step: Dict[int, list] = {}
+    for d in os.listdir(path):
+        st = _snap_step(d)
+        if st is not None and os.path.isdir(os.path.join(path, d)):
+            by_step.setdefault(st, []).append(d)
+    keep_step = _snap_step(keep_name)
+    steps = sorted(by_step)
+    kept = set(steps[-KEEP:])
+    for st in steps:
+        names = sorted(by_step[st], key=lambda d: os.stat(os.path.join(path, d)).st_mtime_ns)
+        if st == keep_step:
+            survivors = {keep_name}
+        elif st in kept:
+            survivors = {names[-1]}
+        else:
+            survivors = set()
+        for d in names:
+            if d not in survivors:
+                shutil.rmtree(os.path.join(path, d), ignore_errors=True)
+    _clean_stale(path)
 
 
 def load_checkpoint(path: str) -> Tuple[Any, Dict[str, Any]]:

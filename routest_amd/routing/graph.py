@@ -304,6 +304,10 @@ class BatchedAstar:
             big_slots = int(os.environ.get("ROUTEST_ASTAR_BIG_SLOTS", str(max(16, min(128, (4 << 30) // per)))))
         self.big_tier = AstarTier(big_slots, big_cap, big_tbits, d) if big_slots > 0 else None
         self.scratch = torch.empty(1, dtype=torch.int32, device=d)
+        # waves per search in the main wave-tier launch / the arena reruns + big tier (1, 2, 4, 8;
+        # 0 = ROUTEST_ASTAR_WAVE_WAVES / ROUTEST_ASTAR_RETRY_WAVES, defaults 1 / 4)
+        self.wave_nw = 0
+        self.retry_nw = 0
         self.last_stats = {}
         # tightest admissible + consistent heuristic: every edge length is 1.15 x its great-circle
         # length (so any path >= 1.15 x the great-circle s-t distance) and every edge is traversed
@@ -370,7 +374,7 @@ class BatchedAstar:
                                  self.big_tier.ws() if self.big_tier else None, out_cost, out_len, out_status,
                                  out_path, self.last_iters, self.scratch, self.max_iters, self.lane_pops,
                                  self.wave_only_below, self.wave_delta, self.arena, self.arena_ctr,
-                                 lane_max_m=self.lane_max_m)
+                                 lane_max_m=self.lane_max_m, wave_nw=self.wave_nw, retry_nw=self.retry_nw)
         self.last_stats = dict(zip(("lane", "wave", "escalated", "lane_ms", "wave_ms", "big_ms", "retried",
                                     "retry_ms"), st))
         self.last_tail = int(st[1])

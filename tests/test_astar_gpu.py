@@ -224,3 +224,31 @@ def test_workspace_is_independent_of_graph_size(graph_and_cost):
     b = BatchedAstar(small, edge_costs(small, default_model(hidden=64, steps=5), device="cuda:0"), "cuda:0",
                      slots=1024, big_slots=0)
     assert a.workspace_bytes == b.workspace_bytes
+
+
+@pytest.mark.parametrize("nw", [1, 2, 4, 8])
+def test_multi_wave_searches_exact(graph_and_cost, nw):
+    """Every waves-per-search instantiation (the s_next reset raced with slower waves
+    when NW > 1) on the three paths that use it: the main wave tier, the arena reruns and the big
+    tier — optimal costs vs scipy Dijkstra, workspace restored (a second run is identical)."""
+    g, cost, _ = graph_and_cost
+    src, dst = synth_route_queries(g, 400, seed=11)
+    ref = dijkstra_ref(g, cost, src, dst)
+    for kw, key in ((dict(cap=128, arena_gb=0.002), "retried"), (dict(cap=128, arena_gb=0), "escalated"),
+                    (dict(), "wave")):
+        a = BatchedAstar(g, cost, "cuda:0", slots=512, **kw)
+        a.wave_nw = nw
+        a.retry_nw = nw
+        c, n, st, p = a.run(src, dst)
+        assert a.last_stats[key] > 0 and a.last_fallbacks == 0, (kw, a.last_stats)
+        assert (st.cpu().numpy() == 0).all(), (kw, np.unique(st.cpu().numpy(), return_counts=True))
+        np.testing.assert_allclose(c.cpu().numpy(), ref, rtol=1e-4)
+        assert np.array_equal(c.cpu().numpy(), a.run(src, dst)[0].cpu().numpy())
+
+
+def test_unsupported_wave_count_is_an_error(graph_and_cost):
+    g, cost, _ = graph_and_cost
+    a = BatchedAstar(g, cost, "cuda:0", slots=64)
+    a.wave_nw = 3
+    with pytest.raises(RuntimeError):
+        a.run([0], [1])

@@ -43,10 +43,52 @@ def test_snapshots_and_pointer(tmp_path):
     assert torch.equal(m.l2.weight, m3.l2.weight)
     o, ts = ck.load_training_state(d)
     assert ts["step"] == 30 and torch.equal(o["exp_avg"], opt["exp_avg"])
-    # re-saving the same step replaces it in place and the pointer stays valid
+    # re-saving the same step replaces it (under a name of its own) and the pointer stays valid
     ck.save_checkpoint(d, m1, trainer_state={"step": 30})
     m, _ = ck.load_checkpoint(d)
     assert torch.equal(m.l2.weight, m1.l2.weight)
+    snaps = sorted(x for x in os.listdir(d) if x.startswith("step_"))
+    assert len(snaps) == 2 and snaps[0] == "step_00000020"      # one copy per step
+    assert open(os.path.join(d, "LATEST")).read().strip() == snaps[1]
+
+
+def test_crash_during_same_step_resave_keeps_a_loadable_snapshot(tmp_path, monkeypatch):
+    """a re-save of the step LATEST names used to move that directory away before the
+    new one took its place; a crash between the two renames left LATEST naming nothing.  Now a
+    crash at ANY rename of the re-save leaves LATEST on a complete snapshot."""
+    for crash_at in range(2):          # the snapshot rename, the pointer swap
+        d = str(tmp_path / f"ck{crash_at}")
+        m1, m2 = _model(1), _model(2)
+        ck.save_checkpoint(d, m1, trainer_state={"step": 10})
+        real_replace = os.replace
+        calls = []
+
+        def dying_replace(src, dst):
+            calls.append(dst)
+            if len(calls) > crash_at:
+                raise KeyboardInterrupt("killed mid re-save")
+            return real_replace(src, dst)
+        monkeypatch.setattr(ck.os, "replace", dying_replace)
+        with pytest.raises(KeyboardInterrupt):
+            ck.save_checkpoint(d, m2, trainer_state={"step": 10})
+        monkeypatch.setattr(ck.os, "replace", real_replace)
+        m, cfg = ck.load_checkpoint(d)                 # never a ValueError: LATEST names a snapshot
+        assert cfg["step"] == 10
+        assert torch.equal(m.l2.weight, m1.l2.weight) or torch.equal(m.l2.weight, m2.l2.weight)
+
+
+def test_stale_staging_directories_are_removed(tmp_path):
+    d = str(tmp_path / "ck")
+    os.makedirs(d)
+    # a save by a process that no longer exists died mid-write
+    dead = subprocess.run([sys.executable, "-c", "import os; print(os.getpid())"], capture_output=True,
+                          text=True).stdout.strip()
+    stale = os.path.join(d, f".staging_{dead}_7")
+    os.makedirs(stale)
+    open(os.path.join(stale, "model.safetensors"), "w").write("x" * 100)
+    ck.save_checkpoint(d, _model(1), trainer_state={"step": 8})
+    assert not os.path.exists(stale)
+    assert ck.load_checkpoint(d)[1]["step"] == 8
 
 
 def test_crash_before_pointer_swap_keeps_previous_snapshot(tmp_path, monkeypatch):
