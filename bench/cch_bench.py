@@ -1,0 +1,87 @@
+"""CCH router benchmark: customization per context, batched legs vs the tiered A*, the same-box
+multi-thread CPU baseline, and the 1M-node city-wide case.  One JSON line per measurement."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from routest_amd.data.graph import synth_road_graph, synth_route_queries  # noqa: E402
+from routest_amd.routing.graph import BatchedAstar, dijkstra_ref, edge_costs  # noqa: E402
+from routest_amd.serve.eta_service import default_model  # noqa: E402
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=100_000)
+    ap.add_argument("--legs", type=int, default=80_000)
+    ap.add_argument("--max-km", type=float, default=25.0)
+    ap.add_argument("--astar", action="store_true")
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    from routest_amd.routing.cch import RoadRouter, RouteContext
+    dev = torch.device("cuda:0")
+    t0 = time.time()
+    g = synth_road_graph(a.nodes, seed=5)
+    m = default_model(hidden=64, steps=50)
+    emit(stage="graph", nodes=g.num_nodes, edges=g.num_edges, s=round(time.time() - t0, 2))
+    t0 = time.time()
+    router = RoadRouter(g, m, device=dev)
+    emit(stage="topology", wall_s=round(time.time() - t0, 2), **router.stats())
+    ctx = RouteContext(weather=2, congestion=1, weekhour=9)
+    for i in range(2):
+        t0 = time.time()
+        key = router.metric(RouteContext(weather=2, congestion=1, weekhour=9 + i))
+        emit(stage="context", wall_ms=round((time.time() - t0) * 1e3, 2), **router.last_metric)
+    key = router.metric(ctx)
+    cost = router.costs(ctx)
+    src, dst = synth_route_queries(g, a.legs, seed=3, max_km=a.max_km)
+    s_t = torch.from_numpy(src).to(dev)
+    d_t = torch.from_numpy(dst).to(dev)
+    for want in (False, True):
+        times = []
+        for _ in range(a.reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = router.gpu.route(key, s_t, d_t, 4096, want)
+            torch.cuda.synchronize()
+            times.append((time.perf_counter() - t0) * 1e3)
+        st = out[2].cpu().numpy()
+        emit(stage="cch_legs", want_path=want, legs=a.legs, ms=round(min(times), 3), ms_all=[round(x, 2) for x in times],
+             legs_per_s=round(a.legs / (min(times) / 1e3)), found=int((st == 0).sum()))
+    sec = out[0].cpu().numpy()
+    k = min(2000, a.legs)
+    ref = dijkstra_ref(g, cost, src[:k], dst[:k])
+    emit(stage="exactness", checked=k, max_rel_err=float(np.max(np.abs(sec[:k] - ref) / np.maximum(ref, 1e-6))))
+    if a.astar:
+        astar = BatchedAstar(g, cost, dev, slots=16384)
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            astar.run(src, dst)
+            torch.cuda.synchronize()
+            ta = (time.perf_counter() - t0) * 1e3
+        emit(stage="astar_legs", legs=a.legs, ms=round(ta, 2), legs_per_s=round(a.legs / (ta / 1e3)))
+    if a.cpu:
+        from routest_amd import _rt
+        threads = len(os.sched_getaffinity(0))
+        c = _rt.CCH(g.indptr, g.indices, g.lat, g.lon, threads)
+        mc = c.customize(cost, g.length_m)
+        emit(stage="cpu_customize", threads=threads, ms=round(mc.customize_ms, 1))
+        for want in (False, True):
+            ms = c.bench(mc, src, dst, want)
+            emit(stage="cpu_legs", threads=threads, want_path=want, legs=a.legs, ms=round(ms, 1),
+                 legs_per_s=round(a.legs / (ms / 1e3)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1170,8 +1170,11 @@ torch::Tensor forest_predict_lds(torch::Tensor records, torch::Tensor nodes2, to
 
 }  // namespace
 
+void bind_cch_gpu(py::module& m);   // cch_bindings.cpp
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "routest_amd native gfx950 kernels";
+  bind_cch_gpu(m);
   m.def("eta_mlp3_forward", &eta_mlp3_forward, "fused featurize + 3-layer MLP forward (bf16 MFMA)");
   m.def("eta_mlp3_forward_hostio", &eta_mlp3_forward_hostio,
         "zero-copy: fused kernel reads records / writes minutes in pinned host memory");

@@ -1,0 +1,933 @@
+// GPU customizable contraction hierarchy: per-context customization + batched elimination-tree
+// queries (SURVEY K9 "edge costs precomputed per (graph, context) and cached"; replaces the
+// per-request ORS directions / matrix calls of RO/Flaskr/utils.py:55-62,97-105,151-156).
+//
+// Preprocessing (node order, chordal supergraph, elimination tree, levels) is host C++
+// (csrc/runtime/cch.h) and metric-independent.  Everything here is per metric, all on the device:
+//
+//  * context costs: 2E ETA records (edge traffic level shifted by the context's congestion, the
+//    context's weather and week-hour) -> the fused featurize+MLP kernel (K1+K2) -> seconds per edge;
+//  * basic customization, one launch per etree HEIGHT level: every node z of the level relaxes all
+//    pairs (u, v) of its upward clique (lower triangle z of arc {u,v}) with a 64-bit atomicMin on a
+//    (weight bits, middle node) word — ties resolve deterministically, exactly like the CPU
+//    reference — and the same launch finalizes the level's own arcs (their best triangle's two
+//    sub-arcs and the metre length they stand for).  Work items are FLATTENED over the level (a
+//    binary search maps an item to its node), so the top of the hierarchy — one node per level with
+//    a clique of hundreds — still spreads over the whole chip;
+//  * perfect customization, one launch per etree DEPTH level, top-down: every ordered pair (a, c) of
+//    a node's arcs tests the intermediate/upper triangle through head(c); 32-bit atomicMin on the
+//    float bits;
+//  * pruning: an arc direction is kept for queries iff its perfect weight equals its basic one;
+//    kept arcs are compacted into 16-byte records {weight, head depth, arc id} per node (hipCUB scan).
+//
+// Queries (csrc/runtime/cch.h "elimination-tree search"): the forward search space of s is its
+// etree ancestor chain, swept bottom-up once with labels in LDS indexed by depth (one wave per chain
+// job; runs of consecutive ranks — the separators — are fetched 64 at a time, so pointer chasing is
+// per run, not per node).  A meet kernel takes each pair's two chains (one wave per pair: LCA by
+// binary search on the chains' node arrays, min over common depths, deepest tie) and lists the
+// shortcut arcs of the chosen up-down path; an unpack kernel expands them to road nodes (one lane
+// per pair, explicit DFS stack in LDS).  Many-to-many matrices reuse each point's two chains.
+#include <hipcub/hipcub.hpp>
+
+#include <chrono>
+#include <cstring>
+
+#include "cch_gpu.h"
+#include "ops.h"
+#include "runtime/rt_core.h"
+
+namespace rt {
+
+namespace {
+
+using EtaRecordDev = rtc::EtaRecord;
+constexpr unsigned long long PACK_INF_D = 0x7F800000FFFFFFFFull;
+constexpr uint32_t EDGE_FLAG_D = 0x80000000u;
+constexpr float F_INF = __builtin_inff();
+
+__device__ __forceinline__ unsigned long long packw(float w, uint32_t p) {
+  return ((unsigned long long)__float_as_uint(w) << 32) | p;
+}
+__device__ __forceinline__ float wof(unsigned long long p) { return __uint_as_float((uint32_t)(p >> 32)); }
+
+// position of b in the sorted upward list of a (a < b), -1 if absent
+__device__ __forceinline__ int find_arc_d(const int32_t* __restrict__ up_ptr, const int32_t* __restrict__ up_head,
+                                          int a, int b) {
+  int lo = up_ptr[a], hi = up_ptr[a + 1];
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (up_head[mid] < b) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < up_ptr[a + 1] && up_head[lo] == b) ? lo : -1;
+}
+
+// largest i in [lo, hi) with ofs[i] <= g
+__device__ __forceinline__ int item_owner(const int64_t* __restrict__ ofs, int lo, int hi, long long g) {
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (ofs[mid] <= g) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void fill_u64_kernel(unsigned long long* __restrict__ p, long long n, unsigned long long v) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+__global__ void edge_scatter_kernel(const float* __restrict__ cost, const int32_t* __restrict__ edge_arc,
+                                    const uint8_t* __restrict__ edge_dir, int E, unsigned long long* __restrict__ up,
+                                    unsigned long long* __restrict__ dn) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int a = edge_arc[e];
+  if (a < 0) return;
+  atomicMin(edge_dir[e] ? dn + a : up + a, packw(cost[e], EDGE_FLAG_D | (uint32_t)e));
+}
+
+struct LevelArgs {
+  const int32_t* up_ptr;
+  const int32_t* up_head;
+  const int32_t* nodes;    // level-ordered node list
+  const int64_t* ofs;      // item prefix over that list
+  int lo, hi;              // node index range of this level
+  long long base, items;
+};
+
+// Basic customization of one height level: items [0, k) of node z finalize arc k-th of z; items
+// [k, k + k(k-1)/2) relax the lower triangle z of one pair of z's upward neighbours.
+__global__ __launch_bounds__(256) void basic_level_kernel(LevelArgs L, unsigned long long* __restrict__ up,
+                                                          unsigned long long* __restrict__ dn,
+                                                          int32_t* __restrict__ sub_up, int32_t* __restrict__ sub_dn,
+                                                          float* __restrict__ len_up, float* __restrict__ len_dn,
+                                                          const float* __restrict__ length) {
+  const long long gi = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (gi >= L.items) return;
+  const long long g = L.base + gi;
+  const int ni = item_owner(L.ofs, L.lo, L.hi, g);
+  const int z = L.nodes[ni];
+  const long long p = g - L.ofs[ni];
+  const int a0 = L.up_ptr[z];
+  const int k = L.up_ptr[z + 1] - a0;
+  if (p < k) {
+    // finalize arc a = (z, v): best triangle's sub-arcs + lengths (all lower arcs are final)
+    const int a = a0 + (int)p;
+    const int v = L.up_head[a];
+#pragma unroll
+    for (int dir = 0; dir < 2; ++dir) {
+      const unsigned long long w = dir ? dn[a] : up[a];
+      int32_t* sub = (dir ? sub_dn : sub_up) + 2 * (long long)a;
+      float* len = dir ? len_dn : len_up;
+      if (!(wof(w) < F_INF)) {
+        sub[0] = -1;
+        sub[1] = -1;
+        len[a] = F_INF;
+        continue;
+      }
+      const uint32_t pl = (uint32_t)w;
+      if (pl & EDGE_FLAG_D) {
+        const int e = (int)(pl & ~EDGE_FLAG_D);
+        sub[0] = -1;
+        sub[1] = e;
+        len[a] = length[e];
+        continue;
+      }
+      const int zz = (int)pl;
+      const int azu = find_arc_d(L.up_ptr, L.up_head, zz, z), azv = find_arc_d(L.up_ptr, L.up_head, zz, v);
+      const int s0 = dir ? azv : azu, s1 = dir ? azu : azv;
+      sub[0] = s0;
+      sub[1] = s1;
+      len[a] = len_dn[s0] + len_up[s1];
+    }
+    return;
+  }
+  // pair (i, j), i < j, row-major over i
+  const long long q = p - k;
+  const double kk = (double)(2 * k - 1);
+  int i = (int)((kk - sqrt(kk * kk - 8.0 * (double)q)) * 0.5);
+  if (i < 0) i = 0;
+  auto row0 = [&](int r) { return (long long)r * (2 * k - r - 1) / 2; };
+  while (i > 0 && row0(i) > q) --i;
+  while (i + 1 < k && row0(i + 1) <= q) ++i;
+  const int j = (int)(q - row0(i)) + i + 1;
+  const int ai = a0 + i, aj = a0 + j;
+  const int u = L.up_head[ai], v = L.up_head[aj];
+  const int t = find_arc_d(L.up_ptr, L.up_head, u, v);
+  if (t < 0) return;   // cannot happen in a chordal completion
+  // u -> z -> v: (z,u) traversed down, (z,v) up;  v -> z -> u: (z,v) down, (z,u) up
+  const float wu = wof(dn[ai]) + wof(up[aj]);
+  const float wd = wof(dn[aj]) + wof(up[ai]);
+  if (wu < F_INF) atomicMin(up + t, packw(wu, (uint32_t)z));
+  if (wd < F_INF) atomicMin(dn + t, packw(wd, (uint32_t)z));
+}
+
+__global__ void perfect_init_kernel(const unsigned long long* __restrict__ up, const unsigned long long* __restrict__ dn,
+                                    uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn, long long M) {
+  for (long long a = blockIdx.x * (long long)blockDim.x + threadIdx.x; a < M; a += (long long)gridDim.x * blockDim.x) {
+    pup[a] = (uint32_t)(up[a] >> 32);
+    pdn[a] = (uint32_t)(dn[a] >> 32);
+  }
+}
+
+// Perfect customization of one depth level: ordered pairs (c, a), a != c, of node x's arcs; the
+// candidate for arc a = (x, y) goes through z = head(c): x -> z on c (basic), z -> y on {z, y}
+// (perfect: an arc between two ancestors, finished by an earlier level).  Consecutive items share c
+// and spread over a (different atomic targets).
+__global__ __launch_bounds__(256) void perfect_level_kernel(LevelArgs L, const unsigned long long* __restrict__ up,
+                                                            const unsigned long long* __restrict__ dn,
+                                                            uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+  const long long gi = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (gi >= L.items) return;
+  const long long g = L.base + gi;
+  const int ni = item_owner(L.ofs, L.lo, L.hi, g);
+  const int x = L.nodes[ni];
+  const long long p = g - L.ofs[ni];
+  const int a0 = L.up_ptr[x];
+  const int k = L.up_ptr[x + 1] - a0;
+  const int c = (int)(p / (k - 1));
+  const int r = (int)(p % (k - 1));
+  const int a = r < c ? r : r + 1;
+  const int ac = a0 + c, aa = a0 + a;
+  const int y = L.up_head[aa], z = L.up_head[ac];
+  const int lo = z < y ? z : y, hi = z < y ? y : z;
+  const int azy = find_arc_d(L.up_ptr, L.up_head, lo, hi);
+  if (azy < 0) return;
+  const float xz = wof(up[ac]), zx = wof(dn[ac]);
+  const float zy = __uint_as_float(z < y ? pup[azy] : pdn[azy]);
+  const float yz = __uint_as_float(z < y ? pdn[azy] : pup[azy]);
+  const float cu = xz + zy, cd = yz + zx;
+  if (cu < F_INF) atomicMin(pup + aa, __float_as_uint(cu));
+  if (cd < F_INF) atomicMin(pdn + aa, __float_as_uint(cd));
+}
+
+__device__ __forceinline__ bool kept(uint32_t p, unsigned long long b) {
+  return __uint_as_float(p) < F_INF && p == (uint32_t)(b >> 32);
+}
+
+__global__ void prune_count_kernel(const int32_t* __restrict__ up_ptr, const uint32_t* __restrict__ pup,
+                                   const uint32_t* __restrict__ pdn, const unsigned long long* __restrict__ up,
+                                   const unsigned long long* __restrict__ dn, int N, int32_t* __restrict__ fcnt,
+                                   int32_t* __restrict__ bcnt) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= N) return;
+  int kf = 0, kb = 0;
+  for (int a = up_ptr[x]; a < up_ptr[x + 1]; ++a) {
+    kf += kept(pup[a], up[a]);
+    kb += kept(pdn[a], dn[a]);
+  }
+  fcnt[x] = kf;
+  bcnt[x] = kb;
+}
+
+__global__ void prune_scatter_kernel(const int32_t* __restrict__ up_ptr, const int32_t* __restrict__ up_head,
+                                     const int32_t* __restrict__ depth, const uint32_t* __restrict__ pup,
+                                     const uint32_t* __restrict__ pdn, const unsigned long long* __restrict__ up,
+                                     const unsigned long long* __restrict__ dn, int N, const int32_t* __restrict__ f_ptr,
+                                     const int32_t* __restrict__ b_ptr, int4* __restrict__ f_rec,
+                                     int4* __restrict__ b_rec) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= N) return;
+  int kf = f_ptr[x], kb = b_ptr[x];
+  for (int a = up_ptr[x]; a < up_ptr[x + 1]; ++a) {
+    const int hd = depth[up_head[a]];
+    if (kept(pup[a], up[a])) f_rec[kf++] = make_int4((int)pup[a], hd, a, 0);
+    if (kept(pdn[a], dn[a])) b_rec[kb++] = make_int4((int)pdn[a], hd, a, 0);
+  }
+}
+
+// ---- context costs (routing/graph.py edge_records / edge_costs) ----
+constexpr float L_REF_M = 10000.f;
+constexpr int32_t MONDAY_2025_08_25 = 2063 * 86400;   // seconds since 2020-01-01 (a Monday)
+
+__global__ void ctx_records_kernel(const uint8_t* __restrict__ base_traffic, int E, int weather, int congestion,
+                                   int weekhour, float age, EtaRecordDev* __restrict__ rec) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  int lvl = (int)base_traffic[e] + congestion - 1;
+  lvl = lvl < 0 ? 0 : (lvl > 3 ? 3 : lvl);
+  // TRAFFIC_LEVELS (Low, Medium, High, Jam) -> features.py traffic codes (High 0, Jam 1, Low 2, Medium 3)
+  const uint8_t code = (uint8_t)((0x01000302u >> (8 * lvl)) & 0xFF);
+  EtaRecordDev r;
+  r.distance_m = L_REF_M;
+  r.driver_age = age;
+  r.wallclock_s = MONDAY_2025_08_25 + weekhour * 3600;
+  r.weather = (uint8_t)weather;
+  r.traffic = code;
+  r.pad = 0;
+  rec[2 * (long long)e] = r;
+  r.distance_m = 0.f;
+  rec[2 * (long long)e + 1] = r;
+}
+
+__global__ void ctx_cost_kernel(const float* __restrict__ minutes, const float* __restrict__ length,
+                                const uint8_t* __restrict__ road_class, int E, float* __restrict__ cost) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const float k60 = (float)(60.0 / 10000.0);
+  const float rate = (minutes[2 * (long long)e] - minutes[2 * (long long)e + 1]) * k60;
+  const float cf[4] = {1.15f, 1.0f, 0.85f, 0.65f};
+  const float sec = rate * length[e] * cf[road_class[e] & 3];
+  const float floor_s = length[e] / (float)(130.0 / 3.6);
+  cost[e] = sec > floor_s ? sec : floor_s;
+}
+
+// ---- queries ----
+
+// One wave per chain job (rank << 1 | dir): sweep the etree ancestor chain bottom-up with labels in
+// LDS by depth, then dump them (dist, pred arc) and the chain's node ranks to the job's scratch row.
+__global__ __launch_bounds__(64) void sweep_kernel(const int32_t* __restrict__ jobs, int J,
+                                                   const int32_t* __restrict__ parent,
+                                                   const int32_t* __restrict__ depth, int N,
+                                                   const int32_t* __restrict__ f_ptr, const int4* __restrict__ f_rec,
+                                                   const int32_t* __restrict__ b_ptr, const int4* __restrict__ b_rec,
+                                                   int stride, float* __restrict__ out_dist,
+                                                   int32_t* __restrict__ out_pred, int32_t* __restrict__ out_node) {
+  extern __shared__ unsigned char smem[];
+  float* sd = reinterpret_cast<float*>(smem);
+  int32_t* sp = reinterpret_cast<int32_t*>(smem + (size_t)stride * 4);
+  const int j = blockIdx.x;
+  if (j >= J) return;
+  const int lane = threadIdx.x;
+  const int code = jobs[j];
+  const int r = code >> 1;
+  const bool fwd = (code & 1) == 0;
+  const int32_t* __restrict__ ptr = fwd ? f_ptr : b_ptr;
+  const int4* __restrict__ rec = fwd ? f_rec : b_rec;
+  const int D = depth[r];
+  for (int d = lane; d <= D; d += 64) {
+    sd[d] = F_INF;
+    sp[d] = -1;
+  }
+  __syncthreads();
+  if (lane == 0) sd[D] = 0.f;
+  __syncthreads();
+  const size_t base = (size_t)j * stride;
+  int x = r, d = D;
+  while (x >= 0 && d >= 0) {
+    // the next run of consecutive ranks on the chain (parent(x + i) == x + i + 1), up to 64
+    const int cand = x + lane;
+    const bool in = cand < N;
+    const int par = in ? parent[cand] : -2;
+    const int pb = in ? ptr[cand] : 0;
+    const int pe = in ? ptr[cand + 1] : 0;
+    const unsigned long long cont = __ballot(in && par == cand + 1);
+    int L = (~cont == 0ull) ? 64 : (__builtin_ctzll(~cont) + 1);
+    if (L > d + 1) L = d + 1;
+    const int next = __shfl(par, L - 1);
+    if (lane < L) out_node[base + (d - lane)] = x + lane;
+    for (int i = 0; i < L; ++i) {
+      const int di = d - i;
+      const float dx = sd[di];
+      if (dx < F_INF) {
+        const int b = __shfl(pb, i), e = __shfl(pe, i);
+        for (int k = b + lane; k < e; k += 64) {
+          const int4 rc = rec[k];
+          const float nd = dx + __int_as_float(rc.x);
+          if (nd < sd[rc.y]) {
+            sd[rc.y] = nd;
+            sp[rc.y] = rc.z;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    x = next;
+    d -= L;
+  }
+  __syncthreads();
+  for (int dd = lane; dd <= D; dd += 64) {
+    out_dist[base + dd] = sd[dd];
+    out_pred[base + dd] = sp[dd];
+  }
+}
+
+// One wave per pair: LCA depth, best common depth (min sum, deepest tie), metres along the chosen
+// shortcut arcs (forward arcs from the meeting node down to s, then backward ones down to t), and —
+// with `arcs` — the arc list in path order (arc << 1 | traversed-down).
+__global__ __launch_bounds__(64) void meet_kernel(int P, const int32_t* __restrict__ pjf, const int32_t* __restrict__ pjb,
+                                                  int jf0, int jb0, const int32_t* __restrict__ jobs, int stride,
+                                                  const float* __restrict__ sdist, const int32_t* __restrict__ spred,
+                                                  const int32_t* __restrict__ snode, const int32_t* __restrict__ depth,
+                                                  const int32_t* __restrict__ arc_lo, const float* __restrict__ len_up,
+                                                  const float* __restrict__ len_dn, float* __restrict__ out_sec,
+                                                  float* __restrict__ out_met, int* __restrict__ out_status,
+                                                  int32_t* __restrict__ arcs, int32_t* __restrict__ narcs, int max_arcs) {
+  __shared__ int32_t fw[4096];
+  const int q = blockIdx.x;
+  if (q >= P) return;
+  const int lane = threadIdx.x;
+  const int jf = pjf ? pjf[q] : jf0 + 2 * q;
+  const int jb = pjb ? pjb[q] : jb0 + 2 * q;
+  const int s = jobs[jf] >> 1, t = jobs[jb] >> 1;
+  const int ds = depth[s], dt = depth[t];
+  const size_t bf = (size_t)jf * stride, bb = (size_t)jb * stride;
+  int status = 1;
+  float best = F_INF;
+  int bestd = -1;
+  if (snode[bf] == snode[bb]) {
+    // chains agree on depths [0, L]
+    int lo = 0, hi = ds < dt ? ds : dt;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (snode[bf + mid] == snode[bb + mid]) lo = mid;
+      else hi = mid - 1;
+    }
+    const int L = lo;
+    for (int d = lane; d <= L; d += 64) {
+      const float v = sdist[bf + d] + sdist[bb + d];
+      if (v < best || (v == best && d > bestd)) {
+        best = v;
+        bestd = d;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ov = __shfl_xor(best, o);
+      const int od = __shfl_xor(bestd, o);
+      if (ov < best || (ov == best && od > bestd)) {
+        best = ov;
+        bestd = od;
+      }
+    }
+    if (best < F_INF) status = 0;
+  }
+  if (lane != 0) return;
+  float met = 0.f;
+  int n = 0;
+  if (status == 0) {
+    int nf = 0;
+    for (int slot = bestd; slot != ds;) {
+      const int a = spred[bf + slot];
+      met += len_up[a];
+      if (nf < 4096) fw[nf] = a;
+      ++nf;
+      slot = depth[arc_lo[a]];
+    }
+    if (arcs != nullptr) {
+      int32_t* out = arcs + (size_t)q * max_arcs;
+      if (nf > 4096 || nf > max_arcs) status = 4;
+      for (int i = nf - 1; i >= 0 && status == 0; --i) out[n++] = fw[i] << 1;
+      for (int slot = bestd; slot != dt && status == 0;) {
+        const int a = spred[bb + slot];
+        met += len_dn[a];
+        if (n >= max_arcs) { status = 4; break; }
+        out[n++] = (a << 1) | 1;
+        slot = depth[arc_lo[a]];
+      }
+    } else {
+      for (int slot = bestd; slot != dt;) {
+        const int a = spred[bb + slot];
+        met += len_dn[a];
+        slot = depth[arc_lo[a]];
+      }
+    }
+  }
+  if (out_sec) out_sec[q] = status == 0 ? best : -1.f;
+  if (out_met) out_met[q] = status == 0 ? met : -1.f;
+  if (out_status) out_status[q] = status;
+  if (narcs) narcs[q] = n;
+}
+
+// One lane per pair: expand the shortcut arcs to road node ids (DFS, first sub-arc first).
+constexpr int UNPACK_STACK = 96;
+__global__ __launch_bounds__(64) void unpack_kernel(int P, const int* __restrict__ src_node, const int32_t* __restrict__ arcs,
+                                                    const int32_t* __restrict__ narcs, int max_arcs,
+                                                    const int32_t* __restrict__ sub_up,
+                                                    const int32_t* __restrict__ sub_dn,
+                                                    const int32_t* __restrict__ arc_lo,
+                                                    const int32_t* __restrict__ up_head,
+                                                    const int32_t* __restrict__ node_of, int* __restrict__ status,
+                                                    int* __restrict__ out_len, int* __restrict__ out_path, int max_path) {
+  __shared__ int32_t stk[64 * UNPACK_STACK];
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P) return;
+  int32_t* st = stk + threadIdx.x * UNPACK_STACK;
+  if (status[q] != 0) {
+    out_len[q] = 0;
+    return;
+  }
+  int* out = out_path + (size_t)q * max_path;
+  int n = 0;
+  out[n++] = src_node[q];
+  const int na = narcs[q];
+  const int32_t* al = arcs + (size_t)q * max_arcs;
+  bool ok = true;
+  for (int k = 0; k < na && ok; ++k) {
+    int sp = 0;
+    st[sp++] = al[k];
+    while (sp > 0) {
+      const int code = st[--sp];
+      const int a = code >> 1, dn = code & 1;
+      const int32_t* sub = (dn ? sub_dn : sub_up) + 2 * (long long)a;
+      const int s0 = sub[0];
+      if (s0 < 0) {
+        if (n >= max_path) { ok = false; break; }
+        out[n++] = node_of[dn ? arc_lo[a] : up_head[a]];
+        continue;
+      }
+      if (sp + 2 > UNPACK_STACK) { ok = false; break; }
+      st[sp++] = sub[1] << 1;        // second: traversed up
+      st[sp++] = (s0 << 1) | 1;      // first: traversed down (popped first)
+    }
+  }
+  if (!ok) {
+    status[q] = 4;
+    out_len[q] = 0;
+    return;
+  }
+  out_len[q] = n;
+}
+
+// (node ids are range-checked by the callers; out-of-range ids are clamped, never dereferenced)
+__global__ void route_jobs_kernel(const int* __restrict__ src, const int* __restrict__ dst, int Q,
+                                  const int32_t* __restrict__ rank, int N, int32_t* __restrict__ jobs) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  int s = src[q], t = dst[q];
+  s = (s < 0 || s >= N) ? 0 : s;
+  t = (t < 0 || t >= N) ? 0 : t;
+  jobs[2 * q] = rank[s] << 1;
+  jobs[2 * q + 1] = (rank[t] << 1) | 1;
+}
+
+// matrix: jobs [R][NM][2] (forward, backward per point); pairs (r, i, j) for i != j
+__global__ void matrix_jobs_kernel(const int* __restrict__ pts, const int* __restrict__ npts, int R, int NM,
+                                   const int32_t* __restrict__ rank, int N, int32_t* __restrict__ jobs) {
+  const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (g >= (long long)R * NM) return;
+  const int r = (int)(g / NM), i = (int)(g % NM);
+  int v = i < npts[r] ? pts[g] : -1;
+  if (v < 0 || v >= N) v = 0;
+  jobs[2 * g] = rank[v] << 1;
+  jobs[2 * g + 1] = (rank[v] << 1) | 1;
+}
+
+__global__ void matrix_pairs_kernel(const int* __restrict__ npts, int R, int NM, int32_t* __restrict__ pjf,
+                                    int32_t* __restrict__ pjb) {
+  const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (g >= (long long)R * NM * NM) return;
+  const int r = (int)(g / ((long long)NM * NM));
+  const int rem = (int)(g % ((long long)NM * NM));
+  const int i = rem / NM, j = rem % NM;
+  pjf[g] = 2 * (r * NM + i);
+  pjb[g] = 2 * (r * NM + j) + 1;
+}
+
+__global__ void matrix_out_kernel(const int* __restrict__ npts, int R, int NM, float* __restrict__ sec,
+                                  float* __restrict__ met, double* __restrict__ D64) {
+  const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (g >= (long long)R * NM * NM) return;
+  const int r = (int)(g / ((long long)NM * NM));
+  const int rem = (int)(g % ((long long)NM * NM));
+  const int i = rem / NM, j = rem % NM;
+  const int n = npts[r];
+  const bool diag = i == j;
+  const bool out = i >= n || j >= n;
+  float s = sec ? sec[g] : 0.f, m = met ? met[g] : 0.f;
+  if (diag || out) s = m = 0.f;
+  else {
+    if (s < 0.f) s = F_INF;
+    if (m < 0.f) m = F_INF;
+  }
+  if (sec) sec[g] = s;
+  if (met) met[g] = m;
+  if (D64) D64[g] = (double)m;
+}
+
+inline int blocks_for(long long n, int b) { return (int)((n + b - 1) / b); }
+
+template <class T>
+hipError_t dmalloc(T*& p, size_t n) {
+  p = nullptr;
+  if (n == 0) n = 1;
+  return hipMalloc((void**)&p, n * sizeof(T));
+}
+template <class T>
+hipError_t up_copy(T*& p, const T* h, size_t n) {
+  hipError_t e = dmalloc(p, n);
+  if (e == hipSuccess && n) e = hipMemcpy(p, h, n * sizeof(T), hipMemcpyHostToDevice);
+  return e;
+}
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+CchMetricDev::~CchMetricDev() {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(device);
+  dfree(cost);
+  dfree(sub_up);
+  dfree(sub_dn);
+  dfree(len_up);
+  dfree(len_dn);
+  dfree(f_ptr);
+  dfree(b_ptr);
+  dfree(f_rec);
+  dfree(b_rec);
+  (void)hipSetDevice(cur);
+}
+
+CchScratch::~CchScratch() {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(device);
+  dfree(dist);
+  dfree(pred);
+  dfree(node);
+  dfree(jobs);
+  dfree(arcs);
+  dfree(narcs);
+  (void)hipSetDevice(cur);
+}
+
+hipError_t CchScratch::ensure(size_t J, size_t P, int stride, int max_arcs) {
+  hipError_t e = hipSuccess;
+  if (J > jobs_cap) {
+    dfree(dist);
+    dfree(pred);
+    dfree(node);
+    dfree(jobs);
+    const size_t cap = std::max(J, jobs_cap * 3 / 2);
+    if ((e = dmalloc(dist, cap * stride)) != hipSuccess) return e;
+    if ((e = dmalloc(pred, cap * stride)) != hipSuccess) return e;
+    if ((e = dmalloc(node, cap * stride)) != hipSuccess) return e;
+    if ((e = dmalloc(jobs, cap)) != hipSuccess) return e;
+    jobs_cap = cap;
+  }
+  if (P > pairs_cap) {
+    dfree(arcs);
+    dfree(narcs);
+    const size_t cap = std::max(P, pairs_cap * 3 / 2);
+    if ((e = dmalloc(arcs, cap * (size_t)max_arcs)) != hipSuccess) return e;
+    if ((e = dmalloc(narcs, cap)) != hipSuccess) return e;
+    pairs_cap = cap;
+  }
+  return e;
+}
+
+CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class, const uint8_t* base_traffic,
+               int device)
+    : T_(std::move(T)), dev_(device) {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (hipSetDevice(dev_) != hipSuccess) throw std::runtime_error("CchGpu: bad device");
+  const int N = T_.N;
+  const int64_t M = T_.M, E = T_.E;
+  if (M >= (int64_t)1 << 31 || E >= (int64_t)1 << 31) throw std::runtime_error("CchGpu: graph too large");
+  std::vector<int32_t> up_ptr32(N + 1);
+  for (int r = 0; r <= N; ++r) up_ptr32[r] = (int32_t)T_.up_ptr[r];
+  // level work prefixes: basic items per node = k(k+1)/2 (k finalize + k(k-1)/2 pairs), height
+  // order; perfect items = k(k-1), depth order
+  bofs_.assign(N + 1, 0);
+  pofs_.assign(N + 1, 0);
+  for (int i = 0; i < N; ++i) {
+    const int64_t kb = T_.up_ptr[T_.hlev_nodes[i] + 1] - T_.up_ptr[T_.hlev_nodes[i]];
+    bofs_[i + 1] = bofs_[i] + kb * (kb + 1) / 2;
+    const int64_t kp = T_.up_ptr[T_.dlev_nodes[i] + 1] - T_.up_ptr[T_.dlev_nodes[i]];
+    pofs_[i + 1] = pofs_[i] + kp * (kp - 1);
+  }
+  hipError_t e = hipSuccess;
+  auto ck = [&](hipError_t x) {
+    if (x != hipSuccess && e == hipSuccess) e = x;
+  };
+  ck(up_copy(d_up_ptr, up_ptr32.data(), N + 1));
+  ck(up_copy(d_up_head, T_.up_head.data(), M));
+  ck(up_copy(d_arc_lo, T_.arc_lo.data(), M));
+  ck(up_copy(d_parent, T_.parent.data(), N));
+  ck(up_copy(d_depth, T_.depth.data(), N));
+  ck(up_copy(d_rank, T_.rank.data(), N));
+  ck(up_copy(d_node, T_.node.data(), N));
+  ck(up_copy(d_edge_arc, T_.edge_arc.data(), E));
+  ck(up_copy(d_edge_dir, T_.edge_dir.data(), E));
+  ck(up_copy(d_length, length, E));
+  if (road_class) ck(up_copy(d_class, road_class, E));
+  if (base_traffic) ck(up_copy(d_base_traffic, base_traffic, E));
+  ck(up_copy(d_hnodes, T_.hlev_nodes.data(), N));
+  ck(up_copy(d_dnodes, T_.dlev_nodes.data(), N));
+  ck(up_copy(d_bofs, bofs_.data(), N + 1));
+  ck(up_copy(d_pofs, pofs_.data(), N + 1));
+  ck(dmalloc(d_up64, M));
+  ck(dmalloc(d_dn64, M));
+  ck(dmalloc(d_pup, M));
+  ck(dmalloc(d_pdn, M));
+  ck(dmalloc(d_fcnt, N));
+  ck(dmalloc(d_bcnt, N));
+  size_t tb = 0;
+  ck(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_fcnt, d_fcnt, N));
+  cub_bytes = tb;
+  ck(hipMalloc(&d_cub, cub_bytes ? cub_bytes : 1));
+  (void)hipSetDevice(cur);
+  if (e != hipSuccess) throw std::runtime_error(std::string("CchGpu: ") + hipGetErrorString(e));
+}
+
+CchGpu::~CchGpu() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    cache_.clear();
+  }
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(dev_);
+  dfree(d_up_ptr);
+  dfree(d_up_head);
+  dfree(d_arc_lo);
+  dfree(d_parent);
+  dfree(d_depth);
+  dfree(d_rank);
+  dfree(d_node);
+  dfree(d_edge_arc);
+  dfree(d_edge_dir);
+  dfree(d_length);
+  dfree(d_class);
+  dfree(d_base_traffic);
+  dfree(d_hnodes);
+  dfree(d_dnodes);
+  dfree(d_bofs);
+  dfree(d_pofs);
+  dfree(d_up64);
+  dfree(d_dn64);
+  dfree(d_pup);
+  dfree(d_pdn);
+  dfree(d_fcnt);
+  dfree(d_bcnt);
+  if (d_cub) (void)hipFree(d_cub);
+  if (rec_buf) (void)hipFree(rec_buf);
+  dfree(min_buf);
+  (void)hipSetDevice(cur);
+}
+
+void CchGpu::set_eta(const void* blob, int H, const NormParams& np, int variant, int num_cus) {
+  std::lock_guard<std::mutex> lk(mu_cust_);
+  eta_blob_ = blob;
+  eta_H_ = H;
+  eta_np_ = np;
+  eta_variant_ = variant;
+  eta_cus_ = num_cus;
+}
+
+hipError_t CchGpu::context_costs(const CchContext& c, float* d_cost, hipStream_t s) {
+  if (eta_blob_ == nullptr || d_class == nullptr || d_base_traffic == nullptr) return hipErrorInvalidValue;
+  const int E = (int)T_.E;
+  hipError_t e = hipSuccess;
+  if (rec_buf == nullptr) {
+    if ((e = hipMalloc(&rec_buf, (size_t)2 * E * sizeof(EtaRecordDev))) != hipSuccess) return e;
+    if ((e = dmalloc(min_buf, (size_t)2 * E)) != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(ctx_records_kernel, dim3(blocks_for(E, 256)), dim3(256), 0, s, d_base_traffic, E, c.weather,
+                     c.congestion, c.weekhour, c.driver_age, (EtaRecordDev*)rec_buf);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  e = launch_eta_mlp3_fwd(rec_buf, min_buf, 2 * E, eta_blob_, eta_H_, eta_np_, eta_variant_, eta_cus_, s, 16);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ctx_cost_kernel, dim3(blocks_for(E, 256)), dim3(256), 0, s, min_buf, d_length, d_class, E, d_cost);
+  return hipGetLastError();
+}
+
+hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_cust_);
+  auto t0 = std::chrono::steady_clock::now();
+  const int N = T_.N;
+  const int64_t M = T_.M, E = T_.E;
+  m.device = dev_;
+  hipError_t e = hipSuccess;
+  auto ck = [&](hipError_t x) {
+    if (x != hipSuccess && e == hipSuccess) e = x;
+  };
+  if (m.cost == nullptr) ck(dmalloc(m.cost, E));
+  if (m.sub_up == nullptr) {
+    ck(dmalloc(m.sub_up, 2 * M));
+    ck(dmalloc(m.sub_dn, 2 * M));
+    ck(dmalloc(m.len_up, M));
+    ck(dmalloc(m.len_dn, M));
+    ck(dmalloc(m.f_ptr, N + 1));
+    ck(dmalloc(m.b_ptr, N + 1));
+  }
+  if (e != hipSuccess) return e;
+  if (d_cost != m.cost) ck(hipMemcpyAsync(m.cost, d_cost, E * sizeof(float), hipMemcpyDeviceToDevice, s));
+  const int fill_blocks = (int)std::min<int64_t>(4096, (M + 255) / 256 + 1);
+  hipLaunchKernelGGL(fill_u64_kernel, dim3(fill_blocks), dim3(256), 0, s, d_up64, (long long)M, PACK_INF_D);
+  hipLaunchKernelGGL(fill_u64_kernel, dim3(fill_blocks), dim3(256), 0, s, d_dn64, (long long)M, PACK_INF_D);
+  hipLaunchKernelGGL(edge_scatter_kernel, dim3(blocks_for(E, 256)), dim3(256), 0, s, m.cost, d_edge_arc, d_edge_dir,
+                     (int)E, d_up64, d_dn64);
+  ck(hipGetLastError());
+  // basic, bottom-up by height
+  for (int h = 0; h <= T_.max_height && e == hipSuccess; ++h) {
+    LevelArgs L{d_up_ptr, d_up_head, d_hnodes, d_bofs, (int)T_.hlev_ptr[h], (int)T_.hlev_ptr[h + 1], 0, 0};
+    if (L.lo >= L.hi) continue;
+    L.base = bofs_[L.lo];
+    L.items = bofs_[L.hi] - bofs_[L.lo];
+    if (L.items <= 0) continue;
+    hipLaunchKernelGGL(basic_level_kernel, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
+                       m.sub_up, m.sub_dn, m.len_up, m.len_dn, d_length);
+    ck(hipGetLastError());
+  }
+  // perfect, top-down by depth
+  hipLaunchKernelGGL(perfect_init_kernel, dim3(fill_blocks), dim3(256), 0, s, d_up64, d_dn64, d_pup, d_pdn, (long long)M);
+  ck(hipGetLastError());
+  for (int d = 0; d <= T_.max_depth && e == hipSuccess; ++d) {
+    LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0};
+    if (L.lo >= L.hi) continue;
+    L.base = pofs_[L.lo];
+    L.items = pofs_[L.hi] - pofs_[L.lo];
+    if (L.items <= 0) continue;
+    hipLaunchKernelGGL(perfect_level_kernel, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64, d_pup,
+                       d_pdn);
+    ck(hipGetLastError());
+  }
+  // prune + compact
+  hipLaunchKernelGGL(prune_count_kernel, dim3(blocks_for(N, 256)), dim3(256), 0, s, d_up_ptr, d_pup, d_pdn, d_up64,
+                     d_dn64, N, d_fcnt, d_bcnt);
+  ck(hipGetLastError());
+  ck(hipMemsetAsync(m.f_ptr, 0, sizeof(int32_t), s));
+  ck(hipMemsetAsync(m.b_ptr, 0, sizeof(int32_t), s));
+  size_t tb = cub_bytes;
+  ck(hipcub::DeviceScan::InclusiveSum(d_cub, tb, d_fcnt, m.f_ptr + 1, N, s));
+  tb = cub_bytes;
+  ck(hipcub::DeviceScan::InclusiveSum(d_cub, tb, d_bcnt, m.b_ptr + 1, N, s));
+  int32_t tot[2] = {0, 0};
+  ck(hipMemcpyAsync(&tot[0], m.f_ptr + N, 4, hipMemcpyDeviceToHost, s));
+  ck(hipMemcpyAsync(&tot[1], m.b_ptr + N, 4, hipMemcpyDeviceToHost, s));
+  ck(hipStreamSynchronize(s));
+  if (e != hipSuccess) return e;
+  if (tot[0] > m.kept_f || m.f_rec == nullptr) {
+    dfree(m.f_rec);
+    ck(dmalloc(m.f_rec, tot[0]));
+  }
+  if (tot[1] > m.kept_b || m.b_rec == nullptr) {
+    dfree(m.b_rec);
+    ck(dmalloc(m.b_rec, tot[1]));
+  }
+  m.kept_f = tot[0];
+  m.kept_b = tot[1];
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(prune_scatter_kernel, dim3(blocks_for(N, 256)), dim3(256), 0, s, d_up_ptr, d_up_head, d_depth,
+                     d_pup, d_pdn, d_up64, d_dn64, N, m.f_ptr, m.b_ptr, m.f_rec, m.b_rec);
+  ck(hipGetLastError());
+  ck(hipStreamSynchronize(s));
+  m.customize_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  m.host_cost.clear();
+  return e;
+}
+
+hipError_t CchGpu::metric_from_costs(uint64_t key, const float* d_cost, hipStream_t s,
+                                     std::shared_ptr<CchMetricDev>& out) {
+  auto m = std::make_shared<CchMetricDev>();
+  m->key = key;
+  hipError_t e = customize(d_cost, *m, s);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto it = cache_.begin(); it != cache_.end(); ++it)
+    if ((*it)->key == key) {
+      cache_.erase(it);
+      break;
+    }
+  cache_.push_front(m);
+  while ((int)cache_.size() > capacity_) cache_.pop_back();
+  out = m;
+  return hipSuccess;
+}
+
+bool CchGpu::cached_metric(uint64_t key, std::shared_ptr<CchMetricDev>& out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto it = cache_.begin(); it != cache_.end(); ++it)
+    if ((*it)->key == key) {
+      out = *it;
+      cache_.splice(cache_.begin(), cache_, it);
+      return true;
+    }
+  return false;
+}
+
+hipError_t CchGpu::metric_for(const CchContext& c, hipStream_t s, std::shared_ptr<CchMetricDev>& out, bool* fresh) {
+  const uint64_t key = c.key();
+  if (fresh) *fresh = false;
+  auto lookup = [&]() -> bool { return cached_metric(key, out); };
+  if (lookup()) return hipSuccess;
+  std::lock_guard<std::mutex> bl(mu_build_);   // one context build at a time (others wait, then hit)
+  if (lookup()) return hipSuccess;
+  auto m = std::make_shared<CchMetricDev>();
+  m->key = key;
+  m->device = dev_;
+  hipError_t e = dmalloc(m->cost, T_.E);
+  if (e != hipSuccess) return e;
+  auto t0 = std::chrono::steady_clock::now();
+  {
+    std::lock_guard<std::mutex> lk(mu_cust_);
+    e = context_costs(c, m->cost, s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  m->cost_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  e = customize(m->cost, *m, s);
+  if (e != hipSuccess) return e;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    cache_.push_front(m);
+    while ((int)cache_.size() > capacity_) cache_.pop_back();
+  }
+  out = m;
+  if (fresh) *fresh = true;
+  return hipSuccess;
+}
+
+hipError_t CchGpu::route(const CchMetricDev& m, const int* d_src, const int* d_dst, int Q, const CchRouteOut& o,
+                         CchScratch& sc, hipStream_t s) {
+  if (Q <= 0) return hipSuccess;
+  const int S = stride();
+  sc.device = dev_;
+  hipError_t e = sc.ensure((size_t)2 * Q, (size_t)Q, S, MAX_ARCS);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(route_jobs_kernel, dim3(blocks_for(Q, 256)), dim3(256), 0, s, d_src, d_dst, Q, d_rank, T_.N,
+                     sc.jobs);
+  hipLaunchKernelGGL(sweep_kernel, dim3(2 * Q), dim3(64), (size_t)S * 8, s, sc.jobs, 2 * Q, d_parent, d_depth, T_.N,
+                     m.f_ptr, m.f_rec, m.b_ptr, m.b_rec, S, sc.dist, sc.pred, sc.node);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(meet_kernel, dim3(Q), dim3(64), 0, s, Q, nullptr, nullptr, 0, 1, sc.jobs, S, sc.dist, sc.pred,
+                     sc.node, d_depth, d_arc_lo, m.len_up, m.len_dn, o.sec, o.metres, o.status,
+                     o.path ? sc.arcs : nullptr, o.path ? sc.narcs : nullptr, MAX_ARCS);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (o.path != nullptr) {
+    hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(Q, 64)), dim3(64), 0, s, Q, d_src, sc.arcs, sc.narcs, MAX_ARCS,
+                       m.sub_up, m.sub_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path, o.max_path);
+    e = hipGetLastError();
+  }
+  return e;
+}
+
+hipError_t CchGpu::matrix(const CchMetricDev& m, const int* d_pts, const int* d_npts, int R, int NM, float* d_sec,
+                          float* d_met, double* d_D64, CchScratch& sc, hipStream_t s) {
+  if (R <= 0 || NM <= 0) return hipSuccess;
+  if (d_sec == nullptr || d_met == nullptr) return hipErrorInvalidValue;   // the meet writes both
+  const int S = stride();
+  sc.device = dev_;
+  const size_t J = (size_t)R * NM * 2, P = (size_t)R * NM * NM;
+  // pair job indices live in the arcs buffer (2 ints per pair)
+  hipError_t e = sc.ensure(J, (P * 2 + MAX_ARCS - 1) / MAX_ARCS + 1, S, MAX_ARCS);
+  if (e != hipSuccess) return e;
+  int32_t* pjf = sc.arcs;
+  int32_t* pjb = sc.arcs + P;
+  float* sec = d_sec;
+  float* met = d_met;
+  hipLaunchKernelGGL(matrix_jobs_kernel, dim3(blocks_for((long long)R * NM, 256)), dim3(256), 0, s, d_pts, d_npts, R, NM,
+                     d_rank, T_.N, sc.jobs);
+  hipLaunchKernelGGL(matrix_pairs_kernel, dim3(blocks_for((long long)P, 256)), dim3(256), 0, s, d_npts, R, NM, pjf, pjb);
+  hipLaunchKernelGGL(sweep_kernel, dim3((unsigned)J), dim3(64), (size_t)S * 8, s, sc.jobs, (int)J, d_parent, d_depth,
+                     T_.N, m.f_ptr, m.f_rec, m.b_ptr, m.b_rec, S, sc.dist, sc.pred, sc.node);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(meet_kernel, dim3((unsigned)P), dim3(64), 0, s, (int)P, pjf, pjb, 0, 0, sc.jobs, S, sc.dist,
+                     sc.pred, sc.node, d_depth, d_arc_lo, m.len_up, m.len_dn, sec, met, nullptr, nullptr, nullptr,
+                     MAX_ARCS);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(matrix_out_kernel, dim3(blocks_for((long long)P, 256)), dim3(256), 0, s, d_npts, R, NM, sec, met,
+                     d_D64);
+  return hipGetLastError();
+}
+
+}  // namespace rt

@@ -1,0 +1,142 @@
+// GPU customizable contraction hierarchy (csrc/cch.hip): customization per routing context and
+// batched elimination-tree queries.  Host preprocessing and the bit-identical CPU reference:
+// csrc/runtime/cch.h.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <list>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+#include "runtime/cch.h"
+
+namespace rt {
+
+// Routing context: the ETA features an edge cost depends on besides the edge itself
+// (routing/graph.py edge_records).  weather: features.py weather code (0..3, 255 unknown);
+// congestion: city-wide traffic level 0..3 (Low, Medium, High, Jam) shifting every edge's level;
+// weekhour: 0 = Monday 00:00 .. 167.
+struct CchContext {
+  int weather = 2, congestion = 1, weekhour = 9;
+  float driver_age = 35.f;
+  uint64_t key() const {
+    return (uint64_t)(weather & 0xFF) | ((uint64_t)(congestion & 0xFF) << 8) | ((uint64_t)(weekhour & 0xFFFF) << 16);
+  }
+};
+
+// One customized metric, kept on the device for as long as its context stays cached.
+struct CchMetricDev {
+  uint64_t key = 0;
+  int device = 0;
+  float* cost = nullptr;           // [E] the edge costs it was customized from
+  int32_t* sub_up = nullptr;       // [2M] per arc: (first sub-arc, traversed down; second, up) | (-1, edge)
+  int32_t* sub_dn = nullptr;
+  float* len_up = nullptr;         // [M] metres of the path an arc stands for
+  float* len_dn = nullptr;
+  int32_t* f_ptr = nullptr;        // [N+1] kept forward arcs of rank r
+  int32_t* b_ptr = nullptr;
+  int4* f_rec = nullptr;           // {weight bits, head depth, arc id, 0}
+  int4* b_rec = nullptr;
+  int64_t kept_f = 0, kept_b = 0;
+  double customize_ms = 0.0, cost_ms = 0.0;
+  std::vector<float> host_cost;    // [E] for the exact host fallback (filled on demand)
+  ~CchMetricDev();
+};
+
+// Per-caller query scratch (chains of every job + the pairs' shortcut-arc lists); grows on demand.
+struct CchScratch {
+  float* dist = nullptr;
+  int32_t* pred = nullptr;
+  int32_t* node = nullptr;
+  size_t jobs_cap = 0;
+  int32_t* jobs = nullptr;         // [2 * cap] (rank << 1 | dir)
+  int32_t* arcs = nullptr;         // [pairs_cap * max_arcs]
+  int32_t* narcs = nullptr;        // [pairs_cap]
+  size_t pairs_cap = 0;
+  int device = 0;
+  ~CchScratch();
+  hipError_t ensure(size_t jobs, size_t pairs, int stride, int max_arcs);
+};
+
+struct CchRouteOut {
+  float* sec = nullptr;            // [Q] seconds (-1 when not found)
+  float* metres = nullptr;         // [Q] metres of the chosen path
+  int* status = nullptr;           // [Q] 0 found, 1 unreachable, 4 too long / unpack overflow
+  int* len = nullptr;              // [Q] path nodes
+  int* path = nullptr;             // [Q, max_path] node ids (nullptr: costs only)
+  int max_path = 0;
+};
+
+class CchGpu {
+ public:
+  // T: host topology (kept); length: [E] metres per original edge; road_class / base_traffic: [E]
+  // per-edge class (0..3) and traffic level before the context's shift (routing/graph.py
+  // edge_traffic with congestion 1), for on-device context costs.
+  CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class, const uint8_t* base_traffic, int device);
+  ~CchGpu();
+  const rcch::Topology& topo() const { return T_; }
+  int device() const { return dev_; }
+  int stride() const { return T_.max_depth + 1; }
+
+  // ETA model used for context costs (the fused K1+K2 kernel's 32x32 blob on this device)
+  void set_eta(const void* blob, int H, const NormParams& np, int variant, int num_cus);
+  bool has_eta() const { return eta_blob_ != nullptr; }
+  // edge costs (s) of a context into d_cost [E] on the device (routing/graph.py edge_costs)
+  hipError_t context_costs(const CchContext& c, float* d_cost, hipStream_t s);
+
+  // customize m from d_cost ([E] on this device; copied into m.cost)
+  hipError_t customize(const float* d_cost, CchMetricDev& m, hipStream_t s);
+
+  // the metric of a context: from the cache, else costs + customization now (LRU, `capacity`)
+  hipError_t metric_for(const CchContext& c, hipStream_t s, std::shared_ptr<CchMetricDev>& out, bool* fresh = nullptr);
+  // a metric from caller-given costs under a caller-chosen key (tests, benches)
+  hipError_t metric_from_costs(uint64_t key, const float* d_cost, hipStream_t s, std::shared_ptr<CchMetricDev>& out);
+  // a cached metric by key (no build); false if absent
+  bool cached_metric(uint64_t key, std::shared_ptr<CchMetricDev>& out);
+  void set_capacity(int n) { std::lock_guard<std::mutex> lk(mu_); capacity_ = n < 1 ? 1 : n; }
+  int cached() { std::lock_guard<std::mutex> lk(mu_); return (int)cache_.size(); }
+
+  // point-to-point: node ids on the device
+  hipError_t route(const CchMetricDev& m, const int* d_src, const int* d_dst, int Q, const CchRouteOut& o,
+                   CchScratch& sc, hipStream_t s);
+  // many-to-many per request: pts [R][NM] node ids (n = npts[r] used), outputs [R][NM][NM] (any may
+  // be nullptr): seconds, metres (f32; both required) and metres as f64 (the greedy kernel's matrix, K6)
+  hipError_t matrix(const CchMetricDev& m, const int* d_pts, const int* d_npts, int R, int NM, float* d_sec,
+                    float* d_met, double* d_D64, CchScratch& sc, hipStream_t s);
+  static constexpr int MAX_ARCS = 1024;   // shortcut arcs per path before unpacking
+
+ private:
+  rcch::Topology T_;
+  int dev_ = 0;
+  // topology on the device
+  int32_t *d_up_ptr = nullptr, *d_up_head = nullptr, *d_arc_lo = nullptr, *d_parent = nullptr, *d_depth = nullptr;
+  int32_t *d_rank = nullptr, *d_node = nullptr, *d_edge_arc = nullptr;
+  uint8_t* d_edge_dir = nullptr;
+  float* d_length = nullptr;
+  uint8_t *d_class = nullptr, *d_base_traffic = nullptr;
+  int32_t *d_hnodes = nullptr, *d_dnodes = nullptr;
+  int64_t *d_bofs = nullptr, *d_pofs = nullptr;    // work-item prefixes in level order
+  std::vector<int64_t> bofs_, pofs_;               // host copies (level boundaries)
+  // customization temporaries (one customization at a time: mu_cust_)
+  unsigned long long *d_up64 = nullptr, *d_dn64 = nullptr;
+  uint32_t *d_pup = nullptr, *d_pdn = nullptr;
+  int32_t *d_fcnt = nullptr, *d_bcnt = nullptr;
+  void* d_cub = nullptr;
+  size_t cub_bytes = 0;
+  void* rec_buf = nullptr;                         // context cost records [2E] + minutes [2E]
+  float* min_buf = nullptr;
+  std::mutex mu_cust_, mu_build_;
+  // ETA
+  const void* eta_blob_ = nullptr;
+  int eta_H_ = 0, eta_variant_ = -1, eta_cus_ = 256;
+  NormParams eta_np_{};
+  // context cache (LRU)
+  std::mutex mu_;
+  std::list<std::shared_ptr<CchMetricDev>> cache_;
+  int capacity_ = 32;
+};
+
+}  // namespace rt

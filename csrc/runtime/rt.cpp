@@ -352,6 +352,7 @@ py::dict py_http_load(int port, int connections, double seconds, const std::stri
 }
 
 void bind_route(py::module& m);   // route_bind.cpp
+void bind_cch(py::module& m);     // cch_bind.cpp
 
 // The same over many different requests (path, body), cycled — e.g. 1k distinct route requests.
 py::dict py_http_load_multi(int port, int connections, double seconds, const std::vector<std::string>& paths,
@@ -404,6 +405,7 @@ py::dict py_http_load_mixed(int port, int connections, double seconds, const std
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "routest_amd CPU native runtime";
   bind_route(m);
+  bind_cch(m);
   m.def("http_load", &py_http_load, py::arg("port"), py::arg("connections") = 1, py::arg("seconds") = 2.0,
         py::arg("path") = "/api/predict_eta", py::arg("body") = "", py::arg("threads") = 1,
         py::arg("max_requests") = 0, py::arg("warmup") = 0);

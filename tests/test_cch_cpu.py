@@ -1,0 +1,142 @@
+"""Customizable contraction hierarchy, CPU reference (csrc/runtime/cch.h via routest_amd._rt.CCH).
+
+* exact: every leg's seconds equal scipy Dijkstra on the same costs (f32 sums: rtol 1e-5), every
+  path is a real edge sequence whose costs / lengths sum to the reported seconds / metres;
+* one-way streets (a directed graph with asymmetric edges) and disconnected components;
+* matrices: entry (i, j) = the leg i -> j, diagonal 0;
+* routing contexts: the request's weather / traffic / pickup hour select different edge costs, and
+  the answer is exact on that context's costs (verdict r3 item 2).
+"""
+import datetime as dt
+
+import numpy as np
+import pytest
+
+from routest_amd.data.graph import synth_road_graph, synth_route_queries
+from routest_amd.routing.graph import dijkstra_ref
+
+rt = pytest.importorskip("routest_amd._rt")
+
+
+def _check_paths(g, cost, src, dst, sec, met, st, paths, every=7):
+    for i in range(0, len(src), every):
+        if st[i] != 0:
+            continue
+        p = np.asarray(paths[i])
+        assert p[0] == src[i] and p[-1] == dst[i]
+        tot = 0.0
+        ln = 0.0
+        for u, v in zip(p[:-1], p[1:]):
+            nb = g.indices[g.indptr[u]:g.indptr[u + 1]]
+            k = np.where(nb == v)[0]
+            assert len(k) >= 1, (u, v)
+            e = g.indptr[u] + k[np.argmin(cost[g.indptr[u] + k])]
+            tot += cost[e]
+            ln += g.length_m[e]
+        assert abs(tot - sec[i]) <= 1e-4 * max(1.0, sec[i])
+        assert abs(ln - met[i]) <= 1e-4 * max(1.0, met[i])
+
+
+@pytest.fixture(scope="module")
+def small():
+    g = synth_road_graph(6000, seed=3)
+    rng = np.random.default_rng(0)
+    cost = (g.length_m / np.array([8.3, 12.5, 16.7, 22.2], np.float32)[g.road_class]
+            * rng.uniform(0.7, 1.6, g.num_edges)).astype(np.float32)       # asymmetric per direction
+    c = rt.CCH(g.indptr, g.indices, g.lat, g.lon, 4)
+    return g, cost, c
+
+
+def test_exact_vs_dijkstra_with_valid_paths(small):
+    g, cost, c = small
+    m = c.customize(cost, g.length_m)
+    src, dst = synth_route_queries(g, 600, seed=1, min_km=0.2)
+    src[:5] = dst[:5]                                   # s == t
+    sec, met, st, paths = c.query(m, src, dst, True)
+    ref = dijkstra_ref(g, cost, src, dst)
+    assert (st == 0).all()
+    np.testing.assert_allclose(sec, ref, rtol=1e-5, atol=1e-4)
+    assert (sec[:5] == 0).all() and all(len(paths[i]) == 1 for i in range(5))
+    _check_paths(g, cost, src, dst, sec, met, st, paths, every=3)
+    s = c.stats()
+    assert s["nodes"] == g.num_nodes and s["max_depth"] > 0 and s["arcs"] >= g.num_edges // 2
+
+
+def test_one_way_streets_and_components():
+    """Directed input (half the streets one-way) + two disconnected islands."""
+    g = synth_road_graph(3000, seed=7)
+    rng = np.random.default_rng(1)
+    src_of = np.repeat(np.arange(g.num_nodes), np.diff(g.indptr))
+    keep = np.ones(g.num_edges, bool)
+    # drop one direction of ~30% of the edges, only where the reverse exists (stay strongly connected
+    # mostly; unreachable pairs are checked against Dijkstra's inf anyway)
+    drop = rng.random(g.num_edges) < 0.3
+    keep &= ~(drop & (src_of < g.indices))
+    # cut the graph into two islands: remove every edge crossing the middle column band
+    mid = (g.lon.min() + g.lon.max()) / 2
+    cross = (g.lon[src_of] < mid) != (g.lon[g.indices] < mid)
+    keep &= ~cross
+    indices = g.indices[keep]
+    counts = np.bincount(src_of[keep], minlength=g.num_nodes)
+    indptr = np.zeros(g.num_nodes + 1, np.int32)
+    np.cumsum(counts, out=indptr[1:])
+    length = g.length_m[keep]
+    cost = (length / 12.0).astype(np.float32)
+    c = rt.CCH(indptr, indices.astype(np.int32), g.lat, g.lon, 4)
+    m = c.customize(cost, length.astype(np.float32))
+    src, dst = synth_route_queries(g, 400, seed=2, min_km=0.1)
+    sec, met, st, paths = c.query(m, src, dst, True)
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import dijkstra
+    A = csr_matrix((cost.astype(np.float64), indices, indptr), shape=(g.num_nodes,) * 2)
+    d = dijkstra(A, directed=True, indices=np.unique(src))
+    row = {s: i for i, s in enumerate(np.unique(src))}
+    ref = np.array([d[row[s], t] for s, t in zip(src, dst)])
+    assert (np.isfinite(ref) == (st == 0)).all()                     # islands: unreachable = status 1
+    assert (st != 0).sum() > 20 and (st == 0).sum() > 100
+    ok = st == 0
+    np.testing.assert_allclose(sec[ok], ref[ok], rtol=1e-5, atol=1e-4)
+
+
+def test_matrix_is_the_legs(small):
+    g, cost, c = small
+    m = c.customize(cost, g.length_m)
+    from routest_amd.routing.cch import RoadRouter
+    r = RoadRouter.__new__(RoadRouter)          # a CPU router around this CCH
+    r.g, r.cpu, r.gpu, r.max_path = g, c, None, 4096
+    r._cpu_metrics = {7: m}
+    nodes = [5, 900, 1700, 4000, 5999]
+    sec, met = r.matrix(nodes, 7)
+    assert sec.shape == (5, 5) and (np.diag(sec) == 0).all() and (np.diag(met) == 0).all()
+    for i in range(5):
+        for j in range(5):
+            if i == j:
+                continue
+            s1, m1, st1, _ = c.query(m, np.array([nodes[i]], np.int32), np.array([nodes[j]], np.int32), False)
+            assert st1[0] == 0 and sec[i, j] == s1[0] and met[i, j] == m1[0]
+
+
+def test_routing_context_changes_costs_and_stays_exact():
+    from routest_amd.routing.cch import RoadRouter, RouteContext
+    from routest_amd.serve.eta_service import default_model
+    g = synth_road_graph(4000, seed=9)
+    router = RoadRouter(g, default_model(hidden=64, steps=60), device=None, threads=4)
+    sunny = RouteContext.from_request({"context": {"weather": "Sunny", "traffic": "Low",
+                                                   "pickup_time": "2025-08-26T03:00:00"}})
+    storm = RouteContext.from_request({"context": {"weather": "Stormy", "traffic": "Jam",
+                                                   "pickup_time": "2025-08-29T18:00:00"}})
+    assert sunny.weekhour == 1 * 24 + 3 and storm.weekhour == 4 * 24 + 18
+    assert sunny.key != storm.key
+    src, dst = synth_route_queries(g, 200, seed=4, min_km=1.0)
+    out = {}
+    for name, ctx in (("sunny", sunny), ("storm", storm)):
+        sec, met, st, paths = router.route(src, dst, ctx)
+        cost = router.costs(ctx)
+        assert (st == 0).all()
+        np.testing.assert_allclose(sec, dijkstra_ref(g, cost, src, dst), rtol=1e-5, atol=1e-4)
+        out[name] = sec
+    assert not np.allclose(out["sunny"], out["storm"])
+    # defaults: Sunny / Low, week-hour of now
+    d = RouteContext.from_request({}, now=dt.datetime(2025, 8, 31, 23, 30))
+    assert (d.weather, d.congestion, d.weekhour) == (2, 0, 6 * 24 + 23)
+    assert RouteContext.from_request({"context": {"weather": "Foggy", "traffic": 3}}).weather == 255

@@ -1,0 +1,96 @@
+"""GPU customizable contraction hierarchy (csrc/cch.hip) vs the CPU reference (csrc/runtime/cch.h)
+and scipy Dijkstra, on the 100k-node synthetic graph with MLP edge costs.
+
+* customization + queries are BIT-identical to the CPU reference (same tie rules, f32 adds);
+* every leg equals Dijkstra; paths are real edge sequences;
+* matrices equal the legs; contexts customize on the GPU and change the answers.
+"""
+import numpy as np
+import pytest
+import torch
+
+from routest_amd.data.graph import synth_road_graph, synth_route_queries
+from routest_amd.routing.graph import dijkstra_ref, edge_costs
+from routest_amd.serve.eta_service import default_model
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def setup():
+    from routest_amd.routing.cch import RoadRouter
+    g = synth_road_graph(100_000, seed=5)
+    m = default_model(hidden=64, steps=50)
+    router = RoadRouter(g, m, device="cuda:0")
+    cost = edge_costs(g, m, device="cuda:0")
+    key = router.metric_from_costs(1 << 40, cost)
+    from routest_amd import _rt
+    cpu = _rt.CCH(g.indptr, g.indices, g.lat, g.lon, 0)
+    mc = cpu.customize(cost, g.length_m)
+    return g, m, router, cost, key, cpu, mc
+
+
+def test_legs_exact_and_bit_identical_to_cpu(setup):
+    g, m, router, cost, key, cpu, mc = setup
+    src, dst = synth_route_queries(g, 3000, seed=1)
+    src[:4] = dst[:4]
+    sec, met, st, paths = router.route(src, dst, key)
+    assert (st == 0).all(), np.unique(st, return_counts=True)
+    ref = dijkstra_ref(g, cost, src, dst)
+    np.testing.assert_allclose(sec, ref, rtol=1e-5, atol=1e-4)
+    s2, m2, st2, p2 = cpu.query(mc, src, dst, True)
+    assert np.array_equal(sec, s2) and np.array_equal(met, m2) and np.array_equal(st, st2)
+    assert all(np.array_equal(a, b) for a, b in zip(paths, p2))
+    for i in range(0, 3000, 61):
+        p = paths[i]
+        assert p[0] == src[i] and p[-1] == dst[i]
+        tot = 0.0
+        for u, v in zip(p[:-1], p[1:]):
+            nb = g.indices[g.indptr[u]:g.indptr[u + 1]]
+            k = np.where(nb == v)[0]
+            assert len(k) == 1
+            tot += cost[g.indptr[u] + k[0]]
+        assert abs(tot - sec[i]) <= 1e-4 * max(1.0, sec[i])
+    # repeatable
+    sec_b = router.route(src, dst, key, want_path=False)[0]
+    assert np.array_equal(sec, sec_b)
+
+
+def test_matrices_equal_legs(setup):
+    g, m, router, cost, key, cpu, mc = setup
+    rng = np.random.default_rng(3)
+    lists = [rng.integers(0, g.num_nodes, rng.integers(2, 12)).tolist() for _ in range(40)]
+    mats = router.matrices(lists, key)
+    for nodes, (sec, met) in zip(lists[:10], mats[:10]):
+        n = len(nodes)
+        ii, jj = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+        nd = np.asarray(nodes, np.int32)
+        s2, m2, st2, _ = cpu.query(mc, nd[ii.ravel()], nd[jj.ravel()], False)
+        s2 = s2.reshape(n, n)
+        m2 = m2.reshape(n, n)
+        off = ~np.eye(n, dtype=bool)
+        assert np.array_equal(sec[off], s2[off]) and np.array_equal(met[off], m2[off])
+        assert (np.diag(sec) == 0).all()
+
+
+def test_context_customization_on_gpu(setup):
+    from routest_amd.routing.cch import RouteContext
+    g, m, router, cost, key, cpu, mc = setup
+    sunny = RouteContext(weather=2, congestion=0, weekhour=3)
+    storm = RouteContext(weather=1, congestion=3, weekhour=4 * 24 + 18)
+    src, dst = synth_route_queries(g, 500, seed=9)
+    res = {}
+    for ctx in (sunny, storm):
+        sec, met, st, _ = router.route(src, dst, ctx, want_path=False)
+        info = router.last_metric
+        c = router.costs(ctx)
+        assert (c > 0).all()
+        np.testing.assert_allclose(sec, dijkstra_ref(g, c, src, dst), rtol=1e-5, atol=1e-4)
+        res[ctx.key] = (sec, c)
+    assert not np.allclose(res[sunny.key][0], res[storm.key][0])
+    # cached: a second use does not customize again
+    router.route(src[:10], dst[:10], sunny, want_path=False)
+    assert router.last_metric["fresh"] is False
+    # the GPU context costs match the CPU edge-cost model within bf16 tolerance
+    from routest_amd.routing.cch import context_costs_cpu
+    np.testing.assert_allclose(res[storm.key][1], context_costs_cpu(g, m, storm), rtol=2e-2, atol=0.05)

@@ -58,7 +58,7 @@ def _run(cmd: List[str]) -> None:
 
 NO_SLP = {"eta_mlp_fwd.hip"}
 # host code that must round exactly like Python (csrc/runtime/route_core.h): no FMA contraction
-NO_CONTRACT = {"native_server.hip", "route_service.hip"}
+NO_CONTRACT = {"native_server.hip", "route_service.hip", "cch.hip"}
 # builtin MFMAs write VGPRs: train_bwd_kernel pins its 256 dW2 accumulators to the AGPRs (inline-asm
 # MFMAs), and with the default heuristic the builtin MFMAs beside them also took AGPR destinations,
 # which made the allocator park accumulator tiles in VGPRs and copy them around every MFMA
@@ -89,17 +89,18 @@ def build_C(force: bool = False, jobs: int = 8) -> str:
                 extra += ["-mllvm", "-amdgpu-mfma-vgpr-form"]
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common, *extra, "-munsafe-fp-atomics",
                               "-I", CSRC, "-I", os.path.join(ROCM, "include"), "-c", src, "-o", obj])
-    bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(BUILD, "bindings.cpp.o")
-    objs.append(bobj)
-    if force or _newer(bobj, [bsrc] + headers):
-        cmd = [hipcc, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-               "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
-               "-I", CSRC, "-I", py_inc]
-        for d in inc:
-            cmd += ["-I", d]
-        cmd += ["-Wno-unused-result", "-Wno-deprecated-declarations", "-c", bsrc, "-o", bobj]
-        jobs_list.append(cmd)
+    # torch binding translation units: csrc/bindings.cpp (the module) + csrc/*_bindings.cpp
+    for bsrc in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):
+        bobj = os.path.join(BUILD, os.path.basename(bsrc) + ".o")
+        objs.append(bobj)
+        if force or _newer(bobj, [bsrc] + headers):
+            cmd = [hipcc, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+                   "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                   "-I", CSRC, "-I", py_inc]
+            for d in inc:
+                cmd += ["-I", d]
+            cmd += ["-Wno-unused-result", "-Wno-deprecated-declarations", "-c", bsrc, "-o", bobj]
+            jobs_list.append(cmd)
     with ThreadPoolExecutor(max(1, jobs)) as ex:
         list(ex.map(_run, jobs_list))
     out = os.path.join(PKG, "_C" + EXT_SUFFIX)
