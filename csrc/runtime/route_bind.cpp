@@ -77,6 +77,71 @@ class PyNodeGrid {
   double c_;
 };
 
+// Maneuvers of graph legs (route_core.h leg_steps) for the Python GraphProvider: the graph's
+// arrays are held once; per call the leg's node path, seconds and the context's edge costs.
+class PyGraphSteps {
+ public:
+  PyGraphSteps(py::array_t<int32_t, py::array::c_style | py::array::forcecast> indptr,
+               py::array_t<int32_t, py::array::c_style | py::array::forcecast> indices,
+               py::array_t<float, py::array::c_style | py::array::forcecast> length,
+               py::array_t<double, py::array::c_style | py::array::forcecast> lat,
+               py::array_t<double, py::array::c_style | py::array::forcecast> lon, py::object edge_name,
+               std::vector<std::string> names)
+      : indptr_(indptr), indices_(indices), length_(length), lat_(lat), lon_(lon), names_(std::move(names)) {
+    const py::ssize_t N = lat.shape(0), E = indices.shape(0);
+    if (indptr.shape(0) != N + 1 || lon.shape(0) != N || length.shape(0) != E || indptr.data()[N] != E)
+      throw std::invalid_argument("graph shapes");
+    if (!edge_name.is_none()) {
+      name_ = edge_name.cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>();
+      if (name_.shape(0) != E) throw std::invalid_argument("edge_name per edge");
+    }
+  }
+  // the graph host view with the given per-edge costs (kept alive by the caller)
+  rtr::GraphHost host(const py::array_t<float, py::array::c_style | py::array::forcecast>& cost) const {
+    if (cost.shape(0) != indices_.shape(0)) throw std::invalid_argument("cost per edge");
+    rtr::GraphHost g;
+    g.indptr = indptr_.data();
+    g.indices = indices_.data();
+    g.length = length_.data();
+    g.cost = cost.data();
+    g.edge_name = name_.size() ? name_.data() : nullptr;
+    g.names = &names_;
+    return g;
+  }
+  py::list steps(py::array_t<int32_t, py::array::c_style | py::array::forcecast> path, double sec,
+                 py::array_t<float, py::array::c_style | py::array::forcecast> cost, double speed_scale,
+                 long long start, long long end) const {
+    const py::ssize_t N = lat_.shape(0);
+    if (cost.shape(0) != indices_.shape(0)) throw std::invalid_argument("cost per edge");
+    for (py::ssize_t i = 0; i < path.shape(0); ++i)
+      if (path.data()[i] < 0 || path.data()[i] >= N) throw std::out_of_range("path node");
+    rtr::GraphHost g;
+    g.indptr = indptr_.data();
+    g.indices = indices_.data();
+    g.length = length_.data();
+    g.cost = cost.data();
+    g.edge_name = name_.size() ? name_.data() : nullptr;
+    g.names = &names_;
+    rtr::Leg L;
+    L.sec = (float)sec;
+    L.path = path.data();
+    L.len = (int)path.shape(0);
+    std::vector<rtr::Step> st;
+    rtr::leg_steps(g, lat_.data(), lon_.data(), L, speed_scale, start, end, st);
+    py::list out;
+    for (const auto& x : st)
+      out.append(py::make_tuple(x.dist, x.dur, x.type, x.instruction, x.name, x.wp0, x.wp1));
+    return out;
+  }
+
+ private:
+  py::array_t<int32_t, py::array::c_style | py::array::forcecast> indptr_, indices_;
+  py::array_t<float, py::array::c_style | py::array::forcecast> length_;
+  py::array_t<double, py::array::c_style | py::array::forcecast> lat_, lon_;
+  py::array_t<int32_t, py::array::c_style | py::array::forcecast> name_;
+  std::vector<std::string> names_;
+};
+
 py::bytes to_bytes(const std::string& s) { return py::bytes(s); }
 
 // Finish an assembled request as the FastAPI handler answers it (no ETA, no persistence).
@@ -135,12 +200,13 @@ py::object route_optimize_cpu(py::bytes body, bool json_ok, const std::string& e
 }
 
 // Graph-provider assembly with given trips and searched legs: `trips` per request as index lists
-// (None for point-to-point), `legs` {(s, t): (seconds, [nodes])} (missing / empty = not found).
+// (None for point-to-point), `legs` {(s, t): (seconds, [nodes]) | (seconds, metres, [nodes])}
+// (missing / empty = not found); with `steps` (GraphSteps) + `cost` the segments carry maneuvers.
 py::object route_assemble_graph(py::bytes body, const std::string& engine,
                                 py::array_t<double, py::array::c_style | py::array::forcecast> glat,
                                 py::array_t<double, py::array::c_style | py::array::forcecast> glon,
                                 py::array_t<int32_t, py::array::c_style | py::array::forcecast> nodes_of_calls,
-                                py::object trips_obj, py::dict legs_obj) {
+                                py::object trips_obj, py::dict legs_obj, py::object steps_obj, py::object cost_obj) {
   const std::string b = body;
   Value root = rtj::Parser(b.data(), b.size()).parse();
   rtr::RouteReq r = rtr::parse_route_request(&root);
@@ -153,12 +219,25 @@ py::object route_assemble_graph(py::bytes body, const std::string& engine,
   std::map<std::pair<int, int>, std::pair<rtr::Leg, std::vector<int32_t>>> table;
   for (auto kv : legs_obj) {
     auto key = kv.first.cast<std::pair<int, int>>();
-    auto val = kv.second.cast<std::pair<double, std::vector<int32_t>>>();
+    py::tuple val = kv.second.cast<py::tuple>();
     auto& e = table[key];
-    e.second = val.second;
-    e.first.sec = (float)val.first;
+    e.first.sec = (float)val[0].cast<double>();
+    if (val.size() == 3) {
+      e.first.metres = (float)val[1].cast<double>();
+      e.second = val[2].cast<std::vector<int32_t>>();
+    } else {
+      e.second = val[1].cast<std::vector<int32_t>>();
+    }
     e.first.len = (int)e.second.size();
     e.first.path = e.second.data();
+  }
+  rtr::GraphHost gh;
+  const rtr::GraphHost* ghp = nullptr;
+  py::array_t<float, py::array::c_style | py::array::forcecast> cost;
+  if (!steps_obj.is_none() && !cost_obj.is_none()) {
+    cost = cost_obj.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+    gh = steps_obj.cast<const PyGraphSteps&>().host(cost);
+    ghp = &gh;
   }
   const int32_t* nodes = nodes_of_calls.data();
   std::vector<rtr::Dir> dirs(calls.size());
@@ -170,7 +249,8 @@ py::object route_assemble_graph(py::bytes body, const std::string& engine,
       auto it = table.find({nodes[off + i], nodes[off + i + 1]});
       legs.push_back(it == table.end() ? &missing : &it->second.first);
     }
-    const std::string e = rtr::graph_directions(calls[k], nodes + off, legs, r.profile, glat.data(), glon.data(), dirs[k]);
+    const std::string e = rtr::graph_directions(calls[k], nodes + off, legs, r.profile, glat.data(), glon.data(), dirs[k],
+                                                ghp);
     off += calls[k].size();
     if (!e.empty()) {
       r.error = e;
@@ -196,7 +276,20 @@ void bind_route(py::module& m) {
   m.def("route_optimize_cpu", &route_optimize_cpu, py::arg("body"), py::arg("json_ok") = true,
         py::arg("engine") = "backend:mi355x", py::arg("circuity") = 1.3, py::arg("step_m") = 150.0,
         py::arg("is_request_route") = false, py::arg("compat200") = true);
-  m.def("route_assemble_graph", &route_assemble_graph);
+  m.def("route_assemble_graph", &route_assemble_graph, py::arg("body"), py::arg("engine"), py::arg("glat"),
+        py::arg("glon"), py::arg("nodes"), py::arg("trips"), py::arg("legs"), py::arg("steps") = py::none(),
+        py::arg("cost") = py::none());
   m.def("py_round", &rtr::py_round);
+  py::class_<PyGraphSteps>(m, "GraphSteps")
+      .def(py::init<py::array_t<int32_t, py::array::c_style | py::array::forcecast>,
+                    py::array_t<int32_t, py::array::c_style | py::array::forcecast>,
+                    py::array_t<float, py::array::c_style | py::array::forcecast>,
+                    py::array_t<double, py::array::c_style | py::array::forcecast>,
+                    py::array_t<double, py::array::c_style | py::array::forcecast>, py::object,
+                    std::vector<std::string>>(),
+           py::arg("indptr"), py::arg("indices"), py::arg("length"), py::arg("lat"), py::arg("lon"),
+           py::arg("edge_name") = py::none(), py::arg("names") = std::vector<std::string>())
+      .def("steps", &PyGraphSteps::steps, py::arg("path"), py::arg("sec"), py::arg("cost"), py::arg("speed_scale"),
+           py::arg("start"), py::arg("end"));
   m.def("bearing_word", [](double a, double b, double c, double d) { return std::string(rtr::bearing_word(a, b, c, d)); });
 }

@@ -443,17 +443,156 @@ inline void haversine_directions(const std::vector<std::pair<double, double>>& c
   out.dur = py_round(tot_d / speed, 1);
 }
 
-// One searched leg: seconds (the f32 A* cost) and the node path.
+// One searched leg: seconds (the f32 router cost), the node path and, from the CCH router, the
+// metre length of that path (< 0: unknown -> summed from node coordinates, the A* legacy).
 struct Leg {
   float sec = 0.f;
   const int32_t* path = nullptr;
   int len = 0;                    // 0 = not found
+  float metres = -1.f;
 };
+
+// Host view of the road graph for maneuvers: CSR, per-edge metres and seconds (the leg's routing
+// context), road name ids (-1 unnamed) and the name table.
+struct GraphHost {
+  const int32_t* indptr = nullptr;
+  const int32_t* indices = nullptr;
+  const float* length = nullptr;
+  const float* cost = nullptr;
+  const int32_t* edge_name = nullptr;
+  const std::vector<std::string>* names = nullptr;
+};
+
+// initial bearing (degrees, [0, 360)) — the same expression bearing_word rounds
+inline double bearing_deg(double lat1, double lon1, double lat2, double lon2) {
+  const double d2r = PY_PI / 180.0, r2d = 180.0 / PY_PI;
+  const double y = std::sin((lon2 - lon1) * d2r) * std::cos(lat2 * d2r);
+  const double x = std::cos(lat1 * d2r) * std::sin(lat2 * d2r) -
+                   std::sin(lat1 * d2r) * std::cos(lat2 * d2r) * std::cos((lon2 - lon1) * d2r);
+  return py_mod(std::atan2(y, x) * r2d + 360.0, 360.0);
+}
+
+// ORS maneuver type of a heading change (degrees, (-180, 180], positive = clockwise = right):
+// 6 straight, 4/5 slight left/right, 0/1 left/right, 2/3 sharp left/right, 9 U-turn
+inline int turn_type(double delta) {
+  const double a = std::fabs(delta);
+  if (a < 25.0) return 6;
+  if (a < 50.0) return delta > 0 ? 5 : 4;
+  if (a < 130.0) return delta > 0 ? 1 : 0;
+  if (a < 170.0) return delta > 0 ? 3 : 2;
+  return 9;
+}
+inline const char* turn_verb(int type) {
+  switch (type) {
+    case 0: return "Turn left";
+    case 1: return "Turn right";
+    case 2: return "Turn sharp left";
+    case 3: return "Turn sharp right";
+    case 4: return "Turn slight left";
+    case 5: return "Turn slight right";
+    case 9: return "Make a U-turn";
+    default: return "Continue straight";
+  }
+}
+inline double heading_change(double b_in, double b_out) {
+  double d = py_mod(b_out - b_in + 180.0, 360.0) - 180.0;
+  if (d == -180.0) d = 180.0;
+  return d;
+}
+
+// the edge a path hop u -> v took: the cheapest under the leg's costs (lowest id on a tie — the
+// router's own rule for parallel edges), -1 if none
+inline int32_t hop_edge(const GraphHost& g, int32_t u, int32_t v) {
+  int32_t best = -1;
+  for (int32_t e = g.indptr[u]; e < g.indptr[u + 1]; ++e)
+    if (g.indices[e] == v && (best < 0 || g.cost[e] < g.cost[best])) best = e;
+  return best;
+}
+
+// One maneuver step of a graph leg (routing/graph.py leg_steps mirrors the fields).
+struct Step {
+  double dist = 0, dur = 0;       // rounded to 0.1
+  int type = 11;
+  std::string instruction, name;
+  long long wp0 = 0, wp1 = 0;
+};
+
+// Maneuvers along one leg's node path.  A new step starts where the road name changes or the
+// heading turns by >= 50 degrees; its type comes from the heading change at its first node, its
+// instruction is "Head <dir>[ on <name>]" for the first step, "<verb>[ onto <name>]" after.
+// Geometry indices: the leg's start coordinate is `start`, path node i is start + 1 + i, the
+// destination coordinate `end`.  Distances / durations are the hop edges' metres / seconds.
+inline void leg_steps(const GraphHost& g, const double* glat, const double* glon, const Leg& L, double speed_scale,
+                      long long start, long long end, std::vector<Step>& out) {
+  out.clear();
+  const int n = L.len;
+  if (n <= 1) {
+    Step s;
+    s.dist = 0.0;
+    s.dur = py_round((double)L.sec * speed_scale, 1);
+    s.instruction = "Depart";
+    s.name = "-";
+    s.wp0 = start;
+    s.wp1 = end;
+    out.push_back(std::move(s));
+    return;
+  }
+  const int H = n - 1;
+  std::vector<int32_t> hop(H), nm(H);
+  std::vector<double> brg(H);
+  for (int h = 0; h < H; ++h) {
+    const int32_t u = L.path[h], v = L.path[h + 1];
+    hop[h] = hop_edge(g, u, v);
+    nm[h] = (hop[h] >= 0 && g.edge_name) ? g.edge_name[hop[h]] : -1;
+    brg[h] = bearing_deg(glat[u], glon[u], glat[v], glon[v]);
+  }
+  auto name_of = [&](int32_t id) -> std::string {
+    return (id >= 0 && g.names && id < (int32_t)g.names->size()) ? (*g.names)[id] : std::string("-");
+  };
+  int h0 = 0;
+  while (h0 < H) {
+    int h1 = h0 + 1;
+    while (h1 < H && nm[h1] == nm[h1 - 1] && std::fabs(heading_change(brg[h1 - 1], brg[h1])) < 50.0) ++h1;
+    Step s;
+    double d = 0.0, t = 0.0;
+    for (int h = h0; h < h1; ++h)
+      if (hop[h] >= 0) {
+        d += (double)g.length[hop[h]];
+        t += (double)g.cost[hop[h]];
+      }
+    s.dist = py_round(d, 1);
+    s.dur = py_round(t * speed_scale, 1);
+    s.name = name_of(nm[h0]);
+    const bool named = nm[h0] >= 0;
+    if (h0 == 0) {
+      s.type = 11;
+      s.instruction = std::string("Head ") + bearing_word(glat[L.path[0]], glon[L.path[0]], glat[L.path[1]], glon[L.path[1]]);
+      if (named) s.instruction += " on " + s.name;
+    } else {
+      s.type = turn_type(heading_change(brg[h0 - 1], brg[h0]));
+      s.instruction = turn_verb(s.type);
+      if (named) s.instruction += " onto " + s.name;
+    }
+    s.wp0 = h0 == 0 ? start : start + 1 + h0;
+    s.wp1 = h1 == H ? end : start + 1 + h1;
+    out.push_back(std::move(s));
+    h0 = h1;
+  }
+}
+
+inline void put_step(std::string& o, const Step& s) {
+  o += "{\"distance\":"; put_float(o, s.dist);
+  o += ",\"duration\":"; put_float(o, s.dur);
+  o += ",\"type\":"; put_int(o, s.type);
+  o += ",\"instruction\":"; put_str(o, s.instruction);
+  o += ",\"name\":"; put_str(o, s.name);
+  o += ",\"way_points\":["; put_int(o, s.wp0); o += ','; put_int(o, s.wp1); o += "]}";
+}
 
 // GraphProvider.feature_from_legs — graph.py.  Returns "" or the ProviderError text.
 inline std::string graph_directions(const std::vector<std::pair<double, double>>& c, const int32_t* nodes,
                                     const std::vector<const Leg*>& legs, int profile, const double* glat,
-                                    const double* glon, Dir& out) {
+                                    const double* glon, Dir& out, const GraphHost* gh = nullptr) {
   const double speed_scale = profile_speed(CAR) / profile_speed(profile);
   out.xy.assign({c[0].first, c[0].second});
   out.raw.assign({1});
@@ -470,7 +609,8 @@ inline std::string graph_directions(const std::vector<std::pair<double, double>>
       put_int(e, nodes[k]); e += " -> "; put_int(e, nodes[k + 1]); e += ")";
       return e;
     }
-    const double dist = L.len > 1 ? path_length_m(glat, glon, L.path, (size_t)L.len) * 1.15 : 0.0;
+    const double dist = L.metres >= 0.f ? (double)L.metres
+                      : L.len > 1 ? path_length_m(glat, glon, L.path, (size_t)L.len) * 1.15 : 0.0;
     for (int i = 0; i < L.len; ++i) {
       out.xy.push_back(np_round6(glon[L.path[i]]));
       out.xy.push_back(np_round6(glat[L.path[i]]));
@@ -483,7 +623,28 @@ inline std::string graph_directions(const std::vector<std::pair<double, double>>
     out.way_points.push_back(end);
     const double dur = (double)L.sec * speed_scale;
     if (k) out.segments += ',';
-    step_pair(out.segments, py_round(dist, 1), py_round(dur, 1), k, nlegs, "Follow the road network", start, end);
+    if (gh != nullptr && gh->cost != nullptr) {
+      // maneuvers along the path, then the arrival step (routing/graph.py feature_from_legs)
+      std::vector<Step> steps;
+      leg_steps(*gh, glat, glon, L, speed_scale, start, end, steps);
+      std::string& sg = out.segments;
+      sg += "{\"distance\":"; put_float(sg, py_round(dist, 1));
+      sg += ",\"duration\":"; put_float(sg, py_round(dur, 1));
+      sg += ",\"steps\":[";
+      for (const Step& st : steps) { put_step(sg, st); sg += ','; }
+      sg += "{\"distance\":0.0,\"duration\":0.0,\"type\":10,\"instruction\":";
+      if (k == nlegs - 1) {
+        put_str(sg, "Arrive at your destination");
+      } else {
+        std::string w = "Arrive at waypoint ";
+        put_int(w, k + 1);
+        put_str(sg, w);
+      }
+      sg += ",\"name\":\"-\",\"way_points\":["; put_int(sg, end); sg += ','; put_int(sg, end);
+      sg += "]}]}";
+    } else {
+      step_pair(out.segments, py_round(dist, 1), py_round(dur, 1), k, nlegs, "Follow the road network", start, end);
+    }
     tot_d += dist;
     tot_t += dur;
   }

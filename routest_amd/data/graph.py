@@ -14,7 +14,7 @@ locations live in (``LV/database/seeders/LocationsTableSeeder.php:13-34``):
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import numpy as np
 
@@ -38,6 +38,8 @@ class RoadGraph:
     features: np.ndarray     # [N, F] f32
     rows: int = 0
     cols: int = 0
+    edge_name: Optional[np.ndarray] = None   # [E] i32 road name id (-1 unnamed)
+    names: Optional[List[str]] = None        # name table
 
     @property
     def num_nodes(self) -> int:
@@ -84,15 +86,25 @@ class RoadGraph:
         return i.astype(np.int32)
 
     def save(self, path: str) -> None:
+        extra = {}
+        if self.edge_name is not None:
+            extra["edge_name"] = self.edge_name
+            extra["names"] = np.array(self.names or [], dtype=str)
         np.savez_compressed(path, **{k: getattr(self, k) for k in (
             "lat", "lon", "indptr", "indices", "length_m", "road_class", "gcn_indptr", "gcn_indices",
-            "gcn_values", "features")}, rows=self.rows, cols=self.cols)
+            "gcn_values", "features")}, rows=self.rows, cols=self.cols, **extra)
 
     @staticmethod
     def load(path: str) -> "RoadGraph":
         z = np.load(path, allow_pickle=False)
-        kw = {k: z[k] for k in z.files if k not in ("rows", "cols")}
-        return RoadGraph(**kw, rows=int(z["rows"]), cols=int(z["cols"]))
+        kw = {k: z[k] for k in z.files if k not in ("rows", "cols", "names")}
+        names = [str(x) for x in z["names"]] if "names" in z.files else None
+        return RoadGraph(**kw, rows=int(z["rows"]), cols=int(z["cols"]), names=names)
+
+    def name_of_edge(self, e: int) -> str:
+        if self.edge_name is None or self.edge_name[e] < 0:
+            return "-"
+        return self.names[int(self.edge_name[e])]
 
 
 def _edge_class(r0, c0, r1, c1) -> np.ndarray:
@@ -129,41 +141,90 @@ def synth_road_graph(num_nodes: int = 100_000, seed: int = 0, feat_dim: int = 32
     s = np.concatenate(src)
     d = np.concatenate(dst)
     cls = _edge_class(rr[s], cc[s], rr[d], cc[d])
-    # directed both ways
-    s2 = np.concatenate([s, d])
-    d2 = np.concatenate([d, s])
-    cls2 = np.concatenate([cls, cls])
-    order = np.lexsort((d2, s2))
-    s2, d2, cls2 = s2[order], d2[order], cls2[order]
+    # road names along the grid lines ("R-<row>" streets run east-west, "C-<col>" north-south, the
+    # suffix by class, like Metro Manila's radial / circumferential roads); diagonals are unnamed
+    suffix = np.array(["Street", "Avenue", "Boulevard", "Expressway"])
+    horiz = rr[s] == rr[d]
+    vert = cc[s] == cc[d]
+    names = [f"R-{r} {suffix[c]}" for r in range(rows) for c in range(4)] + \
+            [f"C-{c} {suffix[k]}" for c in range(cols) for k in range(4)]
+    name_id = np.where(horiz, rr[s] * 4 + cls, np.where(vert, rows * 4 + cc[s] * 4 + cls, -1)).astype(np.int32)
+    return build_graph(lat, lon, s, d, cls, name_id=name_id, names=names, both_ways=True, rng=rng,
+                       feat_dim=feat_dim, rows=rows, cols=cols, bbox=BBOX)
+
+
+def build_graph(lat: np.ndarray, lon: np.ndarray, s: np.ndarray, d: np.ndarray, cls: np.ndarray,
+                length_m: Optional[np.ndarray] = None, name_id: Optional[np.ndarray] = None,
+                names: Optional[List[str]] = None, both_ways: bool = False, seed: int = 0,
+                feat_dim: int = 32, rows: int = 0, cols: int = 0,
+                rng: Optional[np.random.Generator] = None,
+                bbox: Optional[Tuple[float, float, float, float]] = None) -> RoadGraph:
+    """RoadGraph from a directed edge list (``both_ways``: every edge also in reverse): CSR sorted by
+    (source, target) with parallel edges merged (the shortest kept), lengths by haversine x 1.15
+    unless given, the GCN operator and node features."""
+    n = len(lat)
+    lat = np.asarray(lat, dtype=np.float64)
+    lon = np.asarray(lon, dtype=np.float64)
+    s = np.asarray(s, dtype=np.int64)
+    d = np.asarray(d, dtype=np.int64)
+    cls = np.asarray(cls, dtype=np.uint8)
+    if length_m is None:
+        length_m = haversine_m(lat[s], lon[s], lat[d], lon[d]).astype(np.float32) * np.float32(1.15)
+    length_m = np.asarray(length_m, dtype=np.float32)
+    nid = np.asarray(name_id, dtype=np.int32) if name_id is not None else None
+    if both_ways:
+        s, d = np.concatenate([s, d]), np.concatenate([d, s])
+        cls = np.concatenate([cls, cls])
+        length_m = np.concatenate([length_m, length_m])
+        nid = np.concatenate([nid, nid]) if nid is not None else None
+    keep = s != d                                           # no self loops
+    s, d, cls, length_m = s[keep], d[keep], cls[keep], length_m[keep]
+    nid = nid[keep] if nid is not None else None
+    order = np.lexsort((length_m, d, s))
+    s2, d2, cls2, length = s[order], d[order], cls[order], length_m[order]
+    nid = nid[order] if nid is not None else None
+    first = np.ones(len(s2), dtype=bool)                    # parallel edges: keep the shortest
+    first[1:] = (s2[1:] != s2[:-1]) | (d2[1:] != d2[:-1])
+    s2, d2, cls2, length = s2[first], d2[first], cls2[first], length[first]
+    nid = nid[first] if nid is not None else None
     indptr = np.zeros(n + 1, dtype=np.int64)
     np.add.at(indptr, s2 + 1, 1)
     indptr = np.cumsum(indptr).astype(np.int32)
-    length = haversine_m(lat[s2], lon[s2], lat[d2], lon[d2]).astype(np.float32) * np.float32(1.15)
 
     deg = np.diff(indptr).astype(np.float64) + 1.0
-    # Â with self loops, row-sorted CSR
-    gs = np.concatenate([s2, np.arange(n)])
-    gd = np.concatenate([d2, np.arange(n)])
+    # Â with self loops, row-sorted CSR (symmetrised: one-way streets still couple their ends)
+    us = np.concatenate([s2, d2])
+    ud = np.concatenate([d2, s2])
+    pair = np.unique(us * n + ud)
+    us, ud = pair // n, pair % n
+    udeg = np.bincount(us, minlength=n).astype(np.float64) + 1.0
+    gs = np.concatenate([us, np.arange(n)])
+    gd = np.concatenate([ud, np.arange(n)])
     go = np.lexsort((gd, gs))
     gs, gd = gs[go], gd[go]
-    gval = (1.0 / np.sqrt(deg[gs] * deg[gd])).astype(np.float32)
+    gval = (1.0 / np.sqrt(udeg[gs] * udeg[gd])).astype(np.float32)
     gptr = np.zeros(n + 1, dtype=np.int64)
     np.add.at(gptr, gs + 1, 1)
     gptr = np.cumsum(gptr).astype(np.int32)
 
     # node features
+    rng = rng if rng is not None else np.random.default_rng(seed)
+    if bbox is None:
+        bbox = (float(lat.min()), float(lon.min()), float(lat.max()), float(lon.max()))
+    lat0, lon0, lat1, lon1 = bbox
     f = np.zeros((n, feat_dim), dtype=np.float32)
-    f[:, 0] = (lat - lat0) / (lat1 - lat0) * 2 - 1
-    f[:, 1] = (lon - lon0) / (lon1 - lon0) * 2 - 1
-    f[:, 2] = (deg - deg.mean()) / deg.std()
+    f[:, 0] = (lat - lat0) / max(lat1 - lat0, 1e-12) * 2 - 1
+    f[:, 1] = (lon - lon0) / max(lon1 - lon0, 1e-12) * 2 - 1
+    f[:, 2] = (deg - deg.mean()) / max(deg.std(), 1e-12)
     cls_mix = np.zeros((n, 4), dtype=np.float32)
-    np.add.at(cls_mix, (s2, cls2), 1.0)
+    np.add.at(cls_mix, (s2, np.minimum(cls2, 3)), 1.0)
     f[:, 3:7] = cls_mix / np.maximum(1.0, cls_mix.sum(1, keepdims=True))
     k = feat_dim - 7
     proj = rng.standard_normal((2, k)).astype(np.float32)
     f[:, 7:] = np.sin(f[:, 0:2] @ proj * 3.0)
-    return RoadGraph(lat, lon, indptr, d2.astype(np.int32), length, cls2, gptr, gd.astype(np.int32),
-                     gval, f, rows, cols)
+    return RoadGraph(lat, lon, indptr, d2.astype(np.int32), length.astype(np.float32), cls2, gptr,
+                     gd.astype(np.int32), gval, f, rows, cols, edge_name=nid,
+                     names=list(names) if names is not None else None)
 
 
 def synth_route_queries(g: RoadGraph, n: int, seed: int = 0, min_km: float = 1.0,

@@ -71,11 +71,15 @@ def _unpack(visit: np.ndarray, trip_of: np.ndarray, ntrips: np.ndarray, status: 
     return out
 
 
-def batched_trips_device(lat, lon, dem, npts, cap, maxd, circuity: float, device) -> List[TripsOrError]:
+def batched_trips_device(lat, lon, dem, npts, cap, maxd, circuity: float, device,
+                         D: Optional[np.ndarray] = None) -> List[TripsOrError]:
     C = _ext.native(required=True)
     dev = torch.device(device)
     t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt).to(dev)  # noqa: E731
-    D = C.route_haversine_matrix(t(lat), t(lon), t(npts, torch.int32), float(circuity))
+    if D is None:
+        D = C.route_haversine_matrix(t(lat), t(lon), t(npts, torch.int32), float(circuity))
+    else:
+        D = t(np.ascontiguousarray(D, dtype=np.float64))
     visit, trip_of, ntrips, status = C.route_greedy_cvrp(D, t(npts, torch.int32), t(dem), t(cap),
                                                          t(maxd))
     return _unpack(visit.cpu().numpy(), trip_of.cpu().numpy(), ntrips.cpu().numpy(),
@@ -96,10 +100,12 @@ def batched_trips_cpu(lat, lon, dem, npts, cap, maxd, circuity: float,
 
 
 def batched_trips(requests: Sequence[Dict[str, Any]], circuity: float = 1.3,
-                  device: Optional[Any] = None) -> List[TripsOrError]:
+                  device: Optional[Any] = None, D: Optional[np.ndarray] = None) -> List[TripsOrError]:
+    """``D``: given distance matrices [R, nm, nm] (road metres from the CCH router) instead of the
+    haversine K5."""
     if not requests:
         return []
     packed = pack_requests(requests)
     if device is not None and torch.device(device).type == "cuda":
-        return batched_trips_device(*packed, circuity=circuity, device=device)
-    return batched_trips_cpu(*packed, circuity=circuity)
+        return batched_trips_device(*packed, circuity=circuity, device=device, D=D)
+    return batched_trips_cpu(*packed, circuity=circuity, D=D)

@@ -451,20 +451,50 @@ def _path_length(g: RoadGraph, p: np.ndarray) -> float:
 
 
 class GraphProvider(HaversineProvider):
-    """Directions along shortest paths of the road graph (durations from learned edge costs)."""
+    """Directions and road-distance matrices on the road graph (replaces the reference's per-trip
+    ORS directions and per-request ORS matrix, ``RO/Flaskr/utils.py:55-62,97-105,151-156``).
+
+    Engines (``ROUTEST_ROUTER``): ``cch`` (default) — :class:`routing.cch.RoadRouter`, the
+    context-aware customizable contraction hierarchy (GPU, or the CPU reference without one);
+    ``astar`` — the round-3 tiered batched A* / scipy Dijkstra on one fixed cost vector.
+
+    Costs: with ``cost`` given, every request routes on those fixed edge seconds (no context); with
+    ``eta_model`` (and no ``cost``), each request's context (weather, traffic, pickup week-hour) gets
+    its own edge costs from the model.  ``matrix()`` returns the metre length of the time-shortest
+    road path between the points (what the trips will report), not a great-circle estimate.
+    Legs are (seconds, metres, node path); ``segments[].steps`` carry maneuvers along the path
+    (road names, turn types and "Turn left onto ..." text, csrc/runtime/route_core.h leg_steps)."""
 
     name = "graph"
     blocking = True        # GPU searches synchronise the device
+    FIXED_KEY = 1 << 40    # metric key of the fixed-cost mode
 
-    def __init__(self, g: RoadGraph, cost: np.ndarray, device=None):
+    def __init__(self, g: RoadGraph, cost: Optional[np.ndarray] = None, device=None, eta_model=None,
+                 engine: Optional[str] = None):
         super().__init__()
         self.g = g
-        self.cost = np.asarray(cost, dtype=np.float32)
+        self.cost = np.asarray(cost, dtype=np.float32) if cost is not None else None
+        self.eta_model = eta_model
+        if self.cost is None and self.eta_model is None:
+            from ..serve.eta_service import default_model
+            self.eta_model = default_model(hidden=64, steps=100)
+        self.uses_context = self.cost is None
         self.device = device
+        self.engine = (engine or os.environ.get("ROUTEST_ROUTER", "cch")).lower()
+        if self.engine == "astar" and self.cost is None:
+            self.cost = edge_costs(g, self.eta_model, device)
+            self.uses_context = False
         self._astar = None
         self._csr = None
+        self._routers: Dict[str, Any] = {}
+        self._host_costs: Dict[int, np.ndarray] = {}
         import threading
         self._lock = threading.Lock()
+        self._steps = None
+        from .providers import _RT
+        if _RT is not None and hasattr(_RT, "GraphSteps"):
+            self._steps = _RT.GraphSteps(g.indptr, g.indices, g.length_m, g.lat, g.lon, g.edge_name,
+                                         list(g.names or []))
 
     @classmethod
     def synthetic(cls, num_nodes: int = 100_000, eta_model=None, device=None) -> "GraphProvider":
@@ -472,9 +502,69 @@ class GraphProvider(HaversineProvider):
         if eta_model is None:
             from ..serve.eta_service import default_model
             eta_model = default_model(hidden=64, steps=100)
-        return cls(g, edge_costs(g, eta_model, device), device)
+        return cls(g, None, device, eta_model=eta_model)
 
-    def _shortest(self, pairs: List[Tuple[int, int]]) -> List[Tuple[float, List[int]]]:
+    @classmethod
+    def from_path(cls, path: str, eta_model=None, device=None) -> "GraphProvider":
+        from ..data.roads import load_graph
+        return cls(load_graph(path), None, device, eta_model=eta_model)
+
+    # ---- engines ----
+    def router(self, device=None):
+        """The CCH router of a device (one per GPU; ``None``: the provider's own device)."""
+        from .cch import RoadRouter
+        dev = device if device is not None else self.device
+        key = str(torch.device(dev)) if dev is not None else "cpu"
+        with self._lock:
+            r = self._routers.get(key)
+            if r is None:
+                r = RoadRouter(self.g, self.eta_model, device=dev)
+                if self.cost is not None:
+                    r.metric_from_costs(self.FIXED_KEY, self.cost)
+                self._routers[key] = r
+            return r
+
+    def metric_key(self, ctx=None, device=None) -> int:
+        """The metric a request routes on: the fixed one, or its context's (customized on demand)."""
+        if not self.uses_context:
+            return self.FIXED_KEY
+        from .cch import RouteContext
+        return self.router(device).metric(ctx or RouteContext())
+
+    def edge_seconds(self, key: int, device=None) -> np.ndarray:
+        """Host copy of a metric's edge costs (maneuver durations)."""
+        if key == self.FIXED_KEY and self.cost is not None:
+            return self.cost
+        c = self._host_costs.get(key)
+        if c is None:
+            c = np.ascontiguousarray(self.router(device).costs(key), dtype=np.float32)
+            if len(self._host_costs) > 64:
+                self._host_costs.clear()
+            self._host_costs[key] = c
+        return c
+
+    def legs(self, pairs: List[Tuple[int, int]], ctx=None, device=None, key: Optional[int] = None):
+        """[(seconds, metres, node path)] per (s, t) node pair (nan, nan, [] when not found), and the
+        metric key they were computed on (``key``: an already customized metric)."""
+        if self.engine == "astar":
+            return [(sec, (_path_length(self.g, np.asarray(p)) * 1.15 if len(p) > 1 else 0.0) if p else float("nan"), p)
+                    for sec, p in self._shortest_astar(pairs)], self.FIXED_KEY
+        r = self.router(device)
+        if key is None:
+            key = self.metric_key(ctx, device)
+        if not pairs:
+            return [], key
+        sec, met, st, paths = r.route([p[0] for p in pairs], [p[1] for p in pairs], key)
+        return [(float(sec[i]), float(met[i]), paths[i].tolist()) if st[i] == 0 else (float("nan"), float("nan"), [])
+                for i in range(len(pairs))], key
+
+    def _shortest(self, pairs: List[Tuple[int, int]], ctx=None) -> List[Tuple[float, List[int]]]:
+        """(seconds, node path) per pair (the legacy interface of the scorer / alternatives code)."""
+        if self.engine == "astar":
+            return self._shortest_astar(pairs)
+        return [(sec, p) for sec, _, p in self.legs(pairs, ctx)[0]]
+
+    def _shortest_astar(self, pairs: List[Tuple[int, int]]) -> List[Tuple[float, List[int]]]:
         if self.device is not None and torch.device(self.device).type == "cuda":
             # one search workspace per provider: concurrent handler threads take turns
             with self._lock:
@@ -498,30 +588,53 @@ class GraphProvider(HaversineProvider):
             out.append((float(dist[t]), path[::-1]))
         return out
 
+    # ---- provider interface ----
     def leg_pairs(self, coords: List[List[float]]):
         """Snap [[lon, lat], ...] to graph nodes; returns (nodes, consecutive (s, t) node pairs)."""
         nodes = self.g.nearest_nodes([c[1] for c in coords], [c[0] for c in coords])
         return nodes, [(int(nodes[k]), int(nodes[k + 1])) for k in range(len(nodes) - 1)]
 
-    def directions(self, coords: List[List[float]], profile: str) -> Dict[str, Any]:
-        nodes, pairs = self.leg_pairs(coords)
-        return self.feature_from_legs(coords, nodes, self._shortest(pairs), profile)
+    def matrix(self, points: List[Dict[str, float]], profile: str, ctx=None) -> np.ndarray:
+        """Road metres [n, n] between the snapped points along time-shortest paths (R21's matrix)."""
+        nodes = self.g.nearest_nodes([p["lat"] for p in points], [p["lon"] for p in points])
+        if self.engine == "astar":
+            n = len(nodes)
+            pairs = [(int(nodes[i]), int(nodes[j])) for i in range(n) for j in range(n)]
+            L, _ = self.legs(pairs)
+            D = np.array([m if i != j else 0.0 for (i, j), (_, m, _) in
+                          zip([(i, j) for i in range(n) for j in range(n)], L)]).reshape(n, n)
+            return np.where(np.isfinite(D), D, np.inf)
+        _, met = self.router().matrix(list(map(int, nodes)), self.metric_key(ctx))
+        return met.astype(np.float64)
 
-    def feature_from_legs(self, coords: List[List[float]], nodes, legs, profile: str) -> Dict[str, Any]:
-        """ORS-shaped Feature from per-leg (seconds, node path) results.  A leg the search did not
-        find (disconnected stops, or a search that hit its pop/heap limits) is an explicit
+    def directions(self, coords: List[List[float]], profile: str, ctx=None) -> Dict[str, Any]:
+        nodes, pairs = self.leg_pairs(coords)
+        legs, key = self.legs(pairs, ctx)
+        return self.feature_from_legs(coords, nodes, legs, profile, key=key)
+
+    def feature_from_legs(self, coords: List[List[float]], nodes, legs, profile: str,
+                          key: Optional[int] = None, device=None) -> Dict[str, Any]:
+        """ORS-shaped Feature from per-leg (seconds, metres, node path) results (or the legacy
+        (seconds, node path)).  A leg the search did not find (disconnected stops) is an explicit
         :class:`ProviderError`, never a silent straight line."""
         speed_scale = PROFILE_SPEED_MPS["driving-car"] / PROFILE_SPEED_MPS.get(profile, PROFILE_SPEED_MPS["driving-car"])
         geometry: List[List[float]] = [[float(coords[0][0]), float(coords[0][1])]]
         segments, way_points = [], [0]
         tot_d = tot_t = 0.0
-        for k, (sec, path) in enumerate(legs):
+        ecost = None
+        if self._steps is not None and key is not None and self.engine != "astar":
+            ecost = self.edge_seconds(key, device)
+        for k, leg in enumerate(legs):
+            sec, metres, path = leg if len(leg) == 3 else (leg[0], None, leg[1])
             start = len(geometry) - 1
             if not path:
                 raise ProviderError(f"no road path found between waypoints {k} and {k + 1} "
                                     f"(graph nodes {int(nodes[k])} -> {int(nodes[k + 1])})")
             p = np.asarray(path)
-            dist = _path_length(self.g, p) * 1.15 if len(p) > 1 else 0.0
+            if metres is not None:
+                dist = float(metres)
+            else:
+                dist = _path_length(self.g, p) * 1.15 if len(p) > 1 else 0.0
             # node coordinates of the whole leg in one vector op (6 decimals, like ORS)
             geometry.extend(np.round(np.stack([self.g.lon[p], self.g.lat[p]], axis=1)
                                      .astype(np.float64), 6).tolist())
@@ -529,12 +642,18 @@ class GraphProvider(HaversineProvider):
             end = len(geometry) - 1
             way_points.append(end)
             dur = sec * speed_scale
-            segments.append({"distance": round(dist, 1), "duration": round(dur, 1), "steps": [
-                {"distance": round(dist, 1), "duration": round(dur, 1), "type": 11 if k == 0 else 1,
-                 "instruction": "Follow the road network", "name": "-", "way_points": [start, end]},
-                {"distance": 0.0, "duration": 0.0, "type": 10, "instruction": "Arrive at your destination"
-                 if k == len(legs) - 1 else f"Arrive at waypoint {k + 1}", "name": "-",
-                 "way_points": [end, end]}]})
+            arrive = {"distance": 0.0, "duration": 0.0, "type": 10, "instruction": "Arrive at your destination"
+                      if k == len(legs) - 1 else f"Arrive at waypoint {k + 1}", "name": "-",
+                      "way_points": [end, end]}
+            if ecost is not None:
+                steps = [{"distance": d, "duration": t, "type": ty, "instruction": ins, "name": nm,
+                          "way_points": [w0, w1]}
+                         for d, t, ty, ins, nm, w0, w1 in
+                         self._steps.steps(p.astype(np.int32), float(sec), ecost, speed_scale, start, end)]
+            else:
+                steps = [{"distance": round(dist, 1), "duration": round(dur, 1), "type": 11 if k == 0 else 1,
+                          "instruction": "Follow the road network", "name": "-", "way_points": [start, end]}]
+            segments.append({"distance": round(dist, 1), "duration": round(dur, 1), "steps": steps + [arrive]})
             tot_d += dist
             tot_t += dur
         return {"type": "Feature", "bbox": _bbox(geometry),

@@ -44,10 +44,15 @@ def _float(v: Any, default: float) -> float:
         return default
 
 
-def point_to_point(provider, source, dest, profile: str, driver: Dict[str, Any]) -> Dict[str, Any]:
+def _ctx_kw(ctx) -> Dict[str, Any]:
+    """Routing context for context-aware providers (routing/cch.py); others take no such argument."""
+    return {"ctx": ctx} if ctx is not None else {}
+
+
+def point_to_point(provider, source, dest, profile: str, driver: Dict[str, Any], ctx=None) -> Dict[str, Any]:
     coords = [[source["lon"], source["lat"]], [dest["lon"], dest["lat"]]]
     try:
-        feature = provider.directions(coords, profile)
+        feature = provider.directions(coords, profile, **_ctx_kw(ctx))
     except ProviderError as e:
         return {"error": str(e)}
     payload = dest.get("payload", 0)
@@ -68,7 +73,7 @@ def point_to_point(provider, source, dest, profile: str, driver: Dict[str, Any])
 
 
 def assemble_trips(provider, all_points: List[Dict[str, Any]], trips: List[List[int]],
-                   profile: str, source, destinations) -> Dict[str, Any]:
+                   profile: str, source, destinations, ctx=None) -> Dict[str, Any]:
     geometry: List[List[float]] = []
     segments: List[Any] = []
     tot_d = 0.0
@@ -76,7 +81,7 @@ def assemble_trips(provider, all_points: List[Dict[str, Any]], trips: List[List[
     for trip in trips:
         coords = [[all_points[i]["lon"], all_points[i]["lat"]] for i in trip]
         try:
-            f = provider.directions(coords, profile)
+            f = provider.directions(coords, profile, **_ctx_kw(ctx))
         except ProviderError as e:
             return {"error": str(e)}
         geometry += f["geometry"]["coordinates"]
@@ -98,11 +103,11 @@ def assemble_trips(provider, all_points: List[Dict[str, Any]], trips: List[List[
 
 
 def multi_stop(provider, source, destinations, profile: str, driver: Dict[str, Any],
-               trips: Optional[List[List[int]]] = None) -> Dict[str, Any]:
+               trips: Optional[List[List[int]]] = None, ctx=None) -> Dict[str, Any]:
     all_points = [source] + list(destinations)
     if trips is None:
         try:
-            d = provider.matrix(all_points, profile)
+            d = provider.matrix(all_points, profile, **_ctx_kw(ctx))
         except ProviderError as e:
             return {"error": str(e)}
         cap = _float(driver.get("vehicle_capacity", 9e12), 9e12)
@@ -112,7 +117,7 @@ def multi_stop(provider, source, destinations, profile: str, driver: Dict[str, A
             trips = greedy_trips(np.asarray(d, dtype=np.float64).tolist(), demand, cap, max_dist)
         except InfeasibleStops as e:
             return {"error": str(e)}
-    return assemble_trips(provider, all_points, trips, profile, source, destinations)
+    return assemble_trips(provider, all_points, trips, profile, source, destinations, ctx)
 
 
 def optimize_route(input_data: Any, provider, engine: str = "backend:mi355x",
@@ -127,8 +132,13 @@ def optimize_route(input_data: Any, provider, engine: str = "backend:mi355x",
     if not isinstance(source, dict) or "lat" not in source or "lon" not in source:
         return {"error": "source_point with lat/lon is required."}
     destinations = input_data["destination_points"]
+    # road providers route under the request's context (weather, traffic, pickup week-hour)
+    ctx = None
+    if getattr(provider, "uses_context", False):
+        from .cch import RouteContext
+        ctx = RouteContext.from_request(input_data)
     if len(destinations) == 1:
-        feature = point_to_point(provider, source, destinations[0], profile, driver)
+        feature = point_to_point(provider, source, destinations[0], profile, driver, ctx)
         if "error" in feature:
             return feature
         p = feature.setdefault("properties", {})
@@ -137,7 +147,7 @@ def optimize_route(input_data: Any, provider, engine: str = "backend:mi355x",
         p["destinations"] = [destinations[0]]
         _annotate(feature, driver, vehicle_type, engine)
         return feature
-    feature = multi_stop(provider, source, destinations, profile, driver, trips)
+    feature = multi_stop(provider, source, destinations, profile, driver, trips, ctx)
     if "error" in feature:
         return feature
     _annotate(feature, driver, vehicle_type, engine)

@@ -53,19 +53,27 @@ def _valid_points(r: Any) -> bool:
 
 class _LegView:
     """Provider view for the host-side assembly of one flush: ``directions`` answers from the legs
-    searched in the batch's single A* launch; everything else delegates to the real provider."""
+    searched in the batch's launches (keyed by the metric they were routed on); everything else
+    delegates to the real provider."""
 
-    def __init__(self, base, legs: Dict[tuple, tuple]):
+    def __init__(self, base, legs: Dict[tuple, tuple], device=None):
         self.base = base
         self.legs = legs
         self.name = base.name
+        self.uses_context = getattr(base, "uses_context", False)
+        self.device = device
 
-    def matrix(self, points, profile):
-        return self.base.matrix(points, profile)
+    def matrix(self, points, profile, **kw):
+        return self.base.matrix(points, profile, **kw)
 
-    def directions(self, coords, profile):
+    def directions(self, coords, profile, ctx=None):
         nodes, pairs = self.base.leg_pairs(coords)
-        return self.base.feature_from_legs(coords, nodes, [self.legs[p] for p in pairs], profile)
+        key = self.base.metric_key(ctx, self.device) if hasattr(self.base, "metric_key") else None
+        # keyed by (metric, s, t); plain (s, t) keys (routing/alternatives.py) hold fixed-metric legs
+        legs = [self.legs[(key, p[0], p[1])] if (key, p[0], p[1]) in self.legs else self.legs[p] for p in pairs]
+        if key is None:
+            return self.base.feature_from_legs(coords, nodes, legs, profile)
+        return self.base.feature_from_legs(coords, nodes, legs, profile, key=key, device=self.device)
 
 
 class RouteBatcher:
@@ -100,8 +108,67 @@ class RouteBatcher:
                 self._astar[key] = a
             return a
 
+    def _ctx_key(self, payload: Any, device):
+        prov = self.provider
+        if not getattr(prov, "uses_context", False):
+            return None, prov.metric_key(None, device) if hasattr(prov, "metric_key") else None
+        from .cch import RouteContext
+        ctx = RouteContext.from_request(payload)
+        return ctx, prov.metric_key(ctx, device)
+
+    def _graph_plan(self, payloads: List[Any], device) -> tuple:
+        """Road-graph flush: per routing context, ONE many-to-many launch for every multi-stop
+        request's road-metre matrix, ONE greedy launch (K6) over those matrices, then every trip leg
+        (and point-to-point request) in ONE leg launch.  Returns (trips by request, legs dict)."""
+        prov = self.provider
+        trips: Dict[int, Any] = {}
+        legs: Dict[tuple, tuple] = {}
+        valid = [k for k, r in enumerate(payloads) if _valid_points(r)]
+        if not valid:
+            return trips, legs
+        groups: Dict[Any, List[int]] = {}
+        for k in valid:
+            _, key = self._ctx_key(payloads[k], device)
+            groups.setdefault(key, []).append(k)
+        for key, ks in groups.items():
+            pts = {k: [payloads[k]["source_point"]] + list(payloads[k]["destination_points"]) for k in ks}
+            flat = np.array([[p["lon"], p["lat"]] for k in ks for p in pts[k]], dtype=np.float64)
+            nodes_all = prov.g.nearest_nodes(flat[:, 1], flat[:, 0])
+            nodes: Dict[int, np.ndarray] = {}
+            o = 0
+            for k in ks:
+                nodes[k] = nodes_all[o:o + len(pts[k])]
+                o += len(pts[k])
+            multi = [k for k in ks if len(pts[k]) > 2]
+            if multi:
+                mats = prov.router(device).matrices([nodes[k].tolist() for k in multi], key)
+                nm = max(len(pts[k]) for k in multi)
+                D = np.zeros((len(multi), nm, nm))
+                for i, (k, (_, met)) in enumerate(zip(multi, mats)):
+                    n = len(pts[k])
+                    D[i, :n, :n] = met
+                res = batched_trips([payloads[k] for k in multi], device=device, D=D)
+                trips.update(zip(multi, res))
+            pairs = set()
+            for k in ks:
+                if len(pts[k]) == 2:
+                    seqs = [[0, 1]]
+                elif isinstance(trips.get(k), list):
+                    seqs = trips[k]
+                else:
+                    continue
+                for seq in seqs:
+                    n = nodes[k][seq]
+                    pairs.update((int(n[i]), int(n[i + 1])) for i in range(len(n) - 1))
+            pairs = sorted(pairs)
+            if pairs:
+                res, _ = prov.legs(pairs, key=key, device=device)
+                legs.update({(key, s, t): r for (s, t), r in zip(pairs, res)})
+        return trips, legs
+
     def _graph_legs(self, payloads: List[Any], trips: Dict[int, Any], device) -> Dict[tuple, tuple]:
-        """Every leg of the flush -> {(s, t): (seconds, node path)} from ONE batched search."""
+        """Legacy A* engine: every leg of the flush -> {(key, s, t): (seconds, node path)} from ONE
+        batched search on the provider's fixed costs."""
         prov = self.provider
         coord_lists: List[List[List[float]]] = []
         for k, r in enumerate(payloads):
@@ -129,23 +196,31 @@ class RouteBatcher:
             with lock:
                 res = astar.paths([p[0] for p in pairs], [p[1] for p in pairs])
         else:
-            res = prov._shortest(pairs)
-        return dict(zip(pairs, res))
+            res = prov._shortest_astar(pairs) if hasattr(prov, "_shortest_astar") else prov._shortest(pairs)
+        key = prov.FIXED_KEY if hasattr(prov, "FIXED_KEY") else None
+        return {(key, s, t): r for (s, t), r in zip(pairs, res)}
 
     def plan_batch(self, payloads: Sequence[Any], device=None) -> List[tuple]:
         """The GPU phases of a flush: per request ``(trips or InfeasibleStops or None, view)``."""
         payloads = list(payloads)
         name = getattr(self.provider, "name", "")
         trips: Dict[int, Any] = {}
+        view = self.provider
+        if name == "graph" and getattr(self.provider, "engine", "astar") != "astar":
+            try:
+                trips, legs = self._graph_plan(payloads, device)
+            except ProviderError as e:
+                return [(e, None) for _ in payloads]
+            view = _LegView(self.provider, legs, device)
+            return [(trips.get(k), view) for k in range(len(payloads))]
         multi = [k for k, r in enumerate(payloads) if _valid_points(r) and len(r["destination_points"]) > 1]
         if multi and name in ("haversine", "graph"):
             res = batched_trips([payloads[k] for k in multi], circuity=self.provider.circuity,
                                 device=device)
             trips = dict(zip(multi, res))
-        view = self.provider
         if name == "graph":
             try:
-                view = _LegView(self.provider, self._graph_legs(payloads, trips, device))
+                view = _LegView(self.provider, self._graph_legs(payloads, trips, device), device)
             except ProviderError as e:
                 return [(e, None) for _ in payloads]
         return [(trips.get(k), view) for k in range(len(payloads))]

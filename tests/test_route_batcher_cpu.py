@@ -123,7 +123,8 @@ def test_unfound_leg_is_an_explicit_error():
     from routest_amd.routing.graph import GraphProvider
     g = synth_road_graph(2000, seed=6)
     prov = GraphProvider(g, np.ones(g.num_edges, dtype=np.float32))
-    prov._shortest = lambda pairs: [(float("nan"), [])] * len(pairs)
+    prov.legs = lambda pairs, ctx=None, device=None, key=None: (
+        [(float("nan"), float("nan"), [])] * len(pairs), prov.FIXED_KEY)
     req = {"source_point": {"lat": float(g.lat[0]), "lon": float(g.lon[0])},
            "destination_points": [{"lat": float(g.lat[500]), "lon": float(g.lon[500])}]}
     out = optimize_route(req, prov)

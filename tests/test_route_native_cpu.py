@@ -112,8 +112,9 @@ def test_python_numerics_helpers():
 
 
 def test_graph_assembly_byte_identical():
-    """Road-graph provider: the same trips, snapped nodes and searched legs assemble to the same
-    bytes as GraphProvider.feature_from_legs + optimize_route (legs from scipy Dijkstra)."""
+    """Road-graph provider: the same trips, snapped nodes and searched legs (seconds, metres, path
+    from the CPU CCH) assemble to the same bytes — maneuver steps included — as
+    GraphProvider.feature_from_legs + optimize_route."""
     from routest_amd.data.graph import synth_road_graph
     from routest_amd.routing.graph import GraphProvider
     from routest_amd.routing.greedy import InfeasibleStops, greedy_trips
@@ -146,9 +147,9 @@ def test_graph_assembly_byte_identical():
         for c in calls:
             pairs.update((int(nodes[o + i]), int(nodes[o + i + 1])) for i in range(len(c) - 1))
             o += len(c)
-        legs = dict(zip(sorted(pairs), prov._shortest(sorted(pairs))))
+        legs = dict(zip(sorted(pairs), prov.legs(sorted(pairs))[0]))
         got = rt.route_assemble_graph(body, "backend:mi355x", g.lat, g.lon, nodes.astype(np.int32), trips,
-                                      {k: (v[0], v[1]) for k, v in legs.items()})
+                                      {k: tuple(v) for k, v in legs.items()}, prov._steps, prov.cost)
         assert got == (want_st, want), it
         checked += 1
     assert checked > 80
