@@ -975,7 +975,26 @@ static rt::RouteServiceCfg route_cfg_from(const py::dict& d, int device, const v
   if (has("batch_max")) c.batch_max = d["batch_max"].cast<int>();
   if (has("timeout_us")) c.timeout_us = d["timeout_us"].cast<double>();
   if (has("sqlite_path")) c.sqlite_path = d["sqlite_path"].cast<std::string>();
-  if (c.provider == 1) {
+  if (c.provider == 1 && has("cch_ptr")) {
+    // road graph through the CCH router (routing/cch.py RoadRouter.gpu on this device)
+    c.cch = reinterpret_cast<rt::CchGpu*>((uintptr_t)d["cch_ptr"].cast<uint64_t>());
+    TORCH_CHECK(c.cch != nullptr && c.cch->device() == device, "route config: CCH router on the wrong GPU");
+    c.cch_contexts = has("cch_contexts") ? d["cch_contexts"].cast<bool>() : true;
+    if (has("cch_fixed_key")) c.cch_fixed_key = d["cch_fixed_key"].cast<uint64_t>();
+    c.glat = (const double*)tptr("glat", false);
+    c.glon = (const double*)tptr("glon", false);
+    c.h_indptr = (const int*)tptr("h_indptr", false);
+    c.h_indices = (const int*)tptr("h_indices", false);
+    c.h_length = (const float*)tptr("h_length", false);
+    c.h_edge_name = (const int32_t*)tptr("h_edge_name", false);
+    if (has("names")) c.names = d["names"].cast<std::vector<std::string>>();
+    c.N = d["N"].cast<int>();
+    c.snap_c = d["snap_c"].cast<double>();
+    c.max_path = d["max_path"].cast<int>();
+    TORCH_CHECK(c.glat && c.glon && c.h_indptr && c.h_indices && c.h_length && c.N == c.cch->topo().N &&
+                    c.max_path > 0,
+                "CCH route config incomplete");
+  } else if (c.provider == 1) {
     c.glat = (const double*)tptr("glat", false);
     c.glon = (const double*)tptr("glon", false);
     c.h_indptr = (const int*)tptr("h_indptr", false);

@@ -6,6 +6,7 @@
 #include <string>
 #include <vector>
 
+#include "cch_gpu.h"
 #include "common.h"
 #include "ops.h"
 #include "runtime/route_core.h"
@@ -18,7 +19,16 @@ struct PersistentScorer;
 
 struct RouteServiceCfg {
   int device = 0;
-  int provider = 0;                       // 0 haversine, 1 road graph (A*)
+  int provider = 0;                       // 0 haversine, 1 road graph (A* or CCH)
+  // road graph through the customizable contraction hierarchy (csrc/cch.hip): when set, the road
+  // matrices, the greedy's trips and every leg come from it, under each request's routing context
+  // (or one fixed metric when cch_contexts is false); the A* fields below are then unused
+  CchGpu* cch = nullptr;
+  bool cch_contexts = true;
+  uint64_t cch_fixed_key = 0;
+  const float* h_length = nullptr;        // [E] metres per edge (maneuvers)
+  const int32_t* h_edge_name = nullptr;   // [E] road name ids (-1 unnamed), optional
+  std::vector<std::string> names;         // road name table
   double circuity = 1.3, step_m = 150.0;  // HaversineProvider (routing/providers.py)
   std::string engine = "backend:mi355x";
   bool compat200 = true;                  // /api/request_route answers errors with 200 (reference)
@@ -73,6 +83,7 @@ struct RouteJob {
   rtr::Plan plan;
   std::vector<std::vector<std::pair<double, double>>> calls;
   std::vector<int32_t> nodes;
+  int group = 0;                    // routing-context group of its flush (CCH)
   rtr::Assembled asmb;
   float eta_min = NAN;
   std::string eta_iso, request_id;

@@ -26,6 +26,7 @@
 #include <mutex>
 #include <queue>
 #include <random>
+#include <memory>
 #include <thread>
 #include <unordered_map>
 
@@ -160,6 +161,8 @@ bool host_dijkstra(const int* indptr, const int* indices, const float* cost, int
 // One flush in flight between the two stages: its jobs and the legs its responses are built from.
 struct Batch {
   std::vector<RouteJob*> jobs;
+  std::vector<std::shared_ptr<CchMetricDev>> metrics;   // per routing-context group (CCH)
+  std::vector<std::shared_ptr<const std::vector<float>>> host_cost;   // their edge costs on the host
   std::vector<rtr::Leg> legs;
   std::vector<std::vector<int32_t>> host_paths;
   std::vector<int32_t> flat;                 // found paths, compacted (Leg::path points in here)
@@ -204,6 +207,16 @@ struct RouteService::Impl {
   DevBuf<int> d_src, d_dst, d_len, d_st, d_path, d_qidx, d_flat, d_iters;
   DevBuf<float> d_cost;
   DevBuf<long long> d_off;
+  // CCH
+  CchScratch csc;
+  HostBuf<int> h_pts, h_npts2;
+  HostBuf<float> h_met;
+  DevBuf<int> d_pts, d_npts2;
+  DevBuf<float> d_msec, d_mmet, d_met;
+  std::mutex hc_mu;
+  std::unordered_map<uint64_t, std::shared_ptr<const std::vector<float>>> hc_cache;
+  std::atomic<long long> n_ctx_built{0};
+  std::atomic<long long> t_ctx_us{0};
   // ETA
   HostBuf<rtc::EtaRecord> h_rec;
   HostBuf<float> h_eta;
@@ -461,6 +474,297 @@ struct RouteService::Impl {
     return true;
   }
 
+  static uint64_t leg_key(int group, int s, int t) {
+    return ((uint64_t)(uint32_t)group << 48) ^ ((uint64_t)(uint32_t)s << 24) ^ (uint64_t)(uint32_t)t;
+  }
+
+  // edge costs of a metric on the host (maneuver durations, exact host fallback), copied once
+  std::shared_ptr<const std::vector<float>> host_costs(const std::shared_ptr<CchMetricDev>& m) {
+    {
+      std::lock_guard<std::mutex> lk(hc_mu);
+      auto it = hc_cache.find(m->key);
+      if (it != hc_cache.end()) return it->second;
+    }
+    auto v = std::make_shared<std::vector<float>>((size_t)cfg.cch->topo().E);
+    if (hipMemcpyAsync(v->data(), m->cost, v->size() * 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+      return nullptr;
+    std::lock_guard<std::mutex> lk(hc_mu);
+    if (hc_cache.size() > 64) hc_cache.clear();
+    hc_cache[m->key] = v;
+    return v;
+  }
+
+  // CCH: group the flush's jobs by routing context and get (build on first use) each metric
+  bool cch_groups(Batch& b) {
+    const rtc::Stamp now = local_now();
+    const int64_t days = (int64_t)std::floor((double)now.secs / 86400.0);
+    const int now_wh = (int)(((days + 3) % 7 + 7) % 7) * 24 + (int)((now.secs - days * 86400) / 3600);
+    std::unordered_map<uint64_t, int> gidx;
+    std::vector<CchContext> ctxs;
+    for (RouteJob* j : b.jobs) {
+      if (j->fallback || !j->req.error.empty()) continue;
+      CchContext c;
+      uint64_t key = cfg.cch_fixed_key;
+      if (cfg.cch_contexts) {
+        c.weather = j->req.route_weather;
+        c.congestion = j->req.route_congestion;
+        c.weekhour = j->req.route_weekhour >= 0 ? j->req.route_weekhour : now_wh;
+        key = c.key();
+      }
+      auto it = gidx.find(key);
+      if (it == gidx.end()) {
+        it = gidx.emplace(key, (int)ctxs.size()).first;
+        ctxs.push_back(c);
+      }
+      j->group = it->second;
+    }
+    b.metrics.assign(ctxs.size(), nullptr);
+    b.host_cost.assign(ctxs.size(), nullptr);
+    for (size_t g = 0; g < ctxs.size(); ++g) {
+      const double t0 = now_us();
+      if (cfg.cch_contexts) {
+        bool fresh = false;
+        if (cfg.cch->metric_for(ctxs[g], stream, b.metrics[g], &fresh) != hipSuccess) return false;
+        if (fresh) {
+          n_ctx_built.fetch_add(1, std::memory_order_relaxed);
+          t_ctx_us.fetch_add((long long)(now_us() - t0), std::memory_order_relaxed);
+        }
+      } else if (!cfg.cch->cached_metric(cfg.cch_fixed_key, b.metrics[g])) {
+        return false;
+      }
+      b.host_cost[g] = host_costs(b.metrics[g]);
+      if (!b.host_cost[g]) return false;
+    }
+    return true;
+  }
+
+  // CCH: road-metre matrices of every multi-stop job (one sweep + meet launch per context group),
+  // then the greedy (K6) over them — the same kernel as the haversine path, on road distances
+  bool plan_multi_road(Batch& b) {
+    std::vector<RouteJob*> all;
+    for (RouteJob* j : b.jobs)
+      if (!j->fallback && j->req.error.empty() && j->req.dst.size() > 1) all.push_back(j);
+    if (all.empty()) return true;
+    for (size_t g = 0; g < b.metrics.size(); ++g) {
+      std::vector<RouteJob*> m;
+      for (RouteJob* j : all)
+        if (j->group == (int)g) m.push_back(j);
+      if (m.empty()) continue;
+      const int R = (int)m.size();
+      int NM = 1;
+      for (RouteJob* j : m) NM = std::max(NM, (int)j->req.dst.size() + 1);
+      if (NM > 4096) {
+        for (RouteJob* j : m) j->fallback = true;
+        continue;
+      }
+      const size_t RN = (size_t)R * NM;
+      if (h_pts.need(RN) || h_npts2.need(R) || h_dem.need(RN) || h_cap.need(R) || h_maxd.need(R) || h_visit.need(RN) ||
+          h_trip.need(RN) || h_ntrips.need(R) || h_status.need(R) || h_row0.need(RN) || d_pts.need(RN) ||
+          d_npts2.need(R) || d_dem.need(RN) || d_cap.need(R) || d_maxd.need(R) || d_D.need(RN * NM) ||
+          d_msec.need(RN * NM) || d_mmet.need(RN * NM) || d_visit.need(RN) || d_trip.need(RN) || d_ntrips.need(R) ||
+          d_status.need(R))
+        return false;
+      rtc::parallel_chunks((size_t)R, 64, 16, [&](size_t lo, size_t hi) {
+        for (size_t k = lo; k < hi; ++k) {
+          const rtr::RouteReq& r = m[k]->req;
+          const int n = (int)r.dst.size() + 1;
+          int* pt = h_pts.h + k * NM;
+          double* de = h_dem.h + k * NM;
+          std::fill(pt, pt + NM, 0);
+          std::fill(de, de + NM, 0.0);
+          pt[0] = grid.nearest(r.src.lat, r.src.lon, cfg.snap_c);
+          for (int i = 1; i < n; ++i) {
+            pt[i] = grid.nearest(r.dst[i - 1].lat, r.dst[i - 1].lon, cfg.snap_c);
+            de[i] = r.dst[i - 1].demand;
+          }
+          h_npts2.h[k] = n;
+          h_cap.h[k] = r.cap;
+          h_maxd.h[k] = r.maxd;
+        }
+      });
+      hipError_t e = hipSuccess;
+      auto cp = [&](void* d, const void* h, size_t bytes) {
+        if (e == hipSuccess) e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream);
+      };
+      cp(d_pts.d, h_pts.h, RN * 4);
+      cp(d_npts2.d, h_npts2.h, (size_t)R * 4);
+      cp(d_dem.d, h_dem.h, RN * 8);
+      cp(d_cap.d, h_cap.h, (size_t)R * 8);
+      cp(d_maxd.d, h_maxd.h, (size_t)R * 8);
+      if (e == hipSuccess)
+        e = cfg.cch->matrix(*b.metrics[g], d_pts.d, d_npts2.d, R, NM, d_msec.d, d_mmet.d, d_D.d, csc, stream);
+      if (e == hipSuccess)
+        e = launch_greedy_cvrp(d_D.d, d_npts2.d, d_dem.d, d_cap.d, d_maxd.d, R, NM, d_visit.d, d_trip.d, d_ntrips.d,
+                               d_status.d, stream);
+      auto back = [&](void* h, const void* d, size_t bytes) {
+        if (e == hipSuccess) e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream);
+      };
+      back(h_visit.h, d_visit.d, RN * 4);
+      back(h_trip.h, d_trip.d, RN * 4);
+      back(h_ntrips.h, d_ntrips.d, (size_t)R * 4);
+      back(h_status.h, d_status.d, (size_t)R * 4);
+      if (e == hipSuccess)
+        e = hipMemcpy2DAsync(h_row0.h, (size_t)NM * 8, d_D.d, (size_t)NM * NM * 8, (size_t)NM * 8, (size_t)R,
+                             hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return false;
+      for (int k = 0; k < R; ++k) unpack_plan(m[k], h_npts2.h[k], NM, k);
+    }
+    return true;
+  }
+
+  // K6 output of request k -> its Plan (trips, or the infeasible stops by depot distance)
+  void unpack_plan(RouteJob* j, int n, int NM, int k) {
+    rtr::Plan& p = j->plan;
+    const int* vis = h_visit.h + (size_t)k * NM;
+    const int* tof = h_trip.h + (size_t)k * NM;
+    if (h_status.h[k] != 0) {           // batched.py _unpack: unplaced stops by depot distance
+      std::vector<char> placed(n, 0);
+      for (int i = 0; i < NM && vis[i] >= 0; ++i) placed[vis[i]] = 1;
+      std::vector<int> rest;
+      for (int i = 1; i < n; ++i)
+        if (!placed[i]) rest.push_back(i);
+      const double* d0 = h_row0.h + (size_t)k * NM;
+      std::stable_sort(rest.begin(), rest.end(), [&](int a, int c) { return d0[a] < d0[c]; });
+      p.infeasible = true;
+      for (int i : rest) p.infeasible_stops.push_back(i - 1);
+      return;
+    }
+    p.trips.assign(h_ntrips.h[k], std::vector<int>{0});
+    for (int i = 0; i < NM && vis[i] >= 0; ++i) p.trips[tof[i]].push_back(vis[i]);
+    for (auto& t : p.trips) t.push_back(0);
+  }
+
+  // CCH legs: every unique (context, s, t) leg of the flush, one route call per context group
+  // (sweep + meet + unpack launches), then the same path compaction / copy-out as the A* path
+  bool search_legs_cch(Batch& b) {
+    std::vector<rtr::Leg>& legs = b.legs;
+    std::unordered_map<uint64_t, int>& leg_index = b.leg_index;
+    double t0 = now_us();
+    std::vector<RouteJob*> g;
+    for (RouteJob* j : b.jobs)
+      if (!j->fallback && !j->calls.empty()) g.push_back(j);
+    rtc::parallel_chunks(g.size(), 64, 16, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        RouteJob* j = g[i];
+        j->nodes.clear();
+        for (const auto& c : j->calls)
+          for (const auto& pt : c) j->nodes.push_back(grid.nearest(pt.second, pt.first, cfg.snap_c));
+      }
+    });
+    add_t(2, t0);
+    t0 = now_us();
+    const int G = (int)b.metrics.size();
+    std::vector<std::vector<std::pair<int, int>>> pairs(G);
+    std::vector<int> order;                    // leg index -> (group, index in group) flattened
+    for (RouteJob* j : g) {
+      size_t off = 0;
+      for (const auto& c : j->calls) {
+        for (size_t i = 0; i + 1 < c.size(); ++i) {
+          const int s = j->nodes[off + i], t = j->nodes[off + i + 1];
+          if (leg_index.emplace(leg_key(j->group, s, t), -1 - j->group).second) pairs[j->group].emplace_back(s, t);
+        }
+        off += c.size();
+      }
+    }
+    int Q = 0;
+    std::vector<int> goff(G + 1, 0);
+    for (int gi = 0; gi < G; ++gi) goff[gi + 1] = goff[gi] + (int)pairs[gi].size();
+    Q = goff[G];
+    for (int gi = 0; gi < G; ++gi)
+      for (size_t i = 0; i < pairs[gi].size(); ++i)
+        leg_index[leg_key(gi, pairs[gi][i].first, pairs[gi][i].second)] = goff[gi] + (int)i;
+    legs.assign(Q, rtr::Leg());
+    if (Q == 0) return true;
+    n_legs.fetch_add(Q, std::memory_order_relaxed);
+    const int MP = cfg.max_path;
+    if (h_src.need(Q) || h_dst.need(Q) || h_len.need(Q) || h_st.need(Q) || h_cost.need(Q) || h_met.need(Q) ||
+        h_off.need(Q) || d_src.need(Q) || d_dst.need(Q) || d_len.need(Q) || d_st.need(Q) || d_cost.need(Q) ||
+        d_met.need(Q) || d_off.need(Q) || d_path.need((size_t)Q * MP))
+      return false;
+    for (int gi = 0; gi < G; ++gi)
+      for (size_t i = 0; i < pairs[gi].size(); ++i) {
+        h_src.h[goff[gi] + i] = pairs[gi][i].first;
+        h_dst.h[goff[gi] + i] = pairs[gi][i].second;
+      }
+    hipError_t e = hipMemcpyAsync(d_src.d, h_src.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_dst.d, h_dst.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
+    for (int gi = 0; gi < G && e == hipSuccess; ++gi) {
+      const int q0 = goff[gi], n = goff[gi + 1] - goff[gi];
+      if (n == 0) continue;
+      CchRouteOut o;
+      o.sec = d_cost.d + q0;
+      o.metres = d_met.d + q0;
+      o.status = d_st.d + q0;
+      o.len = d_len.d + q0;
+      o.path = d_path.d + (size_t)q0 * MP;
+      o.max_path = MP;
+      e = cfg.cch->route(*b.metrics[gi], d_src.d + q0, d_dst.d + q0, n, o, csc, stream);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_len.h, d_len.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_cost.h, d_cost.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_met.h, d_met.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    add_t(3, t0);
+    t0 = now_us();
+    if (e != hipSuccess) return false;
+    long long total = 0;
+    for (int i = 0; i < Q; ++i) {
+      h_off.h[i] = total;
+      if (h_st.h[i] == 0) total += std::min(h_len.h[i], MP);
+    }
+    if (total > 0) {
+      if (h_flat.need((size_t)total) || d_flat.need((size_t)total)) return false;
+      e = hipMemcpyAsync(d_off.d, h_off.h, (size_t)Q * 8, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(compact_paths_kernel, dim3(Q), dim3(256), 0, stream, d_path.d, MP, d_len.d, d_st.d, d_off.d,
+                           Q, d_flat.d);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess) e = hipMemcpyAsync(h_flat.h, d_flat.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return false;
+      b.flat.assign(h_flat.h, h_flat.h + total);
+    }
+    add_t(4, t0);
+    // legs the GPU could not return (status 4: longer than max_path / unpack stack): exact on the host
+    int nbad = 0;
+    for (int i = 0; i < Q; ++i) nbad += h_st.h[i] == 4;
+    b.host_paths.resize(Q);
+    for (int gi = 0; gi < G; ++gi)
+      for (int i = goff[gi]; i < goff[gi + 1]; ++i) {
+        rtr::Leg& L = legs[i];
+        if (h_st.h[i] == 0) {
+          L.sec = h_cost.h[i];
+          L.metres = h_met.h[i];
+          L.len = std::min(h_len.h[i], MP);
+          L.path = b.flat.data() + h_off.h[i];
+        } else if (h_st.h[i] == 4 && nbad <= 1024 && cfg.h_indptr != nullptr) {
+          const std::vector<float>& hc = *b.host_cost[gi];
+          float c;
+          if (host_dijkstra(cfg.h_indptr, cfg.h_indices, hc.data(), cfg.N, h_src.h[i], h_dst.h[i], 1 << 22, c,
+                            b.host_paths[i])) {
+            L.sec = c;
+            float met = 0.f;
+            const auto& p = b.host_paths[i];
+            for (size_t k = 0; k + 1 < p.size(); ++k) {
+              int32_t best = -1;
+              for (int32_t ee = cfg.h_indptr[p[k]]; ee < cfg.h_indptr[p[k] + 1]; ++ee)
+                if (cfg.h_indices[ee] == p[k + 1] && (best < 0 || hc[ee] < hc[best])) best = ee;
+              if (best >= 0) met += cfg.h_length[best];
+            }
+            L.metres = met;
+            L.len = (int)p.size();
+            L.path = p.data();
+            n_host_legs.fetch_add(1, std::memory_order_relaxed);
+          }
+        }
+      }
+    return true;
+  }
+
   // graph provider: snap, search every unique leg of the flush once, fill the batch's legs
   bool search_legs(Batch& b) {
     std::vector<RouteJob*>& jobs = b.jobs;
@@ -606,11 +910,24 @@ struct RouteService::Impl {
           } else {
             std::vector<const rtr::Leg*> lp;
             for (size_t t = 0; t + 1 < j->calls[k].size(); ++t) {
-              const uint64_t key = ((uint64_t)(uint32_t)j->nodes[off + t] << 32) | (uint32_t)j->nodes[off + t + 1];
+              const int s0 = j->nodes[off + t], s1 = j->nodes[off + t + 1];
+              const uint64_t key = cfg.cch ? leg_key(j->group, s0, s1)
+                                           : (((uint64_t)(uint32_t)s0 << 32) | (uint32_t)s1);
               lp.push_back(&legs[leg_index.at(key)]);
             }
+            rtr::GraphHost gh;
+            const rtr::GraphHost* ghp = nullptr;
+            if (cfg.cch && cfg.h_length != nullptr) {
+              gh.indptr = cfg.h_indptr;
+              gh.indices = cfg.h_indices;
+              gh.length = cfg.h_length;
+              gh.cost = b.host_cost[j->group]->data();
+              gh.edge_name = cfg.h_edge_name;
+              gh.names = &cfg.names;
+              ghp = &gh;
+            }
             perr = rtr::graph_directions(j->calls[k], j->nodes.data() + off, lp, j->req.profile, cfg.glat, cfg.glon,
-                                         dirs[k]);
+                                         dirs[k], ghp);
             off += j->calls[k].size();
           }
         }
@@ -692,6 +1009,19 @@ struct RouteService::Impl {
       pscore_park(cfg.scorer);
     }
     t0 = now_us();
+    if (cfg.provider == 1 && cfg.cch != nullptr) {
+      // road graph through the CCH: contexts -> road matrices + greedy -> legs
+      if (!cch_groups(b) || !plan_multi_road(b)) {
+        fail_all(jobs, "route optimizer unavailable (GPU error)");
+        b.failed = true;
+        return;
+      }
+      add_t(1, t0);
+      for (RouteJob* j : jobs)
+        if (!j->fallback) rtr::directions_calls(j->req, j->plan, j->calls);
+      if (!search_legs_cch(b)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); b.failed = true; }
+      return;
+    }
     if (!plan_multi(jobs)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); b.failed = true; return; }
     add_t(1, t0);
     for (RouteJob* j : jobs)
@@ -783,6 +1113,8 @@ std::vector<long long> RouteService::stats() const {
                               p_->n_host_legs.load(), p_->n_persisted.load()};
   for (int k = 0; k < 8; ++k) v.push_back(p_->t_stage[k].load());
   v.push_back(p_->n_escalated.load());     // A* searches rerun in the big tier
+  v.push_back(p_->n_ctx_built.load());     // routing contexts customized by this service (CCH)
+  v.push_back(p_->t_ctx_us.load());        // ... and their cost + customization time (us)
   return v;
 }
 

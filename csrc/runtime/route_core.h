@@ -241,6 +241,9 @@ struct RouteReq {
   bool eta_ok = false;                     // driver_age coerced (else no ETA fields)
   double eta_age = 30.0;
   uint8_t eta_weather = 2, eta_traffic = 2;
+  // routing context (routing/cch.py RouteContext.from_request): weather code, congestion 0..3 and
+  // the pickup week-hour (-1: now) — read whether or not use_ml_eta is set
+  int route_weather = 2, route_congestion = 0, route_weekhour = -1;
 };
 
 // _float(v, default): float(v) for numbers, default for None / missing / list / dict; strings and
@@ -347,6 +350,22 @@ inline RouteReq parse_route_request(const Value* root) {
         !coerce_float(drv ? drv->get("maximum_distance") : nullptr, 9e12, r.maxd)) {
       r.fallback = true;
       return r;
+    }
+  }
+  // routing context: a non-dict context counts as {} (RouteContext.from_request)
+  {
+    const Value* rc = root->get("context");
+    if (rc && rc->kind != Value::Obj) rc = nullptr;
+    r.route_weather = code_of(rc ? rc->get("weather") : nullptr, rtc::WEATHERS, "Sunny");
+    const int tc = code_of(rc ? rc->get("traffic") : nullptr, rtc::TRAFFICS, "Low");
+    // TRAFFICS order (High, Jam, Low, Medium) -> congestion (2, 3, 0, 1); unknown -> Low
+    r.route_congestion = tc == 0 ? 2 : tc == 1 ? 3 : tc == 3 ? 1 : 0;
+    const Value* pt = rc ? rc->get("pickup_time") : nullptr;
+    rtc::Stamp st;
+    if (pt && pt->kind == Value::Str && rtc::parse_iso(pt->str, st)) {
+      const int64_t days = (int64_t)std::floor((double)st.secs / 86400.0);
+      const int64_t sod = st.secs - days * 86400;
+      r.route_weekhour = (int)(((days + 3) % 7 + 7) % 7) * 24 + (int)(sod / 3600);
     }
   }
   // use_ml_eta (routes.py:97-116): context must be a dict (or falsy), driver_age float-coercible

@@ -1,10 +1,15 @@
 """Config 5 step: R concurrent multi-stop requests on one device, end to end on the GPU.
 
-Per step, for all R requests of this rank (each: depot + 2..10 stops snapped to road-graph nodes):
+Per step, for all R requests of this rank (each: depot + 2..10 stops snapped to road-graph nodes),
+with the CCH router (default, ``router=`` a :class:`routing.cch.RoadRouter`):
 
-  K5 haversine matrices + K6 greedy multi-trip CVRP     (one launch each, all requests)
-  -> every trip leg (consecutive stops, depot returns) as one A* query  (K9, one launch)
-  -> per-leg costs from the learned edge times (the ETA MLP over edge features, ``edge_costs``)
+  road-metre matrices of every request (CCH chain sweeps + meets, one launch set)
+  + K6 greedy multi-trip CVRP over them                    (one launch, all requests)
+  -> every trip leg as one CCH query with its path unpacked  (sweep + meet + unpack launches)
+  -> edge times from the ETA MLP for the step's routing context (customized once, cached)
+
+or, with ``engine="astar"`` (round 3): K5 haversine matrices + K6, then every leg in the tiered
+batched A* (K9).
 
 The legs are derived on the device from K6's visit order; only the (src, dst) node lists cross to
 the host once for the A* launch.  Used by ``bench/route_bench.py`` and the ``route_optimizer`` key of
@@ -28,7 +33,8 @@ from .graph import BatchedAstar
 class BulkRouteStep:
     def __init__(self, g, cost: np.ndarray, device, requests: int, seed: int = 100,
                  max_slots: int = 98304, astar: Optional[BatchedAstar] = None,
-                 radius_km: Optional[float] = None):
+                 radius_km: Optional[float] = None, router=None, key: Optional[int] = None,
+                 engine: str = "cch"):
         self.C = _ext.native(required=True)
         self.dev = d = torch.device(device)
         rng = np.random.default_rng(seed)
@@ -77,15 +83,27 @@ class BulkRouteStep:
         # step on the 100k-node graph (profiles/route_tiering_ab_r3q.jsonl); 98304 slots instead of
         # 65536 once the long legs skip the lane tier: 124.2 -> 119.6 ms (route_wave_slots_ab_r3aj.jsonl).
         # Workspace: lane tier ~8 GB, wave tier ~39 GB, big tier ~4 GB, growth arena 16 GB (of 288 GB)
+        self.engine = engine
+        self.router = self.key = self.astar = None
+        if engine == "cch":
+            from .cch import RoadRouter
+            self.router = router or RoadRouter(g, device=d)
+            self.key = key if key is not None else self.router.metric_from_costs(1 << 41, cost)
+            return
         ws = int(os.environ.get("ROUTEST_BULK_WAVE_SLOTS", "98304"))
         tb = int(os.environ.get("ROUTEST_BULK_WAVE_TBITS", "14"))
         self.astar = astar or BatchedAstar(g, cost, d, slots=slots, wave_slots=min(slots, ws), arena_gb=16,
                                            wave_tbits=tb)
 
     def legs(self):
-        """K5 + K6 for every request, then the trip legs as (src, dst) node tensors on the device."""
+        """Matrices (CCH road metres, or K5 haversine) + K6 for every request, then the trip legs as
+        (src, dst) node tensors on the device."""
         C = self.C
-        D = C.route_haversine_matrix(self.lat, self.lon, self.npts, 1.3)
+        if self.engine == "cch":
+            _, met = self.router.gpu.matrix(self.key, self.snap, self.npts)
+            D = met.double()
+        else:
+            D = C.route_haversine_matrix(self.lat, self.lon, self.npts, 1.3)
         visit, trip_of, ntrips, status = C.route_greedy_cvrp(D, self.npts, self.dem, self.cap, self.maxd)
         snap = self.snap
         valid = visit >= 0
@@ -102,7 +120,11 @@ class BulkRouteStep:
         return src, dst, status
 
     def step(self):
-        """One whole step; returns (legs, per-leg cost [s], per-leg A* status, per-request K6 status)."""
+        """One whole step; returns (legs, per-leg cost [s], per-leg status, per-request K6 status)."""
         src, dst, status = self.legs()
+        if self.engine == "cch":
+            sec, _, st, _, _ = self.router.gpu.route(self.key, src.int().contiguous(), dst.int().contiguous(),
+                                                     self.router.max_path, True)
+            return int(src.numel()), sec, st, status
         c, _, st, _ = self.astar.run(src.cpu().numpy(), dst.cpu().numpy())
         return int(src.numel()), c, st, status

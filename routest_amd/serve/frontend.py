@@ -4,7 +4,8 @@
                        ├─ /api/predict_eta, /predict ........ fused K1+K2 kernel
                        ├─ /api/optimize_route, /route,
                        │  /api/request_route ................ native route service per GPU
-                       │                                       (K5 + K6 + batched A* + C++ GeoJSON)
+                       │                                       (CCH road matrices + K6 + CCH legs
+                       │                                        + C++ GeoJSON with maneuvers)
                        └─ everything else, and requests the native paths do not mirror
                                                  ──relay──> FastAPI app (uvicorn)  127.0.0.1:<private>
 
@@ -67,7 +68,7 @@ def route_configs(sv, devices: Sequence[int], batch_max: int = 1024, timeout_us:
     out = []
     for d in devices:
         astar = None
-        if getattr(sv.provider, "name", "") == "graph":
+        if getattr(sv.provider, "name", "") == "graph" and getattr(sv.provider, "engine", "astar") == "astar":
             from ..routing.graph import BatchedAstar
             astar = BatchedAstar(sv.provider.g, sv.provider.cost, torch.device("cuda", d),
                                  slots=int(getattr(s, "route_astar_slots", 8192)))

@@ -70,7 +70,9 @@ class NativePredictServer:
                  "route_us_parse", "route_us_trips", "route_us_snap", "route_us_astar", "route_us_copyout",
                  "route_us_assemble", "route_us_eta", "route_us_persist",
                  # A* searches that overflowed a wave-tier table and were rerun in the big tier
-                 "route_astar_escalated")
+                 "route_astar_escalated",
+                 # CCH: routing contexts customized by the services, and their total build time (us)
+                 "route_contexts_built", "route_us_context")
         return dict(zip(names, v))
 
     def close(self) -> None:
@@ -90,9 +92,11 @@ def route_config(provider, device, *, engine: str = "backend:mi355x", compat200:
                  batch_max: int = 1024, timeout_us: int = 500, store=None, astar=None) -> dict:
     """The native route service's configuration for one GPU (``csrc/route_service.h``).
 
-    ``provider``: the app's HaversineProvider or GraphProvider.  For the road graph, ``astar`` is a
-    :class:`~routest_amd.routing.graph.BatchedAstar` on ``device`` whose device tensors the service
-    searches with (its three workspace tiers; the caller keeps it alive).
+    ``provider``: the app's HaversineProvider or GraphProvider.  A GraphProvider on the CCH engine
+    hands over its router for ``device`` (the same ``_C.CchGpu`` object the app routes with, so both
+    share the customized contexts and answer byte-identically); on the legacy A* engine ``astar`` is
+    a :class:`~routest_amd.routing.graph.BatchedAstar` on ``device`` whose device tensors the service
+    searches with (the caller keeps it alive).
     ``store``: the app's store — an :class:`SQLiteStore` is written natively (same database file);
     any other store kind is not mirrored, so route requests are then relayed to the Python app
     (the caller passes no route configs)."""
@@ -101,6 +105,27 @@ def route_config(provider, device, *, engine: str = "backend:mi355x", compat200:
            "compat200": bool(compat200), "batch_max": int(batch_max), "timeout_us": float(timeout_us),
            "circuity": float(getattr(provider, "circuity", 1.3)), "step_m": float(getattr(provider, "step_m", 150.0)),
            "sqlite_path": getattr(store, "sqlite_uri", "") if store is not None else ""}
+    if name == "graph" and getattr(provider, "engine", "astar") != "astar":
+        import numpy as np
+        g = provider.g
+        dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        router = provider.router(dev)
+        if router.gpu is None:
+            raise ValueError("the native route service needs the GPU router")
+        cfg.update({
+            "router": "cch", "cch_ptr": int(router.gpu.ptr()), "cch_contexts": bool(provider.uses_context),
+            "cch_fixed_key": int(provider.FIXED_KEY),
+            "glat": torch.from_numpy(np.ascontiguousarray(g.lat, dtype=np.float64)),
+            "glon": torch.from_numpy(np.ascontiguousarray(g.lon, dtype=np.float64)),
+            "h_indptr": torch.from_numpy(np.ascontiguousarray(g.indptr, dtype=np.int32)),
+            "h_indices": torch.from_numpy(np.ascontiguousarray(g.indices, dtype=np.int32)),
+            "h_length": torch.from_numpy(np.ascontiguousarray(g.length_m, dtype=np.float32)),
+            "h_edge_name": (torch.from_numpy(np.ascontiguousarray(g.edge_name, dtype=np.int32))
+                            if g.edge_name is not None else None),
+            "names": list(g.names or []),
+            "N": int(g.num_nodes), "snap_c": float(g.SNAP_C), "max_path": int(router.max_path),
+            "_router": router})
+        return cfg
     if name == "graph":
         import numpy as np
         a = astar
