@@ -16,6 +16,7 @@
 
 #include "ops.h"
 #include "common.h"
+#include "native_model.h"
 #include "route_service.h"
 
 namespace {
@@ -954,8 +955,7 @@ void gcn_train_bwd(torch::Tensor X, torch::Tensor Z, torch::Tensor indptr, torch
 // ---------------------------------------------------------------- native predict server
 // One route service config per GPU from a Python dict (routest_amd/serve/native_server.py
 // route_config): scalars, host arrays (CPU tensors) and device tensors the caller keeps alive.
-static rt::RouteServiceCfg route_cfg_from(const py::dict& d, int device, const void* eta_blob, int H,
-                                          const rt::NormParams& np, int variant, int cus) {
+static rt::RouteServiceCfg route_cfg_from(const py::dict& d, int device) {
   rt::RouteServiceCfg c;
   auto has = [&](const char* k) { return d.contains(k) && !d[k].is_none(); };
   auto tptr = [&](const char* k, bool cuda) -> void* {
@@ -1037,45 +1037,151 @@ static rt::RouteServiceCfg route_cfg_from(const py::dict& d, int device, const v
                     (c.big_ws.slots == 0 || rt::astar_ws_ok(c.big_ws, true)),
                 "A* workspace too small");
   }
-  c.eta_blob = eta_blob;
-  c.H = H;
-  c.np = np;
-  c.variant = variant;
-  c.num_cus = cus;
   return c;
 }
 
-int64_t native_server_start(int64_t port, int64_t threads, std::vector<torch::Tensor> blobs, int64_t H,
-                            std::vector<double> norm, int64_t variant, int64_t max_batch,
-                            std::vector<std::string> cors, bool cors_vercel, bool bind_any,
-                            int64_t upstream_port, py::list routes) {
-  TORCH_CHECK(!blobs.empty(), "need one weight blob per GPU");
-  std::vector<int> devs, cus;
-  std::vector<const void*> ptrs;
-  for (auto& b : blobs) {
-    check_dev(b, "blob");
-    TORCH_CHECK((size_t)b.numel() == rt::eta_mlp3_blob_bytes((int)H), "bad blob");
-    devs.push_back(b.device().index());
-    cus.push_back(num_cus(b.device().index()));
-    ptrs.push_back(b.data_ptr());
-  }
+// One native model (csrc/native_model.h) on `device` from a Python spec (serve/native_server.py
+// native_model_spec): {"kind": "mlp3" | "wide" | "forest", ...device tensors / params..., "host":
+// {fp32 CPU copies for the CPU fallback}}.  The native side copies the device tensors.
+static std::vector<float> host_f32(const py::dict& h, const char* k) {
+  torch::Tensor t = h[k].cast<torch::Tensor>().to(torch::kCPU).to(torch::kFloat32).contiguous();
+  return std::vector<float>(t.data_ptr<float>(), t.data_ptr<float>() + t.numel());
+}
+static rt::MlpHost mlp_host_from(const py::dict& d) {
+  rt::MlpHost m;
+  if (!d.contains("host") || d["host"].is_none()) return m;
+  py::dict h = d["host"].cast<py::dict>();
+  m.w1 = host_f32(h, "w1");
+  m.b1 = host_f32(h, "b1");
+  m.w2 = host_f32(h, "w2");
+  m.b2 = host_f32(h, "b2");
+  m.w3 = host_f32(h, "w3");
+  m.b3 = h["b3"].cast<float>();
+  m.x_mean = host_f32(h, "x_mean");
+  m.x_std = host_f32(h, "x_std");
+  m.y_mean = h["y_mean"].cast<float>();
+  m.y_std = h["y_std"].cast<float>();
+  m.H = (int)m.b1.size();
+  TORCH_CHECK(m.w1.size() == (size_t)m.H * 12 && m.w2.size() == (size_t)m.H * m.H && m.b2.size() == (size_t)m.H &&
+                  m.w3.size() == (size_t)m.H && m.x_mean.size() == 12 && m.x_std.size() == 12,
+              "model host weights shapes");
+  return m;
+}
+static rt::NormParams norm_from(const py::dict& d) {
+  std::vector<double> norm = d["norm"].cast<std::vector<double>>();
   TORCH_CHECK(norm.size() == 8, "norm must hold 4 scales + 4 shifts");
-  TORCH_CHECK(max_batch >= 1 && max_batch <= (1 << 24), "max_batch out of range");
-  TORCH_CHECK(routes.empty() || routes.size() == blobs.size(), "one route config per GPU (or none)");
   rt::NormParams np;
   for (int i = 0; i < 4; ++i) {
     np.scale[i] = (float)norm[i];
     np.shift[i] = (float)norm[4 + i];
   }
-  std::vector<rt::RouteServiceCfg> rcfg;
-  for (size_t g = 0; g < routes.size(); ++g)
-    rcfg.push_back(route_cfg_from(routes[g].cast<py::dict>(), devs[g], ptrs[g], (int)H, np, (int)variant, cus[g]));
+  return np;
+}
+static std::shared_ptr<const rt::NativeModel> model_from(const py::dict& d, int device) {
+  const std::string kind = d["kind"].cast<std::string>();
+  if (kind == "none") return nullptr;        // predictions relayed to the app (unsupported family)
   std::string err;
-  const int64_t h = rt::native_server_start((int)port, (int)threads, devs, ptrs, cus, (int)H, np, (int)variant,
-                                            (int)max_batch, cors, cors_vercel, bind_any, (int)upstream_port, rcfg,
-                                            err);
+  std::shared_ptr<rt::NativeModel> m;
+  auto dev_t = [&](const char* k) {
+    torch::Tensor t = d[k].cast<torch::Tensor>();
+    TORCH_CHECK(t.is_cuda() && t.device().index() == device && t.is_contiguous(), "model tensor ", k,
+                " must be contiguous on GPU ", device);
+    return t;
+  };
+  const c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, device));
+  if (kind == "mlp3") {
+    torch::Tensor blob = dev_t("blob");
+    const int H = d["H"].cast<int>();
+    TORCH_CHECK(blob.scalar_type() == torch::kUInt8 && (size_t)blob.numel() == rt::eta_mlp3_blob_bytes(H), "mlp3 blob");
+    m = rt::make_mlp3_model(device, blob.data_ptr(), (size_t)blob.numel(), H, norm_from(d),
+                            d.contains("variant") ? d["variant"].cast<int>() : -1, num_cus(device), mlp_host_from(d),
+                            err);
+  } else if (kind == "wide") {
+    torch::Tensor w1q = dev_t("w1q"), w2f = dev_t("w2f"), b2 = dev_t("b2"), w3 = dev_t("w3");
+    const int H = d["H"].cast<int>();
+    TORCH_CHECK(b2.scalar_type() == torch::kFloat32 && w3.scalar_type() == torch::kFloat32 && b2.numel() == H &&
+                    w3.numel() == H, "wide b2/w3 f32 [H]");
+    m = rt::make_wide_model(device, H, w1q.data_ptr(), (size_t)w1q.nbytes(), w2f.data_ptr(), (size_t)w2f.nbytes(),
+                            b2.data_ptr<float>(), w3.data_ptr<float>(), d["b3"].cast<float>(), norm_from(d),
+                            mlp_host_from(d), err);
+  } else if (kind == "forest") {
+    rt::ForestHost f;
+    torch::Tensor v = d["values"].cast<torch::Tensor>().to(torch::kCPU).contiguous();
+    torch::Tensor in = d["info"].cast<torch::Tensor>().to(torch::kCPU).contiguous();
+    torch::Tensor r = d["roots"].cast<torch::Tensor>().to(torch::kCPU).contiguous();
+    TORCH_CHECK(v.scalar_type() == torch::kFloat32 && in.scalar_type() == torch::kInt32 &&
+                    r.scalar_type() == torch::kInt32, "forest arrays f32 / int32 / int32");
+    f.values.assign(v.data_ptr<float>(), v.data_ptr<float>() + v.numel());
+    f.info.assign((const uint32_t*)in.data_ptr<int>(), (const uint32_t*)in.data_ptr<int>() + in.numel());
+    f.roots.assign(r.data_ptr<int>(), r.data_ptr<int>() + r.numel());
+    f.base = d["base"].cast<float>();
+    f.le = d["le"].cast<bool>();
+    std::vector<int> fm = d["fmap"].cast<std::vector<int>>();
+    TORCH_CHECK(fm.size() == 12, "fmap: 12 entries");
+    for (int j = 0; j < 12; ++j) f.fmap[j] = fm[j];
+    m = rt::make_forest_model(device, std::move(f), err);
+  } else {
+    TORCH_CHECK(false, "unknown native model kind ", kind);
+  }
+  TORCH_CHECK(m != nullptr, "native model: ", err);
+  return m;
+}
+
+int64_t native_server_start(int64_t port, int64_t threads, std::vector<int64_t> devices, py::list models,
+                            int64_t max_batch, std::vector<std::string> cors, bool cors_vercel, bool bind_any,
+                            int64_t upstream_port, py::list routes) {
+  TORCH_CHECK(!devices.empty() && models.size() == devices.size(), "one model spec per GPU slot");
+  TORCH_CHECK(max_batch >= 1 && max_batch <= (1 << 24), "max_batch out of range");
+  TORCH_CHECK(routes.empty() || routes.size() == devices.size(), "one route config per GPU (or none)");
+  std::vector<int> devs;
+  std::vector<std::shared_ptr<const rt::NativeModel>> ms;
+  for (size_t g = 0; g < devices.size(); ++g) {
+    devs.push_back((int)devices[g]);
+    ms.push_back(model_from(models[g].cast<py::dict>(), (int)devices[g]));
+  }
+  std::vector<rt::RouteServiceCfg> rcfg;
+  for (size_t g = 0; g < routes.size(); ++g) rcfg.push_back(route_cfg_from(routes[g].cast<py::dict>(), devs[g]));
+  std::string err;
+  const int64_t h = rt::native_server_start((int)port, (int)threads, devs, ms, (int)max_batch, cors, cors_vercel,
+                                            bind_any, (int)upstream_port, rcfg, err);
   TORCH_CHECK(h >= 0, "native server: ", err);
   return h;
+}
+
+int64_t native_server_set_models(int64_t h, std::vector<int64_t> devices, py::list models) {
+  TORCH_CHECK(models.size() == devices.size(), "one model spec per GPU slot");
+  std::vector<std::shared_ptr<const rt::NativeModel>> ms;
+  for (size_t g = 0; g < devices.size(); ++g) ms.push_back(model_from(models[g].cast<py::dict>(), (int)devices[g]));
+  std::string err;
+  int64_t ep;
+  {
+    py::gil_scoped_release nogil;
+    ep = rt::native_server_set_models(h, ms, err);
+  }
+  TORCH_CHECK(ep >= 0, "native server: ", err);
+  return ep;
+}
+
+py::dict native_server_health(int64_t h) {
+  uint64_t epoch = 0;
+  auto rows = rt::native_server_health(h, epoch);
+  py::list slots;
+  for (auto& r : rows) {
+    py::dict d;
+    d["device"] = std::stoi(r[0]);
+    d["quarantined"] = r[1] == "1";
+    d["consecutive_failures"] = std::stoll(r[2]);
+    d["failures"] = std::stoll(r[3]);
+    d["rounds"] = std::stoll(r[4]);
+    d["quarantines"] = std::stoll(r[5]);
+    d["fault_injected"] = r[6] == "1";
+    d["model"] = r[7];
+    slots.append(d);
+  }
+  py::dict out;
+  out["model_epoch"] = epoch;
+  out["slots"] = slots;
+  return out;
 }
 
 // ---------------------------------------------------------------- native collectives (comm.hip)
@@ -1281,9 +1387,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gcn_grad_numel", []() { return (int64_t)rt::gcn_grad_numel(); });
   m.def("gcn_train_slab2_rows", [](int64_t n) { return (int64_t)rt::gcn_train_slab2_rows((int)n); });
   m.def("native_server_start", &native_server_start, "native HTTP front end (predictions, routes, relay)",
-        py::arg("port"), py::arg("threads"), py::arg("blobs"), py::arg("H"), py::arg("norm"), py::arg("variant"),
-        py::arg("max_batch"), py::arg("cors"), py::arg("cors_vercel"), py::arg("bind_any"),
-        py::arg("upstream_port") = 0, py::arg("routes") = py::list());
+        py::arg("port"), py::arg("threads"), py::arg("devices"), py::arg("models"), py::arg("max_batch"),
+        py::arg("cors"), py::arg("cors_vercel"), py::arg("bind_any"), py::arg("upstream_port") = 0,
+        py::arg("routes") = py::list());
+  m.def("native_server_set_models", &native_server_set_models,
+        "hot-swap the served models (one spec per GPU slot); returns the new epoch");
+  m.def("native_server_set_fault", [](int64_t h, int64_t slot, bool on) {
+    return rt::native_server_set_fault(h, (int)slot, on);
+  });
+  m.def("native_server_health", &native_server_health, "per-GPU-slot health, models and the model epoch");
   m.def("native_server_stop", [](int64_t h) {
     py::gil_scoped_release nogil;
     rt::native_server_stop(h);

@@ -50,6 +50,7 @@
 #include <vector>
 
 #include "common.h"
+#include "native_model.h"
 #include "ops.h"
 #include "route_service.h"
 #include "runtime/rt_core.h"
@@ -61,20 +62,84 @@ namespace {
 using rtc::EtaRecord;
 using rtc::Stamp;
 
+struct Shared;
+
 struct ServerCfg {
-  int port = 0, threads = 1, device = 0, H = 256, variant = -1, num_cus = 256;
-  const void* blob = nullptr;          // this reactor's device + weight blob (one copy per GPU)
-  NormParams np{};
-  int max_batch = 1 << 20;
+  int port = 0, threads = 1, device = 0, slot = 0, max_batch = 1 << 20;
   int persist_cap = 1024;              // rounds of up to this many rows use the resident scorer
   double persist_idle_ms = 20.0;       // (0 = off); it exits after this long without a request
   double persist_life_ms = 50.0;       // ... or after this long resident (then relaunched)
-  PersistentScorer* scorer = nullptr;  // one per GPU, shared by that GPU's reactors
-  std::mutex* scorer_mu = nullptr;
   std::vector<std::string> cors_exact;
   bool cors_vercel = true;
   int upstream_port = 0;               // Python app for everything not answered natively (0 = none)
   RouteService* routes = nullptr;      // this reactor's GPU's route service (nullptr = relay routes)
+  Shared* sh = nullptr;                // the server's models, scorers and GPU health
+};
+
+// GPU health of one reactor slot: consecutive launch failures quarantine the GPU; a
+// quarantined GPU gets one probe round every probe_ms and is restored by a success.  `fault` is the
+// ROUTEST_FAULT=gpu_fail[@slot] injection hook (launches on the slot fail without running).
+struct SlotHealth {
+  std::atomic<int> consec{0};
+  std::atomic<bool> quarantined{false};
+  std::atomic<long long> failures{0}, rounds{0}, quarantines{0};
+  std::atomic<long long> probe_at_ms{0};
+  std::atomic<bool> fault{false};
+};
+
+inline long long mono_ms() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (long long)ts.tv_sec * 1000 + ts.tv_nsec / 1000000;
+}
+
+// Server-wide state the reactors and route services share.
+struct Shared {
+  std::vector<int> devices;                                // per slot
+  std::mutex model_mu;
+  std::vector<std::shared_ptr<const NativeModel>> models;  // per slot (hot-swapped under model_mu)
+  std::atomic<uint64_t> epoch{0};
+  std::vector<PersistentScorer*> scorers;                  // per slot (nullptr: none)
+  std::vector<std::unique_ptr<std::mutex>> scorer_mus;
+  std::vector<std::unique_ptr<SlotHealth>> health;
+  int quarantine_after = 3;
+  long long probe_ms = 30000;
+  int slots() const { return (int)devices.size(); }
+  std::vector<std::shared_ptr<const NativeModel>> snapshot() {
+    std::lock_guard<std::mutex> lk(model_mu);
+    return models;
+  }
+  std::shared_ptr<const NativeModel> model(int g) {
+    std::lock_guard<std::mutex> lk(model_mu);
+    return models[g];
+  }
+  bool usable(int g) {
+    SlotHealth& h = *health[g];
+    if (!h.quarantined.load(std::memory_order_relaxed)) return true;
+    const long long now = mono_ms();
+    long long due = h.probe_at_ms.load();
+    return now >= due && h.probe_at_ms.compare_exchange_strong(due, now + probe_ms);   // one probe per period
+  }
+  void fail(int g) {
+    SlotHealth& h = *health[g];
+    h.failures.fetch_add(1);
+    if (h.consec.fetch_add(1) + 1 >= quarantine_after && !h.quarantined.exchange(true)) {
+      h.quarantines.fetch_add(1);
+      h.probe_at_ms.store(mono_ms() + probe_ms);
+    }
+  }
+  void ok(int g) {
+    SlotHealth& h = *health[g];
+    h.rounds.fetch_add(1, std::memory_order_relaxed);
+    h.consec.store(0, std::memory_order_relaxed);
+    if (h.quarantined.load(std::memory_order_relaxed)) h.quarantined.store(false);
+  }
+  // park the slot's resident scorer (before a normal launch that may share its hardware queue)
+  void park(int g) {
+    if (g < 0 || g >= (int)scorers.size()) return;
+    std::lock_guard<std::mutex> lk(*scorer_mus[g]);
+    if (scorers[g] != nullptr) pscore_park(scorers[g]);
+  }
 };
 
 struct Conn {
@@ -116,7 +181,7 @@ struct Pending {
 
 struct Stats {
   std::atomic<long long> requests{0}, predictions{0}, launches{0}, errors{0}, resident{0}, fallbacks{0},
-      wire8{0}, route_requests{0}, route_fallbacks{0}, relayed{0};
+      wire8{0}, route_requests{0}, route_fallbacks{0}, relayed{0}, failovers{0}, cpu_rounds{0};
 };
 
 inline Stamp now_local() {
@@ -183,14 +248,17 @@ class Reactor {
     if (hipSetDevice(cfg_.device) != hipSuccess) return;
     if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return;
     cap_ = cfg_.max_batch;
-    if (hipHostMalloc((void**)&h_rec_, (size_t)cap_ * 16, hipHostMallocMapped) != hipSuccess ||
-        hipHostMalloc((void**)&h_rec8_, (size_t)cap_ * 8, hipHostMallocMapped) != hipSuccess ||
-        hipHostMalloc((void**)&h_out_, (size_t)cap_ * 4, hipHostMallocMapped) != hipSuccess)
+    // portable + mapped: a round can be re-run on another GPU when this one is quarantined
+    const unsigned fl = hipHostMallocMapped | hipHostMallocPortable;
+    if (hipHostMalloc((void**)&h_rec_, (size_t)cap_ * 16, fl) != hipSuccess ||
+        hipHostMalloc((void**)&h_rec8_, (size_t)cap_ * 8, fl) != hipSuccess ||
+        hipHostMalloc((void**)&h_out_, (size_t)cap_ * 4, fl) != hipSuccess)
       return;
     if (hipHostGetDevicePointer(&d_rec_, h_rec_, 0) != hipSuccess ||
         hipHostGetDevicePointer(&d_rec8_, h_rec8_, 0) != hipSuccess ||
         hipHostGetDevicePointer((void**)&d_out_, h_out_, 0) != hipSuccess)
       return;
+    streams_[cfg_.device] = stream_;
 
     epoll_event evs[256];
     while (!stop_.load(std::memory_order_relaxed) || inflight_ > 0) {
@@ -226,7 +294,11 @@ class Reactor {
     (void)hipHostFree(h_rec_);
     (void)hipHostFree(h_rec8_);
     (void)hipHostFree(h_out_);
-    (void)hipStreamDestroy(stream_);
+    for (auto& kv : streams_) {
+      (void)hipSetDevice(kv.first);
+      (void)hipStreamDestroy(kv.second);
+    }
+    (void)hipSetDevice(cfg_.device);
   }
 
  private:
@@ -244,6 +316,8 @@ class Reactor {
   float* d_out_ = nullptr;
   int cap_ = 0;
   size_t nrec_ = 0;
+  std::unordered_map<int, hipStream_t> streams_;        // per device (failover launches)
+  std::unordered_map<int, ModelWs> ws_;                 // per device model workspace
   uint64_t next_gen_ = 1;
   std::unordered_map<int, Conn> conns_;
   std::unordered_map<int, int> up2c_;  // upstream fd -> client fd
@@ -469,12 +543,15 @@ class Reactor {
       return;
     }
     const bool is_pe = path == "/api/predict_eta", is_p = path == "/predict";
-    if (!(is_pe || is_p) || method != "POST") {
+    // a model family the native path does not serve (after a hot swap): the app answers
+    const bool no_model = (is_pe || is_p) && method == "POST" && cfg_.sh->model(cfg_.slot) == nullptr;
+    if (!(is_pe || is_p) || method != "POST" || no_model) {
       if (cfg_.upstream_port > 0) {
         relay(c, raw, method == "HEAD");
         return;
       }
       if (!is_pe && !is_p) respond(c, 404, "{\"detail\":\"Not Found\"}", origin, !keep);
+      else if (no_model) respond(c, 503, "{\"error\":\"model unavailable\"}", origin, !keep);
       else respond(c, 405, "{\"detail\":\"Method Not Allowed\"}", origin, !keep);
       return;
     }
@@ -758,40 +835,81 @@ class Reactor {
     }
   }
 
+  // One round on GPU slot g's device with that slot's model (zero-copy: records and minutes stay
+  // in this reactor's portable pinned buffers).
+  hipError_t launch_on(int g, const NativeModel& m) {
+    Shared& sh = *cfg_.sh;
+    if (sh.health[g]->fault.load(std::memory_order_relaxed)) return hipErrorLaunchFailure;   // injected
+    const int dev = sh.devices[g];
+    if (hipSetDevice(dev) != hipSuccess) return hipErrorInvalidDevice;
+    hipStream_t st;
+    auto it = streams_.find(dev);
+    if (it == streams_.end()) {
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipSetDevice(cfg_.device);
+        return hipErrorOutOfMemory;
+      }
+      streams_[dev] = st;
+    } else {
+      st = it->second;
+    }
+    sh.park(g);                        // keep a hardware queue the resident scorer may share free
+    // 8-byte wire records whenever the round is exactly representable and the model reads them
+    // (csrc/runtime/rt_core.h pack_wire8), else 16-byte
+    const bool w8 = m.takes_wire8() && rtc::pack_wire8(h_rec_, nrec_, h_rec8_);
+    if (w8) st_.wire8.fetch_add(1, std::memory_order_relaxed);
+    hipError_t e = m.predict(w8 ? d_rec8_ : d_rec_, w8 ? 8 : 16, d_out_, (int)nrec_, st, ws_[dev]);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipSetDevice(cfg_.device);
+    return e;
+  }
+
+  // Score this round: the own GPU's resident scorer, else a launch on the own GPU, else on the other
+  // healthy GPUs in turn (failover), else the model's fp32 CPU forward.  false: nothing answered.
+  bool score_round() {
+    Shared& sh = *cfg_.sh;
+    const int S = sh.slots(), own = cfg_.slot;
+    auto models = sh.snapshot();       // this round keeps its models alive across a hot swap
+    const NativeModel* m0 = models[own].get();
+    if (m0 != nullptr && m0->mlp3_blob() != nullptr && !sh.health[own]->fault.load(std::memory_order_relaxed) &&
+        !sh.health[own]->quarantined.load(std::memory_order_relaxed)) {
+      std::lock_guard<std::mutex> lk(*sh.scorer_mus[own]);
+      PersistentScorer* ps = sh.scorers[own];
+      if (ps != nullptr && (int)nrec_ <= pscore_cap(ps) && !pscore_broken(ps)) {
+        // small round: the resident kernel (no dispatch, weights already in LDS, no stream sync)
+        std::memcpy(pscore_records(ps), h_rec_, nrec_ * sizeof(EtaRecord));
+        if (pscore_run(ps, (int)nrec_, 200.0) == hipSuccess) {
+          std::memcpy(h_out_, pscore_out(ps), nrec_ * sizeof(float));
+          st_.resident.fetch_add(1, std::memory_order_relaxed);
+          st_.launches.fetch_add(1, std::memory_order_relaxed);
+          sh.ok(own);
+          return true;
+        }
+        st_.fallbacks.fetch_add(1, std::memory_order_relaxed);
+      }
+    }
+    for (int k = 0; k < S; ++k) {
+      const int g = (own + k) % S;
+      if (models[g] == nullptr || !sh.usable(g)) continue;
+      st_.launches.fetch_add(1, std::memory_order_relaxed);
+      if (launch_on(g, *models[g]) == hipSuccess) {
+        sh.ok(g);
+        if (g != own) st_.failovers.fetch_add(1, std::memory_order_relaxed);
+        return true;
+      }
+      sh.fail(g);
+    }
+    if (m0 != nullptr && m0->cpu_predict(h_rec_, h_out_, (int)nrec_)) {
+      st_.cpu_rounds.fetch_add(1, std::memory_order_relaxed);
+      return true;
+    }
+    return false;
+  }
+
   void run_batch() {
     if (pending_.empty()) return;
     if (nrec_ > 0) {
-      hipError_t e = hipErrorNotReady;
-      PersistentScorer* ps = cfg_.scorer;
-      if (ps != nullptr && (int)nrec_ <= pscore_cap(ps)) {
-        // small round: the resident kernel (no dispatch, weights already in LDS, no stream sync)
-        std::lock_guard<std::mutex> lk(*cfg_.scorer_mu);
-        if (!pscore_broken(ps)) {
-          std::memcpy(pscore_records(ps), h_rec_, nrec_ * sizeof(EtaRecord));
-          e = pscore_run(ps, (int)nrec_, 200.0);
-          if (e == hipSuccess) {
-            std::memcpy(h_out_, pscore_out(ps), nrec_ * sizeof(float));
-            st_.resident.fetch_add(1, std::memory_order_relaxed);
-          } else {
-            st_.fallbacks.fetch_add(1, std::memory_order_relaxed);
-          }
-        }
-      }
-      if (e != hipSuccess) {
-        if (ps != nullptr) {            // keep a hardware queue it may share free for this launch
-          std::lock_guard<std::mutex> lk(*cfg_.scorer_mu);
-          pscore_park(ps);
-        }
-        // the kernel reads the records over PCIe (zero-copy): send 8-byte wire records whenever
-        // the round is exactly representable (csrc/runtime/rt_core.h pack_wire8), else 16-byte
-        const bool w8 = rtc::pack_wire8(h_rec_, nrec_, h_rec8_);
-        if (w8) st_.wire8.fetch_add(1, std::memory_order_relaxed);
-        e = launch_eta_mlp3_fwd(w8 ? d_rec8_ : d_rec_, d_out_, (int)nrec_, cfg_.blob, cfg_.H, cfg_.np,
-                                cfg_.variant, cfg_.num_cus, stream_, w8 ? 8 : 16);
-        if (e == hipSuccess) e = hipStreamSynchronize(stream_);
-      }
-      st_.launches.fetch_add(1, std::memory_order_relaxed);
-      if (e != hipSuccess) {
+      if (!score_round()) {
         std::vector<Pending> failed;
         failed.swap(pending_);
         nrec_ = 0;
@@ -856,17 +974,30 @@ class Reactor {
 struct Server {
   ServerCfg cfg;
   Stats stats;
+  Shared sh;
   std::atomic<bool> stop{false};
   std::vector<std::unique_ptr<Reactor>> reactors;
   std::vector<std::thread> threads;
-  std::vector<PersistentScorer*> scorers;
-  std::vector<std::unique_ptr<std::mutex>> scorer_mus;
   std::vector<std::unique_ptr<RouteService>> routes;      // one per GPU
   ~Server() {
     routes.clear();                                          // joins the route workers
-    for (PersistentScorer* p : scorers) pscore_destroy(p);   // stop + wait for the resident kernels
+    for (PersistentScorer* p : sh.scorers)                   // stop + wait for the resident kernels
+      if (p) pscore_destroy(p);
   }
 };
+
+// (re)create slot g's resident scorer for its current model (mlp3 only); caller holds its mutex
+void restart_scorer(Server* s, int g) {
+  Shared& sh = s->sh;
+  if (sh.scorers[g] != nullptr) pscore_destroy(sh.scorers[g]);
+  sh.scorers[g] = nullptr;
+  if (!(s->cfg.persist_idle_ms > 0 && s->cfg.persist_cap > 0)) return;
+  auto m = sh.model(g);
+  if (m == nullptr || m->mlp3_blob() == nullptr) return;
+  hipError_t e = hipSuccess;
+  sh.scorers[g] = pscore_create(sh.devices[g], m->mlp3_blob(), m->H, *m->mlp3_norm(), s->cfg.persist_cap,
+                                s->cfg.persist_idle_ms, s->cfg.persist_life_ms, &e);   // nullptr: normal launches
+}
 
 std::mutex g_srv_mu;
 std::vector<Server*> g_servers;
@@ -874,46 +1005,63 @@ std::vector<Server*> g_servers;
 }  // namespace
 
 int64_t native_server_start(int port, int threads, const std::vector<int>& devices,
-                            const std::vector<const void*>& blobs, const std::vector<int>& num_cus, int H,
-                            const NormParams& np, int variant, int max_batch, const std::vector<std::string>& cors,
-                            bool cors_vercel, bool bind_any, int upstream_port,
+                            const std::vector<std::shared_ptr<const NativeModel>>& models, int max_batch,
+                            const std::vector<std::string>& cors, bool cors_vercel, bool bind_any, int upstream_port,
                             const std::vector<RouteServiceCfg>& routes, std::string& err) {
-  if (devices.empty() || devices.size() != blobs.size() || devices.size() != num_cus.size() ||
-      (!routes.empty() && routes.size() != devices.size())) {
-    err = "devices/blobs/routes mismatch";
+  if (devices.empty() || devices.size() != models.size() || (!routes.empty() && routes.size() != devices.size())) {
+    err = "devices/models/routes mismatch";
     return -1;
   }
   auto* s = new Server();
   s->cfg.port = port;
   s->cfg.threads = threads < 1 ? 1 : threads;
-  s->cfg.H = H;
-  s->cfg.np = np;
-  s->cfg.variant = variant;
   s->cfg.max_batch = max_batch;
   s->cfg.cors_exact = cors;
   s->cfg.cors_vercel = cors_vercel;
   s->cfg.upstream_port = upstream_port;
+  s->cfg.sh = &s->sh;
   if (const char* v = std::getenv("ROUTEST_PERSIST_IDLE_MS")) s->cfg.persist_idle_ms = std::atof(v);
   if (const char* v = std::getenv("ROUTEST_PERSIST_CAP")) s->cfg.persist_cap = std::atoi(v);
   if (const char* v = std::getenv("ROUTEST_PERSIST_LIFE_MS")) s->cfg.persist_life_ms = std::atof(v);
-  if (s->cfg.persist_idle_ms > 0 && s->cfg.persist_cap > 0) {
-    for (size_t g = 0; g < devices.size(); ++g) {
-      hipError_t e = hipSuccess;
-      s->scorers.push_back(pscore_create(devices[g], blobs[g], H, np, s->cfg.persist_cap, s->cfg.persist_idle_ms,
-                                         s->cfg.persist_life_ms, &e));   // nullptr on failure: normal launches
-      s->scorer_mus.push_back(std::make_unique<std::mutex>());
+  Shared& sh = s->sh;
+  if (const char* v = std::getenv("ROUTEST_QUARANTINE_AFTER")) sh.quarantine_after = std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("ROUTEST_QUARANTINE_PROBE_MS")) sh.probe_ms = std::max(1ll, std::atoll(v));
+  sh.devices = devices;
+  sh.models = models;
+  sh.epoch = 1;
+  for (size_t g = 0; g < devices.size(); ++g) {
+    sh.health.push_back(std::make_unique<SlotHealth>());
+    sh.scorers.push_back(nullptr);
+    sh.scorer_mus.push_back(std::make_unique<std::mutex>());
+  }
+  // ROUTEST_FAULT=gpu_fail (every slot) | gpu_fail@<slot>: launches on the slot fail (fault injection)
+  if (const char* v = std::getenv("ROUTEST_FAULT")) {
+    std::string f = v;
+    size_t b = 0;
+    while (b <= f.size()) {
+      size_t e = f.find(',', b);
+      if (e == std::string::npos) e = f.size();
+      std::string t = f.substr(b, e - b);
+      while (!t.empty() && t.front() == ' ') t.erase(t.begin());
+      while (!t.empty() && t.back() == ' ') t.pop_back();
+      if (t == "gpu_fail") {
+        for (auto& h : sh.health) h->fault = true;
+      } else if (t.rfind("gpu_fail@", 0) == 0) {
+        const int g = std::atoi(t.c_str() + 9);
+        if (g >= 0 && g < (int)sh.health.size()) sh.health[g]->fault = true;
+      }
+      b = e + 1;
     }
+  }
+  for (size_t g = 0; g < devices.size(); ++g) {
+    std::lock_guard<std::mutex> lk(*sh.scorer_mus[g]);
+    restart_scorer(s, (int)g);
   }
   for (int i = 0; i < s->cfg.threads; ++i) {
     ServerCfg rc = s->cfg;                       // reactors are spread round-robin over the GPUs
     const size_t g = (size_t)i % devices.size();
     rc.device = devices[g];
-    rc.blob = blobs[g];
-    rc.num_cus = num_cus[g];
-    if (!s->scorers.empty()) {
-      rc.scorer = s->scorers[g];
-      rc.scorer_mu = s->scorer_mus[g].get();
-    }
+    rc.slot = (int)g;
     auto r = std::make_unique<Reactor>(rc, s->stats, s->stop);
     r->set_bind_any(bind_any);
     if (!r->init(err)) {
@@ -925,10 +1073,10 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
   // one route service per GPU; a finished job goes back to the reactor that parsed it
   for (size_t g = 0; g < routes.size(); ++g) {
     RouteServiceCfg rc = routes[g];
-    if (!s->scorers.empty()) {
-      rc.scorer = s->scorers[g];
-      rc.scorer_mu = s->scorer_mus[g].get();
-    }
+    Shared* shp = &s->sh;
+    const int slot = (int)g;
+    rc.eta_model = [shp, slot]() { return shp->model(slot); };
+    rc.park_scorer = [shp, slot]() { shp->park(slot); };
     s->routes.push_back(std::make_unique<RouteService>(rc, [](RouteJob* j) {
       static_cast<JobTag*>(j->tag)->reactor->job_done(j);
     }));
@@ -939,6 +1087,62 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
   std::lock_guard<std::mutex> lk(g_srv_mu);
   g_servers.push_back(s);
   return (int64_t)g_servers.size() - 1;
+}
+
+// Hot swap: the reactors pick the new models up at their next round (rounds in flight finish on the
+// old ones, which are freed with their last reference); the resident scorers restart on the new
+// weights.  Returns the new epoch, or -1.
+int64_t native_server_set_models(int64_t h, const std::vector<std::shared_ptr<const NativeModel>>& models,
+                                 std::string& err) {
+  std::lock_guard<std::mutex> lk(g_srv_mu);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) {
+    err = "no such server";
+    return -1;
+  }
+  Server* s = g_servers[h];
+  if (models.size() != s->sh.devices.size()) {
+    err = "one model per GPU slot";
+    return -1;
+  }
+  uint64_t ep;
+  {
+    std::lock_guard<std::mutex> ml(s->sh.model_mu);
+    s->sh.models = models;
+    ep = s->sh.epoch.fetch_add(1) + 1;
+  }
+  for (size_t g = 0; g < models.size(); ++g) {
+    std::lock_guard<std::mutex> sl(*s->sh.scorer_mus[g]);
+    restart_scorer(s, (int)g);
+  }
+  return (int64_t)ep;
+}
+
+// fault injection per slot (tests; ROUTEST_FAULT=gpu_fail@<slot> at start)
+bool native_server_set_fault(int64_t h, int slot, bool on) {
+  std::lock_guard<std::mutex> lk(g_srv_mu);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return false;
+  Server* s = g_servers[h];
+  if (slot < 0 || slot >= (int)s->sh.health.size()) return false;
+  s->sh.health[slot]->fault = on;
+  return true;
+}
+
+// per slot: device, quarantined, consecutive failures, failures, rounds, quarantines, fault, model
+std::vector<std::vector<std::string>> native_server_health(int64_t h, uint64_t& epoch) {
+  std::vector<std::vector<std::string>> out;
+  std::lock_guard<std::mutex> lk(g_srv_mu);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return out;
+  Server* s = g_servers[h];
+  epoch = s->sh.epoch.load();
+  auto models = s->sh.snapshot();
+  for (size_t g = 0; g < s->sh.devices.size(); ++g) {
+    const SlotHealth& x = *s->sh.health[g];
+    out.push_back({std::to_string(s->sh.devices[g]), x.quarantined.load() ? "1" : "0", std::to_string(x.consec.load()),
+                   std::to_string(x.failures.load()), std::to_string(x.rounds.load()),
+                   std::to_string(x.quarantines.load()), x.fault.load() ? "1" : "0",
+                   models[g] ? models[g]->describe() : std::string("none")});
+  }
+  return out;
 }
 
 void native_server_stop(int64_t h) {
@@ -961,7 +1165,7 @@ void native_server_stop(int64_t h) {
 
 std::vector<long long> native_server_stats(int64_t h) {
   std::lock_guard<std::mutex> lk(g_srv_mu);
-  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(27, 0);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(29, 0);
   Server* s = g_servers[h];
   std::vector<long long> v = {s->stats.requests.load(), s->stats.predictions.load(), s->stats.launches.load(),
                               s->stats.errors.load(), s->stats.resident.load(), s->stats.fallbacks.load(),
@@ -973,6 +1177,8 @@ std::vector<long long> native_server_stats(int64_t h) {
     for (size_t i = 0; i < rs.size() && i < x.size(); ++i) rs[i] += x[i];
   }
   v.insert(v.end(), rs.begin(), rs.end());
+  v.push_back(s->stats.failovers.load());
+  v.push_back(s->stats.cpu_rounds.load());
   return v;
 }
 

@@ -1,5 +1,6 @@
 // Host-side launcher declarations for every routest_amd HIP kernel (gfx950).
 #pragma once
+#include <memory>
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -215,11 +216,15 @@ void pscore_destroy(PersistentScorer* s);
 
 // ---- native front end (predictions, routes, relay to the Python app) : native_server.hip ----
 struct RouteServiceCfg;   // route_service.h
+struct NativeModel;       // native_model.h
 int64_t native_server_start(int port, int threads, const std::vector<int>& devices,
-                            const std::vector<const void*>& blobs, const std::vector<int>& num_cus, int H,
-                            const NormParams& np, int variant, int max_batch, const std::vector<std::string>& cors,
-                            bool cors_vercel, bool bind_any, int upstream_port,
+                            const std::vector<std::shared_ptr<const NativeModel>>& models, int max_batch,
+                            const std::vector<std::string>& cors, bool cors_vercel, bool bind_any, int upstream_port,
                             const std::vector<RouteServiceCfg>& routes, std::string& err);
+int64_t native_server_set_models(int64_t h, const std::vector<std::shared_ptr<const NativeModel>>& models,
+                                 std::string& err);
+bool native_server_set_fault(int64_t h, int slot, bool on);
+std::vector<std::vector<std::string>> native_server_health(int64_t h, uint64_t& epoch);
 void native_server_stop(int64_t h);
 std::vector<long long> native_server_stats(int64_t h);
 

@@ -8,6 +8,7 @@
 
 #include "cch_gpu.h"
 #include "common.h"
+#include "native_model.h"
 #include "ops.h"
 #include "runtime/route_core.h"
 
@@ -55,16 +56,13 @@ struct RouteServiceCfg {
   int max_path = 4096, max_iters = 2000000, lane_pops = 500;
   int wave_only_below = 32768;            // fewer unique legs than this: every search in the wave tier
   float inv_vmax = 0.f, wave_delta = 10.f, lane_max_m = -1.f;
-  // ETA model for use_ml_eta (the fused K1+K2 kernel's 32x32 weight blob on this device)
-  const void* eta_blob = nullptr;
-  int H = 0, variant = -1, num_cus = 256;
-  NormParams np{};
+  // ETA model for use_ml_eta: the native front end's current model of this GPU slot (hot-swapped)
+  std::function<std::shared_ptr<const NativeModel>()> eta_model;
   // persistence: SQLite database path/URI of the Python store ("" = none)
   std::string sqlite_path;
-  // the GPU's resident single-request scorer (persistent_serve.hip): parked before each flush's
+  // parks the GPU's resident single-request scorer (persistent_serve.hip) before each flush's
   // launches so they never queue behind it on a shared hardware queue
-  PersistentScorer* scorer = nullptr;
-  std::mutex* scorer_mu = nullptr;
+  std::function<void()> park_scorer;
 };
 
 // One request handed from a reactor to the service and back.

@@ -220,6 +220,7 @@ struct RouteService::Impl {
   // ETA
   HostBuf<rtc::EtaRecord> h_rec;
   HostBuf<float> h_eta;
+  ModelWs eta_ws;
   DevBuf<rtc::EtaRecord> d_rec;
   DevBuf<float> d_eta;
   // store
@@ -941,7 +942,12 @@ struct RouteService::Impl {
     std::vector<RouteJob*> m;
     for (RouteJob* j : jobs)
       if (!j->fallback && !j->status && j->asmb.ok && j->req.use_ml_eta && j->req.eta_ok) m.push_back(j);
-    if (m.empty() || cfg.eta_blob == nullptr) return true;
+    if (m.empty()) return true;
+    std::shared_ptr<const NativeModel> model = cfg.eta_model ? cfg.eta_model() : nullptr;
+    if (model == nullptr) {          // the served model is one the native path does not run: the app answers
+      for (RouteJob* j : m) j->fallback = true;
+      return true;
+    }
     const int n = (int)m.size();
     if (h_rec.need(n) || h_eta.need(n) || d_rec.need(n) || d_eta.need(n)) return false;
     const rtc::Stamp now = local_now();
@@ -957,11 +963,11 @@ struct RouteService::Impl {
       r.pad = 0;
     }
     hipError_t e = hipMemcpyAsync(d_rec.d, h_rec.h, (size_t)n * 16, hipMemcpyHostToDevice, stream_asm);
-    if (e == hipSuccess)
-      e = launch_eta_mlp3_fwd(d_rec.d, d_eta.d, n, cfg.eta_blob, cfg.H, cfg.np, cfg.variant, cfg.num_cus, stream_asm, 16);
+    if (e == hipSuccess) e = model->predict(d_rec.d, 16, d_eta.d, n, stream_asm, eta_ws);
     if (e == hipSuccess) e = hipMemcpyAsync(h_eta.h, d_eta.d, (size_t)n * 4, hipMemcpyDeviceToHost, stream_asm);
     if (e == hipSuccess) e = hipStreamSynchronize(stream_asm);
-    if (e != hipSuccess) return false;
+    // a failed GPU round: the model's fp32 CPU forward (same fallback as the reactors)
+    if (e != hipSuccess && !model->cpu_predict(h_rec.h, h_eta.h, n)) return false;
     for (int k = 0; k < n; ++k) {
       RouteJob* j = m[k];
       const double mins = (double)h_eta.h[k];
@@ -1004,10 +1010,7 @@ struct RouteService::Impl {
       }
     });
     add_t(0, t0);
-    if (cfg.scorer != nullptr && cfg.scorer_mu != nullptr) {
-      std::lock_guard<std::mutex> lk(*cfg.scorer_mu);
-      pscore_park(cfg.scorer);
-    }
+    if (cfg.park_scorer) cfg.park_scorer();
     t0 = now_us();
     if (cfg.provider == 1 && cfg.cch != nullptr) {
       // road graph through the CCH: contexts -> road matrices + greedy -> legs

@@ -52,6 +52,7 @@ class Services:
     route_batcher: Optional[Any] = None
     started: float = field(default_factory=time.time)
     scorer: Optional[Any] = None
+    native: Optional[Any] = None        # the native front end owning the main port (serve/frontend.py)
     _scorer_lock: Any = field(default_factory=lambda: __import__("threading").Lock())
 
     def get_scorer(self):
@@ -145,7 +146,10 @@ def build_services(settings: Optional[Settings] = None, eta: Optional[EtaService
             provider = ORSProvider(s.ors_api_key)
         elif s.provider == "graph":
             from ..routing.graph import GraphProvider
-            provider = GraphProvider.synthetic(num_nodes=s.graph_nodes, device=route_device)
+            if s.graph_path:
+                provider = GraphProvider.from_path(s.graph_path, device=route_device)
+            else:
+                provider = GraphProvider.synthetic(num_nodes=s.graph_nodes, device=route_device)
         else:
             provider = HaversineProvider()
     if store == "default":

@@ -1,6 +1,7 @@
 """``GET /api/health`` payload (R10, ``RO/Flaskr/routes.py:282-363``): always HTTP 200, overall
 ``ok``/``degraded``; per-check ``status`` + ``latency_ms``.  Adds ``gpu`` (device count, HBM
-free/total, native kernels loaded) and ``model`` (ETA backend) checks."""
+free/total, native kernels loaded), ``model`` (ETA backend) and ``native`` (the native front end
+that owns the main port: GPU-slot quarantine, served model and epoch) checks."""
 from __future__ import annotations
 
 import os
@@ -87,6 +88,24 @@ def _check_collectives(sv: Any) -> Dict[str, Any]:
         return {"status": "error", "latency_ms": int((time.time() - t0) * 1000), "error": str(e)[:200]}
 
 
+def _check_native(sv: Any) -> Dict[str, Any]:
+    """The process that serves the main port (serve/frontend.py ServingStack): per-GPU-slot health
+    of the native front end (quarantine, failures, the model each slot serves, the model epoch after
+    hot swaps), its request counters and the native route services' (CCH contexts built)."""
+    front = getattr(sv, "native", None)
+    if front is None:
+        return {"status": "skipped", "latency_ms": 0, "reason": "no native front end in this process"}
+    t0 = time.time()
+    try:
+        h = front.health()
+        h["status"] = "degraded" if h.get("degraded") else "ok"
+        h["latency_ms"] = int((time.time() - t0) * 1000)
+        h["routes_native"] = bool(getattr(front, "routes", None))
+        return h
+    except Exception as e:
+        return {"status": "error", "latency_ms": int((time.time() - t0) * 1000), "error": str(e)[:200]}
+
+
 def health_payload(sv: Any) -> Dict[str, Any]:
     s = sv.settings
     redis_res = sv.broker.ping()
@@ -97,16 +116,17 @@ def health_payload(sv: Any) -> Dict[str, Any]:
         db_res = sv.store.ping()
     gpu_res = _check_gpu(sv)
     coll_res = _check_collectives(sv)
+    native_res = _check_native(sv)
     model = sv.eta.describe()
     model_res = {"status": ("degraded" if model.get("degraded") else "ok") if sv.eta.batcher is not None
                  else "skipped", **model}
     parts = (redis_res["status"], engine_res["status"], db_res["status"], gpu_res["status"], model_res["status"],
-             coll_res["status"])
+             coll_res["status"], native_res["status"])
     overall = "degraded" if any(p in ("error", "degraded") for p in parts) else "ok"
     return {
         "backend": True,
         "checks": {"engine": engine_res, "redis": redis_res, "supabase": db_res, "gpu": gpu_res,
-                   "model": model_res, "collectives": coll_res},
+                   "model": model_res, "collectives": coll_res, "native": native_res},
         "db": db_res["status"] == "ok",
         "osrm": engine_res["status"] in ("ok", "degraded"),
         "redis": redis_res["status"] == "ok",

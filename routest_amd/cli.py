@@ -22,6 +22,9 @@ def cmd_serve(a: argparse.Namespace) -> None:
         over["provider"] = a.provider
     if a.store:
         over["store_url"] = a.store
+    if a.graph:
+        over["graph_path"] = a.graph
+        over.setdefault("provider", "graph")
     s = load_settings(dotenv_path=a.env_file, **over)
     set_settings(s)
     from .utils.logging import setup_logging
@@ -38,9 +41,8 @@ def cmd_serve(a: argparse.Namespace) -> None:
     sv = build_services(s, eta=eta)
     app = create_app(sv)
     port = a.port or s.port
-    from .models.mlp3 import EtaMLP
-    native_ok = (eta is not None and eta.backend == "hip" and isinstance(eta.model, EtaMLP)
-                 and eta.model.hidden in (64, 128, 256))
+    from .serve.native_server import native_supported
+    native_ok = eta is not None and eta.backend == "hip" and bool(eta.devices) and native_supported(eta.model)
     if a.front == "native" and native_ok:
         # the native front end owns the main port; the FastAPI app answers what it relays
         from .serve.frontend import ServingStack
@@ -114,6 +116,8 @@ def main(argv=None) -> None:
     s.add_argument("--hidden", type=int, default=256)
     s.add_argument("--device", default="")
     s.add_argument("--provider", default="")
+    s.add_argument("--graph", default="", help="road graph file for --provider graph (.gr+.co DIMACS, "
+                   ".edges.csv+.nodes.csv, .npz); default: the synthetic Metro-Manila graph")
     s.add_argument("--store", default="")
     s.add_argument("--env-file", default=".env")
     s.add_argument("--front", choices=["native", "python"], default="native",

@@ -71,6 +71,8 @@ class Settings:
     sse_delta: bool = False              # ROUTEST_SSE_DELTA (Appendix B #7)
     fast_predict: bool = True            # ROUTEST_FAST_PREDICT: pure-ASGI native single-predict path
     graph_nodes: int = 100_000           # ROUTEST_GRAPH_NODES: synthetic road graph for the route scorer
+    graph_path: str = ""                 # ROUTEST_GRAPH_PATH / serve --graph: a real road graph
+                                         # (.gr + .co DIMACS, .edges.csv + .nodes.csv, .npz)
     route_batch: str = "auto"            # ROUTEST_ROUTE_BATCH: auto (on with a GPU) | 1 | 0
     route_batch_max: int = 1024          # ROUTEST_ROUTE_BATCH_MAX: requests per optimizer flush
     route_batch_timeout_us: int = 500    # ROUTEST_ROUTE_BATCH_TIMEOUT_US
@@ -151,6 +153,7 @@ def load_settings(env: Optional[Dict[str, str]] = None, dotenv_path: Optional[st
         sse_delta=_as_bool(g("ROUTEST_SSE_DELTA"), False),
         fast_predict=_as_bool(g("ROUTEST_FAST_PREDICT"), True),
         graph_nodes=_int("ROUTEST_GRAPH_NODES", 100_000),
+        graph_path=g("ROUTEST_GRAPH_PATH") or "",
         route_batch=(g("ROUTEST_ROUTE_BATCH") or "auto").lower(),
         route_batch_max=_int("ROUTEST_ROUTE_BATCH_MAX", 1024),
         route_batch_timeout_us=_int("ROUTEST_ROUTE_BATCH_TIMEOUT_US", 500),

@@ -86,6 +86,7 @@ class EtaService:
         self.allow_pickle = allow_pickle
         self.retry_s = retry_s
         self.error: Optional[str] = None
+        self.on_activate: List[Any] = []   # callbacks(model) after a (re)load: the native front end's hot swap
         self._last_try = 0.0
         self._lock = threading.Lock()
         self.batcher: Optional[MicroBatcher] = None
@@ -108,7 +109,7 @@ class EtaService:
         runners = []
         devs: List[torch.device] = []
         from ..models.forest import ForestModel
-        if isinstance(model, EtaMLP) and model.hidden in (64, 128, 256):
+        if isinstance(model, EtaMLP) and model.hidden in (64, 128, 256, 512, 1024):
             for d in self._gpu_devices():
                 runners.append(GpuRunner(EtaMlpKernel(model, d), d, self.batch_max))
                 devs.append(d)
@@ -132,6 +133,11 @@ class EtaService:
             old.close()
         log.info("ETA model active: %s on %s", getattr(model, "arch", type(model).__name__),
                  [str(d) for d in devs] or "cpu")
+        for cb in list(self.on_activate):
+            try:
+                cb(model)
+            except Exception as e:  # noqa: BLE001 - a hook failure must not undo the Python reload
+                log.error("model activation hook failed: %r", e)
 
     def reload(self, path: Optional[str] = None) -> bool:
         from ..models.checkpoint import load_any

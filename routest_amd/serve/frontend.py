@@ -111,8 +111,23 @@ class ServingStack:
             self.app_server.close()
             raise
         self.port = self.front.port
+        # the app reports the native front end's state in /api/health, and a model (re)load in the
+        # app (/api/admin/reload_model) is hot-swapped into the native front end
+        self.sv = sv
+        sv.native = self.front
+        self._hook = self._swap
+        sv.eta.on_activate.append(self._hook)
+
+    def _swap(self, model) -> None:
+        from .native_server import native_supported
+        self.front.set_model(model if native_supported(model) else None)
 
     def close(self) -> None:
+        try:
+            self.sv.eta.on_activate.remove(self._hook)
+        except ValueError:
+            pass
+        self.sv.native = None
         self.front.close()
         self.app_server.close()
 

@@ -220,3 +220,41 @@ def test_graph_provider_routes_byte_identical():
         assert stats["route_legs"] > 0 and stats["route_service_fallbacks"] == 0, stats
     finally:
         st.close()
+
+
+def test_graph_routes_under_request_context_byte_identical():
+    """Context-aware road routing (verdict r3 item 2): the same request under Stormy / Jam at 18:00
+    Friday vs Sunny / Low at 03:00 gets different durations, each answer byte-identical between
+    the native route service and the Python app (both route through the same GPU CCH object), and
+    every multi-stop trip's reported distance stays within maximum_distance (road-metre matrix)."""
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider
+    from routest_amd.serve.eta_service import default_model
+    import torch
+    g = synth_road_graph(20_000, seed=2)
+    prov = GraphProvider(g, None, device=torch.device("cuda", 0), eta_model=default_model(hidden=64, steps=50))
+    st, sv = _stack(prov, None)
+    try:
+        pays = _payloads(40, g.lat, g.lon, seed=12, max_stops=6)
+        durs = {}
+        for ctx in ({"weather": "Sunny", "traffic": "Low", "pickup_time": "2025-08-26T03:00:00"},
+                    {"weather": "Stormy", "traffic": "Jam", "pickup_time": "2025-08-29T18:00:00"}):
+            for i, p in enumerate(pays):
+                q = dict(p, context=ctx)
+                q["driver_details"] = dict(p["driver_details"], maximum_distance=40_000)
+                a = _req(st.port, "POST", "/api/optimize_route", q)
+                b = _req(st.app_server.port, "POST", "/api/optimize_route", q)
+                assert a[0] == b[0] and a[1] == b[1], (ctx, a[1][:300], b[1][:300])
+                if a[0] == 200:
+                    f = json.loads(a[1])
+                    durs.setdefault(i, []).append(f["properties"]["summary"]["duration"])
+                    # per trip (one directions call each) the reported road metres obey the limit
+                    segs = f["properties"]["segments"]
+                    assert all(s["distance"] <= 40_000 for s in segs)
+                    assert any(len(s["steps"]) > 2 for s in segs) or len(segs) == 0
+        both = [v for v in durs.values() if len(v) == 2]
+        assert len(both) > 10 and sum(v[0] != v[1] for v in both) > len(both) // 2
+        stats = st.front.stats()
+        assert stats["route_contexts_built"] >= 0 and stats["route_service_fallbacks"] == 0, stats
+    finally:
+        st.close()

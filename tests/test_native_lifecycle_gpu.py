@@ -1,0 +1,170 @@
+"""Native front end lifecycle and failure semantics (verdict r3 item 4):
+
+* model hot swap: /api/admin/reload_model (relayed to the app) re-packs the model for every GPU
+  slot of the native front end; the main port then answers with the NEW model, byte-equal to the
+  app;
+* GPU quarantine + failover: with launches failing on one of two reactor GPU slots (a shared-GPU
+  rehearsal: both slots on device 0), no request sees a 5xx — failed rounds re-run on the other
+  slot, the failing slot is quarantined after ROUTEST_QUARANTINE_AFTER failures; with every slot
+  failing the model's fp32 CPU forward answers;
+* model coverage: wide MLPs (H = 1024) and tree ensembles are served natively (the main port stays
+  native), matching the Python path;
+* /api/health reports the native slots."""
+import http.client
+import json
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+BODY = {"summary": {"distance": 12345}, "pickup_time": "2025-08-25T08:30:00", "driver_age": 34,
+        "weather": "Sunny", "traffic": "Medium"}
+
+
+def _req(port, method, path, body=None):
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+    raw = None if body is None else json.dumps(body).encode()
+    c.request(method, path, body=raw, headers={"Content-Type": "application/json"} if raw else {})
+    r = c.getresponse()
+    return r.status, r.read()
+
+
+def _stack(model, tmp_path=None):
+    from routest_amd.api.app import build_services, create_app
+    from routest_amd.config import load_settings
+    from routest_amd.serve.eta_service import EtaService
+    from routest_amd.serve.frontend import ServingStack
+    s = load_settings(env={}, dotenv_path=None, devices=[0], warm_scorer=False)
+    sv = build_services(s, eta=EtaService(model, devices=[0]), store=None)
+    return ServingStack(sv, create_app(sv), model, [0], threads=2), sv
+
+
+def test_reload_hot_swaps_the_native_model(tmp_path):
+    from routest_amd.models.checkpoint import save_checkpoint
+    from routest_amd.serve.eta_service import default_model
+    m1, m2 = default_model(seed=1, steps=30), default_model(seed=2, steps=60)
+    save_checkpoint(str(tmp_path / "m2"), m2, trainer_state={"step": 1})
+    st, sv = _stack(m1)
+    try:
+        a0 = _req(st.port, "POST", "/api/predict_eta", BODY)
+        r = _req(st.port, "POST", "/api/admin/reload_model", {"path": str(tmp_path / "m2")})
+        assert r[0] == 200 and json.loads(r[1])["ok"]
+        assert st.front.model_epoch == 2
+        a1 = _req(st.port, "POST", "/api/predict_eta", BODY)
+        b1 = _req(st.app_server.port, "POST", "/api/predict_eta", BODY)
+        assert a1[0] == b1[0] == 200 and a1[1] == b1[1]          # the new model, byte-equal to the app
+        assert a1[1] != a0[1]
+        h = json.loads(_req(st.port, "GET", "/api/health")[1])
+        assert h["checks"]["native"]["model_epoch"] == 2 and h["checks"]["native"]["status"] == "ok"
+    finally:
+        st.close()
+
+
+def _hammer(port, n, threads=8):
+    codes = []
+    lock = threading.Lock()
+
+    def run(k):
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+        for i in range(n // threads):
+            b = dict(BODY, summary={"distance": 1000 + 17 * (i + k)})
+            c.request("POST", "/api/predict_eta", body=json.dumps(b).encode(),
+                      headers={"Content-Type": "application/json"})
+            r = c.getresponse()
+            r.read()
+            with lock:
+                codes.append(r.status)
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return codes
+
+
+def test_failing_gpu_slot_is_quarantined_without_5xx(monkeypatch):
+    from routest_amd.serve.eta_service import default_model
+    from routest_amd.serve.native_server import NativePredictServer
+    monkeypatch.setenv("ROUTEST_QUARANTINE_AFTER", "3")
+    monkeypatch.setenv("ROUTEST_PERSIST_IDLE_MS", "0")       # every round a normal launch
+    model = default_model(steps=30)
+    with NativePredictServer(model, device=[0, 0], threads=4) as srv:
+        ref = _req(srv.port, "POST", "/api/predict_eta", BODY)
+        assert srv.set_fault(1, True)
+        codes = _hammer(srv.port, 400)
+        assert codes.count(200) == len(codes) == 400          # 0 5xx: failed rounds ran on slot 0
+        h = srv.health()
+        assert h["slots"][1]["quarantined"] and h["slots"][1]["quarantines"] == 1, h
+        assert not h["slots"][0]["quarantined"] and h["degraded"]
+        assert h["stats"]["failovers"] >= 1
+        assert _req(srv.port, "POST", "/api/predict_eta", BODY) == ref
+        # every slot failing: the fp32 CPU forward answers (close to the bf16 kernel)
+        assert srv.set_fault(0, True)
+        codes = _hammer(srv.port, 80, threads=4)
+        assert codes.count(200) == 80
+        assert srv.stats()["cpu_rounds"] > 0
+        st, body = _req(srv.port, "POST", "/api/predict_eta", BODY)
+        assert st == 200
+        np.testing.assert_allclose(json.loads(body)["eta_minutes_ml"], json.loads(ref[1])["eta_minutes_ml"],
+                                   rtol=3e-2)
+        # recovery: the fault cleared, a probe restores the slot
+        srv.set_fault(0, False)
+        srv.set_fault(1, False)
+
+
+def test_env_fault_hook_reaches_the_native_path(monkeypatch):
+    from routest_amd.serve.eta_service import default_model
+    from routest_amd.serve.native_server import NativePredictServer
+    monkeypatch.setenv("ROUTEST_FAULT", "gpu_fail@1")
+    monkeypatch.setenv("ROUTEST_PERSIST_IDLE_MS", "0")
+    with NativePredictServer(default_model(steps=20), device=[0, 0], threads=2) as srv:
+        assert srv.health()["slots"][1]["fault_injected"] and not srv.health()["slots"][0]["fault_injected"]
+        assert _hammer(srv.port, 64, threads=4).count(200) == 64
+
+
+def test_wide_mlp_served_natively_matches_python():
+    from routest_amd.models.mlp3 import EtaMLP
+    from routest_amd.data.synth import synth_trips
+    from routest_amd.ops.eta_mlp import EtaMlpKernel
+    torch.manual_seed(0)
+    m = EtaMLP(1024)
+    x, y = synth_trips(4000, 0)
+    m.fit_normalization(x, y)
+    st, sv = _stack(m)
+    try:
+        assert st.front is not None
+        items = [{"summary": {"distance": 500 + 97 * i}, "pickup_time": "2025-08-27T17:30:00",
+                  "traffic": ["High", "Low", "Jam"][i % 3], "driver_age": 20 + i % 50} for i in range(300)]
+        a = _req(st.port, "POST", "/predict", items)
+        b = _req(st.app_server.port, "POST", "/predict", items)
+        assert a[0] == b[0] == 200
+        pa = [p["eta_minutes_ml"] for p in json.loads(a[1])["predictions"]]
+        pb = [p["eta_minutes_ml"] for p in json.loads(b[1])["predictions"]]
+        np.testing.assert_allclose(pa, pb, rtol=1e-5, atol=1e-4)
+        assert st.front.stats()["predictions"] >= 300            # answered natively
+        assert "wide" in st.front.health()["slots"][0]["model"]
+    finally:
+        st.close()
+
+
+def test_forest_served_natively_matches_cpu_reference():
+    from sklearn.ensemble import HistGradientBoostingRegressor
+    from routest_amd.data.synth import synth_trips
+    from routest_amd.models.forest import ForestModel
+    x, y = synth_trips(5000, 1)
+    hgb = HistGradientBoostingRegressor(max_iter=40, max_leaf_nodes=15, random_state=0).fit(x, y)
+    fm = ForestModel.from_sklearn_hgb(hgb)
+    st, sv = _stack(fm)
+    try:
+        assert st.front is not None and "forest" in st.front.health()["slots"][0]["model"]
+        a = _req(st.port, "POST", "/api/predict_eta", BODY)
+        b = _req(st.app_server.port, "POST", "/api/predict_eta", BODY)
+        assert a[0] == b[0] == 200
+        np.testing.assert_allclose(json.loads(a[1])["eta_minutes_ml"], json.loads(b[1])["eta_minutes_ml"],
+                                   rtol=1e-5)
+        assert st.front.stats()["predictions"] >= 1
+    finally:
+        st.close()
