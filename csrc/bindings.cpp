@@ -1129,7 +1129,7 @@ static std::shared_ptr<const rt::NativeModel> model_from(const py::dict& d, int 
 
 int64_t native_server_start(int64_t port, int64_t threads, std::vector<int64_t> devices, py::list models,
                             int64_t max_batch, std::vector<std::string> cors, bool cors_vercel, bool bind_any,
-                            int64_t upstream_port, py::list routes) {
+                            int64_t upstream_port, py::list routes, std::string history_db) {
   TORCH_CHECK(!devices.empty() && models.size() == devices.size(), "one model spec per GPU slot");
   TORCH_CHECK(max_batch >= 1 && max_batch <= (1 << 24), "max_batch out of range");
   TORCH_CHECK(routes.empty() || routes.size() == devices.size(), "one route config per GPU (or none)");
@@ -1143,7 +1143,7 @@ int64_t native_server_start(int64_t port, int64_t threads, std::vector<int64_t> 
   for (size_t g = 0; g < routes.size(); ++g) rcfg.push_back(route_cfg_from(routes[g].cast<py::dict>(), devs[g]));
   std::string err;
   const int64_t h = rt::native_server_start((int)port, (int)threads, devs, ms, (int)max_batch, cors, cors_vercel,
-                                            bind_any, (int)upstream_port, rcfg, err);
+                                            bind_any, (int)upstream_port, rcfg, history_db, err);
   TORCH_CHECK(h >= 0, "native server: ", err);
   return h;
 }
@@ -1389,7 +1389,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("native_server_start", &native_server_start, "native HTTP front end (predictions, routes, relay)",
         py::arg("port"), py::arg("threads"), py::arg("devices"), py::arg("models"), py::arg("max_batch"),
         py::arg("cors"), py::arg("cors_vercel"), py::arg("bind_any"), py::arg("upstream_port") = 0,
-        py::arg("routes") = py::list());
+        py::arg("routes") = py::list(), py::arg("history_db") = "");
   m.def("native_server_set_models", &native_server_set_models,
         "hot-swap the served models (one spec per GPU slot); returns the new epoch");
   m.def("native_server_set_fault", [](int64_t h, int64_t slot, bool on) {

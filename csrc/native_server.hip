@@ -53,6 +53,7 @@
 #include "native_model.h"
 #include "ops.h"
 #include "route_service.h"
+#include "runtime/history_db.h"
 #include "runtime/rt_core.h"
 
 namespace rt {
@@ -74,6 +75,7 @@ struct ServerCfg {
   int upstream_port = 0;               // Python app for everything not answered natively (0 = none)
   RouteService* routes = nullptr;      // this reactor's GPU's route service (nullptr = relay routes)
   Shared* sh = nullptr;                // the server's models, scorers and GPU health
+  std::string history_db;              // the store's SQLite file: history / locations answered natively
 };
 
 // GPU health of one reactor slot: consecutive launch failures quarantine the GPU; a
@@ -181,7 +183,7 @@ struct Pending {
 
 struct Stats {
   std::atomic<long long> requests{0}, predictions{0}, launches{0}, errors{0}, resident{0}, fallbacks{0},
-      wire8{0}, route_requests{0}, route_fallbacks{0}, relayed{0}, failovers{0}, cpu_rounds{0};
+      wire8{0}, route_requests{0}, route_fallbacks{0}, relayed{0}, failovers{0}, cpu_rounds{0}, history{0};
 };
 
 inline Stamp now_local() {
@@ -317,6 +319,8 @@ class Reactor {
   int cap_ = 0;
   size_t nrec_ = 0;
   std::unordered_map<int, hipStream_t> streams_;        // per device (failover launches)
+  rth::HistoryDb hdb_;                                  // this reactor's connection to the store
+  bool hdb_tried_ = false;
   std::unordered_map<int, ModelWs> ws_;                 // per device model workspace
   uint64_t next_gen_ = 1;
   std::unordered_map<int, Conn> conns_;
@@ -492,14 +496,15 @@ class Reactor {
 
   void respond(Conn& c, int code, const std::string& body, const std::string& origin, bool close_after) {
     if (c.npending > 0) run_batch();   // HTTP/1.1 pipelining: answers leave in request order
-    const char* reason = code == 200 ? "OK" : code == 400 ? "Bad Request" : code == 404 ? "Not Found"
+    const char* reason = code == 200 ? "OK" : code == 204 ? "No Content" : code == 400 ? "Bad Request" : code == 404 ? "Not Found"
                          : code == 405 ? "Method Not Allowed" : code == 411 ? "Length Required"
                          : code == 413 ? "Payload Too Large" : code == 431 ? "Request Header Fields Too Large"
                          : code == 502 ? "Bad Gateway" : code == 503 ? "Service Unavailable" : "Error";
     char head[256];
-    const int hn = std::snprintf(head, sizeof head,
-                                 "HTTP/1.1 %d %s\r\ncontent-type: application/json\r\ncontent-length: %zu\r\n",
-                                 code, reason, body.size());
+    const int hn = code == 204 ? std::snprintf(head, sizeof head, "HTTP/1.1 204 No Content\r\n")
+                               : std::snprintf(head, sizeof head,
+                                               "HTTP/1.1 %d %s\r\ncontent-type: application/json\r\ncontent-length: %zu\r\n",
+                                               code, reason, body.size());
     c.out.append(head, (size_t)hn);
     if (cors_ok(origin)) {
       c.out += "access-control-allow-origin: ";
@@ -542,6 +547,8 @@ class Reactor {
       cfg_.routes->submit(j);
       return;
     }
+    if (!cfg_.history_db.empty() && (method == "GET" || method == "DELETE") && answer_history(c, method, path, keep, origin, raw))
+      return;
     const bool is_pe = path == "/api/predict_eta", is_p = path == "/predict";
     // a model family the native path does not serve (after a hot swap): the app answers
     const bool no_model = (is_pe || is_p) && method == "POST" && cfg_.sh->model(cfg_.slot) == nullptr;
@@ -615,6 +622,56 @@ class Reactor {
     }
     ++c.npending;
     pending_.push_back(std::move(pd));
+  }
+
+  // History list / detail / delete and locations straight from the store's SQLite database
+  // (csrc/runtime/history_db.h, byte-identical to the app); false: not answered here (relay).
+  bool answer_history(Conn& c, const std::string& method, const std::string& path, bool keep,
+                      const std::string& origin, const std::string& raw) {
+    const bool list = path == "/api/history" && method == "GET";
+    const bool item = path.size() > 13 && path.compare(0, 13, "/api/history/") == 0 && path.find('/', 13) == std::string::npos;
+    const bool locs = path == "/api/locations" && method == "GET";
+    if (!list && !item && !locs) return false;
+    if (!hdb_tried_) {
+      hdb_tried_ = true;
+      std::string err;
+      (void)hdb_.open(cfg_.history_db, err);
+    }
+    if (!hdb_.ok()) return false;
+    rth::Reply r;
+    if (list) {
+      // the raw query string of the request line; percent-encoded or repeated params -> the app
+      const size_t le = raw.find("\r\n");
+      const std::string line = raw.substr(0, le);
+      const size_t qm = line.find('?');
+      const size_t sp = line.rfind(' ');
+      std::string q = (qm != std::string::npos && sp != std::string::npos && sp > qm) ? line.substr(qm + 1, sp - qm - 1) : "";
+      if (q.find('%') != std::string::npos || q.find('+') != std::string::npos) return false;
+      std::string lim;
+      int found = 0;
+      size_t b = 0;
+      while (b <= q.size() && !q.empty()) {
+        size_t e = q.find('&', b);
+        if (e == std::string::npos) e = q.size();
+        const std::string kv = q.substr(b, e - b);
+        if (kv.compare(0, 6, "limit=") == 0) { lim = kv.substr(6); ++found; }
+        else if (kv == "limit") { lim.clear(); ++found; }
+        b = e + 1;
+      }
+      if (found > 1) return false;
+      r = hdb_.history(found ? lim.c_str() : nullptr);
+    } else if (item) {
+      const std::string id = path.substr(13);
+      if (id.find('%') != std::string::npos) return false;
+      r = method == "GET" ? hdb_.detail(id) : hdb_.del(id);
+    } else {
+      r = hdb_.locations();
+    }
+    if (r.fallback) return false;
+    st_.history.fetch_add(1, std::memory_order_relaxed);
+    if (c.npending > 0) run_batch();
+    respond(c, r.status, r.body, origin, !keep);
+    return true;
   }
 
   // ---------------------------------------------------------------- route jobs coming back
@@ -1007,7 +1064,8 @@ std::vector<Server*> g_servers;
 int64_t native_server_start(int port, int threads, const std::vector<int>& devices,
                             const std::vector<std::shared_ptr<const NativeModel>>& models, int max_batch,
                             const std::vector<std::string>& cors, bool cors_vercel, bool bind_any, int upstream_port,
-                            const std::vector<RouteServiceCfg>& routes, std::string& err) {
+                            const std::vector<RouteServiceCfg>& routes, const std::string& history_db,
+                            std::string& err) {
   if (devices.empty() || devices.size() != models.size() || (!routes.empty() && routes.size() != devices.size())) {
     err = "devices/models/routes mismatch";
     return -1;
@@ -1020,6 +1078,7 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
   s->cfg.cors_vercel = cors_vercel;
   s->cfg.upstream_port = upstream_port;
   s->cfg.sh = &s->sh;
+  s->cfg.history_db = history_db;
   if (const char* v = std::getenv("ROUTEST_PERSIST_IDLE_MS")) s->cfg.persist_idle_ms = std::atof(v);
   if (const char* v = std::getenv("ROUTEST_PERSIST_CAP")) s->cfg.persist_cap = std::atoi(v);
   if (const char* v = std::getenv("ROUTEST_PERSIST_LIFE_MS")) s->cfg.persist_life_ms = std::atof(v);
@@ -1165,7 +1224,7 @@ void native_server_stop(int64_t h) {
 
 std::vector<long long> native_server_stats(int64_t h) {
   std::lock_guard<std::mutex> lk(g_srv_mu);
-  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(29, 0);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(30, 0);
   Server* s = g_servers[h];
   std::vector<long long> v = {s->stats.requests.load(), s->stats.predictions.load(), s->stats.launches.load(),
                               s->stats.errors.load(), s->stats.resident.load(), s->stats.fallbacks.load(),
@@ -1179,6 +1238,7 @@ std::vector<long long> native_server_stats(int64_t h) {
   v.insert(v.end(), rs.begin(), rs.end());
   v.push_back(s->stats.failovers.load());
   v.push_back(s->stats.cpu_rounds.load());
+  v.push_back(s->stats.history.load());
   return v;
 }
 

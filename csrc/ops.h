@@ -220,7 +220,8 @@ struct NativeModel;       // native_model.h
 int64_t native_server_start(int port, int threads, const std::vector<int>& devices,
                             const std::vector<std::shared_ptr<const NativeModel>>& models, int max_batch,
                             const std::vector<std::string>& cors, bool cors_vercel, bool bind_any, int upstream_port,
-                            const std::vector<RouteServiceCfg>& routes, std::string& err);
+                            const std::vector<RouteServiceCfg>& routes, const std::string& history_db,
+                            std::string& err);
 int64_t native_server_set_models(int64_t h, const std::vector<std::shared_ptr<const NativeModel>>& models,
                                  std::string& err);
 bool native_server_set_fault(int64_t h, int slot, bool on);

@@ -14,6 +14,7 @@
 #include <map>
 #include <memory>
 
+#include "history_db.h"
 #include "route_core.h"
 
 namespace py = pybind11;
@@ -143,6 +144,30 @@ class PyGraphSteps {
 };
 
 py::bytes to_bytes(const std::string& s) { return py::bytes(s); }
+
+// The native history reader (history_db.h) for CPU tests: (status, body) or None (-> the app).
+class PyHistoryDb {
+ public:
+  explicit PyHistoryDb(const std::string& path) {
+    std::string err;
+    if (!db_.open(path, err)) throw std::runtime_error("HistoryDb: " + err);
+  }
+  py::object wrap(const rth::Reply& r) {
+    if (r.fallback) return py::none();
+    return py::make_tuple(r.status, to_bytes(r.body));
+  }
+  py::object history(py::object limit) {
+    if (limit.is_none()) return wrap(db_.history(nullptr));
+    const std::string l = limit.cast<std::string>();
+    return wrap(db_.history(l.c_str()));
+  }
+  py::object detail(const std::string& id) { return wrap(db_.detail(id)); }
+  py::object del(const std::string& id) { return wrap(db_.del(id)); }
+  py::object locations() { return wrap(db_.locations()); }
+
+ private:
+  rth::HistoryDb db_;
+};
 
 // Finish an assembled request as the FastAPI handler answers it (no ETA, no persistence).
 std::pair<int, std::string> finish_plain(const rtr::Assembled& a, bool request_route_compat, bool is_request_route) {
@@ -280,6 +305,12 @@ void bind_route(py::module& m) {
         py::arg("glon"), py::arg("nodes"), py::arg("trips"), py::arg("legs"), py::arg("steps") = py::none(),
         py::arg("cost") = py::none());
   m.def("py_round", &rtr::py_round);
+  py::class_<PyHistoryDb>(m, "HistoryDb")
+      .def(py::init<const std::string&>())
+      .def("history", &PyHistoryDb::history, py::arg("limit") = py::none())
+      .def("detail", &PyHistoryDb::detail)
+      .def("delete", &PyHistoryDb::del)
+      .def("locations", &PyHistoryDb::locations);
   py::class_<PyGraphSteps>(m, "GraphSteps")
       .def(py::init<py::array_t<int32_t, py::array::c_style | py::array::forcecast>,
                     py::array_t<int32_t, py::array::c_style | py::array::forcecast>,

@@ -28,6 +28,14 @@ struct Api {
   int (*finalize)(void*) = nullptr;
   const char* (*errmsg)(void*) = nullptr;
   void (*free_)(void*) = nullptr;
+  int (*column_count)(void*) = nullptr;
+  int (*column_type)(void*, int) = nullptr;
+  double (*column_double)(void*, int) = nullptr;
+  long long (*column_int64)(void*, int) = nullptr;
+  const unsigned char* (*column_text)(void*, int) = nullptr;
+  int (*column_bytes)(void*, int) = nullptr;
+  const char* (*column_name)(void*, int) = nullptr;
+  int (*changes)(void*) = nullptr;
 
   bool load(std::string& err) {
     if (h) return true;
@@ -54,12 +62,21 @@ struct Api {
     sym(finalize, "sqlite3_finalize");
     sym(errmsg, "sqlite3_errmsg");
     sym(free_, "sqlite3_free");
+    sym(column_count, "sqlite3_column_count");
+    sym(column_type, "sqlite3_column_type");
+    sym(column_double, "sqlite3_column_double");
+    sym(column_int64, "sqlite3_column_int64");
+    sym(column_text, "sqlite3_column_text");
+    sym(column_bytes, "sqlite3_column_bytes");
+    sym(column_name, "sqlite3_column_name");
+    sym(changes, "sqlite3_changes");
     if (!ok) err = "libsqlite3: missing symbols";
     return ok;
   }
 };
 
 constexpr int OK = 0, ROW = 100, DONE = 101;
+constexpr int T_INTEGER = 1, T_FLOAT = 2, T_TEXT = 3, T_BLOB = 4, T_NULL = 5;
 constexpr int OPEN_READWRITE = 0x2, OPEN_CREATE = 0x4, OPEN_URI = 0x40, OPEN_NOMUTEX = 0x8000;
 inline void (*const TRANSIENT)(void*) = reinterpret_cast<void (*)(void*)>(-1);
 

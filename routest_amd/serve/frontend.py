@@ -6,6 +6,8 @@
                        │  /api/request_route ................ native route service per GPU
                        │                                       (CCH road matrices + K6 + CCH legs
                        │                                        + C++ GeoJSON with maneuvers)
+                       ├─ /api/history[/<id>] (GET, DELETE),
+                       │  /api/locations .................... the store's SQLite file, natively
                        └─ everything else, and requests the native paths do not mirror
                                                  ──relay──> FastAPI app (uvicorn)  127.0.0.1:<private>
 
@@ -92,9 +94,15 @@ def start_front_end(sv, model, devices: Sequence[int], port: int = 0, upstream_p
                                  timeout_us if timeout_us is not None else s.route_batch_timeout_us)
         else:
             log.info("route requests relayed to the Python app: %s", why)
+    # history / locations read natively from the SQLite store (the app still owns writes it makes)
+    from ..utils.faults import active_faults
+    hist = ""
+    st = sv.store
+    if st is not None and getattr(st, "kind", "") == "sqlite" and "store_fail" not in active_faults():
+        hist = st.sqlite_uri
     srv = NativePredictServer(model, device=list(devices), port=port, threads=max(threads, len(devices)),
                               cors_origins=cors_origins if cors_origins is not None else s.cors_origins,
-                              bind_any=bind_any, upstream_port=upstream_port, routes=cfgs)
+                              bind_any=bind_any, upstream_port=upstream_port, routes=cfgs, history_db=hist)
     return srv
 
 

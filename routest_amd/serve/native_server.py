@@ -85,12 +85,14 @@ class NativePredictServer:
     every GPU slot (rounds in flight finish on the old weights; the resident scorers restart), a
     GPU slot whose launches keep failing is quarantined and its reactors' rounds run on the other
     GPUs — or on the model's fp32 CPU forward when none is left — and :meth:`health` reports it.
+    ``history_db``: the store's SQLite file — GET/DELETE /api/history[/<id>] and GET /api/locations
+    are then answered natively from it (csrc/runtime/history_db.h, byte-identical to the app).
     ``ROUTEST_FAULT=gpu_fail[@slot]`` (or :meth:`set_fault`) injects launch failures."""
 
     def __init__(self, model, device=0, port: int = 0, threads: int = 2, max_batch: int = 1 << 18,
                  cors_origins: Sequence[str] = ("http://localhost:3000", "http://127.0.0.1:3000"),
                  cors_vercel: bool = True, bind_any: bool = False, variant: int = -1,
-                 upstream_port: int = 0, routes: Optional[List[dict]] = None):
+                 upstream_port: int = 0, routes: Optional[List[dict]] = None, history_db: str = ""):
         self.C = native(required=True)
         self.devices = [device] if isinstance(device, int) else list(device)
         self.routes = list(routes or [])      # keeps the route configs' tensors alive
@@ -101,7 +103,8 @@ class NativePredictServer:
         self.model_epoch = 1
         self.h: Optional[int] = self.C.native_server_start(
             self.port, threads, self.devices, specs, max_batch, list(cors_origins), cors_vercel, bind_any,
-            int(upstream_port), self.routes)
+            int(upstream_port), self.routes, history_db)
+        self.history_db = history_db
 
     def set_model(self, model) -> int:
         """Hot swap on every GPU slot; returns the new model epoch.  ``None`` (a model family the
@@ -146,7 +149,9 @@ class NativePredictServer:
                  # CCH: routing contexts customized by the services, and their total build time (us)
                  "route_contexts_built", "route_us_context",
                  # rounds re-run on another GPU slot (failover) / on the CPU forward (no GPU left)
-                 "failovers", "cpu_rounds")
+                 "failovers", "cpu_rounds",
+                 # history / locations requests answered from the store's database natively
+                 "history_native")
         return dict(zip(names, v))
 
     def close(self) -> None:

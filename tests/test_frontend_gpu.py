@@ -171,6 +171,40 @@ def test_relayed_requests_match_the_app(hav, method, path, body):
         assert set(json.loads(a[1])) == set(json.loads(b[1]))
 
 
+def test_history_and_locations_answered_natively_byte_identical(hav):
+    """GET/DELETE /api/history[/<id>] and GET /api/locations come from the store's SQLite file in
+    C++ (csrc/runtime/history_db.h): same status and bytes as the app for every limit form."""
+    st, sv = hav
+    rng = np.random.default_rng(21)
+    lat, lon = 14.55 + rng.normal(0, 0.03, 100), 121.02 + rng.normal(0, 0.03, 100)
+    ids = []
+    for p in _payloads(12, lat, lon, seed=5):
+        d = json.loads(_req(st.port, "POST", "/api/optimize_route", p)[1])
+        if d.get("properties", {}).get("request_id"):
+            ids.append(d["properties"]["request_id"])
+    assert len(ids) >= 5
+    h0 = st.front.stats()["history_native"]
+    paths = ["/api/history", "/api/history?limit=3", "/api/history?limit=0", "/api/history?limit=-2",
+             "/api/history?limit=abc", "/api/history?limit=", "/api/history?limit=2.5", "/api/history?limit=1_0",
+             "/api/history?limit=%33", "/api/history?limit=1&limit=2", "/api/history?foo=1&limit=4",
+             "/api/history?limit=100000", "/api/locations", f"/api/history/{ids[0]}", f"/api/history/{ids[-1]}",
+             "/api/history/00000000-0000-0000-0000-000000000000", "/api/history/not-a-uuid"]
+    for path in paths:
+        a = _req(st.port, "GET", path)
+        b = _req(st.app_server.port, "GET", path)
+        assert a[0] == b[0] and a[1] == b[1], (path, a[:2], b[:2])
+        ha, hb = ({k.lower(): v for k, v in x[2].items()} for x in (a, b))
+        assert ha.get("content-type") == hb.get("content-type"), path
+    assert st.front.stats()["history_native"] - h0 >= len(paths) - 3       # %-encoded/repeated -> app
+    # delete: native answers 204, then both sides agree it is gone
+    a = _req(st.port, "DELETE", f"/api/history/{ids[1]}")
+    assert a[0] == 204 and a[1] == b""
+    for port in (st.port, st.app_server.port):
+        assert _req(port, "GET", f"/api/history/{ids[1]}")[0] == 404
+        assert _req(port, "DELETE", f"/api/history/{ids[1]}")[:2] == _req(st.app_server.port, "DELETE",
+                                                                           f"/api/history/{ids[1]}")[:2]
+
+
 def test_sse_feed_tunnels_through_the_front_end(hav):
     st, sv = hav
     s = socket.create_connection(("127.0.0.1", st.port), timeout=20)
