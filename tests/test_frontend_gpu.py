@@ -187,7 +187,7 @@ def test_history_and_locations_answered_natively_byte_identical(hav):
     paths = ["/api/history", "/api/history?limit=3", "/api/history?limit=0", "/api/history?limit=-2",
              "/api/history?limit=abc", "/api/history?limit=", "/api/history?limit=2.5", "/api/history?limit=1_0",
              "/api/history?limit=%33", "/api/history?limit=1&limit=2", "/api/history?foo=1&limit=4",
-             "/api/history?limit=100000", "/api/locations", f"/api/history/{ids[0]}", f"/api/history/{ids[-1]}",
+             "/api/history?limit=100000", "/api/locations", "/api/ping", f"/api/history/{ids[0]}", f"/api/history/{ids[-1]}",
              "/api/history/00000000-0000-0000-0000-000000000000", "/api/history/not-a-uuid"]
     for path in paths:
         a = _req(st.port, "GET", path)

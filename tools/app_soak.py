@@ -250,6 +250,7 @@ def stack_soak(a, sv, app, model, route_req, eta_req, rng) -> int:
                     "p50_ms": float(lat[len(lat) // 2]) / 1e3, "p99_ms": float(lat[int(len(lat) * 0.99) - 1]) / 1e3,
                     "status_by_endpoint": by, "contract_errors": bad, "body_sample_errors": sample_errors,
                     "native_route_jobs": f1["route_jobs"] - f0["route_jobs"], "relayed": f1["relayed"] - f0["relayed"],
+                    "history_native": f1["history_native"] - f0["history_native"],
                     "route_persisted": f1["route_persisted"] - f0["route_persisted"]})
     sv.close()
     print(json.dumps(out), flush=True)
