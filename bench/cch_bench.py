@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--astar", action="store_true")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--threads", type=int, default=0,
+                    help="CPU baseline threads (0: OMP_NUM_THREADS, the box's CPU share, else the affinity set)")
     a = ap.parse_args()
     from routest_amd.routing.cch import RoadRouter, RouteContext
     dev = torch.device("cuda:0")
@@ -73,7 +75,7 @@ def main():
         emit(stage="astar_legs", legs=a.legs, ms=round(ta, 2), legs_per_s=round(a.legs / (ta / 1e3)))
     if a.cpu:
         from routest_amd import _rt
-        threads = len(os.sched_getaffinity(0))
+        threads = a.threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
         c = _rt.CCH(g.indptr, g.indices, g.lat, g.lon, threads)
         mc = c.customize(cost, g.length_m)
         emit(stage="cpu_customize", threads=threads, ms=round(mc.customize_ms, 1))

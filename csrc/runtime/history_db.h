@@ -48,8 +48,20 @@ class HistoryDb {
   }
   bool ok() const { return db_ != nullptr; }
 
+  // Every call resets its statements on the way out: a statement left on a ROW keeps the
+  // connection's read transaction (its WAL snapshot) open, and later reads would not see rows the
+  // route service or the app wrote or deleted since.
+  struct ResetAll {
+    HistoryDb* h;
+    ~ResetAll() {
+      for (void* st : {h->st_list_, h->st_first_, h->st_req_, h->st_res_, h->st_del_, h->st_loc_})
+        if (st) h->sql_.reset(st);
+    }
+  };
+
   // GET /api/history?limit=<raw>; raw = nullptr when absent
   Reply history(const char* raw_limit) {
+    ResetAll guard{this};
     Reply r;
     int lim = 20;
     if (raw_limit != nullptr && !parse_limit(raw_limit, lim)) return fb();
@@ -131,6 +143,7 @@ class HistoryDb {
 
   // GET /api/history/<id>
   Reply detail(const std::string& id) {
+    ResetAll guard{this};
     Reply r;
     if (!prep(st_req_, "SELECT id,origin_id,stops,status,request_time,engine,vehicle_id,driver_age FROM"
                        " route_requests WHERE id=?") ||
@@ -196,6 +209,7 @@ class HistoryDb {
 
   // DELETE /api/history/<id> -> 204 (reference semantics: 204 whether or not it existed)
   Reply del(const std::string& id) {
+    ResetAll guard{this};
     Reply r;
     if (!prep(st_del_, "DELETE FROM route_requests WHERE id=?")) return fb();
     sql_.reset(st_del_);
@@ -207,6 +221,7 @@ class HistoryDb {
 
   // GET /api/locations
   Reply locations() {
+    ResetAll guard{this};
     Reply r;
     if (!prep(st_loc_, "SELECT * FROM locations ORDER BY created_at, rowid")) return fb();
     sql_.reset(st_loc_);

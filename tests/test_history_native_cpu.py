@@ -59,3 +59,18 @@ def test_history_detail_delete_and_locations(app_and_db):
     assert c.get(f"/api/history/{rid}").status_code == 404          # the app sees the native delete
     assert db.history("100")[1] == c.get("/api/history?limit=100").content
     assert db.locations() == (200, c.get("/api/locations").content)
+
+
+def test_native_reads_see_later_writes_and_deletes(app_and_db):
+    """No statement is left open between calls: a held read transaction would pin an old WAL
+    snapshot, so rows the app writes or deletes afterwards would be missing / still listed."""
+    c, db = app_and_db
+    items = c.get("/api/history?limit=100").json()["items"]
+    assert db.detail(items[0]["request_id"])[0] == 200          # leaves nothing open
+    assert db.history("3")[0] == 200
+    assert c.delete(f"/api/history/{items[1]['request_id']}").status_code == 204
+    p = {"source_point": {"lat": 14.58, "lon": 121.05}, "destination_points": [{"lat": 14.56, "lon": 121.04}],
+         "driver_details": {"driver_name": "late", "vehicle_type": "car"}, "meta": {"origin_id": "late-1"}}
+    assert c.post("/api/optimize_route", json=p).status_code == 200
+    assert db.history("100")[1] == c.get("/api/history?limit=100").content
+    assert db.detail(items[1]["request_id"])[0] == 404
