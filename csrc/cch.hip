@@ -30,6 +30,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "cch_gpu.h"
@@ -94,7 +95,34 @@ struct LevelArgs {
   const int64_t* ofs;      // item prefix over that list
   int lo, hi;              // node index range of this level
   long long base, items;
+  const int64_t* tofs;     // triangle table (nullptr: binary search instead)
+  const int32_t* tri;
 };
+
+// arc {head i, head j} of a node's upward pair (i < j): the triangle table, else a binary search
+__device__ __forceinline__ int pair_arc(const LevelArgs& L, int z, int k, int i, int j, int u, int v) {
+  if (L.tri != nullptr) return L.tri[L.tofs[z] + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)];
+  return find_arc_d(L.up_ptr, L.up_head, u, v);
+}
+
+// one-time triangle table: item g -> (rank z, pair q) -> arc of the pair's heads
+__global__ void tri_build_kernel(const int32_t* __restrict__ up_ptr, const int32_t* __restrict__ up_head,
+                                 const int64_t* __restrict__ tofs, int N, long long T, int32_t* __restrict__ tri) {
+  for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < T; g += (long long)gridDim.x * blockDim.x) {
+    const int z = item_owner(tofs, 0, N, g);
+    const long long q = g - tofs[z];
+    const int a0 = up_ptr[z];
+    const int k = up_ptr[z + 1] - a0;
+    const double kk = (double)(2 * k - 1);
+    int i = (int)((kk - sqrt(kk * kk - 8.0 * (double)q)) * 0.5);
+    if (i < 0) i = 0;
+    auto row0 = [&](int r) { return (long long)r * (2 * k - r - 1) / 2; };
+    while (i > 0 && row0(i) > q) --i;
+    while (i + 1 < k && row0(i + 1) <= q) ++i;
+    const int j = (int)(q - row0(i)) + i + 1;
+    tri[g] = find_arc_d(up_ptr, up_head, up_head[a0 + i], up_head[a0 + j]);
+  }
+}
 
 // Basic customization of one height level: items [0, k) of node z finalize arc k-th of z; items
 // [k, k + k(k-1)/2) relax the lower triangle z of one pair of z's upward neighbours.
@@ -154,7 +182,7 @@ __global__ __launch_bounds__(256) void basic_level_kernel(LevelArgs L, unsigned 
   const int j = (int)(q - row0(i)) + i + 1;
   const int ai = a0 + i, aj = a0 + j;
   const int u = L.up_head[ai], v = L.up_head[aj];
-  const int t = find_arc_d(L.up_ptr, L.up_head, u, v);
+  const int t = pair_arc(L, z, k, i, j, u, v);
   if (t < 0) return;   // cannot happen in a chordal completion
   // u -> z -> v: (z,u) traversed down, (z,v) up;  v -> z -> u: (z,v) down, (z,u) up
   const float wu = wof(dn[ai]) + wof(up[aj]);
@@ -192,7 +220,8 @@ __global__ __launch_bounds__(256) void perfect_level_kernel(LevelArgs L, const u
   const int ac = a0 + c, aa = a0 + a;
   const int y = L.up_head[aa], z = L.up_head[ac];
   const int lo = z < y ? z : y, hi = z < y ? y : z;
-  const int azy = find_arc_d(L.up_ptr, L.up_head, lo, hi);
+  // upward lists are sorted by head, so the pair's order is the heads' order
+  const int azy = pair_arc(L, x, k, c < a ? c : a, c < a ? a : c, lo, hi);
   if (azy < 0) return;
   const float xz = wof(up[ac]), zx = wof(dn[ac]);
   const float zy = __uint_as_float(z < y ? pup[azy] : pdn[azy]);
@@ -704,6 +733,33 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   ck(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_fcnt, d_fcnt, N));
   cub_bytes = tb;
   ck(hipMalloc(&d_cub, cub_bytes ? cub_bytes : 1));
+  // triangle table within ROUTEST_CCH_TRI_GB of HBM (default 16; 0 disables)
+  if (e == hipSuccess) {
+    std::vector<int64_t> tofs(N + 1, 0);
+    for (int z = 0; z < N; ++z) {
+      const int64_t k = T_.up_ptr[z + 1] - T_.up_ptr[z];
+      tofs[z + 1] = tofs[z] + k * (k - 1) / 2;
+    }
+    const char* env = std::getenv("ROUTEST_CCH_TRI_GB");
+    const double budget = env ? std::atof(env) : 16.0;
+    const int64_t T = tofs[N];
+    if (T > 0 && (double)T * 4.0 <= budget * 1073741824.0 && T < ((int64_t)1 << 40)) {
+      if (up_copy(d_tofs, tofs.data(), N + 1) == hipSuccess && dmalloc(d_tri, (size_t)T) == hipSuccess) {
+        hipLaunchKernelGGL(tri_build_kernel, dim3((unsigned)std::min<int64_t>(65536, (T + 255) / 256)), dim3(256), 0, 0,
+                           d_up_ptr, d_up_head, d_tofs, N, (long long)T, d_tri);
+        if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
+          n_tri = T;
+        } else {
+          dfree(d_tri);
+          dfree(d_tofs);
+        }
+      } else {
+        (void)hipGetLastError();
+        dfree(d_tri);
+        dfree(d_tofs);
+      }
+    }
+  }
   (void)hipSetDevice(cur);
   if (e != hipSuccess) throw std::runtime_error(std::string("CchGpu: ") + hipGetErrorString(e));
 }
@@ -732,6 +788,8 @@ CchGpu::~CchGpu() {
   dfree(d_dnodes);
   dfree(d_bofs);
   dfree(d_pofs);
+  dfree(d_tofs);
+  dfree(d_tri);
   dfree(d_up64);
   dfree(d_dn64);
   dfree(d_pup);
@@ -799,7 +857,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   ck(hipGetLastError());
   // basic, bottom-up by height
   for (int h = 0; h <= T_.max_height && e == hipSuccess; ++h) {
-    LevelArgs L{d_up_ptr, d_up_head, d_hnodes, d_bofs, (int)T_.hlev_ptr[h], (int)T_.hlev_ptr[h + 1], 0, 0};
+    LevelArgs L{d_up_ptr, d_up_head, d_hnodes, d_bofs, (int)T_.hlev_ptr[h], (int)T_.hlev_ptr[h + 1], 0, 0, d_tofs, d_tri};
     if (L.lo >= L.hi) continue;
     L.base = bofs_[L.lo];
     L.items = bofs_[L.hi] - bofs_[L.lo];
@@ -812,7 +870,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   hipLaunchKernelGGL(perfect_init_kernel, dim3(fill_blocks), dim3(256), 0, s, d_up64, d_dn64, d_pup, d_pdn, (long long)M);
   ck(hipGetLastError());
   for (int d = 0; d <= T_.max_depth && e == hipSuccess; ++d) {
-    LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0};
+    LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0, d_tofs, d_tri};
     if (L.lo >= L.hi) continue;
     L.base = pofs_[L.lo];
     L.items = pofs_[L.hi] - pofs_[L.lo];

@@ -86,6 +86,8 @@ class PyCchGpu {
     d["top_separator"] = T.separator_top;
     d["build_ms"] = build_ms_;
     d["cached_metrics"] = g_->cached();
+    d["triangle_table"] = g_->has_triangle_table();
+    d["triangles"] = g_->triangles();
     return d;
   }
 

@@ -80,6 +80,8 @@ class CchGpu {
   const rcch::Topology& topo() const { return T_; }
   int device() const { return dev_; }
   int stride() const { return T_.max_depth + 1; }
+  bool has_triangle_table() const { return d_tri != nullptr; }
+  int64_t triangles() const { return n_tri; }
 
   // ETA model used for context costs (the fused K1+K2 kernel's 32x32 blob on this device)
   void set_eta(const void* blob, int H, const NormParams& np, int variant, int num_cus);
@@ -120,6 +122,12 @@ class CchGpu {
   int32_t *d_hnodes = nullptr, *d_dnodes = nullptr;
   int64_t *d_bofs = nullptr, *d_pofs = nullptr;    // work-item prefixes in level order
   std::vector<int64_t> bofs_, pofs_;               // host copies (level boundaries)
+  // triangle table (metric-independent): for the pair (i < j) of rank z's upward arcs, the arc id of
+  // {head i, head j} at tri[tofs[z] + i(2k-i-1)/2 + j-i-1] — the customization's binary searches
+  // done once per graph (nullptr when it would not fit the ROUTEST_CCH_TRI_GB budget)
+  int64_t* d_tofs = nullptr;
+  int32_t* d_tri = nullptr;
+  int64_t n_tri = 0;
   // customization temporaries (one customization at a time: mu_cust_)
   unsigned long long *d_up64 = nullptr, *d_dn64 = nullptr;
   uint32_t *d_pup = nullptr, *d_pdn = nullptr;
