@@ -14,6 +14,7 @@
 #include <map>
 #include <memory>
 
+#include "alternatives.h"
 #include "history_db.h"
 #include "route_core.h"
 
@@ -288,9 +289,38 @@ py::object route_assemble_graph(py::bytes body, const std::string& engine,
   return py::make_tuple(res.first, to_bytes(res.second));
 }
 
+using F64 = py::array_t<double, py::array::c_style | py::array::forcecast>;
+using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
+
+std::vector<int> py_via_nodes(F64 lat, F64 lon, int s, int t, int n, double stretch) {
+  if (lat.shape(0) != lon.shape(0)) throw std::invalid_argument("lat/lon length mismatch");
+  py::gil_scoped_release nogil;
+  return ralt::via_nodes(lat.data(), lon.data(), (int)lat.shape(0), s, t, n, stretch);
+}
+
+std::vector<double> py_alt_scores(F64 lat, F64 lon, F64 delay, std::vector<I32> paths, std::vector<double> seconds,
+                                  int kind) {
+  const int64_t N = lat.shape(0);
+  if (lon.shape(0) != N || delay.shape(0) != N) throw std::invalid_argument("lat/lon/delay length mismatch");
+  if (seconds.size() != paths.size()) throw std::invalid_argument("one seconds value per path");
+  std::vector<double> out(paths.size());
+  for (size_t i = 0; i < paths.size(); ++i) {
+    const int32_t* p = paths[i].data();
+    const size_t n = (size_t)paths[i].shape(0);
+    for (size_t k = 0; k < n; ++k)
+      if (p[k] < 0 || p[k] >= N) throw std::out_of_range("path node out of range");
+    out[i] = ralt::candidate_score(lat.data(), lon.data(), delay.data(), p, n, seconds[i], kind);
+  }
+  return out;
+}
+
 }  // namespace
 
 void bind_route(py::module& m) {
+  m.def("via_nodes", &py_via_nodes, py::arg("lat"), py::arg("lon"), py::arg("s"), py::arg("t"), py::arg("n"),
+        py::arg("stretch") = 1.35);
+  m.def("alt_scores", &py_alt_scores, py::arg("lat"), py::arg("lon"), py::arg("delay"), py::arg("paths"),
+        py::arg("seconds"), py::arg("kind"));
   m.def("haversine_m", &py_haversine);
   m.def("path_length_m", &py_path_length);
   m.def("haversine_matrix", &py_haversine_matrix);

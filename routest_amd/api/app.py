@@ -58,33 +58,76 @@ class Services:
     def get_scorer(self):
         """Candidate-route scorer (GCN on the road graph), built on first use: the provider's graph
         when ``ROUTEST_PROVIDER=graph``, else a synthetic ``ROUTEST_GRAPH_NODES``-node graph.  It is
-        trained (``ROUTEST_SCORER_TRAIN_STEPS``; HIP backward on a GPU, models/gcn_train.py) on the
-        graph's learned edge times — the provider's, or the ETA model's over the synthetic graph."""
+        trained for ``ROUTEST_SCORER_TRAIN_STEPS`` (HIP backward on a GPU):
+
+        * ``ROUTEST_SCORER_TARGET=observed`` (default): on ``ROUTEST_SCORER_TRIPS`` observed trips of
+          the seeded synthetic trip world (models/gcn_observed.py TripWorld: the edge-cost model's
+          seconds plus hidden hot-spot / signal delays — offline there is no real trip log), so it
+          predicts what the edge costs do not know;
+        * ``edge``: the round-3 target, node delays from the learned edge times (gcn_train.py)."""
         with self._scorer_lock:
             if self.scorer is None:
                 from ..routing.scorer import RouteScorer
                 g = getattr(self.provider, "g", None)
-                cost = getattr(self.provider, "cost", None) if g is not None else None
+                prov_graph = g is not None
                 if g is None:
                     from ..data.graph import synth_road_graph
                     g = synth_road_graph(self.settings.graph_nodes)
                 model, info = None, None
+                kind = "edge"
                 steps = int(self.settings.scorer_train_steps)
                 if steps > 0:
-                    if cost is None:
-                        from ..models.mlp3 import EtaMLP
-                        from ..routing.graph import edge_costs
-                        m = getattr(self.eta, "model", None)
-                        if isinstance(m, EtaMLP):
-                            cost = edge_costs(g, m, device=self.route_device)
-                        else:
-                            from ..data.graph import CLASS_SPEED_KMH
-                            cost = (g.length_m / (CLASS_SPEED_KMH[g.road_class] / 3.6)).astype("float32")
-                    from ..models.gcn_train import train
-                    model, info = train(g, cost, steps=steps, lr=5e-3, device=self.route_device, log_every=steps)
-                self.scorer = RouteScorer(g, model=model, device=self.route_device)
+                    cost = self._scorer_costs(g, prov_graph)
+                    if self.settings.scorer_target == "observed":
+                        from ..models.gcn_observed import TripWorld, train_observed
+                        search = self._world_search(g, cost, prov_graph)
+                        obs = TripWorld(g, cost, seed=3).observe(int(self.settings.scorer_trips), search, seed=1)
+                        model, info = train_observed(g, obs, steps=steps, lr=1e-2, device=self.route_device,
+                                                     log_every=steps)
+                        kind = "observed"
+                    else:
+                        from ..models.gcn_train import train
+                        model, info = train(g, cost, steps=steps, lr=5e-3, device=self.route_device, log_every=steps)
+                self.scorer = RouteScorer(g, model=model, device=self.route_device, kind=kind)
                 self.scorer.training = info
+                hook = getattr(self, "on_scorer", None)
+                if hook is not None:
+                    try:
+                        hook(self.scorer)
+                    except Exception as e:  # noqa: BLE001
+                        log.warning("scorer hook failed: %r", e)
             return self.scorer
+
+    def _scorer_costs(self, g, prov_graph: bool):
+        """Edge seconds the scorer's world starts from: the provider's fixed costs, its default
+        context's costs (context-aware CCH provider), or the ETA model's over a synthetic graph."""
+        import numpy as np
+        if prov_graph:
+            if getattr(self.provider, "cost", None) is not None:
+                return np.asarray(self.provider.cost, dtype=np.float32)
+            if hasattr(self.provider, "metric_key"):
+                return self.provider.edge_seconds(self.provider.metric_key(None))
+        from ..models.mlp3 import EtaMLP
+        from ..routing.graph import edge_costs
+        m = getattr(self.eta, "model", None)
+        if isinstance(m, EtaMLP):
+            return edge_costs(g, m, device=self.route_device)
+        from ..data.graph import CLASS_SPEED_KMH
+        return (g.length_m / (CLASS_SPEED_KMH[g.road_class] / 3.6)).astype("float32")
+
+    def _world_search(self, g, cost, prov_graph: bool):
+        """(src, dst) -> [(seconds, path)] exact on ``cost`` (the CCH router of that metric)."""
+        from ..routing.cch import RoadRouter
+        if prov_graph and hasattr(self.provider, "router"):
+            r = self.provider.router()
+        else:
+            r = RoadRouter(g, device=self.route_device)
+        key = r.metric_from_costs(1 << 43, cost)
+
+        def search(src, dst):
+            sec, _, st, paths = r.route(src, dst, key)
+            return [(float(sec[i]), paths[i].tolist()) if st[i] == 0 else (float("nan"), []) for i in range(len(src))]
+        return search
 
     def graph_search(self):
         """(src, dst) -> [(seconds, node path)] on the provider's graph: the route batcher's batched

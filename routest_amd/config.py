@@ -79,7 +79,11 @@ class Settings:
     route_gpu_min_stops: int = 32        # ROUTEST_ROUTE_GPU_MIN_STOPS: haversine requests with fewer
                                          # destinations stay inline (profiles/route_http_r2.jsonl)
     warm_scorer: bool = True             # ROUTEST_WARM_SCORER: build the GCN scorer at startup
-    scorer_train_steps: int = 300        # ROUTEST_SCORER_TRAIN_STEPS: train the GCN scorer on the edge times
+    scorer_train_steps: int = 300        # ROUTEST_SCORER_TRAIN_STEPS: training steps of the GCN scorer
+    # ROUTEST_SCORER_TARGET: "observed" (trip observations: hidden delays the edge costs lack,
+    # models/gcn_observed.py) or "edge" (round 3: the learned edge times themselves)
+    scorer_target: str = "observed"
+    scorer_trips: int = 20000            # ROUTEST_SCORER_TRIPS: observed trips to train on
     sim_tick_min_s: float = 2.0          # ROUTEST_SIM_TICK_MIN (reference: U(2,5) s, utils.py:251)
     sim_tick_max_s: float = 5.0          # ROUTEST_SIM_TICK_MAX
     max_simulations: int = 256           # ROUTEST_MAX_SIMULATIONS (reference: unbounded threads)
@@ -160,6 +164,8 @@ def load_settings(env: Optional[Dict[str, str]] = None, dotenv_path: Optional[st
         route_gpu_min_stops=_int("ROUTEST_ROUTE_GPU_MIN_STOPS", 32),
         warm_scorer=_as_bool(g("ROUTEST_WARM_SCORER"), True),
         scorer_train_steps=_int("ROUTEST_SCORER_TRAIN_STEPS", 300),
+        scorer_target=(g("ROUTEST_SCORER_TARGET") or "observed").lower(),
+        scorer_trips=_int("ROUTEST_SCORER_TRIPS", 20000),
         sim_tick_min_s=_float("ROUTEST_SIM_TICK_MIN", 2.0),
         sim_tick_max_s=_float("ROUTEST_SIM_TICK_MAX", 5.0),
         max_simulations=_int("ROUTEST_MAX_SIMULATIONS", 256),

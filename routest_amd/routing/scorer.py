@@ -24,8 +24,12 @@ from ..models.gcn import GcnScorer, score_routes_ref
 class RouteScorer:
     blocking = True      # GPU synchronisation / graph snapping: handlers run it in the thread pool
 
-    def __init__(self, g: RoadGraph, model: Optional[GcnScorer] = None, device: Optional[Any] = None):
+    def __init__(self, g: RoadGraph, model: Optional[GcnScorer] = None, device: Optional[Any] = None,
+                 kind: str = "edge"):
         self.g = g
+        # "observed": trained on observed trips (predicted hidden seconds, models/gcn_observed.py);
+        # "edge": the round-3 delay-weighted length (routing/alternatives.py picks accordingly)
+        self.kind = kind
         self.model = model or GcnScorer(seed=0)
         self.device = torch.device(device) if device is not None else None
         self._hip = None
@@ -93,5 +97,12 @@ class RouteScorer:
         else:
             scores = score_routes_ref(self.g, self.node_delays(), node_lists)
         best = int(np.argmin(scores)) if len(scores) else None
-        return {"scores": [float(x) for x in scores], "best": best, "engine": self.engine,
-                "trained": self.training is not None, "nodes_per_route": [len(n) for n in node_lists]}
+        out = {"scores": [float(x) for x in scores], "best": best, "engine": self.engine,
+               "trained": self.training is not None, "nodes_per_route": [len(n) for n in node_lists]}
+        if self.kind == "observed":
+            # predicted hidden seconds per route (the part of its time the edge costs do not know)
+            from .alternatives import candidate_scores
+            out["kind"] = "observed"
+            out["hidden_seconds"] = [float(x) for x in candidate_scores(self.g, self.node_delays(), node_lists,
+                                                                         [0.0] * len(node_lists), "observed")]
+        return out

@@ -49,3 +49,41 @@ def test_alternatives_chosen_by_scorer():
     if rt is not None:
         body["alternatives"] = 3
         assert rt.route_optimize_cpu(json.dumps(body).encode()) is None
+
+
+def test_default_scorer_is_trained_on_observed_trips():
+    c, g, sv = _app()
+    sc = sv.get_scorer()
+    assert sc.kind == "observed" and sc.training["target"] == "observed trips" and sc.training["trips"] > 1000
+    rng = np.random.default_rng(5)
+    idx = rng.integers(0, g.num_nodes, 3)
+    body = {"source_point": {"lat": float(g.lat[idx[0]]), "lon": float(g.lon[idx[0]])},
+            "destination_points": [{"lat": float(g.lat[i]), "lon": float(g.lon[i]), "payload": 1} for i in idx[1:]],
+            "driver_details": {"vehicle_type": "car", "vehicle_capacity": 9, "maximum_distance": 1e7},
+            "alternatives": 4}
+    alt = c.post("/api/optimize_route", json=body).json()["properties"]["alternatives"]
+    for leg in alt["legs"]:
+        # observed kind: score = edge-cost seconds + predicted hidden seconds (>= 0)
+        assert all(s >= t - 1e-9 for s, t in zip(leg["scores"], leg["seconds"]))
+    # the same request twice: the same via candidates and picks (per-leg hash order, no RNG state)
+    alt2 = c.post("/api/optimize_route", json=body).json()["properties"]["alternatives"]
+    assert alt2 == alt
+
+
+def test_via_nodes_and_scores_match_the_numpy_fallback(monkeypatch):
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing import alternatives as A
+    g = synth_road_graph(3000, seed=6)
+    rng = np.random.default_rng(1)
+    pairs = [tuple(map(int, rng.integers(0, g.num_nodes, 2))) for _ in range(40)]
+    native = [A.via_nodes(g, s, t, 5) for s, t in pairs]
+    delay = 0.5 + rng.random(g.num_nodes)
+    paths = [list(map(int, rng.integers(0, g.num_nodes, 6))) for _ in range(10)]
+    secs = list(rng.random(10) * 100)
+    sn = A.candidate_scores(g, delay, paths, secs, "observed")
+    se = A.candidate_scores(g, delay, paths, secs, "edge")
+    monkeypatch.setattr(A, "_rt", lambda: None)
+    assert [A.via_nodes(g, s, t, 5) for s, t in pairs] == native
+    assert sum(len(v) for v in native) > 100
+    np.testing.assert_allclose(A.candidate_scores(g, delay, paths, secs, "observed"), sn, rtol=1e-12)
+    np.testing.assert_allclose(A.candidate_scores(g, delay, paths, secs, "edge"), se, rtol=1e-12)
