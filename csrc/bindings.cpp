@@ -1395,6 +1395,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("native_server_set_fault", [](int64_t h, int64_t slot, bool on) {
     return rt::native_server_set_fault(h, (int)slot, on);
   });
+  m.def("native_server_set_scorer", [](int64_t h, std::vector<double> delay, int64_t kind, std::string engine) {
+    return rt::native_server_set_scorer(h, std::move(delay), (int)kind, engine);
+  }, "publish the GCN scorer's node delays for native \"alternatives\" requests");
   m.def("native_server_health", &native_server_health, "per-GPU-slot health, models and the model epoch");
   m.def("native_server_stop", [](int64_t h) {
     py::gil_scoped_release nogil;

@@ -1042,6 +1042,7 @@ struct Server {
   std::vector<std::unique_ptr<Reactor>> reactors;
   std::vector<std::thread> threads;
   std::vector<std::unique_ptr<RouteService>> routes;      // one per GPU
+  std::shared_ptr<AltScorerState> alt = std::make_shared<AltScorerState>();   // "alternatives" scorer
   ~Server() {
     routes.clear();                                          // joins the route workers
     for (PersistentScorer* p : sh.scorers)                   // stop + wait for the resident kernels
@@ -1142,6 +1143,7 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
     const int slot = (int)g;
     rc.eta_model = [shp, slot]() { return shp->model(slot); };
     rc.park_scorer = [shp, slot]() { shp->park(slot); };
+    rc.alt = s->alt;
     s->routes.push_back(std::make_unique<RouteService>(rc, [](RouteJob* j) {
       static_cast<JobTag*>(j->tag)->reactor->job_done(j);
     }));
@@ -1189,6 +1191,18 @@ bool native_server_set_fault(int64_t h, int slot, bool on) {
   Server* s = g_servers[h];
   if (slot < 0 || slot >= (int)s->sh.health.size()) return false;
   s->sh.health[slot]->fault = on;
+  return true;
+}
+
+// the GCN scorer's node delays for "alternatives" requests (empty: none -> the app answers them)
+bool native_server_set_scorer(int64_t h, std::vector<double> delay, int kind, const std::string& engine) {
+  std::lock_guard<std::mutex> lk(g_srv_mu);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return false;
+  Server* s = g_servers[h];
+  std::lock_guard<std::mutex> lk2(s->alt->mu);
+  s->alt->delay = delay.empty() ? nullptr : std::make_shared<const std::vector<double>>(std::move(delay));
+  s->alt->kind = kind;
+  s->alt->engine = engine;
   return true;
 }
 

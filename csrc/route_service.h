@@ -18,6 +18,22 @@ namespace rt {
 
 struct PersistentScorer;
 
+// The GCN candidate-route scorer's node delay factors for "alternatives" requests
+// (routing/alternatives.py; csrc/runtime/alternatives.h), published by the Python side once the
+// scorer is trained (NativePredictServer.set_scorer); until then such requests go to the app.
+struct AltScorerState {
+  std::mutex mu;
+  std::shared_ptr<const std::vector<double>> delay;   // [N] delay factor per graph node
+  int kind = 0;                                       // ralt::OBSERVED / EDGE
+  std::string engine = "gcn-hip";                     // RouteScorer.engine
+  std::shared_ptr<const std::vector<double>> get(int& k, std::string& e) {
+    std::lock_guard<std::mutex> lk(mu);
+    k = kind;
+    e = engine;
+    return delay;
+  }
+};
+
 struct RouteServiceCfg {
   int device = 0;
   int provider = 0;                       // 0 haversine, 1 road graph (A* or CCH)
@@ -63,6 +79,8 @@ struct RouteServiceCfg {
   // parks the GPU's resident single-request scorer (persistent_serve.hip) before each flush's
   // launches so they never queue behind it on a shared hardware queue
   std::function<void()> park_scorer;
+  // GCN scorer for "alternatives" requests (road graph + CCH only)
+  std::shared_ptr<AltScorerState> alt;
 };
 
 // One request handed from a reactor to the service and back.
@@ -82,6 +100,13 @@ struct RouteJob {
   std::vector<std::vector<std::pair<double, double>>> calls;
   std::vector<int32_t> nodes;
   int group = 0;                    // routing-context group of its flush (CCH)
+  // "alternatives": unique leg pairs in order, their via nodes, the chosen candidates (legs owned
+  // here) and the response block
+  std::vector<std::pair<int, int>> alt_pairs;
+  std::vector<std::vector<int>> alt_vias;
+  std::vector<rtr::Leg> alt_legs;
+  std::vector<std::vector<int32_t>> alt_paths;
+  std::string alt_json;
   rtr::Assembled asmb;
   float eta_min = NAN;
   std::string eta_iso, request_id;

@@ -33,6 +33,7 @@
 #include "common.h"
 #include "ops.h"
 #include "route_service.h"
+#include "runtime/alternatives.h"
 #include "runtime/sqlite_lite.h"
 
 namespace rt {
@@ -168,6 +169,10 @@ struct Batch {
   std::vector<int32_t> flat;                 // found paths, compacted (Leg::path points in here)
   std::unordered_map<uint64_t, int> leg_index;
   bool failed = false;
+  // "alternatives" jobs of the flush: the scorer snapshot they use
+  std::shared_ptr<const std::vector<double>> alt_delay;
+  int alt_kind = 0;
+  std::string alt_engine;
 };
 
 inline double now_us() {
@@ -659,16 +664,45 @@ struct RouteService::Impl {
     const int G = (int)b.metrics.size();
     std::vector<std::vector<std::pair<int, int>>> pairs(G);
     std::vector<int> order;                    // leg index -> (group, index in group) flattened
+    auto want = [&](int grp, int s, int t) {
+      if (leg_index.emplace(leg_key(grp, s, t), -1 - grp).second) pairs[grp].emplace_back(s, t);
+    };
     for (RouteJob* j : g) {
       size_t off = 0;
       for (const auto& c : j->calls) {
-        for (size_t i = 0; i + 1 < c.size(); ++i) {
-          const int s = j->nodes[off + i], t = j->nodes[off + i + 1];
-          if (leg_index.emplace(leg_key(j->group, s, t), -1 - j->group).second) pairs[j->group].emplace_back(s, t);
-        }
+        for (size_t i = 0; i + 1 < c.size(); ++i) want(j->group, j->nodes[off + i], j->nodes[off + i + 1]);
         off += c.size();
       }
     }
+    // "alternatives": every unique leg (in order) gets its via nodes; s->w and w->t join the batch
+    std::vector<RouteJob*> alt_jobs;
+    for (RouteJob* j : g)
+      if (j->req.alt_k > 0) alt_jobs.push_back(j);
+    rtc::parallel_chunks(alt_jobs.size(), 1, 16, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        RouteJob* j = alt_jobs[i];
+        j->alt_pairs.clear();
+        std::unordered_map<uint64_t, int> seen;
+        size_t off = 0;
+        for (const auto& c : j->calls) {
+          for (size_t k = 0; k + 1 < c.size(); ++k) {
+            const int s = j->nodes[off + k], t = j->nodes[off + k + 1];
+            if (seen.emplace(((uint64_t)(uint32_t)s << 32) | (uint32_t)t, 0).second) j->alt_pairs.emplace_back(s, t);
+          }
+          off += c.size();
+        }
+        j->alt_vias.assign(j->alt_pairs.size(), {});
+        for (size_t k = 0; k < j->alt_pairs.size(); ++k)
+          j->alt_vias[k] = ralt::via_nodes(cfg.glat, cfg.glon, cfg.N, j->alt_pairs[k].first, j->alt_pairs[k].second,
+                                           j->req.alt_k - 1);
+      }
+    });
+    for (RouteJob* j : alt_jobs)
+      for (size_t k = 0; k < j->alt_pairs.size(); ++k)
+        for (int w : j->alt_vias[k]) {
+          want(j->group, j->alt_pairs[k].first, w);
+          want(j->group, w, j->alt_pairs[k].second);
+        }
     int Q = 0;
     std::vector<int> goff(G + 1, 0);
     for (int gi = 0; gi < G; ++gi) goff[gi + 1] = goff[gi] + (int)pairs[gi].size();
@@ -894,6 +928,94 @@ struct RouteService::Impl {
     return true;
   }
 
+  // "alternatives": per unique leg, the candidates (time-shortest path, then s->w->t per via node
+  // when both parts were found), the scorer's values, the pick, and the response block — exactly
+  // routing/alternatives.py AlternativeLegs.choose + optimize_with_alternatives
+  void choose_alternatives(Batch& b, RouteJob* j) {
+    const std::vector<rtr::Leg>& legs = b.legs;
+    const double* delay = b.alt_delay->data();
+    const size_t P = j->alt_pairs.size();
+    struct Cand {
+      double sec, met;
+      const int32_t* p1;
+      int n1;
+      const int32_t* p2;   // second part (from its node 1 on), or nullptr
+      int n2;
+    };
+    auto leg = [&](int s, int t) -> const rtr::Leg* {
+      auto it = b.leg_index.find(leg_key(j->group, s, t));
+      return it == b.leg_index.end() || it->second < 0 ? nullptr : &legs[it->second];
+    };
+    std::vector<std::vector<Cand>> cands(P);
+    size_t total = 0;
+    for (size_t k = 0; k < P; ++k) {
+      const int s = j->alt_pairs[k].first, t = j->alt_pairs[k].second;
+      const rtr::Leg* d = leg(s, t);
+      if (d && d->len > 0) cands[k].push_back({d->sec, d->metres, d->path, d->len, nullptr, 0});
+      for (int w : j->alt_vias[k]) {
+        const rtr::Leg* a = leg(s, w);
+        const rtr::Leg* c = leg(w, t);
+        if (a && c && a->len > 0 && c->len > 0)
+          cands[k].push_back({a->sec + c->sec, a->metres + c->metres, a->path, a->len, c->path + 1, c->len - 1});
+      }
+      total += cands[k].size();
+    }
+    (void)total;
+    j->alt_legs.assign(P, rtr::Leg());
+    j->alt_paths.assign(P, {});
+    std::string o = ",\"alternatives\":{\"k\":";
+    rtr::put_int(o, j->req.alt_k);
+    o += ",\"scorer\":";
+    rtr::put_str(o, b.alt_engine);
+    o += ",\"legs\":[";
+    std::vector<int32_t> tmp;
+    for (size_t k = 0; k < P; ++k) {
+      if (k) o += ',';
+      o += "{\"from_node\":";
+      rtr::put_int(o, j->alt_pairs[k].first);
+      o += ",\"to_node\":";
+      rtr::put_int(o, j->alt_pairs[k].second);
+      o += ",\"candidates\":";
+      rtr::put_int(o, (long long)cands[k].size());
+      if (cands[k].empty()) {
+        o += '}';
+        continue;       // Leg stays "not found": the assembly reports it like a plain request
+      }
+      std::vector<double> sc(cands[k].size());
+      for (size_t c = 0; c < cands[k].size(); ++c) {
+        const Cand& x = cands[k][c];
+        tmp.assign(x.p1, x.p1 + x.n1);
+        if (x.p2) tmp.insert(tmp.end(), x.p2, x.p2 + x.n2);
+        sc[c] = ralt::candidate_score(cfg.glat, cfg.glon, delay, tmp.data(), tmp.size(), x.sec, b.alt_kind);
+      }
+      const int best = ralt::argmin_score(sc);
+      const Cand& x = cands[k][best];
+      std::vector<int32_t>& own = j->alt_paths[k];
+      own.assign(x.p1, x.p1 + x.n1);
+      if (x.p2) own.insert(own.end(), x.p2, x.p2 + x.n2);
+      rtr::Leg& L = j->alt_legs[k];
+      L.sec = x.sec;
+      L.metres = x.met;
+      L.path = own.data();
+      L.len = (int)own.size();
+      o += ",\"chosen\":";
+      rtr::put_int(o, best);
+      o += ",\"scores\":[";
+      for (size_t c = 0; c < sc.size(); ++c) {
+        if (c) o += ',';
+        rtr::put_float(o, sc[c]);
+      }
+      o += "],\"seconds\":[";
+      for (size_t c = 0; c < cands[k].size(); ++c) {
+        if (c) o += ',';
+        rtr::put_float(o, cands[k][c].sec);
+      }
+      o += "]}";
+    }
+    o += "]}";
+    j->alt_json = std::move(o);
+  }
+
   void assemble_all(Batch& b) {
     std::vector<RouteJob*>& jobs = b.jobs;
     const std::vector<rtr::Leg>& legs = b.legs;
@@ -902,6 +1024,7 @@ struct RouteService::Impl {
       for (size_t i = lo; i < hi; ++i) {
         RouteJob* j = jobs[i];
         if (j->fallback || j->status) continue;
+        if (j->req.alt_k > 0) choose_alternatives(b, j);
         std::vector<rtr::Dir> dirs(j->calls.size());
         std::string perr;
         size_t off = 0;
@@ -912,6 +1035,12 @@ struct RouteService::Impl {
             std::vector<const rtr::Leg*> lp;
             for (size_t t = 0; t + 1 < j->calls[k].size(); ++t) {
               const int s0 = j->nodes[off + t], s1 = j->nodes[off + t + 1];
+              if (j->req.alt_k > 0) {        // the pair's chosen candidate
+                size_t a = 0;
+                while (j->alt_pairs[a].first != s0 || j->alt_pairs[a].second != s1) ++a;
+                lp.push_back(&j->alt_legs[a]);
+                continue;
+              }
               const uint64_t key = cfg.cch ? leg_key(j->group, s0, s1)
                                            : (((uint64_t)(uint32_t)s0 << 32) | (uint32_t)s1);
               lp.push_back(&legs[leg_index.at(key)]);
@@ -934,6 +1063,7 @@ struct RouteService::Impl {
         }
         if (!perr.empty()) j->req.error = perr;
         if (!rtr::assemble(j->req, j->plan, dirs, cfg.engine, j->asmb)) j->fallback = true;
+        else if (j->req.alt_k > 0 && j->asmb.ok) j->asmb.body += j->alt_json;
       }
     });
   }
@@ -1009,6 +1139,15 @@ struct RouteService::Impl {
         if (j->req.fallback) j->fallback = true;
       }
     });
+    // "alternatives" need the road graph through the CCH and a published scorer; else the app
+    bool any_alt = false;
+    for (RouteJob* j : jobs) any_alt |= !j->fallback && j->req.alt_k > 0;
+    if (any_alt) {
+      if (cfg.alt && cfg.provider == 1 && cfg.cch != nullptr) b.alt_delay = cfg.alt->get(b.alt_kind, b.alt_engine);
+      const bool ok = b.alt_delay != nullptr && (int)b.alt_delay->size() == cfg.N;
+      for (RouteJob* j : jobs)
+        if (!j->fallback && j->req.alt_k > 0 && (!ok || !j->req.error.empty())) j->fallback = !ok || j->fallback;
+    }
     add_t(0, t0);
     if (cfg.park_scorer) cfg.park_scorer();
     t0 = now_us();

@@ -125,7 +125,7 @@ class PyGraphSteps {
     g.edge_name = name_.size() ? name_.data() : nullptr;
     g.names = &names_;
     rtr::Leg L;
-    L.sec = (float)sec;
+    L.sec = sec;
     L.path = path.data();
     L.len = (int)path.shape(0);
     std::vector<rtr::Step> st;
@@ -197,7 +197,7 @@ py::object route_optimize_cpu(py::bytes body, bool json_ok, const std::string& e
   const Value* rootp = parsed ? &root : (is_request_route ? nullptr : &empty);
   if (!is_request_route && parsed && root.kind != Value::Obj) rootp = &empty;   // silent: non-dict -> {}
   rtr::RouteReq r = rtr::parse_route_request(rootp);
-  if (r.fallback) return py::none();
+  if (r.fallback || r.alt_k > 0) return py::none();     // alternatives: graph provider + scorer only
   rtr::Plan plan;
   if (r.error.empty() && r.dst.size() > 1) {
     const int n1 = (int)r.dst.size() + 1;
@@ -247,9 +247,9 @@ py::object route_assemble_graph(py::bytes body, const std::string& engine,
     auto key = kv.first.cast<std::pair<int, int>>();
     py::tuple val = kv.second.cast<py::tuple>();
     auto& e = table[key];
-    e.first.sec = (float)val[0].cast<double>();
+    e.first.sec = val[0].cast<double>();
     if (val.size() == 3) {
-      e.first.metres = (float)val[1].cast<double>();
+      e.first.metres = val[1].cast<double>();
       e.second = val[2].cast<std::vector<int32_t>>();
     } else {
       e.second = val[1].cast<std::vector<int32_t>>();

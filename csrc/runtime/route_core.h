@@ -244,6 +244,8 @@ struct RouteReq {
   // routing context (routing/cch.py RouteContext.from_request): weather code, congestion 0..3 and
   // the pickup week-hour (-1: now) — read whether or not use_ml_eta is set
   int route_weather = 2, route_congestion = 0, route_weekhour = -1;
+  // "alternatives": k (app.py _route: a non-bool number >= 2) -> 2..8, else 0 (plain optimizer)
+  int alt_k = 0;
 };
 
 // _float(v, default): float(v) for numbers, default for None / missing / list / dict; strings and
@@ -270,9 +272,14 @@ inline RouteReq parse_route_request(const Value* root) {
   }
   const Value* drv = root->get("driver_details");
   if (drv && drv->truthy() && drv->kind != Value::Obj) { r.fallback = true; return r; }
-  // candidate routes ranked by the GCN scorer: answered by the Python app (routing/alternatives.py)
+  // candidate routes ranked by the GCN scorer (routing/alternatives.py): a number >= 2 asks for
+  // them (bools and strings do not: app.py _route); the route service answers them with the graph
+  // provider once the scorer is ready, else the app does
   const Value* alt = root->get("alternatives");
-  if (alt && alt->truthy()) { r.fallback = true; return r; }
+  if (alt && alt->kind == Value::Num) {
+    if (!std::isfinite(alt->num)) { r.fallback = true; return r; }
+    if (alt->num >= 2) r.alt_k = alt->num >= 8 ? 8 : (int)alt->num;
+  }
   if (drv && !drv->truthy()) drv = nullptr;
   // vehicle_type: (driver.get("vehicle_type") or "car"); str -> lower().strip()
   const Value* vt = drv ? drv->get("vehicle_type") : nullptr;
@@ -465,10 +472,10 @@ inline void haversine_directions(const std::vector<std::pair<double, double>>& c
 // One searched leg: seconds (the f32 router cost), the node path and, from the CCH router, the
 // metre length of that path (< 0: unknown -> summed from node coordinates, the A* legacy).
 struct Leg {
-  float sec = 0.f;
+  double sec = 0.0;               // (f32 search results widen exactly; alternatives sum two legs)
   const int32_t* path = nullptr;
   int len = 0;                    // 0 = not found
-  float metres = -1.f;
+  double metres = -1.0;
 };
 
 // Host view of the road graph for maneuvers: CSR, per-edge metres and seconds (the leg's routing

@@ -125,6 +125,11 @@ class ServingStack:
         sv.native = self.front
         self._hook = self._swap
         sv.eta.on_activate.append(self._hook)
+        # the GCN scorer, once trained, serves "alternatives" requests natively too
+        if self.front.routes:
+            sv.on_scorer = self.front.set_scorer
+            if getattr(sv, "scorer", None) is not None:
+                self.front.set_scorer(sv.scorer)
 
     def _swap(self, model) -> None:
         from .native_server import native_supported
@@ -136,6 +141,8 @@ class ServingStack:
         except ValueError:
             pass
         self.sv.native = None
+        if getattr(self.sv, "on_scorer", None) == self.front.set_scorer:
+            self.sv.on_scorer = None
         self.front.close()
         self.app_server.close()
 

@@ -117,6 +117,19 @@ class NativePredictServer:
     def set_fault(self, slot: int, on: bool = True) -> bool:
         return bool(self.C.native_server_set_fault(self.h, slot, on))
 
+    def set_scorer(self, scorer) -> bool:
+        """Publish the GCN scorer (routing/scorer.py RouteScorer) to the route services: requests with
+        ``"alternatives"`` are then answered natively (csrc/route_service.hip); ``None`` withdraws it."""
+        if self.h is None:
+            return False
+        if scorer is None:
+            return bool(self.C.native_server_set_scorer(self.h, [], 0, ""))
+        import numpy as np
+        from ..routing.alternatives import KINDS
+        delay = np.ascontiguousarray(scorer.node_delays(), dtype=np.float64)
+        return bool(self.C.native_server_set_scorer(self.h, delay.tolist(), KINDS[getattr(scorer, "kind", "edge")],
+                                                    str(getattr(scorer, "engine", "gcn"))))
+
     def health(self) -> Dict:
         if self.h is None:
             return {}

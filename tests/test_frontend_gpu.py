@@ -297,3 +297,44 @@ def test_graph_routes_under_request_context_byte_identical():
         assert stats["route_contexts_built"] >= 0 and stats["route_service_fallbacks"] == 0, stats
     finally:
         st.close()
+
+
+def test_alternatives_answered_natively_byte_identical():
+    """"alternatives": k (verdict r3 item 5): once the scorer (trained on observed trips) is
+    published, the native route service generates the via candidates, routes them on the CCH,
+    scores and picks exactly like routing/alternatives.py — same bytes as the app, not relayed."""
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider
+    from routest_amd.serve.eta_service import default_model
+    import torch
+    g = synth_road_graph(20_000, seed=2)
+    prov = GraphProvider(g, None, device=torch.device("cuda", 0), eta_model=default_model(hidden=64, steps=50))
+    st, sv = _stack(prov, None)
+    try:
+        sv.settings.scorer_train_steps = 60
+        sv.settings.scorer_trips = 4000
+        pays = _payloads(24, g.lat, g.lon, seed=14, max_stops=4)
+        for p in pays:
+            p["alternatives"] = 3 + (len(p["destination_points"]) % 3)
+            p["context"] = {"weather": "Stormy", "traffic": "High"}
+        # before the scorer exists the front end relays them; the app trains it and publishes it
+        r0 = st.front.stats()["relayed"]
+        first = _req(st.port, "POST", "/api/optimize_route", pays[0])
+        assert first[0] in (200, 400) and st.front.stats()["relayed"] == r0 + 1
+        assert sv.scorer is not None and sv.scorer.kind == "observed"
+        j0 = st.front.stats()["route_jobs"]
+        n_alt = 0
+        for path in ("/api/optimize_route", "/api/request_route"):
+            for p in pays:
+                a = _req(st.port, "POST", path, p)
+                b = _req(st.app_server.port, "POST", path, p)
+                assert a[0] == b[0] and a[1] == b[1], (path, a[1][:400], b[1][:400])
+                if a[0] == 200:
+                    alt = json.loads(a[1])["properties"]["alternatives"]
+                    n_alt += 1
+                    assert alt["scorer"] == "gcn-hip" and all(leg["candidates"] >= 1 for leg in alt["legs"])
+        stats = st.front.stats()
+        assert n_alt > 20 and stats["route_jobs"] - j0 == 2 * len(pays), stats
+        assert stats["relayed"] == r0 + 1 + 0 * len(pays), stats
+    finally:
+        st.close()
