@@ -528,7 +528,7 @@ class Reactor {
       c.out += h + "\r\n";
       return;
     }
-    if (path == "/api/ping" && method == "GET") {
+    if (path == "/api/ping" && method == "GET") {             // RO/Flaskr/routes.py:129-131
       respond(c, 200, "{\"ok\":true,\"service\":\"route-optimizer\"}", origin, !keep);
       return;
     }
@@ -549,12 +549,6 @@ class Reactor {
     }
     if (!cfg_.history_db.empty() && (method == "GET" || method == "DELETE") && answer_history(c, method, path, keep, origin, raw))
       return;
-    if (path == "/api/ping" && method == "GET" && cfg_.upstream_port > 0) {   // RO/Flaskr/routes.py:129-131
-      if (c.npending > 0) run_batch();
-      st_.history.fetch_add(1, std::memory_order_relaxed);
-      respond(c, 200, "{\"ok\":true,\"service\":\"route-optimizer\"}", origin, !keep);
-      return;
-    }
     const bool is_pe = path == "/api/predict_eta", is_p = path == "/predict";
     // a model family the native path does not serve (after a hot swap): the app answers
     const bool no_model = (is_pe || is_p) && method == "POST" && cfg_.sh->model(cfg_.slot) == nullptr;
