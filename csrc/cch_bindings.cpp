@@ -195,6 +195,50 @@ class PyCchGpu {
     return py::make_tuple(sec, met);
   }
 
+  // matrix() that also returns the tag of its chains (kept for legs_from_matrix until the next call)
+  py::tuple matrix_keep(int64_t key, torch::Tensor pts, torch::Tensor npts) {
+    auto sm = matrix(key, pts, npts);
+    std::lock_guard<std::mutex> lk(mu_);
+    return py::make_tuple(sm[0], sm[1], (uint64_t)sc_->chain_tag);
+  }
+
+  // legs (r, i, j) between points of the matrix_keep() call `tag` (pts as given to it): its chains
+  // are reused, so only the meet + unpack launches run -> (sec, metres, status, len, path)
+  py::tuple legs_from_matrix(int64_t key, uint64_t tag, torch::Tensor pts, torch::Tensor r, torch::Tensor i,
+                             torch::Tensor j, int64_t max_path, bool want_path) {
+    auto m = get(key);
+    for (const torch::Tensor* t : {&pts, &r, &i, &j})
+      TORCH_CHECK(t->is_cuda() && t->device().index() == dev_ && t->scalar_type() == torch::kInt32 && t->is_contiguous(),
+                  "pts / r / i / j: int32 on the router's GPU");
+    TORCH_CHECK(pts.dim() == 2 && r.numel() == i.numel() && r.numel() == j.numel(), "pts [R, NM]; r, i, j [Q]");
+    const int64_t Q = r.numel();
+    const int R = (int)pts.size(0), NM = (int)pts.size(1);
+    if (Q > 0) {
+      TORCH_CHECK(r.min().item<int>() >= 0 && r.max().item<int>() < R, "leg request index out of range");
+      TORCH_CHECK(torch::minimum(i.min(), j.min()).item<int>() >= 0 && torch::maximum(i.max(), j.max()).item<int>() < NM,
+                  "leg point index out of range");
+    }
+    auto o32 = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, dev_);
+    auto of = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, dev_);
+    auto sec = torch::empty({Q}, of), met = torch::empty({Q}, of);
+    auto st = torch::empty({Q}, o32), len = torch::zeros({Q}, o32);
+    auto path = want_path ? torch::empty({Q, max_path}, o32) : torch::empty({0, max_path}, o32);
+    rt::CchRouteOut o;
+    o.sec = sec.data_ptr<float>();
+    o.metres = met.data_ptr<float>();
+    o.status = st.data_ptr<int>();
+    o.len = len.data_ptr<int>();
+    o.path = want_path ? path.data_ptr<int>() : nullptr;
+    o.max_path = (int)max_path;
+    const c10::DeviceGuard guard(pts.device());
+    std::lock_guard<std::mutex> lk(mu_);
+    TORCH_CHECK(tag != 0 && tag == sc_->chain_tag && sc_->chain_nm == NM && sc_->chain_r == R,
+                "legs_from_matrix: the matrix chains of this tag are gone (another call ran since)");
+    CCH_CHECK_HIP(g_->legs_from_matrix(*m, pts.data_ptr<int>(), r.data_ptr<int>(), i.data_ptr<int>(), j.data_ptr<int>(),
+                                       (int)Q, tag, o, *sc_, stream_of(dev_)));
+    return py::make_tuple(sec, met, st, len, path);
+  }
+
   void set_capacity(int64_t n) { g_->set_capacity((int)n); }
   uintptr_t ptr() const { return reinterpret_cast<uintptr_t>(g_.get()); }
   py::dict topology_arrays() const {
@@ -245,6 +289,9 @@ void bind_cch_gpu(py::module& m) {
       .def("route", &PyCchGpu::route, py::arg("key"), py::arg("src"), py::arg("dst"), py::arg("max_path") = 4096,
            py::arg("want_path") = true)
       .def("matrix", &PyCchGpu::matrix, py::arg("key"), py::arg("pts"), py::arg("npts"))
+      .def("matrix_keep", &PyCchGpu::matrix_keep, py::arg("key"), py::arg("pts"), py::arg("npts"))
+      .def("legs_from_matrix", &PyCchGpu::legs_from_matrix, py::arg("key"), py::arg("tag"), py::arg("pts"), py::arg("r"),
+           py::arg("i"), py::arg("j"), py::arg("max_path") = 4096, py::arg("want_path") = true)
       .def("set_capacity", &PyCchGpu::set_capacity)
       .def("ptr", &PyCchGpu::ptr)
       .def("topology_arrays", &PyCchGpu::topology_arrays);

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <atomic>
 #include <list>
 #include <memory>
 #include <mutex>
@@ -56,6 +57,11 @@ struct CchScratch {
   int32_t* arcs = nullptr;         // [pairs_cap * max_arcs]
   int32_t* narcs = nullptr;        // [pairs_cap]
   size_t pairs_cap = 0;
+  int32_t* pj = nullptr;           // [2 * pj_cap] leg job indices (legs_from_matrix)
+  int32_t* srcnode = nullptr;      // [pj_cap]
+  size_t pj_cap = 0;
+  uint64_t chain_tag = 0;          // the matrix() call whose chains are in dist/pred/node (0: none)
+  int chain_nm = 0, chain_r = 0;
   int device = 0;
   ~CchScratch();
   hipError_t ensure(size_t jobs, size_t pairs, int stride, int max_arcs);
@@ -108,6 +114,10 @@ class CchGpu {
   // be nullptr): seconds, metres (f32; both required) and metres as f64 (the greedy kernel's matrix, K6)
   hipError_t matrix(const CchMetricDev& m, const int* d_pts, const int* d_npts, int R, int NM, float* d_sec,
                     float* d_met, double* d_D64, CchScratch& sc, hipStream_t s);
+  // legs between points of the matrix() call whose chains are still in `sc` (tag = sc.chain_tag
+  // right after it): leg q = (request r[q], point i[q] -> point j[q]); meet + unpack only, no sweeps
+  hipError_t legs_from_matrix(const CchMetricDev& m, const int* d_pts, const int* d_r, const int* d_i, const int* d_j,
+                              int Q, uint64_t tag, const CchRouteOut& o, CchScratch& sc, hipStream_t s);
   static constexpr int MAX_ARCS = 1024;   // shortcut arcs per path before unpacking
 
  private:
@@ -145,6 +155,7 @@ class CchGpu {
   std::mutex mu_;
   std::list<std::shared_ptr<CchMetricDev>> cache_;
   int capacity_ = 32;
+  std::atomic<uint64_t> tag_ctr_{0};
 };
 
 }  // namespace rt

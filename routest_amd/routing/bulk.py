@@ -95,12 +95,16 @@ class BulkRouteStep:
         self.astar = astar or BatchedAstar(g, cost, d, slots=slots, wave_slots=min(slots, ws), arena_gb=16,
                                            wave_tbits=tb)
 
-    def legs(self):
+    reuse_chains = os.environ.get("ROUTEST_BULK_REUSE_CHAINS", "1") != "0"
+
+    def legs(self, with_index: bool = False):
         """Matrices (CCH road metres, or K5 haversine) + K6 for every request, then the trip legs as
-        (src, dst) node tensors on the device."""
+        (src, dst) node tensors on the device (``with_index``: also the legs' (request, from point,
+        to point) indices and the tag of the matrix chains they can reuse)."""
         C = self.C
+        tag = 0
         if self.engine == "cch":
-            _, met = self.router.gpu.matrix(self.key, self.snap, self.npts)
+            _, met, tag = self.router.gpu.matrix_keep(self.key, self.snap, self.npts)
             D = met.double()
         else:
             D = C.route_haversine_matrix(self.lat, self.lon, self.npts, 1.3)
@@ -117,14 +121,29 @@ class BulkRouteStep:
         last = valid & ~next_same
         src = torch.cat([prev_node[valid], vnode[last]])
         dst = torch.cat([vnode[valid], depot[last]])
-        return src, dst, status
+        if not with_index:
+            return src, dst, status
+        vis = visit.clamp_min(0)
+        prev_i = torch.where(prev_same, torch.roll(vis, 1, 1), torch.zeros_like(vis))
+        rows = torch.arange(vis.shape[0], device=vis.device, dtype=vis.dtype)[:, None].expand_as(vis)
+        ri = torch.cat([rows[valid], rows[last]]).int().contiguous()
+        ii = torch.cat([prev_i[valid], vis[last]]).int().contiguous()
+        jj = torch.cat([vis[valid], torch.zeros_like(vis[last])]).int().contiguous()
+        return src, dst, status, (ri, ii, jj, tag)
 
     def step(self):
-        """One whole step; returns (legs, per-leg cost [s], per-leg status, per-request K6 status)."""
-        src, dst, status = self.legs()
+        """One whole step; returns (legs, per-leg cost [s], per-leg status, per-request K6 status).
+        CCH: the legs run between points whose chains the matrix stage already swept, so they reuse
+        them (meet + unpack only; ROUTEST_BULK_REUSE_CHAINS=0 sweeps them again)."""
         if self.engine == "cch":
-            sec, _, st, _, _ = self.router.gpu.route(self.key, src.int().contiguous(), dst.int().contiguous(),
-                                                     self.router.max_path, True)
+            src, dst, status, (ri, ii, jj, tag) = self.legs(with_index=True)
+            if self.reuse_chains:
+                sec, _, st, _, _ = self.router.gpu.legs_from_matrix(self.key, tag, self.snap, ri, ii, jj,
+                                                                    self.router.max_path, True)
+            else:
+                sec, _, st, _, _ = self.router.gpu.route(self.key, src.int().contiguous(), dst.int().contiguous(),
+                                                         self.router.max_path, True)
             return int(src.numel()), sec, st, status
+        src, dst, status = self.legs()
         c, _, st, _ = self.astar.run(src.cpu().numpy(), dst.cpu().numpy())
         return int(src.numel()), c, st, status

@@ -94,3 +94,40 @@ def test_context_customization_on_gpu(setup):
     # the GPU context costs match the CPU edge-cost model within bf16 tolerance
     from routest_amd.routing.cch import context_costs_cpu
     np.testing.assert_allclose(res[storm.key][1], context_costs_cpu(g, m, storm), rtol=2e-2, atol=0.05)
+
+
+def test_legs_from_matrix_chains_equal_fresh_legs(setup):
+    """BulkRouteStep's legs reuse the matrix stage's chains (meet + unpack only): identical seconds,
+    metres, status and paths to sweeping them again; a stale tag is refused."""
+    g, m, router, cost, key, cpu, mc = setup
+    rng = np.random.default_rng(3)
+    R, NM = 300, 7
+    pts = torch.from_numpy(rng.integers(0, g.num_nodes, (R, NM)).astype(np.int32)).cuda()
+    npts = torch.full((R,), NM, dtype=torch.int32, device="cuda")
+    _, _, tag = router.gpu.matrix_keep(key, pts, npts)
+    Q = 2000
+    r = torch.from_numpy(rng.integers(0, R, Q).astype(np.int32)).cuda()
+    i = torch.from_numpy(rng.integers(0, NM, Q).astype(np.int32)).cuda()
+    j = torch.from_numpy(rng.integers(0, NM, Q).astype(np.int32)).cuda()
+    a = router.gpu.legs_from_matrix(key, tag, pts, r, i, j, 4096, True)
+    src = pts[r.long(), i.long()].contiguous()
+    dst = pts[r.long(), j.long()].contiguous()
+    b = router.gpu.route(key, src, dst, 4096, True)
+    for x, y in zip(a[:4], b[:4]):
+        assert torch.equal(x, y)
+    ln = a[3].cpu().numpy()
+    pa, pb = a[4].cpu().numpy(), b[4].cpu().numpy()
+    assert all(np.array_equal(pa[q, :ln[q]], pb[q, :ln[q]]) for q in range(Q))
+    with pytest.raises(RuntimeError):          # route() above replaced the chains
+        router.gpu.legs_from_matrix(key, tag, pts, r, i, j, 4096, True)
+
+
+def test_bulk_route_step_reuse_matches_fresh_sweeps(setup, monkeypatch):
+    from routest_amd.routing.bulk import BulkRouteStep
+    g, m, router, cost, key, cpu, mc = setup
+    step = BulkRouteStep(g, cost, torch.device("cuda:0"), 500, router=router, key=key)
+    n1, c1, st1, k1 = step.step()
+    monkeypatch.setattr(BulkRouteStep, "reuse_chains", False)
+    n2, c2, st2, k2 = step.step()
+    assert n1 == n2 and torch.equal(c1, c2) and torch.equal(st1, st2) and torch.equal(k1, k2)
+    assert int((st1 == 0).sum()) == n1
