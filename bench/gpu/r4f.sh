@@ -3,7 +3,7 @@ ROOT=$GRAFT_REPO_ROOT
 cd $ROOT
 export TMPDIR=/tmp
 O=$ROOT/gpurun_out/r4f; mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests/test_frontend_gpu.py tests/test_gcn_observed.py -x -v --timeout 240 --timeout-method thread > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 3; }
+timeout -k 10 500 python -u -m pytest tests/test_cch_gpu.py tests/test_frontend_gpu.py tests/test_gcn_observed.py -x -v --timeout 240 --timeout-method thread > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 3; }
 tail -1 $O/pytest.log
 timeout -k 10 500 python3 bench/astar_scale.py --engine cch --nodes 1000000 --requests 2000 --radius-km 0 --steps 3 > $O/scale_1m.log 2>&1 || { tail -20 $O/scale_1m.log; exit 4; }
 tail -1 $O/scale_1m.log
