@@ -309,18 +309,50 @@ __global__ void ctx_cost_kernel(const float* __restrict__ minutes, const float* 
 //
 // The chain is walked in runs of consecutive ranks (parent(x + i) == x + i + 1: the separators), up to
 // 64 per run, whose headers (parent, record range) one coalesced load fetches; the next run's header
-// is loaded while the current run is swept.  Inside a run, node i's first 64 kept-arc records are
+// is loaded while the current run is swept.  Inside a run, node i's first 256 kept-arc records (4 per lane) are
 // loaded SWEEP_AHEAD nodes ahead, so the sequential label sweep waits on LDS, not on one global
 // load per chain node (r4c profile: the sweep was 49.6 % of the CCH GPU time at ~25 us per chain).
 constexpr int SWEEP_AHEAD = 3;
+constexpr int SWEEP_RECS = 4;          // records per lane fetched ahead per chain node (256 per node)
 
-__device__ __forceinline__ int4 sweep_fetch(const int4* __restrict__ rec, int pb, int pe, int i, int L, int lane) {
-  int4 v = make_int4(0x7F800000, 0, -1, 0);            // weight +inf: relaxes nothing
-  if (i < L) {
-    const int b = __shfl(pb, i), e = __shfl(pe, i);
-    if (b + lane < e) v = rec[b + lane];
+typedef int sweep_v4i __attribute__((ext_vector_type(4)));
+
+struct SweepRecs {
+  sweep_v4i r[SWEEP_RECS];
+};
+
+// The record prefetch is issued as inline-asm loads the compiler does not track, and each use
+// waits for its own loads with an explicit vmcnt (sweep_wait): compiler-tracked loads that stay in
+// flight across the loop's back edge made it wait for all of them at the top of every iteration.
+// Branch-free: lanes past the node's records load record 0 (always allocated) and are masked where
+// the records are used, so every fetch issues exactly SWEEP_RECS loads.
+__device__ __forceinline__ SweepRecs sweep_fetch(const int4* __restrict__ rec, int pb, int pe, int i, int L, int lane) {
+  SweepRecs v;
+  const int ii = i < 63 ? i : 63;
+  const int b = __shfl(pb, ii);
+  const int e = i < L ? __shfl(pe, ii) : b;
+#pragma unroll
+  for (int k = 0; k < SWEEP_RECS; ++k) {
+    const int idx = b + lane + 64 * k;
+    const int4* p = rec + (idx < e ? idx : 0);
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v.r[k]) : "v"(p));
   }
   return v;
+}
+
+// wait until the loads of the fetch issued `newer` fetches before the current one have landed
+template <int NEWER>
+__device__ __forceinline__ void sweep_wait(SweepRecs& q) {
+  static_assert(NEWER * SWEEP_RECS <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(q.r[0]), "+v"(q.r[1]), "+v"(q.r[2]), "+v"(q.r[3]) : "n"(NEWER * SWEEP_RECS));
+}
+
+__device__ __forceinline__ void sweep_relax(float* sd, int32_t* sp, float dx, int w, int hd, int arc) {
+  const float nd = dx + __int_as_float(w);
+  if (nd < sd[hd]) {
+    sd[hd] = nd;
+    sp[hd] = arc;
+  }
 }
 
 __global__ __launch_bounds__(64) void sweep_kernel(const int32_t* __restrict__ jobs, int J,
@@ -368,36 +400,43 @@ __global__ __launch_bounds__(64) void sweep_kernel(const int32_t* __restrict__ j
     const int npar = nin ? parent[ncand] : -2;
     const int npb = nin ? ptr[ncand] : 0;
     const int npe = nin ? ptr[ncand + 1] : 0;
-    int4 q0 = sweep_fetch(rec, pb, pe, 0, L, lane);
-    int4 q1 = sweep_fetch(rec, pb, pe, 1, L, lane);
-    int4 q2 = sweep_fetch(rec, pb, pe, 2, L, lane);
-    for (int i = 0; i < L; ++i) {
-      const int4 qn = sweep_fetch(rec, pb, pe, i + SWEEP_AHEAD, L, lane);
-      const int di = d - i;
-      const float dx = sd[di];
+    // each node's records were requested three nodes earlier; named buffers, unrolled by four
+    auto node = [&](int i, const SweepRecs& q) {
+      if (i >= L) return;
+      const float dx = sd[d - i];
       if (dx < F_INF) {
-        {
-          const float nd = dx + __int_as_float(q0.x);
-          if (nd < sd[q0.y]) {
-            sd[q0.y] = nd;
-            sp[q0.y] = q0.z;
-          }
-        }
+        // a node's kept arcs have distinct heads: the lanes' updates never collide
         const int b = __shfl(pb, i), e = __shfl(pe, i);
-        for (int k = b + 64 + lane; k < e; k += 64) {      // nodes with more than 64 kept arcs
+#pragma unroll
+        for (int k = 0; k < SWEEP_RECS; ++k)
+          if (b + lane + 64 * k < e) sweep_relax(sd, sp, dx, q.r[k].x, q.r[k].y, q.r[k].z);
+        for (int k = b + 64 * SWEEP_RECS + lane; k < e; k += 64) {     // nodes with > 256 kept arcs
           const int4 rc = rec[k];
-          const float nd = dx + __int_as_float(rc.x);
-          if (nd < sd[rc.y]) {
-            sd[rc.y] = nd;
-            sp[rc.y] = rc.z;
-          }
+          sweep_relax(sd, sp, dx, rc.x, rc.y, rc.z);
         }
         __syncthreads();
       }
-      q0 = q1;
-      q1 = q2;
-      q2 = qn;
+    };
+    SweepRecs qa = sweep_fetch(rec, pb, pe, 0, L, lane);
+    SweepRecs qb = sweep_fetch(rec, pb, pe, 1, L, lane);
+    SweepRecs qc = sweep_fetch(rec, pb, pe, 2, L, lane);
+    for (int i = 0; i < L; i += 4) {
+      SweepRecs qd = sweep_fetch(rec, pb, pe, i + 3, L, lane);
+      sweep_wait<3>(qa);
+      node(i, qa);
+      qa = sweep_fetch(rec, pb, pe, i + 4, L, lane);
+      sweep_wait<3>(qb);
+      node(i + 1, qb);
+      qb = sweep_fetch(rec, pb, pe, i + 5, L, lane);
+      sweep_wait<3>(qc);
+      node(i + 2, qc);
+      qc = sweep_fetch(rec, pb, pe, i + 6, L, lane);
+      sweep_wait<3>(qd);
+      node(i + 3, qd);
     }
+    sweep_wait<0>(qa);          // drain the prefetch past the run's end before the buffers are reused
+    sweep_wait<0>(qb);
+    sweep_wait<0>(qc);
     x = next;
     d -= L;
     cand = ncand;
