@@ -600,10 +600,10 @@ __global__ void route_jobs_kernel(const int* __restrict__ src, const int* __rest
   jobs[2 * q + 1] = (rank[t] << 1) | 1;
 }
 
-// legs from a matrix call's chains: job indices of (r, i) forward and (r, j) backward, source node
-__global__ void leg_pairs_kernel(const int* __restrict__ pts, int NM, const int* __restrict__ r,
-                                 const int* __restrict__ i, const int* __restrict__ j, int Q, int R,
-                                 int32_t* __restrict__ pjf, int32_t* __restrict__ pjb, int* __restrict__ srcnode) {
+// legs from a matrix call's chains: job indices of (r, i) forward and (r, j) backward
+__global__ void leg_pairs_kernel(int NM, const int* __restrict__ r, const int* __restrict__ i,
+                                 const int* __restrict__ j, int Q, int R, int32_t* __restrict__ pjf,
+                                 int32_t* __restrict__ pjb) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= Q) return;
   int rr = r[q], ii = i[q], jj = j[q];
@@ -612,7 +612,6 @@ __global__ void leg_pairs_kernel(const int* __restrict__ pts, int NM, const int*
   jj = jj < 0 ? 0 : (jj >= NM ? NM - 1 : jj);
   pjf[q] = 2 * (rr * NM + ii);
   pjb[q] = 2 * (rr * NM + jj) + 1;
-  srcnode[q] = pts[(long long)rr * NM + ii];
 }
 
 // matrix: jobs [R][NM][2] (forward, backward per point); pairs (r, i, j) for i != j
@@ -709,7 +708,6 @@ CchScratch::~CchScratch() {
   dfree(arcs);
   dfree(narcs);
   dfree(pj);
-  dfree(srcnode);
   (void)hipSetDevice(cur);
 }
 
@@ -1089,7 +1087,7 @@ hipError_t CchGpu::matrix(const CchMetricDev& m, const int* d_pts, const int* d_
   return e;
 }
 
-hipError_t CchGpu::legs_from_matrix(const CchMetricDev& m, const int* d_pts, const int* d_r, const int* d_i,
+hipError_t CchGpu::legs_from_matrix(const CchMetricDev& m, const int* d_src, const int* d_r, const int* d_i,
                                     const int* d_j, int Q, uint64_t tag, const CchRouteOut& o, CchScratch& sc,
                                     hipStream_t s) {
   if (Q <= 0) return hipSuccess;
@@ -1099,23 +1097,21 @@ hipError_t CchGpu::legs_from_matrix(const CchMetricDev& m, const int* d_pts, con
   if (e != hipSuccess) return e;
   if ((size_t)Q > sc.pj_cap) {
     dfree(sc.pj);
-    dfree(sc.srcnode);
     const size_t cap = std::max((size_t)Q, sc.pj_cap * 3 / 2);
     if ((e = dmalloc(sc.pj, 2 * cap)) != hipSuccess) return e;
-    if ((e = dmalloc(sc.srcnode, cap)) != hipSuccess) return e;
     sc.pj_cap = cap;
   }
   int32_t* pjf = sc.pj;
   int32_t* pjb = sc.pj + sc.pj_cap;
-  hipLaunchKernelGGL(leg_pairs_kernel, dim3(blocks_for(Q, 256)), dim3(256), 0, s, d_pts, sc.chain_nm, d_r, d_i, d_j, Q,
-                     sc.chain_r, pjf, pjb, sc.srcnode);
+  hipLaunchKernelGGL(leg_pairs_kernel, dim3(blocks_for(Q, 256)), dim3(256), 0, s, sc.chain_nm, d_r, d_i, d_j, Q,
+                     sc.chain_r, pjf, pjb);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(meet_kernel, dim3(Q), dim3(64), 0, s, Q, pjf, pjb, 0, 0, sc.jobs, S, sc.dist, sc.pred, sc.node,
                      d_depth, d_arc_lo, m.len_up, m.len_dn, o.sec, o.metres, o.status, o.path ? sc.arcs : nullptr,
                      o.path ? sc.narcs : nullptr, MAX_ARCS);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (o.path != nullptr) {
-    hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(Q, 64)), dim3(64), 0, s, Q, sc.srcnode, sc.arcs, sc.narcs,
+    hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(Q, 64)), dim3(64), 0, s, Q, d_src, sc.arcs, sc.narcs,
                        MAX_ARCS, m.sub_up, m.sub_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path, o.max_path);
     e = hipGetLastError();
   }

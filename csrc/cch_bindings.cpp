@@ -231,10 +231,11 @@ class PyCchGpu {
     o.path = want_path ? path.data_ptr<int>() : nullptr;
     o.max_path = (int)max_path;
     const c10::DeviceGuard guard(pts.device());
+    auto src = Q > 0 ? pts.index({r.to(torch::kLong), i.to(torch::kLong)}).contiguous() : torch::empty({0}, o32);
     std::lock_guard<std::mutex> lk(mu_);
     TORCH_CHECK(tag != 0 && tag == sc_->chain_tag && sc_->chain_nm == NM && sc_->chain_r == R,
                 "legs_from_matrix: the matrix chains of this tag are gone (another call ran since)");
-    CCH_CHECK_HIP(g_->legs_from_matrix(*m, pts.data_ptr<int>(), r.data_ptr<int>(), i.data_ptr<int>(), j.data_ptr<int>(),
+    CCH_CHECK_HIP(g_->legs_from_matrix(*m, src.data_ptr<int>(), r.data_ptr<int>(), i.data_ptr<int>(), j.data_ptr<int>(),
                                        (int)Q, tag, o, *sc_, stream_of(dev_)));
     return py::make_tuple(sec, met, st, len, path);
   }

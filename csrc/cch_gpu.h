@@ -58,7 +58,6 @@ struct CchScratch {
   int32_t* narcs = nullptr;        // [pairs_cap]
   size_t pairs_cap = 0;
   int32_t* pj = nullptr;           // [2 * pj_cap] leg job indices (legs_from_matrix)
-  int32_t* srcnode = nullptr;      // [pj_cap]
   size_t pj_cap = 0;
   uint64_t chain_tag = 0;          // the matrix() call whose chains are in dist/pred/node (0: none)
   int chain_nm = 0, chain_r = 0;
@@ -115,8 +114,9 @@ class CchGpu {
   hipError_t matrix(const CchMetricDev& m, const int* d_pts, const int* d_npts, int R, int NM, float* d_sec,
                     float* d_met, double* d_D64, CchScratch& sc, hipStream_t s);
   // legs between points of the matrix() call whose chains are still in `sc` (tag = sc.chain_tag
-  // right after it): leg q = (request r[q], point i[q] -> point j[q]); meet + unpack only, no sweeps
-  hipError_t legs_from_matrix(const CchMetricDev& m, const int* d_pts, const int* d_r, const int* d_i, const int* d_j,
+  // right after it): leg q = (request r[q], point i[q] -> point j[q]) starting at node d_src[q];
+  // meet + unpack only, no sweeps
+  hipError_t legs_from_matrix(const CchMetricDev& m, const int* d_src, const int* d_r, const int* d_i, const int* d_j,
                               int Q, uint64_t tag, const CchRouteOut& o, CchScratch& sc, hipStream_t s);
   static constexpr int MAX_ARCS = 1024;   // shortcut arcs per path before unpacking
 

@@ -1238,13 +1238,13 @@ void native_server_stop(int64_t h) {
 
 std::vector<long long> native_server_stats(int64_t h) {
   std::lock_guard<std::mutex> lk(g_srv_mu);
-  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(30, 0);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(31, 0);
   Server* s = g_servers[h];
   std::vector<long long> v = {s->stats.requests.load(), s->stats.predictions.load(), s->stats.launches.load(),
                               s->stats.errors.load(), s->stats.resident.load(), s->stats.fallbacks.load(),
                               s->stats.wire8.load(), s->stats.route_requests.load(),
                               s->stats.route_fallbacks.load(), s->stats.relayed.load()};
-  std::vector<long long> rs(17, 0);
+  std::vector<long long> rs(18, 0);
   for (auto& r : s->routes) {
     const auto x = r->stats();
     for (size_t i = 0; i < rs.size() && i < x.size(); ++i) rs[i] += x[i];

@@ -18,6 +18,7 @@
 //      database file the Python store reads (reference routes.py:119-125, best effort);
 //   7. completed jobs go back to their reactors (eventfd wake-up), which write the bytes.
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -195,6 +196,7 @@ struct RouteService::Impl {
   std::deque<Batch*> aq;
   bool gpu_done = false;
   // statistics
+  std::atomic<long long> n_legs_reused{0};
   std::atomic<long long> n_jobs{0}, n_flushes{0}, n_fallback{0}, n_legs{0}, n_host_legs{0}, n_persisted{0},
       n_escalated{0};
   // stage times (us): parse, trips (K5+K6), snap, A*, copy-out, assembly, ETA, persistence
@@ -214,6 +216,13 @@ struct RouteService::Impl {
   DevBuf<long long> d_off;
   // CCH
   CchScratch csc;
+  // per context group: the matrix stage's chains (kept for the group's multi-stop legs), the tag of
+  // its matrix call, and each multi-stop job's row in it
+  std::vector<std::unique_ptr<CchScratch>> gsc;
+  std::vector<uint64_t> gtag;
+  std::unordered_map<const RouteJob*, int> jrow;
+  HostBuf<int> h_lr, h_li, h_lj;
+  DevBuf<int> d_lr, d_li, d_lj;
   HostBuf<int> h_pts, h_npts2;
   HostBuf<float> h_met;
   DevBuf<int> d_pts, d_npts2;
@@ -551,6 +560,9 @@ struct RouteService::Impl {
     std::vector<RouteJob*> all;
     for (RouteJob* j : b.jobs)
       if (!j->fallback && j->req.error.empty() && j->req.dst.size() > 1) all.push_back(j);
+    jrow.clear();
+    gtag.assign(b.metrics.size(), 0);
+    while (gsc.size() < b.metrics.size()) gsc.push_back(std::make_unique<CchScratch>());
     if (all.empty()) return true;
     for (size_t g = 0; g < b.metrics.size(); ++g) {
       std::vector<RouteJob*> m;
@@ -599,7 +611,9 @@ struct RouteService::Impl {
       cp(d_cap.d, h_cap.h, (size_t)R * 8);
       cp(d_maxd.d, h_maxd.h, (size_t)R * 8);
       if (e == hipSuccess)
-        e = cfg.cch->matrix(*b.metrics[g], d_pts.d, d_npts2.d, R, NM, d_msec.d, d_mmet.d, d_D.d, csc, stream);
+        e = cfg.cch->matrix(*b.metrics[g], d_pts.d, d_npts2.d, R, NM, d_msec.d, d_mmet.d, d_D.d, *gsc[g], stream);
+      gtag[g] = e == hipSuccess ? gsc[g]->chain_tag : 0;
+      for (int k = 0; k < R; ++k) jrow[m[k]] = k;
       if (e == hipSuccess)
         e = launch_greedy_cvrp(d_D.d, d_npts2.d, d_dem.d, d_cap.d, d_maxd.d, R, NM, d_visit.d, d_trip.d, d_ntrips.d,
                                d_status.d, stream);
@@ -664,13 +678,33 @@ struct RouteService::Impl {
     const int G = (int)b.metrics.size();
     std::vector<std::vector<std::pair<int, int>>> pairs(G);
     std::vector<int> order;                    // leg index -> (group, index in group) flattened
-    auto want = [&](int grp, int s, int t) {
-      if (leg_index.emplace(leg_key(grp, s, t), -1 - grp).second) pairs[grp].emplace_back(s, t);
+    // legs of a multi-stop job run between points of its group's matrix: their chains are reused
+    // (meet + unpack only); every other leg (point-to-point jobs, alternatives' via legs) is routed
+    std::vector<std::vector<std::array<int, 3>>> tri(G);      // (row, i, j) of each matrix-derived pair
+    std::vector<std::vector<std::pair<int, int>>> rest(G);
+    auto want = [&](int grp, int s, int t, int row, int i, int jj) {
+      if (!leg_index.emplace(leg_key(grp, s, t), -1 - grp).second) return;
+      if (row >= 0) {
+        pairs[grp].emplace_back(s, t);
+        tri[grp].push_back({row, i, jj});
+      } else {
+        rest[grp].emplace_back(s, t);
+      }
     };
     for (RouteJob* j : g) {
+      int row = -1;
+      if (gtag.size() > (size_t)j->group && gtag[j->group] != 0 && !j->plan.trips.empty()) {
+        auto it = jrow.find(j);
+        if (it != jrow.end()) row = it->second;
+      }
       size_t off = 0;
-      for (const auto& c : j->calls) {
-        for (size_t i = 0; i + 1 < c.size(); ++i) want(j->group, j->nodes[off + i], j->nodes[off + i + 1]);
+      for (size_t ci = 0; ci < j->calls.size(); ++ci) {
+        const auto& c = j->calls[ci];
+        // call ci of a multi-stop job is trip ci: its points are the trip's point indices
+        const bool from_trip = row >= 0 && ci < j->plan.trips.size() && j->plan.trips[ci].size() == c.size();
+        for (size_t i = 0; i + 1 < c.size(); ++i)
+          want(j->group, j->nodes[off + i], j->nodes[off + i + 1], from_trip ? row : -1,
+               from_trip ? j->plan.trips[ci][i] : 0, from_trip ? j->plan.trips[ci][i + 1] : 0);
         off += c.size();
       }
     }
@@ -700,9 +734,14 @@ struct RouteService::Impl {
     for (RouteJob* j : alt_jobs)
       for (size_t k = 0; k < j->alt_pairs.size(); ++k)
         for (int w : j->alt_vias[k]) {
-          want(j->group, j->alt_pairs[k].first, w);
-          want(j->group, w, j->alt_pairs[k].second);
+          want(j->group, j->alt_pairs[k].first, w, -1, 0, 0);
+          want(j->group, w, j->alt_pairs[k].second, -1, 0, 0);
         }
+    std::vector<int> nA(G);
+    for (int gi = 0; gi < G; ++gi) {
+      nA[gi] = (int)pairs[gi].size();
+      pairs[gi].insert(pairs[gi].end(), rest[gi].begin(), rest[gi].end());
+    }
     int Q = 0;
     std::vector<int> goff(G + 1, 0);
     for (int gi = 0; gi < G; ++gi) goff[gi + 1] = goff[gi] + (int)pairs[gi].size();
@@ -725,17 +764,41 @@ struct RouteService::Impl {
       }
     hipError_t e = hipMemcpyAsync(d_src.d, h_src.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(d_dst.d, h_dst.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
-    for (int gi = 0; gi < G && e == hipSuccess; ++gi) {
+    int QA = 0;
+    for (int gi = 0; gi < G; ++gi) QA += nA[gi];
+    if (QA > 0) {
+      if (h_lr.need(QA) || h_li.need(QA) || h_lj.need(QA) || d_lr.need(QA) || d_li.need(QA) || d_lj.need(QA)) return false;
+      int a = 0;
+      for (int gi = 0; gi < G; ++gi)
+        for (int k = 0; k < nA[gi]; ++k, ++a) {
+          h_lr.h[a] = tri[gi][k][0];
+          h_li.h[a] = tri[gi][k][1];
+          h_lj.h[a] = tri[gi][k][2];
+        }
+      if (e == hipSuccess) e = hipMemcpyAsync(d_lr.d, h_lr.h, (size_t)QA * 4, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = hipMemcpyAsync(d_li.d, h_li.h, (size_t)QA * 4, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = hipMemcpyAsync(d_lj.d, h_lj.h, (size_t)QA * 4, hipMemcpyHostToDevice, stream);
+    }
+    for (int gi = 0, a0 = 0; gi < G && e == hipSuccess; a0 += nA[gi], ++gi) {
       const int q0 = goff[gi], n = goff[gi + 1] - goff[gi];
       if (n == 0) continue;
-      CchRouteOut o;
-      o.sec = d_cost.d + q0;
-      o.metres = d_met.d + q0;
-      o.status = d_st.d + q0;
-      o.len = d_len.d + q0;
-      o.path = d_path.d + (size_t)q0 * MP;
-      o.max_path = MP;
-      e = cfg.cch->route(*b.metrics[gi], d_src.d + q0, d_dst.d + q0, n, o, csc, stream);
+      auto out_at = [&](int q) {
+        CchRouteOut o;
+        o.sec = d_cost.d + q;
+        o.metres = d_met.d + q;
+        o.status = d_st.d + q;
+        o.len = d_len.d + q;
+        o.path = d_path.d + (size_t)q * MP;
+        o.max_path = MP;
+        return o;
+      };
+      if (nA[gi] > 0)
+        e = cfg.cch->legs_from_matrix(*b.metrics[gi], d_src.d + q0, d_lr.d + a0, d_li.d + a0, d_lj.d + a0, nA[gi],
+                                      gtag[gi], out_at(q0), *gsc[gi], stream);
+      if (e == hipSuccess && n > nA[gi])
+        e = cfg.cch->route(*b.metrics[gi], d_src.d + q0 + nA[gi], d_dst.d + q0 + nA[gi], n - nA[gi], out_at(q0 + nA[gi]),
+                           csc, stream);
+      n_legs_reused.fetch_add(nA[gi], std::memory_order_relaxed);
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h_len.h, d_len.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
@@ -1257,6 +1320,7 @@ std::vector<long long> RouteService::stats() const {
   v.push_back(p_->n_escalated.load());     // A* searches rerun in the big tier
   v.push_back(p_->n_ctx_built.load());     // routing contexts customized by this service (CCH)
   v.push_back(p_->t_ctx_us.load());        // ... and their cost + customization time (us)
+  v.push_back(p_->n_legs_reused.load());   // legs that reused their matrix chains (meet + unpack only)
   return v;
 }
 

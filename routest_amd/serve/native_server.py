@@ -161,6 +161,8 @@ class NativePredictServer:
                  "route_astar_escalated",
                  # CCH: routing contexts customized by the services, and their total build time (us)
                  "route_contexts_built", "route_us_context",
+                 # multi-stop legs that reused their matrix chains (no second sweep)
+                 "route_legs_reused",
                  # rounds re-run on another GPU slot (failover) / on the CPU forward (no GPU left)
                  "failovers", "cpu_rounds",
                  # history / locations requests answered from the store's database natively
