@@ -414,8 +414,10 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         if alt and not isinstance(alt, bool) and isinstance(alt, (int, float)) and alt >= 2:
             from ..routing.alternatives import optimize_with_alternatives
             scorer = await run_in_threadpool(sv.get_scorer)
+            # road providers route the candidates themselves (provider.legs); others need a search
+            search = None if hasattr(sv.provider, "legs") else sv.graph_search()
             return await run_in_threadpool(optimize_with_alternatives, payload, sv.provider, scorer,
-                                           sv.graph_search(), s.engine_name, int(alt))
+                                           search, s.engine_name, int(alt))
         return await _optimize_one(payload)
 
     @app.post("/api/request_route")
