@@ -130,6 +130,7 @@ __global__ __launch_bounds__(256) void basic_level_kernel(LevelArgs L, unsigned 
                                                           unsigned long long* __restrict__ dn,
                                                           int32_t* __restrict__ sub_up, int32_t* __restrict__ sub_dn,
                                                           float* __restrict__ len_up, float* __restrict__ len_dn,
+                                                          int32_t* __restrict__ cnt_up, int32_t* __restrict__ cnt_dn,
                                                           const float* __restrict__ length) {
   const long long gi = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (gi >= L.items) return;
@@ -148,10 +149,12 @@ __global__ __launch_bounds__(256) void basic_level_kernel(LevelArgs L, unsigned 
       const unsigned long long w = dir ? dn[a] : up[a];
       int32_t* sub = (dir ? sub_dn : sub_up) + 2 * (long long)a;
       float* len = dir ? len_dn : len_up;
+      int32_t* cnt = dir ? cnt_dn : cnt_up;
       if (!(wof(w) < F_INF)) {
         sub[0] = -1;
         sub[1] = -1;
         len[a] = F_INF;
+        cnt[a] = 0;
         continue;
       }
       const uint32_t pl = (uint32_t)w;
@@ -160,6 +163,7 @@ __global__ __launch_bounds__(256) void basic_level_kernel(LevelArgs L, unsigned 
         sub[0] = -1;
         sub[1] = e;
         len[a] = length[e];
+        cnt[a] = 1;
         continue;
       }
       const int zz = (int)pl;
@@ -168,6 +172,7 @@ __global__ __launch_bounds__(256) void basic_level_kernel(LevelArgs L, unsigned 
       sub[0] = s0;
       sub[1] = s1;
       len[a] = len_dn[s0] + len_up[s1];
+      cnt[a] = cnt_dn[s0] + cnt_up[s1];     // road edges the arc stands for (cooperative unpack)
     }
     return;
   }
@@ -547,15 +552,17 @@ __global__ __launch_bounds__(64) void unpack_kernel(int P, const int* __restrict
                                                     const int32_t* __restrict__ arc_lo,
                                                     const int32_t* __restrict__ up_head,
                                                     const int32_t* __restrict__ node_of, int* __restrict__ status,
-                                                    int* __restrict__ out_len, int* __restrict__ out_path, int max_path) {
+                                                    int* __restrict__ out_len, int* __restrict__ out_path, int max_path,
+                                                    int min_arcs) {
   __shared__ int32_t stk[64 * UNPACK_STACK];
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= P) return;
   int32_t* st = stk + threadIdx.x * UNPACK_STACK;
   if (status[q] != 0) {
-    out_len[q] = 0;
+    if (min_arcs < 0) out_len[q] = 0;
     return;
   }
+  if (narcs[q] <= min_arcs) return;          // unpacked by unpack_coop_kernel
   int* out = out_path + (size_t)q * max_path;
   int n = 0;
   out[n++] = src_node[q];
@@ -586,6 +593,128 @@ __global__ __launch_bounds__(64) void unpack_kernel(int P, const int* __restrict
     return;
   }
   out_len[q] = n;
+}
+
+// Cooperative unpack: UNPACK_LANES lanes per pair share its path.  The arcs' road-edge counts
+// (cnt_*, from the customization) give each shortcut arc its offset in the path, every lane takes a
+// contiguous range of road edges, descends the shortcut tree once to its first edge (counts pick the
+// branch), then walks the DFS for the rest of its range — ~depth + edges/UNPACK_LANES dependent
+// loads per lane instead of one lane walking the whole path (the serial unpack's time was the
+// longest path's DFS).  Pairs with more than UNPACK_MAX_ARCS shortcut arcs take the serial kernel.
+constexpr int UNPACK_LANES = 16;
+constexpr int UNPACK_MAX_ARCS = 256;
+constexpr int UNPACK_SD = 64;                 // per-lane DFS stack (pending second sub-arcs)
+__global__ __launch_bounds__(64) void unpack_coop_kernel(int P, const int* __restrict__ src_node,
+                                                         const int32_t* __restrict__ arcs,
+                                                         const int32_t* __restrict__ narcs, int max_arcs,
+                                                         const int32_t* __restrict__ sub_up,
+                                                         const int32_t* __restrict__ sub_dn,
+                                                         const int32_t* __restrict__ cnt_up,
+                                                         const int32_t* __restrict__ cnt_dn,
+                                                         const int32_t* __restrict__ arc_lo,
+                                                         const int32_t* __restrict__ up_head,
+                                                         const int32_t* __restrict__ node_of, int* __restrict__ status,
+                                                         int* __restrict__ out_len, int* __restrict__ out_path,
+                                                         int max_path) {
+  constexpr int G = 64 / UNPACK_LANES;
+  __shared__ int32_t offs[G][UNPACK_MAX_ARCS + 1];
+  __shared__ int32_t stk[64 * UNPACK_SD];
+  const int lane = threadIdx.x, g = lane / UNPACK_LANES, sl = lane % UNPACK_LANES;
+  const int q = blockIdx.x * G + g;
+  const bool active = q < P;
+  int st = active ? status[q] : 1;
+  const int na = active && st == 0 ? narcs[q] : 0;
+  const bool coop = active && st == 0 && na <= UNPACK_MAX_ARCS;   // longer arc lists: the serial kernel
+  if (active && st != 0 && sl == 0) out_len[q] = 0;
+  // exclusive prefix of the arcs' edge counts, UNPACK_LANES at a time
+  const int32_t* al = arcs + (size_t)(active ? q : 0) * max_arcs;
+  int carry = 0;
+  for (int b = 0; b < (coop ? na : 0); b += UNPACK_LANES) {
+    const int k = b + sl;
+    int c = 0;
+    if (k < na) {
+      const int code = al[k];
+      c = (code & 1) ? cnt_dn[code >> 1] : cnt_up[code >> 1];
+    }
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < UNPACK_LANES; o <<= 1) {
+      const int y = __shfl_up(incl, o, UNPACK_LANES);
+      if (sl >= o) incl += y;
+    }
+    if (k < na) offs[g][k] = carry + incl - c;
+    carry += __shfl(incl, UNPACK_LANES - 1, UNPACK_LANES);
+  }
+  const int E = carry;                       // road edges of the path (uniform in the group)
+  if (coop) {
+    if (sl == 0) offs[g][na] = E;
+    if (E + 1 > max_path) {
+      if (sl == 0) {
+        status[q] = 4;
+        out_len[q] = 0;
+      }
+      st = 4;
+    } else if (sl == 0) {
+      out_len[q] = E + 1;
+    }
+  }
+  __syncthreads();
+  if (!coop || st != 0) return;
+  int* out = out_path + (size_t)q * max_path;
+  if (sl == 0) out[0] = src_node[q];
+  const int per = (E + UNPACK_LANES - 1) / UNPACK_LANES;
+  int e = sl * per;
+  const int e1 = min(E, e + per);
+  if (e >= e1) return;
+  int32_t* sk = stk + lane * UNPACK_SD;
+  // the arc holding edge e
+  int lo = 0, hi = na - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (offs[g][mid] <= e) lo = mid;
+    else hi = mid - 1;
+  }
+  int k = lo;
+  int r = e - offs[g][k];                  // edge index inside arc k
+  int sp = 0;
+  bool ok = true;
+  int code = al[k];
+  // descend to the r-th edge of `code`, keeping the pending second halves
+  auto descend = [&](int c, int rr) -> int {
+    while (true) {
+      const int a = c >> 1, dn = c & 1;
+      const int32_t* sub = (dn ? sub_dn : sub_up) + 2 * (long long)a;
+      const int s0 = sub[0];
+      if (s0 < 0) return c;                  // an original edge
+      const int s1 = sub[1];
+      const int first = (s0 << 1) | 1, second = s1 << 1;     // first traversed down, second up
+      const int c0 = cnt_dn[s0];
+      if (rr < c0) {
+        if (sp >= UNPACK_SD) { ok = false; return c; }
+        sk[sp++] = second;
+        c = first;
+      } else {
+        rr -= c0;
+        c = second;
+      }
+    }
+  };
+  int leaf = descend(code, r);
+  while (ok) {
+    const int a = leaf >> 1, dn = leaf & 1;
+    out[e + 1] = node_of[dn ? arc_lo[a] : up_head[a]];
+    if (++e >= e1) break;
+    if (sp > 0) {
+      leaf = descend(sk[--sp], 0);
+    } else {
+      ++k;                                   // next shortcut arc of the path
+      leaf = descend(al[k], 0);
+    }
+  }
+  if (!ok) {                                 // stack overflow: the exact host fallback takes the leg
+    status[q] = 4;
+    out_len[q] = 0;
+  }
 }
 
 // (node ids are range-checked by the callers; out-of-range ids are clamped, never dereferenced)
@@ -690,6 +819,8 @@ CchMetricDev::~CchMetricDev() {
   dfree(sub_dn);
   dfree(len_up);
   dfree(len_dn);
+  dfree(cnt_up);
+  dfree(cnt_dn);
   dfree(f_ptr);
   dfree(b_ptr);
   dfree(f_rec);
@@ -898,6 +1029,8 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     ck(dmalloc(m.sub_dn, 2 * M));
     ck(dmalloc(m.len_up, M));
     ck(dmalloc(m.len_dn, M));
+    ck(dmalloc(m.cnt_up, M));
+    ck(dmalloc(m.cnt_dn, M));
     ck(dmalloc(m.f_ptr, N + 1));
     ck(dmalloc(m.b_ptr, N + 1));
   }
@@ -917,7 +1050,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     L.items = bofs_[L.hi] - bofs_[L.lo];
     if (L.items <= 0) continue;
     hipLaunchKernelGGL(basic_level_kernel, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
-                       m.sub_up, m.sub_dn, m.len_up, m.len_dn, d_length);
+                       m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
     ck(hipGetLastError());
   }
   // perfect, top-down by depth
@@ -1029,6 +1162,26 @@ hipError_t CchGpu::metric_for(const CchContext& c, hipStream_t s, std::shared_pt
   return hipSuccess;
 }
 
+hipError_t CchGpu::launch_unpack(const CchMetricDev& m, int Q, const int* d_src, CchScratch& sc, const CchRouteOut& o,
+                                 hipStream_t s) {
+  static const bool serial_only = [] {
+    const char* v = std::getenv("ROUTEST_CCH_UNPACK");
+    return v && std::string(v) == "serial";
+  }();
+  if (!serial_only) {
+    constexpr int G = 64 / UNPACK_LANES;
+    hipLaunchKernelGGL(unpack_coop_kernel, dim3((Q + G - 1) / G), dim3(64), 0, s, Q, d_src, sc.arcs, sc.narcs, MAX_ARCS,
+                       m.sub_up, m.sub_dn, m.cnt_up, m.cnt_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path,
+                       o.max_path);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(Q, 64)), dim3(64), 0, s, Q, d_src, sc.arcs, sc.narcs, MAX_ARCS,
+                     m.sub_up, m.sub_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path, o.max_path,
+                     serial_only ? -1 : UNPACK_MAX_ARCS);
+  return hipGetLastError();
+}
+
 hipError_t CchGpu::route(const CchMetricDev& m, const int* d_src, const int* d_dst, int Q, const CchRouteOut& o,
                          CchScratch& sc, hipStream_t s) {
   if (Q <= 0) return hipSuccess;
@@ -1047,9 +1200,7 @@ hipError_t CchGpu::route(const CchMetricDev& m, const int* d_src, const int* d_d
                      o.path ? sc.arcs : nullptr, o.path ? sc.narcs : nullptr, MAX_ARCS);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (o.path != nullptr) {
-    hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(Q, 64)), dim3(64), 0, s, Q, d_src, sc.arcs, sc.narcs, MAX_ARCS,
-                       m.sub_up, m.sub_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path, o.max_path);
-    e = hipGetLastError();
+    e = launch_unpack(m, Q, d_src, sc, o, s);
   }
   return e;
 }
@@ -1111,9 +1262,7 @@ hipError_t CchGpu::legs_from_matrix(const CchMetricDev& m, const int* d_src, con
                      o.path ? sc.narcs : nullptr, MAX_ARCS);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (o.path != nullptr) {
-    hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(Q, 64)), dim3(64), 0, s, Q, d_src, sc.arcs, sc.narcs,
-                       MAX_ARCS, m.sub_up, m.sub_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path, o.max_path);
-    e = hipGetLastError();
+    e = launch_unpack(m, Q, d_src, sc, o, s);
   }
   return e;
 }

@@ -37,6 +37,8 @@ struct CchMetricDev {
   int32_t* sub_dn = nullptr;
   float* len_up = nullptr;         // [M] metres of the path an arc stands for
   float* len_dn = nullptr;
+  int32_t* cnt_up = nullptr;       // [M] road edges the arc stands for (cooperative unpack)
+  int32_t* cnt_dn = nullptr;
   int32_t* f_ptr = nullptr;        // [N+1] kept forward arcs of rank r
   int32_t* b_ptr = nullptr;
   int4* f_rec = nullptr;           // {weight bits, head depth, arc id, 0}
@@ -121,6 +123,8 @@ class CchGpu {
   static constexpr int MAX_ARCS = 1024;   // shortcut arcs per path before unpacking
 
  private:
+  hipError_t launch_unpack(const CchMetricDev& m, int Q, const int* d_src, CchScratch& sc, const CchRouteOut& o,
+                           hipStream_t s);
   rcch::Topology T_;
   int dev_ = 0;
   // topology on the device
