@@ -918,7 +918,7 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   ck(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_fcnt, d_fcnt, N));
   cub_bytes = tb;
   ck(hipMalloc(&d_cub, cub_bytes ? cub_bytes : 1));
-  // triangle table within ROUTEST_CCH_TRI_GB of HBM (default 16; 0 disables)
+  // triangle table within ROUTEST_CCH_TRI_GB of HBM (default 48 — a 1M-node city needs ~38 GB of the 288; 0 disables)
   if (e == hipSuccess) {
     std::vector<int64_t> tofs(N + 1, 0);
     for (int z = 0; z < N; ++z) {
@@ -926,7 +926,7 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
       tofs[z + 1] = tofs[z] + k * (k - 1) / 2;
     }
     const char* env = std::getenv("ROUTEST_CCH_TRI_GB");
-    const double budget = env ? std::atof(env) : 16.0;
+    const double budget = env ? std::atof(env) : 48.0;
     const int64_t T = tofs[N];
     if (T > 0 && (double)T * 4.0 <= budget * 1073741824.0 && T < ((int64_t)1 << 40)) {
       if (up_copy(d_tofs, tofs.data(), N + 1) == hipSuccess && dmalloc(d_tri, (size_t)T) == hipSuccess) {
