@@ -52,9 +52,12 @@ def native_route_load(stack, reqs: Sequence[Dict[str, Any]], concurrency: int, s
             "flushes": f1["route_flushes"] - f0["route_flushes"],
             "legs_searched": f1["route_legs"] - f0["route_legs"],
             "legs_on_host": f1["route_host_legs"] - f0["route_host_legs"],
+            "legs_reusing_matrix_chains": f1.get("route_legs_reused", 0) - f0.get("route_legs_reused", 0),
+            "contexts_customized": f1.get("route_contexts_built", 0) - f0.get("route_contexts_built", 0),
             "legs_escalated": f1.get("route_astar_escalated", 0) - f0.get("route_astar_escalated", 0),
             "fallbacks_to_python": f1["route_service_fallbacks"] - f0["route_service_fallbacks"],
             "stage_ms_per_flush": {k[9:]: (f1[k] - f0[k]) / 1e3 / flushes for k in f1 if k.startswith("route_us_")},
             "client": "native closed-loop (csrc/runtime/http_client.h)",
             "path": f"HTTP/1.1 loopback POST {path} -> native front end (main port) -> route service "
-                    "(K5 + K6 + batched A* + path copy-out + C++ GeoJSON) -> response bytes"}
+                    "(CCH road matrices per routing context + K6 + CCH legs with paths + C++ GeoJSON with "
+                    "maneuvers) -> response bytes"}
