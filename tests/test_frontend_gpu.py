@@ -330,8 +330,9 @@ def test_alternatives_answered_natively_byte_identical():
                 a = _req(st.port, "POST", path, p)
                 b = _req(st.app_server.port, "POST", path, p)
                 assert a[0] == b[0] and a[1] == b[1], (path, a[1][:400], b[1][:400])
-                if a[0] == 200:
-                    alt = json.loads(a[1])["properties"]["alternatives"]
+                d = json.loads(a[1])
+                if a[0] == 200 and "properties" in d:          # (request_route answers errors with 200)
+                    alt = d["properties"]["alternatives"]
                     n_alt += 1
                     assert alt["scorer"] == "gcn-hip" and all(leg["candidates"] >= 1 for leg in alt["legs"])
         stats = st.front.stats()
