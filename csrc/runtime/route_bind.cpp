@@ -335,6 +335,11 @@ void bind_route(py::module& m) {
         py::arg("glon"), py::arg("nodes"), py::arg("trips"), py::arg("legs"), py::arg("steps") = py::none(),
         py::arg("cost") = py::none());
   m.def("py_round", &rtr::py_round);
+  m.def("json_float", [](double v) {     // the native JSON writer's float (tests: == json.dumps)
+    std::string o;
+    rtr::put_float(o, v);
+    return o;
+  });
   py::class_<PyHistoryDb>(m, "HistoryDb")
       .def(py::init<const std::string&>())
       .def("history", &PyHistoryDb::history, py::arg("limit") = py::none())

@@ -41,6 +41,14 @@ constexpr double PY_PI = 3.141592653589793238462643383279502884;
 // builtin round(x, nd): the correctly rounded decimal string, parsed back (CPython double_round).
 inline double py_round(double x, int nd) {
   if (!std::isfinite(x)) return x;
+  // fast path for one decimal (route step distances / durations): when x*10 is clearly away from a
+  // rounding midpoint the integer is the correctly rounded one, and k/10 (one correctly rounded
+  // division) is the double strtod would give for that decimal
+  if (nd == 1 && std::fabs(x) < 1e9) {
+    const double y = x * 10.0;
+    const double k = std::nearbyint(y);
+    if (std::fabs(y - k) < 0.49) return k / 10.0 == 0.0 ? std::copysign(0.0, x) : k / 10.0;
+  }
   char b[64];
   std::snprintf(b, sizeof b, "%.*f", nd, x);
   return std::strtod(b, nullptr);
@@ -132,10 +140,34 @@ inline void put_coord(std::string& o, double v) {
   while (n > 1 && d[n - 1] == '0') --n;
   o.append(d, n);
 }
-inline void put_float(std::string& o, double v) { rtc::append_pyfloat(o, v); }
+// repr: a value with at most one decimal (py_round(x, 1) output: step distances, durations,
+// summaries) prints from its integer tenths; everything else through the shortest round-trip path
+inline void put_float(std::string& o, double v) {
+  const double a = std::fabs(v);
+  if (a >= 1e-4 && a < 1e9) {
+    long long k = (long long)std::nearbyint(v * 10.0);
+    if ((double)k / 10.0 == v) {
+      if (k < 0) { o += '-'; k = -k; }
+      put_int(o, k / 10);
+      o += '.';
+      o += (char)('0' + k % 10);
+      return;
+    }
+  }
+  rtc::append_pyfloat(o, v);
+}
 
 // json.dumps(str, ensure_ascii=False)
 inline void put_str(std::string& o, const std::string& s) {
+  bool plain = true;                      // nothing to escape: one append
+  for (unsigned char c : s)
+    if (c < 0x20 || c == '"' || c == '\\') { plain = false; break; }
+  if (plain) {
+    o += '"';
+    o += s;
+    o += '"';
+    return;
+  }
   o += '"';
   for (unsigned char c : s) {
     switch (c) {
@@ -566,11 +598,16 @@ inline void leg_steps(const GraphHost& g, const double* glat, const double* glon
   const int H = n - 1;
   std::vector<int32_t> hop(H), nm(H);
   std::vector<double> brg(H);
+  // hop headings for the turn decisions: the local equirectangular bearing (one atan2 and one cos;
+  // the segments are metres long, so it agrees with the great-circle bearing to far below the 25 /
+  // 50 degree turn thresholds).  The Python provider runs this same code (_rt.GraphSteps).
+  const double d2r = PY_PI / 180.0, r2d = 180.0 / PY_PI;
   for (int h = 0; h < H; ++h) {
     const int32_t u = L.path[h], v = L.path[h + 1];
     hop[h] = hop_edge(g, u, v);
     nm[h] = (hop[h] >= 0 && g.edge_name) ? g.edge_name[hop[h]] : -1;
-    brg[h] = bearing_deg(glat[u], glon[u], glat[v], glon[v]);
+    const double x = (glon[v] - glon[u]) * std::cos(0.5 * (glat[u] + glat[v]) * d2r), y = glat[v] - glat[u];
+    brg[h] = py_mod(std::atan2(x, y) * r2d + 360.0, 360.0);
   }
   auto name_of = [&](int32_t id) -> std::string {
     return (id >= 0 && g.names && id < (int32_t)g.names->size()) ? (*g.names)[id] : std::string("-");

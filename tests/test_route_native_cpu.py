@@ -153,3 +153,23 @@ def test_graph_assembly_byte_identical():
         assert got == (want_st, want), it
         checked += 1
     assert checked > 80
+
+
+def test_float_fast_paths_match_python():
+    """py_round(x, 1) and the JSON float writer take integer-tenths fast paths (route steps): every
+    result equals Python's round() / json.dumps, midpoints and large magnitudes included."""
+    import json
+    import random
+    rt = __import__("pytest").importorskip("routest_amd._rt")
+    rnd = random.Random(3)
+    vals = [0.05, 0.15, 0.25, 2.675, -0.04, -0.05, 1e8 + 0.05, 123456789.95, 0.0, -0.0, 1e-5, 5e-5,
+            0.45, 1.45, 2.5, 999999999.95, 1e9 + 0.25, 3e15, 1e16, 1e17]
+    for _ in range(20000):
+        e = rnd.uniform(-6, 11)
+        vals.append(rnd.choice([-1, 1]) * 10 ** e)
+        vals.append(round(rnd.uniform(0, 5000), 2) + rnd.choice([0.0, 0.05, 0.049999999, 0.050000001]))
+    for v in vals:
+        r = rt.py_round(v, 1)
+        assert r == round(v, 1) and (str(r) == str(round(v, 1))), v
+        assert rt.json_float(r) == json.dumps(r), r
+        assert rt.json_float(v) == json.dumps(v), v
