@@ -100,7 +100,8 @@ def main_cch(args):
     cost = edge_costs(g, default_model(hidden=64, steps=50), device=d)
     print(f"graph {g.num_nodes} nodes / {len(g.indices)} edges in {time.time() - t0:.1f} s", flush=True)
     t0 = time.time()
-    router = RoadRouter(g, device=d)
+    # city-wide legs on a 1M-node grid run to several thousand road nodes
+    router = RoadRouter(g, device=d, max_path=16384)
     topo_s = time.time() - t0
     print(f"CCH topology in {topo_s:.1f} s: {router.stats()}", flush=True)
     torch.cuda.synchronize()

@@ -374,6 +374,7 @@ __global__ __launch_bounds__(64) void sweep_kernel(const int32_t* __restrict__ j
   if (j >= J) return;
   const int lane = threadIdx.x;
   const int code = jobs[j];
+  if (code < 0) return;                     // matrix padding
   const int r = code >> 1;
   const bool fwd = (code & 1) == 0;
   const int32_t* __restrict__ ptr = fwd ? f_ptr : b_ptr;
@@ -473,6 +474,15 @@ __global__ __launch_bounds__(64) void meet_kernel(int P, const int32_t* __restri
   const int lane = threadIdx.x;
   const int jf = pjf ? pjf[q] : jf0 + 2 * q;
   const int jb = pjb ? pjb[q] : jb0 + 2 * q;
+  if (jobs[jf] < 0 || jobs[jb] < 0) {       // a matrix padding point: nothing to meet
+    if (threadIdx.x == 0) {
+      if (out_sec) out_sec[q] = -1.f;
+      if (out_met) out_met[q] = -1.f;
+      if (out_status) out_status[q] = 1;
+      if (narcs) narcs[q] = 0;
+    }
+    return;
+  }
   const int s = jobs[jf] >> 1, t = jobs[jb] >> 1;
   const int ds = depth[s], dt = depth[t];
   const size_t bf = (size_t)jf * stride, bb = (size_t)jb * stride;
@@ -749,7 +759,12 @@ __global__ void matrix_jobs_kernel(const int* __restrict__ pts, const int* __res
   const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (g >= (long long)R * NM) return;
   const int r = (int)(g / NM), i = (int)(g % NM);
-  int v = i < npts[r] ? pts[g] : -1;
+  if (i >= npts[r]) {                       // padding of a shorter request: no chain is swept
+    jobs[2 * g] = -1;
+    jobs[2 * g + 1] = -1;
+    return;
+  }
+  int v = pts[g];
   if (v < 0 || v >= N) v = 0;
   jobs[2 * g] = rank[v] << 1;
   jobs[2 * g + 1] = (rank[v] << 1) | 1;
