@@ -256,6 +256,9 @@ struct RouteService::Impl {
     }
     sql.busy_timeout(db, 10000);
     sql.exec(db, "PRAGMA journal_mode=WAL", nullptr, nullptr, nullptr);
+    // WAL + NORMAL: a commit appends to the WAL without an fsync (the WAL is synced at checkpoints);
+    // FULL would fsync every flush's commit
+    sql.exec(db, "PRAGMA synchronous=NORMAL", nullptr, nullptr, nullptr);
     sql.exec(db, "PRAGMA foreign_keys=ON", nullptr, nullptr, nullptr);
     const char* q1 = "INSERT INTO route_requests(id,origin_id,stops,request_time,status,engine,vehicle_id,driver_age)"
                      " VALUES(?,?,?,?,?,?,?,?)";
@@ -1253,13 +1256,21 @@ struct RouteService::Impl {
       if (!j->fallback && !j->status && j->asmb.ok && !j->request_route) save.push_back(j);
     if (db && !save.empty()) {
       const std::string now = utc_now_iso();
+      // one transaction per flush, one savepoint per request: a failed insert rolls back only its
+      // own request's rows (SQLiteStore's per-request semantics) and the flush commits once
+      const bool tx = sql.exec(db, "BEGIN", nullptr, nullptr, nullptr) == rtsql::OK;
       for (RouteJob* j : save) {
-        // one transaction per request, like SQLiteStore (a failed insert rolls back its own rows)
-        sql.exec(db, "BEGIN", nullptr, nullptr, nullptr);
+        sql.exec(db, "SAVEPOINT rq", nullptr, nullptr, nullptr);
         j->request_id = persist_one(j, now);
-        sql.exec(db, j->request_id.empty() ? "ROLLBACK" : "COMMIT", nullptr, nullptr, nullptr);
-        if (!j->request_id.empty()) n_persisted.fetch_add(1, std::memory_order_relaxed);
+        if (j->request_id.empty()) sql.exec(db, "ROLLBACK TO rq", nullptr, nullptr, nullptr);
+        sql.exec(db, "RELEASE rq", nullptr, nullptr, nullptr);
       }
+      if (tx && sql.exec(db, "COMMIT", nullptr, nullptr, nullptr) != rtsql::OK) {
+        sql.exec(db, "ROLLBACK", nullptr, nullptr, nullptr);     // nothing of the flush was stored
+        for (RouteJob* j : save) j->request_id.clear();
+      }
+      for (RouteJob* j : save)
+        if (!j->request_id.empty()) n_persisted.fetch_add(1, std::memory_order_relaxed);
     }
     add_t(7, t0);
     for (RouteJob* j : jobs) {

@@ -132,7 +132,7 @@ class PyGraphSteps {
     rtr::leg_steps(g, lat_.data(), lon_.data(), L, speed_scale, start, end, st);
     py::list out;
     for (const auto& x : st)
-      out.append(py::make_tuple(x.dist, x.dur, x.type, x.instruction, x.name, x.wp0, x.wp1));
+      out.append(py::make_tuple(x.dist, x.dur, x.type, x.instruction(), x.name_str(), x.wp0, x.wp1));
     return out;
   }
 

@@ -567,12 +567,26 @@ inline int32_t hop_edge(const GraphHost& g, int32_t u, int32_t v) {
   return best;
 }
 
-// One maneuver step of a graph leg (routing/graph.py leg_steps mirrors the fields).
+// One maneuver step of a graph leg (routing/graph.py leg_steps mirrors the fields).  The text is
+// kept as parts — instruction = (head ? "Head " + head : verb) [+ (head ? " on " : " onto ") + name]
+// when the road is named, name = the road name or "-" — and composed where it is written, so a
+// step costs no string allocation.
 struct Step {
   double dist = 0, dur = 0;       // rounded to 0.1
   int type = 11;
-  std::string instruction, name;
+  const char* verb = "";          // turn verb ("Depart" for a one-node leg)
+  const char* head = nullptr;     // first step: the compass word of "Head <dir>"
+  const std::string* name = nullptr;   // road name (nullptr: unnamed, "-")
   long long wp0 = 0, wp1 = 0;
+  std::string instruction() const {
+    std::string o = head ? std::string("Head ") + head : std::string(verb);
+    if (name) {
+      o += head ? " on " : " onto ";
+      o += *name;
+    }
+    return o;
+  }
+  std::string name_str() const { return name ? *name : std::string("-"); }
 };
 
 // Maneuvers along one leg's node path.  A new step starts where the road name changes or the
@@ -588,16 +602,18 @@ inline void leg_steps(const GraphHost& g, const double* glat, const double* glon
     Step s;
     s.dist = 0.0;
     s.dur = py_round((double)L.sec * speed_scale, 1);
-    s.instruction = "Depart";
-    s.name = "-";
+    s.verb = "Depart";
     s.wp0 = start;
     s.wp1 = end;
-    out.push_back(std::move(s));
+    out.push_back(s);
     return;
   }
   const int H = n - 1;
-  std::vector<int32_t> hop(H), nm(H);
-  std::vector<double> brg(H);
+  thread_local std::vector<int32_t> hop, nm;
+  thread_local std::vector<double> brg;
+  hop.resize(H);
+  nm.resize(H);
+  brg.resize(H);
   // hop headings for the turn decisions: the local equirectangular bearing (one atan2 and one cos;
   // the segments are metres long, so it agrees with the great-circle bearing to far below the 25 /
   // 50 degree turn thresholds).  The Python provider runs this same code (_rt.GraphSteps).
@@ -609,8 +625,8 @@ inline void leg_steps(const GraphHost& g, const double* glat, const double* glon
     const double x = (glon[v] - glon[u]) * std::cos(0.5 * (glat[u] + glat[v]) * d2r), y = glat[v] - glat[u];
     brg[h] = py_mod(std::atan2(x, y) * r2d + 360.0, 360.0);
   }
-  auto name_of = [&](int32_t id) -> std::string {
-    return (id >= 0 && g.names && id < (int32_t)g.names->size()) ? (*g.names)[id] : std::string("-");
+  auto name_of = [&](int32_t id) -> const std::string* {
+    return (id >= 0 && g.names && id < (int32_t)g.names->size()) ? &(*g.names)[id] : nullptr;
   };
   int h0 = 0;
   while (h0 < H) {
@@ -626,20 +642,44 @@ inline void leg_steps(const GraphHost& g, const double* glat, const double* glon
     s.dist = py_round(d, 1);
     s.dur = py_round(t * speed_scale, 1);
     s.name = name_of(nm[h0]);
-    const bool named = nm[h0] >= 0;
     if (h0 == 0) {
       s.type = 11;
-      s.instruction = std::string("Head ") + bearing_word(glat[L.path[0]], glon[L.path[0]], glat[L.path[1]], glon[L.path[1]]);
-      if (named) s.instruction += " on " + s.name;
+      s.head = bearing_word(glat[L.path[0]], glon[L.path[0]], glat[L.path[1]], glon[L.path[1]]);
     } else {
       s.type = turn_type(heading_change(brg[h0 - 1], brg[h0]));
-      s.instruction = turn_verb(s.type);
-      if (named) s.instruction += " onto " + s.name;
+      s.verb = turn_verb(s.type);
     }
     s.wp0 = h0 == 0 ? start : start + 1 + h0;
     s.wp1 = h1 == H ? end : start + 1 + h1;
-    out.push_back(std::move(s));
+    out.push_back(s);
     h0 = h1;
+  }
+}
+
+// the characters of s as json.dumps would escape them inside a string (no quotes)
+inline void put_str_body(std::string& o, const char* s, size_t n) {
+  size_t i = 0;
+  while (i < n) {
+    size_t j = i;
+    while (j < n && (unsigned char)s[j] >= 0x20 && s[j] != '"' && s[j] != '\\') ++j;
+    o.append(s + i, j - i);
+    if (j >= n) break;
+    const unsigned char c = (unsigned char)s[j];
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\n': o += "\\n"; break;
+      case '\r': o += "\\r"; break;
+      case '\t': o += "\\t"; break;
+      case '\b': o += "\\b"; break;
+      case '\f': o += "\\f"; break;
+      default: {
+        char b[8];
+        std::snprintf(b, sizeof b, "\\u%04x", c);
+        o += b;
+      }
+    }
+    i = j + 1;
   }
 }
 
@@ -647,9 +687,21 @@ inline void put_step(std::string& o, const Step& s) {
   o += "{\"distance\":"; put_float(o, s.dist);
   o += ",\"duration\":"; put_float(o, s.dur);
   o += ",\"type\":"; put_int(o, s.type);
-  o += ",\"instruction\":"; put_str(o, s.instruction);
-  o += ",\"name\":"; put_str(o, s.name);
-  o += ",\"way_points\":["; put_int(o, s.wp0); o += ','; put_int(o, s.wp1); o += "]}";
+  o += ",\"instruction\":\"";
+  if (s.head) {
+    o += "Head ";
+    o += s.head;
+  } else {
+    o += s.verb;
+  }
+  if (s.name) {
+    o += s.head ? " on " : " onto ";
+    put_str_body(o, s.name->data(), s.name->size());
+  }
+  o += "\",\"name\":\"";
+  if (s.name) put_str_body(o, s.name->data(), s.name->size());
+  else o += '-';
+  o += "\",\"way_points\":["; put_int(o, s.wp0); o += ','; put_int(o, s.wp1); o += "]}";
 }
 
 // GraphProvider.feature_from_legs — graph.py.  Returns "" or the ProviderError text.

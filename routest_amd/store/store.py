@@ -148,8 +148,9 @@ class SQLiteStore:
         self._db.row_factory = sqlite3.Row
         self._db.execute("PRAGMA foreign_keys=ON")
         self._db.execute("PRAGMA journal_mode=WAL")
-        if self.ephemeral:
-            self._db.execute("PRAGMA synchronous=OFF")
+        # WAL + NORMAL for a file store: commits append to the WAL without an fsync (synced at
+        # checkpoints); the temporary default store needs no durability at all
+        self._db.execute("PRAGMA synchronous=OFF" if self.ephemeral else "PRAGMA synchronous=NORMAL")
         self._db.executescript(SCHEMA)
         if seed:
             self.seed_locations()
