@@ -554,7 +554,7 @@ __global__ __launch_bounds__(64) void meet_kernel(int P, const int32_t* __restri
 }
 
 // One lane per pair: expand the shortcut arcs to road node ids (DFS, first sub-arc first).
-constexpr int UNPACK_STACK = 96;
+constexpr int UNPACK_STACK = 128;
 __global__ __launch_bounds__(64) void unpack_kernel(int P, const int* __restrict__ src_node, const int32_t* __restrict__ arcs,
                                                     const int32_t* __restrict__ narcs, int max_arcs,
                                                     const int32_t* __restrict__ sub_up,
@@ -572,7 +572,7 @@ __global__ __launch_bounds__(64) void unpack_kernel(int P, const int* __restrict
     if (min_arcs < 0) out_len[q] = 0;
     return;
   }
-  if (narcs[q] <= min_arcs) return;          // unpacked by unpack_coop_kernel
+  if (narcs[q] <= min_arcs && out_len[q] != -1) return;   // unpacked by unpack_coop_kernel
   int* out = out_path + (size_t)q * max_path;
   int n = 0;
   out[n++] = src_node[q];
@@ -721,10 +721,7 @@ __global__ __launch_bounds__(64) void unpack_coop_kernel(int P, const int* __res
       leaf = descend(al[k], 0);
     }
   }
-  if (!ok) {                                 // stack overflow: the exact host fallback takes the leg
-    status[q] = 4;
-    out_len[q] = 0;
-  }
+  if (!ok) out_len[q] = -1;                  // stack overflow: the serial kernel redoes the pair
 }
 
 // (node ids are range-checked by the callers; out-of-range ids are clamped, never dereferenced)
