@@ -17,3 +17,6 @@ for G in "$G1" "$G2" "$G3" "$G4"; do
   timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $G -d $O/t1k$i -o train --output-format csv -- python3 $ROOT/bench/train_bench.py --hidden 1024 --batch 65536 --steps 4 --warmup 2 --modes fused > $O/t1k$i.log 2>&1 || exit $((30+i))
 done
 echo done
+cd $ROOT
+timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 7; }
+tail -1 $O/bench.log | cut -c1-300
