@@ -563,7 +563,7 @@ __global__ __launch_bounds__(64) void unpack_kernel(int P, const int* __restrict
                                                     const int32_t* __restrict__ up_head,
                                                     const int32_t* __restrict__ node_of, int* __restrict__ status,
                                                     int* __restrict__ out_len, int* __restrict__ out_path, int max_path,
-                                                    int min_arcs) {
+                                                    int min_arcs, int* __restrict__ out_edge) {
   __shared__ int32_t stk[64 * UNPACK_STACK];
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= P) return;
@@ -589,6 +589,7 @@ __global__ __launch_bounds__(64) void unpack_kernel(int P, const int* __restrict
       const int s0 = sub[0];
       if (s0 < 0) {
         if (n >= max_path) { ok = false; break; }
+        if (out_edge) out_edge[(size_t)q * max_path + n - 1] = sub[1];
         out[n++] = node_of[dn ? arc_lo[a] : up_head[a]];
         continue;
       }
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(64) void unpack_coop_kernel(int P, const int* __res
                                                          const int32_t* __restrict__ up_head,
                                                          const int32_t* __restrict__ node_of, int* __restrict__ status,
                                                          int* __restrict__ out_len, int* __restrict__ out_path,
-                                                         int max_path) {
+                                                         int max_path, int* __restrict__ out_edge) {
   constexpr int G = 64 / UNPACK_LANES;
   __shared__ int32_t offs[G][UNPACK_MAX_ARCS + 1];
   __shared__ int32_t stk[64 * UNPACK_SD];
@@ -671,6 +672,7 @@ __global__ __launch_bounds__(64) void unpack_coop_kernel(int P, const int* __res
   __syncthreads();
   if (!coop || st != 0) return;
   int* out = out_path + (size_t)q * max_path;
+  int* oe = out_edge ? out_edge + (size_t)q * max_path : nullptr;
   if (sl == 0) out[0] = src_node[q];
   const int per = (E + UNPACK_LANES - 1) / UNPACK_LANES;
   int e = sl * per;
@@ -713,6 +715,7 @@ __global__ __launch_bounds__(64) void unpack_coop_kernel(int P, const int* __res
   while (ok) {
     const int a = leaf >> 1, dn = leaf & 1;
     out[e + 1] = node_of[dn ? arc_lo[a] : up_head[a]];
+    if (oe) oe[e] = (dn ? sub_dn : sub_up)[2 * (long long)a + 1];    // a leaf arc's original edge
     if (++e >= e1) break;
     if (sp > 0) {
       leaf = descend(sk[--sp], 0);
@@ -1184,13 +1187,13 @@ hipError_t CchGpu::launch_unpack(const CchMetricDev& m, int Q, const int* d_src,
     constexpr int G = 64 / UNPACK_LANES;
     hipLaunchKernelGGL(unpack_coop_kernel, dim3((Q + G - 1) / G), dim3(64), 0, s, Q, d_src, sc.arcs, sc.narcs, MAX_ARCS,
                        m.sub_up, m.sub_dn, m.cnt_up, m.cnt_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path,
-                       o.max_path);
+                       o.max_path, o.edges);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(Q, 64)), dim3(64), 0, s, Q, d_src, sc.arcs, sc.narcs, MAX_ARCS,
                      m.sub_up, m.sub_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path, o.max_path,
-                     serial_only ? -1 : UNPACK_MAX_ARCS);
+                     serial_only ? -1 : UNPACK_MAX_ARCS, o.edges);
   return hipGetLastError();
 }
 

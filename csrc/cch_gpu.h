@@ -74,6 +74,7 @@ struct CchRouteOut {
   int* status = nullptr;           // [Q] 0 found, 1 unreachable, 4 too long / unpack overflow
   int* len = nullptr;              // [Q] path nodes
   int* path = nullptr;             // [Q, max_path] node ids (nullptr: costs only)
+  int* edges = nullptr;            // [Q, max_path] the road edge of each hop (optional; with path)
   int max_path = 0;
 };
 

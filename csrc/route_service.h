@@ -105,7 +105,7 @@ struct RouteJob {
   std::vector<std::pair<int, int>> alt_pairs;
   std::vector<std::vector<int>> alt_vias;
   std::vector<rtr::Leg> alt_legs;
-  std::vector<std::vector<int32_t>> alt_paths;
+  std::vector<std::vector<int32_t>> alt_paths, alt_edges;
   std::string alt_json;
   rtr::Assembled asmb;
   float eta_min = NAN;

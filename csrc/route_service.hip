@@ -168,6 +168,7 @@ struct Batch {
   std::vector<rtr::Leg> legs;
   std::vector<std::vector<int32_t>> host_paths;
   std::vector<int32_t> flat;                 // found paths, compacted (Leg::path points in here)
+  std::vector<int32_t> flat_e;               // their hop edges (CCH; Leg::edges points in here)
   std::unordered_map<uint64_t, int> leg_index;
   bool failed = false;
   // "alternatives" jobs of the flush: the scorer snapshot they use
@@ -208,10 +209,10 @@ struct RouteService::Impl {
   DevBuf<double> d_lat, d_lon, d_dem, d_cap, d_maxd, d_D;
   DevBuf<int> d_npts, d_visit, d_trip, d_ntrips, d_status;
   // A* buffers
-  HostBuf<int> h_src, h_dst, h_len, h_st, h_qidx, h_flat;
+  HostBuf<int> h_src, h_dst, h_len, h_st, h_qidx, h_flat, h_flat_e;
   HostBuf<float> h_cost;
   HostBuf<long long> h_off;
-  DevBuf<int> d_src, d_dst, d_len, d_st, d_path, d_qidx, d_flat, d_iters;
+  DevBuf<int> d_src, d_dst, d_len, d_st, d_path, d_qidx, d_flat, d_iters, d_edge, d_flat_e;
   DevBuf<float> d_cost;
   DevBuf<long long> d_off;
   // CCH
@@ -758,7 +759,7 @@ struct RouteService::Impl {
     const int MP = cfg.max_path;
     if (h_src.need(Q) || h_dst.need(Q) || h_len.need(Q) || h_st.need(Q) || h_cost.need(Q) || h_met.need(Q) ||
         h_off.need(Q) || d_src.need(Q) || d_dst.need(Q) || d_len.need(Q) || d_st.need(Q) || d_cost.need(Q) ||
-        d_met.need(Q) || d_off.need(Q) || d_path.need((size_t)Q * MP))
+        d_met.need(Q) || d_off.need(Q) || d_path.need((size_t)Q * MP) || d_edge.need((size_t)Q * MP))
       return false;
     for (int gi = 0; gi < G; ++gi)
       for (size_t i = 0; i < pairs[gi].size(); ++i) {
@@ -792,6 +793,7 @@ struct RouteService::Impl {
         o.status = d_st.d + q;
         o.len = d_len.d + q;
         o.path = d_path.d + (size_t)q * MP;
+        o.edges = d_edge.d + (size_t)q * MP;
         o.max_path = MP;
         return o;
       };
@@ -824,10 +826,19 @@ struct RouteService::Impl {
                            Q, d_flat.d);
         e = hipGetLastError();
       }
+      // the hops' road edges the same way (maneuvers look them up instead of scanning adjacency)
+      if (e == hipSuccess && (h_flat_e.need((size_t)total) || d_flat_e.need((size_t)total))) e = hipErrorOutOfMemory;
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(compact_paths_kernel, dim3(Q), dim3(256), 0, stream, d_edge.d, MP, d_len.d, d_st.d, d_off.d,
+                           Q, d_flat_e.d);
+        e = hipGetLastError();
+      }
       if (e == hipSuccess) e = hipMemcpyAsync(h_flat.h, d_flat.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipMemcpyAsync(h_flat_e.h, d_flat_e.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
       if (e == hipSuccess) e = hipStreamSynchronize(stream);
       if (e != hipSuccess) return false;
       b.flat.assign(h_flat.h, h_flat.h + total);
+      b.flat_e.assign(h_flat_e.h, h_flat_e.h + total);
     }
     add_t(4, t0);
     // legs the GPU could not return (status 4: longer than max_path / unpack stack): exact on the host
@@ -842,6 +853,7 @@ struct RouteService::Impl {
           L.metres = h_met.h[i];
           L.len = std::min(h_len.h[i], MP);
           L.path = b.flat.data() + h_off.h[i];
+          L.edges = b.flat_e.data() + h_off.h[i];
         } else if (h_st.h[i] == 4 && nbad <= 1024 && cfg.h_indptr != nullptr) {
           const std::vector<float>& hc = *b.host_cost[gi];
           float c;
@@ -1007,6 +1019,8 @@ struct RouteService::Impl {
       int n1;
       const int32_t* p2;   // second part (from its node 1 on), or nullptr
       int n2;
+      const int32_t* e1;   // hop edges of the parts (nullptr: unknown, looked up on the host)
+      const int32_t* e2;
     };
     auto leg = [&](int s, int t) -> const rtr::Leg* {
       auto it = b.leg_index.find(leg_key(j->group, s, t));
@@ -1017,18 +1031,20 @@ struct RouteService::Impl {
     for (size_t k = 0; k < P; ++k) {
       const int s = j->alt_pairs[k].first, t = j->alt_pairs[k].second;
       const rtr::Leg* d = leg(s, t);
-      if (d && d->len > 0) cands[k].push_back({d->sec, d->metres, d->path, d->len, nullptr, 0});
+      if (d && d->len > 0) cands[k].push_back({d->sec, d->metres, d->path, d->len, nullptr, 0, d->edges, nullptr});
       for (int w : j->alt_vias[k]) {
         const rtr::Leg* a = leg(s, w);
         const rtr::Leg* c = leg(w, t);
         if (a && c && a->len > 0 && c->len > 0)
-          cands[k].push_back({a->sec + c->sec, a->metres + c->metres, a->path, a->len, c->path + 1, c->len - 1});
+          cands[k].push_back({a->sec + c->sec, a->metres + c->metres, a->path, a->len, c->path + 1, c->len - 1,
+                              a->edges, c->edges});
       }
       total += cands[k].size();
     }
     (void)total;
     j->alt_legs.assign(P, rtr::Leg());
     j->alt_paths.assign(P, {});
+    j->alt_edges.assign(P, {});
     std::string o = ",\"alternatives\":{\"k\":";
     rtr::put_int(o, j->req.alt_k);
     o += ",\"scorer\":";
@@ -1064,6 +1080,12 @@ struct RouteService::Impl {
       L.metres = x.met;
       L.path = own.data();
       L.len = (int)own.size();
+      if (x.e1 && (x.p2 == nullptr || x.e2)) {
+        std::vector<int32_t>& oe = j->alt_edges[k];
+        oe.assign(x.e1, x.e1 + (x.n1 - 1));
+        if (x.p2) oe.insert(oe.end(), x.e2, x.e2 + x.n2);     // the second part's hops: n2 of them
+        L.edges = oe.data();
+      }
       o += ",\"chosen\":";
       rtr::put_int(o, best);
       o += ",\"scores\":[";

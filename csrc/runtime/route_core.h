@@ -508,6 +508,7 @@ struct Leg {
   const int32_t* path = nullptr;
   int len = 0;                    // 0 = not found
   double metres = -1.0;
+  const int32_t* edges = nullptr; // the road edge of each hop (len - 1), when the router gave them
 };
 
 // Host view of the road graph for maneuvers: CSR, per-edge metres and seconds (the leg's routing
@@ -620,7 +621,7 @@ inline void leg_steps(const GraphHost& g, const double* glat, const double* glon
   const double d2r = PY_PI / 180.0, r2d = 180.0 / PY_PI;
   for (int h = 0; h < H; ++h) {
     const int32_t u = L.path[h], v = L.path[h + 1];
-    hop[h] = hop_edge(g, u, v);
+    hop[h] = L.edges ? L.edges[h] : hop_edge(g, u, v);
     nm[h] = (hop[h] >= 0 && g.edge_name) ? g.edge_name[hop[h]] : -1;
     const double x = (glon[v] - glon[u]) * std::cos(0.5 * (glat[u] + glat[v]) * d2r), y = glat[v] - glat[u];
     brg[h] = py_mod(std::atan2(x, y) * r2d + 360.0, 360.0);
