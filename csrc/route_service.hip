@@ -18,6 +18,7 @@
 //      database file the Python store reads (reference routes.py:119-125, best effort);
 //   7. completed jobs go back to their reactors (eventfd wake-up), which write the bytes.
 #include <algorithm>
+#include <cstring>
 #include <array>
 #include <atomic>
 #include <chrono>
@@ -288,9 +289,15 @@ struct RouteService::Impl {
       default: return false;
     }
   }
+  // SQLITE_STATIC: every bound string outlives its statement's step (the row texts of a route are
+  // ~100 KB of GeoJSON; a transient binding copied each once more)
   bool bind_text(void* st, int i, const std::string& s) {
-    return sql.bind_text(st, i, s.data(), (int)s.size(), rtsql::TRANSIENT) == rtsql::OK;
+    return sql.bind_text(st, i, s.data(), (int)s.size(), rtsql::STATIC) == rtsql::OK;
   }
+  bool bind_text(void* st, int i, const char* literal) {      // string literals only (static storage)
+    return sql.bind_text(st, i, literal, (int)std::strlen(literal), rtsql::STATIC) == rtsql::OK;
+  }
+  bool bind_text(void* st, int i, std::string&&) = delete;    // a temporary would dangle
 
   // store.py build_rows + SQLiteStore.persist_request_and_result for one job; "" on failure
   std::string persist_one(RouteJob* j, const std::string& now) {
@@ -323,7 +330,8 @@ struct RouteService::Impl {
     std::string geom = "{\"type\":\"LineString\",\"coordinates\":";
     geom += a.coords;
     geom += '}';
-    ok = bind_text(st_res, 1, uuid.next()) && bind_text(st_res, 2, rid) && bind_text(st_res, 3, a.order) &&
+    const std::string res_id = uuid.next();
+    ok = bind_text(st_res, 1, res_id) && bind_text(st_res, 2, rid) && bind_text(st_res, 3, a.order) &&
          sql.bind_double(st_res, 4, rtr::py_round(a.dist, 2)) == rtsql::OK &&
          sql.bind_double(st_res, 5, rtr::py_round(a.dur, 2)) == rtsql::OK && bind_text(st_res, 6, a.segments) &&
          bind_text(st_res, 7, geom);

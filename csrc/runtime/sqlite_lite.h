@@ -79,5 +79,6 @@ constexpr int OK = 0, ROW = 100, DONE = 101;
 constexpr int T_INTEGER = 1, T_FLOAT = 2, T_TEXT = 3, T_BLOB = 4, T_NULL = 5;
 constexpr int OPEN_READWRITE = 0x2, OPEN_CREATE = 0x4, OPEN_URI = 0x40, OPEN_NOMUTEX = 0x8000;
 inline void (*const TRANSIENT)(void*) = reinterpret_cast<void (*)(void*)>(-1);
+inline void (*const STATIC)(void*) = nullptr;      // the caller keeps the bytes alive until step/reset
 
 }  // namespace rtsql
