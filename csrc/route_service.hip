@@ -8,15 +8,18 @@
 //      handed back for the Python app);
 //   2. ONE K5 + ONE K6 launch for every multi-stop request of the flush (csrc/route_kernels.hip);
 //      only the trips and, for infeasible requests, the depot row of D come back to the host;
-//   3. road-graph provider: every waypoint snapped (NodeGrid), the flush's unique legs searched by
-//      the batched A* (csrc/astar.hip: lane stage, then one wave per long search, exact host
-//      Dijkstra for the rare search that exhausts both), and the found paths COMPACTED on the GPU
-//      into one flat array before the copy-out (a leg row is max_path ints; a path is ~200);
-//   4. responses assembled on a thread pool (route_core.h: byte-identical to the FastAPI handler);
+//   3. road-graph provider: every waypoint snapped (NodeGrid), the flush's unique legs searched on
+//      the CCH (csrc/cch.hip, under each request's routing context) or by the batched A*
+//      (csrc/astar.hip), and the found paths COMPACTED on the GPU into one flat array before the
+//      copy-out (a leg row is max_path ints; a path is ~200);
+//   4. responses assembled on the assembly thread (route_core.h: byte-identical to the FastAPI
+//      handler) while the GPU stage runs the next flush;
 //   5. use_ml_eta: one fused featurize+MLP launch (K1+K2) for the flush's ETA records;
-//   6. persistence of /api/optimize_route results: one SQLite transaction per flush into the same
-//      database file the Python store reads (reference routes.py:119-125, best effort);
-//   7. completed jobs go back to their reactors (eventfd wake-up), which write the bytes.
+//   6. persistence of /api/optimize_route results on a thread of its own: every flush waiting is
+//      group-committed in one SQLite transaction into the database file the Python store reads
+//      (reference routes.py:119-125, best effort); WAL checkpoints run on a fourth thread;
+//   7. completed jobs go back to their reactors (eventfd wake-up), which write the bytes -- a
+//      persisted job only after its commit.
 #include <algorithm>
 #include <cstring>
 #include <array>
@@ -176,6 +179,7 @@ struct Batch {
   std::shared_ptr<const std::vector<double>> alt_delay;
   int alt_kind = 0;
   std::string alt_engine;
+  std::vector<RouteJob*> save;               // jobs whose rows the persistence thread writes
 };
 
 inline double now_us() {
@@ -244,7 +248,19 @@ struct RouteService::Impl {
   void* db = nullptr;
   void* st_req = nullptr;
   void* st_res = nullptr;
+  void *st_begin = nullptr, *st_commit = nullptr, *st_rollback = nullptr, *st_sp = nullptr, *st_rel = nullptr,
+       *st_rb = nullptr;
   Uuid4 uuid;
+  // assembly -> persistence hand-off (group commit) and the background WAL checkpointer
+  std::thread th_persist, th_ckpt;
+  std::mutex pmu;
+  std::condition_variable pcv;
+  std::deque<std::vector<RouteJob*>> pq;
+  bool asm_done = false;
+  std::mutex cmu;
+  std::condition_variable ccv;
+  long long commits = 0;
+  bool ck_stop = false;
 
   void open_store() {
     if (cfg.sqlite_path.empty()) return;
@@ -262,15 +278,21 @@ struct RouteService::Impl {
     // FULL would fsync every flush's commit
     sql.exec(db, "PRAGMA synchronous=NORMAL", nullptr, nullptr, nullptr);
     sql.exec(db, "PRAGMA foreign_keys=ON", nullptr, nullptr, nullptr);
+    sql.exec(db, "PRAGMA wal_autocheckpoint=0", nullptr, nullptr, nullptr);   // ckpt_loop checkpoints
     const char* q1 = "INSERT INTO route_requests(id,origin_id,stops,request_time,status,engine,vehicle_id,driver_age)"
                      " VALUES(?,?,?,?,?,?,?,?)";
     const char* q2 = "INSERT INTO route_results(id,request_id,optimized_order,total_distance,total_duration,legs,"
                      "geometry,eta_minutes_ml,eta_completion_time_ml,created_at) VALUES(?,?,?,?,?,?,?,?,?,?)";
-    if (sql.prepare_v2(db, q1, -1, &st_req, nullptr) != rtsql::OK ||
-        sql.prepare_v2(db, q2, -1, &st_res, nullptr) != rtsql::OK) {
-      if (st_req) sql.finalize(st_req);
-      if (st_res) sql.finalize(st_res);
-      st_req = st_res = nullptr;
+    const std::pair<const char*, void**> stmts[] = {
+        {q1, &st_req},         {q2, &st_res},          {"BEGIN", &st_begin}, {"COMMIT", &st_commit},
+        {"ROLLBACK", &st_rollback}, {"SAVEPOINT rq", &st_sp}, {"RELEASE rq", &st_rel}, {"ROLLBACK TO rq", &st_rb}};
+    bool ok = true;
+    for (const auto& [text, st] : stmts) ok = ok && sql.prepare_v2(db, text, -1, st, nullptr) == rtsql::OK;
+    if (!ok) {
+      for (const auto& [text, st] : stmts) {
+        if (*st) sql.finalize(*st);
+        *st = nullptr;
+      }
       sql.close(db);
       db = nullptr;
     }
@@ -383,6 +405,7 @@ struct RouteService::Impl {
     if (hipSetDevice(cfg.device) != hipSuccess) return;
     if (hipStreamCreateWithFlags(&stream_asm, hipStreamNonBlocking) != hipSuccess) return;
     open_store();
+    th_persist = std::thread([this] { persist_loop(); });
     while (true) {
       Batch* b = nullptr;
       {
@@ -395,11 +418,29 @@ struct RouteService::Impl {
       }
       asm_stage(*b);
       n_flushes.fetch_add(1, std::memory_order_relaxed);
-      for (RouteJob* j : b->jobs) done(j);
+      // jobs that persist nothing answer now; the others after their group commit
+      std::vector<RouteJob*> save = std::move(b->save);
+      for (RouteJob* j : b->jobs)
+        if (std::find(save.begin(), save.end(), j) == save.end()) {
+          finish(j);
+          done(j);
+        }
       delete b;
+      if (!save.empty()) {
+        std::unique_lock<std::mutex> lk(pmu);
+        pcv.wait(lk, [&] { return pq.size() < 8; });     // back-pressure on a stalled disk
+        pq.push_back(std::move(save));
+        pcv.notify_all();
+      }
     }
-    if (st_req) sql.finalize(st_req);
-    if (st_res) sql.finalize(st_res);
+    {
+      std::lock_guard<std::mutex> lk(pmu);
+      asm_done = true;
+    }
+    pcv.notify_all();
+    th_persist.join();
+    for (void* st : {st_req, st_res, st_begin, st_commit, st_rollback, st_sp, st_rel, st_rb})
+      if (st) sql.finalize(st);
     if (db) sql.close(db);
     (void)hipStreamDestroy(stream_asm);
   }
@@ -1279,53 +1320,131 @@ struct RouteService::Impl {
       for (RouteJob* j : jobs) j->eta_iso.clear();
     }
     add_t(6, t0);
-    t0 = now_us();
-    // persistence (optimize_route / route only; request_route never persists)
-    std::vector<RouteJob*> save;
+    // persistence (optimize_route / route only; request_route never persists) is the persistence
+    // thread's: it group-commits these with whatever else is waiting
     for (RouteJob* j : jobs)
-      if (!j->fallback && !j->status && j->asmb.ok && !j->request_route) save.push_back(j);
-    if (db && !save.empty()) {
-      const std::string now = utc_now_iso();
-      // one transaction per flush, one savepoint per request: a failed insert rolls back only its
-      // own request's rows (SQLiteStore's per-request semantics) and the flush commits once
-      const bool tx = sql.exec(db, "BEGIN", nullptr, nullptr, nullptr) == rtsql::OK;
-      for (RouteJob* j : save) {
-        sql.exec(db, "SAVEPOINT rq", nullptr, nullptr, nullptr);
+      if (db && !j->fallback && !j->status && j->asmb.ok && !j->request_route) b.save.push_back(j);
+  }
+
+  // the response bytes of a job whose assembly (and persistence, if any) is done
+  void finish(RouteJob* j) {
+    if (j->fallback) { n_fallback.fetch_add(1, std::memory_order_relaxed); return; }
+    if (j->status) return;
+    if (!j->asmb.ok) {
+      j->status = (j->request_route && cfg.compat200) ? 200 : 400;
+      j->out = rtr::error_body(j->asmb.error.empty() ? j->req.error : j->asmb.error);
+      return;
+    }
+    j->status = 200;
+    j->out = std::move(j->asmb.body);
+    if (!j->eta_iso.empty()) {
+      j->out += ",\"eta_minutes_ml\":";
+      rtr::put_float(j->out, (double)j->eta_min);
+      j->out += ",\"eta_completion_time_ml\":";
+      rtr::put_str(j->out, j->eta_iso);
+    }
+    if (!j->request_id.empty()) {
+      j->out += ",\"request_id\":";
+      rtr::put_str(j->out, j->request_id);
+      j->out += ",\"saved\":true";
+    }
+    j->out += "}}";
+  }
+
+  // Group commit: every flush waiting when the thread wakes goes into ONE transaction, one savepoint
+  // per request (a failed insert rolls back only its own request's rows -- SQLiteStore's
+  // per-request semantics).  A response leaves only after its commit, so a client that reads its
+  // request_id back (/api/history/<id>) finds it.
+  void persist_group(std::vector<std::vector<RouteJob*>>& groups) {
+    const std::string now = utc_now_iso();
+    const bool tx = step_once(st_begin);
+    for (auto& g : groups)
+      for (RouteJob* j : g) {
+        step_once(st_sp);
         j->request_id = persist_one(j, now);
-        if (j->request_id.empty()) sql.exec(db, "ROLLBACK TO rq", nullptr, nullptr, nullptr);
-        sql.exec(db, "RELEASE rq", nullptr, nullptr, nullptr);
+        if (j->request_id.empty()) step_once(st_rb);
+        step_once(st_rel);
       }
-      if (tx && sql.exec(db, "COMMIT", nullptr, nullptr, nullptr) != rtsql::OK) {
-        sql.exec(db, "ROLLBACK", nullptr, nullptr, nullptr);     // nothing of the flush was stored
-        for (RouteJob* j : save) j->request_id.clear();
-      }
-      for (RouteJob* j : save)
+    if (tx && !step_once(st_commit)) {
+      step_once(st_rollback);      // nothing of the group was stored
+      for (auto& g : groups)
+        for (RouteJob* j : g) j->request_id.clear();
+    }
+    for (auto& g : groups)
+      for (RouteJob* j : g)
         if (!j->request_id.empty()) n_persisted.fetch_add(1, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> lk(cmu);
+      ++commits;
     }
-    add_t(7, t0);
-    for (RouteJob* j : jobs) {
-      if (j->fallback) { n_fallback.fetch_add(1, std::memory_order_relaxed); continue; }
-      if (j->status) continue;
-      if (!j->asmb.ok) {
-        j->status = (j->request_route && cfg.compat200) ? 200 : 400;
-        j->out = rtr::error_body(j->asmb.error.empty() ? j->req.error : j->asmb.error);
-        continue;
+    ccv.notify_one();
+  }
+
+  bool step_once(void* st) {
+    const int rc = sql.step(st);
+    sql.reset(st);
+    return rc == rtsql::DONE;
+  }
+
+  void persist_loop() {
+    if (db) th_ckpt = std::thread([this] { ckpt_loop(); });
+    while (true) {
+      std::vector<std::vector<RouteJob*>> groups;
+      {
+        std::unique_lock<std::mutex> lk(pmu);
+        pcv.wait(lk, [&] { return asm_done || !pq.empty(); });
+        if (pq.empty()) break;
+        groups.assign(std::make_move_iterator(pq.begin()), std::make_move_iterator(pq.end()));
+        pq.clear();
+        pcv.notify_all();
       }
-      j->status = 200;
-      j->out = std::move(j->asmb.body);
-      if (!j->eta_iso.empty()) {
-        j->out += ",\"eta_minutes_ml\":";
-        rtr::put_float(j->out, (double)j->eta_min);
-        j->out += ",\"eta_completion_time_ml\":";
-        rtr::put_str(j->out, j->eta_iso);
-      }
-      if (!j->request_id.empty()) {
-        j->out += ",\"request_id\":";
-        rtr::put_str(j->out, j->request_id);
-        j->out += ",\"saved\":true";
-      }
-      j->out += "}}";
+      const double t0 = now_us();
+      persist_group(groups);
+      add_t(7, t0);
+      for (auto& g : groups)
+        for (RouteJob* j : g) {
+          finish(j);
+          done(j);
+        }
     }
+    if (th_ckpt.joinable()) {
+      {
+        std::lock_guard<std::mutex> lk(cmu);
+        ck_stop = true;
+      }
+      ccv.notify_all();
+      th_ckpt.join();
+    }
+  }
+
+  // WAL checkpoints on a connection of their own: the writer runs with wal_autocheckpoint=0, so the
+  // copy of WAL frames into the database file and its fsync (half of a commit's cost when the writer
+  // checkpoints itself) stay off the response path.  PASSIVE never blocks the writer.
+  void ckpt_loop() {
+    void* cdb = nullptr;
+    if (sql.open_v2(cfg.sqlite_path.c_str(), &cdb, rtsql::OPEN_READWRITE | rtsql::OPEN_URI | rtsql::OPEN_NOMUTEX,
+                    nullptr) != rtsql::OK) {
+      if (cdb) sql.close(cdb);
+      return;
+    }
+    sql.busy_timeout(cdb, 1000);
+    sql.exec(cdb, "PRAGMA synchronous=NORMAL", nullptr, nullptr, nullptr);
+    long long seen = 0;
+    while (true) {
+      {
+        std::unique_lock<std::mutex> lk(cmu);
+        ccv.wait(lk, [&] { return ck_stop || commits != seen; });
+        if (commits == seen && ck_stop) break;
+        seen = commits;
+      }
+      int log = 0, ck = 0;
+      sql.wal_checkpoint_v2(cdb, nullptr, rtsql::CHECKPOINT_PASSIVE, &log, &ck);
+      std::unique_lock<std::mutex> lk(cmu);     // at most one checkpoint per 20 ms
+      ccv.wait_for(lk, std::chrono::milliseconds(20), [&] { return ck_stop; });
+    }
+    int log = 0, ck = 0;
+    sql.wal_checkpoint_v2(cdb, nullptr, rtsql::CHECKPOINT_PASSIVE, &log, &ck);
+    sql.close(cdb);
   }
 };
 

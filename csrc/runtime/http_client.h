@@ -27,6 +27,7 @@ struct LoadResult {
   // per request kind: responses by status code (http_load_mixed)
   std::vector<std::vector<std::pair<int, long long>>> status_by_kind;
   std::vector<float> lat_us;   // sorted per-request latencies
+  std::vector<std::pair<float, float>> p50_p99_by_kind;   // http_load_mixed: per kind (us)
   double pct(double p) const {
     return lat_us.empty() ? 0.0 : (double)lat_us[std::min(lat_us.size() - 1, (size_t)(p * lat_us.size()))];
   }
@@ -155,6 +156,7 @@ inline LoadResult http_load_mixed(int port, int nconn, double seconds, const std
   std::atomic<long long> total{0}, errors{0}, bytes{0}, next{0};
   std::vector<std::vector<std::vector<long long>>> counts(nthreads, std::vector<std::vector<long long>>(nkinds, std::vector<long long>(600, 0)));
   std::vector<std::vector<float>> lat(nthreads);
+  std::vector<std::vector<std::vector<float>>> lat_k(nthreads, std::vector<std::vector<float>>(nkinds));
   const auto t_end = Clock::now() + std::chrono::microseconds((long long)(seconds * 1e6));
   auto send_next = [&](C& c) {
     const size_t k = (size_t)(next.fetch_add(1, std::memory_order_relaxed) % (long long)reqs.size());
@@ -212,7 +214,9 @@ inline LoadResult http_load_mixed(int port, int nconn, double seconds, const std
           bytes += (long long)(h + 4 + clen);
           c.in.erase(0, h + 4 + clen);
           const auto now = Clock::now();
-          lat[tid].push_back((float)std::chrono::duration<double, std::micro>(now - c.t0).count());
+          const float us = (float)std::chrono::duration<double, std::micro>(now - c.t0).count();
+          lat[tid].push_back(us);
+          lat_k[tid][c.kind].push_back(us);
           total++;
           if (now < t_end) {
             c.t0 = Clock::now();
@@ -243,6 +247,13 @@ inline LoadResult http_load_mixed(int port, int nconn, double seconds, const std
       for (int t = 0; t < nthreads; ++t) c += counts[t][k][code];
       if (c) res.status_by_kind[k].emplace_back(code, c);
     }
+  for (int k = 0; k < nkinds; ++k) {
+    std::vector<float> v;
+    for (int t = 0; t < nthreads; ++t) v.insert(v.end(), lat_k[t][k].begin(), lat_k[t][k].end());
+    std::sort(v.begin(), v.end());
+    auto at = [&](double p) { return v.empty() ? 0.f : v[std::min(v.size() - 1, (size_t)(p * v.size()))]; };
+    res.p50_p99_by_kind.emplace_back(at(0.5), at(0.99));
+  }
   return res;
 }
 

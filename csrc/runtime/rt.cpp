@@ -399,6 +399,9 @@ py::dict py_http_load_mixed(int port, int connections, double seconds, const std
     by.append(k);
   }
   d["status_by_kind"] = by;
+  py::list pk;
+  for (const auto& q : r.p50_p99_by_kind) pk.append(py::make_tuple(q.first, q.second));
+  d["p50_p99_us_by_kind"] = pk;
   return d;
 }
 

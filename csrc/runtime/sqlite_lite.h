@@ -36,6 +36,7 @@ struct Api {
   int (*column_bytes)(void*, int) = nullptr;
   const char* (*column_name)(void*, int) = nullptr;
   int (*changes)(void*) = nullptr;
+  int (*wal_checkpoint_v2)(void*, const char*, int, int*, int*) = nullptr;
 
   bool load(std::string& err) {
     if (h) return true;
@@ -70,6 +71,7 @@ struct Api {
     sym(column_bytes, "sqlite3_column_bytes");
     sym(column_name, "sqlite3_column_name");
     sym(changes, "sqlite3_changes");
+    sym(wal_checkpoint_v2, "sqlite3_wal_checkpoint_v2");
     if (!ok) err = "libsqlite3: missing symbols";
     return ok;
   }
@@ -78,6 +80,7 @@ struct Api {
 constexpr int OK = 0, ROW = 100, DONE = 101;
 constexpr int T_INTEGER = 1, T_FLOAT = 2, T_TEXT = 3, T_BLOB = 4, T_NULL = 5;
 constexpr int OPEN_READWRITE = 0x2, OPEN_CREATE = 0x4, OPEN_URI = 0x40, OPEN_NOMUTEX = 0x8000;
+constexpr int CHECKPOINT_PASSIVE = 0;
 inline void (*const TRANSIENT)(void*) = reinterpret_cast<void (*)(void*)>(-1);
 inline void (*const STATIC)(void*) = nullptr;      // the caller keeps the bytes alive until step/reset
 

@@ -248,7 +248,10 @@ def stack_soak(a, sv, app, model, route_req, eta_req, rng) -> int:
         out.update({"seconds": round(res["seconds"], 1), "requests": int(res["requests"]),
                     "req_per_s": round(res["requests"] / res["seconds"], 1), "transport_errors": int(res["errors"]),
                     "p50_ms": float(lat[len(lat) // 2]) / 1e3, "p99_ms": float(lat[int(len(lat) * 0.99) - 1]) / 1e3,
-                    "status_by_endpoint": by, "contract_errors": bad, "body_sample_errors": sample_errors,
+                    "status_by_endpoint": by,
+                    "p50_p99_ms_by_endpoint": {KINDS[k]: [round(q[0] / 1e3, 2), round(q[1] / 1e3, 2)]
+                                               for k, q in enumerate(res["p50_p99_us_by_kind"])},
+                    "contract_errors": bad, "body_sample_errors": sample_errors,
                     "native_route_jobs": f1["route_jobs"] - f0["route_jobs"], "relayed": f1["relayed"] - f0["relayed"],
                     "history_native": f1["history_native"] - f0["history_native"],
                     "route_flushes": f1["route_flushes"] - f0["route_flushes"],
