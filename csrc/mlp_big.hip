@@ -253,7 +253,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 // consecutive rows, one chunk) hit 16 distinct 16-byte bank groups.  Two stages (128 KB LDS, one
 // workgroup per CU): the loads of stage k+1 are in flight under stage k's 64 MFMAs per wave.
 // Workgroups are remapped XCD-aware (bijective for any grid) so the N/256 unit tiles of one
-// batch-row block run on one XCD and share its X tile through that XCD's L2.
+// batch-row block run on one XCD and share its X tile through that XCD's L2.  (A ring of four
+// 32-deep stages with three in flight and all 12 fragment reads issued before the MFMAs measured
+// SLOWER at the H = 1024 trainer's shape: 174 vs 161 us, profiles/gemm_probe_r4p.jsonl.)
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int G2T = 256, G2K = 64;
 constexpr int G2_STAGE = 2 * G2T * G2K * 2;          // A + B tile bytes per stage (64 KB)
@@ -937,10 +939,11 @@ static int gemm_tile() {
 }
 
 template <int EPI>
-static hipError_t launch_g256(const GemmArgs& a, dim3 grid, dim3 block, int lds, hipStream_t stream) {
+static hipError_t launch_g256(const GemmArgs& a, dim3 grid, dim3 block, hipStream_t stream) {
   static bool attr[64] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
+  const int lds = 2 * G2_STAGE;
   if (!attr[dev & 63]) {
     const hipError_t e = hipFuncSetAttribute((const void*)gemm256_kernel<EPI>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -959,11 +962,10 @@ hipError_t launch_gemm_nt(int epi,const void* W, int ldw, const void* X, int ldx
   if (N % G2T == 0 && K % G2K == 0 && gemm_tile() == 256) {
     GemmArgs a{(const __bf16*)W, (const __bf16*)X, ldw, ldx, N, M, K, b2, w3, ypart, (__bf16*)out, ldo, N / G2T};
     const dim3 grid((unsigned)((N / G2T) * ((M + G2T - 1) / G2T))), block(512);
-    const int lds = 2 * G2_STAGE;
     switch (epi) {
-      case EPI_Y: return launch_g256<EPI_Y>(a, grid, block, lds, stream);
-      case EPI_H2Y: return launch_g256<EPI_H2Y>(a, grid, block, lds, stream);
-      case EPI_STORE: return launch_g256<EPI_STORE>(a, grid, block, lds, stream);
+      case EPI_Y: return launch_g256<EPI_Y>(a, grid, block, stream);
+      case EPI_H2Y: return launch_g256<EPI_H2Y>(a, grid, block, stream);
+      case EPI_STORE: return launch_g256<EPI_STORE>(a, grid, block, stream);
       default: return hipErrorInvalidValue;
     }
   }

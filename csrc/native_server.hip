@@ -136,6 +136,28 @@ struct Shared {
     h.consec.store(0, std::memory_order_relaxed);
     if (h.quarantined.load(std::memory_order_relaxed)) h.quarantined.store(false);
   }
+  // Micro-cache of the app's GET /api/health and GET /metrics answers (ROUTEST_FRONT_CACHE_MS,
+  // default 250; 0 = relay every one): a probe or scrape served from the last answer while it is
+  // younger than the TTL, or while one relay refreshes it (stale-while-revalidate), so at most one
+  // such request per TTL crosses into the single Python process.  Both answers are snapshots of
+  // process state anyway (uptime, counters); only requests WITHOUT an Origin header use the cache
+  // (the app's CORS headers depend on it).
+  struct CacheEnt {
+    std::string resp;                  // full HTTP response bytes (status line .. body)
+    long long t_ms = -1;
+    uint64_t sig = 0;                  // state_sig() when stored: a hot swap or a quarantine change
+    bool inflight = false;             // invalidates it at once
+  };
+  uint64_t state_sig() const {
+    uint64_t v = epoch.load(std::memory_order_relaxed) * 0x9E3779B97F4A7C15ull;
+    for (const auto& h : health)
+      v = v * 1000003ull + (uint64_t)h->quarantines.load(std::memory_order_relaxed) * 2 +
+          (h->quarantined.load(std::memory_order_relaxed) ? 1 : 0);
+    return v;
+  }
+  std::mutex rc_mu;
+  CacheEnt rc[2];
+  long long rc_ttl_ms = 250;
   // park the slot's resident scorer (before a normal launch that may share its hardware queue)
   void park(int g) {
     if (g < 0 || g >= (int)scorers.size()) return;
@@ -157,7 +179,10 @@ struct Conn {
   std::string up_out, up_in;
   size_t up_off = 0;
   bool up_head = false;  // the relayed request was HEAD (no response body)
+  bool up_wait = false;  // a relayed request's answer is outstanding (async also covers route jobs)
   bool tunnel = false;   // streamed upstream answer: bytes flow both ways unparsed from now on
+  int cache_slot = -1;   // the relayed request refreshes Shared::rc[cache_slot]
+  long long up_used_ms = 0;   // last request written to / answer read from the upstream connection
 };
 
 // A route job's reactor-side context.
@@ -183,7 +208,8 @@ struct Pending {
 
 struct Stats {
   std::atomic<long long> requests{0}, predictions{0}, launches{0}, errors{0}, resident{0}, fallbacks{0},
-      wire8{0}, route_requests{0}, route_fallbacks{0}, relayed{0}, failovers{0}, cpu_rounds{0}, history{0};
+      wire8{0}, route_requests{0}, route_fallbacks{0}, relayed{0}, failovers{0}, cpu_rounds{0}, history{0},
+      cached{0};
 };
 
 inline Stamp now_local() {
@@ -554,6 +580,26 @@ class Reactor {
     const bool no_model = (is_pe || is_p) && method == "POST" && cfg_.sh->model(cfg_.slot) == nullptr;
     if (!(is_pe || is_p) || method != "POST" || no_model) {
       if (cfg_.upstream_port > 0) {
+        const int slot = (method == "GET" && origin.empty() && cfg_.sh->rc_ttl_ms > 0)
+                             ? (path == "/api/health" ? 0 : (path == "/metrics" ? 1 : -1)) : -1;
+        if (slot >= 0) {
+          Shared& sh = *cfg_.sh;
+          std::unique_lock<std::mutex> lk(sh.rc_mu);
+          Shared::CacheEnt& e = sh.rc[slot];
+          const long long now = mono_ms();
+          if (e.t_ms >= 0 && e.sig == sh.state_sig() && (now - e.t_ms < sh.rc_ttl_ms || e.inflight)) {
+            if (c.npending > 0) { lk.unlock(); run_batch(); lk.lock(); }
+            c.out += e.resp;
+            lk.unlock();
+            st_.cached.fetch_add(1, std::memory_order_relaxed);
+            if (!keep) c.close_after = true;
+            return;
+          }
+          if (!e.inflight) {
+            e.inflight = true;
+            c.cache_slot = slot;
+          }
+        }
         relay(c, raw, method == "HEAD");
         return;
       }
@@ -736,10 +782,25 @@ class Reactor {
     return true;
   }
 
+  // uvicorn closes a keep-alive connection after 5 idle seconds; a request written as that close
+  // crosses it would come back as a 502, so an upstream connection idle for 2 s is replaced first
+  // (with most relays answered from the micro-cache, client connections idle upstream for long)
+  bool connect_fresh_up(Conn& c) {
+    const long long now = mono_ms();
+    if (c.up >= 0 && !c.tunnel && now - c.up_used_ms > 2000) {
+      epoll_ctl(ep_, EPOLL_CTL_DEL, c.up, nullptr);
+      up2c_.erase(c.up);
+      close(c.up);
+      c.up = -1;
+    }
+    c.up_used_ms = now;
+    return connect_up(c);
+  }
+
   void relay(Conn& c, const std::string& raw, bool head) {
     if (c.npending > 0) run_batch();
     flush(c);
-    if (!connect_up(c)) {
+    if (!connect_fresh_up(c)) {
       respond(c, 502, "{\"error\":\"upstream app unavailable\"}", "", true);
       flush(c);
       return;
@@ -747,6 +808,7 @@ class Reactor {
     st_.relayed.fetch_add(1, std::memory_order_relaxed);
     c.up_out += raw;
     c.up_head = head;
+    c.up_wait = true;
     c.async = true;
     flush_up(c);
   }
@@ -755,7 +817,7 @@ class Reactor {
   void start_tunnel(Conn& c) {
     if (c.npending > 0) run_batch();
     flush(c);
-    if (!connect_up(c)) {
+    if (!connect_fresh_up(c)) {
       respond(c, 502, "{\"error\":\"upstream app unavailable\"}", "", true);
       flush(c);
       return;
@@ -779,7 +841,23 @@ class Reactor {
     c.up_off = 0;
   }
 
+  // a cacheable relay ended: store its answer (a complete 200) or just clear the refresh flag
+  void cache_done(Conn& c, const std::string* resp, size_t n) {
+    Shared& sh = *cfg_.sh;
+    std::lock_guard<std::mutex> lk(sh.rc_mu);
+    Shared::CacheEnt& e = sh.rc[c.cache_slot];
+    if (resp != nullptr && resp->compare(0, 9, "HTTP/1.1 ") == 0 &&
+        resp->find("\r\nconnection: close", 0) > n) {      // (an answer that closes is not reused)
+      e.resp.assign(*resp, 0, n);
+      e.t_ms = mono_ms();
+      e.sig = sh.state_sig();
+    }
+    e.inflight = false;
+    c.cache_slot = -1;
+  }
+
   void upstream_closed(Conn& c) {
+    if (c.cache_slot >= 0) cache_done(c, nullptr, 0);
     if (c.up < 0) return;
     epoll_ctl(ep_, EPOLL_CTL_DEL, c.up, nullptr);
     up2c_.erase(c.up);
@@ -791,7 +869,8 @@ class Reactor {
       flush(c);
       return;
     }
-    if (c.async) {                     // no (complete) answer came back
+    if (c.up_wait) {                   // no (complete) answer came back
+      c.up_wait = false;
       if (!c.up_in.empty() && c.up_in.find("\r\n\r\n") != std::string::npos && !c.up_in.empty()) {
         c.out += c.up_in;              // read-until-close body
         c.up_in.clear();
@@ -837,7 +916,7 @@ class Reactor {
 
   // one relayed response: status line + headers + (content-length | chunked -> tunnel | none)
   void parse_upstream(Conn& c) {
-    while (c.async && !c.up_in.empty()) {
+    while (c.up_wait && !c.up_in.empty()) {
       const size_t hend = c.up_in.find("\r\n\r\n");
       if (hend == std::string::npos) return;
       int code = 0;
@@ -869,6 +948,7 @@ class Reactor {
       const bool no_body = c.up_head || code == 204 || code == 304;
       if (chunked && !no_body) {       // streamed answer (SSE): tunnel from here on
         c.tunnel = true;
+        c.up_wait = false;
         c.async = false;
         c.out += c.up_in;
         c.up_in.clear();
@@ -881,9 +961,12 @@ class Reactor {
       if (!has_len && !no_body) return;          // body until close (upstream_closed delivers it)
       const size_t total = hend + 4 + (no_body ? 0 : clen);
       if (c.up_in.size() < total) return;
+      if (c.cache_slot >= 0) cache_done(c, code == 200 && has_len ? &c.up_in : nullptr, total);
       c.out.append(c.up_in, 0, total);
       c.up_in.erase(0, total);
+      c.up_wait = false;
       c.async = false;
+      c.up_used_ms = mono_ms();
       flush(c);
       if (!c.close_after) {
         parse_requests(c);                       // requests that arrived meanwhile
@@ -1086,6 +1169,7 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
   Shared& sh = s->sh;
   if (const char* v = std::getenv("ROUTEST_QUARANTINE_AFTER")) sh.quarantine_after = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("ROUTEST_QUARANTINE_PROBE_MS")) sh.probe_ms = std::max(1ll, std::atoll(v));
+  if (const char* v = std::getenv("ROUTEST_FRONT_CACHE_MS")) sh.rc_ttl_ms = std::max(0ll, std::atoll(v));
   sh.devices = devices;
   sh.models = models;
   sh.epoch = 1;
@@ -1238,7 +1322,7 @@ void native_server_stop(int64_t h) {
 
 std::vector<long long> native_server_stats(int64_t h) {
   std::lock_guard<std::mutex> lk(g_srv_mu);
-  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(31, 0);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(32, 0);
   Server* s = g_servers[h];
   std::vector<long long> v = {s->stats.requests.load(), s->stats.predictions.load(), s->stats.launches.load(),
                               s->stats.errors.load(), s->stats.resident.load(), s->stats.fallbacks.load(),
@@ -1253,6 +1337,7 @@ std::vector<long long> native_server_stats(int64_t h) {
   v.push_back(s->stats.failovers.load());
   v.push_back(s->stats.cpu_rounds.load());
   v.push_back(s->stats.history.load());
+  v.push_back(s->stats.cached.load());
   return v;
 }
 

@@ -272,7 +272,7 @@ struct RouteService::Impl {
       db = nullptr;
       return;
     }
-    sql.busy_timeout(db, 10000);
+    sql.wait_on_locks(db);
     sql.exec(db, "PRAGMA journal_mode=WAL", nullptr, nullptr, nullptr);
     // WAL + NORMAL: a commit appends to the WAL without an fsync (the WAL is synced at checkpoints);
     // FULL would fsync every flush's commit
@@ -1427,7 +1427,7 @@ struct RouteService::Impl {
       if (cdb) sql.close(cdb);
       return;
     }
-    sql.busy_timeout(cdb, 1000);
+    sql.wait_on_locks(cdb);
     sql.exec(cdb, "PRAGMA synchronous=NORMAL", nullptr, nullptr, nullptr);
     long long seen = 0;
     while (true) {

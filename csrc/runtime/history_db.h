@@ -35,7 +35,7 @@ class HistoryDb {
       close();
       return false;
     }
-    sql_.busy_timeout(db_, 10000);
+    sql_.wait_on_locks(db_);
     sql_.exec(db_, "PRAGMA foreign_keys=ON", nullptr, nullptr, nullptr);
     return true;
   }

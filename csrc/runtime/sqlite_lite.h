@@ -1,13 +1,15 @@
 // Minimal run-time binding of the system SQLite library (libsqlite3.so.0, the same library Python's
 // sqlite3 module uses; the image ships no sqlite3.h).  The native route service writes the
 // reference's two persistence rows (RO/Flaskr/routes.py:134-182; routest_amd/store/store.py
-// SQLiteStore) into the same database file the Python store reads, in WAL mode with a busy timeout
-// so both connections interleave safely.
+// SQLiteStore) into the same database file the Python store reads, in WAL mode with a short-sleep
+// busy handler so the connections interleave safely.
 #pragma once
 #include <dlfcn.h>
 
+#include <chrono>
 #include <cstdint>
 #include <string>
+#include <thread>
 
 namespace rtsql {
 
@@ -37,6 +39,7 @@ struct Api {
   const char* (*column_name)(void*, int) = nullptr;
   int (*changes)(void*) = nullptr;
   int (*wal_checkpoint_v2)(void*, const char*, int, int*, int*) = nullptr;
+  int (*busy_handler)(void*, int (*)(void*, int), void*) = nullptr;
 
   bool load(std::string& err) {
     if (h) return true;
@@ -72,9 +75,20 @@ struct Api {
     sym(column_name, "sqlite3_column_name");
     sym(changes, "sqlite3_changes");
     sym(wal_checkpoint_v2, "sqlite3_wal_checkpoint_v2");
+    sym(busy_handler, "sqlite3_busy_handler");
     if (!ok) err = "libsqlite3: missing symbols";
     return ok;
   }
+
+  // Waits for a lock another connection holds in short sleeps (50 us, then 200 us, then 1 ms; ~20 s
+  // in all) — sqlite3_busy_timeout's back-off sleeps 1, 2, 5, 10 ... 100 ms, so a native DELETE
+  // that met the route persister's group commit (a millisecond) waited tens of milliseconds.
+  static int short_sleeps(void*, int n) {
+    if (n >= 20000) return 0;
+    std::this_thread::sleep_for(std::chrono::microseconds(n < 20 ? 50 : (n < 200 ? 200 : 1000)));
+    return 1;
+  }
+  void wait_on_locks(void* db) { busy_handler(db, &Api::short_sleeps, nullptr); }
 };
 
 constexpr int OK = 0, ROW = 100, DONE = 101;

@@ -166,7 +166,9 @@ class NativePredictServer:
                  # rounds re-run on another GPU slot (failover) / on the CPU forward (no GPU left)
                  "failovers", "cpu_rounds",
                  # history / locations requests answered from the store's database natively
-                 "history_native")
+                 "history_native",
+                 # GET /api/health and /metrics answered from the front end's micro-cache
+                 "cached")
         return dict(zip(names, v))
 
     def close(self) -> None:

@@ -171,6 +171,44 @@ def test_relayed_requests_match_the_app(hav, method, path, body):
         assert set(json.loads(a[1])) == set(json.loads(b[1]))
 
 
+def test_health_and_metrics_micro_cache(hav):
+    """GET /api/health and /metrics without an Origin header are answered from the front end's
+    micro-cache (ROUTEST_FRONT_CACHE_MS, default 250 ms) while the last app answer is fresh: same
+    bytes as that answer, no relay.  With an Origin header (CORS depends on it) they are relayed."""
+    import time
+    st, sv = hav
+    time.sleep(0.3)                                           # whatever an earlier test cached is stale
+    f0 = st.front.stats()
+    a = _req(st.port, "GET", "/metrics")
+    b = _req(st.port, "GET", "/metrics")
+    f1 = st.front.stats()
+    assert a[0] == b[0] == 200 and a[1] == b[1]
+    assert f1["relayed"] - f0["relayed"] == 1 and f1["cached"] - f0["cached"] == 1
+    h1 = _req(st.port, "GET", "/api/health")
+    h2 = _req(st.port, "GET", "/api/health")
+    assert h1[0] == h2[0] == 200 and h1[1] == h2[1] and "status" in json.loads(h1[1])
+    f2 = st.front.stats()
+    assert f2["cached"] - f1["cached"] == 1
+    o = _req(st.port, "GET", "/api/health", headers={"Origin": "http://localhost:3000"})
+    assert o[0] == 200 and st.front.stats()["relayed"] == f2["relayed"] + 1
+    time.sleep(0.3)                                           # stale: the next one refreshes
+    _req(st.port, "GET", "/metrics")
+    assert st.front.stats()["relayed"] == f2["relayed"] + 2
+
+
+def test_relay_after_idle_upstream_connection(hav):
+    """uvicorn closes an idle keep-alive connection after 5 s: a relay on a client connection whose
+    upstream connection sat idle that long goes out on a fresh one (it used to race the close and
+    come back as a 502)."""
+    import time
+    st, sv = hav
+    c = http.client.HTTPConnection("127.0.0.1", st.port, timeout=60)
+    assert _req(st.port, "GET", "/no/such/route", conn=c)[0] == 404     # relayed: opens the upstream
+    time.sleep(5.6)
+    for _ in range(3):
+        assert _req(st.port, "GET", "/no/such/route", conn=c)[0] == 404
+
+
 def test_history_and_locations_answered_natively_byte_identical(hav):
     """GET/DELETE /api/history[/<id>] and GET /api/locations come from the store's SQLite file in
     C++ (csrc/runtime/history_db.h): same status and bytes as the app for every limit form."""

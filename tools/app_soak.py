@@ -254,6 +254,7 @@ def stack_soak(a, sv, app, model, route_req, eta_req, rng) -> int:
                     "contract_errors": bad, "body_sample_errors": sample_errors,
                     "native_route_jobs": f1["route_jobs"] - f0["route_jobs"], "relayed": f1["relayed"] - f0["relayed"],
                     "history_native": f1["history_native"] - f0["history_native"],
+                    "cached": f1["cached"] - f0["cached"],
                     "route_flushes": f1["route_flushes"] - f0["route_flushes"],
                     "route_stage_ms_per_flush": {k[9:]: round((f1[k] - f0[k]) / 1e3 / max(1, f1["route_flushes"] - f0["route_flushes"]), 3)
                                                  for k in f1 if k.startswith("route_us_")},
