@@ -614,7 +614,7 @@ void wgrad_dual(torch::Tensor A0, int64_t M0, torch::Tensor B0, int64_t N0, torc
 
 void wgrad_reduce(torch::Tensor slab, torch::Tensor G, c10::optional<torch::Tensor> slab1,
                   c10::optional<torch::Tensor> G1, c10::optional<torch::Tensor> slab2,
-                  c10::optional<torch::Tensor> G2) {
+                  c10::optional<torch::Tensor> G2, int64_t perm_h) {
   auto chk = [&](const torch::Tensor& sl, const torch::Tensor& g) {
     check_dev(sl, "slab");
     check_dev(g, "G");
@@ -638,7 +638,7 @@ void wgrad_reduce(torch::Tensor slab, torch::Tensor G, c10::optional<torch::Tens
       two ? G1->data_ptr<float>() : nullptr, two ? (int)G1->numel() : 0,
       three ? slab2->data_ptr<float>() : nullptr, three ? (int)slab2->size(0) : 0,
       three ? (long long)slab2->size(1) : 0, three ? G2->data_ptr<float>() : nullptr,
-      three ? (int)G2->numel() : 0));
+      three ? (int)G2->numel() : 0, (int)perm_h));
 }
 
 void check_csr(const torch::Tensor& indptr, const torch::Tensor& indices, const torch::Tensor& values) {
@@ -1343,7 +1343,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_dual", &wgrad_dual, "two split-K weight-gradient GEMMs (dW2|db2 and dW1) in one launch");
   m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs (optionally a second and third region)",
         py::arg("slab"), py::arg("G"), py::arg("slab1") = py::none(), py::arg("G1") = py::none(),
-        py::arg("slab2") = py::none(), py::arg("G2") = py::none());
+        py::arg("slab2") = py::none(), py::arg("G2") = py::none(), py::arg("perm_h") = 0);
   m.def("train_fwd_grid", [](int64_t B, int64_t dev) { return (int64_t)rt::train_fwd_grid((int)B, num_cus((int)dev)); },
         "workgroups of the training forward = rows of its dW3 slab");
   m.def("num_cus", [](int64_t dev) { return (int64_t)num_cus((int)dev); });

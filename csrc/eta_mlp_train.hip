@@ -416,8 +416,9 @@ __device__ __forceinline__ void mfma_drain(f32x16& x, f32x16& y) {
 // stages; within a tile the fragments of hidden tile mt + 1 are read while mt's 8 MFMAs (four
 // interleaved accumulation chains) run.  LDS = W2 image (H*H*2 B) + two dz2 tiles (2 * H * 64 B):
 // exactly 160 KB at H = 256.  Measured at 1M rows: 377 us (profiles/train_kernel_stats_1m_r3_v3.csv).
-// Partial sums of slice s go to slab[s] in the bucket layout (hperm rows and columns,
-// train/fused.py); wgrad_reduce sums them in a fixed order (deterministic).
+// Partial sums of slice s go to slab[s]: dW2 in the register-native layout (one 16-byte store per
+// lane and 4 accumulator registers; wgrad.hip native_to_bucket), dW1 in the bucket layout (hperm
+// rows, train/fused.py); wgrad_reduce sums them in a fixed order (deterministic) into the bucket.
 // PROF (ROUTEST_TRAIN_BWD_PROF=1, diagnostics only): s_memtime per tile segment — [0] the loop-top
 // wait + barrier, [1] staging issue + layer 1, [2] the hidden-tile loop, [3] dW1 — summed per wave
 // into prof[wave][4] (scalar registers: the timed code keeps its VGPR allocation)
@@ -691,32 +692,41 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
   // the last dW2 MFMAs were issued through inline asm, which the hazard recognizer does not see: give
   // them their 16 passes before the epilogue reads the accumulators
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  // D[m][n]: lane -> n = col, register e -> m = (e&3) + 8(e>>2) + 4h; rows / columns to the bucket's
-  // hperm order (the stored unit order of every other gradient path)
+  // dW2 partial in the REGISTER-NATIVE slab layout (train_slab2_index; wgrad_reduce maps it to the
+  // bucket): accumulator tile (w, i, mt) is 1024 contiguous floats, registers 4q .. 4q+3 of lane l at
+  // q*256 + 4l — one 16-byte store per lane and 4 registers, 1 KB per wave-instruction.  (Stored in
+  // the bucket's [row][hperm col] order, the same partial took 4x the store instructions: one dword
+  // per lane, 256 per wave, an issue-bound tail of ~256 KB per workgroup after the last tile.)
   float* o2 = slab2 + (size_t)blockIdx.x * H * LDG;
   float* o1 = slab1 + (size_t)blockIdx.x * H * 16;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      f32x4* t = reinterpret_cast<f32x4*>(o2 + (size_t)(((2 * w + i) * MT + mt) * 1024)) + lane;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        t[64 * q] = (f32x4){acc2[mt][i][4 * q], acc2[mt][i][4 * q + 1], acc2[mt][i][4 * q + 2], acc2[mt][i][4 * q + 3]};
+    }
+  // D[m][n] of dW1: lane -> n = col, register e -> m = (e&3) + 8(e>>2) + 4h, rows in hperm order
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int mo = (e & 3) + 8 * (e >> 2) + 4 * h;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int nc = hperm(32 * (2 * w + i) + col);
-#pragma unroll
-      // (dW2's A rows came out of the hperm-ordered image: D row 32mt + mo IS bucket row 32mt + mo)
-      for (int mt = 0; mt < MT; ++mt) o2[(size_t)(32 * mt + mo) * LDG + nc] = acc2[mt][i][e];
+    for (int i = 0; i < 2; ++i)
       if (col < 16) o1[(size_t)hperm(32 * (2 * w + i) + mo) * 16 + col] = acc1[i][e];
-    }
   }
-  // db2 column (and the zero columns H+1 .. H+15): both lane halves hold rows of image column
-  // 32(2w+i) + col
+  // db2 column (and the zero columns H+1 .. H+15) past the H*H native block, [bucket row][16]: both
+  // lane halves hold rows of image column 32(2w+i) + col (image column = bucket row)
+  float* oc = o2 + (size_t)H * H;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const float d = db2[i] + __shfl_xor(db2[i], 32);
-    const int ur = 32 * (2 * w + i) + col;          // (image column = bucket row, as above)
-    if (h == 0) o2[(size_t)ur * LDG + H] = d;
+    const int ur = 32 * (2 * w + i) + col;
+    if (h == 0) oc[(size_t)ur * 16] = d;
     else
 #pragma unroll
-      for (int c = 1; c < 16; ++c) o2[(size_t)ur * LDG + H + c] = 0.f;
+      for (int c = 1; c < 16; ++c) oc[(size_t)ur * 16 + c] = 0.f;
   }
 }
 

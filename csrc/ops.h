@@ -84,7 +84,7 @@ hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, 
                                hipStream_t stream, const float* slab1 = nullptr, int S1 = 0,
                                long long slab_stride1 = 0, float* G1 = nullptr, int n1 = 0,
                                const float* slab2 = nullptr, int S2 = 0, long long slab_stride2 = 0,
-                               float* G2 = nullptr, int n2 = 0);
+                               float* G2 = nullptr, int n2 = 0, int perm_h0 = 0);
 size_t wgrad_lds_bytes(int NT);
 // two independent wgrad GEMMs (segment 1: N <= 32) in one launch, same K
 hipError_t launch_wgrad_dual(const void* A0, int lda0, int M0, int Mout0, const void* B0, int ldb0,

@@ -251,8 +251,31 @@ struct RedSeg {
   long long slab_stride;
   float* G;
   int S, n;
+  int perm_h;        // 0: slab and G share a layout; H: train_bwd_kernel<H>'s register-native dW2 slabs
 };
 
+__device__ __forceinline__ int red_hperm(int u) { return (u & ~12) | ((u & 4) << 1) | ((u & 8) >> 1); }
+
+// G's index of slab element e (e % 4 == 0) and the stride of its 3 successors in the register-native
+// layout of train_bwd_kernel<H> (eta_mlp_train.hip): accumulator tile (w, i, mt) = 1024 floats, lane
+// l's registers 4q .. 4q+3 at q*256 + 4l — rows 32mt + 8q + 4(l >> 5) + j of bucket column
+// hperm(32(2w+i) + (l & 31)); past H*H the [row][16] block of the db2 / zero columns.
+__device__ __forceinline__ void native_to_bucket(int e, int H, int& g0, int& step) {
+  const int LDG = H + 16, MT = H / 32;
+  if (e >= H * H) {
+    const int x = e - H * H;
+    g0 = (x >> 4) * LDG + H + (x & 15);
+    step = 1;
+    return;
+  }
+  const int blk = e >> 10, rem = e & 1023, q = rem >> 8, l = (rem & 255) >> 2;
+  const int wi = blk / MT, mt = blk - wi * MT;
+  const int nc = red_hperm(32 * wi + (l & 31));
+  g0 = (32 * mt + 8 * q + 4 * (l >> 5)) * LDG + nc;
+  step = LDG;
+}
+
+template <bool NTLOAD>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(RedSeg s0, RedSeg s1, RedSeg s2, int nb0,
                                                            int nb01) {
   const int bx = (int)blockIdx.x;
@@ -272,7 +295,9 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(RedSeg s0, RedSeg s1,
     if (vec) {
       f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
       auto ld = [&](int k) {
-        return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(slab + (long long)k * slab_stride + e));
+        const f32x4* q = reinterpret_cast<const f32x4*>(slab + (long long)k * slab_stride + e);
+        if constexpr (NTLOAD) return __builtin_nontemporal_load(q);
+        else return *q;
       };
       int s = sl;
       for (; s + 3 * RED_SL < S; s += 4 * RED_SL) {
@@ -299,7 +324,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(RedSeg s0, RedSeg s1,
       const float4 v = part[k][c];
       r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
     }
-    if (vec) {
+    if (sg.perm_h > 0) {
+      int g0, step;
+      native_to_bucket(e, sg.perm_h, g0, step);
+      G[g0] = r.x;
+      G[g0 + step] = r.y;
+      G[g0 + 2 * step] = r.z;
+      G[g0 + 3 * step] = r.w;
+    } else if (vec) {
       *reinterpret_cast<float4*>(G + e) = r;
     } else {
       const float rr[4] = {r.x, r.y, r.z, r.w};
@@ -443,16 +475,24 @@ hipError_t launch_wgrad_dual(const void* A0, int lda0, int M0, int Mout0, const 
 hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, float* G, int n,
                                hipStream_t stream, const float* slab1, int S1,
                                long long slab_stride1, float* G1, int n1, const float* slab2, int S2,
-                               long long slab_stride2, float* G2, int n2) {
-  const RedSeg s0{slab, slab_stride, G, S, n};
-  const RedSeg s1{slab1, slab_stride1, G1, S1, slab1 ? n1 : 0};
-  const RedSeg s2{slab2, slab_stride2, G2, S2, slab2 ? n2 : 0};
+                               long long slab_stride2, float* G2, int n2, int perm_h0) {
+  if (perm_h0 > 0 && (perm_h0 % 64 || n != perm_h0 * (perm_h0 + 16))) return hipErrorInvalidValue;
+  const RedSeg s0{slab, slab_stride, G, S, n, perm_h0};
+  const RedSeg s1{slab1, slab_stride1, G1, S1, slab1 ? n1 : 0, 0};
+  const RedSeg s2{slab2, slab_stride2, G2, S2, slab2 ? n2 : 0, 0};
   const int nb0 = (n + 4 * RED_COLS - 1) / (4 * RED_COLS);
   const int nb1 = (s1.n + 4 * RED_COLS - 1) / (4 * RED_COLS);
   const int nb2 = (s2.n + 4 * RED_COLS - 1) / (4 * RED_COLS);
   if (nb0 + nb1 + nb2 == 0) return hipSuccess;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb0 + nb1 + nb2), dim3(256), 0, stream, s0, s1, s2, nb0,
-                     nb0 + nb1);
+  // slab reads: plain loads (default: the slabs were written just before and partly sit in L2 / the
+  // Infinity Cache; 64k-row step 75.1 -> 73.6 us, profiles/train_r4u.jsonl) or nontemporal
+  // (ROUTEST_RED_NT=1)
+  static const bool nt = [] {
+    const char* v = std::getenv("ROUTEST_RED_NT");
+    return v && std::atoi(v) == 1;
+  }();
+  if (nt) hipLaunchKernelGGL(wgrad_reduce_kernel<true>, dim3(nb0 + nb1 + nb2), dim3(256), 0, stream, s0, s1, s2, nb0, nb0 + nb1);
+  else hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(nb0 + nb1 + nb2), dim3(256), 0, stream, s0, s1, s2, nb0, nb0 + nb1);
   return hipGetLastError();
 }
 

@@ -212,7 +212,7 @@ class FusedMlp3Trainer:
         ldg = H + 16
         C.train_bwd(self.xf, rec.shape[0], self.blob, H, self.dz2r, self.slab2, self.slab)
         C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg + ldg:],
-                       self.w3slab, self.G[H * ldg:H * ldg + ldg])
+                       self.w3slab, self.G[H * ldg:H * ldg + ldg], perm_h=H)   # dW2 slabs: register-native
 
     def step(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> torch.Tensor:
         """One optimizer step; returns the device tensor of per-row squared errors (no sync)."""

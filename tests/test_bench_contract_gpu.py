@@ -54,7 +54,7 @@ def test_bench_spawns_ranks_itself_shared_gpu():
 
 
 def test_bench_route_optimizer_probe():
-    """Config 5 inside bench.py: K5 + K6 + one batched A* launch per step, every leg found."""
+    """Config 5 inside bench.py: road matrices + K6 + the legs on the CCH per step, every leg found."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
                         "--batch", "262144", "--p50", "0", "--rec16-steps", "0", "--train-steps", "0",
                         "--gcn-steps", "0", "--route-requests", "2000", "--route-steps", "2"],
@@ -63,7 +63,7 @@ def test_bench_route_optimizer_probe():
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     ro = d["route_optimizer"]
     assert ro["requests_per_step"] == 2000 and ro["steps"] == 2
-    assert ro["astar_unfound_legs"] == 0 and ro["requests_per_s"] > 1e3
+    assert ro["engine"] == "cch" and ro["unfound_legs"] == 0 and ro["requests_per_s"] > 1e3
 
 
 def test_bench_fails_loud_on_too_many_gpus():
