@@ -1124,7 +1124,7 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
       // reach (2N entries): long searches first means the longest ones grow at the same time, and on
       // a 1M-node graph that exhausted the arena and sent 18k searches to the chunked retry (1M-node
       // local step 739 -> 1630 ms; 100k-node route step 150 -> 124.6 ms with it,
-      // profiles/astar_lpt_arena_ab_r3aa.jsonl).  ROUTEST_ASTAR_LPT=0 | 1 forces it off | on.
+      // profiles/superseded/astar_lpt_arena_ab_r3aa.jsonl).  ROUTEST_ASTAR_LPT=0 | 1 forces it off | on.
       static const int lpt_env = [] {
         const char* v = std::getenv("ROUTEST_ASTAR_LPT");
         return v == nullptr ? -1 : (std::atoi(v) != 0 ? 1 : 0);
@@ -1157,7 +1157,7 @@ hipError_t astar_search(const AstarGraphDev& g, const int* src, const int* dst, 
   // the wave tier a chunk at a time (the arena restarts per launch), so each can grow into
   // ROUTEST_ASTAR_RETRY_ENTRIES (default 2^20) entries — on a 1M-node graph thousands of local legs
   // overflowed a 32k-search launch's share, and the few big-tier slots then ran them ~100 at a time
-  // for seconds (profiles/astar_scale_1m_r3n.jsonl).  Only what overflows again goes to the big tier.
+  // for seconds (profiles/superseded/astar_scale_1m_r3n.jsonl).  Only what overflows again goes to the big tier.
   bool wave_timed = false;
   // the reruns and the big tier hold the LARGE searches (f-bands of thousands of nodes): a workgroup
   // of ROUTEST_ASTAR_RETRY_WAVES (default 4; 1, 2, 8) waves per search instead of one wave

@@ -351,7 +351,7 @@ size_t wgrad_lds_bytes(int NT, int KB) {
 size_t wgrad_lds_bytes(int NT) { return wgrad_lds_bytes(NT, 32); }
 
 // rows staged per barrier: ROUTEST_WGRAD_KB = 32 | 64 (default: 2x the bytes in flight per CU,
-// wgrad<3> 23.7 -> 20.9 us, profiles/train_wgrad_ab_r2.md) | 128
+// wgrad<3> 23.7 -> 20.9 us, profiles/superseded/train_wgrad_ab_r2.md) | 128
 static int wgrad_kb() {
   static const int kb = [] {
     const char* v = std::getenv("ROUTEST_WGRAD_KB");

@@ -399,7 +399,7 @@ def create_app(services: Optional[Services] = None, settings: Optional[Settings]
         """One request through the cross-request GPU batcher when enabled, else inline.  With the
         road-graph provider every request is batched (one A* launch per flush: 9x the per-request
         req/s); haversine requests below ``route_gpu_min_stops`` destinations stay inline (their
-        10x10 greedy is cheaper than a queue hop: 1.26k vs 0.97k req/s, profiles/route_http_r2.jsonl)."""
+        10x10 greedy is cheaper than a queue hop: 1.26k vs 0.97k req/s, profiles/superseded/route_http_r2.jsonl)."""
         if sv.route_batcher is not None:
             dests = payload.get("destination_points") if isinstance(payload, dict) else None
             if (getattr(sv.provider, "name", "") == "graph" or

@@ -77,7 +77,7 @@ class Settings:
     route_batch_max: int = 1024          # ROUTEST_ROUTE_BATCH_MAX: requests per optimizer flush
     route_batch_timeout_us: int = 500    # ROUTEST_ROUTE_BATCH_TIMEOUT_US
     route_gpu_min_stops: int = 32        # ROUTEST_ROUTE_GPU_MIN_STOPS: haversine requests with fewer
-                                         # destinations stay inline (profiles/route_http_r2.jsonl)
+                                         # destinations stay inline (profiles/superseded/route_http_r2.jsonl)
     warm_scorer: bool = True             # ROUTEST_WARM_SCORER: build the GCN scorer at startup
     scorer_train_steps: int = 300        # ROUTEST_SCORER_TRAIN_STEPS: training steps of the GCN scorer
     # ROUTEST_SCORER_TARGET: "observed" (trip observations: hidden delays the edge costs lack,

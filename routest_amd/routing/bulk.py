@@ -80,7 +80,7 @@ class BulkRouteStep:
         slots = min(legs_est, max_slots)
         # every search the lane tier leaves (with the length split: ~65k+ of 80k here) in ONE wave-tier
         # launch with 2^14-entry starting tables (fewer growth steps): 163 -> 142 ms per 10k-request
-        # step on the 100k-node graph (profiles/route_tiering_ab_r3q.jsonl); 98304 slots instead of
+        # step on the 100k-node graph (profiles/superseded/route_tiering_ab_r3q.jsonl); 98304 slots instead of
         # 65536 once the long legs skip the lane tier: 124.2 -> 119.6 ms (route_wave_slots_ab_r3aj.jsonl).
         # Workspace: lane tier ~8 GB, wave tier ~39 GB, big tier ~4 GB, growth arena 16 GB (of 288 GB)
         self.engine = engine

@@ -257,13 +257,13 @@ class BatchedAstar:
         self.lane_pops = int(os.environ.get("ROUTEST_ASTAR_LANE_POPS", "500"))
         # interactive batches (a few thousand legs per flush: ~60 lane waves would leave most of the
         # 256 CUs idle) go straight to the wave tier: one 64-lane wave per search fills the chip.
-        # Measured on the native route path at 1k concurrency (profiles/route_http_r3.jsonl): lane
+        # Measured on the native route path at 1k concurrency (profiles/superseded/route_http_r3.jsonl): lane
         # budget 500 -> 19.3k req/s, 100 -> 24.1k, 1 (all wave) -> 26.2k, 2000 -> 10.3k.
         self.wave_only_below = int(os.environ.get("ROUTEST_ASTAR_WAVE_ONLY_BELOW", "32768"))
         self.wave_delta = float(os.environ.get("ROUTEST_ASTAR_DELTA", "10"))
         # legs longer than ~8 median edges (great circle) would spend the lane tier's whole pop budget
         # and start over in the wave tier: they skip the lane tier.  Route step, 100k-node graph
-        # (profiles/astar_lane_split_ab_r3x.jsonl): no split 131.7 ms, 1000 m 124.6 ms, 4000 m 129.3 ms
+        # (profiles/superseded/astar_lane_split_ab_r3x.jsonl): no split 131.7 ms, 1000 m 124.6 ms, 4000 m 129.3 ms
         env_m = os.environ.get("ROUTEST_ASTAR_LANE_MAX_M")
         self.lane_max_m = float(env_m) if env_m is not None else 8.0 * median_edge_m(g)
         if wave_slots is None:
