@@ -63,7 +63,9 @@ __device__ __forceinline__ int find_arc_d(const int32_t* __restrict__ up_ptr, co
   return (lo < up_ptr[a + 1] && up_head[lo] == b) ? lo : -1;
 }
 
-// largest i in [lo, hi) with ofs[i] <= g
+// largest i in [lo, hi) with ofs[i] <= g  (per item, from global memory: staging the block's slice of
+// ofs in LDS and searching that instead measured the same level-kernel times, r4x — the levels are
+// bound by their gathers and atomics, not by this search)
 __device__ __forceinline__ int item_owner(const int64_t* __restrict__ ofs, int lo, int hi, long long g) {
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
