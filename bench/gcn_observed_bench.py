@@ -24,8 +24,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nodes", type=int, default=100_000)
     ap.add_argument("--trips", type=int, default=50_000)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--lr", type=float, default=5e-3)
+    ap.add_argument("--steps", type=int, default=1500)
+    ap.add_argument("--lr", type=float, default=1e-2)
     ap.add_argument("--eval-trips", type=int, default=2000)
     ap.add_argument("--k", type=int, default=6)
     ap.add_argument("--cpu", action="store_true")
