@@ -63,7 +63,7 @@ def parse_args():
                     help="also time this many steps of the GCN route scorer (100k-node graph, 10k "
                          "routes per step over all ranks), replicated and row-partitioned with an "
                          "RCCL all-gather (extra JSON key 'gcn'; skipped on a shared GPU)")
-    ap.add_argument("--train-steps", type=int, default=30,
+    ap.add_argument("--train-steps", type=int, default=200,
                     help="also time this many data-parallel training steps of the same MLP on the "
                          "same ranks (64k rows per GPU, one flat-bucket RCCL all-reduce per step; "
                          "extra JSON key 'dp_training')")
@@ -314,7 +314,7 @@ def main() -> None:
         trt = records_to_tensor(trec).to(dev)
         tr = FusedMlp3Trainer(tmodel, dev, tB, tB * world, lr=1e-3, allreduce=world > 1, comm=comm)
         yn = tr.normalize_targets(torch.from_numpy(ty).to(dev))
-        for _ in range(5):
+        for _ in range(20):                     # (clocks settle: 5 warm steps read ~5 % slow at 64k)
             tr.step(trt, yn)
         torch.cuda.synchronize()
         if comm is not None and not agree(not comm.C.comm_error(comm.h)):
