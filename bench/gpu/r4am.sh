@@ -1,0 +1,12 @@
+# round 4: train_bwd segment timing (1 = as built, 5 = no next-tile staging, 6 = no db2; both keep the
+# fragment prefetch now), 64k / 1M steps, gradient tests
+ROOT=$GRAFT_REPO_ROOT
+cd $ROOT
+export TMPDIR=/tmp
+O=$ROOT/gpurun_out/r4am; mkdir -p $O
+for P in 1 7 8; do
+  ROUTEST_TRAIN_BWD_PROF=$P timeout -k 10 150 python3 bench/train_bench.py --hidden 256 --batch 65536 --steps 3 --warmup 2 --modes fused > $O/p$P.log 2>&1 || { tail -20 $O/p$P.log; exit 2; }
+  echo "PROF=$P $(grep 'train_bwd prof' $O/p$P.log | tail -1)"
+done
+timeout -k 10 150 python3 bench/train_bench.py --hidden 256 --batch 65536 --steps 300 --warmup 30 --modes fused > $O/t64k.log 2>&1 || { tail -20 $O/t64k.log; exit 4; }
+tail -1 $O/t64k.log | cut -c1-300

@@ -283,7 +283,9 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
     // train_bwd_kernel.)  The rows' dy reach the lanes through a 128-byte LDS broadcast.
     {
       float* const dys = dyscr;                      // this wave's 32-float scratch
-      if (h == 0) dys[r] = dy;
+      // (both lane halves hold row r's dy — y came through the cross-half add — so both store it: the
+      // same value to the same slot, and no exec-mask branch)
+      dys[r] = dy;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -312,6 +314,7 @@ __global__ __launch_bounds__(TRAIN_TPB, 1) void eta_mlp3_train_fwd_kernel(
 #pragma unroll
         for (int e = 0; e < 16; ++e) t = __builtin_fmaf(dyv[e], tt[e], t);
         t += __shfl_xor(t, 32);
+        // (kept under the branch: written by both halves — same value, same slot — the kernel spilled)
         if (h == 0) w3part[hperm(32 * mt + r)] += t;
       }
       // db3 = sum of dy over the rows (lanes of half 0 hold each row once)
@@ -419,7 +422,8 @@ __device__ __forceinline__ void mfma_drain(f32x16& x, f32x16& y) {
 // Partial sums of slice s go to slab[s]: dW2 in the register-native layout (one 16-byte store per
 // lane and 4 accumulator registers; wgrad.hip native_to_bucket), dW1 in the bucket layout (hperm
 // rows, train/fused.py); wgrad_reduce sums them in a fixed order (deterministic) into the bucket.
-// PROF (ROUTEST_TRAIN_BWD_PROF=1, diagnostics only): s_memtime per tile segment — [0] the loop-top
+// PROF (ROUTEST_TRAIN_BWD_PROF=1, diagnostics only; 2-6 also drop one part of the work: 2 the
+// fragment prefetch, 3 the dgrad MFMAs, 4 the dW2 MFMAs, 5 the next tile's staging, 6 db2): s_memtime per tile segment — [0] the loop-top
 // wait + barrier, [1] staging issue + layer 1, [2] the hidden-tile loop, [3] dW1 — summed per wave
 // into prof[wave][4] (scalar registers: the timed code keeps its VGPR allocation)
 template <int H, int PROF = 0>
@@ -445,6 +449,7 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
   bf16x8* const rb = w2s + MT * RBF;                         // [2][KS][64] dz2 fragments
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 31, h = lane >> 5;
   const int nw = blockDim.x >> 6;
+  const int wsc = __builtin_amdgcn_readfirstlane(w);
   const int ntiles = (B + 31) >> 5;
   // slice s takes tiles s, s + S, s + 2S, ... in DESCENDING order: the forward wrote the tiles in
   // rounds of increasing index, so every slice starts on the most recently written tiles, which are
@@ -547,7 +552,7 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     asm volatile("" ::: "memory");
     mark(0);
     const bf16x8 x = xn;
-    if (it + 1 < t1) {
+    if (it + 1 < t1 && PROF != 5) {      // (PROF 5, diagnostics: no next-tile staging in flight)
       stage(tile_at(it + 1), buf ^ 1);
       xn = xg[(size_t)tile_at(it + 1) * 64 + 2 * col + h];
     }
@@ -612,7 +617,7 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
       asm volatile("" : "+v"(rbase), "+v"(tbase));
       AFrags nxt = cur;
       bf16x8 wn[2][2];
-      if (mt + 1 < MT && PROF < 2) {
+      if (mt + 1 < MT && PROF != 2) {
         nxt = lda(mt + 1);
         ldw(mt + 1, wn);
       }
@@ -636,7 +641,23 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
         mfma32_vacc(accd[0], cur.a1, wc[0][1]);
         mfma32_vacc(accd[1], cur.a1, wc[1][1]);
       }
-      if ((mt >> 1) == w) {            // db2 of this wave's own two z2 tiles (wave-uniform)
+      // db2 of this wave's own two z2 tiles: the wave index through readfirstlane makes this a scalar
+      // branch (through threadIdx it was an exec-mask one; hidden-tile loop 4129 -> 4043 cycles per
+      // tile, r4ah).  Computing it at every hidden tile and selecting measured slower (4562, r4ak).
+      if constexpr (PROF == 7) {          // (diagnostics: the same sums through v_dot2_f32_bf16)
+        if ((mt >> 1) == wsc) {
+          typedef __bf16 bf16x2t __attribute__((ext_vector_type(2)));
+          const u32x4v q0 = __builtin_bit_cast(u32x4v, cur.t[0]), q1 = __builtin_bit_cast(u32x4v, cur.t[1]);
+          const bf16x2t one2 = {(__bf16)1.f, (__bf16)1.f};
+          float sacc = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            sacc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2t, q0[q]), one2, sacc, false);
+            sacc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2t, q1[q]), one2, sacc, false);
+          }
+          db2[mt & 1] += sacc;
+        }
+      } else if ((mt >> 1) == wsc && PROF != 6 && PROF != 8) {      // (PROF 6 / 8, diagnostics)
         const u32x4v q0 = __builtin_bit_cast(u32x4v, cur.t[0]), q1 = __builtin_bit_cast(u32x4v, cur.t[1]);
         float sacc = 0.f;
 #pragma unroll
@@ -646,8 +667,8 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
         }
         db2[mt & 1] += sacc;
       }
-      if (PROF < 2) cur = nxt;
-      if (mt + 1 < MT && PROF < 2) {
+      if (PROF != 2) cur = nxt;
+      if (mt + 1 < MT && PROF != 2) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           wc[i][0] = wn[i][0];
@@ -656,6 +677,23 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
       }
     }
     mfma_drain(accd[0], accd[1]);
+    if constexpr (PROF == 8) {         // (diagnostics: db2 after the loop, its fragments re-read)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int mt = 2 * wsc + i;
+        float sacc = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const unsigned k0 = 64u * (mt & 3) + 256u * (mt >> 2) + 16u * RB2 * s2;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(tbase ^ k0));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(tbase ^ (k0 + 32u + 8u * RB2)));
+          const u32x4v q0 = __builtin_bit_cast(u32x4v, join4(lo, hi));
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sacc += __uint_as_float(q0[q] << 16) + __uint_as_float(q0[q] & 0xFFFF0000u);
+        }
+        db2[i] += sacc;
+      }
+    }
     mark(2);
     // dW1 += (dh1 * relu'(z1))^T x: x^T as the B operand (features on the lanes)
     const f32x16 xt = mfma32(x, eye, zero);
@@ -952,7 +990,7 @@ static hipError_t launch_train_bwd_h(const void* xf, int B, const void* blob, co
       hipLaunchKernelGGL((train_bwd_kernel<H, P>), dim3(S), dim3(H), LDS, stream, (const __bf16*)xf, B,    \
                          (const unsigned char*)blob, (const bf16x8*)dz2r, slab2, slab1, d);                \
     } else
-    RT_BWD_PMODE(2) RT_BWD_PMODE(3) RT_BWD_PMODE(4) {
+    RT_BWD_PMODE(2) RT_BWD_PMODE(3) RT_BWD_PMODE(4) RT_BWD_PMODE(5) RT_BWD_PMODE(6) RT_BWD_PMODE(7) RT_BWD_PMODE(8) {
 #undef RT_BWD_PMODE
       hipLaunchKernelGGL((train_bwd_kernel<H, 1>), dim3(S), dim3(H), LDS, stream, (const __bf16*)xf, B,
                          (const unsigned char*)blob, (const bf16x8*)dz2r, slab2, slab1, d);
