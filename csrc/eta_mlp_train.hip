@@ -641,29 +641,20 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
         mfma32_vacc(accd[0], cur.a1, wc[0][1]);
         mfma32_vacc(accd[1], cur.a1, wc[1][1]);
       }
-      // db2 of this wave's own two z2 tiles: the wave index through readfirstlane makes this a scalar
-      // branch (through threadIdx it was an exec-mask one; hidden-tile loop 4129 -> 4043 cycles per
-      // tile, r4ah).  Computing it at every hidden tile and selecting measured slower (4562, r4ak).
-      if constexpr (PROF == 7) {          // (diagnostics: the same sums through v_dot2_f32_bf16)
-        if ((mt >> 1) == wsc) {
-          typedef __bf16 bf16x2t __attribute__((ext_vector_type(2)));
-          const u32x4v q0 = __builtin_bit_cast(u32x4v, cur.t[0]), q1 = __builtin_bit_cast(u32x4v, cur.t[1]);
-          const bf16x2t one2 = {(__bf16)1.f, (__bf16)1.f};
-          float sacc = 0.f;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            sacc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2t, q0[q]), one2, sacc, false);
-            sacc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2t, q1[q]), one2, sacc, false);
-          }
-          db2[mt & 1] += sacc;
-        }
-      } else if ((mt >> 1) == wsc && PROF != 6 && PROF != 8) {      // (PROF 6 / 8, diagnostics)
+      // db2 of this wave's own two z2 tiles (row sums of dz2^T): the wave index through readfirstlane
+      // makes this a scalar branch (an exec-mask one through threadIdx), and the bf16 pairs are summed
+      // by v_dot2_f32_bf16 against (1, 1) — 8 instructions instead of ~33 (hidden-tile loop 4129 ->
+      // 4044 -> 3937 cycles per 32-row tile: profiles/train_bwd_segments_r4.md; computing it at every
+      // hidden tile and selecting measured slower, 4562)
+      if ((mt >> 1) == wsc && PROF != 6) {      // (PROF 6, diagnostics: no db2 block)
+        typedef __bf16 bf16x2t __attribute__((ext_vector_type(2)));
         const u32x4v q0 = __builtin_bit_cast(u32x4v, cur.t[0]), q1 = __builtin_bit_cast(u32x4v, cur.t[1]);
+        const bf16x2t one2 = {(__bf16)1.f, (__bf16)1.f};
         float sacc = 0.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          sacc += __uint_as_float(q0[q] << 16) + __uint_as_float(q0[q] & 0xFFFF0000u);
-          sacc += __uint_as_float(q1[q] << 16) + __uint_as_float(q1[q] & 0xFFFF0000u);
+          sacc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2t, q0[q]), one2, sacc, false);
+          sacc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2t, q1[q]), one2, sacc, false);
         }
         db2[mt & 1] += sacc;
       }
@@ -677,23 +668,6 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
       }
     }
     mfma_drain(accd[0], accd[1]);
-    if constexpr (PROF == 8) {         // (diagnostics: db2 after the loop, its fragments re-read)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int mt = 2 * wsc + i;
-        float sacc = 0.f;
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const unsigned k0 = 64u * (mt & 3) + 256u * (mt >> 2) + 16u * RB2 * s2;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(tbase ^ k0));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(tbase ^ (k0 + 32u + 8u * RB2)));
-          const u32x4v q0 = __builtin_bit_cast(u32x4v, join4(lo, hi));
-#pragma unroll
-          for (int q = 0; q < 4; ++q) sacc += __uint_as_float(q0[q] << 16) + __uint_as_float(q0[q] & 0xFFFF0000u);
-        }
-        db2[i] += sacc;
-      }
-    }
     mark(2);
     // dW1 += (dh1 * relu'(z1))^T x: x^T as the B operand (features on the lanes)
     const f32x16 xt = mfma32(x, eye, zero);
@@ -990,7 +964,7 @@ static hipError_t launch_train_bwd_h(const void* xf, int B, const void* blob, co
       hipLaunchKernelGGL((train_bwd_kernel<H, P>), dim3(S), dim3(H), LDS, stream, (const __bf16*)xf, B,    \
                          (const unsigned char*)blob, (const bf16x8*)dz2r, slab2, slab1, d);                \
     } else
-    RT_BWD_PMODE(2) RT_BWD_PMODE(3) RT_BWD_PMODE(4) RT_BWD_PMODE(5) RT_BWD_PMODE(6) RT_BWD_PMODE(7) RT_BWD_PMODE(8) {
+    RT_BWD_PMODE(2) RT_BWD_PMODE(3) RT_BWD_PMODE(4) RT_BWD_PMODE(5) RT_BWD_PMODE(6) {
 #undef RT_BWD_PMODE
       hipLaunchKernelGGL((train_bwd_kernel<H, 1>), dim3(S), dim3(H), LDS, stream, (const __bf16*)xf, B,
                          (const unsigned char*)blob, (const bf16x8*)dz2r, slab2, slab1, d);
