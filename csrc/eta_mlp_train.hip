@@ -642,19 +642,17 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
         mfma32_vacc(accd[1], cur.a1, wc[1][1]);
       }
       // db2 of this wave's own two z2 tiles (row sums of dz2^T): the wave index through readfirstlane
-      // makes this a scalar branch (an exec-mask one through threadIdx), and the bf16 pairs are summed
-      // by v_dot2_f32_bf16 against (1, 1) — 8 instructions instead of ~33 (hidden-tile loop 4129 ->
-      // 4044 -> 3937 cycles per 32-row tile: profiles/train_bwd_segments_r4.md; computing it at every
-      // hidden tile and selecting measured slower, 4562)
+      // makes this a scalar branch (an exec-mask one through threadIdx; hidden-tile loop 4129 -> 4044
+      // cycles per 32-row tile, profiles/train_bwd_segments_r4.md).  Computing it at every hidden tile
+      // and selecting measured slower (4562); summing the pairs with v_dot2_f32_bf16 against (1, 1)
+      // was faster (3937) but did not reproduce these sums (db2 off by 13-54 %, r4an) and is not used.
       if ((mt >> 1) == wsc && PROF != 6) {      // (PROF 6, diagnostics: no db2 block)
-        typedef __bf16 bf16x2t __attribute__((ext_vector_type(2)));
         const u32x4v q0 = __builtin_bit_cast(u32x4v, cur.t[0]), q1 = __builtin_bit_cast(u32x4v, cur.t[1]);
-        const bf16x2t one2 = {(__bf16)1.f, (__bf16)1.f};
         float sacc = 0.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          sacc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2t, q0[q]), one2, sacc, false);
-          sacc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2t, q1[q]), one2, sacc, false);
+          sacc += __uint_as_float(q0[q] << 16) + __uint_as_float(q0[q] & 0xFFFF0000u);
+          sacc += __uint_as_float(q1[q] << 16) + __uint_as_float(q1[q] & 0xFFFF0000u);
         }
         db2[mt & 1] += sacc;
       }
