@@ -255,7 +255,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 // Workgroups are remapped XCD-aware (bijective for any grid) so the N/256 unit tiles of one
 // batch-row block run on one XCD and share its X tile through that XCD's L2.  (A ring of four
 // 32-deep stages with three in flight and all 12 fragment reads issued before the MFMAs measured
-// SLOWER at the H = 1024 trainer's shape: 174 vs 161 us, profiles/gemm_probe_r4p.jsonl.)
+// SLOWER at the H = 1024 trainer's shape: 174 vs 161 us, profiles/gemm_probe_r4p.jsonl; so did reading
+// both k-steps' fragments up front, 166 vs 161 us, r4ap.)
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int G2T = 256, G2K = 64;
 constexpr int G2_STAGE = 2 * G2T * G2K * 2;          // A + B tile bytes per stage (64 KB)
