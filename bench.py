@@ -467,23 +467,33 @@ def main() -> None:
         from routest_amd.routing.cch import RoadRouter, RouteContext
         from routest_amd.routing.graph import edge_costs
         from routest_amd.serve.eta_service import default_model
-        if g is None:
-            g = synth_road_graph(100_000, seed=0)
-        torch.manual_seed(0)
-        route_model = default_model(hidden=a.hidden, steps=200)
-        cost = edge_costs(g, route_model, device=dev)
+        # set-up is per rank (no collective): a failure on any rank is agreed on before the timed
+        # steps, so the section reports an error and the headline line still prints
+        route_err = None
+        try:
+            if g is None:
+                g = synth_road_graph(100_000, seed=0)
+            torch.manual_seed(0)
+            route_model = default_model(hidden=a.hidden, steps=200)
+            cost = edge_costs(g, route_model, device=dev)
+            t0 = time.perf_counter()
+            route_router = RoadRouter(g, route_model, device=dev)
+            topo_s = time.perf_counter() - t0
+            # a routing context built from scratch on the GPU: ETA-model edge costs + customization
+            t0 = time.perf_counter()
+            route_router.metric(RouteContext(weather=1, congestion=3, weekhour=4 * 24 + 18))
+            ctx_ms = (time.perf_counter() - t0) * 1e3
+            ctx_info = dict(route_router.last_metric)
+            bulk = BulkRouteStep(g, cost, dev, a.route_requests // world, seed=100 + rank, router=route_router)
+            bulk.step()
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 - reported, never fatal for the headline
+            route_err = repr(e)[:300]
+    if a.route_steps > 0 and not (share and world > 1) and not agree(route_err is None):
+        route_res = {"error": route_err or "route set-up failed on a peer rank"}
+        route_router = None
+    elif a.route_steps > 0 and not (share and world > 1):
         route_cost = cost
-        t0 = time.perf_counter()
-        route_router = RoadRouter(g, route_model, device=dev)
-        topo_s = time.perf_counter() - t0
-        # a routing context built from scratch on the GPU: ETA-model edge costs + customization
-        t0 = time.perf_counter()
-        route_router.metric(RouteContext(weather=1, congestion=3, weekhour=4 * 24 + 18))
-        ctx_ms = (time.perf_counter() - t0) * 1e3
-        ctx_info = dict(route_router.last_metric)
-        bulk = BulkRouteStep(g, cost, dev, a.route_requests // world, seed=100 + rank, router=route_router)
-        bulk.step()
-        torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
