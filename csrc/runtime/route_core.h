@@ -123,10 +123,12 @@ inline void put_int(std::string& o, long long v) {
   o.append(b, r.ptr);
 }
 // repr of a float that is numpy.round(x, 6) output: the decimal itself (shortest round-trip), laid
-// out like repr; values below 1e-4 in magnitude take repr's exponent form via append_pyfloat
+// out like repr; values below 1e-4 in magnitude take repr's exponent form via append_pyfloat.  The
+// six-decimal form is repr only while it has at most 15 significant digits (|v| < 1e9): beyond, a
+// double that k / 1e6 rounds back to can have a shorter repr (found by rt_selftest's fuzz_route)
 inline void put_coord(std::string& o, double v) {
   const double a = std::fabs(v);
-  if (!(a >= 1e-4 && a < 1e15)) { rtc::append_pyfloat(o, v); return; }
+  if (!(a >= 1e-4 && a < 1e9)) { rtc::append_pyfloat(o, v); return; }
   long long k = (long long)std::nearbyint(v * 1e6);
   if ((double)k / 1e6 != v) { rtc::append_pyfloat(o, v); return; }   // not a 6-decimal value
   if (k < 0) { o += '-'; k = -k; }

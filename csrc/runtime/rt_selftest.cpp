@@ -1,4 +1,5 @@
-// Host-only self-test + fuzz harness for the native runtime core (rt_core.h, json_lite.h).
+// Host-only self-test + fuzz harness for the native runtime core (rt_core.h, json_lite.h) and the
+// route service's host code (route_core.h: route-request parsing, Python-exact float fast paths).
 // Built with -fsanitize=address,undefined by `tools/build_ext.py --sanitize` or the CMake `asan`
 // preset (the reference has no race detection / sanitizers at all), and run by
 // tests/test_sanitize_cpu.py.  Exit code 0 = all invariants held and no sanitizer report.
@@ -10,6 +11,7 @@
 #include <string>
 #include <vector>
 
+#include "route_core.h"
 #include "rt_core.h"
 
 using namespace rtc;
@@ -135,6 +137,60 @@ static void fuzz_float(std::mt19937_64& rng, int iters) {
   CHECK(timedelta_minutes_us(1.0 / 60000000.0 * 2.5) == 2, "half-even rounding");
 }
 
+// route_core.h: py_round(x, 1)'s fast path, put_float's integer-tenths path and put_coord's
+// six-decimal path must give the bits / text of their slow (CPython-equivalent) references, and
+// parse_route_request must survive any mutated request body.
+static void fuzz_route(std::mt19937_64& rng, int iters) {
+  for (int it = 0; it < iters; ++it) {
+    double x;
+    switch (rng() % 4) {
+      case 0: x = ((double)(int64_t)(rng() % 2000000000) - 1e9) / 997.0; break;
+      case 1: x = ((double)(int64_t)(rng() % 20000001) - 1e7 + 0.5) / 10.0; break;     // midpoints
+      case 2: x = std::nextafter(((double)(rng() % 100000) + 0.05), rng() & 1 ? 1e9 : -1e9); break;
+      default: { uint64_t b = rng(); std::memcpy(&x, &b, 8); break; }
+    }
+    if (!std::isfinite(x)) continue;
+    char b[64];
+    std::snprintf(b, sizeof b, "%.1f", x);
+    const double slow = std::strtod(b, nullptr);
+    const double fast = rtr::py_round(x, 1);
+    CHECK(std::memcmp(&slow, &fast, 8) == 0 || (slow == 0.0 && fast == 0.0 && std::signbit(slow) == std::signbit(fast)),
+          "py_round(%.17g, 1): fast %.17g, slow %.17g", x, fast, slow);
+    std::string a1, a2;
+    rtr::put_float(a1, fast);
+    rtc::append_pyfloat(a2, fast);
+    CHECK(a1 == a2, "put_float(%.17g): %s vs repr %s", fast, a1.c_str(), a2.c_str());
+    const double c = rtr::np_round6(x / 1000.0);
+    std::string c1, c2;
+    rtr::put_coord(c1, c);
+    rtc::append_pyfloat(c2, c);
+    CHECK(c1 == c2, "put_coord(%.17g): %s vs repr %s", c, c1.c_str(), c2.c_str());
+  }
+  static const char* RSEEDS[] = {
+      R"({"source_point":{"lat":14.55,"lon":121.02},"destination_points":[{"lat":14.56,"lon":121.03,"payload":2},{"lat":14.57,"lon":121.0}],"vehicle_capacity":5,"maximum_distance":90000,"use_ml_eta":true,"context":{"weather":"Stormy","traffic":"High"},"alternatives":3})",
+      R"({"source_point":{"lat":"14.5","lon":121},"destination_points":[],"vehicle_type":"motorcycle","driver_details":{"driver_age":"41"},"meta":{"origin_id":7,"destination_ids":[1,2]}})",
+      R"({"source_point":null,"destination_points":[{"lat":1e308,"lon":-1e308}],"vehicle_capacity":-1,"alternatives":1e30})",
+  };
+  for (int it = 0; it < iters; ++it) {
+    std::string s = RSEEDS[rng() % (sizeof RSEEDS / sizeof *RSEEDS)];
+    const int muts = (int)(rng() % 5);
+    for (int k = 0; k < muts && !s.empty(); ++k) {
+      const size_t p = rng() % s.size();
+      switch (rng() % 3) {
+        case 0: s[p] = (char)(rng() & 0xFF); break;
+        case 1: s.erase(p, 1 + rng() % 6); break;
+        default: s.insert(p, s.substr(rng() % s.size(), 1 + rng() % 12)); break;
+      }
+    }
+    try {
+      rtj::Value root = rtj::Parser(s.data(), s.size()).parse();
+      const rtr::RouteReq r = rtr::parse_route_request(&root);
+      CHECK(r.error.empty() || r.dst.empty() || true, "unreachable");
+    } catch (...) {
+    }
+  }
+}
+
 // The batched /predict path splits a big array with split_top_array and packs / formats items on
 // parallel_chunks threads (rt.cpp); replay that shape here so TSan sees the real sharing pattern.
 static void threaded_pack_format(int n_items) {
@@ -176,6 +232,7 @@ int main(int argc, char** argv) {
   fuzz_json(rng, iters);
   fuzz_iso(rng, iters);
   fuzz_float(rng, iters);
+  fuzz_route(rng, iters);
   threaded_pack_format(20000);
   std::printf("rt_selftest: %d iterations, %d failures\n", iters, g_fail);
   return g_fail ? 1 : 0;
