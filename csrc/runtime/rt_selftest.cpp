@@ -1,16 +1,21 @@
 // Host-only self-test + fuzz harness for the native runtime core (rt_core.h, json_lite.h) and the
-// route service's host code (route_core.h: route-request parsing, Python-exact float fast paths).
+// route service's host code (route_core.h: route-request parsing, Python-exact float fast paths;
+// alternatives.h: via-node candidates and scores).
 // Built with -fsanitize=address,undefined by `tools/build_ext.py --sanitize` or the CMake `asan`
 // preset (the reference has no race detection / sanitizers at all), and run by
 // tests/test_sanitize_cpu.py.  Exit code 0 = all invariants held and no sanitizer report.
 //
 //   rt_selftest [iterations] [seed]
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <random>
 #include <string>
 #include <vector>
 
+#include "alternatives.h"
 #include "route_core.h"
 #include "rt_core.h"
 
@@ -191,6 +196,41 @@ static void fuzz_route(std::mt19937_64& rng, int iters) {
   }
 }
 
+// alternatives.h: via nodes stay in range, unique, within the detour band, and reproducible; the
+// argmin treats non-finite scores as +inf
+static void fuzz_alternatives(std::mt19937_64& rng, int iters) {
+  for (int it = 0; it < iters / 50; ++it) {
+    const int N = 1 + (int)(rng() % 2000);
+    std::vector<double> lat(N), lon(N);
+    for (int i = 0; i < N; ++i) {
+      lat[i] = 14.5 + (double)(rng() % 100000) * 1e-6 * (rng() % 5 == 0 ? 0.0 : 1.0);
+      lon[i] = 121.0 + (double)(rng() % 100000) * 1e-6;
+    }
+    const int s = (int)(rng() % (N + 4)) - 2, t = (int)(rng() % (N + 4)) - 2, n = (int)(rng() % 12) - 1;
+    const double stretch = 1.0 + (double)(rng() % 1000) / 1000.0;
+    const std::vector<int> v = ralt::via_nodes(lat.data(), lon.data(), N, s, t, n, stretch);
+    CHECK((int)v.size() <= std::max(n, 0), "via_nodes: %zu > n %d", v.size(), n);
+    std::vector<int> seen(v);
+    std::sort(seen.begin(), seen.end());
+    CHECK(std::unique(seen.begin(), seen.end()) == seen.end(), "via_nodes: duplicate candidate");
+    for (int w : v) {
+      CHECK(w >= 0 && w < N, "via_nodes: %d out of [0, %d)", w, N);
+      if (w < 0 || w >= N) break;
+      const double d_st = rtr::haversine_m(lat[s], lon[s], lat[t], lon[t]);
+      const double det = rtr::haversine_m(lat[s], lon[s], lat[w], lon[w]) + rtr::haversine_m(lat[w], lon[w], lat[t], lon[t]);
+      CHECK(det <= stretch * d_st && det >= 1.03 * d_st, "via_nodes: detour %.3f outside band of %.3f", det, d_st);
+    }
+    CHECK(v == ralt::via_nodes(lat.data(), lon.data(), N, s, t, n, stretch), "via_nodes: not reproducible");
+    std::vector<double> sc(rng() % 9);
+    for (double& x : sc) {
+      const int k = (int)(rng() % 4);
+      x = k == 0 ? NAN : k == 1 ? INFINITY : (double)(rng() % 1000);
+    }
+    const int b = ralt::argmin_score(sc);
+    CHECK(sc.empty() ? b == -1 : (b >= 0 && b < (int)sc.size()), "argmin_score: %d of %zu", b, sc.size());
+  }
+}
+
 // The batched /predict path splits a big array with split_top_array and packs / formats items on
 // parallel_chunks threads (rt.cpp); replay that shape here so TSan sees the real sharing pattern.
 static void threaded_pack_format(int n_items) {
@@ -233,6 +273,7 @@ int main(int argc, char** argv) {
   fuzz_iso(rng, iters);
   fuzz_float(rng, iters);
   fuzz_route(rng, iters);
+  fuzz_alternatives(rng, iters);
   threaded_pack_format(20000);
   std::printf("rt_selftest: %d iterations, %d failures\n", iters, g_fail);
   return g_fail ? 1 : 0;
