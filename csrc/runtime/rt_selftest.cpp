@@ -1,6 +1,7 @@
 // Host-only self-test + fuzz harness for the native runtime core (rt_core.h, json_lite.h) and the
 // route service's host code (route_core.h: route-request parsing, Python-exact float fast paths;
-// alternatives.h: via-node candidates and scores).
+// alternatives.h: via-node candidates and scores; history_db.h: the native history reads over a
+// fuzzed database and fuzzed limits / ids).
 // Built with -fsanitize=address,undefined by `tools/build_ext.py --sanitize` or the CMake `asan`
 // preset (the reference has no race detection / sanitizers at all), and run by
 // tests/test_sanitize_cpu.py.  Exit code 0 = all invariants held and no sanitizer report.
@@ -16,6 +17,7 @@
 #include <vector>
 
 #include "alternatives.h"
+#include "history_db.h"
 #include "route_core.h"
 #include "rt_core.h"
 
@@ -231,6 +233,109 @@ static void fuzz_alternatives(std::mt19937_64& rng, int iters) {
   }
 }
 
+// history_db.h over an in-memory database with the store's schema (routest_amd/store/store.py
+// SCHEMA): rows with fuzzed texts (any bytes, non-JSON stops), then list / detail / delete /
+// locations with fuzzed limit strings and ids — every reply a valid status, nothing read out of
+// bounds.  Skipped when libsqlite3 cannot be loaded.
+static void fuzz_history(std::mt19937_64& rng, int iters) {
+  rtsql::Api sql;
+  std::string err;
+  if (!sql.load(err)) {
+    std::printf("fuzz_history: skipped (%s)\n", err.c_str());
+    return;
+  }
+  const std::string uri = "file:rt_selftest_hist?mode=memory&cache=shared";
+  void* db = nullptr;
+  if (sql.open_v2(uri.c_str(), &db, rtsql::OPEN_READWRITE | rtsql::OPEN_CREATE | rtsql::OPEN_URI, nullptr) != rtsql::OK) {
+    std::printf("fuzz_history: skipped (open)\n");
+    return;
+  }
+  const char* ddl =
+      "CREATE TABLE locations (id TEXT PRIMARY KEY, name TEXT NOT NULL, latitude REAL NOT NULL, longitude REAL NOT NULL, created_at TEXT);"
+      "CREATE TABLE route_requests (id TEXT PRIMARY KEY, origin_id TEXT, stops TEXT NOT NULL, request_time TEXT NOT NULL,"
+      " status TEXT NOT NULL DEFAULT 'pending', engine TEXT, vehicle_id TEXT, driver_age REAL);"
+      "CREATE TABLE route_results (id TEXT PRIMARY KEY, request_id TEXT NOT NULL REFERENCES route_requests(id) ON DELETE CASCADE,"
+      " optimized_order TEXT, total_distance REAL, total_duration REAL, legs TEXT, geometry TEXT, eta_minutes_ml REAL,"
+      " eta_completion_time_ml TEXT, created_at TEXT);";
+  CHECK(sql.exec(db, ddl, nullptr, nullptr, nullptr) == rtsql::OK, "history schema");
+  void *ins_req = nullptr, *ins_res = nullptr, *ins_loc = nullptr;
+  sql.prepare_v2(db, "INSERT INTO route_requests(id,origin_id,stops,request_time,status,engine,vehicle_id,driver_age) VALUES(?,?,?,?,?,?,?,?)", -1, &ins_req, nullptr);
+  sql.prepare_v2(db, "INSERT INTO route_results(id,request_id,optimized_order,total_distance,total_duration,legs,geometry,eta_minutes_ml,eta_completion_time_ml,created_at) VALUES(?,?,?,?,?,?,?,?,?,?)", -1, &ins_res, nullptr);
+  sql.prepare_v2(db, "INSERT INTO locations(id,name,latitude,longitude,created_at) VALUES(?,?,?,?,?)", -1, &ins_loc, nullptr);
+  auto junk = [&](size_t maxlen) {
+    static const char* frags[] = {"{\"destination_ids\":[1,2],\"destination_points\":[[14.5,121.0]]}", "[0,2,1]", "null",
+                                  "{\"type\":\"LineString\",\"coordinates\":[]}", "2026-10-17T00:00:00", "\"\\u00e9\"", "{"};
+    std::string t = rng() % 2 ? frags[rng() % 7] : "";
+    const size_t n = rng() % maxlen;
+    for (size_t i = 0; i < n; ++i) t += (char)(rng() & 0xFF);
+    return t;
+  };
+  std::vector<std::string> ids;
+  for (int i = 0; i < 60; ++i) {
+    const std::string rid = "req-" + std::to_string(i), stops = junk(40), tm = junk(24), st = junk(8), eng = junk(8);
+    sql.reset(ins_req);
+    sql.clear_bindings(ins_req);
+    sql.bind_text(ins_req, 1, rid.data(), (int)rid.size(), rtsql::TRANSIENT);
+    if (rng() % 2) sql.bind_null(ins_req, 2); else sql.bind_int64(ins_req, 2, (long long)(rng() % 100));
+    sql.bind_text(ins_req, 3, stops.data(), (int)stops.size(), rtsql::TRANSIENT);
+    sql.bind_text(ins_req, 4, tm.data(), (int)tm.size(), rtsql::TRANSIENT);
+    sql.bind_text(ins_req, 5, st.data(), (int)st.size(), rtsql::TRANSIENT);
+    sql.bind_text(ins_req, 6, eng.data(), (int)eng.size(), rtsql::TRANSIENT);
+    sql.bind_null(ins_req, 7);
+    if (rng() % 3) sql.bind_double(ins_req, 8, (double)(rng() % 90)); else sql.bind_null(ins_req, 8);
+    CHECK(sql.step(ins_req) == rtsql::DONE, "insert request");
+    ids.push_back(rid);
+    if (rng() % 4) {
+      const std::string xid = "res-" + std::to_string(i), order = junk(16), legs = junk(64), geom = junk(64), iso = junk(24);
+      sql.reset(ins_res);
+      sql.clear_bindings(ins_res);
+      sql.bind_text(ins_res, 1, xid.data(), (int)xid.size(), rtsql::TRANSIENT);
+      sql.bind_text(ins_res, 2, rid.data(), (int)rid.size(), rtsql::TRANSIENT);
+      sql.bind_text(ins_res, 3, order.data(), (int)order.size(), rtsql::TRANSIENT);
+      sql.bind_double(ins_res, 4, (double)(rng() % 100000) / 7.0);
+      if (rng() % 5) sql.bind_double(ins_res, 5, (double)(rng() % 100000) / 3.0); else sql.bind_null(ins_res, 5);
+      sql.bind_text(ins_res, 6, legs.data(), (int)legs.size(), rtsql::TRANSIENT);
+      sql.bind_text(ins_res, 7, geom.data(), (int)geom.size(), rtsql::TRANSIENT);
+      if (rng() % 2) sql.bind_double(ins_res, 8, (double)(rng() % 1000) / 9.0); else sql.bind_null(ins_res, 8);
+      sql.bind_text(ins_res, 9, iso.data(), (int)iso.size(), rtsql::TRANSIENT);
+      sql.bind_text(ins_res, 10, iso.data(), (int)iso.size(), rtsql::TRANSIENT);
+      CHECK(sql.step(ins_res) == rtsql::DONE, "insert result");
+    }
+    if (i % 6 == 0) {
+      const std::string lid = "loc-" + std::to_string(i), name = junk(12);
+      sql.reset(ins_loc);
+      sql.clear_bindings(ins_loc);
+      sql.bind_text(ins_loc, 1, lid.data(), (int)lid.size(), rtsql::TRANSIENT);
+      sql.bind_text(ins_loc, 2, name.data(), (int)name.size(), rtsql::TRANSIENT);
+      sql.bind_double(ins_loc, 3, 14.5);
+      sql.bind_double(ins_loc, 4, 121.0);
+      sql.bind_null(ins_loc, 5);
+      CHECK(sql.step(ins_loc) == rtsql::DONE, "insert location");
+    }
+  }
+  for (void* st : {ins_req, ins_res, ins_loc}) sql.finalize(st);
+  rth::HistoryDb h;
+  CHECK(h.open(uri, err), "history open: %s", err.c_str());
+  auto valid = [](const rth::Reply& r) { return r.fallback || (r.status >= 200 && r.status < 600); };
+  static const char* LIMITS[] = {"", "0", "-2", "3", "20", "100000", "abc", "2.5", "1_0", " 7", "99999999999999999999999", "+4"};
+  for (int it = 0; it < iters / 100; ++it) {
+    switch (rng() % 5) {
+      case 0: {
+        const bool absent = rng() % 6 == 0;
+        std::string lim = LIMITS[rng() % (sizeof LIMITS / sizeof *LIMITS)];
+        if (rng() % 4 == 0) lim = junk(10);
+        CHECK(valid(h.history(absent ? nullptr : lim.c_str())), "history(%s)", lim.c_str());
+        break;
+      }
+      case 1: CHECK(valid(h.detail(rng() % 2 ? ids[rng() % ids.size()] : junk(50))), "detail"); break;
+      case 2: CHECK(valid(h.del(rng() % 3 ? ids[rng() % ids.size()] : junk(50))), "delete"); break;
+      default: CHECK(valid(h.locations()), "locations"); break;
+    }
+  }
+  h.close();
+  sql.close(db);
+}
+
 // The batched /predict path splits a big array with split_top_array and packs / formats items on
 // parallel_chunks threads (rt.cpp); replay that shape here so TSan sees the real sharing pattern.
 static void threaded_pack_format(int n_items) {
@@ -274,6 +379,7 @@ int main(int argc, char** argv) {
   fuzz_float(rng, iters);
   fuzz_route(rng, iters);
   fuzz_alternatives(rng, iters);
+  fuzz_history(rng, iters);
   threaded_pack_format(20000);
   std::printf("rt_selftest: %d iterations, %d failures\n", iters, g_fail);
   return g_fail ? 1 : 0;

@@ -141,7 +141,7 @@ def build_sanitize(force: bool = False, kind: str = "asan") -> str:
              else ["-fsanitize=thread"])
     if force or _newer(out, [src] + glob.glob(os.path.join(rdir, "*.h"))):
         _run(["g++", "-std=c++17", "-O1", "-g", *flags, "-fno-omit-frame-pointer", "-pthread", "-I", rdir, src,
-              "-o", out])
+              "-o", out, "-ldl"])
     return out
 
 
