@@ -93,6 +93,9 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
+    from routest_amd.parallel.dp import allreduce_scalars
+    from routest_amd.utils import bench_schema
+
     rank = int(os.environ.get("RANK", "0"))
     local_rank = 0 if share else int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -222,9 +225,7 @@ def main() -> None:
             self.step_ms = ({"p50": d[len(d) // 2], "p90": d[int(len(d) * 0.9)], "min": d[0], "max": d[-1]}
                             if d else None)
             if world > 1:
-                t = torch.tensor([el], device="cpu" if share else dev, dtype=torch.float64)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                el = float(t.item())
+                (el,) = allreduce_scalars([el], dev, "max")
             return el
 
         def last_output(self, i: int) -> torch.Tensor:
@@ -331,26 +332,20 @@ def main() -> None:
         torch.cuda.synchronize()
         tel = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([tel], device="cpu" if share else dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            tel = float(t.item())
+            (tel,) = allreduce_scalars([tel], dev, "max")
         loss = float(tr.sq_err.sum().item()) / tB
-        res = {"samples_per_s": tB * world * a.train_steps / tel,
-               "ms_per_step": tel / a.train_steps * 1e3, "batch_per_gpu": tB,
-               "global_batch": tB * world, "steps": a.train_steps,
-               "allreduce": ("none" if world == 1 else "gloo (shared GPU)" if share and comm is None
-                             else "RCCL, one flat fp32 bucket" if comm is None else
-                             "one-shot over IPC-mapped peer HBM (csrc/comm.hip), one flat fp32 bucket"),
-               "final_local_mse_normalized": loss}
+        res = bench_schema.dp_training(
+            tB * world * a.train_steps / tel, tel / a.train_steps * 1e3, tB, world, a.train_steps,
+            ("none" if world == 1 else "gloo (shared GPU)" if share and comm is None
+             else "RCCL, one flat fp32 bucket" if comm is None else
+             "one-shot over IPC-mapped peer HBM (csrc/comm.hip), one flat fp32 bucket"), loss)
         if comm is not None:
             res["comm_error"] = not agree(not comm.C.comm_error(comm.h))
             # every rank must hold the same parameters after the identical reduced updates
-            ph = torch.tensor([float(tr.P.double().sum())], device="cpu" if share else dev,
-                              dtype=torch.float64)
-            lo, hi = ph.clone(), ph.clone()
-            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-            res["params_identical_across_ranks"] = bool(float(lo.item()) == float(hi.item()))
+            ph = float(tr.P.double().sum())
+            (lo,) = allreduce_scalars([ph], dev, "min")
+            (hi,) = allreduce_scalars([ph], dev, "max")
+            res["params_identical_across_ranks"] = bool(lo == hi)
         del tr, trt
         return res
 
@@ -399,10 +394,11 @@ def main() -> None:
             coll = [{"error": repr(e)[:200]}]
 
     # config 4 on the same ranks: the 2-layer GCN scorer, graph replicated on every GPU (no
-    # collective) and row-partitioned (each rank runs 1/N of the nodes, RCCL all-gather of Z)
+    # collective) and row-partitioned (each rank runs 1/N of the nodes, RCCL all-gather of Z).  The
+    # shared-GPU rehearsal runs every mode too (its "partition" gathers through gloo via host memory)
     gcn_res = None
     g = None
-    if a.gcn_steps > 0 and not (share and world > 1):
+    if a.gcn_steps > 0:
         from routest_amd.data.graph import synth_road_graph
         from routest_amd.models.gcn import GcnScorer, GcnScorerHip, routes_to_csr
         g = synth_road_graph(100_000, seed=0)
@@ -420,10 +416,10 @@ def main() -> None:
             walks.append(path)
         ptr, nodes = routes_to_csr(walks)
         ptr_t, nodes_t = torch.from_numpy(ptr).to(dev), torch.from_numpy(nodes).to(dev)
-        gcn_res = {"nodes": g.num_nodes, "edges": g.num_edges, "routes_per_step": nroutes * world}
-        modes = ["replicate"] + (["partition"] if world > 1 else [])
+        gcn_res = bench_schema.gcn_section(g.num_nodes, g.num_edges, nroutes * world)
+        modes = list(bench_schema.GCN_MODES_N if world > 1 else bench_schema.GCN_MODES_1)
         if world > 1 and devcomm is not None:
-            modes.append("partition_oneshot")     # Z gathered over IPC-mapped peer HBM in one hop
+            modes.append(bench_schema.GCN_MODE_ONESHOT)   # Z gathered over IPC-mapped peer HBM in one hop
         for mode in modes:
             hip = GcnScorerHip(gm, g, dev, mode=mode.split("_")[0], rank=rank, world=world,
                                comm=devcomm if mode.endswith("oneshot") else None)
@@ -446,22 +442,20 @@ def main() -> None:
             torch.cuda.synchronize()
             gel = time.perf_counter() - t0
             if world > 1:
-                t = torch.tensor([gel], device=dev, dtype=torch.float64)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                gel = float(t.item())
-            gcn_res[mode] = {"ms_per_step": gel / a.gcn_steps * 1e3,
-                             "routes_per_s": nroutes * world * a.gcn_steps / gel}
+                (gel,) = allreduce_scalars([gel], dev, "max")
+            bench_schema.gcn_mode(gcn_res, mode, gel, a.gcn_steps, nroutes * world)
             del hip
 
     # config 5 on the same ranks: 10k concurrent multi-stop requests sharded over the ranks, each
     # step CCH road-metre matrices + K6 greedy for all of a rank's requests, then every trip leg as
     # one CCH query with its path unpacked, over MLP-learned edge times (no collective; timing max
     # over ranks).  The routing context's customization happens once, outside the timed steps, and
-    # is reported as `context_customize_ms` (a fresh context, measured separately).
+    # is reported as `context_customize_ms` (a fresh context, measured separately).  The shared-GPU
+    # rehearsal runs it too: each rank on GPU 0 with its share of the requests, reductions via gloo.
     route_res = None
     route_cost = None
     route_router = None
-    if a.route_steps > 0 and not (share and world > 1):
+    if a.route_steps > 0:
         from routest_amd.data.graph import synth_road_graph
         from routest_amd.routing.bulk import BulkRouteStep
         from routest_amd.routing.cch import RoadRouter, RouteContext
@@ -489,10 +483,10 @@ def main() -> None:
             torch.cuda.synchronize()
         except Exception as e:  # noqa: BLE001 - reported, never fatal for the headline
             route_err = repr(e)[:300]
-    if a.route_steps > 0 and not (share and world > 1) and not agree(route_err is None):
+    if a.route_steps > 0 and not agree(route_err is None):
         route_res = {"error": route_err or "route set-up failed on a peer rank"}
         route_router = None
-    elif a.route_steps > 0 and not (share and world > 1):
+    elif a.route_steps > 0:
         route_cost = cost
         if world > 1:
             dist.barrier()
@@ -508,22 +502,10 @@ def main() -> None:
         rel = time.perf_counter() - t0
         unfound = int(unfound)
         if world > 1:
-            t = torch.tensor([rel], device=dev, dtype=torch.float64)
-            tl = torch.tensor([float(legs), float(unfound)], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dist.all_reduce(tl)
-            rel, legs, unfound = float(t[0]), int(tl[0]), int(tl[1])
+            rel, legs, unfound = bench_schema.reduce_route_stats(rel, legs, unfound, dev)
         R = a.route_requests // world * world
-        route_res = {"requests_per_step": R, "steps": a.route_steps, "engine": "cch",
-                     "ms_per_step": rel / a.route_steps * 1e3,
-                     "requests_per_s": R * a.route_steps / rel,
-                     "legs_per_s": legs / rel, "unfound_legs": unfound,
-                     "graph_nodes": g.num_nodes,
-                     "context_customize_ms": ctx_ms,
-                     "context_cost_ms": ctx_info.get("cost_ms"),
-                     "context_customize_gpu_ms": ctx_info.get("customize_ms"),
-                     "topology_build_s": topo_s,
-                     "cch": {k: v for k, v in route_router.stats().items()}}
+        route_res = bench_schema.route_section(R, a.route_steps, rel, legs, unfound, g.num_nodes, ctx_ms,
+                                               ctx_info, topo_s, route_router.stats(), world)
         del bulk
 
     p50_ms = p99_ms = None
@@ -669,6 +651,7 @@ def main() -> None:
             "check_max_err_vs_fp32": err_fp32,
             "finite": ok,
         }
+        out["schema_problems"] = bench_schema.problems(out)
         print(json.dumps(out), flush=True)
     if devcomm is not None:
         torch.cuda.synchronize()

@@ -8,6 +8,7 @@
 #include <chrono>
 #include <memory>
 #include <mutex>
+#include <unordered_map>
 
 #include "cch_gpu.h"
 #include "ops.h"
@@ -102,8 +103,10 @@ class PyCchGpu {
     return d;
   }
 
-  // metric of a routing context (built on first use, then cached on the GPU)
-  py::dict metric_for(int64_t weather, int64_t congestion, int64_t weekhour, double age) {
+  // metric of a routing context (built on first use, then cached on the GPU).  pin: also hold it
+  // outside the LRU until unpin(key) — a caller that customizes several contexts and then queries
+  // them (a flush with more contexts than the cache holds) cannot lose one to eviction in between
+  py::dict metric_for(int64_t weather, int64_t congestion, int64_t weekhour, double age, bool pin) {
     TORCH_CHECK(g_->has_eta(), "CchGpu: set_eta first");
     rt::CchContext c;
     c.weather = (int)weather;
@@ -119,13 +122,29 @@ class PyCchGpu {
       e = g_->metric_for(c, stream_of(dev_), m, &fresh);
     }
     CCH_CHECK_HIP(e);
+    if (pin) pin_ptr(m);
     return info(*m, fresh);
+  }
+
+  void unpin(int64_t key) {
+    std::lock_guard<std::mutex> lk(pin_mu_);
+    auto it = pins_.find((uint64_t)key);
+    if (it != pins_.end() && --it->second.second <= 0) pins_.erase(it);
+  }
+  int64_t pinned() {
+    std::lock_guard<std::mutex> lk(pin_mu_);
+    return (int64_t)pins_.size();
   }
 
   py::dict metric_from_costs(int64_t key, torch::Tensor cost) {
     TORCH_CHECK(cost.is_cuda() && cost.device().index() == dev_ && cost.scalar_type() == torch::kFloat32 &&
                     cost.is_contiguous() && cost.numel() == g_->topo().E,
                 "cost: float32 [E] on the router's GPU");
+    // weights are ordered by their float bits (cch.h pack_w, atomicMin on the bits): NaN, negative
+    // costs and -0.0 would sort above every real weight and drop the edge — reject / normalise
+    TORCH_CHECK(torch::isfinite(cost).all().item<bool>() && (cost >= 0).all().item<bool>(),
+                "edge costs must be finite and >= 0");
+    cost = cost.add(0.0);                       // -0.0 -> +0.0
     const c10::DeviceGuard guard(cost.device());
     std::shared_ptr<rt::CchMetricDev> m;
     hipError_t e;
@@ -258,12 +277,27 @@ class PyCchGpu {
   }
 
  private:
+  void pin_ptr(const std::shared_ptr<rt::CchMetricDev>& m) {
+    std::lock_guard<std::mutex> lk(pin_mu_);
+    auto& p = pins_[m->key];
+    p.first = m;
+    ++p.second;
+  }
+
   std::shared_ptr<rt::CchMetricDev> get(int64_t key) {
     std::shared_ptr<rt::CchMetricDev> m;
-    TORCH_CHECK(g_->cached_metric((uint64_t)key, m), "CchGpu: no cached metric for key ", key,
-                " (evicted or never built)");
+    if (g_->cached_metric((uint64_t)key, m)) return m;
+    {
+      std::lock_guard<std::mutex> lk(pin_mu_);
+      auto it = pins_.find((uint64_t)key);
+      if (it != pins_.end()) return it->second.first;
+    }
+    TORCH_CHECK(false, "CchGpu: no cached metric for key ", key, " (evicted or never built)");
     return m;
   }
+
+  std::mutex pin_mu_;
+  std::unordered_map<uint64_t, std::pair<std::shared_ptr<rt::CchMetricDev>, int>> pins_;
 
   std::unique_ptr<rt::CchGpu> g_;
   std::unique_ptr<rt::CchScratch> sc_;
@@ -284,7 +318,9 @@ void bind_cch_gpu(py::module& m) {
       .def("set_eta", &PyCchGpu::set_eta, py::arg("blob"), py::arg("H"), py::arg("norm"), py::arg("variant") = -1)
       .def("stats", &PyCchGpu::stats)
       .def("metric_for", &PyCchGpu::metric_for, py::arg("weather"), py::arg("congestion"), py::arg("weekhour"),
-           py::arg("driver_age") = 35.0)
+           py::arg("driver_age") = 35.0, py::arg("pin") = false)
+      .def("unpin", &PyCchGpu::unpin, py::arg("key"))
+      .def("pinned", &PyCchGpu::pinned)
       .def("metric_from_costs", &PyCchGpu::metric_from_costs, py::arg("key"), py::arg("cost"))
       .def("costs", &PyCchGpu::costs, py::arg("key"))
       .def("route", &PyCchGpu::route, py::arg("key"), py::arg("src"), py::arg("dst"), py::arg("max_path") = 4096,

@@ -6,6 +6,8 @@
 #include <pybind11/stl.h>
 
 #include <chrono>
+#include <cmath>
+#include <vector>
 #include <memory>
 
 #include "cch.h"
@@ -86,12 +88,19 @@ class PyCCH {
 
   PyMetric customize(arr<float> cost, arr<float> length) {
     if (cost.shape(0) != T_.E || length.shape(0) != T_.E) throw std::invalid_argument("cost/length per edge");
+    // weights are ordered by their float bits (cch.h pack_w): a NaN, a negative cost or -0.0 (sign
+    // bit set) would sort above every real weight and silently drop the edge — reject / normalise
+    std::vector<float> c(cost.data(), cost.data() + T_.E);
+    for (float& x : c) {
+      if (!std::isfinite(x) || x < 0.f) throw std::invalid_argument("edge costs must be finite and >= 0");
+      x += 0.f;                                 // -0.0 -> +0.0
+    }
     PyMetric pm;
     pm.m = std::make_shared<rcch::Metric>();
     auto t0 = std::chrono::steady_clock::now();
     {
       py::gil_scoped_release nogil;
-      rcch::customize(T_, cost.data(), length.data(), *pm.m, pool_);
+      rcch::customize(T_, c.data(), length.data(), *pm.m, pool_);
     }
     pm.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return pm;

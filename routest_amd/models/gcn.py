@@ -106,7 +106,7 @@ class GcnScorerHip:
         self.b1 = model.b1.detach().float().to(d)
         self.b2 = model.b2.detach().float().to(d)
         self.wo = model.wo.detach().float().to(d)
-        self.bo = float(model.bo)
+        self.bo = float(model.bo.detach())
         self.fhid = model.W1.shape[1]
         self.fz = model.W2.shape[1]
         if mode == "partition" and world > 1:
@@ -160,7 +160,14 @@ class GcnScorerHip:
             self.comm.all_gather(own, full)
         else:
             import torch.distributed as dist
-            dist.all_gather_into_tensor(full, own.clone(), group=self.group)
+            if dist.get_backend(self.group) == "gloo":
+                # the shared-GPU rehearsal (every rank on one device, gloo rendezvous): staged
+                # through host memory; the driver's one-rank-per-GPU runs take the RCCL branch
+                h = torch.empty((full.shape[0],) + tuple(full.shape[1:]), dtype=full.dtype)
+                dist.all_gather_into_tensor(h, own.cpu(), group=self.group)
+                full.copy_(h)
+            else:
+                dist.all_gather_into_tensor(full, own.clone(), group=self.group)
 
     def score_routes(self, rptr: torch.Tensor, nodes: torch.Tensor) -> torch.Tensor:
         return self.C.route_score(rptr, nodes, self.latlon, self.delay)

@@ -150,8 +150,18 @@ def optimize_with_alternatives(payload: Dict[str, Any], provider, scorer, search
     ctx = None
     if getattr(provider, "uses_context", False):
         from .cch import RouteContext
-        ctx = RouteContext.from_request(payload)
-    key = provider.metric_key(ctx) if hasattr(provider, "metric_key") else None
+        ctx = RouteContext.from_request(payload)      # resolved once: planning and assembly agree
+    if hasattr(provider, "pinned_metric"):
+        with provider.pinned_metric(ctx) as key:      # the metric stays usable for the whole request
+            return _alternatives_on(payload, provider, scorer, search, engine, k, ctx, key)
+    return _alternatives_on(payload, provider, scorer, search, engine, k, ctx, None)
+
+
+def _alternatives_on(payload, provider, scorer, search, engine, k, ctx, key):
+    from .greedy import InfeasibleStops, greedy_trips
+    from .optimizer import _float, _vehicle_type, optimize_route
+    from .providers import profile_for
+    from .route_batcher import _LegView
     driver = payload.get("driver_details") or {}
     profile = profile_for(_vehicle_type(driver))
     pts = [payload["source_point"]] + list(payload["destination_points"])
@@ -182,9 +192,12 @@ def optimize_with_alternatives(payload: Dict[str, Any], provider, scorer, search
             out = search([a for a, _ in q], [b for _, b in q])
             return [(c, float("nan"), p) for c, p in out]
     chosen, info = AlternativeLegs(provider.g, scorer, run).choose(pairs, k)
-    view = _LegView(provider, {(key, s, t): v for (s, t), v in chosen.items()} if key is not None else chosen)
+    hc = ({key: provider.edge_seconds(key)} if key is not None and getattr(provider, "_steps", None) is not None
+          else None)
+    view = _LegView(provider, {(key, s, t): v for (s, t), v in chosen.items()} if key is not None else chosen,
+                    host_costs=hc)
     try:
-        res = optimize_route(payload, view, engine, trips=trips)
+        res = optimize_route(payload, view, engine, trips=trips, ctx=ctx)
     except ProviderError as e:
         return {"error": str(e)}
     if "error" not in res:

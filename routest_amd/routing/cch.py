@@ -24,6 +24,7 @@ from __future__ import annotations
 import datetime as dt
 import threading
 from collections import OrderedDict
+from contextlib import contextmanager
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -126,6 +127,7 @@ class RoadRouter:
                               np.ascontiguousarray(g.lon, dtype=np.float64), threads)
             self._cpu_metrics: "OrderedDict[int, Any]" = OrderedDict()
             self._cpu_costs: Dict[int, np.ndarray] = {}
+            self._cpu_pins: Dict[int, int] = {}
             self.capacity = capacity
         self.last_metric: Dict[str, Any] = {}
 
@@ -133,26 +135,62 @@ class RoadRouter:
     def stats(self) -> Dict[str, Any]:
         return dict(self.gpu.stats() if self.gpu is not None else self.cpu.stats())
 
-    def metric(self, ctx: RouteContext) -> int:
-        """Make sure the context's metric is customized (and cached); returns its key."""
+    def metric(self, ctx: RouteContext, pin: bool = False) -> int:
+        """Make sure the context's metric is customized (and cached); returns its key.  ``pin``:
+        also hold it outside the LRU until :meth:`unpin` (see :meth:`pinned`)."""
         if self.gpu is not None:
             self.last_metric = dict(self.gpu.metric_for(ctx.weather, ctx.congestion, ctx.weekhour,
-                                                        ctx.driver_age))
+                                                        ctx.driver_age, pin))
             return ctx.key
         with self._lock:
             if ctx.key in self._cpu_metrics:
                 self._cpu_metrics.move_to_end(ctx.key)
                 self.last_metric = {"key": ctx.key, "fresh": False}
-                return ctx.key
-            cost = context_costs_cpu(self.g, self.eta_model, ctx)
-            m = self.cpu.customize(cost, self._length)
-            self._cpu_metrics[ctx.key] = m
-            self._cpu_costs[ctx.key] = cost
-            while len(self._cpu_metrics) > self.capacity:
-                k, _ = self._cpu_metrics.popitem(last=False)
-                self._cpu_costs.pop(k, None)
-            self.last_metric = {"key": ctx.key, "fresh": True, "customize_ms": m.customize_ms}
+            else:
+                cost = context_costs_cpu(self.g, self.eta_model, ctx)
+                m = self.cpu.customize(cost, self._length)
+                self._cpu_metrics[ctx.key] = m
+                self._cpu_costs[ctx.key] = cost
+                self.last_metric = {"key": ctx.key, "fresh": True, "customize_ms": m.customize_ms}
+            if pin:
+                self._cpu_pins[ctx.key] = self._cpu_pins.get(ctx.key, 0) + 1
+            self._evict_cpu()
             return ctx.key
+
+    def _evict_cpu(self) -> None:
+        """LRU beyond ``capacity``, never a pinned metric (caller holds the lock)."""
+        while len(self._cpu_metrics) > self.capacity:
+            k = next((k for k in self._cpu_metrics if k not in self._cpu_pins), None)
+            if k is None:
+                return
+            del self._cpu_metrics[k]
+            self._cpu_costs.pop(k, None)
+
+    def unpin(self, key: int) -> None:
+        if self.gpu is not None:
+            self.gpu.unpin(int(key))
+            return
+        with self._lock:
+            n = self._cpu_pins.get(int(key), 0) - 1
+            if n > 0:
+                self._cpu_pins[int(key)] = n
+            else:
+                self._cpu_pins.pop(int(key), None)
+                self._evict_cpu()
+
+    @contextmanager
+    def pinned(self, ctx_or_key):
+        """``with router.pinned(ctx) as key:`` — the context's metric (customized if needed) stays
+        usable for the whole block, however many other contexts are built meanwhile (a flush with
+        more contexts than the cache holds, or concurrent callers on the same router)."""
+        if isinstance(ctx_or_key, RouteContext):
+            key = self.metric(ctx_or_key, pin=True)
+            try:
+                yield key
+            finally:
+                self.unpin(key)
+        else:
+            yield int(ctx_or_key)
 
     def metric_from_costs(self, key: int, cost: np.ndarray) -> int:
         """A metric from given edge costs (tests / benches), cached under ``key``."""
@@ -175,7 +213,10 @@ class RoadRouter:
     def route(self, src: Sequence[int], dst: Sequence[int], ctx_or_key, want_path: bool = True):
         """(sec [Q], metres [Q], status [Q], paths: list of node-id arrays) — status 0 found,
         1 unreachable, 4 longer than max_path."""
-        key = self.metric(ctx_or_key) if isinstance(ctx_or_key, RouteContext) else int(ctx_or_key)
+        with self.pinned(ctx_or_key) as key:
+            return self._route(src, dst, key, want_path)
+
+    def _route(self, src, dst, key: int, want_path: bool):
         s = np.ascontiguousarray(src, dtype=np.int32)
         t = np.ascontiguousarray(dst, dtype=np.int32)
         if self.gpu is not None:
@@ -192,7 +233,10 @@ class RoadRouter:
 
     def matrix(self, nodes: Sequence[int], ctx_or_key) -> Tuple[np.ndarray, np.ndarray]:
         """(seconds, metres) [n, n] between the given nodes (the diagonal is 0; unreachable = inf)."""
-        key = self.metric(ctx_or_key) if isinstance(ctx_or_key, RouteContext) else int(ctx_or_key)
+        with self.pinned(ctx_or_key) as key:
+            return self._matrix(nodes, key)
+
+    def _matrix(self, nodes, key: int):
         n = len(nodes)
         if self.gpu is not None:
             pts = torch.tensor(np.asarray(nodes, dtype=np.int32)[None, :], device=self.dev)
@@ -210,9 +254,12 @@ class RoadRouter:
 
     def matrices(self, node_lists: Sequence[Sequence[int]], ctx_or_key) -> List[Tuple[np.ndarray, np.ndarray]]:
         """Many requests' matrices at once (ONE sweep + meet launch on the GPU)."""
-        if self.gpu is None or not node_lists:
-            return [self.matrix(n, ctx_or_key) for n in node_lists]
-        key = self.metric(ctx_or_key) if isinstance(ctx_or_key, RouteContext) else int(ctx_or_key)
+        with self.pinned(ctx_or_key) as key:
+            if self.gpu is None or not node_lists:
+                return [self._matrix(n, key) for n in node_lists]
+            return self._matrices(node_lists, key)
+
+    def _matrices(self, node_lists, key: int):
         NM = max(len(n) for n in node_lists)
         pts = np.zeros((len(node_lists), NM), dtype=np.int32)
         npts = np.zeros(len(node_lists), dtype=np.int32)

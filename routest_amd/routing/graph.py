@@ -487,7 +487,8 @@ class GraphProvider(HaversineProvider):
         self._astar = None
         self._csr = None
         self._routers: Dict[str, Any] = {}
-        self._host_costs: Dict[int, np.ndarray] = {}
+        from collections import OrderedDict
+        self._host_costs: "OrderedDict[int, np.ndarray]" = OrderedDict()   # LRU, HOST_COSTS entries
         import threading
         self._lock = threading.Lock()
         self._steps = None
@@ -524,23 +525,40 @@ class GraphProvider(HaversineProvider):
                 self._routers[key] = r
             return r
 
+    HOST_COSTS = 64        # host copies of metrics' edge costs kept (LRU)
+
     def metric_key(self, ctx=None, device=None) -> int:
-        """The metric a request routes on: the fixed one, or its context's (customized on demand)."""
+        """The metric a request routes on: the fixed one, or its context's (customized on demand).
+        The returned key may be evicted again by later customizations: callers that query with it
+        hold :meth:`pinned_metric` instead."""
         if not self.uses_context:
             return self.FIXED_KEY
         from .cch import RouteContext
         return self.router(device).metric(ctx or RouteContext())
 
+    def pinned_metric(self, ctx=None, device=None):
+        """``with prov.pinned_metric(ctx, dev) as key:`` — the request's metric, usable (not evicted)
+        for the whole block."""
+        import contextlib
+        if not self.uses_context:
+            return contextlib.nullcontext(self.FIXED_KEY)
+        from .cch import RouteContext
+        return self.router(device).pinned(ctx or RouteContext())
+
     def edge_seconds(self, key: int, device=None) -> np.ndarray:
-        """Host copy of a metric's edge costs (maneuver durations)."""
+        """Host copy of a metric's edge costs (maneuver durations); LRU of HOST_COSTS metrics."""
         if key == self.FIXED_KEY and self.cost is not None:
             return self.cost
-        c = self._host_costs.get(key)
-        if c is None:
-            c = np.ascontiguousarray(self.router(device).costs(key), dtype=np.float32)
-            if len(self._host_costs) > 64:
-                self._host_costs.clear()
+        with self._lock:
+            c = self._host_costs.get(key)
+            if c is not None:
+                self._host_costs.move_to_end(key)
+                return c
+        c = np.ascontiguousarray(self.router(device).costs(key), dtype=np.float32)
+        with self._lock:
             self._host_costs[key] = c
+            while len(self._host_costs) > self.HOST_COSTS:
+                self._host_costs.popitem(last=False)
         return c
 
     def legs(self, pairs: List[Tuple[int, int]], ctx=None, device=None, key: Optional[int] = None):
@@ -551,7 +569,8 @@ class GraphProvider(HaversineProvider):
                     for sec, p in self._shortest_astar(pairs)], self.FIXED_KEY
         r = self.router(device)
         if key is None:
-            key = self.metric_key(ctx, device)
+            with self.pinned_metric(ctx, device) as k:
+                return self.legs(pairs, device=device, key=k)
         if not pairs:
             return [], key
         sec, met, st, paths = r.route([p[0] for p in pairs], [p[1] for p in pairs], key)
@@ -604,16 +623,18 @@ class GraphProvider(HaversineProvider):
             D = np.array([m if i != j else 0.0 for (i, j), (_, m, _) in
                           zip([(i, j) for i in range(n) for j in range(n)], L)]).reshape(n, n)
             return np.where(np.isfinite(D), D, np.inf)
-        _, met = self.router().matrix(list(map(int, nodes)), self.metric_key(ctx))
+        with self.pinned_metric(ctx) as key:
+            _, met = self.router().matrix(list(map(int, nodes)), key)
         return met.astype(np.float64)
 
     def directions(self, coords: List[List[float]], profile: str, ctx=None) -> Dict[str, Any]:
         nodes, pairs = self.leg_pairs(coords)
-        legs, key = self.legs(pairs, ctx)
-        return self.feature_from_legs(coords, nodes, legs, profile, key=key)
+        with self.pinned_metric(ctx) as key:
+            legs, key = self.legs(pairs, key=key)
+            return self.feature_from_legs(coords, nodes, legs, profile, key=key)
 
     def feature_from_legs(self, coords: List[List[float]], nodes, legs, profile: str,
-                          key: Optional[int] = None, device=None) -> Dict[str, Any]:
+                          key: Optional[int] = None, device=None, ecost=None) -> Dict[str, Any]:
         """ORS-shaped Feature from per-leg (seconds, metres, node path) results (or the legacy
         (seconds, node path)).  A leg the search did not find (disconnected stops) is an explicit
         :class:`ProviderError`, never a silent straight line."""
@@ -621,8 +642,9 @@ class GraphProvider(HaversineProvider):
         geometry: List[List[float]] = [[float(coords[0][0]), float(coords[0][1])]]
         segments, way_points = [], [0]
         tot_d = tot_t = 0.0
-        ecost = None
-        if self._steps is not None and key is not None and self.engine != "astar":
+        if self._steps is None or self.engine == "astar":
+            ecost = None
+        elif ecost is None and key is not None:
             ecost = self.edge_seconds(key, device)
         for k, leg in enumerate(legs):
             sec, metres, path = leg if len(leg) == 3 else (leg[0], None, leg[1])

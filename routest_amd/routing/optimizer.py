@@ -121,8 +121,10 @@ def multi_stop(provider, source, destinations, profile: str, driver: Dict[str, A
 
 
 def optimize_route(input_data: Any, provider, engine: str = "backend:mi355x",
-                   trips: Optional[List[List[int]]] = None) -> Dict[str, Any]:
-    """Pure function: GeoJSON Feature on success, ``{"error": ...}`` on failure (R19)."""
+                   trips: Optional[List[List[int]]] = None, ctx=None) -> Dict[str, Any]:
+    """Pure function: GeoJSON Feature on success, ``{"error": ...}`` on failure (R19).  ``ctx``:
+    the request's routing context as resolved when its legs were planned (the batcher), so a
+    request without ``pickup_time`` is assembled under the same week-hour it was routed in."""
     if not input_data or not isinstance(input_data, dict) or not input_data.get("destination_points"):
         return {"error": "no destination points specified."}
     driver = input_data.get("driver_details") or {}
@@ -133,8 +135,9 @@ def optimize_route(input_data: Any, provider, engine: str = "backend:mi355x",
         return {"error": "source_point with lat/lon is required."}
     destinations = input_data["destination_points"]
     # road providers route under the request's context (weather, traffic, pickup week-hour)
-    ctx = None
-    if getattr(provider, "uses_context", False):
+    if not getattr(provider, "uses_context", False):
+        ctx = None
+    elif ctx is None:
         from .cch import RouteContext
         ctx = RouteContext.from_request(input_data)
     if len(destinations) == 1:

@@ -53,27 +53,40 @@ def _valid_points(r: Any) -> bool:
 
 class _LegView:
     """Provider view for the host-side assembly of one flush: ``directions`` answers from the legs
-    searched in the batch's launches (keyed by the metric they were routed on); everything else
-    delegates to the real provider."""
+    searched in the batch's launches (keyed by the metric they were routed on) and the host copies
+    of those metrics' edge costs taken while they were pinned; everything else delegates to the
+    real provider.  Nothing here customizes or looks up a GPU metric, so assembly cannot stall on
+    (or fail by) a context evicted since the plan."""
 
-    def __init__(self, base, legs: Dict[tuple, tuple], device=None):
+    def __init__(self, base, legs: Dict[tuple, tuple], device=None,
+                 host_costs: Optional[Dict[int, np.ndarray]] = None):
         self.base = base
         self.legs = legs
         self.name = base.name
         self.uses_context = getattr(base, "uses_context", False)
         self.device = device
+        self.host_costs = host_costs or {}
 
     def matrix(self, points, profile, **kw):
         return self.base.matrix(points, profile, **kw)
 
+    def _key(self, ctx) -> Optional[int]:
+        if not hasattr(self.base, "metric_key"):
+            return None
+        if self.uses_context:
+            from .cch import RouteContext
+            return (ctx or RouteContext()).key
+        return self.base.metric_key(None, self.device)
+
     def directions(self, coords, profile, ctx=None):
         nodes, pairs = self.base.leg_pairs(coords)
-        key = self.base.metric_key(ctx, self.device) if hasattr(self.base, "metric_key") else None
+        key = self._key(ctx)
         # keyed by (metric, s, t); plain (s, t) keys (routing/alternatives.py) hold fixed-metric legs
         legs = [self.legs[(key, p[0], p[1])] if (key, p[0], p[1]) in self.legs else self.legs[p] for p in pairs]
         if key is None:
             return self.base.feature_from_legs(coords, nodes, legs, profile)
-        return self.base.feature_from_legs(coords, nodes, legs, profile, key=key, device=self.device)
+        return self.base.feature_from_legs(coords, nodes, legs, profile, key=key, device=self.device,
+                                           ecost=self.host_costs.get(key))
 
 
 class RouteBatcher:
@@ -108,63 +121,78 @@ class RouteBatcher:
                 self._astar[key] = a
             return a
 
-    def _ctx_key(self, payload: Any, device):
-        prov = self.provider
-        if not getattr(prov, "uses_context", False):
-            return None, prov.metric_key(None, device) if hasattr(prov, "metric_key") else None
+    def _contexts(self, payloads: List[Any]) -> List[Any]:
+        """Each request's routing context, resolved ONCE per flush (one ``now`` for requests
+        without a pickup time); carried to assembly with the plan."""
+        if not getattr(self.provider, "uses_context", False):
+            return [None] * len(payloads)
+        import datetime as dt
         from .cch import RouteContext
-        ctx = RouteContext.from_request(payload)
-        return ctx, prov.metric_key(ctx, device)
+        now = dt.datetime.now()
+        return [RouteContext.from_request(p, now=now) if _valid_points(p) else None for p in payloads]
 
-    def _graph_plan(self, payloads: List[Any], device) -> tuple:
+    def _graph_plan(self, payloads: List[Any], device, ctxs: List[Any]) -> tuple:
         """Road-graph flush: per routing context, ONE many-to-many launch for every multi-stop
         request's road-metre matrix, ONE greedy launch (K6) over those matrices, then every trip leg
-        (and point-to-point request) in ONE leg launch.  Returns (trips by request, legs dict)."""
+        (and point-to-point request) in ONE leg launch.  Each context group runs start to finish
+        under a pin of its metric, and its edge costs are copied to the host then, so a flush with
+        more contexts than the metric cache holds never loses one in between.  Returns (trips by
+        request, legs dict, host edge costs by metric key)."""
         prov = self.provider
         trips: Dict[int, Any] = {}
         legs: Dict[tuple, tuple] = {}
+        host_costs: Dict[int, np.ndarray] = {}
         valid = [k for k, r in enumerate(payloads) if _valid_points(r)]
         if not valid:
-            return trips, legs
+            return trips, legs, host_costs
         groups: Dict[Any, List[int]] = {}
+        first: Dict[Any, Any] = {}
         for k in valid:
-            _, key = self._ctx_key(payloads[k], device)
-            groups.setdefault(key, []).append(k)
-        for key, ks in groups.items():
-            pts = {k: [payloads[k]["source_point"]] + list(payloads[k]["destination_points"]) for k in ks}
-            flat = np.array([[p["lon"], p["lat"]] for k in ks for p in pts[k]], dtype=np.float64)
-            nodes_all = prov.g.nearest_nodes(flat[:, 1], flat[:, 0])
-            nodes: Dict[int, np.ndarray] = {}
-            o = 0
-            for k in ks:
-                nodes[k] = nodes_all[o:o + len(pts[k])]
-                o += len(pts[k])
-            multi = [k for k in ks if len(pts[k]) > 2]
-            if multi:
-                mats = prov.router(device).matrices([nodes[k].tolist() for k in multi], key)
-                nm = max(len(pts[k]) for k in multi)
-                D = np.zeros((len(multi), nm, nm))
-                for i, (k, (_, met)) in enumerate(zip(multi, mats)):
-                    n = len(pts[k])
-                    D[i, :n, :n] = met
-                res = batched_trips([payloads[k] for k in multi], device=device, D=D)
-                trips.update(zip(multi, res))
-            pairs = set()
-            for k in ks:
-                if len(pts[k]) == 2:
-                    seqs = [[0, 1]]
-                elif isinstance(trips.get(k), list):
-                    seqs = trips[k]
-                else:
-                    continue
-                for seq in seqs:
-                    n = nodes[k][seq]
-                    pairs.update((int(n[i]), int(n[i + 1])) for i in range(len(n) - 1))
-            pairs = sorted(pairs)
-            if pairs:
-                res, _ = prov.legs(pairs, key=key, device=device)
-                legs.update({(key, s, t): r for (s, t), r in zip(pairs, res)})
-        return trips, legs
+            gk = ctxs[k].key if ctxs[k] is not None else None
+            groups.setdefault(gk, []).append(k)
+            first.setdefault(gk, ctxs[k])
+        for gk, ks in groups.items():
+            with prov.pinned_metric(first[gk], device) as key:
+                self._plan_group(payloads, ks, key, device, trips, legs)
+                if getattr(prov, "_steps", None) is not None:
+                    host_costs[key] = prov.edge_seconds(key, device)
+        return trips, legs, host_costs
+
+    def _plan_group(self, payloads, ks, key, device, trips, legs) -> None:
+        prov = self.provider
+        pts = {k: [payloads[k]["source_point"]] + list(payloads[k]["destination_points"]) for k in ks}
+        flat = np.array([[p["lon"], p["lat"]] for k in ks for p in pts[k]], dtype=np.float64)
+        nodes_all = prov.g.nearest_nodes(flat[:, 1], flat[:, 0])
+        nodes: Dict[int, np.ndarray] = {}
+        o = 0
+        for k in ks:
+            nodes[k] = nodes_all[o:o + len(pts[k])]
+            o += len(pts[k])
+        multi = [k for k in ks if len(pts[k]) > 2]
+        if multi:
+            mats = prov.router(device).matrices([nodes[k].tolist() for k in multi], key)
+            nm = max(len(pts[k]) for k in multi)
+            D = np.zeros((len(multi), nm, nm))
+            for i, (k, (_, met)) in enumerate(zip(multi, mats)):
+                n = len(pts[k])
+                D[i, :n, :n] = met
+            res = batched_trips([payloads[k] for k in multi], device=device, D=D)
+            trips.update(zip(multi, res))
+        pairs = set()
+        for k in ks:
+            if len(pts[k]) == 2:
+                seqs = [[0, 1]]
+            elif isinstance(trips.get(k), list):
+                seqs = trips[k]
+            else:
+                continue
+            for seq in seqs:
+                n = nodes[k][seq]
+                pairs.update((int(n[i]), int(n[i + 1])) for i in range(len(n) - 1))
+        pairs = sorted(pairs)
+        if pairs:
+            res, _ = prov.legs(pairs, key=key, device=device)
+            legs.update({(key, s, t): r for (s, t), r in zip(pairs, res)})
 
     def _graph_legs(self, payloads: List[Any], trips: Dict[int, Any], device) -> Dict[tuple, tuple]:
         """Legacy A* engine: every leg of the flush -> {(key, s, t): (seconds, node path)} from ONE
@@ -201,18 +229,19 @@ class RouteBatcher:
         return {(key, s, t): r for (s, t), r in zip(pairs, res)}
 
     def plan_batch(self, payloads: Sequence[Any], device=None) -> List[tuple]:
-        """The GPU phases of a flush: per request ``(trips or InfeasibleStops or None, view)``."""
+        """The GPU phases of a flush: per request ``(trips or InfeasibleStops or None, view, ctx)``."""
         payloads = list(payloads)
         name = getattr(self.provider, "name", "")
         trips: Dict[int, Any] = {}
         view = self.provider
         if name == "graph" and getattr(self.provider, "engine", "astar") != "astar":
+            ctxs = self._contexts(payloads)
             try:
-                trips, legs = self._graph_plan(payloads, device)
+                trips, legs, hc = self._graph_plan(payloads, device, ctxs)
             except ProviderError as e:
-                return [(e, None) for _ in payloads]
-            view = _LegView(self.provider, legs, device)
-            return [(trips.get(k), view) for k in range(len(payloads))]
+                return [(e, None, None) for _ in payloads]
+            view = _LegView(self.provider, legs, device, hc)
+            return [(trips.get(k), view, ctxs[k]) for k in range(len(payloads))]
         multi = [k for k, r in enumerate(payloads) if _valid_points(r) and len(r["destination_points"]) > 1]
         if multi and name in ("haversine", "graph"):
             res = batched_trips([payloads[k] for k in multi], circuity=self.provider.circuity,
@@ -222,15 +251,16 @@ class RouteBatcher:
             try:
                 view = _LegView(self.provider, self._graph_legs(payloads, trips, device), device)
             except ProviderError as e:
-                return [(e, None) for _ in payloads]
-        return [(trips.get(k), view) for k in range(len(payloads))]
+                return [(e, None, None) for _ in payloads]
+        return [(trips.get(k), view, None) for k in range(len(payloads))]
 
     def assemble(self, payload: Any, plan: tuple) -> Dict[str, Any]:
-        """Host side of one request: GeoJSON Feature (or error) from its planned trips/legs."""
-        t, view = plan
+        """Host side of one request: GeoJSON Feature (or error) from its planned trips/legs, under
+        the routing context it was planned with."""
+        t, view, ctx = plan
         if isinstance(t, (InfeasibleStops, ProviderError)):
             return {"error": str(t)}
-        return optimize_route(payload, view, self.engine, trips=t)
+        return optimize_route(payload, view, self.engine, trips=t, ctx=ctx)
 
     def run_batch(self, payloads: Sequence[Any], device=None) -> List[Dict[str, Any]]:
         """Optimise a list of request payloads together (plan + assembly; also callable directly,

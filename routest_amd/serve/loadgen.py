@@ -46,7 +46,8 @@ def native_route_load(stack, reqs: Sequence[Dict[str, Any]], concurrency: int, s
     f1 = stack.front.stats()
     lat_us = r["latencies_us"]
     flushes = max(1, f1["route_flushes"] - f0["route_flushes"])
-    return {"req_per_s": r["requests"] / r["seconds"], "errors": int(r["errors"]),
+    return {"concurrency": concurrency, "seconds": r["seconds"], "requests": int(r["requests"]),
+            "req_per_s": r["requests"] / r["seconds"], "errors": int(r["errors"]),
             "p50_ms": _pct(lat_us, 0.5), "p99_ms": _pct(lat_us, 0.99),
             "response_MB_per_s": r["bytes"] / r["seconds"] / 1e6,
             "flushes": f1["route_flushes"] - f0["route_flushes"],

@@ -36,13 +36,15 @@ def test_bench_spawns_ranks_itself_shared_gpu():
     env = dict(os.environ, ROUTEST_BENCH_SHARE_GPU="1")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
-                        "--warmup", "1", "--batch", "262144", "--p50", "0", "--rec16-steps", "2"],
+                        "--warmup", "1", "--batch", "262144", "--p50", "0", "--rec16-steps", "2",
+                        "--gcn-steps", "0", "--route-steps", "0"],
                        capture_output=True, text=True, timeout=115, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["shared_gpu"] is True and d["finite"] is True
+    assert d["schema_problems"] == [], d["schema_problems"]
     assert d["config"]["global_batch"] == 2 * 262144
     # two ranks time-sharing one GPU through gloo barriers: a sanity floor, not a rate claim
     assert d["preds_per_s_rec16"] > 1e7
@@ -64,6 +66,7 @@ def test_bench_route_optimizer_probe():
     ro = d["route_optimizer"]
     assert ro["requests_per_step"] == 2000 and ro["steps"] == 2
     assert ro["engine"] == "cch" and ro["unfound_legs"] == 0 and ro["requests_per_s"] > 1e3
+    assert d["schema_problems"] == [], d["schema_problems"]
 
 
 def test_bench_fails_loud_on_too_many_gpus():

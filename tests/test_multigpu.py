@@ -19,6 +19,8 @@ import numpy as np
 import pytest
 import torch
 
+from routest_amd.utils import bench_schema as S
+
 SHARE = os.environ.get("ROUTEST_TEST_SHARE_GPU", "0") == "1"
 pytestmark = [pytest.mark.gpu] + ([] if SHARE else [pytest.mark.multigpu])
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -186,9 +188,19 @@ def test_bench_launches_all_gpus():
     d = json.loads(lines[0])
     assert d["n_gpus"] == n and d["finite"] is True and d["shared_gpu"] is SHARE
     assert d["config"]["global_batch"] == n * 1048576
+    # every section ran and carries the schema's keys (routest_amd/utils/bench_schema.py)
+    assert d["schema_problems"] == [], d["schema_problems"]
     os_ = d["dp_training_oneshot"]
     assert os_ and os_.get("params_identical_across_ranks") is True, os_
     if not SHARE:
         assert d["collectives"] and "error" not in d["collectives"][0]
-        assert d["gcn"]["partition"]["ms_per_step"] > 0 and d["gcn"]["partition_oneshot"]["ms_per_step"] > 0
-        assert d["route_optimizer"]["astar_unfound_legs"] == 0
+    # the GCN partition over the process group (RCCL; gloo via host memory when rehearsing on one
+    # GPU) and over the native one-shot all-gather
+    gcn = d["gcn"]
+    assert set(S.GCN_MODES_N) | {S.GCN_MODE_ONESHOT} <= set(gcn["modes"]), gcn
+    for m in gcn["modes"]:
+        assert gcn[m]["ms_per_step"] > 0, (m, gcn)
+    # the route section: each rank its share of the requests, reductions over every rank
+    ro = d["route_optimizer"]
+    assert ro["ranks"] == n and ro["requests_per_step"] == 2000 // n * n, ro
+    assert ro[S.ROUTE_UNFOUND] == 0 and ro["requests_per_s"] > 0, ro

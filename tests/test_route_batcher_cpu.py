@@ -134,3 +134,94 @@ def test_unfound_leg_is_an_explicit_error():
         assert "no road path" in rb.run_batch([req])[0]["error"]
     finally:
         rb.close()
+
+
+def _ctx_requests(g, n, hours, seed=9):
+    rng = np.random.default_rng(seed)
+    reqs = []
+    for i in range(n):
+        idx = rng.integers(0, g.num_nodes, int(rng.integers(2, 6)))
+        reqs.append({"source_point": {"lat": float(g.lat[idx[0]]), "lon": float(g.lon[idx[0]])},
+                     "destination_points": [{"lat": float(g.lat[j]), "lon": float(g.lon[j]), "payload": 1}
+                                            for j in idx[1:]],
+                     "driver_details": {"driver_name": f"c{i}", "vehicle_capacity": 3, "maximum_distance": 1e7},
+                     "context": {"weather": ["Sunny", "Stormy"][i % 2], "traffic": "Medium",
+                                 "pickup_time": f"2026-10-1{i % 3 + 2}T{hours[i % len(hours)]:02d}:15:00"}})
+    return reqs
+
+
+def test_flush_with_more_contexts_than_the_cache_holds():
+    """every context group of a flush is planned under a pin of its metric, so
+    more distinct contexts than the LRU holds cannot evict a group's metric before it is used."""
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider
+    from routest_amd.serve.eta_service import default_model
+    g = synth_road_graph(2500, seed=4)
+    prov = GraphProvider(g, None, eta_model=default_model(hidden=32, steps=20))
+    r = prov.router()
+    r.capacity = 2                                   # far fewer than the flush's contexts
+    reqs = _ctx_requests(g, 24, hours=[7, 8, 9, 17])
+    rb = RouteBatcher(prov, devices=[None])
+    try:
+        got = rb.run_batch(reqs, None)
+    finally:
+        rb.close()
+    assert all("error" not in x for x in got), [x.get("error") for x in got]
+    assert len(r._cpu_metrics) <= 2 and not r._cpu_pins
+    ref = [optimize_route(q, prov, "backend:mi355x") for q in reqs]
+    assert got == ref
+
+
+def test_plan_carries_the_context_to_assembly():
+    """the context of a request without pickup_time is resolved once, in the
+    plan; assembly neither recomputes it from now() nor customizes anything."""
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider
+    from routest_amd.serve.eta_service import default_model
+    g = synth_road_graph(2000, seed=5)
+    prov = GraphProvider(g, None, eta_model=default_model(hidden=32, steps=20))
+    req = _ctx_requests(g, 1, hours=[10])[0]
+    del req["context"]["pickup_time"]
+    rb = RouteBatcher(prov, devices=[None])
+    try:
+        plan = rb.plan_batch([req], None)[0]
+        assert plan[2] is not None and plan[2].key in {k for (k, _, _) in plan[1].legs}
+
+        def boom(*a, **k):
+            raise AssertionError("assembly must not customize")
+        prov.metric_key = boom
+        prov.pinned_metric = boom
+        out = rb.assemble(req, plan)
+    finally:
+        rb.close()
+    assert "error" not in out and out["properties"]["summary"]["distance"] > 0
+
+
+def test_cch_rejects_nan_and_negative_costs():
+    """costs are ordered by their float bits; NaN / negative are rejected and
+    -0.0 (a zero-length edge) routes like +0.0."""
+    rt = pytest.importorskip("routest_amd._rt")
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import dijkstra_ref
+    g = synth_road_graph(800, seed=1)
+    c = rt.CCH(g.indptr, g.indices, g.lat, g.lon, 2)
+    length = g.length_m.astype(np.float32)
+    cost = (length / 10.0).astype(np.float32)
+    for bad in (np.nan, -1.0, np.inf):
+        cb = cost.copy()
+        cb[5] = bad
+        with pytest.raises(ValueError):
+            c.customize(cb, length)
+    src = np.arange(0, 60, dtype=np.int32)
+    dst = np.arange(400, 460, dtype=np.int32)
+    cp, cz = cost.copy(), cost.copy()
+    cp[:80] = 0.0
+    cz[:80] = -0.0
+    sp, _, stp, _ = c.query(c.customize(cp, length), src, dst, False, 4096)
+    sz, _, stz, _ = c.query(c.customize(cz, length), src, dst, False, 4096)
+    assert np.array_equal(np.asarray(stp), np.asarray(stz)) and np.array_equal(np.asarray(sp), np.asarray(sz))
+    ref = dijkstra_ref(g, cost, src, dst)
+    s0, _, st0, _ = c.query(c.customize(cost, length), src, dst, False, 4096)
+    ok = np.isfinite(ref)
+    assert (np.asarray(st0)[ok] == 0).all()
+    np.testing.assert_allclose(np.asarray(s0)[ok], ref[ok], rtol=1e-5)
