@@ -1176,6 +1176,8 @@ py::dict native_server_health(int64_t h) {
     d["quarantines"] = std::stoll(r[5]);
     d["fault_injected"] = r[6] == "1";
     d["model"] = r[7];
+    d["deadline_timeouts"] = std::stoll(r[8]);
+    d["hang_injected"] = r[9] == "1";
     slots.append(d);
   }
   py::dict out;
@@ -1395,6 +1397,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("native_server_set_fault", [](int64_t h, int64_t slot, bool on) {
     return rt::native_server_set_fault(h, (int)slot, on);
   });
+  m.def("native_server_set_hang", [](int64_t h, int64_t slot, bool on) {
+    return rt::native_server_set_hang(h, (int)slot, on);
+  }, "latency-watchdog fault hook: launches on the slot first wait on a host flag");
   m.def("native_server_set_scorer", [](int64_t h, std::vector<double> delay, int64_t kind, std::string engine) {
     return rt::native_server_set_scorer(h, std::move(delay), (int)kind, engine);
   }, "publish the GCN scorer's node delays for native \"alternatives\" requests");

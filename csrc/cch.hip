@@ -964,9 +964,17 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   }
   (void)hipSetDevice(cur);
   if (e != hipSuccess) throw std::runtime_error(std::string("CchGpu: ") + hipGetErrorString(e));
+  if (const char* gb = std::getenv("ROUTEST_CCH_CACHE_GB")) cache_gb_ = std::atof(gb);
 }
 
 CchGpu::~CchGpu() {
+  {
+    std::lock_guard<std::mutex> lk(bmu_);
+    bstop_ = true;
+    bq_.clear();
+  }
+  bcv_.notify_all();
+  if (bth_.joinable()) bth_.join();
   {
     std::lock_guard<std::mutex> lk(mu_);
     cache_.clear();
@@ -1124,16 +1132,119 @@ hipError_t CchGpu::metric_from_costs(uint64_t key, const float* d_cost, hipStrea
   m->key = key;
   hipError_t e = customize(d_cost, *m, s);
   if (e != hipSuccess) return e;
-  std::lock_guard<std::mutex> lk(mu_);
-  for (auto it = cache_.begin(); it != cache_.end(); ++it)
-    if ((*it)->key == key) {
-      cache_.erase(it);
-      break;
-    }
-  cache_.push_front(m);
-  while ((int)cache_.size() > capacity_) cache_.pop_back();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto it = cache_.begin(); it != cache_.end(); ++it)
+      if ((*it)->key == key) {
+        cache_.erase(it);
+        break;
+      }
+  }
+  insert_cached(m);
   out = m;
   return hipSuccess;
+}
+
+// device bytes of one customized metric (what the LRU budget is divided by)
+static int64_t metric_device_bytes(const CchMetricDev& m, int64_t N, int64_t M, int64_t E) {
+  return E * 4 + M * (8 + 8 + 4 + 4 + 4 + 4) + (N + 1) * 8 + (m.kept_f + m.kept_b) * 16;
+}
+
+void CchGpu::insert_cached(const std::shared_ptr<CchMetricDev>& m) {
+  const int64_t b = metric_device_bytes(*m, T_.N, T_.M, T_.E);
+  metric_bytes_.store(b);
+  std::lock_guard<std::mutex> lk(mu_);
+  if (cache_gb_ > 0.0 && b > 0) capacity_ = (int)std::max<int64_t>(4, (int64_t)(cache_gb_ * 1073741824.0 / (double)b));
+  cache_.push_front(m);
+  while ((int)cache_.size() > capacity_) cache_.pop_back();
+}
+
+void CchGpu::set_cache_gb(double gb) {
+  std::lock_guard<std::mutex> lk(mu_);
+  cache_gb_ = gb > 0.0 ? gb : 0.0;
+  const int64_t b = metric_bytes_.load();
+  if (cache_gb_ > 0.0 && b > 0) capacity_ = (int)std::max<int64_t>(4, (int64_t)(cache_gb_ * 1073741824.0 / (double)b));
+  while ((int)cache_.size() > capacity_) cache_.pop_back();
+}
+
+void CchGpu::request_build(const CchContext& c, bool urgent) {
+  const uint64_t key = c.key();
+  std::shared_ptr<CchMetricDev> m;
+  if (cached_metric(key, m)) {
+    notify_built(key, true);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(bmu_);
+    if (bstop_ || !bpending_.insert(key).second) return;   // stopping, or already queued / building
+    if (urgent) bq_.push_front(c);
+    else bq_.push_back(c);
+    if (!bth_.joinable()) bth_ = std::thread([this] { builder_loop(); });
+  }
+  n_bqueued_.fetch_add(1, std::memory_order_relaxed);
+  bcv_.notify_one();
+}
+
+int CchGpu::add_build_listener(std::function<void(uint64_t, bool)> cb) {
+  std::lock_guard<std::mutex> lk(lmu_);
+  listeners_.emplace_back(next_listener_, std::move(cb));
+  return next_listener_++;
+}
+
+void CchGpu::remove_build_listener(int id) {
+  std::lock_guard<std::mutex> lk(lmu_);
+  for (auto it = listeners_.begin(); it != listeners_.end(); ++it)
+    if (it->first == id) {
+      listeners_.erase(it);
+      break;
+    }
+}
+
+void CchGpu::notify_built(uint64_t key, bool ok) {
+  std::lock_guard<std::mutex> lk(lmu_);
+  for (auto& l : listeners_) l.second(key, ok);
+}
+
+CchGpu::AsyncStats CchGpu::async_stats() {
+  AsyncStats a;
+  a.queued = n_bqueued_.load();
+  a.built = n_bbuilt_.load();
+  a.failed = n_bfailed_.load();
+  std::lock_guard<std::mutex> lk(bmu_);
+  a.pending = (int)bpending_.size();
+  return a;
+}
+
+void CchGpu::builder_loop() {
+  if (hipSetDevice(dev_) != hipSuccess) return;
+  int least = 0, greatest = 0;
+  hipStream_t s = nullptr;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+      hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least) != hipSuccess) {
+    (void)hipGetLastError();
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  }
+  while (true) {
+    CchContext c;
+    {
+      std::unique_lock<std::mutex> lk(bmu_);
+      bcv_.wait(lk, [&] { return bstop_ || !bq_.empty(); });
+      if (bstop_) break;
+      c = bq_.front();
+      bq_.pop_front();
+    }
+    std::shared_ptr<CchMetricDev> m;
+    bool fresh = false;
+    const bool ok = s != nullptr && metric_for(c, s, m, &fresh) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
+    (ok ? n_bbuilt_ : n_bfailed_).fetch_add(1, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> lk(bmu_);
+      bpending_.erase(c.key());
+    }
+    notify_built(c.key(), ok);
+  }
+  if (s) (void)hipStreamDestroy(s);
 }
 
 bool CchGpu::cached_metric(uint64_t key, std::shared_ptr<CchMetricDev>& out) {
@@ -1169,11 +1280,7 @@ hipError_t CchGpu::metric_for(const CchContext& c, hipStream_t s, std::shared_pt
   m->cost_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   e = customize(m->cost, *m, s);
   if (e != hipSuccess) return e;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    cache_.push_front(m);
-    while ((int)cache_.size() > capacity_) cache_.pop_back();
-  }
+  insert_cached(m);
   out = m;
   if (fresh) *fresh = true;
   return hipSuccess;

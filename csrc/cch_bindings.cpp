@@ -89,8 +89,32 @@ class PyCchGpu {
     d["cached_metrics"] = g_->cached();
     d["triangle_table"] = g_->has_triangle_table();
     d["triangles"] = g_->triangles();
+    d["cache_capacity"] = g_->capacity();
+    d["cache_gb"] = g_->cache_gb();
+    d["metric_bytes"] = g_->metric_bytes();
+    const auto a = g_->async_stats();
+    d["async_queued"] = a.queued;
+    d["async_built"] = a.built;
+    d["async_failed"] = a.failed;
+    d["async_pending"] = a.pending;
     return d;
   }
+
+  // queue a context's build on the router's background builder (returns at once)
+  void request_build(int64_t weather, int64_t congestion, int64_t weekhour, double age, bool urgent) {
+    TORCH_CHECK(g_->has_eta(), "CchGpu: set_eta first");
+    rt::CchContext c;
+    c.weather = (int)weather;
+    c.congestion = (int)congestion;
+    c.weekhour = (int)weekhour;
+    c.driver_age = (float)age;
+    g_->request_build(c, urgent);
+  }
+  bool is_cached(int64_t key) {
+    std::shared_ptr<rt::CchMetricDev> m;
+    return g_->cached_metric((uint64_t)key, m);
+  }
+  void set_cache_gb(double gb) { g_->set_cache_gb(gb); }
 
   py::dict info(const rt::CchMetricDev& m, bool fresh) const {
     py::dict d;
@@ -330,6 +354,10 @@ void bind_cch_gpu(py::module& m) {
       .def("legs_from_matrix", &PyCchGpu::legs_from_matrix, py::arg("key"), py::arg("tag"), py::arg("pts"), py::arg("r"),
            py::arg("i"), py::arg("j"), py::arg("max_path") = 4096, py::arg("want_path") = true)
       .def("set_capacity", &PyCchGpu::set_capacity)
+      .def("set_cache_gb", &PyCchGpu::set_cache_gb, py::arg("gb"))
+      .def("request_build", &PyCchGpu::request_build, py::arg("weather"), py::arg("congestion"), py::arg("weekhour"),
+           py::arg("driver_age") = 35.0, py::arg("urgent") = true)
+      .def("is_cached", &PyCchGpu::is_cached, py::arg("key"))
       .def("ptr", &PyCchGpu::ptr)
       .def("topology_arrays", &PyCchGpu::topology_arrays);
 }

@@ -6,9 +6,14 @@
 
 #include <cstdint>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <list>
 #include <memory>
 #include <mutex>
+#include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "common.h"
@@ -106,8 +111,34 @@ class CchGpu {
   hipError_t metric_from_costs(uint64_t key, const float* d_cost, hipStream_t s, std::shared_ptr<CchMetricDev>& out);
   // a cached metric by key (no build); false if absent
   bool cached_metric(uint64_t key, std::shared_ptr<CchMetricDev>& out);
-  void set_capacity(int n) { std::lock_guard<std::mutex> lk(mu_); capacity_ = n < 1 ? 1 : n; }
+  // LRU size: a fixed count (set_capacity), or — the default — as many metrics as fit an HBM budget
+  // (set_cache_gb; ROUTEST_CCH_CACHE_GB, default 48 of the 288 GB), re-derived from each built
+  // metric's device bytes
+  void set_capacity(int n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    capacity_ = n < 1 ? 1 : n;
+    cache_gb_ = 0.0;
+  }
+  void set_cache_gb(double gb);
+  double cache_gb() { std::lock_guard<std::mutex> lk(mu_); return cache_gb_; }
+  int capacity() { std::lock_guard<std::mutex> lk(mu_); return capacity_; }
+  int64_t metric_bytes() const { return metric_bytes_.load(); }
   int cached() { std::lock_guard<std::mutex> lk(mu_); return (int)cache_.size(); }
+
+  // Asynchronous context builds, off every query path: a builder thread customizes queued contexts
+  // on its own lowest-priority stream (query launches on higher-priority streams overtake it) and
+  // tells the listeners (key, ok) when each is cached.  request_build is a no-op for a context
+  // that is queued or building; for one already cached the listeners are told at once (on the
+  // caller's thread: a caller must not hold a lock its listener takes).  urgent: ahead of queued
+  // prefetches (a request waits for it).
+  void request_build(const CchContext& c, bool urgent = true);
+  int add_build_listener(std::function<void(uint64_t, bool)> cb);
+  void remove_build_listener(int id);
+  struct AsyncStats {
+    long long queued = 0, built = 0, failed = 0;
+    int pending = 0;
+  };
+  AsyncStats async_stats();
 
   // point-to-point: node ids on the device
   hipError_t route(const CchMetricDev& m, const int* d_src, const int* d_dst, int Q, const CchRouteOut& o,
@@ -160,7 +191,23 @@ class CchGpu {
   std::mutex mu_;
   std::list<std::shared_ptr<CchMetricDev>> cache_;
   int capacity_ = 32;
+  double cache_gb_ = 48.0;
+  std::atomic<int64_t> metric_bytes_{0};
+  void insert_cached(const std::shared_ptr<CchMetricDev>& m);   // LRU push_front + eviction
   std::atomic<uint64_t> tag_ctr_{0};
+  // asynchronous builds
+  void builder_loop();
+  void notify_built(uint64_t key, bool ok);
+  std::mutex bmu_;
+  std::condition_variable bcv_;
+  std::deque<CchContext> bq_;
+  std::unordered_set<uint64_t> bpending_;          // queued or building
+  std::thread bth_;
+  bool bstop_ = false;
+  std::mutex lmu_;                                 // held while listeners run (removal waits)
+  std::vector<std::pair<int, std::function<void(uint64_t, bool)>>> listeners_;
+  int next_listener_ = 1;
+  std::atomic<long long> n_bqueued_{0}, n_bbuilt_{0}, n_bfailed_{0};
 };
 
 }  // namespace rt

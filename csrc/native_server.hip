@@ -87,7 +87,20 @@ struct SlotHealth {
   std::atomic<long long> failures{0}, rounds{0}, quarantines{0};
   std::atomic<long long> probe_at_ms{0};
   std::atomic<bool> fault{false};
+  std::atomic<bool> hang{false};       // ROUTEST_FAULT=gpu_hang@<slot>: each launch first runs a kernel
+                                       // that waits on a host flag (the watchdog's test)
+  std::atomic<long long> timeouts{0};  // rounds abandoned at the deadline (ROUTEST_GPU_DEADLINE_MS)
 };
+
+// Fault hook of the latency watchdog: one wave that waits until the host releases it (or at most
+// max_ticks of the 100 MHz wall clock), so the launch behind it on the same stream misses its
+// deadline.  Reads only; every wave reaches the exit condition.
+__global__ __launch_bounds__(64) void hang_kernel(const int* release, long long max_ticks) {
+  const long long t0 = wall_clock64();
+  while (__hip_atomic_load(release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
+         wall_clock64() - t0 < max_ticks)
+    __builtin_amdgcn_s_sleep(127);
+}
 
 inline long long mono_ms() {
   struct timespec ts;
@@ -106,6 +119,11 @@ struct Shared {
   std::vector<std::unique_ptr<SlotHealth>> health;
   int quarantine_after = 3;
   long long probe_ms = 30000;
+  double deadline_ms = 500.0;          // ROUTEST_GPU_DEADLINE_MS: a round not done by then is abandoned
+  int* hang_release = nullptr;         // pinned host flag of the gpu_hang fault hook (1 = release)
+  int* hang_release_d = nullptr;
+  // the model each resident scorer was created on: its blob stays allocated while the scorer lives
+  std::vector<std::shared_ptr<const NativeModel>> scorer_models;
   int slots() const { return (int)devices.size(); }
   std::vector<std::shared_ptr<const NativeModel>> snapshot() {
     std::lock_guard<std::mutex> lk(model_mu);
@@ -129,6 +147,16 @@ struct Shared {
       h.quarantines.fetch_add(1);
       h.probe_at_ms.store(mono_ms() + probe_ms);
     }
+  }
+  // a round that missed its deadline: the GPU is quarantined at once (its queue may hold a hung
+  // kernel; rounds fail over to the other GPUs / the CPU), and re-probed after probe_ms
+  void timed_out(int g) {
+    SlotHealth& h = *health[g];
+    h.failures.fetch_add(1);
+    h.timeouts.fetch_add(1);
+    h.consec.fetch_add(1);
+    if (!h.quarantined.exchange(true)) h.quarantines.fetch_add(1);
+    h.probe_at_ms.store(mono_ms() + probe_ms);
   }
   void ok(int g) {
     SlotHealth& h = *health[g];
@@ -209,7 +237,7 @@ struct Pending {
 struct Stats {
   std::atomic<long long> requests{0}, predictions{0}, launches{0}, errors{0}, resident{0}, fallbacks{0},
       wire8{0}, route_requests{0}, route_fallbacks{0}, relayed{0}, failovers{0}, cpu_rounds{0}, history{0},
-      cached{0};
+      cached{0}, timeouts{0};
 };
 
 inline Stamp now_local() {
@@ -326,6 +354,11 @@ class Reactor {
       (void)hipSetDevice(kv.first);
       (void)hipStreamDestroy(kv.second);
     }
+    for (auto& kv : events_) {
+      (void)hipSetDevice(kv.first);
+      (void)hipEventDestroy(kv.second);
+    }
+    reap_retired(true);
     (void)hipSetDevice(cfg_.device);
   }
 
@@ -345,6 +378,17 @@ class Reactor {
   int cap_ = 0;
   size_t nrec_ = 0;
   std::unordered_map<int, hipStream_t> streams_;        // per device (failover launches)
+  std::unordered_map<int, hipEvent_t> events_;          // per device: the round's completion
+  // rounds abandoned at the deadline: their stream, buffers, workspace and model stay allocated
+  // until their kernels drain (checked every round; released at shutdown after the hang flag)
+  struct Retired {
+    int dev;
+    hipEvent_t ev;
+    hipStream_t st;
+    void *rec, *rec8, *out, *ws;
+    std::shared_ptr<const NativeModel> model;
+  };
+  std::vector<Retired> retired_;
   rth::HistoryDb hdb_;                                  // this reactor's connection to the store
   bool hdb_tried_ = false;
   std::unordered_map<int, ModelWs> ws_;                 // per device model workspace
@@ -977,11 +1021,92 @@ class Reactor {
 
   // One round on GPU slot g's device with that slot's model (zero-copy: records and minutes stay
   // in this reactor's portable pinned buffers).
-  hipError_t launch_on(int g, const NativeModel& m) {
+  // Latency watchdog (SURVEY §5.3 "a watchdog on batch latency"): the round's completion event is
+  // polled against the deadline instead of an unbounded stream synchronize.
+  hipError_t wait_deadline(hipStream_t st, hipEvent_t ev, double deadline_ms) {
+    hipError_t e = hipEventRecord(ev, st);
+    if (e != hipSuccess) return e;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0;; ++i) {
+      e = hipEventQuery(ev);
+      if (e != hipErrorNotReady) return e;
+      if (deadline_ms > 0 && (i & 15) == 15 &&
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > deadline_ms)
+        return hipErrorLaunchTimeOut;
+      if (i > 4096) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+
+  // free the buffers of abandoned rounds whose kernels have drained (all: wait for them, bounded)
+  void reap_retired(bool all) {
+    for (size_t i = 0; i < retired_.size();) {
+      Retired& r = retired_[i];
+      (void)hipSetDevice(r.dev);
+      hipError_t q = hipEventQuery(r.ev);
+      if (all && q == hipErrorNotReady) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while ((q = hipEventQuery(r.ev)) == hipErrorNotReady &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+      if (q == hipErrorNotReady) { ++i; continue; }
+      (void)hipEventDestroy(r.ev);
+      (void)hipStreamDestroy(r.st);
+      (void)hipHostFree(r.rec);
+      (void)hipHostFree(r.rec8);
+      (void)hipHostFree(r.out);
+      if (r.ws) (void)hipFree(r.ws);
+      retired_[i] = std::move(retired_.back());
+      retired_.pop_back();
+    }
+    (void)hipSetDevice(cfg_.device);
+  }
+
+  // a round on `dev` missed its deadline: its kernel may still run and write this reactor's
+  // buffers, so they, the stream and the workspace are retired and the round continues on fresh
+  // ones (records copied over)
+  bool retire_round(int dev, hipStream_t st, hipEvent_t ev, std::shared_ptr<const NativeModel> m) {
+    const unsigned fl = hipHostMallocMapped | hipHostMallocPortable;
+    EtaRecord* nr = nullptr;
+    rtc::Wire8* n8 = nullptr;
+    float* no = nullptr;
+    void *dr = nullptr, *d8 = nullptr;
+    float* dout = nullptr;
+    if (hipHostMalloc((void**)&nr, (size_t)cap_ * 16, fl) != hipSuccess ||
+        hipHostMalloc((void**)&n8, (size_t)cap_ * 8, fl) != hipSuccess ||
+        hipHostMalloc((void**)&no, (size_t)cap_ * 4, fl) != hipSuccess || hipHostGetDevicePointer(&dr, nr, 0) != hipSuccess ||
+        hipHostGetDevicePointer(&d8, n8, 0) != hipSuccess || hipHostGetDevicePointer((void**)&dout, no, 0) != hipSuccess) {
+      for (void* p : {(void*)nr, (void*)n8, (void*)no})
+        if (p) (void)hipHostFree(p);
+      return false;                    // keep the old buffers (the slot is quarantined anyway)
+    }
+    std::memcpy(nr, h_rec_, nrec_ * sizeof(EtaRecord));
+    Retired r{dev, ev, st, h_rec_, h_rec8_, h_out_, nullptr, std::move(m)};
+    ModelWs& w = ws_[dev];
+    r.ws = w.p;
+    w.p = nullptr;
+    w.bytes = 0;
+    retired_.push_back(std::move(r));
+    streams_.erase(dev);
+    events_.erase(dev);
+    h_rec_ = nr;
+    h_rec8_ = n8;
+    h_out_ = no;
+    d_rec_ = dr;
+    d_rec8_ = d8;
+    d_out_ = dout;
+    if (dev == cfg_.device) stream_ = nullptr;
+    return true;
+  }
+
+  hipError_t launch_on(int g, const std::shared_ptr<const NativeModel>& mp) {
+    const NativeModel& m = *mp;
     Shared& sh = *cfg_.sh;
     if (sh.health[g]->fault.load(std::memory_order_relaxed)) return hipErrorLaunchFailure;   // injected
     const int dev = sh.devices[g];
     if (hipSetDevice(dev) != hipSuccess) return hipErrorInvalidDevice;
+    if (!retired_.empty()) reap_retired(false);
+    (void)hipSetDevice(dev);
     hipStream_t st;
     auto it = streams_.find(dev);
     if (it == streams_.end()) {
@@ -993,13 +1118,31 @@ class Reactor {
     } else {
       st = it->second;
     }
+    hipEvent_t ev;
+    auto ei = events_.find(dev);
+    if (ei == events_.end()) {
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipSetDevice(cfg_.device);
+        return hipErrorOutOfMemory;
+      }
+      events_[dev] = ev;
+    } else {
+      ev = ei->second;
+    }
     sh.park(g);                        // keep a hardware queue the resident scorer may share free
+    if (sh.health[g]->hang.load(std::memory_order_relaxed) && sh.hang_release_d != nullptr)
+      hipLaunchKernelGGL(hang_kernel, dim3(1), dim3(64), 0, st, sh.hang_release_d, 500000000ll);   // <= 5 s
     // 8-byte wire records whenever the round is exactly representable and the model reads them
     // (csrc/runtime/rt_core.h pack_wire8), else 16-byte
     const bool w8 = m.takes_wire8() && rtc::pack_wire8(h_rec_, nrec_, h_rec8_);
     if (w8) st_.wire8.fetch_add(1, std::memory_order_relaxed);
     hipError_t e = m.predict(w8 ? d_rec8_ : d_rec_, w8 ? 8 : 16, d_out_, (int)nrec_, st, ws_[dev]);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = wait_deadline(st, ev, sh.deadline_ms);
+    if (e == hipErrorLaunchTimeOut) {
+      sh.timed_out(g);
+      st_.timeouts.fetch_add(1, std::memory_order_relaxed);
+      if (!retire_round(dev, st, ev, mp)) e = hipErrorOutOfMemory;
+    }
     (void)hipSetDevice(cfg_.device);
     return e;
   }
@@ -1032,12 +1175,13 @@ class Reactor {
       const int g = (own + k) % S;
       if (models[g] == nullptr || !sh.usable(g)) continue;
       st_.launches.fetch_add(1, std::memory_order_relaxed);
-      if (launch_on(g, *models[g]) == hipSuccess) {
+      const hipError_t e = launch_on(g, models[g]);
+      if (e == hipSuccess) {
         sh.ok(g);
         if (g != own) st_.failovers.fetch_add(1, std::memory_order_relaxed);
         return true;
       }
-      sh.fail(g);
+      if (e != hipErrorLaunchTimeOut) sh.fail(g);    // (a timeout quarantined the slot already)
     }
     if (m0 != nullptr && m0->cpu_predict(h_rec_, h_out_, (int)nrec_)) {
       st_.cpu_rounds.fetch_add(1, std::memory_order_relaxed);
@@ -1121,23 +1265,32 @@ struct Server {
   std::vector<std::unique_ptr<RouteService>> routes;      // one per GPU
   std::shared_ptr<AltScorerState> alt = std::make_shared<AltScorerState>();   // "alternatives" scorer
   ~Server() {
+    if (sh.hang_release) *(volatile int*)sh.hang_release = 1;   // release any gpu_hang kernel
     routes.clear();                                          // joins the route workers
     for (PersistentScorer* p : sh.scorers)                   // stop + wait for the resident kernels
       if (p) pscore_destroy(p);
+    if (sh.hang_release) (void)hipHostFree(sh.hang_release);
   }
 };
 
 // (re)create slot g's resident scorer for its current model (mlp3 only); caller holds its mutex
+void stop_scorer(Server* s, int g) {
+  Shared& sh = s->sh;
+  if (sh.scorers[g] != nullptr) pscore_destroy(sh.scorers[g]);   // waits for the resident kernel
+  sh.scorers[g] = nullptr;
+  sh.scorer_models[g] = nullptr;     // the blob it staged from may go now
+}
+
 void restart_scorer(Server* s, int g) {
   Shared& sh = s->sh;
-  if (sh.scorers[g] != nullptr) pscore_destroy(sh.scorers[g]);
-  sh.scorers[g] = nullptr;
+  stop_scorer(s, g);
   if (!(s->cfg.persist_idle_ms > 0 && s->cfg.persist_cap > 0)) return;
   auto m = sh.model(g);
   if (m == nullptr || m->mlp3_blob() == nullptr) return;
   hipError_t e = hipSuccess;
   sh.scorers[g] = pscore_create(sh.devices[g], m->mlp3_blob(), m->H, *m->mlp3_norm(), s->cfg.persist_cap,
                                 s->cfg.persist_idle_ms, s->cfg.persist_life_ms, &e);   // nullptr: normal launches
+  if (sh.scorers[g] != nullptr) sh.scorer_models[g] = m;   // keeps the blob alive as long as the scorer
 }
 
 std::mutex g_srv_mu;
@@ -1176,7 +1329,15 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
   for (size_t g = 0; g < devices.size(); ++g) {
     sh.health.push_back(std::make_unique<SlotHealth>());
     sh.scorers.push_back(nullptr);
+    sh.scorer_models.push_back(nullptr);
     sh.scorer_mus.push_back(std::make_unique<std::mutex>());
+  }
+  if (const char* v = std::getenv("ROUTEST_GPU_DEADLINE_MS")) sh.deadline_ms = std::atof(v);
+  if (hipHostMalloc((void**)&sh.hang_release, sizeof(int), hipHostMallocMapped | hipHostMallocPortable) == hipSuccess) {
+    *(volatile int*)sh.hang_release = 1;
+    if (hipHostGetDevicePointer((void**)&sh.hang_release_d, sh.hang_release, 0) != hipSuccess) sh.hang_release_d = nullptr;
+  } else {
+    sh.hang_release = nullptr;
   }
   // ROUTEST_FAULT=gpu_fail (every slot) | gpu_fail@<slot>: launches on the slot fail (fault injection)
   if (const char* v = std::getenv("ROUTEST_FAULT")) {
@@ -1193,6 +1354,12 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
       } else if (t.rfind("gpu_fail@", 0) == 0) {
         const int g = std::atoi(t.c_str() + 9);
         if (g >= 0 && g < (int)sh.health.size()) sh.health[g]->fault = true;
+      } else if (t.rfind("gpu_hang@", 0) == 0 && sh.hang_release_d) {   // the watchdog's test hook
+        const int g = std::atoi(t.c_str() + 9);
+        if (g >= 0 && g < (int)sh.health.size()) {
+          sh.health[g]->hang = true;
+          *(volatile int*)sh.hang_release = 0;
+        }
       }
       b = e + 1;
     }
@@ -1215,6 +1382,7 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
     s->reactors.push_back(std::move(r));
   }
   // one route service per GPU; a finished job goes back to the reactor that parsed it
+  s->routes.reserve(routes.size());
   for (size_t g = 0; g < routes.size(); ++g) {
     RouteServiceCfg rc = routes[g];
     Shared* shp = &s->sh;
@@ -1222,6 +1390,22 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
     rc.eta_model = [shp, slot]() { return shp->model(slot); };
     rc.park_scorer = [shp, slot]() { shp->park(slot); };
     rc.alt = s->alt;
+    // watchdog: a flush past the deadline quarantines this GPU and its jobs go to the next GPU's
+    // route service that is not itself broken
+    rc.on_timeout = [shp, slot]() { shp->timed_out(slot); };
+    rc.failover = [s, slot](RouteJob* j) {
+      const int n = (int)s->routes.size();
+      for (int k = 1; k < n; ++k) {
+        RouteService* r = s->routes[(size_t)((slot + k) % n)].get();
+        if (r != nullptr && !r->broken()) {
+          r->submit(j);
+          return true;
+        }
+      }
+      return false;
+    };
+    rc.hang_fault = [shp, slot]() { return shp->health[slot]->hang.load(std::memory_order_relaxed); };
+    rc.hang_release_d = shp->hang_release_d;
     s->routes.push_back(std::make_unique<RouteService>(rc, [](RouteJob* j) {
       static_cast<JobTag*>(j->tag)->reactor->job_done(j);
     }));
@@ -1249,6 +1433,12 @@ int64_t native_server_set_models(int64_t h, const std::vector<std::shared_ptr<co
     err = "one model per GPU slot";
     return -1;
   }
+  // the resident scorers stage weights from their model's blob: stop them first (each also holds
+  // its model, so a scorer can never outlive the blob), then swap, then start them on the new ones
+  for (size_t g = 0; g < models.size(); ++g) {
+    std::lock_guard<std::mutex> sl(*s->sh.scorer_mus[g]);
+    stop_scorer(s, (int)g);
+  }
   uint64_t ep;
   {
     std::lock_guard<std::mutex> ml(s->sh.model_mu);
@@ -1269,6 +1459,20 @@ bool native_server_set_fault(int64_t h, int slot, bool on) {
   Server* s = g_servers[h];
   if (slot < 0 || slot >= (int)s->sh.health.size()) return false;
   s->sh.health[slot]->fault = on;
+  return true;
+}
+
+// the latency watchdog's fault hook per slot: launches on it first run a kernel that waits on a
+// host flag (released when no slot hangs any more, and at shutdown)
+bool native_server_set_hang(int64_t h, int slot, bool on) {
+  std::lock_guard<std::mutex> lk(g_srv_mu);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return false;
+  Server* s = g_servers[h];
+  if (slot < 0 || slot >= (int)s->sh.health.size() || !s->sh.hang_release) return false;
+  s->sh.health[slot]->hang = on;
+  bool any = false;
+  for (auto& x : s->sh.health) any |= x->hang.load();
+  *(volatile int*)s->sh.hang_release = any ? 0 : 1;
   return true;
 }
 
@@ -1297,7 +1501,8 @@ std::vector<std::vector<std::string>> native_server_health(int64_t h, uint64_t& 
     out.push_back({std::to_string(s->sh.devices[g]), x.quarantined.load() ? "1" : "0", std::to_string(x.consec.load()),
                    std::to_string(x.failures.load()), std::to_string(x.rounds.load()),
                    std::to_string(x.quarantines.load()), x.fault.load() ? "1" : "0",
-                   models[g] ? models[g]->describe() : std::string("none")});
+                   models[g] ? models[g]->describe() : std::string("none"), std::to_string(x.timeouts.load()),
+                   x.hang.load() ? "1" : "0"});
   }
   return out;
 }
@@ -1311,6 +1516,7 @@ void native_server_stop(int64_t h) {
     g_servers[h] = nullptr;
   }
   if (!s) return;
+  if (s->sh.hang_release) *(volatile int*)s->sh.hang_release = 1;   // release any gpu_hang kernel first
   s->stop.store(true);
   for (auto& r : s->reactors) {
     uint64_t one = 1;
@@ -1322,7 +1528,7 @@ void native_server_stop(int64_t h) {
 
 std::vector<long long> native_server_stats(int64_t h) {
   std::lock_guard<std::mutex> lk(g_srv_mu);
-  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(32, 0);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(37, 0);
   Server* s = g_servers[h];
   std::vector<long long> v = {s->stats.requests.load(), s->stats.predictions.load(), s->stats.launches.load(),
                               s->stats.errors.load(), s->stats.resident.load(), s->stats.fallbacks.load(),
@@ -1338,6 +1544,13 @@ std::vector<long long> native_server_stats(int64_t h) {
   v.push_back(s->stats.cpu_rounds.load());
   v.push_back(s->stats.history.load());
   v.push_back(s->stats.cached.load());
+  std::vector<long long> rx(4, 0);        // route service stats past the first 18
+  for (auto& r : s->routes) {
+    const auto x = r->stats();
+    for (size_t i = 0; i < rx.size() && 18 + i < x.size(); ++i) rx[i] += x[18 + i];
+  }
+  v.insert(v.end(), rx.begin(), rx.end());
+  v.push_back(s->stats.timeouts.load());
   return v;
 }
 

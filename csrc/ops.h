@@ -225,6 +225,7 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
 int64_t native_server_set_models(int64_t h, const std::vector<std::shared_ptr<const NativeModel>>& models,
                                  std::string& err);
 bool native_server_set_fault(int64_t h, int slot, bool on);
+bool native_server_set_hang(int64_t h, int slot, bool on);
 bool native_server_set_scorer(int64_t h, std::vector<double> delay, int kind, const std::string& engine);
 std::vector<std::vector<std::string>> native_server_health(int64_t h, uint64_t& epoch);
 void native_server_stop(int64_t h);

@@ -17,6 +17,7 @@
 namespace rt {
 
 struct PersistentScorer;
+struct RouteJob;
 
 // The GCN candidate-route scorer's node delay factors for "alternatives" requests
 // (routing/alternatives.py; csrc/runtime/alternatives.h), published by the Python side once the
@@ -81,6 +82,13 @@ struct RouteServiceCfg {
   std::function<void()> park_scorer;
   // GCN scorer for "alternatives" requests (road graph + CCH only)
   std::shared_ptr<AltScorerState> alt;
+  // latency watchdog (ROUTEST_ROUTE_DEADLINE_MS): a flush whose GPU work misses the deadline marks
+  // the service broken until that work drains; its jobs — and every flush meanwhile — are handed
+  // to `failover` (another GPU's route service; false: none left -> relayed to the app)
+  std::function<bool(RouteJob*)> failover;
+  std::function<void()> on_timeout;       // the slot's GPU is quarantined for predictions too
+  std::function<bool()> hang_fault;       // ROUTEST_FAULT=gpu_hang@<slot> (the watchdog's test hook)
+  const int* hang_release_d = nullptr;    // its device-visible release flag
 };
 
 // One request handed from a reactor to the service and back.
@@ -100,6 +108,9 @@ struct RouteJob {
   std::vector<std::vector<std::pair<double, double>>> calls;
   std::vector<int32_t> nodes;
   int group = 0;                    // routing-context group of its flush (CCH)
+  bool parsed = false;              // request parsed (a job deferred for its context keeps it)
+  double defer_t0 = 0.0;            // when it was first deferred for its context's build (us)
+  bool sync_ctx = false;            // its context's background build failed: build it in the flush
   // "alternatives": unique leg pairs in order, their via nodes, the chosen candidates (legs owned
   // here) and the response block
   std::vector<std::pair<int, int>> alt_pairs;
@@ -120,6 +131,7 @@ class RouteService {
   void submit(RouteJob* j);
   // jobs, flushes, fallbacks, legs searched, legs finished on the host, rows persisted
   std::vector<long long> stats() const;
+  bool broken() const;                    // a flush missed the deadline and its GPU work has not drained
 
  private:
   struct Impl;

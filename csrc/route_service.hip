@@ -26,14 +26,17 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <deque>
 #include <functional>
+#include <list>
 #include <mutex>
 #include <queue>
 #include <random>
 #include <memory>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "common.h"
 #include "ops.h"
@@ -54,6 +57,15 @@ __global__ void compact_paths_kernel(const int* __restrict__ rows, int max_path,
   const int n = min(len[q], max_path);
   const long long o = off[q];
   for (int i = threadIdx.x; i < n; i += blockDim.x) flat[o + i] = rows[(size_t)q * max_path + i];
+}
+
+// the watchdog's fault hook (ROUTEST_FAULT=gpu_hang@<slot>): one wave waiting on a host flag, at
+// most max_ticks of the 100 MHz wall clock; reads only, every wave reaches the exit condition
+__global__ __launch_bounds__(64) void route_hang_kernel(const int* release, long long max_ticks) {
+  const long long t0 = wall_clock64();
+  while (__hip_atomic_load(release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
+         wall_clock64() - t0 < max_ticks)
+    __builtin_amdgcn_s_sleep(127);
 }
 
 template <class T>
@@ -233,10 +245,77 @@ struct RouteService::Impl {
   HostBuf<float> h_met;
   DevBuf<int> d_pts, d_npts2;
   DevBuf<float> d_msec, d_mmet, d_met;
+  // host copies of metrics' edge costs (maneuver durations, exact host fallback): LRU by key
   std::mutex hc_mu;
-  std::unordered_map<uint64_t, std::shared_ptr<const std::vector<float>>> hc_cache;
+  std::list<std::pair<uint64_t, std::shared_ptr<const std::vector<float>>>> hc_lru;
+  std::unordered_map<uint64_t, decltype(hc_lru)::iterator> hc_index;
+  static constexpr size_t HC_MAX = 64;
   std::atomic<long long> n_ctx_built{0};
   std::atomic<long long> t_ctx_us{0};
+  // Routing contexts off the flush's critical path (CCH): a job whose context is not customized
+  // yet waits here while the router's background builder customizes it; the rest of its flush
+  // proceeds.  The build's listener puts the jobs back at the head of the queue.
+  bool async_ctx = true;
+  int listener = 0;
+  std::mutex wmu;
+  std::unordered_map<uint64_t, std::vector<RouteJob*>> waiting;
+  std::atomic<long long> n_deferred{0}, t_wait_us{0}, n_prefetch{0};
+  // latency watchdog: every wait on the flush's GPU work is bounded (ROUTEST_ROUTE_DEADLINE_MS)
+  double deadline_ms = 2000.0;
+  std::atomic<bool> broken{false};
+  hipEvent_t ev_gpu{}, ev_asm{};
+  std::atomic<long long> n_failed_over{0};
+
+  hipError_t sync(hipStream_t s, hipEvent_t ev) {
+    hipError_t e = hipEventRecord(ev, s);
+    if (e != hipSuccess) return e;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0;; ++i) {
+      e = hipEventQuery(ev);
+      if (e != hipErrorNotReady) return e;
+      if (deadline_ms > 0 && (i & 15) == 15 &&
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > deadline_ms) {
+        if (!broken.exchange(true) && cfg.on_timeout) cfg.on_timeout();
+        return hipErrorLaunchTimeOut;
+      }
+      if (i > 4096) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+  // the work that missed the deadline has drained: the service's buffers are its own again
+  bool drained() {
+    return (!ev_gpu || hipEventQuery(ev_gpu) != hipErrorNotReady) && (!ev_asm || hipEventQuery(ev_asm) != hipErrorNotReady);
+  }
+  // jobs of a failed / abandoned flush: to another GPU's route service, else relayed to the app
+  void hand_off(std::vector<RouteJob*>& jobs) {
+    for (RouteJob* j : jobs) {
+      if (!j->fallback && !j->status && cfg.failover) {
+        j->plan = rtr::Plan();
+        j->calls.clear();
+        j->nodes.clear();
+        j->group = 0;
+        j->alt_pairs.clear();
+        j->alt_vias.clear();
+        j->alt_legs.clear();
+        j->alt_paths.clear();
+        j->alt_edges.clear();
+        j->alt_json.clear();
+        j->asmb = rtr::Assembled();
+        if (cfg.failover(j)) {
+          n_failed_over.fetch_add(1, std::memory_order_relaxed);
+          continue;
+        }
+      }
+      if (!j->status) j->fallback = true;
+      finish(j);
+      done(j);
+    }
+    jobs.clear();
+  }
+  // prefetch of the next week-hour: (weather, congestion) of requests routed at "now" -> last seen
+  std::unordered_map<int, double> seen_now;
+  int prefetched_wh = -1;
+  std::unordered_set<int> prefetched;      // pairs already queued for prefetched_wh
+  int prefetch_min = 10;
   // ETA
   HostBuf<rtc::EtaRecord> h_rec;
   HostBuf<float> h_eta;
@@ -369,7 +448,20 @@ struct RouteService::Impl {
 
   void run() {
     if (hipSetDevice(cfg.device) != hipSuccess) return;
-    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return;
+    // the query stream at the highest priority: the router's background context builds (lowest
+    // priority, csrc/cch.hip builder_loop) never delay a flush's launches
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, greatest) != hipSuccess) {
+      (void)hipGetLastError();
+      if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return;
+    }
+    if (const char* v = std::getenv("ROUTEST_CCH_ASYNC")) async_ctx = std::string(v) != "0";
+    if (const char* v = std::getenv("ROUTEST_ROUTE_DEADLINE_MS")) deadline_ms = std::atof(v);
+    if (hipEventCreateWithFlags(&ev_gpu, hipEventDisableTiming) != hipSuccess) ev_gpu = nullptr;
+    if (const char* v = std::getenv("ROUTEST_CCH_PREFETCH_MIN")) prefetch_min = std::atoi(v);
+    if (cfg.cch != nullptr && cfg.cch_contexts && async_ctx)
+      listener = cfg.cch->add_build_listener([this](uint64_t key, bool ok) { on_built(key, ok); });
     th_asm = std::thread([this] { asm_loop(); });
     while (true) {
       auto* b = new Batch();
@@ -386,11 +478,49 @@ struct RouteService::Impl {
         b->jobs.assign(q.begin(), q.begin() + take);
         q.erase(q.begin(), q.begin() + take);
       }
+      if (broken.load()) {
+        if (drained()) {
+          broken.store(false);      // the late work finished: buffers and streams usable again
+        } else {
+          hand_off(b->jobs);
+          delete b;
+          continue;
+        }
+      }
+      if (cfg.hang_fault && cfg.hang_release_d && cfg.hang_fault())
+        hipLaunchKernelGGL(route_hang_kernel, dim3(1), dim3(64), 0, stream, cfg.hang_release_d, 500000000ll);
       gpu_stage(*b);
+      if (b->failed) {              // a GPU error or the deadline: another GPU's service answers
+        hand_off(b->jobs);
+        delete b;
+        continue;
+      }
+      if (b->jobs.empty()) {        // every job of the flush is waiting for its routing context
+        delete b;
+        continue;
+      }
       std::unique_lock<std::mutex> lk(amu);
       acv.wait(lk, [&] { return aq.size() < 2; });
       aq.push_back(b);
       acv.notify_all();
+    }
+    // stopping: no more requeues; jobs still waiting for a context go to the app
+    if (listener) cfg.cch->remove_build_listener(listener);
+    std::vector<RouteJob*> left;
+    {
+      std::lock_guard<std::mutex> lk(wmu);
+      for (auto& kv : waiting) left.insert(left.end(), kv.second.begin(), kv.second.end());
+      waiting.clear();
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      left.insert(left.end(), q.begin(), q.end());
+      q.clear();
+    }
+    for (RouteJob* j : left) {
+      j->fallback = true;
+      finish(j);
+      done(j);
     }
     {
       std::lock_guard<std::mutex> lk(amu);
@@ -399,11 +529,13 @@ struct RouteService::Impl {
     acv.notify_all();
     th_asm.join();
     (void)hipStreamDestroy(stream);
+    if (ev_gpu) (void)hipEventDestroy(ev_gpu);
   }
 
   void asm_loop() {
     if (hipSetDevice(cfg.device) != hipSuccess) return;
     if (hipStreamCreateWithFlags(&stream_asm, hipStreamNonBlocking) != hipSuccess) return;
+    if (hipEventCreateWithFlags(&ev_asm, hipEventDisableTiming) != hipSuccess) ev_asm = nullptr;
     open_store();
     th_persist = std::thread([this] { persist_loop(); });
     while (true) {
@@ -443,6 +575,7 @@ struct RouteService::Impl {
       if (st) sql.finalize(st);
     if (db) sql.close(db);
     (void)hipStreamDestroy(stream_asm);
+    if (ev_asm) (void)hipEventDestroy(ev_asm);
   }
 
   void fail_all(std::vector<RouteJob*>& jobs, const char* msg) {
@@ -516,7 +649,7 @@ struct RouteService::Impl {
     if (e == hipSuccess)
       e = hipMemcpy2DAsync(h_row0.h, (size_t)NM * 8, d_D.d, (size_t)NM * NM * 8, (size_t)NM * 8, (size_t)R,
                            hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = sync(stream, ev_gpu);
     if (e != hipSuccess) return false;
     for (int k = 0; k < R; ++k) {
       rtr::Plan& p = m[k]->plan;
@@ -550,26 +683,60 @@ struct RouteService::Impl {
   std::shared_ptr<const std::vector<float>> host_costs(const std::shared_ptr<CchMetricDev>& m) {
     {
       std::lock_guard<std::mutex> lk(hc_mu);
-      auto it = hc_cache.find(m->key);
-      if (it != hc_cache.end()) return it->second;
+      auto it = hc_index.find(m->key);
+      if (it != hc_index.end()) {
+        hc_lru.splice(hc_lru.begin(), hc_lru, it->second);     // most recently used
+        return it->second->second;
+      }
     }
     auto v = std::make_shared<std::vector<float>>((size_t)cfg.cch->topo().E);
     if (hipMemcpyAsync(v->data(), m->cost, v->size() * 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-        hipStreamSynchronize(stream) != hipSuccess)
+        sync(stream, ev_gpu) != hipSuccess)
       return nullptr;
     std::lock_guard<std::mutex> lk(hc_mu);
-    if (hc_cache.size() > 64) hc_cache.clear();
-    hc_cache[m->key] = v;
+    if (hc_index.count(m->key)) return v;
+    hc_lru.emplace_front(m->key, v);
+    hc_index[m->key] = hc_lru.begin();
+    while (hc_lru.size() > HC_MAX) {                            // evict the least recently used
+      hc_index.erase(hc_lru.back().first);
+      hc_lru.pop_back();
+    }
     return v;
   }
 
-  // CCH: group the flush's jobs by routing context and get (build on first use) each metric
+  // a context's background build finished: its waiting jobs go back to the head of the queue
+  // (a failed build: they build it synchronously in their next flush, which reports the error)
+  void on_built(uint64_t key, bool ok) {
+    std::vector<RouteJob*> js;
+    {
+      std::lock_guard<std::mutex> lk(wmu);
+      auto it = waiting.find(key);
+      if (it == waiting.end()) return;
+      js.swap(it->second);
+      waiting.erase(it);
+    }
+    if (!ok)
+      for (RouteJob* j : js) j->sync_ctx = true;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (auto it = js.rbegin(); it != js.rend(); ++it) q.push_front(*it);
+    }
+    cv.notify_one();
+  }
+
+  // CCH: group the flush's jobs by routing context and get each metric.  A context that is not
+  // customized yet does not stall the flush: its jobs leave the batch and wait for the router's
+  // background build (on_built requeues them), the other groups proceed now.  Contexts of requests
+  // routed at "now" are prefetched for the next week-hour shortly before the hour turns.
   bool cch_groups(Batch& b) {
     const rtc::Stamp now = local_now();
     const int64_t days = (int64_t)std::floor((double)now.secs / 86400.0);
-    const int now_wh = (int)(((days + 3) % 7 + 7) % 7) * 24 + (int)((now.secs - days * 86400) / 3600);
+    const int64_t sec_of_day = now.secs - days * 86400;
+    const int now_wh = (int)(((days + 3) % 7 + 7) % 7) * 24 + (int)(sec_of_day / 3600);
+    const double t_now = now_us();
     std::unordered_map<uint64_t, int> gidx;
     std::vector<CchContext> ctxs;
+    std::vector<char> sync;
     for (RouteJob* j : b.jobs) {
       if (j->fallback || !j->req.error.empty()) continue;
       CchContext c;
@@ -579,28 +746,96 @@ struct RouteService::Impl {
         c.congestion = j->req.route_congestion;
         c.weekhour = j->req.route_weekhour >= 0 ? j->req.route_weekhour : now_wh;
         key = c.key();
+        if (j->req.route_weekhour < 0) seen_now[(c.weather & 0xFF) | (c.congestion << 8)] = t_now;
       }
       auto it = gidx.find(key);
       if (it == gidx.end()) {
         it = gidx.emplace(key, (int)ctxs.size()).first;
         ctxs.push_back(c);
+        sync.push_back(0);
       }
       j->group = it->second;
+      if (j->sync_ctx) sync[j->group] = 1;
     }
-    b.metrics.assign(ctxs.size(), nullptr);
-    b.host_cost.assign(ctxs.size(), nullptr);
+    // which groups are ready now
+    std::vector<std::shared_ptr<CchMetricDev>> met(ctxs.size());
+    std::vector<char> ready(ctxs.size(), 1);
     for (size_t g = 0; g < ctxs.size(); ++g) {
-      const double t0 = now_us();
-      if (cfg.cch_contexts) {
+      if (!cfg.cch_contexts) {
+        if (!cfg.cch->cached_metric(cfg.cch_fixed_key, met[g])) return false;
+      } else if (async_ctx && !sync[g]) {
+        ready[g] = cfg.cch->cached_metric(ctxs[g].key(), met[g]) ? 1 : 0;
+      } else {
+        const double t0 = now_us();
         bool fresh = false;
-        if (cfg.cch->metric_for(ctxs[g], stream, b.metrics[g], &fresh) != hipSuccess) return false;
+        if (cfg.cch->metric_for(ctxs[g], stream, met[g], &fresh) != hipSuccess) return false;
         if (fresh) {
           n_ctx_built.fetch_add(1, std::memory_order_relaxed);
           t_ctx_us.fetch_add((long long)(now_us() - t0), std::memory_order_relaxed);
         }
-      } else if (!cfg.cch->cached_metric(cfg.cch_fixed_key, b.metrics[g])) {
-        return false;
       }
+    }
+    // defer the jobs of groups still building; compact the ready groups
+    std::vector<int> remap(ctxs.size(), -1);
+    for (size_t g = 0; g < ctxs.size(); ++g)
+      if (ready[g]) {
+        remap[g] = (int)b.metrics.size();
+        b.metrics.push_back(met[g]);
+      }
+    std::vector<CchContext> to_build;
+    if (b.metrics.size() < ctxs.size()) {
+      std::vector<RouteJob*> keep;
+      keep.reserve(b.jobs.size());
+      {
+        std::lock_guard<std::mutex> lk(wmu);
+        for (RouteJob* j : b.jobs) {
+          if (j->fallback || !j->req.error.empty() || ready[j->group]) {
+            keep.push_back(j);
+            continue;
+          }
+          if (j->defer_t0 == 0.0) {
+            j->defer_t0 = t_now;
+            n_deferred.fetch_add(1, std::memory_order_relaxed);
+          }
+          waiting[ctxs[j->group].key()].push_back(j);
+        }
+      }
+      b.jobs.swap(keep);
+      for (size_t g = 0; g < ctxs.size(); ++g)
+        if (!ready[g]) to_build.push_back(ctxs[g]);
+    }
+    for (RouteJob* j : b.jobs) {
+      if (j->fallback || !j->req.error.empty()) continue;
+      j->group = remap[j->group];
+      if (j->defer_t0 > 0.0) {
+        t_wait_us.fetch_add((long long)(t_now - j->defer_t0), std::memory_order_relaxed);
+        j->defer_t0 = -1.0;                      // counted once
+      }
+    }
+    // (no lock held: a context finished meanwhile notifies on this thread)
+    for (const CchContext& c : to_build) cfg.cch->request_build(c, true);
+    // the next week-hour of the contexts seen at "now" during the last hour, before it begins
+    const int min_in_hour = (int)((sec_of_day % 3600) / 60);
+    const int next_wh = (now_wh + 1) % 168;
+    if (cfg.cch_contexts && async_ctx && prefetch_min > 0 && min_in_hour >= 60 - prefetch_min) {
+      if (prefetched_wh != next_wh) {
+        prefetched_wh = next_wh;
+        prefetched.clear();
+      }
+      for (auto it = seen_now.begin(); it != seen_now.end();) {
+        if (t_now - it->second > 3600e6) { it = seen_now.erase(it); continue; }
+        if (!prefetched.insert(it->first).second) { ++it; continue; }     // queued for next_wh already
+        CchContext c;
+        c.weather = it->first & 0xFF;
+        c.congestion = it->first >> 8;
+        c.weekhour = next_wh;
+        cfg.cch->request_build(c, false);
+        n_prefetch.fetch_add(1, std::memory_order_relaxed);
+        ++it;
+      }
+    }
+    b.host_cost.assign(b.metrics.size(), nullptr);
+    for (size_t g = 0; g < b.metrics.size(); ++g) {
       b.host_cost[g] = host_costs(b.metrics[g]);
       if (!b.host_cost[g]) return false;
     }
@@ -680,7 +915,7 @@ struct RouteService::Impl {
       if (e == hipSuccess)
         e = hipMemcpy2DAsync(h_row0.h, (size_t)NM * 8, d_D.d, (size_t)NM * NM * 8, (size_t)NM * 8, (size_t)R,
                              hipMemcpyDeviceToHost, stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e == hipSuccess) e = sync(stream, ev_gpu);
       if (e != hipSuccess) return false;
       for (int k = 0; k < R; ++k) unpack_plan(m[k], h_npts2.h[k], NM, k);
     }
@@ -858,7 +1093,7 @@ struct RouteService::Impl {
     if (e == hipSuccess) e = hipMemcpyAsync(h_len.h, d_len.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h_cost.h, d_cost.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h_met.h, d_met.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = sync(stream, ev_gpu);
     add_t(3, t0);
     t0 = now_us();
     if (e != hipSuccess) return false;
@@ -884,7 +1119,7 @@ struct RouteService::Impl {
       }
       if (e == hipSuccess) e = hipMemcpyAsync(h_flat.h, d_flat.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
       if (e == hipSuccess) e = hipMemcpyAsync(h_flat_e.h, d_flat_e.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e == hipSuccess) e = sync(stream, ev_gpu);
       if (e != hipSuccess) return false;
       b.flat.assign(h_flat.h, h_flat.h + total);
       b.flat_e.assign(h_flat_e.h, h_flat_e.h + total);
@@ -1005,12 +1240,12 @@ struct RouteService::Impl {
                        ao, pl, d_qidx.d, stream, &rs, cfg.arena.base ? &cfg.arena : nullptr);
     n_escalated.fetch_add(rs.escalated, std::memory_order_relaxed);
     if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = sync(stream, ev_gpu);
     add_t(3, t0);
     t0 = now_us();
     if (e == hipSuccess) e = hipMemcpyAsync(h_len.h, d_len.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h_cost.h, d_cost.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = sync(stream, ev_gpu);
     if (e != hipSuccess) return false;
     long long total = 0;
     for (int i = 0; i < Q; ++i) {
@@ -1026,7 +1261,7 @@ struct RouteService::Impl {
         e = hipGetLastError();
       }
       if (e == hipSuccess) e = hipMemcpyAsync(h_flat.h, d_flat.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e == hipSuccess) e = sync(stream, ev_gpu);
       if (e != hipSuccess) return false;
       b.flat.assign(h_flat.h, h_flat.h + total);     // the next flush reuses the pinned buffer
     }
@@ -1232,12 +1467,20 @@ struct RouteService::Impl {
     hipError_t e = hipMemcpyAsync(d_rec.d, h_rec.h, (size_t)n * 16, hipMemcpyHostToDevice, stream_asm);
     if (e == hipSuccess) e = model->predict(d_rec.d, 16, d_eta.d, n, stream_asm, eta_ws);
     if (e == hipSuccess) e = hipMemcpyAsync(h_eta.h, d_eta.d, (size_t)n * 4, hipMemcpyDeviceToHost, stream_asm);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream_asm);
-    // a failed GPU round: the model's fp32 CPU forward (same fallback as the reactors)
-    if (e != hipSuccess && !model->cpu_predict(h_rec.h, h_eta.h, n)) return false;
+    if (e == hipSuccess) e = sync(stream_asm, ev_asm);
+    // a failed GPU round: the model's fp32 CPU forward (same fallback as the reactors), into a
+    // buffer of its own (a round past the deadline may still write h_eta later)
+    std::vector<float> cpu_eta;
+    const float* eta = h_eta.h;
+    if (e != hipSuccess) {
+      cpu_eta.resize((size_t)n);
+      std::vector<rtc::EtaRecord> rec(h_rec.h, h_rec.h + n);
+      if (!model->cpu_predict(rec.data(), cpu_eta.data(), n)) return false;
+      eta = cpu_eta.data();
+    }
     for (int k = 0; k < n; ++k) {
       RouteJob* j = m[k];
-      const double mins = (double)h_eta.h[k];
+      const double mins = (double)eta[k];
       // EtaService.finish: pickup + timedelta(minutes) — raises (-> no ETA fields) when out of range
       if (!std::isfinite(mins) || std::fabs(mins) > 1.4e9) continue;
       std::string tmp;
@@ -1247,7 +1490,7 @@ struct RouteService::Impl {
       if (a == std::string::npos) continue;
       const size_t b0 = a + 26;
       j->eta_iso = tmp.substr(b0, tmp.size() - 2 - b0);
-      j->eta_min = h_eta.h[k];
+      j->eta_min = eta[k];
     }
     return true;
   }
@@ -1255,11 +1498,15 @@ struct RouteService::Impl {
   // GPU stage: parse, trips (K5 + K6), snapping + the batched A* (graph provider)
   void gpu_stage(Batch& b) {
     std::vector<RouteJob*>& jobs = b.jobs;
-    n_jobs.fetch_add((long long)jobs.size(), std::memory_order_relaxed);
+    long long fresh_jobs = 0;
+    for (RouteJob* j : jobs) fresh_jobs += !j->parsed;
+    n_jobs.fetch_add(fresh_jobs, std::memory_order_relaxed);
     double t0 = now_us();
     rtc::parallel_chunks(jobs.size(), 32, 16, [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         RouteJob* j = jobs[i];
+        if (j->parsed) continue;                 // back from waiting for its routing context
+        j->parsed = true;
         bool parsed = false;
         if (j->json_ok && !j->body.empty()) {
           try {
@@ -1291,21 +1538,20 @@ struct RouteService::Impl {
     if (cfg.provider == 1 && cfg.cch != nullptr) {
       // road graph through the CCH: contexts -> road matrices + greedy -> legs
       if (!cch_groups(b) || !plan_multi_road(b)) {
-        fail_all(jobs, "route optimizer unavailable (GPU error)");
         b.failed = true;
         return;
       }
       add_t(1, t0);
       for (RouteJob* j : jobs)
         if (!j->fallback) rtr::directions_calls(j->req, j->plan, j->calls);
-      if (!search_legs_cch(b)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); b.failed = true; }
+      if (!search_legs_cch(b)) b.failed = true;
       return;
     }
-    if (!plan_multi(jobs)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); b.failed = true; return; }
+    if (!plan_multi(jobs)) { b.failed = true; return; }
     add_t(1, t0);
     for (RouteJob* j : jobs)
       if (!j->fallback) rtr::directions_calls(j->req, j->plan, j->calls);
-    if (cfg.provider == 1 && !search_legs(b)) { fail_all(jobs, "route optimizer unavailable (GPU error)"); b.failed = true; }
+    if (cfg.provider == 1 && !search_legs(b)) b.failed = true;
   }
 
   // assembly stage: GeoJSON, ETA, persistence, response bytes
@@ -1481,7 +1727,14 @@ std::vector<long long> RouteService::stats() const {
   v.push_back(p_->n_ctx_built.load());     // routing contexts customized by this service (CCH)
   v.push_back(p_->t_ctx_us.load());        // ... and their cost + customization time (us)
   v.push_back(p_->n_legs_reused.load());   // legs that reused their matrix chains (meet + unpack only)
+  v.push_back(p_->n_deferred.load());      // jobs that waited for their context's background build
+  v.push_back(p_->t_wait_us.load());       // ... their total wait (us)
+  v.push_back(p_->n_prefetch.load());      // next-week-hour contexts queued ahead of time
+  v.push_back(p_->n_failed_over.load());   // jobs handed to another GPU's route service
   return v;
+}
+
+bool RouteService::broken() const { return p_->broken.load();
 }
 
 }  // namespace rt

@@ -92,8 +92,8 @@ def context_costs_cpu(g: RoadGraph, eta_model, ctx: RouteContext) -> np.ndarray:
 class RoadRouter:
     """Legs and matrices under a routing context (GPU CCH, or the CPU reference)."""
 
-    def __init__(self, g: RoadGraph, eta_model=None, device=None, capacity: int = 32,
-                 max_path: int = 4096, threads: int = 0):
+    def __init__(self, g: RoadGraph, eta_model=None, device=None, capacity: Optional[int] = None,
+                 max_path: int = 4096, threads: int = 0, cache_gb: Optional[float] = None):
         from ..ops import _ext
         self.g = g
         self.dev = torch.device(device) if device is not None else torch.device("cpu")
@@ -116,7 +116,12 @@ class RoadRouter:
                                 torch.from_numpy(np.ascontiguousarray(g.road_class, dtype=np.uint8)),
                                 torch.from_numpy(base_traffic(g)), self.dev.index or 0)
             self.gpu.set_eta(self._kern.packed.blob, self._kern.hidden, list(self._kern.packed.norm), -1)
-            self.gpu.set_capacity(capacity)
+            # LRU of customized contexts: a fixed count if given, else as many as fit the HBM budget
+            # (ROUTEST_CCH_CACHE_GB, default 48 GB of the 288; csrc/cch.hip insert_cached)
+            if capacity is not None:
+                self.gpu.set_capacity(int(capacity))
+            elif cache_gb is not None:
+                self.gpu.set_cache_gb(float(cache_gb))
             self.cpu = None
         else:
             rt = _ext.runtime(required=True)
@@ -128,7 +133,7 @@ class RoadRouter:
             self._cpu_metrics: "OrderedDict[int, Any]" = OrderedDict()
             self._cpu_costs: Dict[int, np.ndarray] = {}
             self._cpu_pins: Dict[int, int] = {}
-            self.capacity = capacity
+            self.capacity = 32 if capacity is None else int(capacity)
         self.last_metric: Dict[str, Any] = {}
 
     # ---- metrics ----
@@ -165,6 +170,21 @@ class RoadRouter:
                 return
             del self._cpu_metrics[k]
             self._cpu_costs.pop(k, None)
+
+    def prefetch(self, ctx: RouteContext, urgent: bool = False) -> bool:
+        """Queue the context's customization on the GPU router's background builder (returns at
+        once; False on the CPU router, which has none)."""
+        if self.gpu is None:
+            return False
+        self.gpu.request_build(ctx.weather, ctx.congestion, ctx.weekhour, ctx.driver_age, urgent)
+        return True
+
+    def is_cached(self, ctx_or_key) -> bool:
+        key = ctx_or_key.key if isinstance(ctx_or_key, RouteContext) else int(ctx_or_key)
+        if self.gpu is not None:
+            return bool(self.gpu.is_cached(key))
+        with self._lock:
+            return key in self._cpu_metrics
 
     def unpin(self, key: int) -> None:
         if self.gpu is not None:

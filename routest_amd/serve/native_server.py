@@ -114,7 +114,13 @@ class NativePredictServer:
         self.model_epoch = int(self.C.native_server_set_models(self.h, self.devices, specs))
         return self.model_epoch
 
-    def set_fault(self, slot: int, on: bool = True) -> bool:
+    def set_fault(self, slot: int, on: bool = True, kind: str = "fail") -> bool:
+        """Fault injection on a GPU slot: ``fail`` — its launches fail without running; ``hang`` —
+        its launches (predictions and route flushes) first run a kernel that waits on a host flag,
+        so they miss the latency watchdog's deadline (``ROUTEST_GPU_DEADLINE_MS`` /
+        ``ROUTEST_ROUTE_DEADLINE_MS``) until the fault is cleared."""
+        if kind == "hang":
+            return bool(self.C.native_server_set_hang(self.h, slot, on))
         return bool(self.C.native_server_set_fault(self.h, slot, on))
 
     def set_scorer(self, scorer) -> bool:
@@ -138,7 +144,7 @@ class NativePredictServer:
         h["stats"] = {k: st.get(k) for k in ("requests", "predictions", "launches", "errors", "resident",
                                              "fallbacks", "failovers", "cpu_rounds", "route_jobs",
                                              "route_flushes", "route_service_fallbacks", "route_legs",
-                                             "route_contexts_built")}
+                                             "route_contexts_built", "route_failed_over", "timeouts")}
         h["degraded"] = any(s["quarantined"] for s in h["slots"])
         return h
 
@@ -168,7 +174,13 @@ class NativePredictServer:
                  # history / locations requests answered from the store's database natively
                  "history_native",
                  # GET /api/health and /metrics answered from the front end's micro-cache
-                 "cached")
+                 "cached",
+                 # CCH contexts off the flush's critical path: jobs that waited for their context's
+                 # background build, their total wait (us), next-week-hour contexts prefetched
+                 "route_ctx_deferred", "route_us_ctx_wait", "route_ctx_prefetched",
+                 # latency watchdog: route jobs handed to another GPU's route service after a
+                 # flush missed its deadline; prediction rounds abandoned at the deadline
+                 "route_failed_over", "timeouts")
         return dict(zip(names, v))
 
     def close(self) -> None:

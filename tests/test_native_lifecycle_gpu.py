@@ -168,3 +168,28 @@ def test_forest_served_natively_matches_cpu_reference():
         assert st.front.stats()["predictions"] >= 1
     finally:
         st.close()
+
+
+def test_hung_gpu_slot_watchdog_and_route_failover():
+    """Verdict r4 item 5 / SURVEY §5.3 "a watchdog on batch latency": with gpu_hang@1 (slot 1's
+    launches wait on a host flag) on a 2-slot shared-GPU rehearsal, no request waits longer than
+    the deadline + one round, nothing answers 5xx, slot 1 is quarantined, and route requests keep
+    being answered natively — slot 1's route service hands its flushes to slot 0's."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16", ROUTEST_GPU_DEADLINE_MS="100", ROUTEST_ROUTE_DEADLINE_MS="300",
+               ROUTEST_PERSIST_IDLE_MS="0", ROUTEST_QUARANTINE_PROBE_MS="60000")
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "_watchdog_child.py")], capture_output=True,
+                       text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["routes_on"]
+    assert d["codes"] == [200] and d["route_codes"] == [200], d
+    assert d["slot1"]["quarantined"] and d["slot1"]["deadline_timeouts"] >= 1, d
+    assert not d["slot0"]["quarantined"], d
+    # deadline (0.1 s predictions / 0.3 s route flushes) + one round, with margin for the host
+    assert d["max_latency_s"] < 1.0, d
+    assert d["route_service_fallbacks"] == 0 and d["route_jobs"] >= d["n_routes"], d
+    assert d["route_failed_over"] >= 1, d
