@@ -572,6 +572,26 @@ def main() -> None:
                 route_res["http"] = native_route_load(srv, route_payloads(g.lat, g.lon, 1000, seed=1), 1000,
                                                       a.route_http_seconds)
         sv.eta.close()
+        # the dashboard's own request (F02 verbatim: use_ml_eta, context, meta, driver_age) at 1k
+        # concurrency on the same port, every answer persisted into a SQLite store on disk — the
+        # canonical product path of /api/optimize_route (RO/Flaskr/routes.py:89-127)
+        if (prov is not None and isinstance(route_res, dict) and "error" not in route_res
+                and a.route_http_seconds > 0):
+            import tempfile
+            from routest_amd.serve.loadgen import f02_payloads
+            from routest_amd.store.store import SQLiteStore
+            with tempfile.TemporaryDirectory(prefix="routest-bench-") as td:
+                store = SQLiteStore(os.path.join(td, "routest.db"))
+                ids = [loc["id"] for loc in store.locations()]
+                sv2 = build_services(ss, eta=EtaService(model, devices=[local_rank]), provider=prov, store=store)
+                with ServingStack(sv2, create_app(sv2), model, [local_rank], threads=8) as srv2:
+                    if srv2.front.routes:
+                        r2 = native_route_load(srv2, f02_payloads(g.lat, g.lon, 1000, seed=2, location_ids=ids),
+                                               1000, a.route_http_seconds)
+                        r2["store"] = "sqlite file (WAL, synchronous=NORMAL), group commit per flush"
+                        route_res["http_f02"] = r2
+                sv2.eta.close()
+                store.close()
 
         # (2) the FastAPI app in-process over ASGI (like the reference's Flask test-client figure)
         import asyncio

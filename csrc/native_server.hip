@@ -97,8 +97,11 @@ struct SlotHealth {
 // deadline.  Reads only; every wave reaches the exit condition.
 __global__ __launch_bounds__(64) void hang_kernel(const int* release, long long max_ticks) {
   const long long t0 = wall_clock64();
-  while (__hip_atomic_load(release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
-         wall_clock64() - t0 < max_ticks)
+  // (also bounded by iterations: ~3.4 us per sleep at 2.4 GHz, 2M of them ~7 s, whatever the
+  // wall clock's rate)
+  for (int it = 0; it < 2000000 && __hip_atomic_load(release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
+                   wall_clock64() - t0 < max_ticks;
+       ++it)
     __builtin_amdgcn_s_sleep(127);
 }
 

@@ -35,7 +35,9 @@ class HistoryDb {
       close();
       return false;
     }
-    sql_.wait_on_locks(db_);
+    // runs on a reactor thread: a lock held elsewhere (the app, the route persister's group commit,
+    // a checkpoint) makes the call fall back to the app after ~2 ms instead of waiting up to ~20 s
+    sql_.wait_briefly(db_);
     sql_.exec(db_, "PRAGMA foreign_keys=ON", nullptr, nullptr, nullptr);
     return true;
   }

@@ -89,6 +89,15 @@ struct Api {
     return 1;
   }
   void wait_on_locks(void* db) { busy_handler(db, &Api::short_sleeps, nullptr); }
+  // For a connection used on an event-loop thread (the native front end's reactors): at most ~2 ms
+  // of 50 us sleeps, then SQLITE_BUSY — the caller relays the request to the app instead of
+  // stalling every connection of its reactor behind a writer's lock.
+  static int brief_sleeps(void*, int n) {
+    if (n >= 40) return 0;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+    return 1;
+  }
+  void wait_briefly(void* db) { busy_handler(db, &Api::brief_sleeps, nullptr); }
 };
 
 constexpr int OK = 0, ROW = 100, DONE = 101;

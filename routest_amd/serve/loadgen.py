@@ -26,6 +26,34 @@ def route_payloads(lat: np.ndarray, lon: np.ndarray, n: int, seed: int = 1) -> L
     return reqs
 
 
+def f02_payloads(lat: np.ndarray, lon: np.ndarray, n: int, seed: int = 2, location_ids: Sequence[str] = (),
+                 radius_km: float = 8.0) -> List[Dict[str, Any]]:
+    """``n`` requests exactly as the dashboard sends them (``FE/app/ui/page.jsx:1578-1617``):
+    ``use_ml_eta``, ``context`` {Sunny, Medium} (no pickup_time: routed at "now"), ``meta`` with the
+    seed locations' ids (``origin_id`` null for "My Current Location" one time in five), capacity
+    9999, ``maximum_distance`` 100 km, 1-10 stops (``MAX_STOPS``) within ``radius_km`` of the depot."""
+    rng = np.random.default_rng(seed)
+    ids = list(location_ids)
+    reqs = []
+    for i in range(n):
+        d = int(rng.integers(0, len(lat)))
+        k = int(rng.integers(1, 11))
+        r = radius_km * np.sqrt(rng.random(k))
+        th = rng.random(k) * 2 * np.pi
+        slat = lat[d] + r * np.cos(th) / 111.195
+        slon = lon[d] + r * np.sin(th) / (111.195 * np.cos(np.radians(lat[d])))
+        meta = {"origin_id": (ids[0] if ids and i % 5 else None),
+                "destination_ids": [ids[1 + (i + j) % (len(ids) - 1)] for j in range(k)] if len(ids) > 1 else [],
+                "vehicle_id": f"VAN-{i % 40:02d}"}
+        reqs.append({"source_point": {"lat": float(lat[d]), "lon": float(lon[d])},
+                     "destination_points": [{"lat": float(a), "lon": float(b), "payload": 1} for a, b in zip(slat, slon)],
+                     "driver_details": {"driver_name": f"Driver {i % 40}", "vehicle_type": "car",
+                                        "vehicle_capacity": 9999, "maximum_distance": 100000,
+                                        "driver_age": int(20 + i % 45)},
+                     "meta": meta, "use_ml_eta": True, "context": {"weather": "Sunny", "traffic": "Medium"}})
+    return reqs
+
+
 def _pct(lat_us: Sequence[float], q: float):
     if not len(lat_us):
         return None
@@ -57,6 +85,8 @@ def native_route_load(stack, reqs: Sequence[Dict[str, Any]], concurrency: int, s
             "contexts_customized": f1.get("route_contexts_built", 0) - f0.get("route_contexts_built", 0),
             "legs_escalated": f1.get("route_astar_escalated", 0) - f0.get("route_astar_escalated", 0),
             "fallbacks_to_python": f1["route_service_fallbacks"] - f0["route_service_fallbacks"],
+            "rows_persisted": f1["route_persisted"] - f0["route_persisted"],
+            "jobs_waited_for_context": f1.get("route_ctx_deferred", 0) - f0.get("route_ctx_deferred", 0),
             "stage_ms_per_flush": {k[9:]: (f1[k] - f0[k]) / 1e3 / flushes for k in f1 if k.startswith("route_us_")},
             "client": "native closed-loop (csrc/runtime/http_client.h)",
             "path": f"HTTP/1.1 loopback POST {path} -> native front end (main port) -> route service "

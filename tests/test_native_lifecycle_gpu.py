@@ -179,7 +179,7 @@ def test_hung_gpu_slot_watchdog_and_route_failover():
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="16", ROUTEST_GPU_DEADLINE_MS="100", ROUTEST_ROUTE_DEADLINE_MS="300",
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="32", ROUTEST_GPU_DEADLINE_MS="100", ROUTEST_ROUTE_DEADLINE_MS="300",
                ROUTEST_PERSIST_IDLE_MS="0", ROUTEST_QUARANTINE_PROBE_MS="60000")
     r = subprocess.run([sys.executable, os.path.join(root, "tests", "_watchdog_child.py")], capture_output=True,
                        text=True, timeout=240, env=env, cwd=root)
@@ -187,6 +187,7 @@ def test_hung_gpu_slot_watchdog_and_route_failover():
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["routes_on"]
     assert d["codes"] == [200] and d["route_codes"] == [200], d
+    print(json.dumps(d))
     assert d["slot1"]["quarantined"] and d["slot1"]["deadline_timeouts"] >= 1, d
     assert not d["slot0"]["quarantined"], d
     # deadline (0.1 s predictions / 0.3 s route flushes) + one round, with margin for the host
