@@ -1,17 +1,24 @@
-# round 5: CCH customization time per context (100k and 1M nodes) and PMC of its level kernels
+# round 5: CCH customization per context — A/B of the level kernels (push/atomic as in round 4,
+# push with skip-if-not-better, perfect as a pull), bit-identity vs the CPU reference, the 1M-node
+# city, and a PMC pass over the kernels that run by default
 ROOT=$GRAFT_REPO_ROOT
-cd /tmp && export TMPDIR=/tmp
+cd $ROOT
 O=$ROOT/gpurun_out/r5c; mkdir -p $O
-timeout -k 10 200 python3 $ROOT/bench/cch_customize_bench.py --contexts 5 --check > $O/cust_100k.jsonl 2>&1 || { tail -20 $O/cust_100k.jsonl; exit 1; }
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/stats -o cust --output-format csv -- python3 $ROOT/bench/cch_customize_bench.py --contexts 3 > $O/stats.log 2>&1 || { tail -20 $O/stats.log; exit 2; }
+stop() { rc=$1; [ $rc -eq 124 -o $rc -eq 137 -o $rc -eq 134 -o $rc -eq 139 ] && { echo "GPU step ended rc=$rc: stopping"; exit $rc; }; [ $rc -ne 0 ] && echo "step rc=$rc"; }
+timeout -k 10 200 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_cch_gpu.py > $O/test_cch_gpu.log 2>&1; stop $?
+timeout -k 10 200 env ROUTEST_CCH_PERFECT=push ROUTEST_CCH_SKIP=0 python3 bench/cch_customize_bench.py --contexts 4 > $O/cust_r4kernels.jsonl 2>&1; stop $?
+timeout -k 10 200 env ROUTEST_CCH_PERFECT=push python3 bench/cch_customize_bench.py --contexts 4 > $O/cust_push_skip.jsonl 2>&1; stop $?
+timeout -k 10 200 python3 bench/cch_customize_bench.py --contexts 4 --check > $O/cust_default.jsonl 2>&1; stop $?
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/stats -o cust --output-format csv -- python3 $ROOT/bench/cch_customize_bench.py --contexts 3 > $O/stats.log 2>&1; stop $?
 G1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_VALU SQ_INSTS_SALU"
 G2="FETCH_SIZE"
 G3="WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"
-G4="TCC_ATOMIC_sum GRBM_GUI_ACTIVE GRBM_COUNT"
 i=0
-for G in "$G1" "$G2" "$G3" "$G4"; do
+for G in "$G1" "$G2" "$G3"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $G -d $O/pmc$i -o cust --output-format csv -- python3 $ROOT/bench/cch_customize_bench.py --contexts 2 > $O/pmc$i.log 2>&1 || echo "pmc group $i failed rc=$?"
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $G -d $O/pmc$i -o cust --output-format csv -- python3 $ROOT/bench/cch_customize_bench.py --contexts 2 > $O/pmc$i.log 2>&1; stop $?
 done
-timeout -k 10 400 python3 $ROOT/bench/cch_customize_bench.py --nodes 1000000 --contexts 3 > $O/cust_1m.jsonl 2>&1 || { tail -20 $O/cust_1m.jsonl; exit 3; }
+cd $ROOT
+timeout -k 10 500 python3 bench/cch_customize_bench.py --nodes 1000000 --contexts 3 > $O/cust_1m.jsonl 2>&1; stop $?
 echo done

@@ -32,6 +32,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "cch_gpu.h"
 #include "ops.h"
@@ -128,6 +129,10 @@ __global__ void tri_build_kernel(const int32_t* __restrict__ up_ptr, const int32
 
 // Basic customization of one height level: items [0, k) of node z finalize arc k-th of z; items
 // [k, k + k(k-1)/2) relax the lower triangle z of one pair of z's upward neighbours.
+// SKIP: a candidate is sent to the atomic only if it beats the target's current value (a plain load;
+// a stale value is only ever larger, so nothing that could win is skipped) — most of a target's
+// candidates lose, and the 64-bit atomics were the level kernels' L2 traffic (round 5)
+template <bool SKIP>
 __global__ __launch_bounds__(256) void basic_level_kernel(LevelArgs L, unsigned long long* __restrict__ up,
                                                           unsigned long long* __restrict__ dn,
                                                           int32_t* __restrict__ sub_up, int32_t* __restrict__ sub_dn,
@@ -194,8 +199,14 @@ __global__ __launch_bounds__(256) void basic_level_kernel(LevelArgs L, unsigned 
   // u -> z -> v: (z,u) traversed down, (z,v) up;  v -> z -> u: (z,v) down, (z,u) up
   const float wu = wof(dn[ai]) + wof(up[aj]);
   const float wd = wof(dn[aj]) + wof(up[ai]);
-  if (wu < F_INF) atomicMin(up + t, packw(wu, (uint32_t)z));
-  if (wd < F_INF) atomicMin(dn + t, packw(wd, (uint32_t)z));
+  if (wu < F_INF) {
+    const unsigned long long pu = packw(wu, (uint32_t)z);
+    if (!SKIP || pu < up[t]) atomicMin(up + t, pu);
+  }
+  if (wd < F_INF) {
+    const unsigned long long pd = packw(wd, (uint32_t)z);
+    if (!SKIP || pd < dn[t]) atomicMin(dn + t, pd);
+  }
 }
 
 __global__ void perfect_init_kernel(const unsigned long long* __restrict__ up, const unsigned long long* __restrict__ dn,
@@ -210,6 +221,7 @@ __global__ void perfect_init_kernel(const unsigned long long* __restrict__ up, c
 // candidate for arc a = (x, y) goes through z = head(c): x -> z on c (basic), z -> y on {z, y}
 // (perfect: an arc between two ancestors, finished by an earlier level).  Consecutive items share c
 // and spread over a (different atomic targets).
+template <bool SKIP>
 __global__ __launch_bounds__(256) void perfect_level_kernel(LevelArgs L, const unsigned long long* __restrict__ up,
                                                             const unsigned long long* __restrict__ dn,
                                                             uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
@@ -234,8 +246,92 @@ __global__ __launch_bounds__(256) void perfect_level_kernel(LevelArgs L, const u
   const float zy = __uint_as_float(z < y ? pup[azy] : pdn[azy]);
   const float yz = __uint_as_float(z < y ? pdn[azy] : pup[azy]);
   const float cu = xz + zy, cd = yz + zx;
-  if (cu < F_INF) atomicMin(pup + aa, __float_as_uint(cu));
-  if (cd < F_INF) atomicMin(pdn + aa, __float_as_uint(cd));
+  if (cu < F_INF && (!SKIP || __float_as_uint(cu) < pup[aa])) atomicMin(pup + aa, __float_as_uint(cu));
+  if (cd < F_INF && (!SKIP || __float_as_uint(cd) < pdn[aa])) atomicMin(pdn + aa, __float_as_uint(cd));
+}
+
+// Perfect customization as a PULL over one depth level (round 5): every arc a = (x, y) of the
+// level's nodes takes the min over x's other arcs c of the candidate through z = head(c), and is
+// written once with a plain store — the level owns its arcs, so no atomics and no per-item decode.
+// Same candidate set and fp32 sums as the push kernel / the CPU reference (bit-identical).
+struct PullArgs {
+  const int32_t* up_ptr;
+  const int32_t* up_head;
+  const int32_t* nodes;    // depth-ordered node list
+  const int64_t* aofs;     // arc prefix over that list
+  int lo, hi;              // node index range of the level
+  long long base, arcs;    // arc range of the level
+  const int64_t* tofs;     // triangle table (required)
+  const int32_t* tri;
+};
+
+__device__ __forceinline__ void pull_cand(const PullArgs& P, int x, int k, int a0, int ia, int ic, float xz_c, float zx_c,
+                                          const uint32_t* __restrict__ pup, const uint32_t* __restrict__ pdn, int y,
+                                          int z, float& bu, float& bd) {
+  const int i = ic < ia ? ic : ia, j = ic < ia ? ia : ic;
+  const int azy = P.tri[P.tofs[x] + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)];
+  const float zy = __uint_as_float(z < y ? pup[azy] : pdn[azy]);
+  const float yz = __uint_as_float(z < y ? pdn[azy] : pup[azy]);
+  const float cu = xz_c + zy, cd = yz + zx_c;
+  bu = cu < bu ? cu : bu;
+  bd = cd < bd ? cd : bd;
+}
+
+// one wave per arc, lanes over the node's other arcs (levels of high-degree nodes: the top
+// separators, k up to ~1400)
+__global__ __launch_bounds__(256) void perfect_pull_wave_kernel(PullArgs P, const unsigned long long* __restrict__ up,
+                                                                const unsigned long long* __restrict__ dn,
+                                                                uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+  const long long g = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (g >= P.arcs) return;
+  const int ni = item_owner(P.aofs, P.lo, P.hi, P.base + g);
+  const int x = P.nodes[ni];
+  const int a0 = P.up_ptr[x];
+  const int k = P.up_ptr[x + 1] - a0;
+  const int ia = (int)(P.base + g - P.aofs[ni]);
+  const int aa = a0 + ia;
+  const int y = P.up_head[aa];
+  float bu = F_INF, bd = F_INF;
+  for (int ic = lane; ic < k; ic += 64) {
+    if (ic == ia) continue;
+    const int ac = a0 + ic;
+    pull_cand(P, x, k, a0, ia, ic, wof(up[ac]), wof(dn[ac]), pup, pdn, y, P.up_head[ac], bu, bd);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ou = __shfl_xor(bu, o), od = __shfl_xor(bd, o);
+    bu = ou < bu ? ou : bu;
+    bd = od < bd ? od : bd;
+  }
+  if (lane == 0) {
+    const float cu = __uint_as_float(pup[aa]), cd = __uint_as_float(pdn[aa]);
+    if (bu < cu) pup[aa] = __float_as_uint(bu);
+    if (bd < cd) pdn[aa] = __float_as_uint(bd);
+  }
+}
+
+// one lane per arc, looping over the node's other arcs (levels of low-degree nodes)
+__global__ __launch_bounds__(256) void perfect_pull_lane_kernel(PullArgs P, const unsigned long long* __restrict__ up,
+                                                                const unsigned long long* __restrict__ dn,
+                                                                uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= P.arcs) return;
+  const int ni = item_owner(P.aofs, P.lo, P.hi, P.base + g);
+  const int x = P.nodes[ni];
+  const int a0 = P.up_ptr[x];
+  const int k = P.up_ptr[x + 1] - a0;
+  const int ia = (int)(P.base + g - P.aofs[ni]);
+  const int aa = a0 + ia;
+  const int y = P.up_head[aa];
+  float bu = __uint_as_float(pup[aa]), bd = __uint_as_float(pdn[aa]);
+  for (int ic = 0; ic < k; ++ic) {
+    if (ic == ia) continue;
+    const int ac = a0 + ic;
+    pull_cand(P, x, k, a0, ia, ic, wof(up[ac]), wof(dn[ac]), pup, pdn, y, P.up_head[ac], bu, bd);
+  }
+  pup[aa] = __float_as_uint(bu);
+  pdn[aa] = __float_as_uint(bd);
 }
 
 __device__ __forceinline__ bool kept(uint32_t p, unsigned long long b) {
@@ -899,11 +995,13 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   // order; perfect items = k(k-1), depth order
   bofs_.assign(N + 1, 0);
   pofs_.assign(N + 1, 0);
+  aofs_.assign(N + 1, 0);
   for (int i = 0; i < N; ++i) {
     const int64_t kb = T_.up_ptr[T_.hlev_nodes[i] + 1] - T_.up_ptr[T_.hlev_nodes[i]];
     bofs_[i + 1] = bofs_[i] + kb * (kb + 1) / 2;
     const int64_t kp = T_.up_ptr[T_.dlev_nodes[i] + 1] - T_.up_ptr[T_.dlev_nodes[i]];
     pofs_[i + 1] = pofs_[i] + kp * (kp - 1);
+    aofs_[i + 1] = aofs_[i] + kp;
   }
   hipError_t e = hipSuccess;
   auto ck = [&](hipError_t x) {
@@ -925,6 +1023,7 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   ck(up_copy(d_dnodes, T_.dlev_nodes.data(), N));
   ck(up_copy(d_bofs, bofs_.data(), N + 1));
   ck(up_copy(d_pofs, pofs_.data(), N + 1));
+  ck(up_copy(d_aofs, aofs_.data(), N + 1));
   ck(dmalloc(d_up64, M));
   ck(dmalloc(d_dn64, M));
   ck(dmalloc(d_pup, M));
@@ -998,6 +1097,7 @@ CchGpu::~CchGpu() {
   dfree(d_dnodes);
   dfree(d_bofs);
   dfree(d_pofs);
+  dfree(d_aofs);
   dfree(d_tofs);
   dfree(d_tri);
   dfree(d_up64);
@@ -1067,6 +1167,24 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   hipLaunchKernelGGL(edge_scatter_kernel, dim3(blocks_for(E, 256)), dim3(256), 0, s, m.cost, d_edge_arc, d_edge_dir,
                      (int)E, d_up64, d_dn64);
   ck(hipGetLastError());
+  static const bool skip = [] {
+    const char* v = std::getenv("ROUTEST_CCH_SKIP");
+    return !(v && std::string(v) == "0");
+  }();
+  // phase boundaries (basic / perfect / prune device times, reported with the metric)
+  struct Events {
+    hipEvent_t e[4] = {};
+    Events() {
+      for (auto& x : e)
+        if (hipEventCreate(&x) != hipSuccess) x = nullptr;
+    }
+    ~Events() {
+      for (auto& x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } evs;
+  hipEvent_t* ev = evs.e;
+  if (ev[0]) (void)hipEventRecord(ev[0], s);
   // basic, bottom-up by height
   for (int h = 0; h <= T_.max_height && e == hipSuccess; ++h) {
     LevelArgs L{d_up_ptr, d_up_head, d_hnodes, d_bofs, (int)T_.hlev_ptr[h], (int)T_.hlev_ptr[h + 1], 0, 0, d_tofs, d_tri};
@@ -1074,23 +1192,52 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     L.base = bofs_[L.lo];
     L.items = bofs_[L.hi] - bofs_[L.lo];
     if (L.items <= 0) continue;
-    hipLaunchKernelGGL(basic_level_kernel, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
-                       m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
+    if (skip)
+      hipLaunchKernelGGL(basic_level_kernel<true>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
+                         m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
+    else
+      hipLaunchKernelGGL(basic_level_kernel<false>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
+                         m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
     ck(hipGetLastError());
   }
+  if (ev[1]) (void)hipEventRecord(ev[1], s);
   // perfect, top-down by depth
   hipLaunchKernelGGL(perfect_init_kernel, dim3(fill_blocks), dim3(256), 0, s, d_up64, d_dn64, d_pup, d_pdn, (long long)M);
   ck(hipGetLastError());
-  for (int d = 0; d <= T_.max_depth && e == hipSuccess; ++d) {
+  // pull (default with the triangle table; ROUTEST_CCH_PERFECT=push: the atomic kernel)
+  static const bool pull = [] {
+    const char* v = std::getenv("ROUTEST_CCH_PERFECT");
+    return !(v && std::string(v) == "push");
+  }();
+  for (int d = 0; d <= T_.max_depth && e == hipSuccess && pull && d_tri != nullptr; ++d) {
+    const int lo = (int)T_.dlev_ptr[d], hi = (int)T_.dlev_ptr[d + 1];
+    if (lo >= hi) continue;
+    PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri};
+    if (P.arcs <= 0 || pofs_[hi] == pofs_[lo]) continue;       // no node of the level has two arcs
+    // mean degree of the level's nodes: wide nodes get a wave per arc, narrow ones a lane per arc
+    if (P.arcs >= 24 * (long long)(hi - lo))
+      hipLaunchKernelGGL(perfect_pull_wave_kernel, dim3((unsigned)((P.arcs + 3) / 4)), dim3(256), 0, s, P, d_up64,
+                         d_dn64, d_pup, d_pdn);
+    else
+      hipLaunchKernelGGL(perfect_pull_lane_kernel, dim3(blocks_for(P.arcs, 256)), dim3(256), 0, s, P, d_up64, d_dn64,
+                         d_pup, d_pdn);
+    ck(hipGetLastError());
+  }
+  for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(pull && d_tri != nullptr); ++d) {
     LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0, d_tofs, d_tri};
     if (L.lo >= L.hi) continue;
     L.base = pofs_[L.lo];
     L.items = pofs_[L.hi] - pofs_[L.lo];
     if (L.items <= 0) continue;
-    hipLaunchKernelGGL(perfect_level_kernel, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64, d_pup,
-                       d_pdn);
+    if (skip)
+      hipLaunchKernelGGL(perfect_level_kernel<true>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
+                         d_pup, d_pdn);
+    else
+      hipLaunchKernelGGL(perfect_level_kernel<false>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
+                         d_pup, d_pdn);
     ck(hipGetLastError());
   }
+  if (ev[2]) (void)hipEventRecord(ev[2], s);
   // prune + compact
   hipLaunchKernelGGL(prune_count_kernel, dim3(blocks_for(N, 256)), dim3(256), 0, s, d_up_ptr, d_pup, d_pdn, d_up64,
                      d_dn64, N, d_fcnt, d_bcnt);
@@ -1120,8 +1267,13 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   hipLaunchKernelGGL(prune_scatter_kernel, dim3(blocks_for(N, 256)), dim3(256), 0, s, d_up_ptr, d_up_head, d_depth,
                      d_pup, d_pdn, d_up64, d_dn64, N, m.f_ptr, m.b_ptr, m.f_rec, m.b_rec);
   ck(hipGetLastError());
+  if (ev[3]) (void)hipEventRecord(ev[3], s);
   ck(hipStreamSynchronize(s));
   m.customize_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  float ms = 0.f;
+  if (ev[0] && ev[1] && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) m.basic_ms = ms;
+  if (ev[1] && ev[2] && hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) m.perfect_ms = ms;
+  if (ev[2] && ev[3] && hipEventElapsedTime(&ms, ev[2], ev[3]) == hipSuccess) m.prune_ms = ms;
   m.host_cost.clear();
   return e;
 }

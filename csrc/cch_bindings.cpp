@@ -122,6 +122,9 @@ class PyCchGpu {
     d["fresh"] = fresh;
     d["cost_ms"] = m.cost_ms;
     d["customize_ms"] = m.customize_ms;
+    d["basic_ms"] = m.basic_ms;
+    d["perfect_ms"] = m.perfect_ms;
+    d["prune_ms"] = m.prune_ms;
     d["kept_f"] = m.kept_f;
     d["kept_b"] = m.kept_b;
     return d;

@@ -50,6 +50,7 @@ struct CchMetricDev {
   int4* b_rec = nullptr;
   int64_t kept_f = 0, kept_b = 0;
   double customize_ms = 0.0, cost_ms = 0.0;
+  double basic_ms = 0.0, perfect_ms = 0.0, prune_ms = 0.0;   // device time per phase
   std::vector<float> host_cost;    // [E] for the exact host fallback (filled on demand)
   ~CchMetricDev();
 };
@@ -167,7 +168,8 @@ class CchGpu {
   uint8_t *d_class = nullptr, *d_base_traffic = nullptr;
   int32_t *d_hnodes = nullptr, *d_dnodes = nullptr;
   int64_t *d_bofs = nullptr, *d_pofs = nullptr;    // work-item prefixes in level order
-  std::vector<int64_t> bofs_, pofs_;               // host copies (level boundaries)
+  int64_t* d_aofs = nullptr;                       // arc prefix in depth order (perfect pull)
+  std::vector<int64_t> bofs_, pofs_, aofs_;        // host copies (level boundaries)
   // triangle table (metric-independent): for the pair (i < j) of rank z's upward arcs, the arc id of
   // {head i, head j} at tri[tofs[z] + i(2k-i-1)/2 + j-i-1] — the customization's binary searches
   // done once per graph (nullptr when it would not fit the ROUTEST_CCH_TRI_GB budget)

@@ -354,11 +354,11 @@ class Reactor {
     (void)hipHostFree(h_rec8_);
     (void)hipHostFree(h_out_);
     for (auto& kv : streams_) {
-      (void)hipSetDevice(kv.first);
+      (void)hipSetDevice(kv.first >= 0 ? kv.first : cfg_.sh->devices[-1 - kv.first]);
       (void)hipStreamDestroy(kv.second);
     }
     for (auto& kv : events_) {
-      (void)hipSetDevice(kv.first);
+      (void)hipSetDevice(kv.first >= 0 ? kv.first : cfg_.sh->devices[-1 - kv.first]);
       (void)hipEventDestroy(kv.second);
     }
     reap_retired(true);
@@ -1068,7 +1068,7 @@ class Reactor {
   // a round on `dev` missed its deadline: its kernel may still run and write this reactor's
   // buffers, so they, the stream and the workspace are retired and the round continues on fresh
   // ones (records copied over)
-  bool retire_round(int dev, hipStream_t st, hipEvent_t ev, std::shared_ptr<const NativeModel> m) {
+  bool retire_round(int dev, int skey, hipStream_t st, hipEvent_t ev, std::shared_ptr<const NativeModel> m) {
     const unsigned fl = hipHostMallocMapped | hipHostMallocPortable;
     EtaRecord* nr = nullptr;
     rtc::Wire8* n8 = nullptr;
@@ -1090,8 +1090,8 @@ class Reactor {
     w.p = nullptr;
     w.bytes = 0;
     retired_.push_back(std::move(r));
-    streams_.erase(dev);
-    events_.erase(dev);
+    streams_.erase(skey);
+    events_.erase(skey);
     h_rec_ = nr;
     h_rec8_ = n8;
     h_out_ = no;
@@ -1110,31 +1110,34 @@ class Reactor {
     if (hipSetDevice(dev) != hipSuccess) return hipErrorInvalidDevice;
     if (!retired_.empty()) reap_retired(false);
     (void)hipSetDevice(dev);
+    // a slot under the gpu_hang fault hook runs on a stream of its own (key -1 - g), on a hardware
+    // queue of its own
+    const bool hang = sh.health[g]->hang.load(std::memory_order_relaxed) && sh.hang_release_d != nullptr;
+    const int skey = hang ? -1 - g : dev;
     hipStream_t st;
-    auto it = streams_.find(dev);
+    auto it = streams_.find(skey);
     if (it == streams_.end()) {
-      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+      if ((hang ? isolated_stream(dev, &st) : hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) {
         (void)hipSetDevice(cfg_.device);
         return hipErrorOutOfMemory;
       }
-      streams_[dev] = st;
+      streams_[skey] = st;
     } else {
       st = it->second;
     }
     hipEvent_t ev;
-    auto ei = events_.find(dev);
+    auto ei = events_.find(skey);
     if (ei == events_.end()) {
       if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
         (void)hipSetDevice(cfg_.device);
         return hipErrorOutOfMemory;
       }
-      events_[dev] = ev;
+      events_[skey] = ev;
     } else {
       ev = ei->second;
     }
     sh.park(g);                        // keep a hardware queue the resident scorer may share free
-    if (sh.health[g]->hang.load(std::memory_order_relaxed) && sh.hang_release_d != nullptr)
-      hipLaunchKernelGGL(hang_kernel, dim3(1), dim3(64), 0, st, sh.hang_release_d, 500000000ll);   // <= 5 s
+    if (hang) hipLaunchKernelGGL(hang_kernel, dim3(1), dim3(64), 0, st, sh.hang_release_d, 500000000ll);   // <= 5 s
     // 8-byte wire records whenever the round is exactly representable and the model reads them
     // (csrc/runtime/rt_core.h pack_wire8), else 16-byte
     const bool w8 = m.takes_wire8() && rtc::pack_wire8(h_rec_, nrec_, h_rec8_);
@@ -1144,7 +1147,7 @@ class Reactor {
     if (e == hipErrorLaunchTimeOut) {
       sh.timed_out(g);
       st_.timeouts.fetch_add(1, std::memory_order_relaxed);
-      if (!retire_round(dev, st, ev, mp)) e = hipErrorOutOfMemory;
+      if (!retire_round(dev, skey, st, ev, mp)) e = hipErrorOutOfMemory;
     }
     (void)hipSetDevice(cfg_.device);
     return e;

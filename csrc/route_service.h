@@ -19,6 +19,17 @@ namespace rt {
 struct PersistentScorer;
 struct RouteJob;
 
+// A stream on a hardware queue of its own (a full CU mask makes the runtime give the stream a
+// dedicated queue): the gpu_hang fault hook runs the hung work on one, so on a shared-GPU
+// rehearsal the other slot's streams are never queued behind it — on a real node the slots are
+// separate GPUs anyway.
+inline hipError_t isolated_stream(int device, hipStream_t* s) {
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+  std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
+  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+
 // The GCN candidate-route scorer's node delay factors for "alternatives" requests
 // (routing/alternatives.py; csrc/runtime/alternatives.h), published by the Python side once the
 // scorer is trained (NativePredictServer.set_scorer); until then such requests go to the app.

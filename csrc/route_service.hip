@@ -267,6 +267,7 @@ struct RouteService::Impl {
   double deadline_ms = 2000.0;
   std::atomic<bool> broken{false};
   hipEvent_t ev_gpu{}, ev_asm{};
+  hipStream_t hang_stream{};              // the gpu_hang fault hook's stream (own hardware queue)
   std::atomic<long long> n_failed_over{0};
 
   hipError_t sync(hipStream_t s, hipEvent_t ev) {
@@ -490,9 +491,21 @@ struct RouteService::Impl {
           continue;
         }
       }
-      if (cfg.hang_fault && cfg.hang_release_d && cfg.hang_fault())
-        hipLaunchKernelGGL(route_hang_kernel, dim3(1), dim3(64), 0, stream, cfg.hang_release_d, 500000000ll);
+      // gpu_hang fault hook: this flush's GPU work goes to a stream on a hardware queue of its own,
+      // behind a kernel that waits on the host flag (abandoned, not destroyed, if it hangs)
+      hipStream_t main_stream = stream;
+      if (cfg.hang_fault && cfg.hang_release_d && cfg.hang_fault()) {
+        if (!hang_stream && isolated_stream(cfg.device, &hang_stream) != hipSuccess) hang_stream = nullptr;
+        if (hang_stream) {
+          stream = hang_stream;
+          hipLaunchKernelGGL(route_hang_kernel, dim3(1), dim3(64), 0, stream, cfg.hang_release_d, 500000000ll);
+        }
+      }
       gpu_stage(*b);
+      if (stream != main_stream) {
+        if (broken.load()) hang_stream = nullptr;      // still busy: a fresh one next time
+        stream = main_stream;
+      }
       if (b->failed) {              // a GPU error or the deadline: another GPU's service answers
         hand_off(b->jobs);
         delete b;
