@@ -334,6 +334,142 @@ __global__ __launch_bounds__(256) void perfect_pull_lane_kernel(PullArgs P, cons
   pdn[aa] = __float_as_uint(bd);
 }
 
+// ---- task-table customization (round 5) ----
+// A wave's work is one precomputed, metric-independent TASK (8 bytes, built once per graph in level
+// order): {node, row/arc index, first column}; its 64 lanes take 64 consecutive columns.  That
+// replaces the per-item chain of the flattened kernels (binary search for the item's node, node id,
+// arc range, the pair decode by sqrt) — which made every wave a ~6-deep chain of dependent global
+// loads — by one scalar load of the task and one of the node's arc range, and the lanes' loads are
+// coalesced along a row of the triangle table.
+struct CustTask {
+  int32_t node;
+  uint16_t row;      // basic: pair row i (ROW_FINAL: the node's own arcs); perfect: the target arc's index
+  uint16_t col0;     // first column (c or j) of the wave's 64
+};
+constexpr uint16_t ROW_FINAL = 0xFFFF;
+
+// Basic customization of one height level, one task per wave: a pair row (i, j0 .. j0+63) of node
+// z relaxes its lower triangles z of the arcs {head i, head j}; a ROW_FINAL task finalizes 64 of
+// z's own arcs (best triangle's two sub-arcs, metres, road-edge counts).  Same math as
+// basic_level_kernel (bit-identical).
+template <bool SKIP>
+__global__ __launch_bounds__(256) void basic_task_kernel(const CustTask* __restrict__ tasks, long long ntask,
+                                                         const int32_t* __restrict__ up_ptr,
+                                                         const int32_t* __restrict__ up_head,
+                                                         const int64_t* __restrict__ tofs, const int32_t* __restrict__ tri,
+                                                         unsigned long long* __restrict__ up,
+                                                         unsigned long long* __restrict__ dn, int32_t* __restrict__ sub_up,
+                                                         int32_t* __restrict__ sub_dn, float* __restrict__ len_up,
+                                                         float* __restrict__ len_dn, int32_t* __restrict__ cnt_up,
+                                                         int32_t* __restrict__ cnt_dn, const float* __restrict__ length) {
+  const long long ti = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ti >= ntask) return;
+  const int lane = threadIdx.x & 63;
+  const CustTask T = tasks[ti];
+  const int z = T.node;
+  const int a0 = up_ptr[z];
+  const int k = up_ptr[z + 1] - a0;
+  if (T.row == ROW_FINAL) {
+    const int p = T.col0 + lane;
+    if (p >= k) return;
+    const int a = a0 + p;
+    const int v = up_head[a];
+#pragma unroll
+    for (int dir = 0; dir < 2; ++dir) {
+      const unsigned long long w = dir ? dn[a] : up[a];
+      int32_t* sub = (dir ? sub_dn : sub_up) + 2 * (long long)a;
+      float* len = dir ? len_dn : len_up;
+      int32_t* cnt = dir ? cnt_dn : cnt_up;
+      if (!(wof(w) < F_INF)) {
+        sub[0] = -1;
+        sub[1] = -1;
+        len[a] = F_INF;
+        cnt[a] = 0;
+        continue;
+      }
+      const uint32_t pl = (uint32_t)w;
+      if (pl & EDGE_FLAG_D) {
+        const int e = (int)(pl & ~EDGE_FLAG_D);
+        sub[0] = -1;
+        sub[1] = e;
+        len[a] = length[e];
+        cnt[a] = 1;
+        continue;
+      }
+      const int zz = (int)pl;
+      const int azu = find_arc_d(up_ptr, up_head, zz, z), azv = find_arc_d(up_ptr, up_head, zz, v);
+      const int s0 = dir ? azv : azu, s1 = dir ? azu : azv;
+      sub[0] = s0;
+      sub[1] = s1;
+      len[a] = len_dn[s0] + len_up[s1];
+      cnt[a] = cnt_dn[s0] + cnt_up[s1];
+    }
+    return;
+  }
+  const int i = T.row;
+  const int j = T.col0 + lane;
+  if (j >= k) return;
+  const int ai = a0 + i, aj = a0 + j;
+  const int t = tri[tofs[z] + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)];
+  if (t < 0) return;
+  const float wu = wof(dn[ai]) + wof(up[aj]);
+  const float wd = wof(dn[aj]) + wof(up[ai]);
+  if (wu < F_INF) {
+    const unsigned long long pu = packw(wu, (uint32_t)z);
+    if (!SKIP || pu < up[t]) atomicMin(up + t, pu);
+  }
+  if (wd < F_INF) {
+    const unsigned long long pd = packw(wd, (uint32_t)z);
+    if (!SKIP || pd < dn[t]) atomicMin(dn + t, pd);
+  }
+}
+
+// Perfect customization of one depth level, one task per wave: target arc a = (x, y) of node x
+// and 64 of x's other arcs c as candidates (through z = head(c)); the wave's min goes to the
+// target with one atomicMin (only if it beats the current value) — 64x fewer atomics than the
+// push kernel, and no serial loop over c as in the one-wave-per-arc pull.
+__global__ __launch_bounds__(256) void perfect_task_kernel(const CustTask* __restrict__ tasks, long long ntask,
+                                                           const int32_t* __restrict__ up_ptr,
+                                                           const int32_t* __restrict__ up_head,
+                                                           const int64_t* __restrict__ tofs,
+                                                           const int32_t* __restrict__ tri,
+                                                           const unsigned long long* __restrict__ up,
+                                                           const unsigned long long* __restrict__ dn,
+                                                           uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+  const long long ti = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ti >= ntask) return;
+  const int lane = threadIdx.x & 63;
+  const CustTask T = tasks[ti];
+  const int x = T.node;
+  const int a0 = up_ptr[x];
+  const int k = up_ptr[x + 1] - a0;
+  const int ia = T.row;
+  const int aa = a0 + ia;
+  const int y = up_head[aa];
+  const int ic = T.col0 + lane;
+  float bu = F_INF, bd = F_INF;
+  if (ic < k && ic != ia) {
+    const int ac = a0 + ic;
+    const int z = up_head[ac];
+    const int i = ic < ia ? ic : ia, j = ic < ia ? ia : ic;
+    const int azy = tri[tofs[x] + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)];
+    const float zy = __uint_as_float(z < y ? pup[azy] : pdn[azy]);
+    const float yz = __uint_as_float(z < y ? pdn[azy] : pup[azy]);
+    bu = wof(up[ac]) + zy;
+    bd = yz + wof(dn[ac]);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ou = __shfl_xor(bu, o), od = __shfl_xor(bd, o);
+    bu = ou < bu ? ou : bu;
+    bd = od < bd ? od : bd;
+  }
+  if (lane == 0) {
+    if (bu < F_INF && __float_as_uint(bu) < pup[aa]) atomicMin(pup + aa, __float_as_uint(bu));
+    if (bd < F_INF && __float_as_uint(bd) < pdn[aa]) atomicMin(pdn + aa, __float_as_uint(bd));
+  }
+}
+
 __device__ __forceinline__ bool kept(uint32_t p, unsigned long long b) {
   return __uint_as_float(p) < F_INF && p == (uint32_t)(b >> 32);
 }
@@ -952,16 +1088,22 @@ CchScratch::~CchScratch() {
   dfree(arcs);
   dfree(narcs);
   dfree(pj);
+  for (void* p : old) (void)hipFree(p);
   (void)hipSetDevice(cur);
 }
 
+// (outgrown buffers are kept until the scratch dies: a hipFree would wait for the whole device)
 hipError_t CchScratch::ensure(size_t J, size_t P, int stride, int max_arcs) {
   hipError_t e = hipSuccess;
+  auto retire = [&](auto*& p) {
+    if (p) old.push_back((void*)p);
+    p = nullptr;
+  };
   if (J > jobs_cap) {
-    dfree(dist);
-    dfree(pred);
-    dfree(node);
-    dfree(jobs);
+    retire(dist);
+    retire(pred);
+    retire(node);
+    retire(jobs);
     const size_t cap = std::max(J, jobs_cap * 3 / 2);
     if ((e = dmalloc(dist, cap * stride)) != hipSuccess) return e;
     if ((e = dmalloc(pred, cap * stride)) != hipSuccess) return e;
@@ -970,8 +1112,8 @@ hipError_t CchScratch::ensure(size_t J, size_t P, int stride, int max_arcs) {
     jobs_cap = cap;
   }
   if (P > pairs_cap) {
-    dfree(arcs);
-    dfree(narcs);
+    retire(arcs);
+    retire(narcs);
     const size_t cap = std::max(P, pairs_cap * 3 / 2);
     if ((e = dmalloc(arcs, cap * (size_t)max_arcs)) != hipSuccess) return e;
     if ((e = dmalloc(narcs, cap)) != hipSuccess) return e;
@@ -1050,6 +1192,7 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
                            d_up_ptr, d_up_head, d_tofs, N, (long long)T, d_tri);
         if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
           n_tri = T;
+          build_tasks();
         } else {
           dfree(d_tri);
           dfree(d_tofs);
@@ -1064,6 +1207,50 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   (void)hipSetDevice(cur);
   if (e != hipSuccess) throw std::runtime_error(std::string("CchGpu: ") + hipGetErrorString(e));
   if (const char* gb = std::getenv("ROUTEST_CCH_CACHE_GB")) cache_gb_ = std::atof(gb);
+}
+
+// the task tables of the task-table customization (metric-independent; level order)
+void CchGpu::build_tasks() {
+  if (const char* v = std::getenv("ROUTEST_CCH_TASKS"))
+    if (std::string(v) == "0") return;
+  const int N = T_.N;
+  std::vector<CustTask> bt, pt;
+  btask_ptr_.assign(T_.max_height + 2, 0);
+  for (int h = 0; h <= T_.max_height; ++h) {
+    for (int64_t q = T_.hlev_ptr[h]; q < T_.hlev_ptr[h + 1]; ++q) {
+      const int z = T_.hlev_nodes[q];
+      const int k = (int)(T_.up_ptr[z + 1] - T_.up_ptr[z]);
+      if (k > 0xFFFE) { bt.clear(); pt.clear(); return; }   // (never on road graphs: k <= ~2k)
+      for (int j0 = 0; j0 < k; j0 += 64) bt.push_back(CustTask{z, ROW_FINAL, (uint16_t)j0});
+      for (int i = 0; i + 1 < k; ++i)
+        for (int j0 = i + 1; j0 < k; j0 += 64) bt.push_back(CustTask{z, (uint16_t)i, (uint16_t)j0});
+    }
+    btask_ptr_[h + 1] = (int64_t)bt.size();
+  }
+  ptask_ptr_.assign(T_.max_depth + 2, 0);
+  for (int d = 0; d <= T_.max_depth; ++d) {
+    for (int64_t q = T_.dlev_ptr[d]; q < T_.dlev_ptr[d + 1]; ++q) {
+      const int x = T_.dlev_nodes[q];
+      const int k = (int)(T_.up_ptr[x + 1] - T_.up_ptr[x]);
+      if (k < 2) continue;
+      for (int a = 0; a < k; ++a)
+        for (int c0 = 0; c0 < k; c0 += 64) pt.push_back(CustTask{x, (uint16_t)a, (uint16_t)c0});
+    }
+    ptask_ptr_[d + 1] = (int64_t)pt.size();
+  }
+  (void)N;
+  CustTask *db = nullptr, *dp = nullptr;
+  const bool ok = up_copy(db, bt.data(), bt.size()) == hipSuccess && up_copy(dp, pt.data(), pt.size()) == hipSuccess;
+  d_btask = db;
+  d_ptask = dp;
+  if (!ok) {
+    (void)hipGetLastError();
+    dfree(d_btask);
+    dfree(d_ptask);
+    return;
+  }
+  n_btask_ = (int64_t)bt.size();
+  n_ptask_ = (int64_t)pt.size();
 }
 
 CchGpu::~CchGpu() {
@@ -1100,6 +1287,8 @@ CchGpu::~CchGpu() {
   dfree(d_aofs);
   dfree(d_tofs);
   dfree(d_tri);
+  dfree(d_btask);
+  dfree(d_ptask);
   dfree(d_up64);
   dfree(d_dn64);
   dfree(d_pup);
@@ -1185,8 +1374,22 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   } evs;
   hipEvent_t* ev = evs.e;
   if (ev[0]) (void)hipEventRecord(ev[0], s);
-  // basic, bottom-up by height
-  for (int h = 0; h <= T_.max_height && e == hipSuccess; ++h) {
+  const bool tasks = d_btask != nullptr && d_ptask != nullptr && d_tri != nullptr;
+  // basic, bottom-up by height: the task kernel when the task tables exist
+  for (int h = 0; h <= T_.max_height && e == hipSuccess && tasks; ++h) {
+    const long long nt = btask_ptr_[h + 1] - btask_ptr_[h];
+    if (nt <= 0) continue;
+    if (skip)
+      hipLaunchKernelGGL(basic_task_kernel<true>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
+                         (const CustTask*)d_btask + btask_ptr_[h], nt, d_up_ptr, d_up_head, d_tofs, d_tri, d_up64,
+                         d_dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
+    else
+      hipLaunchKernelGGL(basic_task_kernel<false>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
+                         (const CustTask*)d_btask + btask_ptr_[h], nt, d_up_ptr, d_up_head, d_tofs, d_tri, d_up64,
+                         d_dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
+    ck(hipGetLastError());
+  }
+  for (int h = 0; h <= T_.max_height && e == hipSuccess && !tasks; ++h) {
     LevelArgs L{d_up_ptr, d_up_head, d_hnodes, d_bofs, (int)T_.hlev_ptr[h], (int)T_.hlev_ptr[h + 1], 0, 0, d_tofs, d_tri};
     if (L.lo >= L.hi) continue;
     L.base = bofs_[L.lo];
@@ -1209,7 +1412,15 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     const char* v = std::getenv("ROUTEST_CCH_PERFECT");
     return !(v && std::string(v) == "push");
   }();
-  for (int d = 0; d <= T_.max_depth && e == hipSuccess && pull && d_tri != nullptr; ++d) {
+  for (int d = 0; d <= T_.max_depth && e == hipSuccess && tasks; ++d) {
+    const long long nt = ptask_ptr_[d + 1] - ptask_ptr_[d];
+    if (nt <= 0) continue;
+    hipLaunchKernelGGL(perfect_task_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
+                       (const CustTask*)d_ptask + ptask_ptr_[d], nt, d_up_ptr, d_up_head, d_tofs, d_tri, d_up64, d_dn64,
+                       d_pup, d_pdn);
+    ck(hipGetLastError());
+  }
+  for (int d = 0; d <= T_.max_depth && e == hipSuccess && !tasks && pull && d_tri != nullptr; ++d) {
     const int lo = (int)T_.dlev_ptr[d], hi = (int)T_.dlev_ptr[d + 1];
     if (lo >= hi) continue;
     PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri};
@@ -1223,7 +1434,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
                          d_pup, d_pdn);
     ck(hipGetLastError());
   }
-  for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(pull && d_tri != nullptr); ++d) {
+  for (int d = 0; d <= T_.max_depth && e == hipSuccess && !tasks && !(pull && d_tri != nullptr); ++d) {
     LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0, d_tofs, d_tri};
     if (L.lo >= L.hi) continue;
     L.base = pofs_[L.lo];
@@ -1523,7 +1734,8 @@ hipError_t CchGpu::legs_from_matrix(const CchMetricDev& m, const int* d_src, con
   hipError_t e = sc.ensure(0, (size_t)Q, S, MAX_ARCS);
   if (e != hipSuccess) return e;
   if ((size_t)Q > sc.pj_cap) {
-    dfree(sc.pj);
+    if (sc.pj) sc.old.push_back((void*)sc.pj);
+    sc.pj = nullptr;
     const size_t cap = std::max((size_t)Q, sc.pj_cap * 3 / 2);
     if ((e = dmalloc(sc.pj, 2 * cap)) != hipSuccess) return e;
     sc.pj_cap = cap;

@@ -89,6 +89,8 @@ class PyCchGpu {
     d["cached_metrics"] = g_->cached();
     d["triangle_table"] = g_->has_triangle_table();
     d["triangles"] = g_->triangles();
+    d["basic_tasks"] = g_->basic_tasks();
+    d["perfect_tasks"] = g_->perfect_tasks();
     d["cache_capacity"] = g_->capacity();
     d["cache_gb"] = g_->cache_gb();
     d["metric_bytes"] = g_->metric_bytes();

@@ -70,6 +70,7 @@ struct CchScratch {
   uint64_t chain_tag = 0;          // the matrix() call whose chains are in dist/pred/node (0: none)
   int chain_nm = 0, chain_r = 0;
   int device = 0;
+  std::vector<void*> old;          // outgrown buffers, freed with the scratch
   ~CchScratch();
   hipError_t ensure(size_t jobs, size_t pairs, int stride, int max_arcs);
 };
@@ -96,6 +97,8 @@ class CchGpu {
   int stride() const { return T_.max_depth + 1; }
   bool has_triangle_table() const { return d_tri != nullptr; }
   int64_t triangles() const { return n_tri; }
+  int64_t basic_tasks() const { return n_btask_; }
+  int64_t perfect_tasks() const { return n_ptask_; }
 
   // ETA model used for context costs (the fused K1+K2 kernel's 32x32 blob on this device)
   void set_eta(const void* blob, int H, const NormParams& np, int variant, int num_cus);
@@ -176,6 +179,12 @@ class CchGpu {
   int64_t* d_tofs = nullptr;
   int32_t* d_tri = nullptr;
   int64_t n_tri = 0;
+  // task tables of the customization (csrc/cch.hip build_tasks): 8-byte wave tasks in level order
+  void build_tasks();
+  void* d_btask = nullptr;
+  void* d_ptask = nullptr;
+  std::vector<int64_t> btask_ptr_, ptask_ptr_;
+  int64_t n_btask_ = 0, n_ptask_ = 0;
   // customization temporaries (one customization at a time: mu_cust_)
   unsigned long long *d_up64 = nullptr, *d_dn64 = nullptr;
   uint32_t *d_pup = nullptr, *d_pdn = nullptr;

@@ -71,37 +71,49 @@ __global__ __launch_bounds__(64) void route_hang_kernel(const int* release, long
     __builtin_amdgcn_s_sleep(127);
 }
 
+// Growable buffers of the service's flushes.  A buffer outgrown while serving is not freed at
+// once: hipFree / hipHostFree wait for the whole device, i.e. for every other service's and
+// reactor's kernels on this GPU (a hung one included) — it is kept until the service ends (the
+// geometric growth bounds the extra memory by the final size).
 template <class T>
 struct DevBuf {
   T* d = nullptr;
   size_t n = 0;
+  std::vector<T*> old;
   hipError_t need(size_t k) {
     if (k <= n) return hipSuccess;
     const size_t m = std::max(k, n * 3 / 2);
-    if (d) (void)hipFree(d);
+    if (d) old.push_back(d);
     d = nullptr;
     n = 0;
     hipError_t e = hipMalloc((void**)&d, m * sizeof(T));
     if (e == hipSuccess) n = m;
     return e;
   }
-  ~DevBuf() { if (d) (void)hipFree(d); }
+  ~DevBuf() {
+    if (d) (void)hipFree(d);
+    for (T* p : old) (void)hipFree(p);
+  }
 };
 template <class T>
 struct HostBuf {
   T* h = nullptr;
   size_t n = 0;
+  std::vector<T*> old;
   hipError_t need(size_t k) {
     if (k <= n) return hipSuccess;
     const size_t m = std::max(k, n * 3 / 2);
-    if (h) (void)hipHostFree(h);
+    if (h) old.push_back(h);
     h = nullptr;
     n = 0;
     hipError_t e = hipHostMalloc((void**)&h, m * sizeof(T), hipHostMallocDefault);
     if (e == hipSuccess) n = m;
     return e;
   }
-  ~HostBuf() { if (h) (void)hipHostFree(h); }
+  ~HostBuf() {
+    if (h) (void)hipHostFree(h);
+    for (T* p : old) (void)hipHostFree(p);
+  }
 };
 
 inline rtc::Stamp local_now() {
