@@ -293,10 +293,38 @@ __global__ __launch_bounds__(256) void perfect_pull_wave_kernel(PullArgs P, cons
   const int aa = a0 + ia;
   const int y = P.up_head[aa];
   float bu = F_INF, bd = F_INF;
-  for (int ic = lane; ic < k; ic += 64) {
-    if (ic == ia) continue;
-    const int ac = a0 + ic;
-    pull_cand(P, x, k, a0, ia, ic, wof(up[ac]), wof(dn[ac]), pup, pdn, y, P.up_head[ac], bu, bd);
+  // four 64-wide chunks of candidates per step, every stage's loads issued together (the serial
+  // tri -> weight chain of a high-degree node's ~22 chunks was the kernel's latency)
+  const long long tb = P.tofs[x];
+  for (int c0 = 0; c0 < k; c0 += 256) {
+    int azy[4], z[4];
+    unsigned long long wu[4], wd[4];
+    bool ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ic = c0 + 64 * u + lane;
+      ok[u] = ic < k && ic != ia;
+      const int i = ic < ia ? ic : ia, j = ic < ia ? ia : ic;
+      azy[u] = ok[u] ? P.tri[tb + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)] : 0;
+      z[u] = ok[u] ? P.up_head[a0 + ic] : 0;
+      wu[u] = ok[u] ? up[a0 + ic] : 0ull;
+      wd[u] = ok[u] ? dn[a0 + ic] : 0ull;
+    }
+    uint32_t gu[4], gd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      gu[u] = ok[u] ? pup[azy[u]] : 0u;
+      gd[u] = ok[u] ? pdn[azy[u]] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!ok[u]) continue;
+      const float zy = __uint_as_float(z[u] < y ? gu[u] : gd[u]);
+      const float yz = __uint_as_float(z[u] < y ? gd[u] : gu[u]);
+      const float cu = wof(wu[u]) + zy, cd = yz + wof(wd[u]);
+      bu = cu < bu ? cu : bu;
+      bd = cd < bd ? cd : bd;
+    }
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
@@ -474,34 +502,57 @@ __device__ __forceinline__ bool kept(uint32_t p, unsigned long long b) {
   return __uint_as_float(p) < F_INF && p == (uint32_t)(b >> 32);
 }
 
-__global__ void prune_count_kernel(const int32_t* __restrict__ up_ptr, const uint32_t* __restrict__ pup,
-                                   const uint32_t* __restrict__ pdn, const unsigned long long* __restrict__ up,
-                                   const unsigned long long* __restrict__ dn, int N, int32_t* __restrict__ fcnt,
-                                   int32_t* __restrict__ bcnt) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+// Pruning, one wave per node: lanes over its arcs (coalesced), ballot counts and in-order
+// positions (round 5; a thread per node walking its arcs serially took 1.5 ms per customization
+// on the 100k graph)
+__global__ __launch_bounds__(256) void prune_count_wave_kernel(const int32_t* __restrict__ up_ptr,
+                                                               const uint32_t* __restrict__ pup,
+                                                               const uint32_t* __restrict__ pdn,
+                                                               const unsigned long long* __restrict__ up,
+                                                               const unsigned long long* __restrict__ dn, int N,
+                                                               int32_t* __restrict__ fcnt, int32_t* __restrict__ bcnt) {
+  const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (x >= N) return;
   int kf = 0, kb = 0;
-  for (int a = up_ptr[x]; a < up_ptr[x + 1]; ++a) {
+  for (int a = up_ptr[x] + lane; a < up_ptr[x + 1]; a += 64) {
     kf += kept(pup[a], up[a]);
     kb += kept(pdn[a], dn[a]);
   }
-  fcnt[x] = kf;
-  bcnt[x] = kb;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    kf += __shfl_xor(kf, o);
+    kb += __shfl_xor(kb, o);
+  }
+  if (lane == 0) {
+    fcnt[x] = kf;
+    bcnt[x] = kb;
+  }
 }
 
-__global__ void prune_scatter_kernel(const int32_t* __restrict__ up_ptr, const int32_t* __restrict__ up_head,
-                                     const int32_t* __restrict__ depth, const uint32_t* __restrict__ pup,
-                                     const uint32_t* __restrict__ pdn, const unsigned long long* __restrict__ up,
-                                     const unsigned long long* __restrict__ dn, int N, const int32_t* __restrict__ f_ptr,
-                                     const int32_t* __restrict__ b_ptr, int4* __restrict__ f_rec,
-                                     int4* __restrict__ b_rec) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void prune_scatter_wave_kernel(
+    const int32_t* __restrict__ up_ptr, const int32_t* __restrict__ up_head, const int32_t* __restrict__ depth,
+    const uint32_t* __restrict__ pup, const uint32_t* __restrict__ pdn, const unsigned long long* __restrict__ up,
+    const unsigned long long* __restrict__ dn, int N, const int32_t* __restrict__ f_ptr, const int32_t* __restrict__ b_ptr,
+    int4* __restrict__ f_rec, int4* __restrict__ b_rec) {
+  const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (x >= N) return;
   int kf = f_ptr[x], kb = b_ptr[x];
-  for (int a = up_ptr[x]; a < up_ptr[x + 1]; ++a) {
-    const int hd = depth[up_head[a]];
-    if (kept(pup[a], up[a])) f_rec[kf++] = make_int4((int)pup[a], hd, a, 0);
-    if (kept(pdn[a], dn[a])) b_rec[kb++] = make_int4((int)pdn[a], hd, a, 0);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int a0 = up_ptr[x]; a0 < up_ptr[x + 1]; a0 += 64) {
+    const int a = a0 + lane;
+    const bool in = a < up_ptr[x + 1];
+    const bool f = in && kept(pup[a], up[a]);
+    const bool b = in && kept(pdn[a], dn[a]);
+    const unsigned long long mf = __ballot(f), mb = __ballot(b);
+    if (f || b) {
+      const int hd = depth[up_head[a]];        // records in arc order, like the serial kernel
+      if (f) f_rec[kf + __popcll(mf & below)] = make_int4((int)pup[a], hd, a, 0);
+      if (b) b_rec[kb + __popcll(mb & below)] = make_int4((int)pdn[a], hd, a, 0);
+    }
+    kf += __popcll(mf);
+    kb += __popcll(mb);
   }
 }
 
@@ -1228,7 +1279,9 @@ void CchGpu::build_tasks() {
     btask_ptr_[h + 1] = (int64_t)bt.size();
   }
   ptask_ptr_.assign(T_.max_depth + 2, 0);
-  for (int d = 0; d <= T_.max_depth; ++d) {
+  const char* pv = std::getenv("ROUTEST_CCH_PERFECT");
+  const bool want_p = pv && std::string(pv) == "tasks";       // (the pull kernels need no table)
+  for (int d = 0; d <= T_.max_depth && want_p; ++d) {
     for (int64_t q = T_.dlev_ptr[d]; q < T_.dlev_ptr[d + 1]; ++q) {
       const int x = T_.dlev_nodes[q];
       const int k = (int)(T_.up_ptr[x + 1] - T_.up_ptr[x]);
@@ -1374,7 +1427,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   } evs;
   hipEvent_t* ev = evs.e;
   if (ev[0]) (void)hipEventRecord(ev[0], s);
-  const bool tasks = d_btask != nullptr && d_ptask != nullptr && d_tri != nullptr;
+  const bool tasks = d_btask != nullptr && d_tri != nullptr;
   // basic, bottom-up by height: the task kernel when the task tables exist
   for (int h = 0; h <= T_.max_height && e == hipSuccess && tasks; ++h) {
     const long long nt = btask_ptr_[h + 1] - btask_ptr_[h];
@@ -1412,7 +1465,14 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     const char* v = std::getenv("ROUTEST_CCH_PERFECT");
     return !(v && std::string(v) == "push");
   }();
-  for (int d = 0; d <= T_.max_depth && e == hipSuccess && tasks; ++d) {
+  // perfect: the pull kernels (measured faster than the perfect task kernel: 12.0 vs 15.3 ms on
+  // the 100k graph, 227 vs 351 ms on the 1M city; ROUTEST_CCH_PERFECT=tasks selects it)
+  static const bool env_ptasks = [] {
+    const char* v = std::getenv("ROUTEST_CCH_PERFECT");
+    return v && std::string(v) == "tasks";
+  }();
+  const bool ptasks = env_ptasks && d_ptask != nullptr;
+  for (int d = 0; d <= T_.max_depth && e == hipSuccess && tasks && ptasks; ++d) {
     const long long nt = ptask_ptr_[d + 1] - ptask_ptr_[d];
     if (nt <= 0) continue;
     hipLaunchKernelGGL(perfect_task_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
@@ -1420,7 +1480,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
                        d_pup, d_pdn);
     ck(hipGetLastError());
   }
-  for (int d = 0; d <= T_.max_depth && e == hipSuccess && !tasks && pull && d_tri != nullptr; ++d) {
+  for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && pull && d_tri != nullptr; ++d) {
     const int lo = (int)T_.dlev_ptr[d], hi = (int)T_.dlev_ptr[d + 1];
     if (lo >= hi) continue;
     PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri};
@@ -1434,7 +1494,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
                          d_pup, d_pdn);
     ck(hipGetLastError());
   }
-  for (int d = 0; d <= T_.max_depth && e == hipSuccess && !tasks && !(pull && d_tri != nullptr); ++d) {
+  for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && !(pull && d_tri != nullptr); ++d) {
     LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0, d_tofs, d_tri};
     if (L.lo >= L.hi) continue;
     L.base = pofs_[L.lo];
@@ -1450,8 +1510,8 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   }
   if (ev[2]) (void)hipEventRecord(ev[2], s);
   // prune + compact
-  hipLaunchKernelGGL(prune_count_kernel, dim3(blocks_for(N, 256)), dim3(256), 0, s, d_up_ptr, d_pup, d_pdn, d_up64,
-                     d_dn64, N, d_fcnt, d_bcnt);
+  hipLaunchKernelGGL(prune_count_wave_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, d_up_ptr, d_pup, d_pdn,
+                     d_up64, d_dn64, N, d_fcnt, d_bcnt);
   ck(hipGetLastError());
   ck(hipMemsetAsync(m.f_ptr, 0, sizeof(int32_t), s));
   ck(hipMemsetAsync(m.b_ptr, 0, sizeof(int32_t), s));
@@ -1475,8 +1535,8 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   m.kept_f = tot[0];
   m.kept_b = tot[1];
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(prune_scatter_kernel, dim3(blocks_for(N, 256)), dim3(256), 0, s, d_up_ptr, d_up_head, d_depth,
-                     d_pup, d_pdn, d_up64, d_dn64, N, m.f_ptr, m.b_ptr, m.f_rec, m.b_rec);
+  hipLaunchKernelGGL(prune_scatter_wave_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, d_up_ptr, d_up_head,
+                     d_depth, d_pup, d_pdn, d_up64, d_dn64, N, m.f_ptr, m.b_ptr, m.f_rec, m.b_rec);
   ck(hipGetLastError());
   if (ev[3]) (void)hipEventRecord(ev[3], s);
   ck(hipStreamSynchronize(s));
