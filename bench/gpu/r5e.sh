@@ -19,4 +19,5 @@ for G in "$G1" "$G2" "$G3"; do
 done
 cd $ROOT
 timeout -k 10 170 python -u -m pytest -x -v -s --timeout 160 --timeout-method thread tests/test_native_lifecycle_gpu.py -k hung > $O/watchdog.log 2>&1; stop $?
+timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1; stop $?
 echo done

@@ -159,3 +159,17 @@ def test_next_hour_is_prefetched(monkeypatch):
         assert st.front.stats()["route_ctx_prefetched"] >= 2
     finally:
         st.close()
+
+
+def test_lru_is_sized_from_an_hbm_budget(stack):
+    """The metric LRU holds as many contexts as fit ROUTEST_CCH_CACHE_GB (default 48 GB), derived
+    from the device bytes of a built metric — not a fixed count."""
+    g, prov, st = stack
+    r = prov.router(torch.device("cuda", 0))
+    s = r.stats()
+    assert s["cache_gb"] == 48.0 and s["metric_bytes"] > 0, s
+    assert s["cache_capacity"] == max(4, int(48.0 * 2 ** 30 // s["metric_bytes"])), s
+    r.gpu.set_cache_gb(1.0)
+    s1 = r.stats()
+    assert s1["cache_capacity"] == max(4, int(2 ** 30 // s["metric_bytes"])) and s1["cached_metrics"] <= s1["cache_capacity"]
+    r.gpu.set_cache_gb(48.0)
