@@ -317,6 +317,7 @@ class Reactor {
         hipHostGetDevicePointer(&d_rec8_, h_rec8_, 0) != hipSuccess ||
         hipHostGetDevicePointer((void**)&d_out_, h_out_, 0) != hipSuccess)
       return;
+    (void)alloc_round(spare_);         // the latency watchdog's spare round buffers
     streams_[cfg_.device] = stream_;
 
     epoll_event evs[256];
@@ -362,6 +363,8 @@ class Reactor {
       (void)hipEventDestroy(kv.second);
     }
     reap_retired(true);
+    for (void* p : {(void*)spare_.rec, (void*)spare_.rec8, (void*)spare_.out})
+      if (p) (void)hipHostFree(p);
     (void)hipSetDevice(cfg_.device);
   }
 
@@ -394,7 +397,7 @@ class Reactor {
   std::vector<Retired> retired_;
   rth::HistoryDb hdb_;                                  // this reactor's connection to the store
   bool hdb_tried_ = false;
-  std::unordered_map<int, ModelWs> ws_;                 // per device model workspace
+  std::unordered_map<int, ModelWs> ws_;                 // per stream key (device, or the gpu_hang stream)
   uint64_t next_gen_ = 1;
   std::unordered_map<int, Conn> conns_;
   std::unordered_map<int, int> up2c_;  // upstream fd -> client fd
@@ -1055,9 +1058,15 @@ class Reactor {
       if (q == hipErrorNotReady) { ++i; continue; }
       (void)hipEventDestroy(r.ev);
       (void)hipStreamDestroy(r.st);
-      (void)hipHostFree(r.rec);
-      (void)hipHostFree(r.rec8);
-      (void)hipHostFree(r.out);
+      if (spare_.rec == nullptr && !all) {           // the drained set is the next spare
+        spare_.rec = (EtaRecord*)r.rec;
+        spare_.rec8 = (rtc::Wire8*)r.rec8;
+        spare_.out = (float*)r.out;
+      } else {
+        (void)hipHostFree(r.rec);
+        (void)hipHostFree(r.rec8);
+        (void)hipHostFree(r.out);
+      }
       if (r.ws) (void)hipFree(r.ws);
       retired_[i] = std::move(retired_.back());
       retired_.pop_back();
@@ -1068,24 +1077,41 @@ class Reactor {
   // a round on `dev` missed its deadline: its kernel may still run and write this reactor's
   // buffers, so they, the stream and the workspace are retired and the round continues on fresh
   // ones (records copied over)
-  bool retire_round(int dev, int skey, hipStream_t st, hipEvent_t ev, std::shared_ptr<const NativeModel> m) {
+  // the round buffers (pinned, mapped): the spare set is allocated up front, so an abandoned round
+  // swaps to it without allocating while a kernel may hang on the GPU; a drained retired set
+  // becomes the next spare
+  struct RoundBufs {
+    EtaRecord* rec = nullptr;
+    rtc::Wire8* rec8 = nullptr;
+    float* out = nullptr;
+  };
+  RoundBufs spare_;
+  bool alloc_round(RoundBufs& b) {
     const unsigned fl = hipHostMallocMapped | hipHostMallocPortable;
-    EtaRecord* nr = nullptr;
-    rtc::Wire8* n8 = nullptr;
-    float* no = nullptr;
+    if (hipHostMalloc((void**)&b.rec, (size_t)cap_ * 16, fl) == hipSuccess &&
+        hipHostMalloc((void**)&b.rec8, (size_t)cap_ * 8, fl) == hipSuccess &&
+        hipHostMalloc((void**)&b.out, (size_t)cap_ * 4, fl) == hipSuccess)
+      return true;
+    for (void* p : {(void*)b.rec, (void*)b.rec8, (void*)b.out})
+      if (p) (void)hipHostFree(p);
+    b = RoundBufs();
+    return false;
+  }
+
+  bool retire_round(int dev, int skey, hipStream_t st, hipEvent_t ev, std::shared_ptr<const NativeModel> m) {
+    if (spare_.rec == nullptr && !alloc_round(spare_)) return false;   // (the slot is quarantined anyway)
+    EtaRecord* nr = spare_.rec;
+    rtc::Wire8* n8 = spare_.rec8;
+    float* no = spare_.out;
     void *dr = nullptr, *d8 = nullptr;
     float* dout = nullptr;
-    if (hipHostMalloc((void**)&nr, (size_t)cap_ * 16, fl) != hipSuccess ||
-        hipHostMalloc((void**)&n8, (size_t)cap_ * 8, fl) != hipSuccess ||
-        hipHostMalloc((void**)&no, (size_t)cap_ * 4, fl) != hipSuccess || hipHostGetDevicePointer(&dr, nr, 0) != hipSuccess ||
-        hipHostGetDevicePointer(&d8, n8, 0) != hipSuccess || hipHostGetDevicePointer((void**)&dout, no, 0) != hipSuccess) {
-      for (void* p : {(void*)nr, (void*)n8, (void*)no})
-        if (p) (void)hipHostFree(p);
-      return false;                    // keep the old buffers (the slot is quarantined anyway)
-    }
+    if (hipHostGetDevicePointer(&dr, nr, 0) != hipSuccess || hipHostGetDevicePointer(&d8, n8, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&dout, no, 0) != hipSuccess)
+      return false;
+    spare_ = RoundBufs();
     std::memcpy(nr, h_rec_, nrec_ * sizeof(EtaRecord));
     Retired r{dev, ev, st, h_rec_, h_rec8_, h_out_, nullptr, std::move(m)};
-    ModelWs& w = ws_[dev];
+    ModelWs& w = ws_[skey];
     r.ws = w.p;
     w.p = nullptr;
     w.bytes = 0;
@@ -1142,7 +1168,7 @@ class Reactor {
     // (csrc/runtime/rt_core.h pack_wire8), else 16-byte
     const bool w8 = m.takes_wire8() && rtc::pack_wire8(h_rec_, nrec_, h_rec8_);
     if (w8) st_.wire8.fetch_add(1, std::memory_order_relaxed);
-    hipError_t e = m.predict(w8 ? d_rec8_ : d_rec_, w8 ? 8 : 16, d_out_, (int)nrec_, st, ws_[dev]);
+    hipError_t e = m.predict(w8 ? d_rec8_ : d_rec_, w8 ? 8 : 16, d_out_, (int)nrec_, st, ws_[skey]);
     if (e == hipSuccess) e = wait_deadline(st, ev, sh.deadline_ms);
     if (e == hipErrorLaunchTimeOut) {
       sh.timed_out(g);

@@ -478,6 +478,8 @@ struct RouteService::Impl {
     if (const char* v = std::getenv("ROUTEST_CCH_PREFETCH_MIN")) prefetch_min = std::atoi(v);
     if (cfg.cch != nullptr && cfg.cch_contexts && async_ctx)
       listener = cfg.cch->add_build_listener([this](uint64_t key, bool ok) { on_built(key, ok); });
+    if (std::getenv("ROUTEST_ROUTE_PREWARM") == nullptr || std::string(std::getenv("ROUTEST_ROUTE_PREWARM")) != "0")
+      prewarm();
     th_asm = std::thread([this] { asm_loop(); });
     while (true) {
       auto* b = new Batch();
@@ -730,6 +732,35 @@ struct RouteService::Impl {
       hc_lru.pop_back();
     }
     return v;
+  }
+
+  // Buffers sized up front for a full flush of dashboard-sized requests (batch_max requests of up to
+  // 10 stops, MAX_STOPS of the UI): growing one mid-serving allocates while other GPU work is in
+  // flight (a flush handed over from another GPU doubles this service's flush size at once).
+  void prewarm() {
+    const size_t R = (size_t)std::max(1, cfg.batch_max), NM = 11, RN = R * NM, Q = RN;
+    const size_t MP = (size_t)std::max(1, cfg.max_path);
+    bool ok = !(h_lat.need(RN) || h_lon.need(RN) || h_dem.need(RN) || h_npts.need(R) || h_cap.need(R) ||
+                h_maxd.need(R) || h_visit.need(RN) || h_trip.need(RN) || h_ntrips.need(R) || h_status.need(R) ||
+                h_row0.need(RN) || d_lat.need(RN) || d_lon.need(RN) || d_dem.need(RN) || d_npts.need(R) ||
+                d_cap.need(R) || d_maxd.need(R) || d_D.need(RN * NM) || d_visit.need(RN) || d_trip.need(RN) ||
+                d_ntrips.need(R) || d_status.need(R));
+    ok = ok && !(h_src.need(Q) || h_dst.need(Q) || h_len.need(Q) || h_st.need(Q) || h_cost.need(Q) ||
+                 h_off.need(Q) || d_src.need(Q) || d_dst.need(Q) || d_len.need(Q) || d_st.need(Q) ||
+                 d_cost.need(Q) || d_off.need(Q) || d_path.need(Q * MP) || h_flat.need(Q * 256) ||
+                 d_flat.need(Q * 256) || h_rec.need(R) || h_eta.need(R) || d_rec.need(R) || d_eta.need(R));
+    if (cfg.cch != nullptr) {
+      ok = ok && !(h_pts.need(RN) || h_npts2.need(R) || d_pts.need(RN) || d_npts2.need(R) || d_msec.need(RN * NM) ||
+                   d_mmet.need(RN * NM) || h_met.need(Q) || d_met.need(Q) || d_edge.need(Q * MP) ||
+                   h_flat_e.need(Q * 256) || d_flat_e.need(Q * 256) || h_lr.need(Q) || h_li.need(Q) || h_lj.need(Q) ||
+                   d_lr.need(Q) || d_li.need(Q) || d_lj.need(Q));
+      const int S = cfg.cch->stride();
+      if (gsc.empty()) gsc.push_back(std::make_unique<CchScratch>());
+      gsc[0]->device = cfg.device;
+      ok = ok && gsc[0]->ensure(RN * 2, std::max(Q, (RN * NM * 2 + CchGpu::MAX_ARCS - 1) / CchGpu::MAX_ARCS + 1), S,
+                                CchGpu::MAX_ARCS) == hipSuccess;
+    }
+    if (!ok) (void)hipGetLastError();       // best effort: the flushes grow what is missing
   }
 
   // a context's background build finished: its waiting jobs go back to the head of the queue
