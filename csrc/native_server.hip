@@ -319,6 +319,16 @@ class Reactor {
       return;
     (void)alloc_round(spare_);         // the latency watchdog's spare round buffers
     streams_[cfg_.device] = stream_;
+    // ROUTEST_HANG_ARM=1 (the watchdog rehearsal): the gpu_hang hook's isolated streams exist from
+    // the start, so arming the fault later creates no hardware queue
+    if (const char* v = std::getenv("ROUTEST_HANG_ARM"))
+      if (std::string(v) == "1")
+        for (int g = 0; g < cfg_.sh->slots(); ++g) {
+          hipStream_t hs;
+          if (hipSetDevice(cfg_.sh->devices[g]) == hipSuccess && isolated_stream(cfg_.sh->devices[g], &hs) == hipSuccess)
+            streams_[-1 - g] = hs;
+        }
+    (void)hipSetDevice(cfg_.device);
 
     epoll_event evs[256];
     while (!stop_.load(std::memory_order_relaxed) || inflight_ > 0) {
@@ -1057,7 +1067,7 @@ class Reactor {
       }
       if (q == hipErrorNotReady) { ++i; continue; }
       (void)hipEventDestroy(r.ev);
-      (void)hipStreamDestroy(r.st);
+      if (r.st) (void)hipStreamDestroy(r.st);
       if (spare_.rec == nullptr && !all) {           // the drained set is the next spare
         spare_.rec = (EtaRecord*)r.rec;
         spare_.rec8 = (rtc::Wire8*)r.rec8;
@@ -1110,13 +1120,16 @@ class Reactor {
       return false;
     spare_ = RoundBufs();
     std::memcpy(nr, h_rec_, nrec_ * sizeof(EtaRecord));
-    Retired r{dev, ev, st, h_rec_, h_rec8_, h_out_, nullptr, std::move(m)};
+    // an isolated (gpu_hang) stream is kept and reused: creating another hardware queue while a
+    // kernel hangs on one can wait for it
+    const bool keep_stream = skey < 0;
+    Retired r{dev, ev, keep_stream ? nullptr : st, h_rec_, h_rec8_, h_out_, nullptr, std::move(m)};
     ModelWs& w = ws_[skey];
     r.ws = w.p;
     w.p = nullptr;
     w.bytes = 0;
     retired_.push_back(std::move(r));
-    streams_.erase(skey);
+    if (!keep_stream) streams_.erase(skey);
     events_.erase(skey);
     h_rec_ = nr;
     h_rec8_ = n8;

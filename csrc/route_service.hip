@@ -480,6 +480,8 @@ struct RouteService::Impl {
       listener = cfg.cch->add_build_listener([this](uint64_t key, bool ok) { on_built(key, ok); });
     if (std::getenv("ROUTEST_ROUTE_PREWARM") == nullptr || std::string(std::getenv("ROUTEST_ROUTE_PREWARM")) != "0")
       prewarm();
+    if (const char* v = std::getenv("ROUTEST_HANG_ARM"))      // the watchdog rehearsal: see native_server.hip
+      if (std::string(v) == "1" && isolated_stream(cfg.device, &hang_stream) != hipSuccess) hang_stream = nullptr;
     th_asm = std::thread([this] { asm_loop(); });
     while (true) {
       auto* b = new Batch();
@@ -516,10 +518,7 @@ struct RouteService::Impl {
         }
       }
       gpu_stage(*b);
-      if (stream != main_stream) {
-        if (broken.load()) hang_stream = nullptr;      // still busy: a fresh one next time
-        stream = main_stream;
-      }
+      stream = main_stream;         // (the hang stream is reused once drained: see drained())
       if (b->failed) {              // a GPU error or the deadline: another GPU's service answers
         hand_off(b->jobs);
         delete b;

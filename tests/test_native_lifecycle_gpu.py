@@ -180,7 +180,8 @@ def test_hung_gpu_slot_watchdog_and_route_failover():
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, GPU_MAX_HW_QUEUES="32", ROUTEST_GPU_DEADLINE_MS="100", ROUTEST_ROUTE_DEADLINE_MS="300",
-               ROUTEST_PERSIST_IDLE_MS="0", ROUTEST_QUARANTINE_PROBE_MS="60000")
+               ROUTEST_PERSIST_IDLE_MS="0", ROUTEST_QUARANTINE_PROBE_MS="60000",
+               ROUTEST_HANG_ARM="1")
     r = subprocess.run([sys.executable, os.path.join(root, "tests", "_watchdog_child.py")], capture_output=True,
                        text=True, timeout=240, env=env, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
