@@ -343,8 +343,7 @@ struct RouteService::Impl {
   void* db = nullptr;
   void* st_req = nullptr;
   void* st_res = nullptr;
-  void *st_begin = nullptr, *st_commit = nullptr, *st_rollback = nullptr, *st_sp = nullptr, *st_rel = nullptr,
-       *st_rb = nullptr;
+  void *st_begin = nullptr, *st_commit = nullptr, *st_rollback = nullptr, *st_undo = nullptr;
   Uuid4 uuid;
   // assembly -> persistence hand-off (group commit) and the background WAL checkpointer
   std::thread th_persist, th_ckpt;
@@ -374,13 +373,14 @@ struct RouteService::Impl {
     sql.exec(db, "PRAGMA synchronous=NORMAL", nullptr, nullptr, nullptr);
     sql.exec(db, "PRAGMA foreign_keys=ON", nullptr, nullptr, nullptr);
     sql.exec(db, "PRAGMA wal_autocheckpoint=0", nullptr, nullptr, nullptr);   // ckpt_loop checkpoints
+    sql.exec(db, "PRAGMA temp_store=MEMORY", nullptr, nullptr, nullptr);      // statement journals in RAM
     const char* q1 = "INSERT INTO route_requests(id,origin_id,stops,request_time,status,engine,vehicle_id,driver_age)"
                      " VALUES(?,?,?,?,?,?,?,?)";
     const char* q2 = "INSERT INTO route_results(id,request_id,optimized_order,total_distance,total_duration,legs,"
                      "geometry,eta_minutes_ml,eta_completion_time_ml,created_at) VALUES(?,?,?,?,?,?,?,?,?,?)";
     const std::pair<const char*, void**> stmts[] = {
         {q1, &st_req},         {q2, &st_res},          {"BEGIN", &st_begin}, {"COMMIT", &st_commit},
-        {"ROLLBACK", &st_rollback}, {"SAVEPOINT rq", &st_sp}, {"RELEASE rq", &st_rel}, {"ROLLBACK TO rq", &st_rb}};
+        {"ROLLBACK", &st_rollback}, {"DELETE FROM route_requests WHERE id=?", &st_undo}};
     bool ok = true;
     for (const auto& [text, st] : stmts) ok = ok && sql.prepare_v2(db, text, -1, st, nullptr) == rtsql::OK;
     if (!ok) {
@@ -458,7 +458,18 @@ struct RouteService::Impl {
       ok = sql.bind_null(st_res, 8) == rtsql::OK && sql.bind_null(st_res, 9) == rtsql::OK;
     }
     ok = ok && bind_text(st_res, 10, now);
-    if (!ok || sql.step(st_res) != rtsql::DONE) return "";
+    if (!ok || sql.step(st_res) != rtsql::DONE) {
+      // per-request semantics of SQLiteStore without a savepoint per request (a savepoint's
+      // statement journal copied every page the request touched: 2x the row cost): a failed
+      // result insert removes the request row it belongs to; a failed statement itself is
+      // atomic, so a failed request insert left nothing behind
+      sql.reset(st_res);
+      sql.reset(st_undo);
+      sql.clear_bindings(st_undo);
+      if (bind_text(st_undo, 1, rid)) (void)sql.step(st_undo);
+      sql.reset(st_undo);
+      return "";
+    }
     return rid;
   }
 
@@ -600,7 +611,7 @@ struct RouteService::Impl {
     }
     pcv.notify_all();
     th_persist.join();
-    for (void* st : {st_req, st_res, st_begin, st_commit, st_rollback, st_sp, st_rel, st_rb})
+    for (void* st : {st_req, st_res, st_begin, st_commit, st_rollback, st_undo})
       if (st) sql.finalize(st);
     if (db) sql.close(db);
     (void)hipStreamDestroy(stream_asm);
@@ -1664,10 +1675,7 @@ struct RouteService::Impl {
     const bool tx = step_once(st_begin);
     for (auto& g : groups)
       for (RouteJob* j : g) {
-        step_once(st_sp);
         j->request_id = persist_one(j, now);
-        if (j->request_id.empty()) step_once(st_rb);
-        step_once(st_rel);
       }
     if (tx && !step_once(st_commit)) {
       step_once(st_rollback);      // nothing of the group was stored
