@@ -132,6 +132,8 @@ struct RouteJob {
   rtr::Assembled asmb;
   float eta_min = NAN;
   std::string eta_iso, request_id;
+  std::string p_stops, p_geom;      // row texts for the persistence thread (prep_persist)
+  bool p_ok = false;
   rtc::Stamp now;
 };
 

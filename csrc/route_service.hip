@@ -139,12 +139,31 @@ inline std::string utc_now_iso() {
   return rtc::isoformat((int64_t)ts.tv_sec, ts.tv_nsec / 1000, tz);
 }
 
-struct Uuid4 {
+// Row ids of the persisted requests/results: time-ordered UUIDs (RFC 9562 version 7: 48-bit Unix
+// milliseconds, a 12-bit sequence within the millisecond, 62 random bits).  Both tables are keyed
+// by TEXT ids with B-tree indexes (and route_results by request_id too): random v4 ids dirtied one
+// random index leaf per row per index in every group commit, time-ordered ones append — the same
+// opaque 36-character ids to every client (the reference's are Postgres v4 uuids).
+struct RowId {
   std::mt19937_64 g{std::random_device{}() ^ ((uint64_t)std::random_device{}() << 32)};
+  uint64_t last_ms = 0;
+  uint32_t seq = 0;
   std::string next() {
-    uint64_t a = g(), b = g();
-    a = (a & 0xFFFFFFFFFFFF0FFFULL) | 0x0000000000004000ULL;   // version 4
-    b = (b & 0x3FFFFFFFFFFFFFFFULL) | 0x8000000000000000ULL;   // variant 10
+    uint64_t ms = (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+                      std::chrono::system_clock::now().time_since_epoch())
+                      .count();
+    if (ms <= last_ms) {                // same (or an earlier) millisecond: keep the order
+      ms = last_ms;
+      if (++seq > 0xFFF) {
+        ++ms;
+        seq = 0;
+      }
+    } else {
+      seq = (uint32_t)(g() & 0x3FF);    // a random start, room to count up in the millisecond
+    }
+    last_ms = ms;
+    const uint64_t a = (ms << 16) | 0x7000ULL | (seq & 0xFFF);                       // version 7
+    const uint64_t b = (g() & 0x3FFFFFFFFFFFFFFFULL) | 0x8000000000000000ULL;        // variant 10
     char s[37];
     std::snprintf(s, sizeof s, "%08x-%04x-%04x-%04x-%012llx", (unsigned)(a >> 32), (unsigned)((a >> 16) & 0xFFFF),
                   (unsigned)(a & 0xFFFF), (unsigned)(b >> 48), (unsigned long long)(b & 0xFFFFFFFFFFFFULL));
@@ -344,7 +363,7 @@ struct RouteService::Impl {
   void* st_req = nullptr;
   void* st_res = nullptr;
   void *st_begin = nullptr, *st_commit = nullptr, *st_rollback = nullptr, *st_undo = nullptr;
-  Uuid4 uuid;
+  RowId uuid;
   // assembly -> persistence hand-off (group commit) and the background WAL checkpointer
   std::thread th_persist, th_ckpt;
   std::mutex pmu;
@@ -417,20 +436,39 @@ struct RouteService::Impl {
   bool bind_text(void* st, int i, std::string&&) = delete;    // a temporary would dangle
 
   // store.py build_rows + SQLiteStore.persist_request_and_result for one job; "" on failure
-  std::string persist_one(RouteJob* j, const std::string& now) {
+  // the row texts of a job (store.py build_rows): stops JSON and the geometry object — built on the
+  // assembly stage's threads, so the single persistence thread (SQLite's one writer) only binds
+  // and steps; false: a meta / stops shape the Python adapter would refuse (persist fails)
+  static bool prep_persist(RouteJob* j) {
     const rtj::Value* root = j->req.root;
     const rtj::Value* meta = root->get("meta");
-    if (meta && meta->truthy() && meta->kind != rtj::Value::Obj) return "";   // .get on a non-dict
+    if (meta && meta->truthy() && meta->kind != rtj::Value::Obj) return false;   // .get on a non-dict
+    if (meta && !meta->truthy()) meta = nullptr;
+    std::string& stops = j->p_stops;
+    stops = "{\"destination_ids\":";
+    const rtj::Value* ids = meta ? meta->get("destination_ids") : nullptr;
+    if (ids && ids->truthy()) { if (!rtr::put_value(stops, *ids)) return false; }
+    else stops += "[]";
+    stops += ",\"destination_points\":";
+    if (!rtr::put_value(stops, *root->get("destination_points"))) return false;
+    stops += '}';
+    std::string& geom = j->p_geom;
+    geom.reserve(j->asmb.coords.size() + 40);
+    geom = "{\"type\":\"LineString\",\"coordinates\":";
+    geom += j->asmb.coords;
+    geom += '}';
+    j->p_ok = true;
+    return true;
+  }
+
+  std::string persist_one(RouteJob* j, const std::string& now) {
+    if (!j->p_ok) return "";
+    const rtj::Value* root = j->req.root;
+    const rtj::Value* meta = root->get("meta");
     if (meta && !meta->truthy()) meta = nullptr;
     const rtj::Value* drv = root->get("driver_details");
     if (drv && !drv->truthy()) drv = nullptr;
-    std::string stops = "{\"destination_ids\":";
-    const rtj::Value* ids = meta ? meta->get("destination_ids") : nullptr;
-    if (ids && ids->truthy()) { if (!rtr::put_value(stops, *ids)) return ""; }
-    else stops += "[]";
-    stops += ",\"destination_points\":";
-    if (!rtr::put_value(stops, *root->get("destination_points"))) return "";
-    stops += '}';
+    const std::string& stops = j->p_stops;
     const std::string rid = uuid.next();
     const rtr::Assembled& a = j->asmb;
     sql.reset(st_req);
@@ -444,9 +482,7 @@ struct RouteService::Impl {
     if (!ok || sql.step(st_req) != rtsql::DONE) return "";
     sql.reset(st_res);
     sql.clear_bindings(st_res);
-    std::string geom = "{\"type\":\"LineString\",\"coordinates\":";
-    geom += a.coords;
-    geom += '}';
+    const std::string& geom = j->p_geom;
     const std::string res_id = uuid.next();
     ok = bind_text(st_res, 1, res_id) && bind_text(st_res, 2, rid) && bind_text(st_res, 3, a.order) &&
          sql.bind_double(st_res, 4, rtr::py_round(a.dist, 2)) == rtsql::OK &&
@@ -1639,6 +1675,11 @@ struct RouteService::Impl {
     // thread's: it group-commits these with whatever else is waiting
     for (RouteJob* j : jobs)
       if (db && !j->fallback && !j->status && j->asmb.ok && !j->request_route) b.save.push_back(j);
+    t0 = now_us();
+    rtc::parallel_chunks(b.save.size(), 16, 16, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) prep_persist(b.save[i]);
+    });
+    add_t(7, t0);
   }
 
   // the response bytes of a job whose assembly (and persistence, if any) is done
