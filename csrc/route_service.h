@@ -133,6 +133,7 @@ struct RouteJob {
   float eta_min = NAN;
   std::string eta_iso, request_id;
   std::string p_stops, p_geom;      // row texts for the persistence thread (prep_persist)
+  std::string p_legs;               // legs side-file reference ("" = the assembled segments inline)
   bool p_ok = false;
   rtc::Stamp now;
 };

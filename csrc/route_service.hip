@@ -20,6 +20,9 @@
 //      (reference routes.py:119-125, best effort); WAL checkpoints run on a fourth thread;
 //   7. completed jobs go back to their reactors (eventfd wake-up), which write the bytes -- a
 //      persisted job only after its commit.
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstring>
 #include <array>
@@ -35,6 +38,7 @@
 #include <random>
 #include <memory>
 #include <thread>
+#include <tuple>
 #include <unordered_map>
 #include <unordered_set>
 
@@ -170,6 +174,47 @@ struct RowId {
     return s;
   }
 };
+
+// Append-only side file of the large route texts (store/store.py BLOB_REF): each result's legs and
+// geometry are written here by the assembly threads at a reserved offset (pwrite, in parallel) and
+// the row holds a 20-odd byte reference, so SQLite's single writer no longer moves ~30-100 KB per
+// route through its WAL.  One log per database path, shared by every GPU's route service.
+struct BlobLog {
+  int fd = -1;
+  std::atomic<long long> off{0};
+  ~BlobLog() {
+    if (fd >= 0) ::close(fd);
+  }
+  // n bytes at a fresh offset; false on an I/O error
+  bool put(const std::string& a, const std::string& b, long long& at) {
+    const long long n = (long long)(a.size() + b.size());
+    at = off.fetch_add(n);
+    for (const auto& [p, len, o] : {std::tuple<const char*, size_t, long long>{a.data(), a.size(), at},
+                                    std::tuple<const char*, size_t, long long>{b.data(), b.size(), at + (long long)a.size()}}) {
+      size_t done = 0;
+      while (done < len) {
+        const ssize_t w = ::pwrite(fd, p + done, len - done, (off_t)(o + (long long)done));
+        if (w <= 0) return false;
+        done += (size_t)w;
+      }
+    }
+    return true;
+  }
+};
+
+std::shared_ptr<BlobLog> blob_log(const std::string& db_path) {
+  static std::mutex mu;
+  static std::unordered_map<std::string, std::weak_ptr<BlobLog>> logs;
+  std::lock_guard<std::mutex> lk(mu);
+  if (auto l = logs[db_path].lock()) return l;
+  auto l = std::make_shared<BlobLog>();
+  l->fd = ::open((db_path + ".blobs").c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+  if (l->fd < 0) return nullptr;
+  const off_t end = ::lseek(l->fd, 0, SEEK_END);
+  l->off.store(end > 0 ? (long long)end : 0);
+  logs[db_path] = l;
+  return l;
+}
 
 // Exact host search for the rare leg both GPU stages gave up on (graph.py _exact_fallback):
 // Dijkstra from s stopping when t is settled.
@@ -375,8 +420,12 @@ struct RouteService::Impl {
   long long commits = 0;
   bool ck_stop = false;
 
+  std::shared_ptr<BlobLog> blobs;          // the side file of legs / geometry (nullptr: inline)
+
   void open_store() {
     if (cfg.sqlite_path.empty()) return;
+    const char* bv = std::getenv("ROUTEST_STORE_BLOBS");
+    if (!(bv && std::string(bv) == "0")) blobs = blob_log(cfg.sqlite_path);
     std::string err;
     if (!sql.load(err)) return;
     if (sql.open_v2(cfg.sqlite_path.c_str(), &db, rtsql::OPEN_READWRITE | rtsql::OPEN_URI | rtsql::OPEN_NOMUTEX,
@@ -438,8 +487,9 @@ struct RouteService::Impl {
   // store.py build_rows + SQLiteStore.persist_request_and_result for one job; "" on failure
   // the row texts of a job (store.py build_rows): stops JSON and the geometry object — built on the
   // assembly stage's threads, so the single persistence thread (SQLite's one writer) only binds
-  // and steps; false: a meta / stops shape the Python adapter would refuse (persist fails)
-  static bool prep_persist(RouteJob* j) {
+  // and steps; with the side file, legs and geometry are written there and the row gets their
+  // references.  false: a meta / stops shape the Python adapter would refuse (persist fails)
+  static bool prep_persist(RouteJob* j, BlobLog* blobs) {
     const rtj::Value* root = j->req.root;
     const rtj::Value* meta = root->get("meta");
     if (meta && meta->truthy() && meta->kind != rtj::Value::Obj) return false;   // .get on a non-dict
@@ -457,6 +507,14 @@ struct RouteService::Impl {
     geom = "{\"type\":\"LineString\",\"coordinates\":";
     geom += j->asmb.coords;
     geom += '}';
+    j->p_legs.clear();
+    long long at = 0;
+    if (blobs != nullptr && blobs->put(j->asmb.segments, geom, at)) {
+      const size_t nl = j->asmb.segments.size(), ng = geom.size();
+      // (octal: "\x01b..." would read as one hex escape)
+      j->p_legs = "\001blob:" + std::to_string(at) + ":" + std::to_string(nl);
+      geom = "\001blob:" + std::to_string(at + (long long)nl) + ":" + std::to_string(ng);
+    }
     j->p_ok = true;
     return true;
   }
@@ -486,7 +544,7 @@ struct RouteService::Impl {
     const std::string res_id = uuid.next();
     ok = bind_text(st_res, 1, res_id) && bind_text(st_res, 2, rid) && bind_text(st_res, 3, a.order) &&
          sql.bind_double(st_res, 4, rtr::py_round(a.dist, 2)) == rtsql::OK &&
-         sql.bind_double(st_res, 5, rtr::py_round(a.dur, 2)) == rtsql::OK && bind_text(st_res, 6, a.segments) &&
+         sql.bind_double(st_res, 5, rtr::py_round(a.dur, 2)) == rtsql::OK && bind_text(st_res, 6, j->p_legs.empty() ? a.segments : j->p_legs) &&
          bind_text(st_res, 7, geom);
     if (ok && !j->eta_iso.empty()) {
       ok = sql.bind_double(st_res, 8, (double)j->eta_min) == rtsql::OK && bind_text(st_res, 9, j->eta_iso);
@@ -1676,8 +1734,9 @@ struct RouteService::Impl {
     for (RouteJob* j : jobs)
       if (db && !j->fallback && !j->status && j->asmb.ok && !j->request_route) b.save.push_back(j);
     t0 = now_us();
+    BlobLog* bl = blobs.get();
     rtc::parallel_chunks(b.save.size(), 16, 16, [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) prep_persist(b.save[i]);
+      for (size_t i = lo; i < hi; ++i) prep_persist(b.save[i], bl);
     });
     add_t(7, t0);
   }
@@ -1791,11 +1850,14 @@ struct RouteService::Impl {
         seen = commits;
       }
       int log = 0, ck = 0;
+      // the side file first: a checkpointed row never reaches the disk ahead of the bytes it refers to
+      if (blobs) (void)::fdatasync(blobs->fd);
       sql.wal_checkpoint_v2(cdb, nullptr, rtsql::CHECKPOINT_PASSIVE, &log, &ck);
       std::unique_lock<std::mutex> lk(cmu);     // at most one checkpoint per 20 ms
       ccv.wait_for(lk, std::chrono::milliseconds(20), [&] { return ck_stop; });
     }
     int log = 0, ck = 0;
+    if (blobs) (void)::fdatasync(blobs->fd);
     sql.wal_checkpoint_v2(cdb, nullptr, rtsql::CHECKPOINT_PASSIVE, &log, &ck);
     sql.close(cdb);
   }

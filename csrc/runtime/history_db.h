@@ -7,6 +7,10 @@
 // float repr, INTEGER -> int, NULL -> null.  Anything unusual (a malformed stored row, an odd limit
 // string, an SQL error) returns `fallback` so the Python app answers with its own error semantics.
 #pragma once
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -39,6 +43,7 @@ class HistoryDb {
     // a checkpoint) makes the call fall back to the app after ~2 ms instead of waiting up to ~20 s
     sql_.wait_briefly(db_);
     sql_.exec(db_, "PRAGMA foreign_keys=ON", nullptr, nullptr, nullptr);
+    blob_path_ = path + ".blobs";
     return true;
   }
   void close() {
@@ -47,6 +52,8 @@ class HistoryDb {
     st_list_ = st_first_ = st_req_ = st_res_ = st_del_ = st_loc_ = nullptr;
     if (db_) sql_.close(db_);
     db_ = nullptr;
+    if (blob_fd_ >= 0) ::close(blob_fd_);
+    blob_fd_ = -1;
   }
   bool ok() const { return db_ != nullptr; }
 
@@ -250,6 +257,31 @@ class HistoryDb {
  private:
   rtsql::Api sql_;
   void* db_ = nullptr;
+  // large route texts written by the native route service live in <db>.blobs; a column holds
+  // "\x01blob:<offset>:<length>" (store/store.py BLOB_REF) — resolved here to the same bytes the app
+  // reads
+  std::string blob_path_;
+  int blob_fd_ = -1;
+  bool resolve(std::string& s) {
+    static const char kRef[] = "\001blob:";
+    if (s.compare(0, sizeof(kRef) - 1, kRef) != 0) return true;
+    char* end = nullptr;
+    const long long off = std::strtoll(s.c_str() + sizeof(kRef) - 1, &end, 10);
+    if (end == nullptr || *end != ':') return false;
+    const long long n = std::strtoll(end + 1, nullptr, 10);
+    if (off < 0 || n < 0 || n > (1ll << 31)) return false;
+    if (blob_fd_ < 0) blob_fd_ = ::open(blob_path_.c_str(), O_RDONLY | O_CLOEXEC);
+    if (blob_fd_ < 0) return false;
+    std::string out((size_t)n, '\0');
+    size_t got = 0;
+    while (got < (size_t)n) {
+      const ssize_t r = ::pread(blob_fd_, &out[got], (size_t)n - got, (off_t)(off + (long long)got));
+      if (r <= 0) return false;
+      got += (size_t)r;
+    }
+    s.swap(out);
+    return true;
+  }
   void *st_list_ = nullptr, *st_first_ = nullptr, *st_req_ = nullptr, *st_res_ = nullptr, *st_del_ = nullptr,
        *st_loc_ = nullptr;
 
@@ -318,7 +350,8 @@ class HistoryDb {
     }
     if (t != rtsql::T_TEXT) return false;
     rtj::Value v;
-    if (!parse(text(st, c), v)) return false;
+    std::string s = text(st, c);
+    if (!resolve(s) || !parse(s, v)) return false;
     if (falsy_default && !v.truthy()) {
       o += dflt;
       return true;

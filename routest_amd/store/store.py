@@ -11,6 +11,13 @@ driver_age}``, ``route_results.{geometry, eta_minutes_ml, eta_completion_time_ml
   ``origin_id: null`` for "My Current Location", which the reference's NOT NULL FK silently
   rejects — Appendix B #5), results cascade-delete with their request.
 * :class:`PostgRESTStore`: the reference's exact REST calls for a Supabase deployment.
+
+Large route texts (a result's ``legs`` and ``geometry``, ~30-100 KB of GeoJSON per route) written by
+the native route service go to an append-only side file ``<db>.blobs`` and the row holds a
+reference (``BLOB_REF`` + ``offset:length``); SQLite's single writer then commits ~300-byte rows
+instead of pushing every route through its WAL (csrc/route_service.hip).  Readers — this class and
+the native history reader (csrc/runtime/history_db.h) — resolve a reference to the same bytes.
+Deleting a request does not reclaim its bytes in the side file.
 """
 from __future__ import annotations
 
@@ -67,11 +74,15 @@ class StoreUnavailable(RuntimeError):
     pass
 
 
+#: prefix of a column value stored in the side file (never the first byte of JSON text)
+BLOB_REF = "\x01blob:"
+
+
 _EPHEMERAL: List[str] = []
 
 
 def _remove_db(path: str) -> None:
-    for suffix in ("", "-wal", "-shm"):
+    for suffix in ("", "-wal", "-shm", ".blobs"):
         try:
             os.remove(path + suffix)
         except OSError:
@@ -143,6 +154,8 @@ class SQLiteStore:
             os.close(fd)
             _EPHEMERAL.append(path)
         self.path = path
+        self.blob_path = path + ".blobs"
+        self._blob_fd: Optional[int] = None
         self._lock = threading.Lock()
         self._db = sqlite3.connect(path, check_same_thread=False, isolation_level=None, timeout=10.0)
         self._db.row_factory = sqlite3.Row
@@ -171,6 +184,9 @@ class SQLiteStore:
                 self._db.close()
             except Exception:  # pragma: no cover
                 pass
+            if self._blob_fd is not None:
+                os.close(self._blob_fd)
+                self._blob_fd = None
         if self.ephemeral:
             _remove_db(self.path)
 
@@ -234,14 +250,26 @@ class SQLiteStore:
         d["stops"] = json.loads(d["stops"]) if d.get("stops") else {}
         return d
 
-    @staticmethod
-    def _res_dict(r: sqlite3.Row, full: bool) -> Dict[str, Any]:
+    def _text(self, v: Any) -> Any:
+        """A column value, with a side-file reference (``BLOB_REF`` + ``offset:length``) resolved."""
+        if not isinstance(v, str) or not v.startswith(BLOB_REF):
+            return v
+        off, n = (int(x) for x in v[len(BLOB_REF):].split(":"))
+        if self._blob_fd is None:
+            self._blob_fd = os.open(self.blob_path, os.O_RDONLY)
+        b = os.pread(self._blob_fd, n, off)
+        if len(b) != n:
+            raise StoreUnavailable(f"route side file {self.blob_path} is short at {off}+{n}")
+        return b.decode("utf-8")
+
+    def _res_dict(self, r: sqlite3.Row, full: bool) -> Dict[str, Any]:
         d = dict(r)
         d["optimized_order"] = json.loads(d["optimized_order"]) if d.get("optimized_order") else []
         legs = d.pop("legs", None)
         geom = d.pop("geometry", None)
         d.pop("request_id", None)
         if full:
+            legs, geom = self._text(legs), self._text(geom)
             d["legs"] = json.loads(legs) if legs else []
             d["geometry"] = json.loads(geom) if geom else None
         return d

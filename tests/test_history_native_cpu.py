@@ -74,3 +74,32 @@ def test_native_reads_see_later_writes_and_deletes(app_and_db):
     assert c.post("/api/optimize_route", json=p).status_code == 200
     assert db.history("100")[1] == c.get("/api/history?limit=100").content
     assert db.detail(items[1]["request_id"])[0] == 404
+
+
+def test_side_file_references_resolve_identically(app_and_db):
+    """Rows written by the native route service keep legs / geometry in <db>.blobs (a reference in
+    the column, store.py BLOB_REF): the app and the native reader resolve them to the same bytes,
+    and the detail is identical to the inline row it replaces."""
+    import sqlite3
+    from routest_amd.store.store import BLOB_REF
+    c, db = app_and_db
+    store = c.app.state.services.store
+    items = c.get("/api/history?limit=100").json()["items"]
+    before = {it["request_id"]: c.get(f"/api/history/{it['request_id']}").content for it in items[:8]}
+    con = sqlite3.connect(store.sqlite_uri, isolation_level=None)
+    with open(store.blob_path, "ab") as f:
+        off = f.tell()
+        for rid in before:
+            legs, geom = con.execute("SELECT legs, geometry FROM route_results WHERE request_id=?", (rid,)).fetchone()
+            lb, gb = legs.encode(), geom.encode()
+            f.write(b"xx" + lb + gb)                 # (some unrelated bytes first)
+            ref_l = f"{BLOB_REF}{off + 2}:{len(lb)}"
+            ref_g = f"{BLOB_REF}{off + 2 + len(lb)}:{len(gb)}"
+            con.execute("UPDATE route_results SET legs=?, geometry=? WHERE request_id=?", (ref_l, ref_g, rid))
+            off += 2 + len(lb) + len(gb)
+    con.close()
+    for rid, ref in before.items():
+        app = c.get(f"/api/history/{rid}")
+        assert app.status_code == 200 and app.content == ref
+        assert db.detail(rid) == (200, ref)
+    assert db.history("100")[1] == c.get("/api/history?limit=100").content
