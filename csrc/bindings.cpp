@@ -1333,7 +1333,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("big_dz2", &big_dz2, "dz2 = dy * w3 * relu'(z2) from h2a (hperm order)");
   m.def("eta_mlp3_train_fwd", &eta_mlp3_train_fwd, "K3: fused featurize+MLP forward (one pass over layer 2) + MSE grad + dW3 partial -> dz2 fragments");
   m.def("train_bwd", &train_bwd, "K3: dgrad + relu'(z1) + dW2|db2 and dW1 split-K partials in one kernel (train_bwd_kernel)");
-  m.def("train_wgrad_slices", [](int64_t B, int64_t device) { return (int64_t)rt::train_wgrad_slices((int)B, num_cus((int)device)); });
+  m.def("train_wgrad_slices", [](int64_t B, int64_t device, int64_t H) {
+    return (int64_t)rt::train_wgrad_slices((int)B, num_cus((int)device), (int)H);
+  }, py::arg("B"), py::arg("device"), py::arg("H") = 256);
   m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + training-blob re-pack");
   m.def("eta_mlp3_train_blob_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_train_blob_bytes((int)H); });
   m.def("mlp3_num_params", [](int64_t H) { return (int64_t)rt::mlp3_num_params((int)H); });

@@ -426,7 +426,16 @@ __device__ __forceinline__ void mfma_drain(f32x16& x, f32x16& y) {
 // fragment prefetch, 3 the dgrad MFMAs, 4 the dW2 MFMAs, 5 the next tile's staging, 6 db2): s_memtime per tile segment — [0] the loop-top
 // wait + barrier, [1] staging issue + layer 1, [2] the hidden-tile loop, [3] dW1 — summed per wave
 // into prof[wave][4] (scalar registers: the timed code keeps its VGPR allocation)
-template <int H, int PROF = 0>
+//
+// NBW = 1 (the column split, small batches): workgroups work in PAIRS on the same k-slice, each
+// owning half of the h1 units (wave w of half c: n-block 4c + w), so a slice's dW2 | dW1 partial is
+// written by two workgroups into disjoint parts of ONE slab — half the slabs (and half the slab
+// bytes written here and read back by wgrad_reduce) for the same number of workgroups.  Each
+// workgroup loads only its half of the W2 fragment image, the dgrad needs no cross-workgroup sum
+// (an h1 unit's dh1 is a full K = H dot product over z2 units), and the two dgrad chains of the one
+// n-block split k into even / odd steps.  The pair shares an XCD (blocks b and b + 8: round-robin
+// XCD dispatch), so the second read of each dz2 tile hits that XCD's L2.
+template <int H, int PROF = 0, int NBW = 2>
 __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     const __bf16* __restrict__ xf, int B, const unsigned char* __restrict__ blob,
     const bf16x8* __restrict__ dz2r, float* __restrict__ slab2, float* __restrict__ slab1,
@@ -445,24 +454,31 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
   typedef __attribute__((address_space(3))) const unsigned char lds_u8c;
   typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16x8* const w2s = reinterpret_cast<bf16x8*>(smem);      // [H/32][KS][64] B fragments
-  bf16x8* const rb = w2s + MT * RBF;                         // [2][KS][64] dz2 fragments
+  static_assert(NBW == 1 || NBW == 2, "n-blocks per wave");
+  constexpr int NW = H / 64, NBL = NW * NBW;                 // waves; n-blocks of this workgroup
+  bf16x8* const w2s = reinterpret_cast<bf16x8*>(smem);      // [NBL][KS][64] B fragments
+  bf16x8* const rb = w2s + NBL * RBF;                        // [2][KS][64] dz2 fragments
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 31, h = lane >> 5;
-  const int nw = blockDim.x >> 6;
+  const int nw = NW;
   const int wsc = __builtin_amdgcn_readfirstlane(w);
   const int ntiles = (B + 31) >> 5;
+  // the k-slice of this workgroup and its half (NBW = 1: blocks b and b + 8 form a pair)
+  const int bid = (int)blockIdx.x;
+  const int half = NBW == 2 ? 0 : (bid >> 3) & 1;
+  const int slice = NBW == 2 ? bid : ((bid & 7) | ((bid >> 4) << 3));
+  const int nb0 = (half * NW + wsc) * NBW;                    // this wave's first n-block (global)
   // slice s takes tiles s, s + S, s + 2S, ... in DESCENDING order: the forward wrote the tiles in
   // rounds of increasing index, so every slice starts on the most recently written tiles, which are
   // still in the 256 MB last-level cache, instead of half the slices streaming the oldest from HBM
-  const int S = gridDim.x;
-  const int nmine = blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / S + 1 : 0;
-  auto tile_at = [&](int i) { return (int)blockIdx.x + (nmine - 1 - i) * S; };
+  const int S = NBW == 2 ? (int)gridDim.x : (int)gridDim.x >> 1;
+  const int nmine = slice < ntiles ? (ntiles - 1 - slice) / S + 1 : 0;
+  auto tile_at = [&](int i) { return slice + (nmine - 1 - i) * S; };
   const int t0 = 0, t1 = nmine;                              // loop positions
 
   // the W2 B-fragment image (kept by adamw_pack_kernel past the forward's blob) into LDS, and the
   // first dz2 tile behind it
-  const unsigned char* w2g = blob + L::BLOB;
-  for (int c = w; c < (int)(MT * RBF / 64); c += nw)
+  const unsigned char* w2g = blob + L::BLOB + (size_t)half * NBL * KS * 1024;   // this half's blocks
+  for (int c = w; c < NBL * KS; c += nw)
     __builtin_amdgcn_global_load_lds((const void*)(w2g + (size_t)c * 1024 + 16 * lane),
                                      (lds_void_t*)(w2s + c * 64), 16, 0, 0);
   // the per-tile dz2 copy is issued through inline asm: issued with the builtin, the compiler tracks
@@ -485,11 +501,14 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     xn = xg[(size_t)tile_at(t0) * 64 + 2 * col + h];
   }
   const bf16x8* w1p = reinterpret_cast<const bf16x8*>(blob + L::W2B);
-  // this wave's two W2 B-fragment blocks in the LDS image (absolute addresses: lane base + immediates)
-  const unsigned wb0[2] = {(unsigned)(((2 * w) * KS * 64 + lane) * 16), (unsigned)(((2 * w + 1) * KS * 64 + lane) * 16)};
-  bf16x8 w1f[2];
+  // this wave's W2 B-fragment blocks in the LDS image (absolute addresses: lane base + immediates)
+  unsigned wb0[NBW];
+  bf16x8 w1f[NBW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) w1f[i] = w1p[(2 * w + i) * 64 + lane];
+  for (int i = 0; i < NBW; ++i) {
+    wb0[i] = (unsigned)(((w * NBW + i) * KS * 64 + lane) * 16);
+    w1f[i] = w1p[(nb0 + i) * 64 + lane];
+  }
   bf16x8 eye;
 #pragma unroll
   for (int j = 0; j < 8; ++j) eye[j] = (__bf16)(8 * h + j == col ? 1.f : 0.f);   // x^T: B (k = 8h + j, n = col)
@@ -511,18 +530,20 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     const int row = 4 * (g >> 1) + q, chunk = 2 * (g & 1) + (p >> 1);
     C0 = row * RB2 + 16 * ((chunk ^ dz2swz(row)) & CM) + 8 * (p & 1);
   }
-  f32x16 acc2[MT][2], acc1[2], zero;
+  f32x16 acc2[MT][NBW], acc1[NBW], zero;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     zero[e] = 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NBW; ++i) {
       acc1[i][e] = 0.f;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc2[mt][i][e] = 0.f;
     }
   }
-  float db2[2] = {0.f, 0.f};           // sums of dz2 over the rows, units 32(2w + i) + col
+  float db2[NBW];                      // sums of dz2 over the rows, units 32(nb0 + i) + col
+#pragma unroll
+  for (int i = 0; i < NBW; ++i) db2[i] = 0.f;
   typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
   typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
   auto pack = [](const f32x16& v, int s, bool relu) {
@@ -559,12 +580,12 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     // the tile image as an absolute LDS address (dynamic LDS starts at 0: no static __shared__ here),
     // so every read is a lane base + an immediate offset
     // layer 1 for the two n-blocks: h1^T (units on the lanes, rows in the registers)
-    bf16x8 h1t[2][2];
+    bf16x8 h1t[NBW][2];
     // (relu on the packed bf16 pairs, v_pk_max_i16 — and relu'(z1) is read back off the same packed
     // values below: one wave per SIMD issues VALU at 4 cycles, and the per-element compare/select
     // mask this replaces was ~150 VALU per tile)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NBW; ++i) {
       const f32x16 hz = mfma32(x, w1f[i], zero);
       float zf[16];
 #pragma unroll
@@ -579,7 +600,7 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
     // while they arrive).  The bases pass through an empty asm per hidden tile, so the XORs are
     // formed where they are used instead of all being hoisted into live registers, and the memory
     // clobber keeps later tiles' reads from being hoisted to the top (both spilled).
-    const unsigned tb0 = (unsigned)(MT * RBF * 16 + buf * RBF * 16);
+    const unsigned tb0 = (unsigned)(NBL * RBF * 16 + buf * RBF * 16);
     unsigned rbase = tb0 | R0, tbase = tb0 | C0;
     struct AFrags {
       bf16x8 a0, a1, t[2];
@@ -597,26 +618,29 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
       }
       return f;
     };
-    auto ldw = [&](int mt, bf16x8 (&wv)[2][2]) {
+    auto ldw = [&](int mt, bf16x8 (&wv)[NBW][2]) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NBW; ++i) {
         const lds_u8c* wf = (const lds_u8c*)(uintptr_t)(wb0[i] + 2048u * mt);
         wv[i][0] = *reinterpret_cast<const lds_bf16x8*>(wf);
         wv[i][1] = *reinterpret_cast<const lds_bf16x8*>(wf + 1024);
       }
     };
     AFrags cur = lda(0);
-    bf16x8 wc[2][2];
+    bf16x8 wc[NBW][2];
     ldw(0, wc);
     // VALU-written MFMA operands (h1t, the zeroed accd) get their wait states before the first
     // inline-asm MFMA reads them
-    asm volatile("s_nop 4" : "+v"(h1t[0][0]), "+v"(h1t[0][1]), "+v"(h1t[1][0]), "+v"(h1t[1][1]),
-                 "+v"(accd[0]), "+v"(accd[1]));
+    if constexpr (NBW == 2)
+      asm volatile("s_nop 4" : "+v"(h1t[0][0]), "+v"(h1t[0][1]), "+v"(h1t[1][0]), "+v"(h1t[1][1]),
+                   "+v"(accd[0]), "+v"(accd[1]));
+    else
+      asm volatile("s_nop 4" : "+v"(h1t[0][0]), "+v"(h1t[0][1]), "+v"(accd[0]), "+v"(accd[1]));
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       asm volatile("" : "+v"(rbase), "+v"(tbase));
       AFrags nxt = cur;
-      bf16x8 wn[2][2];
+      bf16x8 wn[NBW][2];
       if (mt + 1 < MT && PROF != 2) {
         nxt = lda(mt + 1);
         ldw(mt + 1, wn);
@@ -625,28 +649,37 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
       // four independent accumulation chains interleaved (a dependent MFMA waits for its
       // predecessor's result): dW2 = dz2^T (lane m: the unit in image column 32mt + m, rows in the k
       // order of h1t) x h1^T, and the dgrad dh1^T(u1 block) += dz2 (rows on lanes) x W2[:, block]
-      if (PROF != 4) {
+      if constexpr (NBW == 2) {
+        if (PROF != 4) {
+          mfma32_acc(acc2[mt][0], cur.t[0], h1t[0][0]);
+          mfma32_acc(acc2[mt][1], cur.t[0], h1t[1][0]);
+        }
+        if (PROF != 3) {
+          mfma32_vacc(accd[0], cur.a0, wc[0][0]);
+          mfma32_vacc(accd[1], cur.a0, wc[1][0]);
+        }
+        if (PROF != 4) {
+          mfma32_acc(acc2[mt][0], cur.t[1], h1t[0][1]);
+          mfma32_acc(acc2[mt][1], cur.t[1], h1t[1][1]);
+        }
+        if (PROF != 3) {
+          mfma32_vacc(accd[0], cur.a1, wc[0][1]);
+          mfma32_vacc(accd[1], cur.a1, wc[1][1]);
+        }
+      } else {
+        // one n-block: the dgrad's k-steps alternate between two chains (summed after the loop), so
+        // dependent MFMAs stay three or four issues apart
         mfma32_acc(acc2[mt][0], cur.t[0], h1t[0][0]);
-        mfma32_acc(acc2[mt][1], cur.t[0], h1t[1][0]);
-      }
-      if (PROF != 3) {
         mfma32_vacc(accd[0], cur.a0, wc[0][0]);
-        mfma32_vacc(accd[1], cur.a0, wc[1][0]);
-      }
-      if (PROF != 4) {
+        mfma32_vacc(accd[1], cur.a1, wc[0][1]);
         mfma32_acc(acc2[mt][0], cur.t[1], h1t[0][1]);
-        mfma32_acc(acc2[mt][1], cur.t[1], h1t[1][1]);
-      }
-      if (PROF != 3) {
-        mfma32_vacc(accd[0], cur.a1, wc[0][1]);
-        mfma32_vacc(accd[1], cur.a1, wc[1][1]);
       }
       // db2 of this wave's own two z2 tiles (row sums of dz2^T): the wave index through readfirstlane
       // makes this a scalar branch (an exec-mask one through threadIdx; hidden-tile loop 4129 -> 4044
       // cycles per 32-row tile, profiles/train_bwd_segments_r4.md).  Computing it at every hidden tile
       // and selecting measured slower (4562); summing the pairs with v_dot2_f32_bf16 against (1, 1)
       // was faster (3937) but did not reproduce these sums (db2 off by 13-54 %, r4an) and is not used.
-      if ((mt >> 1) == wsc && PROF != 6) {      // (PROF 6, diagnostics: no db2 block)
+      if (mt / NBW == half * NW + wsc && PROF != 6) {      // (PROF 6, diagnostics: no db2 block)
         const u32x4v q0 = __builtin_bit_cast(u32x4v, cur.t[0]), q1 = __builtin_bit_cast(u32x4v, cur.t[1]);
         float sacc = 0.f;
 #pragma unroll
@@ -654,24 +687,28 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
           sacc += __uint_as_float(q0[q] << 16) + __uint_as_float(q0[q] & 0xFFFF0000u);
           sacc += __uint_as_float(q1[q] << 16) + __uint_as_float(q1[q] & 0xFFFF0000u);
         }
-        db2[mt & 1] += sacc;
+        db2[mt % NBW] += sacc;
       }
       if (PROF != 2) cur = nxt;
       if (mt + 1 < MT && PROF != 2) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NBW; ++i) {
           wc[i][0] = wn[i][0];
           wc[i][1] = wn[i][1];
         }
       }
     }
     mfma_drain(accd[0], accd[1]);
+    if constexpr (NBW == 1) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) accd[0][e] += accd[1][e];
+    }
     mark(2);
     // dW1 += (dh1 * relu'(z1))^T x: x^T as the B operand (features on the lanes)
     const f32x16 xt = mfma32(x, eye, zero);
     const bf16x8 xb0 = pack(xt, 0, false), xb1 = pack(xt, 1, false);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NBW; ++i) {
       // dz1 = dh1 * relu'(z1): a bf16 half survives where h1 = relu(z1) is nonzero.  Per packed pair
       // (h1 halves in [0, 0x7F80]): x = (w + 0x7FFF7FFF) & 0x80008000 flags the nonzero halves (no
       // carry crosses a half) and (x << 1) - (x >> 15) widens each flag to 0xFFFF
@@ -697,7 +734,7 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
   }
   if constexpr (PROF) {
     if (lane == 0 && prof != nullptr)
-      for (int k = 0; k < 4; ++k) prof[((size_t)blockIdx.x * nw + w) * 4 + k] = pt[k];
+      for (int k = 0; k < 4; ++k) prof[((size_t)bid * nw + w) * 4 + k] = pt[k];
   }
   // the last dW2 MFMAs were issued through inline asm, which the hazard recognizer does not see: give
   // them their 16 passes before the epilogue reads the accumulators
@@ -707,13 +744,13 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
   // q*256 + 4l — one 16-byte store per lane and 4 registers, 1 KB per wave-instruction.  (Stored in
   // the bucket's [row][hperm col] order, the same partial took 4x the store instructions: one dword
   // per lane, 256 per wave, an issue-bound tail of ~256 KB per workgroup after the last tile.)
-  float* o2 = slab2 + (size_t)blockIdx.x * H * LDG;
-  float* o1 = slab1 + (size_t)blockIdx.x * H * 16;
+  float* o2 = slab2 + (size_t)slice * H * LDG;
+  float* o1 = slab1 + (size_t)slice * H * 16;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NBW; ++i)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      f32x4* t = reinterpret_cast<f32x4*>(o2 + (size_t)(((2 * w + i) * MT + mt) * 1024)) + lane;
+      f32x4* t = reinterpret_cast<f32x4*>(o2 + (size_t)(((nb0 + i) * MT + mt) * 1024)) + lane;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         t[64 * q] = (f32x4){acc2[mt][i][4 * q], acc2[mt][i][4 * q + 1], acc2[mt][i][4 * q + 2], acc2[mt][i][4 * q + 3]};
@@ -723,16 +760,16 @@ __global__ __launch_bounds__(H, 1) void train_bwd_kernel(
   for (int e = 0; e < 16; ++e) {
     const int mo = (e & 3) + 8 * (e >> 2) + 4 * h;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (col < 16) o1[(size_t)hperm(32 * (2 * w + i) + mo) * 16 + col] = acc1[i][e];
+    for (int i = 0; i < NBW; ++i)
+      if (col < 16) o1[(size_t)hperm(32 * (nb0 + i) + mo) * 16 + col] = acc1[i][e];
   }
   // db2 column (and the zero columns H+1 .. H+15) past the H*H native block, [bucket row][16]: both
-  // lane halves hold rows of image column 32(2w+i) + col (image column = bucket row)
+  // lane halves hold rows of image column 32(nb0+i) + col (image column = bucket row)
   float* oc = o2 + (size_t)H * H;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < NBW; ++i) {
     const float d = db2[i] + __shfl_xor(db2[i], 32);
-    const int ur = 32 * (2 * w + i) + col;
+    const int ur = 32 * (nb0 + i) + col;
     if (h == 0) oc[(size_t)ur * 16] = d;
     else
 #pragma unroll
@@ -912,13 +949,37 @@ hipError_t launch_eta_mlp3_train_fwd(const void* rec, const float* target, int B
 // k-slices of train_bwd_kernel: one workgroup per CU at most (its LDS is the whole 160 KB at
 // H = 256), each slice a whole number of 32-row tiles, >= ROUTEST_TRAIN_WGRAD_TILES (default 8) of
 // them so the W2 staging and the slab write are amortised
-int train_wgrad_slices(int B, int num_cus) {
+static int wgrad_min_tiles() {
   static const int min_tiles = [] {
     const char* v = std::getenv("ROUTEST_TRAIN_WGRAD_TILES");
     const int t = v ? std::atoi(v) : 8;
     return t < 1 ? 1 : t;
   }();
+  return min_tiles;
+}
+
+// The column split (train_bwd_kernel NBW = 1) at H = 256 for batches up to
+// ROUTEST_TRAIN_BWD_SPLIT_ROWS (default 262144; 0 disables): there the slab round trip is a large
+// share of the step (64k rows: 75 MB written + read for ~18 GFLOP of backward), while at 1M rows the
+// slabs are amortised and the full n-block width per wave is the faster loop.  A slab count that is
+// a multiple of 8 selects it (pairs b, b + 8 on one XCD need the grid in whole 16s).
+static bool bwd_split(int H, int B, int S) {
+  static const long long rows = [] {
+    const char* v = std::getenv("ROUTEST_TRAIN_BWD_SPLIT_ROWS");
+    return v ? std::atoll(v) : 262144LL;
+  }();
+  return H == 256 && (long long)B <= rows && S >= 8 && S % 8 == 0;
+}
+
+int train_wgrad_slices(int B, int num_cus, int H) {
   const int ntiles = (B + 31) / 32;
+  const int min_tiles = wgrad_min_tiles();
+  if (H == 256) {
+    int Sp = ntiles / min_tiles;
+    if (Sp > num_cus / 2) Sp = num_cus / 2;
+    Sp &= ~7;
+    if (bwd_split(H, B, Sp)) return Sp;
+  }
   int S = ntiles / min_tiles;
   if (S > num_cus) S = num_cus;
   return S < 1 ? 1 : S;
@@ -928,6 +989,7 @@ template <int H>
 static hipError_t launch_train_bwd_h(const void* xf, int B, const void* blob, const void* dz2r, float* slab2,
                                      float* slab1, int S, hipStream_t stream) {
   constexpr size_t LDS = (size_t)H * H * 2 + (size_t)2 * H * 64;
+  constexpr size_t LDS_SPLIT = (size_t)H * H + (size_t)2 * H * 64;       // half the W2 image
   static_assert(LDS <= 160 * 1024, "train_bwd_kernel LDS budget");
   static bool attr_set[64] = {};
   int dev = 0;
@@ -935,6 +997,9 @@ static hipError_t launch_train_bwd_h(const void* xf, int B, const void* blob, co
   if (!attr_set[dev & 63]) {
     hipError_t e = hipFuncSetAttribute((const void*)train_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)LDS);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)train_bwd_kernel<H, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)LDS_SPLIT);
     if (e != hipSuccess) return e;
     attr_set[dev & 63] = true;
   }
@@ -980,8 +1045,12 @@ static hipError_t launch_train_bwd_h(const void* xf, int B, const void* blob, co
                  sum[3] / (S * nwv) / tiles, tiles);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(train_bwd_kernel<H>, dim3(S), dim3(H), LDS, stream, (const __bf16*)xf, B,
-                     (const unsigned char*)blob, (const bf16x8*)dz2r, slab2, slab1, nullptr);
+  if (bwd_split(H, B, S))      // S slabs, 2S workgroups (pairs b, b + 8)
+    hipLaunchKernelGGL((train_bwd_kernel<H, 0, 1>), dim3(2 * S), dim3(H), LDS_SPLIT, stream, (const __bf16*)xf, B,
+                       (const unsigned char*)blob, (const bf16x8*)dz2r, slab2, slab1, nullptr);
+  else
+    hipLaunchKernelGGL(train_bwd_kernel<H>, dim3(S), dim3(H), LDS, stream, (const __bf16*)xf, B,
+                       (const unsigned char*)blob, (const bf16x8*)dz2r, slab2, slab1, nullptr);
   return hipGetLastError();
 }
 

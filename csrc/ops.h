@@ -38,7 +38,7 @@ int train_fwd_grid(int B, int num_cus);   // workgroups = rows of the dW3 slab
 // bucket order); xf must hold ceil(B/32)*32 rows (zeros past B)
 hipError_t launch_train_bwd(const void* xf, int B, const void* blob, int H, const void* dz2r, float* slab2,
                             float* slab1, int S, hipStream_t stream);
-int train_wgrad_slices(int B, int num_cus);
+int train_wgrad_slices(int B, int num_cus, int H = 256);
 size_t eta_mlp3_train_blob_bytes(int H);
 int mlp3_num_params(int H);
 int mlp3_grad_bucket_floats(int H);

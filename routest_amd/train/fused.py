@@ -187,7 +187,7 @@ class FusedMlp3Trainer:
         ldg = H + 16
         # k-slices of the backward kernel (one workgroup per CU at most): dW2|db2 and dW1 partials
         # per slice; dW3|db3 arrives as one row per forward workgroup (w3slab)
-        self.S = self.C.train_wgrad_slices(B, d.index or 0)
+        self.S = self.C.train_wgrad_slices(B, d.index or 0, H)
         self.slab2 = torch.empty(self.S, H * ldg, dtype=torch.float32, device=d)
         self.slab = torch.empty(self.S, H * 16, dtype=torch.float32, device=d)
         self.w3slab = torch.empty(self.C.train_fwd_grid(B, d.index or 0), ldg, dtype=torch.float32,

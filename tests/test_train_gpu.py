@@ -307,3 +307,34 @@ def test_wide_trainer_h1024_steps_and_serves():
     with torch.no_grad():
         ref = model(torch.from_numpy(records_to_features(erec))).reshape(-1)
     torch.testing.assert_close(pred, ref, rtol=3e-2, atol=0.3)
+
+
+@pytest.mark.parametrize("B", [8192, 65536])
+def test_column_split_backward_matches_full_width(B):
+    """train_bwd_kernel's column split (NBW = 1: workgroup pairs own half the h1 units each and
+    write one slab per pair; chosen for H = 256 when the slab count is a multiple of 8) gives the
+    gradients of the full-width kernel (NBW = 2, forced here with a slab count that is not a multiple
+    of 8) up to fp32 summation order."""
+    H = 256
+    m = _model(H)
+    rt, yn = _batch(B, m)
+    tr = FusedMlp3Trainer(m, DEV, B, B)
+    assert tr.S % 8 == 0, tr.S                        # the trainer runs the split
+    tr.forward_backward(rt.to(DEV), yn.to(DEV))
+    torch.cuda.synchronize()
+    g_split = tr.G.clone()
+    ldg = H + 16
+    S = tr.S - 1                                      # not a multiple of 8: full-width launch
+    slab2 = torch.empty(S, H * ldg, dtype=torch.float32, device=DEV)
+    slab = torch.empty(S, H * 16, dtype=torch.float32, device=DEV)
+    C = tr.C
+    C.train_bwd(tr.xf, B, tr.blob, H, tr.dz2r, slab2, slab)
+    C.wgrad_reduce(slab2, tr.G[:H * ldg], slab, tr.G[H * ldg + ldg:], tr.w3slab, tr.G[H * ldg:H * ldg + ldg],
+                   perm_h=H)
+    torch.cuda.synchronize()
+    rel = (g_split - tr.G).norm() / tr.G.norm()
+    assert rel < 1e-5, float(rel)
+    got, ref = grads_from_bucket(g_split, H), grads_from_bucket(tr.G, H)
+    for name in ref:
+        r = (got[name] - ref[name]).norm() / ref[name].norm().clamp_min(1e-12)
+        assert r < 1e-4, (name, float(r))
