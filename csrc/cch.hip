@@ -651,7 +651,9 @@ __global__ __launch_bounds__(64) void sweep_kernel(const int32_t* __restrict__ j
                                                    const int32_t* __restrict__ f_ptr, const int4* __restrict__ f_rec,
                                                    const int32_t* __restrict__ b_ptr, const int4* __restrict__ b_rec,
                                                    int stride, float* __restrict__ out_dist,
-                                                   int32_t* __restrict__ out_pred, int32_t* __restrict__ out_node) {
+                                                   int32_t* __restrict__ out_pred, int32_t* __restrict__ out_node,
+                                                   const CchMView* __restrict__ mv, const int32_t* __restrict__ grp,
+                                                   int gdiv) {
   extern __shared__ unsigned char smem[];
   float* sd = reinterpret_cast<float*>(smem);
   int32_t* sp = reinterpret_cast<int32_t*>(smem + (size_t)stride * 4);
@@ -662,6 +664,13 @@ __global__ __launch_bounds__(64) void sweep_kernel(const int32_t* __restrict__ j
   if (code < 0) return;                     // matrix padding
   const int r = code >> 1;
   const bool fwd = (code & 1) == 0;
+  if (mv != nullptr) {                      // this job's metric (one job per workgroup: uniform)
+    const CchMView& v = mv[grp[j / gdiv]];
+    f_ptr = v.f_ptr;
+    f_rec = v.f_rec;
+    b_ptr = v.b_ptr;
+    b_rec = v.b_rec;
+  }
   const int32_t* __restrict__ ptr = fwd ? f_ptr : b_ptr;
   const int4* __restrict__ rec = fwd ? f_rec : b_rec;
   const int D = depth[r];
@@ -752,11 +761,18 @@ __global__ __launch_bounds__(64) void meet_kernel(int P, const int32_t* __restri
                                                   const int32_t* __restrict__ arc_lo, const float* __restrict__ len_up,
                                                   const float* __restrict__ len_dn, float* __restrict__ out_sec,
                                                   float* __restrict__ out_met, int* __restrict__ out_status,
-                                                  int32_t* __restrict__ arcs, int32_t* __restrict__ narcs, int max_arcs) {
+                                                  int32_t* __restrict__ arcs, int32_t* __restrict__ narcs, int max_arcs,
+                                                  const CchMView* __restrict__ mv, const int32_t* __restrict__ grp,
+                                                  int gdiv) {
   __shared__ int32_t fw[4096];
   const int q = blockIdx.x;
   if (q >= P) return;
   const int lane = threadIdx.x;
+  if (mv != nullptr) {
+    const CchMView& v = mv[grp[q / gdiv]];
+    len_up = v.len_up;
+    len_dn = v.len_dn;
+  }
   const int jf = pjf ? pjf[q] : jf0 + 2 * q;
   const int jb = pjb ? pjb[q] : jb0 + 2 * q;
   if (jobs[jf] < 0 || jobs[jb] < 0) {       // a matrix padding point: nothing to meet
@@ -848,10 +864,16 @@ __global__ __launch_bounds__(64) void unpack_kernel(int P, const int* __restrict
                                                     const int32_t* __restrict__ up_head,
                                                     const int32_t* __restrict__ node_of, int* __restrict__ status,
                                                     int* __restrict__ out_len, int* __restrict__ out_path, int max_path,
-                                                    int min_arcs, int* __restrict__ out_edge) {
+                                                    int min_arcs, int* __restrict__ out_edge,
+                                                    const CchMView* __restrict__ mv, const int32_t* __restrict__ grp) {
   __shared__ int32_t stk[64 * UNPACK_STACK];
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= P) return;
+  if (mv != nullptr) {
+    const CchMView& v = mv[grp[q]];
+    sub_up = v.sub_up;
+    sub_dn = v.sub_dn;
+  }
   int32_t* st = stk + threadIdx.x * UNPACK_STACK;
   if (status[q] != 0) {
     if (min_arcs < 0) out_len[q] = 0;
@@ -911,13 +933,22 @@ __global__ __launch_bounds__(64) void unpack_coop_kernel(int P, const int* __res
                                                          const int32_t* __restrict__ up_head,
                                                          const int32_t* __restrict__ node_of, int* __restrict__ status,
                                                          int* __restrict__ out_len, int* __restrict__ out_path,
-                                                         int max_path, int* __restrict__ out_edge) {
+                                                         int max_path, int* __restrict__ out_edge,
+                                                         const CchMView* __restrict__ mv,
+                                                         const int32_t* __restrict__ grp) {
   constexpr int G = 64 / UNPACK_LANES;
   __shared__ int32_t offs[G][UNPACK_MAX_ARCS + 1];
   __shared__ int32_t stk[64 * UNPACK_SD];
   const int lane = threadIdx.x, g = lane / UNPACK_LANES, sl = lane % UNPACK_LANES;
   const int q = blockIdx.x * G + g;
   const bool active = q < P;
+  if (mv != nullptr && active) {            // (per pair: the four pairs of a wave may differ)
+    const CchMView& v = mv[grp[q]];
+    sub_up = v.sub_up;
+    sub_dn = v.sub_dn;
+    cnt_up = v.cnt_up;
+    cnt_dn = v.cnt_dn;
+  }
   int st = active ? status[q] : 1;
   const int na = active && st == 0 ? narcs[q] : 0;
   const bool coop = active && st == 0 && na <= UNPACK_MAX_ARCS;   // longer arc lists: the serial kernel
@@ -1545,7 +1576,13 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   if (ev[0] && ev[1] && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) m.basic_ms = ms;
   if (ev[1] && ev[2] && hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) m.perfect_ms = ms;
   if (ev[2] && ev[3] && hipEventElapsedTime(&ms, ev[2], ev[3]) == hipSuccess) m.prune_ms = ms;
-  m.host_cost.clear();
+  // the host copy of the costs (maneuver durations, the exact host fallback) is made here, on the
+  // builder's stream, before the metric is published: a flush that first meets this context finds
+  // it ready instead of copying E floats on its own critical path
+  m.host_cost.resize((size_t)E);
+  ck(hipMemcpyAsync(m.host_cost.data(), m.cost, (size_t)E * sizeof(float), hipMemcpyDeviceToHost, s));
+  ck(hipStreamSynchronize(s));
+  if (e != hipSuccess) m.host_cost.clear();
   return e;
 }
 
@@ -1709,28 +1746,30 @@ hipError_t CchGpu::metric_for(const CchContext& c, hipStream_t s, std::shared_pt
   return hipSuccess;
 }
 
-hipError_t CchGpu::launch_unpack(const CchMetricDev& m, int Q, const int* d_src, CchScratch& sc, const CchRouteOut& o,
-                                 hipStream_t s) {
+hipError_t CchGpu::launch_unpack(const CchMetricDev* m, const CchMView* mv, const int* grp, int Q, const int* d_src,
+                                 CchScratch& sc, const CchRouteOut& o, hipStream_t s) {
   static const bool serial_only = [] {
     const char* v = std::getenv("ROUTEST_CCH_UNPACK");
     return v && std::string(v) == "serial";
   }();
+  const int32_t* sub_up = m ? m->sub_up : nullptr;
+  const int32_t* sub_dn = m ? m->sub_dn : nullptr;
   if (!serial_only) {
     constexpr int G = 64 / UNPACK_LANES;
     hipLaunchKernelGGL(unpack_coop_kernel, dim3((Q + G - 1) / G), dim3(64), 0, s, Q, d_src, sc.arcs, sc.narcs, MAX_ARCS,
-                       m.sub_up, m.sub_dn, m.cnt_up, m.cnt_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path,
-                       o.max_path, o.edges);
+                       sub_up, sub_dn, m ? m->cnt_up : nullptr, m ? m->cnt_dn : nullptr, d_arc_lo, d_up_head, d_node,
+                       o.status, o.len, o.path, o.max_path, o.edges, mv, grp);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(Q, 64)), dim3(64), 0, s, Q, d_src, sc.arcs, sc.narcs, MAX_ARCS,
-                     m.sub_up, m.sub_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path, o.max_path,
-                     serial_only ? -1 : UNPACK_MAX_ARCS, o.edges);
+                     sub_up, sub_dn, d_arc_lo, d_up_head, d_node, o.status, o.len, o.path, o.max_path,
+                     serial_only ? -1 : UNPACK_MAX_ARCS, o.edges, mv, grp);
   return hipGetLastError();
 }
 
-hipError_t CchGpu::route(const CchMetricDev& m, const int* d_src, const int* d_dst, int Q, const CchRouteOut& o,
-                         CchScratch& sc, hipStream_t s) {
+hipError_t CchGpu::route_impl(const CchMetricDev* m, const CchMView* mv, const int* grp, const int* d_src,
+                              const int* d_dst, int Q, const CchRouteOut& o, CchScratch& sc, hipStream_t s) {
   if (Q <= 0) return hipSuccess;
   const int S = stride();
   sc.device = dev_;
@@ -1740,20 +1779,31 @@ hipError_t CchGpu::route(const CchMetricDev& m, const int* d_src, const int* d_d
   hipLaunchKernelGGL(route_jobs_kernel, dim3(blocks_for(Q, 256)), dim3(256), 0, s, d_src, d_dst, Q, d_rank, T_.N,
                      sc.jobs);
   hipLaunchKernelGGL(sweep_kernel, dim3(2 * Q), dim3(64), (size_t)S * 8, s, sc.jobs, 2 * Q, d_parent, d_depth, T_.N,
-                     m.f_ptr, m.f_rec, m.b_ptr, m.b_rec, S, sc.dist, sc.pred, sc.node);
+                     m ? m->f_ptr : nullptr, m ? m->f_rec : nullptr, m ? m->b_ptr : nullptr, m ? m->b_rec : nullptr, S,
+                     sc.dist, sc.pred, sc.node, mv, grp, 2);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(meet_kernel, dim3(Q), dim3(64), 0, s, Q, nullptr, nullptr, 0, 1, sc.jobs, S, sc.dist, sc.pred,
-                     sc.node, d_depth, d_arc_lo, m.len_up, m.len_dn, o.sec, o.metres, o.status,
-                     o.path ? sc.arcs : nullptr, o.path ? sc.narcs : nullptr, MAX_ARCS);
+                     sc.node, d_depth, d_arc_lo, m ? m->len_up : nullptr, m ? m->len_dn : nullptr, o.sec, o.metres,
+                     o.status, o.path ? sc.arcs : nullptr, o.path ? sc.narcs : nullptr, MAX_ARCS, mv, grp, 1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (o.path != nullptr) {
-    e = launch_unpack(m, Q, d_src, sc, o, s);
-  }
+  if (o.path != nullptr) e = launch_unpack(m, mv, grp, Q, d_src, sc, o, s);
   return e;
 }
 
-hipError_t CchGpu::matrix(const CchMetricDev& m, const int* d_pts, const int* d_npts, int R, int NM, float* d_sec,
-                          float* d_met, double* d_D64, CchScratch& sc, hipStream_t s) {
+hipError_t CchGpu::route(const CchMetricDev& m, const int* d_src, const int* d_dst, int Q, const CchRouteOut& o,
+                         CchScratch& sc, hipStream_t s) {
+  return route_impl(&m, nullptr, nullptr, d_src, d_dst, Q, o, sc, s);
+}
+
+hipError_t CchGpu::route_multi(const CchMView* d_mv, const int* d_grp, const int* d_src, const int* d_dst, int Q,
+                               const CchRouteOut& o, CchScratch& sc, hipStream_t s) {
+  if (d_mv == nullptr || d_grp == nullptr) return hipErrorInvalidValue;
+  return route_impl(nullptr, d_mv, d_grp, d_src, d_dst, Q, o, sc, s);
+}
+
+hipError_t CchGpu::matrix_impl(const CchMetricDev* m, const CchMView* mv, const int* grp, const int* d_pts,
+                               const int* d_npts, int R, int NM, float* d_sec, float* d_met, double* d_D64,
+                               CchScratch& sc, hipStream_t s) {
   if (R <= 0 || NM <= 0) return hipSuccess;
   if (d_sec == nullptr || d_met == nullptr) return hipErrorInvalidValue;   // the meet writes both
   const int S = stride();
@@ -1769,12 +1819,14 @@ hipError_t CchGpu::matrix(const CchMetricDev& m, const int* d_pts, const int* d_
   hipLaunchKernelGGL(matrix_jobs_kernel, dim3(blocks_for((long long)R * NM, 256)), dim3(256), 0, s, d_pts, d_npts, R, NM,
                      d_rank, T_.N, sc.jobs);
   hipLaunchKernelGGL(matrix_pairs_kernel, dim3(blocks_for((long long)P, 256)), dim3(256), 0, s, d_npts, R, NM, pjf, pjb);
+  // (job 2(r NM + i) + dir and pair r NM^2 + i NM + j belong to request row r)
   hipLaunchKernelGGL(sweep_kernel, dim3((unsigned)J), dim3(64), (size_t)S * 8, s, sc.jobs, (int)J, d_parent, d_depth,
-                     T_.N, m.f_ptr, m.f_rec, m.b_ptr, m.b_rec, S, sc.dist, sc.pred, sc.node);
+                     T_.N, m ? m->f_ptr : nullptr, m ? m->f_rec : nullptr, m ? m->b_ptr : nullptr,
+                     m ? m->b_rec : nullptr, S, sc.dist, sc.pred, sc.node, mv, grp, 2 * NM);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(meet_kernel, dim3((unsigned)P), dim3(64), 0, s, (int)P, pjf, pjb, 0, 0, sc.jobs, S, sc.dist,
-                     sc.pred, sc.node, d_depth, d_arc_lo, m.len_up, m.len_dn, sec, met, nullptr, nullptr, nullptr,
-                     MAX_ARCS);
+                     sc.pred, sc.node, d_depth, d_arc_lo, m ? m->len_up : nullptr, m ? m->len_dn : nullptr, sec, met,
+                     nullptr, nullptr, nullptr, MAX_ARCS, mv, grp, NM * NM);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(matrix_out_kernel, dim3(blocks_for((long long)P, 256)), dim3(256), 0, s, d_npts, R, NM, sec, met,
                      d_D64);
@@ -1785,9 +1837,20 @@ hipError_t CchGpu::matrix(const CchMetricDev& m, const int* d_pts, const int* d_
   return e;
 }
 
-hipError_t CchGpu::legs_from_matrix(const CchMetricDev& m, const int* d_src, const int* d_r, const int* d_i,
-                                    const int* d_j, int Q, uint64_t tag, const CchRouteOut& o, CchScratch& sc,
-                                    hipStream_t s) {
+hipError_t CchGpu::matrix(const CchMetricDev& m, const int* d_pts, const int* d_npts, int R, int NM, float* d_sec,
+                          float* d_met, double* d_D64, CchScratch& sc, hipStream_t s) {
+  return matrix_impl(&m, nullptr, nullptr, d_pts, d_npts, R, NM, d_sec, d_met, d_D64, sc, s);
+}
+
+hipError_t CchGpu::matrix_multi(const CchMView* d_mv, const int* d_row_grp, const int* d_pts, const int* d_npts, int R,
+                                int NM, float* d_sec, float* d_met, double* d_D64, CchScratch& sc, hipStream_t s) {
+  if (d_mv == nullptr || d_row_grp == nullptr) return hipErrorInvalidValue;
+  return matrix_impl(nullptr, d_mv, d_row_grp, d_pts, d_npts, R, NM, d_sec, d_met, d_D64, sc, s);
+}
+
+hipError_t CchGpu::legs_impl(const CchMetricDev* m, const CchMView* mv, const int* grp, const int* d_src,
+                             const int* d_r, const int* d_i, const int* d_j, int Q, uint64_t tag, const CchRouteOut& o,
+                             CchScratch& sc, hipStream_t s) {
   if (Q <= 0) return hipSuccess;
   if (tag == 0 || tag != sc.chain_tag) return hipErrorInvalidValue;   // chains overwritten since
   const int S = stride();
@@ -1806,13 +1869,24 @@ hipError_t CchGpu::legs_from_matrix(const CchMetricDev& m, const int* d_src, con
                      sc.chain_r, pjf, pjb);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(meet_kernel, dim3(Q), dim3(64), 0, s, Q, pjf, pjb, 0, 0, sc.jobs, S, sc.dist, sc.pred, sc.node,
-                     d_depth, d_arc_lo, m.len_up, m.len_dn, o.sec, o.metres, o.status, o.path ? sc.arcs : nullptr,
-                     o.path ? sc.narcs : nullptr, MAX_ARCS);
+                     d_depth, d_arc_lo, m ? m->len_up : nullptr, m ? m->len_dn : nullptr, o.sec, o.metres, o.status,
+                     o.path ? sc.arcs : nullptr, o.path ? sc.narcs : nullptr, MAX_ARCS, mv, grp, 1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (o.path != nullptr) {
-    e = launch_unpack(m, Q, d_src, sc, o, s);
-  }
+  if (o.path != nullptr) e = launch_unpack(m, mv, grp, Q, d_src, sc, o, s);
   return e;
+}
+
+hipError_t CchGpu::legs_from_matrix(const CchMetricDev& m, const int* d_src, const int* d_r, const int* d_i,
+                                    const int* d_j, int Q, uint64_t tag, const CchRouteOut& o, CchScratch& sc,
+                                    hipStream_t s) {
+  return legs_impl(&m, nullptr, nullptr, d_src, d_r, d_i, d_j, Q, tag, o, sc, s);
+}
+
+hipError_t CchGpu::legs_from_matrix_multi(const CchMView* d_mv, const int* d_grp, const int* d_src, const int* d_r,
+                                          const int* d_i, const int* d_j, int Q, uint64_t tag, const CchRouteOut& o,
+                                          CchScratch& sc, hipStream_t s) {
+  if (d_mv == nullptr || d_grp == nullptr) return hipErrorInvalidValue;
+  return legs_impl(nullptr, d_mv, d_grp, d_src, d_r, d_i, d_j, Q, tag, o, sc, s);
 }
 
 }  // namespace rt

@@ -51,7 +51,7 @@ struct CchMetricDev {
   int64_t kept_f = 0, kept_b = 0;
   double customize_ms = 0.0, cost_ms = 0.0;
   double basic_ms = 0.0, perfect_ms = 0.0, prune_ms = 0.0;   // device time per phase
-  std::vector<float> host_cost;    // [E] for the exact host fallback (filled on demand)
+  std::vector<float> host_cost;    // [E] the costs on the host (filled by customize before publishing)
   ~CchMetricDev();
 };
 
@@ -73,6 +73,22 @@ struct CchScratch {
   std::vector<void*> old;          // outgrown buffers, freed with the scratch
   ~CchScratch();
   hipError_t ensure(size_t jobs, size_t pairs, int stride, int max_arcs);
+};
+
+// The device pointers of one metric that the query kernels read — an array of these plus a group
+// index per request row / leg lets ONE launch sequence serve a flush spread over many routing
+// contexts (the *_multi calls below).
+struct CchMView {
+  const int32_t* f_ptr;
+  const int32_t* b_ptr;
+  const int4* f_rec;
+  const int4* b_rec;
+  const float* len_up;
+  const float* len_dn;
+  const int32_t* sub_up;
+  const int32_t* sub_dn;
+  const int32_t* cnt_up;
+  const int32_t* cnt_dn;
 };
 
 struct CchRouteOut {
@@ -158,9 +174,31 @@ class CchGpu {
                               int Q, uint64_t tag, const CchRouteOut& o, CchScratch& sc, hipStream_t s);
   static constexpr int MAX_ARCS = 1024;   // shortcut arcs per path before unpacking
 
+  // The same over several metrics at once: d_mv [G] views (view(m), on the device), d_grp the
+  // metric of each leg (route, legs_from_matrix) or request row (matrix).  Bit-identical per leg to
+  // the single-metric calls.
+  static CchMView view(const CchMetricDev& m) {
+    return CchMView{m.f_ptr, m.b_ptr, m.f_rec, m.b_rec, m.len_up, m.len_dn, m.sub_up, m.sub_dn, m.cnt_up, m.cnt_dn};
+  }
+  hipError_t route_multi(const CchMView* d_mv, const int* d_grp, const int* d_src, const int* d_dst, int Q,
+                         const CchRouteOut& o, CchScratch& sc, hipStream_t s);
+  hipError_t matrix_multi(const CchMView* d_mv, const int* d_row_grp, const int* d_pts, const int* d_npts, int R, int NM,
+                          float* d_sec, float* d_met, double* d_D64, CchScratch& sc, hipStream_t s);
+  hipError_t legs_from_matrix_multi(const CchMView* d_mv, const int* d_grp, const int* d_src, const int* d_r,
+                                    const int* d_i, const int* d_j, int Q, uint64_t tag, const CchRouteOut& o,
+                                    CchScratch& sc, hipStream_t s);
+
  private:
-  hipError_t launch_unpack(const CchMetricDev& m, int Q, const int* d_src, CchScratch& sc, const CchRouteOut& o,
-                           hipStream_t s);
+  // m: one metric; else mv + grp (group of item idx = grp[idx / gdiv])
+  hipError_t route_impl(const CchMetricDev* m, const CchMView* mv, const int* grp, const int* d_src, const int* d_dst,
+                        int Q, const CchRouteOut& o, CchScratch& sc, hipStream_t s);
+  hipError_t matrix_impl(const CchMetricDev* m, const CchMView* mv, const int* grp, const int* d_pts, const int* d_npts,
+                         int R, int NM, float* d_sec, float* d_met, double* d_D64, CchScratch& sc, hipStream_t s);
+  hipError_t legs_impl(const CchMetricDev* m, const CchMView* mv, const int* grp, const int* d_src, const int* d_r,
+                       const int* d_i, const int* d_j, int Q, uint64_t tag, const CchRouteOut& o, CchScratch& sc,
+                       hipStream_t s);
+  hipError_t launch_unpack(const CchMetricDev* m, const CchMView* mv, const int* grp, int Q, const int* d_src,
+                           CchScratch& sc, const CchRouteOut& o, hipStream_t s);
   rcch::Topology T_;
   int dev_ = 0;
   // topology on the device

@@ -120,11 +120,11 @@ struct HostBuf {
   }
 };
 
-inline rtc::Stamp local_now() {
+inline rtc::Stamp local_now(int64_t skew_s = 0) {
   struct timespec ts;
   clock_gettime(CLOCK_REALTIME, &ts);
   struct tm lt;
-  time_t t = ts.tv_sec;
+  time_t t = ts.tv_sec + (time_t)skew_s;
   localtime_r(&t, &lt);
   rtc::Stamp s;
   s.secs = rtc::days_from_civil(lt.tm_year + 1900, (unsigned)lt.tm_mon + 1, (unsigned)lt.tm_mday) * 86400 +
@@ -313,11 +313,16 @@ struct RouteService::Impl {
   DevBuf<long long> d_off;
   // CCH
   CchScratch csc;
-  // per context group: the matrix stage's chains (kept for the group's multi-stop legs), the tag of
-  // its matrix call, and each multi-stop job's row in it
-  std::vector<std::unique_ptr<CchScratch>> gsc;
-  std::vector<uint64_t> gtag;
+  // the matrix stage's chains (kept for the multi-stop legs), the tag of its matrix call and each
+  // multi-stop job's row in it; the flush's metrics as device views (one per context group) and the
+  // group of every request row / leg, so ONE launch sequence serves all the flush's contexts
+  CchScratch msc;
+  uint64_t mtag = 0;
   std::unordered_map<const RouteJob*, int> jrow;
+  HostBuf<CchMView> h_mv;
+  DevBuf<CchMView> d_mv;
+  HostBuf<int> h_rowg, h_lgrp;
+  DevBuf<int> d_rowg, d_lgrp;
   HostBuf<int> h_lr, h_li, h_lj;
   DevBuf<int> d_lr, d_li, d_lj;
   HostBuf<int> h_pts, h_npts2;
@@ -394,6 +399,7 @@ struct RouteService::Impl {
   // prefetch of the next week-hour: (weather, congestion) of requests routed at "now" -> last seen
   std::unordered_map<int, double> seen_now;
   int prefetched_wh = -1;
+  int64_t clock_skew_s = 0;
   std::unordered_set<int> prefetched;      // pairs already queued for prefetched_wh
   int prefetch_min = 10;
   // ETA
@@ -581,6 +587,9 @@ struct RouteService::Impl {
     if (const char* v = std::getenv("ROUTEST_ROUTE_DEADLINE_MS")) deadline_ms = std::atof(v);
     if (hipEventCreateWithFlags(&ev_gpu, hipEventDisableTiming) != hipSuccess) ev_gpu = nullptr;
     if (const char* v = std::getenv("ROUTEST_CCH_PREFETCH_MIN")) prefetch_min = std::atoi(v);
+    // rehearsal knob (bench/route_context_bench.py): shifts the clock "now" routing contexts are
+    // resolved with, so an hour boundary can be crossed on demand
+    if (const char* v = std::getenv("ROUTEST_ROUTE_CLOCK_SKEW_S")) clock_skew_s = std::atoll(v);
     if (cfg.cch != nullptr && cfg.cch_contexts && async_ctx)
       listener = cfg.cch->add_build_listener([this](uint64_t key, bool ok) { on_built(key, ok); });
     if (std::getenv("ROUTEST_ROUTE_PREWARM") == nullptr || std::string(std::getenv("ROUTEST_ROUTE_PREWARM")) != "0")
@@ -813,8 +822,10 @@ struct RouteService::Impl {
     return ((uint64_t)(uint32_t)group << 48) ^ ((uint64_t)(uint32_t)s << 24) ^ (uint64_t)(uint32_t)t;
   }
 
-  // edge costs of a metric on the host (maneuver durations, exact host fallback), copied once
+  // edge costs of a metric on the host (maneuver durations, exact host fallback): the copy the
+  // customization left with the metric (shares its lifetime), else copied once here
   std::shared_ptr<const std::vector<float>> host_costs(const std::shared_ptr<CchMetricDev>& m) {
+    if (m->host_cost.size() == (size_t)cfg.cch->topo().E) return {m, &m->host_cost};
     {
       std::lock_guard<std::mutex> lk(hc_mu);
       auto it = hc_index.find(m->key);
@@ -857,11 +868,11 @@ struct RouteService::Impl {
       ok = ok && !(h_pts.need(RN) || h_npts2.need(R) || d_pts.need(RN) || d_npts2.need(R) || d_msec.need(RN * NM) ||
                    d_mmet.need(RN * NM) || h_met.need(Q) || d_met.need(Q) || d_edge.need(Q * MP) ||
                    h_flat_e.need(Q * 256) || d_flat_e.need(Q * 256) || h_lr.need(Q) || h_li.need(Q) || h_lj.need(Q) ||
-                   d_lr.need(Q) || d_li.need(Q) || d_lj.need(Q));
+                   d_lr.need(Q) || d_li.need(Q) || d_lj.need(Q) || h_rowg.need(R) || d_rowg.need(R) ||
+                   h_lgrp.need(Q) || d_lgrp.need(Q) || h_mv.need(R) || d_mv.need(R));
       const int S = cfg.cch->stride();
-      if (gsc.empty()) gsc.push_back(std::make_unique<CchScratch>());
-      gsc[0]->device = cfg.device;
-      ok = ok && gsc[0]->ensure(RN * 2, std::max(Q, (RN * NM * 2 + CchGpu::MAX_ARCS - 1) / CchGpu::MAX_ARCS + 1), S,
+      msc.device = cfg.device;
+      ok = ok && msc.ensure(RN * 2, std::max(Q, (RN * NM * 2 + CchGpu::MAX_ARCS - 1) / CchGpu::MAX_ARCS + 1), S,
                                 CchGpu::MAX_ARCS) == hipSuccess;
     }
     if (!ok) (void)hipGetLastError();       // best effort: the flushes grow what is missing
@@ -892,7 +903,7 @@ struct RouteService::Impl {
   // background build (on_built requeues them), the other groups proceed now.  Contexts of requests
   // routed at "now" are prefetched for the next week-hour shortly before the hour turns.
   bool cch_groups(Batch& b) {
-    const rtc::Stamp now = local_now();
+    const rtc::Stamp now = local_now(clock_skew_s);
     const int64_t days = (int64_t)std::floor((double)now.secs / 86400.0);
     const int64_t sec_of_day = now.secs - days * 86400;
     const int now_wh = (int)(((days + 3) % 7 + 7) % 7) * 24 + (int)(sec_of_day / 3600);
@@ -1002,86 +1013,104 @@ struct RouteService::Impl {
       b.host_cost[g] = host_costs(b.metrics[g]);
       if (!b.host_cost[g]) return false;
     }
+    // the flush's metrics as device views for the multi-context launches (b.metrics keeps them alive
+    // until the flush is done)
+    const size_t G = b.metrics.size();
+    if (G > 0) {
+      if (h_mv.need(G) || d_mv.need(G)) return false;
+      for (size_t g = 0; g < G; ++g) h_mv.h[g] = CchGpu::view(*b.metrics[g]);
+      if (hipMemcpyAsync(d_mv.d, h_mv.h, G * sizeof(CchMView), hipMemcpyHostToDevice, stream) != hipSuccess) return false;
+    }
     return true;
   }
 
-  // CCH: road-metre matrices of every multi-stop job (one sweep + meet launch per context group),
-  // then the greedy (K6) over them — the same kernel as the haversine path, on road distances
+  // CCH: road-metre matrices of every multi-stop job, then the greedy (K6) over them — the same
+  // kernel as the haversine path, on road distances.  The jobs of all context groups are ONE set of
+  // rows (grouped, a common row width) with each row's group: one upload, one matrix launch sequence
+  // over every row (the sweep / meet kernels read the row's metric from the flush's views), one
+  // greedy launch, one read-back and one wait — a flush spread over 64 routing contexts costs what
+  // a single-context flush of the same size costs.
   bool plan_multi_road(Batch& b) {
-    std::vector<RouteJob*> all;
-    for (RouteJob* j : b.jobs)
-      if (!j->fallback && j->req.error.empty() && j->req.dst.size() > 1) all.push_back(j);
     jrow.clear();
-    gtag.assign(b.metrics.size(), 0);
-    while (gsc.size() < b.metrics.size()) gsc.push_back(std::make_unique<CchScratch>());
-    if (all.empty()) return true;
-    for (size_t g = 0; g < b.metrics.size(); ++g) {
-      std::vector<RouteJob*> m;
-      for (RouteJob* j : all)
-        if (j->group == (int)g) m.push_back(j);
-      if (m.empty()) continue;
-      const int R = (int)m.size();
-      int NM = 1;
-      for (RouteJob* j : m) NM = std::max(NM, (int)j->req.dst.size() + 1);
-      if (NM > 4096) {
-        for (RouteJob* j : m) j->fallback = true;
-        continue;
-      }
-      const size_t RN = (size_t)R * NM;
-      if (h_pts.need(RN) || h_npts2.need(R) || h_dem.need(RN) || h_cap.need(R) || h_maxd.need(R) || h_visit.need(RN) ||
-          h_trip.need(RN) || h_ntrips.need(R) || h_status.need(R) || h_row0.need(RN) || d_pts.need(RN) ||
-          d_npts2.need(R) || d_dem.need(RN) || d_cap.need(R) || d_maxd.need(R) || d_D.need(RN * NM) ||
-          d_msec.need(RN * NM) || d_mmet.need(RN * NM) || d_visit.need(RN) || d_trip.need(RN) || d_ntrips.need(R) ||
-          d_status.need(R))
-        return false;
-      rtc::parallel_chunks((size_t)R, 64, 16, [&](size_t lo, size_t hi) {
-        for (size_t k = lo; k < hi; ++k) {
-          const rtr::RouteReq& r = m[k]->req;
-          const int n = (int)r.dst.size() + 1;
-          int* pt = h_pts.h + k * NM;
-          double* de = h_dem.h + k * NM;
-          std::fill(pt, pt + NM, 0);
-          std::fill(de, de + NM, 0.0);
-          pt[0] = grid.nearest(r.src.lat, r.src.lon, cfg.snap_c);
-          for (int i = 1; i < n; ++i) {
-            pt[i] = grid.nearest(r.dst[i - 1].lat, r.dst[i - 1].lon, cfg.snap_c);
-            de[i] = r.dst[i - 1].demand;
-          }
-          h_npts2.h[k] = n;
-          h_cap.h[k] = r.cap;
-          h_maxd.h[k] = r.maxd;
+    mtag = 0;
+    const int G = (int)b.metrics.size();
+    std::vector<std::vector<RouteJob*>> byg(G);
+    int NM = 1;
+    for (RouteJob* j : b.jobs)
+      if (!j->fallback && j->req.error.empty() && j->req.dst.size() > 1 && j->group >= 0 && j->group < G) {
+        if ((int)j->req.dst.size() + 1 > 4096) {
+          j->fallback = true;
+          continue;
         }
-      });
-      hipError_t e = hipSuccess;
-      auto cp = [&](void* d, const void* h, size_t bytes) {
-        if (e == hipSuccess) e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream);
-      };
-      cp(d_pts.d, h_pts.h, RN * 4);
-      cp(d_npts2.d, h_npts2.h, (size_t)R * 4);
-      cp(d_dem.d, h_dem.h, RN * 8);
-      cp(d_cap.d, h_cap.h, (size_t)R * 8);
-      cp(d_maxd.d, h_maxd.h, (size_t)R * 8);
-      if (e == hipSuccess)
-        e = cfg.cch->matrix(*b.metrics[g], d_pts.d, d_npts2.d, R, NM, d_msec.d, d_mmet.d, d_D.d, *gsc[g], stream);
-      gtag[g] = e == hipSuccess ? gsc[g]->chain_tag : 0;
-      for (int k = 0; k < R; ++k) jrow[m[k]] = k;
-      if (e == hipSuccess)
-        e = launch_greedy_cvrp(d_D.d, d_npts2.d, d_dem.d, d_cap.d, d_maxd.d, R, NM, d_visit.d, d_trip.d, d_ntrips.d,
-                               d_status.d, stream);
-      auto back = [&](void* h, const void* d, size_t bytes) {
-        if (e == hipSuccess) e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream);
-      };
-      back(h_visit.h, d_visit.d, RN * 4);
-      back(h_trip.h, d_trip.d, RN * 4);
-      back(h_ntrips.h, d_ntrips.d, (size_t)R * 4);
-      back(h_status.h, d_status.d, (size_t)R * 4);
-      if (e == hipSuccess)
-        e = hipMemcpy2DAsync(h_row0.h, (size_t)NM * 8, d_D.d, (size_t)NM * NM * 8, (size_t)NM * 8, (size_t)R,
-                             hipMemcpyDeviceToHost, stream);
-      if (e == hipSuccess) e = sync(stream, ev_gpu);
-      if (e != hipSuccess) return false;
-      for (int k = 0; k < R; ++k) unpack_plan(m[k], h_npts2.h[k], NM, k);
+        byg[j->group].push_back(j);
+        NM = std::max(NM, (int)j->req.dst.size() + 1);
+      }
+    std::vector<RouteJob*> m;                  // all rows, grouped
+    std::vector<int> r0(G + 1, 0);
+    for (int g = 0; g < G; ++g) {
+      r0[g] = (int)m.size();
+      m.insert(m.end(), byg[g].begin(), byg[g].end());
     }
+    r0[G] = (int)m.size();
+    if (m.empty()) return true;
+    const int R = (int)m.size();
+    const size_t RN = (size_t)R * NM;
+    if (h_pts.need(RN) || h_npts2.need(R) || h_dem.need(RN) || h_cap.need(R) || h_maxd.need(R) || h_visit.need(RN) ||
+        h_trip.need(RN) || h_ntrips.need(R) || h_status.need(R) || h_row0.need(RN) || d_pts.need(RN) ||
+        d_npts2.need(R) || d_dem.need(RN) || d_cap.need(R) || d_maxd.need(R) || d_D.need(RN * NM) ||
+        d_msec.need(RN * NM) || d_mmet.need(RN * NM) || d_visit.need(RN) || d_trip.need(RN) || d_ntrips.need(R) ||
+        d_status.need(R) || h_rowg.need(R) || d_rowg.need(R))
+      return false;
+    for (int g = 0; g < G; ++g)
+      for (int k = r0[g]; k < r0[g + 1]; ++k) h_rowg.h[k] = g;
+    rtc::parallel_chunks((size_t)R, 64, 16, [&](size_t lo, size_t hi) {
+      for (size_t k = lo; k < hi; ++k) {
+        const rtr::RouteReq& r = m[k]->req;
+        const int n = (int)r.dst.size() + 1;
+        int* pt = h_pts.h + k * NM;
+        double* de = h_dem.h + k * NM;
+        std::fill(pt, pt + NM, 0);
+        std::fill(de, de + NM, 0.0);
+        pt[0] = grid.nearest(r.src.lat, r.src.lon, cfg.snap_c);
+        for (int i = 1; i < n; ++i) {
+          pt[i] = grid.nearest(r.dst[i - 1].lat, r.dst[i - 1].lon, cfg.snap_c);
+          de[i] = r.dst[i - 1].demand;
+        }
+        h_npts2.h[k] = n;
+        h_cap.h[k] = r.cap;
+        h_maxd.h[k] = r.maxd;
+      }
+    });
+    hipError_t e = hipSuccess;
+    auto cp = [&](void* d, const void* h, size_t bytes) {
+      if (e == hipSuccess) e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream);
+    };
+    cp(d_pts.d, h_pts.h, RN * 4);
+    cp(d_npts2.d, h_npts2.h, (size_t)R * 4);
+    cp(d_dem.d, h_dem.h, RN * 8);
+    cp(d_cap.d, h_cap.h, (size_t)R * 8);
+    cp(d_maxd.d, h_maxd.h, (size_t)R * 8);
+    cp(d_rowg.d, h_rowg.h, (size_t)R * 4);
+    if (e == hipSuccess)
+      e = cfg.cch->matrix_multi(d_mv.d, d_rowg.d, d_pts.d, d_npts2.d, R, NM, d_msec.d, d_mmet.d, d_D.d, msc, stream);
+    mtag = e == hipSuccess ? msc.chain_tag : 0;
+    for (int k = 0; k < R; ++k) jrow[m[k]] = k;
+    if (e == hipSuccess)
+      e = launch_greedy_cvrp(d_D.d, d_npts2.d, d_dem.d, d_cap.d, d_maxd.d, R, NM, d_visit.d, d_trip.d, d_ntrips.d,
+                             d_status.d, stream);
+    auto back = [&](void* h, const void* d, size_t bytes) {
+      if (e == hipSuccess) e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream);
+    };
+    back(h_visit.h, d_visit.d, RN * 4);
+    back(h_trip.h, d_trip.d, RN * 4);
+    back(h_ntrips.h, d_ntrips.d, (size_t)R * 4);
+    back(h_status.h, d_status.d, (size_t)R * 4);
+    if (e == hipSuccess)
+      e = hipMemcpy2DAsync(h_row0.h, (size_t)NM * 8, d_D.d, (size_t)NM * NM * 8, (size_t)NM * 8, (size_t)R,
+                           hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = sync(stream, ev_gpu);
+    if (e != hipSuccess) return false;
+    for (int k = 0; k < R; ++k) unpack_plan(m[k], h_npts2.h[k], NM, k);
     return true;
   }
 
@@ -1144,7 +1173,7 @@ struct RouteService::Impl {
     };
     for (RouteJob* j : g) {
       int row = -1;
-      if (gtag.size() > (size_t)j->group && gtag[j->group] != 0 && !j->plan.trips.empty()) {
+      if (mtag != 0 && !j->plan.trips.empty()) {
         auto it = jrow.find(j);
         if (it != jrow.end()) row = it->second;
       }
@@ -1188,70 +1217,75 @@ struct RouteService::Impl {
           want(j->group, j->alt_pairs[k].first, w, -1, 0, 0);
           want(j->group, w, j->alt_pairs[k].second, -1, 0, 0);
         }
-    std::vector<int> nA(G);
+    // leg order: every group's matrix-derived legs (group order), then every other leg (group order)
+    int QA = 0, QR = 0;
     for (int gi = 0; gi < G; ++gi) {
-      nA[gi] = (int)pairs[gi].size();
-      pairs[gi].insert(pairs[gi].end(), rest[gi].begin(), rest[gi].end());
+      QA += (int)pairs[gi].size();
+      QR += (int)rest[gi].size();
     }
-    int Q = 0;
-    std::vector<int> goff(G + 1, 0);
-    for (int gi = 0; gi < G; ++gi) goff[gi + 1] = goff[gi] + (int)pairs[gi].size();
-    Q = goff[G];
-    for (int gi = 0; gi < G; ++gi)
-      for (size_t i = 0; i < pairs[gi].size(); ++i)
-        leg_index[leg_key(gi, pairs[gi][i].first, pairs[gi][i].second)] = goff[gi] + (int)i;
+    const int Q = QA + QR;
+    {
+      int a = 0, r = QA;
+      for (int gi = 0; gi < G; ++gi) {
+        for (const auto& pr : pairs[gi]) leg_index[leg_key(gi, pr.first, pr.second)] = a++;
+        for (const auto& pr : rest[gi]) leg_index[leg_key(gi, pr.first, pr.second)] = r++;
+      }
+    }
     legs.assign(Q, rtr::Leg());
     if (Q == 0) return true;
     n_legs.fetch_add(Q, std::memory_order_relaxed);
     const int MP = cfg.max_path;
     if (h_src.need(Q) || h_dst.need(Q) || h_len.need(Q) || h_st.need(Q) || h_cost.need(Q) || h_met.need(Q) ||
         h_off.need(Q) || d_src.need(Q) || d_dst.need(Q) || d_len.need(Q) || d_st.need(Q) || d_cost.need(Q) ||
-        d_met.need(Q) || d_off.need(Q) || d_path.need((size_t)Q * MP) || d_edge.need((size_t)Q * MP))
+        d_met.need(Q) || d_off.need(Q) || d_path.need((size_t)Q * MP) || d_edge.need((size_t)Q * MP) ||
+        h_lgrp.need(Q) || d_lgrp.need(Q))
       return false;
-    for (int gi = 0; gi < G; ++gi)
-      for (size_t i = 0; i < pairs[gi].size(); ++i) {
-        h_src.h[goff[gi] + i] = pairs[gi][i].first;
-        h_dst.h[goff[gi] + i] = pairs[gi][i].second;
-      }
-    hipError_t e = hipMemcpyAsync(d_src.d, h_src.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_dst.d, h_dst.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
-    int QA = 0;
-    for (int gi = 0; gi < G; ++gi) QA += nA[gi];
-    if (QA > 0) {
-      if (h_lr.need(QA) || h_li.need(QA) || h_lj.need(QA) || d_lr.need(QA) || d_li.need(QA) || d_lj.need(QA)) return false;
-      int a = 0;
-      for (int gi = 0; gi < G; ++gi)
-        for (int k = 0; k < nA[gi]; ++k, ++a) {
+    if (QA > 0 && (h_lr.need(QA) || h_li.need(QA) || h_lj.need(QA) || d_lr.need(QA) || d_li.need(QA) || d_lj.need(QA)))
+      return false;
+    {
+      int a = 0, r = QA;
+      for (int gi = 0; gi < G; ++gi) {
+        for (size_t k = 0; k < pairs[gi].size(); ++k, ++a) {
+          h_src.h[a] = pairs[gi][k].first;
+          h_dst.h[a] = pairs[gi][k].second;
+          h_lgrp.h[a] = gi;
           h_lr.h[a] = tri[gi][k][0];
           h_li.h[a] = tri[gi][k][1];
           h_lj.h[a] = tri[gi][k][2];
         }
+        for (const auto& pr : rest[gi]) {
+          h_src.h[r] = pr.first;
+          h_dst.h[r] = pr.second;
+          h_lgrp.h[r] = gi;
+          ++r;
+        }
+      }
+    }
+    hipError_t e = hipMemcpyAsync(d_src.d, h_src.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_dst.d, h_dst.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_lgrp.d, h_lgrp.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
+    if (QA > 0) {
       if (e == hipSuccess) e = hipMemcpyAsync(d_lr.d, h_lr.h, (size_t)QA * 4, hipMemcpyHostToDevice, stream);
       if (e == hipSuccess) e = hipMemcpyAsync(d_li.d, h_li.h, (size_t)QA * 4, hipMemcpyHostToDevice, stream);
       if (e == hipSuccess) e = hipMemcpyAsync(d_lj.d, h_lj.h, (size_t)QA * 4, hipMemcpyHostToDevice, stream);
     }
-    for (int gi = 0, a0 = 0; gi < G && e == hipSuccess; a0 += nA[gi], ++gi) {
-      const int q0 = goff[gi], n = goff[gi + 1] - goff[gi];
-      if (n == 0) continue;
-      auto out_at = [&](int q) {
-        CchRouteOut o;
-        o.sec = d_cost.d + q;
-        o.metres = d_met.d + q;
-        o.status = d_st.d + q;
-        o.len = d_len.d + q;
-        o.path = d_path.d + (size_t)q * MP;
-        o.edges = d_edge.d + (size_t)q * MP;
-        o.max_path = MP;
-        return o;
-      };
-      if (nA[gi] > 0)
-        e = cfg.cch->legs_from_matrix(*b.metrics[gi], d_src.d + q0, d_lr.d + a0, d_li.d + a0, d_lj.d + a0, nA[gi],
-                                      gtag[gi], out_at(q0), *gsc[gi], stream);
-      if (e == hipSuccess && n > nA[gi])
-        e = cfg.cch->route(*b.metrics[gi], d_src.d + q0 + nA[gi], d_dst.d + q0 + nA[gi], n - nA[gi], out_at(q0 + nA[gi]),
-                           csc, stream);
-      n_legs_reused.fetch_add(nA[gi], std::memory_order_relaxed);
-    }
+    auto out_at = [&](int q) {
+      CchRouteOut o;
+      o.sec = d_cost.d + q;
+      o.metres = d_met.d + q;
+      o.status = d_st.d + q;
+      o.len = d_len.d + q;
+      o.path = d_path.d + (size_t)q * MP;
+      o.edges = d_edge.d + (size_t)q * MP;
+      o.max_path = MP;
+      return o;
+    };
+    if (e == hipSuccess && QA > 0)
+      e = cfg.cch->legs_from_matrix_multi(d_mv.d, d_lgrp.d, d_src.d, d_lr.d, d_li.d, d_lj.d, QA, mtag, out_at(0), msc,
+                                          stream);
+    if (e == hipSuccess && QR > 0)
+      e = cfg.cch->route_multi(d_mv.d, d_lgrp.d + QA, d_src.d + QA, d_dst.d + QA, QR, out_at(QA), csc, stream);
+    n_legs_reused.fetch_add(QA, std::memory_order_relaxed);
     if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h_len.h, d_len.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h_cost.h, d_cost.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
@@ -1292,8 +1326,8 @@ struct RouteService::Impl {
     int nbad = 0;
     for (int i = 0; i < Q; ++i) nbad += h_st.h[i] == 4;
     b.host_paths.resize(Q);
-    for (int gi = 0; gi < G; ++gi)
-      for (int i = goff[gi]; i < goff[gi + 1]; ++i) {
+    for (int i = 0; i < Q; ++i) {
+        const int gi = h_lgrp.h[i];
         rtr::Leg& L = legs[i];
         if (h_st.h[i] == 0) {
           L.sec = h_cost.h[i];
