@@ -248,7 +248,9 @@ class Bench:
                    "cached_max_before_ms": max(w["max_ms"] for w in base),
                    "cached_p99_during_ms": max(w["p99_ms"] for w in during),
                    "cached_max_during_ms": max(w["max_ms"] for w in during),
-                   "async_built": stats.get("async_built"), **self.delta(st, s0)}
+                   **{k: stats.get(k) for k in ("async_built", "async_build_ms", "async_alloc_ms",
+                                                "async_hostcopy_ms")},
+                   **self.delta(st, s0)}
         finally:
             self.close(st, sv, store)
         emit(out)

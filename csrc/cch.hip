@@ -1248,16 +1248,7 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   ck(up_copy(d_bofs, bofs_.data(), N + 1));
   ck(up_copy(d_pofs, pofs_.data(), N + 1));
   ck(up_copy(d_aofs, aofs_.data(), N + 1));
-  ck(dmalloc(d_up64, M));
-  ck(dmalloc(d_dn64, M));
-  ck(dmalloc(d_pup, M));
-  ck(dmalloc(d_pdn, M));
-  ck(dmalloc(d_fcnt, N));
-  ck(dmalloc(d_bcnt, N));
-  size_t tb = 0;
-  ck(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_fcnt, d_fcnt, N));
-  cub_bytes = tb;
-  ck(hipMalloc(&d_cub, cub_bytes ? cub_bytes : 1));
+  ck(alloc_scratch(cs0_));
   // triangle table within ROUTEST_CCH_TRI_GB of HBM (default 48 — a 1M-node city needs ~38 GB of the 288; 0 disables)
   if (e == hipSuccess) {
     std::vector<int64_t> tofs(N + 1, 0);
@@ -1344,7 +1335,9 @@ CchGpu::~CchGpu() {
     bq_.clear();
   }
   bcv_.notify_all();
-  if (bth_.joinable()) bth_.join();
+  for (auto& t : bths_)
+    if (t.joinable()) t.join();
+  for (auto& x : bscr_) free_scratch(*x);
   {
     std::lock_guard<std::mutex> lk(mu_);
     cache_.clear();
@@ -1373,15 +1366,7 @@ CchGpu::~CchGpu() {
   dfree(d_tri);
   dfree(d_btask);
   dfree(d_ptask);
-  dfree(d_up64);
-  dfree(d_dn64);
-  dfree(d_pup);
-  dfree(d_pdn);
-  dfree(d_fcnt);
-  dfree(d_bcnt);
-  if (d_cub) (void)hipFree(d_cub);
-  if (rec_buf) (void)hipFree(rec_buf);
-  dfree(min_buf);
+  free_scratch(cs0_);
   (void)hipSetDevice(cur);
 }
 
@@ -1394,10 +1379,52 @@ void CchGpu::set_eta(const void* blob, int H, const NormParams& np, int variant,
   eta_cus_ = num_cus;
 }
 
-hipError_t CchGpu::context_costs(const CchContext& c, float* d_cost, hipStream_t s) {
+hipError_t CchGpu::alloc_scratch(CustScratch& x) {
+  const int N = T_.N;
+  const int64_t M = T_.M;
+  hipError_t e = hipSuccess;
+  auto ck = [&](hipError_t r) {
+    if (r != hipSuccess && e == hipSuccess) e = r;
+  };
+  ck(dmalloc(x.up64, M));
+  ck(dmalloc(x.dn64, M));
+  ck(dmalloc(x.pup, M));
+  ck(dmalloc(x.pdn, M));
+  ck(dmalloc(x.fcnt, N));
+  ck(dmalloc(x.bcnt, N));
+  size_t tb = 0;
+  ck(hipcub::DeviceScan::InclusiveSum(nullptr, tb, x.fcnt, x.fcnt, N));
+  x.cub_bytes = tb;
+  ck(hipMalloc(&x.cub, x.cub_bytes ? x.cub_bytes : 1));
+  ck(hipHostMalloc((void**)&x.h_stage, (size_t)std::max<int64_t>(1, T_.E) * sizeof(float), hipHostMallocDefault));
+  return e;
+}
+
+void CchGpu::free_scratch(CustScratch& x) {
+  dfree(x.up64);
+  dfree(x.dn64);
+  dfree(x.pup);
+  dfree(x.pdn);
+  dfree(x.fcnt);
+  dfree(x.bcnt);
+  if (x.cub) (void)hipFree(x.cub);
+  x.cub = nullptr;
+  if (x.rec_buf) (void)hipFree(x.rec_buf);
+  x.rec_buf = nullptr;
+  dfree(x.min_buf);
+  if (x.h_stage) (void)hipHostFree(x.h_stage);
+  x.h_stage = nullptr;
+}
+
+hipError_t CchGpu::context_costs(const CchContext& c, float* d_cost, hipStream_t s, CustScratch* cs) {
   if (eta_blob_ == nullptr || d_class == nullptr || d_base_traffic == nullptr) return hipErrorInvalidValue;
   const int E = (int)T_.E;
   hipError_t e = hipSuccess;
+  std::unique_lock<std::mutex> lk(mu_cust_, std::defer_lock);
+  if (cs == nullptr) lk.lock();
+  CustScratch& X = cs ? *cs : cs0_;
+  void*& rec_buf = X.rec_buf;
+  float*& min_buf = X.min_buf;
   if (rec_buf == nullptr) {
     if ((e = hipMalloc(&rec_buf, (size_t)2 * E * sizeof(EtaRecordDev))) != hipSuccess) return e;
     if ((e = dmalloc(min_buf, (size_t)2 * E)) != hipSuccess) return e;
@@ -1408,11 +1435,16 @@ hipError_t CchGpu::context_costs(const CchContext& c, float* d_cost, hipStream_t
   e = launch_eta_mlp3_fwd(rec_buf, min_buf, 2 * E, eta_blob_, eta_H_, eta_np_, eta_variant_, eta_cus_, s, 16);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(ctx_cost_kernel, dim3(blocks_for(E, 256)), dim3(256), 0, s, min_buf, d_length, d_class, E, d_cost);
-  return hipGetLastError();
+  e = hipGetLastError();
+  // the shared temporaries are free again only once this stream has consumed them
+  if (e == hipSuccess && cs == nullptr) e = hipStreamSynchronize(s);
+  return e;
 }
 
-hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s) {
-  std::lock_guard<std::mutex> lk(mu_cust_);
+hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s, CustScratch* cs) {
+  std::unique_lock<std::mutex> lk(mu_cust_, std::defer_lock);
+  if (cs == nullptr) lk.lock();
+  CustScratch& X = cs ? *cs : cs0_;
   auto t0 = std::chrono::steady_clock::now();
   const int N = T_.N;
   const int64_t M = T_.M, E = T_.E;
@@ -1421,6 +1453,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   auto ck = [&](hipError_t x) {
     if (x != hipSuccess && e == hipSuccess) e = x;
   };
+  const auto ta = std::chrono::steady_clock::now();
   if (m.cost == nullptr) ck(dmalloc(m.cost, E));
   if (m.sub_up == nullptr) {
     ck(dmalloc(m.sub_up, 2 * M));
@@ -1432,13 +1465,14 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     ck(dmalloc(m.f_ptr, N + 1));
     ck(dmalloc(m.b_ptr, N + 1));
   }
+  m.alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
   if (e != hipSuccess) return e;
   if (d_cost != m.cost) ck(hipMemcpyAsync(m.cost, d_cost, E * sizeof(float), hipMemcpyDeviceToDevice, s));
   const int fill_blocks = (int)std::min<int64_t>(4096, (M + 255) / 256 + 1);
-  hipLaunchKernelGGL(fill_u64_kernel, dim3(fill_blocks), dim3(256), 0, s, d_up64, (long long)M, PACK_INF_D);
-  hipLaunchKernelGGL(fill_u64_kernel, dim3(fill_blocks), dim3(256), 0, s, d_dn64, (long long)M, PACK_INF_D);
+  hipLaunchKernelGGL(fill_u64_kernel, dim3(fill_blocks), dim3(256), 0, s, X.up64, (long long)M, PACK_INF_D);
+  hipLaunchKernelGGL(fill_u64_kernel, dim3(fill_blocks), dim3(256), 0, s, X.dn64, (long long)M, PACK_INF_D);
   hipLaunchKernelGGL(edge_scatter_kernel, dim3(blocks_for(E, 256)), dim3(256), 0, s, m.cost, d_edge_arc, d_edge_dir,
-                     (int)E, d_up64, d_dn64);
+                     (int)E, X.up64, X.dn64);
   ck(hipGetLastError());
   static const bool skip = [] {
     const char* v = std::getenv("ROUTEST_CCH_SKIP");
@@ -1465,12 +1499,12 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     if (nt <= 0) continue;
     if (skip)
       hipLaunchKernelGGL(basic_task_kernel<true>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
-                         (const CustTask*)d_btask + btask_ptr_[h], nt, d_up_ptr, d_up_head, d_tofs, d_tri, d_up64,
-                         d_dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
+                         (const CustTask*)d_btask + btask_ptr_[h], nt, d_up_ptr, d_up_head, d_tofs, d_tri, X.up64,
+                         X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
     else
       hipLaunchKernelGGL(basic_task_kernel<false>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
-                         (const CustTask*)d_btask + btask_ptr_[h], nt, d_up_ptr, d_up_head, d_tofs, d_tri, d_up64,
-                         d_dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
+                         (const CustTask*)d_btask + btask_ptr_[h], nt, d_up_ptr, d_up_head, d_tofs, d_tri, X.up64,
+                         X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
     ck(hipGetLastError());
   }
   for (int h = 0; h <= T_.max_height && e == hipSuccess && !tasks; ++h) {
@@ -1480,16 +1514,16 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     L.items = bofs_[L.hi] - bofs_[L.lo];
     if (L.items <= 0) continue;
     if (skip)
-      hipLaunchKernelGGL(basic_level_kernel<true>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
+      hipLaunchKernelGGL(basic_level_kernel<true>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
                          m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
     else
-      hipLaunchKernelGGL(basic_level_kernel<false>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
+      hipLaunchKernelGGL(basic_level_kernel<false>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
                          m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
     ck(hipGetLastError());
   }
   if (ev[1]) (void)hipEventRecord(ev[1], s);
   // perfect, top-down by depth
-  hipLaunchKernelGGL(perfect_init_kernel, dim3(fill_blocks), dim3(256), 0, s, d_up64, d_dn64, d_pup, d_pdn, (long long)M);
+  hipLaunchKernelGGL(perfect_init_kernel, dim3(fill_blocks), dim3(256), 0, s, X.up64, X.dn64, X.pup, X.pdn, (long long)M);
   ck(hipGetLastError());
   // pull (default with the triangle table; ROUTEST_CCH_PERFECT=push: the atomic kernel)
   static const bool pull = [] {
@@ -1507,8 +1541,8 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     const long long nt = ptask_ptr_[d + 1] - ptask_ptr_[d];
     if (nt <= 0) continue;
     hipLaunchKernelGGL(perfect_task_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
-                       (const CustTask*)d_ptask + ptask_ptr_[d], nt, d_up_ptr, d_up_head, d_tofs, d_tri, d_up64, d_dn64,
-                       d_pup, d_pdn);
+                       (const CustTask*)d_ptask + ptask_ptr_[d], nt, d_up_ptr, d_up_head, d_tofs, d_tri, X.up64, X.dn64,
+                       X.pup, X.pdn);
     ck(hipGetLastError());
   }
   for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && pull && d_tri != nullptr; ++d) {
@@ -1518,11 +1552,11 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     if (P.arcs <= 0 || pofs_[hi] == pofs_[lo]) continue;       // no node of the level has two arcs
     // mean degree of the level's nodes: wide nodes get a wave per arc, narrow ones a lane per arc
     if (P.arcs >= 24 * (long long)(hi - lo))
-      hipLaunchKernelGGL(perfect_pull_wave_kernel, dim3((unsigned)((P.arcs + 3) / 4)), dim3(256), 0, s, P, d_up64,
-                         d_dn64, d_pup, d_pdn);
+      hipLaunchKernelGGL(perfect_pull_wave_kernel, dim3((unsigned)((P.arcs + 3) / 4)), dim3(256), 0, s, P, X.up64,
+                         X.dn64, X.pup, X.pdn);
     else
-      hipLaunchKernelGGL(perfect_pull_lane_kernel, dim3(blocks_for(P.arcs, 256)), dim3(256), 0, s, P, d_up64, d_dn64,
-                         d_pup, d_pdn);
+      hipLaunchKernelGGL(perfect_pull_lane_kernel, dim3(blocks_for(P.arcs, 256)), dim3(256), 0, s, P, X.up64, X.dn64,
+                         X.pup, X.pdn);
     ck(hipGetLastError());
   }
   for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && !(pull && d_tri != nullptr); ++d) {
@@ -1532,24 +1566,24 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     L.items = pofs_[L.hi] - pofs_[L.lo];
     if (L.items <= 0) continue;
     if (skip)
-      hipLaunchKernelGGL(perfect_level_kernel<true>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
-                         d_pup, d_pdn);
+      hipLaunchKernelGGL(perfect_level_kernel<true>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
+                         X.pup, X.pdn);
     else
-      hipLaunchKernelGGL(perfect_level_kernel<false>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, d_up64, d_dn64,
-                         d_pup, d_pdn);
+      hipLaunchKernelGGL(perfect_level_kernel<false>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
+                         X.pup, X.pdn);
     ck(hipGetLastError());
   }
   if (ev[2]) (void)hipEventRecord(ev[2], s);
   // prune + compact
-  hipLaunchKernelGGL(prune_count_wave_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, d_up_ptr, d_pup, d_pdn,
-                     d_up64, d_dn64, N, d_fcnt, d_bcnt);
+  hipLaunchKernelGGL(prune_count_wave_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, d_up_ptr, X.pup, X.pdn,
+                     X.up64, X.dn64, N, X.fcnt, X.bcnt);
   ck(hipGetLastError());
   ck(hipMemsetAsync(m.f_ptr, 0, sizeof(int32_t), s));
   ck(hipMemsetAsync(m.b_ptr, 0, sizeof(int32_t), s));
-  size_t tb = cub_bytes;
-  ck(hipcub::DeviceScan::InclusiveSum(d_cub, tb, d_fcnt, m.f_ptr + 1, N, s));
-  tb = cub_bytes;
-  ck(hipcub::DeviceScan::InclusiveSum(d_cub, tb, d_bcnt, m.b_ptr + 1, N, s));
+  size_t tb = X.cub_bytes;
+  ck(hipcub::DeviceScan::InclusiveSum(X.cub, tb, X.fcnt, m.f_ptr + 1, N, s));
+  tb = X.cub_bytes;
+  ck(hipcub::DeviceScan::InclusiveSum(X.cub, tb, X.bcnt, m.b_ptr + 1, N, s));
   int32_t tot[2] = {0, 0};
   ck(hipMemcpyAsync(&tot[0], m.f_ptr + N, 4, hipMemcpyDeviceToHost, s));
   ck(hipMemcpyAsync(&tot[1], m.b_ptr + N, 4, hipMemcpyDeviceToHost, s));
@@ -1567,7 +1601,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   m.kept_b = tot[1];
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(prune_scatter_wave_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, d_up_ptr, d_up_head,
-                     d_depth, d_pup, d_pdn, d_up64, d_dn64, N, m.f_ptr, m.b_ptr, m.f_rec, m.b_rec);
+                     d_depth, X.pup, X.pdn, X.up64, X.dn64, N, m.f_ptr, m.b_ptr, m.f_rec, m.b_rec);
   ck(hipGetLastError());
   if (ev[3]) (void)hipEventRecord(ev[3], s);
   ck(hipStreamSynchronize(s));
@@ -1579,10 +1613,20 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   // the host copy of the costs (maneuver durations, the exact host fallback) is made here, on the
   // builder's stream, before the metric is published: a flush that first meets this context finds
   // it ready instead of copying E floats on its own critical path
+  // (through the scratch's pinned stage: a pageable copy is staged by the runtime in pieces on the
+  // copy engines the flushes' transfers use)
+  const auto th = std::chrono::steady_clock::now();
   m.host_cost.resize((size_t)E);
-  ck(hipMemcpyAsync(m.host_cost.data(), m.cost, (size_t)E * sizeof(float), hipMemcpyDeviceToHost, s));
-  ck(hipStreamSynchronize(s));
+  if (X.h_stage != nullptr) {
+    ck(hipMemcpyAsync(X.h_stage, m.cost, (size_t)E * sizeof(float), hipMemcpyDeviceToHost, s));
+    ck(hipStreamSynchronize(s));
+    if (e == hipSuccess) std::memcpy(m.host_cost.data(), X.h_stage, (size_t)E * sizeof(float));
+  } else {
+    ck(hipMemcpyAsync(m.host_cost.data(), m.cost, (size_t)E * sizeof(float), hipMemcpyDeviceToHost, s));
+    ck(hipStreamSynchronize(s));
+  }
   if (e != hipSuccess) m.host_cost.clear();
+  m.hostcopy_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
   return e;
 }
 
@@ -1639,7 +1683,17 @@ void CchGpu::request_build(const CchContext& c, bool urgent) {
     if (bstop_ || !bpending_.insert(key).second) return;   // stopping, or already queued / building
     if (urgent) bq_.push_front(c);
     else bq_.push_back(c);
-    if (!bth_.joinable()) bth_ = std::thread([this] { builder_loop(); });
+    if (bths_.empty()) {
+      // ROUTEST_CCH_BUILDERS concurrent builders (default 3), each with its own temporaries: a
+      // customization is a chain of dependent level launches that keeps a fraction of the GPU busy,
+      // so a burst of fresh contexts builds several at a time
+      static const int nb = [] {
+        const char* v = std::getenv("ROUTEST_CCH_BUILDERS");
+        const int k = v ? std::atoi(v) : 3;
+        return k < 1 ? 1 : (k > 8 ? 8 : k);
+      }();
+      for (int i = 0; i < nb; ++i) bths_.emplace_back([this, i] { builder_loop(i); });
+    }
   }
   n_bqueued_.fetch_add(1, std::memory_order_relaxed);
   bcv_.notify_one();
@@ -1670,19 +1724,57 @@ CchGpu::AsyncStats CchGpu::async_stats() {
   a.queued = n_bqueued_.load();
   a.built = n_bbuilt_.load();
   a.failed = n_bfailed_.load();
+  a.build_ms = us_build_.load() / 1e3;
+  a.alloc_ms = us_alloc_.load() / 1e3;
+  a.hostcopy_ms = us_hostcopy_.load() / 1e3;
   std::lock_guard<std::mutex> lk(bmu_);
   a.pending = (int)bpending_.size();
   return a;
 }
 
-void CchGpu::builder_loop() {
+void CchGpu::builder_loop(int idx) {
+  (void)idx;
   if (hipSetDevice(dev_) != hipSuccess) return;
-  int least = 0, greatest = 0;
+  CustScratch* xs = nullptr;                // this builder's temporaries (freed by the destructor)
+  {
+    auto x = std::make_unique<CustScratch>();
+    if (alloc_scratch(*x) == hipSuccess) {
+      xs = x.get();
+      std::lock_guard<std::mutex> lk(bmu_);
+      bscr_.push_back(std::move(x));
+    } else {
+      free_scratch(*x);
+      (void)hipGetLastError();              // builds below share cs0_ (under mu_cust_)
+    }
+  }
   hipStream_t s = nullptr;
-  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
-      hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least) != hipSuccess) {
-    (void)hipGetLastError();
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  // The builder's kernels run on one CU in every ROUTEST_CCH_BUILDER_CU_SHARE (default 4: 64 of
+  // the 256, spread over every XCD): a stream priority only orders dispatch, and the wide leaf
+  // levels of a 1M-node customization otherwise fill every CU while the flushes' query kernels
+  // wait for slots.  The customization is latency-bound (one dependent level after another), so
+  // a quarter of the CUs costs it little.  1: all CUs, lowest priority.
+  static const int share = [] {
+    const char* v = std::getenv("ROUTEST_CCH_BUILDER_CU_SHARE");
+    const int k = v ? std::atoi(v) : 4;
+    return k < 1 ? 1 : k;
+  }();
+  if (share > 1) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_) != hipSuccess || cus <= 0) cus = 256;
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+    for (int c = share - 1; c < cus; c += share) mask[(size_t)c / 32] |= 1u << (c % 32);
+    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+      (void)hipGetLastError();
+      s = nullptr;
+    }
+  }
+  if (s == nullptr) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least) != hipSuccess) {
+      (void)hipGetLastError();
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+    }
   }
   while (true) {
     CchContext c;
@@ -1695,7 +1787,13 @@ void CchGpu::builder_loop() {
     }
     std::shared_ptr<CchMetricDev> m;
     bool fresh = false;
-    const bool ok = s != nullptr && metric_for(c, s, m, &fresh) == hipSuccess;
+    const auto tb = std::chrono::steady_clock::now();
+    const bool ok = s != nullptr && metric_for(c, s, m, &fresh, xs) == hipSuccess;
+    if (ok && fresh && m) {
+      us_build_.fetch_add((long long)(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tb).count()));
+      us_alloc_.fetch_add((long long)(m->alloc_ms * 1e3));
+      us_hostcopy_.fetch_add((long long)(m->hostcopy_ms * 1e3));
+    }
     if (!ok) (void)hipGetLastError();
     (ok ? n_bbuilt_ : n_bfailed_).fetch_add(1, std::memory_order_relaxed);
     {
@@ -1718,27 +1816,44 @@ bool CchGpu::cached_metric(uint64_t key, std::shared_ptr<CchMetricDev>& out) {
   return false;
 }
 
-hipError_t CchGpu::metric_for(const CchContext& c, hipStream_t s, std::shared_ptr<CchMetricDev>& out, bool* fresh) {
+hipError_t CchGpu::metric_for(const CchContext& c, hipStream_t s, std::shared_ptr<CchMetricDev>& out, bool* fresh,
+                              CustScratch* cs) {
   const uint64_t key = c.key();
   if (fresh) *fresh = false;
   auto lookup = [&]() -> bool { return cached_metric(key, out); };
   if (lookup()) return hipSuccess;
-  std::lock_guard<std::mutex> bl(mu_build_);   // one context build at a time (others wait, then hit)
-  if (lookup()) return hipSuccess;
+  {
+    // a context another caller is building: wait for it, then hit; different contexts build
+    // concurrently (each caller on its own stream and temporaries)
+    std::unique_lock<std::mutex> lk(mu_inflight_);
+    cv_inflight_.wait(lk, [&] { return inflight_.count(key) == 0; });
+    if (lookup()) return hipSuccess;
+    inflight_.insert(key);
+  }
+  struct Done {
+    CchGpu* g;
+    uint64_t k;
+    ~Done() {
+      {
+        std::lock_guard<std::mutex> lk(g->mu_inflight_);
+        g->inflight_.erase(k);
+      }
+      g->cv_inflight_.notify_all();
+    }
+  } done{this, key};
   auto m = std::make_shared<CchMetricDev>();
   m->key = key;
   m->device = dev_;
+  const auto ta = std::chrono::steady_clock::now();
   hipError_t e = dmalloc(m->cost, T_.E);
+  m->alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
   if (e != hipSuccess) return e;
   auto t0 = std::chrono::steady_clock::now();
-  {
-    std::lock_guard<std::mutex> lk(mu_cust_);
-    e = context_costs(c, m->cost, s);
-  }
+  e = context_costs(c, m->cost, s, cs);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return e;
   m->cost_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  e = customize(m->cost, *m, s);
+  e = customize(m->cost, *m, s, cs);
   if (e != hipSuccess) return e;
   insert_cached(m);
   out = m;

@@ -99,6 +99,9 @@ class PyCchGpu {
     d["async_built"] = a.built;
     d["async_failed"] = a.failed;
     d["async_pending"] = a.pending;
+    d["async_build_ms"] = a.build_ms;
+    d["async_alloc_ms"] = a.alloc_ms;
+    d["async_hostcopy_ms"] = a.hostcopy_ms;
     return d;
   }
 

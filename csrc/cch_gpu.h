@@ -51,6 +51,7 @@ struct CchMetricDev {
   int64_t kept_f = 0, kept_b = 0;
   double customize_ms = 0.0, cost_ms = 0.0;
   double basic_ms = 0.0, perfect_ms = 0.0, prune_ms = 0.0;   // device time per phase
+  double alloc_ms = 0.0, hostcopy_ms = 0.0;                    // its device allocations; the host copy
   std::vector<float> host_cost;    // [E] the costs on the host (filled by customize before publishing)
   ~CchMetricDev();
 };
@@ -73,6 +74,19 @@ struct CchScratch {
   std::vector<void*> old;          // outgrown buffers, freed with the scratch
   ~CchScratch();
   hipError_t ensure(size_t jobs, size_t pairs, int stride, int max_arcs);
+};
+
+// Device temporaries of one customization (the up/down arc weights with middles, the perfect
+// pass's packed words, the prune counts, the scan's temp, the context-cost records and minutes).
+struct CustScratch {
+  unsigned long long *up64 = nullptr, *dn64 = nullptr;
+  uint32_t *pup = nullptr, *pdn = nullptr;
+  int32_t *fcnt = nullptr, *bcnt = nullptr;
+  void* cub = nullptr;
+  size_t cub_bytes = 0;
+  void* rec_buf = nullptr;                         // context cost records [2E]
+  float* min_buf = nullptr;                        // their minutes [2E]
+  float* h_stage = nullptr;                        // pinned [E]: the costs' host copy lands here first
 };
 
 // The device pointers of one metric that the query kernels read — an array of these plus a group
@@ -120,13 +134,14 @@ class CchGpu {
   void set_eta(const void* blob, int H, const NormParams& np, int variant, int num_cus);
   bool has_eta() const { return eta_blob_ != nullptr; }
   // edge costs (s) of a context into d_cost [E] on the device (routing/graph.py edge_costs)
-  hipError_t context_costs(const CchContext& c, float* d_cost, hipStream_t s);
+  hipError_t context_costs(const CchContext& c, float* d_cost, hipStream_t s, CustScratch* cs = nullptr);
 
   // customize m from d_cost ([E] on this device; copied into m.cost)
-  hipError_t customize(const float* d_cost, CchMetricDev& m, hipStream_t s);
+  hipError_t customize(const float* d_cost, CchMetricDev& m, hipStream_t s, CustScratch* cs = nullptr);
 
   // the metric of a context: from the cache, else costs + customization now (LRU, `capacity`)
-  hipError_t metric_for(const CchContext& c, hipStream_t s, std::shared_ptr<CchMetricDev>& out, bool* fresh = nullptr);
+  hipError_t metric_for(const CchContext& c, hipStream_t s, std::shared_ptr<CchMetricDev>& out, bool* fresh = nullptr,
+                        CustScratch* cs = nullptr);
   // a metric from caller-given costs under a caller-chosen key (tests, benches)
   hipError_t metric_from_costs(uint64_t key, const float* d_cost, hipStream_t s, std::shared_ptr<CchMetricDev>& out);
   // a cached metric by key (no build); false if absent
@@ -157,6 +172,7 @@ class CchGpu {
   struct AsyncStats {
     long long queued = 0, built = 0, failed = 0;
     int pending = 0;
+    double build_ms = 0.0, alloc_ms = 0.0, hostcopy_ms = 0.0;   // summed over the background builds
   };
   AsyncStats async_stats();
 
@@ -223,15 +239,18 @@ class CchGpu {
   void* d_ptask = nullptr;
   std::vector<int64_t> btask_ptr_, ptask_ptr_;
   int64_t n_btask_ = 0, n_ptask_ = 0;
-  // customization temporaries (one customization at a time: mu_cust_)
-  unsigned long long *d_up64 = nullptr, *d_dn64 = nullptr;
-  uint32_t *d_pup = nullptr, *d_pdn = nullptr;
-  int32_t *d_fcnt = nullptr, *d_bcnt = nullptr;
-  void* d_cub = nullptr;
-  size_t cub_bytes = 0;
-  void* rec_buf = nullptr;                         // context cost records [2E] + minutes [2E]
-  float* min_buf = nullptr;
-  std::mutex mu_cust_, mu_build_;
+  // customization temporaries: cs0_ for callers on their own streams (one at a time: mu_cust_),
+  // one set per background builder (no lock: each builder owns its set)
+  hipError_t alloc_scratch(CustScratch& x);
+  void free_scratch(CustScratch& x);
+  CustScratch cs0_;
+  std::vector<std::unique_ptr<CustScratch>> bscr_;
+  std::mutex mu_cust_;
+  // contexts being built (metric_for: another caller of the same context waits for it; different
+  // contexts build concurrently)
+  std::mutex mu_inflight_;
+  std::condition_variable cv_inflight_;
+  std::unordered_set<uint64_t> inflight_;
   // ETA
   const void* eta_blob_ = nullptr;
   int eta_H_ = 0, eta_variant_ = -1, eta_cus_ = 256;
@@ -245,18 +264,19 @@ class CchGpu {
   void insert_cached(const std::shared_ptr<CchMetricDev>& m);   // LRU push_front + eviction
   std::atomic<uint64_t> tag_ctr_{0};
   // asynchronous builds
-  void builder_loop();
+  void builder_loop(int idx);
   void notify_built(uint64_t key, bool ok);
+  std::vector<std::thread> bths_;                  // ROUTEST_CCH_BUILDERS threads (default 3)
   std::mutex bmu_;
   std::condition_variable bcv_;
   std::deque<CchContext> bq_;
   std::unordered_set<uint64_t> bpending_;          // queued or building
-  std::thread bth_;
   bool bstop_ = false;
   std::mutex lmu_;                                 // held while listeners run (removal waits)
   std::vector<std::pair<int, std::function<void(uint64_t, bool)>>> listeners_;
   int next_listener_ = 1;
   std::atomic<long long> n_bqueued_{0}, n_bbuilt_{0}, n_bfailed_{0};
+  std::atomic<long long> us_build_{0}, us_alloc_{0}, us_hostcopy_{0};
 };
 
 }  // namespace rt
