@@ -235,7 +235,9 @@ class Bench:
                     th = threading.Thread(target=side)
                     th.start()
                 alive = th is not None and th.is_alive()
+                sw = st.front.stats()
                 w = self.window(st, bodies, self.a.concurrency, 0.5)
+                w["stage_ms_per_flush"] = self.delta(st, sw)["stage_ms_per_flush"]
                 w["fresh_in_flight"] = alive or (th is not None and th.is_alive())
                 wins.append(w)
                 emit({"phase": "fresh", "window": k, **w})
