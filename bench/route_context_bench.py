@@ -214,7 +214,10 @@ class Bench:
         try:
             ctx = {"weather": "Sunny", "traffic": "Medium", "pickup_time": PICKUPS[0]}
             bodies = self.payloads(1000, lambda i: ctx, store)
-            self.window(st, bodies, 64, 2.0)
+            for _ in range(30):                        # until the cached context is built and warm
+                w = self.window(st, bodies, 64, 1.0)
+                if w["requests"] > 0 and w["max_ms"] < 1000:
+                    break
             fresh_ctx = [{"weather": w, "traffic": "Jam", "pickup_time": PICKUPS[3]} for w in WEATHERS]
             fresh_bodies = self.payloads(4, lambda i: fresh_ctx[i], store, seed=7)
             res = []
@@ -251,7 +254,7 @@ class Bench:
                    "cached_p99_during_ms": max(w["p99_ms"] for w in during),
                    "cached_max_during_ms": max(w["max_ms"] for w in during),
                    **{k: stats.get(k) for k in ("async_built", "async_build_ms", "async_alloc_ms",
-                                                "async_hostcopy_ms")},
+                                                "async_hostcopy_ms", "builder_max_wg")},
                    **self.delta(st, s0)}
         finally:
             self.close(st, sv, store)

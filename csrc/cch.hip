@@ -1249,6 +1249,7 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   ck(up_copy(d_pofs, pofs_.data(), N + 1));
   ck(up_copy(d_aofs, aofs_.data(), N + 1));
   ck(alloc_scratch(cs0_));
+  if (builder_max_wg_.load() < 0) builder_max_wg_.store(M >= 20000000LL ? 512 : 0);
   // triangle table within ROUTEST_CCH_TRI_GB of HBM (default 48 — a 1M-node city needs ~38 GB of the 288; 0 disables)
   if (e == hipSuccess) {
     std::vector<int64_t> tofs(N + 1, 0);
@@ -1494,18 +1495,26 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   if (ev[0]) (void)hipEventRecord(ev[0], s);
   const bool tasks = d_btask != nullptr && d_tri != nullptr;
   // basic, bottom-up by height: the task kernel when the task tables exist
+  // (builder_max_wg_ > 0, the background builders: a wide level is launched in pieces of at most
+  // max_wg workgroups, one after the other on the stream, so a build never has more than that many
+  // workgroups of memory traffic in flight next to the flushes' query kernels)
+  const int max_wg = cs != nullptr ? std::max(0, builder_max_wg_.load(std::memory_order_relaxed)) : 0;
+  const long long wave_cap = max_wg > 0 ? 4LL * max_wg : (1LL << 40);
   for (int h = 0; h <= T_.max_height && e == hipSuccess && tasks; ++h) {
-    const long long nt = btask_ptr_[h + 1] - btask_ptr_[h];
-    if (nt <= 0) continue;
-    if (skip)
-      hipLaunchKernelGGL(basic_task_kernel<true>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
-                         (const CustTask*)d_btask + btask_ptr_[h], nt, d_up_ptr, d_up_head, d_tofs, d_tri, X.up64,
-                         X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
-    else
-      hipLaunchKernelGGL(basic_task_kernel<false>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
-                         (const CustTask*)d_btask + btask_ptr_[h], nt, d_up_ptr, d_up_head, d_tofs, d_tri, X.up64,
-                         X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
-    ck(hipGetLastError());
+    const long long ntl = btask_ptr_[h + 1] - btask_ptr_[h];
+    for (long long t0 = 0; t0 < ntl && e == hipSuccess; t0 += wave_cap) {
+      const long long nt = std::min(wave_cap, ntl - t0);
+      const CustTask* tk = (const CustTask*)d_btask + btask_ptr_[h] + t0;
+      if (skip)
+        hipLaunchKernelGGL(basic_task_kernel<true>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, tk, nt, d_up_ptr,
+                           d_up_head, d_tofs, d_tri, X.up64, X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up,
+                           m.cnt_dn, d_length);
+      else
+        hipLaunchKernelGGL(basic_task_kernel<false>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, tk, nt, d_up_ptr,
+                           d_up_head, d_tofs, d_tri, X.up64, X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up,
+                           m.cnt_dn, d_length);
+      ck(hipGetLastError());
+    }
   }
   for (int h = 0; h <= T_.max_height && e == hipSuccess && !tasks; ++h) {
     LevelArgs L{d_up_ptr, d_up_head, d_hnodes, d_bofs, (int)T_.hlev_ptr[h], (int)T_.hlev_ptr[h + 1], 0, 0, d_tofs, d_tri};
@@ -1551,13 +1560,20 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri};
     if (P.arcs <= 0 || pofs_[hi] == pofs_[lo]) continue;       // no node of the level has two arcs
     // mean degree of the level's nodes: wide nodes get a wave per arc, narrow ones a lane per arc
-    if (P.arcs >= 24 * (long long)(hi - lo))
-      hipLaunchKernelGGL(perfect_pull_wave_kernel, dim3((unsigned)((P.arcs + 3) / 4)), dim3(256), 0, s, P, X.up64,
-                         X.dn64, X.pup, X.pdn);
-    else
-      hipLaunchKernelGGL(perfect_pull_lane_kernel, dim3(blocks_for(P.arcs, 256)), dim3(256), 0, s, P, X.up64, X.dn64,
-                         X.pup, X.pdn);
-    ck(hipGetLastError());
+    const bool wave = P.arcs >= 24 * (long long)(hi - lo);
+    const long long cap = wave ? wave_cap : 64 * wave_cap;      // arcs per piece (see wave_cap)
+    const long long arcs = P.arcs, base = P.base;
+    for (long long a0 = 0; a0 < arcs && e == hipSuccess; a0 += cap) {
+      P.base = base + a0;
+      P.arcs = std::min(cap, arcs - a0);
+      if (wave)
+        hipLaunchKernelGGL(perfect_pull_wave_kernel, dim3((unsigned)((P.arcs + 3) / 4)), dim3(256), 0, s, P, X.up64,
+                           X.dn64, X.pup, X.pdn);
+      else
+        hipLaunchKernelGGL(perfect_pull_lane_kernel, dim3(blocks_for(P.arcs, 256)), dim3(256), 0, s, P, X.up64,
+                           X.dn64, X.pup, X.pdn);
+      ck(hipGetLastError());
+    }
   }
   for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && !(pull && d_tri != nullptr); ++d) {
     LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0, d_tofs, d_tri};

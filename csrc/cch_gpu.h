@@ -175,6 +175,10 @@ class CchGpu {
     double build_ms = 0.0, alloc_ms = 0.0, hostcopy_ms = 0.0;   // summed over the background builds
   };
   AsyncStats async_stats();
+  // background builds launch wide levels in pieces of at most n workgroups (0: whole levels);
+  // default ROUTEST_CCH_BUILDER_MAX_WG
+  void set_builder_pacing(int n) { builder_max_wg_.store(n < 0 ? 0 : n); }
+  int builder_pacing() const { return builder_max_wg_.load(); }
 
   // point-to-point: node ids on the device
   hipError_t route(const CchMetricDev& m, const int* d_src, const int* d_dst, int Q, const CchRouteOut& o,
@@ -277,6 +281,13 @@ class CchGpu {
   int next_listener_ = 1;
   std::atomic<long long> n_bqueued_{0}, n_bbuilt_{0}, n_bfailed_{0};
   std::atomic<long long> us_build_{0}, us_alloc_{0}, us_hostcopy_{0};
+  // -1 until the constructor picks the default: ROUTEST_CCH_BUILDER_MAX_WG if set, else 512 on a
+  // city-scale hierarchy (>= 20M shortcut arcs: the 1M-node city's builds otherwise raised the
+  // cached requests' p99 1.7x; paced, 1.03x at 2-4x the build time) and whole levels below that
+  std::atomic<int> builder_max_wg_{[] {
+    const char* v = std::getenv("ROUTEST_CCH_BUILDER_MAX_WG");
+    return v ? std::max(0, std::atoi(v)) : -1;
+  }()};
 };
 
 }  // namespace rt

@@ -131,3 +131,30 @@ def test_bulk_route_step_reuse_matches_fresh_sweeps(setup, monkeypatch):
     n2, c2, st2, k2 = step.step()
     assert n1 == n2 and torch.equal(c1, c2) and torch.equal(st1, st2) and torch.equal(k1, k2)
     assert int((st1 == 0).sum()) == n1
+
+
+def test_paced_background_build_bit_identical_to_cpu(setup):
+    """A context built by the background builders with pacing (wide levels launched in pieces of
+    16 workgroups, csrc/cch.hip customize) gives the CPU reference's answers bit for bit."""
+    import time
+    from routest_amd.routing.cch import RouteContext
+    g, m, router, cost, key, cpu, mc = setup
+    router.gpu.set_builder_pacing(16)
+    try:
+        ctx = RouteContext(weather=3, congestion=2, weekhour=2 * 24 + 9)
+        assert not router.is_cached(ctx)
+        router.prefetch(ctx, urgent=True)
+        t_end = time.time() + 60
+        while not router.is_cached(ctx) and time.time() < t_end:
+            time.sleep(0.01)
+        assert router.is_cached(ctx)
+    finally:
+        router.gpu.set_builder_pacing(0)
+    src, dst = synth_route_queries(g, 2000, seed=11)
+    sec, met, st, paths = router.route(src, dst, ctx)
+    assert router.last_metric["fresh"] is False          # the background build was used
+    c = router.costs(ctx)
+    mcc = cpu.customize(c, g.length_m)
+    s2, m2, st2, p2 = cpu.query(mcc, src, dst, True)
+    assert np.array_equal(sec, s2) and np.array_equal(met, m2) and np.array_equal(st, st2)
+    assert all(np.array_equal(a, b) for a, b in zip(paths, p2))
