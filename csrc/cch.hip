@@ -30,6 +30,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -1469,12 +1470,6 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   m.alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
   if (e != hipSuccess) return e;
   if (d_cost != m.cost) ck(hipMemcpyAsync(m.cost, d_cost, E * sizeof(float), hipMemcpyDeviceToDevice, s));
-  const int fill_blocks = (int)std::min<int64_t>(4096, (M + 255) / 256 + 1);
-  hipLaunchKernelGGL(fill_u64_kernel, dim3(fill_blocks), dim3(256), 0, s, X.up64, (long long)M, PACK_INF_D);
-  hipLaunchKernelGGL(fill_u64_kernel, dim3(fill_blocks), dim3(256), 0, s, X.dn64, (long long)M, PACK_INF_D);
-  hipLaunchKernelGGL(edge_scatter_kernel, dim3(blocks_for(E, 256)), dim3(256), 0, s, m.cost, d_edge_arc, d_edge_dir,
-                     (int)E, X.up64, X.dn64);
-  ck(hipGetLastError());
   static const bool skip = [] {
     const char* v = std::getenv("ROUTEST_CCH_SKIP");
     return !(v && std::string(v) == "0");
@@ -1492,108 +1487,119 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     }
   } evs;
   hipEvent_t* ev = evs.e;
-  if (ev[0]) (void)hipEventRecord(ev[0], s);
-  const bool tasks = d_btask != nullptr && d_tri != nullptr;
-  // basic, bottom-up by height: the task kernel when the task tables exist
-  // (builder_max_wg_ > 0, the background builders: a wide level is launched in pieces of at most
-  // max_wg workgroups, one after the other on the stream, so a build never has more than that many
-  // workgroups of memory traffic in flight next to the flushes' query kernels)
-  const int max_wg = cs != nullptr ? std::max(0, builder_max_wg_.load(std::memory_order_relaxed)) : 0;
-  const long long wave_cap = max_wg > 0 ? 4LL * max_wg : (1LL << 40);
-  for (int h = 0; h <= T_.max_height && e == hipSuccess && tasks; ++h) {
-    const long long ntl = btask_ptr_[h + 1] - btask_ptr_[h];
-    for (long long t0 = 0; t0 < ntl && e == hipSuccess; t0 += wave_cap) {
-      const long long nt = std::min(wave_cap, ntl - t0);
-      const CustTask* tk = (const CustTask*)d_btask + btask_ptr_[h] + t0;
+  // the launch sequence from the weights' reset through the prune counts (ev: phase events, or
+  // nullptr when captured into the graph probe below)
+  auto core = [&](hipStream_t s, hipEvent_t* ev) {
+    const int fill_blocks = (int)std::min<int64_t>(4096, (M + 255) / 256 + 1);
+    hipLaunchKernelGGL(fill_u64_kernel, dim3(fill_blocks), dim3(256), 0, s, X.up64, (long long)M, PACK_INF_D);
+    hipLaunchKernelGGL(fill_u64_kernel, dim3(fill_blocks), dim3(256), 0, s, X.dn64, (long long)M, PACK_INF_D);
+    hipLaunchKernelGGL(edge_scatter_kernel, dim3(blocks_for(E, 256)), dim3(256), 0, s, m.cost, d_edge_arc, d_edge_dir,
+                       (int)E, X.up64, X.dn64);
+    ck(hipGetLastError());
+    if (ev && ev[0]) (void)hipEventRecord(ev[0], s);
+    const bool tasks = d_btask != nullptr && d_tri != nullptr;
+    // basic, bottom-up by height: the task kernel when the task tables exist
+    // (builder_max_wg_ > 0, the background builders: a wide level is launched in pieces of at most
+    // max_wg workgroups, one after the other on the stream, so a build never has more than that many
+    // workgroups of memory traffic in flight next to the flushes' query kernels)
+    const int max_wg = cs != nullptr ? std::max(0, builder_max_wg_.load(std::memory_order_relaxed)) : 0;
+    const long long wave_cap = max_wg > 0 ? 4LL * max_wg : (1LL << 40);
+    for (int h = 0; h <= T_.max_height && e == hipSuccess && tasks; ++h) {
+      const long long ntl = btask_ptr_[h + 1] - btask_ptr_[h];
+      for (long long t0 = 0; t0 < ntl && e == hipSuccess; t0 += wave_cap) {
+        const long long nt = std::min(wave_cap, ntl - t0);
+        const CustTask* tk = (const CustTask*)d_btask + btask_ptr_[h] + t0;
+        if (skip)
+          hipLaunchKernelGGL(basic_task_kernel<true>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, tk, nt, d_up_ptr,
+                             d_up_head, d_tofs, d_tri, X.up64, X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up,
+                             m.cnt_dn, d_length);
+        else
+          hipLaunchKernelGGL(basic_task_kernel<false>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, tk, nt, d_up_ptr,
+                             d_up_head, d_tofs, d_tri, X.up64, X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up,
+                             m.cnt_dn, d_length);
+        ck(hipGetLastError());
+      }
+    }
+    for (int h = 0; h <= T_.max_height && e == hipSuccess && !tasks; ++h) {
+      LevelArgs L{d_up_ptr, d_up_head, d_hnodes, d_bofs, (int)T_.hlev_ptr[h], (int)T_.hlev_ptr[h + 1], 0, 0, d_tofs, d_tri};
+      if (L.lo >= L.hi) continue;
+      L.base = bofs_[L.lo];
+      L.items = bofs_[L.hi] - bofs_[L.lo];
+      if (L.items <= 0) continue;
       if (skip)
-        hipLaunchKernelGGL(basic_task_kernel<true>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, tk, nt, d_up_ptr,
-                           d_up_head, d_tofs, d_tri, X.up64, X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up,
-                           m.cnt_dn, d_length);
+        hipLaunchKernelGGL(basic_level_kernel<true>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
+                           m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
       else
-        hipLaunchKernelGGL(basic_task_kernel<false>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, tk, nt, d_up_ptr,
-                           d_up_head, d_tofs, d_tri, X.up64, X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up,
-                           m.cnt_dn, d_length);
+        hipLaunchKernelGGL(basic_level_kernel<false>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
+                           m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
       ck(hipGetLastError());
     }
-  }
-  for (int h = 0; h <= T_.max_height && e == hipSuccess && !tasks; ++h) {
-    LevelArgs L{d_up_ptr, d_up_head, d_hnodes, d_bofs, (int)T_.hlev_ptr[h], (int)T_.hlev_ptr[h + 1], 0, 0, d_tofs, d_tri};
-    if (L.lo >= L.hi) continue;
-    L.base = bofs_[L.lo];
-    L.items = bofs_[L.hi] - bofs_[L.lo];
-    if (L.items <= 0) continue;
-    if (skip)
-      hipLaunchKernelGGL(basic_level_kernel<true>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
-                         m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
-    else
-      hipLaunchKernelGGL(basic_level_kernel<false>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
-                         m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
+    if (ev && ev[1]) (void)hipEventRecord(ev[1], s);
+    // perfect, top-down by depth
+    hipLaunchKernelGGL(perfect_init_kernel, dim3(fill_blocks), dim3(256), 0, s, X.up64, X.dn64, X.pup, X.pdn, (long long)M);
     ck(hipGetLastError());
-  }
-  if (ev[1]) (void)hipEventRecord(ev[1], s);
-  // perfect, top-down by depth
-  hipLaunchKernelGGL(perfect_init_kernel, dim3(fill_blocks), dim3(256), 0, s, X.up64, X.dn64, X.pup, X.pdn, (long long)M);
-  ck(hipGetLastError());
-  // pull (default with the triangle table; ROUTEST_CCH_PERFECT=push: the atomic kernel)
-  static const bool pull = [] {
-    const char* v = std::getenv("ROUTEST_CCH_PERFECT");
-    return !(v && std::string(v) == "push");
-  }();
-  // perfect: the pull kernels (measured faster than the perfect task kernel: 12.0 vs 15.3 ms on
-  // the 100k graph, 227 vs 351 ms on the 1M city; ROUTEST_CCH_PERFECT=tasks selects it)
-  static const bool env_ptasks = [] {
-    const char* v = std::getenv("ROUTEST_CCH_PERFECT");
-    return v && std::string(v) == "tasks";
-  }();
-  const bool ptasks = env_ptasks && d_ptask != nullptr;
-  for (int d = 0; d <= T_.max_depth && e == hipSuccess && tasks && ptasks; ++d) {
-    const long long nt = ptask_ptr_[d + 1] - ptask_ptr_[d];
-    if (nt <= 0) continue;
-    hipLaunchKernelGGL(perfect_task_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
-                       (const CustTask*)d_ptask + ptask_ptr_[d], nt, d_up_ptr, d_up_head, d_tofs, d_tri, X.up64, X.dn64,
-                       X.pup, X.pdn);
-    ck(hipGetLastError());
-  }
-  for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && pull && d_tri != nullptr; ++d) {
-    const int lo = (int)T_.dlev_ptr[d], hi = (int)T_.dlev_ptr[d + 1];
-    if (lo >= hi) continue;
-    PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri};
-    if (P.arcs <= 0 || pofs_[hi] == pofs_[lo]) continue;       // no node of the level has two arcs
-    // mean degree of the level's nodes: wide nodes get a wave per arc, narrow ones a lane per arc
-    const bool wave = P.arcs >= 24 * (long long)(hi - lo);
-    const long long cap = wave ? wave_cap : 64 * wave_cap;      // arcs per piece (see wave_cap)
-    const long long arcs = P.arcs, base = P.base;
-    for (long long a0 = 0; a0 < arcs && e == hipSuccess; a0 += cap) {
-      P.base = base + a0;
-      P.arcs = std::min(cap, arcs - a0);
-      if (wave)
-        hipLaunchKernelGGL(perfect_pull_wave_kernel, dim3((unsigned)((P.arcs + 3) / 4)), dim3(256), 0, s, P, X.up64,
-                           X.dn64, X.pup, X.pdn);
-      else
-        hipLaunchKernelGGL(perfect_pull_lane_kernel, dim3(blocks_for(P.arcs, 256)), dim3(256), 0, s, P, X.up64,
-                           X.dn64, X.pup, X.pdn);
+    // pull (default with the triangle table; ROUTEST_CCH_PERFECT=push: the atomic kernel)
+    static const bool pull = [] {
+      const char* v = std::getenv("ROUTEST_CCH_PERFECT");
+      return !(v && std::string(v) == "push");
+    }();
+    // perfect: the pull kernels (measured faster than the perfect task kernel: 12.0 vs 15.3 ms on
+    // the 100k graph, 227 vs 351 ms on the 1M city; ROUTEST_CCH_PERFECT=tasks selects it)
+    static const bool env_ptasks = [] {
+      const char* v = std::getenv("ROUTEST_CCH_PERFECT");
+      return v && std::string(v) == "tasks";
+    }();
+    const bool ptasks = env_ptasks && d_ptask != nullptr;
+    for (int d = 0; d <= T_.max_depth && e == hipSuccess && tasks && ptasks; ++d) {
+      const long long nt = ptask_ptr_[d + 1] - ptask_ptr_[d];
+      if (nt <= 0) continue;
+      hipLaunchKernelGGL(perfect_task_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s,
+                         (const CustTask*)d_ptask + ptask_ptr_[d], nt, d_up_ptr, d_up_head, d_tofs, d_tri, X.up64, X.dn64,
+                         X.pup, X.pdn);
       ck(hipGetLastError());
     }
-  }
-  for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && !(pull && d_tri != nullptr); ++d) {
-    LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0, d_tofs, d_tri};
-    if (L.lo >= L.hi) continue;
-    L.base = pofs_[L.lo];
-    L.items = pofs_[L.hi] - pofs_[L.lo];
-    if (L.items <= 0) continue;
-    if (skip)
-      hipLaunchKernelGGL(perfect_level_kernel<true>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
-                         X.pup, X.pdn);
-    else
-      hipLaunchKernelGGL(perfect_level_kernel<false>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
-                         X.pup, X.pdn);
+    for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && pull && d_tri != nullptr; ++d) {
+      const int lo = (int)T_.dlev_ptr[d], hi = (int)T_.dlev_ptr[d + 1];
+      if (lo >= hi) continue;
+      PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri};
+      if (P.arcs <= 0 || pofs_[hi] == pofs_[lo]) continue;       // no node of the level has two arcs
+      // mean degree of the level's nodes: wide nodes get a wave per arc, narrow ones a lane per arc
+      const bool wave = P.arcs >= 24 * (long long)(hi - lo);
+      const long long cap = wave ? wave_cap : 64 * wave_cap;      // arcs per piece (see wave_cap)
+      const long long arcs = P.arcs, base = P.base;
+      for (long long a0 = 0; a0 < arcs && e == hipSuccess; a0 += cap) {
+        P.base = base + a0;
+        P.arcs = std::min(cap, arcs - a0);
+        if (wave)
+          hipLaunchKernelGGL(perfect_pull_wave_kernel, dim3((unsigned)((P.arcs + 3) / 4)), dim3(256), 0, s, P, X.up64,
+                             X.dn64, X.pup, X.pdn);
+        else
+          hipLaunchKernelGGL(perfect_pull_lane_kernel, dim3(blocks_for(P.arcs, 256)), dim3(256), 0, s, P, X.up64,
+                             X.dn64, X.pup, X.pdn);
+        ck(hipGetLastError());
+      }
+    }
+    for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && !(pull && d_tri != nullptr); ++d) {
+      LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0, d_tofs, d_tri};
+      if (L.lo >= L.hi) continue;
+      L.base = pofs_[L.lo];
+      L.items = pofs_[L.hi] - pofs_[L.lo];
+      if (L.items <= 0) continue;
+      if (skip)
+        hipLaunchKernelGGL(perfect_level_kernel<true>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
+                           X.pup, X.pdn);
+      else
+        hipLaunchKernelGGL(perfect_level_kernel<false>, dim3(blocks_for(L.items, 256)), dim3(256), 0, s, L, X.up64, X.dn64,
+                           X.pup, X.pdn);
+      ck(hipGetLastError());
+    }
+    if (ev && ev[2]) (void)hipEventRecord(ev[2], s);
+    // prune + compact
+    hipLaunchKernelGGL(prune_count_wave_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, d_up_ptr, X.pup, X.pdn,
+                       X.up64, X.dn64, N, X.fcnt, X.bcnt);
     ck(hipGetLastError());
-  }
-  if (ev[2]) (void)hipEventRecord(ev[2], s);
-  // prune + compact
-  hipLaunchKernelGGL(prune_count_wave_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, d_up_ptr, X.pup, X.pdn,
-                     X.up64, X.dn64, N, X.fcnt, X.bcnt);
-  ck(hipGetLastError());
+  };
+  core(s, ev);
   ck(hipMemsetAsync(m.f_ptr, 0, sizeof(int32_t), s));
   ck(hipMemsetAsync(m.b_ptr, 0, sizeof(int32_t), s));
   size_t tb = X.cub_bytes;
@@ -1626,6 +1632,57 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   if (ev[0] && ev[1] && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) m.basic_ms = ms;
   if (ev[1] && ev[2] && hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) m.perfect_ms = ms;
   if (ev[2] && ev[3] && hipEventElapsedTime(&ms, ev[2], ev[3]) == hipSuccess) m.prune_ms = ms;
+  // diagnostics (ROUTEST_CCH_GRAPH_PROBE=n): the launch sequence above n times eagerly and n times
+  // as one captured HIP graph on a private stream, to price the per-level dispatch gaps (the
+  // replays recompute this metric's values in place: same inputs, same results)
+  static const int probe = [] {
+    const char* v = std::getenv("ROUTEST_CCH_GRAPH_PROBE");
+    return v ? std::atoi(v) : 0;
+  }();
+  if (probe > 0 && e == hipSuccess) {
+    hipStream_t ps = nullptr;
+    hipEvent_t pa = nullptr, pb = nullptr;
+    if (hipStreamCreateWithFlags(&ps, hipStreamNonBlocking) == hipSuccess && hipEventCreate(&pa) == hipSuccess &&
+        hipEventCreate(&pb) == hipSuccess) {
+      float eager = 0.f, graph = 0.f;
+      (void)hipEventRecord(pa, ps);
+      for (int r = 0; r < probe; ++r) core(ps, nullptr);
+      (void)hipEventRecord(pb, ps);
+      (void)hipEventSynchronize(pb);
+      (void)hipEventElapsedTime(&eager, pa, pb);
+      const auto tc = std::chrono::steady_clock::now();
+      hipGraph_t g = nullptr;
+      hipGraphExec_t ge = nullptr;
+      size_t nodes = 0;
+      if (hipStreamBeginCapture(ps, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+        core(ps, nullptr);
+        if (hipStreamEndCapture(ps, &g) == hipSuccess && g != nullptr) {
+          (void)hipGraphGetNodes(g, nullptr, &nodes);
+          if (hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) != hipSuccess) ge = nullptr;
+        }
+      }
+      const double inst_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
+      if (ge != nullptr) {
+        (void)hipGraphLaunch(ge, ps);             // (first replay uploads the graph)
+        (void)hipStreamSynchronize(ps);
+        (void)hipEventRecord(pa, ps);
+        for (int r = 0; r < probe; ++r) (void)hipGraphLaunch(ge, ps);
+        (void)hipEventRecord(pb, ps);
+        (void)hipEventSynchronize(pb);
+        (void)hipEventElapsedTime(&graph, pa, pb);
+      }
+      std::fprintf(stderr,
+                   "[cch graph probe] %d runs: eager %.3f ms/run, graph %.3f ms/run (%zu nodes, capture+instantiate "
+                   "%.1f ms)\n",
+                   probe, eager / probe, ge ? graph / probe : -1.0, nodes, inst_ms);
+      if (ge) (void)hipGraphExecDestroy(ge);
+      if (g) (void)hipGraphDestroy(g);
+      (void)hipGetLastError();
+    }
+    if (pa) (void)hipEventDestroy(pa);
+    if (pb) (void)hipEventDestroy(pb);
+    if (ps) (void)hipStreamDestroy(ps);
+  }
   // the host copy of the costs (maneuver durations, the exact host fallback) is made here, on the
   // builder's stream, before the metric is published: a flush that first meets this context finds
   // it ready instead of copying E floats on its own critical path
