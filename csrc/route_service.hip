@@ -445,7 +445,12 @@ struct RouteService::Impl {
     // WAL + NORMAL: a commit appends to the WAL without an fsync (the WAL is synced at checkpoints);
     // FULL would fsync every flush's commit
     sql.exec(db, "PRAGMA synchronous=NORMAL", nullptr, nullptr, nullptr);
-    sql.exec(db, "PRAGMA foreign_keys=ON", nullptr, nullptr, nullptr);
+    // no foreign-key checks on THIS connection: it inserts each result right after its request in
+    // one transaction, so the reference holds by construction and the parent lookup per result row
+    // is pure cost; deletes (ON DELETE CASCADE) happen on the app's / history reader's connections,
+    // which enforce the keys
+    sql.exec(db, "PRAGMA foreign_keys=OFF", nullptr, nullptr, nullptr);
+    sql.exec(db, "PRAGMA cache_size=-65536", nullptr, nullptr, nullptr);       // 64 MB page cache
     sql.exec(db, "PRAGMA wal_autocheckpoint=0", nullptr, nullptr, nullptr);   // ckpt_loop checkpoints
     sql.exec(db, "PRAGMA temp_store=MEMORY", nullptr, nullptr, nullptr);      // statement journals in RAM
     const char* q1 = "INSERT INTO route_requests(id,origin_id,stops,request_time,status,engine,vehicle_id,driver_age)"
@@ -1800,10 +1805,10 @@ struct RouteService::Impl {
     j->out += "}}";
   }
 
-  // Group commit: every flush waiting when the thread wakes goes into ONE transaction, one savepoint
-  // per request (a failed insert rolls back only its own request's rows -- SQLiteStore's
-  // per-request semantics).  A response leaves only after its commit, so a client that reads its
-  // request_id back (/api/history/<id>) finds it.
+  // Group commit: every flush waiting when the thread wakes goes into ONE transaction (a failed
+  // insert removes only its own request's rows, persist_one -- SQLiteStore's per-request
+  // semantics).  A response leaves only after its commit, so a client that reads its request_id
+  // back (/api/history/<id>) finds it.
   void persist_group(std::vector<std::vector<RouteJob*>>& groups) {
     const std::string now = utc_now_iso();
     const bool tx = step_once(st_begin);
