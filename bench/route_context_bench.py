@@ -254,7 +254,7 @@ class Bench:
                    "cached_p99_during_ms": max(w["p99_ms"] for w in during),
                    "cached_max_during_ms": max(w["max_ms"] for w in during),
                    **{k: stats.get(k) for k in ("async_built", "async_build_ms", "async_alloc_ms",
-                                                "async_hostcopy_ms", "builder_max_wg")},
+                                                "async_hostcopy_ms", "builder_max_wg", "async_paced")},
                    **self.delta(st, s0)}
         finally:
             self.close(st, sv, store)

@@ -1447,6 +1447,9 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   std::unique_lock<std::mutex> lk(mu_cust_, std::defer_lock);
   if (cs == nullptr) lk.lock();
   CustScratch& X = cs ? *cs : cs0_;
+  // a background build while queries are served (or always, set_builder_pacing): paced launches
+  const bool paced = cs != nullptr && builder_max_wg_.load() > 0 && (pace_always_.load() || serving_now());
+  if (paced) n_paced_.fetch_add(1, std::memory_order_relaxed);
   auto t0 = std::chrono::steady_clock::now();
   const int N = T_.N;
   const int64_t M = T_.M, E = T_.E;
@@ -1502,7 +1505,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     // (builder_max_wg_ > 0, the background builders: a wide level is launched in pieces of at most
     // max_wg workgroups, one after the other on the stream, so a build never has more than that many
     // workgroups of memory traffic in flight next to the flushes' query kernels)
-    const int max_wg = cs != nullptr ? std::max(0, builder_max_wg_.load(std::memory_order_relaxed)) : 0;
+    const int max_wg = paced ? std::max(0, builder_max_wg_.load(std::memory_order_relaxed)) : 0;
     const long long wave_cap = max_wg > 0 ? 4LL * max_wg : (1LL << 40);
     for (int h = 0; h <= T_.max_height && e == hipSuccess && tasks; ++h) {
       const long long ntl = btask_ptr_[h + 1] - btask_ptr_[h];
@@ -1800,6 +1803,7 @@ CchGpu::AsyncStats CchGpu::async_stats() {
   a.build_ms = us_build_.load() / 1e3;
   a.alloc_ms = us_alloc_.load() / 1e3;
   a.hostcopy_ms = us_hostcopy_.load() / 1e3;
+  a.paced = n_paced_.load();
   std::lock_guard<std::mutex> lk(bmu_);
   a.pending = (int)bpending_.size();
   return a;

@@ -103,6 +103,7 @@ class PyCchGpu {
     d["async_alloc_ms"] = a.alloc_ms;
     d["async_hostcopy_ms"] = a.hostcopy_ms;
     d["builder_max_wg"] = g_->builder_pacing();
+    d["async_paced"] = a.paced;
     return d;
   }
 
@@ -121,7 +122,7 @@ class PyCchGpu {
     return g_->cached_metric((uint64_t)key, m);
   }
   void set_cache_gb(double gb) { g_->set_cache_gb(gb); }
-  void set_builder_pacing(int n) { g_->set_builder_pacing(n); }
+  void set_builder_pacing(int n, bool always) { g_->set_builder_pacing(n, always); }
 
   py::dict info(const rt::CchMetricDev& m, bool fresh) const {
     py::dict d;
@@ -365,7 +366,7 @@ void bind_cch_gpu(py::module& m) {
            py::arg("i"), py::arg("j"), py::arg("max_path") = 4096, py::arg("want_path") = true)
       .def("set_capacity", &PyCchGpu::set_capacity)
       .def("set_cache_gb", &PyCchGpu::set_cache_gb, py::arg("gb"))
-      .def("set_builder_pacing", &PyCchGpu::set_builder_pacing, py::arg("max_workgroups"))
+      .def("set_builder_pacing", &PyCchGpu::set_builder_pacing, py::arg("max_workgroups"), py::arg("always") = false)
       .def("request_build", &PyCchGpu::request_build, py::arg("weather"), py::arg("congestion"), py::arg("weekhour"),
            py::arg("driver_age") = 35.0, py::arg("urgent") = true)
       .def("is_cached", &PyCchGpu::is_cached, py::arg("key"))

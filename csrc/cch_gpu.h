@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -173,12 +174,29 @@ class CchGpu {
     long long queued = 0, built = 0, failed = 0;
     int pending = 0;
     double build_ms = 0.0, alloc_ms = 0.0, hostcopy_ms = 0.0;   // summed over the background builds
+    long long paced = 0;                                          // of which paced (queries were running)
   };
   AsyncStats async_stats();
-  // background builds launch wide levels in pieces of at most n workgroups (0: whole levels);
-  // default ROUTEST_CCH_BUILDER_MAX_WG
-  void set_builder_pacing(int n) { builder_max_wg_.store(n < 0 ? 0 : n); }
+  // background builds launch wide levels in pieces of at most n workgroups (0: whole levels) —
+  // while queries are being served (note_queries in the last 250 ms), or always; default
+  // ROUTEST_CCH_BUILDER_MAX_WG
+  void set_builder_pacing(int n, bool always = false) {
+    builder_max_wg_.store(n < 0 ? 0 : n);
+    pace_always_.store(always);
+  }
   int builder_pacing() const { return builder_max_wg_.load(); }
+  // a query flush ran now (the route services call this per flush): builds starting within the next
+  // 250 ms are paced
+  void note_queries() {
+    query_us_.store(std::chrono::duration_cast<std::chrono::microseconds>(
+                        std::chrono::steady_clock::now().time_since_epoch()).count(),
+                    std::memory_order_relaxed);
+  }
+  bool serving_now() const {
+    const long long now = std::chrono::duration_cast<std::chrono::microseconds>(
+                              std::chrono::steady_clock::now().time_since_epoch()).count();
+    return now - query_us_.load(std::memory_order_relaxed) < 250000;
+  }
 
   // point-to-point: node ids on the device
   hipError_t route(const CchMetricDev& m, const int* d_src, const int* d_dst, int Q, const CchRouteOut& o,
@@ -281,6 +299,9 @@ class CchGpu {
   int next_listener_ = 1;
   std::atomic<long long> n_bqueued_{0}, n_bbuilt_{0}, n_bfailed_{0};
   std::atomic<long long> us_build_{0}, us_alloc_{0}, us_hostcopy_{0};
+  std::atomic<long long> query_us_{-(1LL << 40)};
+  std::atomic<bool> pace_always_{false};
+  std::atomic<long long> n_paced_{0};              // background builds that ran paced
   // -1 until the constructor picks the default: ROUTEST_CCH_BUILDER_MAX_WG if set, else 512 on a
   // city-scale hierarchy (>= 20M shortcut arcs: the 1M-node city's builds otherwise raised the
   // cached requests' p99 1.7x; paced, 1.03x at 2-4x the build time) and whole levels below that

@@ -995,6 +995,7 @@ struct RouteService::Impl {
   // background build (on_built requeues them), the other groups proceed now.  Contexts of requests
   // routed at "now" are prefetched for the next week-hour shortly before the hour turns.
   bool cch_groups(Batch& b) {
+    if (cfg.cch != nullptr) cfg.cch->note_queries();     // background builds now run paced
     const rtc::Stamp now = local_now(clock_skew_s);
     const int64_t days = (int64_t)std::floor((double)now.secs / 86400.0);
     const int64_t sec_of_day = now.secs - days * 86400;

@@ -139,7 +139,8 @@ def test_paced_background_build_bit_identical_to_cpu(setup):
     import time
     from routest_amd.routing.cch import RouteContext
     g, m, router, cost, key, cpu, mc = setup
-    router.gpu.set_builder_pacing(16)
+    before = router.stats().get("async_paced", 0)
+    router.gpu.set_builder_pacing(16, always=True)
     try:
         ctx = RouteContext(weather=3, congestion=2, weekhour=2 * 24 + 9)
         assert not router.is_cached(ctx)
@@ -148,6 +149,7 @@ def test_paced_background_build_bit_identical_to_cpu(setup):
         while not router.is_cached(ctx) and time.time() < t_end:
             time.sleep(0.01)
         assert router.is_cached(ctx)
+        assert router.stats()["async_paced"] == before + 1
     finally:
         router.gpu.set_builder_pacing(0)
     src, dst = synth_route_queries(g, 2000, seed=11)
