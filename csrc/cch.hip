@@ -264,6 +264,10 @@ struct PullArgs {
   long long base, arcs;    // arc range of the level
   const int64_t* tofs;     // triangle table (required)
   const int32_t* tri;
+  // {node x, x's first arc, x's arc count, the arc's index in x} per depth-ordered arc: one load
+  // instead of the binary search over the level's nodes + two dependent loads (a level of
+  // thousands of nodes searched ~12 dependent steps per wave); nullptr: search
+  const int4* parc;
 };
 
 __device__ __forceinline__ void pull_cand(const PullArgs& P, int x, int k, int a0, int ia, int ic, float xz_c, float zx_c,
@@ -278,62 +282,96 @@ __device__ __forceinline__ void pull_cand(const PullArgs& P, int x, int k, int a
   bd = cd < bd ? cd : bd;
 }
 
-// one wave per arc, lanes over the node's other arcs (levels of high-degree nodes: the top
-// separators, k up to ~1400)
+// S waves per arc (4 / S arcs per workgroup), lanes over the node's other arcs, wave `part` of an
+// arc taking candidate chunks part, part + S, ... (levels of high-degree nodes: the top separators,
+// k up to ~1400 on the 1M-node city — one wave walked ~6 chunks of 256 candidates one after the
+// other; split, each wave walks k / (256 S)).  The parts' minima meet in LDS (min is exact and
+// order-free: bit-identical to one wave).
+template <int S>
 __global__ __launch_bounds__(256) void perfect_pull_wave_kernel(PullArgs P, const unsigned long long* __restrict__ up,
                                                                 const unsigned long long* __restrict__ dn,
                                                                 uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
-  const long long g = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (g >= P.arcs) return;
-  const int ni = item_owner(P.aofs, P.lo, P.hi, P.base + g);
-  const int x = P.nodes[ni];
-  const int a0 = P.up_ptr[x];
-  const int k = P.up_ptr[x + 1] - a0;
-  const int ia = (int)(P.base + g - P.aofs[ni]);
-  const int aa = a0 + ia;
-  const int y = P.up_head[aa];
+  static_assert(S == 1 || S == 2 || S == 4, "waves per arc");
+  constexpr int APB = 4 / S;
+  __shared__ float red[2][4];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long g = (long long)blockIdx.x * APB + w / S;
+  const int part = w % S;
+  const bool active = g < P.arcs;
   float bu = F_INF, bd = F_INF;
-  // four 64-wide chunks of candidates per step, every stage's loads issued together (the serial
-  // tri -> weight chain of a high-degree node's ~22 chunks was the kernel's latency)
-  const long long tb = P.tofs[x];
-  for (int c0 = 0; c0 < k; c0 += 256) {
-    int azy[4], z[4];
-    unsigned long long wu[4], wd[4];
-    bool ok[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int ic = c0 + 64 * u + lane;
-      ok[u] = ic < k && ic != ia;
-      const int i = ic < ia ? ic : ia, j = ic < ia ? ia : ic;
-      azy[u] = ok[u] ? P.tri[tb + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)] : 0;
-      z[u] = ok[u] ? P.up_head[a0 + ic] : 0;
-      wu[u] = ok[u] ? up[a0 + ic] : 0ull;
-      wd[u] = ok[u] ? dn[a0 + ic] : 0ull;
+  int aa = 0;
+  if (active) {
+    int x, a0, k, ia;
+    if (P.parc != nullptr) {
+      const int4 pa = P.parc[P.base + g];
+      x = pa.x;
+      a0 = pa.y;
+      k = pa.z;
+      ia = pa.w;
+    } else {
+      const int ni = item_owner(P.aofs, P.lo, P.hi, P.base + g);
+      x = P.nodes[ni];
+      a0 = P.up_ptr[x];
+      k = P.up_ptr[x + 1] - a0;
+      ia = (int)(P.base + g - P.aofs[ni]);
     }
-    uint32_t gu[4], gd[4];
+    aa = a0 + ia;
+    const int y = P.up_head[aa];
+    // four 64-wide chunks of candidates per step, every stage's loads issued together (the serial
+    // tri -> weight chain of a high-degree node's ~22 chunks was the kernel's latency)
+    const long long tb = P.tofs[x];
+    for (int c0 = 256 * part; c0 < k; c0 += 256 * S) {
+      int azy[4], z[4];
+      unsigned long long wu[4], wd[4];
+      bool ok[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      gu[u] = ok[u] ? pup[azy[u]] : 0u;
-      gd[u] = ok[u] ? pdn[azy[u]] : 0u;
+      for (int u = 0; u < 4; ++u) {
+        const int ic = c0 + 64 * u + lane;
+        ok[u] = ic < k && ic != ia;
+        const int i = ic < ia ? ic : ia, j = ic < ia ? ia : ic;
+        azy[u] = ok[u] ? P.tri[tb + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)] : 0;
+        z[u] = ok[u] ? P.up_head[a0 + ic] : 0;
+        wu[u] = ok[u] ? up[a0 + ic] : 0ull;
+        wd[u] = ok[u] ? dn[a0 + ic] : 0ull;
+      }
+      uint32_t gu[4], gd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        gu[u] = ok[u] ? pup[azy[u]] : 0u;
+        gd[u] = ok[u] ? pdn[azy[u]] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (!ok[u]) continue;
+        const float zy = __uint_as_float(z[u] < y ? gu[u] : gd[u]);
+        const float yz = __uint_as_float(z[u] < y ? gd[u] : gu[u]);
+        const float cu = wof(wu[u]) + zy, cd = yz + wof(wd[u]);
+        bu = cu < bu ? cu : bu;
+        bd = cd < bd ? cd : bd;
+      }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (!ok[u]) continue;
-      const float zy = __uint_as_float(z[u] < y ? gu[u] : gd[u]);
-      const float yz = __uint_as_float(z[u] < y ? gd[u] : gu[u]);
-      const float cu = wof(wu[u]) + zy, cd = yz + wof(wd[u]);
-      bu = cu < bu ? cu : bu;
-      bd = cd < bd ? cd : bd;
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ou = __shfl_xor(bu, o), od = __shfl_xor(bd, o);
+      bu = ou < bu ? ou : bu;
+      bd = od < bd ? od : bd;
     }
   }
+  if constexpr (S > 1) {
+    if (lane == 0) {
+      red[0][w] = bu;
+      red[1][w] = bd;
+    }
+    __syncthreads();
+    if (part != 0) return;
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const float ou = __shfl_xor(bu, o), od = __shfl_xor(bd, o);
-    bu = ou < bu ? ou : bu;
-    bd = od < bd ? od : bd;
+    for (int q = 1; q < S; ++q) {
+      const float ou = red[0][w + q], od = red[1][w + q];
+      bu = ou < bu ? ou : bu;
+      bd = od < bd ? od : bd;
+    }
   }
-  if (lane == 0) {
+  if (active && lane == 0) {
     const float cu = __uint_as_float(pup[aa]), cd = __uint_as_float(pdn[aa]);
     if (bu < cu) pup[aa] = __float_as_uint(bu);
     if (bd < cd) pdn[aa] = __float_as_uint(bd);
@@ -346,11 +384,20 @@ __global__ __launch_bounds__(256) void perfect_pull_lane_kernel(PullArgs P, cons
                                                                 uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= P.arcs) return;
-  const int ni = item_owner(P.aofs, P.lo, P.hi, P.base + g);
-  const int x = P.nodes[ni];
-  const int a0 = P.up_ptr[x];
-  const int k = P.up_ptr[x + 1] - a0;
-  const int ia = (int)(P.base + g - P.aofs[ni]);
+  int x, a0, k, ia;
+  if (P.parc != nullptr) {
+    const int4 pa = P.parc[P.base + g];
+    x = pa.x;
+    a0 = pa.y;
+    k = pa.z;
+    ia = pa.w;
+  } else {
+    const int ni = item_owner(P.aofs, P.lo, P.hi, P.base + g);
+    x = P.nodes[ni];
+    a0 = P.up_ptr[x];
+    k = P.up_ptr[x + 1] - a0;
+    ia = (int)(P.base + g - P.aofs[ni]);
+  }
   const int aa = a0 + ia;
   const int y = P.up_head[aa];
   float bu = __uint_as_float(pup[aa]), bd = __uint_as_float(pdn[aa]);
@@ -377,12 +424,26 @@ struct CustTask {
 };
 constexpr uint16_t ROW_FINAL = 0xFFFF;
 
+// A basic-customization task with its node's arc range and its triangle row's base folded in (24
+// bytes): the wave's first load gives everything the triangle and weight loads need — the 8-byte
+// task cost one more dependent round trip (the node's arc range and triangle offset) per level.
+struct BasicTask {
+  int64_t rowbase;   // pair rows: tofs[z] + i (2k - i - 1) / 2 - i - 1 (column j's triangle at rowbase + j)
+  int32_t node;
+  int32_t a0;        // z's first upward arc
+  uint16_t k;        // z's upward arcs
+  uint16_t row;      // pair row i, or ROW_FINAL
+  uint16_t col0;     // first column of the wave's 64
+  uint16_t pad;
+};
+static_assert(sizeof(BasicTask) == 24, "basic task layout");
+
 // Basic customization of one height level, one task per wave: a pair row (i, j0 .. j0+63) of node
 // z relaxes its lower triangles z of the arcs {head i, head j}; a ROW_FINAL task finalizes 64 of
 // z's own arcs (best triangle's two sub-arcs, metres, road-edge counts).  Same math as
 // basic_level_kernel (bit-identical).
 template <bool SKIP>
-__global__ __launch_bounds__(256) void basic_task_kernel(const CustTask* __restrict__ tasks, long long ntask,
+__global__ __launch_bounds__(256) void basic_task_kernel(const BasicTask* __restrict__ tasks, long long ntask,
                                                          const int32_t* __restrict__ up_ptr,
                                                          const int32_t* __restrict__ up_head,
                                                          const int64_t* __restrict__ tofs, const int32_t* __restrict__ tri,
@@ -394,10 +455,10 @@ __global__ __launch_bounds__(256) void basic_task_kernel(const CustTask* __restr
   const long long ti = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (ti >= ntask) return;
   const int lane = threadIdx.x & 63;
-  const CustTask T = tasks[ti];
+  const BasicTask T = tasks[ti];
   const int z = T.node;
-  const int a0 = up_ptr[z];
-  const int k = up_ptr[z + 1] - a0;
+  const int a0 = T.a0;
+  const int k = T.k;
   if (T.row == ROW_FINAL) {
     const int p = T.col0 + lane;
     if (p >= k) return;
@@ -439,7 +500,7 @@ __global__ __launch_bounds__(256) void basic_task_kernel(const CustTask* __restr
   const int j = T.col0 + lane;
   if (j >= k) return;
   const int ai = a0 + i, aj = a0 + j;
-  const int t = tri[tofs[z] + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)];
+  const int t = tri[T.rowbase + j];
   if (t < 0) return;
   const float wu = wof(dn[ai]) + wof(up[aj]);
   const float wd = wof(dn[aj]) + wof(up[ai]);
@@ -1228,6 +1289,12 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
     pofs_[i + 1] = pofs_[i] + kp * (kp - 1);
     aofs_[i + 1] = aofs_[i] + kp;
   }
+  plev_kmax_.assign((size_t)T_.max_depth + 1, 0);
+  for (int d = 0; d <= T_.max_depth; ++d)
+    for (int64_t i = T_.dlev_ptr[d]; i < T_.dlev_ptr[d + 1]; ++i) {
+      const int x = T_.dlev_nodes[i];
+      plev_kmax_[d] = std::max(plev_kmax_[d], (int)(T_.up_ptr[x + 1] - T_.up_ptr[x]));
+    }
   hipError_t e = hipSuccess;
   auto ck = [&](hipError_t x) {
     if (x != hipSuccess && e == hipSuccess) e = x;
@@ -1249,6 +1316,19 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   ck(up_copy(d_bofs, bofs_.data(), N + 1));
   ck(up_copy(d_pofs, pofs_.data(), N + 1));
   ck(up_copy(d_aofs, aofs_.data(), N + 1));
+  // the perfect pull's per-arc records (ROUTEST_CCH_PARC=0: the binary search instead)
+  if (e == hipSuccess && !(std::getenv("ROUTEST_CCH_PARC") && std::string(std::getenv("ROUTEST_CCH_PARC")) == "0")) {
+    std::vector<int4> parc((size_t)aofs_[N]);
+    for (int i = 0; i < N; ++i) {
+      const int x = T_.dlev_nodes[i];
+      const int a0 = (int)T_.up_ptr[x], k = (int)(T_.up_ptr[x + 1] - T_.up_ptr[x]);
+      for (int ia = 0; ia < k; ++ia) parc[(size_t)aofs_[i] + ia] = make_int4(x, a0, k, ia);
+    }
+    if (!parc.empty() && up_copy(d_parc, parc.data(), (int64_t)parc.size()) != hipSuccess) {
+      (void)hipGetLastError();
+      d_parc = nullptr;
+    }
+  }
   ck(alloc_scratch(cs0_));
   if (builder_max_wg_.load() < 0) builder_max_wg_.store(M >= 20000000LL ? 512 : 0);
   // triangle table within ROUTEST_CCH_TRI_GB of HBM (default 48 — a 1M-node city needs ~38 GB of the 288; 0 disables)
@@ -1267,7 +1347,7 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
                            d_up_ptr, d_up_head, d_tofs, N, (long long)T, d_tri);
         if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
           n_tri = T;
-          build_tasks();
+          build_tasks(tofs);
         } else {
           dfree(d_tri);
           dfree(d_tofs);
@@ -1285,20 +1365,26 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
 }
 
 // the task tables of the task-table customization (metric-independent; level order)
-void CchGpu::build_tasks() {
+void CchGpu::build_tasks(const std::vector<int64_t>& tofs) {
   if (const char* v = std::getenv("ROUTEST_CCH_TASKS"))
     if (std::string(v) == "0") return;
   const int N = T_.N;
-  std::vector<CustTask> bt, pt;
+  std::vector<BasicTask> bt;
+  std::vector<CustTask> pt;
   btask_ptr_.assign(T_.max_height + 2, 0);
   for (int h = 0; h <= T_.max_height; ++h) {
     for (int64_t q = T_.hlev_ptr[h]; q < T_.hlev_ptr[h + 1]; ++q) {
       const int z = T_.hlev_nodes[q];
       const int k = (int)(T_.up_ptr[z + 1] - T_.up_ptr[z]);
       if (k > 0xFFFE) { bt.clear(); pt.clear(); return; }   // (never on road graphs: k <= ~2k)
-      for (int j0 = 0; j0 < k; j0 += 64) bt.push_back(CustTask{z, ROW_FINAL, (uint16_t)j0});
-      for (int i = 0; i + 1 < k; ++i)
-        for (int j0 = i + 1; j0 < k; j0 += 64) bt.push_back(CustTask{z, (uint16_t)i, (uint16_t)j0});
+      const int a0 = (int)T_.up_ptr[z];
+      for (int j0 = 0; j0 < k; j0 += 64)
+        bt.push_back(BasicTask{0, z, a0, (uint16_t)k, ROW_FINAL, (uint16_t)j0, 0});
+      for (int i = 0; i + 1 < k; ++i) {
+        const int64_t rb = tofs[z] + (int64_t)i * (2 * k - i - 1) / 2 - i - 1;
+        for (int j0 = i + 1; j0 < k; j0 += 64)
+          bt.push_back(BasicTask{rb, z, a0, (uint16_t)k, (uint16_t)i, (uint16_t)j0, 0});
+      }
     }
     btask_ptr_[h + 1] = (int64_t)bt.size();
   }
@@ -1316,7 +1402,8 @@ void CchGpu::build_tasks() {
     ptask_ptr_[d + 1] = (int64_t)pt.size();
   }
   (void)N;
-  CustTask *db = nullptr, *dp = nullptr;
+  BasicTask* db = nullptr;
+  CustTask* dp = nullptr;
   const bool ok = up_copy(db, bt.data(), bt.size()) == hipSuccess && up_copy(dp, pt.data(), pt.size()) == hipSuccess;
   d_btask = db;
   d_ptask = dp;
@@ -1364,6 +1451,7 @@ CchGpu::~CchGpu() {
   dfree(d_bofs);
   dfree(d_pofs);
   dfree(d_aofs);
+  dfree(d_parc);
   dfree(d_tofs);
   dfree(d_tri);
   dfree(d_btask);
@@ -1511,7 +1599,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
       const long long ntl = btask_ptr_[h + 1] - btask_ptr_[h];
       for (long long t0 = 0; t0 < ntl && e == hipSuccess; t0 += wave_cap) {
         const long long nt = std::min(wave_cap, ntl - t0);
-        const CustTask* tk = (const CustTask*)d_btask + btask_ptr_[h] + t0;
+        const BasicTask* tk = (const BasicTask*)d_btask + btask_ptr_[h] + t0;
         if (skip)
           hipLaunchKernelGGL(basic_task_kernel<true>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, tk, nt, d_up_ptr,
                              d_up_head, d_tofs, d_tri, X.up64, X.dn64, m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up,
@@ -1564,18 +1652,31 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && pull && d_tri != nullptr; ++d) {
       const int lo = (int)T_.dlev_ptr[d], hi = (int)T_.dlev_ptr[d + 1];
       if (lo >= hi) continue;
-      PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri};
+      PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri, d_parc};
       if (P.arcs <= 0 || pofs_[hi] == pofs_[lo]) continue;       // no node of the level has two arcs
       // mean degree of the level's nodes: wide nodes get a wave per arc, narrow ones a lane per arc
       const bool wave = P.arcs >= 24 * (long long)(hi - lo);
-      const long long cap = wave ? wave_cap : 64 * wave_cap;      // arcs per piece (see wave_cap)
+      // waves per arc by the level's widest node (ROUTEST_CCH_PULL_SPLIT=0: one)
+      static const bool split = !(std::getenv("ROUTEST_CCH_PULL_SPLIT") &&
+                                  std::string(std::getenv("ROUTEST_CCH_PULL_SPLIT")) == "0");
+      const int km = plev_kmax_[d];
+      // (only where the level's arcs alone do not fill the GPU: 1M-city levels of thousands of wide
+      // nodes are bound by their random gathers, and splitting them measured 1 % slower, r5z)
+      const int S = (!split || P.arcs >= 8192) ? 1 : (km > 768 ? 4 : (km > 256 ? 2 : 1));
+      const long long cap = wave ? std::max(1LL, wave_cap / S) : 64 * wave_cap;   // arcs per piece (see wave_cap)
       const long long arcs = P.arcs, base = P.base;
       for (long long a0 = 0; a0 < arcs && e == hipSuccess; a0 += cap) {
         P.base = base + a0;
         P.arcs = std::min(cap, arcs - a0);
-        if (wave)
-          hipLaunchKernelGGL(perfect_pull_wave_kernel, dim3((unsigned)((P.arcs + 3) / 4)), dim3(256), 0, s, P, X.up64,
-                             X.dn64, X.pup, X.pdn);
+        if (wave && S == 4)
+          hipLaunchKernelGGL(perfect_pull_wave_kernel<4>, dim3((unsigned)P.arcs), dim3(256), 0, s, P, X.up64, X.dn64,
+                             X.pup, X.pdn);
+        else if (wave && S == 2)
+          hipLaunchKernelGGL(perfect_pull_wave_kernel<2>, dim3((unsigned)((P.arcs + 1) / 2)), dim3(256), 0, s, P,
+                             X.up64, X.dn64, X.pup, X.pdn);
+        else if (wave)
+          hipLaunchKernelGGL(perfect_pull_wave_kernel<1>, dim3((unsigned)((P.arcs + 3) / 4)), dim3(256), 0, s, P,
+                             X.up64, X.dn64, X.pup, X.pdn);
         else
           hipLaunchKernelGGL(perfect_pull_lane_kernel, dim3(blocks_for(P.arcs, 256)), dim3(256), 0, s, P, X.up64,
                              X.dn64, X.pup, X.pdn);

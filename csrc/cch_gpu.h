@@ -248,7 +248,9 @@ class CchGpu {
   int32_t *d_hnodes = nullptr, *d_dnodes = nullptr;
   int64_t *d_bofs = nullptr, *d_pofs = nullptr;    // work-item prefixes in level order
   int64_t* d_aofs = nullptr;                       // arc prefix in depth order (perfect pull)
+  int4* d_parc = nullptr;                          // per depth-ordered arc: {node, first arc, arcs, index}
   std::vector<int64_t> bofs_, pofs_, aofs_;        // host copies (level boundaries)
+  std::vector<int> plev_kmax_;                     // widest node (upward arcs) per depth level
   // triangle table (metric-independent): for the pair (i < j) of rank z's upward arcs, the arc id of
   // {head i, head j} at tri[tofs[z] + i(2k-i-1)/2 + j-i-1] — the customization's binary searches
   // done once per graph (nullptr when it would not fit the ROUTEST_CCH_TRI_GB budget)
@@ -256,7 +258,7 @@ class CchGpu {
   int32_t* d_tri = nullptr;
   int64_t n_tri = 0;
   // task tables of the customization (csrc/cch.hip build_tasks): 8-byte wave tasks in level order
-  void build_tasks();
+  void build_tasks(const std::vector<int64_t>& tofs);
   void* d_btask = nullptr;
   void* d_ptask = nullptr;
   std::vector<int64_t> btask_ptr_, ptask_ptr_;
