@@ -264,17 +264,28 @@ struct PullArgs {
   long long base, arcs;    // arc range of the level
   const int64_t* tofs;     // triangle table (required)
   const int32_t* tri;
-  // {node x, x's first arc, x's arc count, the arc's index in x} per depth-ordered arc: one load
-  // instead of the binary search over the level's nodes + two dependent loads (a level of
-  // thousands of nodes searched ~12 dependent steps per wave); nullptr: search
-  const int4* parc;
+  // per depth-ordered arc: everything the pull needs before its candidate loads, in one load —
+  // instead of the binary search over the level's nodes (a level of thousands of nodes searched ~12
+  // dependent steps per wave) and the dependent loads of the node's arc range, triangle offset and
+  // the arc's head; nullptr: search
+  const struct PArc* parc;
 };
 
-__device__ __forceinline__ void pull_cand(const PullArgs& P, int x, int k, int a0, int ia, int ic, float xz_c, float zx_c,
-                                          const uint32_t* __restrict__ pup, const uint32_t* __restrict__ pdn, int y,
-                                          int z, float& bu, float& bd) {
+struct PArc {
+  int64_t tb;        // tofs[x]: the node's triangle table offset
+  int32_t a0;        // x's first upward arc
+  int32_t y;         // the arc's head
+  uint16_t k;        // x's upward arcs
+  uint16_t ia;       // the arc's index among them
+  int32_t pad;
+};
+static_assert(sizeof(PArc) == 24, "pull arc record");
+
+__device__ __forceinline__ void pull_cand(const PullArgs& P, long long tb, int k, int a0, int ia, int ic, float xz_c,
+                                          float zx_c, const uint32_t* __restrict__ pup, const uint32_t* __restrict__ pdn,
+                                          int y, int z, float& bu, float& bd) {
   const int i = ic < ia ? ic : ia, j = ic < ia ? ia : ic;
-  const int azy = P.tri[P.tofs[x] + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)];
+  const int azy = P.tri[tb + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)];
   const float zy = __uint_as_float(z < y ? pup[azy] : pdn[azy]);
   const float yz = __uint_as_float(z < y ? pdn[azy] : pup[azy]);
   const float cu = xz_c + zy, cd = yz + zx_c;
@@ -301,25 +312,28 @@ __global__ __launch_bounds__(256) void perfect_pull_wave_kernel(PullArgs P, cons
   float bu = F_INF, bd = F_INF;
   int aa = 0;
   if (active) {
-    int x, a0, k, ia;
+    int a0, k, ia, y;
+    long long tb;
     if (P.parc != nullptr) {
-      const int4 pa = P.parc[P.base + g];
-      x = pa.x;
-      a0 = pa.y;
-      k = pa.z;
-      ia = pa.w;
+      const PArc pa = P.parc[P.base + g];
+      tb = pa.tb;
+      a0 = pa.a0;
+      y = pa.y;
+      k = pa.k;
+      ia = pa.ia;
+      aa = a0 + ia;
     } else {
       const int ni = item_owner(P.aofs, P.lo, P.hi, P.base + g);
-      x = P.nodes[ni];
+      const int x = P.nodes[ni];
       a0 = P.up_ptr[x];
       k = P.up_ptr[x + 1] - a0;
       ia = (int)(P.base + g - P.aofs[ni]);
+      aa = a0 + ia;
+      y = P.up_head[aa];
+      tb = P.tofs[x];
     }
-    aa = a0 + ia;
-    const int y = P.up_head[aa];
     // four 64-wide chunks of candidates per step, every stage's loads issued together (the serial
     // tri -> weight chain of a high-degree node's ~22 chunks was the kernel's latency)
-    const long long tb = P.tofs[x];
     for (int c0 = 256 * part; c0 < k; c0 += 256 * S) {
       int azy[4], z[4];
       unsigned long long wu[4], wd[4];
@@ -384,27 +398,30 @@ __global__ __launch_bounds__(256) void perfect_pull_lane_kernel(PullArgs P, cons
                                                                 uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= P.arcs) return;
-  int x, a0, k, ia;
+  int a0, k, ia, y;
+  long long tb;
   if (P.parc != nullptr) {
-    const int4 pa = P.parc[P.base + g];
-    x = pa.x;
-    a0 = pa.y;
-    k = pa.z;
-    ia = pa.w;
+    const PArc pa = P.parc[P.base + g];
+    tb = pa.tb;
+    a0 = pa.a0;
+    y = pa.y;
+    k = pa.k;
+    ia = pa.ia;
   } else {
     const int ni = item_owner(P.aofs, P.lo, P.hi, P.base + g);
-    x = P.nodes[ni];
+    const int x = P.nodes[ni];
     a0 = P.up_ptr[x];
     k = P.up_ptr[x + 1] - a0;
     ia = (int)(P.base + g - P.aofs[ni]);
+    y = P.up_head[a0 + ia];
+    tb = P.tofs[x];
   }
   const int aa = a0 + ia;
-  const int y = P.up_head[aa];
   float bu = __uint_as_float(pup[aa]), bd = __uint_as_float(pdn[aa]);
   for (int ic = 0; ic < k; ++ic) {
     if (ic == ia) continue;
     const int ac = a0 + ic;
-    pull_cand(P, x, k, a0, ia, ic, wof(up[ac]), wof(dn[ac]), pup, pdn, y, P.up_head[ac], bu, bd);
+    pull_cand(P, tb, k, a0, ia, ic, wof(up[ac]), wof(dn[ac]), pup, pdn, y, P.up_head[ac], bu, bd);
   }
   pup[aa] = __float_as_uint(bu);
   pdn[aa] = __float_as_uint(bd);
@@ -1316,19 +1333,7 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   ck(up_copy(d_bofs, bofs_.data(), N + 1));
   ck(up_copy(d_pofs, pofs_.data(), N + 1));
   ck(up_copy(d_aofs, aofs_.data(), N + 1));
-  // the perfect pull's per-arc records (ROUTEST_CCH_PARC=0: the binary search instead)
-  if (e == hipSuccess && !(std::getenv("ROUTEST_CCH_PARC") && std::string(std::getenv("ROUTEST_CCH_PARC")) == "0")) {
-    std::vector<int4> parc((size_t)aofs_[N]);
-    for (int i = 0; i < N; ++i) {
-      const int x = T_.dlev_nodes[i];
-      const int a0 = (int)T_.up_ptr[x], k = (int)(T_.up_ptr[x + 1] - T_.up_ptr[x]);
-      for (int ia = 0; ia < k; ++ia) parc[(size_t)aofs_[i] + ia] = make_int4(x, a0, k, ia);
-    }
-    if (!parc.empty() && up_copy(d_parc, parc.data(), (int64_t)parc.size()) != hipSuccess) {
-      (void)hipGetLastError();
-      d_parc = nullptr;
-    }
-  }
+
   ck(alloc_scratch(cs0_));
   if (builder_max_wg_.load() < 0) builder_max_wg_.store(M >= 20000000LL ? 512 : 0);
   // triangle table within ROUTEST_CCH_TRI_GB of HBM (default 48 — a 1M-node city needs ~38 GB of the 288; 0 disables)
@@ -1348,6 +1353,7 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
         if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
           n_tri = T;
           build_tasks(tofs);
+          build_pull_records(tofs);
         } else {
           dfree(d_tri);
           dfree(d_tofs);
@@ -1365,6 +1371,27 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
 }
 
 // the task tables of the task-table customization (metric-independent; level order)
+// the perfect pull's per-arc records (ROUTEST_CCH_PARC=0: the binary search instead)
+void CchGpu::build_pull_records(const std::vector<int64_t>& tofs) {
+  if (const char* v = std::getenv("ROUTEST_CCH_PARC"))
+    if (std::string(v) == "0") return;
+  const int N = T_.N;
+  std::vector<PArc> parc((size_t)aofs_[N]);
+  for (int i = 0; i < N; ++i) {
+    const int x = T_.dlev_nodes[i];
+    const int a0 = (int)T_.up_ptr[x], k = (int)(T_.up_ptr[x + 1] - T_.up_ptr[x]);
+    if (k > 0xFFFF) return;                   // (never on road graphs)
+    for (int ia = 0; ia < k; ++ia)
+      parc[(size_t)aofs_[i] + ia] = PArc{tofs[x], a0, (int32_t)T_.up_head[a0 + ia], (uint16_t)k, (uint16_t)ia, 0};
+  }
+  PArc* dp = nullptr;
+  if (!parc.empty() && up_copy(dp, parc.data(), parc.size()) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  d_parc = dp;
+}
+
 void CchGpu::build_tasks(const std::vector<int64_t>& tofs) {
   if (const char* v = std::getenv("ROUTEST_CCH_TASKS"))
     if (std::string(v) == "0") return;
@@ -1652,7 +1679,8 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && pull && d_tri != nullptr; ++d) {
       const int lo = (int)T_.dlev_ptr[d], hi = (int)T_.dlev_ptr[d + 1];
       if (lo >= hi) continue;
-      PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri, d_parc};
+      PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri,
+                 (const PArc*)d_parc};
       if (P.arcs <= 0 || pofs_[hi] == pofs_[lo]) continue;       // no node of the level has two arcs
       // mean degree of the level's nodes: wide nodes get a wave per arc, narrow ones a lane per arc
       const bool wave = P.arcs >= 24 * (long long)(hi - lo);

@@ -248,7 +248,7 @@ class CchGpu {
   int32_t *d_hnodes = nullptr, *d_dnodes = nullptr;
   int64_t *d_bofs = nullptr, *d_pofs = nullptr;    // work-item prefixes in level order
   int64_t* d_aofs = nullptr;                       // arc prefix in depth order (perfect pull)
-  int4* d_parc = nullptr;                          // per depth-ordered arc: {node, first arc, arcs, index}
+  void* d_parc = nullptr;                          // per depth-ordered arc: csrc/cch.hip PArc
   std::vector<int64_t> bofs_, pofs_, aofs_;        // host copies (level boundaries)
   std::vector<int> plev_kmax_;                     // widest node (upward arcs) per depth level
   // triangle table (metric-independent): for the pair (i < j) of rank z's upward arcs, the arc id of
@@ -259,6 +259,7 @@ class CchGpu {
   int64_t n_tri = 0;
   // task tables of the customization (csrc/cch.hip build_tasks): 8-byte wave tasks in level order
   void build_tasks(const std::vector<int64_t>& tofs);
+  void build_pull_records(const std::vector<int64_t>& tofs);
   void* d_btask = nullptr;
   void* d_ptask = nullptr;
   std::vector<int64_t> btask_ptr_, ptask_ptr_;
