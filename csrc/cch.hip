@@ -1888,20 +1888,30 @@ void CchGpu::request_build(const CchContext& c, bool urgent) {
     if (bstop_ || !bpending_.insert(key).second) return;   // stopping, or already queued / building
     if (urgent) bq_.push_front(c);
     else bq_.push_back(c);
-    if (bths_.empty()) {
-      // ROUTEST_CCH_BUILDERS concurrent builders (default 3), each with its own temporaries: a
-      // customization is a chain of dependent level launches that keeps a fraction of the GPU busy,
-      // so a burst of fresh contexts builds several at a time
-      static const int nb = [] {
-        const char* v = std::getenv("ROUTEST_CCH_BUILDERS");
-        const int k = v ? std::atoi(v) : 3;
-        return k < 1 ? 1 : (k > 8 ? 8 : k);
-      }();
-      for (int i = 0; i < nb; ++i) bths_.emplace_back([this, i] { builder_loop(i); });
-    }
+    start_builders_locked();
   }
   n_bqueued_.fetch_add(1, std::memory_order_relaxed);
   bcv_.notify_one();
+}
+
+// ROUTEST_CCH_BUILDERS concurrent builders (default 3), each with its own temporaries: a
+// customization is a chain of dependent level launches that keeps a fraction of the GPU busy, so a
+// burst of fresh contexts builds several at a time.  (caller holds bmu_)
+void CchGpu::start_builders_locked() {
+  if (!bths_.empty() || bstop_) return;
+  static const int nb = [] {
+    const char* v = std::getenv("ROUTEST_CCH_BUILDERS");
+    const int k = v ? std::atoi(v) : 3;
+    return k < 1 ? 1 : (k > 8 ? 8 : k);
+  }();
+  for (int i = 0; i < nb; ++i) bths_.emplace_back([this, i] { builder_loop(i); });
+}
+
+// the builders and their temporaries (device + pinned host allocations) now — a route service
+// calls this at startup, so no allocation happens on the GPU while flushes are in flight
+void CchGpu::start_builders() {
+  std::lock_guard<std::mutex> lk(bmu_);
+  start_builders_locked();
 }
 
 int CchGpu::add_build_listener(std::function<void(uint64_t, bool)> cb) {

@@ -168,6 +168,7 @@ class CchGpu {
   // caller's thread: a caller must not hold a lock its listener takes).  urgent: ahead of queued
   // prefetches (a request waits for it).
   void request_build(const CchContext& c, bool urgent = true);
+  void start_builders();
   int add_build_listener(std::function<void(uint64_t, bool)> cb);
   void remove_build_listener(int id);
   struct AsyncStats {
@@ -290,6 +291,7 @@ class CchGpu {
   std::atomic<uint64_t> tag_ctr_{0};
   // asynchronous builds
   void builder_loop(int idx);
+  void start_builders_locked();
   void notify_built(uint64_t key, bool ok);
   std::vector<std::thread> bths_;                  // ROUTEST_CCH_BUILDERS threads (default 3)
   std::mutex bmu_;

@@ -677,8 +677,10 @@ struct RouteService::Impl {
     // rehearsal knob (bench/route_context_bench.py): shifts the clock "now" routing contexts are
     // resolved with, so an hour boundary can be crossed on demand
     if (const char* v = std::getenv("ROUTEST_ROUTE_CLOCK_SKEW_S")) clock_skew_s = std::atoll(v);
-    if (cfg.cch != nullptr && cfg.cch_contexts && async_ctx)
+    if (cfg.cch != nullptr && cfg.cch_contexts && async_ctx) {
       listener = cfg.cch->add_build_listener([this](uint64_t key, bool ok) { on_built(key, ok); });
+      cfg.cch->start_builders();         // their allocations at startup, not mid-serving
+    }
     if (std::getenv("ROUTEST_ROUTE_PREWARM") == nullptr || std::string(std::getenv("ROUTEST_ROUTE_PREWARM")) != "0")
       prewarm();
     if (const char* v = std::getenv("ROUTEST_HANG_ARM"))      // the watchdog rehearsal: see native_server.hip
