@@ -4,6 +4,7 @@
 // extension (rt.cpp) and into the ASan/UBSan fuzz harness (rt_selftest.cpp).
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <climits>
 #include <cmath>
@@ -11,6 +12,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <utility>
@@ -466,7 +472,54 @@ inline bool split_top_array(const char* s, size_t n, std::vector<std::pair<size_
   return false;
 }
 
-// Run fn(begin, end) over [0, n) on up to `max_threads` threads (serial below `min_per_thread`).
+// A process-wide pool of worker threads (ROUTEST_CPU_POOL, default min(cores, 16)) for
+// parallel_chunks: the route service calls it several times per flush (snapping, plan unpacking,
+// assembly, row texts), and a fresh std::thread per chunk per call cost ~20 us each — thousands of
+// thread creations per second competing for the CPU with the SQLite writer.  Leaked on purpose: its
+// workers are detached and wait on it until the process ends.
+class WorkPool {
+ public:
+  static WorkPool& get() {
+    static WorkPool* p = new WorkPool();
+    return *p;
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  WorkPool() {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const char* v = std::getenv("ROUTEST_CPU_POOL");
+    const unsigned n = v ? (unsigned)std::max(1, std::atoi(v)) : std::min(hw, 16u);
+    for (unsigned i = 0; i < n; ++i) std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    while (true) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+};
+
+// Run fn(begin, end) over [0, n) in up to `max_threads` chunks (serial below `min_per_thread`):
+// the pool's workers and the caller take chunks from a shared counter, the caller returns when all
+// are done.  The caller always works too, so a call made from a pool worker (or in a forked child
+// whose pool has no workers) still finishes; a helper that starts late finds no chunk left and
+// never touches fn.
 template <class F>
 inline void parallel_chunks(size_t n, size_t min_per_thread, unsigned max_threads, F fn) {
   unsigned hw = std::max(1u, std::thread::hardware_concurrency());
@@ -475,14 +528,29 @@ inline void parallel_chunks(size_t n, size_t min_per_thread, unsigned max_thread
     fn((size_t)0, n);
     return;
   }
-  std::vector<std::thread> pool;
   const size_t per = (n + t - 1) / t;
-  for (size_t k = 0; k < t; ++k) {
-    const size_t b = k * per, e = std::min(n, b + per);
-    if (b >= e) break;
-    pool.emplace_back([=, &fn]() { fn(b, e); });
-  }
-  for (auto& th : pool) th.join();
+  const size_t chunks = (n + per - 1) / per;
+  struct State {
+    std::atomic<size_t> next{0}, done{0};
+    std::mutex m;
+    std::condition_variable cv;
+  };
+  auto st = std::make_shared<State>();
+  F* fp = &fn;
+  auto work = [st, fp, chunks, per, n]() {
+    size_t k;
+    while ((k = st->next.fetch_add(1)) < chunks) {
+      (*fp)(k * per, std::min(n, (k + 1) * per));
+      if (st->done.fetch_add(1) + 1 == chunks) {
+        std::lock_guard<std::mutex> lk(st->m);
+        st->cv.notify_all();
+      }
+    }
+  };
+  for (size_t k = 1; k < chunks; ++k) WorkPool::get().submit(work);
+  work();
+  std::unique_lock<std::mutex> lk(st->m);
+  st->cv.wait(lk, [&] { return st->done.load() == chunks; });
 }
 
 }  // namespace rtc
