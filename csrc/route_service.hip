@@ -427,6 +427,7 @@ struct RouteService::Impl {
   bool ck_stop = false;
 
   std::shared_ptr<BlobLog> blobs;          // the side file of legs / geometry (nullptr: inline)
+  rtr::CoordCache coord_cache;             // graph nodes' "[lon,lat]" strings (graph provider)
 
   void open_store() {
     if (cfg.sqlite_path.empty()) return;
@@ -1726,7 +1727,8 @@ struct RouteService::Impl {
           }
         }
         if (!perr.empty()) j->req.error = perr;
-        if (!rtr::assemble(j->req, j->plan, dirs, cfg.engine, j->asmb)) j->fallback = true;
+        if (!rtr::assemble(j->req, j->plan, dirs, cfg.engine, j->asmb, coord_cache.ofs.empty() ? nullptr : &coord_cache))
+          j->fallback = true;
         else if (j->req.alt_k > 0 && j->asmb.ok) j->asmb.body += j->alt_json;
       }
     });
@@ -1998,7 +2000,10 @@ struct RouteService::Impl {
 RouteService::RouteService(const RouteServiceCfg& cfg, std::function<void(RouteJob*)> done) : p_(new Impl) {
   p_->cfg = cfg;
   p_->done = std::move(done);
-  if (cfg.provider == 1 && cfg.glat != nullptr) p_->grid.build(cfg.glat, cfg.glon, (size_t)cfg.N, cfg.snap_c);
+  if (cfg.provider == 1 && cfg.glat != nullptr) {
+    p_->grid.build(cfg.glat, cfg.glon, (size_t)cfg.N, cfg.snap_c);
+    p_->coord_cache.build(cfg.glat, cfg.glon, (size_t)cfg.N);
+  }
   p_->th = std::thread([this] { p_->run(); });
 }
 

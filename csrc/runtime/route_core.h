@@ -433,6 +433,7 @@ inline RouteReq parse_route_request(const Value* root) {
 struct Dir {
   std::vector<double> xy;     // lon, lat pairs (geometry coordinates)
   std::vector<uint8_t> raw;   // per point: 1 = an input coordinate (repr), 0 = rounded node/interp
+  std::vector<int32_t> node;  // graph directions: per point its graph node (-1: not a node)
   std::string segments;       // JSON elements (no brackets), comma-joined
   std::vector<long long> way_points;
   double dist = 0, dur = 0;   // round(tot, 1)
@@ -445,6 +446,23 @@ inline void put_xy(std::string& o, double x, double y, bool raw) {
   if (raw) put_float(o, y); else put_coord(o, y);
   o += ']';
 }
+
+// Every graph node's geometry point "[lon,lat]" (put_xy of its rounded coordinates), formatted
+// once per graph: a route's coordinates are then copies, not ~10k float formats per response
+// (the assembly stage's largest cost).  Byte-identical by construction.
+struct CoordCache {
+  std::string buf;
+  std::vector<int64_t> ofs;   // node n at buf[ofs[n], ofs[n + 1])
+  void build(const double* glat, const double* glon, size_t N) {
+    buf.clear();
+    buf.reserve(N * 24);
+    ofs.assign(N + 1, 0);
+    for (size_t n = 0; n < N; ++n) {
+      put_xy(buf, np_round6(glon[n]), np_round6(glat[n]), false);
+      ofs[n + 1] = (int64_t)buf.size();
+    }
+  }
+};
 
 inline void step_pair(std::string& seg, double d_r, double t_r, int k, int nlegs, const char* instr1,
                       long long start, long long end) {
@@ -473,6 +491,7 @@ inline void haversine_directions(const std::vector<std::pair<double, double>>& c
   const double speed = profile_speed(profile);
   out.xy.assign({c[0].first, c[0].second});
   out.raw.assign({1});
+  out.node.clear();                     // (interpolated points: no node strings)
   out.way_points.assign({0});
   out.segments.clear();
   double tot_d = 0.0;
@@ -714,6 +733,7 @@ inline std::string graph_directions(const std::vector<std::pair<double, double>>
   const double speed_scale = profile_speed(CAR) / profile_speed(profile);
   out.xy.assign({c[0].first, c[0].second});
   out.raw.assign({1});
+  out.node.assign({-1});
   out.way_points.assign({0});
   out.segments.clear();
   double tot_d = 0.0, tot_t = 0.0;
@@ -733,10 +753,12 @@ inline std::string graph_directions(const std::vector<std::pair<double, double>>
       out.xy.push_back(np_round6(glon[L.path[i]]));
       out.xy.push_back(np_round6(glat[L.path[i]]));
       out.raw.push_back(0);
+      out.node.push_back(L.path[i]);
     }
     out.xy.push_back(c[k + 1].first);
     out.xy.push_back(c[k + 1].second);
     out.raw.push_back(1);
+    out.node.push_back(-1);
     const long long end = (long long)out.raw.size() - 1;
     out.way_points.push_back(end);
     const double dur = (double)L.sec * speed_scale;
@@ -784,11 +806,18 @@ inline void put_bbox(std::string& o, const std::vector<double>& xy) {
   o += ']';
 }
 
-inline void put_coords(std::string& o, const std::vector<double>& xy, const std::vector<uint8_t>& raw) {
+inline void put_coords(std::string& o, const std::vector<double>& xy, const std::vector<uint8_t>& raw,
+                       const std::vector<int32_t>* node = nullptr, const CoordCache* cc = nullptr) {
+  const bool cached = cc != nullptr && node != nullptr && node->size() == raw.size();
+  o.reserve(o.size() + raw.size() * 24 + 2);
   o += '[';
   for (size_t i = 0; i < raw.size(); ++i) {
     if (i) o += ',';
-    put_xy(o, xy[2 * i], xy[2 * i + 1], raw[i] != 0);
+    const int32_t n = cached ? (*node)[i] : -1;
+    if (n >= 0 && !raw[i] && (size_t)n + 1 < cc->ofs.size())
+      o.append(cc->buf, (size_t)cc->ofs[n], (size_t)(cc->ofs[n + 1] - cc->ofs[n]));
+    else
+      put_xy(o, xy[2 * i], xy[2 * i + 1], raw[i] != 0);
   }
   o += ']';
 }
@@ -875,7 +904,7 @@ struct Assembled {
 
 // Assemble from the directions results `dirs` (one per directions_calls entry).
 inline bool assemble(const RouteReq& r, const Plan& p, const std::vector<Dir>& dirs,
-                     const std::string& engine, Assembled& a) {
+                     const std::string& engine, Assembled& a, const CoordCache* cc = nullptr) {
   a = Assembled();
   if (!r.error.empty()) { a.error = r.error; return true; }
   if (p.infeasible) { a.error = infeasible_msg(p.infeasible_stops); return true; }
@@ -884,7 +913,7 @@ inline bool assemble(const RouteReq& r, const Plan& p, const std::vector<Dir>& d
     const Dir& d = dirs[0];
     const std::string e = p2p_errors(r, d.dist);
     if (!e.empty()) { a.error = e; return true; }
-    put_coords(a.coords, d.xy, d.raw);
+    put_coords(a.coords, d.xy, d.raw, &d.node, cc);
     a.segments = "[" + d.segments + "]";
     a.order = "[0]";
     a.dist = d.dist;
@@ -907,14 +936,18 @@ inline bool assemble(const RouteReq& r, const Plan& p, const std::vector<Dir>& d
   } else {
     std::vector<double> xy;
     std::vector<uint8_t> raw;
+    std::vector<int32_t> node;
+    bool nodes_ok = cc != nullptr;
     double tot_d = 0.0, tot_t = 0.0;
     for (const Dir& d : dirs) {
       xy.insert(xy.end(), d.xy.begin(), d.xy.end());
       raw.insert(raw.end(), d.raw.begin(), d.raw.end());
+      nodes_ok = nodes_ok && d.node.size() == d.raw.size();
+      if (nodes_ok) node.insert(node.end(), d.node.begin(), d.node.end());
       tot_d += d.dist;
       tot_t += d.dur;
     }
-    put_coords(a.coords, xy, raw);
+    put_coords(a.coords, xy, raw, nodes_ok ? &node : nullptr, cc);
     a.segments = "[";
     bool first = true;
     for (const Dir& d : dirs) {

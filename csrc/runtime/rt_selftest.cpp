@@ -147,6 +147,49 @@ static void fuzz_float(std::mt19937_64& rng, int iters) {
 // route_core.h: py_round(x, 1)'s fast path, put_float's integer-tenths path and put_coord's
 // six-decimal path must give the bits / text of their slow (CPython-equivalent) references, and
 // parse_route_request must survive any mutated request body.
+// route_core.h CoordCache: a route's coordinates copied from the per-node strings equal the
+// formatted ones, byte for byte (nodes near 0, negative, with trailing zeros, repr-form values)
+static void fuzz_coord_cache(std::mt19937_64& rng, int iters) {
+  const size_t N = 512;
+  std::vector<double> lat(N), lon(N);
+  std::uniform_real_distribution<double> U(-180.0, 180.0);
+  for (size_t n = 0; n < N; ++n) {
+    switch (n % 5) {
+      case 0: lat[n] = U(rng) / 2; lon[n] = U(rng); break;
+      case 1: lat[n] = std::round(U(rng) * 1e3) / 1e3; lon[n] = std::round(U(rng) * 10) / 10; break;
+      case 2: lat[n] = U(rng) * 1e-6; lon[n] = -U(rng) * 1e-5; break;
+      case 3: lat[n] = 14.5 + U(rng) * 1e-4; lon[n] = 121.0 + U(rng) * 1e-4; break;
+      default: lat[n] = 0.0; lon[n] = -0.0; break;
+    }
+  }
+  rtr::CoordCache cc;
+  cc.build(lat.data(), lon.data(), N);
+  for (int it = 0; it < iters; ++it) {
+    std::vector<double> xy;
+    std::vector<uint8_t> raw;
+    std::vector<int32_t> node;
+    const int len = 1 + (int)(rng() % 40);
+    for (int i = 0; i < len; ++i) {
+      if (rng() % 4 == 0) {
+        xy.push_back(U(rng));
+        xy.push_back(U(rng) / 2);
+        raw.push_back(1);
+        node.push_back(-1);
+      } else {
+        const int n = (int)(rng() % N);
+        xy.push_back(rtr::np_round6(lon[n]));
+        xy.push_back(rtr::np_round6(lat[n]));
+        raw.push_back(0);
+        node.push_back(n);
+      }
+    }
+    std::string a, b;
+    rtr::put_coords(a, xy, raw);
+    rtr::put_coords(b, xy, raw, &node, &cc);
+    CHECK(a == b, "coord cache: %s vs %s", a.c_str(), b.c_str());
+  }
+}
+
 static void fuzz_route(std::mt19937_64& rng, int iters) {
   for (int it = 0; it < iters; ++it) {
     double x;
@@ -378,6 +421,7 @@ int main(int argc, char** argv) {
   fuzz_iso(rng, iters);
   fuzz_float(rng, iters);
   fuzz_route(rng, iters);
+  fuzz_coord_cache(rng, iters);
   fuzz_alternatives(rng, iters);
   fuzz_history(rng, iters);
   threaded_pack_format(20000);
