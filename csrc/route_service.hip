@@ -428,6 +428,7 @@ struct RouteService::Impl {
 
   std::shared_ptr<BlobLog> blobs;          // the side file of legs / geometry (nullptr: inline)
   rtr::CoordCache coord_cache;             // graph nodes' "[lon,lat]" strings (graph provider)
+  std::vector<double> edge_heading;        // per road edge: rtr::hop_heading (graph provider)
 
   void open_store() {
     if (cfg.sqlite_path.empty()) return;
@@ -1719,6 +1720,7 @@ struct RouteService::Impl {
               gh.cost = b.host_cost[j->group]->data();
               gh.edge_name = cfg.h_edge_name;
               gh.names = &cfg.names;
+              gh.edge_heading = edge_heading.empty() ? nullptr : edge_heading.data();
               ghp = &gh;
             }
             perr = rtr::graph_directions(j->calls[k], j->nodes.data() + off, lp, j->req.profile, cfg.glat, cfg.glon,
@@ -2003,6 +2005,13 @@ RouteService::RouteService(const RouteServiceCfg& cfg, std::function<void(RouteJ
   if (cfg.provider == 1 && cfg.glat != nullptr) {
     p_->grid.build(cfg.glat, cfg.glon, (size_t)cfg.N, cfg.snap_c);
     p_->coord_cache.build(cfg.glat, cfg.glon, (size_t)cfg.N);
+    if (cfg.h_indptr != nullptr && cfg.h_indices != nullptr) {
+      const int64_t E = cfg.h_indptr[cfg.N];
+      p_->edge_heading.resize((size_t)E);
+      for (int u = 0; u < cfg.N; ++u)
+        for (int32_t e = cfg.h_indptr[u]; e < cfg.h_indptr[u + 1]; ++e)
+          p_->edge_heading[(size_t)e] = rtr::hop_heading(cfg.glat, cfg.glon, u, cfg.h_indices[e]);
+    }
   }
   p_->th = std::thread([this] { p_->run(); });
 }

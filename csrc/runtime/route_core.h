@@ -541,7 +541,19 @@ struct GraphHost {
   const float* cost = nullptr;
   const int32_t* edge_name = nullptr;
   const std::vector<std::string>* names = nullptr;
+  // per road edge (CSR order, tail -> head): its hop heading as leg_steps computes it (hop_heading),
+  // formatted once per graph; nullptr: computed per hop
+  const double* edge_heading = nullptr;
 };
+
+// leg_steps' hop heading from u to v: the local equirectangular bearing (one atan2 and one cos;
+// the segments are metres long, so it agrees with the great-circle bearing to far below the 25 /
+// 50 degree turn thresholds).  The Python provider runs this same code (_rt.GraphSteps).
+inline double hop_heading(const double* glat, const double* glon, int32_t u, int32_t v) {
+  const double d2r = PY_PI / 180.0, r2d = 180.0 / PY_PI;
+  const double x = (glon[v] - glon[u]) * std::cos(0.5 * (glat[u] + glat[v]) * d2r), y = glat[v] - glat[u];
+  return py_mod(std::atan2(x, y) * r2d + 360.0, 360.0);
+}
 
 // initial bearing (degrees, [0, 360)) — the same expression bearing_word rounds
 inline double bearing_deg(double lat1, double lon1, double lat2, double lon2) {
@@ -636,16 +648,15 @@ inline void leg_steps(const GraphHost& g, const double* glat, const double* glon
   hop.resize(H);
   nm.resize(H);
   brg.resize(H);
-  // hop headings for the turn decisions: the local equirectangular bearing (one atan2 and one cos;
-  // the segments are metres long, so it agrees with the great-circle bearing to far below the 25 /
-  // 50 degree turn thresholds).  The Python provider runs this same code (_rt.GraphSteps).
-  const double d2r = PY_PI / 180.0, r2d = 180.0 / PY_PI;
+  // hop headings for the turn decisions (hop_heading; from the per-edge table when the hop's edge
+  // is known: the same value, computed once per graph)
   for (int h = 0; h < H; ++h) {
     const int32_t u = L.path[h], v = L.path[h + 1];
     hop[h] = L.edges ? L.edges[h] : hop_edge(g, u, v);
     nm[h] = (hop[h] >= 0 && g.edge_name) ? g.edge_name[hop[h]] : -1;
-    const double x = (glon[v] - glon[u]) * std::cos(0.5 * (glat[u] + glat[v]) * d2r), y = glat[v] - glat[u];
-    brg[h] = py_mod(std::atan2(x, y) * r2d + 360.0, 360.0);
+    brg[h] = (g.edge_heading != nullptr && hop[h] >= 0 && g.indices != nullptr && g.indices[hop[h]] == v)
+                 ? g.edge_heading[hop[h]]
+                 : hop_heading(glat, glon, u, v);
   }
   auto name_of = [&](int32_t id) -> const std::string* {
     return (id >= 0 && g.names && id < (int32_t)g.names->size()) ? &(*g.names)[id] : nullptr;
