@@ -1791,33 +1791,41 @@ struct RouteService::Impl {
     return true;
   }
 
+  // the request body -> j->root / j->req, once (a job back from waiting for its routing context,
+  // or handed over from another GPU's service, is parsed already)
+  static void parse_job(RouteJob* j) {
+    if (j->parsed) return;
+    j->parsed = true;
+    bool parsed = false;
+    if (j->json_ok && !j->body.empty()) {
+      try {
+        j->root = rtj::Parser(j->body.data(), j->body.size()).parse();
+        parsed = true;
+      } catch (const std::exception&) {
+      }
+    }
+    if (j->request_route && (!j->json_ok || (!parsed && !j->body.empty()))) {
+      j->fallback = true;
+      return;
+    }
+    static const rtj::Value empty = [] { rtj::Value v; v.kind = rtj::Value::Obj; return v; }();
+    const rtj::Value* rootp = parsed ? &j->root : (j->request_route ? nullptr : &empty);
+    if (!j->request_route && parsed && j->root.kind != rtj::Value::Obj) rootp = &empty;
+    j->req = rtr::parse_route_request(rootp);
+    if (j->req.fallback) j->fallback = true;
+  }
+
   // GPU stage: parse, trips (K5 + K6), snapping + the batched A* (graph provider)
   void gpu_stage(Batch& b) {
     std::vector<RouteJob*>& jobs = b.jobs;
     long long fresh_jobs = 0;
     for (RouteJob* j : jobs) fresh_jobs += !j->parsed;
-    n_jobs.fetch_add(fresh_jobs, std::memory_order_relaxed);
+    n_jobs.fetch_add(fresh_jobs, std::memory_order_relaxed);   // (submitted unparsed: none normally)
     double t0 = now_us();
+    // (jobs are parsed on the submitting reactor thread, RouteService::submit; this catches any
+    // that were not)
     rtc::parallel_chunks(jobs.size(), 32, 16, [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) {
-        RouteJob* j = jobs[i];
-        if (j->parsed) continue;                 // back from waiting for its routing context
-        j->parsed = true;
-        bool parsed = false;
-        if (j->json_ok && !j->body.empty()) {
-          try {
-            j->root = rtj::Parser(j->body.data(), j->body.size()).parse();
-            parsed = true;
-          } catch (const std::exception&) {
-          }
-        }
-        if (j->request_route && (!j->json_ok || (!parsed && !j->body.empty()))) { j->fallback = true; continue; }
-        static const rtj::Value empty = [] { rtj::Value v; v.kind = rtj::Value::Obj; return v; }();
-        const rtj::Value* rootp = parsed ? &j->root : (j->request_route ? nullptr : &empty);
-        if (!j->request_route && parsed && j->root.kind != rtj::Value::Obj) rootp = &empty;
-        j->req = rtr::parse_route_request(rootp);
-        if (j->req.fallback) j->fallback = true;
-      }
+      for (size_t i = lo; i < hi; ++i) parse_job(jobs[i]);
     });
     // "alternatives" need the road graph through the CCH and a published scorer; else the app
     bool any_alt = false;
@@ -2027,6 +2035,10 @@ RouteService::~RouteService() {
 }
 
 void RouteService::submit(RouteJob* j) {
+  if (!j->parsed) {             // on the submitting reactor's thread: off the flush's critical path
+    p_->n_jobs.fetch_add(1, std::memory_order_relaxed);
+    Impl::parse_job(j);
+  }
   {
     std::lock_guard<std::mutex> lk(p_->mu);
     p_->q.push_back(j);
