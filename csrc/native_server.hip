@@ -302,6 +302,16 @@ class Reactor {
     uint64_t one = 1;
     (void)!write(wake_, &one, 8);
   }
+  // many at once: one lock and one wake-up
+  void jobs_done(const std::vector<RouteJob*>& js) {
+    if (js.empty()) return;
+    {
+      std::lock_guard<std::mutex> lk(done_mu_);
+      done_.insert(done_.end(), js.begin(), js.end());
+    }
+    uint64_t one = 1;
+    (void)!write(wake_, &one, 8);
+  }
 
   void run() {
     if (hipSetDevice(cfg_.device) != hipSuccess) return;
@@ -1454,6 +1464,17 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
     s->routes.push_back(std::make_unique<RouteService>(rc, [](RouteJob* j) {
       static_cast<JobTag*>(j->tag)->reactor->job_done(j);
     }));
+    s->routes.back()->set_done_batch([](std::vector<RouteJob*>& js) {
+      // grouped by the reactor that parsed each job (a flush's jobs come from all of them)
+      std::vector<std::pair<Reactor*, std::vector<RouteJob*>>> by;
+      for (RouteJob* j : js) {
+        Reactor* r = static_cast<JobTag*>(j->tag)->reactor;
+        auto it = std::find_if(by.begin(), by.end(), [r](const auto& p) { return p.first == r; });
+        if (it == by.end()) by.push_back({r, {j}});
+        else it->second.push_back(j);
+      }
+      for (auto& [r, v] : by) r->jobs_done(v);
+    });
   }
   if (!s->routes.empty())
     for (int i = 0; i < s->cfg.threads; ++i) s->reactors[i]->set_routes(s->routes[(size_t)i % devices.size()].get());

@@ -143,6 +143,9 @@ class RouteService {
   RouteService(const RouteServiceCfg& cfg, std::function<void(RouteJob*)> done);
   ~RouteService();
   void submit(RouteJob* j);
+  // finished jobs handed back many at a time (one wake-up per receiver instead of one per job);
+  // set before the first submit.  Unset: `done` per job.
+  void set_done_batch(std::function<void(std::vector<RouteJob*>&)> done_many);
   // jobs, flushes, fallbacks, legs searched, legs finished on the host, rows persisted
   std::vector<long long> stats() const;
   bool broken() const;                    // a flush missed the deadline and its GPU work has not drained

@@ -280,6 +280,15 @@ inline double now_us() {
 struct RouteService::Impl {
   RouteServiceCfg cfg;
   std::function<void(RouteJob*)> done;
+  std::function<void(std::vector<RouteJob*>&)> done_many;
+  void done_all(std::vector<RouteJob*>& js) {
+    if (js.empty()) return;
+    if (done_many) {
+      done_many(js);
+    } else {
+      for (RouteJob* j : js) done(j);
+    }
+  }
   std::mutex mu;
   std::condition_variable cv;
   std::deque<RouteJob*> q;
@@ -786,11 +795,16 @@ struct RouteService::Impl {
       n_flushes.fetch_add(1, std::memory_order_relaxed);
       // jobs that persist nothing answer now; the others after their group commit
       std::vector<RouteJob*> save = std::move(b->save);
-      for (RouteJob* j : b->jobs)
-        if (std::find(save.begin(), save.end(), j) == save.end()) {
-          finish(j);
-          done(j);
-        }
+      std::vector<RouteJob*> now_done;
+      {
+        const std::unordered_set<RouteJob*> saving(save.begin(), save.end());
+        for (RouteJob* j : b->jobs)
+          if (!saving.count(j)) {
+            finish(j);
+            now_done.push_back(j);
+          }
+      }
+      done_all(now_done);
       delete b;
       if (!save.empty()) {
         std::unique_lock<std::mutex> lk(pmu);
@@ -1957,11 +1971,13 @@ struct RouteService::Impl {
       const double t0 = now_us();
       persist_group(groups);
       add_t(7, t0);
+      std::vector<RouteJob*> fin;
       for (auto& g : groups)
         for (RouteJob* j : g) {
           finish(j);
-          done(j);
+          fin.push_back(j);
         }
+      done_all(fin);
     }
     if (th_ckpt.joinable()) {
       {
@@ -2032,6 +2048,10 @@ RouteService::~RouteService() {
   p_->cv.notify_all();
   if (p_->th.joinable()) p_->th.join();
   delete p_;
+}
+
+void RouteService::set_done_batch(std::function<void(std::vector<RouteJob*>&)> done_many) {
+  p_->done_many = std::move(done_many);
 }
 
 void RouteService::submit(RouteJob* j) {
