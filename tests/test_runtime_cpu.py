@@ -220,3 +220,39 @@ def test_wire8_native_packer_matches_python():
             bad["wallclock_s"][3] += 3000 * 3600
         assert rt.pack_wire8(bad.view(np.uint8).reshape(-1, 16)) is None
         assert records_to_wire8(bad) is None
+
+
+def test_parallel_chunks_pool_concurrent_callers():
+    """csrc/runtime/rt_core.h parallel_chunks runs on a process-wide worker pool: several Python
+    threads packing and formatting large batches at once (GIL released, chunks taken from a shared
+    counter by the pool and the callers) get exactly what one caller alone gets."""
+    import threading
+    rng = np.random.default_rng(5)
+    n = 20000
+    items = [{"summary": {"distance": float(rng.integers(100, 50000))}, "driver_age": int(rng.integers(18, 70)),
+              "pickup_time": f"2025-0{1 + i % 9}-1{i % 10}T0{i % 10}:{10 + i % 50}:00",
+              "weather": ["Sunny", "Cloudy", "Stormy", "Windy"][i % 4], "traffic": ["Low", "Jam"][i % 2]}
+             for i in range(n)]
+    body = json.dumps(items).encode()
+    now_secs = 1760000000
+    ref = rt.pack_predict_batch(body, now_secs, 0)
+    minutes = rng.random(n).astype(np.float32) * 90
+    ref_out = rt.format_predict_batch(minutes, ref[1], ref[2], ref[3], ref[4], True)
+    results, errors = [], []
+
+    def worker():
+        try:
+            for _ in range(3):
+                got = rt.pack_predict_batch(body, now_secs, 0)
+                out = rt.format_predict_batch(minutes, got[1], got[2], got[3], got[4], True)
+                results.append(np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+                               and list(got[4]) == list(ref[4]) and out == ref_out)
+        except Exception as e:  # pragma: no cover
+            errors.append(repr(e))
+    ths = [threading.Thread(target=worker) for _ in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors
+    assert len(results) == 24 and all(results)
