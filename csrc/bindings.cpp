@@ -1320,6 +1320,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi"), py::arg("W"), py::arg("X"), py::arg("N"), py::arg("M"), py::arg("K"),
         py::arg("b2") = py::none(), py::arg("w3") = py::none(), py::arg("ypart") = py::none(),
         py::arg("out") = py::none());
+  m.def("gemm_pipe", [](int64_t set) { return (int64_t)rt::gemm_pipe_mode((int)set); },
+        "wide GEMM K loop: 1 phase pipeline, 0 one drain per K-tile; set < 0 only reads", py::arg("set") = -1);
   m.def("big_yreduce", &big_yreduce, "y = sum of partials + b3 (+ dy, dy operand, squared error)",
         py::arg("ypart"), py::arg("nparts"), py::arg("b3"), py::arg("y") = py::none(),
         py::arg("target") = py::none(), py::arg("gscale") = 0.0, py::arg("dy") = py::none(),

@@ -23,6 +23,7 @@
 //   w1p [H/32][64 lanes][8] bf16 (as mlp3_tile.h), w2k [H][H] bf16 row-major with K columns in
 //   hperm order (w2k[n][c] = W2[n][hperm(c)]), w2t [H][H] bf16 row-major = W2^T with K (output
 //   unit) columns in hperm order (training only), b2 / w3 f32 in natural order.
+#include <atomic>
 #include <cstdlib>
 
 #include "common.h"
@@ -261,6 +262,65 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int G2T = 256, G2K = 64;
 constexpr int G2_STAGE = 2 * G2T * G2K * 2;          // A + B tile bytes per stage (64 KB)
 
+// epilogue of both 256 x 256 K loops: acc[i][j] element e = Z^T[unit n0 + 128wu + 16i + 4g + e][row
+// m0 + 64wr + 16j + fr] (g = lane >> 4); hperm swaps unit bits 2, 3: stored position 16i + 4 swap2(g) + e
+template <int EPI>
+__device__ __forceinline__ void g256_epilogue(const GemmArgs& a, f32x4 (&acc)[8][4], int n0, int m0, int wu,
+                                              int wr, int lane) {
+  const int fr = lane & 15, g = lane >> 4, gp = ((g & 1) << 1) | (g >> 1);
+  const int ub = n0 + 128 * wu;
+  if constexpr (EPI == EPI_STORE) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + 64 * wr + 16 * j + fr;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (__bf16)acc[i][j][e];
+        *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + ub + 16 * i + 4 * gp) = o;
+      }
+    }
+  } else {
+    f32x4 bv[8], wv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bv[i] = *reinterpret_cast<const f32x4*>(a.b2 + ub + 16 * i + 4 * g);
+      wv[i] = *reinterpret_cast<const f32x4*>(a.w3 + ub + 16 * i + 4 * g);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + 64 * wr + 16 * j + fr;
+      float ys[2] = {0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = relu_f(acc[i][j][e] + bv[i][e]);
+          ys[i >> 2] = __builtin_fmaf(v, wv[i][e], ys[i >> 2]);
+          o[e] = (__bf16)v;
+        }
+        if constexpr (EPI == EPI_H2Y) {
+          if (m < a.M) *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + ub + 16 * i + 4 * gp) = o;
+        }
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        ys[hh] += __shfl_xor(ys[hh], 16);
+        ys[hh] += __shfl_xor(ys[hh], 32);
+      }
+      if (g == 0 && m < a.M) {
+        float* yp = a.ypart + (size_t)m * (a.N / 64) + (ub >> 6);
+        yp[0] = ys[0];
+        yp[1] = ys[1];
+      }
+    }
+  }
+}
+
+
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm2[];
@@ -329,60 +389,159 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs a) {
     __syncthreads();                                    // ... and stage k fully read
   }
 
-  // epilogue: acc[i][j] element e = Z^T[unit n0 + 128wu + 16i + 4g + e][row m0 + 64wr + 16j + fr]
-  // (g = lane >> 4); hperm swaps unit bits 2, 3: stored position 16i + 4 swap2(g) + e
-  const int g = lane >> 4, gp = ((g & 1) << 1) | (g >> 1);
-  const int ub = n0 + 128 * wu;
-  if constexpr (EPI == EPI_STORE) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + 64 * wr + 16 * j + fr;
-      if (m >= a.M) continue;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        bf16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (__bf16)acc[i][j][e];
-        *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + ub + 16 * i + 4 * gp) = o;
-      }
-    }
-  } else {
-    f32x4 bv[8], wv[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      bv[i] = *reinterpret_cast<const f32x4*>(a.b2 + ub + 16 * i + 4 * g);
-      wv[i] = *reinterpret_cast<const f32x4*>(a.w3 + ub + 16 * i + 4 * g);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + 64 * wr + 16 * j + fr;
-      float ys[2] = {0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        bf16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float v = relu_f(acc[i][j][e] + bv[i][e]);
-          ys[i >> 2] = __builtin_fmaf(v, wv[i][e], ys[i >> 2]);
-          o[e] = (__bf16)v;
-        }
-        if constexpr (EPI == EPI_H2Y) {
-          if (m < a.M) *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + ub + 16 * i + 4 * gp) = o;
-        }
-      }
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        ys[hh] += __shfl_xor(ys[hh], 16);
-        ys[hh] += __shfl_xor(ys[hh], 32);
-      }
-      if (g == 0 && m < a.M) {
-        float* yp = a.ypart + (size_t)m * (a.N / 64) + (ub >> 6);
-        yp[0] = ys[0];
-        yp[1] = ys[1];
-      }
-    }
-  }
+  g256_epilogue<EPI>(a, acc, n0, m0, wu, wr, lane);
 }
+
+// ---------------------------------------------------------------------------------------------
+// gemm256p_kernel: gemm256_kernel's tile, waves, MFMA and epilogue with the K loop as a PHASE
+// pipeline (cdna_hip_programming.md §5, "The 256² 8-phase template").  gemm256_kernel drains its
+// loads and barriers once per 64-deep K-tile with both waves of a SIMD parked at once (PMC r4as: a
+// third of the wave cycles wait there).  Here:
+//   * each K-tile runs as 4 phases, one per quadrant of the wave's 128 x 64 output (64 units x 32
+//     rows, 16 MFMAs): P1 reads the B0 and A0 fragments, P2 B1, P3 A1, P4 none (B0 is still in
+//     registers) — 24 ds_read_b128 per K-tile, as before;
+//   * each LDS buffer is four 16 KB regions (A units half ih = rows 128wu + 64ih + 0..63 of both
+//     unit halves, B rows half jh = rows 64wr + 32jh + 0..31 of all four row quarters), so phase
+//     (ih, jh) reads exactly regions A_ih and B_jh; ONE region's global_load_lds (2 per thread) is
+//     issued per phase: P1 B1(u+1), P2 A1(u+1), P3 A0(u+2), P4 B0(u+2) — each region restaged >= 2
+//     phases after its last read, and K-tile u+1 retired by P4's counted vmcnt(4) (the youngest
+//     two regions stay in flight across the raw barriers; never vmcnt(0) in the steady state);
+//   * the two waves of a SIMD (w, w + 4) are in different groups and group 1 runs ONE barrier behind
+//     group 0, so one group's MFMAs run while the other group reads its fragments and issues its
+//     loads (s_setprio 1 around the MFMAs).
+// Hazard bookkeeping (barrier indices, group 0 phase p: mid 2p, end 2p+1; group 1: 2p+1, 2p+2): a
+// region last read in phase r is retired by both groups at barrier 2r+2, which group 0's phase r+2
+// loads follow; a K-tile's data is retired by both groups' P4 waits before barrier 2p+1, which every
+// read of the next K-tile follows.
+constexpr int GP_REGION = 128 * 128;                 // bytes: 128 rows x 64 k bf16
+constexpr int GP_BUF = 4 * GP_REGION;                 // A0 | A1 | B0 | B1
+
+#define GP_BARRIER()                      \
+  do {                                    \
+    __builtin_amdgcn_sched_barrier(0);    \
+    __builtin_amdgcn_s_barrier();         \
+    __builtin_amdgcn_sched_barrier(0);    \
+  } while (0)
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256p_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm2[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int bid = blockIdx.x;
+  {
+    const int nb = gridDim.x, xcd = bid & 7, q = nb >> 3, r = nb & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int tn = bid % a.tiles_n, tm = bid / a.tiles_n;
+  const int n0 = tn * G2T, m0 = tm * G2T;
+  const int wu = w >> 2, wr = w & 3;                 // group = wu; units [128wu, +128) x rows [64wr, +64)
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // staging: wave w's instruction q of a region writes LDS rows 64q + 8w + (lane >> 3), 16-byte slot
+  // lane & 7, from global chunk slot ^ ((row >> 1) & 7) (the read side's swizzle)
+  const int srow = 8 * w + (lane >> 3);
+  const int sch = (lane & 7) ^ ((srow >> 1) & 7);
+  const __bf16* gA = a.W + (size_t)(n0 + srow) * a.ldw + 8 * sch;     // + (128q + 64ih) rows
+  const __bf16* gB[2][2];
+#pragma unroll
+  for (int jh = 0; jh < 2; ++jh)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int row = m0 + 128 * q + 64 * (w >> 2) + 32 * jh + 8 * (w & 3) + (lane >> 3);
+      gB[jh][q] = a.X + (size_t)min(row, a.M - 1) * a.ldx + 8 * sch;
+    }
+  typedef __attribute__((address_space(3))) void lds_void;
+  // region reg (0 A0, 1 A1, 2 B0, 3 B1) of K-tile kt
+  auto issue = [&](int kt, int reg) {
+    unsigned char* dst = sm2 + (kt & 1) * GP_BUF + reg * GP_REGION + w * 1024;
+    const int k0 = kt * G2K;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const __bf16* src = reg < 2 ? gA + (size_t)(128 * q + 64 * reg) * a.ldw + k0 : gB[reg - 2][q] + k0;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + q * 8192), 16, 0, 0);
+    }
+  };
+
+  const int fr = lane & 15, sw = (lane >> 1) & 7;
+  const int co[2] = {((lane >> 4) ^ sw) << 4, ((4 + (lane >> 4)) ^ sw) << 4};
+  const int offA = (64 * wu + fr) * 128, offB = 2 * GP_REGION + (32 * wr + fr) * 128;
+  bf16x8 fa[4][2], fb[2][2][2];                      // A half [i'][ks]; B halves [jh][j'][ks]
+  auto readA = [&](const unsigned char* buf, int ih) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        fa[i][ks] = *reinterpret_cast<const bf16x8*>(buf + ih * GP_REGION + offA + i * 2048 + co[ks]);
+  };
+  auto readB = [&](const unsigned char* buf, int jh) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        fb[jh][j][ks] = *reinterpret_cast<const bf16x8*>(buf + jh * GP_REGION + offB + j * 2048 + co[ks]);
+  };
+  auto quad = [&](int ih, int jh) {
+    GP_BARRIER();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * ih + i][2 * jh + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][ks], fb[jh][j][ks], acc[4 * ih + i][2 * jh + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    GP_BARRIER();
+  };
+
+  const int nk = a.K / G2K;
+  issue(0, 0);
+  issue(0, 1);
+  issue(0, 2);
+  issue(0, 3);
+  if (nk > 1) {
+    issue(1, 0);
+    issue(1, 2);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  GP_BARRIER();
+  if (wu == 1) GP_BARRIER();                          // group 1: one barrier behind
+  for (int u = 0; u < nk; ++u) {
+    const unsigned char* buf = sm2 + (u & 1) * GP_BUF;
+    // P1: B0 + A0; restage B1 of u + 1
+    readB(buf, 0);
+    readA(buf, 0);
+    if (u + 1 < nk) issue(u + 1, 3);
+    quad(0, 0);
+    // P2: B1; restage A1 of u + 1
+    readB(buf, 1);
+    if (u + 1 < nk) issue(u + 1, 1);
+    quad(0, 1);
+    // P3: A1; restage A0 of u + 2
+    readA(buf, 1);
+    if (u + 2 < nk) issue(u + 2, 0);
+    quad(1, 1);
+    // P4: no reads; restage B0 of u + 2, then retire K-tile u + 1
+    if (u + 2 < nk) {
+      issue(u + 2, 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    quad(1, 0);
+  }
+  if (wu == 0) GP_BARRIER();                          // equal barrier counts on exit
+  g256_epilogue<EPI>(a, acc, n0, m0, wu, wr, lane);
+}
+#undef GP_BARRIER
 
 // ---------------------------------------------------------------------------------------------
 // mlp_big_fused_kernel (inference): records -> featurize -> layer 1 -> layer 2 -> relu.w3 partials
@@ -939,19 +1098,39 @@ static int gemm_tile() {
   return t;
 }
 
+// K loop of the 256 x 256 tile: 1 = phase pipeline (gemm256p_kernel), 0 = one drain per K-tile
+// (gemm256_kernel); ROUTEST_GEMM_PIPE at start-up, gemm_pipe_mode(set) at run time (A/B tests)
+static std::atomic<int> g_gemm_pipe{-1};
+int gemm_pipe_mode(int set) {
+  if (set >= 0) g_gemm_pipe.store(set ? 1 : 0);
+  int v = g_gemm_pipe.load();
+  if (v < 0) {
+    const char* e = std::getenv("ROUTEST_GEMM_PIPE");
+    v = (e == nullptr || std::atoi(e) != 0) ? 1 : 0;
+    int expect = -1;
+    if (!g_gemm_pipe.compare_exchange_strong(expect, v)) v = expect;
+  }
+  return v;
+}
+static bool gemm_pipe() { return gemm_pipe_mode(-1) == 1; }
+
 template <int EPI>
 static hipError_t launch_g256(const GemmArgs& a, dim3 grid, dim3 block, hipStream_t stream) {
   static bool attr[64] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
   const int lds = 2 * G2_STAGE;
+  static_assert(2 * G2_STAGE == 2 * GP_BUF, "both K loops use the same 128 KB of LDS");
   if (!attr[dev & 63]) {
-    const hipError_t e = hipFuncSetAttribute((const void*)gemm256_kernel<EPI>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipError_t e = hipFuncSetAttribute((const void*)gemm256_kernel<EPI>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)gemm256p_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr[dev & 63] = true;
   }
-  hipLaunchKernelGGL(gemm256_kernel<EPI>, grid, block, lds, stream, a);
+  if (gemm_pipe()) hipLaunchKernelGGL(gemm256p_kernel<EPI>, grid, block, lds, stream, a);
+  else hipLaunchKernelGGL(gemm256_kernel<EPI>, grid, block, lds, stream, a);
   return hipGetLastError();
 }
 

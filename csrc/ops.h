@@ -53,6 +53,8 @@ hipError_t launch_big_layer1(const void* rec, int rec_bytes, int B, const void* 
 hipError_t launch_gemm_nt(int epi, const void* W, int ldw, const void* X, int ldx, int N, int M,
                           int K, const float* b2, const float* w3, float* ypart, void* out,
                           int ldo, hipStream_t stream);
+// K loop of the 256 x 256 wide GEMM: 1 phase pipeline (default), 0 one drain per K-tile; < 0 only reads
+int gemm_pipe_mode(int set = -1);
 hipError_t launch_big_fused(const void* rec, int rec_bytes, int B, const void* w1q, const void* w2f,
                             int H, const NormParams& np, const float* b2, const float* w3,
                             float* ypart, hipStream_t stream);

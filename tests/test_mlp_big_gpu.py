@@ -106,6 +106,47 @@ def test_gemm_nt_store_epilogue(M):
     assert (out[:, N:] == 0).all()
 
 
+@pytest.mark.parametrize("N,K,M", [(256, 64, 300), (256, 128, 256), (512, 192, 1000), (1024, 1024, 4097),
+                                   (1024, 1024, 65536)])
+def test_gemm_phase_pipeline_bitwise_equals_drain_loop(N, K, M):
+    """gemm256p_kernel (phase pipeline, staggered wave groups, loads in flight across raw barriers)
+    against gemm256_kernel (one drain per K-tile): the same MFMAs in the same per-accumulator order,
+    so all three epilogues must agree bit for bit — including 1-, 2- and 3-K-tile loops (the
+    prologue / tail waits) and a partial last row tile; and against torch."""
+    from routest_amd.ops import _ext
+    C = _ext.native()
+    g = torch.Generator().manual_seed(N + K + M)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    X = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    b2 = (0.1 * torch.randn(N, generator=g)).to(DEV)
+    w3 = (torch.randn(N, generator=g) / N ** 0.5).to(DEV)
+    prev = C.gemm_pipe(-1)
+    res = {}
+    try:
+        for pipe in (0, 1):
+            C.gemm_pipe(pipe)
+            o2 = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+            C.gemm_nt(2, W, X, N, M, K, out=o2)
+            o1 = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+            y1 = torch.full((M, N // 64), float("nan"), device=DEV)
+            C.gemm_nt(1, W, X, N, M, K, b2=b2, w3=w3, ypart=y1, out=o1)
+            y0 = torch.full((M, N // 64), float("nan"), device=DEV)
+            C.gemm_nt(0, W, X, N, M, K, b2=b2, w3=w3, ypart=y0)
+            torch.cuda.synchronize()
+            res[pipe] = (o2.cpu(), o1.cpu(), y1.cpu(), y0.cpu())
+    finally:
+        C.gemm_pipe(prev)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
+    z = (X.float() @ W.float().T).cpu()
+    got = torch.empty(M, N)
+    got[:, hperm(N)] = res[1][0].float()
+    torch.testing.assert_close(got, z, rtol=1e-2, atol=0.05)
+    y = (torch.relu(z + b2.cpu()) * w3.cpu()).view(M, N // 64, 64).sum(-1)
+    torch.testing.assert_close(res[1][3], y, rtol=1e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("H", [512, 1024])
 @pytest.mark.parametrize("rb", [16, 6])
 def test_big_fused_equals_three_launch_path(H, rb):
