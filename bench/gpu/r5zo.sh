@@ -12,4 +12,7 @@ for p in 0 1; do
     ROUTEST_GEMM_PIPE=$p timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $G -d $O/p${p}_$i -o g --output-format csv -- python3 $ROOT/bench/gemm_probe.py --iters 10 > $O/p${p}_$i.log 2>&1 || { echo "pass p$p g$i failed rc=$?"; tail -5 $O/p${p}_$i.log; exit 1; }
   done
 done
-echo done
+echo pmc done
+cd $ROOT
+timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O/t1k -o train --output-format csv -- python3 bench/train_bench.py --hidden 1024 --batch 65536 --steps 30 --warmup 5 --modes fused > $O/t1k.log 2>&1 || { echo "train stats failed rc=$?"; exit 1; }
+echo stats done
