@@ -121,6 +121,7 @@ struct GemmArgs {
   __bf16* out;       // EPI_H2Y: h2a, EPI_STORE: output; [M][ldo], unit n at hperm position
   int ldo;
   int tiles_n;       // N / 128
+  int st16;          // 256 x 256 epilogue: 16-byte row pieces (1) or 8-byte (0; ROUTEST_GEMM_ST16 A/B knob)
 };
 
 template <int EPI>
@@ -264,22 +265,45 @@ constexpr int G2_STAGE = 2 * G2T * G2K * 2;          // A + B tile bytes per sta
 
 // epilogue of both 256 x 256 K loops: acc[i][j] element e = Z^T[unit n0 + 128wu + 16i + 4g + e][row
 // m0 + 64wr + 16j + fr] (g = lane >> 4); hperm swaps unit bits 2, 3: stored position 16i + 4 swap2(g) + e
+// One row's pieces of fragments 2p and 2p + 1 as 16-byte stores (the 8-byte stores made the epilogue
+// store-issue bound): lane l (g < 2, stored position 4gp) and lane l ^ 32 (position 4gp + 4) hold
+// adjacent 8-byte pieces of both fragments; each swaps one piece with its partner, so the low lane
+// stores fragment 2p's 16 bytes and the high lane fragment 2p + 1's.  Both lanes of a pair have the
+// same row, so they are active together.
+__device__ __forceinline__ void g256_store_pair(__bf16* row, int p, int gp, bool hi, bf16x4 o0, bf16x4 o1) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x2 send = __builtin_bit_cast(u32x2, hi ? o0 : o1);
+  const u32x2 keep = __builtin_bit_cast(u32x2, hi ? o1 : o0);
+  u32x2 recv;
+  recv[0] = (unsigned)__shfl_xor((int)send[0], 32);
+  recv[1] = (unsigned)__shfl_xor((int)send[1], 32);
+  const u32x4 v = hi ? (u32x4){recv[0], recv[1], keep[0], keep[1]} : (u32x4){keep[0], keep[1], recv[0], recv[1]};
+  *reinterpret_cast<u32x4*>(row + 16 * (2 * p + (hi ? 1 : 0)) + 4 * (hi ? gp - 1 : gp)) = v;
+}
+
 template <int EPI>
 __device__ __forceinline__ void g256_epilogue(const GemmArgs& a, f32x4 (&acc)[8][4], int n0, int m0, int wu,
                                               int wr, int lane) {
   const int fr = lane & 15, g = lane >> 4, gp = ((g & 1) << 1) | (g >> 1);
+  const bool hi = lane >= 32;
   const int ub = n0 + 128 * wu;
   if constexpr (EPI == EPI_STORE) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + 64 * wr + 16 * j + fr;
       if (m >= a.M) continue;
+      bf16x4 o[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        bf16x4 o;
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (__bf16)acc[i][j][e];
-        *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + ub + 16 * i + 4 * gp) = o;
+        for (int e = 0; e < 4; ++e) o[i][e] = (__bf16)acc[i][j][e];
+      if (a.st16) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) g256_store_pair(a.out + (size_t)m * a.ldo + ub, p, gp, hi, o[2 * p], o[2 * p + 1]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + ub + 16 * i + 4 * gp) = o[i];
       }
     }
   } else {
@@ -293,17 +317,25 @@ __device__ __forceinline__ void g256_epilogue(const GemmArgs& a, f32x4 (&acc)[8]
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + 64 * wr + 16 * j + fr;
       float ys[2] = {0.f, 0.f};
+      bf16x4 o[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        bf16x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float v = relu_f(acc[i][j][e] + bv[i][e]);
           ys[i >> 2] = __builtin_fmaf(v, wv[i][e], ys[i >> 2]);
-          o[e] = (__bf16)v;
+          o[i][e] = (__bf16)v;
         }
-        if constexpr (EPI == EPI_H2Y) {
-          if (m < a.M) *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + ub + 16 * i + 4 * gp) = o;
+      }
+      if constexpr (EPI == EPI_H2Y) {
+        if (m < a.M) {
+          if (a.st16) {
+#pragma unroll
+            for (int p = 0; p < 4; ++p) g256_store_pair(a.out + (size_t)m * a.ldo + ub, p, gp, hi, o[2 * p], o[2 * p + 1]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + ub + 16 * i + 4 * gp) = o[i];
+          }
         }
       }
 #pragma unroll
@@ -1139,8 +1171,13 @@ hipError_t launch_gemm_nt(int epi,const void* W, int ldw, const void* X, int ldx
                           int ldo, hipStream_t stream) {
   if (M <= 0) return hipSuccess;
   if (N % GT || K % GK || ldw % 8 || ldx % 8 || (out != nullptr && ldo % 8)) return hipErrorInvalidValue;
-  if (N % G2T == 0 && K % G2K == 0 && gemm_tile() == 256) {
-    GemmArgs a{(const __bf16*)W, (const __bf16*)X, ldw, ldx, N, M, K, b2, w3, ypart, (__bf16*)out, ldo, N / G2T};
+  // the 256 x 256 epilogue stores 16-byte pieces of a row (out 16-byte aligned, ldo % 8 == 0)
+  if (N % G2T == 0 && K % G2K == 0 && gemm_tile() == 256 && ((uintptr_t)out & 15) == 0) {
+    static const int st16 = [] {
+      const char* v = std::getenv("ROUTEST_GEMM_ST16");
+      return (v != nullptr && std::atoi(v) == 0) ? 0 : 1;
+    }();
+    GemmArgs a{(const __bf16*)W, (const __bf16*)X, ldw, ldx, N, M, K, b2, w3, ypart, (__bf16*)out, ldo, N / G2T, st16};
     const dim3 grid((unsigned)((N / G2T) * ((M + G2T - 1) / G2T))), block(512);
     switch (epi) {
       case EPI_Y: return launch_g256<EPI_Y>(a, grid, block, stream);
@@ -1149,7 +1186,7 @@ hipError_t launch_gemm_nt(int epi,const void* W, int ldw, const void* X, int ldx
       default: return hipErrorInvalidValue;
     }
   }
-  GemmArgs a{(const __bf16*)W, (const __bf16*)X, ldw, ldx, N, M, K, b2, w3, ypart, (__bf16*)out, ldo, N / GT};
+  GemmArgs a{(const __bf16*)W, (const __bf16*)X, ldw, ldx, N, M, K, b2, w3, ypart, (__bf16*)out, ldo, N / GT, 0};
   const dim3 grid((unsigned)((N / GT) * ((M + GT - 1) / GT))), block(256);
   switch (epi) {
     case EPI_Y: hipLaunchKernelGGL(gemm_nt_kernel<EPI_Y>, grid, block, 0, stream, a); break;
