@@ -96,14 +96,24 @@ def main() -> None:
     from routest_amd.parallel.dp import allreduce_scalars
     from routest_amd.utils import bench_schema
 
+    import datetime
+    from routest_amd.utils.bench_guard import SectionAborted, SectionGuard, env_timeout_s, raise_if_injected
+
     rank = int(os.environ.get("RANK", "0"))
     local_rank = 0 if share else int(os.environ.get("LOCAL_RANK", "0"))
+    # a collective that never completes (a peer died, an RCCL hang) ends in an error after this
+    # long instead of running into the driver's limit with no JSON line printed
+    pg_timeout = datetime.timedelta(seconds=env_timeout_s("ROUTEST_BENCH_PG_TIMEOUT_S", 180.0))
     if world > 1:
         torch.cuda.set_device(local_rank)
         if share:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), timeout=pg_timeout)
+    # every extra section runs under the guard (routest_amd/utils/bench_guard.py): a failure on one
+    # rank becomes an {"error": ...} key on every rank, agreed on over a gloo side group before any
+    # rank enters a collective the failed one would never reach
+    guard = SectionGuard(world, rank, timeout_s=env_timeout_s("ROUTEST_BENCH_HOLD_TIMEOUT_S", 900.0))
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     from routest_amd.parallel.affinity import bind_to_gpu_numa
@@ -291,21 +301,19 @@ def main() -> None:
     rec16_value = None
     if a.rec != 16 and a.rec16_steps > 0:
         del pipe
-        pipe16 = Pipeline(wire(16))
-        el16 = pipe16.timed(min(a.warmup, 3), a.rec16_steps)
-        rec16_value = B * a.rec16_steps * world / el16
-        del pipe16
+
+        def rec16_section():
+            pipe16 = Pipeline(wire(16))
+            guard.checkpoint()                      # (timed() barriers on the main group)
+            el16 = pipe16.timed(min(a.warmup, 3), a.rec16_steps)
+            del pipe16
+            return B * a.rec16_steps * world / el16
+        rec16_value = guard.run("rec16", rec16_section)
+        if isinstance(rec16_value, dict):           # {"error": ...}: reported, not a rate
+            rec16_value = None
 
     # config 3 on the same ranks: the fused DP training step (forward + MSE gradient + dgrad in
     # one kernel, split-K weight gradients, one flat-bucket all-reduce, fused AdamW + re-pack)
-    def agree(ok_local: bool) -> bool:
-        """True only if every rank says so (one collective every rank reaches)."""
-        if world == 1:
-            return ok_local
-        t = torch.tensor([0.0 if ok_local else 1.0], device="cpu" if share else dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item()) == 0.0
-
     def train_probe(comm=None, tB: int = 65536):
         from routest_amd.train.fused import FusedMlp3Trainer
         torch.manual_seed(4321)                 # identical initial parameters on every rank
@@ -316,10 +324,12 @@ def main() -> None:
         tr = FusedMlp3Trainer(tmodel, dev, tB, tB * world, lr=1e-3, allreduce=world > 1, comm=comm)
         yn = tr.normalize_targets(torch.from_numpy(ty).to(dev))
         for _ in range(20):                     # (clocks settle: 5 warm steps read ~5 % slow at 64k)
+            guard.checkpoint()                  # (each step all-reduces the gradient bucket)
             tr.step(trt, yn)
         torch.cuda.synchronize()
-        if comm is not None and not agree(not comm.C.comm_error(comm.h)):
+        if comm is not None and not guard.agree(not comm.C.comm_error(comm.h)):
             return {"error": "one-shot all-reduce: a peer wait timed out during warmup"}
+        guard.checkpoint()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -331,6 +341,7 @@ def main() -> None:
             dist.barrier()
         torch.cuda.synchronize()
         tel = time.perf_counter() - t0
+        guard.checkpoint()
         if world > 1:
             (tel,) = allreduce_scalars([tel], dev, "max")
         loss = float(tr.sq_err.sum().item()) / tB
@@ -340,19 +351,20 @@ def main() -> None:
              else "RCCL, one flat fp32 bucket" if comm is None else
              "one-shot over IPC-mapped peer HBM (csrc/comm.hip), one flat fp32 bucket"), loss)
         if comm is not None:
-            res["comm_error"] = not agree(not comm.C.comm_error(comm.h))
+            res["comm_error"] = not guard.agree(not comm.C.comm_error(comm.h))
             # every rank must hold the same parameters after the identical reduced updates
             ph = float(tr.P.double().sum())
+            guard.checkpoint()
             (lo,) = allreduce_scalars([ph], dev, "min")
             (hi,) = allreduce_scalars([ph], dev, "max")
             res["params_identical_across_ranks"] = bool(lo == hi)
         del tr, trt
         return res
 
-    train_res = train_probe() if a.train_steps > 0 else None
+    train_res = guard.run("train", train_probe) if a.train_steps > 0 else None
     # the same step at 1M rows per GPU (16 MB of records — HBM is never the limit): the fixed
     # per-step costs (slab reduction, AdamW, launch gaps, the all-reduce) amortised over 16x the rows
-    train_big_res = (train_probe(tB=a.train_batch_large)
+    train_big_res = (guard.run("train_large", train_probe, tB=a.train_batch_large)
                      if a.train_steps > 0 and a.train_batch_large > 0 else None)
 
     # the same training step with the native one-shot all-reduce (one hop over all 7 xGMI links at
@@ -362,22 +374,29 @@ def main() -> None:
     devcomm = None
     if a.train_steps > 0 and world > 1 and os.environ.get("ROUTEST_BENCH_ONESHOT", "1") != "0":
         from routest_amd.parallel.comm import DeviceComm
-        err = None
-        try:
-            devcomm = DeviceComm(dev, use_rccl=False)
-            os_ok = devcomm.oneshot
-        except Exception as e:  # noqa: BLE001 - reported, never fatal for the headline
-            os_ok, err = False, repr(e)[:200]
-        # (os_ok, not ok: `ok` holds the headline output check reported as "finite" / exit 3)
-        if agree(os_ok):
-            train_os_res = train_probe(devcomm)
-            if "error" in train_os_res or train_os_res.get("comm_error"):
-                # (agreed on by every rank inside train_probe): no further one-shot use
-                torch.cuda.synchronize()
-                devcomm.close()
-                devcomm = None
-        else:
-            train_os_res = {"error": err or "one-shot set-up failed on a peer rank"}
+        holder = {}
+
+        def oneshot_section():
+            err = None
+            try:
+                guard.checkpoint()               # (the IPC set-up exchanges handles over the group)
+                holder["comm"] = DeviceComm(dev, use_rccl=False)
+                os_ok = holder["comm"].oneshot
+            except SectionAborted:
+                raise
+            except Exception as e:  # noqa: BLE001 - reported, never fatal for the headline
+                os_ok, err = False, repr(e)[:200]
+            # (os_ok, not ok: `ok` holds the headline output check reported as "finite" / exit 3)
+            if not guard.agree(os_ok):
+                holder.pop("comm", None)
+                return {"error": err or "one-shot set-up failed on a peer rank"}
+            return train_probe(holder["comm"])
+        train_os_res = guard.run("oneshot", oneshot_section)
+        devcomm = holder.get("comm")
+        if devcomm is not None and ("error" in train_os_res or train_os_res.get("comm_error")):
+            # (agreed on by every rank inside the section): no further one-shot use
+            torch.cuda.synchronize()
+            devcomm.close()
             devcomm = None
 
     # whole-node runs: what the xGMI links delivered, measured on the same ranks right after the
@@ -388,10 +407,9 @@ def main() -> None:
         # set-up and training probe succeeded on every rank: every decision here depends only on
         # state all ranks agreed on, so no rank can be left waiting on a step another one skipped
         from routest_amd.parallel.collective_probe import sweep
-        try:
-            coll = sweep(dev, native=devcomm)
-        except Exception as e:  # noqa: BLE001 - the headline line must still print
-            coll = [{"error": repr(e)[:200]}]
+        coll = guard.run("collectives", sweep, dev, native=devcomm, checkpoint=guard.checkpoint)
+        if isinstance(coll, dict):
+            coll = [coll]                       # schema: a list whose first row carries "error"
 
     # config 4 on the same ranks: the 2-layer GCN scorer, graph replicated on every GPU (no
     # collective) and row-partitioned (each rank runs 1/N of the nodes, RCCL all-gather of Z).  The
@@ -402,49 +420,57 @@ def main() -> None:
         from routest_amd.data.graph import synth_road_graph
         from routest_amd.models.gcn import GcnScorer, GcnScorerHip, routes_to_csr
         g = synth_road_graph(100_000, seed=0)
-        gm = GcnScorer(seed=0)
-        rng = np.random.default_rng(rank)
-        nroutes = 10_000 // world
-        walks = []
-        for _ in range(nroutes):
-            v = int(rng.integers(0, g.num_nodes))
-            path = [v]
-            for _ in range(int(rng.integers(50, 300))):
-                nb = g.indices[g.indptr[v]:g.indptr[v + 1]]
-                v = int(nb[rng.integers(0, len(nb))])
-                path.append(v)
-            walks.append(path)
-        ptr, nodes = routes_to_csr(walks)
-        ptr_t, nodes_t = torch.from_numpy(ptr).to(dev), torch.from_numpy(nodes).to(dev)
-        gcn_res = bench_schema.gcn_section(g.num_nodes, g.num_edges, nroutes * world)
-        modes = list(bench_schema.GCN_MODES_N if world > 1 else bench_schema.GCN_MODES_1)
-        if world > 1 and devcomm is not None:
-            modes.append(bench_schema.GCN_MODE_ONESHOT)   # Z gathered over IPC-mapped peer HBM in one hop
-        for mode in modes:
-            hip = GcnScorerHip(gm, g, dev, mode=mode.split("_")[0], rank=rank, world=world,
-                               comm=devcomm if mode.endswith("oneshot") else None)
 
-            def gstep():
-                hip.node_delays()
-                return hip.score_routes(ptr_t, nodes_t)
-            for _ in range(5):
-                gstep()
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(a.gcn_steps):
-                gstep()
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            gel = time.perf_counter() - t0
-            if world > 1:
-                (gel,) = allreduce_scalars([gel], dev, "max")
-            bench_schema.gcn_mode(gcn_res, mode, gel, a.gcn_steps, nroutes * world)
-            del hip
+        def gcn_section():
+            gm = GcnScorer(seed=0)
+            rng = np.random.default_rng(rank)
+            nroutes = 10_000 // world
+            walks = []
+            for _ in range(nroutes):
+                v = int(rng.integers(0, g.num_nodes))
+                path = [v]
+                for _ in range(int(rng.integers(50, 300))):
+                    nb = g.indices[g.indptr[v]:g.indptr[v + 1]]
+                    v = int(nb[rng.integers(0, len(nb))])
+                    path.append(v)
+                walks.append(path)
+            ptr, nodes = routes_to_csr(walks)
+            ptr_t, nodes_t = torch.from_numpy(ptr).to(dev), torch.from_numpy(nodes).to(dev)
+            res = bench_schema.gcn_section(g.num_nodes, g.num_edges, nroutes * world)
+            modes = list(bench_schema.GCN_MODES_N if world > 1 else bench_schema.GCN_MODES_1)
+            if world > 1 and devcomm is not None:
+                modes.append(bench_schema.GCN_MODE_ONESHOT)   # Z gathered over IPC-mapped peer HBM in one hop
+            for mode in modes:
+                guard.checkpoint()
+                hip = GcnScorerHip(gm, g, dev, mode=mode.split("_")[0], rank=rank, world=world,
+                                   comm=devcomm if mode.endswith("oneshot") else None)
+
+                def gstep():
+                    hip.node_delays()
+                    return hip.score_routes(ptr_t, nodes_t)
+                for _ in range(5):
+                    guard.checkpoint()          # (partition modes all-gather inside the step)
+                    gstep()
+                torch.cuda.synchronize()
+                guard.checkpoint()
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(a.gcn_steps):
+                    gstep()
+                torch.cuda.synchronize()
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                gel = time.perf_counter() - t0
+                guard.checkpoint()
+                if world > 1:
+                    (gel,) = allreduce_scalars([gel], dev, "max")
+                bench_schema.gcn_mode(res, mode, gel, a.gcn_steps, nroutes * world)
+                del hip
+            return res
+        gcn_res = guard.run("gcn", gcn_section)
 
     # config 5 on the same ranks: 10k concurrent multi-stop requests sharded over the ranks, each
     # step CCH road-metre matrices + K6 greedy for all of a rank's requests, then every trip leg as
@@ -455,168 +481,177 @@ def main() -> None:
     route_res = None
     route_cost = None
     route_router = None
+    route_model = None
     if a.route_steps > 0:
         from routest_amd.data.graph import synth_road_graph
         from routest_amd.routing.bulk import BulkRouteStep
         from routest_amd.routing.cch import RoadRouter, RouteContext
         from routest_amd.routing.graph import edge_costs
         from routest_amd.serve.eta_service import default_model
-        # set-up is per rank (no collective): a failure on any rank is agreed on before the timed
-        # steps, so the section reports an error and the headline line still prints
-        route_err = None
-        try:
-            if g is None:
-                g = synth_road_graph(100_000, seed=0)
+        held = {}
+
+        def route_section():
+            # set-up is per rank (no collective); a failure on any rank is agreed on (the
+            # checkpoint) before the timed steps' barrier
+            gr = g if g is not None else synth_road_graph(100_000, seed=0)
             torch.manual_seed(0)
-            route_model = default_model(hidden=a.hidden, steps=200)
-            cost = edge_costs(g, route_model, device=dev)
+            rmodel = default_model(hidden=a.hidden, steps=200)
+            cost = edge_costs(gr, rmodel, device=dev)
             t0 = time.perf_counter()
-            route_router = RoadRouter(g, route_model, device=dev)
+            router = RoadRouter(gr, rmodel, device=dev)
             topo_s = time.perf_counter() - t0
             # a routing context built from scratch on the GPU: ETA-model edge costs + customization
             t0 = time.perf_counter()
-            route_router.metric(RouteContext(weather=1, congestion=3, weekhour=4 * 24 + 18))
+            router.metric(RouteContext(weather=1, congestion=3, weekhour=4 * 24 + 18))
             ctx_ms = (time.perf_counter() - t0) * 1e3
-            ctx_info = dict(route_router.last_metric)
-            bulk = BulkRouteStep(g, cost, dev, a.route_requests // world, seed=100 + rank, router=route_router)
+            ctx_info = dict(router.last_metric)
+            bulk = BulkRouteStep(gr, cost, dev, a.route_requests // world, seed=100 + rank, router=router)
             bulk.step()
             torch.cuda.synchronize()
-        except Exception as e:  # noqa: BLE001 - reported, never fatal for the headline
-            route_err = repr(e)[:300]
-    if a.route_steps > 0 and not agree(route_err is None):
-        route_res = {"error": route_err or "route set-up failed on a peer rank"}
-        route_router = None
-    elif a.route_steps > 0:
-        route_cost = cost
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        legs, unfound = 0, 0
-        for _ in range(a.route_steps):
-            nl, _, st, _ = bulk.step()
-            legs += nl
-            unfound += (st != 0).sum()          # device-side count, read once after the loop
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        rel = time.perf_counter() - t0
-        unfound = int(unfound)
-        if world > 1:
-            rel, legs, unfound = bench_schema.reduce_route_stats(rel, legs, unfound, dev)
-        R = a.route_requests // world * world
-        route_res = bench_schema.route_section(R, a.route_steps, rel, legs, unfound, g.num_nodes, ctx_ms,
-                                               ctx_info, topo_s, route_router.stats(), world)
-        del bulk
+            guard.checkpoint()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            legs, unfound = 0, 0
+            for _ in range(a.route_steps):
+                nl, _, st, _ = bulk.step()
+                legs += nl
+                unfound += (st != 0).sum()          # device-side count, read once after the loop
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            rel = time.perf_counter() - t0
+            unfound = int(unfound)
+            guard.checkpoint()
+            if world > 1:
+                rel, legs, unfound = bench_schema.reduce_route_stats(rel, legs, unfound, dev)
+            R = a.route_requests // world * world
+            held.update(graph=gr, cost=cost, router=router, model=rmodel)
+            del bulk
+            return bench_schema.route_section(R, a.route_steps, rel, legs, unfound, gr.num_nodes, ctx_ms,
+                                              ctx_info, topo_s, router.stats(), world)
+        route_res = guard.run("route", route_section)
+        if "error" not in route_res:
+            g, route_cost, route_router, route_model = held["graph"], held["cost"], held["router"], held["model"]
 
     p50_ms = p99_ms = None
     p50_fastapi_ms = None
     p50_py_ms = None
     conc = None
+    serving_error = None
     if a.p50 and rank == 0:
-        # (1) headline p50 on the MAIN port of the stack `routest serve` runs (serve/frontend.py
-        #     ServingStack): real HTTP/1.1 over loopback (keep-alive) to the native front end
-        #     (csrc/native_server.hip): socket -> C++ JSON pack -> fused HIP kernel on this GPU
-        #     (zero-copy) -> C++ response formatting; the FastAPI app sits behind it for the long
-        #     tail.  Same endpoint semantics as the FastAPI handler (byte-identical bodies,
-        #     tests/test_frontend_gpu.py).  With the road graph of config 5 loaded, the same port
-        #     also serves the route_optimizer HTTP variant below.
-        import http.client
-        from routest_amd.api.app import build_services, create_app
-        from routest_amd.config import load_settings
-        from routest_amd.serve.eta_service import EtaService
-        from routest_amd.serve.frontend import ServingStack
-        from routest_amd.serve.loadgen import native_route_load, route_payloads
-        body = {"summary": {"distance": 12345}, "pickup_time": "2026-10-15T08:30:00",
-                "driver_age": 34, "weather": "Sunny", "traffic": "Medium"}
-        raw = json.dumps(body).encode()
-        hdr = {"Content-Type": "application/json"}
-        prov = None
-        if g is not None and route_cost is not None:
-            from routest_amd.routing.graph import GraphProvider
-            # context-aware road provider sharing the bench's router (the customized contexts)
-            prov = GraphProvider(g, None, device=dev, eta_model=route_model)
-            prov._routers[str(torch.device(dev))] = route_router
-        ss = load_settings(env={}, dotenv_path=None, devices=[local_rank], warm_scorer=False)
-        sv = build_services(ss, eta=EtaService(model, devices=[local_rank]), provider=prov, store=None)
-        with ServingStack(sv, create_app(sv), model, [local_rank], threads=8) as srv:
-            # native closed-loop client (csrc/runtime/http_client.h): one keep-alive connection,
-            # one request in flight — the client adds ~1 us instead of http.client's ~30 us
-            from routest_amd.ops import _ext
-            rtm = _ext.runtime(required=True)
-            r1 = rtm.http_load(srv.port, 1, 30.0, "/api/predict_eta", raw.decode(), 1,
-                               a.p50_requests, 200)
-            assert r1["errors"] == 0 and r1["requests"] >= a.p50_requests, r1
-            lat = r1["latencies_us"]
-            p50_ms = float(lat[len(lat) // 2]) * 1e-3
-            p99_ms = float(lat[int(len(lat) * 0.99) - 1]) * 1e-3
-            # the same with Python's http.client (what a Python caller would see)
-            conn = http.client.HTTPConnection("127.0.0.1", srv.port)
-            latp = []
-            for j in range(a.p50_requests // 2 + 200):
-                t1 = time.perf_counter()
-                conn.request("POST", "/api/predict_eta", body=raw, headers=hdr)
-                r = conn.getresponse()
-                r.read()
-                if j >= 200:
-                    latp.append(time.perf_counter() - t1)
-                assert r.status == 200
-            latp.sort()
-            p50_py_ms = latp[len(latp) // 2] * 1e3
-            # 16 concurrent single-item clients (separate connections; the reactors batch them)
-            r16 = rtm.http_load(srv.port, 16, 2.0, "/api/predict_eta", raw.decode(), 4, 0, 50)
-            assert r16["errors"] == 0, r16
-            conc = r16["requests"] / r16["seconds"]
-            # config 5 as a service: 1k concurrent multi-stop optimize_route requests on the same
-            # port — CCH road matrices + K6 + CCH legs + path copy-out + C++ GeoJSON (maneuvers)
-            if prov is not None and route_res is not None and srv.front.routes:
-                route_res["http"] = native_route_load(srv, route_payloads(g.lat, g.lon, 1000, seed=1), 1000,
-                                                      a.route_http_seconds)
-        sv.eta.close()
-        # the dashboard's own request (F02 verbatim: use_ml_eta, context, meta, driver_age) at 1k
-        # concurrency on the same port, every answer persisted into a SQLite store on disk — the
-        # canonical product path of /api/optimize_route (RO/Flaskr/routes.py:89-127)
-        if (prov is not None and isinstance(route_res, dict) and "error" not in route_res
-                and a.route_http_seconds > 0):
-            import tempfile
-            from routest_amd.serve.loadgen import f02_payloads
-            from routest_amd.store.store import SQLiteStore
-            with tempfile.TemporaryDirectory(prefix="routest-bench-") as td:
-                store = SQLiteStore(os.path.join(td, "routest.db"))
-                ids = [loc["id"] for loc in store.locations()]
-                sv2 = build_services(ss, eta=EtaService(model, devices=[local_rank]), provider=prov, store=store)
-                with ServingStack(sv2, create_app(sv2), model, [local_rank], threads=8) as srv2:
-                    if srv2.front.routes:
-                        r2 = native_route_load(srv2, f02_payloads(g.lat, g.lon, 1000, seed=2, location_ids=ids),
-                                               1000, a.route_http_seconds)
-                        r2["store"] = "sqlite file (WAL, synchronous=NORMAL), group commit per flush"
-                        route_res["http_f02"] = r2
-                sv2.eta.close()
-                store.close()
-
-        # (2) the FastAPI app in-process over ASGI (like the reference's Flask test-client figure)
-        import asyncio
-        import httpx
-        from routest_amd.api.app import build_services, create_app
-        from routest_amd.config import load_settings
-        from routest_amd.serve.eta_service import EtaService
-        s = load_settings(env={}, dotenv_path=None, devices=[local_rank])
-        app = create_app(build_services(s, eta=EtaService(model, devices=[local_rank]), store=None))
-
-        async def _lat():
-            out = []
-            async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app),
-                                         base_url="http://bench") as c:
-                for j in range(a.p50_requests + 200):
+        # (rank 0 alone; ranks 1..N-1 wait at guard.hold() below.  A failure here is reported as
+        # "serving_error" and the line still prints)
+        try:
+            raise_if_injected("serving", rank)
+            # (1) headline p50 on the MAIN port of the stack `routest serve` runs (serve/frontend.py
+            #     ServingStack): real HTTP/1.1 over loopback (keep-alive) to the native front end
+            #     (csrc/native_server.hip): socket -> C++ JSON pack -> fused HIP kernel on this GPU
+            #     (zero-copy) -> C++ response formatting; the FastAPI app sits behind it for the long
+            #     tail.  Same endpoint semantics as the FastAPI handler (byte-identical bodies,
+            #     tests/test_frontend_gpu.py).  With the road graph of config 5 loaded, the same port
+            #     also serves the route_optimizer HTTP variant below.
+            import http.client
+            from routest_amd.api.app import build_services, create_app
+            from routest_amd.config import load_settings
+            from routest_amd.serve.eta_service import EtaService
+            from routest_amd.serve.frontend import ServingStack
+            from routest_amd.serve.loadgen import native_route_load, route_payloads
+            body = {"summary": {"distance": 12345}, "pickup_time": "2026-10-15T08:30:00",
+                    "driver_age": 34, "weather": "Sunny", "traffic": "Medium"}
+            raw = json.dumps(body).encode()
+            hdr = {"Content-Type": "application/json"}
+            prov = None
+            if g is not None and route_cost is not None:
+                from routest_amd.routing.graph import GraphProvider
+                # context-aware road provider sharing the bench's router (the customized contexts)
+                prov = GraphProvider(g, None, device=dev, eta_model=route_model)
+                prov._routers[str(torch.device(dev))] = route_router
+            ss = load_settings(env={}, dotenv_path=None, devices=[local_rank], warm_scorer=False)
+            sv = build_services(ss, eta=EtaService(model, devices=[local_rank]), provider=prov, store=None)
+            with ServingStack(sv, create_app(sv), model, [local_rank], threads=8) as srv:
+                # native closed-loop client (csrc/runtime/http_client.h): one keep-alive connection,
+                # one request in flight — the client adds ~1 us instead of http.client's ~30 us
+                from routest_amd.ops import _ext
+                rtm = _ext.runtime(required=True)
+                r1 = rtm.http_load(srv.port, 1, 30.0, "/api/predict_eta", raw.decode(), 1,
+                                   a.p50_requests, 200)
+                assert r1["errors"] == 0 and r1["requests"] >= a.p50_requests, r1
+                lat = r1["latencies_us"]
+                p50_ms = float(lat[len(lat) // 2]) * 1e-3
+                p99_ms = float(lat[int(len(lat) * 0.99) - 1]) * 1e-3
+                # the same with Python's http.client (what a Python caller would see)
+                conn = http.client.HTTPConnection("127.0.0.1", srv.port)
+                latp = []
+                for j in range(a.p50_requests // 2 + 200):
                     t1 = time.perf_counter()
-                    r = await c.post("/api/predict_eta", json=body)
-                    dt_ = time.perf_counter() - t1
-                    assert r.status_code == 200, r.text
+                    conn.request("POST", "/api/predict_eta", body=raw, headers=hdr)
+                    r = conn.getresponse()
+                    r.read()
                     if j >= 200:
-                        out.append(dt_)
-            return out
-        lat2 = sorted(asyncio.run(_lat()))
-        p50_fastapi_ms = lat2[len(lat2) // 2] * 1e3
-        app.state.services.eta.close()
+                        latp.append(time.perf_counter() - t1)
+                    assert r.status == 200
+                latp.sort()
+                p50_py_ms = latp[len(latp) // 2] * 1e3
+                # 16 concurrent single-item clients (separate connections; the reactors batch them)
+                r16 = rtm.http_load(srv.port, 16, 2.0, "/api/predict_eta", raw.decode(), 4, 0, 50)
+                assert r16["errors"] == 0, r16
+                conc = r16["requests"] / r16["seconds"]
+                # config 5 as a service: 1k concurrent multi-stop optimize_route requests on the same
+                # port — CCH road matrices + K6 + CCH legs + path copy-out + C++ GeoJSON (maneuvers)
+                if prov is not None and route_res is not None and srv.front.routes:
+                    route_res["http"] = native_route_load(srv, route_payloads(g.lat, g.lon, 1000, seed=1), 1000,
+                                                          a.route_http_seconds)
+            sv.eta.close()
+            # the dashboard's own request (F02 verbatim: use_ml_eta, context, meta, driver_age) at 1k
+            # concurrency on the same port, every answer persisted into a SQLite store on disk — the
+            # canonical product path of /api/optimize_route (RO/Flaskr/routes.py:89-127)
+            if (prov is not None and isinstance(route_res, dict) and "error" not in route_res
+                    and a.route_http_seconds > 0):
+                import tempfile
+                from routest_amd.serve.loadgen import f02_payloads
+                from routest_amd.store.store import SQLiteStore
+                with tempfile.TemporaryDirectory(prefix="routest-bench-") as td:
+                    store = SQLiteStore(os.path.join(td, "routest.db"))
+                    ids = [loc["id"] for loc in store.locations()]
+                    sv2 = build_services(ss, eta=EtaService(model, devices=[local_rank]), provider=prov, store=store)
+                    with ServingStack(sv2, create_app(sv2), model, [local_rank], threads=8) as srv2:
+                        if srv2.front.routes:
+                            r2 = native_route_load(srv2, f02_payloads(g.lat, g.lon, 1000, seed=2, location_ids=ids),
+                                                   1000, a.route_http_seconds)
+                            r2["store"] = "sqlite file (WAL, synchronous=NORMAL), group commit per flush"
+                            route_res["http_f02"] = r2
+                    sv2.eta.close()
+                    store.close()
+
+            # (2) the FastAPI app in-process over ASGI (like the reference's Flask test-client figure)
+            import asyncio
+            import httpx
+            from routest_amd.api.app import build_services, create_app
+            from routest_amd.config import load_settings
+            from routest_amd.serve.eta_service import EtaService
+            s = load_settings(env={}, dotenv_path=None, devices=[local_rank])
+            app = create_app(build_services(s, eta=EtaService(model, devices=[local_rank]), store=None))
+
+            async def _lat():
+                out = []
+                async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app),
+                                             base_url="http://bench") as c:
+                    for j in range(a.p50_requests + 200):
+                        t1 = time.perf_counter()
+                        r = await c.post("/api/predict_eta", json=body)
+                        dt_ = time.perf_counter() - t1
+                        assert r.status_code == 200, r.text
+                        if j >= 200:
+                            out.append(dt_)
+                return out
+            lat2 = sorted(asyncio.run(_lat()))
+            p50_fastapi_ms = lat2[len(lat2) // 2] * 1e3
+            app.state.services.eta.close()
+        except Exception as e:  # noqa: BLE001 - the headline line must still print
+            import traceback
+            traceback.print_exc()
+            serving_error = repr(e)[:300]
 
     if rank == 0:
         preds = B * a.steps * world
@@ -667,12 +702,16 @@ def main() -> None:
             "dp_training_large_batch": train_big_res,
             "gcn": gcn_res,
             "route_optimizer": route_res,
+            "serving_error": serving_error,
             "check_max_err_vs_emulation": err_emu,
             "check_max_err_vs_fp32": err_fp32,
             "finite": ok,
         }
         out["schema_problems"] = bench_schema.problems(out)
         print(json.dumps(out), flush=True)
+    # every rank meets on the gloo side group (ranks 1..N-1 have waited here while rank 0 served),
+    # then the communicators are torn down together
+    guard.hold()
     if devcomm is not None:
         torch.cuda.synchronize()
         devcomm.close()

@@ -44,6 +44,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -76,6 +77,7 @@ struct ServerCfg {
   RouteService* routes = nullptr;      // this reactor's GPU's route service (nullptr = relay routes)
   Shared* sh = nullptr;                // the server's models, scorers and GPU health
   std::string history_db;              // the store's SQLite file: history / locations answered natively
+  std::shared_ptr<const rrec::RecordGraph> record_graph;   // compact route records' graph (history detail)
 };
 
 // GPU health of one reactor slot: consecutive launch failures quarantine the GPU; a
@@ -640,7 +642,10 @@ class Reactor {
       c.async = true;
       ++inflight_;
       st_.route_requests.fetch_add(1, std::memory_order_relaxed);
-      cfg_.routes->submit(j);
+      if (!cfg_.routes->submit(j)) {             // the service is stopping: the app answers
+        j->fallback = true;
+        job_done(j);
+      }
       return;
     }
     if (!cfg_.history_db.empty() && (method == "GET" || method == "DELETE") && answer_history(c, method, path, keep, origin, raw))
@@ -752,6 +757,7 @@ class Reactor {
       hdb_tried_ = true;
       std::string err;
       (void)hdb_.open(cfg_.history_db, err);
+      hdb_.set_graph(cfg_.record_graph);
     }
     if (!hdb_.ok()) return false;
     rth::Reply r;
@@ -1318,9 +1324,15 @@ struct Server {
   std::vector<std::unique_ptr<Reactor>> reactors;
   std::vector<std::thread> threads;
   std::vector<std::unique_ptr<RouteService>> routes;      // one per GPU
+  std::shared_mutex routes_mu;                             // guards routes_open (failover lambdas)
+  bool routes_open = false;                                // set once every service exists
   std::shared_ptr<AltScorerState> alt = std::make_shared<AltScorerState>();   // "alternatives" scorer
   ~Server() {
     if (sh.hang_release) *(volatile int*)sh.hang_release = 1;   // release any gpu_hang kernel
+    {
+      std::unique_lock<std::shared_mutex> lk(routes_mu);     // waits out failovers in flight
+      routes_open = false;
+    }
     routes.clear();                                          // joins the route workers
     for (PersistentScorer* p : sh.scorers)                   // stop + wait for the resident kernels
       if (p) pscore_destroy(p);
@@ -1423,6 +1435,15 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
     std::lock_guard<std::mutex> lk(*sh.scorer_mus[g]);
     restart_scorer(s, (int)g);
   }
+  // one view of the road graph for every route service's compact records and every reactor's
+  // history reader (the same arrays: the services' configs point at the provider's tensors)
+  if (!routes.empty() && routes[0].provider == 1 && routes[0].h_length != nullptr && routes[0].glat != nullptr) {
+    auto rg = std::make_shared<rrec::RecordGraph>();
+    const RouteServiceCfg& r0 = routes[0];
+    rg->own_names = r0.names;
+    rg->build(r0.N, r0.glat, r0.glon, r0.h_indptr, r0.h_indices, r0.h_length, r0.h_edge_name, &rg->own_names);
+    if (rg->ok()) s->cfg.record_graph = rg;
+  }
   for (int i = 0; i < s->cfg.threads; ++i) {
     ServerCfg rc = s->cfg;                       // reactors are spread round-robin over the GPUs
     const size_t g = (size_t)i % devices.size();
@@ -1440,6 +1461,7 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
   s->routes.reserve(routes.size());
   for (size_t g = 0; g < routes.size(); ++g) {
     RouteServiceCfg rc = routes[g];
+    rc.record_graph = s->cfg.record_graph;
     Shared* shp = &s->sh;
     const int slot = (int)g;
     rc.eta_model = [shp, slot]() { return shp->model(slot); };
@@ -1449,12 +1471,19 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
     // route service that is not itself broken
     rc.on_timeout = [shp, slot]() { shp->timed_out(slot); };
     rc.failover = [s, slot](RouteJob* j) {
+      // (shared lock: the list is published once every service exists, and ~Server closes it
+      // before the services are destroyed — a late failover then relays instead of submitting
+      // into a drained or deleted service)
+      std::shared_lock<std::shared_mutex> lk(s->routes_mu);
+      if (!s->routes_open) return false;
       const int n = (int)s->routes.size();
+      if (j->hops >= n - 1) return false;      // every other service has had it: to the app
       for (int k = 1; k < n; ++k) {
         RouteService* r = s->routes[(size_t)((slot + k) % n)].get();
         if (r != nullptr && !r->broken()) {
-          r->submit(j);
-          return true;
+          ++j->hops;
+          if (r->submit(j)) return true;
+          --j->hops;
         }
       }
       return false;
@@ -1475,6 +1504,10 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
       }
       for (auto& [r, v] : by) r->jobs_done(v);
     });
+  }
+  {
+    std::unique_lock<std::shared_mutex> lk(s->routes_mu);
+    s->routes_open = true;
   }
   if (!s->routes.empty())
     for (int i = 0; i < s->cfg.threads; ++i) s->reactors[i]->set_routes(s->routes[(size_t)i % devices.size()].get());

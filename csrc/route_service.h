@@ -3,6 +3,7 @@
 #pragma once
 #include <cmath>
 #include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -11,6 +12,7 @@
 #include "native_model.h"
 #include "ops.h"
 #include "runtime/route_core.h"
+#include "runtime/route_record.h"
 
 #include <mutex>
 
@@ -95,8 +97,14 @@ struct RouteServiceCfg {
   std::shared_ptr<AltScorerState> alt;
   // latency watchdog (ROUTEST_ROUTE_DEADLINE_MS): a flush whose GPU work misses the deadline marks
   // the service broken until that work drains; its jobs — and every flush meanwhile — are handed
-  // to `failover` (another GPU's route service; false: none left -> relayed to the app)
+  // to `failover` (another GPU's route service; false: none left -> relayed to the app).  A job is
+  // handed on at most n-1 times (RouteJob::hops): a failure that repeats on every service (an
+  // allocation, a context build) ends at the app instead of bouncing between services forever
+  //
   std::function<bool(RouteJob*)> failover;
+  // the road graph's compact-record view (csrc/runtime/route_record.h), shared with the native
+  // history readers; unset: the service builds its own when the graph carries edge metres
+  std::shared_ptr<const rrec::RecordGraph> record_graph;
   std::function<void()> on_timeout;       // the slot's GPU is quarantined for predictions too
   std::function<bool()> hang_fault;       // ROUTEST_FAULT=gpu_hang@<slot> (the watchdog's test hook)
   const int* hang_release_d = nullptr;    // its device-visible release flag
@@ -122,6 +130,7 @@ struct RouteJob {
   bool parsed = false;              // request parsed (a job deferred for its context keeps it)
   double defer_t0 = 0.0;            // when it was first deferred for its context's build (us)
   bool sync_ctx = false;            // its context's background build failed: build it in the flush
+  int hops = 0;                     // times handed to another GPU's route service (failover)
   // "alternatives": unique leg pairs in order, their via nodes, the chosen candidates (legs owned
   // here) and the response block
   std::vector<std::pair<int, int>> alt_pairs;
@@ -133,7 +142,7 @@ struct RouteJob {
   float eta_min = NAN;
   std::string eta_iso, request_id;
   std::string p_stops, p_geom;      // row texts for the persistence thread (prep_persist)
-  std::string p_legs;               // legs side-file reference ("" = the assembled segments inline)
+  std::string rec;                  // compact route record (route_record.h; "" = legs / geometry as text)
   bool p_ok = false;
   rtc::Stamp now;
 };
@@ -142,7 +151,8 @@ class RouteService {
  public:
   RouteService(const RouteServiceCfg& cfg, std::function<void(RouteJob*)> done);
   ~RouteService();
-  void submit(RouteJob* j);
+  // false once the service is stopping (the job is not taken: the caller relays it to the app)
+  bool submit(RouteJob* j);
   // finished jobs handed back many at a time (one wake-up per receiver instead of one per job);
   // set before the first submit.  Unset: `done` per job.
   void set_done_batch(std::function<void(std::vector<RouteJob*>&)> done_many);

@@ -175,47 +175,6 @@ struct RowId {
   }
 };
 
-// Append-only side file of the large route texts (store/store.py BLOB_REF): each result's legs and
-// geometry are written here by the assembly threads at a reserved offset (pwrite, in parallel) and
-// the row holds a 20-odd byte reference, so SQLite's single writer no longer moves ~30-100 KB per
-// route through its WAL.  One log per database path, shared by every GPU's route service.
-struct BlobLog {
-  int fd = -1;
-  std::atomic<long long> off{0};
-  ~BlobLog() {
-    if (fd >= 0) ::close(fd);
-  }
-  // n bytes at a fresh offset; false on an I/O error
-  bool put(const std::string& a, const std::string& b, long long& at) {
-    const long long n = (long long)(a.size() + b.size());
-    at = off.fetch_add(n);
-    for (const auto& [p, len, o] : {std::tuple<const char*, size_t, long long>{a.data(), a.size(), at},
-                                    std::tuple<const char*, size_t, long long>{b.data(), b.size(), at + (long long)a.size()}}) {
-      size_t done = 0;
-      while (done < len) {
-        const ssize_t w = ::pwrite(fd, p + done, len - done, (off_t)(o + (long long)done));
-        if (w <= 0) return false;
-        done += (size_t)w;
-      }
-    }
-    return true;
-  }
-};
-
-std::shared_ptr<BlobLog> blob_log(const std::string& db_path) {
-  static std::mutex mu;
-  static std::unordered_map<std::string, std::weak_ptr<BlobLog>> logs;
-  std::lock_guard<std::mutex> lk(mu);
-  if (auto l = logs[db_path].lock()) return l;
-  auto l = std::make_shared<BlobLog>();
-  l->fd = ::open((db_path + ".blobs").c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
-  if (l->fd < 0) return nullptr;
-  const off_t end = ::lseek(l->fd, 0, SEEK_END);
-  l->off.store(end > 0 ? (long long)end : 0);
-  logs[db_path] = l;
-  return l;
-}
-
 // Exact host search for the rare leg both GPU stages gave up on (graph.py _exact_fallback):
 // Dijkstra from s stopping when t is settled.
 bool host_dijkstra(const int* indptr, const int* indices, const float* cost, int N, int s, int t, int max_path,
@@ -359,6 +318,7 @@ struct RouteService::Impl {
   hipEvent_t ev_gpu{}, ev_asm{};
   hipStream_t hang_stream{};              // the gpu_hang fault hook's stream (own hardware queue)
   std::atomic<long long> n_failed_over{0};
+  bool fail_fault = false;                 // ROUTEST_FAULT=route_fail (test hook)
 
   hipError_t sync(hipStream_t s, hipEvent_t ev) {
     hipError_t e = hipEventRecord(ev, s);
@@ -435,14 +395,22 @@ struct RouteService::Impl {
   long long commits = 0;
   bool ck_stop = false;
 
-  std::shared_ptr<BlobLog> blobs;          // the side file of legs / geometry (nullptr: inline)
   rtr::CoordCache coord_cache;             // graph nodes' "[lon,lat]" strings (graph provider)
   std::vector<double> edge_heading;        // per road edge: rtr::hop_heading (graph provider)
+  // compact route records (runtime/route_record.h): the graph view persisted rows are encoded
+  // against — the server's shared one, or this service's own over the tables above
+  std::shared_ptr<const rrec::RecordGraph> rg;
+  const rtr::CoordCache* ccache() const {
+    if (rg) return rg->cc;
+    return coord_cache.ofs.empty() ? nullptr : &coord_cache;
+  }
+  const double* headings() const {
+    if (rg) return rg->heading;
+    return edge_heading.empty() ? nullptr : edge_heading.data();
+  }
 
   void open_store() {
     if (cfg.sqlite_path.empty()) return;
-    const char* bv = std::getenv("ROUTEST_STORE_BLOBS");
-    if (!(bv && std::string(bv) == "0")) blobs = blob_log(cfg.sqlite_path);
     std::string err;
     if (!sql.load(err)) return;
     if (sql.open_v2(cfg.sqlite_path.c_str(), &db, rtsql::OPEN_READWRITE | rtsql::OPEN_URI | rtsql::OPEN_NOMUTEX,
@@ -506,12 +474,13 @@ struct RouteService::Impl {
   }
   bool bind_text(void* st, int i, std::string&&) = delete;    // a temporary would dangle
 
-  // store.py build_rows + SQLiteStore.persist_request_and_result for one job; "" on failure
-  // the row texts of a job (store.py build_rows): stops JSON and the geometry object — built on the
-  // assembly stage's threads, so the single persistence thread (SQLite's one writer) only binds
-  // and steps; with the side file, legs and geometry are written there and the row gets their
-  // references.  false: a meta / stops shape the Python adapter would refuse (persist fails)
-  static bool prep_persist(RouteJob* j, BlobLog* blobs) {
+  // the row texts of a job (store.py build_rows): the stops JSON and, for a route without a compact
+  // record, the geometry object — built on the assembly stage's threads, so the single persistence
+  // thread (SQLite's one writer) only binds and steps.  A graph route's legs and geometry are its
+  // record (j->rec, encoded in assemble_all): ~1-3 KB instead of ~37 KB of text, rebuilt
+  // byte-identically by the history readers.  false: a meta / stops shape the Python adapter would
+  // refuse (persist fails)
+  static bool prep_persist(RouteJob* j) {
     const rtj::Value* root = j->req.root;
     const rtj::Value* meta = root->get("meta");
     if (meta && meta->truthy() && meta->kind != rtj::Value::Obj) return false;   // .get on a non-dict
@@ -525,17 +494,12 @@ struct RouteService::Impl {
     if (!rtr::put_value(stops, *root->get("destination_points"))) return false;
     stops += '}';
     std::string& geom = j->p_geom;
-    geom.reserve(j->asmb.coords.size() + 40);
-    geom = "{\"type\":\"LineString\",\"coordinates\":";
-    geom += j->asmb.coords;
-    geom += '}';
-    j->p_legs.clear();
-    long long at = 0;
-    if (blobs != nullptr && blobs->put(j->asmb.segments, geom, at)) {
-      const size_t nl = j->asmb.segments.size(), ng = geom.size();
-      // (octal: "\x01b..." would read as one hex escape)
-      j->p_legs = "\001blob:" + std::to_string(at) + ":" + std::to_string(nl);
-      geom = "\001blob:" + std::to_string(at + (long long)nl) + ":" + std::to_string(ng);
+    geom.clear();
+    if (j->rec.empty()) {
+      geom.reserve(j->asmb.coords.size() + 40);
+      geom = "{\"type\":\"LineString\",\"coordinates\":";
+      geom += j->asmb.coords;
+      geom += '}';
     }
     j->p_ok = true;
     return true;
@@ -561,7 +525,9 @@ struct RouteService::Impl {
     bool ok = bind_text(st, b + 1, res_id) && bind_text(st, b + 2, rid) && bind_text(st, b + 3, a.order) &&
               sql.bind_double(st, b + 4, rtr::py_round(a.dist, 2)) == rtsql::OK &&
               sql.bind_double(st, b + 5, rtr::py_round(a.dur, 2)) == rtsql::OK &&
-              bind_text(st, b + 6, j->p_legs.empty() ? a.segments : j->p_legs) && bind_text(st, b + 7, j->p_geom);
+              (j->rec.empty() ? bind_text(st, b + 6, a.segments) && bind_text(st, b + 7, j->p_geom)
+                              : sql.bind_blob(st, b + 6, j->rec.data(), (int)j->rec.size(), rtsql::STATIC) == rtsql::OK &&
+                                    sql.bind_null(st, b + 7) == rtsql::OK);
     if (ok && !j->eta_iso.empty()) {
       ok = sql.bind_double(st, b + 8, (double)j->eta_min) == rtsql::OK && bind_text(st, b + 9, j->eta_iso);
     } else if (ok) {
@@ -683,6 +649,9 @@ struct RouteService::Impl {
     }
     if (const char* v = std::getenv("ROUTEST_CCH_ASYNC")) async_ctx = std::string(v) != "0";
     if (const char* v = std::getenv("ROUTEST_ROUTE_DEADLINE_MS")) deadline_ms = std::atof(v);
+    // ROUTEST_FAULT=route_fail: every flush of every service fails (not a timeout) — the hop limit
+    // of the failover must end each job at the app
+    if (const char* v = std::getenv("ROUTEST_FAULT")) fail_fault = std::string(v).find("route_fail") != std::string::npos;
     if (hipEventCreateWithFlags(&ev_gpu, hipEventDisableTiming) != hipSuccess) ev_gpu = nullptr;
     if (const char* v = std::getenv("ROUTEST_CCH_PREFETCH_MIN")) prefetch_min = std::atoi(v);
     // rehearsal knob (bench/route_context_bench.py): shifts the clock "now" routing contexts are
@@ -733,6 +702,7 @@ struct RouteService::Impl {
       }
       gpu_stage(*b);
       stream = main_stream;         // (the hang stream is reused once drained: see drained())
+      if (fail_fault && !b->jobs.empty()) b->failed = true;
       if (b->failed) {              // a GPU error or the deadline: another GPU's service answers
         hand_off(b->jobs);
         delete b;
@@ -1708,6 +1678,13 @@ struct RouteService::Impl {
         std::vector<rtr::Dir> dirs(j->calls.size());
         std::string perr;
         size_t off = 0;
+        // the compact record of a route that will be persisted (graph provider, no alternatives)
+        bool want_rec = rg != nullptr && db != nullptr && !j->request_route && j->req.alt_k == 0 &&
+                        cfg.provider == 1 && !j->calls.empty();
+        rrec::Writer rw;
+        std::vector<uint64_t> durs;
+        std::vector<uint32_t> per_leg;
+        j->rec.clear();
         for (size_t k = 0; k < j->calls.size() && perr.empty(); ++k) {
           if (cfg.provider == 0) {
             rtr::haversine_directions(j->calls[k], j->req.profile, cfg.circuity, cfg.step_m, dirs[k]);
@@ -1734,16 +1711,25 @@ struct RouteService::Impl {
               gh.cost = b.host_cost[j->group]->data();
               gh.edge_name = cfg.h_edge_name;
               gh.names = &cfg.names;
-              gh.edge_heading = edge_heading.empty() ? nullptr : edge_heading.data();
+              gh.edge_heading = headings();
               ghp = &gh;
             }
+            if (k == 0 && want_rec) rrec::begin(rw, *rg, ghp != nullptr, j->req.profile, j->calls.size());
+            durs.clear();
+            per_leg.clear();
+            rtr::StepDurs sd;
+            sd.out = &durs;
+            sd.per_leg = &per_leg;
             perr = rtr::graph_directions(j->calls[k], j->nodes.data() + off, lp, j->req.profile, cfg.glat, cfg.glon,
-                                         dirs[k], ghp);
+                                         dirs[k], ghp, want_rec && ghp ? &sd : nullptr);
             off += j->calls[k].size();
+            if (want_rec && perr.empty())
+              want_rec = !sd.bad && rrec::add_call(rw, *rg, ghp, j->calls[k], lp, durs, per_leg);
           }
         }
         if (!perr.empty()) j->req.error = perr;
-        if (!rtr::assemble(j->req, j->plan, dirs, cfg.engine, j->asmb, coord_cache.ofs.empty() ? nullptr : &coord_cache))
+        if (want_rec && perr.empty()) j->rec = std::move(rw.b);
+        if (!rtr::assemble(j->req, j->plan, dirs, cfg.engine, j->asmb, ccache()))
           j->fallback = true;
         else if (j->req.alt_k > 0 && j->asmb.ok) j->asmb.body += j->alt_json;
       }
@@ -1889,9 +1875,8 @@ struct RouteService::Impl {
     for (RouteJob* j : jobs)
       if (db && !j->fallback && !j->status && j->asmb.ok && !j->request_route) b.save.push_back(j);
     t0 = now_us();
-    BlobLog* bl = blobs.get();
     rtc::parallel_chunks(b.save.size(), 16, 16, [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) prep_persist(b.save[i], bl);
+      for (size_t i = lo; i < hi; ++i) prep_persist(b.save[i]);
     });
     add_t(7, t0);
   }
@@ -2010,14 +1995,11 @@ struct RouteService::Impl {
         seen = commits;
       }
       int log = 0, ck = 0;
-      // the side file first: a checkpointed row never reaches the disk ahead of the bytes it refers to
-      if (blobs) (void)::fdatasync(blobs->fd);
       sql.wal_checkpoint_v2(cdb, nullptr, rtsql::CHECKPOINT_PASSIVE, &log, &ck);
       std::unique_lock<std::mutex> lk(cmu);     // at most one checkpoint per 20 ms
       ccv.wait_for(lk, std::chrono::milliseconds(20), [&] { return ck_stop; });
     }
     int log = 0, ck = 0;
-    if (blobs) (void)::fdatasync(blobs->fd);
     sql.wal_checkpoint_v2(cdb, nullptr, rtsql::CHECKPOINT_PASSIVE, &log, &ck);
     sql.close(cdb);
   }
@@ -2028,13 +2010,26 @@ RouteService::RouteService(const RouteServiceCfg& cfg, std::function<void(RouteJ
   p_->done = std::move(done);
   if (cfg.provider == 1 && cfg.glat != nullptr) {
     p_->grid.build(cfg.glat, cfg.glon, (size_t)cfg.N, cfg.snap_c);
-    p_->coord_cache.build(cfg.glat, cfg.glon, (size_t)cfg.N);
-    if (cfg.h_indptr != nullptr && cfg.h_indices != nullptr) {
-      const int64_t E = cfg.h_indptr[cfg.N];
-      p_->edge_heading.resize((size_t)E);
-      for (int u = 0; u < cfg.N; ++u)
-        for (int32_t e = cfg.h_indptr[u]; e < cfg.h_indptr[u + 1]; ++e)
-          p_->edge_heading[(size_t)e] = rtr::hop_heading(cfg.glat, cfg.glon, u, cfg.h_indices[e]);
+    const auto& shared = cfg.record_graph;
+    if (shared && shared->ok() && shared->N == cfg.N && shared->glat == cfg.glat && shared->indptr == cfg.h_indptr &&
+        shared->length == cfg.h_length) {
+      p_->rg = shared;                 // the server's view of this same graph (its tables too)
+    } else {
+      p_->coord_cache.build(cfg.glat, cfg.glon, (size_t)cfg.N);
+      if (cfg.h_indptr != nullptr && cfg.h_indices != nullptr) {
+        const int64_t E = cfg.h_indptr[cfg.N];
+        p_->edge_heading.resize((size_t)E);
+        for (int u = 0; u < cfg.N; ++u)
+          for (int32_t e = cfg.h_indptr[u]; e < cfg.h_indptr[u + 1]; ++e)
+            p_->edge_heading[(size_t)e] = rtr::hop_heading(cfg.glat, cfg.glon, u, cfg.h_indices[e]);
+      }
+      if (cfg.h_length != nullptr && cfg.h_indptr != nullptr && cfg.h_indices != nullptr) {
+        auto g = std::make_shared<rrec::RecordGraph>();
+        const Impl* ip = p_;
+        g->build(cfg.N, cfg.glat, cfg.glon, cfg.h_indptr, cfg.h_indices, cfg.h_length, cfg.h_edge_name,
+                 &ip->cfg.names, &ip->coord_cache, ip->edge_heading.empty() ? nullptr : ip->edge_heading.data());
+        if (g->ok()) p_->rg = g;
+      }
     }
   }
   p_->th = std::thread([this] { p_->run(); });
@@ -2054,16 +2049,18 @@ void RouteService::set_done_batch(std::function<void(std::vector<RouteJob*>&)> d
   p_->done_many = std::move(done_many);
 }
 
-void RouteService::submit(RouteJob* j) {
+bool RouteService::submit(RouteJob* j) {
   if (!j->parsed) {             // on the submitting reactor's thread: off the flush's critical path
     p_->n_jobs.fetch_add(1, std::memory_order_relaxed);
     Impl::parse_job(j);
   }
   {
     std::lock_guard<std::mutex> lk(p_->mu);
+    if (p_->stop) return false;   // the run loop may have drained its queue already
     p_->q.push_back(j);
   }
   p_->cv.notify_one();
+  return true;
 }
 
 std::vector<long long> RouteService::stats() const {

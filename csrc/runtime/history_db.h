@@ -12,11 +12,13 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "json_lite.h"
 #include "route_core.h"
+#include "route_record.h"
 #include "sqlite_lite.h"
 
 namespace rth {
@@ -56,6 +58,9 @@ class HistoryDb {
     blob_fd_ = -1;
   }
   bool ok() const { return db_ != nullptr; }
+  // the road graph compact route records are rebuilt against (route_record.h); unset: such rows
+  // are relayed to the app
+  void set_graph(std::shared_ptr<const rrec::RecordGraph> g) { rg_ = std::move(g); }
 
   // Every call resets its statements on the way out: a statement left on a ROW keeps the
   // connection's read transaction (its WAL snapshot) open, and later reads would not see rows the
@@ -203,10 +208,23 @@ class HistoryDb {
         o += "\":";
         if (!put_col(o, st_res_, 2 + k)) return fb();
       }
-      o += ",\"legs\":";
-      if (!put_json_col(o, st_res_, 7, "[]", false)) return fb();
-      o += ",\"geometry\":";
-      if (!put_json_col(o, st_res_, 8, "null", false)) return fb();
+      if (sql_.column_type(st_res_, 7) == rtsql::T_BLOB) {
+        // a compact route record: legs and geometry rebuilt by the route service's own formatter,
+        // then through the same json.loads / json.dumps mirror as a text row
+        const void* b = sql_.column_blob(st_res_, 7);
+        const int nb = sql_.column_bytes(st_res_, 7);
+        std::string seg, geo;
+        if (!rg_ || b == nullptr || !rrec::decode(*rg_, b, (size_t)nb, seg, geo)) return fb();
+        o += ",\"legs\":";
+        if (!put_json_text(o, seg)) return fb();
+        o += ",\"geometry\":";
+        if (!put_json_text(o, geo)) return fb();
+      } else {
+        o += ",\"legs\":";
+        if (!put_json_col(o, st_res_, 7, "[]", false)) return fb();
+        o += ",\"geometry\":";
+        if (!put_json_col(o, st_res_, 8, "null", false)) return fb();
+      }
       o += '}';
     } else {
       return fb();
@@ -262,6 +280,7 @@ class HistoryDb {
   // reads
   std::string blob_path_;
   int blob_fd_ = -1;
+  std::shared_ptr<const rrec::RecordGraph> rg_;
   bool resolve(std::string& s) {
     static const char kRef[] = "\001blob:";
     if (s.compare(0, sizeof(kRef) - 1, kRef) != 0) return true;
@@ -356,6 +375,11 @@ class HistoryDb {
       o += dflt;
       return true;
     }
+    return rtr::put_value(o, v);
+  }
+  bool put_json_text(std::string& o, const std::string& s) {
+    rtj::Value v;
+    if (!parse(s, v)) return false;
     return rtr::put_value(o, v);
   }
   // Python int(str): optional surrounding whitespace, sign, digits (underscore forms -> fallback)

@@ -13,10 +13,12 @@
 
 #include <map>
 #include <memory>
+#include <mutex>
 
 #include "alternatives.h"
 #include "history_db.h"
 #include "route_core.h"
+#include "route_record.h"
 
 namespace py = pybind11;
 
@@ -110,6 +112,32 @@ class PyGraphSteps {
     g.names = &names_;
     return g;
   }
+  // the compact route records' view of this graph (built on first use: CoordCache, headings,
+  // fingerprint); shared with a HistoryDb
+  std::shared_ptr<const rrec::RecordGraph> record_graph() const {
+    std::lock_guard<std::mutex> lk(rg_mu_);
+    if (!rg_) {
+      auto g = std::make_shared<rrec::RecordGraph>();
+      g->build((int)lat_.shape(0), lat_.data(), lon_.data(), indptr_.data(), indices_.data(), length_.data(),
+               name_.size() ? name_.data() : nullptr, &names_);
+      rg_ = g;
+    }
+    return rg_;
+  }
+  // (legs JSON, geometry JSON) of a record the native route service persisted (store.py)
+  py::tuple decode_record(py::bytes rec) const {
+    const std::string b = rec;
+    auto g = record_graph();
+    std::string seg, geo, err;
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = rrec::decode(*g, b.data(), b.size(), seg, geo, &err);
+    }
+    if (!ok) throw std::invalid_argument(err);
+    return py::make_tuple(seg, geo);
+  }
+  std::string fingerprint() const { return std::to_string(record_graph()->fp); }
   py::list steps(py::array_t<int32_t, py::array::c_style | py::array::forcecast> path, double sec,
                  py::array_t<float, py::array::c_style | py::array::forcecast> cost, double speed_scale,
                  long long start, long long end) const {
@@ -142,6 +170,8 @@ class PyGraphSteps {
   py::array_t<double, py::array::c_style | py::array::forcecast> lat_, lon_;
   py::array_t<int32_t, py::array::c_style | py::array::forcecast> name_;
   std::vector<std::string> names_;
+  mutable std::mutex rg_mu_;
+  mutable std::shared_ptr<const rrec::RecordGraph> rg_;
 };
 
 py::bytes to_bytes(const std::string& s) { return py::bytes(s); }
@@ -149,9 +179,10 @@ py::bytes to_bytes(const std::string& s) { return py::bytes(s); }
 // The native history reader (history_db.h) for CPU tests: (status, body) or None (-> the app).
 class PyHistoryDb {
  public:
-  explicit PyHistoryDb(const std::string& path) {
+  explicit PyHistoryDb(const std::string& path, py::object graph) {
     std::string err;
     if (!db_.open(path, err)) throw std::runtime_error("HistoryDb: " + err);
+    if (!graph.is_none()) db_.set_graph(graph.cast<const PyGraphSteps&>().record_graph());
   }
   py::object wrap(const rth::Reply& r) {
     if (r.fallback) return py::none();
@@ -232,7 +263,8 @@ py::object route_assemble_graph(py::bytes body, const std::string& engine,
                                 py::array_t<double, py::array::c_style | py::array::forcecast> glat,
                                 py::array_t<double, py::array::c_style | py::array::forcecast> glon,
                                 py::array_t<int32_t, py::array::c_style | py::array::forcecast> nodes_of_calls,
-                                py::object trips_obj, py::dict legs_obj, py::object steps_obj, py::object cost_obj) {
+                                py::object trips_obj, py::dict legs_obj, py::object steps_obj, py::object cost_obj,
+                                bool with_record) {
   const std::string b = body;
   Value root = rtj::Parser(b.data(), b.size()).parse();
   rtr::RouteReq r = rtr::parse_route_request(&root);
@@ -260,11 +292,20 @@ py::object route_assemble_graph(py::bytes body, const std::string& engine,
   rtr::GraphHost gh;
   const rtr::GraphHost* ghp = nullptr;
   py::array_t<float, py::array::c_style | py::array::forcecast> cost;
-  if (!steps_obj.is_none() && !cost_obj.is_none()) {
-    cost = cost_obj.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
-    gh = steps_obj.cast<const PyGraphSteps&>().host(cost);
-    ghp = &gh;
+  std::shared_ptr<const rrec::RecordGraph> rg;
+  if (!steps_obj.is_none()) {
+    const PyGraphSteps& st = steps_obj.cast<const PyGraphSteps&>();
+    if (with_record) rg = st.record_graph();
+    if (!cost_obj.is_none()) {
+      cost = cost_obj.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+      gh = st.host(cost);
+      ghp = &gh;
+    }
   }
+  // (the compact record, as the route service writes it: route_record.h)
+  rrec::Writer rw;
+  bool rec_ok = rg != nullptr;
+  if (rec_ok) rrec::begin(rw, *rg, ghp != nullptr, r.profile, calls.size());
   const int32_t* nodes = nodes_of_calls.data();
   std::vector<rtr::Dir> dirs(calls.size());
   size_t off = 0;
@@ -275,18 +316,29 @@ py::object route_assemble_graph(py::bytes body, const std::string& engine,
       auto it = table.find({nodes[off + i], nodes[off + i + 1]});
       legs.push_back(it == table.end() ? &missing : &it->second.first);
     }
+    std::vector<uint64_t> durs;
+    std::vector<uint32_t> per_leg;
+    rtr::StepDurs sd;
+    sd.out = &durs;
+    sd.per_leg = &per_leg;
     const std::string e = rtr::graph_directions(calls[k], nodes + off, legs, r.profile, glat.data(), glon.data(), dirs[k],
-                                                ghp);
+                                                ghp, rec_ok && ghp ? &sd : nullptr);
     off += calls[k].size();
     if (!e.empty()) {
       r.error = e;
+      rec_ok = false;
       break;
     }
+    if (rec_ok) rec_ok = !sd.bad && rrec::add_call(rw, *rg, ghp, calls[k], legs, durs, per_leg);
   }
   rtr::Assembled a;
   if (!rtr::assemble(r, plan, dirs, engine, a)) return py::none();
   auto res = finish_plain(a, true, false);
-  return py::make_tuple(res.first, to_bytes(res.second));
+  if (!with_record) return py::make_tuple(res.first, to_bytes(res.second));
+  // (status, body, record bytes or None, the row's legs text, the row's geometry text)
+  std::string geo = "{\"type\":\"LineString\",\"coordinates\":" + a.coords + "}";
+  return py::make_tuple(res.first, to_bytes(res.second), rec_ok && a.ok ? py::object(to_bytes(rw.b)) : py::object(py::none()),
+                        a.segments, geo);
 }
 
 using F64 = py::array_t<double, py::array::c_style | py::array::forcecast>;
@@ -333,7 +385,7 @@ void bind_route(py::module& m) {
         py::arg("is_request_route") = false, py::arg("compat200") = true);
   m.def("route_assemble_graph", &route_assemble_graph, py::arg("body"), py::arg("engine"), py::arg("glat"),
         py::arg("glon"), py::arg("nodes"), py::arg("trips"), py::arg("legs"), py::arg("steps") = py::none(),
-        py::arg("cost") = py::none());
+        py::arg("cost") = py::none(), py::arg("with_record") = false);
   m.def("py_round", &rtr::py_round);
   m.def("json_float", [](double v) {     // the native JSON writer's float (tests: == json.dumps)
     std::string o;
@@ -341,7 +393,7 @@ void bind_route(py::module& m) {
     return o;
   });
   py::class_<PyHistoryDb>(m, "HistoryDb")
-      .def(py::init<const std::string&>())
+      .def(py::init<const std::string&, py::object>(), py::arg("path"), py::arg("graph") = py::none())
       .def("history", &PyHistoryDb::history, py::arg("limit") = py::none())
       .def("detail", &PyHistoryDb::detail)
       .def("delete", &PyHistoryDb::del)
@@ -356,6 +408,8 @@ void bind_route(py::module& m) {
            py::arg("indptr"), py::arg("indices"), py::arg("length"), py::arg("lat"), py::arg("lon"),
            py::arg("edge_name") = py::none(), py::arg("names") = std::vector<std::string>())
       .def("steps", &PyGraphSteps::steps, py::arg("path"), py::arg("sec"), py::arg("cost"), py::arg("speed_scale"),
-           py::arg("start"), py::arg("end"));
+           py::arg("start"), py::arg("end"))
+      .def("decode_record", &PyGraphSteps::decode_record, py::arg("record"))
+      .def("fingerprint", &PyGraphSteps::fingerprint);
   m.def("bearing_word", [](double a, double b, double c, double d) { return std::string(rtr::bearing_word(a, b, c, d)); });
 }

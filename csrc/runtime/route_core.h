@@ -623,23 +623,50 @@ struct Step {
   std::string name_str() const { return name ? *name : std::string("-"); }
 };
 
+// Maneuver step durations in and out of leg_steps (csrc/runtime/route_record.h): the writer of a
+// compact route record collects each step's rounded duration as integer tenths (`out`, with the
+// step count per leg in `per_leg`); a reader replays them (`in`) instead of summing edge costs of a
+// routing context it does not have.  `bad`: a duration not exactly k / 10 (never for py_round(x, 1)
+// of a finite non-negative x) or a replay that ran out.
+struct StepDurs {
+  std::vector<uint64_t>* out = nullptr;
+  std::vector<uint32_t>* per_leg = nullptr;
+  const uint64_t* in = nullptr;
+  size_t n_in = 0, pos = 0;
+  bool bad = false;
+  void put(double d) {
+    if (!out) return;
+    const double t = std::nearbyint(d * 10.0);
+    if (!(t >= 0.0 && t < 9.0e15) || t / 10.0 != d || std::signbit(d)) { bad = true; return; }
+    out->push_back((uint64_t)t);
+  }
+  bool take(double& d) {
+    if (!in) return false;
+    if (pos >= n_in) { bad = true; d = 0.0; return true; }
+    d = (double)in[pos++] / 10.0;
+    return true;
+  }
+};
+
 // Maneuvers along one leg's node path.  A new step starts where the road name changes or the
 // heading turns by >= 50 degrees; its type comes from the heading change at its first node, its
 // instruction is "Head <dir>[ on <name>]" for the first step, "<verb>[ onto <name>]" after.
 // Geometry indices: the leg's start coordinate is `start`, path node i is start + 1 + i, the
 // destination coordinate `end`.  Distances / durations are the hop edges' metres / seconds.
 inline void leg_steps(const GraphHost& g, const double* glat, const double* glon, const Leg& L, double speed_scale,
-                      long long start, long long end, std::vector<Step>& out) {
+                      long long start, long long end, std::vector<Step>& out, StepDurs* sd = nullptr) {
   out.clear();
   const int n = L.len;
   if (n <= 1) {
     Step s;
     s.dist = 0.0;
-    s.dur = py_round((double)L.sec * speed_scale, 1);
+    if (!(sd && sd->take(s.dur))) s.dur = py_round((double)L.sec * speed_scale, 1);
+    if (sd) sd->put(s.dur);
     s.verb = "Depart";
     s.wp0 = start;
     s.wp1 = end;
     out.push_back(s);
+    if (sd && sd->per_leg) sd->per_leg->push_back(1);
     return;
   }
   const int H = n - 1;
@@ -670,10 +697,11 @@ inline void leg_steps(const GraphHost& g, const double* glat, const double* glon
     for (int h = h0; h < h1; ++h)
       if (hop[h] >= 0) {
         d += (double)g.length[hop[h]];
-        t += (double)g.cost[hop[h]];
+        if (g.cost) t += (double)g.cost[hop[h]];
       }
     s.dist = py_round(d, 1);
-    s.dur = py_round(t * speed_scale, 1);
+    if (!(sd && sd->take(s.dur))) s.dur = py_round(t * speed_scale, 1);
+    if (sd) sd->put(s.dur);
     s.name = name_of(nm[h0]);
     if (h0 == 0) {
       s.type = 11;
@@ -687,6 +715,7 @@ inline void leg_steps(const GraphHost& g, const double* glat, const double* glon
     out.push_back(s);
     h0 = h1;
   }
+  if (sd && sd->per_leg) sd->per_leg->push_back((uint32_t)out.size());
 }
 
 // the characters of s as json.dumps would escape them inside a string (no quotes)
@@ -740,7 +769,8 @@ inline void put_step(std::string& o, const Step& s) {
 // GraphProvider.feature_from_legs — graph.py.  Returns "" or the ProviderError text.
 inline std::string graph_directions(const std::vector<std::pair<double, double>>& c, const int32_t* nodes,
                                     const std::vector<const Leg*>& legs, int profile, const double* glat,
-                                    const double* glon, Dir& out, const GraphHost* gh = nullptr) {
+                                    const double* glon, Dir& out, const GraphHost* gh = nullptr,
+                                    StepDurs* sd = nullptr) {
   const double speed_scale = profile_speed(CAR) / profile_speed(profile);
   out.xy.assign({c[0].first, c[0].second});
   out.raw.assign({1});
@@ -774,10 +804,10 @@ inline std::string graph_directions(const std::vector<std::pair<double, double>>
     out.way_points.push_back(end);
     const double dur = (double)L.sec * speed_scale;
     if (k) out.segments += ',';
-    if (gh != nullptr && gh->cost != nullptr) {
+    if (gh != nullptr && (gh->cost != nullptr || (sd != nullptr && sd->in != nullptr))) {
       // maneuvers along the path, then the arrival step (routing/graph.py feature_from_legs)
       std::vector<Step> steps;
-      leg_steps(*gh, glat, glon, L, speed_scale, start, end, steps);
+      leg_steps(*gh, glat, glon, L, speed_scale, start, end, steps, sd);
       std::string& sg = out.segments;
       sg += "{\"distance\":"; put_float(sg, py_round(dist, 1));
       sg += ",\"duration\":"; put_float(sg, py_round(dur, 1));
@@ -899,6 +929,34 @@ inline void directions_calls(const RouteReq& r, const Plan& p,
     for (int i : t) c.emplace_back(i == 0 ? r.src.lon : r.dst[i - 1].lon, i == 0 ? r.src.lat : r.dst[i - 1].lat);
     calls.push_back(std::move(c));
   }
+}
+
+// The geometry coordinates and the segments array of a request's directions results, exactly as
+// assemble() writes them (one call: its own; several trips: concatenated, empty segment lists
+// skipped) — the compact route record's reader (route_record.h) rebuilds the persisted texts with it.
+inline void dirs_geometry(const std::vector<Dir>& dirs, const CoordCache* cc, std::string& coords,
+                          std::string& segments) {
+  std::vector<double> xy;
+  std::vector<uint8_t> raw;
+  std::vector<int32_t> node;
+  bool nodes_ok = cc != nullptr;
+  for (const Dir& d : dirs) {
+    xy.insert(xy.end(), d.xy.begin(), d.xy.end());
+    raw.insert(raw.end(), d.raw.begin(), d.raw.end());
+    nodes_ok = nodes_ok && d.node.size() == d.raw.size();
+    if (nodes_ok) node.insert(node.end(), d.node.begin(), d.node.end());
+  }
+  coords.clear();
+  put_coords(coords, xy, raw, nodes_ok ? &node : nullptr, cc);
+  segments = "[";
+  bool first = true;
+  for (const Dir& d : dirs) {
+    if (d.segments.empty()) continue;
+    if (!first) segments += ',';
+    first = false;
+    segments += d.segments;
+  }
+  segments += ']';
 }
 
 // The assembled response (properties left open so ETA / persistence fields can follow) and the

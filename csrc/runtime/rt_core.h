@@ -16,6 +16,7 @@
 #include <deque>
 #include <functional>
 #include <memory>
+#include <exception>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -534,13 +535,21 @@ inline void parallel_chunks(size_t n, size_t min_per_thread, unsigned max_thread
     std::atomic<size_t> next{0}, done{0};
     std::mutex m;
     std::condition_variable cv;
+    std::exception_ptr err;               // the first chunk's exception (rethrown by the caller)
   };
   auto st = std::make_shared<State>();
   F* fp = &fn;
+  // a chunk that throws still counts as done (its exception kept), so the caller never unwinds its
+  // frame — fn and what it captures — while a pool worker may still be calling (*fp)
   auto work = [st, fp, chunks, per, n]() {
     size_t k;
     while ((k = st->next.fetch_add(1)) < chunks) {
-      (*fp)(k * per, std::min(n, (k + 1) * per));
+      try {
+        (*fp)(k * per, std::min(n, (k + 1) * per));
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(st->m);
+        if (!st->err) st->err = std::current_exception();
+      }
       if (st->done.fetch_add(1) + 1 == chunks) {
         std::lock_guard<std::mutex> lk(st->m);
         st->cv.notify_all();
@@ -551,6 +560,7 @@ inline void parallel_chunks(size_t n, size_t min_per_thread, unsigned max_thread
   work();
   std::unique_lock<std::mutex> lk(st->m);
   st->cv.wait(lk, [&] { return st->done.load() == chunks; });
+  if (st->err) std::rethrow_exception(st->err);
 }
 
 }  // namespace rtc

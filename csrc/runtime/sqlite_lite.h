@@ -24,6 +24,7 @@ struct Api {
   int (*bind_double)(void*, int, double) = nullptr;
   int (*bind_int64)(void*, int, long long) = nullptr;
   int (*bind_null)(void*, int) = nullptr;
+  int (*bind_blob)(void*, int, const void*, int, void (*)(void*)) = nullptr;
   int (*step)(void*) = nullptr;
   int (*reset)(void*) = nullptr;
   int (*clear_bindings)(void*) = nullptr;
@@ -35,6 +36,7 @@ struct Api {
   double (*column_double)(void*, int) = nullptr;
   long long (*column_int64)(void*, int) = nullptr;
   const unsigned char* (*column_text)(void*, int) = nullptr;
+  const void* (*column_blob)(void*, int) = nullptr;
   int (*column_bytes)(void*, int) = nullptr;
   const char* (*column_name)(void*, int) = nullptr;
   int (*changes)(void*) = nullptr;
@@ -60,6 +62,7 @@ struct Api {
     sym(bind_double, "sqlite3_bind_double");
     sym(bind_int64, "sqlite3_bind_int64");
     sym(bind_null, "sqlite3_bind_null");
+    sym(bind_blob, "sqlite3_bind_blob");
     sym(step, "sqlite3_step");
     sym(reset, "sqlite3_reset");
     sym(clear_bindings, "sqlite3_clear_bindings");
@@ -71,6 +74,7 @@ struct Api {
     sym(column_double, "sqlite3_column_double");
     sym(column_int64, "sqlite3_column_int64");
     sym(column_text, "sqlite3_column_text");
+    sym(column_blob, "sqlite3_column_blob");
     sym(column_bytes, "sqlite3_column_bytes");
     sym(column_name, "sqlite3_column_name");
     sym(changes, "sqlite3_changes");

@@ -197,6 +197,10 @@ def build_services(settings: Optional[Settings] = None, eta: Optional[EtaService
             provider = HaversineProvider()
     if store == "default":
         store = open_store(s.store_url, s.supabase_url, s.supabase_service_key)
+    # compact route records (native route service) are rebuilt against the provider's road graph
+    steps = getattr(provider, "_steps", None)
+    if steps is not None and hasattr(store, "set_record_graph"):
+        store.set_record_graph(steps)
     broker = make_broker(s.broker, s.redis_url)
     sim = Simulator(broker, s.sim_tick_min_s, s.sim_tick_max_s, s.max_simulations, s.sse_delta)
     # cross-request optimizer batching (routing/route_batcher.py): one worker per GPU

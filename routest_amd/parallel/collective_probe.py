@@ -12,7 +12,7 @@ all_gather busbw = algbw * (n-1)/n.
 from __future__ import annotations
 
 import time
-from typing import Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -22,29 +22,35 @@ import torch.distributed as dist
 DEFAULT_SIZES = (296_000, 4_300_000, 25_600_000, 64 << 20, 256 << 20)
 
 
-def _time(fn, iters: int, warm: int = 3) -> float:
+def _time(fn, iters: int, warm: int = 3, device: Optional[torch.device] = None) -> float:
+    cuda = device is None or device.type == "cuda"
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
     for _ in range(warm):
         fn()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(iters):
         fn()
-    torch.cuda.synchronize()
+    sync()
     dt = (time.perf_counter() - t0) / iters
-    t = torch.tensor([dt], dtype=torch.float64, device=torch.cuda.current_device())
+    t = torch.tensor([dt], dtype=torch.float64, device=torch.cuda.current_device() if cuda else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def sweep(device: torch.device, sizes: Sequence[int] = DEFAULT_SIZES,
-          native: Optional[object] = None) -> List[Dict]:
+          native: Optional[object] = None, checkpoint: Optional[Callable[[], None]] = None) -> List[Dict]:
     """All ranks call this together with the same arguments; every decision below depends on
     those arguments only (never on local timing), so no rank can leave the others waiting in a
-    collective.  Returns the same rows on every rank (times are the max over ranks)."""
+    collective.  Returns the same rows on every rank (times are the max over ranks).
+    ``checkpoint`` (bench.py's SectionGuard) runs before each size's collectives, so a rank that
+    failed is noticed by its peers before they enter the next all-reduce it will never reach."""
     n = dist.get_world_size()
     rows: List[Dict] = []
     for nbytes in sizes:
+        if checkpoint is not None:
+            checkpoint()
         iters = 20 if nbytes <= (4 << 20) else 5
         numel = (nbytes // 4 + 3) // 4 * 4
         x = torch.ones(numel, device=device)
@@ -56,7 +62,7 @@ def sweep(device: torch.device, sizes: Sequence[int] = DEFAULT_SIZES,
         if native is not None and getattr(native, "oneshot", False) and nbytes <= getattr(native, "oneshot_bytes", 0):
             cases.append(("all_reduce_oneshot", lambda: native.all_reduce(x, "oneshot"), 2 * (n - 1) / n))
         for op, fn, factor in cases:
-            dt = _time(fn, iters)
+            dt = _time(fn, iters, device=device)
             moved = nbytes if op != "all_gather" else per * n * 4
             algbw = moved / dt / 1e9
             rows.append({"op": op, "bytes": moved, "us": round(dt * 1e6, 2),

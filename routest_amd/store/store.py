@@ -12,12 +12,15 @@ driver_age}``, ``route_results.{geometry, eta_minutes_ml, eta_completion_time_ml
   rejects — Appendix B #5), results cascade-delete with their request.
 * :class:`PostgRESTStore`: the reference's exact REST calls for a Supabase deployment.
 
-Large route texts (a result's ``legs`` and ``geometry``, ~30-100 KB of GeoJSON per route) written by
-the native route service go to an append-only side file ``<db>.blobs`` and the row holds a
-reference (``BLOB_REF`` + ``offset:length``); SQLite's single writer then commits ~300-byte rows
-instead of pushing every route through its WAL (csrc/route_service.hip).  Readers — this class and
-the native history reader (csrc/runtime/history_db.h) — resolve a reference to the same bytes.
-Deleting a request does not reclaim its bytes in the side file.
+A road-graph route persisted by the native route service does not store its formatted legs and
+geometry (~30-100 KB of GeoJSON per route): ``legs`` holds a compact route record (a BLOB starting
+``RECORD_MAGIC``: waypoints, per-hop adjacency slots, per-step durations; ~1-3 KB,
+csrc/runtime/route_record.h) and ``geometry`` is NULL.  Readers — this class through the graph
+provider's ``_rt.GraphSteps.decode_record`` (:meth:`SQLiteStore.set_record_graph`) and the native
+history reader (csrc/runtime/history_db.h) — rebuild the texts with the route service's own
+formatter, byte-identical to what it answered.  Rows of earlier rounds may instead hold a reference
+(``BLOB_REF`` + ``offset:length``) into the append-only side file ``<db>.blobs``; both readers still
+resolve those.
 """
 from __future__ import annotations
 
@@ -74,8 +77,11 @@ class StoreUnavailable(RuntimeError):
     pass
 
 
-#: prefix of a column value stored in the side file (never the first byte of JSON text)
+#: prefix of a column value stored in the side file (never the first byte of JSON text); rows of
+#: rounds before the compact records still carry it
 BLOB_REF = "\x01blob:"
+#: first bytes of a compact route record (csrc/runtime/route_record.h), stored as a BLOB in `legs`
+RECORD_MAGIC = b"\x02RR1"
 
 
 _EPHEMERAL: List[str] = []
@@ -156,6 +162,7 @@ class SQLiteStore:
         self.path = path
         self.blob_path = path + ".blobs"
         self._blob_fd: Optional[int] = None
+        self._record_graph: Any = None
         self._lock = threading.Lock()
         self._db = sqlite3.connect(path, check_same_thread=False, isolation_level=None, timeout=10.0)
         self._db.row_factory = sqlite3.Row
@@ -262,14 +269,33 @@ class SQLiteStore:
             raise StoreUnavailable(f"route side file {self.blob_path} is short at {off}+{n}")
         return b.decode("utf-8")
 
+    def set_record_graph(self, steps: Any) -> None:
+        """The road graph (``_rt.GraphSteps`` of the GraphProvider) that compact route records are
+        rebuilt against (csrc/runtime/route_record.h)."""
+        self._record_graph = steps
+
+    def _decode_record(self, rec: bytes):
+        g = self._record_graph
+        if g is None:
+            raise StoreUnavailable("a compact route record needs the road graph it was routed on "
+                                   "(serve with the same graph provider)")
+        try:
+            return g.decode_record(rec)
+        except ValueError as e:
+            raise StoreUnavailable(f"route record: {e}") from None
+
     def _res_dict(self, r: sqlite3.Row, full: bool) -> Dict[str, Any]:
         d = dict(r)
         d["optimized_order"] = json.loads(d["optimized_order"]) if d.get("optimized_order") else []
         legs = d.pop("legs", None)
         geom = d.pop("geometry", None)
         d.pop("request_id", None)
-        if full:
+        if full and isinstance(legs, (bytes, bytearray, memoryview)) and bytes(legs[:4]) == RECORD_MAGIC:
+            # a compact record of the native route service: legs and geometry rebuilt by its formatter
+            legs, geom = self._decode_record(bytes(legs))
+        elif full:
             legs, geom = self._text(legs), self._text(geom)
+        if full:
             d["legs"] = json.loads(legs) if legs else []
             d["geometry"] = json.loads(geom) if geom else None
         return d

@@ -108,6 +108,8 @@ def problems(d: Dict[str, Any]) -> List[str]:
         for k in ("http", "http_f02"):
             if k in r:
                 out += _missing(r[k], ROUTE_HTTP, f"route_optimizer.{k}")
+    if d.get("serving_error"):
+        out.append(f"serving: error {str(d['serving_error'])[:120]}")
     coll = d.get("collectives")
     if isinstance(coll, list) and coll and isinstance(coll[0], dict) and "error" in coll[0]:
         out.append(f"collectives: error {str(coll[0]['error'])[:120]}")

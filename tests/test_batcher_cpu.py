@@ -140,12 +140,16 @@ def test_two_consumers_never_strand_requests():
 
     from routest_amd.data.synth import synth_records
 
+    import threading
+    lock = threading.Lock()
+
     class Slow:
         rows = 0
 
         def __call__(self, rec):
             time.sleep(0.0002)
-            Slow.rows += len(rec)
+            with lock:                      # (two workers: a bare += can lose an update)
+                Slow.rows += len(rec)
             return np.arange(len(rec), dtype=np.float32)
 
     rec, _ = synth_records(6000, 1)

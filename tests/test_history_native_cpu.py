@@ -103,3 +103,68 @@ def test_side_file_references_resolve_identically(app_and_db):
         assert app.status_code == 200 and app.content == ref
         assert db.detail(rid) == (200, ref)
     assert db.history("100")[1] == c.get("/api/history?limit=100").content
+
+
+def test_compact_route_records_read_back_identically(tmp_path):
+    """the native route service persists a graph route as a compact record (a
+    BLOB in route_results.legs, geometry NULL; csrc/runtime/route_record.h).  The app (through the
+    provider's GraphSteps) and the native history reader rebuild history detail byte-identically to
+    the same route stored as text — and a reader without the graph relays / refuses instead of
+    answering something else."""
+    import json
+    import sqlite3
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider
+    from routest_amd.routing.greedy import InfeasibleStops, greedy_trips
+    from routest_amd.store.store import RECORD_MAGIC, SQLiteStore, StoreUnavailable
+    g = synth_road_graph(3000, seed=1)
+    prov = GraphProvider(g, (g.length_m / 9.0).astype(np.float32), device=None)
+    store = SQLiteStore(str(tmp_path / "r.db"))
+    store.set_record_graph(prov._steps)
+    rng = np.random.default_rng(7)
+    recs = {}
+    for i in range(40):
+        k = int(rng.integers(1, 8))
+        pts = [{"lat": 14.57 + rng.normal(0, 0.05), "lon": 121.02 + rng.normal(0, 0.05), "payload": 1}
+               for _ in range(k + 1)]
+        p = {"source_point": pts[0], "destination_points": pts[1:],
+             "driver_details": {"driver_name": f"d{i}", "vehicle_type": "car", "vehicle_capacity": 99,
+                                "maximum_distance": 1e7, "driver_age": 30 + i},
+             "meta": {"origin_id": f"o{i}", "destination_ids": [f"x{j}" for j in range(k)]}, "use_ml_eta": False}
+        trips = None
+        if k > 1:
+            try:
+                trips = greedy_trips(np.asarray(prov.matrix(pts, "driving-car")).tolist(), [0.0] + [1.0] * k, 99.0, 1e7)
+            except InfeasibleStops:
+                continue
+        calls = [[pts[0], pts[1]]] if trips is None else [[pts[j] for j in t] for t in trips]
+        nodes = np.concatenate([g.nearest_nodes([q["lat"] for q in c], [q["lon"] for q in c]) for c in calls])
+        pairs, o = set(), 0
+        for c in calls:
+            pairs.update((int(nodes[o + j]), int(nodes[o + j + 1])) for j in range(len(c) - 1))
+            o += len(c)
+        legs = dict(zip(sorted(pairs), prov.legs(sorted(pairs))[0]))
+        st, resp, rec, seg, geo = rt.route_assemble_graph(json.dumps(p).encode(), "backend:mi355x", g.lat, g.lon,
+                                                          nodes.astype(np.int32), trips,
+                                                          {kk: tuple(v) for kk, v in legs.items()}, prov._steps,
+                                                          prov.cost, with_record=True)
+        assert st == 200 and rec is not None and rec[:4] == RECORD_MAGIC
+        rid = store.persist_request_and_result(p, json.loads(resp))
+        recs[rid] = rec
+    assert len(recs) > 25
+    native = rt.HistoryDb(store.sqlite_uri, graph=prov._steps)
+    text_detail = {rid: native.detail(rid) for rid in recs}
+    app_text = {rid: json.dumps(store.history_detail(rid)) for rid in recs}
+    con = sqlite3.connect(store.sqlite_uri, isolation_level=None)
+    for rid, rec in recs.items():
+        con.execute("UPDATE route_results SET legs=?, geometry=NULL WHERE request_id=?", (rec, rid))
+    con.close()
+    for rid in recs:
+        assert native.detail(rid) == text_detail[rid]
+        assert json.dumps(store.history_detail(rid)) == app_text[rid]
+    # no graph: the native reader relays to the app, which refuses rather than answering wrongly
+    assert rt.HistoryDb(store.sqlite_uri).detail(next(iter(recs))) is None
+    store.set_record_graph(None)
+    with pytest.raises(StoreUnavailable):
+        store.history_detail(next(iter(recs)))
+    store.close()

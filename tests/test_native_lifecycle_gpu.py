@@ -197,3 +197,26 @@ def test_hung_gpu_slot_watchdog_and_route_failover():
     # (a rehearsal artefact, not asserted: both slots share ONE device here, and the other slot's
     # route service can stall behind the hung one in the driver for ~the hang's duration — its
     # jobs then go to the app; on a node the other slot is another GPU)
+
+
+def test_route_failover_is_bounded_when_every_service_fails():
+    """a flush failure that repeats on every GPU's route service (not a timeout)
+    must not bounce its jobs between the services forever.  ROUTEST_FAULT=route_fail makes every
+    flush fail; each job is handed to the other slot's service at most once (2 slots: n-1 = 1 hop)
+    and then relayed to the app, which answers it."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ROUTEST_FAULT="route_fail", ROUTEST_PERSIST_IDLE_MS="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "_watchdog_child.py"), "route_fail"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    print(json.dumps(d))
+    assert d["routes_on"] and d["route_codes"] == [200] and d["codes"] == [200], d
+    # every route request answered by the app after at most one hop each
+    assert d["route_service_fallbacks"] == d["n_routes"], d
+    assert d["route_failed_over"] <= d["n_routes"], d
+    assert d["max_route_s"] < 5.0, d
+    assert not d["slot0"]["quarantined"] and not d["slot1"]["quarantined"], d

@@ -155,6 +155,70 @@ def test_graph_assembly_byte_identical():
     assert checked > 80
 
 
+def test_compact_route_record_rebuilds_byte_identical():
+    """csrc/runtime/route_record.h: the record the route service persists for a
+    graph route — waypoints, per-hop adjacency slots, seconds / metres per leg, step durations in
+    tenths — decodes, against the same graph, to exactly the legs and geometry texts the assembly
+    wrote; it is a small fraction of their size; another graph is refused."""
+    from routest_amd.data.graph import synth_road_graph
+    from routest_amd.routing.graph import GraphProvider
+    from routest_amd.routing.greedy import InfeasibleStops, greedy_trips
+    g = synth_road_graph(3000, seed=1)
+    cost = (g.length_m / 9.0).astype(np.float32)
+    prov = GraphProvider(g, cost, device=None)
+    other = GraphProvider(synth_road_graph(3000, seed=2), cost, device=None)
+    checked, rec_bytes, text_bytes = 0, 0, 0
+    for it, p in enumerate(_payloads(300, seed=5, center=(14.57, 121.02), spread=0.08)):
+        body = json.dumps(p).encode()
+        r = json.loads(body)
+        pts = [r.get("source_point")] + list(r.get("destination_points") or [])
+        if not (isinstance(r.get("source_point"), dict) and "lon" in r["source_point"] and
+                isinstance(r.get("destination_points"), list) and r["destination_points"]):
+            continue
+        if not all(isinstance(q, dict) and isinstance(q.get("lat"), (int, float)) and
+                   isinstance(q.get("lon"), (int, float)) for q in pts):
+            continue
+        trips = None
+        if len(pts) > 2:
+            d = prov.matrix(pts, "driving-car")
+            drv = r.get("driver_details") or {}
+            try:
+                trips = greedy_trips(np.asarray(d).tolist(), [0.0] + [float(q.get("payload", 0)) for q in pts[1:]],
+                                     float(drv.get("vehicle_capacity", 9e12)), float(drv.get("maximum_distance", 9e12)))
+            except (InfeasibleStops, TypeError, ValueError):
+                continue
+        calls = [[pts[0], pts[1]]] if trips is None else [[pts[i] for i in t] for t in trips]
+        nodes = np.concatenate([g.nearest_nodes([q["lat"] for q in c], [q["lon"] for q in c]) for c in calls])
+        pairs, o = set(), 0
+        for c in calls:
+            pairs.update((int(nodes[o + i]), int(nodes[o + i + 1])) for i in range(len(c) - 1))
+            o += len(c)
+        legs = dict(zip(sorted(pairs), prov.legs(sorted(pairs))[0]))
+        for with_steps in (True, False):
+            got = rt.route_assemble_graph(body, "backend:mi355x", g.lat, g.lon, nodes.astype(np.int32), trips,
+                                          {k: tuple(v) for k, v in legs.items()}, prov._steps,
+                                          prov.cost if with_steps else None, with_record=True)
+            if got is None or got[0] != 200:
+                break
+            st, resp, rec, seg, geo = got
+            assert rec is not None, it
+            assert prov._steps.decode_record(rec) == (seg, geo), it
+            resp_j = json.loads(resp)
+            assert json.loads(seg) == resp_j["properties"]["segments"]
+            assert json.loads(geo) == resp_j["geometry"]
+            if with_steps:
+                rec_bytes += len(rec)
+                text_bytes += len(seg) + len(geo)
+                checked += 1
+                with pytest.raises(ValueError, match="another road graph"):
+                    other._steps.decode_record(rec)
+                with pytest.raises(ValueError):
+                    prov._steps.decode_record(rec[:-3])
+    assert checked > 80
+    print(f"record {rec_bytes / checked:.0f} B vs text {text_bytes / checked:.0f} B per route")
+    assert rec_bytes * 6 < text_bytes, (rec_bytes, text_bytes)
+
+
 def test_float_fast_paths_match_python():
     """py_round(x, 1) and the JSON float writer take integer-tenths fast paths (route steps): every
     result equals Python's round() / json.dumps, midpoints and large magnitudes included."""
