@@ -612,9 +612,32 @@ void wgrad_dual(torch::Tensor A0, int64_t M0, torch::Tensor B0, int64_t N0, torc
                                      (int)ldo1, (long long)slab1.size(1), (int)N1, cur_stream(A0)));
 }
 
+// dW2|db2 of the wide trainer on 256 x 256 output tiles (wgrad.hip wgrad256_kernel): A [K, >= M], B [K, >= N]
+// bf16 row-major, slab f32 [S, >= M * ldo]; db2_col >= 0 also writes the column sums of A per tile column
+void wgrad256(torch::Tensor A, torch::Tensor B, int64_t M, int64_t N, torch::Tensor slab, int64_t ldo, int64_t db2_col) {
+  check_dev(A, "A");
+  check_dev(B, "B");
+  check_dev(slab, "slab");
+  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "bf16 A/B");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(0) == B.size(0) && A.is_contiguous() && B.is_contiguous(),
+              "A/B must be contiguous [K, *]");
+  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && M <= A.size(1) && N <= B.size(1) && A.size(0) % 64 == 0 &&
+                  A.size(1) % 8 == 0 && B.size(1) % 8 == 0,
+              "wgrad256: M, N multiples of 256 within the operands, K a multiple of 64");
+  TORCH_CHECK(slab.scalar_type() == torch::kFloat32 && slab.dim() == 2 && slab.is_contiguous() &&
+                  (M - 1) * ldo + std::max<int64_t>(N, db2_col >= 0 ? db2_col + N / 256 : 0) <= slab.size(1) &&
+                  ldo >= N,
+              "slab must be f32 [S, >= M * ldo]");
+  TORCH_CHECK(db2_col < 0 || (db2_col >= N && db2_col + N / 256 <= ldo), "db2 columns must lie beside the output");
+  const c10::DeviceGuard guard(A.device());
+  RT_CHECK_HIP(rt::launch_wgrad256(A.data_ptr(), (int)A.size(1), B.data_ptr(), (int)B.size(1), (int)M, (int)N,
+                                   (int)A.size(0), (int)slab.size(0), slab.data_ptr<float>(), (int)ldo,
+                                   (long long)slab.size(1), (int)db2_col, cur_stream(A)));
+}
+
 void wgrad_reduce(torch::Tensor slab, torch::Tensor G, c10::optional<torch::Tensor> slab1,
                   c10::optional<torch::Tensor> G1, c10::optional<torch::Tensor> slab2,
-                  c10::optional<torch::Tensor> G2, int64_t perm_h) {
+                  c10::optional<torch::Tensor> G2, int64_t perm_h, int64_t fold_ld, int64_t fold_col) {
   auto chk = [&](const torch::Tensor& sl, const torch::Tensor& g) {
     check_dev(sl, "slab");
     check_dev(g, "G");
@@ -638,7 +661,7 @@ void wgrad_reduce(torch::Tensor slab, torch::Tensor G, c10::optional<torch::Tens
       two ? G1->data_ptr<float>() : nullptr, two ? (int)G1->numel() : 0,
       three ? slab2->data_ptr<float>() : nullptr, three ? (int)slab2->size(0) : 0,
       three ? (long long)slab2->size(1) : 0, three ? G2->data_ptr<float>() : nullptr,
-      three ? (int)G2->numel() : 0, (int)perm_h));
+      three ? (int)G2->numel() : 0, (int)perm_h, (int)fold_ld, (int)fold_col));
 }
 
 void check_csr(const torch::Tensor& indptr, const torch::Tensor& indices, const torch::Tensor& values) {
@@ -1349,7 +1372,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_dual", &wgrad_dual, "two split-K weight-gradient GEMMs (dW2|db2 and dW1) in one launch");
   m.def("wgrad_reduce", &wgrad_reduce, "deterministic sum of wgrad slabs (optionally a second and third region)",
         py::arg("slab"), py::arg("G"), py::arg("slab1") = py::none(), py::arg("G1") = py::none(),
-        py::arg("slab2") = py::none(), py::arg("G2") = py::none(), py::arg("perm_h") = 0);
+        py::arg("slab2") = py::none(), py::arg("G2") = py::none(), py::arg("perm_h") = 0, py::arg("fold_ld") = 0,
+        py::arg("fold_col") = 0);
+  m.def("wgrad256", &wgrad256, "dW2-shaped weight gradient on 256x256 output tiles, split-K over the slab's rows",
+        py::arg("A"), py::arg("B"), py::arg("M"), py::arg("N"), py::arg("slab"), py::arg("ldo"), py::arg("db2_col") = -1);
   m.def("train_fwd_grid", [](int64_t B, int64_t dev) { return (int64_t)rt::train_fwd_grid((int)B, num_cus((int)dev)); },
         "workgroups of the training forward = rows of its dW3 slab");
   m.def("num_cus", [](int64_t dev) { return (int64_t)num_cus((int)dev); });

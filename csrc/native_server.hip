@@ -125,6 +125,7 @@ struct Shared {
   int quarantine_after = 3;
   long long probe_ms = 30000;
   double deadline_ms = 500.0;          // ROUTEST_GPU_DEADLINE_MS: a round not done by then is abandoned
+  double trace_ms = -1.0;              // ROUTEST_ROUTE_TRACE_MS: log slow / missed rounds (watchdog rehearsal)
   int* hang_release = nullptr;         // pinned host flag of the gpu_hang fault hook (1 = release)
   int* hang_release_d = nullptr;
   // the model each resident scorer was created on: its blob stays allocated while the scorer lives
@@ -1198,7 +1199,15 @@ class Reactor {
     const bool w8 = m.takes_wire8() && rtc::pack_wire8(h_rec_, nrec_, h_rec8_);
     if (w8) st_.wire8.fetch_add(1, std::memory_order_relaxed);
     hipError_t e = m.predict(w8 ? d_rec8_ : d_rec_, w8 ? 8 : 16, d_out_, (int)nrec_, st, ws_[skey]);
+    const auto tw = std::chrono::steady_clock::now();
     if (e == hipSuccess) e = wait_deadline(st, ev, sh.deadline_ms);
+    if (sh.trace_ms >= 0) {
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
+      if (ms > sh.trace_ms || e == hipErrorLaunchTimeOut)
+        std::fprintf(stderr, "[predict slot %d on slot %d t=%.3f] %s %.1f ms (%zu rows)\n", cfg_.slot, g,
+                     std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(),
+                     e == hipErrorLaunchTimeOut ? "DEADLINE after" : "wait", ms, nrec_);
+    }
     if (e == hipErrorLaunchTimeOut) {
       sh.timed_out(g);
       st_.timeouts.fetch_add(1, std::memory_order_relaxed);
@@ -1400,6 +1409,7 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
     sh.scorer_mus.push_back(std::make_unique<std::mutex>());
   }
   if (const char* v = std::getenv("ROUTEST_GPU_DEADLINE_MS")) sh.deadline_ms = std::atof(v);
+  if (const char* v = std::getenv("ROUTEST_ROUTE_TRACE_MS")) sh.trace_ms = std::atof(v);
   if (hipHostMalloc((void**)&sh.hang_release, sizeof(int), hipHostMallocMapped | hipHostMallocPortable) == hipSuccess) {
     *(volatile int*)sh.hang_release = 1;
     if (hipHostGetDevicePointer((void**)&sh.hang_release_d, sh.hang_release, 0) != hipSuccess) sh.hang_release_d = nullptr;
@@ -1470,6 +1480,7 @@ int64_t native_server_start(int port, int threads, const std::vector<int>& devic
     // watchdog: a flush past the deadline quarantines this GPU and its jobs go to the next GPU's
     // route service that is not itself broken
     rc.on_timeout = [shp, slot]() { shp->timed_out(slot); };
+    rc.slot = slot;
     rc.failover = [s, slot](RouteJob* j) {
       // (shared lock: the list is published once every service exists, and ~Server closes it
       // before the services are destroyed — a late failover then relays instead of submitting

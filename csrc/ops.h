@@ -86,7 +86,12 @@ hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, 
                                hipStream_t stream, const float* slab1 = nullptr, int S1 = 0,
                                long long slab_stride1 = 0, float* G1 = nullptr, int n1 = 0,
                                const float* slab2 = nullptr, int S2 = 0, long long slab_stride2 = 0,
-                               float* G2 = nullptr, int n2 = 0, int perm_h0 = 0);
+                               float* G2 = nullptr, int n2 = 0, int perm_h0 = 0, int fold_ld0 = 0,
+                               int fold_col0 = 0);
+// dW2-shaped weight gradient on 256 x 256 output tiles, split-K over S slices (wgrad.hip); db2_col >= 0:
+// column sums of A into slab columns db2_col .. db2_col + N/256 - 1 (fold them with wgrad_reduce)
+hipError_t launch_wgrad256(const void* A, int lda, const void* B, int ldb, int M, int N, int K, int S, float* slab,
+                           int ldo, long long slab_stride, int db2_col, hipStream_t stream);
 size_t wgrad_lds_bytes(int NT);
 // two independent wgrad GEMMs (segment 1: N <= 32) in one launch, same K
 hipError_t launch_wgrad_dual(const void* A0, int lda0, int M0, int Mout0, const void* B0, int ldb0,

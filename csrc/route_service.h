@@ -106,6 +106,7 @@ struct RouteServiceCfg {
   // history readers; unset: the service builds its own when the graph carries edge metres
   std::shared_ptr<const rrec::RecordGraph> record_graph;
   std::function<void()> on_timeout;       // the slot's GPU is quarantined for predictions too
+  int slot = -1;                          // the server's slot (traces: ROUTEST_ROUTE_TRACE_MS)
   std::function<bool()> hang_fault;       // ROUTEST_FAULT=gpu_hang@<slot> (the watchdog's test hook)
   const int* hang_release_d = nullptr;    // its device-visible release flag
 };

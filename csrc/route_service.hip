@@ -24,6 +24,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdarg>
+#include <cstdio>
 #include <cstring>
 #include <array>
 #include <atomic>
@@ -75,6 +77,53 @@ __global__ __launch_bounds__(64) void route_hang_kernel(const int* release, long
     __builtin_amdgcn_s_sleep(127);
 }
 
+// Queue-local copies: the flush's host <-> device transfers run as a small kernel on the flush's own
+// stream (mapped pinned host memory, read / written by the GPU over PCIe) instead of on the copy
+// engines.  The SDMA queues are shared by every stream of the process: a copy queued behind a
+// kernel that never finishes (a hung GPU slot; the watchdog rehearsal's gpu_hang hook) blocked the
+// OTHER slot's copies behind it for the hang's whole duration (r6 trace: the healthy slot's matrix
+// stage missed its 300 ms deadline waiting on its own tiny H2D copies).  On the compute queue a
+// flush's copies wait only for its own stream.  16-byte vector body, byte tail; 2-D for the depot rows.
+__global__ __launch_bounds__(256) void route_copy_kernel(unsigned char* __restrict__ dst,
+                                                         const unsigned char* __restrict__ src, size_t bytes) {
+  const size_t nv = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0 ? bytes / 16 : 0;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride)
+    reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(src)[i];
+  for (size_t i = nv * 16 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < bytes; i += stride) dst[i] = src[i];
+}
+__global__ __launch_bounds__(256) void route_copy2d_kernel(unsigned char* __restrict__ dst, size_t dpitch,
+                                                           const unsigned char* __restrict__ src, size_t spitch,
+                                                           size_t width, size_t height) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < width * height; i += stride) {
+    const size_t r = i / width, c = i - r * width;
+    dst[r * dpitch + c] = src[r * spitch + c];
+  }
+}
+std::atomic<bool>& qcopy_same_va() {
+  static std::atomic<bool> ok{true};
+  return ok;
+}
+hipError_t qcopy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  if (!qcopy_same_va().load(std::memory_order_relaxed)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s);
+  const size_t blocks = std::min<size_t>(1024, (bytes / 16 + 255) / 256 + 1);
+  hipLaunchKernelGGL(route_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (unsigned char*)dst,
+                     (const unsigned char*)src, bytes);
+  return hipGetLastError();
+}
+hipError_t qcopy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
+                   hipStream_t s) {
+  if (width == 0 || height == 0) return hipSuccess;
+  if (!qcopy_same_va().load(std::memory_order_relaxed))
+    return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDefault, s);
+  const size_t blocks = std::min<size_t>(1024, (width * height + 255) / 256);
+  hipLaunchKernelGGL(route_copy2d_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (unsigned char*)dst, dpitch,
+                     (const unsigned char*)src, spitch, width, height);
+  return hipGetLastError();
+}
+
 // Growable buffers of the service's flushes.  A buffer outgrown while serving is not freed at
 // once: hipFree / hipHostFree wait for the whole device, i.e. for every other service's and
 // reactor's kernels on this GPU (a hung one included) — it is kept until the service ends (the
@@ -110,8 +159,12 @@ struct HostBuf {
     if (h) old.push_back(h);
     h = nullptr;
     n = 0;
-    hipError_t e = hipHostMalloc((void**)&h, m * sizeof(T), hipHostMallocDefault);
-    if (e == hipSuccess) n = m;
+    hipError_t e = hipHostMalloc((void**)&h, m * sizeof(T), hipHostMallocMapped | hipHostMallocPortable);
+    if (e == hipSuccess) {
+      n = m;
+      void* dp = nullptr;      // the GPU sees it at the same address (qcopy); else copies take the DMA path
+      if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess || dp != (void*)h) qcopy_same_va().store(false);
+    }
     return e;
   }
   ~HostBuf() {
@@ -299,6 +352,7 @@ struct RouteService::Impl {
   DevBuf<float> d_msec, d_mmet, d_met;
   // host copies of metrics' edge costs (maneuver durations, exact host fallback): LRU by key
   std::mutex hc_mu;
+  HostBuf<float> h_hcost;                  // pinned staging of host_costs' copy
   std::list<std::pair<uint64_t, std::shared_ptr<const std::vector<float>>>> hc_lru;
   std::unordered_map<uint64_t, decltype(hc_lru)::iterator> hc_index;
   static constexpr size_t HC_MAX = 64;
@@ -320,15 +374,33 @@ struct RouteService::Impl {
   std::atomic<long long> n_failed_over{0};
   bool fail_fault = false;                 // ROUTEST_FAULT=route_fail (test hook)
 
-  hipError_t sync(hipStream_t s, hipEvent_t ev) {
+  // ROUTEST_ROUTE_TRACE_MS=<ms>: every wait on the GPU longer than that, every deadline, hand-off and
+  // recovery is logged to stderr with the slot and a steady-clock time stamp (the watchdog rehearsal's
+  // timeline: which wait of which slot stalled, and on what)
+  double trace_ms = -1.0;
+  void trace(const char* fmt, ...) __attribute__((format(printf, 2, 3))) {
+    if (trace_ms < 0) return;
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    std::fprintf(stderr, "[route slot %d t=%.3f] %s\n", cfg.slot,
+                 std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(), buf);
+  }
+  hipError_t sync(hipStream_t s, hipEvent_t ev, const char* what = "") {
     hipError_t e = hipEventRecord(ev, s);
     if (e != hipSuccess) return e;
     const auto t0 = std::chrono::steady_clock::now();
+    auto waited = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     for (int i = 0;; ++i) {
       e = hipEventQuery(ev);
-      if (e != hipErrorNotReady) return e;
-      if (deadline_ms > 0 && (i & 15) == 15 &&
-          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > deadline_ms) {
+      if (e != hipErrorNotReady) {
+        if (trace_ms >= 0 && waited() > trace_ms) trace("wait %s %.1f ms", what, waited());
+        return e;
+      }
+      if (deadline_ms > 0 && (i & 15) == 15 && waited() > deadline_ms) {
+        trace("DEADLINE in %s after %.1f ms", what, waited());
         if (!broken.exchange(true) && cfg.on_timeout) cfg.on_timeout();
         return hipErrorLaunchTimeOut;
       }
@@ -358,6 +430,7 @@ struct RouteService::Impl {
           n_failed_over.fetch_add(1, std::memory_order_relaxed);
           continue;
         }
+        trace("no other route service takes the job (hops %d): relayed to the app", j->hops);
       }
       if (!j->status) j->fallback = true;
       finish(j);
@@ -649,6 +722,7 @@ struct RouteService::Impl {
     }
     if (const char* v = std::getenv("ROUTEST_CCH_ASYNC")) async_ctx = std::string(v) != "0";
     if (const char* v = std::getenv("ROUTEST_ROUTE_DEADLINE_MS")) deadline_ms = std::atof(v);
+    if (const char* v = std::getenv("ROUTEST_ROUTE_TRACE_MS")) trace_ms = std::atof(v);
     // ROUTEST_FAULT=route_fail: every flush of every service fails (not a timeout) — the hop limit
     // of the failover must end each job at the app
     if (const char* v = std::getenv("ROUTEST_FAULT")) fail_fault = std::string(v).find("route_fail") != std::string::npos;
@@ -683,8 +757,10 @@ struct RouteService::Impl {
       }
       if (broken.load()) {
         if (drained()) {
+          trace("drained: serving again");
           broken.store(false);      // the late work finished: buffers and streams usable again
         } else {
+          trace("broken: handing %zu jobs off", b->jobs.size());
           hand_off(b->jobs);
           delete b;
           continue;
@@ -704,6 +780,7 @@ struct RouteService::Impl {
       stream = main_stream;         // (the hang stream is reused once drained: see drained())
       if (fail_fault && !b->jobs.empty()) b->failed = true;
       if (b->failed) {              // a GPU error or the deadline: another GPU's service answers
+        trace("flush of %zu jobs failed: handing off", b->jobs.size());
         hand_off(b->jobs);
         delete b;
         continue;
@@ -849,7 +926,7 @@ struct RouteService::Impl {
     }
     hipError_t e = hipSuccess;
     auto cp = [&](void* d, const void* h, size_t b) {
-      if (e == hipSuccess) e = hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = qcopy(d, h, b, stream);
     };
     cp(d_lat.d, h_lat.h, RN * 8);
     cp(d_lon.d, h_lon.h, RN * 8);
@@ -862,7 +939,7 @@ struct RouteService::Impl {
       e = launch_greedy_cvrp(d_D.d, d_npts.d, d_dem.d, d_cap.d, d_maxd.d, R, NM, d_visit.d, d_trip.d, d_ntrips.d,
                              d_status.d, stream);
     auto back = [&](void* h, const void* d, size_t b) {
-      if (e == hipSuccess) e = hipMemcpyAsync(h, d, b, hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = qcopy(h, d, b, stream);
     };
     back(h_visit.h, d_visit.d, RN * 4);
     back(h_trip.h, d_trip.d, RN * 4);
@@ -870,9 +947,8 @@ struct RouteService::Impl {
     back(h_status.h, d_status.d, (size_t)R * 4);
     // the depot row of every D (the infeasible-stop order key) — the matrices stay on the GPU
     if (e == hipSuccess)
-      e = hipMemcpy2DAsync(h_row0.h, (size_t)NM * 8, d_D.d, (size_t)NM * NM * 8, (size_t)NM * 8, (size_t)R,
-                           hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = sync(stream, ev_gpu);
+      e = qcopy2d(h_row0.h, (size_t)NM * 8, d_D.d, (size_t)NM * NM * 8, (size_t)NM * 8, (size_t)R, stream);
+    if (e == hipSuccess) e = sync(stream, ev_gpu, "k5k6-matrix");
     if (e != hipSuccess) return false;
     for (int k = 0; k < R; ++k) {
       rtr::Plan& p = m[k]->plan;
@@ -915,9 +991,11 @@ struct RouteService::Impl {
       }
     }
     auto v = std::make_shared<std::vector<float>>((size_t)cfg.cch->topo().E);
-    if (hipMemcpyAsync(v->data(), m->cost, v->size() * 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-        sync(stream, ev_gpu) != hipSuccess)
+    // (through the pinned staging buffer: the copy kernel writes device-visible host memory only)
+    if (h_hcost.need(v->size()) != hipSuccess || qcopy(h_hcost.h, m->cost, v->size() * 4, stream) != hipSuccess ||
+        sync(stream, ev_gpu, "host-costs") != hipSuccess)
       return nullptr;
+    std::memcpy(v->data(), h_hcost.h, v->size() * 4);
     std::lock_guard<std::mutex> lk(hc_mu);
     if (hc_index.count(m->key)) return v;
     hc_lru.emplace_front(m->key, v);
@@ -949,7 +1027,8 @@ struct RouteService::Impl {
                    d_mmet.need(RN * NM) || h_met.need(Q) || d_met.need(Q) || d_edge.need(Q * MP) ||
                    h_flat_e.need(Q * 256) || d_flat_e.need(Q * 256) || h_lr.need(Q) || h_li.need(Q) || h_lj.need(Q) ||
                    d_lr.need(Q) || d_li.need(Q) || d_lj.need(Q) || h_rowg.need(R) || d_rowg.need(R) ||
-                   h_lgrp.need(Q) || d_lgrp.need(Q) || h_mv.need(R) || d_mv.need(R));
+                   h_lgrp.need(Q) || d_lgrp.need(Q) || h_mv.need(R) || d_mv.need(R) ||
+                   h_hcost.need((size_t)cfg.cch->topo().E));
       const int S = cfg.cch->stride();
       msc.device = cfg.device;
       ok = ok && msc.ensure(RN * 2, std::max(Q, (RN * NM * 2 + CchGpu::MAX_ARCS - 1) / CchGpu::MAX_ARCS + 1), S,
@@ -1100,7 +1179,7 @@ struct RouteService::Impl {
     if (G > 0) {
       if (h_mv.need(G) || d_mv.need(G)) return false;
       for (size_t g = 0; g < G; ++g) h_mv.h[g] = CchGpu::view(*b.metrics[g]);
-      if (hipMemcpyAsync(d_mv.d, h_mv.h, G * sizeof(CchMView), hipMemcpyHostToDevice, stream) != hipSuccess) return false;
+      if (qcopy(d_mv.d, h_mv.h, G * sizeof(CchMView), stream) != hipSuccess) return false;
     }
     return true;
   }
@@ -1164,7 +1243,7 @@ struct RouteService::Impl {
     });
     hipError_t e = hipSuccess;
     auto cp = [&](void* d, const void* h, size_t bytes) {
-      if (e == hipSuccess) e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = qcopy(d, h, bytes, stream);
     };
     cp(d_pts.d, h_pts.h, RN * 4);
     cp(d_npts2.d, h_npts2.h, (size_t)R * 4);
@@ -1180,16 +1259,15 @@ struct RouteService::Impl {
       e = launch_greedy_cvrp(d_D.d, d_npts2.d, d_dem.d, d_cap.d, d_maxd.d, R, NM, d_visit.d, d_trip.d, d_ntrips.d,
                              d_status.d, stream);
     auto back = [&](void* h, const void* d, size_t bytes) {
-      if (e == hipSuccess) e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = qcopy(h, d, bytes, stream);
     };
     back(h_visit.h, d_visit.d, RN * 4);
     back(h_trip.h, d_trip.d, RN * 4);
     back(h_ntrips.h, d_ntrips.d, (size_t)R * 4);
     back(h_status.h, d_status.d, (size_t)R * 4);
     if (e == hipSuccess)
-      e = hipMemcpy2DAsync(h_row0.h, (size_t)NM * 8, d_D.d, (size_t)NM * NM * 8, (size_t)NM * 8, (size_t)R,
-                           hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = sync(stream, ev_gpu);
+      e = qcopy2d(h_row0.h, (size_t)NM * 8, d_D.d, (size_t)NM * NM * 8, (size_t)NM * 8, (size_t)R, stream);
+    if (e == hipSuccess) e = sync(stream, ev_gpu, "cch-matrix+greedy");
     if (e != hipSuccess) return false;
     for (int k = 0; k < R; ++k) unpack_plan(m[k], h_npts2.h[k], NM, k);
     return true;
@@ -1342,13 +1420,13 @@ struct RouteService::Impl {
         }
       }
     }
-    hipError_t e = hipMemcpyAsync(d_src.d, h_src.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_dst.d, h_dst.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_lgrp.d, h_lgrp.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
+    hipError_t e = qcopy(d_src.d, h_src.h, (size_t)Q * 4, stream);
+    if (e == hipSuccess) e = qcopy(d_dst.d, h_dst.h, (size_t)Q * 4, stream);
+    if (e == hipSuccess) e = qcopy(d_lgrp.d, h_lgrp.h, (size_t)Q * 4, stream);
     if (QA > 0) {
-      if (e == hipSuccess) e = hipMemcpyAsync(d_lr.d, h_lr.h, (size_t)QA * 4, hipMemcpyHostToDevice, stream);
-      if (e == hipSuccess) e = hipMemcpyAsync(d_li.d, h_li.h, (size_t)QA * 4, hipMemcpyHostToDevice, stream);
-      if (e == hipSuccess) e = hipMemcpyAsync(d_lj.d, h_lj.h, (size_t)QA * 4, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = qcopy(d_lr.d, h_lr.h, (size_t)QA * 4, stream);
+      if (e == hipSuccess) e = qcopy(d_li.d, h_li.h, (size_t)QA * 4, stream);
+      if (e == hipSuccess) e = qcopy(d_lj.d, h_lj.h, (size_t)QA * 4, stream);
     }
     auto out_at = [&](int q) {
       CchRouteOut o;
@@ -1367,11 +1445,11 @@ struct RouteService::Impl {
     if (e == hipSuccess && QR > 0)
       e = cfg.cch->route_multi(d_mv.d, d_lgrp.d + QA, d_src.d + QA, d_dst.d + QA, QR, out_at(QA), csc, stream);
     n_legs_reused.fetch_add(QA, std::memory_order_relaxed);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_len.h, d_len.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_cost.h, d_cost.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_met.h, d_met.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = sync(stream, ev_gpu);
+    if (e == hipSuccess) e = qcopy(h_st.h, d_st.d, (size_t)Q * 4, stream);
+    if (e == hipSuccess) e = qcopy(h_len.h, d_len.d, (size_t)Q * 4, stream);
+    if (e == hipSuccess) e = qcopy(h_cost.h, d_cost.d, (size_t)Q * 4, stream);
+    if (e == hipSuccess) e = qcopy(h_met.h, d_met.d, (size_t)Q * 4, stream);
+    if (e == hipSuccess) e = sync(stream, ev_gpu, "cch-legs");
     add_t(3, t0);
     t0 = now_us();
     if (e != hipSuccess) return false;
@@ -1382,7 +1460,7 @@ struct RouteService::Impl {
     }
     if (total > 0) {
       if (h_flat.need((size_t)total) || d_flat.need((size_t)total)) return false;
-      e = hipMemcpyAsync(d_off.d, h_off.h, (size_t)Q * 8, hipMemcpyHostToDevice, stream);
+      e = qcopy(d_off.d, h_off.h, (size_t)Q * 8, stream);
       if (e == hipSuccess) {
         hipLaunchKernelGGL(compact_paths_kernel, dim3(Q), dim3(256), 0, stream, d_path.d, MP, d_len.d, d_st.d, d_off.d,
                            Q, d_flat.d);
@@ -1395,9 +1473,9 @@ struct RouteService::Impl {
                            Q, d_flat_e.d);
         e = hipGetLastError();
       }
-      if (e == hipSuccess) e = hipMemcpyAsync(h_flat.h, d_flat.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
-      if (e == hipSuccess) e = hipMemcpyAsync(h_flat_e.h, d_flat_e.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
-      if (e == hipSuccess) e = sync(stream, ev_gpu);
+      if (e == hipSuccess) e = qcopy(h_flat.h, d_flat.d, (size_t)total * 4, stream);
+      if (e == hipSuccess) e = qcopy(h_flat_e.h, d_flat_e.d, (size_t)total * 4, stream);
+      if (e == hipSuccess) e = sync(stream, ev_gpu, "cch-paths");
       if (e != hipSuccess) return false;
       b.flat.assign(h_flat.h, h_flat.h + total);
       b.flat_e.assign(h_flat_e.h, h_flat_e.h + total);
@@ -1484,8 +1562,8 @@ struct RouteService::Impl {
       h_src.h[i] = pairs[i].first;
       h_dst.h[i] = pairs[i].second;
     }
-    hipError_t e = hipMemcpyAsync(d_src.d, h_src.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_dst.d, h_dst.h, (size_t)Q * 4, hipMemcpyHostToDevice, stream);
+    hipError_t e = qcopy(d_src.d, h_src.h, (size_t)Q * 4, stream);
+    if (e == hipSuccess) e = qcopy(d_dst.d, h_dst.h, (size_t)Q * 4, stream);
     // the tiered search (csrc/astar.hip): interactive flushes (few thousand legs) skip the lane tier
     // (routing/graph.py BatchedAstar.run calls the same function)
     AstarGraphDev gd;
@@ -1517,13 +1595,13 @@ struct RouteService::Impl {
                        cfg.wave_ws.slots > 0 ? &cfg.wave_ws : nullptr, cfg.big_ws.slots > 0 ? &cfg.big_ws : nullptr,
                        ao, pl, d_qidx.d, stream, &rs, cfg.arena.base ? &cfg.arena : nullptr);
     n_escalated.fetch_add(rs.escalated, std::memory_order_relaxed);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_st.h, d_st.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = sync(stream, ev_gpu);
+    if (e == hipSuccess) e = qcopy(h_st.h, d_st.d, (size_t)Q * 4, stream);
+    if (e == hipSuccess) e = sync(stream, ev_gpu, "astar");
     add_t(3, t0);
     t0 = now_us();
-    if (e == hipSuccess) e = hipMemcpyAsync(h_len.h, d_len.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_cost.h, d_cost.d, (size_t)Q * 4, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = sync(stream, ev_gpu);
+    if (e == hipSuccess) e = qcopy(h_len.h, d_len.d, (size_t)Q * 4, stream);
+    if (e == hipSuccess) e = qcopy(h_cost.h, d_cost.d, (size_t)Q * 4, stream);
+    if (e == hipSuccess) e = sync(stream, ev_gpu, "astar-escalate");
     if (e != hipSuccess) return false;
     long long total = 0;
     for (int i = 0; i < Q; ++i) {
@@ -1532,14 +1610,14 @@ struct RouteService::Impl {
     }
     if (total > 0) {
       if (h_flat.need((size_t)total) || d_flat.need((size_t)total)) return false;
-      e = hipMemcpyAsync(d_off.d, h_off.h, (size_t)Q * 8, hipMemcpyHostToDevice, stream);
+      e = qcopy(d_off.d, h_off.h, (size_t)Q * 8, stream);
       if (e == hipSuccess) {
         hipLaunchKernelGGL(compact_paths_kernel, dim3(Q), dim3(256), 0, stream, d_path.d, MP, d_len.d, d_st.d, d_off.d,
                            Q, d_flat.d);
         e = hipGetLastError();
       }
-      if (e == hipSuccess) e = hipMemcpyAsync(h_flat.h, d_flat.d, (size_t)total * 4, hipMemcpyDeviceToHost, stream);
-      if (e == hipSuccess) e = sync(stream, ev_gpu);
+      if (e == hipSuccess) e = qcopy(h_flat.h, d_flat.d, (size_t)total * 4, stream);
+      if (e == hipSuccess) e = sync(stream, ev_gpu, "astar-paths");
       if (e != hipSuccess) return false;
       b.flat.assign(h_flat.h, h_flat.h + total);     // the next flush reuses the pinned buffer
     }
@@ -1760,10 +1838,10 @@ struct RouteService::Impl {
       r.traffic = j->req.eta_traffic;
       r.pad = 0;
     }
-    hipError_t e = hipMemcpyAsync(d_rec.d, h_rec.h, (size_t)n * 16, hipMemcpyHostToDevice, stream_asm);
+    hipError_t e = qcopy(d_rec.d, h_rec.h, (size_t)n * 16, stream_asm);
     if (e == hipSuccess) e = model->predict(d_rec.d, 16, d_eta.d, n, stream_asm, eta_ws);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_eta.h, d_eta.d, (size_t)n * 4, hipMemcpyDeviceToHost, stream_asm);
-    if (e == hipSuccess) e = sync(stream_asm, ev_asm);
+    if (e == hipSuccess) e = qcopy(h_eta.h, d_eta.d, (size_t)n * 4, stream_asm);
+    if (e == hipSuccess) e = sync(stream_asm, ev_asm, "eta");
     // a failed GPU round: the model's fp32 CPU forward (same fallback as the reactors), into a
     // buffer of its own (a round past the deadline may still write h_eta later)
     std::vector<float> cpu_eta;

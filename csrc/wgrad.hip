@@ -252,6 +252,8 @@ struct RedSeg {
   float* G;
   int S, n;
   int perm_h;        // 0: slab and G share a layout; H: train_bwd_kernel<H>'s register-native dW2 slabs
+  int fold_ld = 0;   // > 0: the float4 at column fold_col of every fold_ld-wide row holds partials of
+  int fold_col = 0;  // ONE value (wgrad256's db2 per tile column): stored as (x + y + z + w, 0, 0, 0)
 };
 
 __device__ __forceinline__ int red_hperm(int u) { return (u & ~12) | ((u & 4) << 1) | ((u & 8) >> 1); }
@@ -324,6 +326,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(RedSeg s0, RedSeg s1,
       const float4 v = part[k][c];
       r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
     }
+    if (sg.fold_ld > 0 && e % sg.fold_ld == sg.fold_col) r = make_float4(((r.x + r.y) + r.z) + r.w, 0.f, 0.f, 0.f);
     if (sg.perm_h > 0) {
       int g0, step;
       native_to_bucket(e, sg.perm_h, g0, step);
@@ -338,6 +341,215 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(RedSeg s0, RedSeg s1,
       for (int q = 0; q < 4 && e + q < n; ++q) G[e + q] = rr[q];
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// wgrad256_kernel: the wide trainer's dW2 = dz2^T h1a (M = N = H units, K = batch rows) on 256 x 256
+// OUTPUT-stationary tiles with split-K over the batch (wgrad_kernel<9> was 189 us at
+// 3.4x its MFMA floor, the step's largest kernel).  The tile, waves and MFMA of gemm256_kernel
+// (mlp_big.hip: 8 waves of 128 x 64 on mfma_f32_16x16x32_bf16, global_load_lds staging); both
+// operands are K-MAJOR here (a batch row is a row of dz2 / h1a), so the fragments come from the
+// row-major stage images through ds_read_b64_tr_b16 (T10: a 16-lane group reads 4 rows x 16 columns
+// and each lane receives one column's 4 rows):
+//  * both operands stream from HBM (unlike the forward GEMMs, whose weight tile sits in L2), so the
+//    K loop is a RING of four 32-deep stages (32 KB each) with three in flight: one barrier per
+//    stage, the loads of stage k + 3 issued right after it, counted vmcnt waits (2-stage 64-deep
+//    double buffering measured 190 us: each stage's loads outlived the stage's MFMAs);
+//  * stage image: 32 rows x 512 B per operand; row r's 16-byte chunk ch sits at slot
+//    ch ^ (sw(r) << 1), sw(r) = (r & 3) | ((r >> 3 & 1) << 2) — the 8 rows one 32-lane half of a
+//    transposed read touches (8g + q, 8g + 8 + q) hit 8 distinct 32-byte bank groups (bank of byte a:
+//    (a / 4) % 64; a 512-byte row alone maps every row onto the same banks: 8-way);
+//    global_load_lds writes lane-linearly, so each lane loads the GLOBAL chunk its slot holds;
+//  * grid = S k-slices x tiles; the tiles of one slice run on one XCD (they share the slice's dz2
+//    and h1a rows through that XCD's L2);
+//  * the fp32 partial of slice s goes to slab[s] ([M][ldo]); wgrad_reduce sums the slices in a fixed
+//    order (deterministic);
+//  * db2 (the ones column of h1a, i.e. column sums of dz2) rides along: tile column tn sums rows
+//    [32/tiles_n * tn, +32/tiles_n) of every stage of its A image (one ds_read_b128 per thread and
+//    row group) into slab column db2_col + tn; the reduce folds those tiles_n columns into db2_col.
+struct Wg256Args {
+  const __bf16* A;
+  const __bf16* B;
+  float* slab;
+  long long slab_stride;
+  int lda, ldb, ldo, M, N, K, kslice, tiles_m, tiles_n, S, db2_col;
+};
+constexpr int W256_KT = 32;                     // rows per stage
+constexpr int W256_TILE = W256_KT * 512;        // one operand's stage image (bytes)
+constexpr int W256_STAGE = 2 * W256_TILE;
+constexpr int W256_NST = 4;                     // ring depth (three stages in flight)
+
+__device__ __forceinline__ int w256_sw(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+// byte offset of columns col .. col + 3 (col % 4 == 0) of row r in a stage image
+__device__ __forceinline__ int w256_off(int r, int col) {
+  return r * 512 + (((col >> 3) ^ (w256_sw(r) << 1)) << 4) + (((col >> 2) & 1) << 3);
+}
+// the 16x16x32 operand fragment of columns c0 .. c0 + 15 and rows 0 .. 31: lane l gets column
+// c0 + (l & 15), rows 8 (l >> 4) .. + 7 (two transposed reads of 4 rows)
+__device__ __forceinline__ bf16x8 w256_frag(const unsigned char* img, int c0, int lane) {
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
+  const int r = 8 * g + q;
+  const lds_s16x4* a0 = (const lds_s16x4*)(img + w256_off(r, c0 + 4 * p));
+  const lds_s16x4* a1 = (const lds_s16x4*)(img + w256_off(r + 4, c0 + 4 * p));
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(a1));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ __launch_bounds__(512, 1) void wgrad256_kernel(Wg256Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smw[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int T = a.tiles_m * a.tiles_n;
+  int s, t;
+  {
+    const int bid = (int)blockIdx.x;
+    if (a.S % 8 == 0) {                    // XCD x (= bid % 8) runs slices x, x + 8, ...
+      const int loc = bid >> 3;
+      s = (bid & 7) + 8 * (loc / T);
+      t = loc % T;
+    } else {
+      s = bid / T;
+      t = bid % T;
+    }
+  }
+  const int tm = t / a.tiles_n, tn = t % a.tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int k_begin = s * a.kslice;
+  const int k_end = min(a.K, k_begin + a.kslice);
+  const int nk = k_end > k_begin ? (k_end - k_begin) / W256_KT : 0;
+  const int wu = w & 1, wr = w >> 1;       // units [128 wu, +128) x columns [64 wr, +64)
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // staging: instruction q (0, 1) of wave w fills LDS rows 2 (8q + w) + (lane >> 5), slot lane & 31
+  const __bf16* gA[2];
+  const __bf16* gB[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 2 * (8 * q + w) + (lane >> 5);
+    const int ch = (lane & 31) ^ (w256_sw(r) << 1);
+    gA[q] = a.A + (size_t)(k_begin + r) * a.lda + m0 + 8 * ch;
+    gB[q] = a.B + (size_t)(k_begin + r) * a.ldb + n0 + 8 * ch;
+  }
+  typedef __attribute__((address_space(3))) void lds_void;
+  auto issue = [&](int kt) {                // 4 loads per thread
+    unsigned char* img = smw + (kt & (W256_NST - 1)) * W256_STAGE;
+    const size_t ra = (size_t)W256_KT * kt * a.lda, rb = (size_t)W256_KT * kt * a.ldb;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      __builtin_amdgcn_global_load_lds((const void*)(gA[q] + ra), (lds_void*)(img + (8 * q + w) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gB[q] + rb), (lds_void*)(img + W256_TILE + (8 * q + w) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  // db2: this tile column's rows of each stage (rows_per = 32 / tiles_n), thread -> (row, 8 units)
+  const bool db2 = a.db2_col >= 0 && (a.tiles_n == 1 || a.tiles_n == 2 || a.tiles_n == 4);
+  const int rows_per = db2 ? W256_KT / a.tiles_n : 0;
+  float dsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int drow = tid >> 5, dch = tid & 31;
+
+  for (int kt = 0; kt < 3 && kt < nk; ++kt) issue(kt);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed (stages kt + 1, kt + 2 may stay in flight), then every wave is past stage
+    // kt - 1, whose buffer stage kt + 3 refills
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 3 < nk) issue(kt + 3);
+    const unsigned char* imgA = smw + (kt & (W256_NST - 1)) * W256_STAGE;
+    const unsigned char* imgB = imgA + W256_TILE;
+    bf16x8 fa[8], fb[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = w256_frag(imgA, 128 * wu + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = w256_frag(imgB, 64 * wr + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    if (db2) {
+      for (int rr = 0; rr < rows_per; rr += 16) {
+        if (rr + drow < rows_per) {
+          const int r = rows_per * tn + rr + drow;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(imgA + r * 512 + ((dch ^ (w256_sw(r) << 1)) << 4));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dsum[e] += (float)v[e];
+        }
+      }
+    }
+  }
+
+  // the slice's partial -> slab[s]: acc[i][j] element e = C[unit 128wu + 16i + 4g + e][col 64wr + 16j + fr]
+  float* out = a.slab + (long long)s * a.slab_stride;
+  const int fr = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float* row = out + (size_t)(m0 + 128 * wu + 16 * i + 4 * g + e) * a.ldo + n0 + 64 * wr + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) row[16 * j] = acc[i][j][e];
+    }
+  if (db2) {
+    // the 16 row slots of each unit: lanes l and l + 32 (rows 2w, 2w + 1), then the 8 waves via LDS
+    __syncthreads();                                     // every wave is done with the stages
+    float* red = reinterpret_cast<float*>(smw);          // [8 waves][256 units]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dsum[e] += __shfl_xor(dsum[e], 32);
+    if (lane < 32)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[w * 256 + 8 * dch + e] = dsum[e];
+    __syncthreads();
+    if (tid < 256) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v += red[q * 256 + tid];
+      out[(size_t)(m0 + tid) * a.ldo + a.db2_col + tn] = v;
+    }
+  }
+}
+
+hipError_t launch_wgrad256(const void* A, int lda, const void* B, int ldb, int M, int N, int K, int S, float* slab,
+                           int ldo, long long slab_stride, int db2_col, hipStream_t stream) {
+  if (M % 256 || N % 256 || K % W256_KT || lda % 8 || ldb % 8 || S < 1) return hipErrorInvalidValue;
+  Wg256Args a{};
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.slab = slab;
+  a.slab_stride = slab_stride;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldo = ldo;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.kslice = ((K + S - 1) / S + W256_KT - 1) / W256_KT * W256_KT;
+  a.tiles_m = M / 256;
+  a.tiles_n = N / 256;
+  a.S = S;
+  a.db2_col = db2_col;
+  if (db2_col >= 0 && (db2_col + a.tiles_n > ldo || (a.tiles_n != 1 && a.tiles_n != 2 && a.tiles_n != 4)))
+    return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)wgrad256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       W256_NST * W256_STAGE);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(wgrad256_kernel, dim3((unsigned)(S * a.tiles_m * a.tiles_n)), dim3(512), W256_NST * W256_STAGE,
+                     stream, a);
+  return hipGetLastError();
 }
 
 size_t wgrad_lds_bytes(int NT, int KB) {
@@ -475,9 +687,12 @@ hipError_t launch_wgrad_dual(const void* A0, int lda0, int M0, int Mout0, const 
 hipError_t launch_wgrad_reduce(const float* slab, int S, long long slab_stride, float* G, int n,
                                hipStream_t stream, const float* slab1, int S1,
                                long long slab_stride1, float* G1, int n1, const float* slab2, int S2,
-                               long long slab_stride2, float* G2, int n2, int perm_h0) {
+                               long long slab_stride2, float* G2, int n2, int perm_h0, int fold_ld0,
+                               int fold_col0) {
   if (perm_h0 > 0 && (perm_h0 % 64 || n != perm_h0 * (perm_h0 + 16))) return hipErrorInvalidValue;
-  const RedSeg s0{slab, slab_stride, G, S, n, perm_h0};
+  if (fold_ld0 > 0 && (fold_ld0 % 4 || fold_col0 % 4 || fold_col0 + 4 > fold_ld0 || perm_h0 > 0 || slab_stride % 4))
+    return hipErrorInvalidValue;
+  const RedSeg s0{slab, slab_stride, G, S, n, perm_h0, fold_ld0, fold_col0};
   const RedSeg s1{slab1, slab_stride1, G1, S1, slab1 ? n1 : 0, 0};
   const RedSeg s2{slab2, slab_stride2, G2, S2, slab2 ? n2 : 0, 0};
   const int nb0 = (n + 4 * RED_COLS - 1) / (4 * RED_COLS);

@@ -313,6 +313,14 @@ class RouteBatcher:
 
     def _worker(self, device, idx: int) -> None:
         import torch
+        # the flushes run on a stream of their own: a NON-blocking one, so this worker's launches and
+        # copies never queue behind the legacy null stream's implicit wait for every blocking stream
+        # on the device (a kernel hung on one — the watchdog rehearsal's fault streams are blocking —
+        # stalled every request relayed here for the hang's whole duration)
+        stream = None
+        if device is not None and getattr(device, "type", "") == "cuda":
+            with torch.cuda.device(device):
+                stream = torch.cuda.Stream(device)
         while True:
             first = self.q.get()
             if first is None:
@@ -324,8 +332,8 @@ class RouteBatcher:
                 batch.pop()
             t0 = time.perf_counter()
             try:
-                if device is not None and getattr(device, "type", "") == "cuda":
-                    with torch.cuda.device(device):
+                if stream is not None:
+                    with torch.cuda.device(device), torch.cuda.stream(stream):
                         res = self.plan_batch([b[0] for b in batch], device)
                 else:
                     res = self.plan_batch([b[0] for b in batch], device)

@@ -291,8 +291,19 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
         nt = -(-ntt // self.nsplit2)
         nblk = -(-ntt // nt)
         ncu = self.C.num_cus(d.index if d.index is not None else 0)
-        self.S2 = max(1, min(B // 256, ncu // (nblk * (H // 256))))
-        self.slab2 = torch.empty(self.S2, H * ldg, dtype=torch.float32, device=d)
+        # the 256 x 256 output-tile kernel (wgrad.hip wgrad256_kernel): (H/256)^2 tiles per k-slice and
+        # enough slices for one workgroup per CU; db2 rides along (ROUTEST_WGRAD256=0: the n-blocked
+        # wgrad_kernel)
+        import os
+        self.wg256 = (H % 256 == 0 and B % 64 == 0 and hasattr(self.C, "wgrad256") and
+                      os.environ.get("ROUTEST_WGRAD256", "1") != "0")
+        if self.wg256:
+            self.S2 = max(1, min(B // 64, ncu // ((H // 256) ** 2)))
+            # (zeros: the bucket's pad columns H+1 .. H+15 are never written by the kernel)
+            self.slab2 = torch.zeros(self.S2, H * ldg, dtype=torch.float32, device=d)
+        else:
+            self.S2 = max(1, min(B // 256, ncu // (nblk * (H // 256))))
+            self.slab2 = torch.empty(self.S2, H * ldg, dtype=torch.float32, device=d)
         # dW3|db3 and dW1 (small outputs): one k-slice per CU
         self.S = self._slices(B)
         self.slab = torch.empty(self.S, self.G.numel() - H * ldg, dtype=torch.float32, device=d)
@@ -316,11 +327,16 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
         C.big_dz2y(self.ypart, H // 64, self.b3v, tgt_norm, 2.0 / self.global_batch, self.dy,
                    self.dyb, self.sq_err, self.h2a, self.w3v, H, self.dz2, self.step_ctr, self.slab)
         C.gemm_nt(2, self.w2t, self.dz2, H, B, H, out=self.dh1)
-        # dW2|db2 = dz2^T [h1|1]: one launch, n-blocks of <= 288 columns in the grid
-        C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit2)
+        # dW2|db2 = dz2^T [h1|1]: 256 x 256 output tiles (db2 as per-tile-column partial sums folded by
+        # the reduce), or one launch of n-blocks of <= 288 columns
+        if self.wg256:
+            C.wgrad256(self.dz2, self.h1a, H, H, self.slab2, ldg, H)
+        else:
+            C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit2)
         # dW1 = (dh1 * relu'(h1))^T x: dh1 and its mask h1a are both in the hperm order here
         C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, ldg, 16, self.h1a)
-        C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg:])
+        C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg:],
+                       fold_ld=ldg if self.wg256 else 0, fold_col=H if self.wg256 else 0)
 
 
 def lr_at(step: int, lr: float, warmup: int, total: int, min_ratio: float) -> float:

@@ -179,6 +179,33 @@ def test_wgrad_kernel_vs_fp32(K, M, Mout, N, S):
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3 * (K ** 0.5))
 
 
+@pytest.mark.parametrize("K,H,S", [(8192, 1024, 16), (4096, 512, 8), (65536, 1024, 16), (2048, 256, 3)])
+def test_wgrad256_vs_fp32(K, H, S):
+    """The wide trainer's dW2|db2 on 256 x 256 output tiles (wgrad.hip wgrad256_kernel): fragments
+    through ds_read_b64_tr_b16 from swizzled stage images, split-K into slabs, db2 as per-tile-column
+    partial column sums folded by wgrad_reduce — against fp32 A^T B and A.sum(0)."""
+    from routest_amd.ops import _ext
+    C = _ext.native()
+    g = torch.Generator().manual_seed(K + H)
+    ldg = H + 16
+    A = torch.randn(K, H, generator=g).to(torch.bfloat16)
+    Bm = torch.randn(K, ldg, generator=g).to(torch.bfloat16)
+    Bm[:, H] = 1.0
+    Bm[:, H + 1:] = 0.0
+    ref = A.float().t() @ Bm.float()[:, :H]
+    slab = torch.zeros(S, H * ldg, device=DEV)
+    C.wgrad256(A.to(DEV), Bm.to(DEV), H, H, slab, ldg, H)
+    G = torch.full((H * ldg,), float("nan"), device=DEV)
+    C.wgrad_reduce(slab, G, fold_ld=ldg, fold_col=H)
+    G2 = torch.full((H * ldg,), float("nan"), device=DEV)
+    C.wgrad_reduce(slab, G2, fold_ld=ldg, fold_col=H)
+    got = G.view(H, ldg).cpu()
+    torch.testing.assert_close(got[:, :H], ref, rtol=1e-4, atol=1e-3 * (K ** 0.5))
+    torch.testing.assert_close(got[:, H], A.float().sum(0), rtol=1e-4, atol=1e-3 * (K ** 0.5))
+    assert torch.equal(got[:, H + 1:], torch.zeros(H, 15))
+    assert torch.equal(G, G2)                        # deterministic (fixed-order reduce)
+
+
 @pytest.mark.parametrize("S,n,stride", [(256, 74000, 74000), (37, 1001, 1003), (5, 4096, 4100), (1, 3, 3)])
 def test_wgrad_reduce_exact_and_deterministic(S, n, stride):
     from routest_amd.ops import _ext
