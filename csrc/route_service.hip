@@ -368,10 +368,15 @@ struct RouteService::Impl {
   std::atomic<long long> n_deferred{0}, t_wait_us{0}, n_prefetch{0};
   // latency watchdog: every wait on the flush's GPU work is bounded (ROUTEST_ROUTE_DEADLINE_MS)
   double deadline_ms = 2000.0;
+  // the deadline of the current flush's waits: deadline_ms scaled with its work (a healthy
+  // flush of oversized requests — NM up to 4096 stops, or a context built synchronously — must not
+  // read as a hung GPU and quarantine the slot)
+  std::atomic<double> flush_deadline_ms{2000.0};
   std::atomic<bool> broken{false};
   hipEvent_t ev_gpu{}, ev_asm{};
   hipStream_t hang_stream{};              // the gpu_hang fault hook's stream (own hardware queue)
   std::atomic<long long> n_failed_over{0};
+  std::atomic<long long> n_records{0}, n_record_bytes{0};
   bool fail_fault = false;                 // ROUTEST_FAULT=route_fail (test hook)
 
   // ROUTEST_ROUTE_TRACE_MS=<ms>: every wait on the GPU longer than that, every deadline, hand-off and
@@ -399,7 +404,8 @@ struct RouteService::Impl {
         if (trace_ms >= 0 && waited() > trace_ms) trace("wait %s %.1f ms", what, waited());
         return e;
       }
-      if (deadline_ms > 0 && (i & 15) == 15 && waited() > deadline_ms) {
+      const double dl = flush_deadline_ms.load(std::memory_order_relaxed);
+      if (dl > 0 && (i & 15) == 15 && waited() > dl) {
         trace("DEADLINE in %s after %.1f ms", what, waited());
         if (!broken.exchange(true) && cfg.on_timeout) cfg.on_timeout();
         return hipErrorLaunchTimeOut;
@@ -722,6 +728,7 @@ struct RouteService::Impl {
     }
     if (const char* v = std::getenv("ROUTEST_CCH_ASYNC")) async_ctx = std::string(v) != "0";
     if (const char* v = std::getenv("ROUTEST_ROUTE_DEADLINE_MS")) deadline_ms = std::atof(v);
+    flush_deadline_ms.store(deadline_ms);
     if (const char* v = std::getenv("ROUTEST_ROUTE_TRACE_MS")) trace_ms = std::atof(v);
     // ROUTEST_FAULT=route_fail: every flush of every service fails (not a timeout) — the hop limit
     // of the failover must end each job at the app
@@ -1806,7 +1813,11 @@ struct RouteService::Impl {
           }
         }
         if (!perr.empty()) j->req.error = perr;
-        if (want_rec && perr.empty()) j->rec = std::move(rw.b);
+        if (want_rec && perr.empty()) {
+          j->rec = std::move(rw.b);
+          n_records.fetch_add(1, std::memory_order_relaxed);
+          n_record_bytes.fetch_add((long long)j->rec.size(), std::memory_order_relaxed);
+        }
         if (!rtr::assemble(j->req, j->plan, dirs, cfg.engine, j->asmb, ccache()))
           j->fallback = true;
         else if (j->req.alt_k > 0 && j->asmb.ok) j->asmb.body += j->alt_json;
@@ -1915,6 +1926,19 @@ struct RouteService::Impl {
         if (!j->fallback && j->req.alt_k > 0 && (!ok || !j->req.error.empty())) j->fallback = !ok || j->fallback;
     }
     add_t(0, t0);
+    {
+      double pairs = 0.0;
+      bool sync_build = false;
+      for (RouteJob* j : jobs) {
+        if (j->fallback) continue;
+        const double n = (double)j->req.dst.size() + 1.0;
+        pairs += n * n;
+        sync_build |= j->sync_ctx;
+      }
+      // ~2 M matrix pairs ride on the base deadline; a synchronous context build gets 30 s more
+      flush_deadline_ms.store(deadline_ms <= 0 ? deadline_ms
+                                               : deadline_ms * (1.0 + pairs / 2.0e6) + (sync_build ? 30000.0 : 0.0));
+    }
     if (cfg.park_scorer) cfg.park_scorer();
     t0 = now_us();
     if (cfg.provider == 1 && cfg.cch != nullptr) {
@@ -2153,6 +2177,8 @@ std::vector<long long> RouteService::stats() const {
   v.push_back(p_->t_wait_us.load());       // ... their total wait (us)
   v.push_back(p_->n_prefetch.load());      // next-week-hour contexts queued ahead of time
   v.push_back(p_->n_failed_over.load());   // jobs handed to another GPU's route service
+  v.push_back(p_->n_records.load());       // rows persisted as compact route records
+  v.push_back(p_->n_record_bytes.load());  // ... and their record bytes
   return v;
 }
 

@@ -21,6 +21,7 @@
 //  * the fp32 partial of slice s is written to slab[s] in the caller's layout (the flat gradient
 //    bucket); wgrad_reduce_kernel sums the S slabs in a fixed order — deterministic, no atomics.
 #include <cstdlib>
+#include <string>
 #include <utility>
 
 #include "common.h"
@@ -374,10 +375,14 @@ struct Wg256Args {
   long long slab_stride;
   int lda, ldb, ldo, M, N, K, kslice, tiles_m, tiles_n, S, db2_col;
 };
-constexpr int W256_KT = 32;                     // rows per stage
-constexpr int W256_TILE = W256_KT * 512;        // one operand's stage image (bytes)
-constexpr int W256_STAGE = 2 * W256_TILE;
-constexpr int W256_NST = 4;                     // ring depth (three stages in flight)
+// KT rows per stage, a ring of NST stages (NST - 1 in flight): <64, 2> double-buffers 64-deep stages,
+// <32, 4> keeps three 32-deep stages in flight (ROUTEST_WGRAD256_CFG=32x4)
+template <int KT>
+struct W256Stage {
+  static constexpr int TILE = KT * 512;         // one operand's stage image (bytes)
+  static constexpr int STAGE = 2 * TILE;
+  static constexpr int LOADS = 2 * (KT / 16);   // global_load_lds per thread per stage
+};
 
 __device__ __forceinline__ int w256_sw(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
 // byte offset of columns col .. col + 3 (col % 4 == 0) of row r in a stage image
@@ -400,7 +405,25 @@ __device__ __forceinline__ bf16x8 w256_frag(const unsigned char* img, int c0, in
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// 16-byte LDS-DMA (global_load_lds_dwordx4) in inline asm: hipcc's waitcnt bookkeeping does not see
+// it, so the stage's fragment reads that follow (from ANOTHER buffer) are not preceded by a drain of
+// the prefetch (with the builtin, hipcc emitted vmcnt(0) before them: it cannot tell the buffers
+// apart) — the loop's counted s_waitcnt vmcnt(N) before each barrier is the only wait.  M0 (the
+// destination base) is set and restored in the same statement (cdna_hip_programming.md, LDS-DMA recipe).
+__device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+template <int KT, int NST>
 __global__ __launch_bounds__(512, 1) void wgrad256_kernel(Wg256Args a) {
+  static_assert(KT % 16 == 0 && KT <= 64 && (NST & (NST - 1)) == 0 && NST >= 2, "stage shape");
+  using SG = W256Stage<KT>;
+  constexpr int W256_KT = KT, W256_NST = NST, W256_TILE = SG::TILE, W256_STAGE = SG::STAGE;
+  constexpr int QN = KT / 16;                    // instructions per operand per wave and stage
   extern __shared__ __attribute__((aligned(16))) unsigned char smw[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int T = a.tiles_m * a.tiles_n;
@@ -429,25 +452,30 @@ __global__ __launch_bounds__(512, 1) void wgrad256_kernel(Wg256Args a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // staging: instruction q (0, 1) of wave w fills LDS rows 2 (8q + w) + (lane >> 5), slot lane & 31
-  const __bf16* gA[2];
-  const __bf16* gB[2];
+  // staging: instruction q of wave w fills LDS rows 2 (8q + w) + (lane >> 5), slot lane & 31.  The
+  // source pointers advance one stage per issue and stay live across the loop: a glds address held
+  // in a temporary was reallocated to a ds_read destination right after, and the compiler then
+  // drained the just-issued loads (vmcnt(0)) before the stage's fragment reads
+  const __bf16* gA[QN];
+  const __bf16* gB[QN];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < QN; ++q) {
     const int r = 2 * (8 * q + w) + (lane >> 5);
     const int ch = (lane & 31) ^ (w256_sw(r) << 1);
     gA[q] = a.A + (size_t)(k_begin + r) * a.lda + m0 + 8 * ch;
     gB[q] = a.B + (size_t)(k_begin + r) * a.ldb + n0 + 8 * ch;
   }
-  typedef __attribute__((address_space(3))) void lds_void;
-  auto issue = [&](int kt) {                // 4 loads per thread
-    unsigned char* img = smw + (kt & (W256_NST - 1)) * W256_STAGE;
-    const size_t ra = (size_t)W256_KT * kt * a.lda, rb = (size_t)W256_KT * kt * a.ldb;
+  const size_t stepA = (size_t)W256_KT * a.lda, stepB = (size_t)W256_KT * a.ldb;
+  // the LDS byte address of the dynamic region (wave-uniform)
+  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) unsigned char*)smw);
+  auto issue = [&](int kt) {                // stage kt (issued in order); SG::LOADS loads per thread
+    const unsigned img = lds0 + (unsigned)((kt & (W256_NST - 1)) * W256_STAGE);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      __builtin_amdgcn_global_load_lds((const void*)(gA[q] + ra), (lds_void*)(img + (8 * q + w) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(gB[q] + rb), (lds_void*)(img + W256_TILE + (8 * q + w) * 1024),
-                                       16, 0, 0);
+    for (int q = 0; q < QN; ++q) {
+      glds16_asm(gA[q], __builtin_amdgcn_readfirstlane(img + (8 * q + w) * 1024));
+      glds16_asm(gB[q], __builtin_amdgcn_readfirstlane(img + W256_TILE + (8 * q + w) * 1024));
+      gA[q] += stepA;
+      gB[q] += stepB;
     }
   };
 
@@ -457,26 +485,44 @@ __global__ __launch_bounds__(512, 1) void wgrad256_kernel(Wg256Args a) {
   float dsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int drow = tid >> 5, dch = tid & 31;
 
-  for (int kt = 0; kt < 3 && kt < nk; ++kt) issue(kt);
+  for (int kt = 0; kt < NST - 1 && kt < nk; ++kt) issue(kt);
   for (int kt = 0; kt < nk; ++kt) {
-    // stage kt landed (stages kt + 1, kt + 2 may stay in flight), then every wave is past stage
-    // kt - 1, whose buffer stage kt + 3 refills
-    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 3 < nk) issue(kt + 3);
+    // stage kt landed (up to NST - 2 younger stages may stay in flight), then every wave is past
+    // stage kt - 1, whose buffer stage kt + NST - 1 refills
+    const int younger = min(NST - 2, nk - 1 - kt);
+    if constexpr (NST >= 4) {
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * SG::LOADS) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SG::LOADS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (NST == 3) {
+      if (younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SG::LOADS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      (void)younger;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // a RAW barrier: __syncthreads()' fence would drain the loads still in flight (vmcnt(0));
+    // every read of the buffer about to be refilled was consumed by this wave's MFMAs already
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + NST - 1 < nk) issue(kt + NST - 1);
+    const int ks_n = KT / 32;
     const unsigned char* imgA = smw + (kt & (W256_NST - 1)) * W256_STAGE;
     const unsigned char* imgB = imgA + W256_TILE;
-    bf16x8 fa[8], fb[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = w256_frag(imgA, 128 * wu + 16 * i, lane);
+    for (int ks = 0; ks < ks_n; ++ks) {
+      bf16x8 fa[8], fb[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = w256_frag(imgB, 64 * wr + 16 * j, lane);
+      for (int i = 0; i < 8; ++i) fa[i] = w256_frag(imgA + 32 * ks * 512, 128 * wu + 16 * i, lane);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < 4; ++j) fb[j] = w256_frag(imgB + 32 * ks * 512, 64 * wr + 16 * j, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
     if (db2) {
       for (int rr = 0; rr < rows_per; rr += 16) {
         if (rr + drow < rows_per) {
@@ -519,9 +565,30 @@ __global__ __launch_bounds__(512, 1) void wgrad256_kernel(Wg256Args a) {
   }
 }
 
+template <int KT, int NST>
+static hipError_t launch_w256(const Wg256Args& a, hipStream_t stream) {
+  constexpr int lds = NST * W256Stage<KT>::STAGE;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)wgrad256_kernel<KT, NST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((wgrad256_kernel<KT, NST>), dim3((unsigned)(a.S * a.tiles_m * a.tiles_n)), dim3(512), lds, stream,
+                     a);
+  return hipGetLastError();
+}
+
 hipError_t launch_wgrad256(const void* A, int lda, const void* B, int ldb, int M, int N, int K, int S, float* slab,
                            int ldo, long long slab_stride, int db2_col, hipStream_t stream) {
-  if (M % 256 || N % 256 || K % W256_KT || lda % 8 || ldb % 8 || S < 1) return hipErrorInvalidValue;
+  // stage shape: ROUTEST_WGRAD256_CFG = 64x2 (default) | 32x4
+  static const bool ring = [] {
+    const char* v = std::getenv("ROUTEST_WGRAD256_CFG");
+    return v && std::string(v) == "32x4";
+  }();
+  const int KT = ring ? 32 : 64;
+  if (M % 256 || N % 256 || K % KT || lda % 8 || ldb % 8 || S < 1) return hipErrorInvalidValue;
   Wg256Args a{};
   a.A = (const __bf16*)A;
   a.B = (const __bf16*)B;
@@ -533,23 +600,14 @@ hipError_t launch_wgrad256(const void* A, int lda, const void* B, int ldb, int M
   a.M = M;
   a.N = N;
   a.K = K;
-  a.kslice = ((K + S - 1) / S + W256_KT - 1) / W256_KT * W256_KT;
+  a.kslice = ((K + S - 1) / S + KT - 1) / KT * KT;
   a.tiles_m = M / 256;
   a.tiles_n = N / 256;
   a.S = S;
   a.db2_col = db2_col;
   if (db2_col >= 0 && (db2_col + a.tiles_n > ldo || (a.tiles_n != 1 && a.tiles_n != 2 && a.tiles_n != 4)))
     return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)wgrad256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       W256_NST * W256_STAGE);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  hipLaunchKernelGGL(wgrad256_kernel, dim3((unsigned)(S * a.tiles_m * a.tiles_n)), dim3(512), W256_NST * W256_STAGE,
-                     stream, a);
-  return hipGetLastError();
+  return ring ? launch_w256<32, 4>(a, stream) : launch_w256<64, 2>(a, stream);
 }
 
 size_t wgrad_lds_bytes(int NT, int KB) {

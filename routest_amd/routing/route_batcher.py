@@ -100,6 +100,8 @@ class RouteBatcher:
         self.astar_slots = astar_slots
         self._astar: Dict[Any, Any] = {}
         self._astar_lock = threading.Lock()
+        self._streams: Dict[str, Any] = {}
+        self._stream_lock = threading.Lock()
         self.q: "queue.SimpleQueue[Optional[tuple]]" = queue.SimpleQueue()
         self.flushes = [0] * len(self.devices)
         self.threads = [threading.Thread(target=self._worker, args=(d, i), name=f"route-batch-{i}",
@@ -108,6 +110,16 @@ class RouteBatcher:
             t.start()
 
     # ------------------------------------------------------------------ batch function
+    def _stream_for(self, device):
+        import torch
+        with self._stream_lock:
+            key = str(device)
+            st = self._streams.get(key)
+            if st is None:
+                with torch.cuda.device(device):
+                    st = self._streams[key] = torch.cuda.Stream(device)
+            return st
+
     def _astar_for(self, device):
         """The device's A* workspace and the lock that serialises its searches (two workers on one
         device would otherwise run on the same per-slot state rows at once)."""
@@ -313,14 +325,15 @@ class RouteBatcher:
 
     def _worker(self, device, idx: int) -> None:
         import torch
-        # the flushes run on a stream of their own: a NON-blocking one, so this worker's launches and
-        # copies never queue behind the legacy null stream's implicit wait for every blocking stream
-        # on the device (a kernel hung on one — the watchdog rehearsal's fault streams are blocking —
-        # stalled every request relayed here for the hang's whole duration)
+        # the flushes run on a NON-blocking stream, so their launches and copies never queue behind
+        # the legacy null stream's implicit wait for every blocking stream on the device (a kernel
+        # hung on one — the watchdog rehearsal's fault streams are blocking — stalled every request
+        # relayed here for the hang's whole duration).  ONE stream per device, shared by the
+        # device's workers: their searches share per-device workspaces, and the lock around them is
+        # released when the host calls return, so the GPU work must stay ordered on one stream
         stream = None
         if device is not None and getattr(device, "type", "") == "cuda":
-            with torch.cuda.device(device):
-                stream = torch.cuda.Stream(device)
+            stream = self._stream_for(device)
         while True:
             first = self.q.get()
             if first is None:

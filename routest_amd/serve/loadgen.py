@@ -86,6 +86,8 @@ def native_route_load(stack, reqs: Sequence[Dict[str, Any]], concurrency: int, s
             "legs_escalated": f1.get("route_astar_escalated", 0) - f0.get("route_astar_escalated", 0),
             "fallbacks_to_python": f1["route_service_fallbacks"] - f0["route_service_fallbacks"],
             "rows_persisted": f1["route_persisted"] - f0["route_persisted"],
+            "record_bytes_per_row": ((f1.get("route_record_bytes", 0) - f0.get("route_record_bytes", 0)) /
+                                     max(1, f1.get("route_records", 0) - f0.get("route_records", 0))),
             "jobs_waited_for_context": f1.get("route_ctx_deferred", 0) - f0.get("route_ctx_deferred", 0),
             "stage_ms_per_flush": {k[9:]: (f1[k] - f0[k]) / 1e3 / flushes for k in f1 if k.startswith("route_us_")},
             "client": "native closed-loop (csrc/runtime/http_client.h)",

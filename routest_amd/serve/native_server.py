@@ -180,7 +180,9 @@ class NativePredictServer:
                  "route_ctx_deferred", "route_us_ctx_wait", "route_ctx_prefetched",
                  # latency watchdog: route jobs handed to another GPU's route service after a
                  # flush missed its deadline; prediction rounds abandoned at the deadline
-                 "route_failed_over", "timeouts")
+                 "route_failed_over", "timeouts",
+                 # persisted graph routes stored as compact route records, and their bytes
+                 "route_records", "route_record_bytes")
         return dict(zip(names, v))
 
     def close(self) -> None:

@@ -296,7 +296,7 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
         # wgrad_kernel)
         import os
         self.wg256 = (H % 256 == 0 and B % 64 == 0 and hasattr(self.C, "wgrad256") and
-                      os.environ.get("ROUTEST_WGRAD256", "1") != "0")
+                      os.environ.get("ROUTEST_WGRAD256", "0") == "1")
         if self.wg256:
             self.S2 = max(1, min(B // 64, ncu // ((H // 256) ** 2)))
             # (zeros: the bucket's pad columns H+1 .. H+15 are never written by the kernel)
