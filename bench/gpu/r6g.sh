@@ -18,3 +18,7 @@ done
 G1="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE"
 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $G1 -d $O/pmc_1 -o w --output-format csv -- python3 $ROOT/bench/wgrad_probe.py --iters 5 > $O/pmc_1.log 2>&1 || { echo "pmc failed rc=$?"; exit 1; }
 echo done
+timeout -k 10 300 python -u -m pytest -v --timeout 200 --timeout-method thread tests/test_frontend_gpu.py -k "compact_records" > $O/records_test.log 2>&1; stop $?
+tail -1 $O/records_test.log
+timeout -k 10 500 python -u bench.py > $O/bench.log 2>&1; stop $?
+tail -1 $O/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['route_optimizer']; print(d['value'], d['p50_predict_ms'], d['dp_training']['ms_per_step'], d['dp_training'].get('launch'), d['dp_training_large_batch']['ms_per_step'], r.get('context_customize_gpu_ms'), {k: (r[k]['req_per_s'], r[k]['p99_ms'], r[k].get('record_bytes_per_row')) for k in ('http','http_f02') if k in r}, d['schema_problems'])"

@@ -55,7 +55,7 @@ def main():
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / a.iters * 1e3
         flops = 2.0 * B * H * H
-        print(json.dumps({"kernel": k, "cfg": os.environ.get("ROUTEST_WGRAD256_CFG", "64x2"), "H": H, "batch": B,
+        print(json.dumps({"kernel": k, "cfg": os.environ.get("ROUTEST_WGRAD256_CFG", "32x4"), "H": H, "batch": B,
                           "slices": S, "us": us, "tflops": flops / us / 1e6}), flush=True)
 
 

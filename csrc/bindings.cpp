@@ -537,6 +537,45 @@ void adamw_pack(torch::Tensor P, torch::Tensor G, torch::Tensor M, torch::Tensor
                                      cur_stream(P)));
 }
 
+// wgrad_reduce(slab2 -> G[:H*ldg] register-native, slab -> G[H*ldg+ldg:], w3slab -> G[H*ldg:H*ldg+ldg])
+// followed by adamw_pack(update=True), fused (one rank: no gradient communication in between)
+void reduce_adamw(torch::Tensor slab2, torch::Tensor slab1, torch::Tensor w3slab, torch::Tensor P,
+                  torch::Tensor G, torch::Tensor M, torch::Tensor V, torch::Tensor blob, torch::Tensor step,
+                  int64_t H, double lr, double beta1, double beta2, double eps, double wd, int64_t warmup,
+                  int64_t total_steps, double min_lr_ratio) {
+  TORCH_CHECK(H == 64 || H == 128 || H == 256, "fused trainer: H in (64, 128, 256)");
+  const int64_t N = rt::mlp3_num_params((int)H), ldg = H + 16;
+  for (auto* t : {&P, &M, &V}) {
+    check_dev(*t, "adam state");
+    TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->numel() == N, "P/M/V must be f32 [", N, "]");
+  }
+  check_dev(G, "G");
+  TORCH_CHECK(G.scalar_type() == torch::kFloat32 && G.numel() == rt::mlp3_grad_bucket_floats((int)H),
+              "G must be the flat f32 gradient bucket");
+  auto chk = [&](const torch::Tensor& sl, int64_t w, const char* what) {
+    check_dev(sl, what);
+    TORCH_CHECK(sl.scalar_type() == torch::kFloat32 && sl.dim() == 2 && sl.is_contiguous() &&
+                    sl.size(0) >= 1 && sl.size(1) == w && sl.device() == G.device(),
+                what, ": f32 [S, ", w, "] on G's device");
+  };
+  chk(slab2, H * ldg, "slab2");
+  chk(slab1, 16 * H, "slab1");
+  chk(w3slab, ldg, "w3slab");
+  check_dev(blob, "blob");
+  TORCH_CHECK(blob.scalar_type() == torch::kUInt8 &&
+              (size_t)blob.numel() == rt::eta_mlp3_train_blob_bytes((int)H), "bad training blob");
+  check_dev(step, "step");
+  TORCH_CHECK(step.scalar_type() == torch::kInt32 && step.numel() >= 1, "step: int32");
+  const c10::DeviceGuard guard(P.device());
+  RT_CHECK_HIP(rt::launch_reduce_adamw(
+      slab2.data_ptr<float>(), (int)slab2.size(0), (long long)slab2.size(1), slab1.data_ptr<float>(),
+      (int)slab1.size(0), (long long)slab1.size(1), w3slab.data_ptr<float>(), (int)w3slab.size(0),
+      (long long)w3slab.size(1), G.data_ptr<float>(), P.data_ptr<float>(), M.data_ptr<float>(),
+      V.data_ptr<float>(), blob.data_ptr(), step.data_ptr<int>(), (int)H, (float)lr, (float)beta1,
+      (float)beta2, (float)eps, (float)wd, (int)warmup, (int)total_steps, (float)min_lr_ratio,
+      cur_stream(P)));
+}
+
 // slab: f32 [S, stride]; the partial of k-slice s is written at slab[s, offset + m*ldo + n].
 void wgrad(torch::Tensor A, int64_t M, int64_t Mout, torch::Tensor Bm, int64_t N, torch::Tensor slab,
            int64_t offset, int64_t ldo, c10::optional<torch::Tensor> mask, int64_t nout,
@@ -1362,6 +1401,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return (int64_t)rt::train_wgrad_slices((int)B, num_cus((int)device), (int)H);
   }, py::arg("B"), py::arg("device"), py::arg("H") = 256);
   m.def("adamw_pack", &adamw_pack, "fused AdamW on flat fp32 params + training-blob re-pack");
+  m.def("reduce_adamw", &reduce_adamw, "one-rank fused slab reduction + AdamW + blob re-pack");
   m.def("eta_mlp3_train_blob_bytes", [](int64_t H) { return (int64_t)rt::eta_mlp3_train_blob_bytes((int)H); });
   m.def("mlp3_num_params", [](int64_t H) { return (int64_t)rt::mlp3_num_params((int)H); });
   m.def("mlp3_grad_bucket_floats", [](int64_t H) { return (int64_t)rt::mlp3_grad_bucket_floats((int)H); });

@@ -36,6 +36,7 @@
 #include "lds_fill.h"
 #include "mlp3_tile.h"
 #include "ops.h"
+#include "wgrad_reduce.h"
 
 namespace rt {
 
@@ -797,57 +798,24 @@ __device__ __forceinline__ float sched_lr(const AdamWArgs& a, int t) {
   return lr;
 }
 
+// AdamW on one master parameter e (flat P order: W1 | b1 | W2 | b2 | W3 | b3; o / i its row /
+// column) with gradient g, then its bf16 / f32 copies in the training blob (the forward's LDS image
+// and the backward's W2 fragment image).  Shared by adamw_pack_kernel and the one-rank fused
+// reduce + AdamW (reduce_adamw_kernel): the same fp32 operations in the same order.
 template <int H>
-__global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
-                                                         const float* __restrict__ G,
-                                                         float* __restrict__ M, float* __restrict__ V,
-                                                         unsigned char* __restrict__ blob,
-                                                         const int* __restrict__ step, AdamWArgs a) {
+__device__ __forceinline__ void adamw_param(int e, float g, bool decay, int o, int i, float* __restrict__ P,
+                                            float* __restrict__ M, float* __restrict__ V,
+                                            unsigned char* __restrict__ blob, const int* __restrict__ step,
+                                            const AdamWArgs& a) {
   using L = TrainLayout<H>;
   constexpr int OFF_B1 = 12 * H, OFF_W2 = 13 * H, OFF_B2 = 13 * H + H * H, OFF_W3 = OFF_B2 + H,
-                OFF_B3 = OFF_W3 + H, N = OFF_B3 + 1;
-  constexpr int LDG = H + 16;
-  const float* gW2a = G;
-  const float* gW3a = G + H * LDG;
-  const float* gW1a = gW3a + LDG;
+                OFF_B3 = OFF_W3 + H;
   unsigned char* w2img = blob;
   __bf16* w1p = reinterpret_cast<__bf16*>(blob + L::W2B);
   float* b1p = reinterpret_cast<float*>(blob + L::W2B + L::W1B);
   float* b2p = b1p + H;
   float* w3p = b2p + H;
   float* tail = w3p + H;
-
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= N) return;
-  float g = 0.f;
-  bool decay = false;
-  int o = 0, i = 0;
-  if (e < OFF_B1) {
-    o = e / 12;
-    i = e - o * 12;
-    g = gW1a[hperm(o) * 16 + i];          // dW1 rows at hperm positions (dz1 is stored so)
-    if (i == 10) g += gW1a[hperm(o) * 16 + 12];
-    if (i == 11) g += gW1a[hperm(o) * 16 + 13];
-    decay = true;
-  } else if (e < OFF_W2) {
-    o = e - OFF_B1;
-    g = gW1a[hperm(o) * 16 + 14];
-  } else if (e < OFF_B2) {
-    const int k = e - OFF_W2;
-    o = k / H;
-    i = k - o * H;
-    g = gW2a[hperm(o) * LDG + hperm(i)];
-    decay = true;
-  } else if (e < OFF_W3) {
-    o = e - OFF_B2;
-    g = gW2a[hperm(o) * LDG + H];
-  } else if (e < OFF_B3) {
-    o = e - OFF_W3;
-    g = gW3a[hperm(o)];
-    decay = true;
-  } else {
-    g = gW3a[H];
-  }
   float p = P[e];
   if (a.update) {
     const int t = *step > 0 ? *step : 1;
@@ -891,6 +859,133 @@ __global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
   } else {
     tail[0] = p;
   }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void adamw_pack_kernel(float* __restrict__ P,
+                                                         const float* __restrict__ G,
+                                                         float* __restrict__ M, float* __restrict__ V,
+                                                         unsigned char* __restrict__ blob,
+                                                         const int* __restrict__ step, AdamWArgs a) {
+  constexpr int OFF_B1 = 12 * H, OFF_W2 = 13 * H, OFF_B2 = 13 * H + H * H, OFF_W3 = OFF_B2 + H,
+                OFF_B3 = OFF_W3 + H, N = OFF_B3 + 1;
+  constexpr int LDG = H + 16;
+  const float* gW2a = G;
+  const float* gW3a = G + H * LDG;
+  const float* gW1a = gW3a + LDG;
+
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N) return;
+  float g = 0.f;
+  bool decay = false;
+  int o = 0, i = 0;
+  if (e < OFF_B1) {
+    o = e / 12;
+    i = e - o * 12;
+    g = gW1a[hperm(o) * 16 + i];          // dW1 rows at hperm positions (dz1 is stored so)
+    if (i == 10) g += gW1a[hperm(o) * 16 + 12];
+    if (i == 11) g += gW1a[hperm(o) * 16 + 13];
+    decay = true;
+  } else if (e < OFF_W2) {
+    o = e - OFF_B1;
+    g = gW1a[hperm(o) * 16 + 14];
+  } else if (e < OFF_B2) {
+    const int k = e - OFF_W2;
+    o = k / H;
+    i = k - o * H;
+    g = gW2a[hperm(o) * LDG + hperm(i)];
+    decay = true;
+  } else if (e < OFF_W3) {
+    o = e - OFF_B2;
+    g = gW2a[hperm(o) * LDG + H];
+  } else if (e < OFF_B3) {
+    o = e - OFF_W3;
+    g = gW3a[hperm(o)];
+    decay = true;
+  } else {
+    g = gW3a[H];
+  }
+  adamw_param<H>(e, g, decay, o, i, P, M, V, blob, step, a);
+}
+
+// One-rank step tail: the slab reduction of wgrad_reduce (three segments: the register-native dW2|db2
+// slabs -> gW2a, the dW1 slabs -> gW1a, the forward's dW3|db3 rows -> gW3a) and AdamW + re-pack of
+// the parameters whose gradients the workgroup just summed, in one launch instead of two (the
+// 64k-row step's 7.7 + 5.1 us, profiles/train_kernel_stats_64k_r5o.csv).  Only without gradient
+// communication: an all-reduce must see the whole bucket first.  G is still written (checkpoints,
+// tests, gradient norms read it).  The sums and the AdamW arithmetic are those of wgrad_reduce_kernel
+// and adamw_pack_kernel, so both paths produce the same bits (tests/test_train_gpu.py).
+template <int H>
+__global__ __launch_bounds__(256) void reduce_adamw_kernel(RedSeg s0, RedSeg s1, RedSeg s2, int nb0, int nb01,
+                                                           float* __restrict__ P, float* __restrict__ M,
+                                                           float* __restrict__ V, unsigned char* __restrict__ blob,
+                                                           const int* __restrict__ step, AdamWArgs a) {
+  constexpr int OFF_B1 = 12 * H, OFF_W2 = 13 * H, OFF_B2 = 13 * H + H * H, OFF_W3 = OFF_B2 + H,
+                OFF_B3 = OFF_W3 + H;
+  constexpr int LDG = H + 16;
+  const int bx = (int)blockIdx.x;
+  const int seg = bx < nb0 ? 0 : (bx < nb01 ? 1 : 2);
+  const RedSeg sg = seg == 0 ? s0 : (seg == 1 ? s1 : s2);
+  const int blk = bx - (seg == 0 ? 0 : (seg == 1 ? nb0 : nb01));
+  __shared__ RedPart part;
+  __shared__ float sum[RED_COLS * 4];
+  const float4 r = red_sum<false>(sg, blk, part);
+  const int c = threadIdx.x & (RED_COLS - 1), sl = threadIdx.x / RED_COLS;
+  if (sl == 0) {
+    sum[4 * c] = r.x;
+    sum[4 * c + 1] = r.y;
+    sum[4 * c + 2] = r.z;
+    sum[4 * c + 3] = r.w;
+  }
+  __syncthreads();
+  // thread t < 64: bucket value t of the workgroup (slab element blk * 64 + t)
+  const int t = threadIdx.x;
+  const int x = blk * (RED_COLS * 4) + t;
+  if (t >= RED_COLS * 4 || x >= sg.n) return;
+  const float g = sum[t];
+  int gi;
+  if (seg == 0) {
+    int g0, st;
+    native_to_bucket(x & ~3, H, g0, st);
+    gi = g0 + (x & 3) * st;
+  } else {
+    gi = x;
+  }
+  sg.G[gi] = g;
+  int e = -1, o = 0, i = 0;
+  bool decay = false;
+  float gg = g;
+  if (seg == 0) {                    // gW2a [H][LDG]: row hperm(o), column hperm(i) | H (db2) | zero pad
+    const int row = gi / LDG, col = gi - row * LDG;
+    o = red_hperm(row);
+    if (col < H) {
+      i = red_hperm(col);
+      e = OFF_W2 + o * H + i;
+      decay = true;
+    } else if (col == H) {
+      e = OFF_B2 + o;
+    }
+  } else if (seg == 1) {             // gW1a [H][16]: row hperm(o); cols 0..11 W1 (10 += 12, 11 += 13), 14 b1
+    const int row = x >> 4, col = x & 15;
+    o = red_hperm(row);
+    if (col < 12) {
+      i = col;
+      e = o * 12 + col;
+      if (col >= 10) gg = g + sum[t + 2];     // the same add as adamw_pack_kernel
+      decay = true;
+    } else if (col == 14) {
+      e = OFF_B1 + o;
+    }
+  } else {                           // gW3a [LDG]: hperm(o) | H (db3)
+    if (x < H) {
+      o = red_hperm(x);
+      e = OFF_W3 + o;
+      decay = true;
+    } else if (x == H) {
+      e = OFF_B3;
+    }
+  }
+  if (e >= 0) adamw_param<H>(e, gg, decay, o, i, P, M, V, blob, step, a);
 }
 
 // workgroups of the training forward (= rows of its dW3 slab): one per 8 row tiles, at most one
@@ -1080,6 +1175,31 @@ hipError_t launch_adamw_pack(float* P, const float* G, float* M, float* V, void*
     case 128: hipLaunchKernelGGL(adamw_pack_kernel<128>, grid, block, 0, stream, P, G, M, V, (unsigned char*)blob, step, a); break;
     case 256: hipLaunchKernelGGL(adamw_pack_kernel<256>, grid, block, 0, stream, P, G, M, V, (unsigned char*)blob, step, a); break;
     default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_adamw(const float* slab2, int S2, long long stride2, const float* slab1, int S1,
+                               long long stride1, const float* w3slab, int S3, long long stride3, float* G,
+                               float* P, float* M, float* V, void* blob, const int* step, int H, float lr,
+                               float beta1, float beta2, float eps, float wd, int warmup, int total_steps,
+                               float min_lr_ratio, hipStream_t stream) {
+  if (H != 64 && H != 128 && H != 256) return hipErrorInvalidValue;
+  const int LDG = H + 16;
+  if (stride2 < (long long)H * LDG || stride1 < 16LL * H || stride3 < LDG || S2 < 1 || S1 < 1 || S3 < 1)
+    return hipErrorInvalidValue;
+  AdamWArgs a{lr, beta1, beta2, eps, wd, warmup, total_steps, min_lr_ratio, 1};
+  const RedSeg s0{slab2, stride2, G, S2, H * LDG, H};
+  const RedSeg s1{slab1, stride1, G + H * LDG + LDG, S1, 16 * H, 0};
+  const RedSeg s2{w3slab, stride3, G + H * LDG, S3, LDG, 0};
+  const int per = 4 * RED_COLS;
+  const int nb0 = (s0.n + per - 1) / per, nb1 = (s1.n + per - 1) / per, nb2 = (s2.n + per - 1) / per;
+  const dim3 grid(nb0 + nb1 + nb2), block(256);
+  unsigned char* b = (unsigned char*)blob;
+  switch (H) {
+    case 64: hipLaunchKernelGGL(reduce_adamw_kernel<64>, grid, block, 0, stream, s0, s1, s2, nb0, nb0 + nb1, P, M, V, b, step, a); break;
+    case 128: hipLaunchKernelGGL(reduce_adamw_kernel<128>, grid, block, 0, stream, s0, s1, s2, nb0, nb0 + nb1, P, M, V, b, step, a); break;
+    case 256: hipLaunchKernelGGL(reduce_adamw_kernel<256>, grid, block, 0, stream, s0, s1, s2, nb0, nb0 + nb1, P, M, V, b, step, a); break;
   }
   return hipGetLastError();
 }

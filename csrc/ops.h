@@ -46,6 +46,12 @@ hipError_t launch_adamw_pack(float* P, const float* G, float* M, float* V, void*
                              const int* step, int H, float lr, float beta1, float beta2, float eps,
                              float wd, int warmup, int total_steps, float min_lr_ratio, int update,
                              hipStream_t stream);
+// one-rank fused wgrad_reduce (dW2 register-native slabs | dW1 slabs | dW3 rows) + adamw_pack(update)
+hipError_t launch_reduce_adamw(const float* slab2, int S2, long long stride2, const float* slab1, int S1,
+                               long long stride1, const float* w3slab, int S3, long long stride3, float* G,
+                               float* P, float* M, float* V, void* blob, const int* step, int H, float lr,
+                               float beta1, float beta2, float eps, float wd, int warmup, int total_steps,
+                               float min_lr_ratio, hipStream_t stream);
 
 // ---- wide MLPs (H = 512, 1024): mlp_big.hip ----
 hipError_t launch_big_layer1(const void* rec, int rec_bytes, int B, const void* w1p, int H,

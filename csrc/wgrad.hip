@@ -26,6 +26,7 @@
 
 #include "common.h"
 #include "ops.h"
+#include "wgrad_reduce.h"
 
 namespace rt {
 
@@ -243,91 +244,21 @@ __global__ __launch_bounds__(512, 2) void wgrad_dual_kernel(WgSeg s0, WgSeg s1, 
 // column c with 4 independent loads in flight, then the 16 partials are combined in LDS in a fixed
 // order.  ~n/64 workgroups (1157 for the H=256 bucket) keep every CU streaming the 76 MB of slabs;
 // the previous one-thread-per-column version ran 73 workgroups and 256 dependent loads per thread.
-constexpr int RED_SL = 16, RED_COLS = 16;
-
-// Up to three independent segments (slab regions with their own slice counts) in one launch:
-// blocks [0, nb0) reduce segment 0, [nb0, nb01) segment 1, the rest segment 2.
-struct RedSeg {
-  const float* slab;
-  long long slab_stride;
-  float* G;
-  int S, n;
-  int perm_h;        // 0: slab and G share a layout; H: train_bwd_kernel<H>'s register-native dW2 slabs
-  int fold_ld = 0;   // > 0: the float4 at column fold_col of every fold_ld-wide row holds partials of
-  int fold_col = 0;  // ONE value (wgrad256's db2 per tile column): stored as (x + y + z + w, 0, 0, 0)
-};
-
-__device__ __forceinline__ int red_hperm(int u) { return (u & ~12) | ((u & 4) << 1) | ((u & 8) >> 1); }
-
-// G's index of slab element e (e % 4 == 0) and the stride of its 3 successors in the register-native
-// layout of train_bwd_kernel<H> (eta_mlp_train.hip): accumulator tile (w, i, mt) = 1024 floats, lane
-// l's registers 4q .. 4q+3 at q*256 + 4l — rows 32mt + 8q + 4(l >> 5) + j of bucket column
-// hperm(32(2w+i) + (l & 31)); past H*H the [row][16] block of the db2 / zero columns.
-__device__ __forceinline__ void native_to_bucket(int e, int H, int& g0, int& step) {
-  const int LDG = H + 16, MT = H / 32;
-  if (e >= H * H) {
-    const int x = e - H * H;
-    g0 = (x >> 4) * LDG + H + (x & 15);
-    step = 1;
-    return;
-  }
-  const int blk = e >> 10, rem = e & 1023, q = rem >> 8, l = (rem & 255) >> 2;
-  const int wi = blk / MT, mt = blk - wi * MT;
-  const int nc = red_hperm(32 * wi + (l & 31));
-  g0 = (32 * mt + 8 * q + 4 * (l >> 5)) * LDG + nc;
-  step = LDG;
-}
-
 template <bool NTLOAD>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(RedSeg s0, RedSeg s1, RedSeg s2, int nb0,
                                                            int nb01) {
   const int bx = (int)blockIdx.x;
   const int seg = bx < nb0 ? 0 : (bx < nb01 ? 1 : 2);
   const RedSeg sg = seg == 0 ? s0 : (seg == 1 ? s1 : s2);
-  const float* __restrict__ slab = sg.slab;
-  const long long slab_stride = sg.slab_stride;
   float* __restrict__ G = sg.G;
-  const int S = sg.S, n = sg.n;
+  const int n = sg.n;
   const int blk = bx - (seg == 0 ? 0 : (seg == 1 ? nb0 : nb01));
-  __shared__ float4 part[RED_SL][RED_COLS + 1];
+  __shared__ RedPart part;
+  const float4 r = red_sum<NTLOAD>(sg, blk, part);
   const int c = threadIdx.x & (RED_COLS - 1), sl = threadIdx.x / RED_COLS;
   const int e = (blk * RED_COLS + c) * 4;
-  const bool vec = (slab_stride % 4) == 0 && e + 4 <= n;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e < n) {
-    if (vec) {
-      f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
-      auto ld = [&](int k) {
-        const f32x4* q = reinterpret_cast<const f32x4*>(slab + (long long)k * slab_stride + e);
-        if constexpr (NTLOAD) return __builtin_nontemporal_load(q);
-        else return *q;
-      };
-      int s = sl;
-      for (; s + 3 * RED_SL < S; s += 4 * RED_SL) {
-        const f32x4 v0 = ld(s), v1 = ld(s + RED_SL), v2 = ld(s + 2 * RED_SL), v3 = ld(s + 3 * RED_SL);
-        a4 += v0;
-        a4 += v1;
-        a4 += v2;
-        a4 += v3;
-      }
-      for (; s < S; s += RED_SL) a4 += ld(s);
-      acc = make_float4(a4[0], a4[1], a4[2], a4[3]);
-    } else {
-      float t[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int s = sl; s < S; s += RED_SL)
-        for (int q = 0; q < 4 && e + q < n; ++q) t[q] += slab[(long long)s * slab_stride + e + q];
-      acc = make_float4(t[0], t[1], t[2], t[3]);
-    }
-  }
-  part[sl][c] = acc;
-  __syncthreads();
+  const bool vec = (sg.slab_stride % 4) == 0 && e + 4 <= n;
   if (sl == 0 && e < n) {
-    float4 r = part[0][c];
-    for (int k = 1; k < RED_SL; ++k) {
-      const float4 v = part[k][c];
-      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
-    }
-    if (sg.fold_ld > 0 && e % sg.fold_ld == sg.fold_col) r = make_float4(((r.x + r.y) + r.z) + r.w, 0.f, 0.f, 0.f);
     if (sg.perm_h > 0) {
       int g0, step;
       native_to_bucket(e, sg.perm_h, g0, step);
@@ -375,8 +306,8 @@ struct Wg256Args {
   long long slab_stride;
   int lda, ldb, ldo, M, N, K, kslice, tiles_m, tiles_n, S, db2_col;
 };
-// KT rows per stage, a ring of NST stages (NST - 1 in flight): <64, 2> double-buffers 64-deep stages,
-// <32, 4> keeps three 32-deep stages in flight (ROUTEST_WGRAD256_CFG=32x4)
+// KT rows per stage, a ring of NST stages (NST - 1 in flight): <32, 4> (default) keeps three 32-deep
+// stages in flight, <64, 2> double-buffers 64-deep stages (ROUTEST_WGRAD256_CFG=64x2)
 template <int KT>
 struct W256Stage {
   static constexpr int TILE = KT * 512;         // one operand's stage image (bytes)
@@ -582,10 +513,11 @@ static hipError_t launch_w256(const Wg256Args& a, hipStream_t stream) {
 
 hipError_t launch_wgrad256(const void* A, int lda, const void* B, int ldb, int M, int N, int K, int S, float* slab,
                            int ldo, long long slab_stride, int db2_col, hipStream_t stream) {
-  // stage shape: ROUTEST_WGRAD256_CFG = 64x2 (default) | 32x4
+  // stage shape: ROUTEST_WGRAD256_CFG = 32x4 (default: 159 us against 173 us at H = 1024, 64k rows,
+  // run r6g) | 64x2
   static const bool ring = [] {
     const char* v = std::getenv("ROUTEST_WGRAD256_CFG");
-    return v && std::string(v) == "32x4";
+    return !(v && std::string(v) == "64x2");
   }();
   const int KT = ring ? 32 : 64;
   if (M % 256 || N % 256 || K % KT || lda % 8 || ldb % 8 || S < 1) return hipErrorInvalidValue;

@@ -214,8 +214,30 @@ class FusedMlp3Trainer:
         C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg + ldg:],
                        self.w3slab, self.G[H * ldg:H * ldg + ldg], perm_h=H)   # dW2 slabs: register-native
 
+    def _local_only(self) -> bool:
+        """No gradient communication this step: no device comm, and all-reduce off or one rank."""
+        if self.comm is not None:
+            return False
+        if not self.allreduce:
+            return True
+        import torch.distributed as dist
+        return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
     def step(self, rec: torch.Tensor, tgt_norm: torch.Tensor) -> torch.Tensor:
-        """One optimizer step; returns the device tensor of per-row squared errors (no sync)."""
+        """One optimizer step; returns the device tensor of per-row squared errors (no sync).
+        Without gradient communication the slab reduction and AdamW run as ONE kernel
+        (reduce_adamw: same sums, same update, same bits as wgrad_reduce + adamw_pack);
+        ``ROUTEST_FUSED_ADAMW=0`` keeps them apart."""
+        if type(self) is FusedMlp3Trainer and self._local_only() and \
+                os.environ.get("ROUTEST_FUSED_ADAMW", "1") != "0":
+            C, H, h = self.C, self.H, self.hp
+            C.eta_mlp3_train_fwd(rec, tgt_norm, self.blob, H, self.norm, 2.0 / self.global_batch,
+                                 self.xf, self.w3slab, self.dz2r, self.sq_err, self.step_ctr)
+            C.train_bwd(self.xf, rec.shape[0], self.blob, H, self.dz2r, self.slab2, self.slab)
+            C.reduce_adamw(self.slab2, self.slab, self.w3slab, self.P, self.G, self.M, self.V, self.blob,
+                           self.step_ctr, H, h["lr"], h["beta1"], h["beta2"], h["eps"], h["wd"],
+                           h["warmup"], h["total_steps"], h["min_lr_ratio"])
+            return self.sq_err
         self.forward_backward(rec, tgt_norm)
         if self.comm is not None:
             self.comm.all_reduce(self.G)
@@ -292,11 +314,12 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
         nblk = -(-ntt // nt)
         ncu = self.C.num_cus(d.index if d.index is not None else 0)
         # the 256 x 256 output-tile kernel (wgrad.hip wgrad256_kernel): (H/256)^2 tiles per k-slice and
-        # enough slices for one workgroup per CU; db2 rides along (ROUTEST_WGRAD256=0: the n-blocked
-        # wgrad_kernel)
+        # enough slices for one workgroup per CU; db2 rides along.  Default since run r6g: 159-173 us
+        # against 214 us for the n-blocked wgrad_kernel at H = 1024, 64k rows (profiles/wgrad256_r6.md);
+        # ROUTEST_WGRAD256=0 keeps the latter
         import os
         self.wg256 = (H % 256 == 0 and B % 64 == 0 and hasattr(self.C, "wgrad256") and
-                      os.environ.get("ROUTEST_WGRAD256", "0") == "1")
+                      os.environ.get("ROUTEST_WGRAD256", "1") == "1")
         if self.wg256:
             self.S2 = max(1, min(B // 64, ncu // ((H // 256) ** 2)))
             # (zeros: the bucket's pad columns H+1 .. H+15 are never written by the kernel)

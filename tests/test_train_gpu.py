@@ -159,6 +159,30 @@ def test_graph_captured_step_matches_eager():
     torch.testing.assert_close(graphed.P, eager.P, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("H", [64, 128, 256])
+@pytest.mark.parametrize("B", [1000, 65536])
+def test_fused_reduce_adamw_bitwise_equals_two_kernels(H, B, monkeypatch):
+    """reduce_adamw (the one-rank step tail) == wgrad_reduce + adamw_pack, bit for bit: the
+    gradient bucket, the master weights, both moments and the training blob, over 4 steps."""
+    m = _model(H, 5)
+    rt, yn = _batch(B, m, 6)
+    rt, yn = rt.to(DEV), yn.to(DEV)
+    kw = dict(lr=2e-3, weight_decay=0.01, warmup=2, total_steps=10, allreduce=False)
+    fused = FusedMlp3Trainer(copy.deepcopy(m), DEV, B, B, **kw)
+    split = FusedMlp3Trainer(copy.deepcopy(m), DEV, B, B, **kw)
+    assert fused._local_only()
+    for _ in range(4):
+        monkeypatch.setenv("ROUTEST_FUSED_ADAMW", "1")
+        fused.step(rt, yn)
+        monkeypatch.setenv("ROUTEST_FUSED_ADAMW", "0")
+        split.step(rt, yn)
+    torch.cuda.synchronize()
+    for name in ("G", "P", "M", "V", "blob", "step_ctr"):
+        a, b = getattr(fused, name), getattr(split, name)
+        assert torch.equal(a, b), name
+    assert not torch.equal(fused.P.cpu(), flatten_params(m))
+
+
 @pytest.mark.parametrize("K,M,Mout,N,S", [(65536, 256, 256, 272, 256), (1000, 256, 256, 272, 7),
                                            (4133, 8, 1, 272, 16), (777, 256, 200, 16, 3),
                                            (64, 64, 64, 96, 1)])
