@@ -196,7 +196,7 @@ void big_fused(torch::Tensor records, torch::Tensor w1q, torch::Tensor w2f, torc
 }
 
 void big_layer1(torch::Tensor records, torch::Tensor w1p, int64_t H, std::vector<double> norm,
-                torch::Tensor h1, c10::optional<torch::Tensor> xf) {
+                torch::Tensor h1, c10::optional<torch::Tensor> xf, c10::optional<torch::Tensor> mbits) {
   const int rb = record_bytes(records);
   const int64_t B = records.size(0);
   check_dev(w1p, "w1p");
@@ -210,10 +210,44 @@ void big_layer1(torch::Tensor records, torch::Tensor w1p, int64_t H, std::vector
     check_bf16(*xf, "xf", B, 16);
     xfp = xf->data_ptr();
   }
+  unsigned* mb = nullptr;
+  if (mbits.has_value() && mbits->defined()) {
+    check_dev(*mbits, "mbits");
+    TORCH_CHECK(mbits->scalar_type() == torch::kInt32 && mbits->dim() == 2 && mbits->is_contiguous() &&
+                    mbits->size(0) >= (B + 31) / 32 * 32 && mbits->size(1) == H / 32,
+                "mbits int32 [>= ceil(B/32)*32, H/32] (tiled [row/32][word][row%32])");
+    mb = reinterpret_cast<unsigned*>(mbits->data_ptr<int>());
+  }
   TORCH_CHECK(B < (1LL << 31) - 64, "batch too large");
   const c10::DeviceGuard guard(h1.device());
   RT_CHECK_HIP(rt::launch_big_layer1(kernel_ptr(records, "records"), rb, (int)B, w1p.data_ptr(), (int)H,
-                                     norm_params(norm), h1.data_ptr(), (int)h1.size(1), xfp, cur_stream(h1)));
+                                     norm_params(norm), h1.data_ptr(), (int)h1.size(1), xfp, cur_stream(h1), mb));
+}
+
+// dh1 = dz2 W2 (W = w2t [N][K], X = dz2 [M][K]) consumed by its epilogue: slab1[t] = the dW1 partial
+// (dh1 * relu'(z1))^T xf of batch rows [256 t, 256 t + 256), [N positions][16]
+void gemm_dgrad_dw1(torch::Tensor W, torch::Tensor X, int64_t N, int64_t M, int64_t K, torch::Tensor mbits,
+                    torch::Tensor xf, torch::Tensor slab1) {
+  for (auto* t : {&W, &X, &xf}) {
+    check_dev(*t, "operand");
+    TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->dim() == 2 && t->is_contiguous(), "bf16 2-D contiguous");
+  }
+  TORCH_CHECK(W.size(0) >= N && W.size(1) >= K && X.size(0) >= M && X.size(1) >= K, "operand shapes");
+  TORCH_CHECK(N % 256 == 0 && K % 64 == 0, "N % 256 == 0 and K % 64 == 0 required");
+  check_dev(mbits, "mbits");
+  TORCH_CHECK(mbits.scalar_type() == torch::kInt32 && mbits.dim() == 2 && mbits.is_contiguous() &&
+                  mbits.size(0) >= (M + 31) / 32 * 32 && mbits.size(1) == N / 32,
+              "mbits int32 [>= ceil(M/32)*32, N/32] (big_layer1's tiled relu bit mask)");
+  TORCH_CHECK(xf.size(0) >= M && xf.size(1) == 16, "xf bf16 [>=M, 16]");
+  check_dev(slab1, "slab1");
+  TORCH_CHECK(slab1.scalar_type() == torch::kFloat32 && slab1.dim() == 2 && slab1.is_contiguous() &&
+                  slab1.size(0) >= (M + 255) / 256 && slab1.size(1) >= 16 * N,
+              "slab1 f32 [>= ceil(M/256), >= 16 N]");
+  TORCH_CHECK(M < (1LL << 31) - 256, "M too large");
+  const c10::DeviceGuard guard(W.device());
+  RT_CHECK_HIP(rt::launch_gemm_dgrad_dw1(W.data_ptr(), (int)W.size(1), X.data_ptr(), (int)X.size(1), (int)N, (int)M,
+                                         (int)K, reinterpret_cast<const unsigned*>(mbits.data_ptr<int>()), xf.data_ptr(),
+                                         slab1.data_ptr<float>(), (long long)slab1.size(1), cur_stream(W)));
 }
 
 // epi 0: ypart = relu(W X^T + b2) . w3 per 64-unit block; 1: + h2 stored into out; 2: out = W X^T
@@ -1376,8 +1410,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("route_greedy_cvrp", &route_greedy_cvrp, "K6: batched greedy multi-trip CVRP");
   m.def("big_layer1", &big_layer1, "wide MLP: featurize + layer 1 -> h1 (hperm order)",
         py::arg("records"), py::arg("w1p"), py::arg("H"), py::arg("norm"), py::arg("h1"),
-        py::arg("xf") = py::none());
+        py::arg("xf") = py::none(), py::arg("mbits") = py::none());
   m.def("big_fused", &big_fused, "wide MLP inference: featurize + layer 1 + layer 2 + relu.w3 partials, one launch");
+  m.def("gemm_dgrad_dw1", &gemm_dgrad_dw1, "training dgrad with the dW1 partials in its epilogue (dh1 not stored)");
   m.def("gemm_nt", &gemm_nt, "wide MLP layer GEMM Z^T = W X^T with fused epilogues (0 y-partials, 1 +h2, 2 store)",
         py::arg("epi"), py::arg("W"), py::arg("X"), py::arg("N"), py::arg("M"), py::arg("K"),
         py::arg("b2") = py::none(), py::arg("w3") = py::none(), py::arg("ypart") = py::none(),

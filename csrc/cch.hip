@@ -293,6 +293,52 @@ __device__ __forceinline__ void pull_cand(const PullArgs& P, long long tb, int k
   bd = cd < bd ? cd : bd;
 }
 
+// The wave's minimum over candidate chunks c_begin, c_begin + c_step, ... of arc (x -> y) = x's arc
+// ia (x: arcs a0 .. a0 + k, triangle rows at tb): four 64-wide chunks of candidates per step, every
+// stage's loads issued together (the serial tri -> weight chain of a high-degree node's ~22 chunks
+// was the kernel's latency); bu / bd are reduced over the wave.
+__device__ __forceinline__ void pull_arc_min(const PullArgs& P, long long tb, int a0, int k, int ia, int y, int c_begin,
+                                             int c_step, int lane, const unsigned long long* __restrict__ up,
+                                             const unsigned long long* __restrict__ dn, const uint32_t* __restrict__ pup,
+                                             const uint32_t* __restrict__ pdn, float& bu, float& bd) {
+  for (int c0 = c_begin; c0 < k; c0 += c_step) {
+    int azy[4], z[4];
+    unsigned long long wu[4], wd[4];
+    bool ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ic = c0 + 64 * u + lane;
+      ok[u] = ic < k && ic != ia;
+      const int i = ic < ia ? ic : ia, j = ic < ia ? ia : ic;
+      azy[u] = ok[u] ? P.tri[tb + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)] : 0;
+      z[u] = ok[u] ? P.up_head[a0 + ic] : 0;
+      wu[u] = ok[u] ? up[a0 + ic] : 0ull;
+      wd[u] = ok[u] ? dn[a0 + ic] : 0ull;
+    }
+    uint32_t gu[4], gd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      gu[u] = ok[u] ? pup[azy[u]] : 0u;
+      gd[u] = ok[u] ? pdn[azy[u]] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!ok[u]) continue;
+      const float zy = __uint_as_float(z[u] < y ? gu[u] : gd[u]);
+      const float yz = __uint_as_float(z[u] < y ? gd[u] : gu[u]);
+      const float cu = wof(wu[u]) + zy, cd = yz + wof(wd[u]);
+      bu = cu < bu ? cu : bu;
+      bd = cd < bd ? cd : bd;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ou = __shfl_xor(bu, o), od = __shfl_xor(bd, o);
+    bu = ou < bu ? ou : bu;
+    bd = od < bd ? od : bd;
+  }
+}
+
 // S waves per arc (4 / S arcs per workgroup), lanes over the node's other arcs, wave `part` of an
 // arc taking candidate chunks part, part + S, ... (levels of high-degree nodes: the top separators,
 // k up to ~1400 on the 1M-node city — one wave walked ~6 chunks of 256 candidates one after the
@@ -332,44 +378,7 @@ __global__ __launch_bounds__(256) void perfect_pull_wave_kernel(PullArgs P, cons
       y = P.up_head[aa];
       tb = P.tofs[x];
     }
-    // four 64-wide chunks of candidates per step, every stage's loads issued together (the serial
-    // tri -> weight chain of a high-degree node's ~22 chunks was the kernel's latency)
-    for (int c0 = 256 * part; c0 < k; c0 += 256 * S) {
-      int azy[4], z[4];
-      unsigned long long wu[4], wd[4];
-      bool ok[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int ic = c0 + 64 * u + lane;
-        ok[u] = ic < k && ic != ia;
-        const int i = ic < ia ? ic : ia, j = ic < ia ? ia : ic;
-        azy[u] = ok[u] ? P.tri[tb + (long long)i * (2 * k - i - 1) / 2 + (j - i - 1)] : 0;
-        z[u] = ok[u] ? P.up_head[a0 + ic] : 0;
-        wu[u] = ok[u] ? up[a0 + ic] : 0ull;
-        wd[u] = ok[u] ? dn[a0 + ic] : 0ull;
-      }
-      uint32_t gu[4], gd[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        gu[u] = ok[u] ? pup[azy[u]] : 0u;
-        gd[u] = ok[u] ? pdn[azy[u]] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (!ok[u]) continue;
-        const float zy = __uint_as_float(z[u] < y ? gu[u] : gd[u]);
-        const float yz = __uint_as_float(z[u] < y ? gd[u] : gu[u]);
-        const float cu = wof(wu[u]) + zy, cd = yz + wof(wd[u]);
-        bu = cu < bu ? cu : bu;
-        bd = cd < bd ? cd : bd;
-      }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const float ou = __shfl_xor(bu, o), od = __shfl_xor(bd, o);
-      bu = ou < bu ? ou : bu;
-      bd = od < bd ? od : bd;
-    }
+    pull_arc_min(P, tb, a0, k, ia, y, 256 * part, 256 * S, lane, up, dn, pup, pdn, bu, bd);
   }
   if constexpr (S > 1) {
     if (lane == 0) {
@@ -427,6 +436,60 @@ __global__ __launch_bounds__(256) void perfect_pull_lane_kernel(PullArgs P, cons
   pdn[aa] = __float_as_uint(bd);
 }
 
+// The narrow top of the perfect phase (depths 0 .. d_tail - 1, each <= ROUTEST_CCH_TAIL arcs: the
+// top separators' chains) in ONE launch: a wave per arc at a time, taken in depth order from a global
+// cursor, the same bounded relaxed-poll dependency wait and loop shape as basic_tail_kernel (below).
+// ctl: [0] cursor, [1] timed out, [2 ..] done per depth.
+__global__ __launch_bounds__(256) void perfect_tail_kernel(PullArgs P, int narcs, const int* __restrict__ lvl_end, int nlev,
+                                                           int* __restrict__ ctl, long long max_ticks,
+                                                           const unsigned long long* __restrict__ up,
+                                                           const unsigned long long* __restrict__ dn,
+                                                           uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+  const int lane = threadIdx.x & 63;
+  int* cursor = ctl;
+  int* fail = ctl + 1;
+  int* done = ctl + 2;
+  int lev = 0, prev = -1;
+  while (true) {
+    int got = 0;
+    if (lane == 0) {
+      if (prev >= 0) __hip_atomic_fetch_add(done + prev, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      got = atomicAdd(cursor, 1);
+    }
+    const int ti = __builtin_amdgcn_readlane(got, 0);
+    if (ti >= narcs) break;
+    while (lev < nlev - 1 && ti >= lvl_end[lev]) ++lev;
+    if (lev > 0) {
+      int f = 0;
+      if (lane == 0) {
+        const int need = lvl_end[lev - 1] - (lev >= 2 ? lvl_end[lev - 2] : 0);
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(done + lev - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+          if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+              (long long)__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) {
+            __hip_atomic_fetch_or(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            f = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      }
+      if (__builtin_amdgcn_readlane(f, 0)) break;
+    }
+    const PArc pa = P.parc[P.base + ti];
+    const int aa = pa.a0 + pa.ia;
+    float bu = F_INF, bd = F_INF;
+    pull_arc_min(P, pa.tb, pa.a0, pa.k, pa.ia, pa.y, 0, 256, lane, up, dn, pup, pdn, bu, bd);
+    if (lane == 0) {
+      const float cu = __uint_as_float(pup[aa]), cd = __uint_as_float(pdn[aa]);
+      if (bu < cu) pup[aa] = __float_as_uint(bu);
+      if (bd < cd) pdn[aa] = __float_as_uint(bd);
+    }
+    prev = lev;
+  }
+}
+
 // ---- task-table customization (round 5) ----
 // A wave's work is one precomputed, metric-independent TASK (8 bytes, built once per graph in level
 // order): {node, row/arc index, first column}; its 64 lanes take 64 consecutive columns.  That
@@ -460,19 +523,13 @@ static_assert(sizeof(BasicTask) == 24, "basic task layout");
 // z's own arcs (best triangle's two sub-arcs, metres, road-edge counts).  Same math as
 // basic_level_kernel (bit-identical).
 template <bool SKIP>
-__global__ __launch_bounds__(256) void basic_task_kernel(const BasicTask* __restrict__ tasks, long long ntask,
-                                                         const int32_t* __restrict__ up_ptr,
-                                                         const int32_t* __restrict__ up_head,
-                                                         const int64_t* __restrict__ tofs, const int32_t* __restrict__ tri,
-                                                         unsigned long long* __restrict__ up,
-                                                         unsigned long long* __restrict__ dn, int32_t* __restrict__ sub_up,
-                                                         int32_t* __restrict__ sub_dn, float* __restrict__ len_up,
-                                                         float* __restrict__ len_dn, int32_t* __restrict__ cnt_up,
-                                                         int32_t* __restrict__ cnt_dn, const float* __restrict__ length) {
-  const long long ti = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (ti >= ntask) return;
-  const int lane = threadIdx.x & 63;
-  const BasicTask T = tasks[ti];
+__device__ __forceinline__ void basic_task_run(const BasicTask& T, int lane, const int32_t* __restrict__ up_ptr,
+                                               const int32_t* __restrict__ up_head,
+                                               const int32_t* __restrict__ tri, unsigned long long* __restrict__ up,
+                                               unsigned long long* __restrict__ dn, int32_t* __restrict__ sub_up,
+                                               int32_t* __restrict__ sub_dn, float* __restrict__ len_up,
+                                               float* __restrict__ len_dn, int32_t* __restrict__ cnt_up,
+                                               int32_t* __restrict__ cnt_dn, const float* __restrict__ length) {
   const int z = T.node;
   const int a0 = T.a0;
   const int k = T.k;
@@ -528,6 +585,89 @@ __global__ __launch_bounds__(256) void basic_task_kernel(const BasicTask* __rest
   if (wd < F_INF) {
     const unsigned long long pd = packw(wd, (uint32_t)z);
     if (!SKIP || pd < dn[t]) atomicMin(dn + t, pd);
+  }
+}
+
+template <bool SKIP>
+__global__ __launch_bounds__(256) void basic_task_kernel(const BasicTask* __restrict__ tasks, long long ntask,
+                                                         const int32_t* __restrict__ up_ptr,
+                                                         const int32_t* __restrict__ up_head,
+                                                         const int64_t* __restrict__ tofs, const int32_t* __restrict__ tri,
+                                                         unsigned long long* __restrict__ up,
+                                                         unsigned long long* __restrict__ dn, int32_t* __restrict__ sub_up,
+                                                         int32_t* __restrict__ sub_dn, float* __restrict__ len_up,
+                                                         float* __restrict__ len_dn, int32_t* __restrict__ cnt_up,
+                                                         int32_t* __restrict__ cnt_dn, const float* __restrict__ length) {
+  const long long ti = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ti >= ntask) return;
+  (void)tofs;
+  basic_task_run<SKIP>(tasks[ti], threadIdx.x & 63, up_ptr, up_head, tri, up, dn, sub_up, sub_dn, len_up, len_dn,
+                       cnt_up, cnt_dn, length);
+}
+
+// The narrow top of the basic phase in ONE launch (round 6): the levels
+// [h_tail, max_height] each hold few tasks (the top separator's chain: one node per level), and as
+// separate kernels each cost a dependent launch (~2.6 us) plus its ramp, ~12 us per level in all
+// (profiles/cch_customize_r5.md).  Here every WAVE is an independent worker: lane 0 takes the next
+// task index from a global cursor (tasks in level order), and before a task of tail level l > 0 waits
+// until every task of level l - 1 is done (done[l - 1] == its task count), polling with RELAXED
+// agent-scope loads and one acquire fence after (an acquire poll invalidates the XCD's L2 on every
+// iteration); finishing a task is a release increment of done[l].  Deadlock-free without co-residency:
+// a waiting wave only waits for tasks taken earlier, by running waves, down to level 0, whose
+// predecessors ran in earlier launches.  Every wait is bounded by wall clock (s_memrealtime, 100 MHz):
+// on expiry ctl[1] is set, every wave leaves, and the host reports the customization failed.
+// The loop's exits test wave-uniform values, and lane 0's release of one task and fetch of the next
+// are ONE block before the loop's work: lane-0 code on both sides of the back edge lets the AMDGPU
+// structurizer split the loop per lane, which livelocked the r5t work-queue probe
+// (tools/probes/kernel_chain_probe.hip).  ctl: [0] cursor, [1] timed out, [2 ..] done per tail level.
+template <bool SKIP>
+__global__ __launch_bounds__(256) void basic_tail_kernel(const BasicTask* __restrict__ tasks, int ntask,
+                                                         const int* __restrict__ lvl_end, int nlev,
+                                                         int* __restrict__ ctl, long long max_ticks,
+                                                         const int32_t* __restrict__ up_ptr,
+                                                         const int32_t* __restrict__ up_head,
+                                                         const int32_t* __restrict__ tri,
+                                                         unsigned long long* __restrict__ up,
+                                                         unsigned long long* __restrict__ dn, int32_t* __restrict__ sub_up,
+                                                         int32_t* __restrict__ sub_dn, float* __restrict__ len_up,
+                                                         float* __restrict__ len_dn, int32_t* __restrict__ cnt_up,
+                                                         int32_t* __restrict__ cnt_dn, const float* __restrict__ length) {
+  const int lane = threadIdx.x & 63;
+  int* cursor = ctl;
+  int* fail = ctl + 1;
+  int* done = ctl + 2;
+  int lev = 0;             // tail level of the wave's current task (task indices only grow)
+  int prev = -1;           // tail level of the task finished in the previous iteration
+  while (true) {
+    int got = 0;
+    if (lane == 0) {
+      if (prev >= 0) __hip_atomic_fetch_add(done + prev, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      got = atomicAdd(cursor, 1);
+    }
+    const int ti = __builtin_amdgcn_readlane(got, 0);
+    if (ti >= ntask) break;
+    while (lev < nlev - 1 && ti >= lvl_end[lev]) ++lev;
+    if (lev > 0) {
+      int f = 0;
+      if (lane == 0) {
+        const int need = lvl_end[lev - 1] - (lev >= 2 ? lvl_end[lev - 2] : 0);
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(done + lev - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+          if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+              (long long)__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) {
+            __hip_atomic_fetch_or(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            f = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      }
+      if (__builtin_amdgcn_readlane(f, 0)) break;
+    }
+    basic_task_run<SKIP>(tasks[ti], lane, up_ptr, up_head, tri, up, dn, sub_up, sub_dn, len_up, len_dn, cnt_up,
+                         cnt_dn, length);
+    prev = lev;
   }
 }
 
@@ -1390,6 +1530,29 @@ void CchGpu::build_pull_records(const std::vector<int64_t>& tofs) {
     return;
   }
   d_parc = dp;
+  // the narrow top of the perfect phase: the longest prefix of depths with at most `thr` arcs each
+  // (ROUTEST_CCH_TAIL as for the basic phase)
+  const char* v = std::getenv("ROUTEST_CCH_TAIL");
+  const int64_t thr = v ? std::atoll(v) : 0;
+  int d = 0;
+  while (thr > 0 && d < T_.max_depth && aofs_[T_.dlev_ptr[d + 1]] - aofs_[T_.dlev_ptr[d]] <= thr) ++d;
+  if (d >= 2) {
+    std::vector<int> ends;
+    int64_t mx = 0;
+    const int64_t base = aofs_[T_.dlev_ptr[0]];
+    for (int l = 0; l < d; ++l) {
+      ends.push_back((int)(aofs_[T_.dlev_ptr[l + 1]] - base));
+      mx = std::max<int64_t>(mx, aofs_[T_.dlev_ptr[l + 1]] - aofs_[T_.dlev_ptr[l]]);
+    }
+    int* de = nullptr;
+    if (up_copy(de, ends.data(), ends.size()) == hipSuccess) {
+      d_ptail_end_ = de;
+      n_ptail_lev_ = d;
+      ptail_max_arcs_ = (int)mx;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
 }
 
 void CchGpu::build_tasks(const std::vector<int64_t>& tofs) {
@@ -1429,6 +1592,32 @@ void CchGpu::build_tasks(const std::vector<int64_t>& tofs) {
     ptask_ptr_[d + 1] = (int64_t)pt.size();
   }
   (void)N;
+  // the narrow top of the basic phase: the longest suffix of levels with at most `thr` tasks each
+  // (ROUTEST_CCH_TAIL=<tasks>; default 0: every level its own launch — run r6m: a 4096-task tail of
+  // 500 levels made the basic phase 11.4 -> 39.7 ms, profiles/cch_customize_r6.md)
+  {
+    const char* v = std::getenv("ROUTEST_CCH_TAIL");
+    const int64_t thr = v ? std::atoll(v) : 0;
+    int h = T_.max_height + 1;
+    while (thr > 0 && h > 1 && btask_ptr_[h] - btask_ptr_[h - 1] <= thr) --h;
+    if (thr > 0 && h <= T_.max_height && !bt.empty()) {
+      std::vector<int> ends;
+      int64_t mx = 0;
+      for (int l = h; l <= T_.max_height; ++l) {
+        ends.push_back((int)(btask_ptr_[l + 1] - btask_ptr_[h]));
+        mx = std::max<int64_t>(mx, btask_ptr_[l + 1] - btask_ptr_[l]);
+      }
+      int* d = nullptr;
+      if (up_copy(d, ends.data(), ends.size()) == hipSuccess) {
+        d_tail_end_ = d;
+        h_tail_ = h;
+        n_tail_lev_ = (int)ends.size();
+        tail_max_tasks_ = (int)mx;
+      } else {
+        (void)hipGetLastError();
+      }
+    }
+  }
   BasicTask* db = nullptr;
   CustTask* dp = nullptr;
   const bool ok = up_copy(db, bt.data(), bt.size()) == hipSuccess && up_copy(dp, pt.data(), pt.size()) == hipSuccess;
@@ -1483,6 +1672,8 @@ CchGpu::~CchGpu() {
   dfree(d_tri);
   dfree(d_btask);
   dfree(d_ptask);
+  dfree(d_tail_end_);
+  dfree(d_ptail_end_);
   free_scratch(cs0_);
   (void)hipSetDevice(cur);
 }
@@ -1514,6 +1705,9 @@ hipError_t CchGpu::alloc_scratch(CustScratch& x) {
   x.cub_bytes = tb;
   ck(hipMalloc(&x.cub, x.cub_bytes ? x.cub_bytes : 1));
   ck(hipHostMalloc((void**)&x.h_stage, (size_t)std::max<int64_t>(1, T_.E) * sizeof(float), hipHostMallocDefault));
+  ck(dmalloc(x.tail_ctl, (size_t)T_.max_height + (size_t)T_.max_depth + 8));   // basic | perfect tail
+  if (x.tail_ctl != nullptr)
+    ck(hipMemset(x.tail_ctl, 0, ((size_t)T_.max_height + (size_t)T_.max_depth + 8) * sizeof(int)));
   return e;
 }
 
@@ -1531,6 +1725,7 @@ void CchGpu::free_scratch(CustScratch& x) {
   dfree(x.min_buf);
   if (x.h_stage) (void)hipHostFree(x.h_stage);
   x.h_stage = nullptr;
+  dfree(x.tail_ctl);
 }
 
 hipError_t CchGpu::context_costs(const CchContext& c, float* d_cost, hipStream_t s, CustScratch* cs) {
@@ -1622,7 +1817,9 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     // workgroups of memory traffic in flight next to the flushes' query kernels)
     const int max_wg = paced ? std::max(0, builder_max_wg_.load(std::memory_order_relaxed)) : 0;
     const long long wave_cap = max_wg > 0 ? 4LL * max_wg : (1LL << 40);
-    for (int h = 0; h <= T_.max_height && e == hipSuccess && tasks; ++h) {
+    const bool tail = tasks && h_tail_ >= 0 && X.tail_ctl != nullptr;
+    const int h_end = tail ? h_tail_ - 1 : T_.max_height;
+    for (int h = 0; h <= h_end && e == hipSuccess && tasks; ++h) {
       const long long ntl = btask_ptr_[h + 1] - btask_ptr_[h];
       for (long long t0 = 0; t0 < ntl && e == hipSuccess; t0 += wave_cap) {
         const long long nt = std::min(wave_cap, ntl - t0);
@@ -1637,6 +1834,24 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
                              m.cnt_dn, d_length);
         ck(hipGetLastError());
       }
+    }
+    if (tail && e == hipSuccess) {
+      // the narrow top levels: one persistent launch (basic_tail_kernel), a wave per task at a time
+      const int ntask = (int)(btask_ptr_[T_.max_height + 1] - btask_ptr_[h_tail_]);
+      int blocks = std::max(1, std::min(256, (tail_max_tasks_ + 3) / 4));
+      if (max_wg > 0) blocks = std::min(blocks, max_wg);
+      const long long max_ticks = 100LL * 1000 * 1000;     // 1 s of the 100 MHz clock per wait
+      ck(hipMemsetAsync(X.tail_ctl, 0, ((size_t)n_tail_lev_ + 2) * sizeof(int), s));
+      const BasicTask* tk = (const BasicTask*)d_btask + btask_ptr_[h_tail_];
+      if (skip)
+        hipLaunchKernelGGL(basic_tail_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, tk, ntask, d_tail_end_,
+                           n_tail_lev_, X.tail_ctl, max_ticks, d_up_ptr, d_up_head, d_tri, X.up64, X.dn64, m.sub_up,
+                           m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
+      else
+        hipLaunchKernelGGL(basic_tail_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, tk, ntask, d_tail_end_,
+                           n_tail_lev_, X.tail_ctl, max_ticks, d_up_ptr, d_up_head, d_tri, X.up64, X.dn64, m.sub_up,
+                           m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
+      ck(hipGetLastError());
     }
     for (int h = 0; h <= T_.max_height && e == hipSuccess && !tasks; ++h) {
       LevelArgs L{d_up_ptr, d_up_head, d_hnodes, d_bofs, (int)T_.hlev_ptr[h], (int)T_.hlev_ptr[h + 1], 0, 0, d_tofs, d_tri};
@@ -1676,7 +1891,22 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
                          X.pup, X.pdn);
       ck(hipGetLastError());
     }
-    for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && pull && d_tri != nullptr; ++d) {
+    // the narrow top depths: one persistent launch (perfect_tail_kernel), a wave per arc at a time
+    const bool ptail = !(tasks && ptasks) && pull && d_tri != nullptr && d_parc != nullptr && n_ptail_lev_ > 0 &&
+                       X.tail_ctl != nullptr;
+    if (ptail && e == hipSuccess) {
+      int* pctl = X.tail_ctl + T_.max_height + 4;
+      const int lo = (int)T_.dlev_ptr[0], hi = (int)T_.dlev_ptr[n_ptail_lev_];
+      PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri,
+                 (const PArc*)d_parc};
+      int blocks = std::max(1, std::min(256, (ptail_max_arcs_ + 3) / 4));
+      if (max_wg > 0) blocks = std::min(blocks, max_wg);
+      ck(hipMemsetAsync(pctl, 0, ((size_t)n_ptail_lev_ + 2) * sizeof(int), s));
+      hipLaunchKernelGGL(perfect_tail_kernel, dim3((unsigned)blocks), dim3(256), 0, s, P, (int)P.arcs, d_ptail_end_,
+                         n_ptail_lev_, pctl, 100LL * 1000 * 1000, X.up64, X.dn64, X.pup, X.pdn);
+      ck(hipGetLastError());
+    }
+    for (int d = ptail ? n_ptail_lev_ : 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && pull && d_tri != nullptr; ++d) {
       const int lo = (int)T_.dlev_ptr[d], hi = (int)T_.dlev_ptr[d + 1];
       if (lo >= hi) continue;
       PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri,
@@ -1738,10 +1968,19 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
   ck(hipcub::DeviceScan::InclusiveSum(X.cub, tb, X.fcnt, m.f_ptr + 1, N, s));
   tb = X.cub_bytes;
   ck(hipcub::DeviceScan::InclusiveSum(X.cub, tb, X.bcnt, m.b_ptr + 1, N, s));
-  int32_t tot[2] = {0, 0};
+  int32_t tot[4] = {0, 0, 0, 0};
   ck(hipMemcpyAsync(&tot[0], m.f_ptr + N, 4, hipMemcpyDeviceToHost, s));
   ck(hipMemcpyAsync(&tot[1], m.b_ptr + N, 4, hipMemcpyDeviceToHost, s));
+  if (X.tail_ctl != nullptr) {      // the tails' timed-out flags (zeroed at allocation; set only on expiry)
+    ck(hipMemcpyAsync(&tot[2], X.tail_ctl + 1, 4, hipMemcpyDeviceToHost, s));
+    ck(hipMemcpyAsync(&tot[3], X.tail_ctl + T_.max_height + 5, 4, hipMemcpyDeviceToHost, s));
+  }
   ck(hipStreamSynchronize(s));
+  if (e == hipSuccess && (tot[2] != 0 || tot[3] != 0)) {
+    std::fprintf(stderr, "[cch] %s tail kernel: a level wait exceeded its bound; customization failed\n",
+                 tot[2] ? "basic" : "perfect");
+    e = hipErrorLaunchTimeOut;
+  }
   if (e != hipSuccess) return e;
   if (tot[0] > m.kept_f || m.f_rec == nullptr) {
     dfree(m.f_rec);

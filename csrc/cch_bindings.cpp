@@ -90,6 +90,8 @@ class PyCchGpu {
     d["triangle_table"] = g_->has_triangle_table();
     d["triangles"] = g_->triangles();
     d["basic_tasks"] = g_->basic_tasks();
+    d["basic_tail_levels"] = g_->basic_tail_levels();
+    d["perfect_tail_levels"] = g_->perfect_tail_levels();
     d["perfect_tasks"] = g_->perfect_tasks();
     d["cache_capacity"] = g_->capacity();
     d["cache_gb"] = g_->cache_gb();

@@ -88,6 +88,7 @@ struct CustScratch {
   void* rec_buf = nullptr;                         // context cost records [2E]
   float* min_buf = nullptr;                        // their minutes [2E]
   float* h_stage = nullptr;                        // pinned [E]: the costs' host copy lands here first
+  int* tail_ctl = nullptr;                         // basic_tail_kernel: cursor, timed-out flag, done[level]
 };
 
 // The device pointers of one metric that the query kernels read — an array of these plus a group
@@ -129,6 +130,8 @@ class CchGpu {
   bool has_triangle_table() const { return d_tri != nullptr; }
   int64_t triangles() const { return n_tri; }
   int64_t basic_tasks() const { return n_btask_; }
+  int basic_tail_levels() const { return n_tail_lev_; }   // top basic levels run by ONE persistent launch
+  int perfect_tail_levels() const { return n_ptail_lev_; }  // top perfect depths run by ONE persistent launch
   int64_t perfect_tasks() const { return n_ptask_; }
 
   // ETA model used for context costs (the fused K1+K2 kernel's 32x32 blob on this device)
@@ -265,6 +268,13 @@ class CchGpu {
   void* d_ptask = nullptr;
   std::vector<int64_t> btask_ptr_, ptask_ptr_;
   int64_t n_btask_ = 0, n_ptask_ = 0;
+  // the basic phase's narrow top (levels h_tail_ .. max_height, each <= ROUTEST_CCH_TAIL tasks):
+  // basic_tail_kernel, d_tail_end_[l] = end of tail level l's tasks (relative to h_tail_'s first)
+  int h_tail_ = -1, n_tail_lev_ = 0, tail_max_tasks_ = 0;
+  int* d_tail_end_ = nullptr;
+  // ... and of the perfect phase (depths 0 .. n_ptail_lev_ - 1): perfect_tail_kernel over their arcs
+  int n_ptail_lev_ = 0, ptail_max_arcs_ = 0;
+  int* d_ptail_end_ = nullptr;
   // customization temporaries: cs0_ for callers on their own streams (one at a time: mu_cust_),
   // one set per background builder (no lock: each builder owns its set)
   hipError_t alloc_scratch(CustScratch& x);

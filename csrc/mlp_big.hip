@@ -63,7 +63,8 @@ template <int RB>
 __global__ __launch_bounds__(256) void big_layer1_kernel(const void* __restrict__ rec, int B,
                                                          const bf16x8* __restrict__ w1p, int H,
                                                          NormParams np, __bf16* __restrict__ h1,
-                                                         int ld, __bf16* __restrict__ xf) {
+                                                         int ld, __bf16* __restrict__ xf,
+                                                         unsigned* __restrict__ mbits) {
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int row = tile * 32 + r;
@@ -93,6 +94,17 @@ __global__ __launch_bounds__(256) void big_layer1_kernel(const void* __restrict_
       *reinterpret_cast<bf16x8*>(out + 32 * mt + 8 * h) = v0;
       *reinterpret_cast<bf16x8*>(out + 32 * mt + 16 + 8 * h) = v1;
     }
+    if (mbits != nullptr) {             // relu'(z1) of positions 32mt .. 32mt + 31 as one word per row,
+      unsigned bits = 0;                // from the stored bf16 values (the dgrad epilogue's mask)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        bits |= ((float)v0[k] > 0.f ? 1u : 0u) << (8 * h + k);
+        bits |= ((float)v1[k] > 0.f ? 1u : 0u) << (16 + 8 * h + k);
+      }
+      bits |= (unsigned)__shfl_xor((int)bits, 32);
+      // tiled [row / 32][mt][row % 32]: the 32 rows of this tile store 128 contiguous bytes per mt
+      if (valid && h == 0) mbits[((size_t)tile * (H / 32) + mt) * 32 + r] = bits;
+    }
   }
   if (xf != nullptr && valid && ld > H) {                       // h1a ones-column (db2 input)
     bf16x8 t;
@@ -105,7 +117,7 @@ __global__ __launch_bounds__(256) void big_layer1_kernel(const void* __restrict_
 
 constexpr int GT = 128;          // tile rows (units) and columns (batch rows)
 constexpr int GK = 32;           // K per LDS stage
-constexpr int EPI_Y = 0, EPI_H2Y = 1, EPI_STORE = 2;
+constexpr int EPI_Y = 0, EPI_H2Y = 1, EPI_STORE = 2, EPI_DW1 = 3;
 
 // LDS tile: 128 rows x 64 bytes; 16-byte chunk c of row r at slot c ^ ((r >> 2) & 3) — the 16
 // rows a ds_read_b128 lane group reads (lanes {0-3,12-15,20-27} etc.) hit 16 distinct slots.
@@ -122,6 +134,13 @@ struct GemmArgs {
   int ldo;
   int tiles_n;       // N / 128
   int st16;          // 256 x 256 epilogue: 16-byte row pieces (1) or 8-byte (0; ROUTEST_GEMM_ST16 A/B knob)
+  // EPI_DW1 (256 x 256 loops only): relu' bit mask, words tiled [M / 32][N / 32][32 rows] (bit p % 32
+  // of word p / 32 = hperm position p, written by big_layer1), features xf [M][16] and the dW1 slab
+  // [M / 256 row tiles][N * 16] (position-major, 16 features)
+  const unsigned* mbits = nullptr;
+  const __bf16* xf = nullptr;
+  float* slab1 = nullptr;
+  long long slab1_ld = 0;
 };
 
 template <int EPI>
@@ -282,13 +301,86 @@ __device__ __forceinline__ void g256_store_pair(__bf16* row, int p, int gp, bool
   *reinterpret_cast<u32x4*>(row + 16 * (2 * p + (hi ? 1 : 0)) + 4 * (hi ? gp - 1 : gp)) = v;
 }
 
+// EPI_DW1: the training dgrad dh1 = dz2 W2 consumed in place.  dh1 is needed only for dW1 =
+// (dh1 * relu'(z1))^T [x | 1], so instead of storing it (128 MB at H = 1024, 64k rows) and re-reading it
+// with the mask in a wgrad launch (61 us, profiles/train_h1024_64k_kernel_stats_r6h.csv), the tile
+// rounds it to bf16 exactly as the store did, masks it with h1a, and multiplies it by the tile's 256
+// feature rows on MFMA: one [256 positions][16] partial per row tile, summed by wgrad_reduce.
+//   LDS (the K loop's buffers, free after a barrier): zt [256 positions][256 k] bf16 and xt [16][256 k]
+//   bf16, 512-byte rows, 16-byte chunk ch of row r at slot ch ^ (r & 31) (the 16 rows one fragment
+//   read touches land in 16 distinct slots).  k orders the tile's rows so a lane's 4 rows of one
+//   position are adjacent: row 64wr + 16j + fr -> k = 64wr + 4fr + j (any order works: A and B agree).
+constexpr int DW1_ZT = 256 * 512, DW1_LDS = DW1_ZT + 16 * 512;
+__device__ __forceinline__ int dw1_off(int r, int k) { return r * 512 + ((((k >> 3) ^ (r & 31))) << 4) + ((k & 7) << 1); }
+
 template <int EPI>
 __device__ __forceinline__ void g256_epilogue(const GemmArgs& a, f32x4 (&acc)[8][4], int n0, int m0, int wu,
-                                              int wr, int lane) {
+                                              int wr, int lane, unsigned char* lds = nullptr) {
   const int fr = lane & 15, g = lane >> 4, gp = ((g & 1) << 1) | (g >> 1);
   const bool hi = lane >= 32;
   const int ub = n0 + 128 * wu;
-  if constexpr (EPI == EPI_STORE) {
+  if constexpr (EPI == EPI_DW1) {
+    const int tid = threadIdx.x;
+    // global loads first (they do not touch LDS): the tile's features and the relu' mask words
+    // feature row t >> 1, features 8 (t & 1) .. + 7 (rows past M: zeros)
+    const int xr = tid >> 1, xh = tid & 1;
+    bf16x8 xv;
+    if (m0 + xr < a.M) {
+      xv = *reinterpret_cast<const bf16x8*>(a.xf + (size_t)(m0 + xr) * 16 + 8 * xh);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) xv[q] = (__bf16)0.f;
+    }
+    // relu'(z1) of position 128wu + 16i + 4gp + e: word (ub >> 5) + i / 2 of row m, bit 16 (i & 1) +
+    // 4gp + e; words tiled [m / 32][word][m % 32] (big_layer1): 16 lanes read 64 contiguous bytes
+    const int wpr = a.N / 32;
+    unsigned mk[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + 64 * wr + 16 * j + fr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        mk[j][q] = m < a.M ? a.mbits[((size_t)(m >> 5) * wpr + (ub >> 5) + q) * 32 + (m & 31)] : 0u;
+    }
+    __syncthreads();                                      // every wave is past its last K-loop read
+    {
+      const int k = 64 * (xr >> 6) + 4 * (xr & 15) + ((xr >> 4) & 3);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) *reinterpret_cast<__bf16*>(lds + DW1_ZT + dw1_off(8 * xh + q, k)) = xv[q];
+    }
+    // dz1 = bf16(dh1) * relu'(z1), rows j = 0..3 of a position -> 4 adjacent k
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int bit = 16 * (i & 1) + 4 * gp + e;
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (mk[j][i >> 1] >> bit) & 1u ? (__bf16)acc[i][j][e] : (__bf16)0.f;
+        const int pl = 128 * wu + 16 * i + 4 * gp + e;
+        *reinterpret_cast<bf16x4*>(lds + dw1_off(pl, 64 * wr + 4 * fr)) = v;
+      }
+    }
+    __syncthreads();
+    // [256 positions][16] = zt (A: 16 positions x 32 k) x xt^T (B: 32 k x 16 features); wave w: position
+    // blocks 2w, 2w + 1
+    const int w = tid >> 6;
+    float* orow = a.slab1 + (size_t)(m0 / 256) * a.slab1_ld + (size_t)n0 * 16;
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) {
+      const int pb = 16 * (2 * w + bb);
+      f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const int k = 32 * kk + 8 * g;
+        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(lds + dw1_off(pb + fr, k));
+        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(lds + DW1_ZT + dw1_off(fr, k));
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, d, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) orow[(pb + 4 * g + e) * 16 + fr] = d[e];
+    }
+  } else if constexpr (EPI == EPI_STORE) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + 64 * wr + 16 * j + fr;
@@ -421,7 +513,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs a) {
     __syncthreads();                                    // ... and stage k fully read
   }
 
-  g256_epilogue<EPI>(a, acc, n0, m0, wu, wr, lane);
+  g256_epilogue<EPI>(a, acc, n0, m0, wu, wr, lane, sm2);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -571,7 +663,7 @@ __global__ __launch_bounds__(512, 1) void gemm256p_kernel(GemmArgs a) {
     quad(1, 0);
   }
   if (wu == 0) GP_BARRIER();                          // equal barrier counts on exit
-  g256_epilogue<EPI>(a, acc, n0, m0, wu, wr, lane);
+  g256_epilogue<EPI>(a, acc, n0, m0, wu, wr, lane, sm2);
 }
 #undef GP_BARRIER
 
@@ -1107,15 +1199,16 @@ hipError_t launch_adamw_pack_big(float* P, const float* G, float* M, float* V, v
 }
 
 hipError_t launch_big_layer1(const void* rec, int rec_bytes, int B, const void* w1p, int H,
-                             const NormParams& np, void* h1, int ld, void* xf, hipStream_t stream) {
+                             const NormParams& np, void* h1, int ld, void* xf, hipStream_t stream,
+                             unsigned* mbits) {
   if (B <= 0) return hipSuccess;
   if (H % 32 || ld % 8) return hipErrorInvalidValue;
   const int tiles = (B + 31) / 32;
   const dim3 grid((tiles + 3) / 4), block(256);
   switch (rec_bytes) {
-    case 16: hipLaunchKernelGGL(big_layer1_kernel<16>, grid, block, 0, stream, rec, B, (const bf16x8*)w1p, H, np, (__bf16*)h1, ld, (__bf16*)xf); break;
-    case 8: hipLaunchKernelGGL(big_layer1_kernel<8>, grid, block, 0, stream, rec, B, (const bf16x8*)w1p, H, np, (__bf16*)h1, ld, (__bf16*)xf); break;
-    case 6: hipLaunchKernelGGL(big_layer1_kernel<6>, grid, block, 0, stream, rec, B, (const bf16x8*)w1p, H, np, (__bf16*)h1, ld, (__bf16*)xf); break;
+    case 16: hipLaunchKernelGGL(big_layer1_kernel<16>, grid, block, 0, stream, rec, B, (const bf16x8*)w1p, H, np, (__bf16*)h1, ld, (__bf16*)xf, mbits); break;
+    case 8: hipLaunchKernelGGL(big_layer1_kernel<8>, grid, block, 0, stream, rec, B, (const bf16x8*)w1p, H, np, (__bf16*)h1, ld, (__bf16*)xf, mbits); break;
+    case 6: hipLaunchKernelGGL(big_layer1_kernel<6>, grid, block, 0, stream, rec, B, (const bf16x8*)w1p, H, np, (__bf16*)h1, ld, (__bf16*)xf, mbits); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1194,6 +1287,38 @@ hipError_t launch_gemm_nt(int epi,const void* W, int ldw, const void* X, int ldx
     case EPI_STORE: hipLaunchKernelGGL(gemm_nt_kernel<EPI_STORE>, grid, block, 0, stream, a); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// dgrad with the dW1 epilogue (EPI_DW1): dh1 = dz2 W2 is never stored; slab1 row t receives the
+// [N positions][16] dW1 partial of batch rows [256 t, 256 t + 256).  256 x 256 loops only.
+hipError_t launch_gemm_dgrad_dw1(const void* W, int ldw, const void* X, int ldx, int N, int M, int K,
+                                 const unsigned* mbits, const void* xf, float* slab1, long long slab1_ld,
+                                 hipStream_t stream) {
+  if (M <= 0) return hipSuccess;
+  if (N % G2T || K % G2K || ldw % 8 || ldx % 8 || slab1_ld < 16LL * N || ((uintptr_t)mbits & 15) ||
+      ((uintptr_t)xf & 15) || ((uintptr_t)slab1 & 3))
+    return hipErrorInvalidValue;
+  GemmArgs a{(const __bf16*)W, (const __bf16*)X, ldw, ldx, N, M, K, nullptr, nullptr, nullptr, nullptr, 0, N / G2T, 1};
+  a.mbits = mbits;
+  a.xf = (const __bf16*)xf;
+  a.slab1 = slab1;
+  a.slab1_ld = slab1_ld;
+  static bool attr[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  static_assert(DW1_LDS >= 2 * G2_STAGE && DW1_LDS <= 160 * 1024, "the dW1 epilogue's LDS holds the K loop's");
+  if (!attr[dev & 63]) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm256_kernel<EPI_DW1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       DW1_LDS);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)gemm256p_kernel<EPI_DW1>, hipFuncAttributeMaxDynamicSharedMemorySize, DW1_LDS);
+    if (e != hipSuccess) return e;
+    attr[dev & 63] = true;
+  }
+  const dim3 grid((unsigned)((N / G2T) * ((M + G2T - 1) / G2T))), block(512);
+  if (gemm_pipe()) hipLaunchKernelGGL(gemm256p_kernel<EPI_DW1>, grid, block, DW1_LDS, stream, a);
+  else hipLaunchKernelGGL(gemm256_kernel<EPI_DW1>, grid, block, DW1_LDS, stream, a);
   return hipGetLastError();
 }
 

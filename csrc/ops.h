@@ -55,7 +55,14 @@ hipError_t launch_reduce_adamw(const float* slab2, int S2, long long stride2, co
 
 // ---- wide MLPs (H = 512, 1024): mlp_big.hip ----
 hipError_t launch_big_layer1(const void* rec, int rec_bytes, int B, const void* w1p, int H,
-                             const NormParams& np, void* h1, int ld, void* xf, hipStream_t stream);
+                             const NormParams& np, void* h1, int ld, void* xf, hipStream_t stream,
+                             unsigned* mbits = nullptr);
+// training dgrad dh1 = dz2 W2 with dW1 = (dh1 * relu'(z1))^T xf in its epilogue (dh1 never stored;
+// mbits: big_layer1's relu bit mask [M][N/32]):
+// slab1 [ceil(M / 256)][>= 16 N] f32 partials per 256-row tile (mlp_big.hip EPI_DW1)
+hipError_t launch_gemm_dgrad_dw1(const void* W, int ldw, const void* X, int ldx, int N, int M, int K,
+                                 const unsigned* mbits, const void* xf, float* slab1, long long slab1_ld,
+                                 hipStream_t stream);
 hipError_t launch_gemm_nt(int epi, const void* W, int ldw, const void* X, int ldx, int N, int M,
                           int K, const float* b2, const float* w3, float* ypart, void* out,
                           int ldo, hipStream_t stream);

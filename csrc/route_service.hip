@@ -319,7 +319,14 @@ struct RouteService::Impl {
       n_escalated{0};
   // stage times (us): parse, trips (K5+K6), snap, A*, copy-out, assembly, ETA, persistence
   std::atomic<long long> t_stage[8] = {};
-  void add_t(int k, double t0) { t_stage[k].fetch_add((long long)(now_us() - t0), std::memory_order_relaxed); }
+  void add_t(int k, double t0) {
+    const long long dt = (long long)(now_us() - t0);
+    t_stage[k].fetch_add(dt, std::memory_order_relaxed);
+    if (trace_ms >= 0 && dt > trace_ms * 1e3) {   // a stage that alone outlasts the trace threshold
+      static const char* const names[8] = {"parse", "trips", "snap", "astar", "copyout", "assemble", "eta", "persist"};
+      trace("stage %s took %.1f ms", names[k], dt * 1e-3);
+    }
+  }
   // K5 / K6 buffers
   HostBuf<double> h_lat, h_lon, h_dem, h_cap, h_maxd, h_row0;
   HostBuf<int> h_npts, h_visit, h_trip, h_ntrips, h_status;

@@ -277,8 +277,10 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
                           + per-64-unit partials of h2 . w3
       big_dz2y          : y, dy (scaled 2/global_batch), squared errors, dz2 = dy w3 relu'(z2) and
                           the dW3|db3 split-K slab rows, h2a streamed once
-      gemm_nt(STORE)    : dh1 = dz2 W2 (W2^T operand, kept by the optimizer kernel)
-      wgrad x 2 + reduce: dW2|db2 (column blocks of <= 288), dW1 (relu'(h1) fused)
+      gemm_dgrad_dw1    : dh1 = dz2 W2 (W2^T operand, kept by the optimizer kernel), consumed in its
+                          epilogue: per 256-row tile the dW1 partial (dh1 * relu'(h1))^T x (dh1 is
+                          never stored)
+      wgrad256 + reduce : dW2|db2 on 256 x 256 output tiles; one deterministic slab reduction
       all_reduce(G)     : one collective on the flat bucket (C1: 4.3 MB at H = 1024)
       adamw_pack_big    : AdamW + re-pack of w1p / w2k / w2t / b2 / w3 / b3
     """
@@ -299,7 +301,16 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
         self.h2a = torch.zeros(B, ldg, dtype=bf, device=d)
         self.h2a[:, H] = 1.0                 # ones column (db3 input); kernels never write it
         self.dz2 = torch.empty(B, H, dtype=bf, device=d)
-        self.dh1 = torch.empty(B, H, dtype=bf, device=d)
+        # dW1 in the dgrad GEMM's epilogue (default; ROUTEST_DW1_EPILOGUE=0: dh1 stored, then a masked
+        # wgrad launch): one [H][16] partial per 256-row tile, dh1 never written
+        self.dw1_epi = hasattr(self.C, "gemm_dgrad_dw1") and os.environ.get("ROUTEST_DW1_EPILOGUE", "1") != "0"
+        if self.dw1_epi:
+            self.slab1w = torch.empty((B + 255) // 256, 16 * H, dtype=torch.float32, device=d)
+            # relu'(z1) as bits (big_layer1 writes them): 16x less mask traffic than re-reading h1a
+            self.h1bits = torch.empty((B + 31) // 32 * 32, H // 32, dtype=torch.int32, device=d)
+            self.dh1 = None
+        else:
+            self.dh1 = torch.empty(B, H, dtype=bf, device=d)
         self.dyb = torch.empty(B, 8, dtype=bf, device=d)
         self.dy = torch.empty(B, dtype=torch.float32, device=d)
         self.ypart = torch.empty(B, H // 64, dtype=torch.float32, device=d)
@@ -317,7 +328,6 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
         # enough slices for one workgroup per CU; db2 rides along.  Default since run r6g: 159-173 us
         # against 214 us for the n-blocked wgrad_kernel at H = 1024, 64k rows (profiles/wgrad256_r6.md);
         # ROUTEST_WGRAD256=0 keeps the latter
-        import os
         self.wg256 = (H % 256 == 0 and B % 64 == 0 and hasattr(self.C, "wgrad256") and
                       os.environ.get("ROUTEST_WGRAD256", "1") == "1")
         if self.wg256:
@@ -342,20 +352,30 @@ class FusedMlp3TrainerBig(FusedMlp3Trainer):
         C, H, B = self.C, self.H, rec.shape[0]
         ldg = H + 16
         assert B == self.B, "wide trainer: batch must equal batch_local"
-        C.big_layer1(rec, self.w1p, H, self.norm, self.h1a, self.xf)
+        C.big_layer1(rec, self.w1p, H, self.norm, self.h1a, self.xf, self.h1bits if self.dw1_epi else None)
         C.gemm_nt(1, self.w2k, self.h1a, H, B, H, b2=self.b2v, w3=self.w3v, ypart=self.ypart,
                   out=self.h2a)
         # dy / dyb / squared error + dz2 + the device step counter: one launch
         # ... and dW3|db3 = [h2|1]^T dy into the slab's first H + 16 columns (h2a streamed once)
         C.big_dz2y(self.ypart, H // 64, self.b3v, tgt_norm, 2.0 / self.global_batch, self.dy,
                    self.dyb, self.sq_err, self.h2a, self.w3v, H, self.dz2, self.step_ctr, self.slab)
-        C.gemm_nt(2, self.w2t, self.dz2, H, B, H, out=self.dh1)
+        if self.dw1_epi:
+            C.gemm_dgrad_dw1(self.w2t, self.dz2, H, B, H, self.h1bits, self.xf, self.slab1w)
+        else:
+            C.gemm_nt(2, self.w2t, self.dz2, H, B, H, out=self.dh1)
         # dW2|db2 = dz2^T [h1|1]: 256 x 256 output tiles (db2 as per-tile-column partial sums folded by
         # the reduce), or one launch of n-blocks of <= 288 columns
         if self.wg256:
             C.wgrad256(self.dz2, self.h1a, H, H, self.slab2, ldg, H)
         else:
             C.wgrad(self.dz2, H, H, self.h1a, ldg, self.slab2, 0, ldg, nsplit=self.nsplit2)
+        if self.dw1_epi:
+            # dh1 consumed by the dgrad GEMM's epilogue (gemm_dgrad_dw1 above): dW3|db3 from the slab's
+            # first ldg columns, dW1 from the per-row-tile partials
+            C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg:H * ldg + ldg],
+                           self.slab1w, self.G[H * ldg + ldg:],
+                           fold_ld=ldg if self.wg256 else 0, fold_col=H if self.wg256 else 0)
+            return
         # dW1 = (dh1 * relu'(h1))^T x: dh1 and its mask h1a are both in the hperm order here
         C.wgrad(self.dh1, H, H, self.xf, 16, self.slab, ldg, 16, self.h1a)
         C.wgrad_reduce(self.slab2, self.G[:H * ldg], self.slab, self.G[H * ldg:],

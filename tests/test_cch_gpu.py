@@ -160,3 +160,22 @@ def test_paced_background_build_bit_identical_to_cpu(setup):
     s2, m2, st2, p2 = cpu.query(mcc, src, dst, True)
     assert np.array_equal(sec, s2) and np.array_equal(met, m2) and np.array_equal(st, st2)
     assert all(np.array_equal(a, b) for a, b in zip(paths, p2))
+
+
+@pytest.mark.parametrize("tail", ["64", "4096"])
+def test_persistent_tails_bit_identical_to_cpu(setup, monkeypatch, tail):
+    """ROUTEST_CCH_TAIL: the narrow top levels of both phases in one persistent launch each
+    (basic_tail_kernel / perfect_tail_kernel: work queue + bounded level waits) give the same bits
+    as the per-level launches and the CPU reference."""
+    from routest_amd.routing.cch import RoadRouter
+    g, m, router, cost, key, cpu, mc = setup
+    monkeypatch.setenv("ROUTEST_CCH_TAIL", tail)
+    r2 = RoadRouter(g, m, device="cuda:0")
+    st = r2.stats()
+    assert st["basic_tail_levels"] > 0 and st["perfect_tail_levels"] > 0, st
+    key2 = r2.metric_from_costs(1 << 41, cost)
+    src, dst = synth_route_queries(g, 2000, seed=3)
+    a = r2.route(src, dst, key2, want_path=False)
+    b = cpu.query(mc, src, dst, False)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(np.asarray(x), np.asarray(y))

@@ -333,6 +333,31 @@ def test_wide_trainer_gradients_match_autograd(H, B):
     assert abs(mse - float(loss)) / float(loss) < 2e-2
 
 
+@pytest.mark.parametrize("H", [512, 1024])
+@pytest.mark.parametrize("B", [1000, 65536])
+def test_dgrad_dw1_epilogue_matches_stored_dh1(H, B, monkeypatch):
+    """dW1 from the dgrad GEMM's epilogue (dh1 never stored) == the stored-dh1 + masked wgrad path:
+    the same bf16 dz1 values, summed in another order (fp32); every other gradient bit-identical."""
+    from routest_amd.train.fused import FusedMlp3TrainerBig
+    m = _model(H, 7)
+    rt, yn = _batch(B, m, 8)
+    rt, yn = rt.to(DEV), yn.to(DEV)
+    monkeypatch.setenv("ROUTEST_DW1_EPILOGUE", "1")
+    epi = FusedMlp3Trainer(copy.deepcopy(m), DEV, B, B)
+    monkeypatch.setenv("ROUTEST_DW1_EPILOGUE", "0")
+    ref = FusedMlp3Trainer(copy.deepcopy(m), DEV, B, B)
+    assert isinstance(epi, FusedMlp3TrainerBig) and epi.dw1_epi and not ref.dw1_epi
+    epi.forward_backward(rt, yn)
+    ref.forward_backward(rt, yn)
+    torch.cuda.synchronize()
+    ldg = H + 16
+    w1 = H * ldg + ldg
+    assert torch.equal(epi.G[:w1], ref.G[:w1])
+    a, b = epi.G[w1:].view(H, 16).cpu(), ref.G[w1:].view(H, 16).cpu()
+    torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max()))
+    assert float(b.abs().max()) > 0
+
+
 def test_wide_trainer_h1024_steps_and_serves():
     """A trainer step at H = 1024 runs end to end (optimizer included), the loss falls, and the
     trained weights serve through the wide inference path."""
