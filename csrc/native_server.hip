@@ -1638,7 +1638,7 @@ void native_server_stop(int64_t h) {
 
 std::vector<long long> native_server_stats(int64_t h) {
   std::lock_guard<std::mutex> lk(g_srv_mu);
-  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(39, 0);
+  if (h < 0 || h >= (int64_t)g_servers.size() || !g_servers[h]) return std::vector<long long>(41, 0);
   Server* s = g_servers[h];
   std::vector<long long> v = {s->stats.requests.load(), s->stats.predictions.load(), s->stats.launches.load(),
                               s->stats.errors.load(), s->stats.resident.load(), s->stats.fallbacks.load(),
@@ -1661,7 +1661,7 @@ std::vector<long long> native_server_stats(int64_t h) {
   }
   v.insert(v.end(), rx.begin(), rx.end());
   v.push_back(s->stats.timeouts.load());
-  std::vector<long long> rr(2, 0);        // compact route records: rows, bytes
+  std::vector<long long> rr(4, 0);        // compact route records: rows, bytes; GPU-thread collect / handoff us
   for (auto& r : s->routes) {
     const auto x = r->stats();
     for (size_t i = 0; i < rr.size() && 22 + i < x.size(); ++i) rr[i] += x[22 + i];

@@ -132,6 +132,7 @@ struct RouteJob {
   double defer_t0 = 0.0;            // when it was first deferred for its context's build (us)
   bool sync_ctx = false;            // its context's background build failed: build it in the flush
   int hops = 0;                     // times handed to another GPU's route service (failover)
+  double t_enq_us = 0.0;            // when it entered the flush queue (steady clock, us)
   // "alternatives": unique leg pairs in order, their via nodes, the chosen candidates (legs owned
   // here) and the response block
   std::vector<std::pair<int, int>> alt_pairs;

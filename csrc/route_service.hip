@@ -319,6 +319,8 @@ struct RouteService::Impl {
       n_escalated{0};
   // stage times (us): parse, trips (K5+K6), snap, A*, copy-out, assembly, ETA, persistence
   std::atomic<long long> t_stage[8] = {};
+  // GPU thread waits (us): collecting a flush after its first job, handing it to a full assembly queue
+  std::atomic<long long> t_collect_us{0}, t_handoff_us{0};
   void add_t(int k, double t0) {
     const long long dt = (long long)(now_us() - t0);
     t_stage[k].fetch_add(dt, std::memory_order_relaxed);
@@ -760,11 +762,21 @@ struct RouteService::Impl {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return stop || !q.empty(); });
         if (stop && q.empty()) { delete b; break; }
-        // collect: up to batch_max, or timeout_us after the first arrival
-        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds((long long)cfg.timeout_us);
-        while ((int)q.size() < cfg.batch_max && !stop) {
+        // collect: up to batch_max, or timeout_us after the OLDEST queued job's arrival — jobs that
+        // queued during the previous flush's GPU stage have waited long enough already (timing the
+        // window from this wake-up added up to timeout_us to every flush of a busy service)
+        const double t_wake = now_us();
+        static const bool from_wake = [] {   // ROUTEST_ROUTE_COLLECT=wake: the round-5 window (A/B)
+          const char* v = std::getenv("ROUTEST_ROUTE_COLLECT");
+          return v && std::string(v) == "wake";
+        }();
+        const double t_open = from_wake ? t_wake : q.front()->t_enq_us;
+        const auto deadline = std::chrono::steady_clock::time_point(std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+            std::chrono::duration<double, std::micro>(t_open + cfg.timeout_us)));
+        while ((int)q.size() < cfg.batch_max && !stop && std::chrono::steady_clock::now() < deadline) {
           if (cv.wait_until(lk, deadline) == std::cv_status::timeout) break;
         }
+        t_collect_us.fetch_add((long long)(now_us() - t_wake), std::memory_order_relaxed);
         const size_t take = std::min<size_t>(q.size(), (size_t)cfg.batch_max);
         b->jobs.assign(q.begin(), q.begin() + take);
         q.erase(q.begin(), q.begin() + take);
@@ -803,8 +815,10 @@ struct RouteService::Impl {
         delete b;
         continue;
       }
+      const double t_h = now_us();
       std::unique_lock<std::mutex> lk(amu);
       acv.wait(lk, [&] { return aq.size() < 2; });
+      t_handoff_us.fetch_add((long long)(now_us() - t_h), std::memory_order_relaxed);
       aq.push_back(b);
       acv.notify_all();
     }
@@ -2166,6 +2180,7 @@ bool RouteService::submit(RouteJob* j) {
   {
     std::lock_guard<std::mutex> lk(p_->mu);
     if (p_->stop) return false;   // the run loop may have drained its queue already
+    j->t_enq_us = now_us();
     p_->q.push_back(j);
   }
   p_->cv.notify_one();
@@ -2186,6 +2201,8 @@ std::vector<long long> RouteService::stats() const {
   v.push_back(p_->n_failed_over.load());   // jobs handed to another GPU's route service
   v.push_back(p_->n_records.load());       // rows persisted as compact route records
   v.push_back(p_->n_record_bytes.load());  // ... and their record bytes
+  v.push_back(p_->t_collect_us.load());    // GPU thread: collecting flushes (us)
+  v.push_back(p_->t_handoff_us.load());    // GPU thread: waiting for the assembly queue (us)
   return v;
 }
 

@@ -182,7 +182,9 @@ class NativePredictServer:
                  # flush missed its deadline; prediction rounds abandoned at the deadline
                  "route_failed_over", "timeouts",
                  # persisted graph routes stored as compact route records, and their bytes
-                 "route_records", "route_record_bytes")
+                 "route_records", "route_record_bytes",
+                 # the route services' GPU threads: collecting flushes, waiting for assembly (us)
+                 "route_us_collect", "route_us_handoff")
         return dict(zip(names, v))
 
     def close(self) -> None:
