@@ -1,7 +1,7 @@
-# round 6: slab reduce with eight slice loads in flight — training tests, H = 256 / 1024 steps, stats
+# round 6: slab reduce variants (r6t: eight loads in flight; r6u: 32 slice lanes x 8 columns) — training tests, H = 256 / 1024 steps, stats
 ROOT=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp && cd $ROOT
-O=$ROOT/gpurun_out/r6t; mkdir -p $O
+O=$ROOT/gpurun_out/${RUN:-r6t}; mkdir -p $O
 stop() { rc=$1; [ $rc -eq 124 -o $rc -eq 137 -o $rc -eq 134 -o $rc -eq 139 ] && { echo "GPU step ended rc=$rc: stopping"; exit $rc; }; [ $rc -ne 0 ] && echo "step rc=$rc"; }
 timeout -k 10 600 python -u -m pytest -v --timeout 200 --timeout-method thread tests/test_train_gpu.py > $O/train_tests.log 2>&1; stop $?
 tail -1 $O/train_tests.log; grep -E "FAILED|ERROR" $O/train_tests.log | head
