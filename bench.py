@@ -104,6 +104,10 @@ def main() -> None:
     # a collective that never completes (a peer died, an RCCL hang) ends in an error after this
     # long instead of running into the driver's limit with no JSON line printed
     pg_timeout = datetime.timedelta(seconds=env_timeout_s("ROUTEST_BENCH_PG_TIMEOUT_S", 180.0))
+    # ... and what happens then: CleanUpOnly (2) aborts the hung RCCL communicator, so the waiting
+    # stream completes with an error and the section reports it under the guard; torch's default
+    # (3, SkipCleanUp) tears the whole process down from the watchdog thread — no JSON line
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
     if world > 1:
         torch.cuda.set_device(local_rank)
         if share:
