@@ -140,3 +140,26 @@ def test_routing_context_changes_costs_and_stays_exact():
     d = RouteContext.from_request({}, now=dt.datetime(2025, 8, 31, 23, 30))
     assert (d.weather, d.congestion, d.weekhour) == (2, 0, 6 * 24 + 23)
     assert RouteContext.from_request({"context": {"weather": "Foggy", "traffic": 3}}).weather == 255
+
+
+def test_level_histogram_tool_accounts_for_every_triangle():
+    """tools/cch_levels.py (the level-width histogram behind profiles/cch_levels_100k_r6.json):
+    per-level items sum to the whole phase, the level counts equal the elimination tree's height /
+    depth + 1, and the 'below' shares are monotone in the threshold."""
+    import importlib.util
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "cch_levels.py")
+    spec = importlib.util.spec_from_file_location("cch_levels", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    r = mod.level_stats(3000, seed=2)
+    st = r["stats"]
+    assert r["basic"]["levels"] == st["max_height"] + 1
+    assert r["perfect"]["levels"] == st["max_depth"] + 1
+    for name in ("basic", "perfect"):
+        sec = r[name]
+        assert sec["items"] > 0 and sec["max_items"] <= sec["items"]
+        below = [sec["below"][t] for t in sorted(sec["below"], key=int)]
+        assert all(a["levels"] <= b["levels"] and a["share_of_items"] <= b["share_of_items"] + 1e-12
+                   for a, b in zip(below, below[1:]))
+        assert all(0.0 <= b["share_of_items"] <= 1.0 for b in below)
