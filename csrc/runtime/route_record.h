@@ -288,7 +288,9 @@ inline bool decode(const RecordGraph& g, const void* data, size_t n, std::string
     std::vector<uint64_t> durs;
     for (size_t l = 0; l < nl; ++l) {
       const uint64_t len = r.uv();
-      if (!r.ok || len < 1 || len > (1u << 26)) return fail("malformed route record");
+      // every hop takes at least one byte: a length the remaining bytes cannot hold is malformed
+      // (and is refused before anything is sized by it)
+      if (!r.ok || len < 1 || len > (1u << 26) || len - 1 > (uint64_t)(r.e - r.p)) return fail("malformed route record");
       std::vector<int32_t>& p = paths[l];
       std::vector<int32_t>& ed = edges[l];
       p.resize((size_t)len);

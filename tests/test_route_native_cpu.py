@@ -214,6 +214,19 @@ def test_compact_route_record_rebuilds_byte_identical():
                     other._steps.decode_record(rec)
                 with pytest.raises(ValueError):
                     prov._steps.decode_record(rec[:-3])
+                if checked % 10 == 1:        # corrupted rows: refused or decoded, never a crash
+                    frng = np.random.default_rng(checked)
+                    for _ in range(60):
+                        b = bytearray(rec)
+                        for _ in range(int(frng.integers(1, 4))):
+                            b[int(frng.integers(12, len(b)))] = int(frng.integers(0, 256))
+                        if frng.random() < 0.3:
+                            b = b[:int(frng.integers(12, len(b)))]
+                        try:
+                            out = prov._steps.decode_record(bytes(b))
+                            assert isinstance(out, tuple) and len(out) == 2
+                        except ValueError:
+                            pass
     assert checked > 80
     print(f"record {rec_bytes / checked:.0f} B vs text {text_bytes / checked:.0f} B per route")
     assert rec_bytes * 6 < text_bytes, (rec_bytes, text_bytes)
