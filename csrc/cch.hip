@@ -775,6 +775,577 @@ __global__ __launch_bounds__(256) void prune_scatter_wave_kernel(
   }
 }
 
+// ---- supernodal customization of the top of the elimination tree (round 6) ----
+// The top ~80 % of the etree levels are the nested-dissection separators: CHAINS of nodes (each the
+// only child of the next), one etree level per node, so the per-level kernels above walk them one
+// ~12 us level at a time (963 levels per phase on the 100k graph, profiles/cch_customize_r6.md).
+// A chain with its upper set is a dense FRONT (chordality: every chain node's upward arcs lead into
+// the chain above it or into the top node's upward set), and its customization is dense (min, +)
+// elimination: basic = tropical Gaussian elimination of the chain's pivots (a triangle z of pair
+// {u, v} is "pivot z updates D[u][v]"), perfect = tropical back substitution from the top.  Blocked
+// 32 pivots at a time, a level of the supernode tree takes 2 (basic) / 3 (perfect) launches per
+// block instead of one launch per node — and every candidate is the same single f32 add of the
+// same two operands as in the per-level kernels (min is exact and order-free), so the results are
+// bit-identical to them and to the CPU reference (csrc/runtime/cch.h).
+// A front's D is row-major n x n over its nodes in rank order (chain c0 .. c0 + m - 1 first, then
+// the top's upward set): D[i][j] = weight f_i -> f_j — basic: the packed (weight, middle) word,
+// perfect: two f32 matrices (basic Db, perfect P) in the same bytes.  farc[i][j]: the arc of
+// {f_i, f_j} (-1: none).  Entries between two upper-set nodes (U x U) are only ever TARGETS here
+// (their arcs belong to an ancestor front): basic sends them with one atomicMin each at the end.
+struct SupNode {
+  int64_t dofs;      // first entry of the front in the level's dense buffer
+  int64_t foff;      // first entry of its farc table
+  int32_t c0, m, n;  // first chain rank, chain length, front size
+  int32_t fnode;     // offset of its node list
+};
+struct SupWork {
+  int32_t s, b, t0, t1;   // supernode, block (or row), tile indices
+};
+constexpr int SUP_B = 32;      // pivots per block
+constexpr int SUP_PJ = 32;     // basic panel: front columns per workgroup
+constexpr int SUP_TT = 64;     // basic trailing update: 64 x 64 targets per workgroup
+constexpr int SUP_G1Y = 32;    // perfect GEMM: 32 output columns per workgroup
+constexpr int SUP_G1Z = 512;   // ... over at most 512 intermediate nodes (more: split, atomicMin)
+constexpr int SUP_SJ = 64;     // perfect solve: front columns per workgroup
+
+__device__ __forceinline__ unsigned long long sup_cand(unsigned long long a, unsigned long long b, uint32_t z) {
+  const float w = wof(a) + wof(b);
+  return w < F_INF ? packw(w, z) : PACK_INF_D;
+}
+__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return b < a ? b : a; }
+
+// farc of every front row (once per graph): a wave per row
+__global__ __launch_bounds__(256) void sup_farc_kernel(const SupNode* __restrict__ sn, const SupWork* __restrict__ w,
+                                                       long long nw, const int32_t* __restrict__ fnode,
+                                                       const int32_t* __restrict__ up_ptr,
+                                                       const int32_t* __restrict__ up_head, int32_t* __restrict__ farc) {
+  const long long wi = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wi >= nw) return;
+  const SupWork W = w[wi];
+  const SupNode S = sn[W.s];
+  const int i = W.b, n = S.n;
+  const int fi = fnode[S.fnode + i];
+  for (int j = threadIdx.x & 63; j < n; j += 64) {
+    const int fj = fnode[S.fnode + j];
+    farc[S.foff + (long long)i * n + j] = i == j ? -1 : find_arc_d(up_ptr, up_head, fi < fj ? fi : fj, fi < fj ? fj : fi);
+  }
+}
+
+// basic: a front's rows from the arc weights (all lower levels are done); U x U starts at +inf
+__global__ __launch_bounds__(256) void sup_gather_basic_kernel(const SupNode* __restrict__ sn, const SupWork* __restrict__ w,
+                                                               long long nw, const int32_t* __restrict__ farc,
+                                                               const unsigned long long* __restrict__ up,
+                                                               const unsigned long long* __restrict__ dn,
+                                                               unsigned long long* __restrict__ D) {
+  const long long wi = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wi >= nw) return;
+  const SupWork W = w[wi];
+  const SupNode S = sn[W.s];
+  const int i = W.b, n = S.n;
+  unsigned long long* row = D + S.dofs + (long long)i * n;
+  const int32_t* fr = farc + S.foff + (long long)i * n;
+  for (int j = threadIdx.x & 63; j < n; j += 64) {
+    unsigned long long v = PACK_INF_D;
+    if (i != j && (i < S.m || j < S.m)) {
+      const int a = fr[j];
+      if (a >= 0) v = i < j ? up[a] : dn[a];
+    }
+    row[j] = v;
+  }
+}
+
+// basic, block b of a front: the 32 pivots K = [k0, k1) eliminated in the diagonal block and in the
+// row / column panels of this workgroup's 32 front columns J (every workgroup of the front redoes
+// the 32 x 32 diagonal block: no inter-workgroup dependency), then the rows of K are final: their
+// arcs' weights go out, and they are FINALIZED (best triangle's sub-arcs, metres, road edges —
+// basic_task_run's ROW_FINAL) — a middle node inside K needs the lengths of an arc of K finalized
+// just before, so those go row by row from LDS after the others went in parallel.
+__global__ __launch_bounds__(256) void sup_panel_basic_kernel(
+    const SupNode* __restrict__ sn, const SupWork* __restrict__ w, const int32_t* __restrict__ fnode,
+    const int32_t* __restrict__ farc, unsigned long long* __restrict__ D, unsigned long long* __restrict__ up,
+    unsigned long long* __restrict__ dn, int32_t* __restrict__ sub_up, int32_t* __restrict__ sub_dn,
+    float* __restrict__ len_up, float* __restrict__ len_dn, int32_t* __restrict__ cnt_up, int32_t* __restrict__ cnt_dn,
+    const float* __restrict__ length, const int32_t* __restrict__ up_ptr, const int32_t* __restrict__ up_head) {
+  constexpr int B = SUP_B, J = SUP_PJ, W2 = SUP_B + SUP_PJ;
+  __shared__ unsigned long long Dk[B][B + 1];   // D[K][K]
+  __shared__ unsigned long long R[B][J + 1];    // D[K][J]
+  __shared__ unsigned long long C[J][B + 1];    // D[J][K]
+  __shared__ float lu[B][W2], ld[B][W2];        // finalized metres of the rows of K: columns K | J
+  __shared__ int32_t cu[B][W2], cd[B][W2];
+  const SupWork W = w[blockIdx.x];
+  const SupNode S = sn[W.s];
+  const int n = S.n, tid = threadIdx.x;
+  const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
+  const int j0 = k1 + W.t0 * J, nj = max(0, min(J, n - j0));
+  const bool diag_writer = W.t0 == 0;
+  unsigned long long* Df = D + S.dofs;
+  const int32_t* F = farc + S.foff;
+  for (int e = tid; e < B * B; e += 256) {
+    const int y = e / B, x = e % B;
+    Dk[y][x] = (y < kb && x < kb) ? Df[(long long)(k0 + y) * n + k0 + x] : PACK_INF_D;
+  }
+  for (int e = tid; e < B * J; e += 256) {
+    const int y = e / J, j = e % J;
+    R[y][j] = (y < kb && j < nj) ? Df[(long long)(k0 + y) * n + j0 + j] : PACK_INF_D;
+  }
+  for (int e = tid; e < J * B; e += 256) {
+    const int j = e / B, y = e % B;
+    C[j][y] = (y < kb && j < nj) ? Df[(long long)(j0 + j) * n + k0 + y] : PACK_INF_D;
+  }
+  __syncthreads();
+  // pivot p: entries of rows / columns above p (row p and column p are final and only read)
+  for (int p = 0; p < kb; ++p) {
+    const uint32_t z = (uint32_t)(S.c0 + k0 + p);
+    for (int e = tid; e < B * B; e += 256) {
+      const int y = e / B, x = e % B;
+      if (y > p && x > p && y < kb && x < kb && y != x) Dk[y][x] = umin64(Dk[y][x], sup_cand(Dk[y][p], Dk[p][x], z));
+    }
+    for (int e = tid; e < B * J; e += 256) {
+      const int y = e / J, j = e % J;
+      if (y > p && y < kb && j < nj) R[y][j] = umin64(R[y][j], sup_cand(Dk[y][p], R[p][j], z));
+    }
+    for (int e = tid; e < J * B; e += 256) {
+      const int j = e / B, x = e % B;
+      if (x > p && x < kb && j < nj) C[j][x] = umin64(C[j][x], sup_cand(C[j][p], Dk[p][x], z));
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < B * J; e += 256) {
+    const int y = e / J, j = e % J;
+    if (y < kb && j < nj) {
+      Df[(long long)(k0 + y) * n + j0 + j] = R[y][j];
+      Df[(long long)(j0 + j) * n + k0 + y] = C[j][y];
+      const int a = F[(long long)(k0 + y) * n + j0 + j];
+      if (a >= 0) {
+        up[a] = R[y][j];
+        dn[a] = C[j][y];
+      }
+    }
+  }
+  if (diag_writer)
+    for (int e = tid; e < B * B; e += 256) {
+      const int y = e / B, x = e % B;
+      if (y < kb && x < kb) {
+        Df[(long long)(k0 + y) * n + k0 + x] = Dk[y][x];
+        if (y < x) {
+          const int a = F[(long long)(k0 + y) * n + k0 + x];
+          if (a >= 0) {
+            up[a] = Dk[y][x];
+            dn[a] = Dk[x][y];
+          }
+        }
+      }
+    }
+  // finalize the arcs (x, v), x in K, v in K above x (column v - k0) or in J (column B + j)
+  const int zK = S.c0 + k0;     // rank of K's first pivot
+  auto entry = [&](int x, int col, int& vf) -> int {
+    if (col < B) {
+      if (!(col < kb && col > x)) return -1;
+      vf = k0 + col;
+    } else {
+      if (col - B >= nj) return -1;
+      vf = j0 + col - B;
+    }
+    return F[(long long)(k0 + x) * n + vf];
+  };
+  auto weight = [&](int x, int col, int dir) -> unsigned long long {
+    if (col < B) return dir ? Dk[col][x] : Dk[x][col];
+    return dir ? C[col - B][x] : R[x][col - B];
+  };
+  auto put = [&](int x, int col, int a, int dir, int s0, int s1, float L, int32_t Cn) {
+    (dir ? ld : lu)[x][col] = L;
+    (dir ? cd : cu)[x][col] = Cn;
+    if (col >= B || diag_writer) {
+      int32_t* sub = (dir ? sub_dn : sub_up) + 2 * (long long)a;
+      sub[0] = s0;
+      sub[1] = s1;
+      (dir ? len_dn : len_up)[a] = L;
+      (dir ? cnt_dn : cnt_up)[a] = Cn;
+    }
+  };
+  for (int e = tid; e < B * W2; e += 256) {
+    const int x = e / W2, col = e % W2;
+    if (x >= kb) continue;
+    int vf = 0;
+    const int a = entry(x, col, vf);
+    if (a < 0) continue;
+#pragma unroll
+    for (int dir = 0; dir < 2; ++dir) {
+      const unsigned long long wv = weight(x, col, dir);
+      if (!(wof(wv) < F_INF)) {
+        put(x, col, a, dir, -1, -1, F_INF, 0);
+        continue;
+      }
+      const uint32_t pl = (uint32_t)wv;
+      if (pl & EDGE_FLAG_D) {
+        const int ed = (int)(pl & ~EDGE_FLAG_D);
+        put(x, col, a, dir, -1, ed, length[ed], 1);
+        continue;
+      }
+      const int zz = (int)pl;
+      if (zz >= zK) continue;                    // a middle inside K: row by row below
+      int azx, azv;
+      if (zz >= S.c0) {                          // an earlier block of the chain
+        const long long fz = zz - S.c0;
+        azx = F[fz * n + k0 + x];
+        azv = F[fz * n + vf];
+      } else {                                   // below the front (final since earlier levels)
+        azx = find_arc_d(up_ptr, up_head, zz, zK + x);
+        azv = find_arc_d(up_ptr, up_head, zz, fnode[S.fnode + vf]);
+      }
+      const int s0 = dir ? azv : azx, s1 = dir ? azx : azv;
+      put(x, col, a, dir, s0, s1, len_dn[s0] + len_up[s1], cnt_dn[s0] + cnt_up[s1]);
+    }
+  }
+  __syncthreads();
+  for (int x = 1; x < kb; ++x) {
+    for (int e = tid; e < 2 * W2; e += 256) {
+      const int dir = e / W2, col = e % W2;
+      int vf = 0;
+      const int a = entry(x, col, vf);
+      if (a < 0) continue;
+      const unsigned long long wv = weight(x, col, dir);
+      if (!(wof(wv) < F_INF)) continue;
+      const uint32_t pl = (uint32_t)wv;
+      if (pl & EDGE_FLAG_D) continue;
+      const int zl = (int)pl - zK;
+      if (zl < 0) continue;
+      // zl < x: row zl is final (phase above or an earlier row here); arc (z, x) is its column x
+      const int azx = F[(long long)(k0 + zl) * n + k0 + x];
+      const int azv = F[(long long)(k0 + zl) * n + vf];
+      if (dir == 0)
+        put(x, col, a, 0, azx, azv, ld[zl][x] + lu[zl][col], cd[zl][x] + cu[zl][col]);
+      else
+        put(x, col, a, 1, azv, azx, ld[zl][col] + lu[zl][x], cd[zl][col] + cu[zl][x]);
+    }
+    __syncthreads();
+  }
+}
+
+// basic, block b: the trailing update of the front's targets above K — for every (y, z), both past
+// k1, the best pivot p in K of D[y][p] + D[p][z] (ties: the lowest pivot = the smallest middle rank,
+// as the packed atomicMin).  U x U targets go to their arcs with one atomicMin after the last block.
+__global__ __launch_bounds__(256) void sup_trailing_basic_kernel(const SupNode* __restrict__ sn,
+                                                                 const SupWork* __restrict__ w,
+                                                                 const int32_t* __restrict__ farc,
+                                                                 unsigned long long* __restrict__ D,
+                                                                 unsigned long long* __restrict__ up,
+                                                                 unsigned long long* __restrict__ dn) {
+  constexpr int B = SUP_B, T = SUP_TT;
+  __shared__ float A[T][B + 1];     // weights D[y][K]
+  __shared__ float Bm[B][T + 1];    // weights D[K][z]
+  const SupWork W = w[blockIdx.x];
+  const SupNode S = sn[W.s];
+  const int n = S.n, m = S.m, tid = threadIdx.x;
+  const int k0 = W.b * B, k1 = min(k0 + B, m), kb = k1 - k0;
+  const int y0 = k1 + W.t0 * T, z0 = k1 + W.t1 * T;
+  unsigned long long* Df = D + S.dofs;
+  for (int e = tid; e < T * B; e += 256) {
+    const int r = e / B, p = e % B;
+    A[r][p] = (y0 + r < n && p < kb) ? wof(Df[(long long)(y0 + r) * n + k0 + p]) : F_INF;
+  }
+  for (int e = tid; e < B * T; e += 256) {
+    const int p = e / T, c = e % T;
+    Bm[p][c] = (p < kb && z0 + c < n) ? wof(Df[(long long)(k0 + p) * n + z0 + c]) : F_INF;
+  }
+  __syncthreads();
+  const int ty = tid >> 4, tz = tid & 15;
+  float bw[4][4];
+  int bp[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bw[i][j] = F_INF;
+      bp[i][j] = 0;
+    }
+  for (int p = 0; p < kb; ++p) {
+    float a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = A[ty * 4 + i][p];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = Bm[p][tz + 16 * j];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float s = a[i] + b[j];
+        if (s < bw[i][j]) {        // strict: the first (lowest) pivot keeps a tie
+          bw[i][j] = s;
+          bp[i][j] = p;
+        }
+      }
+  }
+  const bool last = k1 == m;
+  const int32_t* F = farc + S.foff;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int y = y0 + ty * 4 + i, z = z0 + tz + 16 * j;
+      if (y >= n || z >= n || y == z) continue;
+      const unsigned long long c = bw[i][j] < F_INF ? packw(bw[i][j], (uint32_t)(S.c0 + k0 + bp[i][j])) : PACK_INF_D;
+      const long long idx = (long long)y * n + z;
+      const unsigned long long old = Df[idx];
+      if (y >= m && z >= m && last) {
+        const unsigned long long v = umin64(old, c);
+        if (v == PACK_INF_D) continue;
+        const int a = F[idx];
+        if (a < 0) continue;
+        unsigned long long* g = (y < z ? up : dn) + a;
+        if (v < *g) atomicMin(g, v);
+      } else if (c < old) {
+        Df[idx] = c;
+      }
+    }
+}
+
+// perfect: a front's basic weights (f32) of every pair with a chain node, and the perfect weights
+// of U x U (final: an ancestor front's or an earlier level's); the diagonal is +inf (no candidate
+// through the target's own head)
+__global__ __launch_bounds__(256) void sup_gather_perfect_kernel(const SupNode* __restrict__ sn,
+                                                                 const SupWork* __restrict__ w, long long nw,
+                                                                 const int32_t* __restrict__ farc,
+                                                                 const unsigned long long* __restrict__ up,
+                                                                 const unsigned long long* __restrict__ dn,
+                                                                 const uint32_t* __restrict__ pup,
+                                                                 const uint32_t* __restrict__ pdn, float* __restrict__ D) {
+  const long long wi = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wi >= nw) return;
+  const SupWork W = w[wi];
+  const SupNode S = sn[W.s];
+  const int i = W.b, n = S.n;
+  float* Db = D + 2 * S.dofs;
+  float* P = Db + (long long)n * n;
+  const int32_t* fr = farc + S.foff + (long long)i * n;
+  for (int j = threadIdx.x & 63; j < n; j += 64) {
+    float db = F_INF, p = F_INF;
+    const int a = fr[j];
+    if (i != j && a >= 0) {
+      if (i < S.m || j < S.m) {
+        db = wof(i < j ? up[a] : dn[a]);
+        p = db;
+      } else {
+        p = __uint_as_float(i < j ? pup[a] : pdn[a]);
+      }
+    }
+    Db[(long long)i * n + j] = db;
+    P[(long long)i * n + j] = p;
+  }
+}
+
+// perfect, block b (blocks from the top): the candidates through the final part F = [k1, n) —
+// up: P[x][y] = min_z Db[x][z] + P[z][y], dn: P[y][x] = min_z P[y][z] + Db[z][x]  (x in K, y, z in F)
+// — a (min, +) product, 32 x 32 outputs per workgroup over <= 512 z (t1 = split << 1 | dir)
+__global__ __launch_bounds__(256) void sup_gemm_perfect_kernel(const SupNode* __restrict__ sn,
+                                                               const SupWork* __restrict__ w, float* __restrict__ D) {
+  constexpr int B = SUP_B, Y = SUP_G1Y, ZC = 64;
+  __shared__ float As[32][ZC + 1];
+  __shared__ float Bs[ZC][33];
+  const SupWork W = w[blockIdx.x];
+  const SupNode S = sn[W.s];
+  const int n = S.n, tid = threadIdx.x;
+  const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
+  const int y0 = k1 + W.t0 * Y, ny = min(Y, n - y0);
+  const int dir = W.t1 & 1, zs = W.t1 >> 1;
+  const int zbeg = k1 + zs * SUP_G1Z, zend = min(zbeg + SUP_G1Z, n);
+  const bool split = n - k1 > SUP_G1Z;
+  float* Db = D + 2 * S.dofs;
+  float* P = Db + (long long)n * n;
+  const int r = tid >> 3, cq = tid & 7;
+  float best[4] = {F_INF, F_INF, F_INF, F_INF};
+  for (int zc = zbeg; zc < zend; zc += ZC) {
+    const int nz = min(ZC, zend - zc);
+    for (int e = tid; e < 32 * ZC; e += 256) {
+      const int rr = e / ZC, q = e % ZC;
+      float v = F_INF;
+      if (q < nz) {
+        if (dir == 0 && rr < kb) v = Db[(long long)(k0 + rr) * n + zc + q];
+        if (dir == 1 && rr < ny) v = P[(long long)(y0 + rr) * n + zc + q];
+      }
+      As[rr][q] = v;
+    }
+    for (int e = tid; e < ZC * 32; e += 256) {
+      const int q = e / 32, cc = e % 32;
+      float v = F_INF;
+      if (q < nz) {
+        if (dir == 0 && cc < ny) v = P[(long long)(zc + q) * n + y0 + cc];
+        if (dir == 1 && cc < kb) v = Db[(long long)(zc + q) * n + k0 + cc];
+      }
+      Bs[q][cc] = v;
+    }
+    __syncthreads();
+    for (int q = 0; q < nz; ++q) {
+      const float a = As[r][q];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float s = a + Bs[q][cq + 8 * u];
+        best[u] = s < best[u] ? s : best[u];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = cq + 8 * u;
+    if (!(best[u] < F_INF)) continue;
+    long long idx;
+    if (dir == 0) {
+      if (r >= kb || c >= ny) continue;
+      idx = (long long)(k0 + r) * n + y0 + c;
+    } else {
+      if (r >= ny || c >= kb) continue;
+      idx = (long long)(y0 + r) * n + k0 + c;
+    }
+    if (split) atomicMin((uint32_t*)(P + idx), __float_as_uint(best[u]));
+    else if (best[u] < P[idx]) P[idx] = best[u];
+  }
+}
+
+// perfect, block b: the rows of K against this workgroup's 64 columns y of F, top-down through K
+// (candidates through z in K above x), then written out; and the F-part of the K x K targets through
+// these 64 z (atomicMin into P[K][K], finished by sup_kk_perfect_kernel)
+__global__ __launch_bounds__(256) void sup_solve_perfect_kernel(const SupNode* __restrict__ sn,
+                                                                const SupWork* __restrict__ w,
+                                                                const int32_t* __restrict__ farc, float* __restrict__ D,
+                                                                uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+  constexpr int B = SUP_B, Y = SUP_SJ;
+  __shared__ float Dk[B][B + 1];     // Db[K][K]
+  __shared__ float PU[B][Y + 1];     // P[K][y]
+  __shared__ float PD[Y][B + 1];     // P[y][K]
+  __shared__ float DKT[B][Y + 1];    // Db[K][y]
+  __shared__ float DTK[Y][B + 1];    // Db[y][K]
+  const SupWork W = w[blockIdx.x];
+  const SupNode S = sn[W.s];
+  const int n = S.n, tid = threadIdx.x;
+  const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
+  const int y0 = k1 + W.t0 * Y, ny = min(Y, n - y0);
+  float* Db = D + 2 * S.dofs;
+  float* P = Db + (long long)n * n;
+  for (int e = tid; e < B * B; e += 256) {
+    const int y = e / B, x = e % B;
+    Dk[y][x] = (y < kb && x < kb) ? Db[(long long)(k0 + y) * n + k0 + x] : F_INF;
+  }
+  for (int e = tid; e < B * Y; e += 256) {
+    const int x = e / Y, y = e % Y;
+    const bool ok = x < kb && y < ny;
+    PU[x][y] = ok ? P[(long long)(k0 + x) * n + y0 + y] : F_INF;
+    DKT[x][y] = ok ? Db[(long long)(k0 + x) * n + y0 + y] : F_INF;
+  }
+  for (int e = tid; e < Y * B; e += 256) {
+    const int y = e / B, x = e % B;
+    const bool ok = x < kb && y < ny;
+    PD[y][x] = ok ? P[(long long)(y0 + y) * n + k0 + x] : F_INF;
+    DTK[y][x] = ok ? Db[(long long)(y0 + y) * n + k0 + x] : F_INF;
+  }
+  __syncthreads();
+  for (int z = kb - 1; z >= 1; --z) {
+    for (int e = tid; e < B * Y; e += 256) {
+      const int x = e / Y, y = e % Y;
+      if (x < z && y < ny) {
+        const float s = Dk[x][z] + PU[z][y];
+        if (s < PU[x][y]) PU[x][y] = s;
+      }
+    }
+    for (int e = tid; e < Y * B; e += 256) {
+      const int y = e / B, x = e % B;
+      if (x < z && y < ny) {
+        const float s = PD[y][z] + Dk[z][x];
+        if (s < PD[y][x]) PD[y][x] = s;
+      }
+    }
+    __syncthreads();
+  }
+  const int32_t* F = farc + S.foff;
+  for (int e = tid; e < B * Y; e += 256) {
+    const int x = e / Y, y = e % Y;
+    if (x < kb && y < ny) {
+      const long long iu = (long long)(k0 + x) * n + y0 + y;
+      P[iu] = PU[x][y];
+      P[(long long)(y0 + y) * n + k0 + x] = PD[y][x];
+      const int a = F[iu];
+      if (a >= 0) {
+        pup[a] = __float_as_uint(PU[x][y]);
+        pdn[a] = __float_as_uint(PD[y][x]);
+      }
+    }
+  }
+  for (int e = tid; e < B * B; e += 256) {
+    const int x = e / B, y = e % B;
+    if (!(x < y && y < kb)) continue;
+    float bu = F_INF, bd = F_INF;
+    for (int q = 0; q < ny; ++q) {
+      const float su = DKT[x][q] + PD[q][y];
+      const float sd = PU[y][q] + DTK[q][x];
+      bu = su < bu ? su : bu;
+      bd = sd < bd ? sd : bd;
+    }
+    if (bu < F_INF) atomicMin((uint32_t*)(P + (long long)(k0 + x) * n + k0 + y), __float_as_uint(bu));
+    if (bd < F_INF) atomicMin((uint32_t*)(P + (long long)(k0 + y) * n + k0 + x), __float_as_uint(bd));
+  }
+}
+
+// perfect, block b: the K x K targets top-down (x from the top of K: all of its candidates through
+// z in K above x are final), one workgroup per front; four lanes per target split the z loop
+__global__ __launch_bounds__(256) void sup_kk_perfect_kernel(const SupNode* __restrict__ sn,
+                                                             const SupWork* __restrict__ w,
+                                                             const int32_t* __restrict__ farc, float* __restrict__ D,
+                                                             uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+  constexpr int B = SUP_B;
+  __shared__ float Dk[B][B + 1];
+  __shared__ float Pk[B][B + 1];
+  const SupWork W = w[blockIdx.x];
+  const SupNode S = sn[W.s];
+  const int n = S.n, tid = threadIdx.x;
+  const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
+  float* Db = D + 2 * S.dofs;
+  float* P = Db + (long long)n * n;
+  for (int e = tid; e < B * B; e += 256) {
+    const int y = e / B, x = e % B;
+    const bool ok = y < kb && x < kb;
+    Dk[y][x] = ok ? Db[(long long)(k0 + y) * n + k0 + x] : F_INF;
+    Pk[y][x] = ok ? P[(long long)(k0 + y) * n + k0 + x] : F_INF;
+  }
+  __syncthreads();
+  const int g = tid >> 2, q = tid & 3;
+  const int dir = g >> 5, y = g & 31;
+  for (int x = kb - 2; x >= 0; --x) {
+    float best = F_INF;
+    if (y > x && y < kb)
+      for (int z = x + 1 + q; z < kb; z += 4) {
+        if (z == y) continue;
+        const float s = dir == 0 ? Dk[x][z] + Pk[z][y] : Pk[y][z] + Dk[z][x];
+        best = s < best ? s : best;
+      }
+    float o = __shfl_xor(best, 1);
+    best = o < best ? o : best;
+    o = __shfl_xor(best, 2);
+    best = o < best ? o : best;
+    if (q == 0 && y > x && y < kb) {
+      if (dir == 0) {
+        if (best < Pk[x][y]) Pk[x][y] = best;
+      } else {
+        if (best < Pk[y][x]) Pk[y][x] = best;
+      }
+    }
+    __syncthreads();
+  }
+  const int32_t* F = farc + S.foff;
+  for (int e = tid; e < B * B; e += 256) {
+    const int x = e / B, yy = e % B;
+    if (x >= kb || yy >= kb) continue;
+    const long long idx = (long long)(k0 + x) * n + k0 + yy;
+    P[idx] = Pk[x][yy];
+    if (x < yy) {
+      const int a = F[idx];
+      if (a >= 0) {
+        pup[a] = __float_as_uint(Pk[x][yy]);
+        pdn[a] = __float_as_uint(Pk[yy][x]);
+      }
+    }
+  }
+}
+
 // ---- context costs (routing/graph.py edge_records / edge_costs) ----
 constexpr float L_REF_M = 10000.f;
 constexpr int32_t MONDAY_2025_08_25 = 2063 * 86400;   // seconds since 2020-01-01 (a Monday)
@@ -1492,6 +2063,7 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
                            d_up_ptr, d_up_head, d_tofs, N, (long long)T, d_tri);
         if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
           n_tri = T;
+          build_supernodes(tofs);
           build_tasks(tofs);
           build_pull_records(tofs);
         } else {
@@ -1508,6 +2080,240 @@ CchGpu::CchGpu(rcch::Topology T, const float* length, const uint8_t* road_class,
   (void)hipSetDevice(cur);
   if (e != hipSuccess) throw std::runtime_error(std::string("CchGpu: ") + hipGetErrorString(e));
   if (const char* gb = std::getenv("ROUTEST_CCH_CACHE_GB")) cache_gb_ = std::atof(gb);
+}
+
+// The supernodal plan (metric-independent, once per graph).  A supernode is a maximal chain of ranks
+// c0, c0 + 1, ... in which every node is the only child of the next; the chains of at least
+// ROUTEST_CCH_DENSE nodes (default 8; 0: off) and all their ancestor chains are dense fronts, levelled
+// by height in the tree of fronts.  Per level: the gather rows, and per block the panel / trailing
+// (basic) and GEMM / solve / K x K (perfect) workgroup lists.  The nodes outside the fronts keep the
+// per-level kernels: basic by etree height (their heights end far below the top), perfect by depth
+// below their nearest front (all of their ancestors inside fronts are final by then).
+void CchGpu::build_supernodes(const std::vector<int64_t>& tofs) {
+  const char* v = std::getenv("ROUTEST_CCH_DENSE");
+  const int S0 = v ? std::atoi(v) : 8;
+  const int N = T_.N;
+  if (S0 <= 0 || N < 2 || d_tri == nullptr) return;
+  std::vector<int> nch(N, 0);
+  for (int i = 0; i < N; ++i)
+    if (T_.parent[i] >= 0) ++nch[T_.parent[i]];
+  std::vector<int> sid(N), sc0, ssz;
+  for (int i = 0; i < N; ++i) {
+    if (!(i > 0 && T_.parent[i - 1] == i && nch[i] == 1)) {
+      sc0.push_back(i);
+      ssz.push_back(0);
+    }
+    sid[i] = (int)sc0.size() - 1;
+    ++ssz.back();
+  }
+  const int NS = (int)sc0.size();
+  std::vector<int> spar(NS, -1);
+  for (int s = 0; s < NS; ++s) {
+    const int p = T_.parent[sc0[s] + ssz[s] - 1];
+    spar[s] = p >= 0 ? sid[p] : -1;
+  }
+  std::vector<uint8_t> dense(NS, 0);
+  for (int s = 0; s < NS; ++s)
+    if (ssz[s] >= S0)
+      for (int q = s; q >= 0 && !dense[q]; q = spar[q]) dense[q] = 1;
+  std::vector<int> lev(NS, 0);       // children precede parents (ranks grow upward)
+  int L = 0;
+  for (int s = 0; s < NS; ++s) {
+    if (!dense[s]) continue;
+    L = std::max(L, lev[s] + 1);
+    if (spar[s] >= 0) lev[spar[s]] = std::max(lev[spar[s]], lev[s] + 1);
+  }
+  if (L == 0) return;
+  // fronts: chain, then the top node's upward set; every chain arc must lead into the front
+  std::vector<SupNode> sn;
+  std::vector<int32_t> fnode;
+  std::vector<std::vector<int>> by_lev(L);
+  int64_t foff = 0;
+  for (int s = 0; s < NS; ++s) {
+    if (!dense[s]) continue;
+    const int c0 = sc0[s], m = ssz[s], top = c0 + m - 1;
+    const int64_t a0 = T_.up_ptr[top], a1 = T_.up_ptr[top + 1];
+    const int64_t n = m + (a1 - a0);
+    if (n > 32767) return;
+    const int32_t* U0 = T_.up_head.data() + a0;
+    const int32_t* U1 = T_.up_head.data() + a1;
+    for (int i = 0; i < m; ++i)
+      for (int64_t a = T_.up_ptr[c0 + i]; a < T_.up_ptr[c0 + i + 1]; ++a) {
+        const int h = T_.up_head[a];
+        if (!((h > c0 + i && h <= top) || std::binary_search(U0, U1, h))) {
+          std::fprintf(stderr, "[cch] rank %d: arc to %d outside its front; supernodal customization off\n", c0 + i, h);
+          return;
+        }
+      }
+    by_lev[lev[s]].push_back((int)sn.size());
+    sn.push_back(SupNode{0, foff, c0, m, (int32_t)n, (int32_t)fnode.size()});
+    for (int i = 0; i < m; ++i) fnode.push_back(c0 + i);
+    fnode.insert(fnode.end(), U0, U1);
+    foff += n * n;
+  }
+  const auto cdiv = [](int64_t a, int64_t b) { return (a + b - 1) / b; };
+  std::vector<SupWork> work;
+  auto range_of = [&](int64_t from) { return SupRange{from, (int64_t)work.size() - from}; };
+  // every front row (farc build)
+  for (int f = 0; f < (int)sn.size(); ++f)
+    for (int i = 0; i < sn[f].n; ++i) work.push_back(SupWork{f, i, 0, 0});
+  const SupRange all_rows = range_of(0);
+  std::vector<SupLevel> levs(L);
+  int64_t buf = 0;
+  int blocks = 0;
+  for (int l = 0; l < L; ++l) {
+    SupLevel& SL = levs[l];
+    int64_t dofs = 0;
+    int nbmax = 0;
+    for (int f : by_lev[l]) {
+      sn[f].dofs = dofs;
+      dofs += (int64_t)sn[f].n * sn[f].n;
+      nbmax = std::max(nbmax, (int)cdiv(sn[f].m, SUP_B));
+    }
+    buf = std::max(buf, dofs);
+    blocks += nbmax;
+    int64_t w0 = (int64_t)work.size();
+    for (int f : by_lev[l])
+      for (int i = 0; i < sn[f].n; ++i) work.push_back(SupWork{f, i, 0, 0});
+    SL.gather = range_of(w0);
+    for (int r = 0; r < nbmax; ++r) {
+      w0 = (int64_t)work.size();
+      for (int f : by_lev[l]) {
+        const SupNode& S = sn[f];
+        if (cdiv(S.m, SUP_B) <= r) continue;
+        const int k1 = std::min(SUP_B * (r + 1), S.m);
+        const int nt = std::max<int64_t>(1, cdiv(S.n - k1, SUP_PJ));
+        for (int t = 0; t < nt; ++t) work.push_back(SupWork{f, r, t, 0});
+      }
+      SL.panel.push_back(range_of(w0));
+      w0 = (int64_t)work.size();
+      for (int f : by_lev[l]) {
+        const SupNode& S = sn[f];
+        if (cdiv(S.m, SUP_B) <= r) continue;
+        const int k1 = std::min(SUP_B * (r + 1), S.m);
+        const int T = (int)cdiv(S.n - k1, SUP_TT);
+        for (int ty = 0; ty < T; ++ty)
+          for (int tz = 0; tz < T; ++tz) work.push_back(SupWork{f, r, ty, tz});
+      }
+      SL.trail.push_back(range_of(w0));
+      // perfect: the r-th block from the top of every front that has one
+      w0 = (int64_t)work.size();
+      for (int f : by_lev[l]) {
+        const SupNode& S = sn[f];
+        const int nb = (int)cdiv(S.m, SUP_B);
+        if (nb <= r) continue;
+        const int b = nb - 1 - r, k1 = std::min(SUP_B * (b + 1), S.m), nF = S.n - k1;
+        if (nF <= 0) continue;
+        const int TY = (int)cdiv(nF, SUP_G1Y), Z = (int)cdiv(nF, SUP_G1Z);
+        for (int dir = 0; dir < 2; ++dir)
+          for (int zs = 0; zs < Z; ++zs)
+            for (int ty = 0; ty < TY; ++ty) work.push_back(SupWork{f, b, ty, (zs << 1) | dir});
+      }
+      SL.gemm.push_back(range_of(w0));
+      w0 = (int64_t)work.size();
+      for (int f : by_lev[l]) {
+        const SupNode& S = sn[f];
+        const int nb = (int)cdiv(S.m, SUP_B);
+        if (nb <= r) continue;
+        const int b = nb - 1 - r, k1 = std::min(SUP_B * (b + 1), S.m), nF = S.n - k1;
+        for (int t = 0; t < (int)cdiv(nF, SUP_SJ); ++t) work.push_back(SupWork{f, b, t, 0});
+      }
+      SL.solve.push_back(range_of(w0));
+      w0 = (int64_t)work.size();
+      for (int f : by_lev[l]) {
+        const SupNode& S = sn[f];
+        const int nb = (int)cdiv(S.m, SUP_B);
+        if (nb > r) work.push_back(SupWork{f, nb - 1 - r, 0, 0});
+      }
+      SL.kk.push_back(range_of(w0));
+    }
+  }
+  // the other nodes: perfect by depth below their nearest front
+  std::vector<uint8_t> node_in(N, 0);
+  int nodes_in = 0;
+  for (int i = 0; i < N; ++i)
+    if (dense[sid[i]]) {
+      node_in[i] = 1;
+      ++nodes_in;
+    }
+  std::vector<int> rd(N, -1);
+  int R = 0, hmax = -1;
+  for (int x = N - 1; x >= 0; --x) {
+    if (node_in[x]) continue;
+    const int p = T_.parent[x];
+    rd[x] = (p < 0 || node_in[p]) ? 0 : rd[p] + 1;
+    R = std::max(R, rd[x] + 1);
+    hmax = std::max(hmax, T_.height[x]);
+  }
+  std::vector<int64_t> rptr(R + 1, 0);
+  for (int x = 0; x < N; ++x)
+    if (rd[x] >= 0) ++rptr[rd[x] + 1];
+  for (int d = 0; d < R; ++d) rptr[d + 1] += rptr[d];
+  std::vector<int> order(rptr[R]);
+  {
+    std::vector<int64_t> pos(rptr.begin(), rptr.end() - 1);
+    for (int x = 0; x < N; ++x)
+      if (rd[x] >= 0) order[pos[rd[x]]++] = x;
+  }
+  std::vector<PArc> parc;
+  std::vector<int64_t> raofs(R + 1, 0);
+  std::vector<int> rnodes(R, 0), rkmax(R, 0);
+  std::vector<uint8_t> rmulti(R, 0);
+  for (int d = 0; d < R; ++d) {
+    raofs[d] = (int64_t)parc.size();
+    for (int64_t q = rptr[d]; q < rptr[d + 1]; ++q) {
+      const int x = order[q];
+      const int a0 = (int)T_.up_ptr[x], k = (int)(T_.up_ptr[x + 1] - T_.up_ptr[x]);
+      if (k > 0xFFFF) return;
+      ++rnodes[d];
+      rkmax[d] = std::max(rkmax[d], k);
+      if (k >= 2) rmulti[d] = 1;
+      for (int ia = 0; ia < k; ++ia)
+        parc.push_back(PArc{tofs[x], a0, (int32_t)T_.up_head[a0 + ia], (uint16_t)k, (uint16_t)ia, 0});
+    }
+  }
+  raofs[R] = (int64_t)parc.size();
+  // device copies; any failure leaves the plan off (nothing filtered yet)
+  SupNode* dsn = nullptr;
+  SupWork* dwk = nullptr;
+  int32_t *dfn = nullptr, *dfa = nullptr;
+  PArc* dpa = nullptr;
+  bool ok = up_copy(dsn, sn.data(), sn.size()) == hipSuccess && up_copy(dwk, work.data(), work.size()) == hipSuccess &&
+            up_copy(dfn, fnode.data(), fnode.size()) == hipSuccess && dmalloc(dfa, (size_t)foff) == hipSuccess &&
+            up_copy(dpa, parc.data(), parc.size()) == hipSuccess && dmalloc(cs0_.sup_buf, (size_t)buf) == hipSuccess;
+  if (ok) {
+    hipLaunchKernelGGL(sup_farc_kernel, dim3((unsigned)cdiv(all_rows.cnt, 4)), dim3(256), 0, 0, dsn, dwk + all_rows.off,
+                       (long long)all_rows.cnt, dfn, d_up_ptr, d_up_head, dfa);
+    ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+  }
+  if (!ok) {
+    (void)hipGetLastError();
+    dfree(dsn);
+    dfree(dwk);
+    dfree(dfn);
+    dfree(dfa);
+    dfree(dpa);
+    dfree(cs0_.sup_buf);
+    std::fprintf(stderr, "[cch] supernodal plan: device allocation failed; per-level customization\n");
+    return;
+  }
+  d_sup_sn = dsn;
+  d_sup_work = dwk;
+  d_sup_fnode = dfn;
+  d_sup_farc = dfa;
+  d_parc2 = dpa;
+  sup_buf_entries_ = buf;
+  sup_lev_ = std::move(levs);
+  sup_node_ = std::move(node_in);
+  rlev_aofs_ = std::move(raofs);
+  rlev_nodes_ = std::move(rnodes);
+  rlev_kmax_ = std::move(rkmax);
+  rlev_multi_ = std::move(rmulti);
+  sup_fronts_ = (int)sn.size();
+  sup_nodes_ = nodes_in;
+  sup_blocks_ = blocks;
+  sparse_heights_ = hmax + 1;
+  sup_on_ = true;
 }
 
 // the task tables of the task-table customization (metric-independent; level order)
@@ -1533,7 +2339,7 @@ void CchGpu::build_pull_records(const std::vector<int64_t>& tofs) {
   // the narrow top of the perfect phase: the longest prefix of depths with at most `thr` arcs each
   // (ROUTEST_CCH_TAIL as for the basic phase)
   const char* v = std::getenv("ROUTEST_CCH_TAIL");
-  const int64_t thr = v ? std::atoll(v) : 0;
+  const int64_t thr = v && !sup_on_ ? std::atoll(v) : 0;
   int d = 0;
   while (thr > 0 && d < T_.max_depth && aofs_[T_.dlev_ptr[d + 1]] - aofs_[T_.dlev_ptr[d]] <= thr) ++d;
   if (d >= 2) {
@@ -1565,6 +2371,7 @@ void CchGpu::build_tasks(const std::vector<int64_t>& tofs) {
   for (int h = 0; h <= T_.max_height; ++h) {
     for (int64_t q = T_.hlev_ptr[h]; q < T_.hlev_ptr[h + 1]; ++q) {
       const int z = T_.hlev_nodes[q];
+      if (sup_on_ && sup_node_[z]) continue;                // a dense front's (sup_panel_basic_kernel)
       const int k = (int)(T_.up_ptr[z + 1] - T_.up_ptr[z]);
       if (k > 0xFFFE) { bt.clear(); pt.clear(); return; }   // (never on road graphs: k <= ~2k)
       const int a0 = (int)T_.up_ptr[z];
@@ -1597,7 +2404,7 @@ void CchGpu::build_tasks(const std::vector<int64_t>& tofs) {
   // 500 levels made the basic phase 11.4 -> 39.7 ms, profiles/cch_customize_r6.md)
   {
     const char* v = std::getenv("ROUTEST_CCH_TAIL");
-    const int64_t thr = v ? std::atoll(v) : 0;
+    const int64_t thr = v && !sup_on_ ? std::atoll(v) : 0;
     int h = T_.max_height + 1;
     while (thr > 0 && h > 1 && btask_ptr_[h] - btask_ptr_[h - 1] <= thr) --h;
     if (thr > 0 && h <= T_.max_height && !bt.empty()) {
@@ -1674,6 +2481,11 @@ CchGpu::~CchGpu() {
   dfree(d_ptask);
   dfree(d_tail_end_);
   dfree(d_ptail_end_);
+  dfree(d_sup_sn);
+  dfree(d_sup_work);
+  dfree(d_sup_fnode);
+  dfree(d_sup_farc);
+  dfree(d_parc2);
   free_scratch(cs0_);
   (void)hipSetDevice(cur);
 }
@@ -1708,6 +2520,7 @@ hipError_t CchGpu::alloc_scratch(CustScratch& x) {
   ck(dmalloc(x.tail_ctl, (size_t)T_.max_height + (size_t)T_.max_depth + 8));   // basic | perfect tail
   if (x.tail_ctl != nullptr)
     ck(hipMemset(x.tail_ctl, 0, ((size_t)T_.max_height + (size_t)T_.max_depth + 8) * sizeof(int)));
+  if (sup_on_) ck(dmalloc(x.sup_buf, (size_t)sup_buf_entries_));
   return e;
 }
 
@@ -1726,6 +2539,7 @@ void CchGpu::free_scratch(CustScratch& x) {
   if (x.h_stage) (void)hipHostFree(x.h_stage);
   x.h_stage = nullptr;
   dfree(x.tail_ctl);
+  dfree(x.sup_buf);
 }
 
 hipError_t CchGpu::context_costs(const CchContext& c, float* d_cost, hipStream_t s, CustScratch* cs) {
@@ -1867,6 +2681,27 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
                            m.sub_up, m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
       ck(hipGetLastError());
     }
+    // the dense fronts (build_supernodes), bottom-up by front level: gather, then per block of 32
+    // pivots the panel and the trailing update (the task table above left their nodes out)
+    const bool sup = sup_on_ && tasks;
+    if (sup && X.sup_buf == nullptr) ck(hipErrorOutOfMemory);
+    const SupNode* sup_sn = (const SupNode*)d_sup_sn;
+    const SupWork* sup_wk = (const SupWork*)d_sup_work;
+    for (size_t l = 0; sup && l < sup_lev_.size() && e == hipSuccess; ++l) {
+      const SupLevel& SL = sup_lev_[l];
+      hipLaunchKernelGGL(sup_gather_basic_kernel, dim3(blocks_for(SL.gather.cnt, 4)), dim3(256), 0, s, sup_sn,
+                         sup_wk + SL.gather.off, (long long)SL.gather.cnt, d_sup_farc, X.up64, X.dn64, X.sup_buf);
+      for (size_t r = 0; r < SL.panel.size(); ++r) {
+        if (SL.panel[r].cnt > 0)
+          hipLaunchKernelGGL(sup_panel_basic_kernel, dim3((unsigned)SL.panel[r].cnt), dim3(256), 0, s, sup_sn,
+                             sup_wk + SL.panel[r].off, d_sup_fnode, d_sup_farc, X.sup_buf, X.up64, X.dn64, m.sub_up,
+                             m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length, d_up_ptr, d_up_head);
+        if (SL.trail[r].cnt > 0)
+          hipLaunchKernelGGL(sup_trailing_basic_kernel, dim3((unsigned)SL.trail[r].cnt), dim3(256), 0, s, sup_sn,
+                             sup_wk + SL.trail[r].off, d_sup_farc, X.sup_buf, X.up64, X.dn64);
+      }
+      ck(hipGetLastError());
+    }
     if (ev && ev[1]) (void)hipEventRecord(ev[1], s);
     // perfect, top-down by depth
     hipLaunchKernelGGL(perfect_init_kernel, dim3(fill_blocks), dim3(256), 0, s, X.up64, X.dn64, X.pup, X.pdn, (long long)M);
@@ -1882,7 +2717,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
       const char* v = std::getenv("ROUTEST_CCH_PERFECT");
       return v && std::string(v) == "tasks";
     }();
-    const bool ptasks = env_ptasks && d_ptask != nullptr;
+    const bool ptasks = env_ptasks && d_ptask != nullptr && !sup;
     for (int d = 0; d <= T_.max_depth && e == hipSuccess && tasks && ptasks; ++d) {
       const long long nt = ptask_ptr_[d + 1] - ptask_ptr_[d];
       if (nt <= 0) continue;
@@ -1892,7 +2727,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
       ck(hipGetLastError());
     }
     // the narrow top depths: one persistent launch (perfect_tail_kernel), a wave per arc at a time
-    const bool ptail = !(tasks && ptasks) && pull && d_tri != nullptr && d_parc != nullptr && n_ptail_lev_ > 0 &&
+    const bool ptail = !sup && !(tasks && ptasks) && pull && d_tri != nullptr && d_parc != nullptr && n_ptail_lev_ > 0 &&
                        X.tail_ctl != nullptr;
     if (ptail && e == hipSuccess) {
       int* pctl = X.tail_ctl + T_.max_height + 4;
@@ -1906,18 +2741,13 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
                          n_ptail_lev_, pctl, 100LL * 1000 * 1000, X.up64, X.dn64, X.pup, X.pdn);
       ck(hipGetLastError());
     }
-    for (int d = ptail ? n_ptail_lev_ : 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && pull && d_tri != nullptr; ++d) {
-      const int lo = (int)T_.dlev_ptr[d], hi = (int)T_.dlev_ptr[d + 1];
-      if (lo >= hi) continue;
-      PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri,
-                 (const PArc*)d_parc};
-      if (P.arcs <= 0 || pofs_[hi] == pofs_[lo]) continue;       // no node of the level has two arcs
+    // one depth level of the pull (nodes: its node count; km: its widest node's arcs)
+    auto pull_level = [&](PullArgs P, long long nodes, int km) {
       // mean degree of the level's nodes: wide nodes get a wave per arc, narrow ones a lane per arc
-      const bool wave = P.arcs >= 24 * (long long)(hi - lo);
+      const bool wave = P.arcs >= 24 * nodes;
       // waves per arc by the level's widest node (ROUTEST_CCH_PULL_SPLIT=0: one)
       static const bool split = !(std::getenv("ROUTEST_CCH_PULL_SPLIT") &&
                                   std::string(std::getenv("ROUTEST_CCH_PULL_SPLIT")) == "0");
-      const int km = plev_kmax_[d];
       // (only where the level's arcs alone do not fill the GPU: 1M-city levels of thousands of wide
       // nodes are bound by their random gathers, and splitting them measured 1 % slower, r5z)
       const int S = (!split || P.arcs >= 8192) ? 1 : (km > 768 ? 4 : (km > 256 ? 2 : 1));
@@ -1940,8 +2770,43 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
                              X.dn64, X.pup, X.pdn);
         ck(hipGetLastError());
       }
+    };
+    for (int d = ptail ? n_ptail_lev_ : 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && pull && d_tri != nullptr && !sup; ++d) {
+      const int lo = (int)T_.dlev_ptr[d], hi = (int)T_.dlev_ptr[d + 1];
+      if (lo >= hi) continue;
+      PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri,
+                 (const PArc*)d_parc};
+      if (P.arcs <= 0 || pofs_[hi] == pofs_[lo]) continue;       // no node of the level has two arcs
+      pull_level(P, hi - lo, plev_kmax_[d]);
     }
-    for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && !(pull && d_tri != nullptr); ++d) {
+    // the dense fronts top-down by front level (per block from the top: the (min, +) product through
+    // the final part, the solve through K, the K x K targets), then the other nodes by depth below
+    // their nearest front, pulled over d_parc2
+    for (int l = (int)sup_lev_.size() - 1; sup && l >= 0 && e == hipSuccess; --l) {
+      const SupLevel& SL = sup_lev_[l];
+      float* Dp = (float*)X.sup_buf;
+      hipLaunchKernelGGL(sup_gather_perfect_kernel, dim3(blocks_for(SL.gather.cnt, 4)), dim3(256), 0, s, sup_sn,
+                         sup_wk + SL.gather.off, (long long)SL.gather.cnt, d_sup_farc, X.up64, X.dn64, X.pup, X.pdn, Dp);
+      for (size_t r = 0; r < SL.kk.size(); ++r) {
+        if (SL.gemm[r].cnt > 0)
+          hipLaunchKernelGGL(sup_gemm_perfect_kernel, dim3((unsigned)SL.gemm[r].cnt), dim3(256), 0, s, sup_sn,
+                             sup_wk + SL.gemm[r].off, Dp);
+        if (SL.solve[r].cnt > 0)
+          hipLaunchKernelGGL(sup_solve_perfect_kernel, dim3((unsigned)SL.solve[r].cnt), dim3(256), 0, s, sup_sn,
+                             sup_wk + SL.solve[r].off, d_sup_farc, Dp, X.pup, X.pdn);
+        if (SL.kk[r].cnt > 0)
+          hipLaunchKernelGGL(sup_kk_perfect_kernel, dim3((unsigned)SL.kk[r].cnt), dim3(256), 0, s, sup_sn,
+                             sup_wk + SL.kk[r].off, d_sup_farc, Dp, X.pup, X.pdn);
+      }
+      ck(hipGetLastError());
+    }
+    for (size_t d = 0; sup && d < rlev_nodes_.size() && e == hipSuccess; ++d) {
+      if (!rlev_multi_[d]) continue;
+      PullArgs P{d_up_ptr, d_up_head, nullptr, nullptr, 0, 0, rlev_aofs_[d], rlev_aofs_[d + 1] - rlev_aofs_[d], d_tofs,
+                 d_tri, (const PArc*)d_parc2};
+      pull_level(P, rlev_nodes_[d], rlev_kmax_[d]);
+    }
+    for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && !(pull && d_tri != nullptr) && !sup; ++d) {
       LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0, d_tofs, d_tri};
       if (L.lo >= L.hi) continue;
       L.base = pofs_[L.lo];

@@ -93,6 +93,13 @@ class PyCchGpu {
     d["basic_tail_levels"] = g_->basic_tail_levels();
     d["perfect_tail_levels"] = g_->perfect_tail_levels();
     d["perfect_tasks"] = g_->perfect_tasks();
+    d["supernodal"] = g_->supernodal();
+    d["sup_fronts"] = g_->sup_fronts();
+    d["sup_nodes"] = g_->sup_nodes();
+    d["sup_levels"] = g_->sup_levels();
+    d["sup_blocks"] = g_->sup_blocks();
+    d["sparse_heights"] = g_->sparse_heights();
+    d["sparse_depths"] = g_->sparse_depths();
     d["cache_capacity"] = g_->capacity();
     d["cache_gb"] = g_->cache_gb();
     d["metric_bytes"] = g_->metric_bytes();
@@ -191,6 +198,32 @@ class PyCchGpu {
     }
     CCH_CHECK_HIP(e);
     return info(*m, true);
+  }
+
+  // device copies of a cached metric's arrays (tests: two customization paths must agree bit for bit)
+  py::dict metric_dump(int64_t key) {
+    auto m = get(key);
+    const int64_t M = g_->topo().M, N = g_->topo().N;
+    const auto opt = torch::TensorOptions().device(torch::kCUDA, dev_);
+    const c10::DeviceGuard guard(opt.device());
+    py::dict d;
+    auto put = [&](const char* name, const void* src, int64_t n, torch::ScalarType t) {
+      auto out = torch::empty({n}, opt.dtype(t));
+      if (n > 0)
+        CCH_CHECK_HIP(hipMemcpyAsync(out.data_ptr(), src, n * out.element_size(), hipMemcpyDeviceToDevice, stream_of(dev_)));
+      d[name] = out;
+    };
+    put("sub_up", m->sub_up, 2 * M, torch::kInt32);
+    put("sub_dn", m->sub_dn, 2 * M, torch::kInt32);
+    put("len_up", m->len_up, M, torch::kFloat32);
+    put("len_dn", m->len_dn, M, torch::kFloat32);
+    put("cnt_up", m->cnt_up, M, torch::kInt32);
+    put("cnt_dn", m->cnt_dn, M, torch::kInt32);
+    put("f_ptr", m->f_ptr, N + 1, torch::kInt32);
+    put("b_ptr", m->b_ptr, N + 1, torch::kInt32);
+    put("f_rec", m->f_rec, 4 * m->kept_f, torch::kInt32);
+    put("b_rec", m->b_rec, 4 * m->kept_b, torch::kInt32);
+    return d;
   }
 
   torch::Tensor costs(int64_t key) {
@@ -360,6 +393,7 @@ void bind_cch_gpu(py::module& m) {
       .def("pinned", &PyCchGpu::pinned)
       .def("metric_from_costs", &PyCchGpu::metric_from_costs, py::arg("key"), py::arg("cost"))
       .def("costs", &PyCchGpu::costs, py::arg("key"))
+      .def("metric_dump", &PyCchGpu::metric_dump, py::arg("key"))
       .def("route", &PyCchGpu::route, py::arg("key"), py::arg("src"), py::arg("dst"), py::arg("max_path") = 4096,
            py::arg("want_path") = true)
       .def("matrix", &PyCchGpu::matrix, py::arg("key"), py::arg("pts"), py::arg("npts"))

@@ -89,6 +89,7 @@ struct CustScratch {
   float* min_buf = nullptr;                        // their minutes [2E]
   float* h_stage = nullptr;                        // pinned [E]: the costs' host copy lands here first
   int* tail_ctl = nullptr;                         // basic_tail_kernel: cursor, timed-out flag, done[level]
+  unsigned long long* sup_buf = nullptr;           // dense fronts of one supernode level (build_supernodes)
 };
 
 // The device pointers of one metric that the query kernels read — an array of these plus a group
@@ -133,6 +134,14 @@ class CchGpu {
   int basic_tail_levels() const { return n_tail_lev_; }   // top basic levels run by ONE persistent launch
   int perfect_tail_levels() const { return n_ptail_lev_; }  // top perfect depths run by ONE persistent launch
   int64_t perfect_tasks() const { return n_ptask_; }
+  // supernodal customization of the etree's top (csrc/cch.hip build_supernodes; ROUTEST_CCH_DENSE)
+  bool supernodal() const { return sup_on_; }
+  int sup_fronts() const { return sup_fronts_; }
+  int sup_nodes() const { return sup_nodes_; }
+  int sup_levels() const { return (int)sup_lev_.size(); }
+  int sup_blocks() const { return sup_blocks_; }
+  int sparse_heights() const { return sparse_heights_; }
+  int sparse_depths() const { return (int)rlev_nodes_.size(); }
 
   // ETA model used for context costs (the fused K1+K2 kernel's 32x32 blob on this device)
   void set_eta(const void* blob, int H, const NormParams& np, int variant, int num_cus);
@@ -275,6 +284,32 @@ class CchGpu {
   // ... and of the perfect phase (depths 0 .. n_ptail_lev_ - 1): perfect_tail_kernel over their arcs
   int n_ptail_lev_ = 0, ptail_max_arcs_ = 0;
   int* d_ptail_end_ = nullptr;
+  // supernodal top: the chains of at least ROUTEST_CCH_DENSE nodes and every ancestor chain are dense
+  // fronts, customized level by level of the supernode tree (csrc/cch.hip sup_*_kernel); the rest of
+  // the nodes keep the per-level kernels (basic: the task table without the fronts' nodes; perfect:
+  // the pull over d_parc2, by depth below the nearest front)
+  void build_supernodes(const std::vector<int64_t>& tofs);
+  struct SupRange {
+    int64_t off = 0, cnt = 0;
+  };
+  struct SupLevel {
+    SupRange gather;
+    std::vector<SupRange> panel, trail;          // basic, per block (bottom-up)
+    std::vector<SupRange> gemm, solve, kk;       // perfect, per block from the top
+  };
+  bool sup_on_ = false;
+  std::vector<uint8_t> sup_node_;                  // [N] rank in a dense front
+  std::vector<SupLevel> sup_lev_;
+  void* d_sup_sn = nullptr;                        // SupNode per front
+  void* d_sup_work = nullptr;                      // SupWork lists of every launch
+  int32_t* d_sup_fnode = nullptr;                  // the fronts' node lists
+  int32_t* d_sup_farc = nullptr;                   // the fronts' arc tables
+  int64_t sup_buf_entries_ = 0;                    // dense entries of the largest level
+  int sup_fronts_ = 0, sup_nodes_ = 0, sup_blocks_ = 0, sparse_heights_ = 0;
+  void* d_parc2 = nullptr;                         // PArc of the other nodes, by depth below their front
+  std::vector<int64_t> rlev_aofs_;
+  std::vector<int> rlev_nodes_, rlev_kmax_;
+  std::vector<uint8_t> rlev_multi_;                // a node of the level has >= 2 arcs
   // customization temporaries: cs0_ for callers on their own streams (one at a time: mu_cust_),
   // one set per background builder (no lock: each builder owns its set)
   hipError_t alloc_scratch(CustScratch& x);

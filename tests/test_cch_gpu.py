@@ -170,6 +170,7 @@ def test_persistent_tails_bit_identical_to_cpu(setup, monkeypatch, tail):
     from routest_amd.routing.cch import RoadRouter
     g, m, router, cost, key, cpu, mc = setup
     monkeypatch.setenv("ROUTEST_CCH_TAIL", tail)
+    monkeypatch.setenv("ROUTEST_CCH_DENSE", "0")      # (the tails are the per-level path's top)
     r2 = RoadRouter(g, m, device="cuda:0")
     st = r2.stats()
     assert st["basic_tail_levels"] > 0 and st["perfect_tail_levels"] > 0, st
@@ -179,3 +180,24 @@ def test_persistent_tails_bit_identical_to_cpu(setup, monkeypatch, tail):
     b = cpu.query(mc, src, dst, False)
     for x, y in zip(a[:3], b[:3]):
         assert np.array_equal(np.asarray(x), np.asarray(y))
+
+
+def test_supernodal_fronts_bit_identical_to_per_level(setup, monkeypatch):
+    """ROUTEST_CCH_DENSE: the dense-front customization of the elimination tree's top (csrc/cch.hip
+    sup_*_kernel: blocked (min, +) elimination / back substitution per chain) gives the per-level
+    kernels' metric arrays bit for bit — with no fronts (0), every chain a front (1), only long chains
+    (32) and the default — and so the CPU reference's answers (the other tests here run the default)."""
+    from routest_amd.routing.cch import RoadRouter
+    g, m, router, cost, key, cpu, mc = setup
+    st = router.stats()
+    assert st["supernodal"] and st["sup_fronts"] > 0 and st["sparse_depths"] < st["max_depth"], st
+    base = {k: v.cpu() for k, v in router.gpu.metric_dump(key).items()}
+    for thr in ("0", "1", "32"):
+        monkeypatch.setenv("ROUTEST_CCH_DENSE", thr)
+        r2 = RoadRouter(g, m, device="cuda:0")
+        assert bool(r2.stats()["supernodal"]) == (thr != "0"), r2.stats()
+        k2 = r2.metric_from_costs(1 << 42, cost)
+        d = {k: v.cpu() for k, v in r2.gpu.metric_dump(k2).items()}
+        for name, ref in base.items():
+            assert torch.equal(d[name], ref), (thr, name)
+        del r2
