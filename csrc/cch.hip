@@ -805,7 +805,7 @@ constexpr int SUP_B = 32;      // pivots per block
 constexpr int SUP_PJ = 32;     // basic panel: front columns per workgroup
 constexpr int SUP_TT = 64;     // basic trailing update: 64 x 64 targets per workgroup
 constexpr int SUP_G1Y = 32;    // perfect GEMM: 32 output columns per workgroup
-constexpr int SUP_G1Z = 512;   // ... over at most 512 intermediate nodes (more: split, atomicMin)
+constexpr int SUP_G1Z = 128;   // ... over at most 128 intermediate nodes (more: split, atomicMin)
 constexpr int SUP_SJ = 64;     // perfect solve: front columns per workgroup
 
 __device__ __forceinline__ unsigned long long sup_cand(unsigned long long a, unsigned long long b, uint32_t z) {
@@ -831,26 +831,41 @@ __global__ __launch_bounds__(256) void sup_farc_kernel(const SupNode* __restrict
   }
 }
 
-// basic: a front's rows from the arc weights (all lower levels are done); U x U starts at +inf
-__global__ __launch_bounds__(256) void sup_gather_basic_kernel(const SupNode* __restrict__ sn, const SupWork* __restrict__ w,
-                                                               long long nw, const int32_t* __restrict__ farc,
-                                                               const unsigned long long* __restrict__ up,
-                                                               const unsigned long long* __restrict__ dn,
-                                                               unsigned long long* __restrict__ D) {
-  const long long wi = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (wi >= nw) return;
-  const SupWork W = w[wi];
+// basic: a front's rows from the arc weights (all lower levels are done; U x U starts at +inf), a
+// workgroup per row.  An entry whose best triangle so far has a middle node (necessarily below the
+// front: no pivot of it has run) also gets that triangle's finalization now — sub-arcs by binary
+// search, metres, road edges — in SS / SL: the elimination only adds middles from the chain, so if
+// the entry still has this middle at the end, the panel takes it from here (off its serial path).
+__global__ __launch_bounds__(256) void sup_gather_basic_kernel(
+    const SupNode* __restrict__ sn, const SupWork* __restrict__ w, const int32_t* __restrict__ fnode,
+    const int32_t* __restrict__ farc, const unsigned long long* __restrict__ up, const unsigned long long* __restrict__ dn,
+    const int32_t* __restrict__ up_ptr, const int32_t* __restrict__ up_head, const float* __restrict__ len_up,
+    const float* __restrict__ len_dn, const int32_t* __restrict__ cnt_up, const int32_t* __restrict__ cnt_dn,
+    unsigned long long* __restrict__ D, int2* __restrict__ SS, int2* __restrict__ SL) {
+  const SupWork W = w[blockIdx.x];
   const SupNode S = sn[W.s];
   const int i = W.b, n = S.n;
-  unsigned long long* row = D + S.dofs + (long long)i * n;
+  const long long r0 = S.dofs + (long long)i * n;
   const int32_t* fr = farc + S.foff + (long long)i * n;
-  for (int j = threadIdx.x & 63; j < n; j += 64) {
+  const int fi = fnode[S.fnode + i];
+  for (int j = threadIdx.x; j < n; j += 256) {
     unsigned long long v = PACK_INF_D;
     if (i != j && (i < S.m || j < S.m)) {
       const int a = fr[j];
-      if (a >= 0) v = i < j ? up[a] : dn[a];
+      if (a >= 0) {
+        v = i < j ? up[a] : dn[a];
+        const uint32_t pl = (uint32_t)v;
+        if (wof(v) < F_INF && !(pl & EDGE_FLAG_D)) {
+          const int zz = (int)pl, fj = fnode[S.fnode + j];
+          const int lo = i < j ? fi : fj, hi = i < j ? fj : fi;
+          const int azx = find_arc_d(up_ptr, up_head, zz, lo), azv = find_arc_d(up_ptr, up_head, zz, hi);
+          const int s0 = i < j ? azx : azv, s1 = i < j ? azv : azx;
+          SS[r0 + j] = make_int2(s0, s1);
+          SL[r0 + j] = make_int2(__float_as_int(len_dn[s0] + len_up[s1]), cnt_dn[s0] + cnt_up[s1]);
+        }
+      }
     }
-    row[j] = v;
+    D[r0 + j] = v;
   }
 }
 
@@ -858,20 +873,23 @@ __global__ __launch_bounds__(256) void sup_gather_basic_kernel(const SupNode* __
 // row / column panels of this workgroup's 32 front columns J (every workgroup of the front redoes
 // the 32 x 32 diagonal block: no inter-workgroup dependency), then the rows of K are final: their
 // arcs' weights go out, and they are FINALIZED (best triangle's sub-arcs, metres, road edges —
-// basic_task_run's ROW_FINAL) — a middle node inside K needs the lengths of an arc of K finalized
-// just before, so those go row by row from LDS after the others went in parallel.
-__global__ __launch_bounds__(256) void sup_panel_basic_kernel(
-    const SupNode* __restrict__ sn, const SupWork* __restrict__ w, const int32_t* __restrict__ fnode,
-    const int32_t* __restrict__ farc, unsigned long long* __restrict__ D, unsigned long long* __restrict__ up,
-    unsigned long long* __restrict__ dn, int32_t* __restrict__ sub_up, int32_t* __restrict__ sub_dn,
-    float* __restrict__ len_up, float* __restrict__ len_dn, int32_t* __restrict__ cnt_up, int32_t* __restrict__ cnt_dn,
-    const float* __restrict__ length, const int32_t* __restrict__ up_ptr, const int32_t* __restrict__ up_head) {
+// basic_task_run's ROW_FINAL): a middle below the front from the gather's SS / SL, one in an earlier
+// block from its (final) arcs, and one inside K row by row from LDS (it needs the lengths of an arc
+// of K finalized just before).  1024 threads: one entry of each matrix per thread and pivot.
+__global__ __launch_bounds__(1024) void sup_panel_basic_kernel(
+    const SupNode* __restrict__ sn, const SupWork* __restrict__ w, const int32_t* __restrict__ farc,
+    unsigned long long* __restrict__ D, const int2* __restrict__ SS, const int2* __restrict__ SL,
+    unsigned long long* __restrict__ up, unsigned long long* __restrict__ dn, int32_t* __restrict__ sub_up,
+    int32_t* __restrict__ sub_dn, float* __restrict__ len_up, float* __restrict__ len_dn, int32_t* __restrict__ cnt_up,
+    int32_t* __restrict__ cnt_dn, const float* __restrict__ length) {
   constexpr int B = SUP_B, J = SUP_PJ, W2 = SUP_B + SUP_PJ;
+  static_assert(B == 32 && J == 32, "one entry of each matrix per thread");
   __shared__ unsigned long long Dk[B][B + 1];   // D[K][K]
   __shared__ unsigned long long R[B][J + 1];    // D[K][J]
   __shared__ unsigned long long C[J][B + 1];    // D[J][K]
-  __shared__ float lu[B][W2], ld[B][W2];        // finalized metres of the rows of K: columns K | J
-  __shared__ int32_t cu[B][W2], cd[B][W2];
+  __shared__ int32_t FK[B][W2];                 // arcs of the rows of K: columns K | J
+  __shared__ float lu[B][W2], ld[B][W2];        // their finalized metres
+  __shared__ int32_t cu[B][W2], cd[B][W2];      // ... and road edges
   const SupWork W = w[blockIdx.x];
   const SupNode S = sn[W.s];
   const int n = S.n, tid = threadIdx.x;
@@ -880,74 +898,59 @@ __global__ __launch_bounds__(256) void sup_panel_basic_kernel(
   const bool diag_writer = W.t0 == 0;
   unsigned long long* Df = D + S.dofs;
   const int32_t* F = farc + S.foff;
-  for (int e = tid; e < B * B; e += 256) {
-    const int y = e / B, x = e % B;
-    Dk[y][x] = (y < kb && x < kb) ? Df[(long long)(k0 + y) * n + k0 + x] : PACK_INF_D;
-  }
-  for (int e = tid; e < B * J; e += 256) {
-    const int y = e / J, j = e % J;
-    R[y][j] = (y < kb && j < nj) ? Df[(long long)(k0 + y) * n + j0 + j] : PACK_INF_D;
-  }
-  for (int e = tid; e < J * B; e += 256) {
-    const int j = e / B, y = e % B;
-    C[j][y] = (y < kb && j < nj) ? Df[(long long)(j0 + j) * n + k0 + y] : PACK_INF_D;
+  const int ty = tid >> 5, tx = tid & 31;      // (row, column) of this thread's entry of each matrix
+  Dk[ty][tx] = (ty < kb && tx < kb) ? Df[(long long)(k0 + ty) * n + k0 + tx] : PACK_INF_D;
+  R[ty][tx] = (ty < kb && tx < nj) ? Df[(long long)(k0 + ty) * n + j0 + tx] : PACK_INF_D;
+  C[ty][tx] = (tx < kb && ty < nj) ? Df[(long long)(j0 + ty) * n + k0 + tx] : PACK_INF_D;
+  FK[ty][tx] = (ty < kb && tx < kb && tx > ty) ? F[(long long)(k0 + ty) * n + k0 + tx] : -1;
+  FK[ty][B + tx] = (ty < kb && tx < nj) ? F[(long long)(k0 + ty) * n + j0 + tx] : -1;
+  __syncthreads();
+  // pivot p updates the entries of rows / columns above p (row p and column p are final, only read).
+  // The diagonal block first, by one wave (no barrier: a wave's LDS accesses complete in order; the
+  // empty asm keeps the compiler from reordering them across steps) — a later pivot never changes an
+  // entry D[y][p] / D[p][x] of an earlier one, so the panels can use the finished block: each of their
+  // columns (R) / rows (C) only depends on itself, and every wave runs its own without barriers.
+  const int lane = tid & 63, wv = tid >> 6;
+  if (wv == 0)
+    for (int p = 0; p < kb; ++p) {
+      const uint32_t z = (uint32_t)(S.c0 + k0 + p);
+      for (int e = lane; e < B * B; e += 64) {
+        const int y = e >> 5, x = e & 31;
+        if (y > p && x > p && y < kb && x < kb && y != x) Dk[y][x] = umin64(Dk[y][x], sup_cand(Dk[y][p], Dk[p][x], z));
+      }
+      asm volatile("" ::: "memory");
+    }
+  __syncthreads();
+  {
+    const int r = lane & 31, jj = 2 * wv + (lane >> 5);   // R: row r of column jj; C: column r of row jj
+    for (int p = 0; p < kb; ++p) {
+      const uint32_t z = (uint32_t)(S.c0 + k0 + p);
+      if (r > p && r < kb && jj < nj) R[r][jj] = umin64(R[r][jj], sup_cand(Dk[r][p], R[p][jj], z));
+      if (r > p && r < kb && jj < nj) C[jj][r] = umin64(C[jj][r], sup_cand(C[jj][p], Dk[p][r], z));
+      asm volatile("" ::: "memory");
+    }
   }
   __syncthreads();
-  // pivot p: entries of rows / columns above p (row p and column p are final and only read)
-  for (int p = 0; p < kb; ++p) {
-    const uint32_t z = (uint32_t)(S.c0 + k0 + p);
-    for (int e = tid; e < B * B; e += 256) {
-      const int y = e / B, x = e % B;
-      if (y > p && x > p && y < kb && x < kb && y != x) Dk[y][x] = umin64(Dk[y][x], sup_cand(Dk[y][p], Dk[p][x], z));
-    }
-    for (int e = tid; e < B * J; e += 256) {
-      const int y = e / J, j = e % J;
-      if (y > p && y < kb && j < nj) R[y][j] = umin64(R[y][j], sup_cand(Dk[y][p], R[p][j], z));
-    }
-    for (int e = tid; e < J * B; e += 256) {
-      const int j = e / B, x = e % B;
-      if (x > p && x < kb && j < nj) C[j][x] = umin64(C[j][x], sup_cand(C[j][p], Dk[p][x], z));
-    }
-    __syncthreads();
-  }
-  for (int e = tid; e < B * J; e += 256) {
-    const int y = e / J, j = e % J;
-    if (y < kb && j < nj) {
-      Df[(long long)(k0 + y) * n + j0 + j] = R[y][j];
-      Df[(long long)(j0 + j) * n + k0 + y] = C[j][y];
-      const int a = F[(long long)(k0 + y) * n + j0 + j];
-      if (a >= 0) {
-        up[a] = R[y][j];
-        dn[a] = C[j][y];
-      }
+  if (ty < kb && tx < nj) {
+    Df[(long long)(k0 + ty) * n + j0 + tx] = R[ty][tx];
+    Df[(long long)(j0 + tx) * n + k0 + ty] = C[tx][ty];
+    const int a = FK[ty][B + tx];
+    if (a >= 0) {
+      up[a] = R[ty][tx];
+      dn[a] = C[tx][ty];
     }
   }
-  if (diag_writer)
-    for (int e = tid; e < B * B; e += 256) {
-      const int y = e / B, x = e % B;
-      if (y < kb && x < kb) {
-        Df[(long long)(k0 + y) * n + k0 + x] = Dk[y][x];
-        if (y < x) {
-          const int a = F[(long long)(k0 + y) * n + k0 + x];
-          if (a >= 0) {
-            up[a] = Dk[y][x];
-            dn[a] = Dk[x][y];
-          }
-        }
-      }
+  if (diag_writer && ty < kb && tx < kb) {
+    Df[(long long)(k0 + ty) * n + k0 + tx] = Dk[ty][tx];
+    const int a = FK[ty][tx];
+    if (a >= 0) {
+      up[a] = Dk[ty][tx];
+      dn[a] = Dk[tx][ty];
     }
+  }
   // finalize the arcs (x, v), x in K, v in K above x (column v - k0) or in J (column B + j)
   const int zK = S.c0 + k0;     // rank of K's first pivot
-  auto entry = [&](int x, int col, int& vf) -> int {
-    if (col < B) {
-      if (!(col < kb && col > x)) return -1;
-      vf = k0 + col;
-    } else {
-      if (col - B >= nj) return -1;
-      vf = j0 + col - B;
-    }
-    return F[(long long)(k0 + x) * n + vf];
-  };
+  auto vfront = [&](int col) { return col < B ? k0 + col : j0 + col - B; };
   auto weight = [&](int x, int col, int dir) -> unsigned long long {
     if (col < B) return dir ? Dk[col][x] : Dk[x][col];
     return dir ? C[col - B][x] : R[x][col - B];
@@ -963,62 +966,92 @@ __global__ __launch_bounds__(256) void sup_panel_basic_kernel(
       (dir ? cnt_dn : cnt_up)[a] = Cn;
     }
   };
-  for (int e = tid; e < B * W2; e += 256) {
-    const int x = e / W2, col = e % W2;
-    if (x >= kb) continue;
-    int vf = 0;
-    const int a = entry(x, col, vf);
-    if (a < 0) continue;
+  // every entry whose middle is not in K, in two rounds of independent loads: (1) the gather's
+  // finalization (middle below the front), a road edge's metres, or the sub-arcs through an earlier
+  // block's node; (2) those sub-arcs' metres and road edges
+  {
+    constexpr int Q = B * W2 / 1024;
+    int kind[Q][2], s0[Q][2], s1[Q][2];
+    float L[Q][2];
+    int32_t Cn[Q][2];
 #pragma unroll
-    for (int dir = 0; dir < 2; ++dir) {
-      const unsigned long long wv = weight(x, col, dir);
-      if (!(wof(wv) < F_INF)) {
-        put(x, col, a, dir, -1, -1, F_INF, 0);
-        continue;
+    for (int q = 0; q < Q; ++q) {
+      const int e = tid + 1024 * q, x = e / W2, col = e % W2;
+      const int a = FK[x][col];
+#pragma unroll
+      for (int dir = 0; dir < 2; ++dir) {
+        kind[q][dir] = 0;
+        if (a < 0) continue;
+        const unsigned long long wt = weight(x, col, dir);
+        const uint32_t pl = (uint32_t)wt;
+        const int vf = vfront(col);
+        if (!(wof(wt) < F_INF)) {
+          kind[q][dir] = 1;
+          s0[q][dir] = -1;
+          s1[q][dir] = -1;
+          L[q][dir] = F_INF;
+          Cn[q][dir] = 0;
+        } else if (pl & EDGE_FLAG_D) {
+          const int ed = (int)(pl & ~EDGE_FLAG_D);
+          kind[q][dir] = 1;
+          s0[q][dir] = -1;
+          s1[q][dir] = ed;
+          L[q][dir] = length[ed];
+          Cn[q][dir] = 1;
+        } else if ((int)pl < S.c0) {           // below the front: the gather's
+          const long long idx = dir ? (long long)vf * n + k0 + x : (long long)(k0 + x) * n + vf;
+          const int2 ss = SS[S.dofs + idx], sl = SL[S.dofs + idx];
+          kind[q][dir] = 1;
+          s0[q][dir] = ss.x;
+          s1[q][dir] = ss.y;
+          L[q][dir] = __int_as_float(sl.x);
+          Cn[q][dir] = sl.y;
+        } else if ((int)pl < zK) {             // an earlier block of the chain
+          const long long fz = (int)pl - S.c0;
+          const int azx = F[fz * n + k0 + x], azv = F[fz * n + vf];
+          kind[q][dir] = 2;
+          s0[q][dir] = dir ? azv : azx;
+          s1[q][dir] = dir ? azx : azv;
+        }
       }
-      const uint32_t pl = (uint32_t)wv;
-      if (pl & EDGE_FLAG_D) {
-        const int ed = (int)(pl & ~EDGE_FLAG_D);
-        put(x, col, a, dir, -1, ed, length[ed], 1);
-        continue;
-      }
-      const int zz = (int)pl;
-      if (zz >= zK) continue;                    // a middle inside K: row by row below
-      int azx, azv;
-      if (zz >= S.c0) {                          // an earlier block of the chain
-        const long long fz = zz - S.c0;
-        azx = F[fz * n + k0 + x];
-        azv = F[fz * n + vf];
-      } else {                                   // below the front (final since earlier levels)
-        azx = find_arc_d(up_ptr, up_head, zz, zK + x);
-        azv = find_arc_d(up_ptr, up_head, zz, fnode[S.fnode + vf]);
-      }
-      const int s0 = dir ? azv : azx, s1 = dir ? azx : azv;
-      put(x, col, a, dir, s0, s1, len_dn[s0] + len_up[s1], cnt_dn[s0] + cnt_up[s1]);
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+      for (int dir = 0; dir < 2; ++dir)
+        if (kind[q][dir] == 2) {
+          L[q][dir] = len_dn[s0[q][dir]] + len_up[s1[q][dir]];
+          Cn[q][dir] = cnt_dn[s0[q][dir]] + cnt_up[s1[q][dir]];
+        }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int e = tid + 1024 * q, x = e / W2, col = e % W2;
+#pragma unroll
+      for (int dir = 0; dir < 2; ++dir)
+        if (kind[q][dir]) put(x, col, FK[x][col], dir, s0[q][dir], s1[q][dir], L[q][dir], Cn[q][dir]);
     }
   }
   __syncthreads();
+  if (wv != 0) return;
+  // the middles inside K, row by row in one wave (in-order LDS, no barriers)
   for (int x = 1; x < kb; ++x) {
-    for (int e = tid; e < 2 * W2; e += 256) {
-      const int dir = e / W2, col = e % W2;
-      int vf = 0;
-      const int a = entry(x, col, vf);
-      if (a < 0) continue;
-      const unsigned long long wv = weight(x, col, dir);
-      if (!(wof(wv) < F_INF)) continue;
-      const uint32_t pl = (uint32_t)wv;
-      if (pl & EDGE_FLAG_D) continue;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int dir = h, col = lane;
+      const int a = FK[x][col];
+      const unsigned long long wt = a >= 0 ? weight(x, col, dir) : PACK_INF_D;
+      const uint32_t pl = (uint32_t)wt;
       const int zl = (int)pl - zK;
-      if (zl < 0) continue;
-      // zl < x: row zl is final (phase above or an earlier row here); arc (z, x) is its column x
-      const int azx = F[(long long)(k0 + zl) * n + k0 + x];
-      const int azv = F[(long long)(k0 + zl) * n + vf];
-      if (dir == 0)
-        put(x, col, a, 0, azx, azv, ld[zl][x] + lu[zl][col], cd[zl][x] + cu[zl][col]);
-      else
-        put(x, col, a, 1, azv, azx, ld[zl][col] + lu[zl][x], cd[zl][col] + cu[zl][x]);
+      if (wof(wt) < F_INF && !(pl & EDGE_FLAG_D) && zl >= 0) {
+        // zl < x: row zl is final (the round above or an earlier row here); arc (z, x) is its column x
+        const int azx = FK[zl][x], azv = FK[zl][col];
+        if (dir == 0)
+          put(x, col, a, 0, azx, azv, ld[zl][x] + lu[zl][col], cd[zl][x] + cu[zl][col]);
+        else
+          put(x, col, a, 1, azv, azx, ld[zl][col] + lu[zl][x], cd[zl][col] + cu[zl][x]);
+      }
     }
-    __syncthreads();
+    asm volatile("" ::: "memory");
   }
 }
 
@@ -1048,8 +1081,17 @@ __global__ __launch_bounds__(256) void sup_trailing_basic_kernel(const SupNode* 
     const int p = e / T, c = e % T;
     Bm[p][c] = (p < kb && z0 + c < n) ? wof(Df[(long long)(k0 + p) * n + z0 + c]) : F_INF;
   }
-  __syncthreads();
+  // the targets' current words, loaded now (their latency hides behind the loop below)
   const int ty = tid >> 4, tz = tid & 15;
+  unsigned long long old[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int y = y0 + ty * 4 + i, z = z0 + tz + 16 * j;
+      old[i][j] = (y < n && z < n && y != z) ? Df[(long long)y * n + z] : PACK_INF_D;
+    }
+  __syncthreads();
   float bw[4][4];
   int bp[4][4];
 #pragma unroll
@@ -1078,25 +1120,38 @@ __global__ __launch_bounds__(256) void sup_trailing_basic_kernel(const SupNode* 
   }
   const bool last = k1 == m;
   const int32_t* F = farc + S.foff;
+  unsigned long long nv[4][4];
+  int arc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int y = y0 + ty * 4 + i, z = z0 + tz + 16 * j;
-      if (y >= n || z >= n || y == z) continue;
       const unsigned long long c = bw[i][j] < F_INF ? packw(bw[i][j], (uint32_t)(S.c0 + k0 + bp[i][j])) : PACK_INF_D;
-      const long long idx = (long long)y * n + z;
-      const unsigned long long old = Df[idx];
+      nv[i][j] = umin64(old[i][j], c);
+      arc[i][j] = -1;
+      if (y >= n || z >= n || y == z) continue;
       if (y >= m && z >= m && last) {
-        const unsigned long long v = umin64(old, c);
-        if (v == PACK_INF_D) continue;
-        const int a = F[idx];
-        if (a < 0) continue;
-        unsigned long long* g = (y < z ? up : dn) + a;
-        if (v < *g) atomicMin(g, v);
-      } else if (c < old) {
-        Df[idx] = c;
+        if (nv[i][j] != PACK_INF_D) arc[i][j] = F[(long long)y * n + z];
+      } else if (c < old[i][j]) {
+        Df[(long long)y * n + z] = c;
       }
+    }
+  if (!last) return;
+  unsigned long long cur[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int y = y0 + ty * 4 + i, z = z0 + tz + 16 * j;
+      cur[i][j] = arc[i][j] >= 0 ? (y < z ? up : dn)[arc[i][j]] : 0ull;
+    }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int y = y0 + ty * 4 + i, z = z0 + tz + 16 * j;
+      if (arc[i][j] >= 0 && nv[i][j] < cur[i][j]) atomicMin((y < z ? up : dn) + arc[i][j], nv[i][j]);
     }
 }
 
@@ -1136,7 +1191,7 @@ __global__ __launch_bounds__(256) void sup_gather_perfect_kernel(const SupNode* 
 
 // perfect, block b (blocks from the top): the candidates through the final part F = [k1, n) —
 // up: P[x][y] = min_z Db[x][z] + P[z][y], dn: P[y][x] = min_z P[y][z] + Db[z][x]  (x in K, y, z in F)
-// — a (min, +) product, 32 x 32 outputs per workgroup over <= 512 z (t1 = split << 1 | dir)
+// — a (min, +) product, 32 x 32 outputs per workgroup over <= 128 z (t1 = split << 1 | dir)
 __global__ __launch_bounds__(256) void sup_gemm_perfect_kernel(const SupNode* __restrict__ sn,
                                                                const SupWork* __restrict__ w, float* __restrict__ D) {
   constexpr int B = SUP_B, Y = SUP_G1Y, ZC = 64;
@@ -1204,12 +1259,14 @@ __global__ __launch_bounds__(256) void sup_gemm_perfect_kernel(const SupNode* __
 
 // perfect, block b: the rows of K against this workgroup's 64 columns y of F, top-down through K
 // (candidates through z in K above x), then written out; and the F-part of the K x K targets through
-// these 64 z (atomicMin into P[K][K], finished by sup_kk_perfect_kernel)
-__global__ __launch_bounds__(256) void sup_solve_perfect_kernel(const SupNode* __restrict__ sn,
-                                                                const SupWork* __restrict__ w,
-                                                                const int32_t* __restrict__ farc, float* __restrict__ D,
-                                                                uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+// these 64 z (atomicMin into P[K][K], finished by sup_kk_perfect_kernel).  1024 threads: two entries
+// of each direction per thread and step.
+__global__ __launch_bounds__(1024) void sup_solve_perfect_kernel(const SupNode* __restrict__ sn,
+                                                                 const SupWork* __restrict__ w,
+                                                                 const int32_t* __restrict__ farc, float* __restrict__ D,
+                                                                 uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
   constexpr int B = SUP_B, Y = SUP_SJ;
+  static_assert(B * Y == 2048, "two entries per thread");
   __shared__ float Dk[B][B + 1];     // Db[K][K]
   __shared__ float PU[B][Y + 1];     // P[K][y]
   __shared__ float PD[Y][B + 1];     // P[y][K]
@@ -1222,43 +1279,52 @@ __global__ __launch_bounds__(256) void sup_solve_perfect_kernel(const SupNode* _
   const int y0 = k1 + W.t0 * Y, ny = min(Y, n - y0);
   float* Db = D + 2 * S.dofs;
   float* P = Db + (long long)n * n;
-  for (int e = tid; e < B * B; e += 256) {
-    const int y = e / B, x = e % B;
+  {
+    const int y = tid >> 5, x = tid & 31;
     Dk[y][x] = (y < kb && x < kb) ? Db[(long long)(k0 + y) * n + k0 + x] : F_INF;
   }
-  for (int e = tid; e < B * Y; e += 256) {
-    const int x = e / Y, y = e % Y;
-    const bool ok = x < kb && y < ny;
-    PU[x][y] = ok ? P[(long long)(k0 + x) * n + y0 + y] : F_INF;
-    DKT[x][y] = ok ? Db[(long long)(k0 + x) * n + y0 + y] : F_INF;
-  }
-  for (int e = tid; e < Y * B; e += 256) {
-    const int y = e / B, x = e % B;
-    const bool ok = x < kb && y < ny;
-    PD[y][x] = ok ? P[(long long)(y0 + y) * n + k0 + x] : F_INF;
-    DTK[y][x] = ok ? Db[(long long)(y0 + y) * n + k0 + x] : F_INF;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int e = tid + 1024 * q;
+    {
+      const int x = e / Y, y = e % Y;
+      const bool ok = x < kb && y < ny;
+      PU[x][y] = ok ? P[(long long)(k0 + x) * n + y0 + y] : F_INF;
+      DKT[x][y] = ok ? Db[(long long)(k0 + x) * n + y0 + y] : F_INF;
+    }
+    {
+      const int y = e / B, x = e % B;
+      const bool ok = x < kb && y < ny;
+      PD[y][x] = ok ? P[(long long)(y0 + y) * n + k0 + x] : F_INF;
+      DTK[y][x] = ok ? Db[(long long)(y0 + y) * n + k0 + x] : F_INF;
+    }
   }
   __syncthreads();
-  for (int z = kb - 1; z >= 1; --z) {
-    for (int e = tid; e < B * Y; e += 256) {
-      const int x = e / Y, y = e % Y;
-      if (x < z && y < ny) {
-        const float s = Dk[x][z] + PU[z][y];
-        if (s < PU[x][y]) PU[x][y] = s;
+  // top-down through K: a column y of PU (row y of PD) only depends on itself and Dk, so each wave
+  // runs its own 4 columns / rows without barriers (in-order LDS within a wave)
+  {
+    const int lane = tid & 63, x = lane & 31, y1 = 4 * (tid >> 6) + (lane >> 5);
+    for (int z = kb - 1; z >= 1; --z) {
+      if (x < z) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int y = y1 + 2 * i;
+          if (y < ny) {
+            const float su = Dk[x][z] + PU[z][y];
+            if (su < PU[x][y]) PU[x][y] = su;
+            const float sd = PD[y][z] + Dk[z][x];
+            if (sd < PD[y][x]) PD[y][x] = sd;
+          }
+        }
       }
+      asm volatile("" ::: "memory");
     }
-    for (int e = tid; e < Y * B; e += 256) {
-      const int y = e / B, x = e % B;
-      if (x < z && y < ny) {
-        const float s = PD[y][z] + Dk[z][x];
-        if (s < PD[y][x]) PD[y][x] = s;
-      }
-    }
-    __syncthreads();
   }
+  __syncthreads();
   const int32_t* F = farc + S.foff;
-  for (int e = tid; e < B * Y; e += 256) {
-    const int x = e / Y, y = e % Y;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int e = tid + 1024 * q, x = e / Y, y = e % Y;
     if (x < kb && y < ny) {
       const long long iu = (long long)(k0 + x) * n + y0 + y;
       P[iu] = PU[x][y];
@@ -1270,69 +1336,61 @@ __global__ __launch_bounds__(256) void sup_solve_perfect_kernel(const SupNode* _
       }
     }
   }
-  for (int e = tid; e < B * B; e += 256) {
-    const int x = e / B, y = e % B;
-    if (!(x < y && y < kb)) continue;
-    float bu = F_INF, bd = F_INF;
-    for (int q = 0; q < ny; ++q) {
-      const float su = DKT[x][q] + PD[q][y];
-      const float sd = PU[y][q] + DTK[q][x];
-      bu = su < bu ? su : bu;
-      bd = sd < bd ? sd : bd;
+  {
+    const int x = tid >> 5, y = tid & 31;
+    if (x < y && y < kb) {
+      float bu = F_INF, bd = F_INF;
+      for (int q = 0; q < ny; ++q) {
+        const float su = DKT[x][q] + PD[q][y];
+        const float sd = PU[y][q] + DTK[q][x];
+        bu = su < bu ? su : bu;
+        bd = sd < bd ? sd : bd;
+      }
+      if (bu < F_INF) atomicMin((uint32_t*)(P + (long long)(k0 + x) * n + k0 + y), __float_as_uint(bu));
+      if (bd < F_INF) atomicMin((uint32_t*)(P + (long long)(k0 + y) * n + k0 + x), __float_as_uint(bd));
     }
-    if (bu < F_INF) atomicMin((uint32_t*)(P + (long long)(k0 + x) * n + k0 + y), __float_as_uint(bu));
-    if (bd < F_INF) atomicMin((uint32_t*)(P + (long long)(k0 + y) * n + k0 + x), __float_as_uint(bd));
   }
 }
 
 // perfect, block b: the K x K targets top-down (x from the top of K: all of its candidates through
-// z in K above x are final), one workgroup per front; four lanes per target split the z loop
-__global__ __launch_bounds__(256) void sup_kk_perfect_kernel(const SupNode* __restrict__ sn,
-                                                             const SupWork* __restrict__ w,
-                                                             const int32_t* __restrict__ farc, float* __restrict__ D,
-                                                             uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+// z in K above x are final), one wave per front: a lane per (target column / row, direction)
+__global__ __launch_bounds__(64) void sup_kk_perfect_kernel(const SupNode* __restrict__ sn,
+                                                            const SupWork* __restrict__ w,
+                                                            const int32_t* __restrict__ farc, float* __restrict__ D,
+                                                            uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
   constexpr int B = SUP_B;
   __shared__ float Dk[B][B + 1];
   __shared__ float Pk[B][B + 1];
   const SupWork W = w[blockIdx.x];
   const SupNode S = sn[W.s];
-  const int n = S.n, tid = threadIdx.x;
+  const int n = S.n, lane = threadIdx.x;
   const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
   float* Db = D + 2 * S.dofs;
   float* P = Db + (long long)n * n;
-  for (int e = tid; e < B * B; e += 256) {
-    const int y = e / B, x = e % B;
+  for (int e = lane; e < B * B; e += 64) {
+    const int y = e >> 5, x = e & 31;
     const bool ok = y < kb && x < kb;
     Dk[y][x] = ok ? Db[(long long)(k0 + y) * n + k0 + x] : F_INF;
     Pk[y][x] = ok ? P[(long long)(k0 + y) * n + k0 + x] : F_INF;
   }
-  __syncthreads();
-  const int g = tid >> 2, q = tid & 3;
-  const int dir = g >> 5, y = g & 31;
+  asm volatile("" ::: "memory");
+  const int dir = lane >> 5, y = lane & 31;
   for (int x = kb - 2; x >= 0; --x) {
-    float best = F_INF;
-    if (y > x && y < kb)
-      for (int z = x + 1 + q; z < kb; z += 4) {
+    if (y > x && y < kb) {
+      float best = dir == 0 ? Pk[x][y] : Pk[y][x];
+      for (int z = x + 1; z < kb; ++z) {
         if (z == y) continue;
         const float s = dir == 0 ? Dk[x][z] + Pk[z][y] : Pk[y][z] + Dk[z][x];
         best = s < best ? s : best;
       }
-    float o = __shfl_xor(best, 1);
-    best = o < best ? o : best;
-    o = __shfl_xor(best, 2);
-    best = o < best ? o : best;
-    if (q == 0 && y > x && y < kb) {
-      if (dir == 0) {
-        if (best < Pk[x][y]) Pk[x][y] = best;
-      } else {
-        if (best < Pk[y][x]) Pk[y][x] = best;
-      }
+      if (dir == 0) Pk[x][y] = best;
+      else Pk[y][x] = best;
     }
-    __syncthreads();
+    asm volatile("" ::: "memory");
   }
   const int32_t* F = farc + S.foff;
-  for (int e = tid; e < B * B; e += 256) {
-    const int x = e / B, yy = e % B;
+  for (int e = lane; e < B * B; e += 64) {
+    const int x = e >> 5, yy = e & 31;
     if (x >= kb || yy >= kb) continue;
     const long long idx = (long long)(k0 + x) * n + k0 + yy;
     P[idx] = Pk[x][yy];
@@ -2280,7 +2338,7 @@ void CchGpu::build_supernodes(const std::vector<int64_t>& tofs) {
   PArc* dpa = nullptr;
   bool ok = up_copy(dsn, sn.data(), sn.size()) == hipSuccess && up_copy(dwk, work.data(), work.size()) == hipSuccess &&
             up_copy(dfn, fnode.data(), fnode.size()) == hipSuccess && dmalloc(dfa, (size_t)foff) == hipSuccess &&
-            up_copy(dpa, parc.data(), parc.size()) == hipSuccess && dmalloc(cs0_.sup_buf, (size_t)buf) == hipSuccess;
+            up_copy(dpa, parc.data(), parc.size()) == hipSuccess && dmalloc(cs0_.sup_buf, 3 * (size_t)buf) == hipSuccess;
   if (ok) {
     hipLaunchKernelGGL(sup_farc_kernel, dim3((unsigned)cdiv(all_rows.cnt, 4)), dim3(256), 0, 0, dsn, dwk + all_rows.off,
                        (long long)all_rows.cnt, dfn, d_up_ptr, d_up_head, dfa);
@@ -2520,7 +2578,7 @@ hipError_t CchGpu::alloc_scratch(CustScratch& x) {
   ck(dmalloc(x.tail_ctl, (size_t)T_.max_height + (size_t)T_.max_depth + 8));   // basic | perfect tail
   if (x.tail_ctl != nullptr)
     ck(hipMemset(x.tail_ctl, 0, ((size_t)T_.max_height + (size_t)T_.max_depth + 8) * sizeof(int)));
-  if (sup_on_) ck(dmalloc(x.sup_buf, (size_t)sup_buf_entries_));
+  if (sup_on_) ck(dmalloc(x.sup_buf, 3 * (size_t)sup_buf_entries_));   // D | SS | SL
   return e;
 }
 
@@ -2687,15 +2745,18 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
     if (sup && X.sup_buf == nullptr) ck(hipErrorOutOfMemory);
     const SupNode* sup_sn = (const SupNode*)d_sup_sn;
     const SupWork* sup_wk = (const SupWork*)d_sup_work;
+    int2* sup_ss = X.sup_buf ? (int2*)(X.sup_buf + sup_buf_entries_) : nullptr;       // gather's sub-arcs
+    int2* sup_sl = X.sup_buf ? (int2*)(X.sup_buf + 2 * sup_buf_entries_) : nullptr;   // ... metres, edges
     for (size_t l = 0; sup && l < sup_lev_.size() && e == hipSuccess; ++l) {
       const SupLevel& SL = sup_lev_[l];
-      hipLaunchKernelGGL(sup_gather_basic_kernel, dim3(blocks_for(SL.gather.cnt, 4)), dim3(256), 0, s, sup_sn,
-                         sup_wk + SL.gather.off, (long long)SL.gather.cnt, d_sup_farc, X.up64, X.dn64, X.sup_buf);
+      hipLaunchKernelGGL(sup_gather_basic_kernel, dim3((unsigned)SL.gather.cnt), dim3(256), 0, s, sup_sn,
+                         sup_wk + SL.gather.off, d_sup_fnode, d_sup_farc, X.up64, X.dn64, d_up_ptr, d_up_head, m.len_up,
+                         m.len_dn, m.cnt_up, m.cnt_dn, X.sup_buf, sup_ss, sup_sl);
       for (size_t r = 0; r < SL.panel.size(); ++r) {
         if (SL.panel[r].cnt > 0)
-          hipLaunchKernelGGL(sup_panel_basic_kernel, dim3((unsigned)SL.panel[r].cnt), dim3(256), 0, s, sup_sn,
-                             sup_wk + SL.panel[r].off, d_sup_fnode, d_sup_farc, X.sup_buf, X.up64, X.dn64, m.sub_up,
-                             m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length, d_up_ptr, d_up_head);
+          hipLaunchKernelGGL(sup_panel_basic_kernel, dim3((unsigned)SL.panel[r].cnt), dim3(1024), 0, s, sup_sn,
+                             sup_wk + SL.panel[r].off, d_sup_farc, X.sup_buf, sup_ss, sup_sl, X.up64, X.dn64, m.sub_up,
+                             m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
         if (SL.trail[r].cnt > 0)
           hipLaunchKernelGGL(sup_trailing_basic_kernel, dim3((unsigned)SL.trail[r].cnt), dim3(256), 0, s, sup_sn,
                              sup_wk + SL.trail[r].off, d_sup_farc, X.sup_buf, X.up64, X.dn64);
@@ -2792,10 +2853,10 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
           hipLaunchKernelGGL(sup_gemm_perfect_kernel, dim3((unsigned)SL.gemm[r].cnt), dim3(256), 0, s, sup_sn,
                              sup_wk + SL.gemm[r].off, Dp);
         if (SL.solve[r].cnt > 0)
-          hipLaunchKernelGGL(sup_solve_perfect_kernel, dim3((unsigned)SL.solve[r].cnt), dim3(256), 0, s, sup_sn,
+          hipLaunchKernelGGL(sup_solve_perfect_kernel, dim3((unsigned)SL.solve[r].cnt), dim3(1024), 0, s, sup_sn,
                              sup_wk + SL.solve[r].off, d_sup_farc, Dp, X.pup, X.pdn);
         if (SL.kk[r].cnt > 0)
-          hipLaunchKernelGGL(sup_kk_perfect_kernel, dim3((unsigned)SL.kk[r].cnt), dim3(256), 0, s, sup_sn,
+          hipLaunchKernelGGL(sup_kk_perfect_kernel, dim3((unsigned)SL.kk[r].cnt), dim3(64), 0, s, sup_sn,
                              sup_wk + SL.kk[r].off, d_sup_farc, Dp, X.pup, X.pdn);
       }
       ck(hipGetLastError());
