@@ -1,7 +1,7 @@
 #!/bin/bash
 # supernodal CCH v2 (1024-thread panel/solve/kk, gather-side finalization): bit-identity test, times, kernel profile
 set -o pipefail
-O=gpurun_out/r6af; mkdir -p $O
+O=gpurun_out/${OUT:-r6af}; mkdir -p $O
 timeout -k 10 400 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_cch_gpu.py -k "supernodal or legs_exact" > $O/test_cch.log 2>&1 || { tail -30 $O/test_cch.log; exit 1; }
 tail -1 $O/test_cch.log
 timeout -k 10 200 python -u bench/cch_customize_bench.py --nodes 100000 --contexts 6 --check > $O/cust_100k.jsonl 2>&1 || { tail -5 $O/cust_100k.jsonl; exit 1; }

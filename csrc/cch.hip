@@ -905,32 +905,14 @@ __global__ __launch_bounds__(1024) void sup_panel_basic_kernel(
   FK[ty][tx] = (ty < kb && tx < kb && tx > ty) ? F[(long long)(k0 + ty) * n + k0 + tx] : -1;
   FK[ty][B + tx] = (ty < kb && tx < nj) ? F[(long long)(k0 + ty) * n + j0 + tx] : -1;
   __syncthreads();
-  // pivot p updates the entries of rows / columns above p (row p and column p are final, only read).
-  // The diagonal block first, by one wave (no barrier: a wave's LDS accesses complete in order; the
-  // empty asm keeps the compiler from reordering them across steps) — a later pivot never changes an
-  // entry D[y][p] / D[p][x] of an earlier one, so the panels can use the finished block: each of their
-  // columns (R) / rows (C) only depends on itself, and every wave runs its own without barriers.
-  const int lane = tid & 63, wv = tid >> 6;
-  if (wv == 0)
-    for (int p = 0; p < kb; ++p) {
-      const uint32_t z = (uint32_t)(S.c0 + k0 + p);
-      for (int e = lane; e < B * B; e += 64) {
-        const int y = e >> 5, x = e & 31;
-        if (y > p && x > p && y < kb && x < kb && y != x) Dk[y][x] = umin64(Dk[y][x], sup_cand(Dk[y][p], Dk[p][x], z));
-      }
-      asm volatile("" ::: "memory");
-    }
-  __syncthreads();
-  {
-    const int r = lane & 31, jj = 2 * wv + (lane >> 5);   // R: row r of column jj; C: column r of row jj
-    for (int p = 0; p < kb; ++p) {
-      const uint32_t z = (uint32_t)(S.c0 + k0 + p);
-      if (r > p && r < kb && jj < nj) R[r][jj] = umin64(R[r][jj], sup_cand(Dk[r][p], R[p][jj], z));
-      if (r > p && r < kb && jj < nj) C[jj][r] = umin64(C[jj][r], sup_cand(C[jj][p], Dk[p][r], z));
-      asm volatile("" ::: "memory");
-    }
+  // pivot p: entries of rows / columns above p (row p and column p are final and only read)
+  for (int p = 0; p < kb; ++p) {
+    const uint32_t z = (uint32_t)(S.c0 + k0 + p);
+    if (ty > p && tx > p && ty < kb && tx < kb && ty != tx) Dk[ty][tx] = umin64(Dk[ty][tx], sup_cand(Dk[ty][p], Dk[p][tx], z));
+    if (ty > p && ty < kb && tx < nj) R[ty][tx] = umin64(R[ty][tx], sup_cand(Dk[ty][p], R[p][tx], z));
+    if (tx > p && tx < kb && ty < nj) C[ty][tx] = umin64(C[ty][tx], sup_cand(C[ty][p], Dk[p][tx], z));
+    __syncthreads();
   }
-  __syncthreads();
   if (ty < kb && tx < nj) {
     Df[(long long)(k0 + ty) * n + j0 + tx] = R[ty][tx];
     Df[(long long)(j0 + tx) * n + k0 + ty] = C[tx][ty];
@@ -1032,12 +1014,9 @@ __global__ __launch_bounds__(1024) void sup_panel_basic_kernel(
     }
   }
   __syncthreads();
-  if (wv != 0) return;
-  // the middles inside K, row by row in one wave (in-order LDS, no barriers)
   for (int x = 1; x < kb; ++x) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int dir = h, col = lane;
+    if (tid < 2 * W2) {
+      const int dir = tid / W2, col = tid % W2;
       const int a = FK[x][col];
       const unsigned long long wt = a >= 0 ? weight(x, col, dir) : PACK_INF_D;
       const uint32_t pl = (uint32_t)wt;
@@ -1051,7 +1030,7 @@ __global__ __launch_bounds__(1024) void sup_panel_basic_kernel(
           put(x, col, a, 1, azv, azx, ld[zl][col] + lu[zl][x], cd[zl][col] + cu[zl][x]);
       }
     }
-    asm volatile("" ::: "memory");
+    __syncthreads();
   }
 }
 
@@ -1300,27 +1279,27 @@ __global__ __launch_bounds__(1024) void sup_solve_perfect_kernel(const SupNode* 
     }
   }
   __syncthreads();
-  // top-down through K: a column y of PU (row y of PD) only depends on itself and Dk, so each wave
-  // runs its own 4 columns / rows without barriers (in-order LDS within a wave)
-  {
-    const int lane = tid & 63, x = lane & 31, y1 = 4 * (tid >> 6) + (lane >> 5);
-    for (int z = kb - 1; z >= 1; --z) {
-      if (x < z) {
+  for (int z = kb - 1; z >= 1; --z) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int y = y1 + 2 * i;
-          if (y < ny) {
-            const float su = Dk[x][z] + PU[z][y];
-            if (su < PU[x][y]) PU[x][y] = su;
-            const float sd = PD[y][z] + Dk[z][x];
-            if (sd < PD[y][x]) PD[y][x] = sd;
-          }
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 1024 * q;
+      {
+        const int x = e / Y, y = e % Y;
+        if (x < z && y < ny) {
+          const float s = Dk[x][z] + PU[z][y];
+          if (s < PU[x][y]) PU[x][y] = s;
         }
       }
-      asm volatile("" ::: "memory");
+      {
+        const int y = e / B, x = e % B;
+        if (x < z && y < ny) {
+          const float s = PD[y][z] + Dk[z][x];
+          if (s < PD[y][x]) PD[y][x] = s;
+        }
+      }
     }
+    __syncthreads();
   }
-  __syncthreads();
   const int32_t* F = farc + S.foff;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -1353,52 +1332,63 @@ __global__ __launch_bounds__(1024) void sup_solve_perfect_kernel(const SupNode* 
 }
 
 // perfect, block b: the K x K targets top-down (x from the top of K: all of its candidates through
-// z in K above x are final), one wave per front: a lane per (target column / row, direction)
-__global__ __launch_bounds__(64) void sup_kk_perfect_kernel(const SupNode* __restrict__ sn,
-                                                            const SupWork* __restrict__ w,
-                                                            const int32_t* __restrict__ farc, float* __restrict__ D,
-                                                            uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+// z in K above x are final), one workgroup per front; 16 lanes per target split the z loop
+__global__ __launch_bounds__(1024) void sup_kk_perfect_kernel(const SupNode* __restrict__ sn,
+                                                              const SupWork* __restrict__ w,
+                                                              const int32_t* __restrict__ farc, float* __restrict__ D,
+                                                              uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
   constexpr int B = SUP_B;
   __shared__ float Dk[B][B + 1];
   __shared__ float Pk[B][B + 1];
   const SupWork W = w[blockIdx.x];
   const SupNode S = sn[W.s];
-  const int n = S.n, lane = threadIdx.x;
+  const int n = S.n, tid = threadIdx.x;
   const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
   float* Db = D + 2 * S.dofs;
   float* P = Db + (long long)n * n;
-  for (int e = lane; e < B * B; e += 64) {
-    const int y = e >> 5, x = e & 31;
+  {
+    const int y = tid >> 5, x = tid & 31;
     const bool ok = y < kb && x < kb;
     Dk[y][x] = ok ? Db[(long long)(k0 + y) * n + k0 + x] : F_INF;
     Pk[y][x] = ok ? P[(long long)(k0 + y) * n + k0 + x] : F_INF;
   }
-  asm volatile("" ::: "memory");
-  const int dir = lane >> 5, y = lane & 31;
+  __syncthreads();
+  const int g = tid >> 4, q = tid & 15;
+  const int dir = g >> 5, y = g & 31;
   for (int x = kb - 2; x >= 0; --x) {
-    if (y > x && y < kb) {
-      float best = dir == 0 ? Pk[x][y] : Pk[y][x];
-      for (int z = x + 1; z < kb; ++z) {
+    float best = F_INF;
+    if (y > x && y < kb)
+      for (int z = x + 1 + q; z < kb; z += 16) {
         if (z == y) continue;
         const float s = dir == 0 ? Dk[x][z] + Pk[z][y] : Pk[y][z] + Dk[z][x];
         best = s < best ? s : best;
       }
-      if (dir == 0) Pk[x][y] = best;
-      else Pk[y][x] = best;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const float v = __shfl_xor(best, o);
+      best = v < best ? v : best;
     }
-    asm volatile("" ::: "memory");
+    if (q == 0 && y > x && y < kb) {
+      if (dir == 0) {
+        if (best < Pk[x][y]) Pk[x][y] = best;
+      } else {
+        if (best < Pk[y][x]) Pk[y][x] = best;
+      }
+    }
+    __syncthreads();
   }
   const int32_t* F = farc + S.foff;
-  for (int e = lane; e < B * B; e += 64) {
-    const int x = e >> 5, yy = e & 31;
-    if (x >= kb || yy >= kb) continue;
-    const long long idx = (long long)(k0 + x) * n + k0 + yy;
-    P[idx] = Pk[x][yy];
-    if (x < yy) {
-      const int a = F[idx];
-      if (a >= 0) {
-        pup[a] = __float_as_uint(Pk[x][yy]);
-        pdn[a] = __float_as_uint(Pk[yy][x]);
+  {
+    const int x = tid >> 5, yy = tid & 31;
+    if (x < kb && yy < kb) {
+      const long long idx = (long long)(k0 + x) * n + k0 + yy;
+      P[idx] = Pk[x][yy];
+      if (x < yy) {
+        const int a = F[idx];
+        if (a >= 0) {
+          pup[a] = __float_as_uint(Pk[x][yy]);
+          pdn[a] = __float_as_uint(Pk[yy][x]);
+        }
       }
     }
   }
@@ -2856,7 +2846,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
           hipLaunchKernelGGL(sup_solve_perfect_kernel, dim3((unsigned)SL.solve[r].cnt), dim3(1024), 0, s, sup_sn,
                              sup_wk + SL.solve[r].off, d_sup_farc, Dp, X.pup, X.pdn);
         if (SL.kk[r].cnt > 0)
-          hipLaunchKernelGGL(sup_kk_perfect_kernel, dim3((unsigned)SL.kk[r].cnt), dim3(64), 0, s, sup_sn,
+          hipLaunchKernelGGL(sup_kk_perfect_kernel, dim3((unsigned)SL.kk[r].cnt), dim3(1024), 0, s, sup_sn,
                              sup_wk + SL.kk[r].off, d_sup_farc, Dp, X.pup, X.pdn);
       }
       ck(hipGetLastError());
