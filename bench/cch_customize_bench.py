@@ -49,7 +49,14 @@ def main():
            "wall_ms_min": round(min(rest), 3), "wall_ms_mean": round(sum(rest) / len(rest), 3),
            "customize_ms_min": round(min(gpu[1:] or gpu), 3)}
     if a.check:
+        import threading
         import numpy as np
+        done = threading.Event()
+
+        def beat():          # the CPU reference takes minutes on the 1M city: keep the log alive
+            while not done.wait(30):
+                print(json.dumps({"stage": "check_running", "s": round(time.time() - t0, 1)}), flush=True)
+        threading.Thread(target=beat, daemon=True).start()
         from routest_amd import _rt
         c = _rt.CCH(g.indptr, g.indices, g.lat, g.lon, 16)
         cost = router.costs(ctx)
@@ -62,6 +69,7 @@ def main():
         out["bit_identical_vs_cpu"] = bool(np.array_equal(np.asarray(s_gpu), np.asarray(s_cpu)) and
                                            np.array_equal(np.asarray(m_gpu), np.asarray(m_cpu)) and
                                            np.array_equal(np.asarray(st_gpu), np.asarray(st_cpu)))
+        done.set()
     print(json.dumps(out), flush=True)
 
 
