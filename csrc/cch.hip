@@ -2793,9 +2793,11 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
       ck(hipGetLastError());
     }
     // one depth level of the pull (nodes: its node count; km: its widest node's arcs)
-    auto pull_level = [&](PullArgs P, long long nodes, int km) {
-      // mean degree of the level's nodes: wide nodes get a wave per arc, narrow ones a lane per arc
-      const bool wave = P.arcs >= 24 * nodes;
+    auto pull_level = [&](PullArgs P, long long nodes, int km, int wave_km) {
+      // mean degree of the level's nodes: wide nodes get a wave per arc, narrow ones a lane per arc —
+      // or a level with a node of >= wave_km arcs (below the fronts: a lane looping over a ~200-arc
+      // node's candidates was the level's time, 30-50 us, r6ah)
+      const bool wave = P.arcs >= 24 * nodes || km >= wave_km;
       // waves per arc by the level's widest node (ROUTEST_CCH_PULL_SPLIT=0: one)
       static const bool split = !(std::getenv("ROUTEST_CCH_PULL_SPLIT") &&
                                   std::string(std::getenv("ROUTEST_CCH_PULL_SPLIT")) == "0");
@@ -2828,7 +2830,7 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
       PullArgs P{d_up_ptr, d_up_head, d_dnodes, d_aofs, lo, hi, aofs_[lo], aofs_[hi] - aofs_[lo], d_tofs, d_tri,
                  (const PArc*)d_parc};
       if (P.arcs <= 0 || pofs_[hi] == pofs_[lo]) continue;       // no node of the level has two arcs
-      pull_level(P, hi - lo, plev_kmax_[d]);
+      pull_level(P, hi - lo, plev_kmax_[d], 1 << 30);
     }
     // the dense fronts top-down by front level (per block from the top: the (min, +) product through
     // the final part, the solve through K, the K x K targets), then the other nodes by depth below
@@ -2855,7 +2857,11 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
       if (!rlev_multi_[d]) continue;
       PullArgs P{d_up_ptr, d_up_head, nullptr, nullptr, 0, 0, rlev_aofs_[d], rlev_aofs_[d + 1] - rlev_aofs_[d], d_tofs,
                  d_tri, (const PArc*)d_parc2};
-      pull_level(P, rlev_nodes_[d], rlev_kmax_[d]);
+      static const int wave_km = [] {
+        const char* v = std::getenv("ROUTEST_CCH_PULL_WAVE_K");
+        return v ? std::atoi(v) : 64;
+      }();
+      pull_level(P, rlev_nodes_[d], rlev_kmax_[d], wave_km);
     }
     for (int d = 0; d <= T_.max_depth && e == hipSuccess && !(tasks && ptasks) && !(pull && d_tri != nullptr) && !sup; ++d) {
       LevelArgs L{d_up_ptr, d_up_head, d_dnodes, d_pofs, (int)T_.dlev_ptr[d], (int)T_.dlev_ptr[d + 1], 0, 0, d_tofs, d_tri};
