@@ -800,6 +800,7 @@ struct SupNode {
 };
 struct SupWork {
   int32_t s, b, t0, t1;   // supernode, block (or row), tile indices
+  SupNode sn;             // the front itself (one load per workgroup instead of two dependent ones)
 };
 constexpr int SUP_B = 32;      // pivots per block
 constexpr int SUP_PJ = 32;     // basic panel: front columns per workgroup
@@ -822,7 +823,7 @@ __global__ __launch_bounds__(256) void sup_farc_kernel(const SupNode* __restrict
   const long long wi = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (wi >= nw) return;
   const SupWork W = w[wi];
-  const SupNode S = sn[W.s];
+  const SupNode S = W.sn;
   const int i = W.b, n = S.n;
   const int fi = fnode[S.fnode + i];
   for (int j = threadIdx.x & 63; j < n; j += 64) {
@@ -843,7 +844,7 @@ __global__ __launch_bounds__(256) void sup_gather_basic_kernel(
     const float* __restrict__ len_dn, const int32_t* __restrict__ cnt_up, const int32_t* __restrict__ cnt_dn,
     unsigned long long* __restrict__ D, int2* __restrict__ SS, int2* __restrict__ SL) {
   const SupWork W = w[blockIdx.x];
-  const SupNode S = sn[W.s];
+  const SupNode S = W.sn;
   const int i = W.b, n = S.n;
   const long long r0 = S.dofs + (long long)i * n;
   const int32_t* fr = farc + S.foff + (long long)i * n;
@@ -891,7 +892,7 @@ __global__ __launch_bounds__(1024) void sup_panel_basic_kernel(
   __shared__ float lu[B][W2], ld[B][W2];        // their finalized metres
   __shared__ int32_t cu[B][W2], cd[B][W2];      // ... and road edges
   const SupWork W = w[blockIdx.x];
-  const SupNode S = sn[W.s];
+  const SupNode S = W.sn;
   const int n = S.n, tid = threadIdx.x;
   const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
   const int j0 = k1 + W.t0 * J, nj = max(0, min(J, n - j0));
@@ -1047,7 +1048,7 @@ __global__ __launch_bounds__(256) void sup_trailing_basic_kernel(const SupNode* 
   __shared__ float A[T][B + 1];     // weights D[y][K]
   __shared__ float Bm[B][T + 1];    // weights D[K][z]
   const SupWork W = w[blockIdx.x];
-  const SupNode S = sn[W.s];
+  const SupNode S = W.sn;
   const int n = S.n, m = S.m, tid = threadIdx.x;
   const int k0 = W.b * B, k1 = min(k0 + B, m), kb = k1 - k0;
   const int y0 = k1 + W.t0 * T, z0 = k1 + W.t1 * T;
@@ -1147,7 +1148,7 @@ __global__ __launch_bounds__(256) void sup_gather_perfect_kernel(const SupNode* 
   const long long wi = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (wi >= nw) return;
   const SupWork W = w[wi];
-  const SupNode S = sn[W.s];
+  const SupNode S = W.sn;
   const int i = W.b, n = S.n;
   float* Db = D + 2 * S.dofs;
   float* P = Db + (long long)n * n;
@@ -1168,77 +1169,76 @@ __global__ __launch_bounds__(256) void sup_gather_perfect_kernel(const SupNode* 
   }
 }
 
-// perfect, block b (blocks from the top): the candidates through the final part F = [k1, n) —
-// up: P[x][y] = min_z Db[x][z] + P[z][y], dn: P[y][x] = min_z P[y][z] + Db[z][x]  (x in K, y, z in F)
-// — a (min, +) product, 32 x 32 outputs per workgroup over <= 128 z (t1 = split << 1 | dir)
-__global__ __launch_bounds__(256) void sup_gemm_perfect_kernel(const SupNode* __restrict__ sn,
-                                                               const SupWork* __restrict__ w, float* __restrict__ D) {
-  constexpr int B = SUP_B, Y = SUP_G1Y, ZC = 64;
+// perfect, block b (blocks from the top): the candidates through the final part above the next
+// block up, F' = [k1', n) (k1' = the end of the block above K; the whole F = [k1, n) for a front's top
+// block) — up: P[x][y] = min_z Db[x][z] + P[z][y], dn: P[y][x] = min_z P[y][z] + Db[z][x]  (x in K,
+// y in F, z in F') — a (min, +) product, 32 x 32 outputs per workgroup over <= SUP_G1Z z (t1 = split
+// << 1 | dir).  The block above K (z in [k1, k1')) is added by sup_solve_perfect_kernel: it is only
+// final after that block's K x K kernel, which runs in the same launch as this (no data shared).
+__device__ __forceinline__ void sup_gemm_body(const SupWork& W, float* __restrict__ D) {
+  constexpr int B = SUP_B, ZC = 64;
   __shared__ float As[32][ZC + 1];
   __shared__ float Bs[ZC][33];
-  const SupWork W = w[blockIdx.x];
-  const SupNode S = sn[W.s];
+  const SupNode S = W.sn;
   const int n = S.n, tid = threadIdx.x;
+  const int nb = (S.m + B - 1) / B;
   const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
-  const int y0 = k1 + W.t0 * Y, ny = min(Y, n - y0);
+  const int zlo = W.b + 1 < nb ? min(k1 + B, S.m) : k1;
+  const int y0 = k1 + W.t0 * SUP_G1Y, ny = min(SUP_G1Y, n - y0);
   const int dir = W.t1 & 1, zs = W.t1 >> 1;
-  const int zbeg = k1 + zs * SUP_G1Z, zend = min(zbeg + SUP_G1Z, n);
-  const bool split = n - k1 > SUP_G1Z;
+  const int zbeg = zlo + zs * SUP_G1Z, zend = min(zbeg + SUP_G1Z, n);
+  const bool split = n - zlo > SUP_G1Z;
   float* Db = D + 2 * S.dofs;
   float* P = Db + (long long)n * n;
-  const int r = tid >> 3, cq = tid & 7;
-  float best[4] = {F_INF, F_INF, F_INF, F_INF};
+  const int r = tid >> 5, c = tid & 31;
+  float best = F_INF;
   for (int zc = zbeg; zc < zend; zc += ZC) {
     const int nz = min(ZC, zend - zc);
-    for (int e = tid; e < 32 * ZC; e += 256) {
-      const int rr = e / ZC, q = e % ZC;
-      float v = F_INF;
-      if (q < nz) {
-        if (dir == 0 && rr < kb) v = Db[(long long)(k0 + rr) * n + zc + q];
-        if (dir == 1 && rr < ny) v = P[(long long)(y0 + rr) * n + zc + q];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + 1024 * h;
+      {
+        const int rr = e / ZC, q = e % ZC;
+        float v = F_INF;
+        if (q < nz) {
+          if (dir == 0 && rr < kb) v = Db[(long long)(k0 + rr) * n + zc + q];
+          if (dir == 1 && rr < ny) v = P[(long long)(y0 + rr) * n + zc + q];
+        }
+        As[rr][q] = v;
       }
-      As[rr][q] = v;
-    }
-    for (int e = tid; e < ZC * 32; e += 256) {
-      const int q = e / 32, cc = e % 32;
-      float v = F_INF;
-      if (q < nz) {
-        if (dir == 0 && cc < ny) v = P[(long long)(zc + q) * n + y0 + cc];
-        if (dir == 1 && cc < kb) v = Db[(long long)(zc + q) * n + k0 + cc];
+      {
+        const int q = e / 32, cc = e % 32;
+        float v = F_INF;
+        if (q < nz) {
+          if (dir == 0 && cc < ny) v = P[(long long)(zc + q) * n + y0 + cc];
+          if (dir == 1 && cc < kb) v = Db[(long long)(zc + q) * n + k0 + cc];
+        }
+        Bs[q][cc] = v;
       }
-      Bs[q][cc] = v;
     }
     __syncthreads();
     for (int q = 0; q < nz; ++q) {
-      const float a = As[r][q];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float s = a + Bs[q][cq + 8 * u];
-        best[u] = s < best[u] ? s : best[u];
-      }
+      const float sum = As[r][q] + Bs[q][c];
+      best = sum < best ? sum : best;
     }
     __syncthreads();
   }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int c = cq + 8 * u;
-    if (!(best[u] < F_INF)) continue;
-    long long idx;
-    if (dir == 0) {
-      if (r >= kb || c >= ny) continue;
-      idx = (long long)(k0 + r) * n + y0 + c;
-    } else {
-      if (r >= ny || c >= kb) continue;
-      idx = (long long)(y0 + r) * n + k0 + c;
-    }
-    if (split) atomicMin((uint32_t*)(P + idx), __float_as_uint(best[u]));
-    else if (best[u] < P[idx]) P[idx] = best[u];
+  if (!(best < F_INF)) return;
+  long long idx;
+  if (dir == 0) {
+    if (r >= kb || c >= ny) return;
+    idx = (long long)(k0 + r) * n + y0 + c;
+  } else {
+    if (r >= ny || c >= kb) return;
+    idx = (long long)(y0 + r) * n + k0 + c;
   }
+  if (split) atomicMin((uint32_t*)(P + idx), __float_as_uint(best));
+  else if (best < P[idx]) P[idx] = best;
 }
 
 // perfect, block b: the rows of K against this workgroup's 64 columns y of F, top-down through K
 // (candidates through z in K above x), then written out; and the F-part of the K x K targets through
-// these 64 z (atomicMin into P[K][K], finished by sup_kk_perfect_kernel).  1024 threads: two entries
+// these 64 z (atomicMin into P[K][K], finished by sup_kk_body in the next launch).  1024 threads: two entries
 // of each direction per thread and step.
 __global__ __launch_bounds__(1024) void sup_solve_perfect_kernel(const SupNode* __restrict__ sn,
                                                                  const SupWork* __restrict__ w,
@@ -1252,7 +1252,7 @@ __global__ __launch_bounds__(1024) void sup_solve_perfect_kernel(const SupNode* 
   __shared__ float DKT[B][Y + 1];    // Db[K][y]
   __shared__ float DTK[Y][B + 1];    // Db[y][K]
   const SupWork W = w[blockIdx.x];
-  const SupNode S = sn[W.s];
+  const SupNode S = W.sn;
   const int n = S.n, tid = threadIdx.x;
   const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
   const int y0 = k1 + W.t0 * Y, ny = min(Y, n - y0);
@@ -1279,22 +1279,129 @@ __global__ __launch_bounds__(1024) void sup_solve_perfect_kernel(const SupNode* 
     }
   }
   __syncthreads();
-  for (int z = kb - 1; z >= 1; --z) {
+  // the block above K, K' = [k1, k2) (finished in the previous launches: its rows by its solve, its
+  // K' x K' by its K x K kernel): its candidates for this workgroup's entries (the product left it out)
+  const int nbk = (S.m + B - 1) / B;
+  if (W.b + 1 < nbk) {
+    const int k2 = min(k1 + B, S.m), kb2 = k2 - k1;
+    __shared__ float A2[B][B + 1];    // Db[K][K']
+    __shared__ float E2[B][B + 1];    // Db[K'][K]
+    __shared__ float B2[B][Y + 1];    // P[K'][y]
+    __shared__ float C2[Y][B + 1];    // P[y][K']
+    {
+      const int y = tid >> 5, x = tid & 31;
+      A2[y][x] = (y < kb && x < kb2) ? Db[(long long)(k0 + y) * n + k1 + x] : F_INF;
+      E2[y][x] = (y < kb2 && x < kb) ? Db[(long long)(k1 + y) * n + k0 + x] : F_INF;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 1024 * q;
+      {
+        const int z = e / Y, y = e % Y;
+        B2[z][y] = (z < kb2 && y < ny) ? P[(long long)(k1 + z) * n + y0 + y] : F_INF;
+      }
+      {
+        const int y = e / B, z = e % B;
+        C2[y][z] = (z < kb2 && y < ny) ? P[(long long)(y0 + y) * n + k1 + z] : F_INF;
+      }
+    }
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int e = tid + 1024 * q;
       {
         const int x = e / Y, y = e % Y;
-        if (x < z && y < ny) {
-          const float s = Dk[x][z] + PU[z][y];
-          if (s < PU[x][y]) PU[x][y] = s;
+        if (x < kb && y < ny) {
+          float v = PU[x][y];
+          for (int z = 0; z < kb2; ++z) {
+            const float c = A2[x][z] + B2[z][y];
+            v = c < v ? c : v;
+          }
+          PU[x][y] = v;
         }
       }
       {
         const int y = e / B, x = e % B;
-        if (x < z && y < ny) {
-          const float s = PD[y][z] + Dk[z][x];
-          if (s < PD[y][x]) PD[y][x] = s;
+        if (x < kb && y < ny) {
+          float v = PD[y][x];
+          for (int z = 0; z < kb2; ++z) {
+            const float c = C2[y][z] + E2[z][x];
+            v = c < v ? c : v;
+          }
+          PD[y][x] = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // top-down through K, four pivots z0 > z1 > z2 > z3 per barrier: every thread first finishes the
+  // group's own entries of its column (u_i = P[z_i][y] through z_j, j < i) from LDS, then applies
+  // all four to its entry (a group row stores its u).  A group row may be read while its owner
+  // stores it: the value read is either the old one or the finished one, and u_i comes out the same
+  // (its candidates are recomputed either way) — every candidate is the same single add as one pivot
+  // per step, so the minima are bit-identical.
+  for (int zt = kb - 1; zt >= 1; zt -= 4) {
+    const int G = min(4, zt);                 // members zt, zt - 1, ..., zt - G + 1 (>= 1)
+    const int zb = zt - G + 1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 1024 * q;
+      {
+        const int x = e / Y, y = e % Y;
+        if (x < zt && y < ny) {
+          float u[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (i >= G) break;
+            float v = PU[zt - i][y];
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+              const float c = Dk[zt - i][zt - j] + u[j];
+              v = c < v ? c : v;
+            }
+            u[i] = v;
+          }
+          if (x < zb) {
+            float v = PU[x][y];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              if (i >= G) break;
+              const float c = Dk[x][zt - i] + u[i];
+              v = c < v ? c : v;
+            }
+            PU[x][y] = v;
+          } else {
+            PU[x][y] = u[zt - x];
+          }
+        }
+      }
+      {
+        const int y = e / B, x = e % B;
+        if (x < zt && y < ny) {
+          float u[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (i >= G) break;
+            float v = PD[y][zt - i];
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+              const float c = u[j] + Dk[zt - j][zt - i];
+              v = c < v ? c : v;
+            }
+            u[i] = v;
+          }
+          if (x < zb) {
+            float v = PD[y][x];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              if (i >= G) break;
+              const float c = u[i] + Dk[zt - i][x];
+              v = c < v ? c : v;
+            }
+            PD[y][x] = v;
+          } else {
+            PD[y][x] = u[zt - x];
+          }
         }
       }
     }
@@ -1333,15 +1440,12 @@ __global__ __launch_bounds__(1024) void sup_solve_perfect_kernel(const SupNode* 
 
 // perfect, block b: the K x K targets top-down (x from the top of K: all of its candidates through
 // z in K above x are final), one workgroup per front; 16 lanes per target split the z loop
-__global__ __launch_bounds__(1024) void sup_kk_perfect_kernel(const SupNode* __restrict__ sn,
-                                                              const SupWork* __restrict__ w,
-                                                              const int32_t* __restrict__ farc, float* __restrict__ D,
-                                                              uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
+__device__ __forceinline__ void sup_kk_body(const SupWork& W, const int32_t* __restrict__ farc, float* __restrict__ D,
+                                            uint32_t* __restrict__ pup, uint32_t* __restrict__ pdn) {
   constexpr int B = SUP_B;
   __shared__ float Dk[B][B + 1];
   __shared__ float Pk[B][B + 1];
-  const SupWork W = w[blockIdx.x];
-  const SupNode S = sn[W.s];
+  const SupNode S = W.sn;
   const int n = S.n, tid = threadIdx.x;
   const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
   float* Db = D + 2 * S.dofs;
@@ -1392,6 +1496,17 @@ __global__ __launch_bounds__(1024) void sup_kk_perfect_kernel(const SupNode* __r
       }
     }
   }
+}
+
+// one launch per block step of the perfect phase: the K x K kernels of the blocks solved in the
+// previous launch (work items with t0 < 0) beside the products of the next blocks down (1024 threads)
+__global__ __launch_bounds__(1024) void sup_kk_gemm_perfect_kernel(const SupWork* __restrict__ w,
+                                                                   const int32_t* __restrict__ farc,
+                                                                   float* __restrict__ D, uint32_t* __restrict__ pup,
+                                                                   uint32_t* __restrict__ pdn) {
+  const SupWork W = w[blockIdx.x];
+  if (W.t0 < 0) sup_kk_body(W, farc, D, pup, pdn);
+  else sup_gemm_body(W, D);
 }
 
 // ---- context costs (routing/graph.py edge_records / edge_costs) ----
@@ -2244,20 +2359,23 @@ void CchGpu::build_supernodes(const std::vector<int64_t>& tofs) {
           for (int tz = 0; tz < T; ++tz) work.push_back(SupWork{f, r, ty, tz});
       }
       SL.trail.push_back(range_of(w0));
-      // perfect: the r-th block from the top of every front that has one
+      // perfect, launch pair r: [the K x K kernels of the blocks solved at r - 1 | the products of
+      // the r-th blocks from the top], then the r-th blocks' solves
       w0 = (int64_t)work.size();
       for (int f : by_lev[l]) {
         const SupNode& S = sn[f];
         const int nb = (int)cdiv(S.m, SUP_B);
+        if (r >= 1 && nb > r - 1) work.push_back(SupWork{f, nb - r, -1, 0});
         if (nb <= r) continue;
         const int b = nb - 1 - r, k1 = std::min(SUP_B * (b + 1), S.m), nF = S.n - k1;
-        if (nF <= 0) continue;
-        const int TY = (int)cdiv(nF, SUP_G1Y), Z = (int)cdiv(nF, SUP_G1Z);
+        const int zlo = b + 1 < nb ? std::min(k1 + SUP_B, S.m) : k1;
+        if (nF <= 0 || S.n - zlo <= 0) continue;
+        const int TY = (int)cdiv(nF, SUP_G1Y), Z = (int)cdiv(S.n - zlo, SUP_G1Z);
         for (int dir = 0; dir < 2; ++dir)
           for (int zs = 0; zs < Z; ++zs)
             for (int ty = 0; ty < TY; ++ty) work.push_back(SupWork{f, b, ty, (zs << 1) | dir});
       }
-      SL.gemm.push_back(range_of(w0));
+      SL.px.push_back(range_of(w0));
       w0 = (int64_t)work.size();
       for (int f : by_lev[l]) {
         const SupNode& S = sn[f];
@@ -2266,16 +2384,18 @@ void CchGpu::build_supernodes(const std::vector<int64_t>& tofs) {
         const int b = nb - 1 - r, k1 = std::min(SUP_B * (b + 1), S.m), nF = S.n - k1;
         for (int t = 0; t < (int)cdiv(nF, SUP_SJ); ++t) work.push_back(SupWork{f, b, t, 0});
       }
-      SL.solve.push_back(range_of(w0));
-      w0 = (int64_t)work.size();
+      SL.py.push_back(range_of(w0));
+    }
+    {
+      const int64_t w1 = (int64_t)work.size();
       for (int f : by_lev[l]) {
-        const SupNode& S = sn[f];
-        const int nb = (int)cdiv(S.m, SUP_B);
-        if (nb > r) work.push_back(SupWork{f, nb - 1 - r, 0, 0});
+        const int nb = (int)cdiv(sn[f].m, SUP_B);
+        if (nb == nbmax) work.push_back(SupWork{f, 0, -1, 0});   // the last blocks' K x K
       }
-      SL.kk.push_back(range_of(w0));
+      SL.px.push_back(range_of(w1));
     }
   }
+  for (SupWork& wk : work) wk.sn = sn[wk.s];
   // the other nodes: perfect by depth below their nearest front
   std::vector<uint8_t> node_in(N, 0);
   int nodes_in = 0;
@@ -2840,16 +2960,13 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
       float* Dp = (float*)X.sup_buf;
       hipLaunchKernelGGL(sup_gather_perfect_kernel, dim3(blocks_for(SL.gather.cnt, 4)), dim3(256), 0, s, sup_sn,
                          sup_wk + SL.gather.off, (long long)SL.gather.cnt, d_sup_farc, X.up64, X.dn64, X.pup, X.pdn, Dp);
-      for (size_t r = 0; r < SL.kk.size(); ++r) {
-        if (SL.gemm[r].cnt > 0)
-          hipLaunchKernelGGL(sup_gemm_perfect_kernel, dim3((unsigned)SL.gemm[r].cnt), dim3(256), 0, s, sup_sn,
-                             sup_wk + SL.gemm[r].off, Dp);
-        if (SL.solve[r].cnt > 0)
-          hipLaunchKernelGGL(sup_solve_perfect_kernel, dim3((unsigned)SL.solve[r].cnt), dim3(1024), 0, s, sup_sn,
-                             sup_wk + SL.solve[r].off, d_sup_farc, Dp, X.pup, X.pdn);
-        if (SL.kk[r].cnt > 0)
-          hipLaunchKernelGGL(sup_kk_perfect_kernel, dim3((unsigned)SL.kk[r].cnt), dim3(1024), 0, s, sup_sn,
-                             sup_wk + SL.kk[r].off, d_sup_farc, Dp, X.pup, X.pdn);
+      for (size_t r = 0; r < SL.px.size(); ++r) {
+        if (SL.px[r].cnt > 0)
+          hipLaunchKernelGGL(sup_kk_gemm_perfect_kernel, dim3((unsigned)SL.px[r].cnt), dim3(1024), 0, s,
+                             sup_wk + SL.px[r].off, d_sup_farc, Dp, X.pup, X.pdn);
+        if (r < SL.py.size() && SL.py[r].cnt > 0)
+          hipLaunchKernelGGL(sup_solve_perfect_kernel, dim3((unsigned)SL.py[r].cnt), dim3(1024), 0, s, sup_sn,
+                             sup_wk + SL.py[r].off, d_sup_farc, Dp, X.pup, X.pdn);
       }
       ck(hipGetLastError());
     }

@@ -295,7 +295,7 @@ class CchGpu {
   struct SupLevel {
     SupRange gather;
     std::vector<SupRange> panel, trail;          // basic, per block (bottom-up)
-    std::vector<SupRange> gemm, solve, kk;       // perfect, per block from the top
+    std::vector<SupRange> px, py;                // perfect, per block from the top: K x K | product, solve
   };
   bool sup_on_ = false;
   std::vector<uint8_t> sup_node_;                  // [N] rank in a dense front
