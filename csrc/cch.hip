@@ -877,12 +877,11 @@ __global__ __launch_bounds__(256) void sup_gather_basic_kernel(
 // basic_task_run's ROW_FINAL): a middle below the front from the gather's SS / SL, one in an earlier
 // block from its (final) arcs, and one inside K row by row from LDS (it needs the lengths of an arc
 // of K finalized just before).  1024 threads: one entry of each matrix per thread and pivot.
-__global__ __launch_bounds__(1024) void sup_panel_basic_kernel(
-    const SupNode* __restrict__ sn, const SupWork* __restrict__ w, const int32_t* __restrict__ farc,
-    unsigned long long* __restrict__ D, const int2* __restrict__ SS, const int2* __restrict__ SL,
-    unsigned long long* __restrict__ up, unsigned long long* __restrict__ dn, int32_t* __restrict__ sub_up,
-    int32_t* __restrict__ sub_dn, float* __restrict__ len_up, float* __restrict__ len_dn, int32_t* __restrict__ cnt_up,
-    int32_t* __restrict__ cnt_dn, const float* __restrict__ length) {
+__device__ __forceinline__ void sup_panel_body(
+    const SupWork& W, const int32_t* __restrict__ farc, unsigned long long* __restrict__ D, const int2* __restrict__ SS,
+    const int2* __restrict__ SL, unsigned long long* __restrict__ up, unsigned long long* __restrict__ dn,
+    int32_t* __restrict__ sub_up, int32_t* __restrict__ sub_dn, float* __restrict__ len_up, float* __restrict__ len_dn,
+    int32_t* __restrict__ cnt_up, int32_t* __restrict__ cnt_dn, const float* __restrict__ length) {
   constexpr int B = SUP_B, J = SUP_PJ, W2 = SUP_B + SUP_PJ;
   static_assert(B == 32 && J == 32, "one entry of each matrix per thread");
   __shared__ unsigned long long Dk[B][B + 1];   // D[K][K]
@@ -891,7 +890,6 @@ __global__ __launch_bounds__(1024) void sup_panel_basic_kernel(
   __shared__ int32_t FK[B][W2];                 // arcs of the rows of K: columns K | J
   __shared__ float lu[B][W2], ld[B][W2];        // their finalized metres
   __shared__ int32_t cu[B][W2], cd[B][W2];      // ... and road edges
-  const SupWork W = w[blockIdx.x];
   const SupNode S = W.sn;
   const int n = S.n, tid = threadIdx.x;
   const int k0 = W.b * B, k1 = min(k0 + B, S.m), kb = k1 - k0;
@@ -906,6 +904,33 @@ __global__ __launch_bounds__(1024) void sup_panel_basic_kernel(
   FK[ty][tx] = (ty < kb && tx < kb && tx > ty) ? F[(long long)(k0 + ty) * n + k0 + tx] : -1;
   FK[ty][B + tx] = (ty < kb && tx < nj) ? F[(long long)(k0 + ty) * n + j0 + tx] : -1;
   __syncthreads();
+  // the block below K (K- = [k0 - 32, k0), its panels finished in the previous launch): its pivots'
+  // candidates for this workgroup's entries.  That block's trailing update runs in the same launch
+  // as this and leaves the rows and columns of K to here (left-looking for one block).
+  if (W.b > 0) {
+    const int km = k0 - B;                      // (every block but a front's last is full)
+    __shared__ unsigned long long Ay[B][B + 1];   // D[K][K-]
+    __shared__ unsigned long long Aj[J][B + 1];   // D[J][K-]
+    __shared__ unsigned long long Bx[B][B + 1];   // D[K-][K]
+    __shared__ unsigned long long Bj[B][J + 1];   // D[K-][J]
+    Ay[ty][tx] = ty < kb ? Df[(long long)(k0 + ty) * n + km + tx] : PACK_INF_D;
+    Aj[ty][tx] = ty < nj ? Df[(long long)(j0 + ty) * n + km + tx] : PACK_INF_D;
+    Bx[ty][tx] = tx < kb ? Df[(long long)(km + ty) * n + k0 + tx] : PACK_INF_D;
+    Bj[ty][tx] = tx < nj ? Df[(long long)(km + ty) * n + j0 + tx] : PACK_INF_D;
+    __syncthreads();
+    unsigned long long dk = Dk[ty][tx], rr = R[ty][tx], cc = C[ty][tx];
+    const bool odk = ty < kb && tx < kb && ty != tx, orr = ty < kb && tx < nj, occ = ty < nj && tx < kb;
+    for (int p = 0; p < B; ++p) {
+      const uint32_t z = (uint32_t)(S.c0 + km + p);
+      if (odk) dk = umin64(dk, sup_cand(Ay[ty][p], Bx[p][tx], z));
+      if (orr) rr = umin64(rr, sup_cand(Ay[ty][p], Bj[p][tx], z));
+      if (occ) cc = umin64(cc, sup_cand(Aj[ty][p], Bx[p][tx], z));
+    }
+    Dk[ty][tx] = dk;
+    R[ty][tx] = rr;
+    C[ty][tx] = cc;
+    __syncthreads();
+  }
   // pivot p: entries of rows / columns above p (row p and column p are final and only read)
   for (int p = 0; p < kb; ++p) {
     const uint32_t z = (uint32_t)(S.c0 + k0 + p);
@@ -1035,104 +1060,109 @@ __global__ __launch_bounds__(1024) void sup_panel_basic_kernel(
   }
 }
 
-// basic, block b: the trailing update of the front's targets above K — for every (y, z), both past
-// k1, the best pivot p in K of D[y][p] + D[p][z] (ties: the lowest pivot = the smallest middle rank,
-// as the packed atomicMin).  U x U targets go to their arcs with one atomicMin after the last block.
-__global__ __launch_bounds__(256) void sup_trailing_basic_kernel(const SupNode* __restrict__ sn,
-                                                                 const SupWork* __restrict__ w,
-                                                                 const int32_t* __restrict__ farc,
-                                                                 unsigned long long* __restrict__ D,
-                                                                 unsigned long long* __restrict__ up,
-                                                                 unsigned long long* __restrict__ dn) {
+// basic, block b: the trailing update of the front's targets above the next block up — for every
+// (y, z), both past k1' (the end of the block above K; k1 for a front's last block), the best pivot p
+// in K of D[y][p] + D[p][z] (ties: the lowest pivot = the smallest middle rank, as the packed
+// atomicMin); the rows and columns of the block above K get theirs in its panel (same launch as this).
+// U x U targets go to their arcs with one atomicMin after the last block.  1024 threads, 64 x 64
+// targets, four per thread.
+__device__ __forceinline__ void sup_trailing_body(const SupWork& W, const int32_t* __restrict__ farc,
+                                                  unsigned long long* __restrict__ D, unsigned long long* __restrict__ up,
+                                                  unsigned long long* __restrict__ dn) {
   constexpr int B = SUP_B, T = SUP_TT;
   __shared__ float A[T][B + 1];     // weights D[y][K]
   __shared__ float Bm[B][T + 1];    // weights D[K][z]
-  const SupWork W = w[blockIdx.x];
   const SupNode S = W.sn;
   const int n = S.n, m = S.m, tid = threadIdx.x;
+  const int nb = (m + B - 1) / B;
   const int k0 = W.b * B, k1 = min(k0 + B, m), kb = k1 - k0;
-  const int y0 = k1 + W.t0 * T, z0 = k1 + W.t1 * T;
+  const int zr0 = W.b + 1 < nb ? min(k1 + B, m) : k1;
+  const int y0 = zr0 + W.t0 * T, z0 = zr0 + W.t1 * T;
   unsigned long long* Df = D + S.dofs;
-  for (int e = tid; e < T * B; e += 256) {
-    const int r = e / B, p = e % B;
-    A[r][p] = (y0 + r < n && p < kb) ? wof(Df[(long long)(y0 + r) * n + k0 + p]) : F_INF;
-  }
-  for (int e = tid; e < B * T; e += 256) {
-    const int p = e / T, c = e % T;
-    Bm[p][c] = (p < kb && z0 + c < n) ? wof(Df[(long long)(k0 + p) * n + z0 + c]) : F_INF;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int e = tid + 1024 * h;
+    {
+      const int r = e / B, p = e % B;
+      A[r][p] = (y0 + r < n && p < kb) ? wof(Df[(long long)(y0 + r) * n + k0 + p]) : F_INF;
+    }
+    {
+      const int p = e / T, c = e % T;
+      Bm[p][c] = (p < kb && z0 + c < n) ? wof(Df[(long long)(k0 + p) * n + z0 + c]) : F_INF;
+    }
   }
   // the targets' current words, loaded now (their latency hides behind the loop below)
   const int ty = tid >> 4, tz = tid & 15;
-  unsigned long long old[4][4];
+  const int y = y0 + ty;
+  unsigned long long old[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int y = y0 + ty * 4 + i, z = z0 + tz + 16 * j;
-      old[i][j] = (y < n && z < n && y != z) ? Df[(long long)y * n + z] : PACK_INF_D;
-    }
+  for (int j = 0; j < 4; ++j) {
+    const int z = z0 + tz + 16 * j;
+    old[j] = (y < n && z < n && y != z) ? Df[(long long)y * n + z] : PACK_INF_D;
+  }
   __syncthreads();
-  float bw[4][4];
-  int bp[4][4];
+  float bw[4];
+  int bp[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int j = 0; j < 4; ++j) {
+    bw[j] = F_INF;
+    bp[j] = 0;
+  }
+  for (int p = 0; p < kb; ++p) {
+    const float a = A[ty][p];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      bw[i][j] = F_INF;
-      bp[i][j] = 0;
-    }
-  for (int p = 0; p < kb; ++p) {
-    float a[4], b[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = A[ty * 4 + i][p];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = Bm[p][tz + 16 * j];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float s = a[i] + b[j];
-        if (s < bw[i][j]) {        // strict: the first (lowest) pivot keeps a tie
-          bw[i][j] = s;
-          bp[i][j] = p;
-        }
+      const float sum = a + Bm[p][tz + 16 * j];
+      if (sum < bw[j]) {        // strict: the first (lowest) pivot keeps a tie
+        bw[j] = sum;
+        bp[j] = p;
       }
+    }
   }
   const bool last = k1 == m;
   const int32_t* F = farc + S.foff;
-  unsigned long long nv[4][4];
-  int arc[4][4];
+  unsigned long long nv[4];
+  int arc[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int y = y0 + ty * 4 + i, z = z0 + tz + 16 * j;
-      const unsigned long long c = bw[i][j] < F_INF ? packw(bw[i][j], (uint32_t)(S.c0 + k0 + bp[i][j])) : PACK_INF_D;
-      nv[i][j] = umin64(old[i][j], c);
-      arc[i][j] = -1;
-      if (y >= n || z >= n || y == z) continue;
-      if (y >= m && z >= m && last) {
-        if (nv[i][j] != PACK_INF_D) arc[i][j] = F[(long long)y * n + z];
-      } else if (c < old[i][j]) {
-        Df[(long long)y * n + z] = c;
-      }
+  for (int j = 0; j < 4; ++j) {
+    const int z = z0 + tz + 16 * j;
+    const unsigned long long c = bw[j] < F_INF ? packw(bw[j], (uint32_t)(S.c0 + k0 + bp[j])) : PACK_INF_D;
+    nv[j] = umin64(old[j], c);
+    arc[j] = -1;
+    if (y >= n || z >= n || y == z) continue;
+    if (y >= m && z >= m && last) {
+      if (nv[j] != PACK_INF_D) arc[j] = F[(long long)y * n + z];
+    } else if (c < old[j]) {
+      Df[(long long)y * n + z] = c;
     }
+  }
   if (!last) return;
-  unsigned long long cur[4][4];
+  unsigned long long cur[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int j = 0; j < 4; ++j) {
+    const int z = z0 + tz + 16 * j;
+    cur[j] = arc[j] >= 0 ? (y < z ? up : dn)[arc[j]] : 0ull;
+  }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int y = y0 + ty * 4 + i, z = z0 + tz + 16 * j;
-      cur[i][j] = arc[i][j] >= 0 ? (y < z ? up : dn)[arc[i][j]] : 0ull;
-    }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int y = y0 + ty * 4 + i, z = z0 + tz + 16 * j;
-      if (arc[i][j] >= 0 && nv[i][j] < cur[i][j]) atomicMin((y < z ? up : dn) + arc[i][j], nv[i][j]);
-    }
+  for (int j = 0; j < 4; ++j) {
+    const int z = z0 + tz + 16 * j;
+    if (arc[j] >= 0 && nv[j] < cur[j]) atomicMin((y < z ? up : dn) + arc[j], nv[j]);
+  }
+}
+
+// one launch per block step of the basic phase: the panels of block r of every front (work items
+// with t1 < 0) beside the trailing updates of block r - 1 (1024 threads)
+__global__ __launch_bounds__(1024) void sup_step_basic_kernel(
+    const SupWork* __restrict__ w, const int32_t* __restrict__ farc, unsigned long long* __restrict__ D,
+    const int2* __restrict__ SS, const int2* __restrict__ SL, unsigned long long* __restrict__ up,
+    unsigned long long* __restrict__ dn, int32_t* __restrict__ sub_up, int32_t* __restrict__ sub_dn,
+    float* __restrict__ len_up, float* __restrict__ len_dn, int32_t* __restrict__ cnt_up, int32_t* __restrict__ cnt_dn,
+    const float* __restrict__ length) {
+  const SupWork W = w[blockIdx.x];
+  if (W.t1 < 0)
+    sup_panel_body(W, farc, D, SS, SL, up, dn, sub_up, sub_dn, len_up, len_dn, cnt_up, cnt_dn, length);
+  else
+    sup_trailing_body(W, farc, D, up, dn);
 }
 
 // perfect: a front's basic weights (f32) of every pair with a chain node, and the perfect weights
@@ -2321,6 +2351,16 @@ void CchGpu::build_supernodes(const std::vector<int64_t>& tofs) {
   for (int f = 0; f < (int)sn.size(); ++f)
     for (int i = 0; i < sn[f].n; ++i) work.push_back(SupWork{f, i, 0, 0});
   const SupRange all_rows = range_of(0);
+  // the trailing update of front f's block b: targets past the end of the block above it
+  auto push_trail = [&](int f, int b) {
+    const SupNode& S = sn[f];
+    const int nb = (int)cdiv(S.m, SUP_B);
+    const int k1 = std::min(SUP_B * (b + 1), S.m);
+    const int zr0 = b + 1 < nb ? std::min(k1 + SUP_B, S.m) : k1;
+    const int T = (int)cdiv(S.n - zr0, SUP_TT);
+    for (int ty = 0; ty < T; ++ty)
+      for (int tz = 0; tz < T; ++tz) work.push_back(SupWork{f, b, ty, tz});
+  };
   std::vector<SupLevel> levs(L);
   int64_t buf = 0;
   int blocks = 0;
@@ -2340,25 +2380,20 @@ void CchGpu::build_supernodes(const std::vector<int64_t>& tofs) {
       for (int i = 0; i < sn[f].n; ++i) work.push_back(SupWork{f, i, 0, 0});
     SL.gather = range_of(w0);
     for (int r = 0; r < nbmax; ++r) {
+      // basic, step r: the panels of every front's block r (t1 = -1) beside the trailing updates of
+      // its block r - 1 (sup_step_basic_kernel)
       w0 = (int64_t)work.size();
       for (int f : by_lev[l]) {
         const SupNode& S = sn[f];
-        if (cdiv(S.m, SUP_B) <= r) continue;
-        const int k1 = std::min(SUP_B * (r + 1), S.m);
-        const int nt = std::max<int64_t>(1, cdiv(S.n - k1, SUP_PJ));
-        for (int t = 0; t < nt; ++t) work.push_back(SupWork{f, r, t, 0});
+        const int nb = (int)cdiv(S.m, SUP_B);
+        if (nb > r) {
+          const int k1 = std::min(SUP_B * (r + 1), S.m);
+          const int nt = std::max<int64_t>(1, cdiv(S.n - k1, SUP_PJ));
+          for (int t = 0; t < nt; ++t) work.push_back(SupWork{f, r, t, -1});
+        }
+        if (r >= 1 && nb > r - 1) push_trail(f, r - 1);
       }
       SL.panel.push_back(range_of(w0));
-      w0 = (int64_t)work.size();
-      for (int f : by_lev[l]) {
-        const SupNode& S = sn[f];
-        if (cdiv(S.m, SUP_B) <= r) continue;
-        const int k1 = std::min(SUP_B * (r + 1), S.m);
-        const int T = (int)cdiv(S.n - k1, SUP_TT);
-        for (int ty = 0; ty < T; ++ty)
-          for (int tz = 0; tz < T; ++tz) work.push_back(SupWork{f, r, ty, tz});
-      }
-      SL.trail.push_back(range_of(w0));
       // perfect, launch pair r: [the K x K kernels of the blocks solved at r - 1 | the products of
       // the r-th blocks from the top], then the r-th blocks' solves
       w0 = (int64_t)work.size();
@@ -2393,6 +2428,10 @@ void CchGpu::build_supernodes(const std::vector<int64_t>& tofs) {
         if (nb == nbmax) work.push_back(SupWork{f, 0, -1, 0});   // the last blocks' K x K
       }
       SL.px.push_back(range_of(w1));
+      const int64_t w2 = (int64_t)work.size();
+      for (int f : by_lev[l])
+        if ((int)cdiv(sn[f].m, SUP_B) == nbmax) push_trail(f, nbmax - 1);   // the last blocks' trailing
+      SL.panel.push_back(range_of(w2));
     }
   }
   for (SupWork& wk : work) wk.sn = sn[wk.s];
@@ -2539,7 +2578,7 @@ void CchGpu::build_tasks(const std::vector<int64_t>& tofs) {
   for (int h = 0; h <= T_.max_height; ++h) {
     for (int64_t q = T_.hlev_ptr[h]; q < T_.hlev_ptr[h + 1]; ++q) {
       const int z = T_.hlev_nodes[q];
-      if (sup_on_ && sup_node_[z]) continue;                // a dense front's (sup_panel_basic_kernel)
+      if (sup_on_ && sup_node_[z]) continue;                // a dense front's (sup_panel_body)
       const int k = (int)(T_.up_ptr[z + 1] - T_.up_ptr[z]);
       if (k > 0xFFFE) { bt.clear(); pt.clear(); return; }   // (never on road graphs: k <= ~2k)
       const int a0 = (int)T_.up_ptr[z];
@@ -2862,15 +2901,11 @@ hipError_t CchGpu::customize(const float* d_cost, CchMetricDev& m, hipStream_t s
       hipLaunchKernelGGL(sup_gather_basic_kernel, dim3((unsigned)SL.gather.cnt), dim3(256), 0, s, sup_sn,
                          sup_wk + SL.gather.off, d_sup_fnode, d_sup_farc, X.up64, X.dn64, d_up_ptr, d_up_head, m.len_up,
                          m.len_dn, m.cnt_up, m.cnt_dn, X.sup_buf, sup_ss, sup_sl);
-      for (size_t r = 0; r < SL.panel.size(); ++r) {
+      for (size_t r = 0; r < SL.panel.size(); ++r)
         if (SL.panel[r].cnt > 0)
-          hipLaunchKernelGGL(sup_panel_basic_kernel, dim3((unsigned)SL.panel[r].cnt), dim3(1024), 0, s, sup_sn,
+          hipLaunchKernelGGL(sup_step_basic_kernel, dim3((unsigned)SL.panel[r].cnt), dim3(1024), 0, s,
                              sup_wk + SL.panel[r].off, d_sup_farc, X.sup_buf, sup_ss, sup_sl, X.up64, X.dn64, m.sub_up,
                              m.sub_dn, m.len_up, m.len_dn, m.cnt_up, m.cnt_dn, d_length);
-        if (SL.trail[r].cnt > 0)
-          hipLaunchKernelGGL(sup_trailing_basic_kernel, dim3((unsigned)SL.trail[r].cnt), dim3(256), 0, s, sup_sn,
-                             sup_wk + SL.trail[r].off, d_sup_farc, X.sup_buf, X.up64, X.dn64);
-      }
       ck(hipGetLastError());
     }
     if (ev && ev[1]) (void)hipEventRecord(ev[1], s);

@@ -294,7 +294,7 @@ class CchGpu {
   };
   struct SupLevel {
     SupRange gather;
-    std::vector<SupRange> panel, trail;          // basic, per block (bottom-up)
+    std::vector<SupRange> panel;                 // basic, per block step: panels | the block below's trailing
     std::vector<SupRange> px, py;                // perfect, per block from the top: K x K | product, solve
   };
   bool sup_on_ = false;
