@@ -176,9 +176,15 @@ def test_hung_gpu_slot_watchdog_and_route_failover():
     the deadline + one round, nothing answers 5xx, slot 1 is quarantined, and route requests keep
     being answered natively — slot 1's route service hands its flushes to slot 0's, and slot 0 is
     never quarantined (ROUTEST_ROUTE_TRACE_MS=20 in the child's environment prints the timeline)."""
+    import gc
     import os
     import subprocess
     import sys
+    # what earlier tests of this session left behind (routers, servers, their streams and builder
+    # threads) goes before the child measures 100 ms deadlines on the shared GPU
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, GPU_MAX_HW_QUEUES="32", ROUTEST_GPU_DEADLINE_MS="100", ROUTEST_ROUTE_DEADLINE_MS="300",
                ROUTEST_PERSIST_IDLE_MS="0", ROUTEST_QUARANTINE_PROBE_MS="60000",
