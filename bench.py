@@ -594,7 +594,7 @@ def main() -> None:
             from routest_amd.api.app import build_services, create_app
             from routest_amd.config import load_settings
             from routest_amd.serve.eta_service import EtaService
-            from routest_amd.serve.frontend import ServingStack
+            from routest_amd.serve.frontend import ServingStack, route_pipelines_for
             from routest_amd.serve.loadgen import native_route_load, route_payloads
             body = {"summary": {"distance": 12345}, "pickup_time": "2026-10-15T08:30:00",
                     "driver_age": 34, "weather": "Sunny", "traffic": "Medium"}
@@ -606,7 +606,10 @@ def main() -> None:
                 # context-aware road provider sharing the bench's router (the customized contexts)
                 prov = GraphProvider(g, None, device=dev, eta_model=route_model)
                 prov._routers[str(torch.device(dev))] = route_router
-            ss = load_settings(env={}, dotenv_path=None, devices=[local_rank], warm_scorer=False)
+            # native route services per GPU (ROUTEST_ROUTE_PIPELINES, config.py route_pipelines)
+            pipes = max(0, int(os.environ.get("ROUTEST_ROUTE_PIPELINES", "0")))
+            ss = load_settings(env={}, dotenv_path=None, devices=[local_rank], warm_scorer=False,
+                               route_pipelines=pipes)
             sv = build_services(ss, eta=EtaService(model, devices=[local_rank]), provider=prov, store=None)
             with ServingStack(sv, create_app(sv), model, [local_rank], threads=8) as srv:
                 # native closed-loop client (csrc/runtime/http_client.h): one keep-alive connection,
@@ -641,6 +644,7 @@ def main() -> None:
                 if prov is not None and route_res is not None and srv.front.routes:
                     route_res["http"] = native_route_load(srv, route_payloads(g.lat, g.lon, 1000, seed=1), 1000,
                                                           a.route_http_seconds)
+                    route_res["http"]["route_pipelines_per_gpu"] = route_pipelines_for(sv)
             sv.eta.close()
             # the dashboard's own request (F02 verbatim: use_ml_eta, context, meta, driver_age) at 1k
             # concurrency on the same port, every answer persisted into a SQLite store on disk — the
@@ -659,6 +663,7 @@ def main() -> None:
                             r2 = native_route_load(srv2, f02_payloads(g.lat, g.lon, 1000, seed=2, location_ids=ids),
                                                    1000, a.route_http_seconds)
                             r2["store"] = "sqlite file (WAL, synchronous=NORMAL), group commit per flush"
+                            r2["route_pipelines_per_gpu"] = route_pipelines_for(sv2)
                             route_res["http_f02"] = r2
                     sv2.eta.close()
                     store.close()

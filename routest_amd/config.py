@@ -76,6 +76,10 @@ class Settings:
     route_batch: str = "auto"            # ROUTEST_ROUTE_BATCH: auto (on with a GPU) | 1 | 0
     route_batch_max: int = 1024          # ROUTEST_ROUTE_BATCH_MAX: requests per optimizer flush
     route_batch_timeout_us: int = 500    # ROUTEST_ROUTE_BATCH_TIMEOUT_US
+    route_pipelines: int = 0             # ROUTEST_ROUTE_PIPELINES: native route services per GPU (each
+                                         # its own GPU / assembly / persistence threads, so one flush's
+                                         # host stages overlap another's GPU stages); 0 = auto:
+                                         # serve/frontend.py route_pipelines_for
     route_gpu_min_stops: int = 32        # ROUTEST_ROUTE_GPU_MIN_STOPS: haversine requests with fewer
                                          # destinations stay inline (profiles/superseded/route_http_r2.jsonl)
     warm_scorer: bool = True             # ROUTEST_WARM_SCORER: build the GCN scorer at startup
@@ -161,6 +165,7 @@ def load_settings(env: Optional[Dict[str, str]] = None, dotenv_path: Optional[st
         route_batch=(g("ROUTEST_ROUTE_BATCH") or "auto").lower(),
         route_batch_max=_int("ROUTEST_ROUTE_BATCH_MAX", 1024),
         route_batch_timeout_us=_int("ROUTEST_ROUTE_BATCH_TIMEOUT_US", 500),
+        route_pipelines=max(0, _int("ROUTEST_ROUTE_PIPELINES", 0)),
         route_gpu_min_stops=_int("ROUTEST_ROUTE_GPU_MIN_STOPS", 32),
         warm_scorer=_as_bool(g("ROUTEST_WARM_SCORER"), True),
         scorer_train_steps=_int("ROUTEST_SCORER_TRAIN_STEPS", 300),

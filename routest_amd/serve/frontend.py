@@ -62,6 +62,22 @@ def native_route_reason(sv) -> Optional[str]:
     return None
 
 
+def route_pipelines_for(sv) -> int:
+    """Native route services per GPU: ``settings.route_pipelines`` if set, else 2 when the route
+    service persists every answer itself (SQLite store) and 1 otherwise.
+
+    Measured on one MI355X (profiles/route_pipelines_r6ax.md): with persistence, a flush holds its
+    GPU thread ~4 ms and then ~4 ms of assembly + group commit, so a second service per GPU keeps the
+    GPU fed — the dashboard's request went 51.8k -> 85.0k req/s, p99 22.3 -> 15.1 ms.  Without a
+    store the route path is bound by response bytes (~7.5 GB/s of GeoJSON over loopback): a second
+    service added 6 % throughput but moved p99 from 14 to 34 ms, so it stays at one."""
+    k = int(getattr(sv.settings, "route_pipelines", 0) or 0)
+    if k > 0:
+        return k
+    st = sv.store
+    return 2 if st is not None and getattr(st, "kind", "") == "sqlite" else 1
+
+
 def route_configs(sv, devices: Sequence[int], batch_max: int = 1024, timeout_us: int = 500) -> List[dict]:
     """One native route service config per GPU (serve/native_server.py route_config)."""
     import torch
@@ -90,6 +106,11 @@ def start_front_end(sv, model, devices: Sequence[int], port: int = 0, upstream_p
     if routes:
         why = native_route_reason(sv)
         if why is None:
+            # route_pipelines > 1: that many slots (route service + scorer) per GPU; the reactors
+            # spread over the slots, so the GPU stages of one flush overlap the host stages
+            # (assembly, persistence) of another on the same GPU
+            k = route_pipelines_for(sv)
+            devices = [d for d in devices for _ in range(k)]
             cfgs = route_configs(sv, devices, batch_max or s.route_batch_max,
                                  timeout_us if timeout_us is not None else s.route_batch_timeout_us)
         else:

@@ -22,6 +22,23 @@ def test_dotenv_then_env_then_overrides(tmp_path):
     assert s3.ors_api_key == "primary" and s3.store_url.startswith("sqlite")
 
 
+def test_route_pipelines_setting():
+    """Native route services per GPU: explicit, or auto (2 when the route service persists every
+    answer into the SQLite store, else 1; serve/frontend.py route_pipelines_for)."""
+    from types import SimpleNamespace
+    from routest_amd.serve.frontend import route_pipelines_for
+    assert load_settings(env={}, dotenv_path=None).route_pipelines == 0          # auto
+    assert load_settings(env={"ROUTEST_ROUTE_PIPELINES": "2"}, dotenv_path=None).route_pipelines == 2
+    assert load_settings(env={"ROUTEST_ROUTE_PIPELINES": "-1"}, dotenv_path=None).route_pipelines == 0
+    assert load_settings(env={}, dotenv_path=None, route_pipelines=3).route_pipelines == 3
+    auto = load_settings(env={}, dotenv_path=None)
+    assert route_pipelines_for(SimpleNamespace(settings=auto, store=None)) == 1
+    assert route_pipelines_for(SimpleNamespace(settings=auto, store=SimpleNamespace(kind="sqlite"))) == 2
+    assert route_pipelines_for(SimpleNamespace(settings=auto, store=SimpleNamespace(kind="postgrest"))) == 1
+    three = load_settings(env={}, dotenv_path=None, route_pipelines=3)
+    assert route_pipelines_for(SimpleNamespace(settings=three, store=None)) == 3
+
+
 def test_sse_stream_receives_tracker_update():
     import httpx
     from routest_amd.api.app import build_services, create_app
