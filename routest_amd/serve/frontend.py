@@ -108,9 +108,11 @@ def start_front_end(sv, model, devices: Sequence[int], port: int = 0, upstream_p
         if why is None:
             # route_pipelines > 1: that many slots (route service + scorer) per GPU; the reactors
             # spread over the slots, so the GPU stages of one flush overlap the host stages
-            # (assembly, persistence) of another on the same GPU
+            # (assembly, persistence) of another on the same GPU.  Slots go round by round over the
+            # GPUs ([0, 1, .., 0, 1, ..]): a failover goes to slot + 1 first
+            # (csrc/native_server.hip), which is then another GPU, not the hung one's sibling
             k = route_pipelines_for(sv)
-            devices = [d for d in devices for _ in range(k)]
+            devices = [d for _ in range(k) for d in devices]
             cfgs = route_configs(sv, devices, batch_max or s.route_batch_max,
                                  timeout_us if timeout_us is not None else s.route_batch_timeout_us)
         else:
