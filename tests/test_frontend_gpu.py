@@ -396,7 +396,9 @@ def test_graph_routes_persist_compact_records_read_back_identically():
     store = SQLiteStore(":memory:")
     st, sv = _stack(prov, store)
     try:
-        assert st.front.routes
+        # with the route service persisting into the store: two route services on the one GPU
+        # (serve/frontend.py route_pipelines_for), both writing the same SQLite file
+        assert len(st.front.routes) == 2
         ctx = {"weather": "Rainy", "traffic": "High", "pickup_time": "2025-08-27T08:15:00"}
         resp = {}
         for i, p in enumerate(_payloads(30, g.lat, g.lon, seed=31, max_stops=6)):
