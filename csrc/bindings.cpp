@@ -1070,6 +1070,7 @@ static rt::RouteServiceCfg route_cfg_from(const py::dict& d, int device) {
   if (has("compat200")) c.compat200 = d["compat200"].cast<bool>();
   if (has("batch_max")) c.batch_max = d["batch_max"].cast<int>();
   if (has("timeout_us")) c.timeout_us = d["timeout_us"].cast<double>();
+  if (has("chunk_threads")) c.chunk_threads = d["chunk_threads"].cast<int>();
   if (has("sqlite_path")) c.sqlite_path = d["sqlite_path"].cast<std::string>();
   if (c.provider == 1 && has("cch_ptr")) {
     // road graph through the CCH router (routing/cch.py RoadRouter.gpu on this device)

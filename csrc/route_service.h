@@ -65,6 +65,7 @@ struct RouteServiceCfg {
   bool compat200 = true;                  // /api/request_route answers errors with 200 (reference)
   int batch_max = 1024;
   double timeout_us = 500.0;
+  int chunk_threads = 16;                 // host fan-out per parallel_chunks call (assembly, legs)
   // road graph, host side (assembly, snapping, exact fallback)
   const double* glat = nullptr;
   const double* glon = nullptr;

@@ -292,6 +292,10 @@ inline double now_us() {
 struct RouteService::Impl {
   RouteServiceCfg cfg;
   std::function<void(RouteJob*)> done;
+  // chunks per parallel_chunks call: cfg.chunk_threads, a 1/k share of the process's CPU pool when
+  // k route services run per GPU (profiles/route_pipelines_r6ax.md: two services' full fan-outs
+  // oversubscribed the box's CPU share and raised the no-store p99 from 15 to 34 ms)
+  unsigned chunk_threads() const { return (unsigned)(cfg.chunk_threads < 1 ? 1 : cfg.chunk_threads); }
   std::function<void(std::vector<RouteJob*>&)> done_many;
   void done_all(std::vector<RouteJob*>& js) {
     if (js.empty()) return;
@@ -1251,7 +1255,7 @@ struct RouteService::Impl {
       return false;
     for (int g = 0; g < G; ++g)
       for (int k = r0[g]; k < r0[g + 1]; ++k) h_rowg.h[k] = g;
-    rtc::parallel_chunks((size_t)R, 64, 16, [&](size_t lo, size_t hi) {
+    rtc::parallel_chunks((size_t)R, 64, chunk_threads(), [&](size_t lo, size_t hi) {
       for (size_t k = lo; k < hi; ++k) {
         const rtr::RouteReq& r = m[k]->req;
         const int n = (int)r.dst.size() + 1;
@@ -1332,7 +1336,7 @@ struct RouteService::Impl {
     std::vector<RouteJob*> g;
     for (RouteJob* j : b.jobs)
       if (!j->fallback && !j->calls.empty()) g.push_back(j);
-    rtc::parallel_chunks(g.size(), 64, 16, [&](size_t lo, size_t hi) {
+    rtc::parallel_chunks(g.size(), 64, chunk_threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         RouteJob* j = g[i];
         j->nodes.clear();
@@ -1379,7 +1383,7 @@ struct RouteService::Impl {
     std::vector<RouteJob*> alt_jobs;
     for (RouteJob* j : g)
       if (j->req.alt_k > 0) alt_jobs.push_back(j);
-    rtc::parallel_chunks(alt_jobs.size(), 1, 16, [&](size_t lo, size_t hi) {
+    rtc::parallel_chunks(alt_jobs.size(), 1, chunk_threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         RouteJob* j = alt_jobs[i];
         j->alt_pairs.clear();
@@ -1556,7 +1560,7 @@ struct RouteService::Impl {
     std::vector<RouteJob*> g;
     for (RouteJob* j : jobs)
       if (!j->fallback && !j->calls.empty()) g.push_back(j);
-    rtc::parallel_chunks(g.size(), 64, 16, [&](size_t lo, size_t hi) {
+    rtc::parallel_chunks(g.size(), 64, chunk_threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         RouteJob* j = g[i];
         j->nodes.clear();
@@ -1776,7 +1780,7 @@ struct RouteService::Impl {
     std::vector<RouteJob*>& jobs = b.jobs;
     const std::vector<rtr::Leg>& legs = b.legs;
     const std::unordered_map<uint64_t, int>& leg_index = b.leg_index;
-    rtc::parallel_chunks(jobs.size(), 8, 16, [&](size_t lo, size_t hi) {
+    rtc::parallel_chunks(jobs.size(), 8, chunk_threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         RouteJob* j = jobs[i];
         if (j->fallback || j->status) continue;
@@ -1934,7 +1938,7 @@ struct RouteService::Impl {
     double t0 = now_us();
     // (jobs are parsed on the submitting reactor thread, RouteService::submit; this catches any
     // that were not)
-    rtc::parallel_chunks(jobs.size(), 32, 16, [&](size_t lo, size_t hi) {
+    rtc::parallel_chunks(jobs.size(), 32, chunk_threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) parse_job(jobs[i]);
     });
     // "alternatives" need the road graph through the CCH and a published scorer; else the app
@@ -1998,7 +2002,7 @@ struct RouteService::Impl {
     for (RouteJob* j : jobs)
       if (db && !j->fallback && !j->status && j->asmb.ok && !j->request_route) b.save.push_back(j);
     t0 = now_us();
-    rtc::parallel_chunks(b.save.size(), 16, 16, [&](size_t lo, size_t hi) {
+    rtc::parallel_chunks(b.save.size(), 16, chunk_threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) prep_persist(b.save[i]);
     });
     add_t(7, t0);

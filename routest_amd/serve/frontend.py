@@ -78,8 +78,13 @@ def route_pipelines_for(sv) -> int:
     return 2 if st is not None and getattr(st, "kind", "") == "sqlite" else 1
 
 
-def route_configs(sv, devices: Sequence[int], batch_max: int = 1024, timeout_us: int = 500) -> List[dict]:
-    """One native route service config per GPU (serve/native_server.py route_config)."""
+def route_configs(sv, devices: Sequence[int], batch_max: int = 1024, timeout_us: int = 500,
+                  chunk_threads: int = 16) -> List[dict]:
+    """One native route service config per slot (serve/native_server.py route_config).
+
+    ``chunk_threads``: host fan-out per parallel_chunks call of each service.  Halving it with two
+    services per GPU cut the no-store p99 from 34 to 24 ms but did not help the persisted path
+    (profiles/route_pipelines_r6ax.md, run r6bb), so it stays at 16."""
     import torch
     from .native_server import route_config
     s = sv.settings
@@ -91,7 +96,8 @@ def route_configs(sv, devices: Sequence[int], batch_max: int = 1024, timeout_us:
             astar = BatchedAstar(sv.provider.g, sv.provider.cost, torch.device("cuda", d),
                                  slots=int(getattr(s, "route_astar_slots", 8192)))
         out.append(route_config(sv.provider, d, engine=s.engine_name, compat200=s.compat_request_route_200,
-                                batch_max=batch_max, timeout_us=timeout_us, store=sv.store, astar=astar))
+                                batch_max=batch_max, timeout_us=timeout_us, store=sv.store, astar=astar,
+                                chunk_threads=chunk_threads))
     return out
 
 

@@ -201,7 +201,8 @@ class NativePredictServer:
 
 
 def route_config(provider, device, *, engine: str = "backend:mi355x", compat200: bool = True,
-                 batch_max: int = 1024, timeout_us: int = 500, store=None, astar=None) -> dict:
+                 batch_max: int = 1024, timeout_us: int = 500, store=None, astar=None,
+                 chunk_threads: int = 16) -> dict:
     """The native route service's configuration for one GPU (``csrc/route_service.h``).
 
     ``provider``: the app's HaversineProvider or GraphProvider.  A GraphProvider on the CCH engine
@@ -215,6 +216,7 @@ def route_config(provider, device, *, engine: str = "backend:mi355x", compat200:
     name = getattr(provider, "name", "")
     cfg = {"provider": "graph" if name == "graph" else "haversine", "engine": engine,
            "compat200": bool(compat200), "batch_max": int(batch_max), "timeout_us": float(timeout_us),
+           "chunk_threads": max(1, int(chunk_threads)),
            "circuity": float(getattr(provider, "circuity", 1.3)), "step_m": float(getattr(provider, "step_m", 150.0)),
            "sqlite_path": getattr(store, "sqlite_uri", "") if store is not None else ""}
     if name == "graph" and getattr(provider, "engine", "astar") != "astar":
